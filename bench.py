@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""Headline benchmark: GPT-3 13B pre-training step (Fleet sharding stage-3 over RCCL/xGMI, bf16
+AMP-O2, fused AdamW, full recompute) + ResNet-50 bf16 data-parallel, on N MI355X GPUs of one node.
+
+Metric (BASELINE.json): "tokens/sec GPT-3-13B sharding-3 + ResNet50 img/s, at 1/2/4/8 MI355X".
+`value` = whole-job GPT-3 13B training tokens/s; ResNet-50 img/s is reported in `secondary`.
+Weak scaling: per-GPU micro-batch fixed as N grows. Data: synthetic tokens / images, random init.
+
+Launch (N>1): python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+              --master-port P bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+import torch  # noqa: E402
+
+BASELINE_METRIC = "tokens/sec GPT-3-13B sharding-3 + ResNet50 img/s, at 1/2/4/8 MI355X"
+PEAK_BF16 = 2.5e15
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=4)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--model", default="gpt3-13b", help="gpt3-13b | gpt3-6.7b | gpt3-1.3b | tiny")
+    p.add_argument("--micro-batch", type=int, default=4)
+    p.add_argument("--accum", type=int, default=1, help="gradient accumulation steps per optimizer step")
+    p.add_argument("--seq-len", type=int, default=2048)
+    p.add_argument("--recompute", type=int, default=1)
+    p.add_argument("--sharding-stage", type=int, default=3)
+    p.add_argument("--tp", type=int, default=1)
+    p.add_argument("--resnet", type=int, default=1, help="also run the ResNet-50 DP benchmark")
+    p.add_argument("--resnet-batch", type=int, default=256, help="per-GPU ResNet-50 batch")
+    p.add_argument("--resnet-steps", type=int, default=10)
+    p.add_argument("--skip-gpt", type=int, default=0)
+    return p.parse_args()
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def timed(step_fn, steps, warmup, dist_on):
+    import torch.distributed as dist
+    for _ in range(warmup):
+        step_fn()
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step_fn()
+    torch.cuda.synchronize()
+    if dist_on:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist_on:
+        t = torch.tensor([dt], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt
+
+
+def gpt_bench(args, paddle, world, dist_on):
+    from paddlepaddle_amd.models.gpt import GPTConfig, GPTForPretraining, GPTPretrainingCriterion
+    cfgs = {"gpt3-13b": GPTConfig.gpt3_13b, "gpt3-6.7b": GPTConfig.gpt3_6_7b, "gpt3-1.3b": GPTConfig.gpt3_1_3b,
+            "tiny": GPTConfig.tiny}
+    cfg = cfgs[args.model](max_position_embeddings=max(args.seq_len, 128), use_recompute=bool(args.recompute),
+                           tensor_parallel_degree=args.tp)
+    paddle.set_default_dtype("bfloat16")
+    paddle.seed(1234 + int(os.environ.get("RANK", "0")))
+    t0 = time.time()
+    model = GPTForPretraining(cfg)
+    crit = GPTPretrainingCriterion(cfg)
+    paddle.set_default_dtype("float32")
+    nparams = sum(p.size for p in model.parameters())
+    log(f"[gpt] built {args.model}: {nparams / 1e9:.2f}B params in {time.time() - t0:.1f}s")
+    clip = paddle.nn.ClipGradByGlobalNorm(1.0)
+    opt = paddle.optimizer.AdamW(learning_rate=1e-4, parameters=model.parameters(), weight_decay=0.01,
+                                 grad_clip=clip, multi_precision=True,
+                                 apply_decay_param_fun=lambda n: not ("norm" in n or n.endswith("b_0")))
+    if world > 1 and args.sharding_stage > 0:
+        from paddlepaddle_amd.distributed.sharding import group_sharded_parallel
+        level = {1: "os", 2: "os_g", 3: "p_g_os"}[args.sharding_stage]
+        model, opt, _ = group_sharded_parallel(model, opt, level=level)
+    elif world > 1:
+        model = paddle.DataParallel(model)
+    B, S = args.micro_batch, args.seq_len
+    gen = torch.Generator(device="cuda").manual_seed(7)
+    data = torch.randint(0, cfg.vocab_size, (args.accum, B, S + 1), device="cuda", generator=gen)
+    ids = [paddle.Tensor(data[i, :, :-1]) for i in range(args.accum)]
+    lbl = [paddle.Tensor(data[i, :, 1:]) for i in range(args.accum)]
+    state = {}
+
+    def step():
+        for a in range(args.accum):
+            logits = model(ids[a])
+            loss = crit(logits, lbl[a])
+            if args.accum > 1:
+                loss = loss * (1.0 / args.accum)
+            loss.backward()
+        opt.step()
+        opt.clear_grad()
+        state["loss"] = loss
+
+    dt = timed(step, args.steps, args.warmup, dist_on)
+    tokens = args.steps * args.accum * B * S * world
+    tps = tokens / dt
+    fpt = cfg.flops_per_token(S, recompute=False)
+    mfu = tps * fpt / (PEAK_BF16 * world)
+    log(f"[gpt] loss={float(state['loss']):.4f} step={dt / args.steps * 1000:.1f}ms tokens/s={tps:.0f} "
+        f"MFU(6N model flops)={mfu * 100:.1f}% mem={torch.cuda.max_memory_allocated() / 2**30:.1f}GiB")
+    del model, opt, ids, lbl
+    torch.cuda.empty_cache()
+    return tps, dt / args.steps * 1000, B * args.accum * world, mfu
+
+
+def resnet_bench(args, paddle, world, dist_on):
+    from paddlepaddle_amd.vision.models import resnet50
+    paddle.seed(99)
+    model = resnet50(num_classes=1000, data_format="NHWC")
+    opt = paddle.optimizer.Momentum(learning_rate=0.1, momentum=0.9, parameters=model.parameters(),
+                                    weight_decay=1e-4, multi_precision=True)
+    model, opt = paddle.amp.decorate(model, opt, level="O2", dtype="bfloat16")
+    if world > 1:
+        model = paddle.DataParallel(model)
+    B = args.resnet_batch
+    x = paddle.Tensor(torch.randn(B, 224, 224, 3, device="cuda", dtype=torch.bfloat16))
+    y = paddle.Tensor(torch.randint(0, 1000, (B,), device="cuda"))
+
+    def step():
+        with paddle.amp.auto_cast(level="O2", dtype="bfloat16"):
+            out = model(x)
+        loss = paddle.nn.functional.cross_entropy(out.astype("float32"), y)
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+
+    dt = timed(step, args.resnet_steps, max(args.warmup, 3), dist_on)
+    ips = args.resnet_steps * B * world / dt
+    log(f"[resnet50] step={dt / args.resnet_steps * 1000:.1f}ms img/s={ips:.0f}")
+    return ips
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    import paddlepaddle_amd as paddle
+    dist_on = world > 1
+    if dist_on:
+        paddle.distributed.init_parallel_env()
+    else:
+        torch.cuda.set_device(0)
+    tps = step_ms = gb = mfu = None
+    if not args.skip_gpt:
+        tps, step_ms, gb, mfu = gpt_bench(args, paddle, world, dist_on)
+    ips = resnet_bench(args, paddle, world, dist_on) if args.resnet else None
+    if int(os.environ.get("RANK", "0")) == 0:
+        par = (f"sharding{args.sharding_stage}_dp{world}" if world > 1 else "single") + \
+              (f"_tp{args.tp}" if args.tp > 1 else "")
+        line = {
+            "metric": BASELINE_METRIC,
+            "value": round(tps, 1) if tps is not None else None,
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(step_ms, 2) if step_ms is not None else None,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic tokens/images, random-init weights",
+            "config": {"model": f"GPT-3 {args.model.split('-')[-1].upper()} (h5120 L40 a40 ffn20480 V50304)"
+                       if args.model == "gpt3-13b" else args.model,
+                       "global_batch": gb, "seq_len": args.seq_len, "micro_batch": args.micro_batch,
+                       "accum_steps": args.accum, "parallelism": par, "recompute": bool(args.recompute),
+                       "optimizer": "AdamW fp32-master fused HIP", "amp": "O2 bf16"},
+            "mfu_6N": round(mfu, 4) if mfu is not None else None,
+            "secondary": {"metric": "ResNet50 img/s (bf16 NHWC, DP)", "value": round(ips, 1) if ips else None,
+                          "per_gpu_batch": args.resnet_batch},
+        }
+        print(json.dumps(line), flush=True)
+    if dist_on:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

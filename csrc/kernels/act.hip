@@ -1,0 +1,224 @@
+// Elementwise activation kernels + fused rotary embedding for gfx950.
+// Reference behaviour: paddle/phi/kernels/gpu/gelu_kernel.cu, fusion/gpu/fused_bias_act_kernel.cu,
+// incubate swiglu, fusion/gpu/fused_rope_kernel.cu.
+// All kernels: 16-byte vectors per thread, grid-stride, grid capped at 256 CUs x 8 workgroups.
+#include "common.h"
+
+using namespace pa;
+
+namespace {
+
+constexpr float kSqrt2OverPi = 0.7978845608028654f;
+constexpr float kCoeff = 0.044715f;
+constexpr float kInvSqrt2 = 0.7071067811865476f;
+constexpr float kInvSqrt2Pi = 0.3989422804014327f;
+
+__device__ __forceinline__ float gelu_f(float x, bool approx) {
+  if (approx) {
+    const float u = kSqrt2OverPi * (x + kCoeff * x * x * x);
+    return 0.5f * x * (1.f + tanhf(u));
+  }
+  return 0.5f * x * (1.f + erff(x * kInvSqrt2));
+}
+
+__device__ __forceinline__ float gelu_grad_f(float x, bool approx) {
+  if (approx) {
+    const float u = kSqrt2OverPi * (x + kCoeff * x * x * x);
+    const float t = tanhf(u);
+    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kSqrt2OverPi * (1.f + 3.f * kCoeff * x * x);
+  }
+  return 0.5f * (1.f + erff(x * kInvSqrt2)) + x * kInvSqrt2Pi * __expf(-0.5f * x * x);
+}
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
+
+inline unsigned grid_for(int64_t nvec) {
+  int64_t g = cdiv(nvec, 256);
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void gelu_fwd_k(const T* __restrict__ x, T* __restrict__ y, int64_t nvec, bool approx) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    float v[8];
+    load8<T>(x + i * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = gelu_f(v[j], approx);
+    store8<T>(y + i * 8, v);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void gelu_bwd_k(const T* __restrict__ x, const T* __restrict__ dy, T* __restrict__ dx,
+                                                  int64_t nvec, bool approx) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    float v[8], g[8];
+    load8<T>(x + i * 8, v);
+    load8<T>(dy + i * 8, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = g[j] * gelu_grad_f(v[j], approx);
+    store8<T>(dx + i * 8, v);
+  }
+}
+
+// y[r, c] = gelu_tanh(x[r, c] + b[c])
+template <typename T>
+__global__ __launch_bounds__(256) void bias_gelu_fwd_k(const T* __restrict__ x, const T* __restrict__ b,
+                                                       T* __restrict__ y, int64_t nvec, int64_t cols) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    float v[8], bv[8];
+    load8<T>(x + i * 8, v);
+    load8<T>(b + (i * 8) % cols, bv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = gelu_f(v[j] + bv[j], true);
+    store8<T>(y + i * 8, v);
+  }
+}
+
+// y = silu(a) * b over [rows, cols]; a, b have row stride `ld` (halves of a [rows, 2*cols] buffer allowed)
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_fwd_k(const T* __restrict__ a, const T* __restrict__ b, T* __restrict__ y,
+                                                    int64_t rows, int64_t cols, int64_t ld) {
+  const int64_t vpr = cols / 8, nvec = rows * vpr;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / vpr, c = (i % vpr) * 8;
+    float av[8], bv[8];
+    load8<T>(a + r * ld + c, av);
+    load8<T>(b + r * ld + c, bv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) av[j] = silu_f(av[j]) * bv[j];
+    store8<T>(y + r * cols + c, av);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void swiglu_bwd_k(const T* __restrict__ a, const T* __restrict__ b,
+                                                    const T* __restrict__ dy, T* __restrict__ da, T* __restrict__ db,
+                                                    int64_t rows, int64_t cols, int64_t ld, int64_t ldo) {
+  const int64_t vpr = cols / 8, nvec = rows * vpr;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / vpr, c = (i % vpr) * 8;
+    float av[8], bv[8], g[8], oa[8], ob[8];
+    load8<T>(a + r * ld + c, av);
+    load8<T>(b + r * ld + c, bv);
+    load8<T>(dy + r * cols + c, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float s = 1.f / (1.f + __expf(-av[j]));
+      ob[j] = g[j] * av[j] * s;
+      oa[j] = g[j] * bv[j] * s * (1.f + av[j] * (1.f - s));
+    }
+    store8<T>(da + r * ldo + c, oa);
+    store8<T>(db + r * ldo + c, ob);
+  }
+}
+
+// Rotary embedding on x [B,S,H,D]; cos/sin fp32 [>=S, D].
+// neox: rotate halves (d, d+D/2); else interleaved pairs (2i, 2i+1). inverse: use -sin (backward).
+template <typename T, bool NEOX>
+__global__ __launch_bounds__(256) void rope_k(const T* __restrict__ x, const float* __restrict__ cs,
+                                              const float* __restrict__ sn, T* __restrict__ out, int64_t B, int64_t S,
+                                              int64_t H, int64_t D, float sgn) {
+  // NEOX: one thread handles 8 elements of the first half and the matching 8 of the second half
+  const int64_t per_row = NEOX ? D / 16 : D / 8;
+  const int64_t n = B * S * H * per_row;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t row = i / per_row;          // (b, s, h)
+    const int64_t k = i % per_row;
+    const int64_t s = (row / H) % S;
+    const T* xr = x + row * D;
+    T* orow = out + row * D;
+    if (NEOX) {
+      const int64_t d0 = k * 8, d1 = d0 + D / 2;
+      float a[8], b[8], oa[8], ob[8];
+      load8<T>(xr + d0, a);
+      load8<T>(xr + d1, b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float c0 = cs[s * D + d0 + j], s0 = sn[s * D + d0 + j] * sgn;
+        const float c1 = cs[s * D + d1 + j], s1 = sn[s * D + d1 + j] * sgn;
+        oa[j] = a[j] * c0 - b[j] * s0;
+        ob[j] = b[j] * c1 + a[j] * s1;
+      }
+      store8<T>(orow + d0, oa);
+      store8<T>(orow + d1, ob);
+    } else {
+      const int64_t d0 = k * 8;
+      float a[8], o[8];
+      load8<T>(xr + d0, a);
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const float c0 = cs[s * D + d0 + j], s0 = sn[s * D + d0 + j] * sgn;
+        const float c1 = cs[s * D + d0 + j + 1], s1 = sn[s * D + d0 + j + 1] * sgn;
+        o[j] = a[j] * c0 - a[j + 1] * s0;
+        o[j + 1] = a[j + 1] * c1 + a[j] * s1;
+      }
+      store8<T>(orow + d0, o);
+    }
+  }
+}
+
+}  // namespace
+
+PA_EXPORT int pa_gelu_fwd(const void* x, void* y, int64_t n, int approx, int dtype, hipStream_t st) {
+  const int64_t nvec = n / 8;
+  PA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((gelu_fwd_k<T>), dim3(grid_for(nvec)), dim3(256), 0, st,
+                                                 (const T*)x, (T*)y, nvec, approx != 0));
+  PA_CHECK_LAUNCH();
+  return 0;
+}
+
+PA_EXPORT int pa_gelu_bwd(const void* x, const void* dy, void* dx, int64_t n, int approx, int dtype, hipStream_t st) {
+  const int64_t nvec = n / 8;
+  PA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((gelu_bwd_k<T>), dim3(grid_for(nvec)), dim3(256), 0, st,
+                                                 (const T*)x, (const T*)dy, (T*)dx, nvec, approx != 0));
+  PA_CHECK_LAUNCH();
+  return 0;
+}
+
+PA_EXPORT int pa_bias_gelu_fwd(const void* x, const void* b, void* y, int64_t rows, int64_t cols, int dtype,
+                               hipStream_t st) {
+  const int64_t nvec = rows * cols / 8;
+  PA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((bias_gelu_fwd_k<T>), dim3(grid_for(nvec)), dim3(256), 0, st,
+                                                 (const T*)x, (const T*)b, (T*)y, nvec, cols));
+  PA_CHECK_LAUNCH();
+  return 0;
+}
+
+PA_EXPORT int pa_swiglu_fwd(const void* a, const void* b, void* y, int64_t rows, int64_t cols, int64_t ld, int dtype,
+                            hipStream_t st) {
+  const int64_t nvec = rows * cols / 8;
+  PA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((swiglu_fwd_k<T>), dim3(grid_for(nvec)), dim3(256), 0, st,
+                                                 (const T*)a, (const T*)b, (T*)y, rows, cols, ld));
+  PA_CHECK_LAUNCH();
+  return 0;
+}
+
+PA_EXPORT int pa_swiglu_bwd(const void* a, const void* b, const void* dy, void* da, void* db, int64_t rows,
+                            int64_t cols, int64_t ld_packed, int dtype, hipStream_t st) {
+  const int64_t ld = ld_packed & 0xffffffffLL, ldo = (ld_packed >> 32) & 0xffffffffLL;
+  const int64_t nvec = rows * cols / 8;
+  PA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((swiglu_bwd_k<T>), dim3(grid_for(nvec)), dim3(256), 0, st,
+                                                 (const T*)a, (const T*)b, (const T*)dy, (T*)da, (T*)db, rows, cols,
+                                                 ld, ldo));
+  PA_CHECK_LAUNCH();
+  return 0;
+}
+
+PA_EXPORT int pa_rope_fwd(const void* x, const float* cs, const float* sn, void* out, int64_t B, int64_t S, int64_t H,
+                          int64_t D, int flags, int dtype, hipStream_t st) {
+  const bool neox = flags & 1;
+  const float sgn = (flags & 2) ? -1.f : 1.f;
+  const int64_t n = B * S * H * (neox ? D / 16 : D / 8);
+  if (neox) {
+    PA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((rope_k<T, true>), dim3(grid_for(n)), dim3(256), 0, st,
+                                                   (const T*)x, cs, sn, (T*)out, B, S, H, D, sgn));
+  } else {
+    PA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((rope_k<T, false>), dim3(grid_for(n)), dim3(256), 0, st,
+                                                   (const T*)x, cs, sn, (T*)out, B, S, H, D, sgn));
+  }
+  PA_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,34 @@
+"""paddle.device. Reference: python/paddle/device/__init__.py. 'gpu' = HIP device (MI355X)."""
+from __future__ import annotations
+
+import torch
+
+from ..framework.place import (set_device, get_device, is_compiled_with_cuda, is_compiled_with_rocm,  # noqa: F401
+                               is_compiled_with_xpu, is_compiled_with_ipu, is_compiled_with_cinn,
+                               is_compiled_with_custom_device, CPUPlace, CUDAPlace)
+from . import cuda  # noqa: F401
+from .cuda import Stream, Event, current_stream, stream_guard, synchronize  # noqa: F401
+
+
+def get_all_device_type():
+    return ["cpu", "gpu"] if torch.cuda.is_available() else ["cpu"]
+
+
+def get_all_custom_device_type():
+    return []
+
+
+def get_available_device():
+    return ["cpu"] + [f"gpu:{i}" for i in range(torch.cuda.device_count())]
+
+
+def get_available_custom_device():
+    return []
+
+
+def get_cudnn_version():
+    return None
+
+
+def device_count():
+    return torch.cuda.device_count()

@@ -1,0 +1,59 @@
+"""Global flags. Reference: paddle/common/flags.cc, paddle.set_flags/get_flags."""
+from __future__ import annotations
+
+import os
+
+_FLAGS = {
+    "FLAGS_check_nan_inf": False,
+    "FLAGS_check_nan_inf_level": 0,
+    "FLAGS_use_hip_kernels": True,        # route hot ops to hand-written HIP kernels
+    "FLAGS_cudnn_deterministic": False,
+    "FLAGS_embedding_deterministic": 0,
+    "FLAGS_fraction_of_gpu_memory_to_use": 0.92,
+    "FLAGS_allocator_strategy": "auto_growth",
+    "FLAGS_eager_delete_tensor_gb": 0.0,
+    "FLAGS_use_cuda_graph": False,
+    "FLAGS_enable_pir_api": False,
+    "FLAGS_print_ir": False,
+    "FLAGS_call_stack_level": 1,
+    "FLAGS_dp_bucket_mb": 128,            # DataParallel fused all-reduce bucket (xGMI ring friendly)
+    "FLAGS_sharding_bucket_mb": 256,
+}
+
+for _k in list(_FLAGS):
+    if _k in os.environ:
+        _v = os.environ[_k]
+        _d = _FLAGS[_k]
+        if isinstance(_d, bool):
+            _FLAGS[_k] = _v.lower() in ("1", "true", "yes")
+        elif isinstance(_d, int):
+            _FLAGS[_k] = int(_v)
+        elif isinstance(_d, float):
+            _FLAGS[_k] = float(_v)
+        else:
+            _FLAGS[_k] = _v
+
+
+def _norm(k):
+    return k if k.startswith("FLAGS_") else "FLAGS_" + k
+
+
+def set_flags(flags: dict):
+    for k, v in flags.items():
+        _FLAGS[_norm(k)] = v
+
+
+def get_flags(flags):
+    if isinstance(flags, str):
+        flags = [flags]
+    out = {}
+    for k in flags:
+        k = _norm(k)
+        if k not in _FLAGS:
+            raise ValueError(f"flag {k} not found")
+        out[k] = _FLAGS[k]
+    return out
+
+
+def flag(k, default=None):
+    return _FLAGS.get(_norm(k), default)

@@ -1,0 +1,2 @@
+"""Model zoo used by the benchmarks (GPT-3, LLaMA, ResNet)."""
+from .gpt import GPTConfig, GPTModel, GPTForPretraining, GPTPretrainingCriterion  # noqa: F401

@@ -1,0 +1,254 @@
+"""GPT-3 family (1.3B / 6.7B / 13B / 175B shapes) — the flagship training model.
+
+Reference model: test/deprecated/auto_parallel/auto_parallel_gpt_model.py:602 (GPTModel),
+:740 (GPTForPretraining), :829 (GPTPretrainingCriterion); PaddleNLP gpt3 configs (pre-LN, GELU,
+learned absolute positions, tied input/output embedding).
+
+MI355X-native layer (per decoder block):
+  LN (HIP norm kernel) → fused QKV GEMM (hipBLASLt, bias in epilogue) → flash attention on
+  [B,S,H,D] views of the QKV buffer (HIP MFMA kernel, causal) → out-proj GEMM → dropout+residual
+  → LN → FFN1 GEMM + fused bias-GELU (HIP) → FFN2 GEMM → dropout+residual.
+Tensor parallel (mp_degree>1): QKV/FFN1 column-parallel, out-proj/FFN2 row-parallel, vocab-parallel
+embedding + parallel cross-entropy (parallel/tensor_parallel.py). Activation recompute per block.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+
+import torch
+
+from .. import nn
+from ..framework.tensor import Tensor, _wrap
+from ..nn import functional as F
+from ..nn import initializer as I
+from .. import ops as _ops
+
+
+@dataclasses.dataclass
+class GPTConfig:
+    vocab_size: int = 50304
+    hidden_size: int = 5120
+    num_hidden_layers: int = 40
+    num_attention_heads: int = 40
+    intermediate_size: int = 20480
+    max_position_embeddings: int = 2048
+    hidden_dropout_prob: float = 0.1
+    attention_probs_dropout_prob: float = 0.0
+    initializer_range: float = 0.02
+    layer_norm_eps: float = 1e-5
+    tie_word_embeddings: bool = True
+    use_recompute: bool = False
+    recompute_granularity: str = "full"
+    tensor_parallel_degree: int = 1
+    sequence_parallel: bool = False
+    fuse_attention_qkv: bool = True
+
+    @staticmethod
+    def gpt3_13b(**kw):
+        return GPTConfig(**kw)
+
+    @staticmethod
+    def gpt3_6_7b(**kw):
+        d = dict(hidden_size=4096, num_hidden_layers=32, num_attention_heads=32, intermediate_size=16384)
+        d.update(kw)
+        return GPTConfig(**d)
+
+    @staticmethod
+    def gpt3_1_3b(**kw):
+        d = dict(hidden_size=2048, num_hidden_layers=24, num_attention_heads=16, intermediate_size=8192)
+        d.update(kw)
+        return GPTConfig(**d)
+
+    @staticmethod
+    def gpt3_175b(**kw):
+        d = dict(hidden_size=12288, num_hidden_layers=96, num_attention_heads=96, intermediate_size=49152)
+        d.update(kw)
+        return GPTConfig(**d)
+
+    @staticmethod
+    def tiny(**kw):
+        d = dict(vocab_size=512, hidden_size=128, num_hidden_layers=2, num_attention_heads=2, intermediate_size=512,
+                 max_position_embeddings=128, hidden_dropout_prob=0.0)
+        d.update(kw)
+        return GPTConfig(**d)
+
+    def num_params(self):
+        h, L, f, V, P = (self.hidden_size, self.num_hidden_layers, self.intermediate_size, self.vocab_size,
+                         self.max_position_embeddings)
+        per_layer = 4 * h * h + 4 * h + 2 * h * f + f + h + 4 * h
+        return L * per_layer + V * h + P * h + 2 * h
+
+    def flops_per_token(self, seq_len, recompute=False):
+        """Training FLOPs per token: 6N (fwd+bwd GEMMs) + attention scores; +2N with full recompute."""
+        n = self.num_params() - self.max_position_embeddings * self.hidden_size
+        attn = 12 * self.num_hidden_layers * self.hidden_size * seq_len  # QK^T + PV fwd+bwd (causal halves it; count dense)
+        f = 6 * n + attn
+        if recompute:
+            f += 2 * n + attn / 3
+        return f
+
+
+def _tp():
+    from ..parallel import tensor_parallel as tp
+    return tp
+
+
+class GPTEmbeddings(nn.Layer):
+    def __init__(self, cfg: GPTConfig):
+        super().__init__()
+        init = I.Normal(0.0, cfg.initializer_range)
+        if cfg.tensor_parallel_degree > 1:
+            self.word_embeddings = _tp().VocabParallelEmbedding(cfg.vocab_size, cfg.hidden_size,
+                                                                weight_attr=nn.ParamAttr(initializer=init))
+        else:
+            self.word_embeddings = nn.Embedding(cfg.vocab_size, cfg.hidden_size,
+                                                weight_attr=nn.ParamAttr(initializer=init))
+        self.position_embeddings = nn.Embedding(cfg.max_position_embeddings, cfg.hidden_size,
+                                                weight_attr=nn.ParamAttr(initializer=init))
+        self.dropout = nn.Dropout(cfg.hidden_dropout_prob)
+
+    def forward(self, input_ids, position_ids=None):
+        if position_ids is None:
+            S = input_ids.shape[-1]
+            position_ids = _wrap(torch.arange(S, device=input_ids._t.device).unsqueeze(0))
+        x = self.word_embeddings(input_ids) + self.position_embeddings(position_ids)
+        return self.dropout(x)
+
+
+class GPTAttention(nn.Layer):
+    def __init__(self, cfg: GPTConfig):
+        super().__init__()
+        h = cfg.hidden_size
+        self.num_heads = cfg.num_attention_heads
+        self.head_dim = h // self.num_heads
+        self.tp = cfg.tensor_parallel_degree
+        init = I.Normal(0.0, cfg.initializer_range)
+        out_init = I.Normal(0.0, cfg.initializer_range / math.sqrt(2.0 * cfg.num_hidden_layers))
+        if self.tp > 1:
+            tp = _tp()
+            self.qkv_proj = tp.ColumnParallelLinear(h, 3 * h, weight_attr=nn.ParamAttr(initializer=init),
+                                                    has_bias=True, gather_output=False)
+            self.out_proj = tp.RowParallelLinear(h, h, weight_attr=nn.ParamAttr(initializer=out_init),
+                                                 has_bias=True, input_is_parallel=True)
+            self.local_heads = self.num_heads // self.tp
+        else:
+            self.qkv_proj = nn.Linear(h, 3 * h, weight_attr=nn.ParamAttr(initializer=init))
+            self.out_proj = nn.Linear(h, h, weight_attr=nn.ParamAttr(initializer=out_init))
+            self.local_heads = self.num_heads
+        self.attn_dropout = cfg.attention_probs_dropout_prob
+
+    def forward(self, x):
+        qkv = self.qkv_proj(x)._t  # [B, S, 3*h_local]
+        B, S = qkv.shape[0], qkv.shape[1]
+        qkv = qkv.view(B, S, self.local_heads, 3, self.head_dim)
+        q, k, v = qkv[:, :, :, 0], qkv[:, :, :, 1], qkv[:, :, :, 2]
+        o = _ops.flash_attention(q, k, v, causal=True, dropout=self.attn_dropout, training=self.training)
+        o = o.reshape(B, S, self.local_heads * self.head_dim)
+        return self.out_proj(_wrap(o))
+
+
+class GPTMLP(nn.Layer):
+    def __init__(self, cfg: GPTConfig):
+        super().__init__()
+        h, f = cfg.hidden_size, cfg.intermediate_size
+        init = I.Normal(0.0, cfg.initializer_range)
+        out_init = I.Normal(0.0, cfg.initializer_range / math.sqrt(2.0 * cfg.num_hidden_layers))
+        self.tp = cfg.tensor_parallel_degree
+        if self.tp > 1:
+            tp = _tp()
+            self.linear1 = tp.ColumnParallelLinear(h, f, weight_attr=nn.ParamAttr(initializer=init), has_bias=True,
+                                                   gather_output=False, fuse_bias_act="gelu")
+            self.linear2 = tp.RowParallelLinear(f, h, weight_attr=nn.ParamAttr(initializer=out_init), has_bias=True,
+                                                input_is_parallel=True)
+        else:
+            self.linear1 = nn.Linear(h, f, weight_attr=nn.ParamAttr(initializer=init))
+            self.linear2 = nn.Linear(f, h, weight_attr=nn.ParamAttr(initializer=out_init))
+
+    def forward(self, x):
+        if self.tp > 1:
+            h = self.linear1(x)
+        else:
+            w, b = self.linear1.weight._t, self.linear1.bias._t
+            xt = x._t
+            if xt.dtype != w.dtype:
+                xt = xt.to(w.dtype)
+            h = _wrap(_ops.fused_linear(xt, w, b, act="gelu"))
+        return self.linear2(h)
+
+
+class GPTDecoderLayer(nn.Layer):
+    def __init__(self, cfg: GPTConfig):
+        super().__init__()
+        self.norm1 = nn.LayerNorm(cfg.hidden_size, epsilon=cfg.layer_norm_eps)
+        self.self_attn = GPTAttention(cfg)
+        self.norm2 = nn.LayerNorm(cfg.hidden_size, epsilon=cfg.layer_norm_eps)
+        self.mlp = GPTMLP(cfg)
+        self.dropout1 = nn.Dropout(cfg.hidden_dropout_prob)
+        self.dropout2 = nn.Dropout(cfg.hidden_dropout_prob)
+
+    def forward(self, x):
+        x = x + self.dropout1(self.self_attn(self.norm1(x)))
+        x = x + self.dropout2(self.mlp(self.norm2(x)))
+        return x
+
+
+class GPTModel(nn.Layer):
+    def __init__(self, cfg: GPTConfig):
+        super().__init__()
+        self.config = cfg
+        self.embeddings = GPTEmbeddings(cfg)
+        self.layers = nn.LayerList([GPTDecoderLayer(cfg) for _ in range(cfg.num_hidden_layers)])
+        self.norm = nn.LayerNorm(cfg.hidden_size, epsilon=cfg.layer_norm_eps)
+
+    def forward(self, input_ids, position_ids=None):
+        x = self.embeddings(input_ids, position_ids)
+        rc = self.config.use_recompute and self.training
+        if rc:
+            from ..distributed.fleet.recompute import recompute
+        for layer in self.layers:
+            x = recompute(layer, x) if rc else layer(x)
+        return self.norm(x)
+
+
+class GPTForPretraining(nn.Layer):
+    def __init__(self, cfg: GPTConfig):
+        super().__init__()
+        self.config = cfg
+        self.gpt = GPTModel(cfg)
+        if not cfg.tie_word_embeddings:
+            self.lm_head_weight = self.create_parameter([cfg.vocab_size // max(cfg.tensor_parallel_degree, 1),
+                                                         cfg.hidden_size],
+                                                        default_initializer=I.Normal(0.0, cfg.initializer_range))
+
+    def forward(self, input_ids, position_ids=None):
+        h = self.gpt(input_ids, position_ids)
+        w = self.gpt.embeddings.word_embeddings.weight if self.config.tie_word_embeddings else self.lm_head_weight
+        ht, wt = h._t, w._t
+        if ht.dtype != wt.dtype:
+            ht = ht.to(wt.dtype)
+        if self.config.tensor_parallel_degree > 1:
+            ht = _tp().c_identity(ht)
+        logits = torch.matmul(ht, wt.t())  # [B, S, V(_local)]
+        return _wrap(logits)
+
+
+class GPTPretrainingCriterion(nn.Layer):
+    """Mean token cross-entropy (fused HIP softmax-CE; vocab-parallel CE under TP)."""
+
+    def __init__(self, cfg: GPTConfig = None, ignore_index=-100):
+        super().__init__()
+        self.cfg = cfg
+        self.ignore_index = ignore_index
+
+    def forward(self, logits, labels, loss_mask=None):
+        lt = logits._t
+        if self.cfg is not None and self.cfg.tensor_parallel_degree > 1:
+            per_tok = _tp().parallel_cross_entropy_raw(lt, labels._t, self.ignore_index)
+        else:
+            per_tok = _ops.softmax_cross_entropy(lt, labels._t, self.ignore_index)
+        if loss_mask is not None:
+            m = loss_mask._t.reshape(per_tok.shape).float()
+            return _wrap((per_tok * m).sum() / m.sum().clamp_min(1.0))
+        valid = (labels._t != self.ignore_index).sum().clamp_min(1)
+        return _wrap(per_tok.sum() / valid)

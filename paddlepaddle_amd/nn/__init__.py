@@ -1,0 +1,7 @@
+"""paddle.nn. Reference: python/paddle/nn/__init__.py."""
+from . import functional, initializer, utils  # noqa: F401
+from .layer import *  # noqa: F401,F403
+from .layer.layers import Layer, ParamAttr  # noqa: F401
+from .clip import ClipGradByGlobalNorm, ClipGradByNorm, ClipGradByValue  # noqa: F401
+from ..framework.tensor import Parameter  # noqa: F401
+from . import quant  # noqa: F401

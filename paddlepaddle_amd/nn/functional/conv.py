@@ -1,0 +1,150 @@
+"""Convolutions. Reference: python/paddle/nn/functional/conv.py, phi/kernels/gpu/conv_kernel.cu (cuDNN).
+
+MI355X path: MIOpen through ATen with NHWC (channels_last) bf16 tensors — NHWC data_format is a
+zero-copy view here (logical NCHW with channels-last strides), which is what MIOpen's fast
+implicit-GEMM/Winograd solvers want on CDNA.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ...amp.state import maybe_cast
+from ...framework.tensor import Tensor, _wrap
+from ...tensor._helpers import T
+
+
+def _tuple(v, n):
+    if isinstance(v, (list, tuple)):
+        return tuple(int(x) for x in v)
+    return (int(v),) * n
+
+
+def _padding(padding, n, x_spatial, k_spatial, stride, dilation):
+    """Return (torch_padding, pre_pad) where pre_pad is an explicit asymmetric F.pad list or None."""
+    if isinstance(padding, str):
+        p = padding.upper()
+        if p == "VALID":
+            return 0, None
+        if p == "SAME":
+            pads = []
+            for xs, ks, st, dl in zip(x_spatial, k_spatial, stride, dilation):
+                out = (xs + st - 1) // st
+                total = max((out - 1) * st + (ks - 1) * dl + 1 - xs, 0)
+                pads.append((total // 2, total - total // 2))
+            if all(a == b for a, b in pads):
+                return tuple(a for a, _ in pads), None
+            flat = []
+            for a, b in reversed(pads):
+                flat += [a, b]
+            return 0, flat
+    if isinstance(padding, (list, tuple)):
+        if len(padding) and isinstance(padding[0], (list, tuple)):
+            sp = [tuple(p) for p in padding]
+            sp = [p for p in sp if True]
+            # [[0,0],[0,0],[t,b],[l,r]] (NCHW) or [[0,0],[t,b],[l,r],[0,0]] (NHWC)
+            sp = [p for p in sp][-n - 1:-1] if len(sp) == n + 2 and tuple(sp[-1]) == (0, 0) and tuple(sp[1]) != (0, 0) else sp[-n:]
+            if all(a == b for a, b in sp):
+                return tuple(a for a, _ in sp), None
+            flat = []
+            for a, b in reversed(sp):
+                flat += [a, b]
+            return 0, flat
+        if len(padding) == 2 * n:
+            pairs = [(padding[2 * i], padding[2 * i + 1]) for i in range(n)]
+            if all(a == b for a, b in pairs):
+                return tuple(a for a, _ in pairs), None
+            flat = []
+            for a, b in reversed(pairs):
+                flat += [a, b]
+            return 0, flat
+        return tuple(int(p) for p in padding), None
+    return int(padding), None
+
+
+def _to_cf(t, data_format, n):
+    """channel-last logical -> channel-first logical (zero-copy view)."""
+    if data_format in ("NHWC", "NLC", "NDHWC"):
+        return t.permute(0, n + 1, *range(1, n + 1)), True
+    return t, False
+
+
+def _from_cf(t, cl, n):
+    if cl:
+        return t.permute(0, *range(2, n + 2), 1)
+    return t
+
+
+def _convnd(n, x, weight, bias, stride, padding, dilation, groups, data_format):
+    t = T(x)
+    w = T(weight)
+    t, w = maybe_cast("conv2d", t, w)
+    b = T(bias)
+    if b is not None and b.dtype != w.dtype:
+        b = b.to(w.dtype)
+    t, cl = _to_cf(t, data_format, n)
+    stride = _tuple(stride, n)
+    dilation = _tuple(dilation, n)
+    pad, pre = _padding(padding, n, t.shape[2:], w.shape[2:], stride, dilation)
+    if pre is not None:
+        t = F.pad(t, pre)
+    if cl and n == 2 and not w.is_contiguous(memory_format=torch.channels_last):
+        w = w.contiguous(memory_format=torch.channels_last)
+    fn = {1: F.conv1d, 2: F.conv2d, 3: F.conv3d}[n]
+    out = fn(t, w, b, stride, pad, dilation, groups)
+    return _wrap(_from_cf(out, cl, n))
+
+
+def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NCL", name=None):
+    return _convnd(1, x, weight, bias, stride, padding, dilation, groups, data_format)
+
+
+def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NCHW", name=None):
+    return _convnd(2, x, weight, bias, stride, padding, dilation, groups, data_format)
+
+
+def conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NCDHW", name=None):
+    return _convnd(3, x, weight, bias, stride, padding, dilation, groups, data_format)
+
+
+def _conv_transpose_nd(n, x, weight, bias, stride, padding, output_padding, dilation, groups, output_size,
+                       data_format):
+    t = T(x)
+    w = T(weight)
+    t, w = maybe_cast("conv2d_transpose", t, w)
+    b = T(bias)
+    if b is not None and b.dtype != w.dtype:
+        b = b.to(w.dtype)
+    t, cl = _to_cf(t, data_format, n)
+    stride = _tuple(stride, n)
+    dilation = _tuple(dilation, n)
+    if isinstance(padding, str):
+        padding = 0 if padding.upper() == "VALID" else tuple((k - 1) * d // 2 for k, d in zip(w.shape[2:], dilation))
+    pad = _tuple(padding, n) if not (isinstance(padding, (list, tuple)) and len(padding) == 2 * n) else \
+        tuple(padding[2 * i] for i in range(n))
+    op = _tuple(output_padding, n)
+    if output_size is not None:
+        osz = _tuple(output_size, n) if not isinstance(output_size, Tensor) else tuple(output_size._t.tolist())
+        op = tuple(o - ((i - 1) * s - 2 * p + d * (k - 1) + 1) for o, i, s, p, d, k in
+                   zip(osz, t.shape[2:], stride, pad, dilation, w.shape[2:]))
+    fn = {1: F.conv_transpose1d, 2: F.conv_transpose2d, 3: F.conv_transpose3d}[n]
+    out = fn(t, w, b, stride, pad, op, groups, dilation)
+    return _wrap(_from_cf(out, cl, n))
+
+
+def conv1d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1, dilation=1,
+                     output_size=None, data_format="NCL", name=None):
+    return _conv_transpose_nd(1, x, weight, bias, stride, padding, output_padding, dilation, groups,
+                              output_size, data_format)
+
+
+def conv2d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0, dilation=1, groups=1,
+                     output_size=None, data_format="NCHW", name=None):
+    return _conv_transpose_nd(2, x, weight, bias, stride, padding, output_padding, dilation, groups,
+                              output_size, data_format)
+
+
+def conv3d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1, dilation=1,
+                     output_size=None, data_format="NCDHW", name=None):
+    return _conv_transpose_nd(3, x, weight, bias, stride, padding, output_padding, dilation, groups,
+                              output_size, data_format)

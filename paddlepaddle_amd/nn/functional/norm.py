@@ -1,0 +1,90 @@
+"""Normalisation. Reference: python/paddle/nn/functional/norm.py, phi layer_norm/rms_norm/batch_norm kernels.
+layer_norm / rms_norm run on the HIP kernels in csrc/kernels/norm.hip."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from ...framework.tensor import Tensor, _wrap
+from ...tensor._helpers import T
+from ... import ops as _ops
+
+
+def layer_norm(x, normalized_shape, weight=None, bias=None, epsilon=1e-05, name=None):
+    t = T(x)
+    if isinstance(normalized_shape, int):
+        normalized_shape = [normalized_shape]
+    ns = list(normalized_shape)
+    w, b = T(weight), T(bias)
+    if len(ns) == 1:
+        return _wrap(_ops.layer_norm(t, w, b, epsilon))
+    n = int(np.prod(ns))
+    y = _ops.layer_norm(t.reshape(*t.shape[: t.dim() - len(ns)], n), None if w is None else w.reshape(n),
+                        None if b is None else b.reshape(n), epsilon)
+    return _wrap(y.reshape(t.shape))
+
+
+def rms_norm(x, normalized_shape=None, weight=None, epsilon=1e-6, name=None):
+    t = T(x)
+    return _wrap(_ops.rms_norm(t, T(weight), epsilon))
+
+
+def batch_norm(x, running_mean, running_var, weight=None, bias=None, training=False, momentum=0.9,
+               epsilon=1e-05, data_format="NCHW", use_global_stats=None, name=None):
+    t = T(x)
+    cl = data_format in ("NHWC", "NLC", "NDHWC")
+    nd = t.dim()
+    if cl:
+        t = t.permute(0, nd - 1, *range(1, nd - 1))
+    use_batch = training and not use_global_stats
+    rm, rv = T(running_mean), T(running_var)
+    w, b = T(weight), T(bias)
+    if t.dtype in (torch.float16, torch.bfloat16) and w is not None and w.dtype != torch.float32:
+        w, b = w.float(), b.float() if b is not None else None
+    out = F.batch_norm(t, rm, rv, w, b, use_batch, 1.0 - momentum, epsilon)
+    if cl:
+        out = out.permute(0, *range(2, nd), 1)
+    return _wrap(out)
+
+
+def instance_norm(x, running_mean=None, running_var=None, weight=None, bias=None, use_input_stats=True,
+                  momentum=0.9, eps=1e-05, data_format="NCHW", name=None):
+    t = T(x)
+    cl = data_format in ("NHWC", "NLC", "NDHWC")
+    nd = t.dim()
+    if cl:
+        t = t.permute(0, nd - 1, *range(1, nd - 1))
+    out = F.instance_norm(t, T(running_mean), T(running_var), T(weight), T(bias), use_input_stats,
+                          1.0 - momentum, eps)
+    if cl:
+        out = out.permute(0, *range(2, nd), 1)
+    return _wrap(out)
+
+
+def group_norm(x, num_groups, epsilon=1e-05, weight=None, bias=None, data_format="NCHW", name=None):
+    t = T(x)
+    cl = data_format in ("NHWC", "NLC", "NDHWC")
+    nd = t.dim()
+    if cl:
+        t = t.permute(0, nd - 1, *range(1, nd - 1))
+    out = F.group_norm(t, num_groups, T(weight), T(bias), epsilon)
+    if cl:
+        out = out.permute(0, *range(2, nd), 1)
+    return _wrap(out)
+
+
+def local_response_norm(x, size, alpha=1e-4, beta=0.75, k=1.0, data_format="NCHW", name=None):
+    t = T(x)
+    cl = data_format in ("NHWC", "NLC", "NDHWC")
+    nd = t.dim()
+    if cl:
+        t = t.permute(0, nd - 1, *range(1, nd - 1))
+    out = F.local_response_norm(t, size, alpha, beta, k)
+    if cl:
+        out = out.permute(0, *range(2, nd), 1)
+    return _wrap(out)
+
+
+def normalize(x, p=2, axis=1, epsilon=1e-12, name=None):
+    return _wrap(F.normalize(T(x), float(p), axis, epsilon))

@@ -1,0 +1,16 @@
+"""Hot-op layer: hand-written CDNA4 HIP kernels with autograd, plus the CPU reference paths.
+
+Every function here takes/returns *device buffers* (torch tensors) — the paddle Tensor wrapper is
+applied by the callers in ``nn.functional`` / ``incubate``. On a HIP device the kernel in
+``csrc/kernels`` runs (see ``_loader.hip_enabled_for``); on CPU the reference math runs.
+"""
+from __future__ import annotations
+
+from .activation import gelu, silu, swiglu, softmax, bias_gelu  # noqa: F401
+from .norm import rms_norm, layer_norm  # noqa: F401
+from .loss import softmax_cross_entropy  # noqa: F401
+from .attention import flash_attention, attention_reference  # noqa: F401
+from .rope import apply_rotary  # noqa: F401
+from .linear import fused_linear  # noqa: F401
+from . import optim  # noqa: F401
+from ._loader import has as has_kernel, hip_enabled_for, LIB_PATH  # noqa: F401

@@ -1,0 +1,171 @@
+"""Adam / AdamW. Reference: python/paddle/optimizer/{adam,adamw}.py, phi fused_adam_kernel.cu.
+
+On a HIP device every parameter group is updated by ONE multi-tensor kernel launch
+(ops.optim / csrc/kernels/adamw.hip): fp32 moments, optional fp32 master weights with the
+bf16/fp16 parameter rewritten in the same pass, per-tensor weight-decay and lr multipliers in
+the device table.
+"""
+from __future__ import annotations
+
+import struct
+
+import torch
+
+from ..ops import _loader as L
+from ..ops import optim as _opt
+from .optimizer import Optimizer
+
+
+def _f2i(x):
+    return struct.unpack("<i", struct.pack("<f", float(x)))[0]
+
+
+class Adam(Optimizer):
+    _acc_names = ("moment1", "moment2", "beta1_pow_acc", "beta2_pow_acc")
+    _decoupled = False
+
+    def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-08, parameters=None,
+                 weight_decay=None, grad_clip=None, lazy_mode=False, multi_precision=False, use_multi_tensor=False,
+                 amsgrad=False, name=None):
+        super().__init__(learning_rate, parameters, weight_decay, grad_clip, name, multi_precision)
+        self._beta1, self._beta2, self._epsilon = beta1, beta2, epsilon
+        self._amsgrad = amsgrad
+        self._tables = {}
+        self._param_step = {}
+
+    def _coeff_for(self, group, p):
+        return 0.0
+
+    def _hyper(self, group):
+        b1 = group.get("beta1", self._beta1)
+        b2 = group.get("beta2", self._beta2)
+        eps = group.get("epsilon", self._epsilon)
+        return float(b1), float(b2), float(eps)
+
+    def _update_group(self, group, params):
+        b1, b2, eps = self._hyper(group)
+        lr = self._group_lr(group)
+        steps = []
+        for p in params:
+            s = self._param_step.get(id(p), 0) + 1
+            self._param_step[id(p)] = s
+            steps.append(s)
+        dev_ok = L.hip_enabled_for(params[0]._t) and L.has("pa_adamw_multi") and not self._amsgrad
+        same_step = all(s == steps[0] for s in steps)
+        if dev_ok and same_step and (self._decoupled or not self._has_l2(group, params)):
+            self._fused(group, params, lr, b1, b2, eps, steps[0])
+            return
+        for p, s in zip(params, steps):
+            self._single(group, p, lr, b1, b2, eps, s)
+
+    def _has_l2(self, group, params):
+        return self.regularization is not None or "weight_decay" in group or \
+            any(getattr(p, "regularizer", None) is not None for p in params)
+
+    def _single(self, group, p, lr, b1, b2, eps, step):
+        master = self._master(p)
+        w = master if master is not None else p._t.detach()
+        g = p._t.grad.float()
+        if not self._decoupled:
+            g = self._regularized_grad(p, g, group)
+        m = self._acc("moment1", p)
+        v = self._acc("moment2", p)
+        plr = lr * (p.optimize_attr.get("learning_rate", 1.0) if hasattr(p, "optimize_attr") else 1.0)
+        coeff = self._coeff_for(group, p)
+        if coeff:
+            w.mul_(1.0 - plr * coeff)
+        m.mul_(b1).add_(g, alpha=1 - b1)
+        v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        bc1 = 1 - b1 ** step
+        bc2 = 1 - b2 ** step
+        if self._amsgrad:
+            vm = self._acc("moment2_max", p)
+            torch.maximum(vm, v, out=vm)
+            denom = (vm / bc2).sqrt_().add_(eps)
+        else:
+            denom = (v / bc2).sqrt_().add_(eps)
+        w.addcdiv_(m, denom, value=-plr / bc1)
+        if master is not None:
+            p._t.detach().copy_(master)
+        self._acc("beta1_pow_acc", p, shape=[1]).fill_(b1 ** step)
+        self._acc("beta2_pow_acc", p, shape=[1]).fill_(b2 ** step)
+
+    def _fused(self, group, params, lr, b1, b2, eps, step):
+        masters = [self._master(p) for p in params]
+        fp32 = [m if m is not None else p._t.detach() for p, m in zip(params, masters)]
+        grads = [p._t.grad for p in params]
+        key = (id(group), tuple(t.data_ptr() for t in fp32), tuple(g.data_ptr() for g in grads))
+        tab = self._tables.get(id(group))
+        if tab is None or tab[0] != key:
+            ms = [self._acc("moment1", p) for p in params]
+            vs = [self._acc("moment2", p) for p in params]
+            lowps = [p._t.detach() if m is not None else None for p, m in zip(params, masters)]
+            rows, items = [], []
+            for i, (w, g, m, v, lp, p) in enumerate(zip(fp32, grads, ms, vs, lowps, params)):
+                n = w.numel()
+                gdt = L._DT[g.dtype]
+                ldt = 3 if lp is None else L._DT[lp.dtype]
+                lr_mult = p.optimize_attr.get("learning_rate", 1.0) if hasattr(p, "optimize_attr") else 1.0
+                rows.append([w.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(),
+                             0 if lp is None else lp.data_ptr(), n, gdt | (ldt << 8),
+                             _f2i(self._coeff_for(group, p)), _f2i(lr_mult)])
+                for s in range(0, n, _opt._CHUNK):
+                    items.append([i, s])
+            dev = fp32[0].device
+            t_rows = torch.tensor(rows, dtype=torch.int64).to(dev, non_blocking=True)
+            t_items = torch.tensor(items, dtype=torch.int64).to(dev, non_blocking=True)
+            tab = (key, t_rows, t_items, len(items), fp32, grads)
+            self._tables[id(group)] = tab
+        _, t_rows, t_items, n_items, _, _ = tab
+        bc1 = 1 - b1 ** step
+        bc2 = 1 - b2 ** step
+        inv_scale = getattr(self, "_inv_scale_tensor", None)
+        L.call("pa_adamw_multi", L.ptr(t_rows), L.ptr(t_items), n_items, L.ptr(inv_scale), float(lr), float(b1),
+               float(b2), float(eps), 0.0, float(bc1), float(bc2), L.ptr(None), L.stream_ptr())
+        self._last_step = step
+
+    def state_dict(self):
+        # materialise beta-pow accumulators paddle-style
+        for p in self._parameter_list:
+            s = self._param_step.get(id(p))
+            if s:
+                b1, b2, _ = self._hyper({})
+                self._acc("beta1_pow_acc", p, shape=[1]).fill_(b1 ** s)
+                self._acc("beta2_pow_acc", p, shape=[1]).fill_(b2 ** s)
+        return super().state_dict()
+
+    def set_state_dict(self, state_dict):
+        super().set_state_dict(state_dict)
+        import math
+        b1 = self._beta1
+        for p in self._parameter_list:
+            d = self._accumulators.get("beta1_pow_acc", {})
+            if id(p) in d:
+                v = float(d[id(p)].reshape(-1)[0].item())
+                if 0 < v < 1 and 0 < b1 < 1:
+                    self._param_step[id(p)] = int(round(math.log(v) / math.log(b1)))
+        self._tables.clear()
+
+
+class AdamW(Adam):
+    _decoupled = True
+
+    def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8, parameters=None,
+                 weight_decay=0.01, lr_ratio=None, apply_decay_param_fun=None, grad_clip=None, lazy_mode=False,
+                 multi_precision=False, amsgrad=False, name=None):
+        super().__init__(learning_rate, beta1, beta2, epsilon, parameters, None, grad_clip, lazy_mode,
+                         multi_precision, False, amsgrad, name)
+        self._weight_decay = weight_decay
+        self._lr_ratio = lr_ratio
+        self._apply_decay_param_fun = apply_decay_param_fun
+
+    def _coeff_for(self, group, p):
+        wd = group.get("weight_decay", self._weight_decay)
+        if hasattr(wd, "_coeff"):
+            wd = wd._coeff
+        if self._apply_decay_param_fun is not None and not self._apply_decay_param_fun(p.name):
+            return 0.0
+        return float(wd or 0.0)
+
+    def _group_lr(self, group, param=None):
+        return super()._group_lr(group, None)

@@ -1,0 +1,192 @@
+"""Numerics of every hand-written HIP kernel against a plain PyTorch fp32 reference of the same op.
+Each test also asserts the native library is the code path that ran."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from paddlepaddle_amd import ops  # noqa: E402
+from paddlepaddle_amd.ops import _loader as L  # noqa: E402
+
+DEV = "cuda"
+
+
+def _lib_loaded():
+    assert L._LIB is not None, "HIP kernel library not loaded"
+
+
+def _tol(dt):
+    return {torch.float32: 2e-5, torch.bfloat16: 2e-2, torch.float16: 2e-3}[dt]
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("cols", [64, 512, 1000, 5120, 12288])
+def test_rms_norm(dt, cols):
+    torch.manual_seed(0)
+    x = torch.randn(37, cols, device=DEV, dtype=dt, requires_grad=True)
+    w = (torch.rand(cols, device=DEV) + 0.5).to(dt).requires_grad_(True)
+    if cols % 8:
+        pytest.skip("cols must be a multiple of 8 for the HIP path")
+    y = ops.rms_norm(x, w, 1e-6)
+    _lib_loaded()
+    xr, wr = x.detach().float().requires_grad_(True), w.detach().float().requires_grad_(True)
+    yr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * wr
+    torch.testing.assert_close(y.float(), yr, atol=_tol(dt) * 4, rtol=_tol(dt))
+    g = torch.randn_like(yr)
+    y.backward(g.to(dt))
+    yr.backward(g)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=_tol(dt) * 8, rtol=_tol(dt) * 2)
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=_tol(dt) * 40, rtol=_tol(dt) * 4)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cols", [256, 5120, 16384])
+def test_layer_norm(dt, cols):
+    torch.manual_seed(1)
+    x = (torch.randn(29, cols, device=DEV) * 3 + 1).to(dt).requires_grad_(True)
+    w = torch.randn(cols, device=DEV).to(dt).requires_grad_(True)
+    b = torch.randn(cols, device=DEV).to(dt).requires_grad_(True)
+    y = ops.layer_norm(x, w, b, 1e-5)
+    _lib_loaded()
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    yr = F.layer_norm(xr, (cols,), wr, br, 1e-5)
+    torch.testing.assert_close(y.float(), yr, atol=_tol(dt) * 8, rtol=_tol(dt))
+    g = torch.randn_like(yr)
+    y.backward(g.to(dt))
+    yr.backward(g)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=_tol(dt) * 10, rtol=_tol(dt) * 2)
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=_tol(dt) * 60, rtol=_tol(dt) * 4)
+    torch.testing.assert_close(b.grad.float(), br.grad, atol=_tol(dt) * 60, rtol=_tol(dt) * 4)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cols", [8, 128, 4096, 50304])
+def test_softmax(dt, cols):
+    x = (torch.randn(13, cols, device=DEV) * 4).to(dt).requires_grad_(True)
+    y = ops.softmax(x, -1)
+    _lib_loaded()
+    xr = x.detach().float().requires_grad_(True)
+    yr = torch.softmax(xr, -1)
+    torch.testing.assert_close(y.float(), yr, atol=_tol(dt), rtol=_tol(dt) * 2)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dt))
+    yr.backward(g)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=_tol(dt) * 2, rtol=_tol(dt) * 4)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("V", [64, 50304])
+def test_softmax_cross_entropy(dt, V):
+    torch.manual_seed(3)
+    logits = (torch.randn(33, V, device=DEV) * 3).to(dt).requires_grad_(True)
+    labels = torch.randint(0, V, (33,), device=DEV)
+    labels[5] = -100
+    l = ops.softmax_cross_entropy(logits, labels, -100)
+    _lib_loaded()
+    lr = logits.detach().float().requires_grad_(True)
+    ref = F.cross_entropy(lr, labels, ignore_index=-100, reduction="none")
+    torch.testing.assert_close(l, ref, atol=1e-3 if dt == torch.float32 else 3e-2, rtol=1e-3)
+    g = torch.rand(33, device=DEV)
+    l.backward(g)
+    ref.backward(g)
+    torch.testing.assert_close(logits.grad.float(), lr.grad, atol=1e-5 if dt == torch.float32 else 3e-3,
+                               rtol=1e-3 if dt == torch.float32 else 3e-2)
+
+
+@pytest.mark.parametrize("approx", [False, True])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_gelu(approx, dt):
+    x = (torch.randn(4, 1024, device=DEV) * 3).to(dt).requires_grad_(True)
+    y = ops.gelu(x, approx)
+    _lib_loaded()
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.gelu(xr, approximate="tanh" if approx else "none")
+    torch.testing.assert_close(y.float(), yr, atol=_tol(dt) * 2, rtol=_tol(dt))
+    g = torch.randn_like(yr)
+    y.backward(g.to(dt))
+    yr.backward(g)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=_tol(dt) * 4, rtol=_tol(dt) * 2)
+
+
+def test_bias_gelu():
+    x = torch.randn(64, 2048, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    b = torch.randn(2048, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = ops.bias_gelu(x, b)
+    _lib_loaded()
+    xr, br = x.detach().float().requires_grad_(True), b.detach().float().requires_grad_(True)
+    yr = F.gelu(xr + br, approximate="tanh")
+    torch.testing.assert_close(y.float(), yr, atol=4e-2, rtol=2e-2)
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=6e-2, rtol=3e-2)
+    torch.testing.assert_close(b.grad.float(), br.grad, atol=0.5, rtol=3e-2)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_swiglu_packed(dt):
+    xy = torch.randn(40, 2 * 512, device=DEV).to(dt).requires_grad_(True)
+    a, b = xy.chunk(2, -1)
+    y = ops.swiglu(a, b)
+    _lib_loaded()
+    xr = xy.detach().float().requires_grad_(True)
+    ar, br = xr.chunk(2, -1)
+    yr = F.silu(ar) * br
+    torch.testing.assert_close(y.float(), yr, atol=_tol(dt) * 4, rtol=_tol(dt))
+    g = torch.randn_like(yr)
+    y.backward(g.to(dt))
+    yr.backward(g)
+    torch.testing.assert_close(xy.grad.float(), xr.grad, atol=_tol(dt) * 4, rtol=_tol(dt) * 2)
+
+
+@pytest.mark.parametrize("neox", [True, False])
+def test_rope(neox):
+    from paddlepaddle_amd.ops.rope import rope_tables, _rotate_ref
+    B, S, H, D = 2, 64, 4, 128
+    cos, sin = rope_tables(S, D, device=DEV, neox=neox)
+    x = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = ops.apply_rotary(x, cos, sin, neox)
+    _lib_loaded()
+    xr = x.detach().float().requires_grad_(True)
+    yr = _rotate_ref(xr, cos, sin, neox, False)
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=2e-2)
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=5e-2, rtol=3e-2)
+
+
+def test_adamw_multi_tensor_master_weights():
+    import paddlepaddle_amd as paddle
+    torch.manual_seed(5)
+    shapes = [(1000,), (33, 17), (4096, 8), (7,)]
+    ps = [paddle.Parameter(torch.randn(s, device=DEV).bfloat16()) for s in shapes]
+    ref = [p._t.detach().float().clone().requires_grad_(True) for p in ps]
+    opt = paddle.optimizer.AdamW(1e-2, parameters=ps, weight_decay=0.1, multi_precision=True)
+    topt = torch.optim.AdamW(ref, lr=1e-2, weight_decay=0.1, eps=1e-8)
+    for step in range(3):
+        gs = [torch.randn(s, device=DEV) for s in shapes]
+        for p, g in zip(ps, gs):
+            p._t.grad = g.bfloat16()
+        for r, g in zip(ref, gs):
+            r.grad = g.bfloat16().float()
+        opt.step()
+        topt.step()
+    _lib_loaded()
+    for p, r in zip(ps, ref):
+        m = opt._master_weights[id(p)]
+        torch.testing.assert_close(m, r.detach(), atol=2e-5, rtol=1e-5)
+        torch.testing.assert_close(p._t.float(), r.detach(), atol=1e-2, rtol=1e-2)
+
+
+def test_global_norm_multi():
+    from paddlepaddle_amd.ops.optim import global_sq_norm
+    ts = [torch.randn(n, device=DEV, dtype=dt) for n, dt in [(100000, torch.float32), (333, torch.bfloat16),
+                                                              (70000, torch.bfloat16)]]
+    got = global_sq_norm(ts)
+    _lib_loaded()
+    ref = sum(t.float().pow(2).sum() for t in ts)
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-3)
