@@ -1,0 +1,575 @@
+// Flash attention forward + backward for gfx950 (CDNA4), bf16 in / fp32 accumulate.
+// Reference behaviour: paddle/phi/kernels/gpu/flash_attn_kernel.cu / flash_attn_grad_kernel.cu
+// (layout [batch, seq, heads, head_dim], causal = bottom-right aligned, GQA, LSE output).
+//
+// MFMA: v_mfma_f32_32x32x16_bf16 (lane l: r = l&31, h = l>>5;
+//   A[row r][k 8h+j], B[k 8h+j][col r], D[row (i&3)+8(i>>2)+4h][col r]).
+//
+// Forward (per workgroup: 4 waves x 32 queries = 128-query block; K/V tiles of 64 keys in LDS):
+//   S^T = K Q^T        -> the query is the MFMA column, so each lane owns one query and the row
+//                         max / sum are in-lane (+ one xor-32 exchange), no LDS for P;
+//   O^T += V^T P^T     -> the S^T accumulator is re-used directly as the B operand (bf16-packed),
+//                         V^T comes from ds_read_b64_tr_b16 transposed LDS reads; O^T keeps the
+//                         query on the lane, so the online-softmax rescale is per lane.
+//   K/V of tile j+1 are prefetched into registers while tile j computes (async-stage split).
+// Backward (per workgroup: 4 waves x 32 keys = 128-key block, loop over 32-query blocks):
+//   S = Q K^T, P = exp(S - LSE), dP = dO V^T, dS = P (dP - delta);
+//   dV^T += dO^T P and dK^T += Q^T dS with P / dS as B operands (no lane movement),
+//   dQ += dS K via a bf16 dS^T tile in LDS, accumulated into fp32 with global atomics.
+#include "common.h"
+
+using namespace pa;
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+namespace {
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8_t a, bf16x8_t b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+union Frag {
+  bf16x8_t v;
+  uint4 u;
+  s16x4 h[2];
+};
+
+// LDS byte offset of 16-byte chunk `ch` of row `row` in a [rows][NCH*8] bf16 image that serves
+// both ds_read_b128 row reads and ds_read_b64_tr_b16 transposed reads without bank conflicts.
+template <int NCH>
+__device__ __forceinline__ int img_off(int row, int ch) {
+  int sw;
+  if (NCH >= 16) sw = ((row & 3) << 2) | ((row >> 2) & 3);
+  else if (NCH == 8) sw = ((row & 3) << 1) | ((row >> 2) & 1);
+  else sw = (row & 3);
+  return row * (NCH * 16) + 16 * (ch ^ (sw & (NCH - 1)));
+}
+
+__device__ __forceinline__ uint4 lds_b128(const char* smem, int off) {
+  return *reinterpret_cast<const uint4*>(smem + off);
+}
+
+__device__ __forceinline__ s16x4 lds_tr(const char* smem, int off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(reinterpret_cast<uintptr_t>(smem + off)));
+}
+
+__device__ __forceinline__ bf16x8_t pack8(const float* f) {
+  Frag x;
+  x.u.x = pack_bf16(f[0], f[1]);
+  x.u.y = pack_bf16(f[2], f[3]);
+  x.u.z = pack_bf16(f[4], f[5]);
+  x.u.w = pack_bf16(f[6], f[7]);
+  return x.v;
+}
+
+struct FwdArgs {
+  const uint16_t* q; const uint16_t* k; const uint16_t* v; uint16_t* o; float* lse;
+  int64_t qs[3], ks[3], vs[3], os[3];  // strides (batch, seq, head) in elements
+  int B, Sq, Sk, H, Hk;
+  float scale_log2;
+  int causal;
+};
+
+// ------------------------------------------------------------------------------------- forward
+template <int D>
+__global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs p) {
+  constexpr int NCH = D / 8;       // 16-byte chunks per row
+  constexpr int KS = D / 16;       // k-steps over head dim
+  constexpr int NDT = D / 32;      // 32-wide output d tiles
+  constexpr int BN = 64;           // keys per tile
+  constexpr int TILE_BYTES = BN * D * 2;
+  constexpr int LOADS = BN * NCH / 256;  // 16-byte chunks per thread per tensor
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES];
+  char* ks_lds = smem;
+  char* vs_lds = smem + TILE_BYTES;
+
+  const int nqb = gridDim.x;
+  const int qb = p.causal ? (nqb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
+  const int bh = blockIdx.y;
+  const int b = bh / p.H, h = bh % p.H;
+  const int hk = h / (p.H / p.Hk);
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
+  const int qi = qb * 128 + w * 32 + r;
+  const int shift = p.Sk - p.Sq;
+
+  // Q fragments (B operand of S^T = K Q^T): lane holds Q[qi][16ks + 8hf + j]
+  bf16x8_t qf[KS];
+  {
+    const uint16_t* qrow = p.q + (int64_t)b * p.qs[0] + (int64_t)(qi < p.Sq ? qi : 0) * p.qs[1] + (int64_t)h * p.qs[2];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      Frag f;
+      if (qi < p.Sq) f.u = *reinterpret_cast<const uint4*>(qrow + ks * 16 + hf * 8);
+      else f.u = make_uint4(0, 0, 0, 0);
+      qf[ks] = f.v;
+    }
+  }
+
+  f32x16 oacc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) oacc[dt] = zero16();
+  float m_run = -INFINITY, l_run = 0.f;
+
+  int kv_end = p.Sk;
+  if (p.causal) {
+    const int last_q = min(qb * 128 + 127, p.Sq - 1);
+    kv_end = min(p.Sk, last_q + shift + 1);
+  }
+  const int n_tiles = kv_end > 0 ? (kv_end + BN - 1) / BN : 0;
+
+  const uint16_t* kbase = p.k + (int64_t)b * p.ks[0] + (int64_t)hk * p.ks[2];
+  const uint16_t* vbase = p.v + (int64_t)b * p.vs[0] + (int64_t)hk * p.vs[2];
+
+  uint4 kreg[LOADS], vreg[LOADS];
+  auto gload = [&](int tile) {
+    const int kv0 = tile * BN;
+#pragma unroll
+    for (int i = 0; i < LOADS; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx / NCH, ch = idx % NCH;
+      const int key = kv0 + row;
+      if (key < p.Sk) {
+        kreg[i] = *reinterpret_cast<const uint4*>(kbase + (int64_t)key * p.ks[1] + ch * 8);
+        vreg[i] = *reinterpret_cast<const uint4*>(vbase + (int64_t)key * p.vs[1] + ch * 8);
+      } else {
+        kreg[i] = make_uint4(0, 0, 0, 0);
+        vreg[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < LOADS; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx / NCH, ch = idx % NCH;
+      *reinterpret_cast<uint4*>(ks_lds + img_off<NCH>(row, ch)) = kreg[i];
+      *reinterpret_cast<uint4*>(vs_lds + img_off<NCH>(row, ch)) = vreg[i];
+    }
+  };
+
+  if (n_tiles > 0) gload(0);
+  for (int t = 0; t < n_tiles; ++t) {
+    __syncthreads();  // previous tile's LDS reads are done
+    lstore();
+    __syncthreads();
+    if (t + 1 < n_tiles) gload(t + 1);  // overlaps with the MFMA work below
+    const int kv0 = t * BN;
+
+    // ---- S^T = K Q^T for two 32-key sub-tiles
+    f32x16 sacc[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      sacc[kt] = zero16();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        Frag a;
+        a.u = lds_b128(ks_lds, img_off<NCH>(kt * 32 + r, 2 * ks + hf));
+        sacc[kt] = mfma32(a.v, qf[ks], sacc[kt]);
+      }
+    }
+    // ---- scale, mask, online softmax (log2 domain)
+    float mloc = -INFINITY;
+    const bool need_mask = (kv0 + BN > p.Sk) || (p.causal && (kv0 + BN - 1 > qb * 128 + shift));
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float s = sacc[kt][i] * p.scale_log2;
+        if (need_mask) {
+          const int kj = kv0 + kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hf;
+          if (kj >= p.Sk || (p.causal && kj > qi + shift)) s = -INFINITY;
+        }
+        sacc[kt][i] = s;
+        mloc = fmaxf(mloc, s);
+      }
+    }
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    const float m_new = fmaxf(m_run, mloc);
+    const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+    const float alpha = exp2f(m_run - m_use);
+    float psum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float e = exp2f(sacc[kt][i] - m_use);
+        sacc[kt][i] = e;
+        psum += e;
+      }
+    }
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+
+    // ---- P^T as bf16 B fragments: fragment s of sub-tile kt = regs 8s..8s+7
+    bf16x8_t pf[2][2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float tmp[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) tmp[j] = sacc[kt][8 * s + j];
+        pf[kt][s] = pack8(tmp);
+      }
+
+    // ---- O^T += V^T P^T (A = V^T via transposed LDS reads)
+    const int gi = lane & 15, qq = gi >> 2, pp = gi & 3, G1 = (lane >> 4) & 1;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      const int cch = (dt * 32 + 16 * G1) / 8 + (pp >> 1);
+      const int cb = 8 * (pp & 1);
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int R0 = kt * 32 + 16 * s + 4 * hf;
+          Frag a;
+          a.h[0] = lds_tr(vs_lds, img_off<NCH>(R0 + qq, cch) + cb);
+          a.h[1] = lds_tr(vs_lds, img_off<NCH>(R0 + 8 + qq, cch) + cb);
+          oacc[dt] = mfma32(a.v, pf[kt][s], oacc[dt]);
+        }
+      }
+    }
+  }
+
+  // ---- epilogue
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  if (qi < p.Sq) {
+    uint16_t* orow = p.o + (int64_t)b * p.os[0] + (int64_t)qi * p.os[1] + (int64_t)h * p.os[2];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d0 = dt * 32 + 8 * g + 4 * hf;
+        uint2 v2;
+        v2.x = pack_bf16(oacc[dt][4 * g + 0] * inv, oacc[dt][4 * g + 1] * inv);
+        v2.y = pack_bf16(oacc[dt][4 * g + 2] * inv, oacc[dt][4 * g + 3] * inv);
+        *reinterpret_cast<uint2*>(orow + d0) = v2;
+      }
+    }
+    if (hf == 0) {
+      const float lse = (m_run == -INFINITY) ? INFINITY : (m_run * kLn2 + __logf(l_tot));
+      p.lse[((int64_t)b * p.H + h) * p.Sq + qi] = lse;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------- backward
+struct BwdArgs {
+  const uint16_t* q; const uint16_t* k; const uint16_t* v; const uint16_t* o; const uint16_t* dout;
+  const float* lse; float* dq_acc; const float* delta; uint16_t* dk; uint16_t* dv;
+  int64_t qs[3], ks[3], vs[3], dos[3], dks[3], dvs[3];
+  int B, Sq, Sk, H, Hk;
+  float scale, scale_log2;
+  int causal;
+};
+
+// delta[b,h,q] = sum_d dO * O
+__global__ __launch_bounds__(256) void fa_bwd_delta(const uint16_t* __restrict__ o, const uint16_t* __restrict__ dout,
+                                                    float* __restrict__ delta, int64_t o_sb, int64_t o_ss, int64_t o_sh,
+                                                    int64_t d_sb, int64_t d_ss, int64_t d_sh, int B, int Sq, int H, int D) {
+  const int per_row = D / 8;  // lanes per (b,q,h) row
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t row = gid / per_row;
+  const int c = (int)(gid % per_row);
+  const int64_t nrows = (int64_t)B * Sq * H;
+  float s = 0.f;
+  int bb = 0, qq = 0, hh = 0;
+  if (row < nrows) {
+    hh = (int)(row % H);
+    qq = (int)((row / H) % Sq);
+    bb = (int)(row / ((int64_t)H * Sq));
+    float a[8], g[8];
+    load8<bf16>((const bf16*)(o + bb * o_sb + qq * o_ss + hh * o_sh + c * 8), a);
+    load8<bf16>((const bf16*)(dout + bb * d_sb + qq * d_ss + hh * d_sh + c * 8), g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += a[j] * g[j];
+  }
+  for (int off = per_row / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (row < nrows && c == 0) delta[((int64_t)bb * H + hh) * Sq + qq] = s;
+}
+
+// dq[b,q,h,:] (bf16, strided) = dq_acc[b,q,h,:] (fp32, contiguous [B,Sq,H,D])
+__global__ __launch_bounds__(256) void fa_bwd_dq_convert(const float* __restrict__ acc, uint16_t* __restrict__ dq,
+                                                         int64_t s_b, int64_t s_s, int64_t s_h, int B, int Sq, int H,
+                                                         int D) {
+  const int64_t n = (int64_t)B * Sq * H * D / 8;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t e = i * 8;
+    const int d = (int)(e % D);
+    const int64_t row = e / D;
+    const int hh = (int)(row % H), qq = (int)((row / H) % Sq), bb = (int)(row / ((int64_t)H * Sq));
+    float v[8];
+    load8<float>(acc + e, v);
+    store8<bf16>((bf16*)(dq + bb * s_b + qq * s_s + hh * s_h + d), v);
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
+  constexpr int NCH = D / 8;
+  constexpr int KS = D / 16;
+  constexpr int NDT = D / 32;
+  constexpr int BK = 128;  // keys per workgroup (4 waves x 32)
+  constexpr int BM = 32;   // queries per inner step
+  constexpr int KT_BYTES = BK * D * 2;
+  constexpr int QT_BYTES = BM * D * 2;
+  constexpr int DST_BYTES = BK * BM * 2;  // dS^T [128 keys][32 q] bf16, 64-byte rows
+  __shared__ __attribute__((aligned(16))) char smem[KT_BYTES + 2 * QT_BYTES + DST_BYTES + 2 * BM * 4];
+  char* k_lds = smem;
+  char* q_lds = smem + KT_BYTES;
+  char* do_lds = q_lds + QT_BYTES;
+  char* ds_lds = do_lds + QT_BYTES;
+  float* lse_s = reinterpret_cast<float*>(ds_lds + DST_BYTES);
+  float* dlt_s = lse_s + BM;
+
+  const int kb = blockIdx.x;
+  const int bh = blockIdx.y;
+  const int b = bh / p.H, h = bh % p.H;
+  const int hk = h / (p.H / p.Hk);
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
+  const int gi = lane & 15, qq = gi >> 2, pp = gi & 3, G1 = (lane >> 4) & 1;
+  const int shift = p.Sk - p.Sq;
+  const int kj = kb * BK + w * 32 + r;  // this lane's key (MFMA column)
+
+  // K tile -> LDS (row image, also read transposed for dQ)
+  const uint16_t* kbase = p.k + (int64_t)b * p.ks[0] + (int64_t)hk * p.ks[2];
+  const uint16_t* vbase = p.v + (int64_t)b * p.vs[0] + (int64_t)hk * p.vs[2];
+#pragma unroll
+  for (int i = 0; i < BK * NCH / 256; ++i) {
+    const int idx = tid + 256 * i;
+    const int row = idx / NCH, ch = idx % NCH;
+    const int key = kb * BK + row;
+    uint4 val = make_uint4(0, 0, 0, 0);
+    if (key < p.Sk) val = *reinterpret_cast<const uint4*>(kbase + (int64_t)key * p.ks[1] + ch * 8);
+    *reinterpret_cast<uint4*>(k_lds + img_off<NCH>(row, ch)) = val;
+  }
+  // V fragments for this lane's key (B operand of dP = dO V^T)
+  bf16x8_t vf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    Frag f;
+    if (kj < p.Sk) f.u = *reinterpret_cast<const uint4*>(vbase + (int64_t)kj * p.vs[1] + ks * 16 + hf * 8);
+    else f.u = make_uint4(0, 0, 0, 0);
+    vf[ks] = f.v;
+  }
+
+  f32x16 dk_acc[NDT], dv_acc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) { dk_acc[dt] = zero16(); dv_acc[dt] = zero16(); }
+
+  // query range that sees any key of this block
+  int q_begin = 0;
+  if (p.causal) q_begin = max(0, kb * BK - shift);
+  q_begin = (q_begin / BM) * BM;
+  const uint16_t* qbase = p.q + (int64_t)b * p.qs[0] + (int64_t)h * p.qs[2];
+  const uint16_t* dobase = p.dout + (int64_t)b * p.dos[0] + (int64_t)h * p.dos[2];
+  const float* lse_b = p.lse + ((int64_t)b * p.H + h) * p.Sq;
+  const float* dlt_b = p.delta + ((int64_t)b * p.H + h) * p.Sq;
+  float* dqb = p.dq_acc + (int64_t)b * p.Sq * p.H * D + (int64_t)h * D;  // contiguous [B,Sq,H,D]
+
+  for (int q0 = q_begin; q0 < p.Sq; q0 += BM) {
+    __syncthreads();  // previous iteration's LDS reads done
+#pragma unroll
+    for (int i = 0; i < BM * NCH / 256; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx / NCH, ch = idx % NCH;
+      const int qx = q0 + row;
+      uint4 a = make_uint4(0, 0, 0, 0), g = make_uint4(0, 0, 0, 0);
+      if (qx < p.Sq) {
+        a = *reinterpret_cast<const uint4*>(qbase + (int64_t)qx * p.qs[1] + ch * 8);
+        g = *reinterpret_cast<const uint4*>(dobase + (int64_t)qx * p.dos[1] + ch * 8);
+      }
+      *reinterpret_cast<uint4*>(q_lds + img_off<NCH>(row, ch)) = a;
+      *reinterpret_cast<uint4*>(do_lds + img_off<NCH>(row, ch)) = g;
+    }
+    if (tid < BM) {
+      const int qx = q0 + tid;
+      lse_s[tid] = qx < p.Sq ? lse_b[qx] * kLog2e : INFINITY;
+      dlt_s[tid] = qx < p.Sq ? dlt_b[qx] : 0.f;
+    }
+    __syncthreads();
+
+    // S = Q K^T and dP = dO V^T : rows q (registers), cols = this lane's key
+    f32x16 sacc = zero16(), pacc = zero16();
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      Frag qa, da, kb8;
+      qa.u = lds_b128(q_lds, img_off<NCH>(r, 2 * ks + hf));
+      da.u = lds_b128(do_lds, img_off<NCH>(r, 2 * ks + hf));
+      kb8.u = lds_b128(k_lds, img_off<NCH>(w * 32 + r, 2 * ks + hf));
+      sacc = mfma32(qa.v, kb8.v, sacc);
+      pacc = mfma32(da.v, vf[ks], pacc);
+    }
+    float pv[16], dsv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int qr = (i & 3) + 8 * (i >> 2) + 4 * hf;
+      const int qx = q0 + qr;
+      float pr = exp2f(sacc[i] * p.scale_log2 - lse_s[qr]);
+      if (kj >= p.Sk || (p.causal && kj > qx + shift)) pr = 0.f;
+      pv[i] = pr;
+      dsv[i] = pr * (pacc[i] - dlt_s[qr]);
+    }
+    bf16x8_t pf[2], sf[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) { pf[s] = pack8(pv + 8 * s); sf[s] = pack8(dsv + 8 * s); }
+
+    // dV^T += dO^T P ; dK^T += Q^T dS  (A via transposed reads of the dO / Q images)
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      const int cch = (dt * 32 + 16 * G1) / 8 + (pp >> 1);
+      const int cb = 8 * (pp & 1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int R0 = 16 * s + 4 * hf;
+        Frag a, c;
+        a.h[0] = lds_tr(do_lds, img_off<NCH>(R0 + qq, cch) + cb);
+        a.h[1] = lds_tr(do_lds, img_off<NCH>(R0 + 8 + qq, cch) + cb);
+        dv_acc[dt] = mfma32(a.v, pf[s], dv_acc[dt]);
+        c.h[0] = lds_tr(q_lds, img_off<NCH>(R0 + qq, cch) + cb);
+        c.h[1] = lds_tr(q_lds, img_off<NCH>(R0 + 8 + qq, cch) + cb);
+        dk_acc[dt] = mfma32(c.v, sf[s], dk_acc[dt]);
+      }
+    }
+
+    // dS^T tile [128 keys][32 q] bf16: lane writes its key row, 4 consecutive q per 8-byte store
+    {
+      char* rowp = ds_lds + (w * 32 + r) * (BM * 2);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint2 v2;
+        v2.x = pack_bf16(dsv[4 * g + 0], dsv[4 * g + 1]);
+        v2.y = pack_bf16(dsv[4 * g + 2], dsv[4 * g + 3]);
+        *reinterpret_cast<uint2*>(rowp + (8 * g + 4 * hf) * 2) = v2;
+      }
+    }
+    __syncthreads();
+    // dQ[q][d] += sum_key dS[q][key] K[key][d] ; wave w handles d tiles dt = w, w+4, ...
+    for (int dt = w; dt < NDT; dt += 4) {
+      f32x16 qacc = zero16();
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        Frag a, bb;
+        // A = dS[q=r][key = 16ks + 8hf + j]: transposed read of the dS^T image (rows = keys)
+        const int kr0 = 16 * ks + 8 * hf;
+        a.h[0] = lds_tr(ds_lds, (kr0 + qq) * (BM * 2) + (16 * G1 + 4 * pp) * 2);
+        a.h[1] = lds_tr(ds_lds, (kr0 + 4 + qq) * (BM * 2) + (16 * G1 + 4 * pp) * 2);
+        // B = K[key = 16ks + 8hf + j][d = dt*32 + r]: transposed read of the K image
+        const int cch = (dt * 32 + 16 * G1) / 8 + (pp >> 1);
+        bb.h[0] = lds_tr(k_lds, img_off<NCH>(kr0 + qq, cch) + 8 * (pp & 1));
+        bb.h[1] = lds_tr(k_lds, img_off<NCH>(kr0 + 4 + qq, cch) + 8 * (pp & 1));
+        qacc = mfma32(a.v, bb.v, qacc);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int qr = (i & 3) + 8 * (i >> 2) + 4 * hf;
+        const int qx = q0 + qr;
+        if (qx < p.Sq) atomicAdd(dqb + (int64_t)qx * p.H * D + dt * 32 + r, qacc[i] * p.scale);
+      }
+    }
+  }
+
+  // write dK = scale * (dK^T)^T, dV = (dV^T)^T : lane = key, 4 consecutive d per 8-byte store
+  if (kj < p.Sk) {
+    uint16_t* dkrow = p.dk + (int64_t)b * p.dks[0] + (int64_t)kj * p.dks[1] + (int64_t)h * p.dks[2];
+    uint16_t* dvrow = p.dv + (int64_t)b * p.dvs[0] + (int64_t)kj * p.dvs[1] + (int64_t)h * p.dvs[2];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d0 = dt * 32 + 8 * g + 4 * hf;
+        uint2 a, c;
+        a.x = pack_bf16(dk_acc[dt][4 * g] * p.scale, dk_acc[dt][4 * g + 1] * p.scale);
+        a.y = pack_bf16(dk_acc[dt][4 * g + 2] * p.scale, dk_acc[dt][4 * g + 3] * p.scale);
+        c.x = pack_bf16(dv_acc[dt][4 * g], dv_acc[dt][4 * g + 1]);
+        c.y = pack_bf16(dv_acc[dt][4 * g + 2], dv_acc[dt][4 * g + 3]);
+        *reinterpret_cast<uint2*>(dkrow + d0) = a;
+        *reinterpret_cast<uint2*>(dvrow + d0) = c;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// strides: host array of 12 int64 = q(b,s,h), k(b,s,h), v(b,s,h), o(b,s,h)
+PA_EXPORT int pa_flash_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
+                                const int64_t* strides, int B, int Sq, int Sk, int H, int Hk, int D, float scale,
+                                int causal, hipStream_t st) {
+  if (H % Hk != 0) return 3;
+  FwdArgs a;
+  a.q = (const uint16_t*)q; a.k = (const uint16_t*)k; a.v = (const uint16_t*)v; a.o = (uint16_t*)o; a.lse = lse;
+  for (int i = 0; i < 3; ++i) {
+    a.qs[i] = strides[i]; a.ks[i] = strides[3 + i]; a.vs[i] = strides[6 + i]; a.os[i] = strides[9 + i];
+  }
+  a.B = B; a.Sq = Sq; a.Sk = Sk; a.H = H; a.Hk = Hk;
+  a.scale_log2 = scale * kLog2e;
+  a.causal = causal;
+  dim3 grid((unsigned)((Sq + 127) / 128), (unsigned)(B * H));
+  if (D == 128) hipLaunchKernelGGL(fa_fwd_kernel<128>, grid, dim3(256), 0, st, a);
+  else if (D == 64) hipLaunchKernelGGL(fa_fwd_kernel<64>, grid, dim3(256), 0, st, a);
+  else return 4;
+  PA_CHECK_LAUNCH();
+  return 0;
+}
+
+// strides: host array of 24 int64 = q, k, v, o, do, dq, dk, dv  (each b,s,h)
+PA_EXPORT int pa_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                                const float* lse, void* dq, void* dk, void* dv, float* dq_acc, float* delta,
+                                const int64_t* strides, int B, int Sq, int Sk, int H, int Hk, int D, float scale,
+                                int causal, hipStream_t st) {
+  if (H % Hk != 0) return 3;
+  if (D != 128 && D != 64) return 4;
+  const int64_t* qs = strides; const int64_t* ks = strides + 3; const int64_t* vs = strides + 6;
+  const int64_t* os = strides + 9; const int64_t* dos = strides + 12; const int64_t* dqs = strides + 15;
+  const int64_t* dks = strides + 18; const int64_t* dvs = strides + 21;
+  // delta = rowsum(dO * O)
+  {
+    const int64_t threads = (int64_t)B * Sq * H * (D / 8);
+    hipLaunchKernelGGL(fa_bwd_delta, dim3((unsigned)cdiv(threads, 256)), dim3(256), 0, st, (const uint16_t*)o,
+                       (const uint16_t*)dout, delta, os[0], os[1], os[2], dos[0], dos[1], dos[2], B, Sq, H, D);
+    PA_CHECK_LAUNCH();
+  }
+  hipMemsetAsync(dq_acc, 0, (size_t)B * Sq * H * D * sizeof(float), st);
+  BwdArgs a;
+  a.q = (const uint16_t*)q; a.k = (const uint16_t*)k; a.v = (const uint16_t*)v; a.o = (const uint16_t*)o;
+  a.dout = (const uint16_t*)dout; a.lse = lse; a.dq_acc = dq_acc; a.delta = delta;
+  a.dk = (uint16_t*)dk; a.dv = (uint16_t*)dv;
+  for (int i = 0; i < 3; ++i) {
+    a.qs[i] = qs[i]; a.ks[i] = ks[i]; a.vs[i] = vs[i]; a.dos[i] = dos[i]; a.dks[i] = dks[i]; a.dvs[i] = dvs[i];
+  }
+  a.B = B; a.Sq = Sq; a.Sk = Sk; a.H = H; a.Hk = Hk;
+  a.scale = scale; a.scale_log2 = scale * kLog2e; a.causal = causal;
+  dim3 grid((unsigned)((Sk + 127) / 128), (unsigned)(B * H));
+  if (D == 128) hipLaunchKernelGGL(fa_bwd_kernel<128>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(fa_bwd_kernel<64>, grid, dim3(256), 0, st, a);
+  PA_CHECK_LAUNCH();
+  {
+    const int64_t nvec = (int64_t)B * Sq * H * D / 8;
+    int64_t g = cdiv(nvec, 256);
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(fa_bwd_dq_convert, dim3((unsigned)g), dim3(256), 0, st, dq_acc, (uint16_t*)dq, dqs[0], dqs[1],
+                       dqs[2], B, Sq, H, D);
+    PA_CHECK_LAUNCH();
+  }
+  return 0;
+}

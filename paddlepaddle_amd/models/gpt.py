@@ -142,8 +142,7 @@ class GPTAttention(nn.Layer):
         qkv = self.qkv_proj(x)._t  # [B, S, 3*h_local]
         B, S = qkv.shape[0], qkv.shape[1]
         qkv = qkv.view(B, S, self.local_heads, 3, self.head_dim)
-        q, k, v = qkv[:, :, :, 0], qkv[:, :, :, 1], qkv[:, :, :, 2]
-        o = _ops.flash_attention(q, k, v, causal=True, dropout=self.attn_dropout, training=self.training)
+        o = _ops.flash_attention_qkvpacked(qkv, causal=True, dropout=self.attn_dropout, training=self.training)
         o = o.reshape(B, S, self.local_heads * self.head_dim)
         return self.out_proj(_wrap(o))
 

@@ -103,7 +103,9 @@ class Layer:
 
     training = True
 
-    def __init__(self, name_scope=None, dtype="float32"):
+    def __init__(self, name_scope=None, dtype=None):
+        if dtype is None:
+            dtype = _dt.get_default_dtype()
         object.__setattr__(self, "_parameters", collections.OrderedDict())
         object.__setattr__(self, "_sub_layers", collections.OrderedDict())
         object.__setattr__(self, "_buffers", collections.OrderedDict())

@@ -9,7 +9,7 @@ from __future__ import annotations
 from .activation import gelu, silu, swiglu, softmax, bias_gelu  # noqa: F401
 from .norm import rms_norm, layer_norm  # noqa: F401
 from .loss import softmax_cross_entropy  # noqa: F401
-from .attention import flash_attention, attention_reference  # noqa: F401
+from .attention import flash_attention, flash_attention_qkvpacked, attention_reference  # noqa: F401
 from .rope import apply_rotary  # noqa: F401
 from .linear import fused_linear  # noqa: F401
 from . import optim  # noqa: F401

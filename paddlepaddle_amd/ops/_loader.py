@@ -95,8 +95,8 @@ def _declare(L):
         "pa_sq_norm_multi": [_vp, _vp, _i64, _vp, _vp],
         "pa_scale_multi": [_vp, _i64, _vp, _vp],
         # attention
-        "pa_flash_attn_fwd": [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _f32, _i32, _vp],
-        "pa_flash_attn_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+        "pa_flash_attn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _f32, _i32, _vp],
+        "pa_flash_attn_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                               _i32, _i32, _i32, _i32, _i32, _i32, _f32, _i32, _vp],
         # gemm
         "pa_gemm_bf16": [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp],

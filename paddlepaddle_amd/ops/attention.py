@@ -62,39 +62,102 @@ def _sdpa(q, k, v, causal, scale, mask, dropout, training):
     return o.transpose(1, 2)
 
 
+def _strides(t):
+    st = t.stride()
+    return [st[0], st[1], st[2]]
+
+
+def _i64arr(vals):
+    import ctypes
+    return (ctypes.c_int64 * len(vals))(*[int(v) for v in vals])
+
+
+def _fa_fwd(q, k, v, causal, scale):
+    B, Sq, H, D = q.shape
+    Sk, Hk = k.shape[1], k.shape[2]
+    o = torch.empty(B, Sq, H, D, dtype=q.dtype, device=q.device)
+    lse = torch.empty(B, H, Sq, dtype=torch.float32, device=q.device)
+    st = _i64arr(_strides(q) + _strides(k) + _strides(v) + _strides(o))
+    L.call("pa_flash_attn_fwd", L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(o), L.ptr(lse), st, B, Sq, Sk, H, Hk, D,
+           float(scale), int(causal), L.stream_ptr())
+    return o, lse
+
+
+def _fa_bwd(q, k, v, o, lse, do, dq, dk, dv, causal, scale):
+    B, Sq, H, D = q.shape
+    Sk, Hk = k.shape[1], k.shape[2]
+    dq_acc = torch.empty(B, Sq, H, D, dtype=torch.float32, device=q.device)
+    delta = torch.empty(B, H, Sq, dtype=torch.float32, device=q.device)
+    st = _i64arr(_strides(q) + _strides(k) + _strides(v) + _strides(o) + _strides(do) + _strides(dq)
+                 + _strides(dk) + _strides(dv))
+    L.call("pa_flash_attn_bwd", L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(o), L.ptr(do), L.ptr(lse), L.ptr(dq),
+           L.ptr(dk), L.ptr(dv), L.ptr(dq_acc), L.ptr(delta), st, B, Sq, Sk, H, Hk, D, float(scale), int(causal),
+           L.stream_ptr())
+
+
+def _lastdim_contig(t):
+    return t.stride(-1) == 1 and t.data_ptr() % 16 == 0 and all(s % 8 == 0 for s in t.stride()[:-1])
+
+
 class _FlashAttnHIP(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, causal, scale):
-        B, Sq, H, D = q.shape
-        Sk, Hk = k.shape[1], k.shape[2]
-        qc, kc, vc = q.contiguous(), k.contiguous(), v.contiguous()
-        o = torch.empty_like(qc)
-        lse = torch.empty(B, H, Sq, dtype=torch.float32, device=q.device)
-        L.call("pa_flash_attn_fwd", L.ptr(qc), L.ptr(kc), L.ptr(vc), L.ptr(o), L.ptr(lse), B, Sq, Sk, H, Hk, D,
-               float(scale), int(causal), L.stream_ptr())
-        ctx.save_for_backward(qc, kc, vc, o, lse)
+        q, k, v = [t if _lastdim_contig(t) else t.contiguous() for t in (q, k, v)]
+        o, lse = _fa_fwd(q, k, v, causal, scale)
+        ctx.save_for_backward(q, k, v, o, lse)
         ctx.causal, ctx.scale = causal, scale
         return o
 
     @staticmethod
     def backward(ctx, do):
-        qc, kc, vc, o, lse = ctx.saved_tensors
-        B, Sq, H, D = qc.shape
-        Sk, Hk = kc.shape[1], kc.shape[2]
-        doc = do.contiguous().to(qc.dtype)
-        dq_acc = torch.zeros(B, Sq, H, D, dtype=torch.float32, device=qc.device)
-        dk = torch.empty(B, Sk, H, D, dtype=qc.dtype, device=qc.device) if Hk != H else torch.empty_like(kc)
-        dv = torch.empty(B, Sk, H, D, dtype=qc.dtype, device=qc.device) if Hk != H else torch.empty_like(vc)
-        delta = torch.empty(B, H, Sq, dtype=torch.float32, device=qc.device)
-        dq = torch.empty_like(qc)
-        L.call("pa_flash_attn_bwd", L.ptr(qc), L.ptr(kc), L.ptr(vc), L.ptr(o), L.ptr(doc), L.ptr(lse),
-               L.ptr(dq), L.ptr(dk), L.ptr(dv), L.ptr(dq_acc), L.ptr(delta), B, Sq, Sk, H, Hk, D,
-               float(ctx.scale), int(ctx.causal), L.stream_ptr())
+        q, k, v, o, lse = ctx.saved_tensors
+        B, Sq, H, D = q.shape
+        Sk, Hk = k.shape[1], k.shape[2]
+        do = do.to(q.dtype)
+        if not _lastdim_contig(do):
+            do = do.contiguous()
+        dq = torch.empty(B, Sq, H, D, dtype=q.dtype, device=q.device)
+        dk = torch.empty(B, Sk, H, D, dtype=q.dtype, device=q.device)
+        dv = torch.empty(B, Sk, H, D, dtype=q.dtype, device=q.device)
+        _fa_bwd(q, k, v, o, lse, do, dq, dk, dv, ctx.causal, ctx.scale)
         if Hk != H:
             g = H // Hk
             dk = dk.view(B, Sk, Hk, g, D).sum(3)
             dv = dv.view(B, Sk, Hk, g, D).sum(3)
         return dq, dk, dv, None, None
+
+
+class _FlashAttnQKVPackedHIP(torch.autograd.Function):
+    """qkv [B, S, H, 3, D] (PaddleNLP fused-QKV layout) -> o [B, S, H, D]; grad is one dqkv buffer."""
+
+    @staticmethod
+    def forward(ctx, qkv, causal, scale):
+        q, k, v = qkv[:, :, :, 0], qkv[:, :, :, 1], qkv[:, :, :, 2]
+        o, lse = _fa_fwd(q, k, v, causal, scale)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.causal, ctx.scale = causal, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        do = do.to(qkv.dtype)
+        if not _lastdim_contig(do):
+            do = do.contiguous()
+        dqkv = torch.empty_like(qkv)
+        q, k, v = qkv[:, :, :, 0], qkv[:, :, :, 1], qkv[:, :, :, 2]
+        _fa_bwd(q, k, v, o, lse, do, dqkv[:, :, :, 0], dqkv[:, :, :, 1], dqkv[:, :, :, 2], ctx.causal, ctx.scale)
+        return dqkv, None, None
+
+
+def flash_attention_qkvpacked(qkv, causal=True, scale=None, dropout=0.0, training=True):
+    """qkv [B,S,H,3,D] -> [B,S,H,D]."""
+    D = qkv.shape[-1]
+    scale = 1.0 / math.sqrt(D) if scale is None else float(scale)
+    q, k, v = qkv[:, :, :, 0], qkv[:, :, :, 1], qkv[:, :, :, 2]
+    if _hip_ok(q, k, v, None, dropout, training) and _lastdim_contig(qkv):
+        return _FlashAttnQKVPackedHIP.apply(qkv, bool(causal), scale)
+    return flash_attention(q, k, v, causal=causal, scale=scale, dropout=dropout, training=training)
 
 
 def _hip_ok(q, k, v, mask, dropout, training):
