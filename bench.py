@@ -88,7 +88,7 @@ def gpt_bench(args, paddle, world, dist_on):
     opt = paddle.optimizer.AdamW(learning_rate=1e-4, parameters=model.parameters(), weight_decay=0.01,
                                  grad_clip=clip, multi_precision=True,
                                  apply_decay_param_fun=lambda n: not ("norm" in n or n.endswith("b_0")))
-    if world > 1 and args.sharding_stage > 0:
+    if args.sharding_stage > 0:  # same engine at every N (at N=1 the collectives are no-ops)
         from paddlepaddle_amd.distributed.sharding import group_sharded_parallel
         level = {1: "os", 2: "os_g", 3: "p_g_os"}[args.sharding_stage]
         model, opt, _ = group_sharded_parallel(model, opt, level=level)
@@ -165,7 +165,7 @@ def main():
         tps, step_ms, gb, mfu = gpt_bench(args, paddle, world, dist_on)
     ips = resnet_bench(args, paddle, world, dist_on) if args.resnet else None
     if int(os.environ.get("RANK", "0")) == 0:
-        par = (f"sharding{args.sharding_stage}_dp{world}" if world > 1 else "single") + \
+        par = (f"sharding_stage{args.sharding_stage}_degree{world}" if args.sharding_stage else f"dp{world}") + \
               (f"_tp{args.tp}" if args.tp > 1 else "")
         line = {
             "metric": BASELINE_METRIC,

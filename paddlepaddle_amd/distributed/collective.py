@@ -261,12 +261,13 @@ def all_gather(tensor_list, tensor, group=None, sync_op=True):
         tensor_list.clear() if isinstance(tensor_list, list) else None
         tensor_list.append(_wrap(t.clone()))
         return _ret(None, sync_op)
-    out = torch.empty((n,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-    w = dist.all_gather_into_tensor(out, t.contiguous(), group=_pg(group), async_op=not sync_op)
+    out = torch.empty(n * t.numel(), dtype=t.dtype, device=t.device)
+    w = dist.all_gather_into_tensor(out, t.contiguous().view(-1), group=_pg(group), async_op=not sync_op)
 
     def post():
+        o = out.view((n,) + tuple(t.shape))
         tensor_list.clear()
-        tensor_list.extend(_wrap(out[i]) for i in range(n))
+        tensor_list.extend(_wrap(o[i]) for i in range(n))
     return _ret(w, sync_op, post)
 
 
@@ -314,8 +315,8 @@ def reduce_scatter(tensor, tensor_list, op=ReduceOp.SUM, group=None, sync_op=Tru
         tensor._t.copy_(tensor_list[0]._t)
         return _ret(None, sync_op)
     inp = torch.cat([t._t.reshape(-1) for t in tensor_list]).contiguous()
-    w = dist.reduce_scatter_tensor(tensor._t, inp.view((len(tensor_list),) + tuple(tensor._t.shape)),
-                                   op=_TORCH_OP[op], group=_pg(group), async_op=not sync_op)
+    w = dist.reduce_scatter_tensor(tensor._t.view(-1), inp, op=_TORCH_OP[op], group=_pg(group),
+                                   async_op=not sync_op)
     return _ret(w, sync_op)
 
 
@@ -374,8 +375,15 @@ def alltoall(out_tensor_list, in_tensor_list, group=None, sync_op=True):
         out_tensor_list.extend(_wrap(t._t.clone()) for t in in_tensor_list)
         return _ret(None, sync_op)
     ins = [t._t.contiguous() for t in in_tensor_list]
-    outs = [torch.empty_like(t) for t in ins]
-    w = dist.all_to_all(outs, ins, group=_pg(group), async_op=not sync_op)
+    if all(t.shape == ins[0].shape for t in ins):
+        # one all_to_all_single over a packed buffer (single RCCL launch; also what gloo supports)
+        send = torch.cat([t.reshape(-1) for t in ins])
+        recv = torch.empty_like(send)
+        w = dist.all_to_all_single(recv, send, group=_pg(group), async_op=not sync_op)
+        outs = list(recv.view((n,) + tuple(ins[0].shape)).unbind(0))
+    else:
+        outs = [torch.empty_like(t) for t in ins]
+        w = dist.all_to_all(outs, ins, group=_pg(group), async_op=not sync_op)
 
     def post():
         out_tensor_list.clear()

@@ -1,0 +1,477 @@
+"""ZeRO-style sharded data parallelism (Fleet sharding stage 1 / 2 / 3) over RCCL.
+
+Reference: python/paddle/distributed/sharding/group_sharded.py:50 (group_sharded_parallel),
+fleet/meta_parallel/sharding/group_sharded_stage2.py:47, group_sharded_optimizer_stage2.py:53,
+group_sharded_stage3.py:85 (forward pre/post hooks gather & release params, backward hooks
+reduce-scatter grads, optimizer steps on the local shard).
+
+MI355X-native design (one process per GPU, flat buffers, no per-parameter collectives):
+* Parameters are grouped into *units* (each block of a LayerList = one unit, everything else = the
+  root unit) and, inside a unit, into flat buffers by (dtype, weight-decay). A flat buffer is padded
+  to a multiple of the sharding degree W; rank r owns elements [r*S, (r+1)*S).
+* Every model parameter's storage is a view into its unit's full flat buffer, and every gradient is a
+  view into the unit's full flat grad buffer, so a collective moves one contiguous buffer per unit.
+* Gradients are reduce-scattered per unit as soon as the unit's backward is done (overlaps with the
+  remaining backward), in bf16, and accumulated into an fp32 shard gradient (gradient accumulation
+  safe). The optimizer runs only on the local shards (fused multi-tensor AdamW with fp32 master
+  shard). Stage 1/2 then all-gather the updated shards back into the replicated flat params.
+* Stage 3 additionally frees each unit's full parameter storage after use (forward post-hook;
+  re-gathered by a pre-backward hook on the unit output) and prefetches the next unit's all-gather on
+  RCCL's stream while the current unit computes. With 288 GB HBM per GPU, units are whole
+  transformer blocks (a 13B block is 630 MB in bf16) — few, large collectives that keep the xGMI
+  rings in their bandwidth-bound regime.
+"""
+from __future__ import annotations
+
+import contextlib
+
+import torch
+import torch.distributed as dist
+
+from ..distributed import collective as C
+from ..framework.tensor import Parameter, Tensor, _wrap
+from ..nn.layer.common import LayerList
+from ..nn.layer.layers import Layer
+
+
+def _is_nccl(pg):
+    return dist.get_backend(pg) == "nccl"
+
+
+class _Flat:
+    """One flat buffer of same-dtype, same-decay parameters of a unit."""
+
+    def __init__(self, params, world, rank, decay):
+        self.params = params
+        self.world, self.rank = world, rank
+        self.decay = decay
+        t0 = params[0]._t
+        self.dtype, self.device = t0.dtype, t0.device
+        self.numels = [p._t.numel() for p in params]
+        total = sum(self.numels)
+        self.shard_size = (total + world - 1) // world
+        self.padded = self.shard_size * world
+        self.offsets = []
+        off = 0
+        for n in self.numels:
+            self.offsets.append(off)
+            off += n
+        full = torch.zeros(self.padded, dtype=self.dtype, device=self.device)
+        with torch.no_grad():
+            for p, o, n in zip(params, self.offsets, self.numels):
+                full[o:o + n].copy_(p._t.detach().reshape(-1))
+        self.full = full
+        # alias over the same storage with its own version counter: collectives write through it so
+        # re-gathering (stage 3) does not bump the version of tensors autograd saved in forward
+        self.gbuf = torch.empty(0, dtype=self.dtype, device=self.device).set_(full.untyped_storage(), 0,
+                                                                             (self.padded,))
+        # local shard as an optimizer-visible Parameter (trainable flat view of my slice)
+        sh = full[rank * self.shard_size:(rank + 1) * self.shard_size].detach()
+        if world > 1:
+            sh = sh.clone()
+        # degree 1: the shard IS the full buffer and grads stay in the flat bf16 grad buffer
+        self.shard = Parameter(sh, trainable=True, name=f"sharded_flat_{id(self)}")
+        self.shard.need_clip = True
+        self.shard_grad = torch.zeros(self.shard_size, dtype=torch.float32, device=self.device) if world > 1 else None
+        self.full_grad = None
+        # re-point model params at views of the full buffer
+        for p, o, n in zip(params, self.offsets, self.numels):
+            req = p._t.requires_grad
+            p._t = full[o:o + n].view(p._t.shape).detach().requires_grad_(req)
+
+    # -- grads
+    def alloc_full_grad(self):
+        if self.full_grad is None:
+            self.full_grad = torch.zeros(self.padded, dtype=self.dtype, device=self.device)
+            for p, o, n in zip(self.params, self.offsets, self.numels):
+                p._t.grad = self.full_grad[o:o + n].view(p._t.shape)
+        return self.full_grad
+
+    def fold_param_grads(self):
+        """Make sure every param grad lives in full_grad (autograd may have replaced a .grad)."""
+        fg = self.alloc_full_grad()
+        for p, o, n in zip(self.params, self.offsets, self.numels):
+            g = p._t.grad
+            v = fg[o:o + n]
+            if g is None:
+                continue
+            if g.data_ptr() != v.data_ptr():
+                v.copy_(g.reshape(-1))
+                p._t.grad = v.view(p._t.shape)
+
+    def drop_full_grad(self):
+        for p in self.params:
+            p._t.grad = None
+        self.full_grad = None
+
+    # -- params (stage 3 storage management)
+    def free_full(self):
+        self.full.untyped_storage().resize_(0)
+
+    def alloc_full(self):
+        st = self.full.untyped_storage()
+        need = self.padded * self.full.element_size()
+        if st.size() != need:
+            st.resize_(need)
+
+
+class _Unit:
+    def __init__(self, name, layer, params, world, rank, decay_fn):
+        self.name = name
+        self.layer = layer
+        self.flats = []
+        groups = {}
+        for p in params:
+            key = (p._t.dtype, bool(decay_fn(p)))
+            groups.setdefault(key, []).append(p)
+        for (dt, dec), ps in groups.items():
+            self.flats.append(_Flat(ps, world, rank, dec))
+        self.n_params = len(params)
+        self.ready = set()
+        self.gathered = True
+        self.gather_work = []
+        self.rs_work = []
+        self.rs_tmp = []
+        self.id_set = {id(p) for p in params}
+
+
+class GroupShardedEngine:
+    """Implements stage 1/2/3 over a model + inner optimizer."""
+
+    def __init__(self, model, optimizer, stage, group=None, decay_fn=None):
+        self.model = model
+        self.stage = stage
+        self.group = group
+        self.pg = C._pg(group)
+        self.world = C.get_world_size(group)
+        self.rank = C.get_rank(group) if group is not None else (dist.get_rank() if dist.is_initialized() else 0)
+        self.inner_opt = optimizer
+        if decay_fn is None:
+            fn = getattr(optimizer, "_apply_decay_param_fun", None)
+            decay_fn = (lambda p: fn(p.name)) if fn is not None else (lambda p: True)
+        self._broadcast_params()
+        self.units = self._build_units(decay_fn)
+        self._flat_by_param = {}
+        for u in self.units:
+            for f in u.flats:
+                for p in f.params:
+                    self._flat_by_param[id(p)] = (u, f)
+        self._queued = False
+        self._in_backward = False
+        self._install_hooks()
+        self._rebind_optimizer(optimizer)
+        if stage == 3:
+            for u in self.units[1:]:
+                self._release(u)
+
+    # ------------------------------------------------------------------ construction
+    def _broadcast_params(self):
+        if self.world == 1:
+            return
+        src = self.group.ranks[0] if self.group is not None else 0
+        with torch.no_grad():
+            for p in self.model.parameters():
+                dist.broadcast(p._t.data, src=src, group=self.pg)
+
+    def _build_units(self, decay_fn):
+        unit_layers = []
+        seen = set()
+        for _, l in self.model.named_sublayers(include_self=True):
+            if isinstance(l, LayerList):
+                for child in l:
+                    unit_layers.append(child)
+        units = []
+        claimed = set()
+        for i, l in enumerate(unit_layers):
+            ps = [p for p in l.parameters() if not p.stop_gradient and id(p) not in claimed]
+            if not ps:
+                continue
+            claimed.update(id(p) for p in ps)
+            units.append((f"unit{i}", l, ps))
+        root_ps = [p for p in self.model.parameters() if not p.stop_gradient and id(p) not in claimed]
+        out = []
+        if root_ps:
+            out.append(_Unit("root", self.model, root_ps, self.world, self.rank, decay_fn))
+        for name, l, ps in units:
+            out.append(_Unit(name, l, ps, self.world, self.rank, decay_fn))
+        return out
+
+    def _rebind_optimizer(self, opt):
+        shards = []
+        decay_ids = set()
+        for u in self.units:
+            for f in u.flats:
+                shards.append(f.shard)
+                if f.decay:
+                    decay_ids.add(f.shard.name)
+        opt._param_groups = [{"params": shards}]
+        opt._parameter_list = shards
+        if hasattr(opt, "_apply_decay_param_fun"):
+            opt._apply_decay_param_fun = (lambda n, _d=decay_ids: n in _d)
+        clip = getattr(opt, "_grad_clip", None)
+        if clip is not None and hasattr(clip, "_extra_sq_norm_fn") and self.world > 1:
+            pg = self.pg
+
+            def _allreduce_sq(sq):
+                dist.all_reduce(sq, group=pg)
+                return sq
+            clip._extra_sq_norm_fn = _allreduce_sq
+
+    # ------------------------------------------------------------------ hooks
+    def _install_hooks(self):
+        for ui, u in enumerate(self.units):
+            for f in u.flats:
+                for p in f.params:
+                    p._t.register_post_accumulate_grad_hook(self._make_grad_hook(u))
+            if ui == 0:
+                continue  # root unit: gathered for the whole step (embedding / tied head / final norm)
+            u.layer.register_forward_pre_hook(self._make_fwd_pre(ui))
+            u.layer.register_forward_post_hook(self._make_fwd_post(ui))
+
+    def _make_fwd_pre(self, ui):
+        def hook(layer, inputs):
+            u = self.units[ui]
+            self._gather(u)
+            self._wait_gather(u)
+            if self.stage == 3 and torch.is_grad_enabled() and ui + 1 < len(self.units):
+                self._gather(self.units[ui + 1])  # prefetch next block
+            return None
+        return hook
+
+    def _make_fwd_post(self, ui):
+        def hook(layer, inputs, out):
+            u = self.units[ui]
+            if torch.is_grad_enabled():
+                t = out._t if isinstance(out, Tensor) else None
+                if t is not None and t.requires_grad:
+                    t.register_hook(self._make_pre_backward(ui))
+            if self.stage == 3 and not self._in_backward:
+                self._release(u)
+            return None
+        return hook
+
+    def _make_pre_backward(self, ui):
+        def hook(g):
+            self._in_backward = True
+            self._queue_finalize()
+            u = self.units[ui]
+            self._gather(u)
+            self._wait_gather(u)
+            for f in u.flats:
+                f.alloc_full_grad()  # grads accumulate in place into the unit's flat grad buffer
+            if self.stage == 3 and ui - 1 >= 1:
+                self._gather(self.units[ui - 1])
+            return None
+        return hook
+
+    def _make_grad_hook(self, u):
+        is_root = u is self.units[0] if self.units else False
+
+        def hook(t):
+            self._queue_finalize()
+            u.ready.add(id(t))
+            # root unit (tied embedding used twice) is flushed at the end of backward instead
+            if u is not self.units[0] and len(u.ready) == u.n_params:
+                self._reduce_scatter(u)
+                if self.stage == 3:
+                    self._release(u)
+        return hook
+
+    def _queue_finalize(self):
+        if not self._queued:
+            self._queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._finalize_backward)
+
+    # ------------------------------------------------------------------ collectives
+    def _gather(self, u):
+        if u.gathered or self.world == 1:
+            u.gathered = True
+            return
+        for f in u.flats:
+            f.alloc_full()
+            out = f.gbuf
+            inp = f.shard._t.detach()
+            if inp.dtype != out.dtype:
+                inp = inp.to(out.dtype)
+            u.gather_work.append(dist.all_gather_into_tensor(out, inp, group=self.pg, async_op=True))
+        u.gathered = True
+
+    def _wait_gather(self, u):
+        for w in u.gather_work:
+            w.wait()
+        u.gather_work = []
+
+    def _release(self, u):
+        if self.stage != 3 or self.world == 1:
+            return
+        self._wait_gather(u)
+        for f in u.flats:
+            f.free_full()
+        u.gathered = False
+
+    def _reduce_scatter(self, u):
+        for f in u.flats:
+            f.fold_param_grads()
+            fg = f.full_grad
+            if self.world == 1:
+                continue  # grads stay (and accumulate) in the flat buffer
+            tmp = torch.empty(f.shard_size, dtype=fg.dtype, device=fg.device)
+            if _is_nccl(self.pg):
+                w = dist.reduce_scatter_tensor(tmp, fg, op=dist.ReduceOp.AVG, group=self.pg, async_op=True)
+            else:
+                fg.mul_(1.0 / self.world)
+                w = dist.reduce_scatter_tensor(tmp, fg, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+            u.rs_work.append(w)
+            u.rs_tmp.append((f, tmp))
+        u.ready = set()
+
+    def _finalize_backward(self):
+        # flush units whose grads were never (fully) produced, then join every reduce-scatter
+        for u in self.units:
+            if u.ready or (not u.rs_tmp and any(f.full_grad is not None for f in u.flats)):
+                self._reduce_scatter(u)
+        for u in self.units:
+            for w in u.rs_work:
+                w.wait()
+            for f, tmp in u.rs_tmp:
+                f.shard_grad.add_(tmp.float())
+                f.drop_full_grad()
+            u.rs_work, u.rs_tmp = [], []
+            if self.world == 1:
+                continue
+            if self.stage == 3 and u is not self.units[0]:
+                self._release(u)
+            else:
+                for f in u.flats:
+                    if f.full_grad is not None:
+                        f.drop_full_grad()
+        self._queued = False
+        self._in_backward = False
+
+    # ------------------------------------------------------------------ optimizer
+    @torch.no_grad()
+    def step(self):
+        for u in self.units:
+            for f in u.flats:
+                if self.world == 1:
+                    f.shard._t.grad = f.alloc_full_grad()
+                else:
+                    f.shard._t.grad = f.shard_grad
+        self.inner_opt.step()
+        if self.world == 1:
+            return  # shard aliases the full buffer: nothing to publish
+        for u in self.units:
+            if self.stage == 3 and u is not self.units[0]:
+                continue
+            for f in u.flats:
+                dist.all_gather_into_tensor(f.gbuf, f.shard._t.detach().to(f.full.dtype), group=self.pg)
+
+    def clear_grad(self, set_to_zero=True):
+        for u in self.units:
+            for f in u.flats:
+                if self.world == 1:
+                    if f.full_grad is not None:
+                        f.full_grad.zero_()
+                else:
+                    f.shard_grad.zero_()
+                f.shard._t.grad = None
+
+    @torch.no_grad()
+    def gather_all(self):
+        """Materialise every full parameter (for state_dict / eval under stage 3)."""
+        for u in self.units:
+            self._gather(u)
+            self._wait_gather(u)
+
+
+class GroupShardedModel(Layer):
+    def __init__(self, engine):
+        super().__init__()
+        object.__setattr__(self, "_engine", engine)
+        self._layers = engine.model
+
+    def forward(self, *args, **kwargs):
+        e = self._engine
+        if e.units:
+            e._gather(e.units[0])
+            e._wait_gather(e.units[0])
+            if torch.is_grad_enabled():
+                for f in e.units[0].flats:
+                    f.alloc_full_grad()
+        return self._layers(*args, **kwargs)
+
+    def state_dict(self, *args, **kwargs):
+        self._engine.gather_all()
+        return self._layers.state_dict(*args, **kwargs)
+
+    def set_state_dict(self, sd, use_structured_name=True):
+        self._engine.gather_all()
+        r = self._layers.set_state_dict(sd, use_structured_name)
+        for u in self._engine.units:
+            for f in u.flats:
+                f.shard._t.data.copy_(f.full[f.rank * f.shard_size:(f.rank + 1) * f.shard_size])
+        return r
+
+    def get_all_parameters(self, convert2cpu=False):
+        self._engine.gather_all()
+
+    def parameters(self, include_sublayers=True):
+        return self._layers.parameters(include_sublayers)
+
+    def named_parameters(self, prefix="", include_sublayers=True, remove_duplicate=True):
+        return self._layers.named_parameters(prefix, include_sublayers, remove_duplicate)
+
+
+class GroupShardedOptimizer:
+    def __init__(self, engine):
+        self._engine = engine
+        self._inner = engine.inner_opt
+
+    def step(self):
+        self._engine.step()
+
+    def clear_grad(self, set_to_zero=True):
+        self._engine.clear_grad(set_to_zero)
+
+    clear_gradients = clear_grad
+
+    def minimize(self, loss, *a, **k):
+        loss.backward()
+        self.step()
+
+    def get_lr(self):
+        return self._inner.get_lr()
+
+    def set_lr(self, v):
+        self._inner.set_lr(v)
+
+    def state_dict(self):
+        return self._inner.state_dict()
+
+    def set_state_dict(self, sd):
+        self._inner.set_state_dict(sd)
+
+    def __getattr__(self, k):
+        return getattr(self._inner, k)
+
+
+def group_sharded_parallel(model, optimizer, level, scaler=None, group=None, offload=False, sync_buffers=False,
+                           buffer_max_size=2 ** 23, segment_size=2 ** 20, sync_comm=False, dp_group=None,
+                           exclude_layer=None):
+    """level: 'os' (stage 1), 'os_g' (stage 2), 'p_g_os' (stage 3)."""
+    stage = {"os": 1, "os_g": 2, "p_g_os": 3}[level]
+    if not C.is_initialized() and C.get_world_size() > 1:
+        C.init_parallel_env()
+    eng = GroupShardedEngine(model, optimizer, stage, group)
+    return GroupShardedModel(eng), GroupShardedOptimizer(eng), scaler
+
+
+def save_group_sharded_model(model, output, optimizer=None):
+    import os
+    from ..framework.io import save
+    os.makedirs(output, exist_ok=True)
+    sd = model.state_dict()
+    if C.get_rank() == 0:
+        save(sd, os.path.join(output, "model.pdmodel"))
+    if optimizer is not None:
+        save(optimizer.state_dict(), os.path.join(output, f"model.pdopt.rank{C.get_rank()}"))

@@ -1,0 +1,184 @@
+"""Multi-process (gloo, world_size=2, CPU) tests of collectives, DataParallel and sharding stage 1/2/3.
+Each parallel run must reproduce single-process full-batch training of the same model."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _setup(rank, world, port):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), PADDLE_AMD_FORCE_CPU="1")
+    import paddlepaddle_amd as paddle
+    paddle.distributed.init_parallel_env(backend="gloo")
+    return paddle
+
+
+def _make_model(paddle):
+    from paddlepaddle_amd.models.gpt import GPTConfig, GPTForPretraining, GPTPretrainingCriterion
+    paddle.seed(11)
+    cfg = GPTConfig.tiny(num_hidden_layers=3, hidden_dropout_prob=0.0)
+    return cfg, GPTForPretraining(cfg), GPTPretrainingCriterion(cfg)
+
+
+def _data(cfg):
+    g = torch.Generator().manual_seed(5)
+    return torch.randint(0, cfg.vocab_size, (4, 17), generator=g)
+
+
+def _train(paddle, model, crit, opt, ids, steps=3):
+    losses = []
+    for _ in range(steps):
+        loss = crit(model(ids[:, :-1]), ids[:, 1:])
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        losses.append(float(loss))
+    return losses
+
+
+def _collectives_worker(rank, world, port, q):
+    paddle = _setup(rank, world, port)
+    import paddlepaddle_amd.distributed as dist
+    t = paddle.to_tensor([float(rank + 1)] * 4)
+    dist.all_reduce(t)
+    out = {"allreduce": t.numpy().tolist()}
+    lst = []
+    dist.all_gather(lst, paddle.to_tensor([rank]))
+    out["allgather"] = [int(x.numpy()[0]) for x in lst]
+    b = paddle.to_tensor([rank * 10])
+    dist.broadcast(b, src=1)
+    out["broadcast"] = int(b.numpy()[0])
+    rs = paddle.zeros([2])
+    dist.reduce_scatter(rs, [paddle.to_tensor([1.0, 2.0]), paddle.to_tensor([3.0, 4.0])])
+    out["reduce_scatter"] = rs.numpy().tolist()
+    objs = []
+    dist.all_gather_object(objs, {"r": rank})
+    out["objs"] = objs
+    outs = []
+    dist.alltoall(outs, [paddle.to_tensor([rank * 2]), paddle.to_tensor([rank * 2 + 1])])
+    out["alltoall"] = [int(x.numpy()[0]) for x in outs]
+    q.put((rank, out))
+    dist.barrier()
+
+
+def _dp_worker(rank, world, port, mode, q):
+    paddle = _setup(rank, world, port)
+    cfg, model, crit = _make_model(paddle)
+    ids = _data(cfg)
+    local = ids[rank * 2:(rank + 1) * 2]
+    opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    if mode == "dp":
+        model = paddle.DataParallel(model)
+    else:
+        from paddlepaddle_amd.distributed.sharding import group_sharded_parallel
+        model, opt, _ = group_sharded_parallel(model, opt, level=mode)
+    losses = _train(paddle, model, crit, opt, paddle.Tensor(local))
+    sd = {k: v.numpy() for k, v in model.state_dict().items()}
+    q.put((rank, losses, sd))
+    paddle.distributed.barrier()
+
+
+def _spawn(fn, *args, world=2):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=fn, args=(r, world, port, *args, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=150) for _ in range(world)]
+    finally:
+        for p in procs:
+            p.join(timeout=10)
+            if p.is_alive():
+                p.kill()
+    for p in procs:
+        p.join(timeout=60)
+    return sorted(res, key=lambda x: x[0])
+
+
+def test_collectives_gloo():
+    res = _spawn(_collectives_worker)
+    for rank, out in res:
+        assert out["allreduce"] == [3.0] * 4
+        assert out["allgather"] == [0, 1]
+        assert out["broadcast"] == 10
+        assert out["objs"] == [{"r": 0}, {"r": 1}]
+    assert res[0][1]["reduce_scatter"] == [2.0, 4.0] and res[1][1]["reduce_scatter"] == [6.0, 8.0]
+    assert res[0][1]["alltoall"] == [0, 2] and res[1][1]["alltoall"] == [1, 3]
+
+
+def _reference():
+    sys.path.insert(0, ROOT)
+    os.environ["PADDLE_AMD_FORCE_CPU"] = "1"
+    import paddlepaddle_amd as paddle
+    cfg, model, crit = _make_model(paddle)
+    ids = _data(cfg)
+    opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    # full batch == mean of the two half-batch losses (equal sizes)
+    losses = []
+    for _ in range(3):
+        l0 = crit(model(paddle.Tensor(ids[:2, :-1])), paddle.Tensor(ids[:2, 1:]))
+        l1 = crit(model(paddle.Tensor(ids[2:, :-1])), paddle.Tensor(ids[2:, 1:]))
+        loss = (l0 + l1) * 0.5
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        losses.append(float(loss))
+    return losses, {k: v.numpy() for k, v in model.state_dict().items()}
+
+
+@pytest.mark.parametrize("mode", ["dp", "os", "os_g", "p_g_os"])
+def test_data_parallel_and_sharding_match_single_process(mode):
+    ref_losses, ref_sd = _reference()
+    res = _spawn(_dp_worker, mode)
+    (_, l0, sd0), (_, l1, sd1) = res
+    np.testing.assert_allclose((np.array(l0) + np.array(l1)) / 2, ref_losses, rtol=1e-4, atol=1e-5)
+    for k in ref_sd:
+        np.testing.assert_allclose(sd0[k], ref_sd[k], rtol=2e-3, atol=2e-4, err_msg=f"{mode}:{k}")
+        np.testing.assert_allclose(sd1[k], sd0[k], rtol=0, atol=0, err_msg=f"{mode}:{k} replicas differ")
+
+
+@pytest.mark.parametrize("level", ["os", "os_g", "p_g_os"])
+def test_sharding_degree1_matches_plain(level):
+    """Degree-1 sharding (single process, no collectives) must equal plain training, incl. accumulation."""
+    sys.path.insert(0, ROOT)
+    os.environ["PADDLE_AMD_FORCE_CPU"] = "1"
+    import paddlepaddle_amd as paddle
+    from paddlepaddle_amd.distributed.sharding import group_sharded_parallel
+
+    def run(shard):
+        cfg, model, crit = _make_model(paddle)
+        ids = _data(cfg)
+        opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(),
+                                     grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+        if shard:
+            model, opt, _ = group_sharded_parallel(model, opt, level=level)
+        for _ in range(2):
+            for a in range(2):  # gradient accumulation
+                sl = slice(a * 2, a * 2 + 2)
+                loss = crit(model(paddle.Tensor(ids[sl, :-1])), paddle.Tensor(ids[sl, 1:])) * 0.5
+                loss.backward()
+            opt.step()
+            opt.clear_grad()
+        return {k: v.numpy() for k, v in model.state_dict().items()}
+
+    ref, got = run(False), run(True)
+    for k in ref:
+        np.testing.assert_allclose(got[k], ref[k], rtol=1e-5, atol=1e-6, err_msg=k)
