@@ -28,13 +28,13 @@ PEAK_BF16 = 2.5e15
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=4)
+    p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--model", default="gpt3-13b", help="gpt3-13b | gpt3-6.7b | gpt3-1.3b | tiny")
-    p.add_argument("--micro-batch", type=int, default=4)
-    p.add_argument("--accum", type=int, default=1, help="gradient accumulation steps per optimizer step")
+    p.add_argument("--micro-batch", type=int, default=2)
+    p.add_argument("--accum", type=int, default=8, help="gradient accumulation steps per optimizer step")
     p.add_argument("--seq-len", type=int, default=2048)
-    p.add_argument("--recompute", type=int, default=1)
+    p.add_argument("--recompute", type=int, default=0)
     p.add_argument("--sharding-stage", type=int, default=3)
     p.add_argument("--tp", type=int, default=1)
     p.add_argument("--resnet", type=int, default=1, help="also run the ResNet-50 DP benchmark")

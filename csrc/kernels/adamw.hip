@@ -111,7 +111,24 @@ __global__ __launch_bounds__(256) void sq_norm_multi_k(const int64_t* __restrict
     const int64_t n = table[ti * 3 + 1];
     const int dt = (int)table[ti * 3 + 2];
     const int64_t e = s + kChunk < n ? s + kChunk : n;
-    for (int64_t i = s + threadIdx.x; i < e; i += 256) {
+    int64_t i0 = s;
+    if ((((uintptr_t)X) & 15) == 0) {  // 16-byte vector path
+      const int per = dt == kF32 ? 4 : 8;
+      const int64_t ev = s + ((e - s) / per) * per;
+      for (int64_t i = s + (int64_t)threadIdx.x * per; i < ev; i += 256 * per) {
+        if (dt == kF32) {
+          const float4 v = *reinterpret_cast<const float4*>((const float*)X + i);
+          acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+        } else {
+          float v[8];
+          if (dt == kBF16) load8<bf16>((const bf16*)X + i, v); else load8<f16>((const f16*)X + i, v);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc += v[j] * v[j];
+        }
+      }
+      i0 = ev;
+    }
+    for (int64_t i = i0 + threadIdx.x; i < e; i += 256) {
       const float x = ld_any(X, i, dt);
       acc += x * x;
     }

@@ -112,8 +112,10 @@ class GPTEmbeddings(nn.Layer):
         if position_ids is None:
             S = input_ids.shape[-1]
             position_ids = _wrap(torch.arange(S, device=input_ids._t.device).unsqueeze(0))
-        x = self.word_embeddings(input_ids) + self.position_embeddings(position_ids)
-        return self.dropout(x)
+        x = self.word_embeddings(input_ids)._t
+        pe = self.position_embeddings(position_ids)._t
+        p = self.dropout.p if self.training else 0.0
+        return _wrap(_ops.dropout_add(x + pe, None, p, self.training))
 
 
 class GPTAttention(nn.Layer):
@@ -187,8 +189,10 @@ class GPTDecoderLayer(nn.Layer):
         self.dropout2 = nn.Dropout(cfg.hidden_dropout_prob)
 
     def forward(self, x):
-        x = x + self.dropout1(self.self_attn(self.norm1(x)))
-        x = x + self.dropout2(self.mlp(self.norm2(x)))
+        # residual + dropout fused in one HIP pass (mask regenerated from a seed in backward)
+        p = self.dropout1.p if self.training else 0.0
+        x = _wrap(_ops.dropout_add(self.self_attn(self.norm1(x))._t, x._t, p, self.training))
+        x = _wrap(_ops.dropout_add(self.mlp(self.norm2(x))._t, x._t, p, self.training))
         return x
 
 

@@ -36,7 +36,7 @@ def dropout(x, p=0.5, axis=None, training=True, mode="upscale_in_train", name=No
         out = t * mask
         return _wrap(out / (1 - p) if mode == "upscale_in_train" else out)
     if mode == "upscale_in_train":
-        return _wrap(F.dropout(t, p, True))
+        return _wrap(_ops.dropout_add(t, None, p, True))
     mask = (torch.rand_like(t, dtype=torch.float32) >= p).to(t.dtype)
     return _wrap(t * mask)
 

@@ -11,6 +11,7 @@ from .norm import rms_norm, layer_norm  # noqa: F401
 from .loss import softmax_cross_entropy  # noqa: F401
 from .attention import flash_attention, flash_attention_qkvpacked, attention_reference  # noqa: F401
 from .rope import apply_rotary  # noqa: F401
-from .linear import fused_linear  # noqa: F401
+from .linear import fused_linear, colsum  # noqa: F401
+from .dropout import dropout_add  # noqa: F401
 from . import optim  # noqa: F401
 from ._loader import has as has_kernel, hip_enabled_for, LIB_PATH  # noqa: F401

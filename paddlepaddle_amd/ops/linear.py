@@ -1,34 +1,119 @@
 """Linear layers with fused epilogues.
 
-Reference: paddle/phi/kernels/fusion/gpu/fused_gemm_epilogue_kernel.cu,
+Reference: paddle/phi/kernels/fusion/gpu/fused_gemm_epilogue_kernel.cu (+_grad),
 python/paddle/incubate/nn/functional/fused_matmul_bias.py.
 paddle's Linear weight is [in_features, out_features]: y = x @ W + b.
-The GEMM itself runs on hipBLASLt (plain library GEMM, bias folded into the GEMM as beta·C);
-the activation epilogue (bias+GELU) is a fused HIP pass (csrc/kernels/act.hip). A hand-written
-MFMA GEMM (csrc/kernels/gemm.hip) is used when it beats the library on a shape (see ops/gemm.py).
+
+MI355X path (one autograd node per linear):
+  forward : hipBLASLt GEMM with the bias folded into the epilogue (addmm); for GELU MLPs the
+            pre-activation h = x@W is kept and a fused HIP pass computes gelu(h + b)
+  backward: dX = dY Wᵀ and dW = Xᵀ dY on hipBLASLt; the bias gradient is a HIP column reduction
+            (csrc/kernels/linear_epi.hip: coalesced 2-D grid, fp32 partials, no atomics) and, for
+            GELU, one fused pass produces dH = dY·gelu'(h + b) together with db.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn.functional as F
 
+from . import _loader as L
 from .activation import bias_gelu, gelu
 
 
+def colsum(x2d):
+    """Column sums of a [rows, cols] tensor (bias gradient)."""
+    rows, cols = x2d.shape
+    if L.hip_enabled_for(x2d) and x2d.dtype in L._DT and cols % 8 == 0 and x2d.is_contiguous():
+        out = torch.empty(cols, dtype=x2d.dtype, device=x2d.device)
+        ws = torch.empty(256 * cols, dtype=torch.float32, device=x2d.device)
+        L.call("pa_colsum", L.ptr(x2d), L.ptr(out), L.ptr(ws), rows, cols, L.dcode(x2d), L.stream_ptr())
+        return out
+    return x2d.float().sum(0).to(x2d.dtype)
+
+
+def _mm_grads(x2, w, dy2, need_x, need_w):
+    dx = torch.mm(dy2, w.t()) if need_x else None
+    dw = torch.mm(x2.t(), dy2) if need_w else None
+    return dx, dw
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        y = torch.addmm(b, x2, w) if b is not None else torch.mm(x2, w)
+        ctx.save_for_backward(x2, w)
+        ctx.has_b = b is not None
+        ctx.shape = shape
+        return y.view(*shape[:-1], w.shape[1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if dy2.dtype != x2.dtype:
+            dy2 = dy2.to(x2.dtype)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        dx, dw = _mm_grads(x2, w, dy2, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        db = colsum(dy2) if ctx.has_b and ctx.needs_input_grad[2] else None
+        if dx is not None:
+            dx = dx.view(ctx.shape)
+        return dx, dw, db
+
+
+class _LinearBiasGeluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        h = torch.mm(x2, w)
+        y = bias_gelu(h, b)
+        ctx.save_for_backward(x2, w, b, h)
+        ctx.shape = shape
+        return y.view(*shape[:-1], w.shape[1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, b, h = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1]).to(h.dtype).contiguous()
+        rows, cols = h.shape
+        dh = torch.empty_like(h)
+        db = torch.empty(cols, dtype=b.dtype, device=b.device)
+        ws = torch.empty(256 * cols, dtype=torch.float32, device=h.device)
+        L.call("pa_bias_gelu_bwd", L.ptr(h), L.ptr(b), L.ptr(dy2), L.ptr(dh), L.ptr(db), L.ptr(ws), rows, cols,
+               L.dcode(h), L.stream_ptr())
+        dx, dw = _mm_grads(x2, w, dh, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        if dx is not None:
+            dx = dx.view(ctx.shape)
+        return dx, dw, db
+
+
+def _hip_linear_ok(x, w, b):
+    return (L.hip_enabled_for(x) and x.dtype in (torch.bfloat16, torch.float16) and w.dtype == x.dtype
+            and (b is None or b.dtype == x.dtype) and w.shape[1] % 8 == 0 and w.dim() == 2)
+
+
 def fused_linear(x, w, b=None, act=None):
+    hip = _hip_linear_ok(x, w, b)
     if act is None:
+        if hip:
+            return _LinearFn.apply(x, w, b)
         if b is None:
             return torch.matmul(x, w)
         if x.dim() == 2:
             return torch.addmm(b, x, w)
         return torch.addmm(b, x.reshape(-1, x.shape[-1]), w).view(*x.shape[:-1], w.shape[-1])
     if act in ("gelu", "gelu_tanh", "gelu_approximate"):
+        if hip and b is not None:
+            return _LinearBiasGeluFn.apply(x, w, b)
         h = torch.matmul(x, w)
         if b is not None:
             return bias_gelu(h, b)
         return gelu(h, approximate=True)
     if act == "gelu_erf":
-        h = torch.matmul(x, w) if b is None else fused_linear(x, w, b)
+        h = fused_linear(x, w, b)
         return gelu(h, approximate=False)
     if act == "relu":
         h = fused_linear(x, w, b)

@@ -190,3 +190,65 @@ def test_global_norm_multi():
     _lib_loaded()
     ref = sum(t.float().pow(2).sum() for t in ts)
     torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-3)
+
+
+def test_linear_fused_bias_grad():
+    from paddlepaddle_amd.ops.linear import _LinearFn
+    x = torch.randn(4, 96, 256, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.randn(256, 512, device=DEV) * 0.05).bfloat16().requires_grad_(True)
+    b = torch.randn(512, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = ops.fused_linear(x, w, b)
+    _lib_loaded()
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    yr = xr @ wr + br
+    torch.testing.assert_close(y.float(), yr, atol=5e-2, rtol=2e-2)
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    torch.testing.assert_close(b.grad.float(), br.grad, atol=0.5, rtol=2e-2)
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=0.5, rtol=3e-2)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=0.1, rtol=3e-2)
+
+
+def test_linear_bias_gelu_fused():
+    x = torch.randn(128, 256, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.randn(256, 1024, device=DEV) * 0.05).bfloat16().requires_grad_(True)
+    b = torch.randn(1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = ops.fused_linear(x, w, b, act="gelu")
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    yr = F.gelu(xr @ wr + br, approximate="tanh")
+    torch.testing.assert_close(y.float(), yr, atol=5e-2, rtol=3e-2)
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    torch.testing.assert_close(b.grad.float(), br.grad, atol=0.6, rtol=3e-2)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=0.15, rtol=3e-2)
+
+
+def test_colsum():
+    x = torch.randn(3000, 5120, device=DEV, dtype=torch.bfloat16)
+    got = ops.colsum(x)
+    _lib_loaded()
+    torch.testing.assert_close(got.float(), x.float().sum(0), atol=0.3, rtol=1e-2)
+
+
+def test_dropout_add_statistics_and_grad():
+    torch.manual_seed(0)
+    x = torch.ones(1 << 20, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    r = torch.zeros(1 << 20, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = ops.dropout_add(x, r, 0.1, True)
+    _lib_loaded()
+    kept = (y != 0).float().mean().item()
+    assert abs(kept - 0.9) < 0.005
+    vals = y[y != 0].float()
+    assert torch.allclose(vals, torch.full_like(vals, 1 / 0.9), rtol=1e-2)
+    y.backward(torch.ones_like(y))
+    # grad mask == forward mask, scaled
+    torch.testing.assert_close(x.grad.float(), y.detach().float(), atol=1e-2, rtol=1e-2)
+    assert torch.all(r.grad == 1)
+    # recompute determinism: same seed state -> same mask
+    torch.manual_seed(5)
+    a = ops.dropout_add(x.detach(), None, 0.3, True)
+    torch.manual_seed(5)
+    b = ops.dropout_add(x.detach(), None, 0.3, True)
+    assert torch.equal(a, b)
