@@ -199,13 +199,13 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs p) {
     mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
     const float m_new = fmaxf(m_run, mloc);
     const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-    const float alpha = exp2f(m_run - m_use);
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
     float psum = 0.f;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float e = exp2f(sacc[kt][i] - m_use);
+        const float e = __builtin_amdgcn_exp2f(sacc[kt][i] - m_use);
         sacc[kt][i] = e;
         psum += e;
       }
@@ -333,9 +333,10 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
   constexpr int KT_BYTES = BK * D * 2;
   constexpr int QT_BYTES = BM * D * 2;
   constexpr int DST_BYTES = BK * BM * 2;  // dS^T [128 keys][32 q] bf16, 64-byte rows
-  __shared__ __attribute__((aligned(16))) char smem[KT_BYTES + 2 * QT_BYTES + DST_BYTES + 2 * BM * 4];
+  __shared__ __attribute__((aligned(16))) char smem[2 * KT_BYTES + 2 * QT_BYTES + DST_BYTES + 2 * BM * 4];
   char* k_lds = smem;
-  char* q_lds = smem + KT_BYTES;
+  char* v_lds = smem + KT_BYTES;
+  char* q_lds = v_lds + KT_BYTES;
   char* do_lds = q_lds + QT_BYTES;
   char* ds_lds = do_lds + QT_BYTES;
   float* lse_s = reinterpret_cast<float*>(ds_lds + DST_BYTES);
@@ -358,18 +359,13 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
     const int idx = tid + 256 * i;
     const int row = idx / NCH, ch = idx % NCH;
     const int key = kb * BK + row;
-    uint4 val = make_uint4(0, 0, 0, 0);
-    if (key < p.Sk) val = *reinterpret_cast<const uint4*>(kbase + (int64_t)key * p.ks[1] + ch * 8);
+    uint4 val = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+    if (key < p.Sk) {
+      val = *reinterpret_cast<const uint4*>(kbase + (int64_t)key * p.ks[1] + ch * 8);
+      vv = *reinterpret_cast<const uint4*>(vbase + (int64_t)key * p.vs[1] + ch * 8);
+    }
     *reinterpret_cast<uint4*>(k_lds + img_off<NCH>(row, ch)) = val;
-  }
-  // V fragments for this lane's key (B operand of dP = dO V^T)
-  bf16x8_t vf[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    Frag f;
-    if (kj < p.Sk) f.u = *reinterpret_cast<const uint4*>(vbase + (int64_t)kj * p.vs[1] + ks * 16 + hf * 8);
-    else f.u = make_uint4(0, 0, 0, 0);
-    vf[ks] = f.v;
+    *reinterpret_cast<uint4*>(v_lds + img_off<NCH>(row, ch)) = vv;
   }
 
   f32x16 dk_acc[NDT], dv_acc[NDT];
@@ -386,52 +382,87 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
   const float* dlt_b = p.delta + ((int64_t)b * p.H + h) * p.Sq;
   float* dqb = p.dq_acc + (int64_t)b * p.Sq * p.H * D + (int64_t)h * D;  // contiguous [B,Sq,H,D]
 
-  for (int q0 = q_begin; q0 < p.Sq; q0 += BM) {
-    __syncthreads();  // previous iteration's LDS reads done
+  // Q / dO / LSE / delta of the next query block are prefetched into registers while the current
+  // block computes (async-stage split): the HBM latency is hidden behind ~40 MFMAs per wave.
+  constexpr int QLOADS = BM * NCH / 256;
+  uint4 qreg[QLOADS], dreg[QLOADS];
+  float lse_r = INFINITY, dlt_r = 0.f;
+  auto prefetch = [&](int q0) {
 #pragma unroll
-    for (int i = 0; i < BM * NCH / 256; ++i) {
+    for (int i = 0; i < QLOADS; ++i) {
       const int idx = tid + 256 * i;
       const int row = idx / NCH, ch = idx % NCH;
       const int qx = q0 + row;
-      uint4 a = make_uint4(0, 0, 0, 0), g = make_uint4(0, 0, 0, 0);
+      qreg[i] = make_uint4(0, 0, 0, 0);
+      dreg[i] = make_uint4(0, 0, 0, 0);
       if (qx < p.Sq) {
-        a = *reinterpret_cast<const uint4*>(qbase + (int64_t)qx * p.qs[1] + ch * 8);
-        g = *reinterpret_cast<const uint4*>(dobase + (int64_t)qx * p.dos[1] + ch * 8);
+        qreg[i] = *reinterpret_cast<const uint4*>(qbase + (int64_t)qx * p.qs[1] + ch * 8);
+        dreg[i] = *reinterpret_cast<const uint4*>(dobase + (int64_t)qx * p.dos[1] + ch * 8);
       }
-      *reinterpret_cast<uint4*>(q_lds + img_off<NCH>(row, ch)) = a;
-      *reinterpret_cast<uint4*>(do_lds + img_off<NCH>(row, ch)) = g;
     }
     if (tid < BM) {
       const int qx = q0 + tid;
-      lse_s[tid] = qx < p.Sq ? lse_b[qx] * kLog2e : INFINITY;
-      dlt_s[tid] = qx < p.Sq ? dlt_b[qx] : 0.f;
+      lse_r = qx < p.Sq ? lse_b[qx] * kLog2e : INFINITY;
+      dlt_r = qx < p.Sq ? dlt_b[qx] : 0.f;
+    }
+  };
+  if (q_begin < p.Sq) prefetch(q_begin);
+
+  for (int q0 = q_begin; q0 < p.Sq; q0 += BM) {
+    __syncthreads();  // previous iteration's LDS reads done
+#pragma unroll
+    for (int i = 0; i < QLOADS; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx / NCH, ch = idx % NCH;
+      *reinterpret_cast<uint4*>(q_lds + img_off<NCH>(row, ch)) = qreg[i];
+      *reinterpret_cast<uint4*>(do_lds + img_off<NCH>(row, ch)) = dreg[i];
+    }
+    if (tid < BM) {
+      lse_s[tid] = lse_r;
+      dlt_s[tid] = dlt_r;
     }
     __syncthreads();
+    if (q0 + BM < p.Sq) prefetch(q0 + BM);
 
     // S = Q K^T and dP = dO V^T : rows q (registers), cols = this lane's key
     f32x16 sacc = zero16(), pacc = zero16();
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      Frag qa, da, kb8;
+      Frag qa, da, kb8, vb8;
       qa.u = lds_b128(q_lds, img_off<NCH>(r, 2 * ks + hf));
       da.u = lds_b128(do_lds, img_off<NCH>(r, 2 * ks + hf));
       kb8.u = lds_b128(k_lds, img_off<NCH>(w * 32 + r, 2 * ks + hf));
+      vb8.u = lds_b128(v_lds, img_off<NCH>(w * 32 + r, 2 * ks + hf));
       sacc = mfma32(qa.v, kb8.v, sacc);
-      pacc = mfma32(da.v, vf[ks], pacc);
+      pacc = mfma32(da.v, vb8.v, pacc);
     }
-    float pv[16], dsv[16];
+    // P and dS computed in place, then packed straight into bf16 MFMA fragments.
+    // lse/delta for this lane's 16 query rows: 4 x 16-byte LDS reads each (rows 8g+4hf .. +3)
+    const bool need_mask = kj >= p.Sk || (p.causal && kb * BK + BK - 1 > q0 + shift);
+    float4 l4[4], d4[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      l4[g] = *reinterpret_cast<const float4*>(lse_s + 8 * g + 4 * hf);
+      d4[g] = *reinterpret_cast<const float4*>(dlt_s + 8 * g + 4 * hf);
+    }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int qr = (i & 3) + 8 * (i >> 2) + 4 * hf;
-      const int qx = q0 + qr;
-      float pr = exp2f(sacc[i] * p.scale_log2 - lse_s[qr]);
-      if (kj >= p.Sk || (p.causal && kj > qx + shift)) pr = 0.f;
-      pv[i] = pr;
-      dsv[i] = pr * (pacc[i] - dlt_s[qr]);
+      const float lv = (&l4[i >> 2].x)[i & 3], dv = (&d4[i >> 2].x)[i & 3];
+      float pr = __builtin_amdgcn_exp2f(sacc[i] * p.scale_log2 - lv);
+      if (need_mask && (kj >= p.Sk || (p.causal && kj > q0 + qr + shift))) pr = 0.f;
+      sacc[i] = pr;
+      pacc[i] = pr * (pacc[i] - dv);
     }
     bf16x8_t pf[2], sf[2];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) { pf[s] = pack8(pv + 8 * s); sf[s] = pack8(dsv + 8 * s); }
+    for (int s = 0; s < 2; ++s) {
+      float a[8], c[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { a[j] = sacc[8 * s + j]; c[j] = pacc[8 * s + j]; }
+      pf[s] = pack8(a);
+      sf[s] = pack8(c);
+    }
 
     // dV^T += dO^T P ; dK^T += Q^T dS  (A via transposed reads of the dO / Q images)
 #pragma unroll
@@ -453,13 +484,14 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
 
     // dS^T tile [128 keys][32 q] bf16: lane writes its key row, 4 consecutive q per 8-byte store
     {
+      // fragment s, elements 0..3 = q 16s+4hf+0..3, elements 4..7 = q 16s+8+4hf+0..3
       char* rowp = ds_lds + (w * 32 + r) * (BM * 2);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        uint2 v2;
-        v2.x = pack_bf16(dsv[4 * g + 0], dsv[4 * g + 1]);
-        v2.y = pack_bf16(dsv[4 * g + 2], dsv[4 * g + 3]);
-        *reinterpret_cast<uint2*>(rowp + (8 * g + 4 * hf) * 2) = v2;
+      for (int s = 0; s < 2; ++s) {
+        Frag f;
+        f.v = sf[s];
+        *reinterpret_cast<uint2*>(rowp + (16 * s + 4 * hf) * 2) = make_uint2(f.u.x, f.u.y);
+        *reinterpret_cast<uint2*>(rowp + (16 * s + 8 + 4 * hf) * 2) = make_uint2(f.u.z, f.u.w);
       }
     }
     __syncthreads();
@@ -479,11 +511,23 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
         bb.h[1] = lds_tr(k_lds, img_off<NCH>(kr0 + 4 + qq, cch) + 8 * (pp & 1));
         qacc = mfma32(a.v, bb.v, qacc);
       }
+      if (p.causal >= 0) {
+        float* dst = dqb + (int64_t)q0 * p.H * D + dt * 32 + r;
+        const int64_t rs = (int64_t)p.H * D;
+        if (q0 + BM <= p.Sq) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qr = (i & 3) + 8 * (i >> 2) + 4 * hf;
-        const int qx = q0 + qr;
-        if (qx < p.Sq) atomicAdd(dqb + (int64_t)qx * p.H * D + dt * 32 + r, qacc[i] * p.scale);
+          for (int i = 0; i < 16; ++i)
+            atomicAdd(dst + (int64_t)((i & 3) + 8 * (i >> 2) + 4 * hf) * rs, qacc[i] * p.scale);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int qr = (i & 3) + 8 * (i >> 2) + 4 * hf;
+            if (q0 + qr < p.Sq) atomicAdd(dst + (int64_t)qr * rs, qacc[i] * p.scale);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) asm volatile("" ::"v"(qacc[i]));
       }
     }
   }
@@ -572,4 +616,13 @@ PA_EXPORT int pa_flash_attn_bwd(const void* q, const void* k, const void* v, con
     PA_CHECK_LAUNCH();
   }
   return 0;
+}
+
+// ablation hook (timing only): causal flag -1/-2 skips the dQ atomics
+PA_EXPORT int pa_flash_attn_bwd_ablate(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                                       const float* lse, void* dq, void* dk, void* dv, float* dq_acc, float* delta,
+                                       const int64_t* strides, int B, int Sq, int Sk, int H, int Hk, int D,
+                                       float scale, int causal, hipStream_t st) {
+  return pa_flash_attn_bwd(q, k, v, o, dout, lse, dq, dk, dv, dq_acc, delta, strides, B, Sq, Sk, H, Hk, D, scale,
+                           causal, st);
 }
