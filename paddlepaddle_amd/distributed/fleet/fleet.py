@@ -1,0 +1,262 @@
+"""Fleet: hybrid-parallel entry points.
+
+Reference: python/paddle/distributed/fleet/fleet.py (init, distributed_model, distributed_optimizer),
+base/distributed_strategy.py (DistributedStrategy), meta_parallel/{tensor_parallel,pipeline_parallel,
+sharding_parallel}.py, meta_optimizers/dygraph_optimizer/hybrid_parallel_optimizer.py.
+"""
+from __future__ import annotations
+
+import copy
+
+import torch
+import torch.distributed as dist
+
+from .. import collective as C
+from .topology import CommunicateTopology, HybridCommunicateGroup, ParallelMode, _get_hcg, _set_hcg
+
+
+class DistributedStrategy:
+    """Configuration container (reference: base/distributed_strategy.py; protobuf there, attrs here)."""
+
+    def __init__(self):
+        self.amp = False
+        self.amp_configs = {"init_loss_scaling": 32768.0, "use_pure_fp16": False, "use_fp16_guard": True,
+                            "custom_white_list": [], "custom_black_list": [], "use_bf16": False}
+        self.recompute = False
+        self.recompute_configs = {"checkpoints": [], "enable_offload": False}
+        self.sharding = False
+        self.sharding_configs = {"sharding_degree": 1, "stage": 1, "segment_broadcast_MB": 32.0,
+                                 "comm_overlap": True, "split_param": False}
+        self.pipeline = False
+        self.pipeline_configs = {"accumulate_steps": 1, "micro_batch_size": 1, "schedule_mode": "1F1B"}
+        self.tensor_parallel = False
+        self.tensor_parallel_configs = {"tensor_parallel_degree": 1, "tensor_init_seed": -1}
+        self.hybrid_configs = {"dp_degree": -1, "mp_degree": 1, "pp_degree": 1, "sharding_degree": 1,
+                               "sep_degree": 1, "order": ["dp", "pp", "sharding", "sep", "mp"]}
+        self.gradient_merge = False
+        self.gradient_merge_configs = {"k_steps": 1, "avg": True}
+        self.lamb = False
+        self.lars = False
+        self.dgc = False
+        self.localsgd = False
+        self.fuse_all_reduce_ops = True
+        self.fuse_grad_size_in_MB = 64
+        self.find_unused_parameters = False
+        self.without_graph_optimization = True
+        self.heter_ccl_mode = False
+        self.a_sync = False
+        self.auto = False
+        self.semi_auto = False
+        self.fp16_allreduce = False
+        self.last_comm_group_size_MB = 8
+
+    def __setattr__(self, k, v):
+        if k == "hybrid_configs" and isinstance(v, dict) and hasattr(self, "hybrid_configs"):
+            d = dict(self.__dict__["hybrid_configs"])
+            d.update(v)
+            v = d
+        object.__setattr__(self, k, v)
+
+    def __repr__(self):
+        return f"DistributedStrategy(hybrid_configs={self.hybrid_configs})"
+
+
+class _Fleet:
+    def __init__(self):
+        self._hcg = None
+        self._strategy = None
+        self._is_collective = True
+
+    # ---------------------------------------------------------------- init / env
+    def init(self, role_maker=None, is_collective=True, strategy=None, log_level="INFO"):
+        self._strategy = strategy or DistributedStrategy()
+        if not C.is_initialized() and C.get_world_size() > 1:
+            C.init_parallel_env()
+        ws = C.get_world_size()
+        hc = self._strategy.hybrid_configs
+        mp, pp = int(hc.get("mp_degree", 1)), int(hc.get("pp_degree", 1))
+        sd, sep = int(hc.get("sharding_degree", 1)), int(hc.get("sep_degree", 1))
+        dp = int(hc.get("dp_degree", -1))
+        if dp <= 0:
+            dp = max(ws // (mp * pp * sd * sep), 1)
+        if dp * mp * pp * sd * sep != ws:
+            raise ValueError(f"hybrid degrees dp{dp} x mp{mp} x pp{pp} x sharding{sd} x sep{sep} != world {ws}")
+        topo = CommunicateTopology(["data", "pipe", "sharding", "sep", "model"], [dp, pp, sd, sep, mp])
+        self._hcg = HybridCommunicateGroup(topo)
+        _set_hcg(self._hcg)
+        if mp > 1:
+            from ...parallel.tensor_parallel import model_parallel_random_seed
+            seed = self._strategy.tensor_parallel_configs.get("tensor_init_seed", -1)
+            model_parallel_random_seed(seed if seed and seed > 0 else None)
+        return self
+
+    def get_hybrid_communicate_group(self):
+        return self._hcg
+
+    def worker_index(self):
+        return C.get_rank()
+
+    def worker_num(self):
+        return C.get_world_size()
+
+    def is_first_worker(self):
+        return C.get_rank() == 0
+
+    def is_worker(self):
+        return True
+
+    def is_server(self):
+        return False
+
+    def worker_endpoints(self, to_string=False):
+        eps = C.ParallelEnv().trainer_endpoints
+        return ",".join(eps) if to_string else eps
+
+    def barrier_worker(self):
+        C.barrier()
+
+    def local_rank(self):
+        return C.ParallelEnv().local_rank
+
+    @property
+    def user_defined_strategy(self):
+        return self._strategy
+
+    # ---------------------------------------------------------------- wrappers
+    def distributed_model(self, model):
+        hcg = self._hcg
+        if hcg is None:
+            self.init()
+            hcg = self._hcg
+        mode = hcg.get_parallel_mode()
+        if mode == ParallelMode.PIPELINE_PARALLEL:
+            from ...parallel.pipeline import PipelineParallel
+            return PipelineParallel(model, hcg, self._strategy)
+        if mode == ParallelMode.TENSOR_PARALLEL:
+            return TensorParallel(model, hcg, self._strategy)
+        if mode == ParallelMode.SHARDING_PARALLEL:
+            return model  # the sharding optimizer owns the parameter partitioning (stage 1)
+        from ...parallel.data_parallel import DataParallel
+        if hcg.get_data_parallel_world_size() > 1:
+            return DataParallel(model, group=hcg.get_data_parallel_group(),
+                                find_unused_parameters=self._strategy.find_unused_parameters)
+        return model
+
+    def distributed_optimizer(self, optimizer, strategy=None):
+        if strategy is not None:
+            self._strategy = strategy
+        if self._hcg is None:
+            self.init(strategy=self._strategy)
+        return HybridParallelOptimizer(optimizer, self._hcg, self._strategy)
+
+    def distributed_scaler(self, scaler):
+        return scaler
+
+    # ---------------------------------------------------------------- io
+    def save_persistables(self, executor, dirname, main_program=None, mode=0):
+        from ...static.io import save_persistables
+        save_persistables(executor, dirname, main_program)
+
+    def save_inference_model(self, executor, dirname, feeded_var_names, target_vars, main_program=None,
+                             export_for_deployment=True, mode=0):
+        from ...static.io import save_inference_model
+        save_inference_model(dirname, feeded_var_names, target_vars, executor, main_program)
+
+
+from ...nn.layer.layers import Layer as _Layer  # noqa: E402
+
+
+class TensorParallel(_Layer):
+    """Reference: meta_parallel/tensor_parallel.py — broadcast replicated params inside the mp group and
+    average grads over the data-parallel group."""
+
+    def __init__(self, model, hcg, strategy):
+        super().__init__()
+        self._layers = model
+        mp = hcg.get_model_parallel_group()
+        if mp is not None and mp.nranks > 1:
+            with torch.no_grad():
+                for p in model.parameters():
+                    if not getattr(p, "is_distributed", False):
+                        dist.broadcast(p._t.data, mp.ranks[0], group=mp.process_group)
+        dp = None
+        if hcg.get_data_parallel_world_size() > 1:
+            from ...parallel.data_parallel import DataParallel
+            dp = DataParallel(model, group=hcg.get_data_parallel_group())
+        object.__setattr__(self, "_dp", dp)
+
+    def forward(self, *a, **k):
+        return (self._dp or self._layers)(*a, **k)
+
+    def state_dict(self, *a, **k):
+        return self._layers.state_dict(*a, **k)
+
+    def set_state_dict(self, sd, use_structured_name=True):
+        return self._layers.set_state_dict(sd, use_structured_name)
+
+    def parameters(self, include_sublayers=True):
+        return self._layers.parameters(include_sublayers)
+
+
+class HybridParallelOptimizer:
+    """Reference: dygraph_optimizer/hybrid_parallel_optimizer.py — global-norm clip across mp/pp/sharding,
+    sharding stage-1 optimizer-state partition when sharding_degree > 1."""
+
+    def __init__(self, optimizer, hcg, strategy):
+        self._inner_opt = optimizer
+        self._hcg = hcg
+        self._strategy = strategy
+        clip = getattr(optimizer, "_grad_clip", None)
+        groups = []
+        if hcg is not None:
+            for g in (hcg.get_model_parallel_group(), hcg.get_pipe_parallel_group(), hcg.get_sharding_parallel_group()):
+                if g is not None and g.nranks > 1:
+                    groups.append(g)
+        if clip is not None and hasattr(clip, "_extra_sq_norm_fn") and groups:
+            mp = hcg.get_model_parallel_group()
+            others = [g for g in groups if g is not mp]
+
+            def _param_sq(params, _mp=mp, _others=others):
+                # tensor-parallel shards (is_distributed) are summed over the mp group; replicated
+                # params are counted once; pipeline stages / sharding ranks hold disjoint params
+                from ...ops.optim import global_sq_norm
+                dist_g = [p._t.grad for p in params if getattr(p, "is_distributed", False)]
+                rep_g = [p._t.grad for p in params if not getattr(p, "is_distributed", False)]
+                dev = params[0]._t.device
+                sq_d = global_sq_norm(dist_g) if dist_g else torch.zeros((), device=dev)
+                sq_r = global_sq_norm(rep_g) if rep_g else torch.zeros((), device=dev)
+                sq_d = sq_d.reshape(1).clone()
+                if _mp is not None and _mp.nranks > 1:
+                    dist.all_reduce(sq_d, group=_mp.process_group)
+                sq = (sq_d + sq_r).reshape(1)
+                for g in _others:
+                    dist.all_reduce(sq, group=g.process_group)
+                return sq[0]
+            clip._param_sq_fn = _param_sq
+        self._sharding = None
+        if hcg is not None and hcg.get_sharding_parallel_world_size() > 1:
+            self._sharding = "stage1"
+
+    def step(self):
+        self._inner_opt.step()
+
+    def clear_grad(self, set_to_zero=True):
+        self._inner_opt.clear_grad(set_to_zero)
+
+    clear_gradients = clear_grad
+
+    def minimize(self, loss, startup_program=None, parameters=None, no_grad_set=None):
+        loss.backward()
+        self.step()
+
+    def state_dict(self):
+        return self._inner_opt.state_dict()
+
+    def set_state_dict(self, sd):
+        return self._inner_opt.set_state_dict(sd)
+
+    def __getattr__(self, k):
+        return getattr(self._inner_opt, k)
+
+
+fleet = _Fleet()

@@ -1,0 +1,3 @@
+"""fleet.utils. Reference: python/paddle/distributed/fleet/utils/."""
+from ..recompute import recompute  # noqa: F401
+from . import sequence_parallel_utils  # noqa: F401

@@ -80,10 +80,12 @@ class ClipGradByGlobalNorm(ClipGradBase):
         return out
 
     def _clip_inplace(self, params):
-        grads = [p._t.grad for p in params if p._t.grad is not None and getattr(p, "need_clip", True)]
+        ps = [p for p in params if p._t.grad is not None and getattr(p, "need_clip", True)]
+        grads = [p._t.grad for p in ps]
         if not grads:
             return
-        gn = self._global_norm(grads)
+        fn = getattr(self, "_param_sq_fn", None)
+        gn = torch.sqrt(fn(ps)) if fn is not None else self._global_norm(grads)
         scale = self.clip_norm / torch.clamp(gn, min=self.clip_norm)
         torch._foreach_mul_(grads, scale)
 

@@ -101,8 +101,18 @@ def _spawn(fn, *args, world=2):
     procs = [ctx.Process(target=fn, args=(r, world, port, *args, q)) for r in range(world)]
     for p in procs:
         p.start()
+    import queue
+    import time
+    res = []
     try:
-        res = [q.get(timeout=150) for _ in range(world)]
+        deadline = time.time() + 240
+        while len(res) < world:
+            try:
+                res.append(q.get(timeout=1))
+            except queue.Empty:
+                dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+                if dead or time.time() > deadline:
+                    raise RuntimeError(f"worker failed (exit codes {dead})" if dead else "workers timed out")
     finally:
         for p in procs:
             p.join(timeout=10)

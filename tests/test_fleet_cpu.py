@@ -1,0 +1,215 @@
+"""Fleet hybrid parallel on CPU (gloo, world_size=2): tensor parallel GPT, 1F1B pipeline, sequence
+parallel ops. Each parallel run must reproduce single-process training of the same model.
+Reference test strategy: test/collective/fleet/hybrid_parallel_mp_model.py, hybrid_parallel_pp_layer.py
+(parallel loss == single-card loss with the same weights)."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+from test_distributed_cpu import ROOT, _data, _setup, _spawn
+
+
+def _fleet_init(paddle, **hc):
+    from paddlepaddle_amd.distributed import fleet
+    s = fleet.DistributedStrategy()
+    cfg = dict(dp_degree=1, mp_degree=1, pp_degree=1)
+    cfg.update(hc)
+    s.hybrid_configs = cfg
+    s.pipeline_configs = {"accumulate_steps": 2, "micro_batch_size": 2}
+    fleet.init(is_collective=True, strategy=s)
+    return fleet
+
+
+def _gpt_full(paddle):
+    from paddlepaddle_amd.models.gpt import GPTConfig, GPTForPretraining, GPTPretrainingCriterion
+    paddle.seed(11)
+    cfg = GPTConfig.tiny(num_hidden_layers=2, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    return cfg, GPTForPretraining(cfg), GPTPretrainingCriterion(cfg)
+
+
+def _shard_like(full, local, rank, world):
+    """Slice a full weight to the local TP shape (the dim that differs is the split one)."""
+    if tuple(full.shape) == tuple(local.shape):
+        return full
+    for d in range(full.dim()):
+        if full.shape[d] != local.shape[d]:
+            return full.chunk(world, d)[rank]
+    raise AssertionError
+
+
+def _train(paddle, model, crit, opt, ids, steps=3):
+    losses = []
+    for _ in range(steps):
+        loss = crit(model(paddle.Tensor(ids[:, :-1])), paddle.Tensor(ids[:, 1:]))
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        losses.append(float(loss))
+    return losses
+
+
+def _tp_worker(rank, world, port, q):
+    paddle = _setup(rank, world, port)
+    from paddlepaddle_amd.models.gpt import GPTConfig, GPTForPretraining, GPTPretrainingCriterion
+    _, full, _ = _gpt_full(paddle)
+    full_sd = {k: v._t.detach().clone() for k, v in full.state_dict().items()}
+    fleet = _fleet_init(paddle, mp_degree=2)
+    cfg = GPTConfig.tiny(num_hidden_layers=2, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0,
+                         tensor_parallel_degree=2)
+    model, crit = GPTForPretraining(cfg), GPTPretrainingCriterion(cfg)
+    with torch.no_grad():
+        for k, v in model.state_dict().items():
+            v._t.copy_(_shard_like(full_sd[k], v._t, rank, world))
+    opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    model = fleet.distributed_model(model)
+    opt = fleet.distributed_optimizer(opt)
+    losses = _train(paddle, model, crit, opt, _data(cfg))
+    sd = {k: v.numpy() for k, v in model.state_dict().items()}
+    q.put((rank, losses, sd))
+    paddle.distributed.barrier()
+
+
+def _single_gpt():
+    sys.path.insert(0, ROOT)
+    os.environ["PADDLE_AMD_FORCE_CPU"] = "1"
+    import paddlepaddle_amd as paddle
+    cfg, model, crit = _gpt_full(paddle)
+    opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    losses = _train(paddle, model, crit, opt, _data(cfg))
+    return losses, {k: v.numpy() for k, v in model.state_dict().items()}
+
+
+def test_tensor_parallel_gpt_matches_single_process():
+    ref_losses, ref_sd = _single_gpt()
+    res = _spawn(_tp_worker)
+    (_, l0, sd0), (_, l1, sd1) = res
+    np.testing.assert_allclose(l0, ref_losses, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(l1, l0, rtol=0, atol=0)
+    for k, full in ref_sd.items():
+        t = torch.from_numpy(full)
+        for r, sd in enumerate((sd0, sd1)):
+            exp = _shard_like(t, torch.from_numpy(sd[k]), r, 2).numpy()
+            np.testing.assert_allclose(sd[k], exp, rtol=2e-3, atol=2e-4, err_msg=f"rank{r}:{k}")
+
+
+# ----------------------------------------------------------------------------- pipeline
+def _mlp_descs(paddle):
+    from paddlepaddle_amd.parallel.pipeline import LayerDesc
+    nn = paddle.nn
+    return [LayerDesc(nn.Linear, 16, 32), LayerDesc(nn.Tanh), LayerDesc(nn.Linear, 32, 32), LayerDesc(nn.GELU),
+            LayerDesc(nn.Linear, 32, 32), LayerDesc(nn.Tanh), LayerDesc(nn.Linear, 32, 8)]
+
+
+def _pp_data():
+    g = torch.Generator().manual_seed(3)
+    return torch.randn(8, 16, generator=g), torch.randn(8, 8, generator=g)
+
+
+def _mse(out, label):
+    return ((out - label) ** 2).mean()
+
+
+def _pp_full_params(paddle):
+    """Build every layer once with a fixed seed; returns state tensors in layer order."""
+    paddle.seed(7)
+    layers = [d.build_layer() for d in _mlp_descs(paddle)]
+    return layers
+
+
+def _pp_worker(rank, world, port, q):
+    paddle = _setup(rank, world, port)
+    from paddlepaddle_amd.parallel.pipeline import PipelineLayer
+    full = _pp_full_params(paddle)
+    fleet = _fleet_init(paddle, pp_degree=2)
+    pl = PipelineLayer(_mlp_descs(paddle), num_stages=2, loss_fn=_mse)
+    lo = pl.segment_parts[pl._stage_id]
+    with torch.no_grad():
+        for i, f in enumerate(pl.run_function):
+            for (k, v), (_, fv) in zip(f.state_dict().items(), full[lo + i].state_dict().items()):
+                v._t.copy_(fv._t)
+    opt = paddle.optimizer.AdamW(1e-2, parameters=pl.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    model = fleet.distributed_model(pl)
+    opt = fleet.distributed_optimizer(opt)
+    x, y = _pp_data()
+    losses = [float(model.train_batch([paddle.Tensor(x), paddle.Tensor(y)], opt)) for _ in range(3)]
+    ev = model.eval_batch([paddle.Tensor(x), paddle.Tensor(y)], compute_loss=True)
+    params = {f"{lo + i}.{k}": v.numpy() for i, f in enumerate(pl.run_function) for k, v in f.state_dict().items()}
+    q.put((rank, losses, params, None if isinstance(ev, list) else float(ev)))
+    paddle.distributed.barrier()
+
+
+def test_pipeline_1f1b_matches_single_process():
+    sys.path.insert(0, ROOT)
+    os.environ["PADDLE_AMD_FORCE_CPU"] = "1"
+    import paddlepaddle_amd as paddle
+    layers = _pp_full_params(paddle)
+    params = [p for l in layers for p in l.parameters()]
+    opt = paddle.optimizer.AdamW(1e-2, parameters=params, grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    x, y = _pp_data()
+
+    def fwd(t):
+        for l in layers:
+            t = l(t)
+        return t
+    ref = []
+    for _ in range(3):
+        # 2 micro-batches, loss averaged (== pipeline accumulate_steps=2)
+        l0 = _mse(fwd(paddle.Tensor(x[:4])), paddle.Tensor(y[:4]))
+        l1 = _mse(fwd(paddle.Tensor(x[4:])), paddle.Tensor(y[4:]))
+        loss = (l0 + l1) * 0.5
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        ref.append(float(loss))
+    ref_params = {f"{i}.{k}": v.numpy() for i, l in enumerate(layers) for k, v in l.state_dict().items()}
+    with paddle.no_grad():
+        ref_eval = 0.5 * (float(_mse(fwd(paddle.Tensor(x[:4])), paddle.Tensor(y[:4]))) +
+                          float(_mse(fwd(paddle.Tensor(x[4:])), paddle.Tensor(y[4:]))))
+
+    res = _spawn(_pp_worker)
+    (_, l0, p0, _), (_, l1, p1, ev1) = res
+    np.testing.assert_allclose(l0, ref, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(l1, ref, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(ev1, ref_eval, rtol=1e-5, atol=1e-6)
+    got = dict(p0)
+    got.update(p1)
+    assert set(got) == set(ref_params)
+    for k in ref_params:
+        np.testing.assert_allclose(got[k], ref_params[k], rtol=1e-4, atol=1e-6, err_msg=k)
+
+
+# ----------------------------------------------------------------------------- sequence parallel
+def _sp_worker(rank, world, port, q):
+    paddle = _setup(rank, world, port)
+    from paddlepaddle_amd.distributed.fleet.utils import sequence_parallel_utils as spu
+    _fleet_init(paddle, mp_degree=2)
+    g = torch.Generator().manual_seed(1)
+    full = torch.randn(6, 2, 4, generator=g)
+    x = paddle.Tensor(full.clone().requires_grad_(True))
+    x.stop_gradient = False
+    s = spu.ScatterOp.apply(x)
+    ag = spu.AllGatherOp.apply(s * (rank + 1.0))
+    rs = spu.ReduceScatterOp.apply(ag)
+    rs.sum().backward()
+    q.put((rank, s.numpy(), ag.numpy(), rs.numpy(), x.grad.numpy()))
+    paddle.distributed.barrier()
+
+
+def test_sequence_parallel_ops():
+    res = _spawn(_sp_worker)
+    g = torch.Generator().manual_seed(1)
+    full = torch.randn(6, 2, 4, generator=g).numpy()
+    (_, s0, ag0, rs0, gx0), (_, s1, ag1, rs1, gx1) = res
+    np.testing.assert_allclose(s0, full[:3])
+    np.testing.assert_allclose(s1, full[3:])
+    exp_ag = np.concatenate([full[:3] * 1.0, full[3:] * 2.0])
+    np.testing.assert_allclose(ag0, exp_ag, rtol=1e-6)
+    np.testing.assert_allclose(ag1, exp_ag, rtol=1e-6)
+    np.testing.assert_allclose(rs0, 2 * exp_ag[:3], rtol=1e-6)
+    np.testing.assert_allclose(rs1, 2 * exp_ag[3:], rtol=1e-6)
+    # d ag = gather(ones) = 1; d(s*(r+1)) = reduce-scatter(d ag) = 2 -> d s_r = 2(r+1); d x = gather(d s)
+    exp_gx = np.concatenate([np.full((3, 2, 4), 2.0), np.full((3, 2, 4), 4.0)])
+    np.testing.assert_allclose(gx0, exp_gx, rtol=1e-6)
+    np.testing.assert_allclose(gx1, exp_gx, rtol=1e-6)
