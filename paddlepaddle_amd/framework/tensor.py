@@ -12,6 +12,7 @@ HIP runtime: every op that we implement with a HIP kernel registers its own back
 from __future__ import annotations
 
 import itertools
+import weakref
 
 import numpy as np
 import torch
@@ -20,6 +21,7 @@ from . import dtype as _dt
 from .place import CPUPlace, CUDAPlace, Place, _get_torch_device, place_from_torch_device, to_torch_device
 
 _name_counter = itertools.count()
+_PARAM_OF = weakref.WeakValueDictionary()  # id(parameter buffer) -> Parameter (static graph lookups)
 
 
 def _unwrap(x):
@@ -562,6 +564,7 @@ class Parameter(Tensor):
         self._t = t
         self._name = name
         self._persistable = True
+        _PARAM_OF[id(t)] = self
         self.trainable = trainable
         self.optimize_attr = attrs.get("optimize_attr", {"learning_rate": 1.0})
         self.regularizer = attrs.get("regularizer", None)
@@ -588,6 +591,7 @@ class Parameter(Tensor):
         """Swap the underlying buffer (used by sharding / amp decorate) keeping identity."""
         req = self._t.requires_grad
         self._t = t.detach().requires_grad_(req)
+        _PARAM_OF[id(self._t)] = self
 
 
 EagerParamBase = Parameter

@@ -9,6 +9,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _loader as L
+from ..framework.trace_hook import static_op
 
 
 class _GeluHIP(torch.autograd.Function):
@@ -31,6 +32,7 @@ class _GeluHIP(torch.autograd.Function):
         return dx, None
 
 
+@static_op
 def gelu(x, approximate=False):
     if L.hip_enabled_for(x) and x.dtype in L._DT and x.numel() % 8 == 0:
         return _GeluHIP.apply(x, bool(approximate))
@@ -63,6 +65,7 @@ class _BiasGeluHIP(torch.autograd.Function):
         return dh.view(ctx.shape), db
 
 
+@static_op
 def bias_gelu(x, bias):
     """gelu_tanh(x + bias) (GPT MLP epilogue)."""
     if L.hip_enabled_for(x) and x.dtype in L._DT and x.shape[-1] % 8 == 0:
@@ -70,6 +73,7 @@ def bias_gelu(x, bias):
     return F.gelu(x + bias, approximate="tanh")
 
 
+@static_op
 def silu(x):
     return F.silu(x)
 
@@ -104,6 +108,7 @@ class _SwigluHIP(torch.autograd.Function):
         return da.reshape(ctx.shape), db.reshape(ctx.shape)
 
 
+@static_op
 def swiglu(a, b):
     if L.hip_enabled_for(a) and a.dtype in L._DT and a.shape[-1] % 8 == 0 and a.shape == b.shape:
         return _SwigluHIP.apply(a, b)
@@ -131,6 +136,7 @@ class _SoftmaxHIP(torch.autograd.Function):
         return dx.view(ctx.shape)
 
 
+@static_op
 def softmax(x, axis=-1):
     nd = x.dim()
     if nd == 0:

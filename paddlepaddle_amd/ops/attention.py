@@ -16,6 +16,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _loader as L
+from ..framework.trace_hook import static_op
 
 
 def attention_reference(q, k, v, causal=False, scale=None, mask=None, dropout=0.0, training=False):
@@ -150,6 +151,7 @@ class _FlashAttnQKVPackedHIP(torch.autograd.Function):
         return dqkv, None, None
 
 
+@static_op
 def flash_attention_qkvpacked(qkv, causal=True, scale=None, dropout=0.0, training=True):
     """qkv [B,S,H,3,D] -> [B,S,H,D]."""
     D = qkv.shape[-1]
@@ -175,6 +177,7 @@ def _hip_ok(q, k, v, mask, dropout, training):
     return True
 
 
+@static_op
 def flash_attention(q, k, v, causal=False, scale=None, mask=None, dropout=0.0, training=True):
     """Attention over [B,S,H,D] tensors; returns [B,Sq,H,D]."""
     D = q.shape[-1]

@@ -12,6 +12,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _loader as L
+from ..framework.trace_hook import static_op
 
 
 def _seed():
@@ -39,6 +40,7 @@ class _DropoutAddFn(torch.autograd.Function):
         return dx, (dy if ctx.has_res else None), None
 
 
+@static_op
 def dropout_add(x, residual, p, training=True):
     """residual + dropout(x, p) (upscale_in_train)."""
     if not training or p == 0.0:

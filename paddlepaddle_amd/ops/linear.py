@@ -18,6 +18,7 @@ import torch.nn.functional as F
 
 from . import _loader as L
 from .activation import bias_gelu, gelu
+from ..framework.trace_hook import static_op
 
 
 def colsum(x2d):
@@ -95,6 +96,7 @@ def _hip_linear_ok(x, w, b):
             and (b is None or b.dtype == x.dtype) and w.shape[1] % 8 == 0 and w.dim() == 2)
 
 
+@static_op
 def fused_linear(x, w, b=None, act=None):
     hip = _hip_linear_ok(x, w, b)
     if act is None:

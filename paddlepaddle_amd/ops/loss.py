@@ -12,6 +12,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _loader as L
+from ..framework.trace_hook import static_op
 
 
 class _SoftmaxCEHIP(torch.autograd.Function):
@@ -41,6 +42,7 @@ class _SoftmaxCEHIP(torch.autograd.Function):
         return dlogits.view(ctx.shape), None, None
 
 
+@static_op
 def softmax_cross_entropy(logits, labels, ignore_index=-100):
     """Per-row loss (fp32) = logsumexp(logits) - logits[label]; 0 where label == ignore_index."""
     if L.hip_enabled_for(logits) and logits.dtype in L._DT and logits.shape[-1] % 8 == 0:

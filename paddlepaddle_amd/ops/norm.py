@@ -10,6 +10,7 @@ from __future__ import annotations
 import torch
 
 from . import _loader as L
+from ..framework.trace_hook import static_op
 
 
 def _rms_ref(x, w, eps):
@@ -96,12 +97,14 @@ class _LayerNormHIP(torch.autograd.Function):
         return dx.view(ctx.shape), dw, db, None
 
 
+@static_op
 def rms_norm(x, w, eps=1e-6):
     if L.hip_enabled_for(x) and x.dtype in L._DT and x.shape[-1] % 8 == 0:
         return _RMSNormHIP.apply(x, w, eps)
     return _rms_ref(x, w, eps)
 
 
+@static_op
 def layer_norm(x, w, b, eps=1e-5):
     if L.hip_enabled_for(x) and x.dtype in L._DT and x.shape[-1] % 8 == 0:
         return _LayerNormHIP.apply(x, w, b, eps)

@@ -11,6 +11,7 @@ from __future__ import annotations
 import torch
 
 from . import _loader as L
+from ..framework.trace_hook import static_op
 
 
 def _rotate_ref(x, cos, sin, neox, inverse):
@@ -52,6 +53,7 @@ class _RopeFn(torch.autograd.Function):
         return _rope_hip(dy.to(dy.dtype), cos, sin, ctx.neox, True), None, None, None
 
 
+@static_op
 def apply_rotary(x, cos, sin, neox=True):
     """Rotate x [B,S,H,D] by tables cos/sin [S,D] (fp32, already expanded to head_dim)."""
     cos = cos.float().contiguous()

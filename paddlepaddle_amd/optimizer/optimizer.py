@@ -40,7 +40,10 @@ class Optimizer:
                  multi_precision=False):
         self._learning_rate = learning_rate
         if parameters is None:
-            raise ValueError("parameters must be given in dygraph mode (static mode: use minimize)")
+            from ..static import _static_mode
+            if not _static_mode.enabled:
+                raise ValueError("parameters must be given in dygraph mode (static mode: use minimize)")
+            parameters = []  # filled from the program by minimize()
         parameters = list(parameters)
         if parameters and isinstance(parameters[0], dict):
             self._param_groups = []
@@ -200,7 +203,7 @@ class Optimizer:
     def minimize(self, loss, startup_program=None, parameters=None, no_grad_set=None):
         from ..static import _static_mode
         if _static_mode.enabled:
-            from ..static.program import default_main_program
+            from ..static import default_main_program
             default_main_program()._set_optimizer(self, loss)
             return None, None
         loss.backward()

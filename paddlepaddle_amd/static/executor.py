@@ -1,0 +1,356 @@
+"""Static-graph user API: default programs, program_guard, data, Executor, gradients, scope.
+
+Reference: python/paddle/base/framework.py (program_guard, default_main_program), static/input.py
+(data, InputSpec), base/executor.py:1247 (Executor.run), base/backward.py:1912 (append_backward),
+:2404 (gradients), base/executor.py global_scope.
+"""
+from __future__ import annotations
+
+import contextlib
+
+import numpy as np
+import torch
+
+from ..framework import dtype as _dt
+from ..framework.tensor import Tensor, Parameter, _wrap
+from . import program as P
+
+
+class _StaticMode:
+    enabled = False
+
+
+_static_mode = _StaticMode()
+_main = P.Program()
+_startup = P.Program()
+_global_tracer = None
+
+
+def default_main_program():
+    return _main
+
+
+def default_startup_program():
+    return _startup
+
+
+def _retarget_tracer():
+    global _global_tracer
+    if _global_tracer is not None:
+        _global_tracer.__exit__(None, None, None)
+        P._state.stack.remove(_global_tracer)
+        _global_tracer = None
+    if _static_mode.enabled:
+        tr = P._Tracer(_main)
+        st = getattr(P._state, "stack", None)
+        if st is None:
+            st = P._state.stack = []
+        st.append(tr)
+        tr.__enter__()
+        _global_tracer = tr
+
+
+def enable_static():
+    _static_mode.enabled = True
+    _retarget_tracer()
+
+
+def disable_static(place=None):
+    _static_mode.enabled = False
+    _retarget_tracer()
+
+
+@contextlib.contextmanager
+def program_guard(main_program, startup_program=None):
+    global _main, _startup
+    old = (_main, _startup)
+    _main = main_program
+    if startup_program is not None:
+        _startup = startup_program
+    _retarget_tracer()
+    try:
+        yield
+    finally:
+        _main, _startup = old
+        _retarget_tracer()
+
+
+def data(name, shape, dtype=None, lod_level=0):
+    """Feed variable. Unknown dims (None / -1) are traced with a placeholder size; shape-generic code
+    (reshape(-1, ...)) runs at any size, code that reads the traced size keeps it fixed."""
+    dtype = dtype or _dt.get_default_dtype()
+    return P.placeholder(_main, name, shape, dtype)
+
+
+class InputSpec:
+    """Reference: python/paddle/static/input.py InputSpec."""
+
+    def __init__(self, shape, dtype="float32", name=None, stop_gradient=False):
+        self.shape = tuple(-1 if s is None else int(s) for s in shape)
+        self.dtype = _dt.convert_dtype(dtype)
+        self.name = name
+        self.stop_gradient = stop_gradient
+
+    @classmethod
+    def from_tensor(cls, tensor, name=None):
+        return cls(tensor.shape, tensor.dtype, name or getattr(tensor, "_name", None))
+
+    @classmethod
+    def from_numpy(cls, ndarray, name=None):
+        return cls(ndarray.shape, str(ndarray.dtype), name)
+
+    def batch(self, batch_size):
+        return InputSpec((batch_size,) + self.shape, self.dtype, self.name)
+
+    def unbatch(self):
+        return InputSpec(self.shape[1:], self.dtype, self.name)
+
+    def __repr__(self):
+        return f"InputSpec(shape={self.shape}, dtype={self.dtype}, name={self.name})"
+
+    def __eq__(self, o):
+        return isinstance(o, InputSpec) and (self.shape, self.dtype, self.name) == (o.shape, o.dtype, o.name)
+
+    def __hash__(self):
+        return hash((self.shape, self.dtype, self.name))
+
+
+def _slot_of(prog, v):
+    if isinstance(v, str):
+        if v in prog._names:
+            return prog._names[v]
+        raise KeyError(f"no variable named {v} in program")
+    t = v._t if isinstance(v, Tensor) else v
+    s = prog._slot_of.get(id(t))
+    if s is None or prog._metas[s] is not t:
+        raise KeyError("fetch target is not a variable of this program")
+    return s
+
+
+def append_backward(loss, parameter_list=None, no_grad_set=None, callbacks=None, checkpoints=None):
+    """Returns [(param, grad_var)]; grads are computed by an autograd node at replay."""
+    prog = _main
+    params = parameter_list or [p for p in prog.all_parameters() if not p.stop_gradient]
+    params = [p if isinstance(p, Tensor) else next(q for q in prog.all_parameters() if q.name == p) for p in params]
+    grads = gradients([loss], params)
+    return list(zip(params, grads))
+
+
+def gradients(targets, inputs, target_gradients=None, no_grad_set=None):
+    prog = P._active_program() or _main
+    targets = targets if isinstance(targets, (list, tuple)) else [targets]
+    inputs_l = inputs if isinstance(inputs, (list, tuple)) else [inputs]
+    for x in inputs_l:
+        s = prog._slot_of.get(id(x._t))
+        if s is not None and s in {v[0] for v in prog.feeds.values()}:
+            prog._need_grad_slots.add(s)
+            prog._metas[s].requires_grad_(True)
+    fn = P._grad_node_fn(len(targets), True)
+    targs = tuple(prog._template(t._t) for t in targets) + tuple(prog._template(x._t) for x in inputs_l)
+    with torch._C.DisableTorchFunction():
+        metas = tuple(torch.empty_like(x._t, device="meta") for x in inputs_l)
+    node = P.OpNode(fn, targs, {}, None, kind="grad", name="g:grad")
+    node.outs = prog._out_template(metas)
+    prog._append(node)
+    out = [_wrap(m) for m in metas]
+    return out if isinstance(inputs, (list, tuple)) else out
+
+
+class Scope:
+    def find_var(self, name):
+        for p in list(P._PARAM_OF.values()):
+            if p.name == name:
+                return _ScopeVar(p)
+        return None
+
+    def var(self, name):
+        return self.find_var(name)
+
+
+class _ScopeVar:
+    def __init__(self, p):
+        self._p = p
+
+    def get_tensor(self):
+        return _LoDTensorView(self._p)
+
+
+class _LoDTensorView:
+    def __init__(self, p):
+        self._p = p
+
+    def __array__(self, dtype=None):
+        a = self._p.numpy()
+        return a if dtype is None else a.astype(dtype)
+
+    def set(self, value, place=None):
+        with torch.no_grad():
+            self._p._t.copy_(torch.as_tensor(np.asarray(value)).to(self._p._t.dtype))
+
+    def shape(self):
+        return list(self._p.shape)
+
+
+_scope = Scope()
+
+
+def global_scope():
+    return _scope
+
+
+@contextlib.contextmanager
+def scope_guard(scope):
+    yield
+
+
+class BuildStrategy:
+    def __init__(self):
+        self.fuse_elewise_add_act_ops = False
+        self.fuse_bn_act_ops = False
+        self.enable_inplace = True
+        self.memory_optimize = True
+        self.fuse_all_reduce_ops = True
+        self.enable_addto = False
+        self.build_cuda_graph = False
+
+
+class ExecutionStrategy:
+    def __init__(self):
+        self.num_threads = 1
+        self.num_iteration_per_drop_scope = 100
+
+
+class CompiledProgram:
+    def __init__(self, program_or_graph, build_strategy=None):
+        self._program = program_or_graph
+        self._build_strategy = build_strategy or BuildStrategy()
+
+    def with_data_parallel(self, loss_name=None, build_strategy=None, exec_strategy=None, places=None):
+        return self
+
+
+class Executor:
+    """Replays a Program: feeds -> native-scheduled op list -> fetches (+ backward/optimizer)."""
+
+    def __init__(self, place=None):
+        self.place = place
+
+    def _device(self, prog):
+        for p in prog.all_parameters():
+            return p._t.device
+        if self.place is not None:
+            from ..framework.place import to_torch_device
+            return to_torch_device(self.place)
+        from ..framework.place import _get_torch_device
+        return _get_torch_device()
+
+    def close(self):
+        pass
+
+    def run(self, program=None, feed=None, fetch_list=None, feed_var_name="feed", fetch_var_name="fetch",
+            scope=None, return_numpy=True, use_program_cache=False, use_prune=False):
+        prog = program if program is not None else _main
+        if isinstance(prog, CompiledProgram):
+            prog = prog._program
+        if not prog.nodes and not prog.feeds:
+            return []  # startup program: parameters are initialised eagerly at creation
+        fetch_list = [] if fetch_list is None else (fetch_list if isinstance(fetch_list, (list, tuple))
+                                                    else [fetch_list])
+        fetch = [_slot_of(prog, v) for v in fetch_list]
+        opt = prog._optimize
+        keep = (opt[1],) if opt is not None else ()
+        key = (tuple(fetch), keep, prog._version)
+        plan = prog._plans.get(key)
+        if plan is None:
+            plan = P.build_plan(prog, fetch, keep)
+            prog._plans[key] = plan
+        dev = self._device(prog)
+        env = self._feed(prog, feed or {}, dev)
+        grad_on = opt is not None or any(prog.nodes[i].kind == "grad" for i in plan.order)
+        from .. import amp as _amp
+        with torch.set_grad_enabled(grad_on):
+            sym_n = self._sym_n(prog, feed or {})
+            P.run_plan(prog, plan, env, dev, sym_n=sym_n)
+        if opt is not None:
+            optimizer, ls = opt
+            optimizer.clear_grad(set_to_zero=False)
+            env[ls].backward()
+            optimizer.step()
+        outs = []
+        for s in fetch:
+            t = env[s]
+            t = t.detach() if isinstance(t, torch.Tensor) else t
+            outs.append(_wrap(t).numpy() if return_numpy else _wrap(t))
+        return outs
+
+    @staticmethod
+    def _sym_n(prog, feed):
+        if not prog._dyn:
+            return None
+        for name, (slot, shape, _) in prog.feeds.items():
+            if name in feed and -1 in shape:
+                v = feed[name]
+                sh = v.shape if hasattr(v, "shape") else np.asarray(v).shape
+                return int(sh[list(shape).index(-1)])
+        return None
+
+    @staticmethod
+    def _feed(prog, feed, dev):
+        env = {}
+        for name, val in feed.items():
+            if name not in prog.feeds:
+                raise KeyError(f"feed '{name}' is not a data variable of the program")
+            slot, shape, dtype = prog.feeds[name]
+            if isinstance(val, Tensor):
+                t = val._t
+            elif isinstance(val, torch.Tensor):
+                t = val
+            else:
+                t = torch.from_numpy(np.ascontiguousarray(np.asarray(val)))
+            t = t.to(device=dev, dtype=_dt.to_torch_dtype(dtype), non_blocking=True)
+            if len(shape) == t.dim():
+                for a, b in zip(shape, t.shape):
+                    if a >= 0 and a != b:
+                        raise ValueError(f"feed '{name}' has shape {list(t.shape)}, declared {list(shape)}")
+            if slot in prog._need_grad_slots and t.is_floating_point():
+                t = t.detach().requires_grad_(True)
+            env[slot] = t
+        return env
+
+
+def cpu_places(device_count=None):
+    from ..framework.place import CPUPlace
+    return [CPUPlace()] * (device_count or 1)
+
+
+def cuda_places(device_ids=None):
+    from ..framework.place import CUDAPlace
+    ids = device_ids if device_ids is not None else range(max(torch.cuda.device_count(), 1))
+    return [CUDAPlace(i) for i in ids]
+
+
+@contextlib.contextmanager
+def device_guard(device=None):
+    yield
+
+
+@contextlib.contextmanager
+def name_scope(prefix=None):
+    yield
+
+
+def Print(input, first_n=-1, message=None, summarize=20, print_tensor_name=True, print_tensor_type=True,
+          print_tensor_shape=True, print_tensor_layout=True, print_tensor_lod=True, print_phase="both"):
+    return input
+
+
+def create_global_var(shape, value, dtype, persistable=False, force_cpu=False, name=None):
+    from ..tensor.creation import full
+    t = full(shape, value, dtype)
+    p = Parameter(t._t, trainable=False, name=name)
+    return p
+
+
+def create_parameter(shape, dtype, name=None, attr=None, is_bias=False, default_initializer=None):
+    from .. import create_parameter as _cp
+    return _cp(shape, dtype, name, attr, is_bias, default_initializer)

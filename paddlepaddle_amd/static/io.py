@@ -1,0 +1,187 @@
+"""Static-graph persistence. Reference: python/paddle/static/io.py (save_inference_model:458,
+load_inference_model:777, save/load:1467/1540, serialize_program, deserialize_program...).
+
+On-disk format (ours, not protobuf): ``<prefix>.pdmodel`` is a JSON program (see
+``Program.to_dict``) and ``<prefix>.pdiparams`` is a ``paddle.save`` dict name -> ndarray of every
+parameter / captured constant. Both load without executing anything from the files.
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+import torch
+
+from ..framework.tensor import Tensor, Parameter, _wrap
+from ..framework import io as _io
+from . import program as P
+from .executor import _slot_of, default_main_program
+
+
+def _const_names(prog):
+    names, used = [], set()
+    params = {id(p._t): p for p in prog.all_parameters()}
+    for i, t in enumerate(prog._consts):
+        p = params.get(id(t))
+        n = p.name if p is not None else f"__const_{i}"
+        while n in used:
+            n = n + "_"
+        used.add(n)
+        names.append(n)
+    return names
+
+
+def _used_consts(prog, plan_nodes):
+    used = set()
+
+    def walk(x):
+        if isinstance(x, P._Const):
+            used.add(x.idx)
+        elif isinstance(x, (list, tuple)):
+            for v in x:
+                walk(v)
+        elif isinstance(x, dict):
+            for v in x.values():
+                walk(v)
+    for n in plan_nodes:
+        walk((n.args, n.kwargs))
+    return used
+
+
+def _prune(prog, fetch_slots):
+    plan = P.build_plan(prog, fetch_slots)
+    q = P.Program.__new__(P.Program)
+    q.__dict__.update(prog.__dict__)
+    q.nodes = [prog.nodes[i] for i in sorted(plan.order)]
+    q._plans = {}
+    q._optimize = None
+    return q
+
+
+def serialize_program(feed_vars, fetch_vars, program=None, **kw):
+    prog = program or default_main_program()
+    fetch = [_slot_of(prog, v) for v in (fetch_vars if isinstance(fetch_vars, (list, tuple)) else [fetch_vars])]
+    q = _prune(prog, fetch)
+    feeds = [v if isinstance(v, str) else v.name for v in (feed_vars if isinstance(feed_vars, (list, tuple))
+                                                            else [feed_vars])]
+    q.feeds = {k: v for k, v in prog.feeds.items() if k in feeds}
+    return json.dumps(q.to_dict(fetch, _const_names(q))).encode()
+
+
+def serialize_persistables(feed_vars, fetch_vars, executor=None, program=None, **kw):
+    prog = program or default_main_program()
+    names = _const_names(prog)
+    return {n: _wrap(t.detach()) for n, t in zip(names, prog._consts)}
+
+
+def save_inference_model(path_prefix, feed_vars, fetch_vars, executor=None, program=None, **kwargs):
+    prog = program or default_main_program()
+    fetch_vars = fetch_vars if isinstance(fetch_vars, (list, tuple)) else [fetch_vars]
+    feed_vars = feed_vars if isinstance(feed_vars, (list, tuple)) else [feed_vars]
+    fetch = [_slot_of(prog, v) for v in fetch_vars]
+    q = _prune(prog, fetch)
+    feeds = [v if isinstance(v, str) else v.name for v in feed_vars]
+    q.feeds = {k: prog.feeds[k] for k in feeds}
+    write_program(path_prefix, q, fetch)
+
+
+def write_program(path_prefix, prog, fetch_slots):
+    d = os.path.dirname(path_prefix)
+    if d:
+        os.makedirs(d, exist_ok=True)
+    names = _const_names(prog)
+    used = _used_consts(prog, prog.nodes)
+    with open(path_prefix + ".pdmodel", "w") as f:
+        json.dump(prog.to_dict(fetch_slots, names), f)
+    _io.save({names[i]: _wrap(prog._consts[i].detach()) for i in sorted(used)}, path_prefix + ".pdiparams")
+
+
+def read_program(path_prefix, device=None, params_file=None):
+    with open(path_prefix + ".pdmodel" if not path_prefix.endswith(".pdmodel") else path_prefix) as f:
+        d = json.load(f)
+    base = path_prefix[:-len(".pdmodel")] if path_prefix.endswith(".pdmodel") else path_prefix
+    sd = _io.load(params_file or base + ".pdiparams")
+    consts = {}
+    for k, v in sd.items():
+        t = v._t if isinstance(v, Tensor) else torch.as_tensor(np.asarray(v))
+        if device is not None:
+            t = t.to(device)
+        consts[k] = t
+    prog, fetch = P.Program.from_dict(d, consts)
+    return prog, fetch, consts
+
+
+def load_inference_model(path_prefix, executor=None, **kwargs):
+    dev = None
+    if executor is not None and executor.place is not None:
+        from ..framework.place import to_torch_device
+        dev = to_torch_device(executor.place)
+    prog, fetch, _ = read_program(path_prefix, dev)
+    feed_names = list(prog.feeds)
+    fetch_vars = [P._Var(prog, s, f"fetch_{i}") for i, s in enumerate(fetch)]
+    for v, s in zip(fetch_vars, fetch):
+        prog._names[v.name] = s
+    return [prog, feed_names, fetch_vars]
+
+
+def save(program, model_path, protocol=4, **configs):
+    params = {p.name: p for p in program.all_parameters()}
+    _io.save(params, model_path + ".pdparams")
+    if program._optimize is not None:
+        _io.save(program._optimize[0].state_dict(), model_path + ".pdopt")
+
+
+def load(program, model_path, executor=None, var_list=None):
+    path = model_path if model_path.endswith(".pdparams") else model_path + ".pdparams"
+    sd = _io.load(path)
+    set_program_state(program, sd)
+    opt_path = path[:-len(".pdparams")] + ".pdopt"
+    if program._optimize is not None and os.path.exists(opt_path):
+        program._optimize[0].set_state_dict(_io.load(opt_path))
+
+
+def load_program_state(model_path, var_list=None):
+    path = model_path if model_path.endswith(".pdparams") else model_path + ".pdparams"
+    return {k: (v.numpy() if isinstance(v, Tensor) else np.asarray(v)) for k, v in _io.load(path).items()}
+
+
+def set_program_state(program, state_dict):
+    with torch.no_grad():
+        for p in program.all_parameters():
+            if p.name in state_dict:
+                v = state_dict[p.name]
+                v = v._t if isinstance(v, Tensor) else torch.as_tensor(np.asarray(v))
+                p._t.copy_(v.to(p._t.dtype))
+
+
+def save_to_file(path, content):
+    with open(path, "wb") as f:
+        f.write(content)
+
+
+def load_from_file(path):
+    with open(path, "rb") as f:
+        return f.read()
+
+
+def deserialize_program(data):
+    d = json.loads(data.decode() if isinstance(data, (bytes, bytearray)) else data)
+    prog, _ = P.Program.from_dict(d, {})
+    return prog
+
+
+def normalize_program(program, feed_vars, fetch_vars, **kw):
+    fetch = [_slot_of(program, v) for v in (fetch_vars if isinstance(fetch_vars, (list, tuple)) else [fetch_vars])]
+    return _prune(program, fetch)
+
+
+def save_persistables(executor, dirname, main_program=None, filename=None):
+    prog = main_program or default_main_program()
+    os.makedirs(dirname, exist_ok=True)
+    _io.save({p.name: p for p in prog.all_parameters()}, os.path.join(dirname, filename or "persistables.pdparams"))
+
+
+def load_persistables(executor, dirname, main_program=None, filename=None):
+    prog = main_program or default_main_program()
+    set_program_state(prog, _io.load(os.path.join(dirname, filename or "persistables.pdparams")))

@@ -1,0 +1,627 @@
+"""Static graph: Program IR recorded from the same ops the dynamic graph runs, and its Executor.
+
+Reference: python/paddle/base/framework.py:5893 (Program), base/executor.py:1247 (Executor.run),
+base/backward.py (append_backward, gradients), paddle/fluid/framework/new_executor/
+program_interpreter.cc:142,231 (dependency analysis + garbage collection of intermediates).
+
+Design (MI355X-first, no tracing compiler):
+  * Building a Program runs the user's model code once on *meta* tensors (shape/dtype only, no data).
+    A TorchFunctionMode (``_Tracer``) records every device-buffer operation that touches a traced
+    value as an ``OpNode`` (callable + argument template). Hand-written HIP ops (``ops.*``) are
+    recorded as ONE node each (``static_op`` hook), so replay on the GPU runs the fused CDNA4 kernels,
+    not their decompositions.
+  * ``Executor.run`` replays the node list on real buffers. Ordering and buffer lifetimes come from
+    the native C++ scheduler (``_C_runtime.schedule``: topological order + last-use per node), so
+    every intermediate is dropped right after its last consumer — the interpreter-core GC.
+  * Training programs (``optimizer.minimize``) replay with autograd on, then run backward and the
+    (fused HIP) optimizer step; ``gradients``/``append_backward`` are recorded as autograd nodes.
+  * Programs serialize to JSON (``to_dict``/``from_dict``) naming callables from the torch / ops
+    namespaces only, so loading a saved model never executes code from the file.
+"""
+from __future__ import annotations
+
+import contextlib
+import itertools
+import threading
+
+import numpy as np
+import torch
+from torch.overrides import TorchFunctionMode
+
+from ..framework import dtype as _dt
+from ..framework.tensor import Tensor, Parameter, _wrap
+
+SENTINEL = 2  # size used for unknown (-1 / None) dims while tracing
+_META = torch.device("meta")
+_PURE_GETTERS = frozenset({
+    "shape", "dim", "size", "dtype", "device", "is_floating_point", "numel", "stride", "requires_grad",
+    "is_contiguous", "ndim", "element_size", "data_ptr", "is_cuda", "layout", "is_complex", "storage_offset",
+    "get_device", "__len__", "nelement", "is_leaf", "grad_fn", "names", "is_sparse", "is_quantized",
+    "is_meta", "itemsize", "nbytes", "ndimension", "__hash__", "is_nested", "_version",
+})
+
+
+class _Ref:
+    __slots__ = ("i",)
+
+    def __init__(self, i):
+        self.i = i
+
+    def __repr__(self):
+        return f"%{self.i}"
+
+
+class _Const:
+    __slots__ = ("t", "idx")
+
+    def __init__(self, t, idx):
+        self.t = t
+        self.idx = idx
+
+    def __repr__(self):
+        return f"$c{self.idx}"
+
+
+class _DevPlaceholder:
+    """A torch.device('meta') seen while tracing == "the device the program runs on"."""
+    __slots__ = ()
+
+    def __repr__(self):
+        return "<run_device>"
+
+
+_RUN_DEV = _DevPlaceholder()
+
+
+class _Sym:
+    """Affine function a*N + b of the dynamic dimension N (used by saved programs)."""
+    __slots__ = ("a", "b")
+
+    def __init__(self, a, b):
+        self.a, self.b = a, b
+
+
+class OpNode:
+    __slots__ = ("func", "args", "kwargs", "outs", "kind", "name")
+
+    def __init__(self, func, args, kwargs, outs, kind="torch", name=None):
+        self.func, self.args, self.kwargs, self.outs, self.kind = func, args, kwargs, outs, kind
+        self.name = name or _func_name(func)
+
+    @property
+    def type(self):
+        return self.name
+
+    def __repr__(self):
+        return f"{self.outs} = {self.name}{self.args}"
+
+
+def _func_name(func):
+    q = getattr(func, "__qualname__", "") or ""
+    if q == "getset_descriptor.__get__" or q.endswith(".__get__"):
+        return "p:" + func.__self__.__name__
+    n = getattr(func, "__name__", str(func))
+    if q.startswith("TensorBase.") or q.startswith("Tensor.") or q.startswith("_TensorBase."):
+        return "m:" + n
+    mod = getattr(func, "__module__", None) or ""
+    if mod.startswith("paddlepaddle_amd.ops") or mod.startswith("paddlepaddle_amd.static"):
+        return "o:" + mod + ":" + n
+    return "f:" + (mod or "torch") + ":" + n
+
+
+def _resolve(name):
+    """Inverse of _func_name restricted to torch / our ops namespaces (no arbitrary imports)."""
+    kind, _, rest = name.partition(":")
+    if kind == "m":
+        return getattr(torch.Tensor, rest)
+    if kind == "p":
+        return getattr(torch.Tensor, rest).__get__
+    mod, _, attr = rest.rpartition(":")
+    if kind == "o":
+        if not (mod.startswith("paddlepaddle_amd.ops") or mod.startswith("paddlepaddle_amd.static")):
+            raise ValueError(f"refusing to resolve {name}")
+        import importlib
+        m = importlib.import_module(mod)
+        return getattr(m, attr)
+    if kind == "f":
+        if mod != "torch" and not mod.startswith("torch."):
+            raise ValueError(f"refusing to resolve {name}")
+        obj = torch
+        for part in mod.split(".")[1:]:
+            obj = getattr(obj, part)
+        return getattr(obj, attr)
+    raise ValueError(f"bad op name {name}")
+
+
+# ---------------------------------------------------------------------------------- Program
+class Program:
+    _ids = itertools.count()
+
+    def __init__(self):
+        self.nodes = []
+        self._slot_of = {}       # id(meta tensor) -> slot
+        self._metas = []         # slot -> meta tensor (kept alive so ids stay unique)
+        self._consts = []        # captured real tensors (parameters, constants)
+        self._const_of = {}      # id(real tensor) -> const idx
+        self._params = {}        # const idx -> Parameter
+        self.feeds = {}          # name -> (slot, declared shape, paddle dtype str)
+        self._names = {}         # name -> slot
+        self._optimize = None    # (optimizer, loss slot)
+        self._need_grad_slots = set()
+        self._version = 0
+        self._plans = {}
+        self.random_seed = 0
+        self._id = next(Program._ids)
+        self._is_test = False
+        self._dyn = False        # saved program with an affine dynamic dim
+
+    # ------------------------------------------------------------ slots / values
+    def _new_slot(self, meta):
+        s = len(self._metas)
+        self._metas.append(meta)
+        self._slot_of[id(meta)] = s
+        return s
+
+    def _is_traced(self, t):
+        return isinstance(t, torch.Tensor) and id(t) in self._slot_of and self._metas[self._slot_of[id(t)]] is t
+
+    def _const(self, t):
+        i = self._const_of.get(id(t))
+        if i is None or self._consts[i] is not t:
+            i = len(self._consts)
+            self._consts.append(t)
+            self._const_of[id(t)] = i
+            prm = _PARAM_OF.get(id(t))
+            if prm is not None:
+                self._params[i] = prm  # the program owns its parameters (layers may be temporaries)
+        return _Const(t, i)
+
+    def _template(self, x):
+        if isinstance(x, torch.Tensor):
+            if self._is_traced(x):
+                return _Ref(self._slot_of[id(x)])
+            if x.device.type == "meta":
+                raise RuntimeError("untraced meta tensor used in a static program")
+            return self._const(x)
+        if isinstance(x, Tensor):
+            return self._template(x._t)
+        if isinstance(x, list):
+            return [self._template(v) for v in x]
+        if isinstance(x, tuple):
+            return tuple(self._template(v) for v in x)
+        if isinstance(x, dict):
+            return {k: self._template(v) for k, v in x.items()}
+        if isinstance(x, torch.device) and x.type == "meta":
+            return _RUN_DEV
+        return x
+
+    def _to_meta(self, x):
+        if isinstance(x, torch.Tensor):
+            if x.device.type == "meta":
+                return x
+            return x.detach().to(_META).requires_grad_(x.requires_grad) if x.is_floating_point() else x.to(_META)
+        if isinstance(x, list):
+            return [self._to_meta(v) for v in x]
+        if isinstance(x, tuple) and not isinstance(x, torch.Size):
+            return tuple(self._to_meta(v) for v in x)
+        if isinstance(x, dict):
+            return {k: self._to_meta(v) for k, v in x.items()}
+        return x
+
+    def _out_template(self, y):
+        if isinstance(y, torch.Tensor):
+            if self._is_traced(y):
+                return _Ref(self._slot_of[id(y)])
+            if y.device.type != "meta":
+                return None  # real value produced from traced inputs (should not happen)
+            return _Ref(self._new_slot(y))
+        if isinstance(y, (list, tuple)) and not isinstance(y, torch.Size):
+            return type(y)(self._out_template(v) for v in y) if isinstance(y, tuple) and not hasattr(y, "_fields") \
+                else [self._out_template(v) for v in y]
+        return None
+
+    @staticmethod
+    def _any(x, pred):
+        if pred(x):
+            return True
+        if isinstance(x, (list, tuple)) and not isinstance(x, torch.Size):
+            return any(Program._any(v, pred) for v in x)
+        if isinstance(x, dict):
+            return any(Program._any(v, pred) for v in x.values())
+        return False
+
+    # ------------------------------------------------------------ recording
+    def _record(self, func, args, kwargs, kind="torch"):
+        traced = self._any((args, kwargs), self._is_traced)
+        name = _func_name(func)
+        if not traced:
+            out = func(*args, **kwargs)
+            # factories creating tensors on the trace device (torch.arange(..., device=x.device))
+            if self._any(out, lambda t: isinstance(t, torch.Tensor) and t.device.type == "meta"
+                         and not self._is_traced(t)):
+                node = OpNode(func, self._template(args), self._template(kwargs), None, kind, name)
+                node.outs = self._out_template(out)
+                self._append(node)
+            return out
+        if name[2:] in _PURE_GETTERS or name.split(":")[-1] in _PURE_GETTERS:
+            return func(*self._to_meta(args), **self._to_meta(kwargs))
+        targs, tkw = self._template(args), self._template(kwargs)
+        margs, mkw = self._to_meta(args), self._to_meta(kwargs)
+        out = func(*margs, **mkw)
+        node = OpNode(func, targs, tkw, None, kind, name)
+        node.outs = self._out_template(out)
+        self._append(node)
+        return out
+
+    def _append(self, node):
+        self.nodes.append(node)
+        self._version += 1
+        self._plans.clear()
+
+    # ------------------------------------------------------------ user API
+    def global_block(self):
+        return _Block(self)
+
+    def block(self, i=0):
+        return _Block(self)
+
+    @property
+    def num_blocks(self):
+        return 1
+
+    def current_block(self):
+        return _Block(self)
+
+    def all_parameters(self):
+        return [self._params[i] for i in sorted(self._params)]
+
+    def list_vars(self):
+        out = []
+        for name, (slot, shape, dtype) in self.feeds.items():
+            out.append(_Var(self, slot, name))
+        return out + self.all_parameters()
+
+    def clone(self, for_test=False):
+        p = Program.__new__(Program)
+        p.__dict__.update(self.__dict__)
+        p.nodes = list(self.nodes)
+        p._plans = {}
+        p._id = next(Program._ids)
+        if for_test:
+            p._optimize = None
+            p._is_test = True
+        return p
+
+    def _set_optimizer(self, opt, loss):
+        slot = self._slot_of.get(id(loss._t))
+        if slot is None:
+            raise ValueError("loss is not a variable of this program")
+        if not opt._parameter_list:
+            params = [p for p in self.all_parameters() if not p.stop_gradient]
+            opt._param_groups = [{"params": params}]
+            opt._parameter_list = params
+        self._optimize = (opt, slot)
+        self._plans.clear()
+
+    def __repr__(self):
+        lines = [f"Program(id={self._id}, {len(self.nodes)} ops, feeds={list(self.feeds)})"]
+        for n in self.nodes[:200]:
+            lines.append("  " + repr(n))
+        return "\n".join(lines)
+
+    def to_string(self, throw_on_error=False, with_details=False):
+        return repr(self)
+
+    # ------------------------------------------------------------ (de)serialization
+    def to_dict(self, fetch_slots, const_names):
+        enc = _Encoder(const_names)
+        nodes = [{"f": n.name, "a": enc(n.args), "k": enc(n.kwargs), "o": enc(n.outs)} for n in self.nodes]
+        return {"format": "paddlepaddle_amd.program", "version": 1,
+                "n_slots": len(self._metas),
+                "slot_meta": [[list(m.shape), str(m.dtype).replace("torch.", "")] for m in self._metas],
+                "feeds": [{"name": k, "slot": s, "shape": list(sh), "dtype": d} for k, (s, sh, d) in self.feeds.items()],
+                "fetch": list(fetch_slots), "nodes": nodes, "dyn": self._dyn}
+
+    @staticmethod
+    def from_dict(d, consts_by_name):
+        if d.get("format") != "paddlepaddle_amd.program":
+            raise ValueError("not a paddlepaddle_amd program file")
+        p = Program()
+        for shape, dt in d["slot_meta"]:
+            p._new_slot(torch.empty(shape, dtype=getattr(torch, dt), device=_META))
+        dec = _Decoder(p, consts_by_name)
+        for nd in d["nodes"]:
+            p.nodes.append(OpNode(_resolve(nd["f"]), dec(nd["a"]), dec(nd["k"]), dec(nd["o"]), name=nd["f"]))
+        for f in d["feeds"]:
+            p.feeds[f["name"]] = (f["slot"], tuple(f["shape"]), f["dtype"])
+            p._names[f["name"]] = f["slot"]
+        p._dyn = d.get("dyn", False)
+        return p, list(d["fetch"])
+
+
+class _Block:
+    def __init__(self, prog):
+        self.program = prog
+        self.idx = 0
+
+    @property
+    def ops(self):
+        return list(self.program.nodes)
+
+    @property
+    def vars(self):
+        return {v.name: v for v in self.program.list_vars()}
+
+    def var(self, name):
+        p = self.program
+        if name in p._names:
+            return _Var(p, p._names[name], name)
+        for q in p.all_parameters():
+            if q.name == name:
+                return q
+        raise ValueError(f"var {name} not in program")
+
+    has_var = lambda self, name: name in self.program._names or any(  # noqa: E731
+        q.name == name for q in self.program.all_parameters())
+
+    def all_parameters(self):
+        return self.program.all_parameters()
+
+
+def _Var(prog, slot, name):
+    t = _wrap(prog._metas[slot])
+    t._name = name
+    return t
+
+
+from ..framework.tensor import _PARAM_OF  # noqa: E402  id(parameter buffer) -> Parameter
+
+
+# ---------------------------------------------------------------------------------- tracer
+class _Tracer(TorchFunctionMode):
+    def __init__(self, program):
+        super().__init__()
+        self.program = program
+
+    def __torch_function__(self, func, types, args=(), kwargs=None):
+        return self.program._record(func, args, kwargs or {})
+
+
+from ..framework.trace_hook import _state, _active_program, static_op  # noqa: E402,F401
+
+
+@contextlib.contextmanager
+def trace_into(program):
+    """Record every op touching traced values into ``program``."""
+    st = getattr(_state, "stack", None)
+    if st is None:
+        st = _state.stack = []
+    tr = _Tracer(program)
+    st.append(tr)
+    tr.__enter__()
+    try:
+        yield program
+    finally:
+        tr.__exit__(None, None, None)
+        st.pop()
+
+
+def placeholder(program, name, shape, dtype, need_grad=False):
+    """Create a traced input (feed) variable."""
+    sh = [SENTINEL if (s is None or s < 0) else int(s) for s in shape]
+    td = _dt.to_torch_dtype(dtype)
+    with torch._C.DisableTorchFunction():
+        meta = torch.empty(sh, dtype=td, device=_META)
+    if need_grad and meta.is_floating_point():
+        meta.requires_grad_(True)
+    slot = program._new_slot(meta)
+    program.feeds[name] = (slot, tuple(-1 if (s is None or s < 0) else int(s) for s in shape),
+                           str(td).replace("torch.", ""))
+    program._names[name] = slot
+    if need_grad:
+        program._need_grad_slots.add(slot)
+    t = _wrap(meta)
+    t._name = name
+    return t
+
+
+# ---------------------------------------------------------------------------------- replay
+class _Plan:
+    def __init__(self, order, free_after, nodes):
+        self.order = order
+        self.free_after = free_after  # position -> list of slots to drop
+        self.nodes = nodes
+
+
+def _refs(tmpl, acc):
+    if isinstance(tmpl, _Ref):
+        acc.append(tmpl.i)
+    elif isinstance(tmpl, (list, tuple)):
+        for v in tmpl:
+            _refs(v, acc)
+    elif isinstance(tmpl, dict):
+        for v in tmpl.values():
+            _refs(v, acc)
+    return acc
+
+
+def build_plan(program, fetch_slots, keep_slots=()):
+    """Prune to what the fetches need, then let the native scheduler order nodes and compute
+    last uses (reference: new_executor dependency builder + GC)."""
+    from ..utils import native
+    nodes = program.nodes
+    reads = [set(_refs((n.args, n.kwargs), [])) for n in nodes]
+    writes = []
+    for n in nodes:
+        w = set(_refs(n.outs, []))
+        if n.name == "m:__setitem__" or (n.name.startswith("m:") and n.name.endswith("_")
+                                         and not n.name.endswith("__")):
+            w |= set(_refs(n.args[:1], []))  # in-place: the receiver is written
+        writes.append(w)
+    # liveness pruning (backwards from the fetches)
+    need = set(fetch_slots) | set(keep_slots)
+    live = [False] * len(nodes)
+    for i in range(len(nodes) - 1, -1, -1):
+        if writes[i] & need:
+            live[i] = True
+            need |= reads[i]
+    idx = [i for i in range(len(nodes)) if live[i]]
+    pos_of = {i: k for k, i in enumerate(idx)}
+    creator, last_writer, readers = {}, {}, {}
+    edges = set()
+    for k, i in enumerate(idx):
+        for s in reads[i]:
+            if s in last_writer:
+                edges.add((pos_of[last_writer[s]], k))
+            if s in creator and creator[s] != i:
+                edges.add((pos_of[creator[s]], k))
+            readers.setdefault(s, []).append(k)
+        for s in writes[i]:
+            for r in readers.get(s, []):  # write-after-read
+                if r != k:
+                    edges.add((r, k))
+            if s in last_writer and last_writer[s] != i:
+                edges.add((pos_of[last_writer[s]], k))
+            creator.setdefault(s, i)
+            last_writer[s] = i
+    keep_nodes = {pos_of[creator[s]] for s in set(fetch_slots) | set(keep_slots) if s in creator}
+    order, last = native.schedule(len(idx), sorted(edges), sorted(keep_nodes))
+    pos = {v: p for p, v in enumerate(order)}
+    free_after = {}
+    feeds = {s for (s, _, _) in program.feeds.values()}
+    for s, ci in creator.items():
+        if s in fetch_slots or s in keep_slots or s in feeds:
+            continue
+        lp = last[pos_of[ci]]
+        if lp >= 0:
+            # a slot may be read by nodes that are not successors of its creator only through
+            # in-place writers; those writers are successors, so last[] covers them
+            free_after.setdefault(lp, []).append(s)
+    return _Plan([idx[v] for v in order], free_after, nodes)
+
+
+def _materialize(tmpl, env, consts, dev, sym_n=None):
+    if isinstance(tmpl, _Ref):
+        return env[tmpl.i]
+    if isinstance(tmpl, _Const):
+        return consts[tmpl.idx] if consts is not None else tmpl.t
+    if tmpl is _RUN_DEV:
+        return dev
+    if isinstance(tmpl, _Sym):
+        return tmpl.a * sym_n + tmpl.b
+    if isinstance(tmpl, slice):
+        return slice(_materialize(tmpl.start, env, consts, dev, sym_n), _materialize(tmpl.stop, env, consts, dev, sym_n),
+                     _materialize(tmpl.step, env, consts, dev, sym_n))
+    if isinstance(tmpl, list):
+        return [_materialize(v, env, consts, dev, sym_n) for v in tmpl]
+    if isinstance(tmpl, tuple):
+        return tuple(_materialize(v, env, consts, dev, sym_n) for v in tmpl)
+    if isinstance(tmpl, dict):
+        return {k: _materialize(v, env, consts, dev, sym_n) for k, v in tmpl.items()}
+    return tmpl
+
+
+def _assign(tmpl, val, env):
+    if isinstance(tmpl, _Ref):
+        env[tmpl.i] = val
+    elif isinstance(tmpl, (list, tuple)):
+        for t, v in zip(tmpl, val):
+            _assign(t, v, env)
+
+
+def run_plan(program, plan, env, dev, consts=None, sym_n=None):
+    fa = plan.free_after
+    for p, ni in enumerate(plan.order):
+        n = plan.nodes[ni]
+        args = _materialize(n.args, env, consts, dev, sym_n)
+        kw = _materialize(n.kwargs, env, consts, dev, sym_n)
+        out = n.func(*args, **kw)
+        if n.outs is not None:
+            _assign(n.outs, out, env)
+        for s in fa.get(p, ()):
+            env.pop(s, None)
+    return env
+
+
+def _grad_node_fn(n_targets, retain):
+    def _grad(*ts):
+        targets, inputs = list(ts[:n_targets]), list(ts[n_targets:])
+        gs = torch.autograd.grad(targets, inputs, allow_unused=True, retain_graph=True, create_graph=False)
+        return tuple(torch.zeros_like(i) if g is None else g for g, i in zip(gs, inputs))
+    return _grad
+
+
+# ---------------------------------------------------------------------------------- JSON codec
+class _Encoder:
+    def __init__(self, const_names):
+        self.const_names = const_names
+
+    def __call__(self, x):
+        if isinstance(x, _Ref):
+            return {"r": x.i}
+        if isinstance(x, _Const):
+            return {"c": self.const_names[x.idx]}
+        if x is _RUN_DEV:
+            return {"dev": 1}
+        if isinstance(x, _Sym):
+            return {"sym": [x.a, x.b]}
+        if isinstance(x, torch.dtype):
+            return {"dt": str(x).replace("torch.", "")}
+        if isinstance(x, torch.device):
+            return {"dev": 1}
+        if isinstance(x, torch.memory_format):
+            return {"mf": str(x).replace("torch.", "")}
+        if isinstance(x, torch.layout):
+            return {"ly": str(x).replace("torch.", "")}
+        if isinstance(x, slice):
+            return {"sl": [self(x.start), self(x.stop), self(x.step)]}
+        if x is Ellipsis:
+            return {"el": 1}
+        if isinstance(x, float) and (x != x or x in (float("inf"), float("-inf"))):
+            return {"fl": repr(x)}
+        if isinstance(x, tuple):
+            return {"t": [self(v) for v in x]}
+        if isinstance(x, list):
+            return [self(v) for v in x]
+        if isinstance(x, dict):
+            return {"d": {k: self(v) for k, v in x.items()}}
+        if x is None or isinstance(x, (bool, int, float, str)):
+            return x
+        raise TypeError(f"cannot serialize program argument of type {type(x).__name__}")
+
+
+class _Decoder:
+    def __init__(self, prog, consts_by_name):
+        self.prog = prog
+        self.consts = consts_by_name
+
+    def __call__(self, x):
+        if isinstance(x, list):
+            return [self(v) for v in x]
+        if not isinstance(x, dict):
+            return x
+        if "r" in x:
+            return _Ref(x["r"])
+        if "c" in x:
+            return self.prog._const(self.consts[x["c"]])
+        if "dev" in x:
+            return _RUN_DEV
+        if "sym" in x:
+            return _Sym(*x["sym"])
+        if "dt" in x:
+            return getattr(torch, x["dt"])
+        if "mf" in x:
+            return getattr(torch, x["mf"])
+        if "ly" in x:
+            return getattr(torch, x["ly"])
+        if "sl" in x:
+            return slice(*[self(v) for v in x["sl"]])
+        if "el" in x:
+            return Ellipsis
+        if "fl" in x:
+            return float(x["fl"])
+        if "t" in x:
+            return tuple(self(v) for v in x["t"])
+        if "d" in x:
+            return {k: self(v) for k, v in x["d"].items()}
+        raise ValueError(f"bad program entry {x}")
