@@ -1,13 +1,4 @@
-"""paddle.hapi (in progress)."""
-
-
-class Model:
-    pass
-
-
-def summary(*a, **k):
-    raise NotImplementedError
-
-
-def flops(*a, **k):
-    raise NotImplementedError
+"""paddle.hapi: high-level Model API, callbacks, summary, flops."""
+from .model import Model  # noqa: F401
+from .model_summary import summary, flops  # noqa: F401
+from . import callbacks  # noqa: F401
