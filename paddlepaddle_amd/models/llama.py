@@ -1,0 +1,311 @@
+"""LLaMA / LLaMA-2 / LLaMA-3 decoder (PaddleNLP-style llama modeling) on the MI355X hot-op set.
+
+Reference: the reference's auto-parallel llama test models (test/auto_parallel/hybrid_strategy/
+semi_auto_llama.py, test/deprecated/auto_parallel/auto_parallel_gpt_model.py for the shared
+structure) and PaddleNLP's llama/modeling.py which the reference benchmarks.
+
+MI355X mapping per block:
+  * RMSNorm -> HIP wave-per-row kernel (ops.rms_norm)
+  * fused QKV projection (one GEMM, [h, (H + 2*Hkv) * D]) -> RoPE HIP kernel on q/k
+  * GQA flash attention -> HIP MFMA kernel (ops.flash_attention; K/V heads shared by H/Hkv q heads)
+  * fused gate/up projection (one GEMM, [h, 2*ffn]) -> SwiGLU HIP kernel reading both halves in place
+  * tensor parallel: column-parallel QKV / gate-up, row-parallel o / down, vocab-parallel embedding +
+    parallel cross-entropy (parallel/tensor_parallel.py)
+Decoding keeps a preallocated per-layer KV cache sized for ``max_length`` (HBM-resident; 288 GB per
+GPU holds the 70B cache for long contexts) and appends one position per step.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+from .. import nn
+from .. import ops as _ops
+from ..framework.tensor import _wrap
+from ..nn import initializer as I
+
+
+@dataclass
+class LlamaConfig:
+    vocab_size: int = 32000
+    hidden_size: int = 4096
+    intermediate_size: int = 11008
+    num_hidden_layers: int = 32
+    num_attention_heads: int = 32
+    num_key_value_heads: int = 32
+    max_position_embeddings: int = 4096
+    rms_norm_eps: float = 1e-5
+    rope_theta: float = 10000.0
+    initializer_range: float = 0.02
+    tie_word_embeddings: bool = False
+    use_recompute: bool = False
+    tensor_parallel_degree: int = 1
+    pad_token_id: int = 0
+    bos_token_id: int = 1
+    eos_token_id: int = 2
+
+    @staticmethod
+    def llama2_7b(**kw):
+        return LlamaConfig(**kw)
+
+    @staticmethod
+    def llama2_13b(**kw):
+        d = dict(hidden_size=5120, intermediate_size=13824, num_hidden_layers=40, num_attention_heads=40,
+                 num_key_value_heads=40)
+        d.update(kw)
+        return LlamaConfig(**d)
+
+    @staticmethod
+    def llama2_70b(**kw):
+        d = dict(hidden_size=8192, intermediate_size=28672, num_hidden_layers=80, num_attention_heads=64,
+                 num_key_value_heads=8)
+        d.update(kw)
+        return LlamaConfig(**d)
+
+    @staticmethod
+    def llama3_8b(**kw):
+        d = dict(vocab_size=128256, hidden_size=4096, intermediate_size=14336, num_hidden_layers=32,
+                 num_attention_heads=32, num_key_value_heads=8, max_position_embeddings=8192, rope_theta=500000.0,
+                 bos_token_id=128000, eos_token_id=128001)
+        d.update(kw)
+        return LlamaConfig(**d)
+
+    @staticmethod
+    def tiny(**kw):
+        d = dict(vocab_size=512, hidden_size=128, intermediate_size=256, num_hidden_layers=2, num_attention_heads=4,
+                 num_key_value_heads=2, max_position_embeddings=256)
+        d.update(kw)
+        return LlamaConfig(**d)
+
+    @property
+    def head_dim(self):
+        return self.hidden_size // self.num_attention_heads
+
+    def num_params(self):
+        h, f, L, V = self.hidden_size, self.intermediate_size, self.num_hidden_layers, self.vocab_size
+        kv = self.num_key_value_heads * self.head_dim
+        per = h * (h + 2 * kv) + h * h + 3 * h * f + 2 * h
+        return L * per + V * h * (1 if self.tie_word_embeddings else 2) + h
+
+    def flops_per_token(self, seq_len):
+        return 6 * self.num_params() + 12 * self.num_hidden_layers * self.hidden_size * seq_len
+
+
+def _tp():
+    from ..parallel import tensor_parallel as tp
+    return tp
+
+
+class LlamaRMSNorm(nn.Layer):
+    def __init__(self, cfg):
+        super().__init__()
+        self.weight = self.create_parameter([cfg.hidden_size], default_initializer=I.Constant(1.0))
+        self.eps = cfg.rms_norm_eps
+
+    def forward(self, x):
+        return _wrap(_ops.rms_norm(x._t, self.weight._t, self.eps))
+
+
+class _Rope:
+    """Resident fp32 cos/sin tables, rebuilt only when a longer sequence or another device shows up."""
+
+    def __init__(self, dim, base):
+        self.dim, self.base = dim, base
+        self.cos = self.sin = None
+
+    def tables(self, n, device):
+        if self.cos is None or self.cos.shape[0] < n or self.cos.device != device:
+            m = max(n, 256)
+            self.cos, self.sin = _ops.rope.rope_tables(m, self.dim, self.base, device=device, neox=True)
+        return self.cos, self.sin
+
+
+class LlamaAttention(nn.Layer):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.cfg = cfg
+        self.tp = max(cfg.tensor_parallel_degree, 1)
+        self.H = cfg.num_attention_heads // self.tp
+        self.Hkv = max(cfg.num_key_value_heads // self.tp, 1)
+        self.D = cfg.head_dim
+        h = cfg.hidden_size
+        out = (cfg.num_attention_heads + 2 * cfg.num_key_value_heads) * self.D
+        init = nn.ParamAttr(initializer=I.Normal(0.0, cfg.initializer_range))
+        if self.tp > 1:
+            tp = _tp()
+            self.qkv_proj = tp.ColumnParallelLinear(h, out, weight_attr=init, has_bias=False, gather_output=False)
+            self.o_proj = tp.RowParallelLinear(h, h, weight_attr=init, has_bias=False, input_is_parallel=True)
+        else:
+            self.qkv_proj = nn.Linear(h, out, weight_attr=init, bias_attr=False)
+            self.o_proj = nn.Linear(h, h, weight_attr=init, bias_attr=False)
+        self.rope = _Rope(self.D, cfg.rope_theta)
+
+    def _qkv(self, x):
+        t = self.qkv_proj(x)._t
+        B, S = t.shape[0], t.shape[1]
+        # per-rank layout [H | Hkv | Hkv] heads (column-parallel shards keep whole heads)
+        q, k, v = t.split([self.H * self.D, self.Hkv * self.D, self.Hkv * self.D], -1)
+        return q.view(B, S, self.H, self.D), k.view(B, S, self.Hkv, self.D), v.view(B, S, self.Hkv, self.D)
+
+    def forward(self, x, cache=None, pos=0):
+        q, k, v = self._qkv(x)
+        B, S = q.shape[0], q.shape[1]
+        cos, sin = self.rope.tables(pos + S, q.device)
+        q = _ops.apply_rotary(q, cos[pos:pos + S], sin[pos:pos + S])
+        k = _ops.apply_rotary(k, cos[pos:pos + S], sin[pos:pos + S])
+        if cache is not None:
+            kc, vc = cache
+            kc[:B, pos:pos + S].copy_(k)
+            vc[:B, pos:pos + S].copy_(v)
+            k, v = kc[:B, :pos + S], vc[:B, :pos + S]
+            causal = S > 1
+        else:
+            causal = True
+        o = _ops.flash_attention(q, k, v, causal=causal)
+        return self.o_proj(_wrap(o.reshape(B, S, self.H * self.D)))
+
+
+class LlamaMLP(nn.Layer):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        h, f = cfg.hidden_size, cfg.intermediate_size
+        self.tp = max(cfg.tensor_parallel_degree, 1)
+        init = nn.ParamAttr(initializer=I.Normal(0.0, cfg.initializer_range))
+        if self.tp > 1:
+            tp = _tp()
+            # gate/up interleaved per rank: each rank's shard holds [gate_r | up_r]
+            self.gate_up_proj = tp.ColumnParallelLinear(h, 2 * f, weight_attr=init, has_bias=False, gather_output=False)
+            self.down_proj = tp.RowParallelLinear(f, h, weight_attr=init, has_bias=False, input_is_parallel=True)
+        else:
+            self.gate_up_proj = nn.Linear(h, 2 * f, weight_attr=init, bias_attr=False)
+            self.down_proj = nn.Linear(f, h, weight_attr=init, bias_attr=False)
+
+    def forward(self, x):
+        gu = self.gate_up_proj(x)._t
+        g, u = gu.chunk(2, -1)
+        return self.down_proj(_wrap(_ops.swiglu(g, u)))
+
+
+class LlamaDecoderLayer(nn.Layer):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.input_layernorm = LlamaRMSNorm(cfg)
+        self.self_attn = LlamaAttention(cfg)
+        self.post_attention_layernorm = LlamaRMSNorm(cfg)
+        self.mlp = LlamaMLP(cfg)
+
+    def forward(self, x, cache=None, pos=0):
+        h = self.self_attn(self.input_layernorm(x), cache, pos)
+        x = _wrap(x._t + h._t)
+        h = self.mlp(self.post_attention_layernorm(x))
+        return _wrap(x._t + h._t)
+
+
+class LlamaModel(nn.Layer):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.config = cfg
+        init = nn.ParamAttr(initializer=I.Normal(0.0, cfg.initializer_range))
+        if cfg.tensor_parallel_degree > 1:
+            self.embed_tokens = _tp().VocabParallelEmbedding(cfg.vocab_size, cfg.hidden_size, weight_attr=init)
+        else:
+            self.embed_tokens = nn.Embedding(cfg.vocab_size, cfg.hidden_size, weight_attr=init)
+        self.layers = nn.LayerList([LlamaDecoderLayer(cfg) for _ in range(cfg.num_hidden_layers)])
+        self.norm = LlamaRMSNorm(cfg)
+
+    def forward(self, input_ids, caches=None, pos=0):
+        x = self.embed_tokens(input_ids)
+        rc = self.config.use_recompute and self.training and caches is None
+        if rc:
+            from ..distributed.fleet.recompute import recompute
+        for i, layer in enumerate(self.layers):
+            if rc:
+                x = recompute(layer, x)
+            else:
+                x = layer(x, None if caches is None else caches[i], pos)
+        return self.norm(x)
+
+
+class LlamaForCausalLM(nn.Layer):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.config = cfg
+        self.llama = LlamaModel(cfg)
+        if not cfg.tie_word_embeddings:
+            tp = max(cfg.tensor_parallel_degree, 1)
+            self.lm_head_weight = self.create_parameter([cfg.vocab_size // tp, cfg.hidden_size],
+                                                        default_initializer=I.Normal(0.0, cfg.initializer_range))
+            if tp > 1:
+                self.lm_head_weight.is_distributed = True
+
+    def _logits(self, h):
+        w = self.llama.embed_tokens.weight if self.config.tie_word_embeddings else self.lm_head_weight
+        ht = h._t if h._t.dtype == w._t.dtype else h._t.to(w._t.dtype)
+        if self.config.tensor_parallel_degree > 1:
+            ht = _tp().c_identity(ht)
+        return _wrap(torch.matmul(ht, w._t.t()))
+
+    def forward(self, input_ids, caches=None, pos=0):
+        return self._logits(self.llama(input_ids, caches, pos))
+
+    # ------------------------------------------------------------------ generation
+    def new_cache(self, batch, max_length):
+        cfg = self.config
+        p = next(iter(self.parameters()))
+        Hkv = max(cfg.num_key_value_heads // max(cfg.tensor_parallel_degree, 1), 1)
+        shape = (batch, max_length, Hkv, cfg.head_dim)
+        return [(torch.zeros(shape, dtype=p._t.dtype, device=p._t.device),
+                 torch.zeros(shape, dtype=p._t.dtype, device=p._t.device)) for _ in range(cfg.num_hidden_layers)]
+
+    @torch.no_grad()
+    def generate(self, input_ids, max_new_tokens=16, decode_strategy="greedy_search", temperature=1.0, top_k=0,
+                 top_p=1.0, eos_token_id=None):
+        """Prefill once, then one token per step against the KV cache. Returns (ids, scores)."""
+        ids = input_ids._t
+        B, S = ids.shape
+        caches = self.new_cache(B, S + max_new_tokens)
+        logits = self.forward(_wrap(ids), caches, 0)._t[:, -1].float()
+        out, scores = [], []
+        eos = self.config.eos_token_id if eos_token_id is None else eos_token_id
+        done = torch.zeros(B, dtype=torch.bool, device=ids.device)
+        for t in range(max_new_tokens):
+            if decode_strategy == "sampling":
+                lg = logits / max(temperature, 1e-5)
+                if top_k:
+                    kth = lg.topk(top_k, -1).values[:, -1:]
+                    lg = lg.masked_fill(lg < kth, float("-inf"))
+                probs = torch.softmax(lg, -1)
+                if top_p < 1.0:
+                    sp, si = probs.sort(-1, descending=True)
+                    keep = sp.cumsum(-1) - sp <= top_p
+                    probs = torch.zeros_like(probs).scatter_(-1, si, sp * keep)
+                    probs = probs / probs.sum(-1, keepdim=True)
+                nxt = torch.multinomial(probs, 1).squeeze(-1)
+            else:
+                nxt = logits.argmax(-1)
+            scores.append(torch.log_softmax(logits, -1).gather(-1, nxt[:, None]).squeeze(-1))
+            nxt = torch.where(done, torch.full_like(nxt, self.config.pad_token_id), nxt)
+            out.append(nxt)
+            done |= nxt == eos
+            if bool(done.all()) or t == max_new_tokens - 1:
+                break
+            logits = self.forward(_wrap(nxt[:, None]), caches, S + t)._t[:, -1].float()
+        return _wrap(torch.stack(out, 1)), _wrap(torch.stack(scores, 1))
+
+
+class LlamaPretrainingCriterion(nn.Layer):
+    def __init__(self, cfg: LlamaConfig = None, ignore_index=-100):
+        super().__init__()
+        self.cfg = cfg
+        self.ignore_index = ignore_index
+
+    def forward(self, logits, labels):
+        lt = logits._t
+        if self.cfg is not None and self.cfg.tensor_parallel_degree > 1:
+            per_tok = _tp().parallel_cross_entropy_raw(lt, labels._t, self.ignore_index)
+        else:
+            per_tok = _ops.softmax_cross_entropy(lt, labels._t, self.ignore_index)
+        valid = (labels._t != self.ignore_index).sum().clamp_min(1)
+        return _wrap(per_tok.sum() / valid)

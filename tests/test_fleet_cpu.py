@@ -213,3 +213,54 @@ def test_sequence_parallel_ops():
     exp_gx = np.concatenate([np.full((3, 2, 4), 2.0), np.full((3, 2, 4), 4.0)])
     np.testing.assert_allclose(gx0, exp_gx, rtol=1e-6)
     np.testing.assert_allclose(gx1, exp_gx, rtol=1e-6)
+
+
+# ----------------------------------------------------------------------------- llama TP
+def _llama_tp_shard(name, full, rank, world, cfg):
+    H, Hk, D, f = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim, cfg.intermediate_size
+    if name.endswith("qkv_proj.weight"):
+        q, k, v = full.split([H * D, Hk * D, Hk * D], -1)
+        return torch.cat([q.chunk(world, -1)[rank], k.chunk(world, -1)[rank], v.chunk(world, -1)[rank]], -1)
+    if name.endswith("gate_up_proj.weight"):
+        g, u = full.chunk(2, -1)
+        return torch.cat([g.chunk(world, -1)[rank], u.chunk(world, -1)[rank]], -1)
+    if name.endswith("o_proj.weight") or name.endswith("down_proj.weight") or "embed_tokens" in name \
+            or name == "lm_head_weight":
+        return full.chunk(world, 0)[rank]
+    return full
+
+
+def _llama_tp_worker(rank, world, port, q):
+    paddle = _setup(rank, world, port)
+    from paddlepaddle_amd.models.llama import LlamaConfig, LlamaForCausalLM, LlamaPretrainingCriterion
+    paddle.seed(4)
+    cfg1 = LlamaConfig.tiny()
+    full = LlamaForCausalLM(cfg1)
+    full_sd = {k: v._t.detach().clone() for k, v in full.state_dict().items()}
+    fleet = _fleet_init(paddle, mp_degree=2)
+    cfg = LlamaConfig.tiny(tensor_parallel_degree=2)
+    model, crit = LlamaForCausalLM(cfg), LlamaPretrainingCriterion(cfg)
+    with torch.no_grad():
+        for k, v in model.state_dict().items():
+            v._t.copy_(_llama_tp_shard(k, full_sd[k], rank, world, cfg))
+    opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    model = fleet.distributed_model(model)
+    opt = fleet.distributed_optimizer(opt)
+    losses = _train(paddle, model, crit, opt, _data(cfg))
+    q.put((rank, losses))
+    paddle.distributed.barrier()
+
+
+def test_llama_tensor_parallel_matches_single_process():
+    sys.path.insert(0, ROOT)
+    os.environ["PADDLE_AMD_FORCE_CPU"] = "1"
+    import paddlepaddle_amd as paddle
+    from paddlepaddle_amd.models.llama import LlamaConfig, LlamaForCausalLM, LlamaPretrainingCriterion
+    paddle.seed(4)
+    cfg = LlamaConfig.tiny()
+    model, crit = LlamaForCausalLM(cfg), LlamaPretrainingCriterion(cfg)
+    opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    ref = _train(paddle, model, crit, opt, _data(cfg))
+    res = _spawn(_llama_tp_worker)
+    for _, l in res:
+        np.testing.assert_allclose(l, ref, rtol=1e-4, atol=1e-5)
