@@ -51,6 +51,8 @@ def hip_enabled_for(t: torch.Tensor) -> bool:
     """True if a HIP kernel should run for a tensor on this device."""
     if not t.is_cuda or not flag("FLAGS_use_hip_kernels", True):
         return False
+    if type(t) is not torch.Tensor and type(t) is not torch.nn.Parameter:
+        return False  # distributed / wrapper tensors (auto-parallel DTensor) take the sharding-aware path
     if _load() is None:
         if os.environ.get("PADDLE_AMD_ALLOW_FALLBACK", "0") == "1":
             return False

@@ -95,7 +95,9 @@ class Optimizer:
         k = id(p)
         if k not in d:
             t = p._t
-            if shape is None:
+            if shape is None and type(t) is not torch.Tensor:
+                d[k] = torch.full_like(t.detach(), init, dtype=dtype)  # distributed params: same placements
+            elif shape is None:
                 d[k] = torch.full(t.shape, init, dtype=dtype, device=t.device)
             else:
                 d[k] = torch.full(shape, init, dtype=dtype, device=t.device)
@@ -181,6 +183,8 @@ class Optimizer:
 
     @no_grad()
     def step(self):
+        from ..ops.linear import bump_weight_epoch
+        bump_weight_epoch()  # weights change: drop per-step forward-layout weight copies
         self._step_count += 1
         self._apply_clip()
         for group in self._param_groups:

@@ -285,7 +285,10 @@ class LBFGS(Optimizer):
                                history_size=history_size, line_search_fn=line_search_fn)
 
     def step(self, closure):
+        from ..ops.linear import bump_weight_epoch
+
         def _c():
+            bump_weight_epoch()  # line search evaluates the closure at moved weights
             with torch.enable_grad():
                 for t in self._torch_params:
                     t.grad = None
