@@ -5,3 +5,28 @@ from .collective import (ReduceOp, Group, ParallelEnv, init_parallel_env, get_ra
                          broadcast_object_list, reduce, reduce_scatter, scatter, scatter_object_list, gather,
                          alltoall, alltoall_single, send, recv, isend, irecv, P2POp, batch_isend_irecv, wait,
                          get_backend, get_global_rank)
+from .auto_parallel import (ProcessMesh, Shard, Replicate, Partial, Placement, ReduceType, shard_tensor,  # noqa
+                            dtensor_from_local, dtensor_from_fn, reshard, unshard_dtensor, shard_layer,
+                            shard_optimizer, shard_scaler, ShardingStage1, ShardingStage2, ShardingStage3,
+                            shard_dataloader, Strategy, DistModel, to_static, get_mesh, set_mesh)
+from . import auto_parallel  # noqa: F401
+from ..parallel.data_parallel import DataParallel  # noqa: F401,E402
+
+
+def __getattr__(name):
+    # heavier subsystems are imported on first use (fleet pulls in pipeline/TP layers)
+    import importlib
+    if name in ("fleet", "sharding", "checkpoint", "launch", "spawn_mod", "utils", "communication", "rpc"):
+        mod = importlib.import_module(f".{name}", __name__)
+        globals()[name] = mod
+        return mod
+    if name in ("save_state_dict", "load_state_dict"):
+        from . import checkpoint
+        return getattr(checkpoint, name)
+    if name == "spawn":
+        from .spawn import spawn
+        return spawn
+    if name == "group_sharded_parallel":
+        from ..parallel.sharding import group_sharded_parallel
+        return group_sharded_parallel
+    raise AttributeError(name)

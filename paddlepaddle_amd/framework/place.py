@@ -128,7 +128,9 @@ _current_place = None
 
 def _default_place():
     if torch.cuda.is_available() and os.environ.get("PADDLE_AMD_FORCE_CPU", "0") != "1":
-        idx = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
+        # launcher-assigned device id (``--devices 4,5``) wins over the local rank
+        idx = int(os.environ.get("PADDLE_AMD_DEVICE_ID", os.environ.get("LOCAL_RANK", "0")))
+        idx %= max(torch.cuda.device_count(), 1)
         return CUDAPlace(idx)
     return CPUPlace()
 
