@@ -49,22 +49,32 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def _dev():
+    from paddlepaddle_amd.framework.place import _get_torch_device
+    return _get_torch_device()
+
+
+def _sync():
+    if torch.cuda.is_available() and _dev().type == "cuda":
+        torch.cuda.synchronize()
+
+
 def timed(step_fn, steps, warmup, dist_on):
     import torch.distributed as dist
     for _ in range(warmup):
         step_fn()
     if dist_on:
         dist.barrier()
-    torch.cuda.synchronize()
+    _sync()
     t0 = time.perf_counter()
     for i in range(steps):
         step_fn()
-    torch.cuda.synchronize()
+    _sync()
     if dist_on:
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist_on:
-        t = torch.tensor([dt], device="cuda")
+        t = torch.tensor([dt], device=_dev())
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     return dt
@@ -95,19 +105,27 @@ def gpt_bench(args, paddle, world, dist_on):
     elif world > 1:
         model = paddle.DataParallel(model)
     B, S = args.micro_batch, args.seq_len
-    gen = torch.Generator(device="cuda").manual_seed(7)
-    data = torch.randint(0, cfg.vocab_size, (args.accum, B, S + 1), device="cuda", generator=gen)
+    dev = _dev()
+    gen = torch.Generator(device=dev).manual_seed(7 + int(os.environ.get("RANK", "0")))
+    data = torch.randint(0, cfg.vocab_size, (args.accum, B, S + 1), device=dev, generator=gen)
     ids = [paddle.Tensor(data[i, :, :-1]) for i in range(args.accum)]
     lbl = [paddle.Tensor(data[i, :, 1:]) for i in range(args.accum)]
     state = {}
+    import contextlib
+    no_sync = getattr(model, "no_sync", None)
 
     def step():
         for a in range(args.accum):
-            logits = model(ids[a])
-            loss = crit(logits, lbl[a])
-            if args.accum > 1:
-                loss = loss * (1.0 / args.accum)
-            loss.backward()
+            # accumulation micro-batches skip the gradient reduce-scatter / all-reduce; the last one
+            # reduces (overlapped with its backward)
+            ctx = no_sync() if (no_sync is not None and world > 1 and a < args.accum - 1) else \
+                contextlib.nullcontext()
+            with ctx:
+                logits = model(ids[a])
+                loss = crit(logits, lbl[a])
+                if args.accum > 1:
+                    loss = loss * (1.0 / args.accum)
+                loss.backward()
         opt.step()
         opt.clear_grad()
         state["loss"] = loss
@@ -117,10 +135,12 @@ def gpt_bench(args, paddle, world, dist_on):
     tps = tokens / dt
     fpt = cfg.flops_per_token(S, recompute=False)
     mfu = tps * fpt / (PEAK_BF16 * world)
+    mem = torch.cuda.max_memory_allocated() / 2**30 if dev.type == "cuda" else 0.0
     log(f"[gpt] loss={float(state['loss']):.4f} step={dt / args.steps * 1000:.1f}ms tokens/s={tps:.0f} "
-        f"MFU(6N model flops)={mfu * 100:.1f}% mem={torch.cuda.max_memory_allocated() / 2**30:.1f}GiB")
+        f"MFU(6N model flops)={mfu * 100:.1f}% mem={mem:.1f}GiB")
     del model, opt, ids, lbl
-    torch.cuda.empty_cache()
+    if dev.type == "cuda":
+        torch.cuda.empty_cache()
     return tps, dt / args.steps * 1000, B * args.accum * world, mfu
 
 
@@ -134,8 +154,8 @@ def resnet_bench(args, paddle, world, dist_on):
     if world > 1:
         model = paddle.DataParallel(model)
     B = args.resnet_batch
-    x = paddle.Tensor(torch.randn(B, 224, 224, 3, device="cuda", dtype=torch.bfloat16))
-    y = paddle.Tensor(torch.randint(0, 1000, (B,), device="cuda"))
+    x = paddle.Tensor(torch.randn(B, 224, 224, 3, device=_dev(), dtype=torch.bfloat16))
+    y = paddle.Tensor(torch.randint(0, 1000, (B,), device=_dev()))
 
     def step():
         with paddle.amp.auto_cast(level="O2", dtype="bfloat16"):
@@ -158,7 +178,7 @@ def main():
     dist_on = world > 1
     if dist_on:
         paddle.distributed.init_parallel_env()
-    else:
+    elif torch.cuda.is_available() and os.environ.get("PADDLE_AMD_FORCE_CPU", "0") != "1":
         torch.cuda.set_device(0)
     tps = step_ms = gb = mfu = None
     if not args.skip_gpt:

@@ -72,6 +72,8 @@ class _Flat:
         # degree 1: the shard IS the full buffer and grads stay in the flat bf16 grad buffer
         self.shard = Parameter(sh, trainable=True, name=f"sharded_flat_{id(self)}")
         self.shard.need_clip = True
+        if world > 1 and sh.dtype != torch.float32 and hasattr(self.shard._t, "grad_dtype"):
+            self.shard._t.grad_dtype = None  # bf16 shard, fp32 reduce-scattered gradient
         self.shard_grad = torch.zeros(self.shard_size, dtype=torch.float32, device=self.device) if world > 1 else None
         self.full_grad = None
         # re-point model params at views of the full buffer
@@ -158,11 +160,43 @@ class GroupShardedEngine:
                     self._flat_by_param[id(p)] = (u, f)
         self._queued = False
         self._in_backward = False
+        self._sync = True
+        self.keep_params = self._decide_keep_params()
         self._install_hooks()
         self._rebind_optimizer(optimizer)
         if stage == 3:
             for u in self.units[1:]:
                 self._release(u)
+
+    def _decide_keep_params(self):
+        """Stage 3 on a 288 GB MI355X: when the full bf16 parameters + gradients take a modest share of
+        HBM, keep each unit's gathered parameters resident from its first all-gather until the
+        optimizer step (ZeRO-3 "live parameters"), instead of re-gathering twice per micro-batch.
+        Per step that is one all-gather + one reduce-scatter of the model instead of 3 x accum."""
+        if self.stage != 3 or self.world == 1:
+            return False
+        from ..framework.flags import flag
+        mode = str(flag("FLAGS_sharding_stage3_keep_params", "auto")).lower()
+        if mode in ("0", "false", "off"):
+            return False
+        if mode in ("1", "true", "on"):
+            return True
+        nbytes = sum(f.padded * f.full.element_size() for u in self.units for f in u.flats)
+        dev = self.units[0].flats[0].device if self.units else torch.device("cpu")
+        if dev.type != "cuda":
+            return False
+        total = torch.cuda.get_device_properties(dev).total_memory
+        return 2 * nbytes < 0.35 * total
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Gradient-accumulation micro-batches: grads accumulate locally, no reduce-scatter."""
+        old = self._sync
+        self._sync = False
+        try:
+            yield
+        finally:
+            self._sync = old
 
     # ------------------------------------------------------------------ construction
     def _broadcast_params(self):
@@ -245,7 +279,7 @@ class GroupShardedEngine:
                 t = out._t if isinstance(out, Tensor) else None
                 if t is not None and t.requires_grad:
                     t.register_hook(self._make_pre_backward(ui))
-            if self.stage == 3 and not self._in_backward:
+            if self.stage == 3 and not self._in_backward and not self.keep_params:
                 self._release(u)
             return None
         return hook
@@ -265,15 +299,15 @@ class GroupShardedEngine:
         return hook
 
     def _make_grad_hook(self, u):
-        is_root = u is self.units[0] if self.units else False
-
         def hook(t):
             self._queue_finalize()
             u.ready.add(id(t))
+            if not self._sync:
+                return  # accumulation micro-batch: grads stay in the unit's flat grad buffer
             # root unit (tied embedding used twice) is flushed at the end of backward instead
             if u is not self.units[0] and len(u.ready) == u.n_params:
                 self._reduce_scatter(u)
-                if self.stage == 3:
+                if self.stage == 3 and not self.keep_params:
                     self._release(u)
         return hook
 
@@ -326,6 +360,14 @@ class GroupShardedEngine:
         u.ready = set()
 
     def _finalize_backward(self):
+        if not self._sync:
+            for u in self.units:
+                u.ready = set()
+                if self.stage == 3 and u is not self.units[0] and not self.keep_params:
+                    self._release(u)
+            self._queued = False
+            self._in_backward = False
+            return
         # flush units whose grads were never (fully) produced, then join every reduce-scatter
         for u in self.units:
             if u.ready or (not u.rs_tmp and any(f.full_grad is not None for f in u.flats)):
@@ -340,7 +382,8 @@ class GroupShardedEngine:
             if self.world == 1:
                 continue
             if self.stage == 3 and u is not self.units[0]:
-                self._release(u)
+                if not self.keep_params:
+                    self._release(u)
             else:
                 for f in u.flats:
                     if f.full_grad is not None:
@@ -362,6 +405,8 @@ class GroupShardedEngine:
             return  # shard aliases the full buffer: nothing to publish
         for u in self.units:
             if self.stage == 3 and u is not self.units[0]:
+                if self.keep_params:
+                    u.gathered = False  # stale after the update; storage kept, re-filled on next use
                 continue
             for f in u.flats:
                 dist.all_gather_into_tensor(f.gbuf, f.shard._t.detach().to(f.full.dtype), group=self.pg)
@@ -399,6 +444,9 @@ class GroupShardedModel(Layer):
                 for f in e.units[0].flats:
                     f.alloc_full_grad()
         return self._layers(*args, **kwargs)
+
+    def no_sync(self):
+        return self._engine.no_sync()
 
     def state_dict(self, *args, **kwargs):
         self._engine.gather_all()

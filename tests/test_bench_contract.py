@@ -1,0 +1,36 @@
+"""bench.py driver contract on CPU: torchrun with 2 ranks (gloo), bf16 GPT (sharding stage 3 with
+no_sync accumulation) + ResNet-50 DP, exactly one JSON line from rank 0 with the required fields."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_bench_two_ranks_json_line():
+    env = dict(os.environ, PADDLE_AMD_FORCE_CPU="1", PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--model",
+           "tiny", "--steps", "2", "--warmup", "1", "--seq-len", "64", "--micro-batch", "2", "--accum", "2",
+           "--resnet-batch", "2", "--resnet-steps", "1"]
+    r = subprocess.run(cmd, env=env, capture_output=True, timeout=600, cwd="/tmp")
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    lines = [l for l in r.stdout.decode().splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in d
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["value"] > 0 and d["dtype"] == "bf16"
+    assert d["config"]["parallelism"] == "sharding_stage3_degree2"
+    assert d["secondary"]["value"] > 0

@@ -165,6 +165,54 @@ def test_data_parallel_and_sharding_match_single_process(mode):
         np.testing.assert_allclose(sd1[k], sd0[k], rtol=0, atol=0, err_msg=f"{mode}:{k} replicas differ")
 
 
+def _accum_worker(rank, world, port, level, keep, q):
+    paddle = _setup(rank, world, port)
+    paddle.set_flags({"FLAGS_sharding_stage3_keep_params": keep})
+    cfg, model, crit = _make_model(paddle)
+    ids = _data(cfg)
+    local = ids[rank * 2:(rank + 1) * 2]
+    opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    from paddlepaddle_amd.distributed.sharding import group_sharded_parallel
+    model, opt, _ = group_sharded_parallel(model, opt, level=level)
+    assert model._engine.keep_params == (level == "p_g_os" and keep == "1")
+    for _ in range(2):
+        for a in range(2):  # 2 micro-batches of 1 sequence; first one without reduce-scatter
+            x = paddle.Tensor(local[a:a + 1])
+            ctx = model.no_sync() if a == 0 else __import__("contextlib").nullcontext()
+            with ctx:
+                loss = crit(model(x[:, :-1]), x[:, 1:]) * 0.5
+                loss.backward()
+        opt.step()
+        opt.clear_grad()
+    sd = {k: v.numpy() for k, v in model.state_dict().items()}
+    q.put((rank, sd))
+    paddle.distributed.barrier()
+
+
+@pytest.mark.parametrize("level,keep", [("os_g", "auto"), ("p_g_os", "0"), ("p_g_os", "1")])
+def test_sharding_no_sync_accumulation_matches_single_process(level, keep):
+    """no_sync micro-batches + (stage 3) resident gathered params == single-process accumulation."""
+    sys.path.insert(0, ROOT)
+    os.environ["PADDLE_AMD_FORCE_CPU"] = "1"
+    import paddlepaddle_amd as paddle
+    cfg, model, crit = _make_model(paddle)
+    ids = _data(cfg)
+    opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    for _ in range(2):
+        # global batch = 4 sequences = 2 ranks x 2 micro-batches; mean over everything
+        for i in range(4):
+            x = paddle.Tensor(ids[i:i + 1])
+            loss = crit(model(x[:, :-1]), x[:, 1:]) * 0.25
+            loss.backward()
+        opt.step()
+        opt.clear_grad()
+    ref = {k: v.numpy() for k, v in model.state_dict().items()}
+    (_, sd0), (_, sd1) = _spawn(_accum_worker, level, keep)
+    for k in ref:
+        np.testing.assert_allclose(sd0[k], ref[k], rtol=2e-3, atol=2e-4, err_msg=f"{level}/{keep}:{k}")
+        np.testing.assert_allclose(sd1[k], sd0[k], rtol=0, atol=0)
+
+
 @pytest.mark.parametrize("level", ["os", "os_g", "p_g_os"])
 def test_sharding_degree1_matches_plain(level):
     """Degree-1 sharding (single process, no collectives) must equal plain training, incl. accumulation."""
