@@ -1,0 +1,60 @@
+"""paddle.incubate.autograd (functional forward/reverse-mode AD). Reference:
+python/paddle/incubate/autograd/functional.py (vjp, jvp, Jacobian, Hessian)."""
+from __future__ import annotations
+
+import torch
+
+from ..framework.tensor import Tensor, _wrap
+from ..autograd import Jacobian, jacobian, hessian  # noqa: F401
+
+
+def _fn(func):
+    def f(*xs):
+        out = func(*[_wrap(x) for x in xs])
+        if isinstance(out, (list, tuple)):
+            return tuple(o._t for o in out)
+        return out._t
+    return f
+
+
+def _ts(x):
+    return tuple(v._t for v in x) if isinstance(x, (list, tuple)) else (x._t,)
+
+
+def vjp(func, xs, v=None):
+    ys, g = torch.autograd.functional.vjp(_fn(func), _ts(xs), None if v is None else _ts(v))
+    wrap = (lambda t: tuple(_wrap(a) for a in t) if isinstance(t, tuple) else _wrap(t))
+    gs = wrap(g)
+    return wrap(ys), (gs if isinstance(xs, (list, tuple)) else gs[0] if isinstance(gs, tuple) else gs)
+
+
+def jvp(func, xs, v=None):
+    ys, g = torch.autograd.functional.jvp(_fn(func), _ts(xs), None if v is None else _ts(v))
+    wrap = (lambda t: tuple(_wrap(a) for a in t) if isinstance(t, tuple) else _wrap(t))
+    return wrap(ys), wrap(g)
+
+
+class Hessian:
+    def __init__(self, func, xs, is_batched=False):
+        self.func, self.xs = func, xs
+        H = torch.autograd.functional.hessian(_fn(func), _ts(xs))
+        self._t = H[0][0] if isinstance(H, tuple) else H
+
+    def __getitem__(self, idx):
+        return _wrap(self._t[idx])
+
+    @property
+    def shape(self):
+        return list(self._t.shape)
+
+
+def enable_prim():
+    pass
+
+
+def disable_prim():
+    pass
+
+
+def prim_enabled():
+    return False
