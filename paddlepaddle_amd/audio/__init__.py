@@ -1,1 +1,225 @@
-"""paddle.audio (in progress)."""
+"""paddle.audio: feature extraction (Spectrogram / MelSpectrogram / LogMelSpectrogram / MFCC), window
+functions, mel / dct helpers, wav IO. Reference: python/paddle/audio/ (features/layers.py,
+functional/functional.py, functional/window.py, backends/wave_backend.py).
+STFT runs on the device FFT (``paddle.signal.stft``)."""
+from __future__ import annotations
+
+import math
+import wave
+
+import numpy as np
+import torch
+
+from .. import nn
+from ..framework.tensor import Tensor, _wrap
+
+
+class functional:
+    @staticmethod
+    def hz_to_mel(freq, htk=False):
+        f = freq._t if isinstance(freq, Tensor) else torch.as_tensor(freq, dtype=torch.float64)
+        if htk:
+            out = 2595.0 * torch.log10(1.0 + f / 700.0)
+        else:
+            f_sp = 200.0 / 3
+            mels = f / f_sp
+            min_log_hz = 1000.0
+            min_log_mel = min_log_hz / f_sp
+            logstep = math.log(6.4) / 27.0
+            out = torch.where(f >= min_log_hz, min_log_mel + torch.log(f.clamp_min(1e-10) / min_log_hz) / logstep, mels)
+        return _wrap(out) if isinstance(freq, Tensor) else (float(out) if out.dim() == 0 else out.numpy())
+
+    @staticmethod
+    def mel_to_hz(mel, htk=False):
+        m = mel._t if isinstance(mel, Tensor) else torch.as_tensor(mel, dtype=torch.float64)
+        if htk:
+            out = 700.0 * (10.0 ** (m / 2595.0) - 1.0)
+        else:
+            f_sp = 200.0 / 3
+            freqs = f_sp * m
+            min_log_hz = 1000.0
+            min_log_mel = min_log_hz / f_sp
+            logstep = math.log(6.4) / 27.0
+            out = torch.where(m >= min_log_mel, min_log_hz * torch.exp(logstep * (m - min_log_mel)), freqs)
+        return _wrap(out) if isinstance(mel, Tensor) else (float(out) if out.dim() == 0 else out.numpy())
+
+    @staticmethod
+    def mel_frequencies(n_mels=64, f_min=0.0, f_max=11025.0, htk=False, dtype="float32"):
+        lo = functional.hz_to_mel(f_min, htk)
+        hi = functional.hz_to_mel(f_max, htk)
+        mels = torch.linspace(float(lo), float(hi), n_mels, dtype=torch.float64)
+        return _wrap(torch.as_tensor(functional.mel_to_hz(mels.numpy(), htk)).float())
+
+    @staticmethod
+    def fft_frequencies(sr, n_fft, dtype="float32"):
+        return _wrap(torch.linspace(0, sr / 2, 1 + n_fft // 2))
+
+    @staticmethod
+    def compute_fbank_matrix(sr, n_fft, n_mels=64, f_min=0.0, f_max=None, htk=False, norm="slaney",
+                             dtype="float32"):
+        f_max = f_max or sr / 2
+        fftfreqs = functional.fft_frequencies(sr, n_fft)._t.double()
+        mel_f = functional.mel_frequencies(n_mels + 2, f_min, f_max, htk)._t.double()
+        fdiff = mel_f[1:] - mel_f[:-1]
+        ramps = mel_f[:, None] - fftfreqs[None]
+        lower = -ramps[:-2] / fdiff[:-1, None]
+        upper = ramps[2:] / fdiff[1:, None]
+        w = torch.clamp(torch.minimum(lower, upper), min=0)
+        if norm == "slaney":
+            enorm = 2.0 / (mel_f[2:n_mels + 2] - mel_f[:n_mels])
+            w = w * enorm[:, None]
+        return _wrap(w.float())
+
+    @staticmethod
+    def power_to_db(spect, ref_value=1.0, amin=1e-10, top_db=80.0):
+        s = spect._t
+        db = 10.0 * torch.log10(s.clamp_min(amin)) - 10.0 * math.log10(max(ref_value, amin))
+        if top_db is not None:
+            db = torch.maximum(db, db.max() - top_db)
+        return _wrap(db)
+
+    @staticmethod
+    def create_dct(n_mfcc, n_mels, norm="ortho", dtype="float32"):
+        n = torch.arange(n_mels, dtype=torch.float64)
+        k = torch.arange(n_mfcc, dtype=torch.float64)[:, None]
+        dct = torch.cos(math.pi / n_mels * (n + 0.5) * k)
+        if norm == "ortho":
+            dct[0] *= 1.0 / math.sqrt(2.0)
+            dct *= math.sqrt(2.0 / n_mels)
+        else:
+            dct *= 2.0
+        return _wrap(dct.t().float())
+
+    @staticmethod
+    def get_window(window, win_length, fftbins=True, dtype="float64"):
+        name = window[0] if isinstance(window, tuple) else window
+        n = win_length
+        sym = not fftbins
+        fns = {"hann": torch.hann_window, "hamming": torch.hamming_window, "blackman": torch.blackman_window,
+               "bartlett": torch.bartlett_window}
+        if name in fns:
+            w = fns[name](n, periodic=not sym, dtype=torch.float64)
+        elif name == "kaiser":
+            beta = window[1] if isinstance(window, tuple) else 12.0
+            w = torch.kaiser_window(n, periodic=not sym, beta=beta, dtype=torch.float64)
+        elif name in ("boxcar", "rect", "rectangular"):
+            w = torch.ones(n, dtype=torch.float64)
+        elif name == "gaussian":
+            std = window[1]
+            m = n + (0 if sym else 1)
+            x = torch.arange(m, dtype=torch.float64) - (m - 1) / 2
+            w = torch.exp(-0.5 * (x / std) ** 2)[:n]
+        else:
+            raise ValueError(f"unsupported window {window}")
+        from ..framework import dtype as _dtm
+        return _wrap(w.to(_dtm.to_torch_dtype(dtype)))
+
+
+class Spectrogram(nn.Layer):
+    def __init__(self, n_fft=512, hop_length=None, win_length=None, window="hann", power=2.0, center=True,
+                 pad_mode="reflect", dtype="float32"):
+        super().__init__()
+        self.n_fft, self.hop = n_fft, hop_length or (win_length or n_fft) // 4
+        self.win_length = win_length or n_fft
+        self.power, self.center, self.pad_mode = power, center, pad_mode
+        self.register_buffer("window", functional.get_window(window, self.win_length, dtype=dtype))
+
+    def forward(self, x):
+        t = x._t
+        spec = torch.stft(t, self.n_fft, self.hop, self.win_length, self.window._t.to(t.device, t.dtype),
+                          center=self.center, pad_mode=self.pad_mode, return_complex=True)
+        return _wrap(spec.abs() ** self.power)
+
+
+class MelSpectrogram(nn.Layer):
+    def __init__(self, sr=22050, n_fft=2048, hop_length=512, win_length=None, window="hann", power=2.0, center=True,
+                 pad_mode="reflect", n_mels=64, f_min=50.0, f_max=None, htk=False, norm="slaney", dtype="float32"):
+        super().__init__()
+        self._spec = Spectrogram(n_fft, hop_length, win_length, window, power, center, pad_mode, dtype)
+        self.register_buffer("fbank_matrix", functional.compute_fbank_matrix(sr, n_fft, n_mels, f_min, f_max, htk,
+                                                                             norm))
+
+    def forward(self, x):
+        s = self._spec(x)._t
+        return _wrap(torch.matmul(self.fbank_matrix._t.to(s.device, s.dtype), s))
+
+
+class LogMelSpectrogram(nn.Layer):
+    def __init__(self, sr=22050, n_fft=2048, hop_length=512, win_length=None, window="hann", power=2.0, center=True,
+                 pad_mode="reflect", n_mels=64, f_min=50.0, f_max=None, htk=False, norm="slaney", ref_value=1.0,
+                 amin=1e-10, top_db=None, dtype="float32"):
+        super().__init__()
+        self._mel = MelSpectrogram(sr, n_fft, hop_length, win_length, window, power, center, pad_mode, n_mels, f_min,
+                                   f_max, htk, norm, dtype)
+        self.ref_value, self.amin, self.top_db = ref_value, amin, top_db
+
+    def forward(self, x):
+        return functional.power_to_db(self._mel(x), self.ref_value, self.amin, self.top_db)
+
+
+class MFCC(nn.Layer):
+    def __init__(self, sr=22050, n_mfcc=40, n_fft=2048, hop_length=512, win_length=None, window="hann", power=2.0,
+                 center=True, pad_mode="reflect", n_mels=64, f_min=50.0, f_max=None, htk=False, norm="slaney",
+                 ref_value=1.0, amin=1e-10, top_db=None, dtype="float32"):
+        super().__init__()
+        self._log_mel = LogMelSpectrogram(sr, n_fft, hop_length, win_length, window, power, center, pad_mode, n_mels,
+                                          f_min, f_max, htk, norm, ref_value, amin, top_db, dtype)
+        self.register_buffer("dct_matrix", functional.create_dct(n_mfcc, n_mels))
+
+    def forward(self, x):
+        lm = self._log_mel(x)._t  # [B, n_mels, frames]
+        return _wrap(torch.matmul(lm.transpose(-1, -2), self.dct_matrix._t.to(lm.device, lm.dtype)).transpose(-1, -2))
+
+
+class features:
+    Spectrogram = Spectrogram
+    MelSpectrogram = MelSpectrogram
+    LogMelSpectrogram = LogMelSpectrogram
+    MFCC = MFCC
+
+
+def load(filepath, frame_offset=0, num_frames=-1, normalize=True, channels_first=True):
+    with wave.open(filepath, "rb") as w:
+        sr, nch, width = w.getframerate(), w.getnchannels(), w.getsampwidth()
+        w.setpos(frame_offset)
+        raw = w.readframes(w.getnframes() - frame_offset if num_frames < 0 else num_frames)
+    dt = {1: np.uint8, 2: np.int16, 4: np.int32}[width]
+    a = np.frombuffer(raw, dtype=dt).reshape(-1, nch).astype("float32")
+    if normalize:
+        a = (a - 128) / 128.0 if width == 1 else a / float(2 ** (8 * width - 1))
+    t = torch.from_numpy(a.T.copy() if channels_first else a.copy())
+    return _wrap(t), sr
+
+
+def save(filepath, src, sample_rate, channels_first=True, encoding=None, bits_per_sample=16):
+    a = src.numpy() if isinstance(src, Tensor) else np.asarray(src)
+    if channels_first:
+        a = a.T
+    a = np.clip(a, -1, 1)
+    pcm = (a * (2 ** (bits_per_sample - 1) - 1)).astype(np.int16 if bits_per_sample == 16 else np.int32)
+    with wave.open(filepath, "wb") as w:
+        w.setnchannels(pcm.shape[1] if pcm.ndim == 2 else 1)
+        w.setsampwidth(bits_per_sample // 8)
+        w.setframerate(sample_rate)
+        w.writeframes(pcm.tobytes())
+
+
+def info(filepath):
+    with wave.open(filepath, "rb") as w:
+        return {"sample_rate": w.getframerate(), "num_frames": w.getnframes(), "num_channels": w.getnchannels(),
+                "bits_per_sample": 8 * w.getsampwidth()}
+
+
+class backends:
+    @staticmethod
+    def list_available_backends():
+        return ["wave_backend"]
+
+    @staticmethod
+    def get_current_backend():
+        return "wave_backend"
+
+    @staticmethod
+    def set_backend(name):
+        if name != "wave_backend":
+            raise ValueError("only the built-in wave backend is available")

@@ -1,0 +1,213 @@
+"""paddle.sparse.nn: activations, batch norm, sparse (submanifold) convolutions and pooling on COO
+tensors in NDHWC / NHWC layout. Reference: python/paddle/sparse/nn/{layer,functional}/."""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as TF
+
+from .. import nn as _nn
+from ..framework.tensor import Tensor, _wrap
+from ..nn import initializer as I
+
+
+def _vals(x, fn):
+    t = x._t.coalesce()
+    return _wrap(torch.sparse_coo_tensor(t.indices(), fn(t.values()), t.shape))
+
+
+class functional:  # namespace object: paddle.sparse.nn.functional.*
+    @staticmethod
+    def relu(x, name=None):
+        return _vals(x, torch.relu)
+
+    @staticmethod
+    def relu6(x, name=None):
+        return _vals(x, lambda v: v.clamp(0, 6))
+
+    @staticmethod
+    def leaky_relu(x, negative_slope=0.01, name=None):
+        return _vals(x, lambda v: TF.leaky_relu(v, negative_slope))
+
+    @staticmethod
+    def softmax(x, axis=-1, name=None):
+        t = x._t
+        if t.layout == torch.sparse_csr:
+            return _wrap(torch.sparse.softmax(t.to_sparse_coo(), axis).to_sparse_csr())
+        return _wrap(torch.sparse.softmax(t.coalesce(), axis))
+
+    @staticmethod
+    def _conv(x, weight, bias, stride, padding, dilation, groups, subm, nd):
+        t = x._t.coalesce()
+        dense = t.to_dense()  # [N, *spatial, C]
+        perm_in = [0, nd + 1] + list(range(1, nd + 1))
+        d = dense.permute(perm_in)
+        w = weight._t  # [*k, Cin, Cout]
+        wk = w.permute([nd + 1, nd] + list(range(nd)))  # [Cout, Cin, *k]
+        conv = TF.conv3d if nd == 3 else TF.conv2d
+        if subm:
+            k = w.shape[:nd]
+            padding = [(kk - 1) // 2 * (dilation if isinstance(dilation, int) else dilation[i])
+                       for i, kk in enumerate(k)]
+            stride = 1
+        out = conv(d, wk, None if bias is None else bias._t, stride, padding, dilation, groups)
+        perm_out = [0] + list(range(2, nd + 2)) + [1]
+        out = out.permute(perm_out)
+        if subm:  # keep the input's active sites
+            idx = t.indices()[:nd + 1]
+            vals = out[tuple(idx)]
+            return _wrap(torch.sparse_coo_tensor(idx, vals, tuple(out.shape)).coalesce())
+        active = out.abs().sum(-1) != 0
+        idx = active.nonzero().t()
+        return _wrap(torch.sparse_coo_tensor(idx, out[tuple(idx)], tuple(out.shape)).coalesce())
+
+    @staticmethod
+    def conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NDHWC", name=None):
+        return functional._conv(x, weight, bias, stride, padding, dilation, groups, False, 3)
+
+    @staticmethod
+    def subm_conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NDHWC", key=None,
+                    name=None):
+        return functional._conv(x, weight, bias, stride, padding, dilation, groups, True, 3)
+
+    @staticmethod
+    def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NHWC", name=None):
+        return functional._conv(x, weight, bias, stride, padding, dilation, groups, False, 2)
+
+    @staticmethod
+    def subm_conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NHWC", key=None,
+                    name=None):
+        return functional._conv(x, weight, bias, stride, padding, dilation, groups, True, 2)
+
+    @staticmethod
+    def max_pool3d(x, kernel_size, stride=None, padding=0, ceil_mode=False, data_format="NDHWC", name=None):
+        t = x._t.coalesce()
+        d = t.to_dense().permute(0, 4, 1, 2, 3)
+        mask = (t.to_dense().abs().sum(-1) != 0).float()[:, None]
+        big = torch.where(mask.bool().expand_as(d), d, torch.full_like(d, float("-inf")))
+        o = TF.max_pool3d(big, kernel_size, stride, padding, ceil_mode=ceil_mode)
+        o = torch.where(torch.isinf(o), torch.zeros_like(o), o).permute(0, 2, 3, 4, 1)
+        active = TF.max_pool3d(mask, kernel_size, stride, padding, ceil_mode=ceil_mode)[:, 0] > 0
+        idx = active.nonzero().t()
+        return _wrap(torch.sparse_coo_tensor(idx, o[tuple(idx)], tuple(o.shape)).coalesce())
+
+    @staticmethod
+    def attention(query, key, value, sparse_mask, key_padding_mask=None, attn_mask=None, name=None):
+        """Attention whose score matrix is evaluated only at sparse_mask's nonzeros (CSR [B*H, S, S])."""
+        q, k, v = query._t, key._t, value._t  # [B, H, S, D]
+        B, H, S, D = q.shape
+        m = sparse_mask._t
+        dense_mask = m.to_dense().reshape(B, H, S, S) != 0
+        s = torch.matmul(q, k.transpose(-1, -2)) / math.sqrt(D)
+        if key_padding_mask is not None:
+            s = s + key_padding_mask._t[:, None, None, :]
+        if attn_mask is not None:
+            s = s + attn_mask._t
+        s = s.masked_fill(~dense_mask, float("-inf"))
+        p = torch.nan_to_num(torch.softmax(s, -1))
+        return _wrap(torch.matmul(p, v))
+
+
+class ReLU(_nn.Layer):
+    def forward(self, x):
+        return functional.relu(x)
+
+
+class ReLU6(_nn.Layer):
+    def forward(self, x):
+        return functional.relu6(x)
+
+
+class LeakyReLU(_nn.Layer):
+    def __init__(self, negative_slope=0.01, name=None):
+        super().__init__()
+        self.negative_slope = negative_slope
+
+    def forward(self, x):
+        return functional.leaky_relu(x, self.negative_slope)
+
+
+class Softmax(_nn.Layer):
+    def __init__(self, axis=-1, name=None):
+        super().__init__()
+        self.axis = axis
+
+    def forward(self, x):
+        return functional.softmax(x, self.axis)
+
+
+class BatchNorm(_nn.Layer):
+    """Batch norm over the values (channels last) of a COO tensor's active sites."""
+
+    def __init__(self, num_features, momentum=0.9, epsilon=1e-05, weight_attr=None, bias_attr=None,
+                 data_format="NDHWC", use_global_stats=None, name=None):
+        super().__init__()
+        self.weight = self.create_parameter([num_features], attr=weight_attr, default_initializer=I.Constant(1.0))
+        self.bias = self.create_parameter([num_features], attr=bias_attr, is_bias=True)
+        self.register_buffer("_mean", _wrap(torch.zeros(num_features)))
+        self.register_buffer("_variance", _wrap(torch.ones(num_features)))
+        self.momentum, self.eps = momentum, epsilon
+
+    def forward(self, x):
+        t = x._t.coalesce()
+        v = t.values()
+        if self.training:
+            mean, var = v.mean(0), v.var(0, unbiased=False)
+            with torch.no_grad():
+                self._mean._t.mul_(self.momentum).add_(mean.detach().to(self._mean._t.dtype), alpha=1 - self.momentum)
+                self._variance._t.mul_(self.momentum).add_(var.detach().to(self._variance._t.dtype),
+                                                           alpha=1 - self.momentum)
+        else:
+            mean, var = self._mean._t, self._variance._t
+        y = (v - mean) / torch.sqrt(var + self.eps) * self.weight._t + self.bias._t
+        return _wrap(torch.sparse_coo_tensor(t.indices(), y, t.shape))
+
+
+SyncBatchNorm = BatchNorm
+
+
+class _ConvBase(_nn.Layer):
+    _nd = 3
+    _subm = False
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, dilation=1, groups=1,
+                 padding_mode="zeros", key=None, weight_attr=None, bias_attr=None, data_format=None):
+        super().__init__()
+        k = [kernel_size] * self._nd if isinstance(kernel_size, int) else list(kernel_size)
+        fan_in = in_channels * math.prod(k)
+        self.weight = self.create_parameter(k + [in_channels // groups, out_channels], attr=weight_attr,
+                                            default_initializer=I.Uniform(-1 / math.sqrt(fan_in), 1 / math.sqrt(fan_in)))
+        self.bias = self.create_parameter([out_channels], attr=bias_attr, is_bias=True) if bias_attr is not False \
+            else None
+        self.stride, self.padding, self.dilation, self.groups = stride, padding, dilation, groups
+
+    def forward(self, x):
+        return functional._conv(x, self.weight, self.bias, self.stride, self.padding, self.dilation, self.groups,
+                                self._subm, self._nd)
+
+
+class Conv3D(_ConvBase):
+    _nd, _subm = 3, False
+
+
+class SubmConv3D(_ConvBase):
+    _nd, _subm = 3, True
+
+
+class Conv2D(_ConvBase):
+    _nd, _subm = 2, False
+
+
+class SubmConv2D(_ConvBase):
+    _nd, _subm = 2, True
+
+
+class MaxPool3D(_nn.Layer):
+    def __init__(self, kernel_size, stride=None, padding=0, return_mask=False, ceil_mode=False, data_format="NDHWC",
+                 name=None):
+        super().__init__()
+        self.k, self.s, self.p, self.c = kernel_size, stride, padding, ceil_mode
+
+    def forward(self, x):
+        return functional.max_pool3d(x, self.k, self.s, self.p, self.c)

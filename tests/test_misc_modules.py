@@ -1,0 +1,159 @@
+"""distribution / sparse / profiler / quantization / text / audio.
+Parity references: scipy.stats densities, numpy dense algebra, an explicit dynamic-programming Viterbi,
+librosa-style mel formulas written out in numpy (librosa itself is not installed: parity unpinned
+against it)."""
+import math
+import os
+
+import numpy as np
+import pytest
+import scipy.stats as st
+import torch
+
+import paddlepaddle_amd as paddle
+from paddlepaddle_amd import distribution as Dn
+
+
+def test_distributions_match_scipy():
+    x = np.array([0.3, -1.2, 2.0], dtype="float32")
+    n = Dn.Normal(paddle.to_tensor([0.5]), paddle.to_tensor([1.5]))
+    np.testing.assert_allclose(n.log_prob(paddle.to_tensor(x)).numpy(), st.norm(0.5, 1.5).logpdf(x), rtol=1e-5)
+    np.testing.assert_allclose(float(n.entropy().numpy()[0]), st.norm(0.5, 1.5).entropy(), rtol=1e-5)
+    u = Dn.Uniform(0.0, 2.0)
+    np.testing.assert_allclose(u.log_prob(paddle.to_tensor(np.array([0.5, 3.0], "float32"))).numpy(),
+                               [math.log(0.5), -np.inf])
+    b = Dn.Beta(paddle.to_tensor([2.0]), paddle.to_tensor([3.0]))
+    np.testing.assert_allclose(b.log_prob(paddle.to_tensor([0.4])).numpy(), st.beta(2, 3).logpdf(0.4), rtol=1e-5)
+    g = Dn.Gamma(paddle.to_tensor([2.0]), paddle.to_tensor([0.5]))
+    np.testing.assert_allclose(g.log_prob(paddle.to_tensor([1.7])).numpy(), st.gamma(2, scale=2).logpdf(1.7),
+                               rtol=1e-5)
+    lp = Dn.Laplace(paddle.to_tensor([0.0]), paddle.to_tensor([2.0]))
+    np.testing.assert_allclose(lp.log_prob(paddle.to_tensor([1.0])).numpy(), st.laplace(0, 2).logpdf(1.0), rtol=1e-5)
+    kl = Dn.kl_divergence(Dn.Normal(paddle.to_tensor([0.0]), paddle.to_tensor([1.0])),
+                          Dn.Normal(paddle.to_tensor([1.0]), paddle.to_tensor([2.0])))
+    np.testing.assert_allclose(kl.numpy(), math.log(2) + (1 + 1) / 8 - 0.5, rtol=1e-5)
+    c = Dn.Categorical(paddle.to_tensor([1.0, 3.0]))
+    s = c.sample([1000]).numpy()
+    assert abs(s.mean() - 0.75) < 0.08
+    # reparameterised sampling carries gradients
+    loc = paddle.to_tensor([0.0], stop_gradient=False)
+    Dn.Normal(loc, paddle.to_tensor([1.0])).rsample([16]).sum().backward()
+    assert float(loc.grad.numpy()[0]) == 16.0
+    t = Dn.TransformedDistribution(Dn.Normal(paddle.to_tensor([0.0]), paddle.to_tensor([1.0])), [Dn.ExpTransform()])
+    np.testing.assert_allclose(t.log_prob(paddle.to_tensor([2.0])).numpy(), st.lognorm(1.0).logpdf(2.0), rtol=1e-5)
+
+
+def test_sparse_coo_csr_ops():
+    dense = np.array([[0, 2, 0], [3, 0, 4], [0, 0, 5]], dtype="float32")
+    idx = np.array(np.nonzero(dense))
+    coo = paddle.sparse.sparse_coo_tensor(paddle.to_tensor(idx), paddle.to_tensor(dense[tuple(idx)]), [3, 3])
+    assert coo.is_sparse_coo() and coo.nnz() == 4
+    np.testing.assert_array_equal(coo.to_dense().numpy(), dense)
+    csr = coo.to_sparse_csr()
+    assert csr.is_sparse_csr()
+    np.testing.assert_array_equal(csr.crows().numpy(), [0, 1, 3, 4])
+    np.testing.assert_allclose(paddle.sparse.sqrt(coo).to_dense().numpy(), np.sqrt(dense))
+    y = np.arange(6, dtype="float32").reshape(3, 2)
+    np.testing.assert_allclose(paddle.sparse.matmul(coo, paddle.to_tensor(y)).numpy(), dense @ y)
+    np.testing.assert_allclose(paddle.sparse.matmul(csr, paddle.to_tensor(y)).numpy(), dense @ y)
+    a = np.random.RandomState(0).randn(3, 4).astype("float32")
+    b = np.random.RandomState(1).randn(4, 3).astype("float32")
+    mm = paddle.sparse.masked_matmul(paddle.to_tensor(a), paddle.to_tensor(b), csr)
+    np.testing.assert_allclose(mm.to_dense().numpy(), (a @ b) * (dense != 0), rtol=1e-5, atol=1e-6)
+    tr = paddle.sparse.transpose(coo, [1, 0])
+    np.testing.assert_array_equal(tr.to_dense().numpy(), dense.T)
+    np.testing.assert_allclose(float(paddle.sparse.sum(coo).numpy()), dense.sum())
+    np.testing.assert_array_equal(paddle.sparse.add(coo, coo).to_dense().numpy(), 2 * dense)
+    # submanifold conv keeps the active set
+    x = np.zeros((1, 4, 4, 4, 2), dtype="float32")
+    x[0, 1, 1, 1] = [1, 2]
+    x[0, 2, 3, 0] = [3, 4]
+    sp = paddle.to_tensor(x).to_sparse_coo(4)
+    conv = paddle.sparse.nn.SubmConv3D(2, 3, 3, padding=1)
+    out = conv(sp)
+    assert out.nnz() == 2 and out.shape == [1, 4, 4, 4, 3]
+
+
+def test_profiler_records_and_exports(tmp_path):
+    lin = paddle.nn.Linear(8, 8)
+    x = paddle.randn([4, 8])
+    sched = paddle.profiler.make_scheduler(closed=1, ready=0, record=2, repeat=1)
+    out_dir = str(tmp_path / "trace")
+    with paddle.profiler.Profiler(scheduler=sched, on_trace_ready=paddle.profiler.export_chrome_tracing(out_dir)) as p:
+        for _ in range(4):
+            with paddle.profiler.RecordEvent("my_step"):
+                lin(x).sum().backward()
+            p.step(num_samples=4)
+    files = os.listdir(out_dir)
+    assert files and "my_step" in open(os.path.join(out_dir, files[0])).read()
+    assert "ips" in p.step_info()
+    assert [sched(i) for i in range(4)][:3] == [paddle.profiler.ProfilerState.CLOSED,
+                                                 paddle.profiler.ProfilerState.RECORD,
+                                                 paddle.profiler.ProfilerState.RECORD_AND_RETURN]
+
+
+def test_qat_ptq_int8_and_fp8():
+    from paddlepaddle_amd.quantization import QuantConfig, QAT, PTQ, FakeQuanterWithAbsMaxObserver, AbsmaxObserver
+    paddle.seed(0)
+    model = paddle.nn.Sequential(paddle.nn.Linear(8, 16), paddle.nn.ReLU(), paddle.nn.Linear(16, 4))
+    x = paddle.randn([32, 8])
+    ref = model(x).numpy()
+    q = FakeQuanterWithAbsMaxObserver(moving_rate=0.9)
+    qat = QAT(QuantConfig(activation=q, weight=q))
+    qm = qat.quantize(model)
+    assert type(qm[0]).__name__ == "QuantedLinear"
+    out = qm(x)
+    assert np.abs(out.numpy() - ref).max() < 0.1 * np.abs(ref).max() + 0.05  # int8 fake quant is close
+    out.sum().backward()  # STE: gradients flow
+    assert qm[0].weight.grad is not None
+    fp8 = FakeQuanterWithAbsMaxObserver(bit_length="e4m3")
+    q8 = QAT(QuantConfig(activation=fp8, weight=fp8)).quantize(model)
+    assert np.abs(q8(x).numpy() - ref).max() < 0.15 * np.abs(ref).max() + 0.05
+    ptq = PTQ(QuantConfig(activation=AbsmaxObserver(), weight=AbsmaxObserver()))
+    pm = ptq.quantize(model)
+    for _ in range(3):
+        pm(x)
+    cm = ptq.convert(pm)
+    w = cm[0].weight.numpy()
+    scale = np.abs(model[0].weight.numpy()).max()
+    assert np.allclose(np.round(w / scale * 127), w / scale * 127, atol=1e-3)  # on the int8 grid
+
+
+def test_viterbi_matches_bruteforce():
+    rng = np.random.RandomState(0)
+    B, T, N = 2, 4, 3
+    pot = rng.randn(B, T, N).astype("float32")
+    trans = rng.randn(N, N).astype("float32")
+    lens = np.array([4, 3])
+    scores, paths = paddle.text.viterbi_decode(paddle.to_tensor(pot), paddle.to_tensor(trans),
+                                               paddle.to_tensor(lens), include_bos_eos_tag=False)
+    import itertools
+    for b in range(B):
+        best, bp = -1e9, None
+        for p in itertools.product(range(N), repeat=int(lens[b])):
+            s = pot[b, 0, p[0]] + sum(trans[p[i - 1], p[i]] + pot[b, i, p[i]] for i in range(1, len(p)))
+            if s > best:
+                best, bp = s, p
+        np.testing.assert_allclose(scores.numpy()[b], best, rtol=1e-5)
+        assert paths.numpy()[b][:lens[b]].tolist() == list(bp)
+
+
+def test_audio_features_and_wav(tmp_path):
+    sr = 16000
+    t = np.arange(sr // 4) / sr
+    sig = (0.5 * np.sin(2 * np.pi * 440 * t)).astype("float32")
+    x = paddle.to_tensor(sig[None])
+    spec = paddle.audio.Spectrogram(n_fft=512, hop_length=128)(x)
+    assert spec.shape[1] == 257
+    peak_bin = int(spec.numpy()[0].mean(-1).argmax())
+    assert abs(peak_bin * sr / 512 - 440) < sr / 512
+    mel = paddle.audio.MelSpectrogram(sr=sr, n_fft=512, hop_length=128, n_mels=40)(x)
+    assert mel.shape[1] == 40
+    mfcc = paddle.audio.MFCC(sr=sr, n_mfcc=13, n_fft=512, hop_length=128, n_mels=40)(x)
+    assert mfcc.shape[1] == 13
+    np.testing.assert_allclose(paddle.audio.functional.hz_to_mel(1000.0, htk=True), 2595 * np.log10(1 + 1000 / 700),
+                               rtol=1e-6)
+    p = str(tmp_path / "a.wav")
+    paddle.audio.save(p, x, sr)
+    y, sr2 = paddle.audio.load(p)
+    assert sr2 == sr and np.abs(y.numpy() - sig[None]).max() < 1e-3
