@@ -79,15 +79,19 @@ class ClipGradByGlobalNorm(ClipGradBase):
                 out.append((p, _wrap((g._t * scale.to(g._t.dtype)))))
         return out
 
+    def _coef(self, ps):
+        """Device fp32 scalar clip_norm / max(global_norm, clip_norm) over the grads of ``ps``."""
+        grads = [p._t.grad for p in ps]
+        fn = getattr(self, "_param_sq_fn", None)
+        gn = torch.sqrt(fn(ps)) if fn is not None else self._global_norm(grads)
+        return (self.clip_norm / torch.clamp(gn.float(), min=self.clip_norm)).reshape(())
+
     def _clip_inplace(self, params):
         ps = [p for p in params if p._t.grad is not None and getattr(p, "need_clip", True)]
         grads = [p._t.grad for p in ps]
         if not grads:
             return
-        fn = getattr(self, "_param_sq_fn", None)
-        gn = torch.sqrt(fn(ps)) if fn is not None else self._global_norm(grads)
-        scale = self.clip_norm / torch.clamp(gn, min=self.clip_norm)
-        torch._foreach_mul_(grads, scale)
+        torch._foreach_mul_(grads, self._coef(ps))
 
 
 def clip_grad_norm_(parameters, max_norm, norm_type=2.0, error_if_nonfinite=False):

@@ -36,6 +36,20 @@ class Adam(Optimizer):
     def _coeff_for(self, group, p):
         return 0.0
 
+    def _apply_clip(self):
+        """Global-norm clipping folded into the fused update: the clip coefficient stays a device
+        scalar that the AdamW kernel multiplies into every gradient it reads (no separate pass over
+        the gradients). Other clips, or parameters that take the per-tensor path, scale explicitly."""
+        self._clip_coef = None
+        clip = self._grad_clip
+        from ..nn.clip import ClipGradByGlobalNorm
+        ps = [p for p in self._parameter_list if p._t.grad is not None]
+        if (isinstance(clip, ClipGradByGlobalNorm) and ps and all(getattr(p, "need_clip", True) for p in ps)
+                and L.hip_enabled_for(ps[0]._t) and L.has("pa_adamw_multi") and not self._amsgrad):
+            self._clip_coef = clip._coef(ps)
+            return
+        super()._apply_clip()
+
     def _hyper(self, group):
         b1 = group.get("beta1", self._beta1)
         b2 = group.get("beta2", self._beta2)
@@ -55,6 +69,9 @@ class Adam(Optimizer):
         if dev_ok and same_step and (self._decoupled or not self._has_l2(group, params)):
             self._fused(group, params, lr, b1, b2, eps, steps[0])
             return
+        coef = getattr(self, "_clip_coef", None)
+        if coef is not None:  # deferred clip, but this group takes the per-tensor path
+            torch._foreach_mul_([p._t.grad for p in params], coef)
         for p, s in zip(params, steps):
             self._single(group, p, lr, b1, b2, eps, s)
 
@@ -120,6 +137,9 @@ class Adam(Optimizer):
         bc1 = 1 - b1 ** step
         bc2 = 1 - b2 ** step
         inv_scale = getattr(self, "_inv_scale_tensor", None)
+        coef = getattr(self, "_clip_coef", None)
+        if coef is not None:
+            inv_scale = coef if inv_scale is None else (coef * inv_scale.reshape(())).reshape(())
         L.call("pa_adamw_multi", L.ptr(t_rows), L.ptr(t_items), n_items, L.ptr(inv_scale), float(lr), float(b1),
                float(b2), float(eps), 0.0, float(bc1), float(bc2), L.ptr(None), L.stream_ptr())
         self._last_step = step

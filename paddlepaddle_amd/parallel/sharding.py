@@ -76,6 +76,7 @@ class _Flat:
             self.shard._t.grad_dtype = None  # bf16 shard, fp32 reduce-scattered gradient
         self.shard_grad = torch.zeros(self.shard_size, dtype=torch.float32, device=self.device) if world > 1 else None
         self.full_grad = None
+        self.ready_fn = None  # engine's grad-ready handler (set once the unit is built)
         # re-point model params at views of the full buffer
         for p, o, n in zip(params, self.offsets, self.numels):
             req = p._t.requires_grad
@@ -84,9 +85,14 @@ class _Flat:
     # -- grads
     def alloc_full_grad(self):
         if self.full_grad is None:
+            from ..ops.linear import register_main_grad
             self.full_grad = torch.zeros(self.padded, dtype=self.dtype, device=self.device)
             for p, o, n in zip(self.params, self.offsets, self.numels):
-                p._t.grad = self.full_grad[o:o + n].view(p._t.shape)
+                view = self.full_grad[o:o + n].view(p._t.shape)
+                p._t.grad = view
+                if p._t.dim() == 2 and self.ready_fn is not None:
+                    # linear weights: the wgrad GEMM accumulates into this view directly
+                    register_main_grad(p._t, view, self.ready_fn)
         return self.full_grad
 
     def fold_param_grads(self):
@@ -102,8 +108,10 @@ class _Flat:
                 p._t.grad = v.view(p._t.shape)
 
     def drop_full_grad(self):
+        from ..ops.linear import unregister_main_grad
         for p in self.params:
             p._t.grad = None
+            unregister_main_grad(p._t)
         self.full_grad = None
 
     # -- params (stage 3 storage management)
@@ -254,9 +262,11 @@ class GroupShardedEngine:
     # ------------------------------------------------------------------ hooks
     def _install_hooks(self):
         for ui, u in enumerate(self.units):
+            hook = self._make_grad_hook(u)
             for f in u.flats:
+                f.ready_fn = hook
                 for p in f.params:
-                    p._t.register_post_accumulate_grad_hook(self._make_grad_hook(u))
+                    p._t.register_post_accumulate_grad_hook(hook)
             if ui == 0:
                 continue  # root unit: gathered for the whole step (embedding / tied head / final norm)
             u.layer.register_forward_pre_hook(self._make_fwd_pre(ui))
