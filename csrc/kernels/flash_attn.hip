@@ -372,6 +372,19 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) { dk_acc[dt] = zero16(); dv_acc[dt] = zero16(); }
 
+  // This lane's K / V rows as MFMA B fragments, loaded once: they are the same for every query
+  // block, so the S / dP chains below read only Q / dO from LDS (half the LDS traffic of that phase).
+  __syncthreads();
+  bf16x8_t kfr[KS], vfr[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    Frag kb8, vb8;
+    kb8.u = lds_b128(k_lds, img_off<NCH>(w * 32 + r, 2 * ks + hf));
+    vb8.u = lds_b128(v_lds, img_off<NCH>(w * 32 + r, 2 * ks + hf));
+    kfr[ks] = kb8.v;
+    vfr[ks] = vb8.v;
+  }
+
   // query range that sees any key of this block
   int q_begin = 0;
   if (p.causal) q_begin = max(0, kb * BK - shift);
@@ -386,7 +399,11 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
   // block computes (async-stage split): the HBM latency is hidden behind ~40 MFMAs per wave.
   constexpr int QLOADS = BM * NCH / 256;
   uint4 qreg[QLOADS], dreg[QLOADS];
-  float lse_r = INFINITY, dlt_r = 0.f;
+  float lse_r = -INFINITY, dlt_r = 0.f;
+  const float inv_scale = 1.f / p.scale;
+  // dQ accumulator of this (b, h) as a buffer resource: 32-bit offsets, no 64-bit address math per atomic
+  const __amdgpu_buffer_rsrc_t dq_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      dqb, 0, (int)((int64_t)(p.Sq - 1) * p.H * D * 4 + D * 4), 0x00020000);
   auto prefetch = [&](int q0) {
 #pragma unroll
     for (int i = 0; i < QLOADS; ++i) {
@@ -401,9 +418,11 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
       }
     }
     if (tid < BM) {
+      // row constants enter the S / dP accumulators as their initial values:
+      // S' = Q K^T - LSE/scale  ->  P = exp2(scale*log2e * S');   dP' = dO V^T - delta  ->  dS = P * dP'
       const int qx = q0 + tid;
-      lse_r = qx < p.Sq ? lse_b[qx] * kLog2e : INFINITY;
-      dlt_r = qx < p.Sq ? dlt_b[qx] : 0.f;
+      lse_r = qx < p.Sq ? -lse_b[qx] * inv_scale : -INFINITY;
+      dlt_r = qx < p.Sq ? -dlt_b[qx] : 0.f;
     }
   };
   if (q_begin < p.Sq) prefetch(q_begin);
@@ -424,35 +443,33 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
     __syncthreads();
     if (q0 + BM < p.Sq) prefetch(q0 + BM);
 
-    // S = Q K^T and dP = dO V^T : rows q (registers), cols = this lane's key
-    f32x16 sacc = zero16(), pacc = zero16();
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      Frag qa, da, kb8, vb8;
-      qa.u = lds_b128(q_lds, img_off<NCH>(r, 2 * ks + hf));
-      da.u = lds_b128(do_lds, img_off<NCH>(r, 2 * ks + hf));
-      kb8.u = lds_b128(k_lds, img_off<NCH>(w * 32 + r, 2 * ks + hf));
-      vb8.u = lds_b128(v_lds, img_off<NCH>(w * 32 + r, 2 * ks + hf));
-      sacc = mfma32(qa.v, kb8.v, sacc);
-      pacc = mfma32(da.v, vb8.v, pacc);
-    }
-    // P and dS computed in place, then packed straight into bf16 MFMA fragments.
-    // lse/delta for this lane's 16 query rows: 4 x 16-byte LDS reads each (rows 8g+4hf .. +3)
-    const bool need_mask = kj >= p.Sk || (p.causal && kb * BK + BK - 1 > q0 + shift);
-    float4 l4[4], d4[4];
+    // S' = Q K^T - LSE/scale and dP' = dO V^T - delta : rows q (registers), cols = this lane's key.
+    // Row constants for this lane's 16 query rows (8g + 4hf + 0..3): 4 x 16-byte LDS reads each.
+    f32x16 sacc, pacc;
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      l4[g] = *reinterpret_cast<const float4*>(lse_s + 8 * g + 4 * hf);
-      d4[g] = *reinterpret_cast<const float4*>(dlt_s + 8 * g + 4 * hf);
+      const float4 l4 = *reinterpret_cast<const float4*>(lse_s + 8 * g + 4 * hf);
+      const float4 d4 = *reinterpret_cast<const float4*>(dlt_s + 8 * g + 4 * hf);
+      sacc[4 * g + 0] = l4.x; sacc[4 * g + 1] = l4.y; sacc[4 * g + 2] = l4.z; sacc[4 * g + 3] = l4.w;
+      pacc[4 * g + 0] = d4.x; pacc[4 * g + 1] = d4.y; pacc[4 * g + 2] = d4.z; pacc[4 * g + 3] = d4.w;
     }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      Frag qa, da;
+      qa.u = lds_b128(q_lds, img_off<NCH>(r, 2 * ks + hf));
+      da.u = lds_b128(do_lds, img_off<NCH>(r, 2 * ks + hf));
+      sacc = mfma32(qa.v, kfr[ks], sacc);
+      pacc = mfma32(da.v, vfr[ks], pacc);
+    }
+    // P and dS computed in place, then packed straight into bf16 MFMA fragments.
+    const bool need_mask = kj >= p.Sk || (p.causal && kb * BK + BK - 1 > q0 + shift);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int qr = (i & 3) + 8 * (i >> 2) + 4 * hf;
-      const float lv = (&l4[i >> 2].x)[i & 3], dv = (&d4[i >> 2].x)[i & 3];
-      float pr = __builtin_amdgcn_exp2f(sacc[i] * p.scale_log2 - lv);
+      float pr = __builtin_amdgcn_exp2f(sacc[i] * p.scale_log2);
       if (need_mask && (kj >= p.Sk || (p.causal && kj > q0 + qr + shift))) pr = 0.f;
       sacc[i] = pr;
-      pacc[i] = pr * (pacc[i] - dv);
+      pacc[i] = pr * pacc[i];
     }
     bf16x8_t pf[2], sf[2];
 #pragma unroll
@@ -482,16 +499,20 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
       }
     }
 
-    // dS^T tile [128 keys][32 q] bf16: lane writes its key row, 4 consecutive q per 8-byte store
+    // dS^T tile [128 keys][32 q] bf16: lane writes its key row, 4 consecutive q per 8-byte store.
+    // 64-byte rows: the 8-byte column slot is XORed with (row >> 2) & 3 so that the 16 rows of a
+    // store's lane group land on distinct banks (rows r, r+4, r+8, r+12 would collide otherwise).
     {
       // fragment s, elements 0..3 = q 16s+4hf+0..3, elements 4..7 = q 16s+8+4hf+0..3
-      char* rowp = ds_lds + (w * 32 + r) * (BM * 2);
+      const int row = w * 32 + r;
+      char* rowp = ds_lds + row * (BM * 2);
+      const int sw = ((row >> 2) & 3) << 3;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         Frag f;
         f.v = sf[s];
-        *reinterpret_cast<uint2*>(rowp + (16 * s + 4 * hf) * 2) = make_uint2(f.u.x, f.u.y);
-        *reinterpret_cast<uint2*>(rowp + (16 * s + 8 + 4 * hf) * 2) = make_uint2(f.u.z, f.u.w);
+        *reinterpret_cast<uint2*>(rowp + (((16 * s + 4 * hf) * 2) ^ sw)) = make_uint2(f.u.x, f.u.y);
+        *reinterpret_cast<uint2*>(rowp + (((16 * s + 8 + 4 * hf) * 2) ^ sw)) = make_uint2(f.u.z, f.u.w);
       }
     }
     __syncthreads();
@@ -503,8 +524,9 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
         Frag a, bb;
         // A = dS[q=r][key = 16ks + 8hf + j]: transposed read of the dS^T image (rows = keys)
         const int kr0 = 16 * ks + 8 * hf;
-        a.h[0] = lds_tr(ds_lds, (kr0 + qq) * (BM * 2) + (16 * G1 + 4 * pp) * 2);
-        a.h[1] = lds_tr(ds_lds, (kr0 + 4 + qq) * (BM * 2) + (16 * G1 + 4 * pp) * 2);
+        const int ra = kr0 + qq, rb = kr0 + 4 + qq;
+        a.h[0] = lds_tr(ds_lds, ra * (BM * 2) + (((16 * G1 + 4 * pp) * 2) ^ (((ra >> 2) & 3) << 3)));
+        a.h[1] = lds_tr(ds_lds, rb * (BM * 2) + (((16 * G1 + 4 * pp) * 2) ^ (((rb >> 2) & 3) << 3)));
         // B = K[key = 16ks + 8hf + j][d = dt*32 + r]: transposed read of the K image
         const int cch = (dt * 32 + 16 * G1) / 8 + (pp >> 1);
         bb.h[0] = lds_tr(k_lds, img_off<NCH>(kr0 + qq, cch) + 8 * (pp & 1));
@@ -512,18 +534,15 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
         qacc = mfma32(a.v, bb.v, qacc);
       }
       if (p.causal >= 0) {
-        float* dst = dqb + (int64_t)q0 * p.H * D + dt * 32 + r;
-        const int64_t rs = (int64_t)p.H * D;
-        if (q0 + BM <= p.Sq) {
+        // byte offsets into this (b, h)'s dQ rows (row stride H*D floats); out-of-range rows
+        // (ragged last block) fall outside the buffer resource and are dropped by the hardware
+        const int rs = p.H * D * 4;
+        const int base = q0 * rs + (dt * 32 + r) * 4;
 #pragma unroll
-          for (int i = 0; i < 16; ++i)
-            atomicAdd(dst + (int64_t)((i & 3) + 8 * (i >> 2) + 4 * hf) * rs, qacc[i] * p.scale);
-        } else {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int qr = (i & 3) + 8 * (i >> 2) + 4 * hf;
-            if (q0 + qr < p.Sq) atomicAdd(dst + (int64_t)qr * rs, qacc[i] * p.scale);
-          }
+        for (int i = 0; i < 16; ++i) {
+          const int qr = (i & 3) + 8 * (i >> 2) + 4 * hf;
+          const int off = (q0 + qr < p.Sq) ? base + qr * rs : 0x7ffffff0;
+          __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(qacc[i] * p.scale, dq_rsrc, off, 0, 0);
         }
       } else {
 #pragma unroll

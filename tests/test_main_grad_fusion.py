@@ -58,7 +58,8 @@ def test_sharding_engine_fused_wgrad_matches_plain_gpu():
         return {k: v.astype("float32").numpy() for k, v in model.state_dict().items()}
     ref, got = run(False), run(True)
     for k in ref:
-        np.testing.assert_allclose(got[k], ref[k], rtol=2e-2, atol=2e-3, err_msg=k)
+        # bf16 weights: accumulating inside the GEMM rounds differently from GEMM + add
+        np.testing.assert_allclose(got[k], ref[k], rtol=2e-2, atol=5e-3, err_msg=k)
 
 
 @pytest.mark.gpu
