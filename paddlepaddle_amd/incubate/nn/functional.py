@@ -320,15 +320,17 @@ def masked_multihead_attention(x, cache_kv=None, bias=None, src_mask=None, cum_o
     bi = torch.arange(B, device=xt.device)
     cache[0][bi, :, steps] = k.to(cache.dtype)
     cache[1][bi, :, steps] = v.to(cache.dtype)
-    pos = torch.arange(L, device=xt.device)
-    valid = pos[None, :] <= steps[:, None]  # [B, L]
-    s = torch.einsum("bhd,bhld->bhl", q.float(), cache[0].float()) / math.sqrt(D)
-    if src_mask is not None:
+    if src_mask is None:  # HIP flash-decoding over the dense cache (ops.dense_decode_attention)
+        o = _ops.dense_decode_attention(q, cache[0], cache[1], steps + 1).to(xt.dtype)
+    else:
+        pos = torch.arange(L, device=xt.device)
+        valid = pos[None, :] <= steps[:, None]  # [B, L]
+        s = torch.einsum("bhd,bhld->bhl", q.float(), cache[0].float()) / math.sqrt(D)
         sm = _t(src_mask).float().reshape(B, 1, -1)
         s[..., :sm.shape[-1]] = s[..., :sm.shape[-1]] + sm
-    s = s.masked_fill(~valid[:, None], float("-inf"))
-    p = torch.softmax(s, -1)
-    o = torch.einsum("bhl,bhld->bhd", p, cache[1].float()).to(xt.dtype)
+        s = s.masked_fill(~valid[:, None], float("-inf"))
+        p = torch.softmax(s, -1)
+        o = torch.einsum("bhl,bhld->bhd", p, cache[1].float()).to(xt.dtype)
     out = o.reshape(B, H * D)
     if out_shift is not None:
         out = out + _t(out_shift)
@@ -420,15 +422,10 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
         blk = bt[bidx, steps // bs]
         kc[blk, :, steps % bs] = k.to(kc.dtype)
         vc[blk, :, steps % bs] = v.to(vc.dtype)
-        L = int(steps.max()) + 1
+        L = max(int(dec[b]) for b, _ in dec_b) + 1
         nblk = (L + bs - 1) // bs
-        tab = bt[bidx, :nblk]                               # [nd, nblk]
-        K = kc[tab].permute(0, 2, 1, 3, 4).reshape(len(dec_b), H, nblk * bs, D)
-        Vv = vc[tab].permute(0, 2, 1, 3, 4).reshape(len(dec_b), H, nblk * bs, D)
-        s = torch.einsum("nhd,nhld->nhl", q.float(), K.float()) / math.sqrt(D)
-        valid = torch.arange(nblk * bs, device=x.device)[None] <= steps[:, None]
-        s = s.masked_fill(~valid[:, None], float("-inf"))
-        o = torch.einsum("nhl,nhld->nhd", torch.softmax(s, -1), Vv.float())
+        # HIP flash-decoding kernel (ops.paged_decode_attention) streams each sequence's blocks
+        o = _ops.paged_decode_attention(q.to(kc.dtype), kc, vc, bt[bidx, :nblk], steps + 1, max_len=L)
         out[toks] = o.to(out.dtype)
     res = out.reshape(x.shape[0], H * D)
     if out_shift is not None:

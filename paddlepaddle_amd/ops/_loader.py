@@ -100,6 +100,8 @@ def _declare(L):
         "pa_flash_attn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _f32, _i32, _vp],
         "pa_flash_attn_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                               _i32, _i32, _i32, _i32, _i32, _i32, _f32, _i32, _vp],
+        "pa_paged_decode_attn": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
+                                 _i64, _i64, _f32, _vp],
         # gemm epilogue companions
         "pa_colsum": [_vp, _vp, _vp, _i64, _i64, _i32, _vp],
         "pa_bias_gelu_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp],

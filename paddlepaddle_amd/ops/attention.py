@@ -185,3 +185,95 @@ def flash_attention(q, k, v, causal=False, scale=None, mask=None, dropout=0.0, t
     if _hip_ok(q, k, v, mask, dropout, training):
         return _FlashAttnHIP.apply(q, k, v, bool(causal), scale)
     return _sdpa(q, k, v, causal, scale, mask, dropout, training)
+
+
+def paged_decode_reference(q, key_cache, value_cache, block_tables, lens, scale=None):
+    """fp32 reference: q [N,H,D]; caches [num_blocks,Hkv,bs,D]; block_tables [N,max_blocks]; lens [N]
+    (cached tokens per sequence, the current one included). Returns [N,H,D] in q's dtype."""
+    N, H, D = q.shape
+    _, Hkv, bs, _ = key_cache.shape
+    scale = 1.0 / math.sqrt(D) if scale is None else float(scale)
+    nblk = block_tables.shape[1]
+    tab = block_tables.long()
+    K = key_cache[tab].permute(0, 2, 1, 3, 4).reshape(N, Hkv, nblk * bs, D).float()
+    V = value_cache[tab].permute(0, 2, 1, 3, 4).reshape(N, Hkv, nblk * bs, D).float()
+    G = H // Hkv
+    qf = q.float().view(N, Hkv, G, D)
+    s = torch.einsum("nkgd,nkld->nkgl", qf, K) * scale
+    valid = torch.arange(nblk * bs, device=q.device)[None] < lens.long()[:, None]
+    s = s.masked_fill(~valid[:, None, None], float("-inf"))
+    o = torch.einsum("nkgl,nkld->nkgd", torch.softmax(s, -1), V)
+    return o.reshape(N, H, D).to(q.dtype)
+
+
+def _decode_splits(N, Hkv, max_len, bs):
+    """Flash-decoding split count: enough workgroups to fill 256 CUs (≈4 per CU), but every split
+    keeps ≥ 4 cache blocks so each of the workgroup's 4 waves has a block to stream."""
+    nblk = max(1, (max_len + bs - 1) // bs)
+    want = max(1, -(-1024 // max(1, N * Hkv)))
+    return int(max(1, min(want, nblk // 4, 64)))
+
+
+def _decode_hip_ok(q, key_cache, value_cache, Hkv):
+    N, H, D = q.shape
+    return (L.hip_enabled_for(q) and L.has("pa_paged_decode_attn") and q.dtype == torch.bfloat16
+            and key_cache.dtype == torch.bfloat16 and value_cache.dtype == torch.bfloat16 and D == 128
+            and H % Hkv == 0 and H // Hkv in (1, 2, 4, 8) and key_cache.is_contiguous()
+            and value_cache.is_contiguous())
+
+
+def _decode_launch(q, kc, vc, tables, lens, Hkv, bs, blk_stride, head_stride, scale, max_len):
+    N, H, D = q.shape
+    q = q.contiguous()
+    tables = tables.to(torch.int32).contiguous()
+    lens32 = lens.to(torch.int32).contiguous()
+    max_blocks = tables.shape[1]
+    splits = _decode_splits(N, Hkv, max_len, bs)
+    part_o = torch.empty(N * H * splits * D, dtype=torch.float32, device=q.device)
+    part_ml = torch.empty(N * H * splits * 2, dtype=torch.float32, device=q.device)
+    out = torch.empty_like(q)
+    L.call("pa_paged_decode_attn", L.ptr(q), L.ptr(kc), L.ptr(vc), L.ptr(tables), L.ptr(lens32), L.ptr(part_o),
+           L.ptr(part_ml), L.ptr(out), N, H, Hkv, D, bs, max_blocks, splits, int(blk_stride), int(head_stride),
+           float(scale), L.stream_ptr())
+    return out
+
+
+@static_op
+def paged_decode_attention(q, key_cache, value_cache, block_tables, lens, scale=None, max_len=None):
+    """One-token-per-sequence attention over a paged KV cache (block_multihead_attention decode).
+    q [N,H,D]; caches [num_blocks,Hkv,block_size,D]; block_tables [N,max_blocks]; lens [N] cached
+    tokens incl. the current one. HIP flash-decoding kernel (csrc/kernels/decode_attn.hip) for bf16,
+    head_dim 128; otherwise the fp32 reference. ``max_len`` bounds lens (host hint for the split count;
+    defaults to the block-table capacity, so no device sync)."""
+    N, H, D = q.shape
+    _, Hkv, bs, _ = key_cache.shape
+    scale = 1.0 / math.sqrt(D) if scale is None else float(scale)
+    if not _decode_hip_ok(q, key_cache, value_cache, Hkv):
+        return paged_decode_reference(q, key_cache, value_cache, block_tables, lens, scale)
+    ml = block_tables.shape[1] * bs if max_len is None else int(max_len)
+    return _decode_launch(q, key_cache, value_cache, block_tables, lens, Hkv, bs, Hkv * bs * D, bs * D, scale, ml)
+
+
+_VBLK = 64  # virtual block size when a dense cache is streamed by the paged kernel
+
+
+@static_op
+def dense_decode_attention(q, key_cache, value_cache, lens, scale=None, max_len=None):
+    """Decode attention over a dense per-sequence cache [B,Hkv,max_len,D] (masked_multihead_attention
+    layout). The same HIP kernel streams it as virtual 64-token blocks: block j of sequence b starts at
+    b*Hkv*max_len*D + j*64*D and heads are max_len*D apart, so the block table is just b*Hkv*nb + j."""
+    N, H, D = q.shape
+    B, Hkv, Lc, _ = key_cache.shape
+    scale = 1.0 / math.sqrt(D) if scale is None else float(scale)
+    if not _decode_hip_ok(q, key_cache, value_cache, Hkv) or Lc % _VBLK != 0:
+        valid = torch.arange(Lc, device=q.device)[None] < lens.long()[:, None]
+        G = H // Hkv
+        s = torch.einsum("nkgd,nkld->nkgl", q.float().view(N, Hkv, G, D), key_cache.float()) * scale
+        s = s.masked_fill(~valid[:, None, None], float("-inf"))
+        o = torch.einsum("nkgl,nkld->nkgd", torch.softmax(s, -1), value_cache.float())
+        return o.reshape(N, H, D).to(q.dtype)
+    nb = Lc // _VBLK
+    tables = (torch.arange(N, device=q.device, dtype=torch.int32)[:, None] * (Hkv * nb)
+              + torch.arange(nb, device=q.device, dtype=torch.int32)[None])
+    ml = Lc if max_len is None else int(max_len)
+    return _decode_launch(q, key_cache, value_cache, tables, lens, Hkv, _VBLK, _VBLK * D, Lc * D, scale, ml)
