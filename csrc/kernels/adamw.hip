@@ -137,6 +137,73 @@ __global__ __launch_bounds__(256) void sq_norm_multi_k(const int64_t* __restrict
   if (threadIdx.x == 0) partial[blockIdx.x] = acc;
 }
 
+// Multi-tensor Momentum (paddle/phi/kernels/gpu/momentum_kernel.cu semantics): same table rows as
+// AdamW with m* = velocity (fp32) and v* unused; wd = L2 coefficient folded into the gradient.
+//   g = grad * rescale * inv_scale + wd * p;  vel = mu * vel + g;  p -= lr * (nesterov ? g + mu * vel : vel)
+__global__ __launch_bounds__(256) void momentum_multi_k(const int64_t* __restrict__ table,
+                                                        const int64_t* __restrict__ items, int64_t n_items,
+                                                        const float* __restrict__ inv_scale_p, float lr, float mu,
+                                                        float rescale, int nesterov) {
+  const float gs = rescale * (inv_scale_p ? *inv_scale_p : 1.f);
+  for (int64_t it = blockIdx.x; it < n_items; it += gridDim.x) {
+    const int64_t ti = items[it * 2], s = items[it * 2 + 1];
+    const int64_t* r = table + ti * 9;
+    float* __restrict__ P = (float*)r[0];
+    const void* G = (const void*)r[1];
+    float* __restrict__ VEL = (float*)r[2];
+    void* LP = (void*)r[4];
+    const int64_t n = r[5];
+    const int gdt = (int)(r[6] & 0xff), ldt = (int)((r[6] >> 8) & 0xff);
+    const float wd = __int_as_float((int)r[7]);
+    const float plr = lr * __int_as_float((int)r[8]);
+    const int64_t e = s + kChunk < n ? s + kChunk : n;
+    const bool vec = ((((uintptr_t)P | (uintptr_t)VEL) & 15) == 0) &&
+                     ((((uintptr_t)G) & (gdt == kF32 ? 15 : 7)) == 0) &&
+                     (ldt == 3 || ((((uintptr_t)LP) & (ldt == kF32 ? 15 : 7)) == 0)) && (s % 4 == 0);
+    int64_t i0 = s;
+    if (vec) {
+      const int64_t ev = s + ((e - s) / 4) * 4;
+      for (int64_t i = s + (int64_t)threadIdx.x * 4; i < ev; i += 256 * 4) {
+        float4 p = *(float4*)(P + i), v = *(float4*)(VEL + i);
+        float g[4];
+        if (gdt == kF32) {
+          float4 gg = *(const float4*)((const float*)G + i);
+          g[0] = gg.x; g[1] = gg.y; g[2] = gg.z; g[3] = gg.w;
+        } else {
+          uint2 gg = *(const uint2*)((const uint16_t*)G + i);
+          if (gdt == kBF16) { g[0] = lo_bf16(gg.x); g[1] = hi_bf16(gg.x); g[2] = lo_bf16(gg.y); g[3] = hi_bf16(gg.y); }
+          else { g[0] = lo_f16(gg.x); g[1] = hi_f16(gg.x); g[2] = lo_f16(gg.y); g[3] = hi_f16(gg.y); }
+        }
+        float pa_[4] = {p.x, p.y, p.z, p.w}, va[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float gj = g[j] * gs + wd * pa_[j];
+          va[j] = mu * va[j] + gj;
+          pa_[j] -= plr * (nesterov ? gj + mu * va[j] : va[j]);
+        }
+        *(float4*)(P + i) = make_float4(pa_[0], pa_[1], pa_[2], pa_[3]);
+        *(float4*)(VEL + i) = make_float4(va[0], va[1], va[2], va[3]);
+        if (ldt == kBF16) {
+          *(uint2*)((uint16_t*)LP + i) = make_uint2(pack_bf16(pa_[0], pa_[1]), pack_bf16(pa_[2], pa_[3]));
+        } else if (ldt == kF16) {
+          *(uint2*)((uint16_t*)LP + i) = make_uint2(pack_f16(pa_[0], pa_[1]), pack_f16(pa_[2], pa_[3]));
+        } else if (ldt == kF32) {
+          *(float4*)((float*)LP + i) = make_float4(pa_[0], pa_[1], pa_[2], pa_[3]);
+        }
+      }
+      i0 = ev;
+    }
+    for (int64_t i = i0 + threadIdx.x; i < e; i += 256) {
+      const float p = P[i];
+      const float gj = ld_any(G, i, gdt) * gs + wd * p;
+      const float v = mu * VEL[i] + gj;
+      const float np = p - plr * (nesterov ? gj + mu * v : v);
+      VEL[i] = v; P[i] = np;
+      if (ldt != 3) st_any(LP, i, ldt, np);
+    }
+  }
+}
+
 }  // namespace
 
 PA_EXPORT int pa_adamw_multi(const int64_t* table, const int64_t* items, int64_t n_items, const float* inv_scale,
@@ -153,10 +220,20 @@ PA_EXPORT int pa_adamw_multi(const int64_t* table, const int64_t* items, int64_t
 // partial must hold 1024 floats; caller sums it.
 PA_EXPORT int pa_sq_norm_multi(const int64_t* table, const int64_t* items, int64_t n_items, float* partial,
                                hipStream_t st) {
-  hipMemsetAsync(partial, 0, 1024 * sizeof(float), st);
+  (void)hipMemsetAsync(partial, 0, 1024 * sizeof(float), st);
   if (n_items <= 0) return 0;
   int64_t g = n_items < 1024 ? n_items : 1024;
   hipLaunchKernelGGL(sq_norm_multi_k, dim3((unsigned)g), dim3(256), 0, st, table, items, n_items, partial);
+  PA_CHECK_LAUNCH();
+  return 0;
+}
+
+PA_EXPORT int pa_momentum_multi(const int64_t* table, const int64_t* items, int64_t n_items, const float* inv_scale,
+                                float lr, float mu, float rescale, int nesterov, hipStream_t st) {
+  if (n_items <= 0) return 0;
+  int64_t g = n_items < 4096 ? n_items : 4096;
+  hipLaunchKernelGGL(momentum_multi_k, dim3((unsigned)g), dim3(256), 0, st, table, items, n_items, inv_scale, lr, mu,
+                     rescale, nesterov);
   PA_CHECK_LAUNCH();
   return 0;
 }

@@ -1,0 +1,365 @@
+// Batch norm over channels-last (NHWC / [rows, C]) activations with the activation and residual add
+// fused in, for gfx950. Reference behaviour: paddle/phi/kernels/gpu/batch_norm_kernel.cu (training
+// statistics, biased variance in the running average with factor 1 - momentum),
+// batch_norm_grad_kernel.cu, and fusion/gpu/fused_bn_add_activation (bn + add + relu).
+//
+// A ResNet BN layer is three HBM passes in each direction, so the design is purely about bytes:
+//   fwd: stats (read x) -> tiny finalize -> apply (read x [+ residual], write y = act(bn(x) [+ r]))
+//   bwd: reduce (read dy, x [, y for the relu mask]) -> tiny finalize -> apply (read dy, x [, y],
+//        write dx [and d_residual = masked dy])
+// The relu mask is recomputed from the saved output y (the next conv keeps y alive anyway), so no
+// mask tensor is stored and the separate relu / add kernels disappear.
+//
+// Reductions are channel-parallel: a workgroup owns CB channels (8 per lane, one 16-byte load) and a
+// contiguous row range; lanes along the rows keep fp32 partials, folded through LDS into per-(row
+// chunk, channel) partials; the finalize kernel folds the chunks in fp64.
+#include "common.h"
+
+using namespace pa;
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ void ld8(const uint16_t* p, float* f) { load8<bf16>(reinterpret_cast<const bf16*>(p), f); }
+__device__ __forceinline__ void st8(uint16_t* p, const float* f) { store8<bf16>(reinterpret_cast<bf16*>(p), f); }
+
+// MODE 0: acc1 = sum x, acc2 = sum x^2.
+// MODE 1: dyp = relu ? (y > 0 ? dy : 0) : dy; acc1 = sum dyp, acc2 = sum dyp * (x - mean).
+template <int MODE, bool RELU>
+__global__ __launch_bounds__(kThreads) void bn_reduce_k(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+                                                        const uint16_t* __restrict__ y, const float* __restrict__ mean,
+                                                        float* __restrict__ partial, int64_t R, int C, int CB,
+                                                        int64_t rows_per_chunk) {
+  const int tcx = CB >> 3;               // lanes along channels
+  const int rpi = kThreads / tcx;        // rows per iteration
+  const int tx = threadIdx.x % tcx, ty = threadIdx.x / tcx;
+  const int c0 = blockIdx.x * CB + tx * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
+  const int64_t r1 = min(R, r0 + rows_per_chunk);
+  float a1[8], a2[8], mu[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { a1[j] = 0.f; a2[j] = 0.f; mu[j] = 0.f; }
+  if (MODE == 1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mu[j] = mean[c0 + j];
+  }
+  // U rows per trip keep U 16-byte loads per tensor in flight (the stats pass reads one tensor)
+  constexpr int U = MODE == 0 ? 4 : 2;
+  int64_t r = r0 + ty;
+  for (; r + (U - 1) * rpi < r1; r += U * rpi) {
+    float xs[U][8], gs[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u) ld8(x + (r + u * rpi) * C + c0, xs[u]);
+    if (MODE == 1) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) ld8(dy + (r + u * rpi) * C + c0, gs[u]);
+      if (RELU) {
+        float ys[U][8];
+#pragma unroll
+        for (int u = 0; u < U; ++u) ld8(y + (r + u * rpi) * C + c0, ys[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) gs[u][j] = ys[u][j] > 0.f ? gs[u][j] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (MODE == 0) {
+          a1[j] += xs[u][j];
+          a2[j] += xs[u][j] * xs[u][j];
+        } else {
+          a1[j] += gs[u][j];
+          a2[j] += gs[u][j] * (xs[u][j] - mu[j]);
+        }
+      }
+  }
+  for (; r < r1; r += rpi) {
+    float xa[8];
+    ld8(x + r * C + c0, xa);
+    if (MODE == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { a1[j] += xa[j]; a2[j] += xa[j] * xa[j]; }
+    } else {
+      float ga[8];
+      ld8(dy + r * C + c0, ga);
+      if (RELU) {
+        float ya[8];
+        ld8(y + r * C + c0, ya);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ga[j] = ya[j] > 0.f ? ga[j] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { a1[j] += ga[j]; a2[j] += ga[j] * (xa[j] - mu[j]); }
+    }
+  }
+  // fold the rpi row-lanes: sm[ty][channel] for each accumulator
+  __shared__ float sm[2][kThreads * 8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sm[0][ty * CB + tx * 8 + j] = a1[j];
+    sm[1][ty * CB + tx * 8 + j] = a2[j];
+  }
+  __syncthreads();
+  for (int cc = threadIdx.x; cc < 2 * CB; cc += kThreads) {
+    const int which = cc / CB, c = cc % CB;
+    float s = 0.f;
+    for (int t = 0; t < rpi; ++t) s += sm[which][t * CB + c];
+    partial[((int64_t)which * gridDim.y + blockIdx.y) * C + blockIdx.x * CB + c] = s;
+  }
+}
+
+// fold the chunk partials of 64 channels per 1024-thread block: lane (c, k) sums chunks k, k+16, ...
+// (8 independent loads per trip — the fold is latency-bound, not bandwidth-bound) in fp64, then the
+// 16 chunk-lanes combine through LDS. Result valid in threads with k == 0.
+constexpr int kFoldLanes = 16;
+__device__ __forceinline__ bool fold_chunks(const float* __restrict__ partial, int chunks, int C, double* s1,
+                                            double* s2, int* c_out) {
+  __shared__ double sm1[kFoldLanes][64], sm2[kFoldLanes][64];
+  const int cl = threadIdx.x & 63, k = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    const float* p1 = partial + c;
+    const float* p2 = partial + (int64_t)chunks * C + c;
+    int j = k;
+    for (; j + 7 * kFoldLanes < chunks; j += 8 * kFoldLanes) {
+      float u[8], v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        u[q] = p1[(int64_t)(j + q * kFoldLanes) * C];
+        v[q] = p2[(int64_t)(j + q * kFoldLanes) * C];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) { a += u[q]; b += v[q]; }
+    }
+    for (; j < chunks; j += kFoldLanes) {
+      a += p1[(int64_t)j * C];
+      b += p2[(int64_t)j * C];
+    }
+  }
+  sm1[k][cl] = a;
+  sm2[k][cl] = b;
+  __syncthreads();
+  double t1 = 0.0, t2 = 0.0;
+  if (k == 0) {
+#pragma unroll
+    for (int q = 0; q < kFoldLanes; ++q) { t1 += sm1[q][cl]; t2 += sm2[q][cl]; }
+  }
+  *s1 = t1;
+  *s2 = t2;
+  *c_out = c;
+  return k == 0 && c < C;
+}
+
+// forward finalize: batch mean / rstd, running stats, fused scale / shift
+__global__ __launch_bounds__(1024) void bn_fwd_finalize_k(const float* __restrict__ partial, int chunks, int C, int64_t R,
+                                                         const float* __restrict__ w, const float* __restrict__ b,
+                                                         float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                         float momentum, float eps, float* __restrict__ save_mean,
+                                                         float* __restrict__ save_rstd, float* __restrict__ ss) {
+  double s1, s2;
+  int c;
+  if (!fold_chunks(partial, chunks, C, &s1, &s2, &c)) return;
+  const double m = s1 / (double)R;
+  double var = s2 / (double)R - m * m;
+  var = var > 0.0 ? var : 0.0;
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  save_mean[c] = (float)m;
+  save_rstd[c] = rstd;
+  if (run_mean) run_mean[c] = momentum * run_mean[c] + (1.f - momentum) * (float)m;
+  if (run_var) run_var[c] = momentum * run_var[c] + (1.f - momentum) * (float)var;
+  const float sc = (w ? w[c] : 1.f) * rstd;
+  ss[c] = sc;
+  ss[C + c] = (b ? b[c] : 0.f) - (float)m * sc;
+}
+
+// backward finalize: dweight / dbias and the per-channel dx coefficients
+//   dx = a * dyp - bc * x + d0 with a = w * rstd, bc = a * rstd^2 * sum(dyp (x - mean)) / R,
+//   d0 = bc * mean - a * sum(dyp) / R   (use_global_stats: bc = 0, d0 = 0)
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float* __restrict__ partial, int chunks, int C, int64_t R,
+                                                         const float* __restrict__ w, const float* __restrict__ mean,
+                                                         const float* __restrict__ rstd, float* __restrict__ dw,
+                                                         float* __restrict__ db, float* __restrict__ coef,
+                                                         int global_stats) {
+  double s1, s2;
+  int c;
+  if (!fold_chunks(partial, chunks, C, &s1, &s2, &c)) return;
+  const float rs = rstd[c];
+  if (dw) dw[c] = (float)s2 * rs;
+  if (db) db[c] = (float)s1;
+  const float a = (w ? w[c] : 1.f) * rs;
+  float bc = 0.f, d0 = 0.f;
+  if (!global_stats) {
+    bc = (float)((double)a * rs * rs * s2 / (double)R);
+    d0 = bc * mean[c] - (float)((double)a * s1 / (double)R);
+  }
+  coef[c] = a;
+  coef[C + c] = bc;
+  coef[2 * C + c] = d0;
+}
+
+// y = act(x * scale + shift [+ res])
+template <bool RELU, bool RES>
+__global__ __launch_bounds__(kThreads) void bn_apply_k(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
+                                                       const float* __restrict__ ss, uint16_t* __restrict__ y,
+                                                       int64_t nvec, int C) {
+  const int cv = C >> 3;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * kThreads) {
+    const int c0 = (int)(i % cv) * 8;
+    float f[8], r[8];
+    ld8(x + i * 8, f);
+    if (RES) ld8(res + i * 8, r);
+    const float4 s0 = *reinterpret_cast<const float4*>(ss + c0), s1 = *reinterpret_cast<const float4*>(ss + c0 + 4);
+    const float4 h0 = *reinterpret_cast<const float4*>(ss + C + c0), h1 = *reinterpret_cast<const float4*>(ss + C + c0 + 4);
+    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = f[j] * sc[j] + sh[j];
+      if (RES) v += r[j];
+      if (RELU) v = fmaxf(v, 0.f);
+      f[j] = v;
+    }
+    st8(y + i * 8, f);
+  }
+}
+
+// dx = a * dyp - bc * x + d0; dres = dyp
+template <bool RELU, bool DRES>
+__global__ __launch_bounds__(kThreads) void bn_bwd_apply_k(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+                                                           const uint16_t* __restrict__ y, const float* __restrict__ coef,
+                                                           uint16_t* __restrict__ dx, uint16_t* __restrict__ dres,
+                                                           int64_t nvec, int C) {
+  const int cv = C >> 3;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * kThreads) {
+    const int c0 = (int)(i % cv) * 8;
+    float g[8], f[8];
+    ld8(dy + i * 8, g);
+    ld8(x + i * 8, f);
+    if (RELU) {
+      float yy[8];
+      ld8(y + i * 8, yy);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = yy[j] > 0.f ? g[j] : 0.f;
+    }
+    if (DRES) st8(dres + i * 8, g);
+    float a[8], bc[8], d0[8], o[8];
+    load8<float>(coef + c0, a);
+    load8<float>(coef + C + c0, bc);
+    load8<float>(coef + 2 * C + c0, d0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = a[j] * g[j] - bc[j] * f[j] + d0[j];
+    st8(dx + i * 8, o);
+  }
+}
+
+int pick_cb(int C) {
+  if (C % 512 == 0) return 512;
+  if (C % 256 == 0) return 256;
+  if (C % 128 == 0) return 128;
+  if (C % 64 == 0) return 64;
+  if (C % 32 == 0) return 32;
+  if (C % 16 == 0) return 16;
+  return 8;
+}
+
+// row chunking: ~512 workgroups over the chip (2 per CU, each lane with two 16-byte loads in
+// flight per tensor), each at least 8 row-iterations deep; fewer chunks keep the fold cheap
+void plan(int64_t R, int C, int* CB, int* chunks, int64_t* rows_per_chunk) {
+  *CB = pick_cb(C);
+  const int rpi = kThreads / (*CB / 8);
+  const int gx = C / *CB;
+  int64_t want = 512 / gx;
+  if (want < 1) want = 1;
+  int64_t rpc = (R + want - 1) / want;
+  const int64_t min_rows = 8 * rpi;
+  if (rpc < min_rows) rpc = min_rows;
+  rpc = (rpc + rpi - 1) / rpi * rpi;
+  *rows_per_chunk = rpc;
+  *chunks = (int)((R + rpc - 1) / rpc);
+}
+
+unsigned apply_grid(int64_t nvec) {
+  int64_t g = (nvec + kThreads * 4 - 1) / (kThreads * 4);
+  if (g > 8192) g = 8192;
+  return (unsigned)(g < 1 ? 1 : g);
+}
+
+}  // namespace
+
+// Number of row chunks (partial workspace = 2 * chunks * C floats) for a reduction over [R, C].
+PA_EXPORT int pa_bn_chunks(int64_t R, int C) {
+  int CB, chunks;
+  int64_t rpc;
+  plan(R, C, &CB, &chunks, &rpc);
+  return chunks;
+}
+
+// Training forward. x, res, y: [R, C] bf16 (res may be null); w, b, run_mean, run_var fp32 [C] (any
+// may be null); partial: 2 * chunks * C fp32; save_mean, save_rstd: [C]; ss: [2, C] scale / shift.
+// training = 0: save_mean / save_rstd are inputs (running stats already turned into mean / rstd).
+PA_EXPORT int pa_bn_fwd_nhwc(const void* x, const void* res, void* y, const float* w, const float* b, float* run_mean,
+                             float* run_var, float* save_mean, float* save_rstd, float* partial, float* ss, int64_t R,
+                             int C, float momentum, float eps, int relu, int training, hipStream_t st) {
+  if (C % 8 != 0 || R < 1) return 3;
+  int CB, chunks;
+  int64_t rpc;
+  plan(R, C, &CB, &chunks, &rpc);
+  if (training) {
+    hipLaunchKernelGGL((bn_reduce_k<0, false>), dim3(C / CB, chunks), dim3(kThreads), 0, st, (const uint16_t*)x,
+                       nullptr, nullptr, nullptr, partial, R, C, CB, rpc);
+    PA_CHECK_LAUNCH();
+    hipLaunchKernelGGL(bn_fwd_finalize_k, dim3((C + 63) / 64), dim3(1024), 0, st, partial, chunks, C, R, w, b,
+                       run_mean, run_var, momentum, eps, save_mean, save_rstd, ss);
+    PA_CHECK_LAUNCH();
+  }
+  const int64_t nvec = R * C / 8;
+  const unsigned g = apply_grid(nvec);
+#define PA_BN_APPLY(RL, RS)                                                                                      \
+  hipLaunchKernelGGL((bn_apply_k<RL, RS>), dim3(g), dim3(kThreads), 0, st, (const uint16_t*)x, (const uint16_t*)res, \
+                     ss, (uint16_t*)y, nvec, C)
+  if (relu && res) PA_BN_APPLY(true, true);
+  else if (relu) PA_BN_APPLY(true, false);
+  else if (res) PA_BN_APPLY(false, true);
+  else PA_BN_APPLY(false, false);
+#undef PA_BN_APPLY
+  PA_CHECK_LAUNCH();
+  return 0;
+}
+
+// Backward. dy, x, y: [R, C] bf16 (y only read when relu); dx out; dres out (null: no residual
+// gradient); dw, db fp32 [C] out (nullable); coef: [3, C] workspace; partial: 2 * chunks * C.
+PA_EXPORT int pa_bn_bwd_nhwc(const void* dy, const void* x, const void* y, void* dx, void* dres, const float* w,
+                             const float* mean, const float* rstd, float* dw, float* db, float* partial, float* coef,
+                             int64_t R, int C, int relu, int global_stats, hipStream_t st) {
+  if (C % 8 != 0 || R < 1) return 3;
+  int CB, chunks;
+  int64_t rpc;
+  plan(R, C, &CB, &chunks, &rpc);
+  if (relu)
+    hipLaunchKernelGGL((bn_reduce_k<1, true>), dim3(C / CB, chunks), dim3(kThreads), 0, st, (const uint16_t*)x,
+                       (const uint16_t*)dy, (const uint16_t*)y, mean, partial, R, C, CB, rpc);
+  else
+    hipLaunchKernelGGL((bn_reduce_k<1, false>), dim3(C / CB, chunks), dim3(kThreads), 0, st, (const uint16_t*)x,
+                       (const uint16_t*)dy, nullptr, mean, partial, R, C, CB, rpc);
+  PA_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_bwd_finalize_k, dim3((C + 63) / 64), dim3(1024), 0, st, partial, chunks, C, R, w, mean, rstd,
+                     dw, db, coef, global_stats);
+  PA_CHECK_LAUNCH();
+  const int64_t nvec = R * C / 8;
+  const unsigned g = apply_grid(nvec);
+#define PA_BN_BWD(RL, DR)                                                                                         \
+  hipLaunchKernelGGL((bn_bwd_apply_k<RL, DR>), dim3(g), dim3(kThreads), 0, st, (const uint16_t*)dy,                \
+                     (const uint16_t*)x, (const uint16_t*)y, coef, (uint16_t*)dx, (uint16_t*)dres, nvec, C)
+  if (relu && dres) PA_BN_BWD(true, true);
+  else if (relu) PA_BN_BWD(true, false);
+  else if (dres) PA_BN_BWD(false, true);
+  else PA_BN_BWD(false, false);
+#undef PA_BN_BWD
+  PA_CHECK_LAUNCH();
+  return 0;
+}

@@ -32,19 +32,42 @@ def rms_norm(x, normalized_shape=None, weight=None, epsilon=1e-6, name=None):
 
 def batch_norm(x, running_mean, running_var, weight=None, bias=None, training=False, momentum=0.9,
                epsilon=1e-05, data_format="NCHW", use_global_stats=None, name=None):
+    return fused_bn_act(x, running_mean, running_var, weight, bias, training, momentum, epsilon, data_format,
+                        use_global_stats)
+
+
+def fused_bn_act(x, running_mean, running_var, weight=None, bias=None, training=False, momentum=0.9,
+                 epsilon=1e-05, data_format="NCHW", use_global_stats=None, act=None, residual=None):
+    """act(batch_norm(x) [+ residual]) — batch_norm with the fused_bn_add_activation epilogue
+    (reference: python/paddle/incubate/layers/nn.py:1092). Channels-last bf16 input runs the HIP
+    kernels of csrc/kernels/bn.hip (ops.batch_norm_act_nhwc); other layouts / dtypes run torch.
+    Running statistics follow the reference: biased batch variance, factor 1 - momentum."""
     t = T(x)
     cl = data_format in ("NHWC", "NLC", "NDHWC")
-    nd = t.dim()
-    if cl:
-        t = t.permute(0, nd - 1, *range(1, nd - 1))
     use_batch = training and not use_global_stats
     rm, rv = T(running_mean), T(running_var)
     w, b = T(weight), T(bias)
+    r = T(residual)
+    if cl and t.dim() >= 2:
+        return _wrap(_ops.batch_norm_act_nhwc(t, w, b, rm, rv, use_batch, momentum, epsilon, act, r))
+    nd = t.dim()
     if t.dtype in (torch.float16, torch.bfloat16) and w is not None and w.dtype != torch.float32:
         w, b = w.float(), b.float() if b is not None else None
-    out = F.batch_norm(t, rm, rv, w, b, use_batch, 1.0 - momentum, epsilon)
-    if cl:
-        out = out.permute(0, *range(2, nd), 1)
+    if use_batch and rm is not None:
+        red = [0] + list(range(2, nd))
+        with torch.no_grad():
+            var, mean = torch.var_mean(t.detach().float(), red, unbiased=False)
+            rm.mul_(momentum).add_((1.0 - momentum) * mean.to(rm.dtype))
+            rv.mul_(momentum).add_((1.0 - momentum) * var.to(rv.dtype))
+        out = F.batch_norm(t, None, None, w, b, True, 0.0, epsilon)
+    else:
+        out = F.batch_norm(t, rm, rv, w, b, use_batch, 1.0 - momentum, epsilon)
+    if r is not None:
+        out = out + r
+    if act == "relu":
+        out = torch.relu(out)
+    elif act is not None:
+        out = getattr(F, act)(out)
     return _wrap(out)
 
 

@@ -38,6 +38,19 @@ class _BatchNormBase(Layer):
         return F.batch_norm(x, self._mean, self._variance, self.weight, self.bias, self.training, self._momentum,
                             self._epsilon, self._data_format, self._use_global_stats)
 
+    def fused_forward(self, x, act=None, residual=None):
+        """act(self(x) [+ residual]) in one fused pass where the layer is a plain batch norm
+        (fused_bn_add_activation, F.fused_bn_act); layers that override forward (SyncBatchNorm,
+        legacy BatchNorm with its own act) compose the ops instead."""
+        if type(self).forward is _BatchNormBase.forward:
+            return F.fused_bn_act(x, self._mean, self._variance, self.weight, self.bias, self.training,
+                                  self._momentum, self._epsilon, self._data_format, self._use_global_stats, act,
+                                  residual)
+        y = self(x)
+        if residual is not None:
+            y = y + residual
+        return getattr(F, act)(y) if act else y
+
     def extra_repr(self):
         return f"num_features={self._num_features}, momentum={self._momentum}, epsilon={self._epsilon}"
 

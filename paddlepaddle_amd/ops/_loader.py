@@ -96,6 +96,7 @@ def _declare(L):
         "pa_adamw_multi": [_vp, _vp, _i64, _vp, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _vp, _vp],
         "pa_sq_norm_multi": [_vp, _vp, _i64, _vp, _vp],
         "pa_scale_multi": [_vp, _i64, _vp, _vp],
+        "pa_momentum_multi": [_vp, _vp, _i64, _vp, _f32, _f32, _f32, _i32, _vp],
         # attention
         "pa_flash_attn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _f32, _i32, _vp],
         "pa_flash_attn_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
@@ -107,11 +108,10 @@ def _declare(L):
         "pa_bias_gelu_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp],
         "pa_dropout_add_fwd": [_vp, _vp, _vp, _i64, _f32, ctypes.c_uint64, _i32, _vp],
         "pa_dropout_bwd": [_vp, _vp, _i64, _f32, ctypes.c_uint64, _i32, _vp],
-        # gemm
-        "pa_gemm_bf16": [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp],
         # batch norm (NHWC)
-        "pa_bn_fwd_nhwc": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _f32, _f32, _i32, _i32, _vp],
-        "pa_bn_bwd_nhwc": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _i32, _vp],
+        "pa_bn_chunks": [_i64, _i32],
+        "pa_bn_fwd_nhwc": [_vp] * 11 + [_i64, _i32, _f32, _f32, _i32, _i32, _vp],
+        "pa_bn_bwd_nhwc": [_vp] * 12 + [_i64, _i32, _i32, _i32, _vp],
         "pa_version": [],
     }
     for name, args in sigs.items():

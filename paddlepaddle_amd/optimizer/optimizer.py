@@ -170,13 +170,17 @@ class Optimizer:
         ps = [p for p in self._parameter_list if p._t.grad is not None]
         clip._clip_inplace(ps)
 
-    def _regularized_grad(self, p, g, group):
+    def _regularizer_for(self, p, group):
         reg = getattr(p, "regularizer", None) or group.get("weight_decay_obj", None) or self.regularization
         if "weight_decay" in group and not isinstance(group["weight_decay"], (L1Decay, L2Decay)):
             wd = group["weight_decay"]
             reg = L2Decay(wd) if wd else None
         elif "weight_decay" in group:
             reg = group["weight_decay"]
+        return reg
+
+    def _regularized_grad(self, p, g, group):
+        reg = self._regularizer_for(p, group)
         if reg is None:
             return g
         return reg(p._t.detach().to(g.dtype), g)

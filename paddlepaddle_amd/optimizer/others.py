@@ -45,6 +45,58 @@ class Momentum(_PerParam):
         super().__init__(learning_rate, parameters, weight_decay, grad_clip, name, multi_precision)
         self._momentum, self._nesterov, self._rescale = momentum, use_nesterov, rescale_grad
 
+    def _update_group(self, group, params):
+        """On a HIP device every fp32 (or fp32-master) parameter of the group is updated by one
+        multi-tensor launch (csrc/kernels/adamw.hip momentum_multi_k): L2 decay, velocity, the
+        parameter and its bf16 shadow in one pass. Others take the per-tensor path."""
+        from ..ops import _loader as L
+        fused, rest = [], []
+        if L.hip_enabled_for(params[0]._t) and L.has("pa_momentum_multi"):
+            for p in params:
+                reg = self._regularizer_for(p, group)
+                ok_reg = reg is None or type(reg).__name__ == "L2Decay"
+                ok_dt = p._t.dtype == torch.float32 or self._multi_precision
+                (fused if ok_reg and ok_dt and p._t.grad.dtype in L._DT else rest).append(p)
+        else:
+            rest = params
+        if fused:
+            self._fused(group, fused)
+        for p in rest:
+            self._update_param(group, p)
+
+    def _fused(self, group, params):
+        from ..ops import _loader as L
+        from ..ops import optim as _opt
+        from .adam import _f2i
+        masters = [self._master(p) for p in params]
+        fp32 = [m if m is not None else p._t.detach() for p, m in zip(params, masters)]
+        grads = [p._t.grad for p in params]
+        key = (tuple(t.data_ptr() for t in fp32), tuple(g.data_ptr() for g in grads))
+        tabs = self.__dict__.setdefault("_mt_tables", {})
+        tab = tabs.get(id(group))
+        if tab is None or tab[0] != key:
+            rows, items = [], []
+            for i, (w, g, m, p) in enumerate(zip(fp32, grads, masters, params)):
+                vel = self._acc("velocity", p)
+                reg = self._regularizer_for(p, group)
+                lr_mult = p.optimize_attr.get("learning_rate", 1.0) if hasattr(p, "optimize_attr") else 1.0
+                ldt = 3 if m is None else L._DT[p._t.dtype]
+                rows.append([w.data_ptr(), g.data_ptr(), vel.data_ptr(), 0, 0 if m is None else p._t.data_ptr(),
+                             w.numel(), L._DT[g.dtype] | (ldt << 8), _f2i(reg._coeff if reg is not None else 0.0),
+                             _f2i(lr_mult)])
+                for s0 in range(0, w.numel(), _opt._CHUNK):
+                    items.append([i, s0])
+            dev = fp32[0].device
+            tab = (key, torch.tensor(rows, dtype=torch.int64).to(dev, non_blocking=True),
+                   torch.tensor(items, dtype=torch.int64).to(dev, non_blocking=True), len(items), fp32, grads)
+            tabs[id(group)] = tab
+        _, t_rows, t_items, n_items, _, _ = tab
+        lr = self._group_lr(group, None)
+        mu = group.get("momentum", self._momentum)
+        L.call("pa_momentum_multi", L.ptr(t_rows), L.ptr(t_items), n_items,
+               L.ptr(getattr(self, "_inv_scale_tensor", None)), float(lr), float(mu), float(self._rescale),
+               int(bool(self._nesterov)), L.stream_ptr())
+
     def _update_param(self, group, p):
         master, w, g, lr = self._prep(group, p)
         g = g.to(w.dtype) * self._rescale

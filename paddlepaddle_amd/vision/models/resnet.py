@@ -8,6 +8,18 @@ from __future__ import annotations
 from ... import nn
 
 
+def _bn_act(bn, x, act="relu", residual=None):
+    """bn(x) [+ residual] -> act as one fused pass (fused_bn_add_activation) when the norm layer
+    supports it; any other norm layer composes the ops."""
+    f = getattr(bn, "fused_forward", None)
+    if f is not None:
+        return f(x, act, residual)
+    y = bn(x)
+    if residual is not None:
+        y = y + residual
+    return nn.functional.relu(y) if act == "relu" else y
+
+
 class BasicBlock(nn.Layer):
     expansion = 1
 
@@ -26,11 +38,10 @@ class BasicBlock(nn.Layer):
 
     def forward(self, x):
         identity = x
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
+        out = _bn_act(self.bn1, self.conv1(x))
         if self.downsample is not None:
             identity = self.downsample(x)
-        return self.relu(out + identity)
+        return _bn_act(self.bn2, self.conv2(out), "relu", identity)
 
 
 class BottleneckBlock(nn.Layer):
@@ -54,12 +65,11 @@ class BottleneckBlock(nn.Layer):
 
     def forward(self, x):
         identity = x
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
+        out = _bn_act(self.bn1, self.conv1(x))
+        out = _bn_act(self.bn2, self.conv2(out))
         if self.downsample is not None:
             identity = self.downsample(x)
-        return self.relu(out + identity)
+        return _bn_act(self.bn3, self.conv3(out), "relu", identity)
 
 
 class ResNet(nn.Layer):
@@ -103,7 +113,7 @@ class ResNet(nn.Layer):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(_bn_act(self.bn1, self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         if self.with_pool:
             x = self.avgpool(x)

@@ -11,11 +11,12 @@ import os
 import re
 
 CATS = [
+    ("bn/bn+relu(+add) (HIP)", re.compile(r"bn_(reduce|apply|bwd_apply|fwd_finalize|bwd_finalize)_k")),
     ("miopen/ck(conv/bn)", re.compile(r"miopen|igemm|naive_conv|batchnorm|grouped_conv|SubTensorOp|MIOpen", re.I)),
     ("gemm(hipBLASLt/rocBLAS)", re.compile(r"^Cijk_|^Custom_Cijk|gemm|Gemm|rocblas")),
     ("flash_attn(HIP)", re.compile(r"fa_(fwd|bwd)|fa_delta|dq_convert")),
     ("norm(HIP)", re.compile(r"norm_(fwd|bwd)|layer_?norm|rms_?norm")),
-    ("softmax/CE(HIP)", re.compile(r"softmax|xent|ce_")),
+    ("softmax/CE(HIP)", re.compile(r"softmax|xent|\bce_|_ce_")),
     ("epilogue/act/dropout(HIP)", re.compile(r"gelu|swiglu|rope|colsum|dropout|bias_")),
     ("optimizer(HIP)", re.compile(r"adamw|sq_norm|momentum")),
     ("rccl", re.compile(r"nccl|rccl|ncclDevKernel", re.I)),
