@@ -7,6 +7,7 @@ from ..framework.place import (set_device, get_device, is_compiled_with_cuda, is
                                is_compiled_with_xpu, is_compiled_with_ipu, is_compiled_with_cinn,
                                is_compiled_with_custom_device, CPUPlace, CUDAPlace)
 from . import cuda  # noqa: F401
+from . import pinned  # noqa: F401
 from .cuda import Stream, Event, current_stream, stream_guard, synchronize  # noqa: F401
 
 

@@ -311,7 +311,9 @@ class Tensor:
         return _wrap(self._t.to(dev, non_blocking=not blocking))
 
     def pin_memory(self):
-        return _wrap(self._t.pin_memory())
+        """Page-locked copy from the native pinned pool (csrc/runtime/pinned_pool.cpp)."""
+        from ..device import pinned
+        return _wrap(pinned.pin(self._t.cpu()))
 
     def to(self, *args, **kwargs):
         device = kwargs.pop("device", None)

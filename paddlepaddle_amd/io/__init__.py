@@ -2,9 +2,10 @@
 Reference: python/paddle/io/reader.py:262 (DataLoader), python/paddle/io/dataloader/*.
 
 Design: the worker pool (multiprocess, shared-memory transport) is the PyTorch-ROCm one; batch
-assembly of numpy samples into contiguous (optionally pinned) host buffers is done by the native
-C++ collator (``csrc/runtime/collate.cpp`` → ``_C_runtime``) when built, and the H2D copy is
-issued non-blocking so it overlaps the previous step's compute.
+assembly of numpy samples into contiguous host buffers is done by the native C++ collator
+(``csrc/runtime`` → ``_C_runtime``). With ``use_buffer_reader`` on a GPU the loader double-buffers:
+the next batch is staged into the native pinned pool (``csrc/runtime/pinned_pool.cpp``) and copied
+on a side HIP stream while the caller computes on the current one.
 """
 from __future__ import annotations
 
@@ -312,6 +313,31 @@ class _BS(_tud.Sampler):
         return len(self.bs)
 
 
+def _stage_batch(x, device, stream, pinned):
+    """CPU batch -> pooled pinned memory -> async copy to ``device`` on ``stream``."""
+    if isinstance(x, torch.Tensor):
+        if x.device.type != "cpu":
+            return x.to(device, non_blocking=True)
+        src = x if pinned.is_pooled(x) else pinned.pin(x)
+        return pinned.copy_to_device(src, device, stream)
+    if isinstance(x, (list, tuple)):
+        return [_stage_batch(v, device, stream, pinned) for v in x]
+    if isinstance(x, dict):
+        return {k: _stage_batch(v, device, stream, pinned) for k, v in x.items()}
+    return x
+
+
+def _record_stream(x, stream):
+    if isinstance(x, torch.Tensor):
+        x.record_stream(stream)
+    elif isinstance(x, (list, tuple)):
+        for v in x:
+            _record_stream(v, stream)
+    elif isinstance(x, dict):
+        for v in x.values():
+            _record_stream(v, stream)
+
+
 def _wrap_out(x, device, non_blocking):
     if isinstance(x, torch.Tensor):
         if device is not None and device.type == "cuda":
@@ -355,13 +381,13 @@ class DataLoader:
             tds = _TorchIterDS(dataset)
             self._loader = _tud.DataLoader(tds, batch_size=batch_size, drop_last=drop_last,
                                            collate_fn=self._collate_np, num_workers=num_workers,
-                                           pin_memory=self._pin, timeout=timeout, worker_init_fn=worker_init_fn,
+                                           pin_memory=False, timeout=timeout, worker_init_fn=worker_init_fn,
                                            prefetch_factor=prefetch_factor if num_workers > 0 else None,
                                            persistent_workers=persistent_workers and num_workers > 0)
         else:
             tds = _TorchDS(dataset)
             self._loader = _tud.DataLoader(tds, batch_sampler=_BS(self.batch_sampler), collate_fn=self._collate_np,
-                                           num_workers=num_workers, pin_memory=self._pin, timeout=timeout,
+                                           num_workers=num_workers, pin_memory=False, timeout=timeout,
                                            worker_init_fn=worker_init_fn,
                                            prefetch_factor=prefetch_factor if num_workers > 0 else None,
                                            persistent_workers=persistent_workers and num_workers > 0)
@@ -376,8 +402,40 @@ class DataLoader:
         return len(self.batch_sampler)
 
     def __iter__(self):
-        for b in self._loader:
-            yield _wrap_out(b, self._device, self._pin)
+        if not self._pin:
+            for b in self._loader:
+                yield _wrap_out(b, self._device, False)
+            return
+        # use_buffer_reader: double-buffered H2D. Batch i+1 is staged through the native pinned pool
+        # (device/pinned.py) and copied on a side stream while the caller computes on batch i.
+        from ..device import pinned as _pinned
+        dev = self._device
+        side = torch.cuda.Stream(dev)
+
+        def stage(b):
+            with torch.cuda.stream(side):
+                out = _stage_batch(b, dev, side, _pinned)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            return out, ev
+
+        def release(staged):
+            out, ev = staged
+            cur = torch.cuda.current_stream(dev)
+            cur.wait_event(ev)
+            _record_stream(out, cur)
+            return _wrap_out(out, None, False)
+
+        it = iter(self._loader)
+        try:
+            nxt = stage(next(it))
+        except StopIteration:
+            return
+        for b in it:
+            cur = nxt
+            nxt = stage(b)
+            yield release(cur)
+        yield release(nxt)
 
     def __call__(self):
         return self.__iter__()

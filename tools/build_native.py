@@ -74,7 +74,7 @@ def build_runtime(verbose=False):
     if not _newer(srcs, out):
         return out
     inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
-    _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", *inc, *srcs, "-o", out])
+    _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", *inc, *srcs, "-o", out, "-ldl"])
     if verbose:
         print(f"built {out}")
     return out
