@@ -138,6 +138,14 @@ def gpt_bench(args, paddle, world, dist_on):
     mem = torch.cuda.max_memory_allocated() / 2**30 if dev.type == "cuda" else 0.0
     log(f"[gpt] loss={float(state['loss']):.4f} step={dt / args.steps * 1000:.1f}ms tokens/s={tps:.0f} "
         f"MFU(6N model flops)={mfu * 100:.1f}% mem={mem:.1f}GiB")
+    try:
+        from paddlepaddle_amd.ops import gemm as _G
+        ch = _G.choices()
+        log(f"[gpt] GEMM backend per shape: {sum(v == 'hip' for v in ch.values())} hand-written / "
+            f"{sum(v == 'blas' for v in ch.values())} hipBLASLt: " +
+            "; ".join(f"{k[0]}{list(k[1:4])}={v}" for k, v in sorted(ch.items(), key=str)))
+    except Exception:  # pragma: no cover
+        pass
     del model, opt, ids, lbl
     if dev.type == "cuda":
         torch.cuda.empty_cache()

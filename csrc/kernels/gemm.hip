@@ -1,0 +1,541 @@
+// Hand-written bf16 GEMM with fused epilogues for gfx950 (CDNA4 MFMA).
+// Reference behaviour: paddle/phi/kernels/gpu/matmul_kernel.cu (cuBLAS) and
+// paddle/phi/kernels/fusion/gpu/fused_gemm_epilogue_kernel.cu (cublasLt bias / GELU epilogues,
+// the pre-activation "reserve space" kept for the backward).
+//
+//   C[M,N] = epilogue( A[M,K] . B[K,N] )
+//
+// Operand layouts (template): each operand is either K-major (A stored [M][K], B stored [N][K]) or
+// MN-major (A stored [K][M], B stored [K][N]); this covers the three linear-layer products
+//   forward  y  = x  . W      (A K-major, B MN-major: paddle's W is [in, out])
+//   dgrad    dx = dy . W^T    (A K-major, B K-major)
+//   wgrad    dW = x^T . dy    (A MN-major, B MN-major)
+// without any transpose copies.
+//
+// Structure (CDNA4 playbook, cdna_hip_programming.md section 5):
+//   * 256 x BN x 64 tiles, 8 waves (512 threads) as 2 (M) x 4 (N); per wave 128 x BN/4;
+//     v_mfma_f32_16x16x32_bf16, operands swapped (D = B^T-frag x A-frag) so each lane ends with
+//     4 consecutive output columns of one row -> 8/16-byte epilogue stores.
+//   * global -> LDS with global_load_lds_dwordx4 (no VGPR staging), two LDS stages (128 KiB for
+//     256x256): tile t+1 is in flight while tile t is consumed.
+//   * K-major images: [rows][64 k] with 128-B rows, 16-B chunk XOR-swizzle chunk ^ ((row>>1)&7):
+//     the ds_read_b128 of 16 rows x one chunk hits 16 distinct bank slots.
+//   * MN-major images: [64 k][R] rows, read with ds_read_b64_tr_b16 (hardware transpose) and
+//     swizzled chunk ^ 2*((k&3) | ((k>>3)&1)<<2) so each 32-lane half reads 8 distinct 32-B slots.
+//   * glds writes LDS lane-linearly, so the swizzle is applied to the per-lane GLOBAL source address
+//     and undone on the LDS read (both sides or neither).
+//   * XCD-aware bijective block remap + grouped tile order so the blocks of one XCD share A / B
+//     panels in their private L2.
+//   * epilogue: + bias[N], tanh-GELU (optionally storing the pre-activation for the backward),
+//     accumulate into an existing C (gradient-accumulation fusion), bf16 or fp32 output.
+#include "common.h"
+
+using namespace pa;
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+union Frag8 {
+  bf16x8_t v;
+  uint4 u;
+  s16x4 h[2];
+};
+
+constexpr int kBM = 256;
+constexpr int kBK = 64;
+constexpr int kThreads = 512;
+
+enum EpiFlags : int {
+  kEpiBias = 1,       // + bias[n]
+  kEpiGelu = 2,       // tanh-GELU after the bias
+  kEpiAux = 4,        // store the pre-activation (x.W + b) to aux (bf16, ldc)
+  kEpiAccum = 8,      // C += result (read-modify-write)
+  kEpiOutF32 = 16,    // C is fp32
+};
+
+struct GemmArgs {
+  const uint16_t* a;
+  const uint16_t* b;
+  void* c;
+  const uint16_t* bias;
+  uint16_t* aux;
+  int64_t lda, ldb, ldc;
+  int M, N, K;
+  int tiles_m, tiles_n;
+  int flags;
+  float alpha;
+};
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+
+// global_load_lds_dwordx4 issued from inline asm: hipcc treats a builtin LDS-DMA as a pending write to
+// every LDS object and puts s_waitcnt vmcnt(0) in front of the next ds_read, which would drain the
+// prefetch pipeline each phase. The kernels retire the DMA themselves with counted vmcnt + barrier.
+// M0 holds the wave-uniform LDS destination (lane i writes base + 16 i).
+__device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(lds_wave_base));
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
+}
+
+__device__ __forceinline__ s16x4 lds_tr(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(reinterpret_cast<uintptr_t>(p)));
+}
+
+// swizzle of an MN-major image row (even chunk XOR so 32-B pairs stay together)
+__device__ __forceinline__ int mn_swz(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
+
+// ---- staging of one operand tile (R rows of the output dimension x 64 k) into LDS
+// K-major: image [R][64] (128-B rows).  MN-major: image [64][R] (2R-byte rows).
+template <int R, bool KMAJ>
+__device__ __forceinline__ void stage(const uint16_t* __restrict__ g, int64_t ld, int r0, int rmax, int k0,
+                                      char* img, int wave, int lane) {
+  constexpr int NQ = R / 64;  // glds instructions per thread (R*64*2 bytes / (512 * 16))
+  if constexpr (KMAJ) {
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      const int q = i * 8 + wave;               // wave-instruction id: 8 rows x 128 B
+      const int row = q * 8 + (lane >> 3);
+      const int lc = (lane & 7) ^ ((row >> 1) & 7);
+      int gr = r0 + row;
+      gr = gr < rmax ? gr : rmax - 1;
+      glds16(g + (int64_t)gr * ld + k0 + lc * 8, img + q * 1024);
+    }
+  } else {
+    constexpr int CPR = R / 8;  // 16-B chunks per k-row
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      const int q = i * 8 + wave;
+      const int lin = q * 64 + lane;
+      const int row = lin / CPR;                // k
+      const int lc = (lin % CPR) ^ mn_swz(row);
+      int gc = r0 + lc * 8;
+      gc = gc < rmax ? gc : rmax - 8;
+      glds16(g + (int64_t)(k0 + row) * ld + gc, img + q * 1024);
+    }
+  }
+}
+
+// ---- fragment read: 16 rows (output dim) x 8 k for k-substep s (32 k) -> mfma operand
+template <int R, bool KMAJ>
+__device__ __forceinline__ bf16x8_t frag(const char* img, int rbase, int s, int lane) {
+  Frag8 f;
+  if constexpr (KMAJ) {
+    const int row = rbase + (lane & 15);
+    const int c = s * 4 + (lane >> 4);
+    f.u = *reinterpret_cast<const uint4*>(img + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+  } else {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+    const int col = rbase + pp * 4;           // first of 4 columns supplied by this lane
+    const int lc = col >> 3, sub = (col & 7) * 2;
+    const int k1 = s * 32 + g * 8 + q, k2 = k1 + 4;
+    f.h[0] = lds_tr(img + k1 * (R * 2) + ((lc ^ mn_swz(k1)) << 4) + sub);
+    f.h[1] = lds_tr(img + k2 * (R * 2) + ((lc ^ mn_swz(k2)) << 4) + sub);
+  }
+  return f.v;
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+template <int BN, bool AK, bool BKM>
+__global__ __launch_bounds__(kThreads, 1) void gemm_bf16_kernel(GemmArgs p) {
+  constexpr int A_BYTES = kBM * kBK * 2;
+  constexpr int B_BYTES = BN * kBK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int MR = (kBM / 2) / 16;  // 8 m-fragments per wave
+  constexpr int NR = (BN / 4) / 16;   // n-fragments per wave
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // tile order: XCD-contiguous chunks, grouped by 8 m-tiles so neighbours share B panels
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int pid = xcd_remap((int)blockIdx.x, nwg);
+  constexpr int GM = 8;
+  const int per_group = GM * p.tiles_n;
+  const int gid = pid / per_group;
+  const int first_m = gid * GM;
+  const int gsz = min(p.tiles_m - first_m, GM);
+  const int tm = first_m + (pid % per_group) % gsz;
+  const int tn = (pid % per_group) / gsz;
+  const int m0 = tm * kBM, n0 = tn * BN;
+
+  f32x4 acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K / kBK;
+  auto stage_tile = [&](int t, int buf) {
+    char* base = smem + buf * STAGE;
+    stage<kBM, AK>(p.a, p.lda, m0, p.M, t * kBK, base, wave, lane);
+    stage<BN, BKM>(p.b, p.ldb, n0, p.N, t * kBK, base + A_BYTES, wave, lane);
+  };
+
+  stage_tile(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int t = 0; t < nk; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nk) stage_tile(t + 1, cur ^ 1);
+    const char* aimg = smem + cur * STAGE;
+    const char* bimg = aimg + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8_t bf[NR];
+#pragma unroll
+      for (int j = 0; j < NR; ++j) bf[j] = frag<BN, BKM>(bimg, wn * (BN / 4) + j * 16, s, lane);
+#pragma unroll
+      for (int i = 0; i < MR; ++i) {
+        const bf16x8_t af = frag<kBM, AK>(aimg, wm * (kBM / 2) + i * 16, s, lane);
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af, acc[i][j], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds C[m = mb + i*16 + (lane&15)][n = nb + j*16 + 4*(lane>>4) + 0..3]
+  const int flags = p.flags;
+  const int mrow0 = m0 + wm * (kBM / 2) + (lane & 15);
+  const int ncol0 = n0 + wn * (BN / 4) + 4 * (lane >> 4);
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const int n = ncol0 + j * 16;
+    if (n >= p.N) continue;  // N % 4 == 0 is required by the launcher
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (flags & kEpiBias) {
+      const uint2 braw = *reinterpret_cast<const uint2*>(p.bias + n);
+      bv[0] = lo_bf16(braw.x); bv[1] = hi_bf16(braw.x); bv[2] = lo_bf16(braw.y); bv[3] = hi_bf16(braw.y);
+    }
+#pragma unroll
+    for (int i = 0; i < MR; ++i) {
+      const int m = mrow0 + i * 16;
+      if (m >= p.M) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * p.alpha + bv[e];
+      const int64_t off = (int64_t)m * p.ldc + n;
+      if (flags & kEpiAux) {
+        *reinterpret_cast<uint2*>(p.aux + off) = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
+      }
+      if (flags & kEpiGelu) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
+      }
+      if (flags & kEpiOutF32) {
+        float4* cp = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.c) + off);
+        if (flags & kEpiAccum) {
+          const float4 o = *cp;
+          v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+        }
+        *cp = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        uint2* cp = reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.c) + off);
+        if (flags & kEpiAccum) {
+          const uint2 o = *cp;
+          v[0] += lo_bf16(o.x); v[1] += hi_bf16(o.x); v[2] += lo_bf16(o.y); v[3] += hi_bf16(o.y);
+        }
+        *cp = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// 256x256x64 8-wave kernel with the 4-phase-per-K-tile interleave (cdna_hip_programming.md 5,
+// "256^2 8-phase template"): every K-tile is split into four 16-KiB half-tiles
+//   H0 = A rows 0..127, H1 = B cols 0..127, H2 = A rows 128..255, H3 = B cols 128..255
+// and each phase {ds_read a register subtile ; issue ONE half-tile of glds ; barrier ; 16 MFMA ;
+// barrier}. Reads: phase 0 H0+H1, phase 1 H3, phase 2 H2. Half-tile j (= 4 * tile + h) is issued in
+// phase j - 6, so 5-6 phases of load latency are hidden, and each read is preceded by a counted vmcnt
+// in the phase before it. The wm == 1 waves run one barrier behind the wm == 0 waves (ping-pong:
+// per SIMD one wave is in its MFMA cluster while the other reads LDS / issues glds); because of the
+// stagger a half-tile is restaged at least two phases after its last ds_read (WAR), and a read
+// happens at least one barrier after the wait that retires it in both wave groups (RAW).
+// Wave (wm, wn) owns rows {wm*64.., 128+wm*64..} x cols {wn*32.., 128+wn*32..}: the four phases
+// compute its quadrants (top,L) (top,R) (bottom,L) (bottom,R).
+__device__ __forceinline__ void bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate must be a literal)
+__device__ __forceinline__ void vm_wait(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+template <bool AK, bool BKM>
+__global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p) {
+  constexpr int HALF = 128 * kBK * 2;  // 16 KiB
+  constexpr int STAGE = 4 * HALF;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int pid = xcd_remap((int)blockIdx.x, nwg);
+  constexpr int GM = 8;
+  const int per_group = GM * p.tiles_n;
+  const int gid = pid / per_group;
+  const int first_m = gid * GM;
+  const int gsz = min(p.tiles_m - first_m, GM);
+  const int tm = first_m + (pid % per_group) % gsz;
+  const int tn = (pid % per_group) / gsz;
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int nk = p.K / kBK;
+
+  // issue half-tile j (tile j>>2, half j&3) into buffer (j>>2)&1
+  auto issue = [&](int j) {
+    const int t = j >> 2, h = j & 3;
+    char* dst = smem + (t & 1) * STAGE + h * HALF;
+    if (h == 0) stage<128, AK>(p.a, p.lda, m0, p.M, t * kBK, dst, wave, lane);
+    else if (h == 2) stage<128, AK>(p.a, p.lda, m0 + 128, p.M, t * kBK, dst, wave, lane);
+    else if (h == 1) stage<128, BKM>(p.b, p.ldb, n0, p.N, t * kBK, dst, wave, lane);
+    else stage<128, BKM>(p.b, p.ldb, n0 + 128, p.N, t * kBK, dst, wave, lane);
+  };
+
+  f32x4 acc[2][4][2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][i][b][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Half-tile j is issued in phase j - 6 (phase = 4 * tile + p). Before each phase that reads a
+  // half-tile the waves wait (in the previous phase, before its first barrier) until that half-tile
+  // is retired: vmcnt = 2 * (half-tiles issued after it).
+  const int last_j = 4 * nk - 1;
+  auto wait_for = [&](int phase, int jstar) {
+    const int issued = min(phase + 6, last_j);
+    vm_wait(2 * max(issued - jstar, 0));
+  };
+  const int npro = min(6, 4 * nk);
+#pragma unroll 1
+  for (int j = 0; j < npro; ++j) issue(j);
+  vm_wait(2 * max(min(5, last_j) - 1, 0));  // H0, H1 of tile 0
+  bar();
+  // ping-pong: the wm == 1 waves run one barrier behind, so on every SIMD one wave issues its
+  // MFMA cluster while the other does its ds_reads / glds (+1 barrier at the end for wm == 0).
+  const bool lag = __builtin_amdgcn_readfirstlane(wm) == 1;
+  if (lag) bar();
+
+  bf16x8_t af[4][2], bl[2][2], br[2][2];
+  const int ar = wm * 64, bc = wn * 32;
+
+#pragma unroll 1
+  for (int t = 0; t < nk; ++t) {
+    const char* buf = smem + (t & 1) * STAGE;
+    const int ph = 4 * t;
+    // ---- phase 0: read A-top + B-left; issue j = ph + 6; MFMA (top, L)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bl[j][ks] = frag<128, BKM>(buf + HALF, bc + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i][ks] = frag<128, AK>(buf, ar + i * 16, ks, lane);
+    }
+    if (ph + 6 <= last_j) issue(ph + 6);
+    wait_for(ph, ph + 3);  // B-right of this tile, read in phase 1
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[0][i][0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[j][ks], af[i][ks], acc[0][i][0][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // ---- phase 1: read B-right; issue j = ph + 7; MFMA (top, R)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) br[j][ks] = frag<128, BKM>(buf + 3 * HALF, bc + j * 16, ks, lane);
+    if (ph + 7 <= last_j) issue(ph + 7);
+    wait_for(ph + 1, ph + 2);  // A-bottom of this tile, read in phase 2
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[0][i][1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(br[j][ks], af[i][ks], acc[0][i][1][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // ---- phase 2: read A-bottom; issue j = ph + 8; MFMA (bottom, L)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i][ks] = frag<128, AK>(buf + 2 * HALF, ar + i * 16, ks, lane);
+    if (ph + 8 <= last_j) issue(ph + 8);
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[1][i][0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[j][ks], af[i][ks], acc[1][i][0][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // ---- phase 3: issue j = ph + 9; wait for H0/H1 of tile t+1; MFMA (bottom, R)
+    if (ph + 9 <= last_j) issue(ph + 9);
+    if (t + 1 < nk) wait_for(ph + 3, ph + 5);
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[1][i][1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(br[j][ks], af[i][ks], acc[1][i][1][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+  }
+  if (!lag) bar();
+
+  // ---- epilogue
+  const int flags = p.flags;
+#pragma unroll
+  for (int bh = 0; bh < 2; ++bh)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + bh * 128 + bc + j * 16 + 4 * (lane >> 4);
+      if (n >= p.N) continue;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (flags & kEpiBias) {
+        const uint2 braw = *reinterpret_cast<const uint2*>(p.bias + n);
+        bv[0] = lo_bf16(braw.x); bv[1] = hi_bf16(braw.x); bv[2] = lo_bf16(braw.y); bv[3] = hi_bf16(braw.y);
+      }
+#pragma unroll
+      for (int ah = 0; ah < 2; ++ah)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = m0 + ah * 128 + ar + i * 16 + (lane & 15);
+          if (m >= p.M) continue;
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[ah][i][bh][j][e] * p.alpha + bv[e];
+          const int64_t off = (int64_t)m * p.ldc + n;
+          if (flags & kEpiAux)
+            *reinterpret_cast<uint2*>(p.aux + off) = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
+          if (flags & kEpiGelu) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
+          }
+          if (flags & kEpiOutF32) {
+            float4* cp = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.c) + off);
+            if (flags & kEpiAccum) {
+              const float4 o = *cp;
+              v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+            }
+            *cp = make_float4(v[0], v[1], v[2], v[3]);
+          } else {
+            uint2* cp = reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.c) + off);
+            if (flags & kEpiAccum) {
+              const uint2 o = *cp;
+              v[0] += lo_bf16(o.x); v[1] += hi_bf16(o.x); v[2] += lo_bf16(o.y); v[3] += hi_bf16(o.y);
+            }
+            *cp = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
+          }
+        }
+    }
+}
+
+template <bool AK, bool BKM>
+int launch256(const GemmArgs& a0, hipStream_t st) {
+  GemmArgs a = a0;
+  a.tiles_m = (a.M + 255) / 256;
+  a.tiles_n = (a.N + 255) / 256;
+  const int smem = 2 * 4 * 128 * kBK * 2;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKM>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((gemm256_kernel<AK, BKM>), dim3(a.tiles_m * a.tiles_n), dim3(kThreads), smem, st, a);
+  return (int)hipGetLastError();
+}
+
+template <int BN, bool AK, bool BKM>
+int launch(const GemmArgs& a0, hipStream_t st) {
+  if constexpr (BN == 0) return launch256<AK, BKM>(a0, st);
+  GemmArgs a = a0;
+  constexpr int BNk0 = BN == 0 ? 256 : BN;
+  a.tiles_m = (a.M + kBM - 1) / kBM;
+  a.tiles_n = (a.N + BNk0 - 1) / BNk0;
+  constexpr int BNk = BN == 0 ? 256 : BN;
+  const int smem = 2 * (kBM + BNk) * kBK * 2;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)gemm_bf16_kernel<BNk, AK, BKM>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((gemm_bf16_kernel<BNk, AK, BKM>), dim3(a.tiles_m * a.tiles_n), dim3(kThreads), smem, st, a);
+  return (int)hipGetLastError();
+}
+
+template <int BN>
+int dispatch_layout(const GemmArgs& a, int a_kmajor, int b_kmajor, hipStream_t st) {
+  if (a_kmajor && !b_kmajor) return launch<BN, true, false>(a, st);
+  if (a_kmajor && b_kmajor) return launch<BN, true, true>(a, st);
+  if (!a_kmajor && !b_kmajor) return launch<BN, false, false>(a, st);
+  return launch<BN, false, true>(a, st);
+}
+
+}  // namespace
+
+// C = epi(alpha * A.B). A: [M][K] (a_kmajor) or [K][M]; B: [N][K] (b_kmajor) or [K][N].
+// Requirements (checked by the Python wrapper too): K % 64 == 0, 16-byte aligned rows
+// (lda, ldb % 8 == 0), M % 8 == 0 if A is MN-major, N % 8 == 0, ldc % 4 == 0.
+PA_EXPORT int pa_gemm_bf16(const void* a, const void* b, void* c, const void* bias, void* aux, int64_t M, int64_t N,
+                           int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor, int b_kmajor, int flags,
+                           float alpha, int bn, hipStream_t st) {
+  if (K % kBK != 0 || N % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || ldc % 4 != 0) return 1;
+  if (!a_kmajor && M % 8 != 0) return 1;
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  GemmArgs g{};
+  g.a = (const uint16_t*)a; g.b = (const uint16_t*)b; g.c = c;
+  g.bias = (const uint16_t*)bias; g.aux = (uint16_t*)aux;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.flags = flags; g.alpha = alpha;
+  // bn: 256 / 128 = two-stage kernel with 256x256 / 256x128 tiles; 1 = 4-phase ping-pong 256x256 kernel
+  if (bn == 128) return dispatch_layout<128>(g, a_kmajor, b_kmajor, st);
+  if (bn == 1) return dispatch_layout<0>(g, a_kmajor, b_kmajor, st);
+  return dispatch_layout<256>(g, a_kmajor, b_kmajor, st);
+}

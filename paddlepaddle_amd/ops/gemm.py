@@ -1,0 +1,134 @@
+"""Hand-written CDNA4 bf16 GEMM (csrc/kernels/gemm.hip) with fused epilogues.
+
+Reference: paddle/phi/kernels/gpu/matmul_kernel.cu, paddle/phi/kernels/fusion/gpu/fused_gemm_epilogue_kernel.cu.
+
+``gemm(a, b)`` takes 2-D views of any row/column-major layout (a transposed view is read in place — the
+kernel has K-major and MN-major operand paths, so ``x.t() @ dy`` needs no copy) and fuses
+``+ bias``, tanh-GELU (optionally storing the pre-activation), ``alpha`` scaling and in-place accumulation
+into an existing output (fp32 or bf16) into the GEMM epilogue.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _loader as L
+
+EPI_BIAS, EPI_GELU, EPI_AUX, EPI_ACCUM, EPI_OUT_F32 = 1, 2, 4, 8, 16
+
+
+def _layout(t, outer_dim):
+    """(ld, kmajor) of a 2-D operand whose K dimension is ``1 - outer_dim``; None if unsupported."""
+    s0, s1 = t.stride()
+    kdim = 1 - outer_dim
+    if t.stride(kdim) == 1 and t.shape[kdim] >= 1:
+        ld = t.stride(outer_dim)
+        return (ld if t.shape[outer_dim] > 1 else t.shape[kdim]), True
+    if t.stride(outer_dim) == 1:
+        ld = t.stride(kdim)
+        return (ld if t.shape[kdim] > 1 else t.shape[outer_dim]), False
+    return None
+
+
+def supported(a, b, out_dtype=None):
+    """Shape/layout/dtype conditions of the HIP kernel for C = a @ b."""
+    if a.dim() != 2 or b.dim() != 2 or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
+        return False
+    if not L.has("pa_gemm_bf16") or not L.hip_enabled_for(a):
+        return False
+    M, K = a.shape
+    N = b.shape[1]
+    if K % 64 or N % 8 or K == 0:
+        return False
+    la, lb = _layout(a, 0), _layout(b, 1)
+    if la is None or lb is None or la[0] % 8 or lb[0] % 8:
+        return False
+    if not la[1] and M % 8:
+        return False
+    if a.data_ptr() % 16 or b.data_ptr() % 16:
+        return False
+    return True
+
+
+def gemm(a, b, bias=None, gelu=False, aux=None, out=None, accumulate=False, alpha=1.0, out_dtype=None, bn=None):
+    """C = epi(alpha * a @ b). ``aux`` (bf16 [M, N]) receives the pre-activation when ``gelu``;
+    ``accumulate`` adds into ``out`` (bf16 or fp32, [M, N] contiguous rows)."""
+    M, K = a.shape
+    N = b.shape[1]
+    lda, ak = _layout(a, 0)
+    ldb, bk = _layout(b, 1)
+    if out is None:
+        out = torch.empty(M, N, dtype=out_dtype or torch.bfloat16, device=a.device)
+    assert out.stride(1) == 1 and out.stride(0) % 4 == 0
+    flags = 0
+    if bias is not None:
+        flags |= EPI_BIAS
+    if gelu:
+        flags |= EPI_GELU
+    if aux is not None:
+        flags |= EPI_AUX
+        assert aux.stride(0) == out.stride(0) and aux.dtype == torch.bfloat16
+    if accumulate:
+        flags |= EPI_ACCUM
+    if out.dtype == torch.float32:
+        flags |= EPI_OUT_F32
+    if bn is None:
+        bn = _pick_bn(M, N)
+    L.call("pa_gemm_bf16", L.ptr(a), L.ptr(b), L.ptr(out), L.ptr(bias), L.ptr(aux), M, N, K, lda, ldb, out.stride(0),
+           int(ak), int(bk), flags, float(alpha), int(bn), L.stream_ptr())
+    return out
+
+
+def _pick_bn(M, N, cus=256):
+    """Tile width: 256x256 unless the 256x128 grid fills the 256 CUs with a smaller tail."""
+    def eff(bn):
+        t = -(-M // 256) * -(-N // bn)
+        waves = -(-t // cus)
+        return t / (waves * cus) * (1.0 if bn == 256 else 0.9)
+    return 256 if eff(256) >= eff(128) else 128
+
+
+# ---------------------------------------------------------------------------------------------
+# Per-shape backend choice. For every (product, shape, layout, epilogue) key the first eager call
+# times the hand-written kernel (fused epilogue) against hipBLASLt (+ the separate epilogue pass)
+# on scratch outputs and keeps the faster one — our own TunableOp. Inside a hipGraph capture no
+# timing happens (hipBLASLt is used until the key has been tuned eagerly).
+# FLAGS_gemm_backend = "auto" (default) | "hip" | "blas" forces a side.
+_CHOICE = {}
+
+
+def _capturing():
+    try:
+        return torch.cuda.is_current_stream_capturing()
+    except Exception:  # pragma: no cover
+        return False
+
+
+def choose(key, candidates):
+    """Name of the faster entry of ``candidates`` ({name: zero-arg callable without side effects})."""
+    mode = L.flag("FLAGS_gemm_backend", "auto")
+    if mode in candidates:
+        return mode
+    ch = _CHOICE.get(key)
+    if ch is not None:
+        return ch
+    if _capturing():
+        return "blas"
+    times = {n: [] for n in candidates}
+    for fn in candidates.values():
+        fn()
+    for _ in range(3):
+        for n, fn in candidates.items():
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            fn()
+            e.record()
+            e.synchronize()
+            times[n].append(s.elapsed_time(e))
+    ch = min(times, key=lambda n: min(times[n]))
+    _CHOICE[key] = ch
+    return ch
+
+
+def choices():
+    """The tuned decisions so far: {key: backend} (for logs / profiles)."""
+    return dict(_CHOICE)

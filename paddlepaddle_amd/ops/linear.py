@@ -5,11 +5,15 @@ python/paddle/incubate/nn/functional/fused_matmul_bias.py.
 paddle's Linear weight is [in_features, out_features]: y = x @ W + b.
 
 MI355X path (one autograd node per linear):
-  forward : hipBLASLt GEMM with the bias folded into the epilogue (addmm); for GELU MLPs the
-            pre-activation h = x@W is kept and a fused HIP pass computes gelu(h + b)
-  backward: dX = dY Wᵀ and dW = Xᵀ dY on hipBLASLt; the bias gradient is a HIP column reduction
-            (csrc/kernels/linear_epi.hip: coalesced 2-D grid, fp32 partials, no atomics) and, for
-            GELU, one fused pass produces dH = dY·gelu'(h + b) together with db.
+  forward : y = x W (+b) on either the hand-written MFMA GEMM (csrc/kernels/gemm.hip: bias and
+            tanh-GELU fused into the epilogue, pre-activation stored for the backward) or hipBLASLt
+            (addmm, then a HIP bias+GELU pass) — per shape, whichever measured faster on first use
+            (ops/gemm.py choose()).
+  backward: dX = dY Wᵀ and dW = Xᵀ dY on the same per-shape choice; the hand-written kernel reads
+            the transposed operands in place (MN-major LDS images + ds_read_b64_tr_b16) and accumulates
+            dW straight into the sharding engine's grad buffer. The bias gradient is a HIP column
+            reduction (csrc/kernels/linear_epi.hip) and, for GELU, one fused pass produces
+            dH = dY·gelu'(h + b) together with db.
 """
 from __future__ import annotations
 
@@ -17,6 +21,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _loader as L
+from . import gemm as G
 from .activation import bias_gelu, gelu
 from ..framework.trace_hook import static_op
 
@@ -70,10 +75,39 @@ def _fwd_weight(w):
     return wt
 
 
-def _fwd_mm(x2, w, b=None):
+def _blas_fwd(x2, w, b=None):
     wt = _fwd_weight(w)
     wv = wt.t() if wt is not None else w
     return torch.addmm(b, x2, wv) if b is not None else torch.mm(x2, wv)
+
+
+def _fwd_mm(x2, w, b=None):
+    if G.supported(x2, w):
+        key = ("fwd", x2.shape[0], w.shape[1], x2.shape[1], b is not None)
+        ch = G.choose(key, {"blas": lambda: _blas_fwd(x2, w, b), "hip": lambda: G.gemm(x2, w, bias=b)})
+        if ch == "hip":
+            return G.gemm(x2, w, bias=b)
+    return _blas_fwd(x2, w, b)
+
+
+def _fwd_bias_gelu(x2, w, b):
+    """(y, pre, bias_for_bwd): y = gelu(x2 @ w + b); pre / bias_for_bwd feed pa_bias_gelu_bwd."""
+    if G.supported(x2, w):
+        M, N = x2.shape[0], w.shape[1]
+
+        def hip():
+            pre = torch.empty(M, N, dtype=x2.dtype, device=x2.device)
+            return G.gemm(x2, w, bias=b, gelu=True, aux=pre), pre
+
+        def blas():
+            h = _blas_fwd(x2, w)
+            return bias_gelu(h, b), h
+        ch = G.choose(("fwd_gelu", M, N, x2.shape[1]), {"blas": blas, "hip": hip})
+        if ch == "hip":
+            y, pre = hip()
+            return y, pre, torch.zeros_like(b)
+    h = _blas_fwd(x2, w)
+    return bias_gelu(h, b), h, b
 
 
 # ---------------------------------------------------------------------------------------------
@@ -107,17 +141,53 @@ def _main_grad_of(w):
     return ent
 
 
+def _dgrad(dy2, w):
+    wt = w.t()
+    if G.supported(dy2, wt):
+        key = ("dgrad", dy2.shape[0], wt.shape[1], dy2.shape[1])
+        if G.choose(key, {"blas": lambda: torch.mm(dy2, wt), "hip": lambda: G.gemm(dy2, wt)}) == "hip":
+            return G.gemm(dy2, wt)
+    return torch.mm(dy2, wt)
+
+
+def _wgrad(x2, dy2, acc=None):
+    """x2^T @ dy2, accumulated in place into ``acc`` when given (main-grad fusion)."""
+    xt = x2.t()
+    if G.supported(xt, dy2):
+        key = ("wgrad", xt.shape[0], dy2.shape[1], xt.shape[1], None if acc is None else acc.dtype)
+        if acc is None:
+            cands = {"blas": lambda: torch.mm(xt, dy2), "hip": lambda: G.gemm(xt, dy2)}
+        else:
+            scratch = []
+
+            def _s():
+                if not scratch:
+                    scratch.append(torch.zeros_like(acc))
+                return scratch[0]
+            cands = {"blas": lambda: _s().addmm_(xt, dy2),
+                     "hip": lambda: G.gemm(xt, dy2, out=_s(), accumulate=True)}
+        ch = G.choose(key, cands)
+        if ch == "hip":
+            if acc is None:
+                return G.gemm(xt, dy2)
+            G.gemm(xt, dy2, out=acc, accumulate=True)
+            return acc
+    if acc is None:
+        return torch.mm(xt, dy2)
+    return acc.addmm_(xt, dy2)
+
+
 def _mm_grads(x2, w, dy2, need_x, need_w):
-    dx = torch.mm(dy2, w.t()) if need_x else None
+    dx = _dgrad(dy2, w) if need_x else None
     dw = None
     if need_w:
         ent = _main_grad_of(w)
         if ent is not None and ent[1].dtype == dy2.dtype:
             _, buf, on_ready = ent
-            buf.addmm_(x2.t(), dy2)
+            _wgrad(x2, dy2, acc=buf)
             on_ready(w)
         else:
-            dw = torch.mm(x2.t(), dy2)
+            dw = _wgrad(x2, dy2)
     return dx, dw
 
 
@@ -152,9 +222,8 @@ class _LinearBiasGeluFn(torch.autograd.Function):
     def forward(ctx, x, w, b):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
-        h = _fwd_mm(x2, w)
-        y = bias_gelu(h, b)
-        ctx.save_for_backward(x2, w, b, h)
+        y, h, bb = _fwd_bias_gelu(x2, w, b)
+        ctx.save_for_backward(x2, w, bb, h)
         ctx.shape = shape
         return y.view(*shape[:-1], w.shape[1])
 
