@@ -476,6 +476,192 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// 256 x 160 x 64 tiles in a 3-stage LDS ring (3 x 52 KiB = 156 KiB of the 160 KiB LDS): two K-tiles
+// of glds stay in flight while one is consumed, so the global->LDS latency is hidden by two K-tiles of
+// MFMA work instead of one (PMC on the 256x256 two-stage kernel: 36 % of wave cycles waiting on
+// vmcnt / barrier). 160 columns also give whole waves of tiles on the GPT shapes (N = 5120 / 15360 /
+// 20480 -> 32 / 96 / 128 column tiles; 256x256 leaves 1.25 waves at N = 5120).
+// 8 waves as 4 (M) x 2 (N), wave tile 64 x 80 (4 x 5 MFMA fragments).
+// B images of 160 columns: K-major [160][64] (as above); MN-major [64][160] with 320-B rows, which
+// already rotate by 64 B per row, plus a 32-B XOR on rows with bit 3 set so the 8 rows of one
+// ds_read_b64_tr_b16 half-wave land on 8 distinct 32-B slots.
+constexpr int kBN3 = 160;
+
+template <int R, bool KMAJ>
+__device__ __forceinline__ void stage_r(const uint16_t* __restrict__ g, int64_t ld, int r0, int rmax, int k0,
+                                        char* img, int wave, int lane) {
+  constexpr int NI = R / 8;               // wave-instructions (1 KiB each) per operand tile
+  constexpr int PER = (NI + 7) / 8;       // per wave; the overflow slots repeat an existing instruction
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    int q = i * 8 + wave;
+    if (q >= NI) q -= 8 * PER - NI;       // same bytes to the same LDS place: a benign duplicate
+    if constexpr (KMAJ) {
+      const int row = q * 8 + (lane >> 3);
+      const int lc = (lane & 7) ^ ((row >> 1) & 7);
+      int gr = r0 + row;
+      gr = gr < rmax ? gr : rmax - 1;
+      glds16(g + (int64_t)gr * ld + k0 + lc * 8, img + q * 1024);
+    } else {
+      constexpr int CPR = R / 8;
+      const int lin = q * 64 + lane;
+      const int row = lin / CPR;
+      const int sw = (R == 160) ? (((row >> 3) & 1) << 1) : mn_swz(row);
+      const int lc = (lin % CPR) ^ sw;
+      int gc = r0 + lc * 8;
+      gc = gc < rmax ? gc : rmax - 8;
+      glds16(g + (int64_t)(k0 + row) * ld + gc, img + q * 1024);
+    }
+  }
+}
+
+template <int R, bool KMAJ>
+__device__ __forceinline__ bf16x8_t frag_r(const char* img, int rbase, int s, int lane) {
+  if constexpr (KMAJ || R != 160) {
+    return frag<R, KMAJ>(img, rbase, s, lane);
+  } else {
+    Frag8 f;
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+    const int col = rbase + pp * 4;
+    const int lc = col >> 3, sub = (col & 7) * 2;
+    const int k1 = s * 32 + g * 8 + q, k2 = k1 + 4;
+    f.h[0] = lds_tr(img + k1 * (R * 2) + ((lc ^ (((k1 >> 3) & 1) << 1)) << 4) + sub);
+    f.h[1] = lds_tr(img + k2 * (R * 2) + ((lc ^ (((k2 >> 3) & 1) << 1)) << 4) + sub);
+    return f.v;
+  }
+}
+
+template <bool AK, bool BKM>
+__global__ __launch_bounds__(kThreads, 1) void gemm3s_kernel(GemmArgs p) {
+  constexpr int BN = kBN3;
+  constexpr int A_BYTES = kBM * kBK * 2;
+  constexpr int B_BYTES = BN * kBK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int MR = 4, NR = 5;
+  constexpr int NL = (kBM / 8 + 7) / 8 + (BN / 8 + 7) / 8;  // glds per thread per K-tile (4 + 3)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int pid = xcd_remap((int)blockIdx.x, nwg);
+  constexpr int GM = 8;
+  const int per_group = GM * p.tiles_n;
+  const int gid = pid / per_group;
+  const int first_m = gid * GM;
+  const int gsz = min(p.tiles_m - first_m, GM);
+  const int tm = first_m + (pid % per_group) % gsz;
+  const int tn = (pid % per_group) / gsz;
+  const int m0 = tm * kBM, n0 = tn * BN;
+
+  f32x4 acc[MR][NR];
+#pragma unroll
+  for (int i = 0; i < MR; ++i)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K / kBK;
+  auto stage_tile = [&](int t) {
+    char* base = smem + (t % 3) * STAGE;
+    stage_r<kBM, AK>(p.a, p.lda, m0, p.M, t * kBK, base, wave, lane);
+    stage_r<BN, BKM>(p.b, p.ldb, n0, p.N, t * kBK, base + A_BYTES, wave, lane);
+  };
+
+  stage_tile(0);
+  if (nk > 1) {
+    stage_tile(1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  bar();
+
+#pragma unroll 1
+  for (int t = 0; t < nk; ++t) {
+    const bool pre = t + 2 < nk;
+    if (pre) stage_tile(t + 2);
+    const char* aimg = smem + (t % 3) * STAGE;
+    const char* bimg = aimg + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8_t bf[NR];
+#pragma unroll
+      for (int j = 0; j < NR; ++j) bf[j] = frag_r<BN, BKM>(bimg, wn * 80 + j * 16, s, lane);
+#pragma unroll
+      for (int i = 0; i < MR; ++i) {
+        const bf16x8_t af = frag_r<kBM, AK>(aimg, wm * 64 + i * 16, s, lane);
+#pragma unroll
+        for (int j = 0; j < NR; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af, acc[i][j], 0, 0, 0);
+      }
+    }
+    if (pre) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+  }
+
+  const int flags = p.flags;
+  const int mrow0 = m0 + wm * 64 + (lane & 15);
+  const int ncol0 = n0 + wn * 80 + 4 * (lane >> 4);
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const int n = ncol0 + j * 16;
+    if (n >= p.N) continue;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (flags & kEpiBias) {
+      const uint2 braw = *reinterpret_cast<const uint2*>(p.bias + n);
+      bv[0] = lo_bf16(braw.x); bv[1] = hi_bf16(braw.x); bv[2] = lo_bf16(braw.y); bv[3] = hi_bf16(braw.y);
+    }
+#pragma unroll
+    for (int i = 0; i < MR; ++i) {
+      const int m = mrow0 + i * 16;
+      if (m >= p.M) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * p.alpha + bv[e];
+      const int64_t off = (int64_t)m * p.ldc + n;
+      if (flags & kEpiAux)
+        *reinterpret_cast<uint2*>(p.aux + off) = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
+      if (flags & kEpiGelu) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
+      }
+      if (flags & kEpiOutF32) {
+        float4* cp = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.c) + off);
+        if (flags & kEpiAccum) {
+          const float4 o = *cp;
+          v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+        }
+        *cp = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        uint2* cp = reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.c) + off);
+        if (flags & kEpiAccum) {
+          const uint2 o = *cp;
+          v[0] += lo_bf16(o.x); v[1] += hi_bf16(o.x); v[2] += lo_bf16(o.y); v[3] += hi_bf16(o.y);
+        }
+        *cp = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
+      }
+    }
+  }
+}
+
+template <bool AK, bool BKM>
+int launch3s(const GemmArgs& a0, hipStream_t st) {
+  GemmArgs a = a0;
+  a.tiles_m = (a.M + kBM - 1) / kBM;
+  a.tiles_n = (a.N + kBN3 - 1) / kBN3;
+  const int smem = 3 * (kBM + kBN3) * kBK * 2;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm3s_kernel<AK, BKM>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((gemm3s_kernel<AK, BKM>), dim3(a.tiles_m * a.tiles_n), dim3(kThreads), smem, st, a);
+  return (int)hipGetLastError();
+}
+
 template <bool AK, bool BKM>
 int launch256(const GemmArgs& a0, hipStream_t st) {
   GemmArgs a = a0;
@@ -494,6 +680,7 @@ int launch256(const GemmArgs& a0, hipStream_t st) {
 template <int BN, bool AK, bool BKM>
 int launch(const GemmArgs& a0, hipStream_t st) {
   if constexpr (BN == 0) return launch256<AK, BKM>(a0, st);
+  if constexpr (BN == 160) return launch3s<AK, BKM>(a0, st);
   GemmArgs a = a0;
   constexpr int BNk0 = BN == 0 ? 256 : BN;
   a.tiles_m = (a.M + kBM - 1) / kBM;
@@ -534,7 +721,9 @@ PA_EXPORT int pa_gemm_bf16(const void* a, const void* b, void* c, const void* bi
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = (int)M; g.N = (int)N; g.K = (int)K;
   g.flags = flags; g.alpha = alpha;
-  // bn: 256 / 128 = two-stage kernel with 256x256 / 256x128 tiles; 1 = 4-phase ping-pong 256x256 kernel
+  // bn: 160 = three-stage 256x160 kernel; 256 / 128 = two-stage kernel with 256x256 / 256x128 tiles;
+  // 1 = 4-phase ping-pong 256x256 kernel
+  if (bn == 160) return dispatch_layout<160>(g, a_kmajor, b_kmajor, st);
   if (bn == 128) return dispatch_layout<128>(g, a_kmajor, b_kmajor, st);
   if (bn == 1) return dispatch_layout<0>(g, a_kmajor, b_kmajor, st);
   return dispatch_layout<256>(g, a_kmajor, b_kmajor, st);

@@ -72,14 +72,19 @@ def gemm(a, b, bias=None, gelu=False, aux=None, out=None, accumulate=False, alph
     if out.dtype == torch.float32:
         flags |= EPI_OUT_F32
     if bn is None:
-        bn = _pick_bn(M, N)
+        bn = _pick_bn(M, N, bk)
     L.call("pa_gemm_bf16", L.ptr(a), L.ptr(b), L.ptr(out), L.ptr(bias), L.ptr(aux), M, N, K, lda, ldb, out.stride(0),
            int(ak), int(bk), flags, float(alpha), int(bn), L.stream_ptr())
     return out
 
 
-def _pick_bn(M, N, cus=256):
-    """Tile width: 256x256 unless the 256x128 grid fills the 256 CUs with a smaller tail."""
+def _pick_bn(M, N, b_kmajor, cus=256):
+    """Kernel variant. Measured on MI355X (profiles/gemm_mfma_vs_hipblaslt.log): the 3-stage 256x160
+    kernel is the fastest whenever B is K-major (its 160-column MN-major image would read unaligned
+    320-B rows); otherwise the 2-stage 256x256 kernel, or 256x128 when that fills the CUs better."""
+    if b_kmajor:
+        return 160
+
     def eff(bn):
         t = -(-M // 256) * -(-N // bn)
         waves = -(-t // cus)

@@ -20,7 +20,7 @@ def timeit(fn, iters=20):
     return s.elapsed_time(e) / iters
 
 
-VARIANTS = {256: "2st-256", 128: "2st-128", 1: "pp-256"}
+VARIANTS = {160: "3s-160", 256: "2st-256", 128: "2st-128"}
 
 
 def main():
