@@ -46,19 +46,40 @@ __global__ __launch_bounds__(256) void colsum_partial_k(const T* __restrict__ x,
   store8<float>(part + (int64_t)blockIdx.y * cols + c, acc);
 }
 
+// Fold [nparts, cols] fp32 partials: a block owns 64 columns (8 x 8-column vectors) and spreads the
+// partitions over 32 row groups, then reduces the groups through LDS — cols/64 blocks instead of one
+// serial 256-deep loop per thread (which left all but ~10 CUs idle on a 20480-column bias).
 template <typename T>
 __global__ __launch_bounds__(256) void fold_partials_k(const float* __restrict__ part, T* __restrict__ out,
                                                        int64_t cols, int nparts) {
-  const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
-  if (c >= cols) return;
+  __shared__ float red[32][65];
+  const int cv = threadIdx.x & 7, rg = threadIdx.x >> 3;
+  const int64_t c = (int64_t)blockIdx.x * 64 + cv * 8;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int p = 0; p < nparts; ++p) {
-    float v[8];
-    load8<float>(part + (int64_t)p * cols + c, v);
+  if (c < cols) {
+    for (int p = rg; p < nparts; p += 32) {
+      float v[8];
+      load8<float>(part + (int64_t)p * cols + c, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += v[j];
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
   }
-  store8<T>(out + c, acc);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rg][cv * 8 + j] = acc[j];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float sum = 0.f;
+#pragma unroll 8
+    for (int g = 0; g < 32; ++g) sum += red[g][threadIdx.x];
+    red[0][threadIdx.x] = sum;
+  }
+  __syncthreads();
+  if (rg == 0 && c < cols) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = red[0][cv * 8 + j];
+    store8<T>(out + c, v);
+  }
 }
 
 // dh = dy * gelu'(h + b) ; part[p, c] += dh   (h = pre-bias GEMM output)
@@ -134,7 +155,7 @@ inline unsigned grid_ew(int64_t nvec) {
 // workspace: fp32 [256 * cols] (caller-provided, reused)
 PA_EXPORT int pa_colsum(const void* x, void* out, float* ws, int64_t rows, int64_t cols, int dtype, hipStream_t st) {
   const int np = nparts_for(rows);
-  dim3 g1((unsigned)cdiv(cols, 2048), (unsigned)np), g2((unsigned)cdiv(cols, 2048));
+  dim3 g1((unsigned)cdiv(cols, 2048), (unsigned)np), g2((unsigned)cdiv(cols, 64));
   PA_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL((colsum_partial_k<T>), g1, dim3(256), 0, st, (const T*)x, ws, rows, cols, np);
     hipLaunchKernelGGL((fold_partials_k<T>), g2, dim3(256), 0, st, ws, (T*)out, cols, np);
@@ -146,7 +167,7 @@ PA_EXPORT int pa_colsum(const void* x, void* out, float* ws, int64_t rows, int64
 PA_EXPORT int pa_bias_gelu_bwd(const void* h, const void* b, const void* dy, void* dh, void* db, float* ws,
                                int64_t rows, int64_t cols, int dtype, hipStream_t st) {
   const int np = nparts_for(rows);
-  dim3 g1((unsigned)cdiv(cols, 2048), (unsigned)np), g2((unsigned)cdiv(cols, 2048));
+  dim3 g1((unsigned)cdiv(cols, 2048), (unsigned)np), g2((unsigned)cdiv(cols, 64));
   PA_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL((bias_gelu_bwd_k<T>), g1, dim3(256), 0, st, (const T*)h, (const T*)b, (const T*)dy, (T*)dh,
                        ws, rows, cols, np);

@@ -130,7 +130,9 @@ class _Fleet:
             hcg = self._hcg
         mode = hcg.get_parallel_mode()
         if mode == ParallelMode.PIPELINE_PARALLEL:
-            from ...parallel.pipeline import PipelineParallel
+            from ...parallel.pipeline import PipelineParallel, PipelineParallelWithInterleave
+            if getattr(model, "get_num_virtual_stages", lambda: 1)() > 1:
+                return PipelineParallelWithInterleave(model, hcg, self._strategy)
             return PipelineParallel(model, hcg, self._strategy)
         if mode == ParallelMode.TENSOR_PARALLEL:
             return TensorParallel(model, hcg, self._strategy)

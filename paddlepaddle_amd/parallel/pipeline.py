@@ -8,6 +8,14 @@ Activations move between neighbouring stages with RCCL send/recv (one xGMI hop o
 shapes are exchanged once per micro-batch as a small int64 header so ragged last micro-batches work.
 Schedule = 1F1B (warm-up = stages - stage_id - 1 forwards, then one-forward-one-backward, then
 cool-down backwards), so at most `stages` micro-batch activations are alive per stage.
+
+Interleaved 1F1B (virtual pipeline, reference pipeline_parallel.py PipelineParallelWithInterleave):
+with V virtual stages each rank holds V model chunks (chunk c = v * stages + stage_id), the ring wraps
+from the last stage back to the first, and the warm-up is (stages - stage_id - 1) * 2 + (V - 1) * stages
+virtual micro-batches — the bubble shrinks by V. Every message carries a (kind, chunk, micro-batch)
+header and each rank reads its peer's stream in send order, stashing messages it does not need yet,
+so forward activations and backward gradients that share one link (always at 2 stages, and on the
+ring's wrap edge) can never be mismatched, on gloo or RCCL alike.
 """
 from __future__ import annotations
 
@@ -19,6 +27,9 @@ import torch.distributed as dist
 from .. import nn
 from ..distributed import collective as C
 from ..framework.tensor import Tensor, _wrap
+
+_FWD, _BWD = 0, 1
+_HDR = 13  # ndim, shape[8], dtype, kind, chunk, micro-batch
 
 
 class LayerDesc:
@@ -68,28 +79,43 @@ class PipelineLayer(nn.Layer):
         self._recompute_interval = recompute_interval
         self._layers_desc = list(layers)
         n = len(self._layers_desc)
-        self.segment_parts = self._segment(n, num_stages, seg_method)
-        lo, hi = self.segment_parts[self._stage_id], self.segment_parts[self._stage_id + 1]
-        self._start, self._end = lo, hi
+        V = int(num_virtual_pipeline_stages or 1)
+        self._num_virtual_stages = V
+        self.segment_parts = self._segment(n, num_stages * V, seg_method)
         self.run_function = []
         self.shared_layers = nn.LayerDict()
         self._built = nn.LayerList()
-        for i in range(lo, hi):
-            d = self._layers_desc[i]
-            if isinstance(d, SharedLayerDesc):
-                if d.layer_name not in self.shared_layers:
-                    self.shared_layers[d.layer_name] = d.build_layer()
-                l = self.shared_layers[d.layer_name]
-                self.run_function.append(_SharedCall(l, d.forward_func) if d.forward_func else l)
-            elif isinstance(d, LayerDesc):
-                l = d.build_layer()
-                self._built.append(l)
-                self.run_function.append(l)
-            elif isinstance(d, nn.Layer):
-                self._built.append(d)
-                self.run_function.append(d)
-            else:
-                self.run_function.append(d)  # plain callable
+        self._model_chunks = []
+        for v in range(V):
+            c = v * num_stages + self._stage_id
+            lo, hi = self.segment_parts[c], self.segment_parts[c + 1]
+            if v == 0:
+                self._start, self._end = lo, hi
+            fns = []
+            for i in range(lo, hi):
+                d = self._layers_desc[i]
+                if isinstance(d, SharedLayerDesc):
+                    if d.layer_name not in self.shared_layers:
+                        self.shared_layers[d.layer_name] = d.build_layer()
+                    l = self.shared_layers[d.layer_name]
+                    fns.append(_SharedCall(l, d.forward_func) if d.forward_func else l)
+                elif isinstance(d, LayerDesc):
+                    l = d.build_layer()
+                    self._built.append(l)
+                    fns.append(l)
+                elif isinstance(d, nn.Layer):
+                    self._built.append(d)
+                    fns.append(d)
+                else:
+                    fns.append(d)  # plain callable
+            self._model_chunks.append(fns)
+        self.run_function = self._model_chunks[0] if V == 1 else [f for ch in self._model_chunks for f in ch]
+
+    def get_num_virtual_stages(self):
+        return self._num_virtual_stages
+
+    def get_model_chunks(self):
+        return self._model_chunks
 
     @staticmethod
     def _segment(n, stages, method):
@@ -103,14 +129,15 @@ class PipelineLayer(nn.Layer):
         return parts
 
     def get_stage_from_index(self, idx):
-        for s in range(self._num_stages):
-            if self.segment_parts[s] <= idx < self.segment_parts[s + 1]:
-                return s
+        for c in range(len(self.segment_parts) - 1):
+            if self.segment_parts[c] <= idx < self.segment_parts[c + 1]:
+                return c % self._num_stages
         return self._num_stages - 1
 
-    def forward(self, x):
+    def forward(self, x, chunk_id=None):
         from ..distributed.fleet.recompute import recompute
-        for i, f in enumerate(self.run_function):
+        fns = self.run_function if chunk_id is None else self._model_chunks[chunk_id]
+        for i, f in enumerate(fns):
             if self._recompute_interval and self.training and i % self._recompute_interval == 0 and \
                     isinstance(f, nn.Layer):
                 x = recompute(f, x)
@@ -136,18 +163,19 @@ class PipelineParallel(nn.Layer):
         self.next_rank = self.group.ranks[self.stage_id + 1] if not self.is_last else None
         self._dp_sync = hcg.get_data_parallel_world_size() > 1
         self._pending = []
+        self._stash = {}
 
     # --------------------------------------------------------------- p2p
     def _dev(self):
         p = next(iter(self._layers.parameters()), None)
         return p._t.device if p is not None else torch.device("cpu")
 
-    def _send(self, t, dst):
+    def _send(self, t, dst, kind=_FWD, key=(0, 0)):
         # non-blocking: a stage may send its next activation before the neighbour has posted the
         # receive (1F1B would dead-lock on rendezvous sends); buffers are kept alive until joined
         t = t.contiguous()
-        hdr = torch.tensor([t.dim()] + list(t.shape) + [0] * (8 - t.dim()) + [_DT_CODE[t.dtype]], dtype=torch.int64,
-                           device=t.device)
+        hdr = torch.tensor([t.dim()] + list(t.shape) + [0] * (8 - t.dim()) + [_DT_CODE[t.dtype], kind, key[0], key[1]],
+                           dtype=torch.int64, device=t.device)
         pg = self.group.process_group
         self._pending.append((dist.isend(hdr, dst, group=pg), hdr))
         self._pending.append((dist.isend(t, dst, group=pg), t))
@@ -157,14 +185,24 @@ class PipelineParallel(nn.Layer):
             w.wait()
         self._pending = []
 
-    def _recv(self, src):
-        hdr = torch.empty(10, dtype=torch.int64, device=self._dev())
-        dist.recv(hdr, src, group=self.group.process_group)
-        nd = int(hdr[0])
-        shape = [int(v) for v in hdr[1:1 + nd]]
-        t = torch.empty(shape, dtype=_CODE_DT[int(hdr[9])], device=self._dev())
-        dist.recv(t, src, group=self.group.process_group)
-        return t
+    def _recv(self, src, kind=_FWD, key=(0, 0)):
+        """The (kind, key) message from ``src``: the peer's stream is read in send order and messages
+        that are not the one asked for are stashed for a later call."""
+        stash = self._stash.setdefault(src, {})
+        want = (kind, tuple(key))
+        if want in stash:
+            return stash.pop(want)
+        while True:
+            hdr = torch.empty(_HDR, dtype=torch.int64, device=self._dev())
+            dist.recv(hdr, src, group=self.group.process_group)
+            h = [int(v) for v in hdr.tolist()]
+            nd = h[0]
+            t = torch.empty(h[1:1 + nd], dtype=_CODE_DT[h[9]], device=self._dev())
+            dist.recv(t, src, group=self.group.process_group)
+            got = (h[10], (h[11], h[12]))
+            if got == want:
+                return t
+            stash[got] = t
 
     # --------------------------------------------------------------- schedule
     def _split(self, data):
@@ -175,27 +213,27 @@ class PipelineParallel(nn.Layer):
         n = self.accumulate_steps
         return [_wrap(c) for c in t.chunk(n, 0)]
 
-    def _forward_step(self, mb_input, mb_label):
+    def _forward_step(self, mb_input, mb_label, mb=0):
         if self.is_first:
             x = mb_input
         else:
-            xt = self._recv(self.prev_rank).requires_grad_(True)
+            xt = self._recv(self.prev_rank, _FWD, (0, mb)).requires_grad_(True)
             x = _wrap(xt)
         out = self._layers(x)
         if self.is_last:
             loss = self._layers._loss_fn(out, mb_label) if self._layers._loss_fn is not None else out
             return x, loss
-        self._send(out._t.detach(), self.next_rank)
+        self._send(out._t.detach(), self.next_rank, _FWD, (0, mb))
         return x, out
 
-    def _backward_step(self, inp, out):
+    def _backward_step(self, inp, out, mb=0):
         if self.is_last:
             (out._t / self.accumulate_steps).backward()
         else:
-            g = self._recv(self.next_rank)
+            g = self._recv(self.next_rank, _BWD, (0, mb))
             out._t.backward(g)
         if not self.is_first:
-            self._send(inp._t.grad, self.prev_rank)
+            self._send(inp._t.grad, self.prev_rank, _BWD, (0, mb))
 
     def forward_backward_pipeline(self, data, scaler=None):
         inputs, labels = (data if isinstance(data, (list, tuple)) and len(data) == 2 else (data, None))
@@ -206,24 +244,29 @@ class PipelineParallel(nn.Layer):
         steady = n - warm
         queue = []
         losses = []
-        fi = 0
+        fi = bi = 0
         for _ in range(warm):
-            x, y = self._forward_step(mb_in[fi], mb_lb[fi])
+            x, y = self._forward_step(mb_in[fi], mb_lb[fi], fi)
             queue.append((x, y))
             if self.is_last:
                 losses.append(y)
             fi += 1
         for i in range(steady):
-            x, y = self._forward_step(mb_in[fi], mb_lb[fi])
+            x, y = self._forward_step(mb_in[fi], mb_lb[fi], fi)
             queue.append((x, y))
             if self.is_last:
                 losses.append(y)
             fi += 1
             inp, out = queue.pop(0)
-            self._backward_step(inp, out)
+            self._backward_step(inp, out, bi)
+            bi += 1
         for _ in range(warm):
             inp, out = queue.pop(0)
-            self._backward_step(inp, out)
+            self._backward_step(inp, out, bi)
+            bi += 1
+        return self._finish(losses)
+
+    def _finish(self, losses):
         self._join_sends()
         if self._dp_sync:
             g = self._hcg.get_data_parallel_group()
@@ -256,7 +299,7 @@ class PipelineParallel(nn.Layer):
         mb_lb = self._split(labels) if (self.is_last and labels is not None) else [None] * self.accumulate_steps
         outs = []
         for i in range(self.accumulate_steps):
-            _, y = self._forward_step(mb_in[i], mb_lb[i] if compute_loss else None)
+            _, y = self._forward_step(mb_in[i], mb_lb[i] if compute_loss else None, i)
             if self.is_last:
                 outs.append(y._t.float().mean() if compute_loss else y._t)
         self._join_sends()
@@ -273,3 +316,98 @@ class PipelineParallel(nn.Layer):
 
 _DT_CODE = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2, torch.int64: 3, torch.int32: 4, torch.bool: 5}
 _CODE_DT = {v: k for k, v in _DT_CODE.items()}
+
+
+class PipelineParallelWithInterleave(PipelineParallel):
+    """Interleaved 1F1B over V model chunks per rank (reference:
+    fleet/meta_parallel/pipeline_parallel.py PipelineParallelWithInterleave). accumulate_steps must be a
+    multiple of the number of stages; chunk v of stage s computes layers segment v * stages + s."""
+
+    def __init__(self, layers, hcg, strategy):
+        super().__init__(layers, hcg, strategy)
+        self.V = layers.get_num_virtual_stages()
+        if self.V < 2:
+            raise ValueError("PipelineParallelWithInterleave needs num_virtual_pipeline_stages >= 2")
+        S = self.num_stages
+        self.prev_rank = self.group.ranks[(self.stage_id - 1) % S]
+        self.next_rank = self.group.ranks[(self.stage_id + 1) % S]
+        if self.accumulate_steps % S:
+            raise ValueError(f"accumulate_steps ({self.accumulate_steps}) must be a multiple of the "
+                             f"pipeline degree ({S}) for the interleaved schedule")
+
+    def _chunk_of(self, k, forward):
+        v = (k // self.num_stages) % self.V
+        return v if forward else self.V - 1 - v
+
+    def _mb_of(self, k):
+        S = self.num_stages
+        return (k // (S * self.V)) * S + k % S
+
+    def _vforward(self, k, mb_in, mb_lb, store, losses):
+        v, mb = self._chunk_of(k, True), self._mb_of(k)
+        first = self.stage_id == 0 and v == 0
+        last = self.stage_id == self.num_stages - 1 and v == self.V - 1
+        if first:
+            x = mb_in[mb]
+        else:
+            # chunk v of stage 0 consumes chunk v-1 of the last stage (ring wrap)
+            x = _wrap(self._recv(self.prev_rank, _FWD, (v if self.stage_id else v - 1, mb)).requires_grad_(True))
+        out = self._layers(x, chunk_id=v)
+        if last:
+            out = self._layers._loss_fn(out, mb_lb[mb]) if self._layers._loss_fn is not None else out
+            losses.append(out)
+        else:
+            self._send(out._t.detach(), self.next_rank, _FWD, (v, mb))
+        store[(v, mb)] = (x, out)
+
+    def _vbackward(self, k, store):
+        v, mb = self._chunk_of(k, False), self._mb_of(k)
+        first = self.stage_id == 0 and v == 0
+        last = self.stage_id == self.num_stages - 1 and v == self.V - 1
+        x, out = store.pop((v, mb))
+        if last:
+            (out._t / self.accumulate_steps).backward()
+        else:
+            # the gradient of chunk v's output comes from chunk v (or v+1 across the wrap) downstream
+            src_v = v + 1 if self.stage_id == self.num_stages - 1 else v
+            out._t.backward(self._recv(self.next_rank, _BWD, (src_v, mb)))
+        if not first:
+            self._send(x._t.grad, self.prev_rank, _BWD, (v, mb))
+
+    def forward_backward_pipeline(self, data, scaler=None):
+        inputs, labels = (data if isinstance(data, (list, tuple)) and len(data) == 2 else (data, None))
+        n = self.accumulate_steps
+        mb_in = self._split(inputs) if self.stage_id == 0 else [None] * n
+        mb_lb = self._split(labels) if (self.stage_id == self.num_stages - 1 and labels is not None) else [None] * n
+        total = n * self.V
+        warm = min((self.num_stages - self.stage_id - 1) * 2 + (self.V - 1) * self.num_stages, total)
+        store, losses = {}, []
+        fk = bk = 0
+        for _ in range(warm):
+            self._vforward(fk, mb_in, mb_lb, store, losses)
+            fk += 1
+        for _ in range(total - warm):
+            self._vforward(fk, mb_in, mb_lb, store, losses)
+            fk += 1
+            self._vbackward(bk, store)
+            bk += 1
+        while bk < total:
+            self._vbackward(bk, store)
+            bk += 1
+        self.is_last = self.stage_id == self.num_stages - 1  # loss lives on the last stage's last chunk
+        return self._finish(losses)
+
+    @torch.no_grad()
+    def eval_batch(self, data, compute_loss=True):
+        self._layers.eval()
+        inputs, labels = (data if isinstance(data, (list, tuple)) and len(data) == 2 else (data, None))
+        n = self.accumulate_steps
+        mb_in = self._split(inputs) if self.stage_id == 0 else [None] * n
+        mb_lb = self._split(labels) if (self.stage_id == self.num_stages - 1 and labels is not None) else [None] * n
+        store, losses = {}, []
+        for k in range(n * self.V):
+            self._vforward(k, mb_in, mb_lb if compute_loss else [None] * n, store, losses)
+        self._join_sends()
+        if self.stage_id == self.num_stages - 1 and compute_loss:
+            return _wrap(torch.stack([l._t.float().mean() for l in losses]).mean())
+        return [l._t for l in losses]

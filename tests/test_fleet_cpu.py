@@ -11,13 +11,13 @@ import torch
 from test_distributed_cpu import ROOT, _data, _setup, _spawn
 
 
-def _fleet_init(paddle, **hc):
+def _fleet_init(paddle, acc=2, **hc):
     from paddlepaddle_amd.distributed import fleet
     s = fleet.DistributedStrategy()
     cfg = dict(dp_degree=1, mp_degree=1, pp_degree=1)
     cfg.update(hc)
     s.hybrid_configs = cfg
-    s.pipeline_configs = {"accumulate_steps": 2, "micro_batch_size": 2}
+    s.pipeline_configs = {"accumulate_steps": acc, "micro_batch_size": 2}
     fleet.init(is_collective=True, strategy=s)
     return fleet
 
@@ -264,3 +264,71 @@ def test_llama_tensor_parallel_matches_single_process():
     res = _spawn(_llama_tp_worker)
     for _, l in res:
         np.testing.assert_allclose(l, ref, rtol=1e-4, atol=1e-5)
+
+
+# ----------------------------------------------------------------------------- interleaved pipeline (VPP)
+def _vpp_descs(paddle):
+    from paddlepaddle_amd.parallel.pipeline import LayerDesc
+    nn = paddle.nn
+    return [LayerDesc(nn.Linear, 16, 32), LayerDesc(nn.Tanh), LayerDesc(nn.Linear, 32, 32), LayerDesc(nn.GELU),
+            LayerDesc(nn.Linear, 32, 32), LayerDesc(nn.Tanh), LayerDesc(nn.Linear, 32, 8), LayerDesc(nn.Tanh)]
+
+
+def _vpp_worker(rank, world, port, q):
+    paddle = _setup(rank, world, port)
+    from paddlepaddle_amd.parallel.pipeline import PipelineLayer, PipelineParallelWithInterleave
+    paddle.seed(11)
+    full = [d.build_layer() for d in _vpp_descs(paddle)]
+    fleet = _fleet_init(paddle, acc=4, pp_degree=2)
+    pl = PipelineLayer(_vpp_descs(paddle), num_stages=2, loss_fn=_mse, num_virtual_pipeline_stages=2)
+    # chunks: segments of 2 layers; stage s holds segments s and 2 + s
+    idx = {}
+    for v, fns in enumerate(pl.get_model_chunks()):
+        c = v * 2 + pl._stage_id
+        for j, f in enumerate(fns):
+            idx[pl.segment_parts[c] + j] = f
+    with torch.no_grad():
+        for i, f in idx.items():
+            for (k, v), (_, fv) in zip(f.state_dict().items(), full[i].state_dict().items()):
+                v._t.copy_(fv._t)
+    opt = paddle.optimizer.SGD(0.1, parameters=pl.parameters())
+    model = fleet.distributed_model(pl)
+    assert isinstance(model, PipelineParallelWithInterleave)
+    x, y = _pp_data()
+    losses = [float(model.train_batch([paddle.Tensor(x), paddle.Tensor(y)], opt)) for _ in range(2)]
+    params = {f"{i}.{k}": v.numpy() for i, f in idx.items() for k, v in f.state_dict().items()}
+    q.put((rank, losses, params, None))
+    paddle.distributed.barrier()
+
+
+def test_pipeline_interleaved_matches_single_process():
+    sys.path.insert(0, ROOT)
+    os.environ["PADDLE_AMD_FORCE_CPU"] = "1"
+    import paddlepaddle_amd as paddle
+    paddle.seed(11)
+    layers = [d.build_layer() for d in _vpp_descs(paddle)]
+    params = [p for l in layers for p in l.parameters()]
+    opt = paddle.optimizer.SGD(0.1, parameters=params)
+    x, y = _pp_data()
+
+    def fwd(t):
+        for l in layers:
+            t = l(t)
+        return t
+    ref = []
+    for _ in range(2):
+        loss = sum(_mse(fwd(paddle.Tensor(x[i:i + 2])), paddle.Tensor(y[i:i + 2])) for i in range(0, 8, 2)) * 0.25
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        ref.append(float(loss))
+    ref_params = {f"{i}.{k}": v.numpy() for i, l in enumerate(layers) for k, v in l.state_dict().items()}
+    res = _spawn(_vpp_worker)
+    (_, l0, p0, _), (_, l1, p1, _) = res
+    np.testing.assert_allclose(l0, ref, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(l1, ref, rtol=1e-5, atol=1e-6)
+    got = dict(p0)
+    got.update(p1)
+    assert set(got) == set(ref_params)
+    for k in ref_params:
+        np.testing.assert_allclose(got[k], ref_params[k], rtol=1e-4, atol=1e-6, err_msg=k)
