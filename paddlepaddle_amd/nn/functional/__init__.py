@@ -12,3 +12,4 @@ from .vision import *  # noqa: F401,F403
 from ...tensor.math import sigmoid, tanh  # noqa: F401
 from ...tensor.manipulation import unfold as _tensor_unfold  # noqa: F401
 from .common import unfold  # noqa: F401,E402
+from .extension import *  # noqa: F401,F403,E402

@@ -1,0 +1,161 @@
+"""CPU tests of the less common nn APIs (fractional pooling, hsigmoid, RNN-T, adaptive softmax, sparse /
+flashmask attention, beam-search decoding) against direct reference formulas."""
+import itertools
+import math
+
+import numpy as np
+import torch
+
+import paddlepaddle_amd as paddle
+
+F = paddle.nn.functional
+
+
+def test_fractional_max_pool_reference_example():
+    # paddle docstring example: [2,4,3,1,5,2,3], output 5, u = 0.3 -> [2,4,1,5,3]
+    x = paddle.to_tensor(np.array([2, 4, 3, 1, 5, 2, 3], dtype="float32").reshape(1, 1, 1, 7))
+    y = F.fractional_max_pool2d(x, output_size=[1, 5], random_u=0.3)
+    np.testing.assert_array_equal(y.numpy().ravel(), [2, 4, 1, 5, 3])
+
+
+def test_fractional_max_pool_mask_points_at_max():
+    x = paddle.randn([2, 3, 11, 9])
+    y, m = F.fractional_max_pool2d(x, output_size=[4, 5], random_u=0.7, return_mask=True)
+    flat = x.numpy().reshape(2, 3, -1)
+    got = np.take_along_axis(flat, m.numpy().reshape(2, 3, -1), 2).reshape(y.shape)
+    np.testing.assert_array_equal(got, y.numpy())
+    y3 = paddle.nn.FractionalMaxPool3D(output_size=2, random_u=0.4)(paddle.randn([1, 2, 5, 5, 5]))
+    assert y3.shape == [1, 2, 2, 2, 2]
+
+
+def _hsig_ref(x, label, num_classes, w, b):
+    out = []
+    L = (num_classes - 1).bit_length()
+    for i in range(x.shape[0]):
+        c = int(label[i]) + num_classes
+        length = c.bit_length() - 1
+        tot = 0.0
+        for j in range(L):
+            if j < length:
+                idx = (c >> (j + 1)) - 1
+                pre = float(np.clip(x[i] @ w[idx] + b[idx, 0], -40, 40))
+                bit = (c >> j) & 1
+            else:
+                pre, bit = 0.0, 0
+            tot += math.log1p(math.exp(pre)) - bit * pre
+        out.append(tot)
+    return np.array(out, dtype=np.float32)[:, None]
+
+
+def test_hsigmoid_loss_default_tree():
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((5, 4)).astype("float32")
+    w = rng.standard_normal((6, 4)).astype("float32")
+    b = rng.standard_normal((6, 1)).astype("float32")
+    lab = np.array([0, 3, 6, 2, 5])
+    got = F.hsigmoid_loss(paddle.to_tensor(x), paddle.to_tensor(lab), 7, paddle.to_tensor(w), paddle.to_tensor(b))
+    np.testing.assert_allclose(got.numpy(), _hsig_ref(x, lab, 7, w, b), rtol=1e-5, atol=1e-5)
+
+
+def _rnnt_ref(lp, lab, T_, U):
+    # brute force over all monotonic alignments (small sizes)
+    total = -np.inf
+    blank = 0
+    for emits in itertools.combinations(range(T_ + U - 1), U):
+        t = u = 0
+        s = 0.0
+        ok = True
+        for k in range(T_ + U - 1):
+            if k in emits:
+                s += lp[t, u, lab[u]]
+                u += 1
+            else:
+                s += lp[t, u, blank]
+                t += 1
+            if t >= T_:
+                ok = False
+                break
+        if not ok:
+            continue
+        s += lp[T_ - 1, U, blank]
+        total = np.logaddexp(total, s)
+    return -total
+
+
+def test_rnnt_loss_matches_alignment_sum():
+    torch.manual_seed(0)
+    logits = torch.randn(1, 3, 3, 4)
+    lab = np.array([[1, 2]])
+    got = F.rnnt_loss(paddle.to_tensor(logits.numpy()), paddle.to_tensor(lab), paddle.to_tensor([3]),
+                      paddle.to_tensor([2]), fastemit_lambda=0.0, reduction="sum")
+    ref = _rnnt_ref(torch.log_softmax(logits, -1)[0].numpy(), lab[0], 3, 2)
+    np.testing.assert_allclose(float(got), ref, rtol=1e-5)
+
+
+def test_adaptive_log_softmax_normalised():
+    paddle.seed(3)
+    a = paddle.nn.AdaptiveLogSoftmaxWithLoss(8, 20, [5, 12], div_value=2.0)
+    x = paddle.randn([6, 8])
+    lp = a.log_prob(x).numpy()
+    np.testing.assert_allclose(np.exp(lp).sum(1), np.ones(6), rtol=1e-5)
+    lab = np.array([0, 4, 6, 11, 13, 19])
+    out, loss = a(x, paddle.to_tensor(lab))
+    np.testing.assert_allclose(out.numpy(), lp[np.arange(6), lab], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(float(loss), -lp[np.arange(6), lab].mean(), rtol=1e-5)
+
+
+def test_sparse_attention_equals_masked_dense():
+    q = paddle.randn([1, 2, 4, 8])
+    off = np.array([[[0, 1, 3, 5, 8], [0, 2, 3, 4, 6]]], dtype="int32")
+    col = np.array([[[0, 0, 1, 1, 2, 0, 2, 3], [0, 1, 1, 2, 0, 3, 0, 0]]], dtype="int32")
+    got = F.sparse_attention(q, q, q, paddle.to_tensor(off), paddle.to_tensor(col)).numpy()
+    qt = torch.from_numpy(q.numpy())
+    for h in range(2):
+        m = torch.zeros(4, 4, dtype=torch.bool)
+        for r in range(4):
+            for p in range(off[0, h, r], off[0, h, r + 1]):
+                m[r, col[0, h, p]] = True
+        s = (qt[0, h] @ qt[0, h].T) / math.sqrt(8)
+        ref = torch.softmax(s.masked_fill(~m, float("-inf")), -1) @ qt[0, h]
+        np.testing.assert_allclose(got[0, h], ref.numpy(), rtol=1e-5, atol=1e-5)
+
+
+def test_flashmask_causal_document_mask():
+    # two documents of 4 tokens: key j of doc 0 is masked for rows >= 4 (start row 4)
+    q = paddle.randn([1, 8, 1, 16])
+    se = np.array([4] * 4 + [8] * 4, dtype="int32").reshape(1, 1, 8, 1)
+    got = F.flashmask_attention(q, q, q, paddle.to_tensor(se), causal=True).numpy()
+    qt = torch.from_numpy(q.numpy())[0, :, 0]
+    keep = torch.ones(8, 8, dtype=torch.bool).tril()
+    keep[4:, :4] = False
+    s = (qt @ qt.T) / 4.0
+    ref = torch.softmax(s.masked_fill(~keep, float("-inf")), -1) @ qt
+    np.testing.assert_allclose(got[0, :, 0], ref.numpy(), rtol=1e-4, atol=1e-5)
+
+
+class _ToyCell(paddle.nn.Layer):
+    """Deterministic cell: logits depend only on the previous token (a fixed transition table)."""
+
+    def __init__(self, table):
+        super().__init__()
+        self.table = torch.tensor(table, dtype=torch.float32)
+
+    def forward(self, inputs, states):
+        ids = inputs._t if hasattr(inputs, "_t") else inputs
+        logits = self.table[ids.long()]
+        return paddle.Tensor(logits), states
+
+
+def test_beam_search_decoder_finds_best_path():
+    # vocab {0: start, 1, 2, 3: end}; greedy from start picks 1 (0.6) but the best full path is 2 -> end
+    table = np.log(np.array([[1e-9, 0.55, 0.45, 1e-9],
+                             [1e-9, 0.5, 1e-9, 0.5],
+                             [1e-9, 1e-9, 1e-9, 1.0],
+                             [1e-9, 1e-9, 1e-9, 1.0]]))
+    cell = _ToyCell(table)
+    dec = paddle.nn.BeamSearchDecoder(cell, start_token=0, end_token=3, beam_size=2)
+    init = paddle.zeros([1, 4])
+    out, states, lens = paddle.nn.dynamic_decode(dec, inits=init, max_step_num=5, return_length=True)
+    ids = out.numpy()  # [batch, time, beam]
+    assert list(ids[0, :2, 0]) == [2, 3]
+    assert int(lens.numpy()[0, 0]) == 2
