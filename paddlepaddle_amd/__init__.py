@@ -47,6 +47,8 @@ from . import autograd, nn, optimizer, amp, io, distributed, device, utils  # no
 from .autograd import grad, PyLayer  # noqa: F401
 from . import linalg, fft, signal, static, jit, metric, vision, hapi, incubate, profiler, distribution, sparse  # noqa: F401,E402
 from . import callbacks, text, audio, geometric, quantization, inference, regularizer, onnx, models, parallel  # noqa: F401,E402
+import importlib as _il  # noqa: E402
+linalg = _il.import_module(".linalg", __name__)  # `from . import linalg` would keep tensor.linalg bound by *
 from .hapi import Model, summary, flops  # noqa: F401,E402
 from .parallel.data_parallel import DataParallel  # noqa: F401,E402
 from .nn.layer.layers import ParamAttr  # noqa: F401,E402
@@ -169,3 +171,17 @@ class version:
 
 
 CUDAPlace = CUDAPlace
+
+
+def block_diag(inputs, name=None):
+    """Block-diagonal matrix from a list of 0-D / 1-D / 2-D tensors (reference tensor/creation.py)."""
+    import torch as _t
+    from .framework.tensor import _wrap as _w
+    ts = []
+    for x in inputs:
+        t = x._t if hasattr(x, "_t") else _t.as_tensor(x)
+        ts.append(t.reshape(1, -1) if t.dim() < 2 else t)
+    return _w(_t.block_diag(*ts))
+
+
+from . import sysconfig  # noqa: F401,E402

@@ -223,3 +223,81 @@ class backends:
     def set_backend(name):
         if name != "wave_backend":
             raise ValueError("only the built-in wave backend is available")
+
+
+class _AudioDataset:
+    """Local-file audio classification dataset (no download: point ``data_dir`` at an extracted copy).
+    Returns (waveform or feature, label) pairs; feat_type 'raw' | 'melspectrogram' | 'mfcc' | ...
+    (reference python/paddle/audio/datasets/{esc50,tess}.py)."""
+    n_class = 0
+
+    def __init__(self, mode="train", split=1, feat_type="raw", archive=None, data_dir=None, **kwargs):
+        import os
+        if data_dir is None or not os.path.isdir(data_dir):
+            raise RuntimeError(f"{type(self).__name__}: no network access — pass data_dir= pointing at the "
+                               "extracted dataset")
+        self.mode, self.split, self.feat_type, self.kwargs = mode, split, feat_type, kwargs
+        self.files, self.labels = self._scan(data_dir)
+
+    def _scan(self, data_dir):
+        raise NotImplementedError
+
+    def __len__(self):
+        return len(self.files)
+
+    def __getitem__(self, idx):
+        wav, sr = load(self.files[idx])
+        x = wav
+        if self.feat_type != "raw":
+            layer = {"melspectrogram": MelSpectrogram, "logmelspectrogram": LogMelSpectrogram,
+                     "mfcc": MFCC, "spectrogram": Spectrogram}[self.feat_type.lower()]
+            x = layer(sr=sr, **self.kwargs) if layer is not Spectrogram else layer(**self.kwargs)
+            x = x(wav)
+        return x, self.labels[idx]
+
+
+class ESC50(_AudioDataset):
+    n_class = 50
+
+    def _scan(self, data_dir):
+        import csv
+        import os
+        meta = os.path.join(data_dir, "meta", "esc50.csv")
+        files, labels = [], []
+        with open(meta) as f:
+            for row in csv.DictReader(f):
+                fold = int(row["fold"])
+                if (self.mode == "train") == (fold != self.split):
+                    files.append(os.path.join(data_dir, "audio", row["filename"]))
+                    labels.append(int(row["target"]))
+        return files, labels
+
+
+class TESS(_AudioDataset):
+    n_class = 7
+    label_list = ["angry", "disgust", "fear", "happy", "neutral", "ps", "sad"]
+
+    def _scan(self, data_dir):
+        import os
+        files, labels = [], []
+        for root, _, names in os.walk(data_dir):
+            for i, n in enumerate(sorted(names)):
+                if not n.endswith(".wav"):
+                    continue
+                emo = n.rsplit(".", 1)[0].split("_")[-1].lower()
+                if emo not in self.label_list:
+                    continue
+                if (self.mode == "train") == (i % 5 != self.split - 1):
+                    files.append(os.path.join(root, n))
+                    labels.append(self.label_list.index(emo))
+        return files, labels
+
+
+class datasets:  # namespace: paddle.audio.datasets.ESC50 / TESS
+    ESC50 = ESC50
+    TESS = TESS
+
+
+import sys as _sys  # noqa: E402
+for _n in ("functional", "features", "backends", "datasets"):
+    _sys.modules[__name__ + "." + _n] = globals()[_n]

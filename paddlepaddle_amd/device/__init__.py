@@ -33,3 +33,27 @@ def get_cudnn_version():
 
 def device_count():
     return torch.cuda.device_count()
+
+
+def is_compiled_with_distribute():
+    """RCCL (torch.distributed 'nccl' backend) and gloo are built in."""
+    import torch.distributed as dist
+    return dist.is_available()
+
+
+def set_stream(stream=None):
+    """Make ``stream`` the current stream of its device; returns the previous one."""
+    prev = current_stream()
+    if stream is not None:
+        torch.cuda.set_stream(getattr(stream, "_s", stream))
+    return prev
+
+
+class XPUPlace:
+    def __init__(self, *a, **k):
+        raise RuntimeError("XPU devices are not supported by this MI355X framework")
+
+
+class IPUPlace:
+    def __init__(self, *a, **k):
+        raise RuntimeError("IPU devices are not supported by this MI355X framework")

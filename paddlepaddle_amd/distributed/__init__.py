@@ -11,6 +11,7 @@ from .auto_parallel import (ProcessMesh, Shard, Replicate, Partial, Placement, R
                             shard_dataloader, Strategy, DistModel, to_static, get_mesh, set_mesh)
 from . import auto_parallel  # noqa: F401
 from ..parallel.data_parallel import DataParallel  # noqa: F401,E402
+from .extras import *  # noqa: F401,F403,E402
 
 
 def __getattr__(name):

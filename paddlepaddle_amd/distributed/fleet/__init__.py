@@ -34,3 +34,91 @@ class Role:
     HETER_WORKER = 3
     ALL = 4
     COORDINATOR = 5
+
+
+class UtilBase:
+    """fleet.util: all_reduce / barrier / all_gather helpers over the default group (reference
+    fleet/base/util_factory.py UtilBase)."""
+
+    def all_reduce(self, input, mode="sum", comm_world="worker"):
+        import numpy as np
+        import torch
+        import torch.distributed as dist
+        t = torch.as_tensor(np.asarray(input), dtype=torch.float64)
+        if dist.is_initialized():
+            op = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[mode]
+            dist.all_reduce(t, op=op)
+        return t.numpy()
+
+    def barrier(self, comm_world="worker"):
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.barrier()
+
+    def all_gather(self, input, comm_world="worker"):
+        import torch.distributed as dist
+        if not dist.is_initialized():
+            return [input]
+        out = [None] * dist.get_world_size()
+        dist.all_gather_object(out, input)
+        return out
+
+    def get_file_shard(self, files):
+        import torch.distributed as dist
+        r, n = (dist.get_rank(), dist.get_world_size()) if dist.is_initialized() else (0, 1)
+        return files[r::n]
+
+    def print_on_rank(self, message, rank_id):
+        import torch.distributed as dist
+        if (dist.get_rank() if dist.is_initialized() else 0) == rank_id:
+            print(message)
+
+
+util = UtilBase()
+Fleet = type(fleet)
+
+
+class MultiSlotDataGenerator:
+    """PS data generator (reference fleet/data_generator): subclasses implement generate_sample(line)
+    returning an iterator of [(slot_name, [values...]), ...]; run_from_memory / run_from_stdin print the
+    MultiSlot text format."""
+
+    def __init__(self):
+        self._proto_info = None
+        self.batch_size_ = 32
+
+    def set_batch(self, batch_size):
+        self.batch_size_ = batch_size
+
+    def generate_sample(self, line):
+        raise NotImplementedError
+
+    def generate_batch(self, samples):
+        def it():
+            for s in samples:
+                yield s
+        return it
+
+    def _format(self, sample):
+        out = []
+        for name, vals in sample:
+            out.append(str(len(vals)))
+            out.extend(str(v) for v in vals)
+        return " ".join(out)
+
+    def run_from_memory(self, lines=None):
+        res = []
+        for line in lines or []:
+            for s in self.generate_sample(line)():
+                res.append(self._format(s))
+        return res
+
+    def run_from_stdin(self):
+        import sys
+        for line in sys.stdin:
+            for s in self.generate_sample(line)():
+                sys.stdout.write(self._format(s) + "\n")
+
+
+class MultiSlotStringDataGenerator(MultiSlotDataGenerator):
+    pass

@@ -58,3 +58,29 @@ def disable_prim():
 
 def prim_enabled():
     return False
+
+
+def grad(outputs, inputs, grad_outputs=None):
+    """Reverse-mode gradients (reference incubate.autograd.grad over primitive ops)."""
+    from ..autograd import grad as _grad
+    single = not isinstance(inputs, (list, tuple))
+    r = _grad(outputs, inputs, grad_outputs, create_graph=True, allow_unused=True)
+    return r[0] if single and isinstance(r, (list, tuple)) else r
+
+
+def forward_grad(outputs, inputs, grad_inputs=None):
+    """Forward-mode directional derivative d outputs / d inputs . grad_inputs, computed as the transpose of
+    a VJP (double-backward), which needs no separate forward-mode rules."""
+    import torch
+    outs = outputs if isinstance(outputs, (list, tuple)) else [outputs]
+    ins = inputs if isinstance(inputs, (list, tuple)) else [inputs]
+    if grad_inputs is None:
+        gins = [torch.ones_like(i._t) for i in ins]
+    else:
+        gins = [g._t for g in (grad_inputs if isinstance(grad_inputs, (list, tuple)) else [grad_inputs])]
+    us = [torch.zeros_like(o._t, requires_grad=True) for o in outs]
+    vjp = torch.autograd.grad([o._t for o in outs], [i._t for i in ins], us, create_graph=True, allow_unused=True)
+    pairs = [(v, g) for v, g in zip(vjp, gins) if v is not None]
+    jv = torch.autograd.grad([v for v, _ in pairs], us, [g for _, g in pairs], create_graph=True, allow_unused=True)
+    res = [_wrap(j if j is not None else torch.zeros_like(u)) for j, u in zip(jv, us)]
+    return res if isinstance(outputs, (list, tuple)) else res[0]

@@ -102,3 +102,5 @@ class ModelAverage:
 
     def minimize(self, loss, startup_program=None, parameters=None, no_grad_set=None):
         self.step()
+
+from ..optimizer import LBFGS  # noqa: F401,E402  (reference keeps an incubate alias)

@@ -268,3 +268,37 @@ def convert_to_mixed_precision(*a, **k):
 
 
 Tensor = _Handle
+
+
+class PredictorPool:
+    """A fixed pool of predictors built from one Config (reference inference PredictorPool)."""
+
+    def __init__(self, config, size=1):
+        self._preds = [create_predictor(config) for _ in range(max(1, size))]
+
+    def retrive(self, idx):
+        return self._preds[idx]
+
+    retrieve = retrive
+
+
+def get_num_bytes_of_data_type(dtype):
+    return {DataType.FLOAT32: 4, DataType.FLOAT16: 2, DataType.BFLOAT16: 2, DataType.INT64: 8, DataType.INT32: 4,
+            DataType.UINT8: 1, DataType.INT8: 1, DataType.BOOL: 1, DataType.FLOAT64: 8}.get(dtype, 4)
+
+
+def get_trt_compile_version():
+    return (0, 0, 0)
+
+
+def get_trt_runtime_version():
+    return (0, 0, 0)
+
+
+class XpuConfig:
+    def __init__(self, *a, **k):
+        raise RuntimeError("XPU devices are not supported by this MI355X framework")
+
+
+def _get_phi_kernel_name(op_name):
+    return op_name

@@ -211,3 +211,11 @@ class MaxPool3D(_nn.Layer):
 
     def forward(self, x):
         return functional.max_pool3d(x, self.k, self.s, self.p, self.c)
+
+
+functional.subm_conv2d_igemm = functional.subm_conv2d  # implicit-GEMM variants: same math, same entry
+functional.subm_conv3d_igemm = functional.subm_conv3d
+
+import sys as _sys  # noqa: E402
+# `import paddle.sparse.nn.functional as F` works like in the reference (a namespace object as module)
+_sys.modules[__name__ + ".functional"] = functional

@@ -9,6 +9,7 @@ from .io import (save_inference_model, load_inference_model, save, load, load_pr
                  set_program_state, serialize_program, serialize_persistables, deserialize_program,
                  save_to_file, load_from_file, normalize_program, save_persistables, load_persistables)
 from . import nn  # noqa: F401
+from .extras import *  # noqa: F401,F403
 from ..framework.tensor import Tensor as Variable  # noqa: F401
 
 ParallelExecutor = Executor

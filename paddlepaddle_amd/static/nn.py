@@ -96,3 +96,4 @@ def data_norm(input, *a, **k):
 
 def sequence_softmax(input, use_cudnn=False, name=None):
     return F.softmax(input, axis=-1)
+from .control_flow import *  # noqa: F401,F403,E402

@@ -72,3 +72,13 @@ def pack_sequence_as(structure, flat):
             return {k: _p(s[k]) for k in sorted(s)}
         return next(it)
     return _p(structure)
+
+
+def require_version(min_version, max_version=None):
+    """Raise if the installed framework version is outside [min_version, max_version]."""
+    from .. import __version__ as v
+
+    def key(x):
+        return [int(p) if p.isdigit() else 0 for p in str(x).split("+")[0].split(".")][:4]
+    if key(v) < key(min_version) or (max_version is not None and key(v) > key(max_version)):
+        raise Exception(f"paddlepaddle_amd version {v} does not satisfy [{min_version}, {max_version}]")
