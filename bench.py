@@ -176,6 +176,14 @@ def resnet_bench(args, paddle, world, dist_on):
     dt = timed(step, args.resnet_steps, max(args.warmup, 3), dist_on)
     ips = args.resnet_steps * B * world / dt
     log(f"[resnet50] step={dt / args.resnet_steps * 1000:.1f}ms img/s={ips:.0f}")
+    try:
+        from paddlepaddle_amd.ops import gemm as _G
+        for kind in ("conv1x1", "convKxK"):
+            cv = {k: v for k, v in _G.choices().items() if k[0] == kind}
+            log(f"[resnet50] {kind} backend per shape: {sum(v == 'hip' for v in cv.values())} hand-written MFMA / "
+                f"{sum(v == 'blas' for v in cv.values())} MIOpen")
+    except Exception:  # pragma: no cover
+        pass
     return ips
 
 

@@ -67,7 +67,25 @@ struct GemmArgs {
   int tiles_m, tiles_n;
   int flags;
   float alpha;
+  int64_t c_split;  // split-K: blockIdx.y = K slice of p.K elements; output slab stride (fp32 elements)
+  // implicit-GEMM convolution (NHWC): A[p][k] = x[n, ho*s - pad + kh*dil, wo*s - pad + kw*dil, c],
+  // p = (n, ho, wo), k = (kh * KW + kw) * C + c; out-of-image taps read the 128-byte zero page
+  const uint16_t* zero;
+  int cH, cW, cC, cHo, cWo, cKW, cStride, cPadH, cPadW, cDil;
 };
+
+// split-K view: slice blockIdx.y of K (p.K elements each) and its own fp32 output slab
+template <bool AK, bool BKM>
+__device__ __forceinline__ GemmArgs split_view(const GemmArgs& p0) {
+  GemmArgs p = p0;
+  const int64_t ks = blockIdx.y;
+  if (ks) {
+    p.a += ks * (int64_t)p.K * (AK ? 1 : p.lda);
+    p.b += ks * (int64_t)p.K * (BKM ? 1 : p.ldb);
+    p.c = reinterpret_cast<float*>(p.c) + ks * p.c_split;
+  }
+  return p;
+}
 
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
@@ -147,7 +165,8 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 }
 
 template <int BN, bool AK, bool BKM>
-__global__ __launch_bounds__(kThreads, 1) void gemm_bf16_kernel(GemmArgs p) {
+__global__ __launch_bounds__(kThreads, 1) void gemm_bf16_kernel(GemmArgs p0) {
+  const GemmArgs p = split_view<AK, BKM>(p0);
   constexpr int A_BYTES = kBM * kBK * 2;
   constexpr int B_BYTES = BN * kBK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
@@ -290,7 +309,8 @@ __device__ __forceinline__ void vm_wait(int n) {
 }
 
 template <bool AK, bool BKM>
-__global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p) {
+__global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p0) {
+  const GemmArgs p = split_view<AK, BKM>(p0);
   constexpr int HALF = 128 * kBK * 2;  // 16 KiB
   constexpr int STAGE = 4 * HALF;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -532,8 +552,52 @@ __device__ __forceinline__ bf16x8_t frag_r(const char* img, int rbase, int s, in
   }
 }
 
-template <bool AK, bool BKM>
-__global__ __launch_bounds__(kThreads, 1) void gemm3s_kernel(GemmArgs p) {
+// Per-thread precomputed output pixels of the 4 A rows this thread stages (implicit-GEMM conv).
+struct ConvRows {
+  int pix[4];  // n * H * W (first pixel of the image), or -1 for rows past M
+  int hb[4], wb[4];
+};
+
+__device__ __forceinline__ ConvRows conv_rows(const GemmArgs& p, int m0, int wave, int lane) {
+  ConvRows r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (i * 8 + wave) * 8 + (lane >> 3);
+    const int m = m0 + row;
+    if (m < p.M) {
+      const int hw = p.cHo * p.cWo;
+      const int n = m / hw, rem = m - n * hw;
+      const int ho = rem / p.cWo, wo = rem - ho * p.cWo;
+      r.pix[i] = n * p.cH * p.cW;
+      r.hb[i] = ho * p.cStride - p.cPadH;
+      r.wb[i] = wo * p.cStride - p.cPadW;
+    } else {
+      r.pix[i] = -1; r.hb[i] = 0; r.wb[i] = 0;
+    }
+  }
+  return r;
+}
+
+// A tile (256 pixels x 64 channels of one filter tap) of K-tile k0, same LDS image as stage_r<256, true>
+__device__ __forceinline__ void stage_conv(const GemmArgs& p, const ConvRows& cr, int k0, char* img, int wave,
+                                           int lane) {
+  const int tap = k0 / p.cC, c0 = k0 - tap * p.cC;
+  const int kh = tap / p.cKW, kw = tap - kh * p.cKW;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = i * 8 + wave;
+    const int row = q * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ ((row >> 1) & 7);
+    const int hi = cr.hb[i] + kh * p.cDil, wi = cr.wb[i] + kw * p.cDil;
+    const bool ok = cr.pix[i] >= 0 && hi >= 0 && hi < p.cH && wi >= 0 && wi < p.cW;
+    const uint16_t* src = ok ? p.a + ((int64_t)(cr.pix[i] + hi * p.cW + wi) * p.cC + c0 + lc * 8) : p.zero + lc * 8;
+    glds16(src, img + q * 1024);
+  }
+}
+
+template <bool AK, bool BKM, bool CONV = false>
+__global__ __launch_bounds__(kThreads, 1) void gemm3s_kernel(GemmArgs p0) {
+  const GemmArgs p = split_view<AK, BKM>(p0);
   constexpr int BN = kBN3;
   constexpr int A_BYTES = kBM * kBK * 2;
   constexpr int B_BYTES = BN * kBK * 2;
@@ -563,9 +627,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm3s_kernel(GemmArgs p) {
     for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = p.K / kBK;
+  ConvRows cr;
+  if constexpr (CONV) cr = conv_rows(p, m0, wave, lane);
   auto stage_tile = [&](int t) {
     char* base = smem + (t % 3) * STAGE;
-    stage_r<kBM, AK>(p.a, p.lda, m0, p.M, t * kBK, base, wave, lane);
+    if constexpr (CONV) stage_conv(p, cr, t * kBK, base, wave, lane);
+    else stage_r<kBM, AK>(p.a, p.lda, m0, p.M, t * kBK, base, wave, lane);
     stage_r<BN, BKM>(p.b, p.ldb, n0, p.N, t * kBK, base + A_BYTES, wave, lane);
   };
 
@@ -647,23 +714,25 @@ __global__ __launch_bounds__(kThreads, 1) void gemm3s_kernel(GemmArgs p) {
   }
 }
 
-template <bool AK, bool BKM>
-int launch3s(const GemmArgs& a0, hipStream_t st) {
+template <bool AK, bool BKM, bool CONV = false>
+int launch3s(const GemmArgs& a0, int splits, hipStream_t st) {
   GemmArgs a = a0;
   a.tiles_m = (a.M + kBM - 1) / kBM;
   a.tiles_n = (a.N + kBN3 - 1) / kBN3;
   const int smem = 3 * (kBM + kBN3) * kBK * 2;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm3s_kernel<AK, BKM>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    (void)hipFuncSetAttribute((const void*)gemm3s_kernel<AK, BKM, CONV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              smem);
     attr_set = true;
   }
-  hipLaunchKernelGGL((gemm3s_kernel<AK, BKM>), dim3(a.tiles_m * a.tiles_n), dim3(kThreads), smem, st, a);
+  hipLaunchKernelGGL((gemm3s_kernel<AK, BKM, CONV>), dim3(a.tiles_m * a.tiles_n, splits), dim3(kThreads), smem, st,
+                     a);
   return (int)hipGetLastError();
 }
 
 template <bool AK, bool BKM>
-int launch256(const GemmArgs& a0, hipStream_t st) {
+int launch256(const GemmArgs& a0, int splits, hipStream_t st) {
   GemmArgs a = a0;
   a.tiles_m = (a.M + 255) / 256;
   a.tiles_n = (a.N + 255) / 256;
@@ -673,14 +742,14 @@ int launch256(const GemmArgs& a0, hipStream_t st) {
     hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKM>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr_set = true;
   }
-  hipLaunchKernelGGL((gemm256_kernel<AK, BKM>), dim3(a.tiles_m * a.tiles_n), dim3(kThreads), smem, st, a);
+  hipLaunchKernelGGL((gemm256_kernel<AK, BKM>), dim3(a.tiles_m * a.tiles_n, splits), dim3(kThreads), smem, st, a);
   return (int)hipGetLastError();
 }
 
 template <int BN, bool AK, bool BKM>
-int launch(const GemmArgs& a0, hipStream_t st) {
-  if constexpr (BN == 0) return launch256<AK, BKM>(a0, st);
-  if constexpr (BN == 160) return launch3s<AK, BKM>(a0, st);
+int launch(const GemmArgs& a0, int splits, hipStream_t st) {
+  if constexpr (BN == 0) return launch256<AK, BKM>(a0, splits, st);
+  if constexpr (BN == 160) return launch3s<AK, BKM>(a0, splits, st);
   GemmArgs a = a0;
   constexpr int BNk0 = BN == 0 ? 256 : BN;
   a.tiles_m = (a.M + kBM - 1) / kBM;
@@ -692,16 +761,16 @@ int launch(const GemmArgs& a0, hipStream_t st) {
     hipFuncSetAttribute((const void*)gemm_bf16_kernel<BNk, AK, BKM>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr_set = true;
   }
-  hipLaunchKernelGGL((gemm_bf16_kernel<BNk, AK, BKM>), dim3(a.tiles_m * a.tiles_n), dim3(kThreads), smem, st, a);
+  hipLaunchKernelGGL((gemm_bf16_kernel<BNk, AK, BKM>), dim3(a.tiles_m * a.tiles_n, splits), dim3(kThreads), smem, st, a);
   return (int)hipGetLastError();
 }
 
 template <int BN>
-int dispatch_layout(const GemmArgs& a, int a_kmajor, int b_kmajor, hipStream_t st) {
-  if (a_kmajor && !b_kmajor) return launch<BN, true, false>(a, st);
-  if (a_kmajor && b_kmajor) return launch<BN, true, true>(a, st);
-  if (!a_kmajor && !b_kmajor) return launch<BN, false, false>(a, st);
-  return launch<BN, false, true>(a, st);
+int dispatch_layout(const GemmArgs& a, int a_kmajor, int b_kmajor, int splits, hipStream_t st) {
+  if (a_kmajor && !b_kmajor) return launch<BN, true, false>(a, splits, st);
+  if (a_kmajor && b_kmajor) return launch<BN, true, true>(a, splits, st);
+  if (!a_kmajor && !b_kmajor) return launch<BN, false, false>(a, splits, st);
+  return launch<BN, false, true>(a, splits, st);
 }
 
 }  // namespace
@@ -711,20 +780,46 @@ int dispatch_layout(const GemmArgs& a, int a_kmajor, int b_kmajor, hipStream_t s
 // (lda, ldb % 8 == 0), M % 8 == 0 if A is MN-major, N % 8 == 0, ldc % 4 == 0.
 PA_EXPORT int pa_gemm_bf16(const void* a, const void* b, void* c, const void* bias, void* aux, int64_t M, int64_t N,
                            int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor, int b_kmajor, int flags,
-                           float alpha, int bn, hipStream_t st) {
-  if (K % kBK != 0 || N % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || ldc % 4 != 0) return 1;
+                           float alpha, int bn, int splits, hipStream_t st) {
+  // split-K (splits > 1): K is split into `splits` slices of K / splits elements; slice s writes fp32
+  // partials to c + s * M * ldc (no bias / activation / accumulate); the caller reduces the slabs.
+  if (splits < 1) splits = 1;
+  if (K % splits != 0) return 1;
+  const int64_t Kc = K / splits;
+  if (Kc % kBK != 0 || N % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || ldc % 4 != 0) return 1;
   if (!a_kmajor && M % 8 != 0) return 1;
+  if (splits > 1 && (flags & (kEpiBias | kEpiGelu | kEpiAux | kEpiAccum))) return 1;
+  if (splits > 1 && !(flags & kEpiOutF32)) return 1;
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   GemmArgs g{};
   g.a = (const uint16_t*)a; g.b = (const uint16_t*)b; g.c = c;
   g.bias = (const uint16_t*)bias; g.aux = (uint16_t*)aux;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
-  g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.M = (int)M; g.N = (int)N; g.K = (int)Kc;
   g.flags = flags; g.alpha = alpha;
+  g.c_split = M * ldc;
   // bn: 160 = three-stage 256x160 kernel; 256 / 128 = two-stage kernel with 256x256 / 256x128 tiles;
   // 1 = 4-phase ping-pong 256x256 kernel
-  if (bn == 160) return dispatch_layout<160>(g, a_kmajor, b_kmajor, st);
-  if (bn == 128) return dispatch_layout<128>(g, a_kmajor, b_kmajor, st);
-  if (bn == 1) return dispatch_layout<0>(g, a_kmajor, b_kmajor, st);
-  return dispatch_layout<256>(g, a_kmajor, b_kmajor, st);
+  if (bn == 160) return dispatch_layout<160>(g, a_kmajor, b_kmajor, splits, st);
+  if (bn == 128) return dispatch_layout<128>(g, a_kmajor, b_kmajor, splits, st);
+  if (bn == 1) return dispatch_layout<0>(g, a_kmajor, b_kmajor, splits, st);
+  return dispatch_layout<256>(g, a_kmajor, b_kmajor, splits, st);
+}
+
+// Implicit-GEMM NHWC convolution forward: out[N*Ho*Wo, Cout] = im2col(x) . W^T (+ bias), with
+// x [N, H, W, C] bf16 (C % 64 == 0), w [Cout, KH, KW, C] bf16 (channels-last filter), out NHWC bf16.
+// Runs on the 3-stage 256x160 kernel; `zero` is a >= 128-byte zeroed device buffer for padding taps.
+PA_EXPORT int pa_conv2d_nhwc_fwd(const void* x, const void* w, const void* bias, void* out, const void* zero, int N,
+                                 int H, int W, int C, int Cout, int KH, int KW, int stride, int pad_h, int pad_w,
+                                 int dil, int Ho, int Wo, hipStream_t st) {
+  if (C % kBK != 0 || Cout % 8 != 0 || N <= 0) return 1;
+  GemmArgs g{};
+  g.a = (const uint16_t*)x; g.b = (const uint16_t*)w; g.c = out; g.bias = (const uint16_t*)bias;
+  g.M = N * Ho * Wo; g.N = Cout; g.K = KH * KW * C;
+  g.lda = C; g.ldb = (int64_t)KH * KW * C; g.ldc = Cout;
+  g.flags = bias ? kEpiBias : 0; g.alpha = 1.f;
+  g.zero = (const uint16_t*)zero;
+  g.cH = H; g.cW = W; g.cC = C; g.cHo = Ho; g.cWo = Wo; g.cKW = KW; g.cStride = stride; g.cPadH = pad_h;
+  g.cPadW = pad_w; g.cDil = dil;
+  return launch3s<true, true, true>(g, 1, st);
 }

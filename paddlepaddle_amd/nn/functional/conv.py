@@ -82,16 +82,36 @@ def _convnd(n, x, weight, bias, stride, padding, dilation, groups, data_format):
     b = T(bias)
     if b is not None and b.dtype != w.dtype:
         b = b.to(w.dtype)
+    x_raw = t
     t, cl = _to_cf(t, data_format, n)
     stride = _tuple(stride, n)
     dilation = _tuple(dilation, n)
     pad, pre = _padding(padding, n, t.shape[2:], w.shape[2:], stride, dilation)
-    if pre is not None:
-        t = F.pad(t, pre)
-    if cl and n == 2 and not w.is_contiguous(memory_format=torch.channels_last):
-        w = w.contiguous(memory_format=torch.channels_last)
     fn = {1: F.conv1d, 2: F.conv2d, 3: F.conv3d}[n]
-    out = fn(t, w, b, stride, pad, dilation, groups)
+
+    def miopen(tt, ww):
+        if pre is not None:
+            tt = F.pad(tt, pre)
+        if cl and n == 2 and not ww.is_contiguous(memory_format=torch.channels_last):
+            ww = ww.contiguous(memory_format=torch.channels_last)
+        return fn(tt, ww, b, stride, pad, dilation, groups)
+
+    # NHWC 1x1 convolutions: hand-written MFMA GEMM (ops/conv.py) when it measured faster than MIOpen
+    if cl and n == 2 and pre is None and stride[0] == stride[1]:
+        from ... import ops as _ops
+        if (pad == 0 or pad == (0, 0)) and _ops.conv.eligible(x_raw, w, groups, True):
+            y = _ops.conv.conv1x1_nhwc(x_raw, w, b, stride[0],
+                                       lambda xx, ww: _from_cf(miopen(_to_cf(xx, data_format, n)[0], ww), cl, n))
+            if y is not None:
+                return _wrap(y)
+        elif (w.shape[2] > 1 or w.shape[3] > 1) and dilation[0] == dilation[1] and \
+                (isinstance(pad, int) or pad[0] == pad[1]) and _ops.conv.eligible_implicit(x_raw, w, groups):
+            pd = pad if isinstance(pad, int) else pad[0]
+            y = _ops.conv.conv_implicit_nhwc(x_raw, w, b, stride[0], pd, dilation[0],
+                                             lambda xx, ww: _from_cf(miopen(_to_cf(xx, data_format, n)[0], ww), cl, n))
+            if y is not None:
+                return _wrap(y)
+    out = miopen(t, w)
     return _wrap(_from_cf(out, cl, n))
 
 

@@ -1,0 +1,174 @@
+"""NHWC convolutions on the hand-written MFMA GEMM: 1x1 (forward and both gradients as GEMMs) and
+KxK implicit-GEMM forward.
+
+Reference: paddle/phi/kernels/gpu/conv_kernel.cu / conv_grad_kernel.cu (cuDNN). In NHWC a 1x1 convolution
+is a plain GEMM over the N*H*W pixel rows — no im2col:
+  forward  Y[P, Cout] = X[P, Cin] . W^T       (W [Cout, Cin] is the K-major B operand)
+  dgrad    dX[P, Cin] = dY[P, Cout] . W       (MN-major B)
+  wgrad    dW[Cout, Cin] = dY^T . X            (both operands MN-major, K = P split over workgroups)
+A stride-s 1x1 convolution subsamples X first (and scatters dX back). ResNet-50 has 16 such layers
+(bottleneck conv1/conv3 + the projection shortcuts). Each shape is timed once against the MIOpen path
+(forward + both gradients) and the faster one is kept (ops/gemm.py choose()).
+
+KxK (3x3, 7x7 with C % 64 == 0) forward: implicit GEMM on the 3-stage kernel (csrc/kernels/gemm.hip
+pa_conv2d_nhwc_fwd): every 64-deep K tile is one filter tap x 64 channels, so an A row is a contiguous
+128-byte channel slice of a shifted pixel, fetched straight to LDS by glds (taps in the padding read a
+zero page); the filter in channels-last [Cout, KH, KW, C] is the K-major B operand. Gradients use MIOpen.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _loader as L
+from . import gemm as G
+
+
+def _splits(M, N, K):
+    return G.pick_splits(M, N, K, bn=G._pick_bn(M, N, False))
+
+
+class _Conv1x1(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, stride):
+        N, H, W, Cin = x.shape
+        Cout = w.shape[0]
+        xs = x[:, ::stride, ::stride, :].contiguous() if stride > 1 else x
+        Ho, Wo = xs.shape[1], xs.shape[2]
+        x2 = xs.reshape(-1, Cin)
+        w2 = w.reshape(Cout, Cin)
+        y2 = G.gemm(x2, w2.t(), bias=b)
+        ctx.save_for_backward(x2, w2)
+        ctx.meta = (N, H, W, Cin, Cout, Ho, Wo, stride, b is not None)
+        return y2.view(N, Ho, Wo, Cout)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w2 = ctx.saved_tensors
+        N, H, W, Cin, Cout, Ho, Wo, stride, has_b = ctx.meta
+        dy2 = dy.reshape(-1, Cout)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx2 = G.gemm(dy2, w2)
+            dx = dx2.view(N, Ho, Wo, Cin)
+            if stride > 1:
+                full = torch.zeros(N, H, W, Cin, dtype=dx.dtype, device=dx.device)
+                full[:, ::stride, ::stride, :] = dx
+                dx = full
+        if ctx.needs_input_grad[1]:
+            P = dy2.shape[0]
+            if P % 64 == 0:
+                dw = G.gemm_splitk(dy2.t(), x2, _splits(Cout, Cin, P), out_dtype=w2.dtype)
+            else:  # pixel count not a multiple of the 64-deep K tile
+                dw = torch.mm(dy2.t(), x2)
+            dw = dw.view(Cout, Cin, 1, 1)
+        if has_b and ctx.needs_input_grad[2]:
+            db = dy2.float().sum(0).to(dy2.dtype)
+        return dx, dw, db, None
+
+
+def eligible(x_nhwc, w, groups, padding_is_zero, dilation_ok=True):
+    """Shape / layout conditions of the GEMM path for a 2-D NHWC convolution."""
+    if not (x_nhwc.is_cuda and x_nhwc.dtype == torch.bfloat16 and w.dtype == torch.bfloat16):
+        return False
+    if x_nhwc.dim() != 4 or w.dim() != 4 or tuple(w.shape[2:]) != (1, 1) or groups != 1 or not padding_is_zero:
+        return False
+    if not x_nhwc.is_contiguous() or not L.has("pa_gemm_bf16") or not L.hip_enabled_for(x_nhwc):
+        return False
+    cin, cout = x_nhwc.shape[3], w.shape[0]
+    return cin % 64 == 0 and cout % 64 == 0 and x_nhwc.numel() > 0  # K of forward / data-gradient GEMMs
+
+
+def conv1x1_nhwc(x, w, b, stride, fallback):
+    """x: [N, H, W, Cin] contiguous bf16; w: [Cout, Cin, 1, 1]; ``fallback()`` runs the MIOpen path and
+    returns the NHWC result. Picks the faster per shape (forward + backward timed once)."""
+    key = ("conv1x1", tuple(x.shape), w.shape[0], stride, b is not None, x.requires_grad or w.requires_grad)
+
+    def hip():
+        return _Conv1x1.apply(x, w, b, stride)
+
+    def _fb_bench(fn):
+        def run():
+            xx = x.detach().requires_grad_(True)
+            ww = w.detach().requires_grad_(True)
+            with torch.enable_grad():
+                y = fn(xx, ww)
+                y.backward(torch.ones_like(y))
+        return run
+    if key not in G._CHOICE and not G._capturing() and L.flag("FLAGS_gemm_backend", "auto") == "auto":
+        G.choose(key, {"hip": _fb_bench(lambda xx, ww: _Conv1x1.apply(xx, ww, b, stride)),
+                       "blas": _fb_bench(lambda xx, ww: fallback(xx, ww))})
+    ch = G.choose(key, {"hip": hip, "blas": lambda: None})
+    if ch == "hip":
+        return hip()
+    return None
+
+
+_ZERO = {}
+
+
+def _zero_page(dev):
+    z = _ZERO.get(dev)
+    if z is None:
+        z = _ZERO[dev] = torch.zeros(128, dtype=torch.bfloat16, device=dev)
+    return z
+
+
+class _ConvImplicit(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad, dil):
+        N, H, W, C = x.shape
+        Cout, _, KH, KW = w.shape
+        Ho = (H + 2 * pad - dil * (KH - 1) - 1) // stride + 1
+        Wo = (W + 2 * pad - dil * (KW - 1) - 1) // stride + 1
+        wk = w.permute(0, 2, 3, 1)
+        if not wk.is_contiguous():
+            wk = wk.contiguous()
+        out = torch.empty(N, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
+        L.call("pa_conv2d_nhwc_fwd", L.ptr(x), L.ptr(wk), L.ptr(b), L.ptr(out), L.ptr(_zero_page(x.device)), N, H, W,
+               C, Cout, KH, KW, stride, pad, pad, dil, Ho, Wo, L.stream_ptr())
+        ctx.save_for_backward(x, w)
+        ctx.cfg = (stride, pad, dil, b is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        stride, pad, dil, has_b = ctx.cfg
+        xc = x.permute(0, 3, 1, 2)
+        dyc = dy.permute(0, 3, 1, 2)
+        wc = w if w.is_contiguous(memory_format=torch.channels_last) else w.contiguous(memory_format=torch.channels_last)
+        mask = [ctx.needs_input_grad[0], ctx.needs_input_grad[1], has_b and ctx.needs_input_grad[2]]
+        gi, gw, gb = torch.ops.aten.convolution_backward(dyc, xc, wc, [w.shape[0]] if has_b else None, [stride] * 2,
+                                                         [pad] * 2, [dil] * 2, False, [0, 0], 1, mask)
+        dx = gi.permute(0, 2, 3, 1) if gi is not None else None
+        return dx, gw, gb, None, None, None
+
+
+def eligible_implicit(x_nhwc, w, groups):
+    if not (x_nhwc.is_cuda and x_nhwc.dtype == torch.bfloat16 and w.dtype == torch.bfloat16):
+        return False
+    if x_nhwc.dim() != 4 or w.dim() != 4 or groups != 1 or not x_nhwc.is_contiguous():
+        return False
+    if not L.has("pa_conv2d_nhwc_fwd") or not L.hip_enabled_for(x_nhwc):
+        return False
+    return x_nhwc.shape[3] % 64 == 0 and w.shape[0] % 8 == 0 and x_nhwc.numel() > 0
+
+
+def conv_implicit_nhwc(x, w, b, stride, pad, dil, fallback):
+    """KxK NHWC convolution: implicit-GEMM forward when it measured faster than MIOpen for this shape."""
+    key = ("convKxK", tuple(x.shape), tuple(w.shape), stride, pad, dil, b is not None)
+
+    def run(xx, ww):
+        return _ConvImplicit.apply(xx, ww, b, stride, pad, dil)
+    if key not in G._CHOICE and not G._capturing() and L.flag("FLAGS_gemm_backend", "auto") == "auto":
+        def fwd(fn):
+            def go():
+                with torch.no_grad():
+                    fn(x, w)
+            return go
+        G.choose(key, {"hip": fwd(run), "blas": fwd(fallback)})
+    if G.choose(key, {"hip": None, "blas": None}) == "hip":
+        return run(x, w)
+    return None

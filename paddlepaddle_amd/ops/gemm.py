@@ -74,8 +74,32 @@ def gemm(a, b, bias=None, gelu=False, aux=None, out=None, accumulate=False, alph
     if bn is None:
         bn = _pick_bn(M, N, bk)
     L.call("pa_gemm_bf16", L.ptr(a), L.ptr(b), L.ptr(out), L.ptr(bias), L.ptr(aux), M, N, K, lda, ldb, out.stride(0),
-           int(ak), int(bk), flags, float(alpha), int(bn), L.stream_ptr())
+           int(ak), int(bk), flags, float(alpha), int(bn), 1, L.stream_ptr())
     return out
+
+
+def gemm_splitk(a, b, splits, out_dtype=torch.bfloat16, bn=None):
+    """C = a @ b with K split over ``splits`` slices computed by separate workgroups (fp32 slabs, summed
+    here): fills the chip when M x N has few tiles but K is long (weight gradients of convolutions)."""
+    M, K = a.shape
+    N = b.shape[1]
+    lda, ak = _layout(a, 0)
+    ldb, bk = _layout(b, 1)
+    ws = torch.empty(splits, M, N, dtype=torch.float32, device=a.device)
+    if bn is None:
+        bn = _pick_bn(M, N, bk)
+    L.call("pa_gemm_bf16", L.ptr(a), L.ptr(b), L.ptr(ws), L.ptr(None), L.ptr(None), M, N, K, lda, ldb, N,
+           int(ak), int(bk), EPI_OUT_F32, 1.0, int(bn), int(splits), L.stream_ptr())
+    return ws.sum(0, dtype=torch.float32).to(out_dtype) if splits > 1 else ws[0].to(out_dtype)
+
+
+def pick_splits(M, N, K, bn=256, cus=256, max_ws_bytes=256 << 20):
+    """Largest power-of-two split keeping K-slices a multiple of 64 that brings the grid to ~2 waves."""
+    tiles = -(-M // 256) * -(-N // bn)
+    s = 1
+    while tiles * s * 2 <= 2 * cus and K % (s * 2 * 64) == 0 and (s * 2) * M * N * 4 <= max_ws_bytes:
+        s *= 2
+    return s
 
 
 def _pick_bn(M, N, b_kmajor, cus=256):

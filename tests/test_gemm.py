@@ -68,3 +68,47 @@ def test_gemm_large_gpt_shape():
     ref = _ref(a, b)
     err = (c.float() - ref).abs().max().item()
     assert err < 0.25 + 1e-2 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("bn", [256, 128])
+def test_gemm_splitk_wgrad_layout(bn):
+    # conv-style weight gradient: few output tiles, long K split over workgroups
+    P, Cout, Cin = 4096, 64, 256
+    g = torch.Generator(device=DEV).manual_seed(5)
+    dy = torch.randn(P, Cout, device=DEV, generator=g).to(torch.bfloat16)
+    x = torch.randn(P, Cin, device=DEV, generator=g).to(torch.bfloat16)
+    out = G.gemm_splitk(dy.t(), x, 8, out_dtype=torch.float32, bn=bn)
+    ref = dy.float().t() @ x.float()
+    torch.testing.assert_close(out, ref, atol=0.05, rtol=1e-3)
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_conv1x1_nhwc_gemm_path(stride):
+    from paddlepaddle_amd.ops import conv as C
+    torch.manual_seed(0)
+    x = torch.randn(4, 16, 16, 128, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    w = (torch.randn(192, 128, 1, 1, device=DEV) * 0.05).to(torch.bfloat16).requires_grad_(True)
+    assert C.eligible(x, w, 1, True)
+    y = C._Conv1x1.apply(x, w, None, stride)
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(xr, wr, None, stride).permute(0, 2, 3, 1)
+    torch.testing.assert_close(y.float(), yr, atol=0.05, rtol=2e-2)
+    gy = torch.randn_like(yr)
+    y.backward(gy.to(torch.bfloat16))
+    yr.backward(gy)
+    torch.testing.assert_close(x.grad.float(), xr.grad.permute(0, 2, 3, 1), atol=0.05, rtol=2e-2)
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=0.5, rtol=2e-2)
+
+
+@pytest.mark.parametrize("k,stride,pad", [(3, 1, 1), (3, 2, 1), (1, 1, 0), (5, 1, 2)])
+def test_conv_implicit_gemm_fwd(k, stride, pad):
+    from paddlepaddle_amd.ops import conv as C
+    torch.manual_seed(1)
+    x = torch.randn(3, 13, 11, 64, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(72, 64, k, k, device=DEV) * 0.05).to(torch.bfloat16)
+    b = torch.randn(72, device=DEV).to(torch.bfloat16)
+    assert C.eligible_implicit(x, w, 1)
+    y = C._ConvImplicit.apply(x, w, b, stride, pad, 1)
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float(), b.float(), stride, pad)
+    torch.testing.assert_close(y.float(), ref.permute(0, 2, 3, 1), atol=0.06, rtol=2e-2)
