@@ -115,19 +115,28 @@ def _zero_page(dev):
     return z
 
 
+def _implicit_fwd(x, wk, b, N, H, W, C, Cout, KH, KW, stride, pad, dil):
+    Ho = (H + 2 * pad - dil * (KH - 1) - 1) // stride + 1
+    Wo = (W + 2 * pad - dil * (KW - 1) - 1) // stride + 1
+    out = torch.empty(N, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
+    L.call("pa_conv2d_nhwc_fwd", L.ptr(x), L.ptr(wk), L.ptr(b), L.ptr(out), L.ptr(_zero_page(x.device)), N, H, W,
+           C, Cout, KH, KW, stride, pad, pad, dil, Ho, Wo, L.stream_ptr())
+    return out
+
+
 class _ConvImplicit(torch.autograd.Function):
+    """Forward: implicit GEMM. Data gradient (stride 1, no dilation): the same implicit GEMM over dY with
+    the filter flipped and its channel axes swapped (W'[c, kh, kw, co] = W[co, KH-1-kh, KW-1-kw, c]),
+    padding KH-1-pad. Weight gradient and the strided data gradient: MIOpen."""
+
     @staticmethod
     def forward(ctx, x, w, b, stride, pad, dil):
         N, H, W, C = x.shape
         Cout, _, KH, KW = w.shape
-        Ho = (H + 2 * pad - dil * (KH - 1) - 1) // stride + 1
-        Wo = (W + 2 * pad - dil * (KW - 1) - 1) // stride + 1
         wk = w.permute(0, 2, 3, 1)
         if not wk.is_contiguous():
             wk = wk.contiguous()
-        out = torch.empty(N, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
-        L.call("pa_conv2d_nhwc_fwd", L.ptr(x), L.ptr(wk), L.ptr(b), L.ptr(out), L.ptr(_zero_page(x.device)), N, H, W,
-               C, Cout, KH, KW, stride, pad, pad, dil, Ho, Wo, L.stream_ptr())
+        out = _implicit_fwd(x, wk, b, N, H, W, C, Cout, KH, KW, stride, pad, dil)
         ctx.save_for_backward(x, w)
         ctx.cfg = (stride, pad, dil, b is not None)
         return out
@@ -136,13 +145,25 @@ class _ConvImplicit(torch.autograd.Function):
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         stride, pad, dil, has_b = ctx.cfg
+        N, H, W, C = x.shape
+        Cout, _, KH, KW = w.shape
+        dy = dy.contiguous()
+        dx = None
+        own_dx = (ctx.needs_input_grad[0] and stride == 1 and dil == 1 and Cout % 64 == 0 and C % 8 == 0
+                  and 2 * pad <= KH - 1 + pad and KH == KW)
+        if own_dx:
+            # [C, KH, KW, Cout] flipped filter (K-major B operand of the transposed convolution)
+            wt = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()
+            Ho, Wo = dy.shape[1], dy.shape[2]
+            dx = _implicit_fwd(dy, wt, None, N, Ho, Wo, Cout, C, KH, KW, 1, KH - 1 - pad, 1)
         xc = x.permute(0, 3, 1, 2)
         dyc = dy.permute(0, 3, 1, 2)
         wc = w if w.is_contiguous(memory_format=torch.channels_last) else w.contiguous(memory_format=torch.channels_last)
-        mask = [ctx.needs_input_grad[0], ctx.needs_input_grad[1], has_b and ctx.needs_input_grad[2]]
+        mask = [ctx.needs_input_grad[0] and not own_dx, ctx.needs_input_grad[1], has_b and ctx.needs_input_grad[2]]
         gi, gw, gb = torch.ops.aten.convolution_backward(dyc, xc, wc, [w.shape[0]] if has_b else None, [stride] * 2,
                                                          [pad] * 2, [dil] * 2, False, [0, 0], 1, mask)
-        dx = gi.permute(0, 2, 3, 1) if gi is not None else None
+        if gi is not None:
+            dx = gi.permute(0, 2, 3, 1)
         return dx, gw, gb, None, None, None
 
 
@@ -158,17 +179,23 @@ def eligible_implicit(x_nhwc, w, groups):
 
 def conv_implicit_nhwc(x, w, b, stride, pad, dil, fallback):
     """KxK NHWC convolution: implicit-GEMM forward when it measured faster than MIOpen for this shape."""
-    key = ("convKxK", tuple(x.shape), tuple(w.shape), stride, pad, dil, b is not None)
+    key = ("convKxK", tuple(x.shape), tuple(w.shape), stride, pad, dil, b is not None,
+           x.requires_grad or w.requires_grad)
 
     def run(xx, ww):
         return _ConvImplicit.apply(xx, ww, b, stride, pad, dil)
+
+    def bench(fn):
+        def go():
+            xx = x.detach().requires_grad_(x.requires_grad)
+            ww = w.detach().requires_grad_(w.requires_grad)
+            with torch.enable_grad():
+                y = fn(xx, ww)
+                if y.requires_grad:
+                    y.backward(torch.ones_like(y))
+        return go
     if key not in G._CHOICE and not G._capturing() and L.flag("FLAGS_gemm_backend", "auto") == "auto":
-        def fwd(fn):
-            def go():
-                with torch.no_grad():
-                    fn(x, w)
-            return go
-        G.choose(key, {"hip": fwd(run), "blas": fwd(fallback)})
+        G.choose(key, {"hip": bench(run), "blas": bench(fallback)})
     if G.choose(key, {"hip": None, "blas": None}) == "hip":
         return run(x, w)
     return None

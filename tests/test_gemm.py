@@ -112,3 +112,20 @@ def test_conv_implicit_gemm_fwd(k, stride, pad):
     y = C._ConvImplicit.apply(x, w, b, stride, pad, 1)
     ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float(), b.float(), stride, pad)
     torch.testing.assert_close(y.float(), ref.permute(0, 2, 3, 1), atol=0.06, rtol=2e-2)
+
+
+@pytest.mark.parametrize("k,pad", [(3, 1), (5, 2), (3, 0)])
+def test_conv_implicit_gemm_dgrad(k, pad):
+    from paddlepaddle_amd.ops import conv as C
+    torch.manual_seed(2)
+    x = torch.randn(2, 9, 10, 64, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    w = (torch.randn(128, 64, k, k, device=DEV) * 0.05).to(torch.bfloat16).requires_grad_(True)
+    y = C._ConvImplicit.apply(x, w, None, 1, pad, 1)
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(xr, wr, None, 1, pad)
+    g = torch.randn_like(yr)
+    y.backward(g.permute(0, 2, 3, 1).to(torch.bfloat16))
+    yr.backward(g)
+    torch.testing.assert_close(x.grad.float(), xr.grad.permute(0, 2, 3, 1), atol=0.08, rtol=2e-2)
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=0.5, rtol=3e-2)
