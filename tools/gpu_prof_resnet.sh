@@ -1,0 +1,2 @@
+#!/bin/bash
+bash "$(dirname "$0")/gpu_prof.sh" resnet50_r1c --skip-gpt 1 --resnet-steps 10
