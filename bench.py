@@ -30,7 +30,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--model", default="gpt3-13b", help="gpt3-13b | gpt3-6.7b | gpt3-1.3b | tiny")
+    p.add_argument("--model", default="gpt3-13b",
+                   help="gpt3-13b | gpt3-6.7b | gpt3-1.3b | tiny | llama2-70b | llama2-13b | llama2-7b | llama-tiny")
+    p.add_argument("--pp", type=int, default=1, help="pipeline degree (LLaMA pipeline path)")
+    p.add_argument("--vpp", type=int, default=1, help="virtual pipeline stages per rank (interleaved 1F1B)")
     p.add_argument("--micro-batch", type=int, default=2)
     p.add_argument("--accum", type=int, default=8, help="gradient accumulation steps per optimizer step")
     p.add_argument("--seq-len", type=int, default=2048)
@@ -152,6 +155,63 @@ def gpt_bench(args, paddle, world, dist_on):
     return tps, dt / args.steps * 1000, B * args.accum * world, mfu
 
 
+def llama_bench(args, paddle, world, dist_on):
+    """LLaMA-2 pre-training with fleet hybrid parallel: PP (1F1B / interleaved) x TP x DP, bf16 AMP-O2 params,
+    fused AdamW with fp32 master weights. BASELINE config: LLaMA-2 70B PP4 x TP2 on 8 MI355X."""
+    from paddlepaddle_amd.distributed import fleet
+    from paddlepaddle_amd.models.llama import LlamaConfig, LlamaForCausalLMPipe
+    pp, tp = args.pp, args.tp
+    if world % (pp * tp):
+        raise SystemExit(f"world {world} is not a multiple of pp*tp = {pp * tp}")
+    dp = world // (pp * tp)
+    st = fleet.DistributedStrategy()
+    st.hybrid_configs = dict(dp_degree=dp, mp_degree=tp, pp_degree=pp)
+    st.pipeline_configs = {"accumulate_steps": args.accum, "micro_batch_size": args.micro_batch}
+    fleet.init(is_collective=True, strategy=st)
+    presets = {"llama2-70b": LlamaConfig.llama2_70b, "llama2-13b": LlamaConfig.llama2_13b,
+               "llama2-7b": LlamaConfig.llama2_7b, "llama-tiny": LlamaConfig.tiny}
+    cfg = presets[args.model](max_position_embeddings=max(args.seq_len, 128), tensor_parallel_degree=tp,
+                              use_recompute=bool(args.recompute))
+    paddle.set_default_dtype("bfloat16")
+    paddle.seed(1234)
+    model = LlamaForCausalLMPipe(cfg, num_stages=pp, num_virtual_pipeline_stages=args.vpp if args.vpp > 1 else None,
+                                 recompute_interval=1 if args.recompute else 0)
+    paddle.set_default_dtype("float32")
+    opt = paddle.optimizer.AdamW(learning_rate=1e-4, parameters=model.parameters(), weight_decay=0.01,
+                                 multi_precision=True, grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0))
+    model = fleet.distributed_model(model)
+    opt = fleet.distributed_optimizer(opt)
+    dev = _dev()
+    gb = args.micro_batch * args.accum
+    gen = torch.Generator(device=dev).manual_seed(7 + fleet.get_hybrid_communicate_group().get_data_parallel_rank())
+    data = torch.randint(0, cfg.vocab_size, (gb, args.seq_len + 1), device=dev, generator=gen)
+    x, y = paddle.Tensor(data[:, :-1].contiguous()), paddle.Tensor(data[:, 1:].contiguous())
+    state = {}
+
+    if pp > 1:
+        def step():
+            state["loss"] = model.train_batch([x, y], opt)
+    else:  # no pipeline: plain gradient accumulation over the same PipelineLayer
+        mbs = [(paddle.Tensor(c), paddle.Tensor(d)) for c, d in zip(x._t.chunk(args.accum), y._t.chunk(args.accum))]
+        crit = model._layers._loss_fn if hasattr(model, "_layers") else model._loss_fn
+
+        def step():
+            for xi, yi in mbs:
+                loss = crit(model(xi), yi) * (1.0 / args.accum)
+                loss.backward()
+            opt.step()
+            opt.clear_grad()
+            state["loss"] = loss
+
+    dt = timed(step, args.steps, args.warmup, dist_on)
+    tokens = args.steps * gb * dp * args.seq_len
+    tps = tokens / dt
+    mfu = tps * cfg.flops_per_token(args.seq_len) / (PEAK_BF16 * world)
+    log(f"[llama] {args.model} pp{pp} tp{tp} dp{dp}: loss={float(state['loss']):.4f} step={dt / args.steps * 1000:.1f}ms "
+        f"tokens/s={tps:.0f} MFU={mfu * 100:.1f}%")
+    return tps, dt / args.steps * 1000, gb * dp, mfu
+
+
 def resnet_bench(args, paddle, world, dist_on):
     from paddlepaddle_amd.vision.models import resnet50
     paddle.seed(99)
@@ -197,12 +257,18 @@ def main():
     elif torch.cuda.is_available() and os.environ.get("PADDLE_AMD_FORCE_CPU", "0") != "1":
         torch.cuda.set_device(0)
     tps = step_ms = gb = mfu = None
-    if not args.skip_gpt:
+    is_llama = args.model.startswith("llama")
+    if is_llama:
+        tps, step_ms, gb, mfu = llama_bench(args, paddle, world, dist_on)
+        args.resnet = 0
+    elif not args.skip_gpt:
         tps, step_ms, gb, mfu = gpt_bench(args, paddle, world, dist_on)
     ips = resnet_bench(args, paddle, world, dist_on) if args.resnet else None
     if int(os.environ.get("RANK", "0")) == 0:
         par = (f"sharding_stage{args.sharding_stage}_degree{world}" if args.sharding_stage else f"dp{world}") + \
               (f"_tp{args.tp}" if args.tp > 1 else "")
+        if is_llama:
+            par = f"pp{args.pp}_tp{args.tp}_dp{world // (args.pp * args.tp)}" + (f"_vpp{args.vpp}" if args.vpp > 1 else "")
         line = {
             "metric": BASELINE_METRIC,
             "value": round(tps, 1) if tps is not None else None,
@@ -217,7 +283,8 @@ def main():
             "dtype": "bf16",
             "data": "synthetic tokens/images, random-init weights",
             "config": {"model": f"GPT-3 {args.model.split('-')[-1].upper()} (h5120 L40 a40 ffn20480 V50304)"
-                       if args.model == "gpt3-13b" else args.model,
+                       if args.model == "gpt3-13b" else args.model.replace("llama2-", "LLaMA-2 ").upper()
+                       if is_llama else args.model,
                        "global_batch": gb, "seq_len": args.seq_len, "micro_batch": args.micro_batch,
                        "accum_steps": args.accum, "parallelism": par, "recompute": bool(args.recompute),
                        "optimizer": "AdamW fp32-master fused HIP", "amp": "O2 bf16"},

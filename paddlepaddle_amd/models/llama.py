@@ -309,3 +309,61 @@ class LlamaPretrainingCriterion(nn.Layer):
             per_tok = _ops.softmax_cross_entropy(lt, labels._t, self.ignore_index)
         valid = (labels._t != self.ignore_index).sum().clamp_min(1)
         return _wrap(per_tok.sum() / valid)
+
+
+# ----------------------------------------------------------------------------------------- pipeline
+class LlamaEmbeddingPipe(nn.Layer):
+    """First pipeline segment: token ids -> hidden states (vocab-parallel under TP)."""
+
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        init = nn.ParamAttr(initializer=I.Normal(0.0, cfg.initializer_range))
+        if cfg.tensor_parallel_degree > 1:
+            self.embed_tokens = _tp().VocabParallelEmbedding(cfg.vocab_size, cfg.hidden_size, weight_attr=init)
+        else:
+            self.embed_tokens = nn.Embedding(cfg.vocab_size, cfg.hidden_size, weight_attr=init)
+
+    def forward(self, input_ids):
+        return self.embed_tokens(input_ids)
+
+
+class LlamaDecoderLayerPipe(LlamaDecoderLayer):
+    def forward(self, x):
+        return super().forward(x)
+
+
+class LlamaHeadPipe(nn.Layer):
+    """Last pipeline segment: final RMSNorm + LM head (vocab-sharded logits under TP)."""
+
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.config = cfg
+        self.norm = LlamaRMSNorm(cfg)
+        tp = max(cfg.tensor_parallel_degree, 1)
+        self.lm_head_weight = self.create_parameter([cfg.vocab_size // tp, cfg.hidden_size],
+                                                    default_initializer=I.Normal(0.0, cfg.initializer_range))
+        if tp > 1:
+            self.lm_head_weight.is_distributed = True
+
+    def forward(self, x):
+        h = self.norm(x)
+        w = self.lm_head_weight
+        ht = h._t if h._t.dtype == w._t.dtype else h._t.to(w._t.dtype)
+        if self.config.tensor_parallel_degree > 1:
+            ht = _tp().c_identity(ht)
+        return _wrap(torch.matmul(ht, w._t.t()))
+
+
+def LlamaForCausalLMPipe(cfg: LlamaConfig, num_stages=None, num_virtual_pipeline_stages=None, seg_method="uniform",
+                         recompute_interval=0):
+    """LLaMA as a PipelineLayer (reference: PaddleNLP LlamaForCausalLMPipe, built from LayerDescs):
+    [embedding] + L x [decoder layer] + [norm + lm head], loss = LlamaPretrainingCriterion. Composes with
+    tensor parallelism (cfg.tensor_parallel_degree) and interleaved virtual stages: the PP4 x TP2 layout of
+    the 70B config puts 20 decoder layers and 8.75B parameters on each MI355X."""
+    from ..parallel.pipeline import LayerDesc, PipelineLayer
+    descs = [LayerDesc(LlamaEmbeddingPipe, cfg)]
+    descs += [LayerDesc(LlamaDecoderLayerPipe, cfg) for _ in range(cfg.num_hidden_layers)]
+    descs.append(LayerDesc(LlamaHeadPipe, cfg))
+    return PipelineLayer(descs, num_stages=num_stages, loss_fn=LlamaPretrainingCriterion(cfg), seg_method=seg_method,
+                         recompute_interval=recompute_interval,
+                         num_virtual_pipeline_stages=num_virtual_pipeline_stages)

@@ -34,3 +34,17 @@ def test_bench_two_ranks_json_line():
     assert d["n_gpus"] == 2 and d["steps"] == 2 and d["value"] > 0 and d["dtype"] == "bf16"
     assert d["config"]["parallelism"] == "sharding_stage3_degree2"
     assert d["secondary"]["value"] > 0
+
+
+def test_bench_llama_pipeline_x_tp_four_ranks():
+    env = dict(os.environ, PADDLE_AMD_FORCE_CPU="1", PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "4", "--model",
+           "llama-tiny", "--pp", "2", "--tp", "2", "--steps", "2", "--warmup", "1", "--seq-len", "32",
+           "--micro-batch", "1", "--accum", "4"]
+    r = subprocess.run(cmd, env=env, capture_output=True, timeout=600, cwd="/tmp")
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    lines = [l for l in r.stdout.decode().splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 4 and d["value"] > 0 and d["config"]["parallelism"] == "pp2_tp2_dp1"

@@ -332,3 +332,65 @@ def test_pipeline_interleaved_matches_single_process():
     assert set(got) == set(ref_params)
     for k in ref_params:
         np.testing.assert_allclose(got[k], ref_params[k], rtol=1e-4, atol=1e-6, err_msg=k)
+
+
+# ----------------------------------------------------------------------------- llama PP x TP (4 ranks)
+def _pipe_to_full_name(stage_layer_index, name, n_layers):
+    """Parameter name of a LlamaForCausalLMPipe segment layer -> LlamaForCausalLM name."""
+    i = stage_layer_index
+    if i == 0:
+        return "llama." + name                      # embed_tokens.weight
+    if i == n_layers + 1:
+        return "llama.norm.weight" if name.startswith("norm.") else "lm_head_weight"
+    return f"llama.layers.{i - 1}." + name
+
+
+def _llama_pp_tp_worker(rank, world, port, q):
+    paddle = _setup(rank, world, port)
+    from paddlepaddle_amd.models.llama import (LlamaConfig, LlamaForCausalLM, LlamaForCausalLMPipe)
+    paddle.seed(4)
+    cfg1 = LlamaConfig.tiny(num_hidden_layers=2)
+    full = LlamaForCausalLM(cfg1)
+    full_sd = {k: v._t.detach().clone() for k, v in full.state_dict().items()}
+    fleet = _fleet_init(paddle, acc=2, mp_degree=2, pp_degree=2)
+    hcg = fleet.get_hybrid_communicate_group()
+    mp_rank = hcg.get_model_parallel_rank()
+    cfg = LlamaConfig.tiny(num_hidden_layers=2, tensor_parallel_degree=2)
+    pipe = LlamaForCausalLMPipe(cfg)
+    with torch.no_grad():
+        for j, f in enumerate(pipe.run_function):
+            li = pipe.segment_parts[pipe._stage_id] + j
+            for k, v in f.state_dict().items():
+                fk = _pipe_to_full_name(li, k, cfg.num_hidden_layers)
+                v._t.copy_(_llama_tp_shard(fk, full_sd[fk], mp_rank, 2, cfg))
+    opt = paddle.optimizer.SGD(0.05, parameters=pipe.parameters())
+    model = fleet.distributed_model(pipe)
+    ids = torch.randint(0, cfg.vocab_size, (4, 17), generator=torch.Generator().manual_seed(9))
+    x, y = paddle.Tensor(ids[:, :-1].clone()), paddle.Tensor(ids[:, 1:].clone())
+    losses = [float(model.train_batch([x, y], opt)) for _ in range(2)]
+    q.put((rank, losses))
+    paddle.distributed.barrier()
+
+
+def test_llama_pipeline_x_tensor_parallel_matches_single_process():
+    sys.path.insert(0, ROOT)
+    os.environ["PADDLE_AMD_FORCE_CPU"] = "1"
+    import paddlepaddle_amd as paddle
+    from paddlepaddle_amd.models.llama import LlamaConfig, LlamaForCausalLM, LlamaPretrainingCriterion
+    paddle.seed(4)
+    cfg = LlamaConfig.tiny(num_hidden_layers=2)
+    model, crit = LlamaForCausalLM(cfg), LlamaPretrainingCriterion(cfg)
+    opt = paddle.optimizer.SGD(0.05, parameters=model.parameters())
+    ids = torch.randint(0, cfg.vocab_size, (4, 17), generator=torch.Generator().manual_seed(9))
+    ref = []
+    for _ in range(2):
+        l0 = crit(model(paddle.Tensor(ids[:2, :-1].clone())), paddle.Tensor(ids[:2, 1:].clone()))
+        l1 = crit(model(paddle.Tensor(ids[2:, :-1].clone())), paddle.Tensor(ids[2:, 1:].clone()))
+        loss = (l0 + l1) * 0.5
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        ref.append(float(loss))
+    res = _spawn(_llama_pp_tp_worker, world=4)
+    for _, l in res:
+        np.testing.assert_allclose(l, ref, rtol=1e-4, atol=1e-5)
