@@ -111,14 +111,14 @@ __device__ __forceinline__ int mn_swz(int k) { return ((k & 3) | (((k >> 3) & 1)
 
 // ---- staging of one operand tile (R rows of the output dimension x 64 k) into LDS
 // K-major: image [R][64] (128-B rows).  MN-major: image [64][R] (2R-byte rows).
-template <int R, bool KMAJ>
+template <int R, bool KMAJ, int NW = 8>
 __device__ __forceinline__ void stage(const uint16_t* __restrict__ g, int64_t ld, int r0, int rmax, int k0,
                                       char* img, int wave, int lane) {
-  constexpr int NQ = R / 64;  // glds instructions per thread (R*64*2 bytes / (512 * 16))
+  constexpr int NQ = R / (8 * NW);  // glds instructions per thread (R*64*2 bytes / (NW * 64 * 16))
   if constexpr (KMAJ) {
 #pragma unroll
     for (int i = 0; i < NQ; ++i) {
-      const int q = i * 8 + wave;               // wave-instruction id: 8 rows x 128 B
+      const int q = i * NW + wave;              // wave-instruction id: 8 rows x 128 B
       const int row = q * 8 + (lane >> 3);
       const int lc = (lane & 7) ^ ((row >> 1) & 7);
       int gr = r0 + row;
@@ -129,7 +129,7 @@ __device__ __forceinline__ void stage(const uint16_t* __restrict__ g, int64_t ld
     constexpr int CPR = R / 8;  // 16-B chunks per k-row
 #pragma unroll
     for (int i = 0; i < NQ; ++i) {
-      const int q = i * 8 + wave;
+      const int q = i * NW + wave;
       const int lin = q * 64 + lane;
       const int row = lin / CPR;                // k
       const int lc = (lin % CPR) ^ mn_swz(row);
@@ -164,18 +164,22 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-template <int BN, bool AK, bool BKM>
-__global__ __launch_bounds__(kThreads, 1) void gemm_bf16_kernel(GemmArgs p0) {
+// NW = 8: waves 2 (M) x 4 (N), wave tile 128 x BN/4, 2 waves per SIMD.
+// NW = 4: waves 2 (M) x 2 (N), wave tile 128 x BN/2 (256 accumulator registers, 1 wave per SIMD):
+//         a third less LDS read traffic per MFMA than the 8-wave form.
+template <int BN, bool AK, bool BKM, int NW = 8>
+__global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmArgs p0) {
   const GemmArgs p = split_view<AK, BKM>(p0);
+  constexpr int WN = NW / 2;
   constexpr int A_BYTES = kBM * kBK * 2;
   constexpr int B_BYTES = BN * kBK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int MR = (kBM / 2) / 16;  // 8 m-fragments per wave
-  constexpr int NR = (BN / 4) / 16;   // n-fragments per wave
+  constexpr int NR = (BN / WN) / 16;  // n-fragments per wave
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave / WN, wn = wave % WN;
 
   // tile order: XCD-contiguous chunks, grouped by 8 m-tiles so neighbours share B panels
   const int nwg = p.tiles_m * p.tiles_n;
@@ -198,8 +202,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_kernel(GemmArgs p0) {
   const int nk = p.K / kBK;
   auto stage_tile = [&](int t, int buf) {
     char* base = smem + buf * STAGE;
-    stage<kBM, AK>(p.a, p.lda, m0, p.M, t * kBK, base, wave, lane);
-    stage<BN, BKM>(p.b, p.ldb, n0, p.N, t * kBK, base + A_BYTES, wave, lane);
+    stage<kBM, AK, NW>(p.a, p.lda, m0, p.M, t * kBK, base, wave, lane);
+    stage<BN, BKM, NW>(p.b, p.ldb, n0, p.N, t * kBK, base + A_BYTES, wave, lane);
   };
 
   stage_tile(0, 0);
@@ -215,7 +219,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_kernel(GemmArgs p0) {
     for (int s = 0; s < 2; ++s) {
       bf16x8_t bf[NR];
 #pragma unroll
-      for (int j = 0; j < NR; ++j) bf[j] = frag<BN, BKM>(bimg, wn * (BN / 4) + j * 16, s, lane);
+      for (int j = 0; j < NR; ++j) bf[j] = frag<BN, BKM>(bimg, wn * (BN / WN) + j * 16, s, lane);
 #pragma unroll
       for (int i = 0; i < MR; ++i) {
         const bf16x8_t af = frag<kBM, AK>(aimg, wm * (kBM / 2) + i * 16, s, lane);
@@ -231,7 +235,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_bf16_kernel(GemmArgs p0) {
   // ---- epilogue: lane holds C[m = mb + i*16 + (lane&15)][n = nb + j*16 + 4*(lane>>4) + 0..3]
   const int flags = p.flags;
   const int mrow0 = m0 + wm * (kBM / 2) + (lane & 15);
-  const int ncol0 = n0 + wn * (BN / 4) + 4 * (lane >> 4);
+  const int ncol0 = n0 + wn * (BN / WN) + 4 * (lane >> 4);
 #pragma unroll
   for (int j = 0; j < NR; ++j) {
     const int n = ncol0 + j * 16;
@@ -751,17 +755,19 @@ int launch(const GemmArgs& a0, int splits, hipStream_t st) {
   if constexpr (BN == 0) return launch256<AK, BKM>(a0, splits, st);
   if constexpr (BN == 160) return launch3s<AK, BKM>(a0, splits, st);
   GemmArgs a = a0;
-  constexpr int BNk0 = BN == 0 ? 256 : BN;
+  constexpr int NW = BN == 4 ? 4 : 8;                  // BN code 4: 256x256 tile with 4 waves
+  constexpr int BNk = (BN == 0 || BN == 4) ? 256 : BN;
   a.tiles_m = (a.M + kBM - 1) / kBM;
-  a.tiles_n = (a.N + BNk0 - 1) / BNk0;
-  constexpr int BNk = BN == 0 ? 256 : BN;
+  a.tiles_n = (a.N + BNk - 1) / BNk;
   const int smem = 2 * (kBM + BNk) * kBK * 2;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)gemm_bf16_kernel<BNk, AK, BKM>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BNk, AK, BKM, NW>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr_set = true;
   }
-  hipLaunchKernelGGL((gemm_bf16_kernel<BNk, AK, BKM>), dim3(a.tiles_m * a.tiles_n, splits), dim3(kThreads), smem, st, a);
+  hipLaunchKernelGGL((gemm_bf16_kernel<BNk, AK, BKM, NW>), dim3(a.tiles_m * a.tiles_n, splits), dim3(NW * 64), smem,
+                     st, a);
   return (int)hipGetLastError();
 }
 
@@ -803,6 +809,7 @@ PA_EXPORT int pa_gemm_bf16(const void* a, const void* b, void* c, const void* bi
   if (bn == 160) return dispatch_layout<160>(g, a_kmajor, b_kmajor, splits, st);
   if (bn == 128) return dispatch_layout<128>(g, a_kmajor, b_kmajor, splits, st);
   if (bn == 1) return dispatch_layout<0>(g, a_kmajor, b_kmajor, splits, st);
+  if (bn == 4) return dispatch_layout<4>(g, a_kmajor, b_kmajor, splits, st);
   return dispatch_layout<256>(g, a_kmajor, b_kmajor, splits, st);
 }
 

@@ -28,7 +28,7 @@ def _ref(a, b):
 
 @pytest.mark.parametrize("a_kmaj", [True, False])
 @pytest.mark.parametrize("b_kmaj", [True, False])
-@pytest.mark.parametrize("bn", [160, 256, 128, 1])
+@pytest.mark.parametrize("bn", [160, 256, 128, 1, 4])
 @pytest.mark.parametrize("M,N,K", [(512, 512, 256), (264, 392, 128), (1000, 776, 320)])
 def test_gemm_layouts(a_kmaj, b_kmaj, bn, M, N, K):
     a, b = _operands(M, N, K, a_kmaj, b_kmaj)

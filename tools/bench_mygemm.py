@@ -20,7 +20,7 @@ def timeit(fn, iters=20):
     return s.elapsed_time(e) / iters
 
 
-VARIANTS = {160: "3s-160", 256: "2st-256", 128: "2st-128"}
+VARIANTS = {4: "4w-256", 256: "2st-256", 160: "3s-160"}
 
 
 def main():
