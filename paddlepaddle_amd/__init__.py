@@ -185,3 +185,6 @@ def block_diag(inputs, name=None):
 
 
 from . import sysconfig  # noqa: F401,E402
+from .tensor import _bind_reference_extras as _bre  # noqa: E402
+from .tensor.search import top_p_sampling  # noqa: F401,E402
+_bre()

@@ -73,3 +73,24 @@ def collect_operator_stats():
 
 def compare_accuracy(dump_path, another_dump_path, output_filename, loss_scale=1, dump_all_tensors=False):
     raise NotImplementedError("compare_accuracy needs paddle dump files; not produced by this framework")
+
+
+def check_layer_numerics(func):
+    """Decorator for a Layer.forward: checks its tensor inputs and outputs for NaN / Inf
+    (reference amp/debugging.py check_layer_numerics)."""
+    import functools
+
+    @functools.wraps(func)
+    def wrapper(self, *args, **kwargs):
+        from ..framework.tensor import Tensor
+        name = type(self).__name__
+        for i, a in enumerate(args):
+            if isinstance(a, Tensor) and a._t.is_floating_point():
+                check_numerics(a, name, f"input_{i}", DebugMode.CHECK_NAN_INF_AND_ABORT)
+        out = func(self, *args, **kwargs)
+        outs = out if isinstance(out, (list, tuple)) else [out]
+        for i, o in enumerate(outs):
+            if isinstance(o, Tensor) and o._t.is_floating_point():
+                check_numerics(o, name, f"output_{i}", DebugMode.CHECK_NAN_INF_AND_ABORT)
+        return out
+    return wrapper

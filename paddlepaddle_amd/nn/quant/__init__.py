@@ -38,3 +38,18 @@ def weight_only_linear(x, weight, bias=None, weight_scale=None, weight_dtype="in
 
 def llm_int8_linear(x, weight, bias=None, weight_scale=None, threshold=6.0):
     return weight_only_linear(x, weight, bias, weight_scale)
+
+
+from ..layer.layers import Layer as _Layer  # noqa: E402
+
+
+class Stub(_Layer):
+    """Placeholder in a model's forward that QAT / PTQ replace with the configured observer / quanter
+    (reference nn/quant/stub.py); identity until then."""
+
+    def __init__(self, observer=None):
+        super().__init__()
+        self._observer = observer
+
+    def forward(self, input):
+        return input

@@ -111,3 +111,35 @@ Tensor.__matmul__ = _matmul_amp
 Tensor.__rmatmul__ = lambda self, other: math.matmul(other, self)
 
 _bind_methods()
+
+
+def _bind_reference_extras():
+    """Functions the reference also exposes as Tensor methods (tensor_method_func) although they take
+    several tensors or none: x.concat([y]) etc. follow the function signatures."""
+    import paddlepaddle_amd as _p
+    from .. import signal as _signal
+    for name in ("create_parameter", "create_tensor", "multiplex", "block_diag", "add_n", "broadcast_shape",
+                 "is_tensor", "concat", "scatter_nd", "stack", "rank", "broadcast_tensors", "polar"):
+        fn = getattr(_p, name, None)
+        if fn is not None and not hasattr(Tensor, name):
+            setattr(Tensor, name, fn)
+    if not hasattr(Tensor, "top_p_sampling"):
+        Tensor.top_p_sampling = search.top_p_sampling
+    if not hasattr(Tensor, "stft"):
+        Tensor.stft = _signal.stft
+        Tensor.istft = _signal.istft
+
+    def set_(self, source=None, shape=None, stride=None, offset=0, name=None):
+        """Make this tensor share ``source``'s storage (optionally as a strided view)."""
+        import torch
+        if source is None:
+            self._t = torch.empty(0, dtype=self._t.dtype, device=self._t.device)
+            return self
+        src = source._t if isinstance(source, Tensor) else torch.as_tensor(source)
+        if shape is not None:
+            src = src.as_strided(list(shape), list(stride) if stride is not None else
+                                 torch.empty(list(shape)).stride(), offset)
+        self._t = src
+        return self
+    if not hasattr(Tensor, "set_"):
+        Tensor.set_ = set_

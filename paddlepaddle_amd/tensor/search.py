@@ -94,3 +94,35 @@ def index_of_max(x):
 def masked_argmax(x, mask, axis=-1):
     t = T(x).masked_fill(~T(mask), float("-inf"))
     return _wrap(torch.argmax(t, axis))
+
+
+def top_p_sampling(x, ps, threshold=None, topp_seed=None, seed=-1, k=0, mode="truncated", return_top=False,
+                   name=None):
+    """Nucleus sampling over probabilities x [B, V] with per-row top-p ``ps`` [B] (reference
+    tensor/search.py top_p_sampling): returns (scores [B, 1], ids [B, 1]) and, with return_top, the top-k
+    (scores, ids). ``threshold`` drops candidates below a per-row probability; ``k`` > 0 caps the candidate
+    count; ``seed`` >= 0 makes the draw reproducible."""
+    import torch
+    from ..framework.tensor import _wrap
+    p = x._t.float()
+    pp = ps._t.float().reshape(-1, 1)
+    sp, si = p.sort(-1, descending=True)
+    keep = (sp.cumsum(-1) - sp) < pp
+    keep[:, 0] = True
+    if threshold is not None:
+        keep &= sp >= threshold._t.float().reshape(-1, 1)
+        keep[:, 0] = True
+    if k and k > 0:
+        keep[:, k:] = False
+    w = sp * keep
+    g = None
+    if seed is not None and seed >= 0:
+        g = torch.Generator(device=p.device).manual_seed(int(seed))
+    pick = torch.multinomial(w / w.sum(-1, keepdim=True), 1, generator=g)
+    ids = si.gather(1, pick)
+    scores = p.gather(1, ids).to(x._t.dtype)
+    out = (_wrap(scores), _wrap(ids.to(torch.int64)))
+    if return_top:
+        kk = max(int(k), 1)
+        out = out + (_wrap(sp[:, :kk].to(x._t.dtype)), _wrap(si[:, :kk]))
+    return out

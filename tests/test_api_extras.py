@@ -119,3 +119,21 @@ def test_reference_all_coverage(mod):
     m = importlib.import_module("paddlepaddle_amd" + ("." + mod if mod else ""))
     missing = [n for n in names if not hasattr(m, n)]
     assert not missing, f"paddle.{mod} missing {missing}"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference checkout not mounted")
+def test_reference_tensor_methods_coverage():
+    names = None
+    for node in ast.parse(open(os.path.join(REF, "tensor", "__init__.py")).read()).body:
+        if isinstance(node, ast.Assign) and any(getattr(t, "id", None) == "tensor_method_func" for t in node.targets):
+            names = [e.value for e in node.value.elts]
+    missing = [n for n in names if not hasattr(paddle.Tensor, n)]
+    assert not missing, missing
+
+
+def test_top_p_sampling_respects_nucleus():
+    x = paddle.to_tensor([[0.05, 0.6, 0.3, 0.05]] * 64)
+    _, ids = paddle.top_p_sampling(x, paddle.to_tensor([0.5] * 64), seed=3)
+    assert set(ids.numpy().ravel().tolist()) == {1}
+    _, ids = paddle.top_p_sampling(x, paddle.to_tensor([0.85] * 64), seed=3)
+    assert set(ids.numpy().ravel().tolist()) <= {1, 2}
