@@ -57,6 +57,28 @@ __device__ __forceinline__ int img_off(int row, int ch) {
   return row * (NCH * 16) + 16 * (ch ^ (sw & (NCH - 1)));
 }
 
+// Workgroup barrier that orders LDS only: waits for this wave's LDS ops (lgkmcnt) but leaves global
+// memory ops in flight. __syncthreads() would also drain vmcnt, i.e. wait for the fire-and-forget dQ
+// atomics of the previous query block at every step (they have no consumer inside the kernel).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Global loads the compiler does not track (see fa_bwd_kernel): the caller waits with a counted vmcnt.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 gload16_async(const void* p) {
+  u32x4 r;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+__device__ __forceinline__ float gload4_async(const float* p) {
+  float r;
+  asm volatile("global_load_dword %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+
 __device__ __forceinline__ uint4 lds_b128(const char* smem, int off) {
   return *reinterpret_cast<const uint4*>(smem + off);
 }
@@ -398,49 +420,71 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
   // Q / dO / LSE / delta of the next query block are prefetched into registers while the current
   // block computes (async-stage split): the HBM latency is hidden behind ~40 MFMAs per wave.
   constexpr int QLOADS = BM * NCH / 256;
-  uint4 qreg[QLOADS], dreg[QLOADS];
+  u32x4 qreg[QLOADS], dreg[QLOADS];
   float lse_r = -INFINITY, dlt_r = 0.f;
   const float inv_scale = 1.f / p.scale;
   // dQ accumulator of this (b, h) as a buffer resource: 32-bit offsets, no 64-bit address math per atomic
   const __amdgpu_buffer_rsrc_t dq_rsrc = __builtin_amdgcn_make_buffer_rsrc(
       dqb, 0, (int)((int64_t)(p.Sq - 1) * p.H * D * 4 + D * 4), 0x00020000);
+  // The prefetch loads are issued from inline asm so that hipcc does not track them: at the loop top the
+  // kernel waits with a counted vmcnt that leaves the previous block's 16 fire-and-forget dQ atomics
+  // (issued after these loads) in flight, instead of the vmcnt(0) the compiler would emit.
+  // Loads are unconditional (rows clamped into range, zeroed after the wait): an asm result written
+  // under a divergent branch could be merged by a register copy before the data has arrived.
+  float lse_raw = 0.f, dlt_raw = 0.f;
+  bool row_ok = false;
+  bool q_ok[QLOADS];
   auto prefetch = [&](int q0) {
 #pragma unroll
     for (int i = 0; i < QLOADS; ++i) {
       const int idx = tid + 256 * i;
       const int row = idx / NCH, ch = idx % NCH;
       const int qx = q0 + row;
-      qreg[i] = make_uint4(0, 0, 0, 0);
-      dreg[i] = make_uint4(0, 0, 0, 0);
-      if (qx < p.Sq) {
-        qreg[i] = *reinterpret_cast<const uint4*>(qbase + (int64_t)qx * p.qs[1] + ch * 8);
-        dreg[i] = *reinterpret_cast<const uint4*>(dobase + (int64_t)qx * p.dos[1] + ch * 8);
-      }
+      q_ok[i] = qx < p.Sq;
+      const int qc = q_ok[i] ? qx : p.Sq - 1;
+      qreg[i] = gload16_async(qbase + (int64_t)qc * p.qs[1] + ch * 8);
+      dreg[i] = gload16_async(dobase + (int64_t)qc * p.dos[1] + ch * 8);
     }
-    if (tid < BM) {
-      // row constants enter the S / dP accumulators as their initial values:
-      // S' = Q K^T - LSE/scale  ->  P = exp2(scale*log2e * S');   dP' = dO V^T - delta  ->  dS = P * dP'
-      const int qx = q0 + tid;
-      lse_r = qx < p.Sq ? -lse_b[qx] * inv_scale : -INFINITY;
-      dlt_r = qx < p.Sq ? -dlt_b[qx] : 0.f;
-    }
+    const int qx = q0 + (tid & (BM - 1));
+    row_ok = qx < p.Sq;
+    const int qc = row_ok ? qx : p.Sq - 1;
+    lse_raw = gload4_async(lse_b + qc);
+    dlt_raw = gload4_async(dlt_b + qc);
   };
   if (q_begin < p.Sq) prefetch(q_begin);
+  const bool has_atomics = w < NDT;  // waves that own a dQ d-tile issue 16 atomics per block
 
   for (int q0 = q_begin; q0 < p.Sq; q0 += BM) {
-    __syncthreads();  // previous iteration's LDS reads done
+    if (q0 == q_begin || !has_atomics) {
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(qreg[0]), "+v"(dreg[0]), "+v"(lse_raw), "+v"(dlt_raw)::"memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(16)" : "+v"(qreg[0]), "+v"(dreg[0]), "+v"(lse_raw), "+v"(dlt_raw)::"memory");
+    }
+    if constexpr (QLOADS > 1) asm volatile("" : "+v"(qreg[QLOADS - 1]), "+v"(dreg[QLOADS - 1]));
+#pragma unroll
+    for (int i = 0; i < QLOADS; ++i) {
+      if (!q_ok[i]) {
+        qreg[i] = u32x4{0u, 0u, 0u, 0u};
+        dreg[i] = u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+    // row constants enter the S / dP accumulators as their initial values:
+    // S' = Q K^T - LSE/scale  ->  P = exp2(scale*log2e * S');   dP' = dO V^T - delta  ->  dS = P * dP'
+    lse_r = row_ok ? -lse_raw * inv_scale : -INFINITY;
+    dlt_r = row_ok ? -dlt_raw : 0.f;
+    lds_barrier();  // previous iteration's LDS reads done
 #pragma unroll
     for (int i = 0; i < QLOADS; ++i) {
       const int idx = tid + 256 * i;
       const int row = idx / NCH, ch = idx % NCH;
-      *reinterpret_cast<uint4*>(q_lds + img_off<NCH>(row, ch)) = qreg[i];
-      *reinterpret_cast<uint4*>(do_lds + img_off<NCH>(row, ch)) = dreg[i];
+      *reinterpret_cast<u32x4*>(q_lds + img_off<NCH>(row, ch)) = qreg[i];
+      *reinterpret_cast<u32x4*>(do_lds + img_off<NCH>(row, ch)) = dreg[i];
     }
     if (tid < BM) {
       lse_s[tid] = lse_r;
       dlt_s[tid] = dlt_r;
     }
-    __syncthreads();
+    lds_barrier();
     if (q0 + BM < p.Sq) prefetch(q0 + BM);
 
     // S' = Q K^T - LSE/scale and dP' = dO V^T - delta : rows q (registers), cols = this lane's key.
@@ -515,7 +559,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
         *reinterpret_cast<uint2*>(rowp + (((16 * s + 8 + 4 * hf) * 2) ^ sw)) = make_uint2(f.u.z, f.u.w);
       }
     }
-    __syncthreads();
+    lds_barrier();
     // dQ[q][d] += sum_key dS[q][key] K[key][d] ; wave w handles d tiles dt = w, w+4, ...
     for (int dt = w; dt < NDT; dt += 4) {
       f32x16 qacc = zero16();
