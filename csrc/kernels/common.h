@@ -36,9 +36,13 @@ __device__ __forceinline__ float bf16_bits_to_f(uint32_t b) { return __uint_as_f
 __device__ __forceinline__ float lo_bf16(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float hi_bf16(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
+// one v_cvt_pk_bf16_f32 (RNE, NaN-preserving) for the pair; the scalar __float2bfloat16 form costs
+// two converts + a shift + an OR per pair
+typedef float pa_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 pa_bf16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
-  bf16 x = __float2bfloat16(a), y = __float2bfloat16(b);
-  return (uint32_t)(*reinterpret_cast<uint16_t*>(&x)) | ((uint32_t)(*reinterpret_cast<uint16_t*>(&y)) << 16);
+  const pa_f32x2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, pa_bf16x2));
 }
 __device__ __forceinline__ uint32_t pack_f16(float a, float b) {
   f16 x = __float2half(a), y = __float2half(b);
