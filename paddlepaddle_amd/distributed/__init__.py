@@ -12,6 +12,7 @@ from .auto_parallel import (ProcessMesh, Shard, Replicate, Partial, Placement, R
 from . import auto_parallel  # noqa: F401
 from ..parallel.data_parallel import DataParallel  # noqa: F401,E402
 from .extras import *  # noqa: F401,F403,E402
+from .watchdog import enable_comm_watchdog, disable_comm_watchdog  # noqa: F401,E402
 
 
 def __getattr__(name):

@@ -172,6 +172,10 @@ def init_parallel_env(backend=None, timeout_s=1800):
         if backend == "nccl" and use_gpu:
             kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
         dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        wd = os.environ.get("PADDLE_AMD_COMM_WATCHDOG")
+        if wd:
+            from .watchdog import enable_comm_watchdog
+            enable_comm_watchdog(timeout_s=float(wd), report_dir=os.environ.get("PADDLE_AMD_COMM_WATCHDOG_DIR"))
     ws = dist.get_world_size()
     _default_group = Group(dist.get_rank(), 0, list(range(ws)), None, "_default_pg")
     _groups[0] = _default_group
