@@ -184,7 +184,7 @@ def block_diag(inputs, name=None):
     return _w(_t.block_diag(*ts))
 
 
-from . import sysconfig  # noqa: F401,E402
+from . import sysconfig, hub, reader, dataset, base, _C_ops, _legacy_C_ops  # noqa: F401,E402
 from .tensor import _bind_reference_extras as _bre  # noqa: E402
 from .tensor.search import top_p_sampling  # noqa: F401,E402
 _bre()

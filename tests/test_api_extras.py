@@ -137,3 +137,31 @@ def test_top_p_sampling_respects_nucleus():
     assert set(ids.numpy().ravel().tolist()) == {1}
     _, ids = paddle.top_p_sampling(x, paddle.to_tensor([0.85] * 64), seed=3)
     assert set(ids.numpy().ravel().tolist()) <= {1, 2}
+
+
+def test_legacy_reader_decorators():
+    r = paddle.reader.compose(lambda: iter([1, 2, 3]), lambda: iter([(4,), (5,), (6,)]))
+    assert list(r()) == [(1, 4), (2, 5), (3, 6)]
+    assert list(paddle.reader.chain(lambda: iter([1]), lambda: iter([2, 3]))()) == [1, 2, 3]
+    assert sorted(paddle.reader.buffered(lambda: iter(range(5)), 2)()) == list(range(5))
+    assert list(paddle.reader.xmap_readers(lambda x: x + 1, lambda: iter(range(8)), 3, 4, order=True)()) == \
+        list(range(1, 9))
+    c = paddle.reader.cache(lambda: iter([7, 8]))
+    assert list(c()) == [7, 8] and list(c()) == [7, 8]
+
+
+def test_hub_local(tmp_path):
+    (tmp_path / "hubconf.py").write_text("def tiny(scale=1):\n    '''tiny model'''\n    return scale * 3\n")
+    assert "tiny" in paddle.hub.list(str(tmp_path), source="local")
+    assert paddle.hub.help(str(tmp_path), "tiny", source="local") == "tiny model"
+    assert paddle.hub.load(str(tmp_path), "tiny", source="local", scale=2) == 6
+
+
+def test_c_ops_and_base_namespaces():
+    out = paddle._C_ops.add(paddle.ones([2]), paddle.ones([2]))
+    np.testing.assert_array_equal(out.numpy(), [2, 2])
+    x = paddle.ones([2])
+    paddle._C_ops.scale_(x, 3.0)
+    np.testing.assert_array_equal(x.numpy(), [3, 3])
+    assert paddle.base.framework.in_dygraph_mode()
+    assert paddle.base.Program is paddle.static.Program
