@@ -152,19 +152,41 @@ class LlamaAttention(nn.Layer):
     def forward(self, x, cache=None, pos=0):
         q, k, v = self._qkv(x)
         B, S = q.shape[0], q.shape[1]
+        if cache is not None and isinstance(pos, torch.Tensor):
+            return self._decode_step(q, k, v, cache, pos)
         cos, sin = self.rope.tables(pos + S, q.device)
         q = _ops.apply_rotary(q, cos[pos:pos + S], sin[pos:pos + S])
         k = _ops.apply_rotary(k, cos[pos:pos + S], sin[pos:pos + S])
         if cache is not None:
+            # cache layout [B, Hkv, max_len, D] (the decode kernel's dense layout); prefill reads it back
+            # as a strided [B, S, Hkv, D] view
             kc, vc = cache
-            kc[:B, pos:pos + S].copy_(k)
-            vc[:B, pos:pos + S].copy_(v)
-            k, v = kc[:B, :pos + S], vc[:B, :pos + S]
+            kc[:B, :, pos:pos + S].copy_(k.transpose(1, 2))
+            vc[:B, :, pos:pos + S].copy_(v.transpose(1, 2))
+            k, v = kc[:B, :, :pos + S].transpose(1, 2), vc[:B, :, :pos + S].transpose(1, 2)
             causal = S > 1
         else:
             causal = True
         o = _ops.flash_attention(q, k, v, causal=causal)
         return self.o_proj(_wrap(o.reshape(B, S, self.H * self.D)))
+
+    def _decode_step(self, q, k, v, cache, pos_t):
+        """One token per sequence at the device-side position ``pos_t`` ([1] int64): no host value is
+        read, so the step can be captured once into a hipGraph and replayed for every token. RoPE rows
+        are gathered at pos_t, K/V are scattered into the dense cache at pos_t, and attention is the
+        flash-decoding HIP kernel over the first pos_t + 1 cached tokens."""
+        kc, vc = cache
+        B = q.shape[0]
+        Lc = kc.shape[2]
+        cos, sin = self.rope.tables(Lc, q.device)
+        cs, sn = cos.index_select(0, pos_t), sin.index_select(0, pos_t)
+        q = _ops.apply_rotary(q, cs, sn)
+        k = _ops.apply_rotary(k, cs, sn)
+        kc[:B].index_copy_(2, pos_t, k.transpose(1, 2))
+        vc[:B].index_copy_(2, pos_t, v.transpose(1, 2))
+        lens = (pos_t + 1).to(torch.int32).expand(B).contiguous()
+        o = _ops.dense_decode_attention(q.reshape(B, self.H, self.D), kc[:B], vc[:B], lens, max_len=Lc)
+        return self.o_proj(_wrap(o.reshape(B, 1, self.H * self.D)))
 
 
 class LlamaMLP(nn.Layer):
@@ -255,16 +277,22 @@ class LlamaForCausalLM(nn.Layer):
         cfg = self.config
         p = next(iter(self.parameters()))
         Hkv = max(cfg.num_key_value_heads // max(cfg.tensor_parallel_degree, 1), 1)
-        shape = (batch, max_length, Hkv, cfg.head_dim)
+        max_length = -(-max_length // 64) * 64  # whole 64-token blocks for the decode kernel
+        shape = (batch, Hkv, max_length, cfg.head_dim)
         return [(torch.zeros(shape, dtype=p._t.dtype, device=p._t.device),
                  torch.zeros(shape, dtype=p._t.dtype, device=p._t.device)) for _ in range(cfg.num_hidden_layers)]
 
     @torch.no_grad()
     def generate(self, input_ids, max_new_tokens=16, decode_strategy="greedy_search", temperature=1.0, top_k=0,
-                 top_p=1.0, eos_token_id=None):
-        """Prefill once, then one token per step against the KV cache. Returns (ids, scores)."""
+                 top_p=1.0, eos_token_id=None, use_graph=False):
+        """Prefill once, then one token per step against the KV cache. Returns (ids, scores).
+        ``use_graph`` (greedy, HIP device): the decode step is captured once into a hipGraph and replayed
+        per token — decode is launch-bound at serving batch sizes, the graph turns ~15 launches per layer
+        into one submission per token."""
         ids = input_ids._t
         B, S = ids.shape
+        if use_graph and decode_strategy == "greedy_search" and ids.is_cuda:
+            return self._generate_graph(ids, max_new_tokens, eos_token_id)
         caches = self.new_cache(B, S + max_new_tokens)
         logits = self.forward(_wrap(ids), caches, 0)._t[:, -1].float()
         out, scores = [], []
@@ -292,6 +320,51 @@ class LlamaForCausalLM(nn.Layer):
             if bool(done.all()) or t == max_new_tokens - 1:
                 break
             logits = self.forward(_wrap(nxt[:, None]), caches, S + t)._t[:, -1].float()
+        return _wrap(torch.stack(out, 1)), _wrap(torch.stack(scores, 1))
+
+
+    def _decode_logits(self, tok, caches, pos_t):
+        x = self.llama.embed_tokens(_wrap(tok))
+        for i, layer in enumerate(self.llama.layers):
+            x = layer(x, caches[i], pos_t)
+        return self._logits(self.llama.norm(x))._t[:, -1].float()
+
+    def _generate_graph(self, ids, max_new_tokens, eos_token_id):
+        B, S = ids.shape
+        caches = self.new_cache(B, S + max_new_tokens)
+        logits = self.forward(_wrap(ids), caches, 0)._t[:, -1].float()
+        eos = self.config.eos_token_id if eos_token_id is None else eos_token_id
+        tok = torch.empty(B, 1, dtype=ids.dtype, device=ids.device)
+        pos_t = torch.zeros(1, dtype=torch.int64, device=ids.device)
+        out, scores = [], []
+        done = torch.zeros(B, dtype=torch.bool, device=ids.device)
+
+        def take(lg):
+            nxt = lg.argmax(-1)
+            scores.append(torch.log_softmax(lg, -1).gather(-1, nxt[:, None]).squeeze(-1))
+            nxt = torch.where(done, torch.full_like(nxt, self.config.pad_token_id), nxt)
+            out.append(nxt)
+            done.logical_or_(nxt == eos)
+            return nxt
+
+        nxt = take(logits)
+        if max_new_tokens > 1:
+            tok.copy_(nxt[:, None])
+            pos_t.fill_(S)
+            # warm up once eagerly on a side stream (allocator / kernel choices settle), then capture
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                self._decode_logits(tok, caches, pos_t)
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                static_logits = self._decode_logits(tok, caches, pos_t)
+            for t in range(1, max_new_tokens):
+                tok.copy_(nxt[:, None])
+                pos_t.fill_(S + t - 1)
+                g.replay()
+                nxt = take(static_logits)
         return _wrap(torch.stack(out, 1)), _wrap(torch.stack(scores, 1))
 
 
