@@ -779,6 +779,103 @@ int dispatch_layout(const GemmArgs& a, int a_kmajor, int b_kmajor, int splits, h
   return launch<BN, false, true>(a, splits, st);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Small-M GEMM for decode (serving): C[M <= 64, N] = A[M, K] . B[K, N] with A K-major (activations,
+// a few rows) and B MN-major (paddle's [in, out] weights, streamed once). The work is bandwidth-bound
+// on B, so the kernel is built around keeping many weight bytes in flight: 4 waves, tile 64 x 128, K
+// split over gridDim.y, a 4-deep LDS ring filled by glds (3 K-tiles = 72 KiB per CU in flight), one
+// barrier per K-tile. Rows >= M are clamped reads whose results are never stored. Each split writes an
+// fp32 slab; pa_gemm_small_m_reduce sums the slabs (+ bias) into bf16.
+constexpr int kSmBM = 64, kSmBN = 128, kSmNW = 4, kSmStages = 4;
+
+__global__ __launch_bounds__(kSmNW * 64, 1) void gemm_small_m_kernel(const uint16_t* __restrict__ a, int64_t lda,
+                                                                    const uint16_t* __restrict__ b, int64_t ldb,
+                                                                    float* __restrict__ ws, int M, int N, int k_per) {
+  constexpr int A_BYTES = kSmBM * kBK * 2, B_BYTES = kSmBN * kBK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int NL = kSmBM / (8 * kSmNW) + kSmBN / (8 * kSmNW);  // glds per thread per K-tile (2 + 4)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int n0 = blockIdx.x * kSmBN;
+  const int ks = blockIdx.y;
+  const uint16_t* ap = a + (int64_t)ks * k_per;
+  const uint16_t* bp = b + (int64_t)ks * k_per * ldb;
+  const int nk = k_per / kBK;
+
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto stage_tile = [&](int t) {
+    char* base = smem + (t % kSmStages) * STAGE;
+    stage<kSmBM, true, kSmNW>(ap, lda, 0, M, t * kBK, base, wave, lane);
+    stage<kSmBN, false, kSmNW>(bp, ldb, n0, N, t * kBK, base + A_BYTES, wave, lane);
+  };
+  const int pro = min(kSmStages - 1, nk);
+  for (int t = 0; t < pro; ++t) stage_tile(t);
+  // wait for tile 0: (pro - 1) tiles may stay in flight
+  if (pro >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NL) : "memory");
+  else if (pro == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  bar();
+
+#pragma unroll 1
+  for (int t = 0; t < nk; ++t) {
+    if (t + kSmStages - 1 < nk) stage_tile(t + kSmStages - 1);
+    const char* aimg = smem + (t % kSmStages) * STAGE;
+    const char* bimg = aimg + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8_t bf[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[j] = frag<kSmBN, false>(bimg, wave * 32 + j * 16, s, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bf16x8_t af = frag<kSmBM, true>(aimg, i * 16, s, lane);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af, acc[i][j], 0, 0, 0);
+      }
+    }
+    // retire tile t+1 (tiles issued after it may stay in flight)
+    const int after = min(nk - 1, t + kSmStages - 1) - (t + 1);
+    if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NL) : "memory");
+    else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+  }
+  // lane holds C[m = i*16 + (lane&15)][n = n0 + wave*32 + j*16 + 4*(lane>>4) + 0..3]
+  float* out = ws + (int64_t)ks * M * N;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = i * 16 + (lane & 15);
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wave * 32 + j * 16 + 4 * (lane >> 4);
+      if (n < N)
+        *reinterpret_cast<float4*>(out + (int64_t)m * N + n) =
+            make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void gemm_small_m_reduce_k(const float* __restrict__ ws, const uint16_t* __restrict__ bias,
+                                                            uint16_t* __restrict__ c, int64_t ldc, int M, int N,
+                                                            int splits) {
+  const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i4 >= (int64_t)M * N) return;
+  const int m = (int)(i4 / N), n = (int)(i4 % N);
+  float4 acc = *reinterpret_cast<const float4*>(ws + i4);
+  for (int s = 1; s < splits; ++s) {
+    const float4 v = *reinterpret_cast<const float4*>(ws + (int64_t)s * M * N + i4);
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  if (bias) {
+    const uint2 braw = *reinterpret_cast<const uint2*>(bias + n);
+    acc.x += lo_bf16(braw.x); acc.y += hi_bf16(braw.x); acc.z += lo_bf16(braw.y); acc.w += hi_bf16(braw.y);
+  }
+  *reinterpret_cast<uint2*>(c + (int64_t)m * ldc + n) = make_uint2(pack_bf16(acc.x, acc.y), pack_bf16(acc.z, acc.w));
+}
+
 }  // namespace
 
 // C = epi(alpha * A.B). A: [M][K] (a_kmajor) or [K][M]; B: [N][K] (b_kmajor) or [K][N].
@@ -829,4 +926,23 @@ PA_EXPORT int pa_conv2d_nhwc_fwd(const void* x, const void* w, const void* bias,
   g.cH = H; g.cW = W; g.cC = C; g.cHo = Ho; g.cWo = Wo; g.cKW = KW; g.cStride = stride; g.cPadH = pad_h;
   g.cPadW = pad_w; g.cDil = dil;
   return launch3s<true, true, true>(g, 1, st);
+}
+
+// Decode-shape GEMM: c[M, N] (bf16, row stride ldc) = a[M, K] (K-major) . b[K, N] (N-major) (+ bias),
+// M <= 64, K % (64 * splits) == 0, N % 8 == 0; `ws` = fp32 workspace of splits * M * N floats.
+PA_EXPORT int pa_gemm_small_m(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc,
+                              const void* bias, float* ws, int M, int N, int K, int splits, hipStream_t st) {
+  if (M < 1 || M > kSmBM || N % 8 != 0 || splits < 1 || K % (kBK * splits) != 0 || lda % 8 || ldb % 8) return 1;
+  const int smem = kSmStages * (kSmBM + kSmBN) * kBK * 2;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm_small_m_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(gemm_small_m_kernel, dim3((N + kSmBN - 1) / kSmBN, splits), dim3(kSmNW * 64), smem, st,
+                     (const uint16_t*)a, lda, (const uint16_t*)b, ldb, ws, M, N, K / splits);
+  const int64_t n4 = (int64_t)M * N / 4;
+  hipLaunchKernelGGL(gemm_small_m_reduce_k, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, ws,
+                     (const uint16_t*)bias, (uint16_t*)c, ldc, M, N, splits);
+  return (int)hipGetLastError();
 }

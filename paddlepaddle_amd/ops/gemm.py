@@ -161,3 +161,32 @@ def choose(key, candidates):
 def choices():
     """The tuned decisions so far: {key: backend} (for logs / profiles)."""
     return dict(_CHOICE)
+
+
+# ---------------------------------------------------------------------------------------------
+# Decode-shape GEMM (M <= 64 rows x a weight in paddle's [in, out] layout): bandwidth-bound on the
+# weight, so the kernel streams it with a 4-deep glds ring and splits K over workgroups to fill the chip.
+def small_m_supported(a, b):
+    if a.dim() != 2 or b.dim() != 2 or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
+        return False
+    if not L.has("pa_gemm_small_m") or not L.hip_enabled_for(a):
+        return False
+    M, K = a.shape
+    N = b.shape[1]
+    return (1 <= M <= 64 and a.stride(1) == 1 and a.stride(0) % 8 == 0 and b.stride(1) == 1 and b.stride(0) % 8 == 0
+            and N % 8 == 0 and K % 64 == 0 and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0)
+
+
+def gemm_small_m(a, b, bias=None, splits=None, cus=256):
+    M, K = a.shape
+    N = b.shape[1]
+    if splits is None:
+        blocks = -(-N // 128)
+        splits = 1
+        while blocks * splits * 2 <= 2 * cus and K % (64 * splits * 2) == 0 and K // (splits * 2) >= 256:
+            splits *= 2
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    ws = torch.empty(splits * M * N, dtype=torch.float32, device=a.device)
+    L.call("pa_gemm_small_m", L.ptr(a), a.stride(0), L.ptr(b), b.stride(0), L.ptr(out), out.stride(0), L.ptr(bias),
+           L.ptr(ws), M, N, K, int(splits), L.stream_ptr())
+    return out
