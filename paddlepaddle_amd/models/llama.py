@@ -178,15 +178,25 @@ class LlamaAttention(nn.Layer):
         kc, vc = cache
         B = q.shape[0]
         Lc = kc.shape[2]
-        cos, sin = self.rope.tables(Lc, q.device)
-        cs, sn = cos.index_select(0, pos_t), sin.index_select(0, pos_t)
+        ctx = _DECODE_CTX.get(id(pos_t))
+        if ctx is None or ctx[0] is not pos_t or ctx[1] != (Lc, B, q.device):
+            # per-step constants shared by every layer (computed once per captured step, not per layer)
+            cos, sin = self.rope.tables(Lc, q.device)
+            ctx = (pos_t, (Lc, B, q.device), cos.index_select(0, pos_t), sin.index_select(0, pos_t),
+                   (pos_t + 1).to(torch.int32).expand(B).contiguous())
+            _DECODE_CTX.clear()
+            _DECODE_CTX[id(pos_t)] = ctx
+        _, _, cs, sn, lens = ctx
         q = _ops.apply_rotary(q, cs, sn)
         k = _ops.apply_rotary(k, cs, sn)
         kc[:B].index_copy_(2, pos_t, k.transpose(1, 2))
         vc[:B].index_copy_(2, pos_t, v.transpose(1, 2))
-        lens = (pos_t + 1).to(torch.int32).expand(B).contiguous()
         o = _ops.dense_decode_attention(q.reshape(B, self.H, self.D), kc[:B], vc[:B], lens, max_len=Lc)
         return self.o_proj(_wrap(o.reshape(B, 1, self.H * self.D)))
+
+
+# decode-step constants keyed by the position tensor; _decode_logits clears it at the start of each step
+_DECODE_CTX = {}
 
 
 class LlamaMLP(nn.Layer):
@@ -324,6 +334,7 @@ class LlamaForCausalLM(nn.Layer):
 
 
     def _decode_logits(self, tok, caches, pos_t):
+        _DECODE_CTX.clear()  # recompute the per-step RoPE rows / lengths once, in this step (and graph)
         x = self.llama.embed_tokens(_wrap(tok))
         for i, layer in enumerate(self.llama.layers):
             x = layer(x, caches[i], pos_t)
