@@ -355,13 +355,13 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
   constexpr int KT_BYTES = BK * D * 2;
   constexpr int QT_BYTES = BM * D * 2;
   constexpr int DST_BYTES = BK * BM * 2;  // dS^T [128 keys][32 q] bf16, 64-byte rows
-  __shared__ __attribute__((aligned(16))) char smem[2 * KT_BYTES + 2 * QT_BYTES + DST_BYTES + 2 * BM * 4];
+  __shared__ __attribute__((aligned(16))) char smem[2 * KT_BYTES + 2 * QT_BYTES + 2 * DST_BYTES + 2 * BM * 4];
   char* k_lds = smem;
   char* v_lds = smem + KT_BYTES;
   char* q_lds = v_lds + KT_BYTES;
   char* do_lds = q_lds + QT_BYTES;
   char* ds_lds = do_lds + QT_BYTES;
-  float* lse_s = reinterpret_cast<float*>(ds_lds + DST_BYTES);
+  float* lse_s = reinterpret_cast<float*>(ds_lds + 2 * DST_BYTES);  // ds_lds: two dS^T buffers
   float* dlt_s = lse_s + BM;
 
   const int kb = blockIdx.x;
@@ -454,6 +454,44 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
   if (q_begin < p.Sq) prefetch(q_begin);
   const bool has_atomics = w < NDT;  // waves that own a dQ d-tile issue 16 atomics per block
 
+  // dQ[q][d] += sum_key dS[q][key] K[key][d] for the query block whose dS^T is in `dsb`; wave w handles
+  // d tiles dt = w, w+4, ... Software-pipelined by one block: block i's dQ runs in iteration i+1 (after
+  // that iteration's second barrier), so no barrier is needed between the dS^T store and its reads.
+  auto dq_step = [&](const char* dsb, int qb0) {
+    for (int dt = w; dt < NDT; dt += 4) {
+      f32x16 qacc = zero16();
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        Frag a, bb;
+        // A = dS[q=r][key = 16ks + 8hf + j]: transposed read of the dS^T image (rows = keys)
+        const int kr0 = 16 * ks + 8 * hf;
+        const int ra = kr0 + qq, rb = kr0 + 4 + qq;
+        a.h[0] = lds_tr(dsb, ra * (BM * 2) + (((16 * G1 + 4 * pp) * 2) ^ (((ra >> 2) & 3) << 3)));
+        a.h[1] = lds_tr(dsb, rb * (BM * 2) + (((16 * G1 + 4 * pp) * 2) ^ (((rb >> 2) & 3) << 3)));
+        // B = K[key = 16ks + 8hf + j][d = dt*32 + r]: transposed read of the K image
+        const int cch = (dt * 32 + 16 * G1) / 8 + (pp >> 1);
+        bb.h[0] = lds_tr(k_lds, img_off<NCH>(kr0 + qq, cch) + 8 * (pp & 1));
+        bb.h[1] = lds_tr(k_lds, img_off<NCH>(kr0 + 4 + qq, cch) + 8 * (pp & 1));
+        qacc = mfma32(a.v, bb.v, qacc);
+      }
+      if (p.causal >= 0) {
+        // byte offsets into this (b, h)'s dQ rows (row stride H*D floats); out-of-range rows
+        // (ragged last block) fall outside the buffer resource and are dropped by the hardware
+        const int rs = p.H * D * 4;
+        const int base = qb0 * rs + (dt * 32 + r) * 4;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int qr = (i & 3) + 8 * (i >> 2) + 4 * hf;
+          const int off = (qb0 + qr < p.Sq) ? base + qr * rs : 0x7ffffff0;
+          __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(qacc[i] * p.scale, dq_rsrc, off, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) asm volatile("" ::"v"(qacc[i]));
+      }
+    }
+    };
+
   for (int q0 = q_begin; q0 < p.Sq; q0 += BM) {
     if (q0 == q_begin || !has_atomics) {
       asm volatile("s_waitcnt vmcnt(0)" : "+v"(qreg[0]), "+v"(dreg[0]), "+v"(lse_raw), "+v"(dlt_raw)::"memory");
@@ -486,6 +524,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
     }
     lds_barrier();
     if (q0 + BM < p.Sq) prefetch(q0 + BM);
+    if (q0 > q_begin) dq_step(ds_lds + ((((q0 - q_begin) / BM - 1) & 1) * DST_BYTES), q0 - BM);
 
     // S' = Q K^T - LSE/scale and dP' = dO V^T - delta : rows q (registers), cols = this lane's key.
     // Row constants for this lane's 16 query rows (8g + 4hf + 0..3): 4 x 16-byte LDS reads each.
@@ -549,7 +588,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
     {
       // fragment s, elements 0..3 = q 16s+4hf+0..3, elements 4..7 = q 16s+8+4hf+0..3
       const int row = w * 32 + r;
-      char* rowp = ds_lds + row * (BM * 2);
+      char* rowp = ds_lds + (((q0 - q_begin) / BM) & 1) * DST_BYTES + row * (BM * 2);
       const int sw = ((row >> 2) & 3) << 3;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -559,40 +598,12 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
         *reinterpret_cast<uint2*>(rowp + (((16 * s + 8 + 4 * hf) * 2) ^ sw)) = make_uint2(f.u.z, f.u.w);
       }
     }
+  }
+  // dQ of the last query block
+  if (q_begin < p.Sq) {
     lds_barrier();
-    // dQ[q][d] += sum_key dS[q][key] K[key][d] ; wave w handles d tiles dt = w, w+4, ...
-    for (int dt = w; dt < NDT; dt += 4) {
-      f32x16 qacc = zero16();
-#pragma unroll
-      for (int ks = 0; ks < BK / 16; ++ks) {
-        Frag a, bb;
-        // A = dS[q=r][key = 16ks + 8hf + j]: transposed read of the dS^T image (rows = keys)
-        const int kr0 = 16 * ks + 8 * hf;
-        const int ra = kr0 + qq, rb = kr0 + 4 + qq;
-        a.h[0] = lds_tr(ds_lds, ra * (BM * 2) + (((16 * G1 + 4 * pp) * 2) ^ (((ra >> 2) & 3) << 3)));
-        a.h[1] = lds_tr(ds_lds, rb * (BM * 2) + (((16 * G1 + 4 * pp) * 2) ^ (((rb >> 2) & 3) << 3)));
-        // B = K[key = 16ks + 8hf + j][d = dt*32 + r]: transposed read of the K image
-        const int cch = (dt * 32 + 16 * G1) / 8 + (pp >> 1);
-        bb.h[0] = lds_tr(k_lds, img_off<NCH>(kr0 + qq, cch) + 8 * (pp & 1));
-        bb.h[1] = lds_tr(k_lds, img_off<NCH>(kr0 + 4 + qq, cch) + 8 * (pp & 1));
-        qacc = mfma32(a.v, bb.v, qacc);
-      }
-      if (p.causal >= 0) {
-        // byte offsets into this (b, h)'s dQ rows (row stride H*D floats); out-of-range rows
-        // (ragged last block) fall outside the buffer resource and are dropped by the hardware
-        const int rs = p.H * D * 4;
-        const int base = q0 * rs + (dt * 32 + r) * 4;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int qr = (i & 3) + 8 * (i >> 2) + 4 * hf;
-          const int off = (q0 + qr < p.Sq) ? base + qr * rs : 0x7ffffff0;
-          __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(qacc[i] * p.scale, dq_rsrc, off, 0, 0);
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) asm volatile("" ::"v"(qacc[i]));
-      }
-    }
+    const int q_last = q_begin + ((p.Sq - 1 - q_begin) / BM) * BM;
+    dq_step(ds_lds + ((((q_last - q_begin) / BM) & 1) * DST_BYTES), q_last);
   }
 
   // write dK = scale * (dK^T)^T, dV = (dV^T)^T : lane = key, 4 consecutive d per 8-byte store
