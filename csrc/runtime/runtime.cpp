@@ -159,11 +159,13 @@ int64_t write_blobs(const std::string& path, const std::string& header, const st
 
 void register_pinned_pool(py::module& m);    // pinned_pool.cpp
 void register_comm_watchdog(py::module& m);  // comm_watchdog.cpp
+void register_ps_table(py::module& m);       // ps_table.cpp
 
 PYBIND11_MODULE(_C_runtime, m) {
   m.doc() = "paddlepaddle_amd native runtime (collate, scheduler, bucket planner, tensor files, pinned pool)";
   register_pinned_pool(m);
   register_comm_watchdog(m);
+  register_ps_table(m);
   m.def("stack_into", &stack_into, py::arg("arrays"), py::arg("out"));
   m.def("plan_buckets", &plan_buckets, py::arg("sizes"), py::arg("bucket_bytes"));
   m.def("schedule", &schedule, py::arg("n"), py::arg("edges"), py::arg("keep"));

@@ -16,16 +16,41 @@ barrier_worker = fleet.barrier_worker
 local_rank = fleet.local_rank
 save_persistables = fleet.save_persistables
 save_inference_model = fleet.save_inference_model
-
-
-class UserDefinedRoleMaker:
-    def __init__(self, *a, **k):
-        pass
+is_server = fleet.is_server
+is_worker = fleet.is_worker
+init_server = fleet.init_server
+run_server = fleet.run_server
+init_worker = fleet.init_worker
+stop_worker = fleet.stop_worker
+server_num = fleet.server_num
+server_index = fleet.server_index
+server_endpoints = fleet.server_endpoints
+load_model = fleet.load_model
+shrink = fleet.shrink
 
 
 class PaddleCloudRoleMaker:
-    def __init__(self, is_collective=True, **k):
+    """Role from the environment (reference fleet/base/role_maker.py PaddleCloudRoleMaker): collective mode
+    uses the torch.distributed env; PS mode reads TRAINING_ROLE, PADDLE_PSERVERS_IP_PORT_LIST,
+    PADDLE_TRAINERS_NUM, PADDLE_TRAINER_ID, POD_IP / PADDLE_PORT (parsed by distributed.ps.PsRuntime)."""
+
+    def __init__(self, is_collective=False, **k):
         self.is_collective = is_collective
+        self._kwargs = k
+
+
+class UserDefinedRoleMaker(PaddleCloudRoleMaker):
+    """Explicit role (reference UserDefinedRoleMaker): current_id, role (Role.WORKER / Role.SERVER),
+    worker_num, server_endpoints."""
+
+    def __init__(self, is_collective=False, init_gloo=False, current_id=0, role=None, worker_num=1,
+                 server_endpoints=None, worker_endpoints=None, **k):
+        super().__init__(is_collective=is_collective, **k)
+        self._current_id = int(current_id)
+        self._role = "PSERVER" if role == Role.SERVER else "TRAINER"
+        self._worker_num = int(worker_num)
+        self._server_endpoints = ",".join(server_endpoints or [])
+        self._worker_endpoints = list(worker_endpoints or [])
 
 
 class Role:

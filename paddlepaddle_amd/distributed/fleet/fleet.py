@@ -66,10 +66,20 @@ class _Fleet:
         self._hcg = None
         self._strategy = None
         self._is_collective = True
+        self._ps = None  # parameter-server runtime (PS mode)
 
     # ---------------------------------------------------------------- init / env
     def init(self, role_maker=None, is_collective=True, strategy=None, log_level="INFO"):
         self._strategy = strategy or DistributedStrategy()
+        if role_maker is not None:
+            is_collective = getattr(role_maker, "is_collective", is_collective)
+        self._is_collective = bool(is_collective)
+        if not self._is_collective:
+            # parameter-server mode (reference fleet.init with a PS role maker -> TheOnePSRuntime)
+            from ..ps import the_one_ps as _ps
+            self._ps = _ps.PsRuntime(role_maker, self._strategy)
+            _ps.set_runtime(self._ps)
+            return self
         if not C.is_initialized() and C.get_world_size() > 1:
             C.init_parallel_env()
         ws = C.get_world_size()
@@ -94,25 +104,63 @@ class _Fleet:
         return self._hcg
 
     def worker_index(self):
-        return C.get_rank()
+        return self._ps.index if self._ps is not None and self._ps.role == "TRAINER" else C.get_rank()
 
     def worker_num(self):
-        return C.get_world_size()
+        return self._ps.n_trainers if self._ps is not None else C.get_world_size()
+
+    def server_num(self):
+        return self._ps.n_servers if self._ps is not None else 0
+
+    def server_index(self):
+        return self._ps.index if self._ps is not None and self._ps.role == "PSERVER" else 0
+
+    def server_endpoints(self, to_string=False):
+        eps = self._ps.server_endpoints if self._ps is not None else []
+        return ",".join(eps) if to_string else eps
 
     def is_first_worker(self):
-        return C.get_rank() == 0
+        return self.is_worker() and self.worker_index() == 0
 
     def is_worker(self):
-        return True
+        return self._ps is None or self._ps.role == "TRAINER"
 
     def is_server(self):
-        return False
+        return self._ps is not None and self._ps.role == "PSERVER"
+
+    # ---------------------------------------------------------------- parameter-server mode
+    def _need_ps(self):
+        if self._ps is None:
+            raise RuntimeError("not in parameter-server mode: fleet.init(role_maker=PaddleCloudRoleMaker("
+                               "is_collective=False)) first")
+        return self._ps
+
+    def init_server(self, *args, **kwargs):
+        self._need_ps().init_server(*args, **kwargs)
+
+    def run_server(self):
+        self._need_ps().run_server()
+
+    def init_worker(self, scopes=None):
+        self._need_ps().init_worker(scopes)
+
+    def stop_worker(self):
+        self._need_ps().stop_worker()
+
+    def load_model(self, path, mode=0):
+        return self._need_ps().load(path)
+
+    def shrink(self, threshold=None):
+        return self._need_ps().shrink(0 if threshold is None else threshold)
 
     def worker_endpoints(self, to_string=False):
         eps = C.ParallelEnv().trainer_endpoints
         return ",".join(eps) if to_string else eps
 
     def barrier_worker(self):
+        if self._ps is not None:
+            self._ps.barrier_worker()
+            return
         C.barrier()
 
     def local_rank(self):
@@ -147,6 +195,11 @@ class _Fleet:
     def distributed_optimizer(self, optimizer, strategy=None):
         if strategy is not None:
             self._strategy = strategy
+        if self._ps is not None:
+            from ..ps.layers import PsOptimizer
+            if strategy is not None:
+                self._ps.a_sync = bool(getattr(strategy, "a_sync", False))
+            return PsOptimizer(optimizer, self._ps)
         if self._hcg is None:
             self.init(strategy=self._strategy)
         return HybridParallelOptimizer(optimizer, self._hcg, self._strategy)
@@ -156,6 +209,8 @@ class _Fleet:
 
     # ---------------------------------------------------------------- io
     def save_persistables(self, executor, dirname, main_program=None, mode=0):
+        if self._ps is not None:  # tables live on the servers: each saves its shards
+            return self._ps.save(dirname, mode)
         from ...static.io import save_persistables
         save_persistables(executor, dirname, main_program)
 

@@ -219,8 +219,22 @@ def spectral_norm(weight, dim=0, power_iters=1, eps=1e-12, name=None):
 
 def sparse_embedding(input, size, padding_idx=None, is_test=False, entry=None, table_class="MemorySparseTable",
                      param_attr=None, dtype="float32", slot=None):
-    # parameter-server sparse tables are out of scope on a GPU node: a dense embedding of the same shape
+    """Lookup into a parameter-server sparse table (distributed/ps) when this process is a PS trainer; without a
+    PS runtime (single process / collective mode) a local dense embedding of the same shape."""
+    from ..distributed.ps import the_one_ps as _ps
+    rt = _ps.get_runtime()
+    if rt is not None and rt.client is not None:
+        from ..distributed.ps.layers import DistributedEmbedding
+        name = getattr(param_attr, "name", None) or f"sparse_embedding_{size[0]}x{size[1]}"
+        cache = _SPARSE_EMB.get(name)
+        if cache is None:
+            cache = _SPARSE_EMB[name] = DistributedEmbedding(size, name=name, padding_idx=padding_idx, entry=entry)
+        cache.training = not is_test
+        return cache(input)
     return _nn.Embedding(size[0], size[1], padding_idx=padding_idx, weight_attr=param_attr)(input)
+
+
+_SPARSE_EMB = {}
 
 
 def _lod(*a, **k):
