@@ -18,7 +18,8 @@ from .watchdog import enable_comm_watchdog, disable_comm_watchdog  # noqa: F401,
 def __getattr__(name):
     # heavier subsystems are imported on first use (fleet pulls in pipeline/TP layers)
     import importlib
-    if name in ("fleet", "sharding", "checkpoint", "launch", "spawn_mod", "utils", "communication", "rpc"):
+    if name in ("fleet", "sharding", "checkpoint", "launch", "spawn_mod", "utils", "communication", "rpc", "ps",
+                "elastic"):
         mod = importlib.import_module(f".{name}", __name__)
         globals()[name] = mod
         return mod
