@@ -97,12 +97,33 @@ __device__ __forceinline__ bf16x8_t pack8(const float* f) {
   return x.v;
 }
 
+// 1-D grid of nb * BH workgroups -> (head bh, block rank). Dispatch is round-robin over the 8 XCDs
+// (workgroup id mod 8). With grp > 0 (BH % 8 == 0): XCD x owns heads x, x+8, ...; it walks them in groups
+// of `grp` heads, and inside a group rank-major (rank 0 = heaviest block under the causal mask first),
+// head-minor. So every XCD gets the same mix of block sizes, the heavy blocks go first, and the
+// workgroups in flight on one XCD touch only ~grp heads' K/V (L2 reuse).
+__device__ __forceinline__ void block_map(int L, int BH, int nb, int grp, int& bh, int& rank) {
+  if (grp > 0) {
+    const int xcd = L & 7, i = L >> 3;
+    const int hpx = BH >> 3;
+    const int gi = i / (grp * nb);
+    const int g_eff = min(grp, hpx - gi * grp);
+    const int j = i - gi * grp * nb;
+    rank = j / g_eff;
+    bh = xcd + 8 * (gi * grp + j % g_eff);
+  } else {
+    bh = L % BH;
+    rank = L / BH;
+  }
+}
+
 struct FwdArgs {
   const uint16_t* q; const uint16_t* k; const uint16_t* v; uint16_t* o; float* lse;
   int64_t qs[3], ks[3], vs[3], os[3];  // strides (batch, seq, head) in elements
   int B, Sq, Sk, H, Hk;
   float scale_log2;
   int causal;
+  int grp;  // heads per dispatch group (block_map)
 };
 
 // ------------------------------------------------------------------------------------- forward
@@ -118,9 +139,10 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs p) {
   char* ks_lds = smem;
   char* vs_lds = smem + TILE_BYTES;
 
-  const int nqb = gridDim.x;
-  const int qb = p.causal ? (nqb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
-  const int bh = blockIdx.y;
+  const int nqb = (p.Sq + 127) / 128;
+  int bh, rank;
+  block_map((int)blockIdx.x, p.B * p.H, nqb, p.grp, bh, rank);
+  const int qb = p.causal ? (nqb - 1 - rank) : rank;
   const int b = bh / p.H, h = bh % p.H;
   const int hk = h / (p.H / p.Hk);
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
@@ -294,6 +316,207 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(FwdArgs p) {
   }
 }
 
+// ------------------------------------------------------------------------------------- forward v2
+// Same math and lane layout as fa_fwd_kernel; the data movement and softmax bookkeeping differ:
+//   * K/V tiles go global -> LDS by global_load_lds (no register round trip, no VALU for the LDS
+//     writes). glds writes LDS lane-linearly, so the image swizzle is applied to the per-lane global
+//     source chunk (ch = slot ^ swizzle(row)); the image is the same one img_off() addresses.
+//   * Two LDS stages: tile t+1 is fetched while tile t computes, one barrier per tile.
+//   * Deferred rescale: the running max (reference for exp2) is only raised when a tile's max exceeds
+//     it by more than 2^8 (in exp2 units); otherwise P values up to 256 are accumulated against the
+//     stale reference. The 64 O-accumulator multiplies then run on a few tiles per row, not all.
+//   * The softmax scale is folded into the exp2 argument: p = exp2(s * c - m * c), one FMA per score,
+//     and the max is taken on raw scores.
+__device__ __forceinline__ void glds16_fa(const void* g, const char* lds) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(lds));
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int D>
+__global__ __launch_bounds__(256, 2) void fa_fwd2_kernel(FwdArgs p) {
+  constexpr int NCH = D / 8;
+  constexpr int KS = D / 16;
+  constexpr int NDT = D / 32;
+  constexpr int BN = 64;
+  constexpr int TILE_BYTES = BN * D * 2;
+  constexpr int NI = TILE_BYTES / 1024 / 4;  // glds per wave per tensor per tile
+  constexpr float kDefer = 8.f;              // log2 of the largest accepted P before a rescale
+  __shared__ __attribute__((aligned(1024))) char smem[4 * TILE_BYTES];  // [stage][K | V]
+
+  const int nqb = (p.Sq + 127) / 128;
+  int bh, rank;
+  block_map((int)blockIdx.x, p.B * p.H, nqb, p.grp, bh, rank);
+  const int qb = p.causal ? (nqb - 1 - rank) : rank;
+  const int b = bh / p.H, h = bh % p.H;
+  const int hk = h / (p.H / p.Hk);
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
+  const int qi = qb * 128 + w * 32 + r;
+  const int shift = p.Sk - p.Sq;
+  const float c = p.scale_log2;
+
+  bf16x8_t qf[KS];
+  {
+    const uint16_t* qrow = p.q + (int64_t)b * p.qs[0] + (int64_t)(qi < p.Sq ? qi : 0) * p.qs[1] + (int64_t)h * p.qs[2];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      Frag f;
+      if (qi < p.Sq) f.u = *reinterpret_cast<const uint4*>(qrow + ks * 16 + hf * 8);
+      else f.u = make_uint4(0, 0, 0, 0);
+      qf[ks] = f.v;
+    }
+  }
+
+  f32x16 oacc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) oacc[dt] = zero16();
+  float m_run = -INFINITY, l_run = 0.f;
+
+  int kv_end = p.Sk;
+  if (p.causal) {
+    const int last_q = min(qb * 128 + 127, p.Sq - 1);
+    kv_end = min(p.Sk, last_q + shift + 1);
+  }
+  const int n_tiles = kv_end > 0 ? (kv_end + BN - 1) / BN : 0;
+
+  const uint16_t* kbase = p.k + (int64_t)b * p.ks[0] + (int64_t)hk * p.ks[2];
+  const uint16_t* vbase = p.v + (int64_t)b * p.vs[0] + (int64_t)hk * p.vs[2];
+
+  // this lane's (row, chunk) in each of its NI 1-KiB pieces (tile independent)
+  auto issue = [&](int tile, int stage) {
+    const char* kdst = smem + stage * 2 * TILE_BYTES;
+    const char* vdst = kdst + TILE_BYTES;
+    const int kv0 = tile * BN;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int q = w * NI + i;
+      const int o = q * 1024 + lane * 16;
+      const int row = o / (NCH * 16), slot = (o % (NCH * 16)) / 16;
+      const int ch = (img_off<NCH>(row, slot) - row * (NCH * 16)) / 16;  // slot ^ swizzle(row)
+      int key = kv0 + row;
+      key = key < p.Sk ? key : p.Sk - 1;  // rows past the end are masked to -inf below
+      glds16_fa(kbase + (int64_t)key * p.ks[1] + ch * 8, kdst + q * 1024);
+      glds16_fa(vbase + (int64_t)key * p.vs[1] + ch * 8, vdst + q * 1024);
+    }
+  };
+
+  const int gi = lane & 15, qq = gi >> 2, pp = gi & 3, G1 = (lane >> 4) & 1;
+  if (n_tiles > 0) issue(0, 0);
+  for (int t = 0; t < n_tiles; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile t are in LDS
+    raw_barrier();                                     // ... everyone's, and stage (t+1)&1 is free
+    if (t + 1 < n_tiles) issue(t + 1, (t + 1) & 1);
+    const char* ks_lds = smem + (t & 1) * 2 * TILE_BYTES;
+    const char* vs_lds = ks_lds + TILE_BYTES;
+    const int kv0 = t * BN;
+
+    f32x16 sacc[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      sacc[kt] = zero16();
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        Frag a;
+        a.u = lds_b128(ks_lds, img_off<NCH>(kt * 32 + r, 2 * ks + hf));
+        sacc[kt] = mfma32(a.v, qf[ks], sacc[kt]);
+      }
+    }
+    float mloc = -INFINITY;
+    const bool need_mask = (kv0 + BN > p.Sk) || (p.causal && (kv0 + BN - 1 > qb * 128 + shift));
+    if (need_mask) {
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int kj = kv0 + kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hf;
+          if (kj >= p.Sk || (p.causal && kj > qi + shift)) sacc[kt][i] = -INFINITY;
+        }
+    }
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) mloc = fmaxf(mloc, sacc[kt][i]);
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    const float m_new = fmaxf(m_run, mloc);
+    // (m_new - m_run) * c: +inf on a row's first live tile, NaN while the row is all -inf (no rescale)
+    if (__ballot((m_new - m_run) * c > kDefer)) {
+      const float alpha = (m_run == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f((m_run - m_new) * c);
+      m_run = m_new;
+      l_run *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+    }
+    const float mc = (m_run == -INFINITY) ? 0.f : m_run * c;
+    float psum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[kt][i], c, -mc));
+        sacc[kt][i] = e;
+        psum += e;
+      }
+    l_run += psum;
+
+    bf16x8_t pf[2][2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float tmp[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) tmp[j] = sacc[kt][8 * s + j];
+        pf[kt][s] = pack8(tmp);
+      }
+
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      const int cch = (dt * 32 + 16 * G1) / 8 + (pp >> 1);
+      const int cb = 8 * (pp & 1);
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int R0 = kt * 32 + 16 * s + 4 * hf;
+          Frag a;
+          a.h[0] = lds_tr(vs_lds, img_off<NCH>(R0 + qq, cch) + cb);
+          a.h[1] = lds_tr(vs_lds, img_off<NCH>(R0 + 8 + qq, cch) + cb);
+          oacc[dt] = mfma32(a.v, pf[kt][s], oacc[dt]);
+        }
+      }
+    }
+  }
+
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  if (qi < p.Sq) {
+    uint16_t* orow = p.o + (int64_t)b * p.os[0] + (int64_t)qi * p.os[1] + (int64_t)h * p.os[2];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d0 = dt * 32 + 8 * g + 4 * hf;
+        uint2 v2;
+        v2.x = pack_bf16(oacc[dt][4 * g + 0] * inv, oacc[dt][4 * g + 1] * inv);
+        v2.y = pack_bf16(oacc[dt][4 * g + 2] * inv, oacc[dt][4 * g + 3] * inv);
+        *reinterpret_cast<uint2*>(orow + d0) = v2;
+      }
+    }
+    if (hf == 0) {
+      const float lse = (m_run == -INFINITY) ? INFINITY : (m_run * c * kLn2 + __logf(l_tot));
+      p.lse[((int64_t)b * p.H + h) * p.Sq + qi] = lse;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------- backward
 struct BwdArgs {
   const uint16_t* q; const uint16_t* k; const uint16_t* v; const uint16_t* o; const uint16_t* dout;
@@ -302,6 +525,7 @@ struct BwdArgs {
   int B, Sq, Sk, H, Hk;
   float scale, scale_log2;
   int causal;
+  int grp;
 };
 
 // delta[b,h,q] = sum_d dO * O
@@ -364,8 +588,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
   float* lse_s = reinterpret_cast<float*>(ds_lds + 2 * DST_BYTES);  // ds_lds: two dS^T buffers
   float* dlt_s = lse_s + BM;
 
-  const int kb = blockIdx.x;
-  const int bh = blockIdx.y;
+  int kb, bh;  // key block 0 is the heaviest under the causal mask: rank order
+  block_map((int)blockIdx.x, p.B * p.H, (p.Sk + 127) / 128, p.grp, bh, kb);
   const int b = bh / p.H, h = bh % p.H;
   const int hk = h / (p.H / p.Hk);
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hf = lane >> 5;
@@ -629,6 +853,25 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(BwdArgs p) {
 
 }  // namespace
 
+// heads per dispatch group for block_map: all of an XCD's heads at once (global heaviest-first) while that
+// is at most 512 workgroups per XCD, else groups that keep ~`inflight` workgroups (2 per CU forward, 1
+// backward) on a few heads for L2 reuse of their K/V (or Q/dO); 0 (plain head-fastest order) when B*H is
+// not a multiple of 8.
+static int fa_group(int BH, int nb, int inflight) {
+  if (BH % 8 != 0) return 0;
+  const int hpx = BH / 8;
+  if (hpx * nb <= 512) return hpx;
+  return std::max(1, (inflight + nb - 1) / nb);
+}
+
+static int g_fwd_variant = 2;  // 1: register-staged single-buffer kernel, 2: fa_fwd2_kernel
+
+// A/B switch for the microbenchmarks
+PA_EXPORT int pa_flash_attn_set_fwd_variant(int v) {
+  g_fwd_variant = v;
+  return 0;
+}
+
 // strides: host array of 12 int64 = q(b,s,h), k(b,s,h), v(b,s,h), o(b,s,h)
 PA_EXPORT int pa_flash_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
                                 const int64_t* strides, int B, int Sq, int Sk, int H, int Hk, int D, float scale,
@@ -642,10 +885,17 @@ PA_EXPORT int pa_flash_attn_fwd(const void* q, const void* k, const void* v, voi
   a.B = B; a.Sq = Sq; a.Sk = Sk; a.H = H; a.Hk = Hk;
   a.scale_log2 = scale * kLog2e;
   a.causal = causal;
-  dim3 grid((unsigned)((Sq + 127) / 128), (unsigned)(B * H));
-  if (D == 128) hipLaunchKernelGGL(fa_fwd_kernel<128>, grid, dim3(256), 0, st, a);
-  else if (D == 64) hipLaunchKernelGGL(fa_fwd_kernel<64>, grid, dim3(256), 0, st, a);
-  else return 4;
+  const int nqb = (Sq + 127) / 128;
+  a.grp = fa_group(B * H, nqb, 64);
+  dim3 grid((unsigned)(B * H * nqb));
+  if (D != 128 && D != 64) return 4;
+  if (g_fwd_variant == 2) {
+    if (D == 128) hipLaunchKernelGGL(fa_fwd2_kernel<128>, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(fa_fwd2_kernel<64>, grid, dim3(256), 0, st, a);
+  } else {
+    if (D == 128) hipLaunchKernelGGL(fa_fwd_kernel<128>, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(fa_fwd_kernel<64>, grid, dim3(256), 0, st, a);
+  }
   PA_CHECK_LAUNCH();
   return 0;
 }
@@ -677,7 +927,9 @@ PA_EXPORT int pa_flash_attn_bwd(const void* q, const void* k, const void* v, con
   }
   a.B = B; a.Sq = Sq; a.Sk = Sk; a.H = H; a.Hk = Hk;
   a.scale = scale; a.scale_log2 = scale * kLog2e; a.causal = causal;
-  dim3 grid((unsigned)((Sk + 127) / 128), (unsigned)(B * H));
+  const int nkb = (Sk + 127) / 128;
+  a.grp = fa_group(B * H, nkb, 32);
+  dim3 grid((unsigned)(B * H * nkb));
   if (D == 128) hipLaunchKernelGGL(fa_bwd_kernel<128>, grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(fa_bwd_kernel<64>, grid, dim3(256), 0, st, a);
   PA_CHECK_LAUNCH();
