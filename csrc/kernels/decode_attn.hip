@@ -8,10 +8,10 @@
 // blocks for ALL query heads of the GQA group (K/V bytes are read once for the group), writes a
 // partial (m, l, o); a second tiny kernel merges the splits.
 //
-// Work split inside a workgroup (256 threads = 4 waves): a wave takes one cache block at a time
-// (block b of its split goes to wave b % 4); within the wave 16 lanes cover one key's D = 128
-// elements (8 bf16 each, one 16-byte load), so a wave-instruction covers 4 keys. Dot products
-// reduce over the 16 lanes with 4 xor-shuffles.
+// Work split inside a workgroup (256 threads = 4 waves): the split's keys go to the waves in 16-key
+// chunks, round-robin; within the wave 16 lanes cover one key's D = 128 elements (8 bf16 each, one
+// 16-byte load), so a wave-instruction covers 4 keys and a chunk is 4 of them (8 loads in flight per
+// lane). Dot products reduce over the 16 lanes with 4 xor-shuffles.
 #include "common.h"
 
 using namespace pa;
@@ -60,42 +60,52 @@ __global__ __launch_bounds__(256) void paged_decode_k(const uint16_t* __restrict
     for (int j = 0; j < EPL; ++j) o[g][j] = 0.f;
   }
 
-  for (int blk = b0 + w; blk < b1; blk += 4) {
-    const int pb = tables[(int64_t)n * max_blocks + blk];
-    const int64_t boff = (int64_t)pb * blk_stride + (int64_t)hk * head_stride;
-    const uint16_t* kb = kc + boff;
-    const uint16_t* vb = vc + boff;
-    const int kend = min(bs, len - blk * bs);
-    for (int k0 = 0; k0 < kend; k0 += 4) {
-      const int key = k0 + sub;
-      const bool valid = key < kend;
-      float kf[8], vf[8];
-      if (valid) {
-        load8<bf16>(reinterpret_cast<const bf16*>(kb + (int64_t)key * D + li * EPL), kf);
-        load8<bf16>(reinterpret_cast<const bf16*>(vb + (int64_t)key * D + li * EPL), vf);
-      } else {
+  // Keys of this split in 16-key chunks dealt round-robin to the 4 waves (balanced to one chunk); 4 keys
+  // per 16-lane group per chunk, all 8 loads issued before the first use, and the online softmax rescales
+  // once per 4 keys. A key's cache row comes from its block-table entry (any block size). Keys past the end
+  // read the last valid row (finite data) and are masked to -inf.
+  const int kbeg = b0 * bs, kfin = min(b1 * bs, len);
+  const int64_t trow = (int64_t)n * max_blocks;
+  for (int c0 = kbeg + 16 * w; c0 < kfin; c0 += 64) {
+    float kf[4][8], vf[4][8];
+    bool valid[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { kf[j] = 0.f; vf[j] = 0.f; }
+    for (int u = 0; u < 4; ++u) {
+      const int key = c0 + 4 * u + sub;
+      valid[u] = key < kfin;
+      const int kk = valid[u] ? key : kfin - 1;
+      const int blk = kk / bs;
+      const int64_t off = (int64_t)tables[trow + blk] * blk_stride + (int64_t)hk * head_stride +
+                          (int64_t)(kk - blk * bs) * D + li * EPL;
+      load8<bf16>(reinterpret_cast<const bf16*>(kc + off), kf[u]);
+      load8<bf16>(reinterpret_cast<const bf16*>(vc + off), vf[u]);
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float sc[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float t = 0.f;
+#pragma unroll
+        for (int j = 0; j < EPL; ++j) t += qv[g][j] * kf[u][j];
+        t += __shfl_xor(t, 1, 64);
+        t += __shfl_xor(t, 2, 64);
+        t += __shfl_xor(t, 4, 64);
+        t += __shfl_xor(t, 8, 64);
+        sc[u] = valid[u] ? t : -INFINITY;
       }
+      const float mx = fmaxf(fmaxf(sc[0], sc[1]), fmaxf(sc[2], sc[3]));
+      const float mn = fmaxf(m[g], mx);
+      if (mn == -INFINITY) continue;  // nothing valid yet in this lane group
+      const float a = (m[g] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m[g] - mn);
+      float pe[4];
 #pragma unroll
-      for (int g = 0; g < G; ++g) {
-        float s = 0.f;
+      for (int u = 0; u < 4; ++u) pe[u] = __builtin_amdgcn_exp2f(sc[u] - mn);  // exp2(-inf) = 0
+      l[g] = l[g] * a + (pe[0] + pe[1]) + (pe[2] + pe[3]);
 #pragma unroll
-        for (int j = 0; j < EPL; ++j) s += qv[g][j] * kf[j];
-        s += __shfl_xor(s, 1, 64);
-        s += __shfl_xor(s, 2, 64);
-        s += __shfl_xor(s, 4, 64);
-        s += __shfl_xor(s, 8, 64);
-        if (!valid) s = -INFINITY;
-        // online softmax per 16-lane key group (each group keeps its own m / l / o)
-        const float mn = fmaxf(m[g], s);
-        const float a = (m[g] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m[g] - mn);
-        const float pexp = (s == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(s - mn);
-        l[g] = l[g] * a + pexp;
-#pragma unroll
-        for (int j = 0; j < EPL; ++j) o[g][j] = o[g][j] * a + pexp * vf[j];
-        m[g] = mn;
-      }
+      for (int j = 0; j < EPL; ++j)
+        o[g][j] = o[g][j] * a + pe[0] * vf[0][j] + pe[1] * vf[1][j] + pe[2] * vf[2][j] + pe[3] * vf[3][j];
+      m[g] = mn;
     }
   }
 

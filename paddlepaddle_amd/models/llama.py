@@ -150,10 +150,10 @@ class LlamaAttention(nn.Layer):
         return q.view(B, S, self.H, self.D), k.view(B, S, self.Hkv, self.D), v.view(B, S, self.Hkv, self.D)
 
     def forward(self, x, cache=None, pos=0):
+        if cache is not None and isinstance(pos, torch.Tensor):
+            return self._decode_step(x, cache, pos)
         q, k, v = self._qkv(x)
         B, S = q.shape[0], q.shape[1]
-        if cache is not None and isinstance(pos, torch.Tensor):
-            return self._decode_step(q, k, v, cache, pos)
         cos, sin = self.rope.tables(pos + S, q.device)
         q = _ops.apply_rotary(q, cos[pos:pos + S], sin[pos:pos + S])
         k = _ops.apply_rotary(k, cos[pos:pos + S], sin[pos:pos + S])
@@ -170,13 +170,15 @@ class LlamaAttention(nn.Layer):
         o = _ops.flash_attention(q, k, v, causal=causal)
         return self.o_proj(_wrap(o.reshape(B, S, self.H * self.D)))
 
-    def _decode_step(self, q, k, v, cache, pos_t):
+    def _decode_step(self, x, cache, pos_t):
         """One token per sequence at the device-side position ``pos_t`` ([1] int64): no host value is
-        read, so the step can be captured once into a hipGraph and replayed for every token. RoPE rows
-        are gathered at pos_t, K/V are scattered into the dense cache at pos_t, and attention is the
-        flash-decoding HIP kernel over the first pos_t + 1 cached tokens."""
+        read, so the step can be captured once into a hipGraph and replayed for every token. One fused
+        kernel rotates Q/K with the RoPE rows at pos_t, splits the QKV projection and writes K/V into the
+        dense cache at pos_t; attention is the flash-decoding HIP kernel over the first pos_t + 1 tokens."""
         kc, vc = cache
-        B = q.shape[0]
+        t = self.qkv_proj(x)._t
+        B = t.shape[0]
+        q = t  # dtype / device carrier for the context below
         Lc = kc.shape[2]
         ctx = _DECODE_CTX.get(id(pos_t))
         if ctx is None or ctx[0] is not pos_t or ctx[1] != (Lc, B, q.device):
@@ -187,11 +189,8 @@ class LlamaAttention(nn.Layer):
             _DECODE_CTX.clear()
             _DECODE_CTX[id(pos_t)] = ctx
         _, _, cs, sn, lens = ctx
-        q = _ops.apply_rotary(q, cs, sn)
-        k = _ops.apply_rotary(k, cs, sn)
-        kc[:B].index_copy_(2, pos_t, k.transpose(1, 2))
-        vc[:B].index_copy_(2, pos_t, v.transpose(1, 2))
-        o = _ops.dense_decode_attention(q.reshape(B, self.H, self.D), kc[:B], vc[:B], lens, max_len=Lc)
+        q = _ops.decode_rope_cache(t.reshape(B, -1), self.H, self.Hkv, self.D, cs, sn, pos_t, kc, vc)
+        o = _ops.dense_decode_attention(q, kc[:B], vc[:B], lens, max_len=Lc)
         return self.o_proj(_wrap(o.reshape(B, 1, self.H * self.D)))
 
 
@@ -247,8 +246,27 @@ class LlamaModel(nn.Layer):
         self.layers = nn.LayerList([LlamaDecoderLayer(cfg) for _ in range(cfg.num_hidden_layers)])
         self.norm = LlamaRMSNorm(cfg)
 
+    def _forward_infer(self, x, caches, pos):
+        """Inference layer loop with the residual adds fused into the following RMSNorm (one HIP pass for
+        x += h; n = norm(x)), including across layer boundaries and into the final norm."""
+        xt, h = x._t, None
+        for i, layer in enumerate(self.layers):
+            if h is None:
+                n = _ops.rms_norm(xt, layer.input_layernorm.weight._t, layer.input_layernorm.eps)
+            else:
+                xt, n = _ops.add_rms_norm(xt, h, layer.input_layernorm.weight._t, layer.input_layernorm.eps,
+                                          inplace=i > 0)
+            a = layer.self_attn(_wrap(n), None if caches is None else caches[i], pos)._t
+            xt, n = _ops.add_rms_norm(xt, a, layer.post_attention_layernorm.weight._t,
+                                      layer.post_attention_layernorm.eps, inplace=i > 0)
+            h = layer.mlp(_wrap(n))._t
+        _, out = _ops.add_rms_norm(xt, h, self.norm.weight._t, self.norm.eps, inplace=True)
+        return _wrap(out)
+
     def forward(self, input_ids, caches=None, pos=0):
         x = self.embed_tokens(input_ids)
+        if not torch.is_grad_enabled() and len(self.layers) > 0 and x._t.is_cuda:
+            return self._forward_infer(x, caches, pos)
         rc = self.config.use_recompute and self.training and caches is None
         if rc:
             from ..distributed.fleet.recompute import recompute
@@ -336,6 +354,8 @@ class LlamaForCausalLM(nn.Layer):
     def _decode_logits(self, tok, caches, pos_t):
         _DECODE_CTX.clear()  # recompute the per-step RoPE rows / lengths once, in this step (and graph)
         x = self.llama.embed_tokens(_wrap(tok))
+        if not torch.is_grad_enabled() and x._t.is_cuda:
+            return self._logits(self.llama._forward_infer(x, caches, pos_t))._t[:, -1].float()
         for i, layer in enumerate(self.llama.layers):
             x = layer(x, caches[i], pos_t)
         return self._logits(self.llama.norm(x))._t[:, -1].float()

@@ -257,6 +257,9 @@ def paged_decode_attention(q, key_cache, value_cache, block_tables, lens, scale=
 _VBLK = 64  # virtual block size when a dense cache is streamed by the paged kernel
 
 
+_DENSE_TABLES = {}
+
+
 @static_op
 def dense_decode_attention(q, key_cache, value_cache, lens, scale=None, max_len=None):
     """Decode attention over a dense per-sequence cache [B,Hkv,max_len,D] (masked_multihead_attention
@@ -273,7 +276,13 @@ def dense_decode_attention(q, key_cache, value_cache, lens, scale=None, max_len=
         o = torch.einsum("nkgl,nkld->nkgd", torch.softmax(s, -1), value_cache.float())
         return o.reshape(N, H, D).to(q.dtype)
     nb = Lc // _VBLK
-    tables = (torch.arange(N, device=q.device, dtype=torch.int32)[:, None] * (Hkv * nb)
-              + torch.arange(nb, device=q.device, dtype=torch.int32)[None])
+    key = (N, Hkv, nb, q.device)
+    tables = _DENSE_TABLES.get(key)
+    if tables is None:  # identical for every layer / step: built once (also outside any captured graph)
+        tables = (torch.arange(N, device=q.device, dtype=torch.int32)[:, None] * (Hkv * nb)
+                  + torch.arange(nb, device=q.device, dtype=torch.int32)[None])
+        if len(_DENSE_TABLES) > 64:
+            _DENSE_TABLES.clear()
+        _DENSE_TABLES[key] = tables
     ml = Lc if max_len is None else int(max_len)
     return _decode_launch(q, key_cache, value_cache, tables, lens, Hkv, _VBLK, _VBLK * D, Lc * D, scale, ml)

@@ -132,8 +132,18 @@ def _capturing():
         return False
 
 
-def choose(key, candidates):
-    """Name of the faster entry of ``candidates`` ({name: zero-arg callable without side effects})."""
+def _flush_caches(dev):
+    """Evict L2 and the 256 MB MALL (Infinity Cache): write a 512 MB scratch buffer."""
+    buf = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+    buf.zero_()
+    return buf
+
+
+def choose(key, candidates, cold=False):
+    """Name of the faster entry of ``candidates`` ({name: zero-arg callable without side effects}).
+    ``cold``: time every call after evicting the caches — for weight-streaming (decode) GEMMs, whose weights
+    come from HBM in a real step (the whole model streams through) but would sit in the 256 MB MALL when one
+    GEMM is repeated."""
     mode = L.flag("FLAGS_gemm_backend", "auto")
     if mode in candidates:
         return mode
@@ -145,8 +155,11 @@ def choose(key, candidates):
     times = {n: [] for n in candidates}
     for fn in candidates.values():
         fn()
+    dev = torch.cuda.current_device()
     for _ in range(3):
         for n, fn in candidates.items():
+            if cold:
+                _flush_caches(dev)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             fn()

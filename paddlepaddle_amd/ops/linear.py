@@ -84,7 +84,8 @@ def _blas_fwd(x2, w, b=None):
 def _fwd_mm(x2, w, b=None):
     if x2.shape[0] <= 64 and G.small_m_supported(x2, w):
         key = ("fwd_small_m", x2.shape[0], w.shape[1], x2.shape[1], b is not None)
-        ch = G.choose(key, {"blas": lambda: _blas_fwd(x2, w, b), "hip": lambda: G.gemm_small_m(x2, w, b)})
+        ch = G.choose(key, {"blas": lambda: _blas_fwd(x2, w, b), "hip": lambda: G.gemm_small_m(x2, w, b)},
+                      cold=True)
         if ch == "hip":
             return G.gemm_small_m(x2, w, b)
         return _blas_fwd(x2, w, b)

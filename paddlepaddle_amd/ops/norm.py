@@ -109,3 +109,20 @@ def layer_norm(x, w, b, eps=1e-5):
     if L.hip_enabled_for(x) and x.dtype in L._DT and x.shape[-1] % 8 == 0:
         return _LayerNormHIP.apply(x, w, b, eps)
     return _ln_ref(x, w, b, eps)
+
+
+def add_rms_norm(x, r, w, eps=1e-6, inplace=False):
+    """(s, y) with s = x + r and y = rms_norm(s) * w, in one HIP pass (inference: no autograd). With
+    ``inplace`` the sum is written into ``x``. Reference: incubate.nn.functional.fused_rms_norm(residual=...)."""
+    if (L.hip_enabled_for(x) and x.dtype in L._DT and x.shape[-1] % 8 == 0 and x.shape[-1] <= 8192
+            and r.shape == x.shape and x.is_contiguous() and r.is_contiguous() and w.dtype == x.dtype
+            and L.has("pa_add_rms_norm_fwd") and not (torch.is_grad_enabled() and
+                                                      (x.requires_grad or r.requires_grad or w.requires_grad))):
+        s = x if inplace else torch.empty_like(x)
+        y = torch.empty_like(x)
+        cols = x.shape[-1]
+        L.call("pa_add_rms_norm_fwd", L.ptr(x), L.ptr(r), L.ptr(w), L.ptr(s), L.ptr(y), x.numel() // cols, cols,
+               float(eps), L.dcode(x), L.stream_ptr())
+        return s, y
+    s = x + r
+    return s, rms_norm(s, w, eps)

@@ -72,3 +72,24 @@ def rope_tables(seq_len, dim, base=10000.0, device=None, neox=True):
     else:
         emb = torch.repeat_interleave(f, 2, -1)
     return emb.cos(), emb.sin()
+
+
+def decode_rope_cache(qkv, H, Hkv, D, cos_row, sin_row, pos_t, k_cache, v_cache):
+    """Decode step, one token per sequence: qkv [B, (H + 2*Hkv)*D] (the fused projection output) ->
+    rotated q [B, H, D]; rotated k and v are written into the dense caches [Bc, Hkv, Lc, D] at the
+    device-side position ``pos_t`` ([1] int64). cos_row / sin_row: fp32 [1, D] rows at that position."""
+    B = qkv.shape[0]
+    if (L.hip_enabled_for(qkv) and qkv.dtype in L._DT and D % 16 == 0 and qkv.stride(-1) == 1
+            and k_cache.is_contiguous() and v_cache.is_contiguous() and L.has("pa_decode_rope_cache")):
+        q = torch.empty(B, H, D, dtype=qkv.dtype, device=qkv.device)
+        cs = cos_row.float().contiguous()
+        sn = sin_row.float().contiguous()
+        L.call("pa_decode_rope_cache", L.ptr(qkv), qkv.stride(0), L.ptr(cs), L.ptr(sn), L.ptr(pos_t), L.ptr(q),
+               L.ptr(k_cache), L.ptr(v_cache), B, H, Hkv, D, k_cache.shape[2], L.dcode(qkv), L.stream_ptr())
+        return q
+    q, k, v = qkv.split([H * D, Hkv * D, Hkv * D], -1)
+    q = apply_rotary(q.reshape(B, 1, H, D), cos_row, sin_row)
+    k = apply_rotary(k.reshape(B, 1, Hkv, D), cos_row, sin_row)
+    k_cache[:B].index_copy_(2, pos_t, k.transpose(1, 2))
+    v_cache[:B].index_copy_(2, pos_t, v.reshape(B, 1, Hkv, D).transpose(1, 2))
+    return q.reshape(B, H, D)
