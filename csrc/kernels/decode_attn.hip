@@ -28,6 +28,7 @@ __global__ __launch_bounds__(256) void paged_decode_k(const uint16_t* __restrict
                                                        const int* __restrict__ lens,       // [N]
                                                        float* __restrict__ part_o,         // [N, H, S, D]
                                                        float* __restrict__ part_ml,        // [N, H, S, 2]
+                                                       uint16_t* __restrict__ out,         // [N, H, D] (splits 1)
                                                        int H, int Hkv, int bs, int max_blocks, int splits,
                                                        int64_t blk_stride, int64_t head_stride,
                                                        float scale_log2) {
@@ -134,6 +135,12 @@ __global__ __launch_bounds__(256) void paged_decode_k(const uint16_t* __restrict
       ll += sm_l[s][g] * f;
       oo += sm_o[s][g][d] * f;
     }
+    if (splits == 1) {  // the whole key range is here: write the normalised output, no combine pass
+      const float v = ll > 0.f ? oo / ll : 0.f;
+      bf16 x = __float2bfloat16(v);
+      out[((int64_t)n * H + hk * G + g) * D + d] = *reinterpret_cast<uint16_t*>(&x);
+      continue;
+    }
     const int64_t row = ((int64_t)n * H + hk * G + g) * splits + sp;
     part_o[row * D + d] = oo;
     if (d == 0) {
@@ -182,7 +189,7 @@ PA_EXPORT int pa_paged_decode_attn(const void* q, const void* kc, const void* vc
   dim3 grid((unsigned)N, (unsigned)Hkv, (unsigned)splits);
 #define PA_DEC(GG)                                                                                                  \
   hipLaunchKernelGGL((paged_decode_k<128, GG>), grid, dim3(256), 0, st, (const uint16_t*)q, (const uint16_t*)kc,   \
-                     (const uint16_t*)vc, tables, lens, part_o, part_ml, H, Hkv, bs, max_blocks, splits, blk_stride,      \
+                     (const uint16_t*)vc, tables, lens, part_o, part_ml, (uint16_t*)out, H, Hkv, bs, max_blocks, splits, blk_stride,      \
                      head_stride, sl2)
   switch (G) {
     case 1: PA_DEC(1); break;
@@ -193,6 +200,7 @@ PA_EXPORT int pa_paged_decode_attn(const void* q, const void* kc, const void* vc
   }
 #undef PA_DEC
   PA_CHECK_LAUNCH();
+  if (splits == 1) return 0;
   hipLaunchKernelGGL(paged_decode_combine_k, dim3((unsigned)(N * H)), dim3(128), 0, st, part_o, part_ml,
                      (uint16_t*)out, splits, D);
   PA_CHECK_LAUNCH();

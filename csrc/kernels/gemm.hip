@@ -785,12 +785,16 @@ int dispatch_layout(const GemmArgs& a, int a_kmajor, int b_kmajor, int splits, h
 // on B, so the kernel is built around keeping many weight bytes in flight: 4 waves, tile 64 x 128, K
 // split over gridDim.y, a 4-deep LDS ring filled by glds (3 K-tiles = 72 KiB per CU in flight), one
 // barrier per K-tile. Rows >= M are clamped reads whose results are never stored. Each split writes an
-// fp32 slab; pa_gemm_small_m_reduce sums the slabs (+ bias) into bf16.
+// fp32 slab; pa_gemm_small_m_reduce sums the slabs (+ bias) into bf16. Without a split the accumulators
+// go straight to C. (A last-arriving-split reduction inside the kernel measured 2-3x slower: the agent-scope
+// release fence it needs writes back the whole XCD L2 in every workgroup.)
 constexpr int kSmBM = 64, kSmBN = 128, kSmNW = 4, kSmStages = 4;
 
 __global__ __launch_bounds__(kSmNW * 64, 1) void gemm_small_m_kernel(const uint16_t* __restrict__ a, int64_t lda,
                                                                     const uint16_t* __restrict__ b, int64_t ldb,
-                                                                    float* __restrict__ ws, int M, int N, int k_per) {
+                                                                    float* __restrict__ ws, int M, int N, int k_per,
+                                                                    const uint16_t* __restrict__ bias,
+                                                                    uint16_t* __restrict__ c, int64_t ldc) {
   constexpr int A_BYTES = kSmBM * kBK * 2, B_BYTES = kSmBN * kBK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int NL = kSmBM / (8 * kSmNW) + kSmBN / (8 * kSmNW);  // glds per thread per K-tile (2 + 4)
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -843,6 +847,25 @@ __global__ __launch_bounds__(kSmNW * 64, 1) void gemm_small_m_kernel(const uint1
     bar();
   }
   // lane holds C[m = i*16 + (lane&15)][n = n0 + wave*32 + j*16 + 4*(lane>>4) + 0..3]
+  if (gridDim.y == 1) {  // no split: bias + bf16 straight from the accumulators, no reduction pass
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = i * 16 + (lane & 15);
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + wave * 32 + j * 16 + 4 * (lane >> 4);
+        if (n >= N) continue;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if (bias) {
+          const uint2 braw = *reinterpret_cast<const uint2*>(bias + n);
+          v[0] += lo_bf16(braw.x); v[1] += hi_bf16(braw.x); v[2] += lo_bf16(braw.y); v[3] += hi_bf16(braw.y);
+        }
+        *reinterpret_cast<uint2*>(c + (int64_t)m * ldc + n) = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
+      }
+    }
+    return;
+  }
   float* out = ws + (int64_t)ks * M * N;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -940,7 +963,9 @@ PA_EXPORT int pa_gemm_small_m(const void* a, int64_t lda, const void* b, int64_t
     attr_set = true;
   }
   hipLaunchKernelGGL(gemm_small_m_kernel, dim3((N + kSmBN - 1) / kSmBN, splits), dim3(kSmNW * 64), smem, st,
-                     (const uint16_t*)a, lda, (const uint16_t*)b, ldb, ws, M, N, K / splits);
+                     (const uint16_t*)a, lda, (const uint16_t*)b, ldb, ws, M, N, K / splits, (const uint16_t*)bias,
+                     (uint16_t*)c, ldc);
+  if (splits == 1) return (int)hipGetLastError();
   const int64_t n4 = (int64_t)M * N / 4;
   hipLaunchKernelGGL(gemm_small_m_reduce_k, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, ws,
                      (const uint16_t*)bias, (uint16_t*)c, ldc, M, N, splits);

@@ -199,7 +199,7 @@ def gemm_small_m(a, b, bias=None, splits=None, cus=256):
         while blocks * splits * 2 <= 2 * cus and K % (64 * splits * 2) == 0 and K // (splits * 2) >= 256:
             splits *= 2
     out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
-    ws = torch.empty(splits * M * N, dtype=torch.float32, device=a.device)
+    ws = torch.empty(splits * M * N if splits > 1 else 1, dtype=torch.float32, device=a.device)
     L.call("pa_gemm_small_m", L.ptr(a), a.stride(0), L.ptr(b), b.stride(0), L.ptr(out), out.stride(0), L.ptr(bias),
            L.ptr(ws), M, N, K, int(splits), L.stream_ptr())
     return out

@@ -1,2 +1,2 @@
 #!/bin/bash
-bash "$(dirname "$0")/gpu_prof.sh" resnet50_r1c --skip-gpt 1 --resnet-steps 10
+bash "$(dirname "$0")/gpu_prof.sh" resnet50_r1d --skip-gpt 1 --resnet-steps 10
