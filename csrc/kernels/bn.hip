@@ -26,23 +26,30 @@ __device__ __forceinline__ void st8(uint16_t* p, const float* f) { store8<bf16>(
 
 // MODE 0: acc1 = sum x, acc2 = sum x^2.
 // MODE 1: dyp = relu ? (y > 0 ? dy : 0) : dy; acc1 = sum dyp, acc2 = sum dyp * (x - mean).
-template <int MODE, bool RELU>
+// MASKX (with RELU, no residual in the forward): the relu mask is recomputed from x as
+// x * scale + shift > 0 with the forward's scale / shift (ss), the same expression the forward applied,
+// so y is not read (one tensor fewer in both backward passes).
+template <int MODE, bool RELU, bool MASKX = false>
 __global__ __launch_bounds__(kThreads) void bn_reduce_k(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
                                                         const uint16_t* __restrict__ y, const float* __restrict__ mean,
                                                         float* __restrict__ partial, int64_t R, int C, int CB,
-                                                        int64_t rows_per_chunk) {
+                                                        int64_t rows_per_chunk, const float* __restrict__ ss = nullptr) {
   const int tcx = CB >> 3;               // lanes along channels
   const int rpi = kThreads / tcx;        // rows per iteration
   const int tx = threadIdx.x % tcx, ty = threadIdx.x / tcx;
   const int c0 = blockIdx.x * CB + tx * 8;
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
   const int64_t r1 = min(R, r0 + rows_per_chunk);
-  float a1[8], a2[8], mu[8];
+  float a1[8], a2[8], mu[8], sc[8], sh[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { a1[j] = 0.f; a2[j] = 0.f; mu[j] = 0.f; }
+  for (int j = 0; j < 8; ++j) { a1[j] = 0.f; a2[j] = 0.f; mu[j] = 0.f; sc[j] = 0.f; sh[j] = 0.f; }
   if (MODE == 1) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) mu[j] = mean[c0 + j];
+  }
+  if (MASKX) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { sc[j] = ss[c0 + j]; sh[j] = ss[C + c0 + j]; }
   }
   // U rows per trip keep U 16-byte loads per tensor in flight (the stats pass reads one tensor)
   constexpr int U = MODE == 0 ? 4 : 2;
@@ -54,7 +61,12 @@ __global__ __launch_bounds__(kThreads) void bn_reduce_k(const uint16_t* __restri
     if (MODE == 1) {
 #pragma unroll
       for (int u = 0; u < U; ++u) ld8(dy + (r + u * rpi) * C + c0, gs[u]);
-      if (RELU) {
+      if (RELU && MASKX) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) gs[u][j] = xs[u][j] * sc[j] + sh[j] > 0.f ? gs[u][j] : 0.f;
+      } else if (RELU) {
         float ys[U][8];
 #pragma unroll
         for (int u = 0; u < U; ++u) ld8(y + (r + u * rpi) * C + c0, ys[u]);
@@ -86,7 +98,10 @@ __global__ __launch_bounds__(kThreads) void bn_reduce_k(const uint16_t* __restri
     } else {
       float ga[8];
       ld8(dy + r * C + c0, ga);
-      if (RELU) {
+      if (RELU && MASKX) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ga[j] = xa[j] * sc[j] + sh[j] > 0.f ? ga[j] : 0.f;
+      } else if (RELU) {
         float ya[8];
         ld8(y + r * C + c0, ya);
 #pragma unroll
@@ -228,19 +243,25 @@ __global__ __launch_bounds__(kThreads) void bn_apply_k(const uint16_t* __restric
   }
 }
 
-// dx = a * dyp - bc * x + d0; dres = dyp
-template <bool RELU, bool DRES>
+// dx = a * dyp - bc * x + d0; dres = dyp   (MASKX: relu mask from x * scale + shift, see bn_reduce_k)
+template <bool RELU, bool DRES, bool MASKX = false>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply_k(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
                                                            const uint16_t* __restrict__ y, const float* __restrict__ coef,
                                                            uint16_t* __restrict__ dx, uint16_t* __restrict__ dres,
-                                                           int64_t nvec, int C) {
+                                                           int64_t nvec, int C, const float* __restrict__ ss = nullptr) {
   const int cv = C >> 3;
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * kThreads) {
     const int c0 = (int)(i % cv) * 8;
     float g[8], f[8];
     ld8(dy + i * 8, g);
     ld8(x + i * 8, f);
-    if (RELU) {
+    if (RELU && MASKX) {
+      float sc[8], sh[8];
+      load8<float>(ss + c0, sc);
+      load8<float>(ss + C + c0, sh);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = f[j] * sc[j] + sh[j] > 0.f ? g[j] : 0.f;
+    } else if (RELU) {
       float yy[8];
       ld8(y + i * 8, yy);
 #pragma unroll
@@ -333,14 +354,19 @@ PA_EXPORT int pa_bn_fwd_nhwc(const void* x, const void* res, void* y, const floa
 
 // Backward. dy, x, y: [R, C] bf16 (y only read when relu); dx out; dres out (null: no residual
 // gradient); dw, db fp32 [C] out (nullable); coef: [3, C] workspace; partial: 2 * chunks * C.
+// ss: the forward's [2, C] scale / shift, given for relu without residual (mask from x, y not read).
 PA_EXPORT int pa_bn_bwd_nhwc(const void* dy, const void* x, const void* y, void* dx, void* dres, const float* w,
                              const float* mean, const float* rstd, float* dw, float* db, float* partial, float* coef,
-                             int64_t R, int C, int relu, int global_stats, hipStream_t st) {
+                             int64_t R, int C, int relu, int global_stats, const float* ss, hipStream_t st) {
   if (C % 8 != 0 || R < 1) return 3;
   int CB, chunks;
   int64_t rpc;
   plan(R, C, &CB, &chunks, &rpc);
-  if (relu)
+  const bool maskx = relu && ss != nullptr;  // relu mask from x and the forward's scale / shift, y unused
+  if (maskx)
+    hipLaunchKernelGGL((bn_reduce_k<1, true, true>), dim3(C / CB, chunks), dim3(kThreads), 0, st, (const uint16_t*)x,
+                       (const uint16_t*)dy, nullptr, mean, partial, R, C, CB, rpc, ss);
+  else if (relu)
     hipLaunchKernelGGL((bn_reduce_k<1, true>), dim3(C / CB, chunks), dim3(kThreads), 0, st, (const uint16_t*)x,
                        (const uint16_t*)dy, (const uint16_t*)y, mean, partial, R, C, CB, rpc);
   else
@@ -355,7 +381,10 @@ PA_EXPORT int pa_bn_bwd_nhwc(const void* dy, const void* x, const void* y, void*
 #define PA_BN_BWD(RL, DR)                                                                                         \
   hipLaunchKernelGGL((bn_bwd_apply_k<RL, DR>), dim3(g), dim3(kThreads), 0, st, (const uint16_t*)dy,                \
                      (const uint16_t*)x, (const uint16_t*)y, coef, (uint16_t*)dx, (uint16_t*)dres, nvec, C)
-  if (relu && dres) PA_BN_BWD(true, true);
+  if (maskx) {
+    hipLaunchKernelGGL((bn_bwd_apply_k<true, false, true>), dim3(g), dim3(kThreads), 0, st, (const uint16_t*)dy,
+                       (const uint16_t*)x, nullptr, coef, (uint16_t*)dx, nullptr, nvec, C, ss);
+  } else if (relu && dres) PA_BN_BWD(true, true);
   else if (relu) PA_BN_BWD(true, false);
   else if (dres) PA_BN_BWD(false, true);
   else PA_BN_BWD(false, false);

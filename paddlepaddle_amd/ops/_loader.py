@@ -115,7 +115,7 @@ def _declare(L):
         # batch norm (NHWC)
         "pa_bn_chunks": [_i64, _i32],
         "pa_bn_fwd_nhwc": [_vp] * 11 + [_i64, _i32, _f32, _f32, _i32, _i32, _vp],
-        "pa_bn_bwd_nhwc": [_vp] * 12 + [_i64, _i32, _i32, _i32, _vp],
+        "pa_bn_bwd_nhwc": [_vp] * 12 + [_i64, _i32, _i32, _i32, _vp, _vp],
         # fused decode step
         "pa_add_rms_norm_fwd": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _f32, _i32, _vp],
         "pa_decode_rope_cache": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i64, _i32, _vp],

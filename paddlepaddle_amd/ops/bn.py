@@ -70,13 +70,16 @@ class _BNActHIP(torch.autograd.Function):
                L.ptr(running_mean if training else None), L.ptr(running_var if training else None), L.ptr(mean),
                L.ptr(rstd), L.ptr(partial), L.ptr(ss), R, C, float(momentum), float(eps), int(relu), int(training),
                L.stream_ptr())
-        ctx.save_for_backward(x2, y if relu else None, weight, mean, rstd)
+        # relu without residual: the backward recomputes the mask from x with scale / shift (ss) instead of
+        # reading y; with a residual the mask needs y
+        mask_x = bool(relu) and residual is None
+        ctx.save_for_backward(x2, y if relu and not mask_x else None, weight, mean, rstd, ss if mask_x else None)
         ctx.flags = (bool(relu), bool(training), residual is not None, weight is not None, bias is not None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x2, y, weight, mean, rstd = ctx.saved_tensors
+        x2, y, weight, mean, rstd, ss = ctx.saved_tensors
         relu, training, has_res, has_w, has_b = ctx.flags
         R, C = x2.shape
         dev = x2.device
@@ -89,7 +92,7 @@ class _BNActHIP(torch.autograd.Function):
         coef = torch.empty(3, C, dtype=torch.float32, device=dev)
         L.call("pa_bn_bwd_nhwc", L.ptr(dy), L.ptr(x2), L.ptr(y), L.ptr(dx), L.ptr(dres), L.ptr(weight), L.ptr(mean),
                L.ptr(rstd), L.ptr(dw), L.ptr(db), L.ptr(partial), L.ptr(coef), R, C, int(relu), int(not training),
-               L.stream_ptr())
+               L.ptr(ss), L.stream_ptr())
         if dw is not None and dw.dtype != weight.dtype:
             dw = dw.to(weight.dtype)
         return dx, dw, db, dres, None, None, None, None, None, None
