@@ -788,8 +788,9 @@ int dispatch_layout(const GemmArgs& a, int a_kmajor, int b_kmajor, int splits, h
 // fp32 slab; pa_gemm_small_m_reduce sums the slabs (+ bias) into bf16. Without a split the accumulators
 // go straight to C. (A last-arriving-split reduction inside the kernel measured 2-3x slower: the agent-scope
 // release fence it needs writes back the whole XCD L2 in every workgroup.)
-constexpr int kSmBM = 64, kSmBN = 128, kSmNW = 4, kSmStages = 4;
+constexpr int kSmBM = 64, kSmBN = 128, kSmNW = 4;
 
+template <int kSmStages>
 __global__ __launch_bounds__(kSmNW * 64, 1) void gemm_small_m_kernel(const uint16_t* __restrict__ a, int64_t lda,
                                                                     const uint16_t* __restrict__ b, int64_t ldb,
                                                                     float* __restrict__ ws, int M, int N, int k_per,
@@ -954,17 +955,26 @@ PA_EXPORT int pa_conv2d_nhwc_fwd(const void* x, const void* w, const void* bias,
 // Decode-shape GEMM: c[M, N] (bf16, row stride ldc) = a[M, K] (K-major) . b[K, N] (N-major) (+ bias),
 // M <= 64, K % (64 * splits) == 0, N % 8 == 0; `ws` = fp32 workspace of splits * M * N floats.
 PA_EXPORT int pa_gemm_small_m(const void* a, int64_t lda, const void* b, int64_t ldb, void* c, int64_t ldc,
-                              const void* bias, float* ws, int M, int N, int K, int splits, hipStream_t st) {
+                              const void* bias, float* ws, int M, int N, int K, int splits, int stages, hipStream_t st) {
   if (M < 1 || M > kSmBM || N % 8 != 0 || splits < 1 || K % (kBK * splits) != 0 || lda % 8 || ldb % 8) return 1;
-  const int smem = kSmStages * (kSmBM + kSmBN) * kBK * 2;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_small_m_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(gemm_small_m_kernel, dim3((N + kSmBN - 1) / kSmBN, splits), dim3(kSmNW * 64), smem, st,
-                     (const uint16_t*)a, lda, (const uint16_t*)b, ldb, ws, M, N, K / splits, (const uint16_t*)bias,
-                     (uint16_t*)c, ldc);
+  if (stages != 3 && stages != 4) return 2;
+  // 4 stages: 96 KiB LDS, one workgroup per CU; 3 stages: 72 KiB, two per CU
+  const int smem = stages * (kSmBM + kSmBN) * kBK * 2;
+  static bool attr_set[2] = {false, false};
+  const dim3 grid((N + kSmBN - 1) / kSmBN, splits), block(kSmNW * 64);
+#define PA_SMM(S)                                                                                                \
+  do {                                                                                                          \
+    if (!attr_set[S - 3]) {                                                                                     \
+      (void)hipFuncSetAttribute((const void*)gemm_small_m_kernel<S>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                smem);                                                                          \
+      attr_set[S - 3] = true;                                                                                   \
+    }                                                                                                           \
+    hipLaunchKernelGGL(gemm_small_m_kernel<S>, grid, block, smem, st, (const uint16_t*)a, lda, (const uint16_t*)b, \
+                       ldb, ws, M, N, K / splits, (const uint16_t*)bias, (uint16_t*)c, ldc);                    \
+  } while (0)
+  if (stages == 3) PA_SMM(3);
+  else PA_SMM(4);
+#undef PA_SMM
   if (splits == 1) return (int)hipGetLastError();
   const int64_t n4 = (int64_t)M * N / 4;
   hipLaunchKernelGGL(gemm_small_m_reduce_k, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, ws,

@@ -190,7 +190,7 @@ def small_m_supported(a, b):
             and N % 8 == 0 and K % 64 == 0 and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0)
 
 
-def gemm_small_m(a, b, bias=None, splits=None, cus=256):
+def gemm_small_m(a, b, bias=None, splits=None, cus=256, stages=4):
     M, K = a.shape
     N = b.shape[1]
     if splits is None:
@@ -201,5 +201,26 @@ def gemm_small_m(a, b, bias=None, splits=None, cus=256):
     out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
     ws = torch.empty(splits * M * N if splits > 1 else 1, dtype=torch.float32, device=a.device)
     L.call("pa_gemm_small_m", L.ptr(a), a.stride(0), L.ptr(b), b.stride(0), L.ptr(out), out.stride(0), L.ptr(bias),
-           L.ptr(ws), M, N, K, int(splits), L.stream_ptr())
+           L.ptr(ws), M, N, K, int(splits), int(stages), L.stream_ptr())
     return out
+
+
+def small_m_variants(M, N, K, cus=256):
+    """(splits, stages) candidates for a decode GEMM, timed by the autotuner: split counts that divide the
+    K tiles (at least 4 K-tiles per workgroup) and put between ~0.5 and 4 workgroups per CU, each with the
+    4-stage (1 workgroup / CU) and 3-stage (2 / CU) LDS ring."""
+    kt = K // 64
+    blocks = -(-N // 128)
+    out = []
+    for d in range(1, kt + 1):
+        if kt % d or kt // d < 4:
+            continue
+        wgs = blocks * d
+        if wgs > 6 * cus or (wgs < cus // 2 and kt // d > 4 and d < kt):
+            continue
+        out.append(d)
+    if not out:
+        out = [1]
+    # keep at most 4 split counts: the ones closest to 1 and 2 workgroups per CU
+    out = sorted(out, key=lambda d: min(abs(blocks * d - cus), abs(blocks * d - 2 * cus)))[:4]
+    return [(d, st) for d in sorted(out) for st in (4, 3)]

@@ -83,11 +83,17 @@ def _blas_fwd(x2, w, b=None):
 
 def _fwd_mm(x2, w, b=None):
     if x2.shape[0] <= 64 and G.small_m_supported(x2, w):
-        key = ("fwd_small_m", x2.shape[0], w.shape[1], x2.shape[1], b is not None)
-        ch = G.choose(key, {"blas": lambda: _blas_fwd(x2, w, b), "hip": lambda: G.gemm_small_m(x2, w, b)},
-                      cold=True)
-        if ch == "hip":
-            return G.gemm_small_m(x2, w, b)
+        M, K, N = x2.shape[0], x2.shape[1], w.shape[1]
+        key = ("fwd_small_m", M, N, K, b is not None)
+        cands = {"blas": lambda: _blas_fwd(x2, w, b)}
+        for d, st in G.small_m_variants(M, N, K):
+            cands[f"hip_s{d}_st{st}"] = (lambda d=d, st=st: G.gemm_small_m(x2, w, b, splits=d, stages=st))
+        ch = G.choose(key, cands, cold=True)
+        if ch.startswith("hip"):
+            if ch == "hip":  # FLAGS_gemm_backend=hip: default split heuristic
+                return G.gemm_small_m(x2, w, b)
+            d, st = (int(v[1:]) for v in ch[4:].replace("st", "t").split("_"))
+            return G.gemm_small_m(x2, w, b, splits=d, stages=st)
         return _blas_fwd(x2, w, b)
     if G.supported(x2, w):
         key = ("fwd", x2.shape[0], w.shape[1], x2.shape[1], b is not None)

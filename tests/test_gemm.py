@@ -131,13 +131,15 @@ def test_conv_implicit_gemm_dgrad(k, pad):
     torch.testing.assert_close(w.grad.float(), wr.grad, atol=0.5, rtol=3e-2)
 
 
-@pytest.mark.parametrize("M,K,N,splits", [(32, 4096, 1280, None), (1, 512, 264, 2), (64, 1024, 4096, 4), (17, 256, 8, 1)])
-def test_gemm_small_m_decode_shapes(M, K, N, splits):
+@pytest.mark.parametrize("stages", [4, 3])
+@pytest.mark.parametrize("M,K,N,splits", [(32, 4096, 1280, None), (1, 512, 264, 2), (64, 1024, 4096, 4), (17, 256, 8, 1),
+                                          (32, 11008, 512, 43)])
+def test_gemm_small_m_decode_shapes(M, K, N, splits, stages):
     g = torch.Generator(device=DEV).manual_seed(9)
     a = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
     b = (torch.randn(K, N, device=DEV, generator=g) * 0.05).to(torch.bfloat16)
     bias = torch.randn(N, device=DEV, generator=g).to(torch.bfloat16)
     assert G.small_m_supported(a, b)
-    c = G.gemm_small_m(a, b, bias, splits=splits)
+    c = G.gemm_small_m(a, b, bias, splits=splits, stages=stages)
     ref = a.float() @ b.float() + bias.float()
     torch.testing.assert_close(c.float(), ref, atol=0.05, rtol=2e-2)
