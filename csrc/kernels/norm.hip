@@ -306,4 +306,39 @@ PA_EXPORT int pa_layer_norm_bwd(const void* dy, const void* x, const void* w, co
   return 0;
 }
 
+// Weight / bias gradient finalize of the norm backwards in one launch: out_a[c] = sum_p part_a[p][c],
+// out_b[c] = sum_p part_b[p][c] (part_b / out_b may be null), written in the parameters' dtypes.
+// Block = 64 columns x 4 part groups, folded through LDS; grid (cols / 64, 2).
+__global__ __launch_bounds__(256) void reduce_parts_k(const float* __restrict__ pa, const float* __restrict__ pb,
+                                                      void* oa, void* ob, int nparts, int64_t cols, int dta, int dtb) {
+  const float* part = blockIdx.y == 0 ? pa : pb;
+  void* out = blockIdx.y == 0 ? oa : ob;
+  const int dt = blockIdx.y == 0 ? dta : dtb;
+  if (part == nullptr || out == nullptr) return;
+  const int cx = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + cx;
+  float acc = 0.f;
+  if (c < cols) {
+#pragma unroll 8
+    for (int p = g; p < nparts; p += 4) acc += part[(int64_t)p * cols + c];
+  }
+  __shared__ float sm[4][64];
+  sm[g][cx] = acc;
+  __syncthreads();
+  if (g == 0 && c < cols) {
+    const float v = sm[0][cx] + sm[1][cx] + sm[2][cx] + sm[3][cx];
+    if (dt == kF32) reinterpret_cast<float*>(out)[c] = v;
+    else if (dt == kBF16) reinterpret_cast<bf16*>(out)[c] = from_f<bf16>(v);
+    else reinterpret_cast<f16*>(out)[c] = from_f<f16>(v);
+  }
+}
+
+PA_EXPORT int pa_reduce_parts(const float* pa, const float* pb, void* oa, void* ob, int nparts, int64_t cols, int dta,
+                              int dtb, hipStream_t st) {
+  hipLaunchKernelGGL(reduce_parts_k, dim3((unsigned)((cols + 63) / 64), 2), dim3(256), 0, st, pa, pb, oa, ob, nparts,
+                     cols, dta, dtb);
+  PA_CHECK_LAUNCH();
+  return 0;
+}
+
 PA_EXPORT int pa_version() { return 1; }

@@ -78,7 +78,7 @@ def _declare(L):
         "pa_rms_norm_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp],
         "pa_layer_norm_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _f32, _i32, _vp],
         "pa_layer_norm_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp],
-        "pa_reduce_cols_f32": [_vp, _vp, _i64, _i64, _i64, _i32, _vp],
+        "pa_reduce_parts": [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp],
         # softmax / cross entropy
         "pa_softmax_fwd": [_vp, _vp, _i64, _i64, _i32, _vp],
         "pa_softmax_bwd": [_vp, _vp, _vp, _i64, _i64, _i32, _vp],

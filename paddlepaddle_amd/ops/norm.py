@@ -13,6 +13,19 @@ from . import _loader as L
 from ..framework.trace_hook import static_op
 
 
+def _finalize_parts(pa, pb, dta, dtb, nparts, cols):
+    """Sum the [nparts, cols] fp32 partials of the weight (and bias) gradient into the parameters' dtypes:
+    one HIP launch for both instead of a reduction + a cast each."""
+    dev = (pa if pa is not None else pb).device
+    if L.has("pa_reduce_parts") and all(d in L._DT for d in (dta, dtb) if d is not None):
+        oa = torch.empty(cols, dtype=dta, device=dev) if pa is not None else None
+        ob = torch.empty(cols, dtype=dtb, device=dev) if pb is not None else None
+        L.call("pa_reduce_parts", L.ptr(pa), L.ptr(pb), L.ptr(oa), L.ptr(ob), nparts, cols,
+               L._DT[dta] if dta is not None else 0, L._DT[dtb] if dtb is not None else 0, L.stream_ptr())
+        return oa, ob
+    return (pa.sum(0).to(dta) if pa is not None else None), (pb.sum(0).to(dtb) if pb is not None else None)
+
+
 def _rms_ref(x, w, eps):
     xf = x.float()
     r = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
@@ -57,7 +70,7 @@ class _RMSNormHIP(torch.autograd.Function):
         dw_part = torch.empty(nparts, cols, dtype=torch.float32, device=x2.device) if wc is not None else None
         L.call("pa_rms_norm_bwd", L.ptr(dy2), L.ptr(x2), L.ptr(wc), L.ptr(rstd), L.ptr(dx), L.ptr(dw_part),
                rows, cols, L.dcode(x2) | (nparts << 8), L.stream_ptr())
-        dw = dw_part.sum(0).to(ctx.w_dtype) if wc is not None else None
+        dw, _ = _finalize_parts(dw_part, None, ctx.w_dtype, None, nparts, cols) if wc is not None else (None, None)
         return dx.view(ctx.shape), dw, None
 
 
@@ -92,8 +105,8 @@ class _LayerNormHIP(torch.autograd.Function):
         db_part = torch.empty(nparts, cols, dtype=torch.float32, device=x2.device)
         L.call("pa_layer_norm_bwd", L.ptr(dy2), L.ptr(x2), L.ptr(wc), L.ptr(mean), L.ptr(rstd), L.ptr(dx),
                L.ptr(dw_part), L.ptr(db_part), L.ptr(None), rows, cols, L.dcode(x2) | (nparts << 8), L.stream_ptr())
-        dw = dw_part.sum(0).to(ctx.w_dtype) if wc is not None else None
-        db = db_part.sum(0).to(ctx.b_dtype) if ctx.has_b else None
+        dw, db = _finalize_parts(dw_part if wc is not None else None, db_part if ctx.has_b else None, ctx.w_dtype,
+                                 ctx.b_dtype, nparts, cols)
         return dx.view(ctx.shape), dw, db, None
 
 
