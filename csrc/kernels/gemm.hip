@@ -30,6 +30,8 @@
 //     accumulate into an existing C (gradient-accumulation fusion), bf16 or fp32 output.
 #include "common.h"
 
+#include <climits>
+
 using namespace pa;
 
 namespace {
@@ -140,6 +142,68 @@ __device__ __forceinline__ void stage(const uint16_t* __restrict__ g, int64_t ld
   }
 }
 
+// Weight gradient of a KxK NHWC convolution as a GEMM: dW^T[m = (kh*KW + kw)*C + c][n = co] =
+//   sum_p x[n_img, ho*s - pad + kh*dil, wo*s - pad + kw*dil, c] * dy[p][co],  p = (n_img, ho, wo).
+// A (M x K, MN-major: 8 consecutive m are 8 channels of one tap) is gathered per (pixel, tap) here; the
+// image is the one stage<256, false> builds (chunk lc of k-row `row` at slot lc ^ mn_swz(row)).
+// kglob = first pixel of the K tile (split-K slices included); taps outside the image read the zero page.
+// Per-lane gather state for the NQ pieces a lane stages per K tile: the (tap, channel) of its m chunk is
+// fixed for the whole K loop; the pixel (n, ho, wo) of its k-row advances by 64 pixels per K tile, updated
+// incrementally (no integer division inside the loop).
+template <int NW>
+struct ConvWState {
+  static constexpr int NQ = kBM / (8 * NW);
+  int c[NQ], hoff[NQ], woff[NQ];  // channel, kh*dil - pad, kw*dil - pad  (hoff = INT_MIN: m past M)
+  int n[NQ], ho[NQ], wo[NQ];
+};
+
+template <int NW>
+__device__ __forceinline__ void convw_init(const GemmArgs& p, int m0, int64_t kglob, ConvWState<NW>& st, int wave,
+                                           int lane) {
+  constexpr int CPR = kBM / 8;
+  const int hw = p.cHo * p.cWo;
+#pragma unroll
+  for (int i = 0; i < ConvWState<NW>::NQ; ++i) {
+    const int q = i * NW + wave;
+    const int lin = q * 64 + lane;
+    const int row = lin / CPR;
+    const int lc = (lin % CPR) ^ mn_swz(row);
+    const int m = m0 + lc * 8;
+    const int tap = m / p.cC, kh = tap / p.cKW, kw = tap - kh * p.cKW;
+    st.c[i] = m - tap * p.cC;
+    st.hoff[i] = m < p.M ? kh * p.cDil - p.cPadH : INT_MIN / 2;
+    st.woff[i] = kw * p.cDil - p.cPadW;
+    const int pix = (int)(kglob + row);
+    st.n[i] = pix / hw;
+    const int rem = pix - st.n[i] * hw;
+    st.ho[i] = rem / p.cWo;
+    st.wo[i] = rem - st.ho[i] * p.cWo;
+  }
+}
+
+template <int NW>
+__device__ __forceinline__ void convw_advance(const GemmArgs& p, ConvWState<NW>& st, int dho, int dwo) {
+#pragma unroll
+  for (int i = 0; i < ConvWState<NW>::NQ; ++i) {
+    st.wo[i] += dwo;
+    st.ho[i] += dho;
+    if (st.wo[i] >= p.cWo) { st.wo[i] -= p.cWo; st.ho[i] += 1; }
+    while (st.ho[i] >= p.cHo) { st.ho[i] -= p.cHo; st.n[i] += 1; }
+  }
+}
+
+template <int NW>
+__device__ __forceinline__ void stage_convw(const GemmArgs& p, const ConvWState<NW>& st, char* img, int wave) {
+#pragma unroll
+  for (int i = 0; i < ConvWState<NW>::NQ; ++i) {
+    const int q = i * NW + wave;
+    const int hi = st.ho[i] * p.cStride + st.hoff[i], wi = st.wo[i] * p.cStride + st.woff[i];
+    const bool ok = hi >= 0 && hi < p.cH && wi >= 0 && wi < p.cW;
+    const uint16_t* src = ok ? p.a + (((int64_t)st.n[i] * p.cH + hi) * p.cW + wi) * p.cC + st.c[i] : p.zero;
+    glds16(src, img + q * 1024);
+  }
+}
+
 // ---- fragment read: 16 rows (output dim) x 8 k for k-substep s (32 k) -> mfma operand
 template <int R, bool KMAJ>
 __device__ __forceinline__ bf16x8_t frag(const char* img, int rbase, int s, int lane) {
@@ -167,9 +231,11 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // NW = 8: waves 2 (M) x 4 (N), wave tile 128 x BN/4, 2 waves per SIMD.
 // NW = 4: waves 2 (M) x 2 (N), wave tile 128 x BN/2 (256 accumulator registers, 1 wave per SIMD):
 //         a third less LDS read traffic per MFMA than the 8-wave form.
-template <int BN, bool AK, bool BKM, int NW = 8>
+template <int BN, bool AK, bool BKM, int NW = 8, bool CONVW = false>
 __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmArgs p0) {
   const GemmArgs p = split_view<AK, BKM>(p0);
+  const int64_t kslice = CONVW ? (int64_t)blockIdx.y * p0.K : 0;  // first pixel of this split (conv wgrad)
+  (void)kslice;
   constexpr int WN = NW / 2;
   constexpr int A_BYTES = kBM * kBK * 2;
   constexpr int B_BYTES = BN * kBK * 2;
@@ -200,9 +266,21 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmArgs p0) {
     for (int j = 0; j < NR; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = p.K / kBK;
+  ConvWState<NW> cw;  // conv weight gradient: gather state of the A operand (tiles staged in order t = 0, 1, ..)
+  int cw_dho = 0, cw_dwo = 0;
+  if constexpr (CONVW) {
+    convw_init<NW>(p0, m0, kslice, cw, wave, lane);
+    cw_dho = kBK / p0.cWo;
+    cw_dwo = kBK - cw_dho * p0.cWo;
+  }
   auto stage_tile = [&](int t, int buf) {
     char* base = smem + buf * STAGE;
-    stage<kBM, AK, NW>(p.a, p.lda, m0, p.M, t * kBK, base, wave, lane);
+    if constexpr (CONVW) {
+      stage_convw<NW>(p0, cw, base, wave);
+      convw_advance<NW>(p0, cw, cw_dho, cw_dwo);
+    } else {
+      stage<kBM, AK, NW>(p.a, p.lda, m0, p.M, t * kBK, base, wave, lane);
+    }
     stage<BN, BKM, NW>(p.b, p.ldb, n0, p.N, t * kBK, base + A_BYTES, wave, lane);
   };
 
@@ -950,6 +1028,37 @@ PA_EXPORT int pa_conv2d_nhwc_fwd(const void* x, const void* w, const void* bias,
   g.cH = H; g.cW = W; g.cC = C; g.cHo = Ho; g.cWo = Wo; g.cKW = KW; g.cStride = stride; g.cPadH = pad_h;
   g.cPadW = pad_w; g.cDil = dil;
   return launch3s<true, true, true>(g, 1, st);
+}
+
+// Weight gradient of a KxK NHWC convolution, transposed: ws[splits][KH*KW*C][Cout] fp32 slabs (summed by the
+// caller) of dW^T = im2col(x)^T . dy, the im2col rows gathered on the fly (stage_convw). x [N, H, W, C],
+// dy [N, Ho, Wo, Cout] bf16; C % 8 == 0, Cout % 8 == 0, (N*Ho*Wo) % (64 * splits) == 0.
+PA_EXPORT int pa_conv2d_nhwc_wgrad(const void* x, const void* dy, float* ws, const void* zero, int N, int H, int W,
+                                   int C, int Cout, int KH, int KW, int stride, int pad_h, int pad_w, int dil, int Ho,
+                                   int Wo, int splits, hipStream_t st) {
+  const int64_t P = (int64_t)N * Ho * Wo;
+  if (C % 8 || Cout % 8 || splits < 1 || P % (64 * splits) || P / splits > 0x7fffffff) return 1;
+  GemmArgs g{};
+  g.a = (const uint16_t*)x; g.b = (const uint16_t*)dy; g.c = ws;
+  g.lda = 0; g.ldb = Cout; g.ldc = Cout;
+  g.M = KH * KW * C; g.N = Cout; g.K = (int)(P / splits);
+  g.flags = kEpiOutF32; g.alpha = 1.f;
+  g.c_split = (int64_t)g.M * Cout;
+  g.zero = (const uint16_t*)zero;
+  g.cH = H; g.cW = W; g.cC = C; g.cHo = Ho; g.cWo = Wo; g.cKW = KW; g.cStride = stride; g.cPadH = pad_h;
+  g.cPadW = pad_w; g.cDil = dil;
+  g.tiles_m = (g.M + kBM - 1) / kBM;
+  g.tiles_n = (g.N + 127) / 128;
+  const int smem = 2 * (kBM + 128) * kBK * 2;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<128, false, false, 8, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((gemm_bf16_kernel<128, false, false, 8, true>), dim3(g.tiles_m * g.tiles_n, splits), dim3(512),
+                     smem, st, g);
+  return (int)hipGetLastError();
 }
 
 // Decode-shape GEMM: c[M, N] (bf16, row stride ldc) = a[M, K] (K-major) . b[K, N] (N-major) (+ bias),

@@ -124,10 +124,35 @@ def _implicit_fwd(x, wk, b, N, H, W, C, Cout, KH, KW, stride, pad, dil):
     return out
 
 
+def _wgrad_splits(P, M, N, cus=256, max_ws_bytes=256 << 20):
+    """Split-K factor for the implicit weight gradient: about two workgroups per CU, K slices a multiple of
+    the 64-pixel tile, fp32 slabs within the workspace budget."""
+    tiles = -(-M // 256) * -(-N // 128)
+    s = 1
+    while (tiles * s * 2 <= 2 * cus and P % (64 * s * 2) == 0 and (s * 2) * M * N * 4 <= max_ws_bytes):
+        s *= 2
+    return s
+
+
+def _implicit_wgrad(x, dy, w, N, H, W, C, Cout, KH, KW, stride, pad, dil, Ho, Wo):
+    """dW [Cout, C, KH, KW] = im2col(x)^T . dy as a split-K implicit GEMM (csrc/kernels/gemm.hip
+    pa_conv2d_nhwc_wgrad: the im2col rows are gathered per pixel and tap on the fly, no im2col buffer)."""
+    M = KH * KW * C
+    splits = _wgrad_splits(N * Ho * Wo, M, Cout)
+    ws = torch.empty(splits, M, Cout, dtype=torch.float32, device=x.device)
+    L.call("pa_conv2d_nhwc_wgrad", L.ptr(x), L.ptr(dy), L.ptr(ws), L.ptr(_zero_page(x.device)), N, H, W, C, Cout, KH,
+           KW, stride, pad, pad, dil, Ho, Wo, splits, L.stream_ptr())
+    dwt = ws.sum(0) if splits > 1 else ws[0]
+    return dwt.view(KH, KW, C, Cout).permute(3, 2, 0, 1).to(w.dtype).contiguous(memory_format=torch.channels_last) \
+        if w.is_contiguous(memory_format=torch.channels_last) and not w.is_contiguous() else \
+        dwt.view(KH, KW, C, Cout).permute(3, 2, 0, 1).to(w.dtype).contiguous()
+
+
 class _ConvImplicit(torch.autograd.Function):
     """Forward: implicit GEMM. Data gradient (stride 1, no dilation): the same implicit GEMM over dY with
     the filter flipped and its channel axes swapped (W'[c, kh, kw, co] = W[co, KH-1-kh, KW-1-kw, c]),
-    padding KH-1-pad. Weight gradient and the strided data gradient: MIOpen."""
+    padding KH-1-pad. Weight gradient: split-K implicit GEMM gathering the im2col rows of x (any stride /
+    padding / dilation). The strided data gradient: MIOpen."""
 
     @staticmethod
     def forward(ctx, x, w, b, stride, pad, dil):
@@ -156,14 +181,37 @@ class _ConvImplicit(torch.autograd.Function):
             wt = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()
             Ho, Wo = dy.shape[1], dy.shape[2]
             dx = _implicit_fwd(dy, wt, None, N, Ho, Wo, Cout, C, KH, KW, 1, KH - 1 - pad, 1)
-        xc = x.permute(0, 3, 1, 2)
-        dyc = dy.permute(0, 3, 1, 2)
-        wc = w if w.is_contiguous(memory_format=torch.channels_last) else w.contiguous(memory_format=torch.channels_last)
-        mask = [ctx.needs_input_grad[0] and not own_dx, ctx.needs_input_grad[1], has_b and ctx.needs_input_grad[2]]
-        gi, gw, gb = torch.ops.aten.convolution_backward(dyc, xc, wc, [w.shape[0]] if has_b else None, [stride] * 2,
-                                                         [pad] * 2, [dil] * 2, False, [0, 0], 1, mask)
-        if gi is not None:
-            dx = gi.permute(0, 2, 3, 1)
+        Ho, Wo = dy.shape[1], dy.shape[2]
+        P = N * Ho * Wo
+        own_dw = (ctx.needs_input_grad[1] and L.has("pa_conv2d_nhwc_wgrad") and C % 8 == 0 and Cout % 8 == 0
+                  and P % 64 == 0)
+        if own_dw:
+            # per-shape choice against MIOpen's weight gradient (profiles/conv_wgrad_vs_miopen.log)
+            def _miopen_dw():
+                return torch.ops.aten.convolution_backward(
+                    dy.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2), w, None, [stride] * 2, [pad] * 2, [dil] * 2,
+                    False, [0, 0], 1, [False, True, False])[1]
+            key = ("convw", tuple(x.shape), tuple(w.shape), stride, pad, dil)
+            own_dw = G.choose(key, {"hip": lambda: _implicit_wgrad(x, dy, w, N, H, W, C, Cout, KH, KW, stride, pad,
+                                                                   dil, Ho, Wo),
+                                    "blas": _miopen_dw}) == "hip"
+        gw = None
+        if own_dw:
+            gw = _implicit_wgrad(x, dy, w, N, H, W, C, Cout, KH, KW, stride, pad, dil, Ho, Wo)
+        mask = [ctx.needs_input_grad[0] and not own_dx, ctx.needs_input_grad[1] and not own_dw,
+                has_b and ctx.needs_input_grad[2]]
+        gb = None
+        if any(mask):
+            xc = x.permute(0, 3, 1, 2)
+            dyc = dy.permute(0, 3, 1, 2)
+            wc = w if w.is_contiguous(memory_format=torch.channels_last) else \
+                w.contiguous(memory_format=torch.channels_last)
+            gi, gw2, gb = torch.ops.aten.convolution_backward(dyc, xc, wc, [w.shape[0]] if has_b else None,
+                                                              [stride] * 2, [pad] * 2, [dil] * 2, False, [0, 0], 1, mask)
+            if gi is not None:
+                dx = gi.permute(0, 2, 3, 1)
+            if gw2 is not None:
+                gw = gw2
         return dx, gw, gb, None, None, None
 
 

@@ -131,6 +131,29 @@ def test_conv_implicit_gemm_dgrad(k, pad):
     torch.testing.assert_close(w.grad.float(), wr.grad, atol=0.5, rtol=3e-2)
 
 
+@pytest.mark.parametrize("shape,C,Cout,k,stride,pad,dil", [((4, 8, 8), 64, 64, 3, 1, 1, 1),
+                                                          ((4, 16, 16), 64, 72, 3, 2, 1, 1),
+                                                          ((2, 12, 16), 128, 64, 3, 1, 1, 1),
+                                                          ((2, 8, 16), 64, 64, 5, 1, 2, 1),
+                                                          ((2, 8, 16), 64, 64, 3, 1, 2, 2)])
+def test_conv_implicit_gemm_wgrad(shape, C, Cout, k, stride, pad, dil):
+    """Weight gradient by the split-K implicit GEMM (im2col rows gathered per pixel and tap)."""
+    from paddlepaddle_amd.ops import conv as Cv
+    torch.manual_seed(3)
+    N, H, W = shape
+    x = torch.randn(N, H, W, C, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(Cout, C, k, k, device=DEV) * 0.05).to(torch.bfloat16).requires_grad_(True)
+    y = Cv._ConvImplicit.apply(x, w, None, stride, pad, dil)
+    P = y.shape[0] * y.shape[1] * y.shape[2]
+    assert P % 64 == 0  # the HIP weight-gradient path, not MIOpen
+    wr = w.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), wr, None, stride, pad, dil)
+    g = torch.randn_like(yr)
+    y.backward(g.permute(0, 2, 3, 1).to(torch.bfloat16))
+    yr.backward(g)
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=0.5, rtol=3e-2)
+
+
 @pytest.mark.parametrize("stages", [4, 3])
 @pytest.mark.parametrize("M,K,N,splits", [(32, 4096, 1280, None), (1, 512, 264, 2), (64, 1024, 4096, 4), (17, 256, 8, 1),
                                           (32, 11008, 512, 43)])
