@@ -126,7 +126,9 @@ class _DenseTable:
 
     def pull(self, min_version):
         with self.cv:
-            self.cv.wait_for(lambda: self.version >= min_version, timeout=600)
+            if not self.cv.wait_for(lambda: self.version >= min_version, timeout=600):
+                raise TimeoutError(f"dense table: version {min_version} not reached (at {self.version}); "
+                                   f"a trainer stopped pushing")
             return self.w.clone(), self.version
 
 
@@ -155,7 +157,8 @@ def _srv_barrier(key, n):
     with cv:
         _SRV["barriers"][key] = _SRV["barriers"].get(key, 0) + 1
         cv.notify_all()
-        cv.wait_for(lambda: _SRV["barriers"][key] >= n, timeout=900)
+        if not cv.wait_for(lambda: _SRV["barriers"][key] >= n, timeout=900):
+            raise TimeoutError(f"barrier {key}: {_SRV['barriers'][key]} of {n} trainers arrived")
     return True
 
 
