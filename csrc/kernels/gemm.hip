@@ -110,6 +110,10 @@ __device__ __forceinline__ s16x4 lds_tr(const char* p) {
 
 // swizzle of an MN-major image row (even chunk XOR so 32-B pairs stay together)
 __device__ __forceinline__ int mn_swz(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
+// the swizzle restricted to a k-row of R columns (R / 8 chunks): a no-op for R >= 128; for R = 64 it keeps
+// the chunk inside its row (slot <-> global chunk stays a bijection)
+template <int R>
+__device__ __forceinline__ int mn_swz_r(int k) { return mn_swz(k) & (R / 8 - 1); }
 
 // ---- staging of one operand tile (R rows of the output dimension x 64 k) into LDS
 // K-major: image [R][64] (128-B rows).  MN-major: image [64][R] (2R-byte rows).
@@ -134,7 +138,7 @@ __device__ __forceinline__ void stage(const uint16_t* __restrict__ g, int64_t ld
       const int q = i * NW + wave;
       const int lin = q * 64 + lane;
       const int row = lin / CPR;                // k
-      const int lc = (lin % CPR) ^ mn_swz(row);
+      const int lc = (lin % CPR) ^ mn_swz_r<R>(row);
       int gc = r0 + lc * 8;
       gc = gc < rmax ? gc : rmax - 8;
       glds16(g + (int64_t)(k0 + row) * ld + gc, img + q * 1024);
@@ -217,8 +221,8 @@ __device__ __forceinline__ bf16x8_t frag(const char* img, int rbase, int s, int 
     const int col = rbase + pp * 4;           // first of 4 columns supplied by this lane
     const int lc = col >> 3, sub = (col & 7) * 2;
     const int k1 = s * 32 + g * 8 + q, k2 = k1 + 4;
-    f.h[0] = lds_tr(img + k1 * (R * 2) + ((lc ^ mn_swz(k1)) << 4) + sub);
-    f.h[1] = lds_tr(img + k2 * (R * 2) + ((lc ^ mn_swz(k2)) << 4) + sub);
+    f.h[0] = lds_tr(img + k1 * (R * 2) + ((lc ^ mn_swz_r<R>(k1)) << 4) + sub);
+    f.h[1] = lds_tr(img + k2 * (R * 2) + ((lc ^ mn_swz_r<R>(k2)) << 4) + sub);
   }
   return f.v;
 }
@@ -1035,9 +1039,10 @@ PA_EXPORT int pa_conv2d_nhwc_fwd(const void* x, const void* w, const void* bias,
 // dy [N, Ho, Wo, Cout] bf16; C % 8 == 0, Cout % 8 == 0, (N*Ho*Wo) % (64 * splits) == 0.
 PA_EXPORT int pa_conv2d_nhwc_wgrad(const void* x, const void* dy, float* ws, const void* zero, int N, int H, int W,
                                    int C, int Cout, int KH, int KW, int stride, int pad_h, int pad_w, int dil, int Ho,
-                                   int Wo, int splits, hipStream_t st) {
+                                   int Wo, int splits, int bn, hipStream_t st) {
   const int64_t P = (int64_t)N * Ho * Wo;
   if (C % 8 || Cout % 8 || splits < 1 || P % (64 * splits) || P / splits > 0x7fffffff) return 1;
+  if (bn != 64 && bn != 128 && bn != 256) return 2;
   GemmArgs g{};
   g.a = (const uint16_t*)x; g.b = (const uint16_t*)dy; g.c = ws;
   g.lda = 0; g.ldb = Cout; g.ldc = Cout;
@@ -1048,16 +1053,23 @@ PA_EXPORT int pa_conv2d_nhwc_wgrad(const void* x, const void* dy, float* ws, con
   g.cH = H; g.cW = W; g.cC = C; g.cHo = Ho; g.cWo = Wo; g.cKW = KW; g.cStride = stride; g.cPadH = pad_h;
   g.cPadW = pad_w; g.cDil = dil;
   g.tiles_m = (g.M + kBM - 1) / kBM;
-  g.tiles_n = (g.N + 127) / 128;
-  const int smem = 2 * (kBM + 128) * kBK * 2;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<128, false, false, 8, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr_set = true;
-  }
-  hipLaunchKernelGGL((gemm_bf16_kernel<128, false, false, 8, true>), dim3(g.tiles_m * g.tiles_n, splits), dim3(512),
-                     smem, st, g);
+  g.tiles_n = (g.N + bn - 1) / bn;
+  const int smem = 2 * (kBM + bn) * kBK * 2;
+  static bool attr_set[3] = {false, false, false};
+#define PA_WG(BNV, I)                                                                                           \
+  do {                                                                                                          \
+    if (!attr_set[I]) {                                                                                         \
+      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<BNV, false, false, 8, true>,                      \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, smem);                              \
+      attr_set[I] = true;                                                                                       \
+    }                                                                                                           \
+    hipLaunchKernelGGL((gemm_bf16_kernel<BNV, false, false, 8, true>), dim3(g.tiles_m * g.tiles_n, splits),     \
+                       dim3(512), smem, st, g);                                                                 \
+  } while (0)
+  if (bn == 256) PA_WG(256, 1);
+  else if (bn == 64) PA_WG(64, 2);
+  else PA_WG(128, 0);
+#undef PA_WG
   return (int)hipGetLastError();
 }
 

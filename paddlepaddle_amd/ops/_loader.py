@@ -109,7 +109,7 @@ def _declare(L):
                          _i32, _i32, _vp],
         "pa_gemm_small_m": [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp],
         "pa_conv2d_nhwc_fwd": [_vp, _vp, _vp, _vp, _vp] + [_i32] * 13 + [_vp],
-        "pa_conv2d_nhwc_wgrad": [_vp, _vp, _vp, _vp] + [_i32] * 14 + [_vp],
+        "pa_conv2d_nhwc_wgrad": [_vp, _vp, _vp, _vp] + [_i32] * 15 + [_vp],
         "pa_bias_gelu_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp],
         "pa_dropout_add_fwd": [_vp, _vp, _vp, _i64, _f32, ctypes.c_uint64, _i32, _vp],
         "pa_dropout_bwd": [_vp, _vp, _i64, _f32, ctypes.c_uint64, _i32, _vp],

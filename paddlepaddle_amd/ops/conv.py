@@ -124,10 +124,10 @@ def _implicit_fwd(x, wk, b, N, H, W, C, Cout, KH, KW, stride, pad, dil):
     return out
 
 
-def _wgrad_splits(P, M, N, cus=256, max_ws_bytes=256 << 20):
+def _wgrad_splits(P, M, N, bn=128, cus=256, max_ws_bytes=256 << 20):
     """Split-K factor for the implicit weight gradient: about two workgroups per CU, K slices a multiple of
     the 64-pixel tile, fp32 slabs within the workspace budget."""
-    tiles = -(-M // 256) * -(-N // 128)
+    tiles = -(-M // 256) * -(-N // bn)
     s = 1
     while (tiles * s * 2 <= 2 * cus and P % (64 * s * 2) == 0 and (s * 2) * M * N * 4 <= max_ws_bytes):
         s *= 2
@@ -138,10 +138,11 @@ def _implicit_wgrad(x, dy, w, N, H, W, C, Cout, KH, KW, stride, pad, dil, Ho, Wo
     """dW [Cout, C, KH, KW] = im2col(x)^T . dy as a split-K implicit GEMM (csrc/kernels/gemm.hip
     pa_conv2d_nhwc_wgrad: the im2col rows are gathered per pixel and tap on the fly, no im2col buffer)."""
     M = KH * KW * C
-    splits = _wgrad_splits(N * Ho * Wo, M, Cout)
+    bn = 256 if Cout % 256 == 0 else (64 if Cout <= 64 else 128)
+    splits = _wgrad_splits(N * Ho * Wo, M, Cout, bn)
     ws = torch.empty(splits, M, Cout, dtype=torch.float32, device=x.device)
     L.call("pa_conv2d_nhwc_wgrad", L.ptr(x), L.ptr(dy), L.ptr(ws), L.ptr(_zero_page(x.device)), N, H, W, C, Cout, KH,
-           KW, stride, pad, pad, dil, Ho, Wo, splits, L.stream_ptr())
+           KW, stride, pad, pad, dil, Ho, Wo, splits, bn, L.stream_ptr())
     dwt = ws.sum(0) if splits > 1 else ws[0]
     return dwt.view(KH, KW, C, Cout).permute(3, 2, 0, 1).to(w.dtype).contiguous(memory_format=torch.channels_last) \
         if w.is_contiguous(memory_format=torch.channels_last) and not w.is_contiguous() else \

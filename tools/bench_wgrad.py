@@ -38,5 +38,5 @@ for (H, C, stride) in [(56, 64, 1), (56, 128, 2), (28, 128, 1), (28, 256, 2), (1
     err = ((a.float() - b.float()).abs().max() / b.float().abs().max()).item()
     to, tm = timed(ours), timed(miopen)
     print(f"H{H} C{C} s{stride}: ours {to * 1e3:7.1f} us ({fl / to / 1e9:5.0f} TF) | MIOpen {tm * 1e3:7.1f} us "
-          f"({fl / tm / 1e9:5.0f} TF) x{tm / to:.2f} relerr {err:.1e} splits {Cv._wgrad_splits(B * Ho * Ho, 9 * C, C)}",
+          f"({fl / tm / 1e9:5.0f} TF) x{tm / to:.2f} relerr {err:.1e} splits {Cv._wgrad_splits(B * Ho * Ho, 9 * C, C, 256 if C % 256 == 0 else (64 if C <= 64 else 128))}",
           flush=True)
