@@ -28,7 +28,18 @@ def _t(x):
 # --------------------------------------------------------------------------------------- norms
 def fused_rms_norm(x, norm_weight, norm_bias, epsilon, begin_norm_axis, bias=None, residual=None, quant_scale=-1,
                    quant_round_type=0, quant_max_bound=0, quant_min_bound=0):
-    """out = rms_norm(x + bias + residual); returns (out, residual_out) when residual is given."""
+    """out = rms_norm(x + bias + residual); returns (out, residual_out) when residual is given. Residual without
+    bias: the add and the norm are one HIP pass (ops.add_rms_norm) when no gradient is needed."""
+    if residual is not None and bias is None and norm_weight is not None:
+        xt, rt = _t(x), _t(residual)
+        shape = xt.shape
+        cols = int(math.prod(shape[begin_norm_axis:]))
+        s, y = _ops.add_rms_norm(xt.reshape(-1, cols).contiguous(), rt.reshape(-1, cols).contiguous(),
+                                 _t(norm_weight).reshape(-1), epsilon)
+        y = y.reshape(shape)
+        if norm_bias is not None:
+            y = y + _t(norm_bias)
+        return _wrap(y), _wrap(s.reshape(shape))
     xt = _t(x)
     if bias is not None:
         xt = xt + _t(bias)
