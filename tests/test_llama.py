@@ -127,3 +127,22 @@ def test_llama_graph_decode_matches_eager_generate():
     agree = (ref._t == got._t).float().mean().item()
     assert agree > 0.9, (ref.numpy(), got.numpy())  # bf16 near-ties may flip a late token
     assert torch.equal(ref._t[:, :4], got._t[:, :4])
+
+
+@pytest.mark.gpu
+def test_llama_fused_inference_forward_matches_training_path():
+    """The inference layer loop (residual adds fused into the following RMSNorm, ops.add_rms_norm) gives the
+    same logits as the autograd path that runs the add and the norm separately."""
+    paddle.set_device("gpu")
+    paddle.seed(11)
+    cfg = LlamaConfig.tiny(hidden_size=512, num_attention_heads=4, num_key_value_heads=2, intermediate_size=1024,
+                           num_hidden_layers=3)
+    model = LlamaForCausalLM(cfg)
+    model.to(dtype="bfloat16")
+    ids = paddle.to_tensor(torch.randint(0, cfg.vocab_size, (2, 64), generator=torch.Generator().manual_seed(3))
+                           .numpy(), place=paddle.CUDAPlace(0))
+    ref = model(ids)._t.float()  # grad enabled: unfused path
+    with torch.no_grad():
+        got = model(ids)._t.float()
+    err = (got - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-2, err
