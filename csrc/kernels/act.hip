@@ -4,6 +4,8 @@
 // All kernels: 16-byte vectors per thread, grid-stride, grid capped at 256 CUs x 8 workgroups.
 #include "common.h"
 
+#include <algorithm>
+
 using namespace pa;
 
 namespace {
@@ -14,19 +16,12 @@ constexpr float kInvSqrt2 = 0.7071067811865476f;
 constexpr float kInvSqrt2Pi = 0.3989422804014327f;
 
 __device__ __forceinline__ float gelu_f(float x, bool approx) {
-  if (approx) {
-    const float u = kSqrt2OverPi * (x + kCoeff * x * x * x);
-    return 0.5f * x * (1.f + tanhf(u));
-  }
+  if (approx) return gelu_tanh_fast(x);
   return 0.5f * x * (1.f + erff(x * kInvSqrt2));
 }
 
 __device__ __forceinline__ float gelu_grad_f(float x, bool approx) {
-  if (approx) {
-    const float u = kSqrt2OverPi * (x + kCoeff * x * x * x);
-    const float t = tanhf(u);
-    return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kSqrt2OverPi * (1.f + 3.f * kCoeff * x * x);
-  }
+  if (approx) return gelu_tanh_grad_fast(x);
   return 0.5f * (1.f + erff(x * kInvSqrt2)) + x * kInvSqrt2Pi * __expf(-0.5f * x * x);
 }
 
@@ -65,15 +60,21 @@ __global__ __launch_bounds__(256) void gelu_bwd_k(const T* __restrict__ x, const
 
 // y[r, c] = gelu_tanh(x[r, c] + b[c])
 template <typename T>
+// 2-D grid: blockIdx.x = 2048-column strip (a thread's 8 columns and their bias are fixed), blockIdx.y strides
+// over the rows — no per-element index division.
 __global__ __launch_bounds__(256) void bias_gelu_fwd_k(const T* __restrict__ x, const T* __restrict__ b,
-                                                       T* __restrict__ y, int64_t nvec, int64_t cols) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
-    float v[8], bv[8];
-    load8<T>(x + i * 8, v);
-    load8<T>(b + (i * 8) % cols, bv);
+                                                       T* __restrict__ y, int64_t rows, int64_t cols) {
+  const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c >= cols) return;
+  float bv[8];
+  load8<T>(b + c, bv);
+#pragma unroll 4
+  for (int64_t r = blockIdx.y; r < rows; r += gridDim.y) {
+    float v[8];
+    load8<T>(x + r * cols + c, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = gelu_f(v[j] + bv[j], true);
-    store8<T>(y + i * 8, v);
+    for (int j = 0; j < 8; ++j) v[j] = gelu_tanh_fast(v[j] + bv[j]);
+    store8<T>(y + r * cols + c, v);
   }
 }
 
@@ -180,9 +181,10 @@ PA_EXPORT int pa_gelu_bwd(const void* x, const void* dy, void* dx, int64_t n, in
 
 PA_EXPORT int pa_bias_gelu_fwd(const void* x, const void* b, void* y, int64_t rows, int64_t cols, int dtype,
                                hipStream_t st) {
-  const int64_t nvec = rows * cols / 8;
-  PA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((bias_gelu_fwd_k<T>), dim3(grid_for(nvec)), dim3(256), 0, st,
-                                                 (const T*)x, (const T*)b, (T*)y, nvec, cols));
+  const unsigned gx = (unsigned)cdiv(cols / 8, 256);
+  const unsigned gy = (unsigned)std::max<int64_t>(1, std::min<int64_t>(rows, 2048 / gx));
+  PA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((bias_gelu_fwd_k<T>), dim3(gx, gy), dim3(256), 0, st,
+                                                 (const T*)x, (const T*)b, (T*)y, rows, cols));
   PA_CHECK_LAUNCH();
   return 0;
 }

@@ -89,6 +89,20 @@ template <> __device__ __forceinline__ void store8<float>(float* p, const float*
   *reinterpret_cast<float4*>(p + 4) = make_float4(f[4], f[5], f[6], f[7]);
 }
 
+// ---- tanh-approximated GELU without tanhf: with s = sigmoid(2u) = 1 / (1 + 2^(-2u log2 e)),
+// u = sqrt(2/pi) (x + 0.044715 x^3):  gelu(x) = x s,  gelu'(x) = s + 2 x s (1 - s) sqrt(2/pi) (1 + 3 * 0.044715 x^2).
+// One v_exp_f32 + one v_rcp_f32 per element (tanhf is a long VALU sequence; these epilogue / elementwise
+// passes are VALU-bound with it). Saturates correctly: 2^(+inf) -> s = 0, 2^(-inf) -> s = 1.
+__device__ __forceinline__ float gelu_sig2u(float x) {
+  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-2.8853900817779268f * u));  // 2 log2(e)
+}
+__device__ __forceinline__ float gelu_tanh_fast(float x) { return x * gelu_sig2u(x); }
+__device__ __forceinline__ float gelu_tanh_grad_fast(float x) {
+  const float s = gelu_sig2u(x);
+  return s + 2.f * x * s * (1.f - s) * 0.7978845608028654f * (1.f + 0.134145f * x * x);
+}
+
 // ---- wave / block reductions (wave64)
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

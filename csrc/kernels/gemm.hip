@@ -89,10 +89,7 @@ __device__ __forceinline__ GemmArgs split_view(const GemmArgs& p0) {
   return p;
 }
 
-__device__ __forceinline__ float gelu_tanh(float x) {
-  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
-  return 0.5f * x * (1.f + tanhf(u));
-}
+__device__ __forceinline__ float gelu_tanh(float x) { return gelu_tanh_fast(x); }
 
 // global_load_lds_dwordx4 issued from inline asm: hipcc treats a builtin LDS-DMA as a pending write to
 // every LDS object and puts s_waitcnt vmcnt(0) in front of the next ds_read, which would drain the

@@ -15,11 +15,7 @@ namespace {
 constexpr float kSqrt2OverPi = 0.7978845608028654f;
 constexpr float kCoeff = 0.044715f;
 
-__device__ __forceinline__ float gelu_tanh_grad(float x) {
-  const float u = kSqrt2OverPi * (x + kCoeff * x * x * x);
-  const float t = tanhf(u);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kSqrt2OverPi * (1.f + 3.f * kCoeff * x * x);
-}
+__device__ __forceinline__ float gelu_tanh_grad(float x) { return gelu_tanh_grad_fast(x); }
 
 // ---- counter-based RNG (64-bit mix, splitmix/murmur finaliser) -> uniform [0,1)
 __device__ __forceinline__ uint32_t hash32(uint64_t seed, uint64_t i) {
