@@ -66,7 +66,7 @@ class _RMSNormHIP(torch.autograd.Function):
         if dy2.dtype != x2.dtype:
             dy2 = dy2.to(x2.dtype)
         dx = torch.empty_like(x2)
-        nparts = min(max((rows + 63) // 64, 1), 512)
+        nparts = min(max((rows + 15) // 16, 1), 512)  # >= ~3 workgroups per CU in the weight-gradient pass
         dw_part = torch.empty(nparts, cols, dtype=torch.float32, device=x2.device) if wc is not None else None
         L.call("pa_rms_norm_bwd", L.ptr(dy2), L.ptr(x2), L.ptr(wc), L.ptr(rstd), L.ptr(dx), L.ptr(dw_part),
                rows, cols, L.dcode(x2) | (nparts << 8), L.stream_ptr())
@@ -100,7 +100,7 @@ class _LayerNormHIP(torch.autograd.Function):
         rows, cols = x2.shape
         dy2 = dy.contiguous().view(rows, cols).to(x2.dtype)
         dx = torch.empty_like(x2)
-        nparts = min(max((rows + 63) // 64, 1), 512)
+        nparts = min(max((rows + 15) // 16, 1), 512)  # >= ~3 workgroups per CU in the weight-gradient pass
         dw_part = torch.empty(nparts, cols, dtype=torch.float32, device=x2.device)
         db_part = torch.empty(nparts, cols, dtype=torch.float32, device=x2.device)
         L.call("pa_layer_norm_bwd", L.ptr(dy2), L.ptr(x2), L.ptr(wc), L.ptr(mean), L.ptr(rstd), L.ptr(dx),

@@ -34,3 +34,13 @@ ws = torch.empty(256 * C, dtype=torch.float32, device="cuda")
 t = timed(lambda: L.call("pa_bias_gelu_bwd", L.ptr(h), L.ptr(b), L.ptr(dy), L.ptr(dh), L.ptr(db), L.ptr(ws), R, C,
                          L.dcode(h), L.stream_ptr()))
 print(f"bias_gelu_bwd: {t:6.1f} us ({6 * R * C / t / 1e3:5.0f} GB/s)")
+
+from paddlepaddle_amd.ops import norm as Nm  # noqa: E402
+x = torch.randn(4096, 5120, device="cuda").to(torch.bfloat16).requires_grad_(True)
+w = torch.rand(5120, device="cuda").to(torch.bfloat16).requires_grad_(True)
+bb = torch.randn(5120, device="cuda").to(torch.bfloat16).requires_grad_(True)
+yy = Nm._LayerNormHIP.apply(x, w, bb, 1e-5)
+g = torch.randn_like(yy)
+tf = timed(lambda: Nm._LayerNormHIP.apply(x, w, bb, 1e-5), 20)
+tb = timed(lambda: torch.autograd.grad(Nm._LayerNormHIP.apply(x, w, bb, 1e-5), (x, w, bb), g), 20) - tf
+print(f"layer_norm [4096, 5120]: fwd {tf:6.1f} us  bwd {tb:6.1f} us")
