@@ -133,8 +133,12 @@ def _capturing():
 
 
 def _flush_caches(dev):
-    """Evict L2 and the 256 MB MALL (Infinity Cache): write a 512 MB scratch buffer."""
-    buf = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+    """Evict L2 and the 256 MB MALL (Infinity Cache): write a 512 MB scratch buffer (skipped when the device
+    has no room for it — the timing is then warm, which only biases the choice, never breaks it)."""
+    try:
+        buf = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+    except torch.OutOfMemoryError:
+        return None
     buf.zero_()
     return buf
 
