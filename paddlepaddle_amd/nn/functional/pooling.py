@@ -30,7 +30,21 @@ def _pad_arg(padding, n):
     return padding
 
 
+def _scalar(v):
+    if isinstance(v, (list, tuple)):
+        return v[0] if len(set(v)) == 1 else None
+    return v
+
+
 def _maxpool(n, x, kernel_size, stride, padding, return_mask, ceil_mode, data_format):
+    if n == 2 and data_format == "NHWC" and not isinstance(padding, str):
+        # channels-last HIP kernel (ops/pool.py): first-max mask kept as uint8, gather backward
+        from ...ops import pool as _pool
+        xt = T(x)
+        k, s, p = _scalar(kernel_size), _scalar(stride if stride is not None else kernel_size), _scalar(padding)
+        if k is not None and s is not None and p is not None and _pool.maxpool2d_nhwc_supported(
+                xt, k, s, p, ceil_mode=ceil_mode, return_mask=return_mask):
+            return _wrap(_pool.maxpool2d_nhwc(xt, k, s, p))
     t, cl = _cf(T(x), data_format)
     fn = {1: F.max_pool1d, 2: F.max_pool2d, 3: F.max_pool3d}[n]
     pad = _pad_arg(padding, n)

@@ -252,3 +252,20 @@ def test_dropout_add_statistics_and_grad():
     torch.manual_seed(5)
     b = ops.dropout_add(x.detach(), None, 0.3, True)
     assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,k,s,p", [((2, 17, 15, 64), 3, 2, 1), ((3, 12, 12, 32), 2, 2, 0), ((1, 9, 11, 16), 3, 1, 1)])
+def test_maxpool_nhwc_matches_torch(shape, k, s, p):
+    from paddlepaddle_amd.ops import pool as P
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(*shape, generator=g).to("cuda", torch.bfloat16).requires_grad_(True)
+    assert P.maxpool2d_nhwc_supported(x, k, s, p)
+    y = P.maxpool2d_nhwc(x, k, s, p)
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = torch.nn.functional.max_pool2d(xr, k, s, p)
+    assert torch.equal(y.float(), yr.permute(0, 2, 3, 1))
+    gy = torch.randn(yr.shape, generator=g).to("cuda")
+    y.backward(gy.permute(0, 2, 3, 1).to(torch.bfloat16))
+    yr.backward(gy.to(torch.bfloat16).float())
+    torch.testing.assert_close(x.grad.float(), xr.grad.permute(0, 2, 3, 1), atol=2e-2, rtol=1e-2)
