@@ -12,6 +12,7 @@ import re
 
 CATS = [
     ("bn/bn+relu(+add) (HIP)", re.compile(r"bn_(reduce|apply|bwd_apply|fwd_finalize|bwd_finalize)_k")),
+    ("maxpool NHWC (HIP)", re.compile(r"maxpool_nhwc_(fwd|bwd)_k")),
     ("miopen/ck(conv/bn)", re.compile(r"miopen|igemm|naive_conv|batchnorm|grouped_conv|SubTensorOp|MIOpen", re.I)),
     ("gemm(hipBLASLt/rocBLAS)", re.compile(r"^Cijk_|^Custom_Cijk|gemm|Gemm|rocblas")),
     ("flash_attn(HIP)", re.compile(r"fa_(fwd|bwd)|fa_delta|dq_convert")),
@@ -31,15 +32,38 @@ def category(name):
     return "other"
 
 
+def _window_rows(d, last_ms):
+    """kernel_stats-shaped rows rebuilt from kernel_trace.csv, restricted to the trace's last ``last_ms``."""
+    f = sorted(glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True))
+    if not f:
+        raise SystemExit(f"no kernel_trace.csv under {d}")
+    tr = [(r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(f[0]))]
+    t_end = max(e for _, _, e in tr)
+    agg = {}
+    for n, s, e in tr:
+        if s >= t_end - last_ms * 1e6:
+            c, t = agg.get(n, (0, 0))
+            agg[n] = (c + 1, t + e - s)
+    tot = sum(t for _, t in agg.values()) or 1
+    return [{"Name": n, "Calls": c, "TotalDurationNs": t, "AverageNs": t / c, "Percentage": 100.0 * t / tot}
+            for n, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--last-ms", type=float, default=0.0,
+                    help="only kernels that start in the last N ms of the trace (steady-state steps, excluding "
+                         "one-time per-shape tuning such as the MIOpen find runs)")
     a = ap.parse_args()
-    f = sorted(glob.glob(os.path.join(a.dir, "**", "*kernel_stats.csv"), recursive=True))
-    if not f:
-        raise SystemExit(f"no kernel_stats.csv under {a.dir}")
-    rows = list(csv.DictReader(open(f[0])))
+    if a.last_ms > 0:
+        rows = _window_rows(a.dir, a.last_ms)
+    else:
+        f = sorted(glob.glob(os.path.join(a.dir, "**", "*kernel_stats.csv"), recursive=True))
+        if not f:
+            raise SystemExit(f"no kernel_stats.csv under {a.dir}")
+        rows = list(csv.DictReader(open(f[0])))
     total = sum(float(r["TotalDurationNs"]) for r in rows)
     cats = {}
     for r in rows:
