@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Headline benchmark: GPT-3 13B pre-training step (Fleet sharding stage-3 over RCCL/xGMI, bf16
-AMP-O2, fused AdamW, full recompute) + ResNet-50 bf16 data-parallel, on N MI355X GPUs of one node.
+"""Headline benchmark: GPT-3 13B pre-training step (Fleet sharding stage-3 over RCCL/xGMI, optionally
+composed with tensor parallelism via fleet's hybrid topology; bf16 AMP-O2, fused AdamW, no activation
+recompute by default) + ResNet-50 bf16 data-parallel, on N MI355X GPUs of one node.
 
 Metric (BASELINE.json): "tokens/sec GPT-3-13B sharding-3 + ResNet50 img/s, at 1/2/4/8 MI355X".
 `value` = whole-job GPT-3 13B training tokens/s; ResNet-50 img/s is reported in `secondary`.
@@ -8,6 +9,8 @@ Weak scaling: per-GPU micro-batch fixed as N grows. Data: synthetic tokens / ima
 
 Launch (N>1): python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
               --master-port P bench.py --gpus N --steps K --warmup W
+`python bench.py --gpus N` without a launcher starts those N ranks itself (a child torchrun, before any
+GPU call) and exits with its status; under a launcher WORLD_SIZE must equal --gpus.
 """
 from __future__ import annotations
 
@@ -39,7 +42,10 @@ def parse():
     p.add_argument("--seq-len", type=int, default=2048)
     p.add_argument("--recompute", type=int, default=0)
     p.add_argument("--sharding-stage", type=int, default=3)
-    p.add_argument("--tp", type=int, default=1)
+    p.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (GPT: sharding over world/tp ranks)")
+    p.add_argument("--stage3-keep-params", default="auto",
+                   help="sharding stage 3: auto | 1 (keep gathered params resident from first use until the "
+                        "optimizer step) | 0 (release after each unit's forward/backward, re-gather per micro-batch)")
     p.add_argument("--resnet", type=int, default=1, help="also run the ResNet-50 DP benchmark")
     p.add_argument("--resnet-batch", type=int, default=256, help="per-GPU ResNet-50 batch")
     p.add_argument("--resnet-steps", type=int, default=10)
@@ -87,10 +93,25 @@ def gpt_bench(args, paddle, world, dist_on):
     from paddlepaddle_amd.models.gpt import GPTConfig, GPTForPretraining, GPTPretrainingCriterion
     cfgs = {"gpt3-13b": GPTConfig.gpt3_13b, "gpt3-6.7b": GPTConfig.gpt3_6_7b, "gpt3-1.3b": GPTConfig.gpt3_1_3b,
             "tiny": GPTConfig.tiny}
+    tp = args.tp
+    if world % tp:
+        raise SystemExit(f"world {world} is not a multiple of tp {tp}")
+    n_shard = world // tp
+    data_rank = int(os.environ.get("RANK", "0"))
+    shard_group = None
+    if world > 1 or tp > 1:
+        # fleet hybrid topology: mp = tp (contiguous ranks: one xGMI hop), sharding = world / tp
+        from paddlepaddle_amd.distributed import fleet
+        st = fleet.DistributedStrategy()
+        st.hybrid_configs = dict(dp_degree=1, mp_degree=tp, pp_degree=1, sharding_degree=n_shard)
+        fleet.init(is_collective=True, strategy=st)
+        hcg = fleet.get_hybrid_communicate_group()
+        data_rank = hcg.get_sharding_parallel_rank()
+        shard_group = hcg.get_sharding_parallel_group()
     cfg = cfgs[args.model](max_position_embeddings=max(args.seq_len, 128), use_recompute=bool(args.recompute),
-                           tensor_parallel_degree=args.tp)
+                           tensor_parallel_degree=tp)
     paddle.set_default_dtype("bfloat16")
-    paddle.seed(1234 + int(os.environ.get("RANK", "0")))
+    paddle.seed(1234)
     t0 = time.time()
     model = GPTForPretraining(cfg)
     crit = GPTPretrainingCriterion(cfg)
@@ -101,15 +122,20 @@ def gpt_bench(args, paddle, world, dist_on):
     opt = paddle.optimizer.AdamW(learning_rate=1e-4, parameters=model.parameters(), weight_decay=0.01,
                                  grad_clip=clip, multi_precision=True,
                                  apply_decay_param_fun=lambda n: not ("norm" in n or n.endswith("b_0")))
+    keep = None
     if args.sharding_stage > 0:  # same engine at every N (at N=1 the collectives are no-ops)
         from paddlepaddle_amd.distributed.sharding import group_sharded_parallel
+        from paddlepaddle_amd.framework.flags import set_flags
+        set_flags({"FLAGS_sharding_stage3_keep_params": args.stage3_keep_params})
         level = {1: "os", 2: "os_g", 3: "p_g_os"}[args.sharding_stage]
-        model, opt, _ = group_sharded_parallel(model, opt, level=level)
+        model, opt, _ = group_sharded_parallel(model, opt, level=level, group=shard_group)
+        keep = model._engine.keep_params
     elif world > 1:
         model = paddle.DataParallel(model)
     B, S = args.micro_batch, args.seq_len
     dev = _dev()
-    gen = torch.Generator(device=dev).manual_seed(7 + int(os.environ.get("RANK", "0")))
+    # tensor-parallel ranks see the same tokens; sharding ranks see different ones
+    gen = torch.Generator(device=dev).manual_seed(7 + data_rank)
     data = torch.randint(0, cfg.vocab_size, (args.accum, B, S + 1), device=dev, generator=gen)
     ids = [paddle.Tensor(data[i, :, :-1]) for i in range(args.accum)]
     lbl = [paddle.Tensor(data[i, :, 1:]) for i in range(args.accum)]
@@ -121,7 +147,7 @@ def gpt_bench(args, paddle, world, dist_on):
         for a in range(args.accum):
             # accumulation micro-batches skip the gradient reduce-scatter / all-reduce; the last one
             # reduces (overlapped with its backward)
-            ctx = no_sync() if (no_sync is not None and world > 1 and a < args.accum - 1) else \
+            ctx = no_sync() if (no_sync is not None and n_shard > 1 and a < args.accum - 1) else \
                 contextlib.nullcontext()
             with ctx:
                 logits = model(ids[a])
@@ -134,7 +160,7 @@ def gpt_bench(args, paddle, world, dist_on):
         state["loss"] = loss
 
     dt = timed(step, args.steps, args.warmup, dist_on)
-    tokens = args.steps * args.accum * B * S * world
+    tokens = args.steps * args.accum * B * S * n_shard
     tps = tokens / dt
     fpt = cfg.flops_per_token(S, recompute=False)
     mfu = tps * fpt / (PEAK_BF16 * world)
@@ -152,7 +178,8 @@ def gpt_bench(args, paddle, world, dist_on):
     del model, opt, ids, lbl
     if dev.type == "cuda":
         torch.cuda.empty_cache()
-    return tps, dt / args.steps * 1000, B * args.accum * world, mfu
+    gpt_bench.keep_params = keep
+    return tps, dt / args.steps * 1000, B * args.accum * n_shard, mfu
 
 
 def llama_bench(args, paddle, world, dist_on):
@@ -249,9 +276,28 @@ def resnet_bench(args, paddle, world, dist_on):
     return ips
 
 
+def _relaunch(args):
+    """--gpus N with no launcher: run N ranks under torch.distributed.run as a child process (this process
+    has not touched the GPU) and exit with its status."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    sys.exit(subprocess.call(cmd, env=env))
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        _relaunch(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     import paddlepaddle_amd as paddle
     dist_on = world > 1
     if dist_on:
@@ -267,12 +313,15 @@ def main():
         tps, step_ms, gb, mfu = gpt_bench(args, paddle, world, dist_on)
     ips = resnet_bench(args, paddle, world, dist_on) if args.resnet else None
     if int(os.environ.get("RANK", "0")) == 0:
-        par = (f"sharding_stage{args.sharding_stage}_degree{world}" if args.sharding_stage else f"dp{world}") + \
+        ns = world // max(args.tp, 1)
+        par = (f"sharding_stage{args.sharding_stage}_degree{ns}" if args.sharding_stage else f"dp{ns}") + \
               (f"_tp{args.tp}" if args.tp > 1 else "")
         if is_llama:
             par = f"pp{args.pp}_tp{args.tp}_dp{world // (args.pp * args.tp)}" + (f"_vpp{args.vpp}" if args.vpp > 1 else "")
+        metric = BASELINE_METRIC if args.model == "gpt3-13b" else \
+            f"tokens/sec {args.model} training ({par})"
         line = {
-            "metric": BASELINE_METRIC,
+            "metric": metric,
             "value": round(tps, 1) if tps is not None else None,
             "unit": "tokens/s",
             "n_gpus": world,
@@ -289,7 +338,11 @@ def main():
                        if is_llama else args.model,
                        "global_batch": gb, "seq_len": args.seq_len, "micro_batch": args.micro_batch,
                        "accum_steps": args.accum, "parallelism": par, "recompute": bool(args.recompute),
-                       "optimizer": "AdamW fp32-master fused HIP", "amp": "O2 bf16"},
+                       "optimizer": "AdamW fp32-master fused HIP", "amp": "O2 bf16",
+                       **({"stage3_params": ("gathered once per step, resident until the optimizer step"
+                                             if getattr(gpt_bench, "keep_params", None) else
+                                             "released after each block, re-gathered per micro-batch")}
+                          if (args.sharding_stage == 3 and not is_llama and world // max(args.tp, 1) > 1) else {})},
             "mfu_6N": round(mfu, 4) if mfu is not None else None,
             "secondary": {"metric": "ResNet50 img/s (bf16 NHWC, DP)", "value": round(ips, 1) if ips else None,
                           "per_gpu_batch": args.resnet_batch},

@@ -41,10 +41,11 @@ def _is_nccl(pg):
 class _Flat:
     """One flat buffer of same-dtype, same-decay parameters of a unit."""
 
-    def __init__(self, params, world, rank, decay):
+    def __init__(self, params, world, rank, decay, distributed=False):
         self.params = params
         self.world, self.rank = world, rank
         self.decay = decay
+        self.distributed = distributed  # tensor-parallel shards (differ across the mp group)
         t0 = params[0]._t
         self.dtype, self.device = t0.dtype, t0.device
         self.numels = [p._t.numel() for p in params]
@@ -72,6 +73,7 @@ class _Flat:
         # degree 1: the shard IS the full buffer and grads stay in the flat bf16 grad buffer
         self.shard = Parameter(sh, trainable=True, name=f"sharded_flat_{id(self)}")
         self.shard.need_clip = True
+        self.shard.is_distributed = distributed
         if world > 1 and sh.dtype != torch.float32 and hasattr(self.shard._t, "grad_dtype"):
             self.shard._t.grad_dtype = None  # bf16 shard, fp32 reduce-scattered gradient
         self.shard_grad = torch.zeros(self.shard_size, dtype=torch.float32, device=self.device) if world > 1 else None
@@ -132,10 +134,10 @@ class _Unit:
         self.flats = []
         groups = {}
         for p in params:
-            key = (p._t.dtype, bool(decay_fn(p)))
+            key = (p._t.dtype, bool(decay_fn(p)), bool(getattr(p, "is_distributed", False)))
             groups.setdefault(key, []).append(p)
-        for (dt, dec), ps in groups.items():
-            self.flats.append(_Flat(ps, world, rank, dec))
+        for (dt, dec, dist_), ps in groups.items():
+            self.flats.append(_Flat(ps, world, rank, dec, dist_))
         self.n_params = len(params)
         self.ready = set()
         self.gathered = True
@@ -148,11 +150,19 @@ class _Unit:
 class GroupShardedEngine:
     """Implements stage 1/2/3 over a model + inner optimizer."""
 
-    def __init__(self, model, optimizer, stage, group=None, decay_fn=None):
+    def __init__(self, model, optimizer, stage, group=None, decay_fn=None, mp_group=None, dp_group=None,
+                 keep_params=None, pp_group=None):
         self.model = model
         self.stage = stage
         self.group = group
         self.pg = C._pg(group)
+        # hybrid composition (reference: dygraph_sharding_optimizer.py:54 takes hcg's sharding group;
+        # group_sharded_stage3.py:85 dp_group): tensor-parallel shards live in the mp group, an outer
+        # data-parallel group (replicas of the sharded state) averages the shard gradients
+        self.mp_group = mp_group if (mp_group is not None and getattr(mp_group, "nranks", 1) > 1) else None
+        self.dp_group = dp_group if (dp_group is not None and getattr(dp_group, "nranks", 1) > 1) else None
+        self.pp_group = pp_group if (pp_group is not None and getattr(pp_group, "nranks", 1) > 1) else None
+        self._keep_override = keep_params
         self.world = C.get_world_size(group)
         self.rank = C.get_rank(group) if group is not None else (dist.get_rank() if dist.is_initialized() else 0)
         self.inner_opt = optimizer
@@ -183,6 +193,8 @@ class GroupShardedEngine:
         Per step that is one all-gather + one reduce-scatter of the model instead of 3 x accum."""
         if self.stage != 3 or self.world == 1:
             return False
+        if self._keep_override is not None:
+            return bool(self._keep_override)
         from ..framework.flags import flag
         mode = str(flag("FLAGS_sharding_stage3_keep_params", "auto")).lower()
         if mode in ("0", "false", "off"):
@@ -208,12 +220,14 @@ class GroupShardedEngine:
 
     # ------------------------------------------------------------------ construction
     def _broadcast_params(self):
-        if self.world == 1:
-            return
-        src = self.group.ranks[0] if self.group is not None else 0
         with torch.no_grad():
-            for p in self.model.parameters():
-                dist.broadcast(p._t.data, src=src, group=self.pg)
+            if self.world > 1:
+                src = self.group.ranks[0] if self.group is not None else 0
+                for p in self.model.parameters():
+                    dist.broadcast(p._t.data, src=src, group=self.pg)
+            if self.dp_group is not None:  # replicas of the sharded state start identical
+                for p in self.model.parameters():
+                    dist.broadcast(p._t.data, src=self.dp_group.ranks[0], group=self.dp_group.process_group)
 
     def _build_units(self, decay_fn):
         unit_layers = []
@@ -251,13 +265,35 @@ class GroupShardedEngine:
         if hasattr(opt, "_apply_decay_param_fun"):
             opt._apply_decay_param_fun = (lambda n, _d=decay_ids: n in _d)
         clip = getattr(opt, "_grad_clip", None)
-        if clip is not None and hasattr(clip, "_extra_sq_norm_fn") and self.world > 1:
-            pg = self.pg
+        if clip is not None and hasattr(clip, "_extra_sq_norm_fn") and (
+                self.world > 1 or self.mp_group is not None or self.pp_group is not None):
+            pg = self.pg if self.world > 1 else None
+            mp_pg = self.mp_group.process_group if self.mp_group is not None else None
+            pp_pg = self.pp_group.process_group if self.pp_group is not None else None
 
-            def _allreduce_sq(sq):
-                dist.all_reduce(sq, group=pg)
-                return sq
-            clip._extra_sq_norm_fn = _allreduce_sq
+            def _param_sq(params):
+                # shards partition each flat over the sharding group (sum there); tensor-parallel flats
+                # are also disjoint across the mp group (sum there), replicated flats are counted once
+                from ..ops.optim import global_sq_norm
+                dev = params[0]._t.device
+                dg = [p._t.grad for p in params if getattr(p, "is_distributed", False)]
+                rg = [p._t.grad for p in params if not getattr(p, "is_distributed", False)]
+                sq_d = (global_sq_norm(dg) if dg else torch.zeros((), device=dev)).float().reshape(1).clone()
+                sq_r = (global_sq_norm(rg) if rg else torch.zeros((), device=dev)).float().reshape(1)
+                if mp_pg is not None:
+                    dist.all_reduce(sq_d, group=mp_pg)
+                sq = sq_d + sq_r
+                if pg is not None:
+                    dist.all_reduce(sq, group=pg)
+                if pp_pg is not None:  # pipeline stages hold disjoint layers
+                    dist.all_reduce(sq, group=pp_pg)
+                return sq[0]
+            clip._param_sq_fn = _param_sq
+            if mp_pg is None and pp_pg is None and pg is not None:  # optimizers that clip through _global_norm
+                def _allreduce_sq(sq):
+                    dist.all_reduce(sq, group=pg)
+                    return sq
+                clip._extra_sq_norm_fn = _allreduce_sq
 
     # ------------------------------------------------------------------ hooks
     def _install_hooks(self):
@@ -404,12 +440,19 @@ class GroupShardedEngine:
     # ------------------------------------------------------------------ optimizer
     @torch.no_grad()
     def step(self):
+        dp_work = []
         for u in self.units:
             for f in u.flats:
                 if self.world == 1:
                     f.shard._t.grad = f.alloc_full_grad()
                 else:
                     f.shard._t.grad = f.shard_grad
+                if self.dp_group is not None:  # replicas of this shard: average across the outer dp group
+                    g = f.shard._t.grad
+                    g.mul_(1.0 / self.dp_group.nranks)
+                    dp_work.append(dist.all_reduce(g, group=self.dp_group.process_group, async_op=True))
+        for w in dp_work:
+            w.wait()
         self.inner_opt.step()
         if self.world == 1:
             return  # shard aliases the full buffer: nothing to publish
@@ -431,6 +474,22 @@ class GroupShardedEngine:
                     f.shard_grad.zero_()
                 f.shard._t.grad = None
 
+    def pre_forward(self):
+        """Root unit (embeddings / tied head / final norm) is gathered for the whole step."""
+        if not self.units:
+            return
+        self._gather(self.units[0])
+        self._wait_gather(self.units[0])
+        if torch.is_grad_enabled():
+            for f in self.units[0].flats:
+                f.alloc_full_grad()
+
+    @torch.no_grad()
+    def reshard_from_full(self):
+        for u in self.units:
+            for f in u.flats:
+                f.shard._t.data.copy_(f.full[f.rank * f.shard_size:(f.rank + 1) * f.shard_size])
+
     @torch.no_grad()
     def gather_all(self):
         """Materialise every full parameter (for state_dict / eval under stage 3)."""
@@ -446,13 +505,7 @@ class GroupShardedModel(Layer):
         self._layers = engine.model
 
     def forward(self, *args, **kwargs):
-        e = self._engine
-        if e.units:
-            e._gather(e.units[0])
-            e._wait_gather(e.units[0])
-            if torch.is_grad_enabled():
-                for f in e.units[0].flats:
-                    f.alloc_full_grad()
+        self._engine.pre_forward()
         return self._layers(*args, **kwargs)
 
     def no_sync(self):
@@ -465,9 +518,7 @@ class GroupShardedModel(Layer):
     def set_state_dict(self, sd, use_structured_name=True):
         self._engine.gather_all()
         r = self._layers.set_state_dict(sd, use_structured_name)
-        for u in self._engine.units:
-            for f in u.flats:
-                f.shard._t.data.copy_(f.full[f.rank * f.shard_size:(f.rank + 1) * f.shard_size])
+        self._engine.reshard_from_full()
         return r
 
     def get_all_parameters(self, convert2cpu=False):
@@ -520,7 +571,16 @@ def group_sharded_parallel(model, optimizer, level, scaler=None, group=None, off
     stage = {"os": 1, "os_g": 2, "p_g_os": 3}[level]
     if not C.is_initialized() and C.get_world_size() > 1:
         C.init_parallel_env()
-    eng = GroupShardedEngine(model, optimizer, stage, group)
+    mp_group = None
+    from ..distributed.fleet.topology import _get_hcg
+    hcg = _get_hcg()
+    if hcg is not None:
+        mp_group = hcg.get_model_parallel_group()
+        if group is None and hcg.get_sharding_parallel_world_size() > 1:
+            group = hcg.get_sharding_parallel_group()
+    if offload:
+        raise NotImplementedError("group_sharded_parallel(offload=True) is not supported yet")
+    eng = GroupShardedEngine(model, optimizer, stage, group, mp_group=mp_group, dp_group=dp_group)
     return GroupShardedModel(eng), GroupShardedOptimizer(eng), scaler
 
 

@@ -32,6 +32,15 @@ def _ws(g):
     return 1 if g is None else g.nranks
 
 
+def _mp_init_ctx(world):
+    """Distributed (per-mp-rank) weights draw from the tracker's model_parallel_rng stream so the shards
+    of one logical weight differ across the mp group (reference mp_layers.py creates them under
+    get_rng_state_tracker().rng_state())."""
+    if world > 1 and "model_parallel_rng" in _TRACKER.states_:
+        return _TRACKER.rng_state()
+    return contextlib.nullcontext()
+
+
 def _rank(g):
     return 0 if g is None else g.rank
 
@@ -157,7 +166,8 @@ class ColumnParallelLinear(nn.Layer):
         self.out_per = out_features // self.world
         self.gather_output = gather_output
         self.act = fuse_bias_act
-        self.weight = self.create_parameter([in_features, self.out_per], attr=weight_attr)
+        with _mp_init_ctx(self.world):
+            self.weight = self.create_parameter([in_features, self.out_per], attr=weight_attr)
         self.weight.is_distributed = self.world > 1
         self.bias = self.create_parameter([self.out_per], is_bias=True) if has_bias in (None, True) else None
         if self.bias is not None:
@@ -183,7 +193,8 @@ class RowParallelLinear(nn.Layer):
         assert in_features % self.world == 0
         self.in_per = in_features // self.world
         self.input_is_parallel = input_is_parallel
-        self.weight = self.create_parameter([self.in_per, out_features], attr=weight_attr)
+        with _mp_init_ctx(self.world):
+            self.weight = self.create_parameter([self.in_per, out_features], attr=weight_attr)
         self.weight.is_distributed = self.world > 1
         self.bias = self.create_parameter([out_features], is_bias=True) if has_bias else None
 
@@ -212,8 +223,9 @@ class VocabParallelEmbedding(nn.Layer):
         self.world = _ws(self.group)
         self.per = (num_embeddings + self.world - 1) // self.world
         self.start = _rank(self.group) * self.per
-        self.weight = self.create_parameter([self.per, embedding_dim], attr=weight_attr,
-                                            default_initializer=I.XavierNormal())
+        with _mp_init_ctx(self.world):
+            self.weight = self.create_parameter([self.per, embedding_dim], attr=weight_attr,
+                                                default_initializer=I.XavierNormal())
         self.weight.is_distributed = self.world > 1
 
     def forward(self, x):

@@ -48,3 +48,28 @@ def test_bench_llama_pipeline_x_tp_four_ranks():
     assert len(lines) == 1
     d = json.loads(lines[0])
     assert d["n_gpus"] == 4 and d["value"] > 0 and d["config"]["parallelism"] == "pp2_tp2_dp1"
+
+
+def test_bench_self_launch_sharding_x_tp_four_ranks():
+    """`bench.py --gpus 4 --tp 2` with no launcher starts the 4 ranks itself; GPT runs fleet's hybrid
+    topology (sharding stage 3 over 2 ranks x tensor parallel 2)."""
+    env = dict(os.environ, PADDLE_AMD_FORCE_CPU="1", PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--tp", "2", "--model", "tiny",
+           "--steps", "2", "--warmup", "1", "--seq-len", "64", "--micro-batch", "2", "--accum", "2", "--resnet", "0"]
+    r = subprocess.run(cmd, env=env, capture_output=True, timeout=600, cwd="/tmp")
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    lines = [l for l in r.stdout.decode().splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 4 and d["value"] > 0
+    assert d["config"]["parallelism"] == "sharding_stage3_degree2_tp2"
+    assert d["config"]["global_batch"] == 2 * 2 * 2
+
+
+def test_bench_rejects_world_mismatch():
+    env = dict(os.environ, PADDLE_AMD_FORCE_CPU="1", PYTHONPATH=ROOT, WORLD_SIZE="1", RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--resnet", "0"], env=env,
+                       capture_output=True, timeout=300, cwd="/tmp")
+    assert r.returncode != 0 and b"WORLD_SIZE" in r.stderr

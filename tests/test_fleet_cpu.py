@@ -394,3 +394,55 @@ def test_llama_pipeline_x_tensor_parallel_matches_single_process():
     res = _spawn(_llama_pp_tp_worker, world=4)
     for _, l in res:
         np.testing.assert_allclose(l, ref, rtol=1e-4, atol=1e-5)
+
+
+# ----------------------------------------------------------------------------- sharding x mp / sharding x dp
+def _hybrid_sharding_worker(rank, world, port, mp_deg, stage, q):
+    """fleet hybrid topology with sharding_degree > 1 (reference: dygraph_sharding_optimizer.py:54 over
+    hcg's sharding group, group_sharded_stage3.py:85): data split over the sharding (and dp) ranks,
+    weights split over the mp ranks. The averaged loss and the gathered weights must match the
+    single-process run on the whole batch."""
+    paddle = _setup(rank, world, port)
+    from paddlepaddle_amd.models.gpt import GPTConfig, GPTForPretraining, GPTPretrainingCriterion
+    _, full, _ = _gpt_full(paddle)
+    full_sd = {k: v._t.detach().clone() for k, v in full.state_dict().items()}
+    n_data = world // mp_deg
+    shard_deg = 2
+    fleet = _fleet_init(paddle, mp_degree=mp_deg, sharding_degree=shard_deg, dp_degree=n_data // shard_deg)
+    fleet.fleet._strategy.sharding_configs["stage"] = stage
+    hcg = fleet.get_hybrid_communicate_group()
+    mp_rank = hcg.get_model_parallel_rank()
+    data_rank = hcg.get_data_parallel_rank() * shard_deg + hcg.get_sharding_parallel_rank()
+    cfg = GPTConfig.tiny(num_hidden_layers=2, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0,
+                         tensor_parallel_degree=mp_deg)
+    model, crit = GPTForPretraining(cfg), GPTPretrainingCriterion(cfg)
+    with torch.no_grad():
+        for k, v in model.state_dict().items():
+            v._t.copy_(_shard_like(full_sd[k], v._t, mp_rank, mp_deg))
+    opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    model = fleet.distributed_model(model)
+    opt = fleet.distributed_optimizer(opt)
+    ids = _data(cfg)
+    per = ids.shape[0] // n_data
+    losses = _train(paddle, model, crit, opt, ids[data_rank * per:(data_rank + 1) * per])
+    sd = {k: v.numpy() for k, v in model.state_dict().items()}
+    q.put((rank, mp_rank, losses, sd))
+    paddle.distributed.barrier()
+
+
+def _check_hybrid(res, mp_deg):
+    ref_losses, ref_sd = _single_gpt()
+    mean_loss = np.mean([r[2] for r in res], axis=0)
+    np.testing.assert_allclose(mean_loss, ref_losses, rtol=1e-4, atol=1e-5)
+    for _, mp_rank, _, sd in res:
+        for k, full in ref_sd.items():
+            exp = _shard_like(torch.from_numpy(full), torch.from_numpy(sd[k]), mp_rank, mp_deg).numpy()
+            np.testing.assert_allclose(sd[k], exp, rtol=2e-3, atol=2e-4, err_msg=f"mp{mp_rank}:{k}")
+
+
+def test_sharding_stage3_x_tensor_parallel_gpt_four_ranks():
+    _check_hybrid(_spawn(_hybrid_sharding_worker, 2, 3, world=4), 2)
+
+
+def test_sharding_stage2_x_data_parallel_gpt_four_ranks():
+    _check_hybrid(_spawn(_hybrid_sharding_worker, 1, 2, world=4), 1)
