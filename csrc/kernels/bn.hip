@@ -392,3 +392,73 @@ PA_EXPORT int pa_bn_bwd_nhwc(const void* dy, const void* x, const void* y, void*
   PA_CHECK_LAUNCH();
   return 0;
 }
+
+// ---- split-phase entry points (cross-rank SyncBatchNorm: the per-channel sums are all-reduced between
+// the reduction and the apply; reference: sync_batch_norm_utils.h:575 all-reduces the backward stats)
+
+namespace {
+__global__ __launch_bounds__(1024) void bn_fold_k(const float* __restrict__ partial, int chunks, int C,
+                                                  float* __restrict__ sums) {
+  double s1, s2;
+  int c;
+  if (!fold_chunks(partial, chunks, C, &s1, &s2, &c)) return;
+  sums[c] = (float)s1;
+  sums[C + c] = (float)s2;
+}
+}  // namespace
+
+// mode 0: sums = [sum x, sum x^2]; mode 1: sums = [sum dyp, sum dyp * (x - mean)] with dyp the relu-masked
+// dy (mask from y, or from x * ss[0] + ss[1] when ss is given). sums: [2, C] fp32; partial as above.
+PA_EXPORT int pa_bn_reduce_nhwc(int mode, const void* x, const void* dy, const void* y, const float* mean,
+                                const float* ss, float* partial, float* sums, int64_t R, int C, int relu,
+                                hipStream_t st) {
+  if (C % 8 != 0 || R < 1) return 3;
+  int CB, chunks;
+  int64_t rpc;
+  plan(R, C, &CB, &chunks, &rpc);
+  const dim3 grid(C / CB, chunks);
+  const uint16_t *xp = (const uint16_t*)x, *dp = (const uint16_t*)dy, *yp = (const uint16_t*)y;
+  if (mode == 0)
+    hipLaunchKernelGGL((bn_reduce_k<0, false>), grid, dim3(kThreads), 0, st, xp, nullptr, nullptr, nullptr, partial,
+                       R, C, CB, rpc);
+  else if (relu && ss)
+    hipLaunchKernelGGL((bn_reduce_k<1, true, true>), grid, dim3(kThreads), 0, st, xp, dp, nullptr, mean, partial, R,
+                       C, CB, rpc, ss);
+  else if (relu)
+    hipLaunchKernelGGL((bn_reduce_k<1, true>), grid, dim3(kThreads), 0, st, xp, dp, yp, mean, partial, R, C, CB, rpc);
+  else
+    hipLaunchKernelGGL((bn_reduce_k<1, false>), grid, dim3(kThreads), 0, st, xp, dp, nullptr, mean, partial, R, C, CB,
+                       rpc);
+  PA_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_fold_k, dim3((C + 63) / 64), dim3(1024), 0, st, partial, chunks, C, sums);
+  PA_CHECK_LAUNCH();
+  return 0;
+}
+
+// dx = coef[0] * dyp - coef[1] * x + coef[2] (coef: [3, C] fp32, computed by the caller from global sums);
+// dres = dyp when given.
+PA_EXPORT int pa_bn_bwd_apply_nhwc(const void* dy, const void* x, const void* y, const float* coef, void* dx,
+                                   void* dres, int64_t R, int C, int relu, const float* ss, hipStream_t st) {
+  if (C % 8 != 0 || R < 1) return 3;
+  const int64_t nvec = R * C / 8;
+  const unsigned g = apply_grid(nvec);
+  const uint16_t *dp = (const uint16_t*)dy, *xp = (const uint16_t*)x, *yp = (const uint16_t*)y;
+  uint16_t *dxp = (uint16_t*)dx, *drp = (uint16_t*)dres;
+  if (relu && ss && !dres)
+    hipLaunchKernelGGL((bn_bwd_apply_k<true, false, true>), dim3(g), dim3(kThreads), 0, st, dp, xp, nullptr, coef,
+                       dxp, nullptr, nvec, C, ss);
+  else if (relu && dres)
+    hipLaunchKernelGGL((bn_bwd_apply_k<true, true>), dim3(g), dim3(kThreads), 0, st, dp, xp, yp, coef, dxp, drp, nvec, C,
+                       nullptr);
+  else if (relu)
+    hipLaunchKernelGGL((bn_bwd_apply_k<true, false>), dim3(g), dim3(kThreads), 0, st, dp, xp, yp, coef, dxp, nullptr,
+                       nvec, C, nullptr);
+  else if (dres)
+    hipLaunchKernelGGL((bn_bwd_apply_k<false, true>), dim3(g), dim3(kThreads), 0, st, dp, xp, nullptr, coef, dxp, drp,
+                       nvec, C, nullptr);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_k<false, false>), dim3(g), dim3(kThreads), 0, st, dp, xp, nullptr, coef, dxp,
+                       nullptr, nvec, C, nullptr);
+  PA_CHECK_LAUNCH();
+  return 0;
+}

@@ -92,36 +92,26 @@ class BatchNorm(_BatchNormBase):
 
 
 class SyncBatchNorm(_BatchNormBase):
-    """Cross-rank BN: batch statistics all-reduced over the data-parallel group (RCCL)."""
+    """Cross-rank BN: batch statistics and the backward's gradient statistics are all-reduced over the
+    group (RCCL). Channels-last bf16 inputs run the split-phase HIP kernels (ops/bn.py sync_batch_norm).
+    Reference: python/paddle/nn/layer/norm.py SyncBatchNorm, phi/kernels/gpu/sync_batch_norm_kernel.cu."""
+
+    def __init__(self, num_features, momentum=0.9, epsilon=1e-05, weight_attr=None, bias_attr=None,
+                 data_format="NCHW", name=None, process_group=None):
+        super().__init__(num_features, momentum, epsilon, weight_attr, bias_attr, data_format)
+        self._process_group = process_group
 
     def forward(self, x):
         from ...distributed import collective as C
-        if not self.training or not C.is_initialized() or C.get_world_size() == 1:
+        from ...ops.bn import sync_batch_norm
+        grp = self._process_group
+        if not self.training or not C.is_initialized() or C.get_world_size(grp) == 1:
             return super().forward(x)
-        t = x._t
-        cl = self._data_format in ("NHWC", "NLC", "NDHWC")
-        if cl:
-            t = t.movedim(-1, 1)
-        red = [0] + list(range(2, t.dim()))
-        n = torch.tensor([t.numel() / t.shape[1]], device=t.device, dtype=torch.float32)
-        s = t.float().sum(red)
-        ss = (t.float() ** 2).sum(red)
-        buf = torch.cat([s, ss, n])
-        C._all_reduce_raw(buf)
-        N = buf[-1]
-        mean = buf[: t.shape[1]] / N
-        var = buf[t.shape[1]: 2 * t.shape[1]] / N - mean ** 2
-        with torch.no_grad():
-            m = self._momentum
-            self._mean._t.mul_(m).add_((1 - m) * mean)
-            self._variance._t.mul_(m).add_((1 - m) * var * N / (N - 1))
-        shape = [1, -1] + [1] * (t.dim() - 2)
-        y = (t.float() - mean.view(shape)) * torch.rsqrt(var.view(shape) + self._epsilon)
-        if self.weight is not None:
-            y = y * self.weight._t.view(shape) + self.bias._t.view(shape)
-        y = y.to(t.dtype)
-        if cl:
-            y = y.movedim(1, -1)
+        cl = self._data_format in ("NHWC", "NLC", "NDHWC") or x.ndim == 2
+        w = self.weight._t if self.weight is not None else None
+        b = self.bias._t if self.bias is not None else None
+        y = sync_batch_norm(x._t, w, b, self._mean._t, self._variance._t, self._momentum, self._epsilon,
+                            channel_last=cl, pg=C._pg(grp))
         return _wrap(y)
 
     @classmethod

@@ -117,6 +117,8 @@ def _declare(L):
         "pa_bn_chunks": [_i64, _i32],
         "pa_bn_fwd_nhwc": [_vp] * 11 + [_i64, _i32, _f32, _f32, _i32, _i32, _vp],
         "pa_bn_bwd_nhwc": [_vp] * 12 + [_i64, _i32, _i32, _i32, _vp, _vp],
+        "pa_bn_reduce_nhwc": [_i32] + [_vp] * 7 + [_i64, _i32, _i32, _vp],
+        "pa_bn_bwd_apply_nhwc": [_vp] * 6 + [_i64, _i32, _i32, _vp, _vp],
         # fused decode step
         "pa_add_rms_norm_fwd": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _f32, _i32, _vp],
         "pa_decode_rope_cache": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i64, _i32, _vp],
@@ -138,7 +140,20 @@ def has(name):
     return l is not None and hasattr(l, name)
 
 
+# per-launcher dispatch counters: tests assert that the HIP path (not a fallback) ran
+CALLS: dict = {}
+
+
+def calls(name):
+    return CALLS.get(name, 0)
+
+
+def reset_calls():
+    CALLS.clear()
+
+
 def call(name, *args):
+    CALLS[name] = CALLS.get(name, 0) + 1
     rc = getattr(lib(), name)(*args)
     if rc != 0:
         raise RuntimeError(f"HIP kernel {name} failed with code {rc}")

@@ -134,3 +134,100 @@ def batch_norm_act_nhwc(x, weight, bias, running_mean, running_var, training=Tru
     r2 = residual.reshape(-1, C) if residual is not None else None
     return batch_norm_act_reference(x2, weight, bias, running_mean, running_var, training, momentum, eps, act,
                                     r2).view(x.shape)
+
+
+# ------------------------------------------------------------------ cross-rank (sync) batch norm
+def _sync_hip_ok(x2, weight, bias):
+    if not L.hip_enabled_for(x2) or not L.has("pa_bn_reduce_nhwc"):
+        return False
+    if x2.dtype != torch.bfloat16 or x2.shape[-1] % 8 != 0 or not x2.is_contiguous():
+        return False
+    return all(t is None or (t.dtype == torch.float32 and t.is_contiguous()) for t in (weight, bias))
+
+
+def _channel_sums(mode, x2, dy=None, mean=None):
+    """[2, C] fp32: mode 0 -> (sum x, sum x^2); mode 1 -> (sum dy, sum dy * (x - mean))."""
+    R, C = x2.shape
+    if _sync_hip_ok(x2, None, None) and (dy is None or (dy.dtype == x2.dtype and dy.is_contiguous())):
+        sums = torch.empty(2, C, dtype=torch.float32, device=x2.device)
+        partial = torch.empty(2 * _chunks(R, C) * C, dtype=torch.float32, device=x2.device)
+        L.call("pa_bn_reduce_nhwc", int(mode), L.ptr(x2), L.ptr(dy), L.ptr(None), L.ptr(mean), L.ptr(None),
+               L.ptr(partial), L.ptr(sums), R, C, 0, L.stream_ptr())
+        return sums
+    xf = x2.float()
+    if mode == 0:
+        return torch.stack([xf.sum(0), (xf * xf).sum(0)])
+    gf = dy.float()
+    return torch.stack([gf.sum(0), (gf * (xf - mean)).sum(0)])
+
+
+class _SyncBN(torch.autograd.Function):
+    """Batch statistics over every rank of ``group`` (reference: sync_batch_norm_kernel.cu +
+    sync_batch_norm_utils.h:575). Forward all-reduces (sum x, sum x^2, count); backward all-reduces
+    (sum dy, sum dy * (x - mean)) so dx carries the cross-rank terms. dweight / dbias stay local (the
+    data-parallel gradient all-reduce sums them, as in the reference's KeBNBackwardScaleBias)."""
+
+    @staticmethod
+    def forward(ctx, x2, weight, bias, running_mean, running_var, momentum, eps, pg):
+        import torch.distributed as dist
+        R, C = x2.shape
+        sums = _channel_sums(0, x2)
+        buf = torch.cat([sums.reshape(-1), torch.full((1,), float(R), device=x2.device)])
+        dist.all_reduce(buf, group=pg)
+        N = buf[-1]
+        mean = buf[:C] / N
+        var = (buf[C:2 * C] / N - mean * mean).clamp_min(0.0)
+        rstd = torch.rsqrt(var + eps)
+        with torch.no_grad():
+            if running_mean is not None:
+                running_mean.mul_(momentum).add_((1 - momentum) * mean.to(running_mean.dtype))
+                running_var.mul_(momentum).add_((1 - momentum) * var.to(running_var.dtype))
+        w = weight.float() if weight is not None else torch.ones_like(mean)
+        b = bias.float() if bias is not None else torch.zeros_like(mean)
+        sc = w * rstd
+        ss = torch.stack([sc, b - mean * sc]).contiguous()
+        if _sync_hip_ok(x2, weight, bias):
+            y = torch.empty_like(x2)
+            L.call("pa_bn_fwd_nhwc", L.ptr(x2), L.ptr(None), L.ptr(y), L.ptr(None), L.ptr(None), L.ptr(None),
+                   L.ptr(None), L.ptr(mean), L.ptr(rstd), L.ptr(None), L.ptr(ss), R, C, 0.0, float(eps), 0, 0,
+                   L.stream_ptr())
+        else:
+            y = (x2.float() * ss[0] + ss[1]).to(x2.dtype)
+        ctx.save_for_backward(x2, weight, mean, rstd)
+        ctx.pg, ctx.N = pg, N
+        ctx.has = (weight is not None, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        import torch.distributed as dist
+        x2, weight, mean, rstd = ctx.saved_tensors
+        has_w, has_b = ctx.has
+        R, C = x2.shape
+        dy = dy.contiguous()
+        local = _channel_sums(1, x2, dy, mean)  # [sum dy, sum dy * (x - mean)] on this rank
+        dw = (local[1] * rstd).to(weight.dtype) if has_w else None
+        db = local[0].to(weight.dtype if has_w else torch.float32) if has_b else None
+        glob = local.clone()
+        dist.all_reduce(glob, group=ctx.pg)
+        N = ctx.N
+        a = (weight.float() if has_w else torch.ones_like(mean)) * rstd
+        bc = a * rstd * rstd * glob[1] / N
+        d0 = bc * mean - a * glob[0] / N
+        coef = torch.stack([a, bc, d0]).contiguous()
+        if _sync_hip_ok(x2, weight, None) and dy.dtype == x2.dtype:
+            dx = torch.empty_like(x2)
+            L.call("pa_bn_bwd_apply_nhwc", L.ptr(dy), L.ptr(x2), L.ptr(None), L.ptr(coef), L.ptr(dx), L.ptr(None),
+                   R, C, 0, L.ptr(None), L.stream_ptr())
+        else:
+            dx = (coef[0] * dy.float() - coef[1] * x2.float() + coef[2]).to(x2.dtype)
+        return dx, dw, db, None, None, None, None, None
+
+
+def sync_batch_norm(x, weight, bias, running_mean, running_var, momentum=0.9, eps=1e-5, channel_last=True, pg=None):
+    """Training-mode batch norm whose statistics span every rank of the process group ``pg``."""
+    t = x if channel_last else x.movedim(1, -1)
+    C = t.shape[-1]
+    x2 = t.contiguous().view(-1, C)
+    y = _SyncBN.apply(x2, weight, bias, running_mean, running_var, float(momentum), float(eps), pg).view(t.shape)
+    return y if channel_last else y.movedim(-1, 1)

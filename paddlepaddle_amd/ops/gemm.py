@@ -137,7 +137,7 @@ def _flush_caches(dev):
     has no room for it — the timing is then warm, which only biases the choice, never breaks it)."""
     try:
         buf = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
-    except torch.OutOfMemoryError:
+    except torch.cuda.OutOfMemoryError:
         return None
     buf.zero_()
     return buf

@@ -22,3 +22,12 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _reset_hip_dispatch_counters(request):
+    """GPU tests assert per-launcher dispatch counts (ops._loader.CALLS): start each test from zero."""
+    if "gpu" in request.keywords:
+        from paddlepaddle_amd.ops import _loader as L
+        L.reset_calls()
+    yield

@@ -96,6 +96,7 @@ def test_bn_act_hip_matches_fp32(shape, act, with_res, training):
     torch.testing.assert_close(b.grad, br.grad, rtol=2e-2, atol=2e-1)
     if with_res:
         torch.testing.assert_close(res.grad.float(), rr.grad.view(shape), rtol=2e-2, atol=2e-2)
+    assert L.calls("pa_bn_fwd_nhwc") == 1 and L.calls("pa_bn_bwd_nhwc") == 1
 
 
 @pytest.mark.gpu
@@ -120,6 +121,8 @@ def test_momentum_multi_tensor_hip_matches_fp32(nesterov):
             vel[i] = 0.9 * vel[i] + gj
             masters[i] = masters[i] - 0.1 * (gj + 0.9 * vel[i] if nesterov else vel[i])
     assert getattr(opt, "_mt_tables", None), "fused multi-tensor path not taken"
+    from paddlepaddle_amd.ops import _loader as L
+    assert L.calls("pa_momentum_multi") == 3
     for p, m in zip(params, masters):
         torch.testing.assert_close(opt._master(p), m, rtol=1e-5, atol=1e-5)
         torch.testing.assert_close(p._t.float(), m.bfloat16().float(), rtol=1e-2, atol=1e-2)

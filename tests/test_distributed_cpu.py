@@ -240,3 +240,59 @@ def test_sharding_degree1_matches_plain(level):
     ref, got = run(False), run(True)
     for k in ref:
         np.testing.assert_allclose(got[k], ref[k], rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+# ----------------------------------------------------------------------------- SyncBatchNorm
+def _sbn_data(fmt):
+    g = torch.Generator().manual_seed(21)
+    shape = (4, 6, 5, 3) if fmt == "NCHW" else (4, 5, 3, 6)
+    return torch.randn(*shape, generator=g) * 2 + 0.5, torch.randn(*shape, generator=g)
+
+
+def _sbn_worker(rank, world, port, fmt, q):
+    paddle = _setup(rank, world, port)
+    x, r = _sbn_data(fmt)
+    per = x.shape[0] // world
+    xs = paddle.Tensor(x[rank * per:(rank + 1) * per].clone())
+    xs.stop_gradient = False
+    bn = paddle.nn.SyncBatchNorm(6, data_format=fmt)
+    with torch.no_grad():
+        bn.weight._t.copy_(torch.linspace(0.5, 1.5, 6))
+        bn.bias._t.copy_(torch.linspace(-0.2, 0.3, 6))
+    y = bn(xs)
+    (y * paddle.Tensor(r[rank * per:(rank + 1) * per])).sum().backward()
+    q.put((rank, y.numpy(), xs.grad.numpy(), bn.weight.grad.numpy(), bn.bias.grad.numpy(), bn._mean.numpy(),
+           bn._variance.numpy()))
+    paddle.distributed.barrier()
+
+
+def _sbn_reference(fmt):
+    sys.path.insert(0, ROOT)
+    os.environ["PADDLE_AMD_FORCE_CPU"] = "1"
+    import paddlepaddle_amd as paddle
+    x, r = _sbn_data(fmt)
+    xt = paddle.Tensor(x.clone())
+    xt.stop_gradient = False
+    bn = paddle.nn.BatchNorm2D(6, data_format=fmt)
+    with torch.no_grad():
+        bn.weight._t.copy_(torch.linspace(0.5, 1.5, 6))
+        bn.bias._t.copy_(torch.linspace(-0.2, 0.3, 6))
+    y = bn(xt)
+    (y * paddle.Tensor(r)).sum().backward()
+    return y.numpy(), xt.grad.numpy(), bn.weight.grad.numpy(), bn.bias.grad.numpy(), bn._mean.numpy(), \
+        bn._variance.numpy()
+
+
+@pytest.mark.parametrize("fmt", ["NCHW", "NHWC"])
+def test_sync_batch_norm_matches_full_batch(fmt):
+    """2 ranks x half batch == BatchNorm2D on the full batch: outputs, input gradients (cross-rank
+    terms included), summed weight/bias gradients and running statistics (sync_batch_norm_utils.h:575)."""
+    y, dx, dw, db, rm, rv = _sbn_reference(fmt)
+    res = sorted(_spawn(_sbn_worker, fmt), key=lambda t: t[0])
+    np.testing.assert_allclose(np.concatenate([t[1] for t in res]), y, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(np.concatenate([t[2] for t in res]), dx, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(res[0][3] + res[1][3], dw, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(res[0][4] + res[1][4], db, rtol=1e-5, atol=1e-5)
+    for t in res:
+        np.testing.assert_allclose(t[5], rm, rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(t[6], rv, rtol=1e-5, atol=1e-6)

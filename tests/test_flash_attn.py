@@ -33,6 +33,7 @@ def _run(B, Sq, Sk, H, Hk, D, causal, dt=torch.bfloat16, spike=False, seed=0):
         scale = b.abs().max().item() + 1e-6
         e = (a.float() - b).abs().max().item() / scale
         assert e < 2.5e-2, f"{name} rel err {e}"
+    assert L.calls("pa_flash_attn_fwd") > 0 and L.calls("pa_flash_attn_bwd") > 0
 
 
 @pytest.mark.parametrize("causal", [False, True])

@@ -10,6 +10,32 @@ from paddlepaddle_amd.ops import gemm as G  # noqa: E402
 
 DEV = "cuda"
 
+# launchers each test must have dispatched (ops._loader.CALLS, reset per test by conftest)
+_EXPECT = {
+    "test_gemm_small_m": ["pa_gemm_small_m"],
+    "test_conv_implicit_gemm_fwd": ["pa_conv2d_nhwc_fwd"],
+    "test_conv_implicit_gemm_dgrad": ["pa_conv2d_nhwc_fwd"],
+    "test_conv_implicit_gemm_wgrad": ["pa_conv2d_nhwc_fwd", "pa_conv2d_nhwc_wgrad"],
+    "test_": ["pa_gemm_bf16"],
+}
+
+
+@pytest.fixture(autouse=True)
+def _assert_dispatch(request):
+    from paddlepaddle_amd.framework.flags import get_flags, set_flags
+    name = request.node.originalname
+    old = get_flags(["FLAGS_gemm_backend"])["FLAGS_gemm_backend"]
+    set_flags({"FLAGS_gemm_backend": "hip"})  # numerics of the hand-written kernels, not the autotuner's pick
+    try:
+        yield
+    finally:
+        set_flags({"FLAGS_gemm_backend": old})
+    for prefix, launchers in _EXPECT.items():
+        if name.startswith(prefix):
+            for n in launchers:
+                assert L.calls(n) > 0, f"{n} did not run in {name}: {dict(L.CALLS)}"
+            break
+
 
 def _operands(M, N, K, a_kmaj, b_kmaj, seed=0):
     g = torch.Generator(device=DEV).manual_seed(seed)

@@ -14,8 +14,14 @@ from paddlepaddle_amd.ops import _loader as L  # noqa: E402
 DEV = "cuda"
 
 
-def _lib_loaded():
+def _lib_loaded(*launchers):
+    """The native library is loaded and each named launcher actually dispatched (ops._loader.CALLS;
+    the counters are reset per test by conftest)."""
     assert L._LIB is not None, "HIP kernel library not loaded"
+    for n in launchers:
+        assert L.calls(n) > 0, f"{n} did not run (calls: {dict(L.CALLS)})"
+    if not launchers:
+        assert sum(L.CALLS.values()) > 0, "no HIP launcher ran"
 
 
 def _tol(dt):
@@ -31,13 +37,14 @@ def test_rms_norm(dt, cols):
     if cols % 8:
         pytest.skip("cols must be a multiple of 8 for the HIP path")
     y = ops.rms_norm(x, w, 1e-6)
-    _lib_loaded()
+    _lib_loaded("pa_rms_norm_fwd")
     xr, wr = x.detach().float().requires_grad_(True), w.detach().float().requires_grad_(True)
     yr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * wr
     torch.testing.assert_close(y.float(), yr, atol=_tol(dt) * 4, rtol=_tol(dt))
     g = torch.randn_like(yr)
     y.backward(g.to(dt))
     yr.backward(g)
+    _lib_loaded("pa_rms_norm_bwd")
     torch.testing.assert_close(x.grad.float(), xr.grad, atol=_tol(dt) * 8, rtol=_tol(dt) * 2)
     torch.testing.assert_close(w.grad.float(), wr.grad, atol=_tol(dt) * 40, rtol=_tol(dt) * 4)
 
@@ -50,13 +57,14 @@ def test_layer_norm(dt, cols):
     w = torch.randn(cols, device=DEV).to(dt).requires_grad_(True)
     b = torch.randn(cols, device=DEV).to(dt).requires_grad_(True)
     y = ops.layer_norm(x, w, b, 1e-5)
-    _lib_loaded()
+    _lib_loaded("pa_layer_norm_fwd")
     xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
     yr = F.layer_norm(xr, (cols,), wr, br, 1e-5)
     torch.testing.assert_close(y.float(), yr, atol=_tol(dt) * 8, rtol=_tol(dt))
     g = torch.randn_like(yr)
     y.backward(g.to(dt))
     yr.backward(g)
+    _lib_loaded("pa_layer_norm_bwd")
     torch.testing.assert_close(x.grad.float(), xr.grad, atol=_tol(dt) * 10, rtol=_tol(dt) * 2)
     torch.testing.assert_close(w.grad.float(), wr.grad, atol=_tol(dt) * 60, rtol=_tol(dt) * 4)
     torch.testing.assert_close(b.grad.float(), br.grad, atol=_tol(dt) * 60, rtol=_tol(dt) * 4)
@@ -67,7 +75,7 @@ def test_layer_norm(dt, cols):
 def test_softmax(dt, cols):
     x = (torch.randn(13, cols, device=DEV) * 4).to(dt).requires_grad_(True)
     y = ops.softmax(x, -1)
-    _lib_loaded()
+    _lib_loaded("pa_softmax_fwd")
     xr = x.detach().float().requires_grad_(True)
     yr = torch.softmax(xr, -1)
     torch.testing.assert_close(y.float(), yr, atol=_tol(dt), rtol=_tol(dt) * 2)
@@ -85,7 +93,7 @@ def test_softmax_cross_entropy(dt, V):
     labels = torch.randint(0, V, (33,), device=DEV)
     labels[5] = -100
     l = ops.softmax_cross_entropy(logits, labels, -100)
-    _lib_loaded()
+    _lib_loaded("pa_softmax_ce_fwd")
     lr = logits.detach().float().requires_grad_(True)
     ref = F.cross_entropy(lr, labels, ignore_index=-100, reduction="none")
     torch.testing.assert_close(l, ref, atol=1e-3 if dt == torch.float32 else 3e-2, rtol=1e-3)
@@ -101,7 +109,7 @@ def test_softmax_cross_entropy(dt, V):
 def test_gelu(approx, dt):
     x = (torch.randn(4, 1024, device=DEV) * 3).to(dt).requires_grad_(True)
     y = ops.gelu(x, approx)
-    _lib_loaded()
+    _lib_loaded("pa_gelu_fwd")
     xr = x.detach().float().requires_grad_(True)
     yr = F.gelu(xr, approximate="tanh" if approx else "none")
     torch.testing.assert_close(y.float(), yr, atol=_tol(dt) * 2, rtol=_tol(dt))
@@ -115,7 +123,7 @@ def test_bias_gelu():
     x = torch.randn(64, 2048, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     b = torch.randn(2048, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     y = ops.bias_gelu(x, b)
-    _lib_loaded()
+    _lib_loaded("pa_bias_gelu_fwd")
     xr, br = x.detach().float().requires_grad_(True), b.detach().float().requires_grad_(True)
     yr = F.gelu(xr + br, approximate="tanh")
     torch.testing.assert_close(y.float(), yr, atol=4e-2, rtol=2e-2)
@@ -131,7 +139,7 @@ def test_swiglu_packed(dt):
     xy = torch.randn(40, 2 * 512, device=DEV).to(dt).requires_grad_(True)
     a, b = xy.chunk(2, -1)
     y = ops.swiglu(a, b)
-    _lib_loaded()
+    _lib_loaded("pa_swiglu_fwd")
     xr = xy.detach().float().requires_grad_(True)
     ar, br = xr.chunk(2, -1)
     yr = F.silu(ar) * br
@@ -149,7 +157,7 @@ def test_rope(neox):
     cos, sin = rope_tables(S, D, device=DEV, neox=neox)
     x = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     y = ops.apply_rotary(x, cos, sin, neox)
-    _lib_loaded()
+    _lib_loaded("pa_rope_fwd")
     xr = x.detach().float().requires_grad_(True)
     yr = _rotate_ref(xr, cos, sin, neox, False)
     torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=2e-2)
@@ -175,7 +183,7 @@ def test_adamw_multi_tensor_master_weights():
             r.grad = g.bfloat16().float()
         opt.step()
         topt.step()
-    _lib_loaded()
+    _lib_loaded("pa_adamw_multi")
     for p, r in zip(ps, ref):
         m = opt._master_weights[id(p)]
         torch.testing.assert_close(m, r.detach(), atol=2e-5, rtol=1e-5)
@@ -187,13 +195,28 @@ def test_global_norm_multi():
     ts = [torch.randn(n, device=DEV, dtype=dt) for n, dt in [(100000, torch.float32), (333, torch.bfloat16),
                                                               (70000, torch.bfloat16)]]
     got = global_sq_norm(ts)
-    _lib_loaded()
+    _lib_loaded("pa_sq_norm_multi")
     ref = sum(t.float().pow(2).sum() for t in ts)
     torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-3)
 
 
-def test_linear_fused_bias_grad():
-    from paddlepaddle_amd.ops.linear import _LinearFn
+@pytest.fixture(params=["hip", "blas"])
+def gemm_backend(request):
+    from paddlepaddle_amd.framework.flags import get_flags, set_flags
+    old = get_flags(["FLAGS_gemm_backend"])["FLAGS_gemm_backend"]
+    set_flags({"FLAGS_gemm_backend": request.param})
+    yield request.param
+    set_flags({"FLAGS_gemm_backend": old})
+
+
+def _gemm_dispatch(backend):
+    if backend == "hip":
+        _lib_loaded("pa_gemm_bf16")
+    else:
+        assert L.calls("pa_gemm_bf16") == 0, "FLAGS_gemm_backend=blas must not run the hand-written GEMM"
+
+
+def test_linear_fused_bias_grad(gemm_backend):
     x = torch.randn(4, 96, 256, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     w = (torch.randn(256, 512, device=DEV) * 0.05).bfloat16().requires_grad_(True)
     b = torch.randn(512, device=DEV, dtype=torch.bfloat16, requires_grad=True)
@@ -208,9 +231,10 @@ def test_linear_fused_bias_grad():
     torch.testing.assert_close(b.grad.float(), br.grad, atol=0.5, rtol=2e-2)
     torch.testing.assert_close(w.grad.float(), wr.grad, atol=0.5, rtol=3e-2)
     torch.testing.assert_close(x.grad.float(), xr.grad, atol=0.1, rtol=3e-2)
+    _gemm_dispatch(gemm_backend)
 
 
-def test_linear_bias_gelu_fused():
+def test_linear_bias_gelu_fused(gemm_backend):
     x = torch.randn(128, 256, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     w = (torch.randn(256, 1024, device=DEV) * 0.05).bfloat16().requires_grad_(True)
     b = torch.randn(1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
@@ -223,12 +247,13 @@ def test_linear_bias_gelu_fused():
     yr.backward(g)
     torch.testing.assert_close(b.grad.float(), br.grad, atol=0.6, rtol=3e-2)
     torch.testing.assert_close(x.grad.float(), xr.grad, atol=0.15, rtol=3e-2)
+    _gemm_dispatch(gemm_backend)
 
 
 def test_colsum():
     x = torch.randn(3000, 5120, device=DEV, dtype=torch.bfloat16)
     got = ops.colsum(x)
-    _lib_loaded()
+    _lib_loaded("pa_colsum")
     torch.testing.assert_close(got.float(), x.float().sum(0), atol=0.3, rtol=1e-2)
 
 
@@ -237,7 +262,7 @@ def test_dropout_add_statistics_and_grad():
     x = torch.ones(1 << 20, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     r = torch.zeros(1 << 20, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     y = ops.dropout_add(x, r, 0.1, True)
-    _lib_loaded()
+    _lib_loaded("pa_dropout_add_fwd")
     kept = (y != 0).float().mean().item()
     assert abs(kept - 0.9) < 0.005
     vals = y[y != 0].float()
@@ -269,3 +294,4 @@ def test_maxpool_nhwc_matches_torch(shape, k, s, p):
     y.backward(gy.permute(0, 2, 3, 1).to(torch.bfloat16))
     yr.backward(gy.to(torch.bfloat16).float())
     torch.testing.assert_close(x.grad.float(), xr.grad.permute(0, 2, 3, 1), atol=2e-2, rtol=1e-2)
+    _lib_loaded("pa_maxpool_nhwc_fwd", "pa_maxpool_nhwc_bwd")
