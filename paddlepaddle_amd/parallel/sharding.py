@@ -267,7 +267,7 @@ class GroupShardedEngine:
         clip = getattr(opt, "_grad_clip", None)
         if clip is not None and hasattr(clip, "_extra_sq_norm_fn") and (
                 self.world > 1 or self.mp_group is not None or self.pp_group is not None):
-            pg = self.pg if self.world > 1 else None
+            pg, shard_sum = self.pg, self.world > 1  # pg None = the default (world) group
             mp_pg = self.mp_group.process_group if self.mp_group is not None else None
             pp_pg = self.pp_group.process_group if self.pp_group is not None else None
 
@@ -283,13 +283,13 @@ class GroupShardedEngine:
                 if mp_pg is not None:
                     dist.all_reduce(sq_d, group=mp_pg)
                 sq = sq_d + sq_r
-                if pg is not None:
+                if shard_sum:
                     dist.all_reduce(sq, group=pg)
                 if pp_pg is not None:  # pipeline stages hold disjoint layers
                     dist.all_reduce(sq, group=pp_pg)
                 return sq[0]
             clip._param_sq_fn = _param_sq
-            if mp_pg is None and pp_pg is None and pg is not None:  # optimizers that clip through _global_norm
+            if mp_pg is None and pp_pg is None and shard_sum:  # optimizers that clip through _global_norm
                 def _allreduce_sq(sq):
                     dist.all_reduce(sq, group=pg)
                     return sq
