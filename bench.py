@@ -42,7 +42,9 @@ def parse():
     p.add_argument("--seq-len", type=int, default=2048)
     p.add_argument("--recompute", type=int, default=0)
     p.add_argument("--sharding-stage", type=int, default=3)
-    p.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (GPT: sharding over world/tp ranks)")
+    p.add_argument("--tp", type=int, default=None,
+                   help="tensor-parallel degree (GPT: sharding over world/tp ranks). Default: the BASELINE config "
+                        "'GPT-3 13B sharding stage-3 + TP=2' -> 2 on any multi-GPU run of GPT, 1 on one GPU")
     p.add_argument("--stage3-keep-params", default="auto",
                    help="sharding stage 3: auto | 1 (keep gathered params resident from first use until the "
                         "optimizer step) | 0 (release after each unit's forward/backward, re-gather per micro-batch)")
@@ -293,6 +295,8 @@ def _relaunch(args):
 
 def main():
     args = parse()
+    if args.tp is None:
+        args.tp = 2 if (args.gpus > 1 and args.gpus % 2 == 0 and not args.model.startswith("llama")) else 1
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         _relaunch(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))

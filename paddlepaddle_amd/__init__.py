@@ -40,6 +40,8 @@ from .tensor.creation import range as _range_op  # noqa: F401
 from .tensor.einsum import einsum  # noqa: F401
 from .tensor import linalg as _linalg_mod
 from .tensor.math import inverse  # noqa: F401
+from .tensor.linalg import eigvalsh  # noqa: F401
+from .tensor.creation import _memcpy  # noqa: F401
 from . import ops  # noqa: F401
 
 # ---------------------------------------------------------------- subpackages

@@ -92,27 +92,131 @@ class functional:
 
     @staticmethod
     def get_window(window, win_length, fftbins=True, dtype="float64"):
-        name = window[0] if isinstance(window, tuple) else window
-        n = win_length
-        sym = not fftbins
-        fns = {"hann": torch.hann_window, "hamming": torch.hamming_window, "blackman": torch.blackman_window,
-               "bartlett": torch.bartlett_window}
-        if name in fns:
-            w = fns[name](n, periodic=not sym, dtype=torch.float64)
-        elif name == "kaiser":
-            beta = window[1] if isinstance(window, tuple) else 12.0
-            w = torch.kaiser_window(n, periodic=not sym, beta=beta, dtype=torch.float64)
-        elif name in ("boxcar", "rect", "rectangular"):
-            w = torch.ones(n, dtype=torch.float64)
-        elif name == "gaussian":
-            std = window[1]
-            m = n + (0 if sym else 1)
-            x = torch.arange(m, dtype=torch.float64) - (m - 1) / 2
-            w = torch.exp(-0.5 * (x / std) ** 2)[:n]
+        """Window of ``win_length`` samples; ``fftbins`` -> periodic (the symmetric window of length n + 1
+        without its last sample). ``window`` is a name or (name, *params). Reference:
+        python/paddle/audio/functional/window.py get_window (same window family and parameter order)."""
+        if isinstance(window, (tuple, list)):
+            name, params = window[0], tuple(window[1:])
         else:
-            raise ValueError(f"unsupported window {window}")
+            name, params = window, ()
+        n = int(win_length)
+        m = n + 1 if fftbins else n
+        if name not in _WINDOWS:
+            raise ValueError(f"Unknown window type: {name}")
+        fn, needs = _WINDOWS[name]
+        if len(params) < needs:
+            raise ValueError(f"The '{name}' window needs one or more parameters -- pass a tuple.")
+        w = fn(m, *params) if m > 1 else torch.ones(m, dtype=torch.float64)
+        w = w[:n]
         from ..framework import dtype as _dtm
         return _wrap(w.to(_dtm.to_torch_dtype(dtype)))
+
+
+def _cos_sum(m, coeffs):
+    x = torch.linspace(-math.pi, math.pi, m, dtype=torch.float64)
+    w = torch.zeros(m, dtype=torch.float64)
+    for k, a in enumerate(coeffs):
+        w = w + a * torch.cos(k * x)
+    return w
+
+
+def _w_general_gaussian(m, p, sig):
+    n = torch.arange(m, dtype=torch.float64) - (m - 1.0) / 2.0
+    return torch.exp(-0.5 * torch.abs(n / sig) ** (2 * p))
+
+
+def _w_exponential(m, center=None, tau=1.0):
+    c = (m - 1) / 2 if center is None else center
+    return torch.exp(-torch.abs(torch.arange(m, dtype=torch.float64) - c) / tau)
+
+
+def _w_triang(m):
+    n = torch.arange(1, (m + 1) // 2 + 1, dtype=torch.float64)
+    w = 2 * n / (m + 1.0) if m % 2 == 1 else (2 * n - 1.0) / m
+    return torch.cat([w, w.flip(0)[1:]]) if m % 2 == 1 else torch.cat([w, w.flip(0)])
+
+
+def _w_bohman(m):
+    fac = torch.abs(torch.linspace(-1, 1, m, dtype=torch.float64)[1:-1])
+    w = (1 - fac) * torch.cos(math.pi * fac) + 1.0 / math.pi * torch.sin(math.pi * fac)
+    z = torch.zeros(1, dtype=torch.float64)
+    return torch.cat([z, w, z])
+
+
+def _w_tukey(m, alpha=0.5):
+    if alpha <= 0:
+        return torch.ones(m, dtype=torch.float64)
+    if alpha >= 1:
+        return _cos_sum(m, [0.5, 0.5])
+    n = torch.arange(m, dtype=torch.float64)
+    width = math.floor(alpha * (m - 1) / 2.0)
+    w = torch.ones(m, dtype=torch.float64)
+    n1, n3 = n[:width + 1], n[m - width - 1:]
+    w[:width + 1] = 0.5 * (1 + torch.cos(math.pi * (-1 + 2.0 * n1 / alpha / (m - 1))))
+    w[m - width - 1:] = 0.5 * (1 + torch.cos(math.pi * (-2.0 / alpha + 1 + 2.0 * n3 / alpha / (m - 1))))
+    return w
+
+
+def _w_taylor(m, nbar=4, sll=30, norm=True):
+    b = 10 ** (sll / 20)
+    a = math.acosh(b) / math.pi
+    s2 = nbar ** 2 / (a ** 2 + (nbar - 0.5) ** 2)
+    ma = torch.arange(1, nbar, dtype=torch.float64)
+    fm = torch.empty(nbar - 1, dtype=torch.float64)
+    signs = torch.empty_like(ma)
+    signs[::2] = 1
+    signs[1::2] = -1
+    m2 = ma * ma
+    for mi in range(len(ma)):
+        numer = signs[mi] * torch.prod(1 - m2[mi] / s2 / (a ** 2 + (ma - 0.5) ** 2))
+        denom = 2 * torch.prod(1 - m2[mi] / torch.cat([m2[:mi], m2[mi + 1:]]))
+        fm[mi] = numer / denom
+    x = torch.arange(m, dtype=torch.float64)
+
+    def w_of(xx):
+        return 1 + 2 * torch.matmul(fm, torch.cos(2 * math.pi * ma.unsqueeze(1) * (xx - m / 2.0 + 0.5) / m))
+    w = w_of(x)
+    if norm:
+        w = w / w_of(torch.tensor([(m - 1) / 2.0], dtype=torch.float64))
+    return w
+
+
+def _w_kaiser(m, beta=12.0):
+    n = torch.arange(m, dtype=torch.float64)
+    alpha = (m - 1) / 2.0
+    return torch.special.i0(beta * torch.sqrt(1 - ((n - alpha) / alpha) ** 2)) / torch.special.i0(
+        torch.tensor(float(beta), dtype=torch.float64))
+
+
+def _w_gaussian(m, std):
+    n = torch.arange(m, dtype=torch.float64) - (m - 1.0) / 2.0
+    return torch.exp(-n ** 2 / (2 * std * std))
+
+
+def _w_bartlett(m):
+    n = torch.arange(m, dtype=torch.float64)
+    return torch.where(n <= (m - 1) / 2.0, 2.0 * n / (m - 1), 2.0 - 2.0 * n / (m - 1))
+
+
+_WINDOWS = {
+    "hamming": (lambda m: _cos_sum(m, [0.54, 0.46]), 0),
+    "hann": (lambda m: _cos_sum(m, [0.5, 0.5]), 0),
+    "blackman": (lambda m: _cos_sum(m, [0.42, 0.50, 0.08]), 0),
+    "nuttall": (lambda m: _cos_sum(m, [0.3635819, 0.4891775, 0.1365995, 0.0106411]), 0),
+    "cosine": (lambda m: torch.sin(math.pi / m * (torch.arange(m, dtype=torch.float64) + 0.5)), 0),
+    "gaussian": (_w_gaussian, 1),
+    "general_gaussian": (_w_general_gaussian, 2),
+    "exponential": (_w_exponential, 0),
+    "triang": (_w_triang, 0),
+    "bohman": (_w_bohman, 0),
+    "tukey": (_w_tukey, 0),
+    "taylor": (_w_taylor, 0),
+    "bartlett": (_w_bartlett, 0),
+    "kaiser": (_w_kaiser, 0),
+    "boxcar": (lambda m: torch.ones(m, dtype=torch.float64), 0),
+    "rect": (lambda m: torch.ones(m, dtype=torch.float64), 0),
+    "rectangular": (lambda m: torch.ones(m, dtype=torch.float64), 0),
+}
 
 
 class Spectrogram(nn.Layer):

@@ -121,11 +121,16 @@ EagerPyLayerContext = PyLayerContext
 
 
 def backward(tensors, grad_tensors=None, retain_graph=False):
+    """paddle.autograd.backward: a missing (None) gradient of any output — scalar or not — is ones_like(output).
+    Reference: python/paddle/autograd/backward_mode.py backward."""
     ts = [tensors] if isinstance(tensors, Tensor) else list(tensors)
-    gs = None
+    gs = [None] * len(ts)
     if grad_tensors is not None:
-        gs = [grad_tensors] if isinstance(grad_tensors, Tensor) else list(grad_tensors)
-        gs = [None if g is None else _u(g) for g in gs]
+        gl = [grad_tensors] if isinstance(grad_tensors, Tensor) else list(grad_tensors)
+        if len(gl) != len(ts):
+            raise ValueError("The length of grad_tensors must be equal to the length of tensors")
+        gs = [None if g is None else _u(g) for g in gl]
+    gs = [torch.ones_like(t._t) if g is None else g for t, g in zip(ts, gs)]
     torch.autograd.backward([t._t for t in ts], gs, retain_graph=retain_graph)
 
 

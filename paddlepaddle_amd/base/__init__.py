@@ -9,4 +9,5 @@ from ..static import (Program, program_guard, Executor, global_scope, scope_guar
 from ..framework.place import CPUPlace, CUDAPlace, CUDAPinnedPlace  # noqa: F401
 from ..framework import in_dynamic_mode as in_dygraph_mode  # noqa: F401
 from ..framework.tensor import Tensor as Variable  # noqa: F401
+from ..framework.flags import set_flags, get_flags  # noqa: F401,E402
 from . import core, framework, dygraph  # noqa: F401,E402

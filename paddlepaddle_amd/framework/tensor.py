@@ -99,7 +99,11 @@ class Tensor:
             t = _to_torch_tensor(data, dtype, place)
         if dtype is not None:
             t = t.to(_dt.to_torch_dtype(dtype))
-        self._t = t if stop_gradient or not t.is_floating_point() else t.requires_grad_(True)
+        if stop_gradient or t.is_floating_point() or t.is_complex():
+            self._t = t if stop_gradient else t.requires_grad_(True)
+        else:  # paddle lets integer / bool tensors carry stop_gradient=False (no gradient ever flows to them)
+            self._t = t
+            self.__dict__["_sg_override"] = False
         self._name = name
         self._persistable = False
 
@@ -152,12 +156,19 @@ class Tensor:
 
     @property
     def stop_gradient(self):
-        return not self._t.requires_grad
+        if self._t.requires_grad:
+            return False
+        return self.__dict__.get("_sg_override", True)
 
     @stop_gradient.setter
     def stop_gradient(self, v):
         v = bool(v)
         t = self._t
+        self.__dict__.pop("_sg_override", None)
+        if not (t.is_floating_point() or t.is_complex()):
+            if not v:
+                self.__dict__["_sg_override"] = False
+            return
         if v:
             if t.requires_grad:
                 self._t = t.detach() if not t.is_leaf else t.requires_grad_(False)
@@ -176,7 +187,11 @@ class Tensor:
     @property
     def grad(self):
         g = self._t.grad
-        return None if g is None else _wrap(g)
+        if g is None:
+            return None
+        w = _wrap(g)
+        w.__dict__["_sg_override"] = False  # paddle's gradient tensors report stop_gradient=False
+        return w
 
     @grad.setter
     def grad(self, v):
@@ -391,7 +406,7 @@ class Tensor:
     # ---------------------------------------------------------------- autograd
     def backward(self, grad_tensor=None, retain_graph=False):
         g = _unwrap(grad_tensor)
-        if g is None and self._t.numel() != 1:
+        if g is None:
             g = torch.ones_like(self._t)
         self._t.backward(g, retain_graph=retain_graph)
 
@@ -548,6 +563,10 @@ def to_tensor(data, dtype=None, place=None, stop_gradient=True):
     else:
         t = _to_torch_tensor(data, dtype, place)
     if not stop_gradient:
+        if not (t.is_floating_point() or t.is_complex()):
+            w = _wrap(t)
+            w.__dict__["_sg_override"] = False
+            return w
         t = t.detach().requires_grad_(True) if t.requires_grad else t.requires_grad_(True)
     return _wrap(t)
 
@@ -591,8 +610,13 @@ class Parameter(Tensor):
 
     def _replace_data(self, t):
         """Swap the underlying buffer (used by sharding / amp decorate) keeping identity."""
-        req = self._t.requires_grad
-        self._t = t.detach().requires_grad_(req)
+        req = self._t.requires_grad or self.__dict__.get("_sg_override") is False
+        if req and not (t.is_floating_point() or t.is_complex()):
+            self._t = t.detach()  # e.g. Layer.astype("int8"): keeps stop_gradient=False, no grad flows
+            self.__dict__["_sg_override"] = False
+        else:
+            self._t = t.detach().requires_grad_(req)
+            self.__dict__.pop("_sg_override", None)
         _PARAM_OF[id(self._t)] = self
 
 

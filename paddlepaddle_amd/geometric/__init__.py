@@ -96,9 +96,15 @@ def reindex_graph(x, neighbors, count, value_buffer=None, index_buffer=None, nam
 
 
 def reindex_heter_graph(x, neighbors, count, value_buffer=None, index_buffer=None, name=None):
+    """Heterogeneous reindex: one (neighbors, count) pair per edge type over the SAME centre nodes x; ids are
+    shared across types (x first, then new neighbours in first-seen order over the concatenation) and the
+    dst of each type repeats x by that type's counts. Reference: python/paddle/geometric/reindex.py."""
     nb = torch.cat([_t(n) for n in neighbors])
-    ct = torch.cat([_t(c) for c in count])
-    return reindex_graph(x, nb, ct)
+    src, _, nodes = reindex_graph(x, nb, torch.zeros(len(_t(x)), dtype=torch.int64))
+    nx = len(_t(x))
+    dst = torch.cat([torch.repeat_interleave(torch.arange(nx, dtype=torch.int64), _t(c).cpu().to(torch.int64))
+                     for c in count]).to(_t(x).device)
+    return src, _wrap(dst), nodes
 
 
 def sample_neighbors(row, colptr, input_nodes, sample_size=-1, eids=None, return_eids=False, perm_buffer=None,

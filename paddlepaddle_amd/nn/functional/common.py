@@ -62,21 +62,23 @@ def feature_alpha_dropout(x, p=0.5, training=True, name=None):
 
 
 def pad(x, pad, mode="constant", value=0.0, data_format="NCHW", pad_from_left_axis=True, name=None):
+    """paddle.nn.functional.pad. Reference: python/paddle/nn/functional/common.py pad (Note 1-3):
+    constant mode with a list whose length is not 2*(N-2) pads whole axes — a 2N list from the first axis
+    forward (``pad_from_left_axis``) or from the last axis backward, a shorter list from the last axis;
+    every other case pads the spatial axes of ``data_format`` ([left, right, top, bottom, front, back])."""
     t = T(x)
-    if isinstance(pad, Tensor):
+    pad_is_tensor = isinstance(pad, Tensor)
+    if pad_is_tensor:
         pad = pad._t.tolist()
     pad = [int(p) for p in pad]
     nd = t.dim()
-    if len(pad) == 2 * nd:
-        # paddle full-rank pad is [d0_before, d0_after, d1_before, ...]; torch wants last dim first
-        tp = []
-        for i in reversed(range(nd)):
-            tp += [pad[2 * i], pad[2 * i + 1]]
-        if mode == "constant":
-            return _wrap(F.pad(t, tp, "constant", value))
-        pad = pad[4:] if nd == 4 else pad
-    # spatial pad (paddle order: [left, right, top, bottom, front, back]) == torch order
-    channel_last = data_format in ("NHWC", "NLC", "NDHWC")
+    if mode == "constant" and not pad_is_tensor and len(pad) != 2 * (nd - 2):
+        pairs = [(pad[2 * i], pad[2 * i + 1]) for i in range(len(pad) // 2)]
+        if len(pad) == 2 * nd and pad_from_left_axis:
+            pairs = pairs[::-1]  # pairs[0] belongs to axis 0; torch's list starts at the last axis
+        tp = [v for pr in pairs for v in pr]
+        return _wrap(F.pad(t, tp, "constant", value))
+    channel_last = data_format in ("NHWC", "NLC", "NDHWC", "NWC")
     if channel_last:
         perm = [0, nd - 1] + list(range(1, nd - 1))
         t = t.permute(*perm)

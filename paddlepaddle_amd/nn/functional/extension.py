@@ -137,15 +137,18 @@ def hsigmoid_loss(input, label, num_classes, weight, bias=None, path_table=None,
 # ----------------------------------------------------------------------------------- RNN-T
 def rnnt_loss(input, label, input_lengths, label_lengths, blank=0, fastemit_lambda=0.001, reduction="mean",
               name=None):
-    """RNN transducer loss. input: [B, T, U+1, V] logits (log-softmax applied here, as warp-transducer does).
-    The forward variable is computed in log space over anti-diagonals; FastEmit scales the gradient of the
-    label-emission terms by (1 + lambda) and leaves the loss value unchanged."""
-    logits = T(input).float()
+    """RNN transducer loss. Reference: python/paddle/nn/functional/loss.py rnnt_loss: ``input`` [B, T, U+1, V]
+    holds LOG-PROBABILITIES (the docstring's contract; its example, -2.85042444, is computed on them as given).
+    The forward variable alpha[t, u] is a log-space recursion; FastEmit scales the gradient of the
+    label-emission terms by (1 + lambda) and leaves the loss value unchanged. Output dtype = input dtype."""
+    logits = T(input)
+    if not logits.is_floating_point():
+        logits = logits.float()
     lab = T(label).to(torch.int64)
     tl = T(input_lengths).to(torch.int64)
     ul = T(label_lengths).to(torch.int64)
     B, Tm, U1, V = logits.shape
-    lp = logits.log_softmax(-1)
+    lp = logits
     blank_lp = lp[..., blank]                                        # [B, T, U+1]
     lab_pad = torch.cat([lab, torch.zeros(B, 1, dtype=torch.int64, device=lab.device)], 1)[:, :U1]
     emit_lp = lp.gather(3, lab_pad.view(B, 1, U1, 1).expand(B, Tm, U1, 1)).squeeze(3)  # [B, T, U+1]
@@ -155,7 +158,7 @@ def rnnt_loss(input, label, input_lengths, label_lengths, blank=0, fastemit_lamb
     for t in range(Tm):
         for u in range(U1):
             if t == 0 and u == 0:
-                alpha[t][u] = torch.zeros(B, device=lp.device)
+                alpha[t][u] = torch.zeros(B, device=lp.device, dtype=lp.dtype)
                 continue
             cands = []
             if t > 0:

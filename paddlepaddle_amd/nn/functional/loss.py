@@ -233,8 +233,39 @@ def margin_cross_entropy(logits, label, margin1=1.0, margin2=0.5, margin3=0.0, s
 
 def rnnt_loss(input, label, input_lengths, label_lengths, blank=0, fastemit_lambda=0.001, reduction="mean",
               name=None):
-    import torchaudio  # noqa: F401  (not available: documented gap)
-    raise NotImplementedError("rnnt_loss requires torchaudio which is not installed in this image")
+    from .extension import rnnt_loss as _rnnt
+    return _rnnt(input, label, input_lengths, label_lengths, blank, fastemit_lambda, reduction, name)
+
+
+def edit_distance(input, label, normalized=True, ignored_tokens=None, input_length=None, label_length=None,
+                  name=None):
+    """Levenshtein distance between each pair of int64 sequences. Returns (sequence_num [1] int64,
+    distances [B, 1] float32) in the order phi's edit_distance kernel writes them (the reference docstring
+    prints them under swapped names). ``normalized`` divides by the label length.
+    Reference: python/paddle/nn/functional/loss.py edit_distance, phi/kernels/cpu/edit_distance_kernel.cc."""
+    import numpy as _np
+    if ignored_tokens:
+        raise ValueError(f"Expected ignored_tokens is None (got {ignored_tokens})")
+    a = T(input).detach().cpu().numpy()
+    b = T(label).detach().cpu().numpy()
+    B = a.shape[0]
+    la = T(input_length).cpu().numpy().reshape(-1) if input_length is not None else _np.full(B, a.shape[1])
+    lb = T(label_length).cpu().numpy().reshape(-1) if label_length is not None else _np.full(B, b.shape[1])
+    out = _np.zeros((B, 1), dtype=_np.float32)
+    for i in range(B):
+        x, y = a[i, :int(la[i])], b[i, :int(lb[i])]
+        m, n = len(x), len(y)
+        prev = _np.arange(n + 1, dtype=_np.int64)
+        for r in range(1, m + 1):
+            cur = _np.empty(n + 1, dtype=_np.int64)
+            cur[0] = r
+            for c in range(1, n + 1):
+                cur[c] = min(prev[c] + 1, cur[c - 1] + 1, prev[c - 1] + (x[r - 1] != y[c - 1]))
+            prev = cur
+        d = float(prev[n])
+        out[i, 0] = d / n if normalized and n > 0 else d
+    dev = T(input).device
+    return (_wrap(torch.tensor([B], dtype=torch.int64, device=dev)), _wrap(torch.from_numpy(out).to(dev)))
 
 
 def adaptive_log_softmax_with_loss(input, label, head_weight, tail_weights, cutoffs, head_bias=None, name=None):

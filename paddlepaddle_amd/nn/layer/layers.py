@@ -406,6 +406,7 @@ class Layer:
             self._apply_to_tensors(lambda t: t.to(dev), floating_only=False)
         if dtype is not None:
             td = _dt.to_torch_dtype(dtype)
+            # floating parameters / buffers are cast (to any dtype: paddle's Layer.astype("int8") casts weights)
             self._apply_to_tensors(lambda t: t.to(td))
             for l in self.sublayers(include_self=True):
                 object.__setattr__(l, "_dtype", _dt.convert_dtype(dtype).name)

@@ -24,7 +24,8 @@ _SKIP = {"T", "TT", "to_tensor", "shape_arg", "axis_arg", "dtype_arg", "wrap", "
          "zeros", "ones", "empty", "full", "eye", "linspace", "logspace", "rand", "randn", "randint", "randperm",
          "uniform", "normal", "standard_normal", "tril_indices", "triu_indices", "assign", "add_n", "concat",
          "stack", "broadcast_tensors", "multiplex", "cartesian_prod", "hstack", "vstack", "dstack",
-         "column_stack", "row_stack", "complex", "polar", "log_normal", "scatter_nd", "broadcast_shape"}
+         "column_stack", "row_stack", "complex", "polar", "log_normal", "scatter_nd", "broadcast_shape",
+         "create_array", "array_write", "array_read", "array_length", "uniform_random_batch_size_like"}
 
 _VARARG_SHAPE = {"reshape", "reshape_", "tile", "expand", "broadcast_to", "view"}
 
@@ -130,15 +131,17 @@ def _bind_reference_extras():
         Tensor.istft = _signal.istft
 
     def set_(self, source=None, shape=None, stride=None, offset=0, name=None):
-        """Make this tensor share ``source``'s storage (optionally as a strided view)."""
+        """Make this tensor share ``source``'s storage (optionally as a strided view); ``offset`` is in BYTES
+        from the start of ``source``'s data (reference: python/paddle/tensor/creation.py set_)."""
         import torch
         if source is None:
             self._t = torch.empty(0, dtype=self._t.dtype, device=self._t.device)
             return self
         src = source._t if isinstance(source, Tensor) else torch.as_tensor(source)
-        if shape is not None:
-            src = src.as_strided(list(shape), list(stride) if stride is not None else
-                                 torch.empty(list(shape)).stride(), offset)
+        if shape is not None or offset:
+            shp = list(shape) if shape is not None else list(src.shape)
+            st = list(stride) if stride is not None else list(torch.empty(shp, device="meta").stride())
+            src = src.as_strided(shp, st, src.storage_offset() + offset // src.element_size())
         self._t = src
         return self
     if not hasattr(Tensor, "set_"):

@@ -163,7 +163,11 @@ def assign(x, output=None):
             t = t.float()
     if output is not None:
         with torch.no_grad():
-            output._t.copy_(t)
+            if tuple(output._t.shape) != tuple(t.shape) or output._t.dtype != t.dtype:
+                # paddle's assign(x, output) gives output x's shape and dtype (the variable is re-bound)
+                output._t = t.detach().clone() if output.stop_gradient else t.detach().clone().requires_grad_(True)
+            else:
+                output._t.copy_(t)
         return output
     return _wrap(t)
 
@@ -204,3 +208,50 @@ def fill_constant(shape, dtype, value, force_cpu=False, out=None, name=None):
 
 def range(start=0, end=None, step=1, dtype=None, name=None):  # noqa: A001
     return arange(start, end, step, dtype)
+
+
+# ----------------------------------------------------------------------------- tensor arrays
+# paddle.tensor.array_*: in dygraph a TensorArray is a plain Python list of Tensors
+# (reference: python/paddle/tensor/array.py; the static LOD_TENSOR_ARRAY variable is the graph form).
+def create_array(dtype, initialized_list=None):
+    arr = []
+    for v in initialized_list or []:
+        if not isinstance(v, Tensor):
+            raise TypeError("create_array: initialized_list must hold Tensors")
+        arr.append(v)
+    return arr
+
+
+def _array_index(i):
+    return int(i.item()) if isinstance(i, Tensor) else int(i)
+
+
+def array_write(x, i, array=None):
+    if array is None:
+        array = []
+    k = _array_index(i)
+    if k < len(array):
+        array[k] = x
+    elif k == len(array):
+        array.append(x)
+    else:
+        raise IndexError(f"array_write: index {k} is past the end of an array of length {len(array)}")
+    return array
+
+
+def array_read(array, i):
+    return array[_array_index(i)]
+
+
+def array_length(array):
+    return len(array)  # dygraph: a Python int (reference: python/paddle/tensor/array.py array_length)
+
+
+def _memcpy(input, place=None, output=None):
+    """paddle._memcpy: copy ``input`` to ``place`` (reference: python/paddle/tensor/creation.py _memcpy)."""
+    from ..framework.place import to_torch_device
+    t = input._t.detach().to(to_torch_device(place) if place is not None else input._t.device, copy=True)
+    if output is not None:
+        output._t = t
+        return output
+    return _wrap(t)

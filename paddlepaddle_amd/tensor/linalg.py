@@ -50,7 +50,9 @@ def slogdet(x, name=None):
 
 
 def matrix_rank(x, tol=None, hermitian=False, atol=None, rtol=None, name=None):
-    return _wrap(torch.linalg.matrix_rank(T(x), atol=atol if tol is None else tol, rtol=rtol, hermitian=hermitian))
+    # phi's matrix_rank kernel returns int32 (reference docstring: dtype=int32)
+    return _wrap(torch.linalg.matrix_rank(T(x), atol=atol if tol is None else tol, rtol=rtol,
+                                          hermitian=hermitian).to(torch.int32))
 
 
 def matrix_power(x, n, name=None):
@@ -81,7 +83,7 @@ def qr(x, mode="reduced", name=None):
 def lu(x, pivot=True, get_infos=False, name=None):
     lu_, piv, info = torch.linalg.lu_factor_ex(T(x), pivot=pivot)
     res = (_wrap(lu_), _wrap(piv.to(torch.int32)))
-    return res + (_wrap(info),) if get_infos else res
+    return res + (_wrap(info.to(torch.int32)),) if get_infos else res
 
 
 def lu_unpack(x, y, unpack_ludata=True, unpack_pivots=True, name=None):
@@ -140,7 +142,7 @@ def triangular_solve(x, y, upper=True, transpose=False, unitriangular=False, nam
 
 def lstsq(x, y, rcond=None, driver=None, name=None):
     r = torch.linalg.lstsq(T(x), T(y), rcond=rcond, driver=driver)
-    return _wrap(r.solution), _wrap(r.residuals), _wrap(r.rank), _wrap(r.singular_values)
+    return _wrap(r.solution), _wrap(r.residuals), _wrap(r.rank.to(torch.int32)), _wrap(r.singular_values)
 
 
 def pinv(x, rcond=1e-15, hermitian=False, name=None):

@@ -317,6 +317,12 @@ def take_along_axis(arr, indices, axis, broadcast=True):
 def put_along_axis(arr, indices, values, axis, reduce="assign", include_self=True, broadcast=True):
     t, i = T(arr), T(indices).long()
     v = TT(values, t).to(t.dtype)
+    if broadcast and i.dim() == t.dim():
+        # paddle broadcasts indices against arr on every axis but `axis` (put_along_axis docstring:
+        # indices [[0]] on a [2, 3] arr with axis=0 writes the whole first row)
+        shape = [i.shape[d] if d == axis % t.dim() else t.shape[d] for d in range(t.dim())]
+        if list(i.shape) != shape:
+            i = i.expand(shape)
     if v.dim() == 0 or v.shape != i.shape:
         v = v.expand_as(i) if v.dim() <= i.dim() else v
     if reduce == "assign":
@@ -537,3 +543,10 @@ def fill_diagonal_(x, value, offset=0, wrap=False, name=None):
 
 def fill_diagonal_tensor(x, y, offset=0, dim1=0, dim2=1, name=None):
     return _wrap(torch.diagonal_scatter(T(x), T(y), offset, dim1, dim2))
+
+
+def fill_diagonal_tensor_(x, y, offset=0, dim1=0, dim2=1, name=None):
+    """In-place paddle.Tensor.fill_diagonal_tensor_. Reference: python/paddle/tensor/manipulation.py."""
+    with torch.no_grad():
+        torch.diagonal(x._t, offset, dim1, dim2).copy_(T(y))
+    return x

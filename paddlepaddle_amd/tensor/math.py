@@ -11,6 +11,7 @@ import math as _math
 
 import numpy as _np
 np = _np
+
 import torch
 
 from ..amp.state import maybe_cast
@@ -74,6 +75,42 @@ for _n, (_f, _fi) in _UNARY.items():
     _make_unary(_n, _f, _fi)
 bitwise_invert = _g["bitwise_not"]
 bitwise_invert_ = _g["bitwise_not_"]
+
+
+def _round_half_away(t, decimals=0):
+    if not t.is_floating_point():
+        return t
+    if decimals:
+        s = 10.0 ** decimals
+        return torch.sign(t) * torch.floor(torch.abs(t) * s + 0.5) / s
+    return torch.sign(t) * torch.floor(torch.abs(t) + 0.5)
+
+
+def round(x, decimals=0, name=None):  # noqa: A001
+    """paddle.round: halves round AWAY from zero (phi RoundFunctor uses std::round), not to even as
+    torch.round does: round(-0.5) = -1. Reference: python/paddle/tensor/ops.py round."""
+    return _wrap(_round_half_away(T(x), decimals))
+
+
+def round_(x, decimals=0, name=None):
+    x._t.copy_(_round_half_away(x._t, decimals))
+    return x
+
+
+def _digamma_paddle(t):
+    # phi's digamma (Eigen) is NaN at the poles (0, -1, -2, ...); torch returns -inf at 0
+    r = torch.digamma(t)
+    return torch.where((t <= 0) & (t == torch.floor(t)), torch.full_like(r, float("nan")), r)
+
+
+def digamma(x, name=None):
+    """paddle.digamma. Reference: python/paddle/tensor/math.py digamma (NaN at non-positive integers)."""
+    return _wrap(_digamma_paddle(T(x)))
+
+
+def digamma_(x, name=None):
+    x._t.copy_(_digamma_paddle(x._t))
+    return x
 
 
 def logit(x, eps=None, name=None):
@@ -165,8 +202,7 @@ _BINARY = {
     "logaddexp": (torch.logaddexp, None), "heaviside": (torch.heaviside, None), "gcd": (torch.gcd, None),
     "lcm": (torch.lcm, None), "copysign": (torch.copysign, None), "nextafter": (torch.nextafter, None),
     "bitwise_and": (torch.bitwise_and, None), "bitwise_or": (torch.bitwise_or, None),
-    "bitwise_xor": (torch.bitwise_xor, None), "bitwise_left_shift": (torch.bitwise_left_shift, None),
-    "bitwise_right_shift": (torch.bitwise_right_shift, None),
+    "bitwise_xor": (torch.bitwise_xor, None),
     "logical_and": (torch.logical_and, None), "logical_or": (torch.logical_or, None),
     "logical_xor": (torch.logical_xor, None), "xlogy": (torch.xlogy, None),
     "ldexp": (lambda a, b: a * torch.pow(2.0, b), None),
@@ -176,6 +212,46 @@ for _n, (_f, _fi) in _BINARY.items():
 
 mod = _g["remainder"]
 mod_ = _g["remainder_"]
+
+
+def _unsigned_of(dt):
+    return {torch.int8: torch.uint8, torch.int16: torch.int16, torch.int32: torch.int32,
+            torch.int64: torch.int64, torch.uint8: torch.uint8}[dt]
+
+
+def bitwise_left_shift(x, y, is_arithmetic=True, out=None, name=None):
+    """paddle.bitwise_left_shift. Reference: python/paddle/tensor/math.py bitwise_left_shift (the arithmetic
+    and logical left shifts are the same operation on two's-complement integers)."""
+    return _wrap(torch.bitwise_left_shift(T(x), T(y)))
+
+
+def bitwise_right_shift(x, y, is_arithmetic=True, out=None, name=None):
+    """paddle.bitwise_right_shift: arithmetic (sign-extending) by default; ``is_arithmetic=False`` is the
+    logical shift (zero fill), computed on the unsigned reinterpretation of the bits.
+    Reference: python/paddle/tensor/math.py bitwise_right_shift."""
+    tx, ty = T(x), T(y)
+    if is_arithmetic or tx.dtype == torch.uint8:
+        return _wrap(torch.bitwise_right_shift(tx, ty))
+    if tx.dtype == torch.int8:
+        return _wrap(torch.bitwise_right_shift(tx.view(torch.uint8), ty.to(torch.uint8)).view(torch.int8))
+    bits = torch.iinfo(tx.dtype).bits
+    ty = ty.to(tx.dtype)
+    # logical shift of a signed value: arithmetic shift, then clear the sign-extended high bits
+    sh = torch.bitwise_right_shift(tx, ty)
+    mask = torch.where(ty > 0, torch.bitwise_left_shift(torch.ones_like(tx), (bits - ty).clamp(min=0, max=bits - 1)) - 1,
+                       torch.full_like(tx, -1))
+    mask = torch.where(ty >= bits, torch.zeros_like(tx), mask)
+    return _wrap(torch.bitwise_and(sh, mask))
+
+
+def bitwise_left_shift_(x, y, is_arithmetic=True, out=None, name=None):
+    x._t.copy_(bitwise_left_shift(x, y, is_arithmetic)._t)
+    return x
+
+
+def bitwise_right_shift_(x, y, is_arithmetic=True, out=None, name=None):
+    x._t.copy_(bitwise_right_shift(x, y, is_arithmetic)._t)
+    return x
 floor_mod = _g["remainder"]
 floor_mod_ = _g["remainder_"]
 
@@ -321,9 +397,37 @@ def cross(x, y, axis=9, name=None):
 
 
 def tensordot(x, y, axes=2, name=None):
+    """paddle.tensordot. Reference: python/paddle/tensor/manipulation.py tensordot: ``axes`` is an int n (last n
+    of x with first n of y), a flat list (the same axes of x and y), or [axes_x, axes_y] where the shorter list is
+    extended with the longer one's tail; contracted axes broadcast (size 1 against size n)."""
+    tx, ty = T(x), T(y)
     if isinstance(axes, Tensor):
         axes = axes._t.tolist()
-    return _wrap(torch.tensordot(T(x), T(y), dims=axes))
+    if isinstance(axes, int):
+        ax_x, ax_y = list(range(tx.dim() - axes, tx.dim())), list(range(axes))
+    else:
+        axes = list(axes)
+        if len(axes) == 0:
+            ax_x, ax_y = [], []
+        elif builtins.all(isinstance(a, int) for a in axes):
+            ax_x, ax_y = list(axes), list(axes)
+        else:
+            seqs = [list(a._t.tolist() if isinstance(a, Tensor) else a) for a in axes[:2]]
+            ax_x = seqs[0]
+            ax_y = seqs[1] if len(seqs) > 1 else list(seqs[0])
+            if len(ax_x) < len(ax_y):
+                ax_x = ax_x + ax_y[len(ax_x):]
+            elif len(ax_y) < len(ax_x):
+                ax_y = ax_y + ax_x[len(ax_y):]
+    ax_x = [a % tx.dim() for a in ax_x]
+    ax_y = [a % ty.dim() for a in ax_y]
+    for a, b in zip(ax_x, ax_y):
+        if tx.shape[a] != ty.shape[b]:
+            if tx.shape[a] == 1:
+                ty = ty.sum(b, keepdim=True)
+            elif ty.shape[b] == 1:
+                tx = tx.sum(a, keepdim=True)
+    return _wrap(torch.tensordot(tx, ty, dims=(ax_x, ax_y)))
 
 
 def multiplex(inputs, index, name=None):
@@ -412,8 +516,42 @@ def _minmax(fn):
     return op
 
 
-max = _minmax(torch.amax)  # noqa: A001
-min = _minmax(torch.amin)  # noqa: A001
+class _MaxAllTies(torch.autograd.Function):
+    """paddle.max / paddle.min gradient: EVERY element equal to the extreme receives the full upstream gradient
+    (paddle/phi/kernels/funcs/reduce_grad_functions.h MaxOrMinGrad: dx = dy * (x == y)); amax / amin instead
+    split it evenly between ties (torch.amax's rule). Reference: python/paddle/tensor/math.py max (docstring
+    example: 5 tied maxima each get 1.0 from max and 0.2 from amax)."""
+
+    @staticmethod
+    def forward(ctx, t, dims, keepdim, is_max):
+        r = (torch.amax if is_max else torch.amin)(t, dim=dims, keepdim=True)
+        ctx.save_for_backward(t, r)
+        return r if keepdim else r.reshape([d for i, d in enumerate(t.shape) if i not in dims])
+
+    @staticmethod
+    def backward(ctx, g):
+        t, r = ctx.saved_tensors
+        return (t == r).to(g.dtype) * g.reshape(r.shape), None, None, None
+
+
+def _minmax_ties(is_max):
+    def op(x, axis=None, keepdim=False, name=None):
+        t = T(x)
+        ax = axis_arg(axis)
+        if not t.requires_grad or not torch.is_grad_enabled():
+            fn = torch.amax if is_max else torch.amin
+            if ax is None:
+                r = fn(t)
+                return _wrap(r.reshape([1] * t.dim()) if keepdim else r)
+            return _wrap(fn(t, dim=ax, keepdim=keepdim))
+        dims = tuple(range(t.dim())) if ax is None else tuple(a % builtins.max(t.dim(), 1) for a in
+                                                               (ax if isinstance(ax, tuple) else (ax,)))
+        return _wrap(_MaxAllTies.apply(t, dims, keepdim, is_max))
+    return op
+
+
+max = _minmax_ties(True)  # noqa: A001
+min = _minmax_ties(False)  # noqa: A001
 amax = _minmax(torch.amax)
 amin = _minmax(torch.amin)
 

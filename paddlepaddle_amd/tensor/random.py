@@ -126,3 +126,12 @@ def geometric_(x, probs, name=None):
     with torch.no_grad():
         x._t.geometric_(probs)
     return x
+
+
+def uniform_random_batch_size_like(input, shape, dtype="float32", input_dim_idx=0, output_dim_idx=0, min=-1.0,  # noqa: A002
+                                   max=1.0, seed=0):  # noqa: A002
+    """U(min, max) samples of ``shape`` with dim ``output_dim_idx`` replaced by ``input.shape[input_dim_idx]``.
+    Reference: python/paddle/tensor/random.py uniform_random_batch_size_like."""
+    shp = list(shape)
+    shp[output_dim_idx] = T(input).shape[input_dim_idx]
+    return uniform(shp, dtype=dtype, min=min, max=max, seed=seed)

@@ -20,8 +20,8 @@ def _port():
 def test_bench_two_ranks_json_line():
     env = dict(os.environ, PADDLE_AMD_FORCE_CPU="1", PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--model",
-           "tiny", "--steps", "2", "--warmup", "1", "--seq-len", "64", "--micro-batch", "2", "--accum", "2",
+           "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--tp", "1",
+           "--model", "tiny", "--steps", "2", "--warmup", "1", "--seq-len", "64", "--micro-batch", "2", "--accum", "2",
            "--resnet-batch", "2", "--resnet-steps", "1"]
     r = subprocess.run(cmd, env=env, capture_output=True, timeout=600, cwd="/tmp")
     assert r.returncode == 0, r.stderr.decode()[-3000:]

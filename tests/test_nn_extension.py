@@ -86,10 +86,23 @@ def test_rnnt_loss_matches_alignment_sum():
     torch.manual_seed(0)
     logits = torch.randn(1, 3, 3, 4)
     lab = np.array([[1, 2]])
-    got = F.rnnt_loss(paddle.to_tensor(logits.numpy()), paddle.to_tensor(lab), paddle.to_tensor([3]),
+    # the reference contract: input holds log-probabilities (rnnt_loss docstring)
+    lp = torch.log_softmax(logits, -1)
+    got = F.rnnt_loss(paddle.to_tensor(lp.numpy()), paddle.to_tensor(lab), paddle.to_tensor([3]),
                       paddle.to_tensor([2]), fastemit_lambda=0.0, reduction="sum")
-    ref = _rnnt_ref(torch.log_softmax(logits, -1)[0].numpy(), lab[0], 3, 2)
+    ref = _rnnt_ref(lp[0].numpy(), lab[0], 3, 2)
     np.testing.assert_allclose(float(got), ref, rtol=1e-5)
+
+
+def test_rnnt_loss_reference_docstring_value():
+    """python/paddle/nn/functional/loss.py rnnt_loss example: -2.85042444 (float64 in, float64 out)."""
+    acts = np.array([[[[0.1, 0.6, 0.1, 0.1, 0.1], [0.1, 0.1, 0.6, 0.1, 0.1], [0.1, 0.1, 0.2, 0.8, 0.1]],
+                      [[0.1, 0.6, 0.1, 0.1, 0.1], [0.1, 0.1, 0.2, 0.1, 0.1], [0.7, 0.1, 0.2, 0.1, 0.1]]]])
+    got = F.rnnt_loss(paddle.to_tensor(acts, stop_gradient=False), paddle.to_tensor([[1, 2]], "int32"),
+                      paddle.to_tensor([2], "int32"), paddle.to_tensor([2], "int32"), blank=0, fastemit_lambda=0.0,
+                      reduction="sum")
+    assert got.dtype == paddle.float64
+    np.testing.assert_allclose(float(got), -2.85042444, rtol=1e-7)
 
 
 def test_adaptive_log_softmax_normalised():

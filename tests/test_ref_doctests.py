@@ -1,0 +1,29 @@
+"""Parity pinned by the reference's own docstring examples (tools/ref_doctests.py): every deterministic
+``>>>`` example of the listed reference modules runs against paddlepaddle_amd (``import paddle`` aliased) and
+its printed output must match the documented one. Skipped when the reference tree is not present (GPU box)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference"
+
+MODULES = ["tensor", "nn/functional", "nn/layer", "fft.py", "signal.py", "geometric", "autograd",
+           "audio/functional"]
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "python", "paddle")), reason="reference tree not present")
+def test_reference_doc_examples_pass_rate(tmp_path):
+    out = tmp_path / "res.json"
+    env = dict(os.environ, PADDLE_AMD_FORCE_CPU="1", OMP_NUM_THREADS="4")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "ref_doctests.py"), "--ref", REF, "--modules",
+                        *MODULES, "--json", str(out)], env=env, capture_output=True, timeout=1500, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    res = json.loads(out.read_text())
+    print(r.stdout.decode().strip().splitlines()[-1])
+    assert res["deterministic"] > 1000
+    bad = [f"{f['status']} {f['where']}: {f['source'][:80]}" for f in res["failures"]]
+    assert res["pass_rate"] >= 0.97, "\n".join(bad[:40])
