@@ -236,59 +236,14 @@ def sparse_attention(query, key, value, sparse_csr_offset, sparse_csr_columns, k
     return _wrap(p @ v)
 
 
-def _flashmask(startend, Sq, Sk, causal, device):
-    """Boolean keep-mask [B, H|1, Sq, Sk] from startend_row_indices [B, H|1, Sk, n] (n = 1, 2 or 4)."""
-    se = startend.to(torch.int64)
-    rows = torch.arange(Sq, device=device).view(1, 1, Sq, 1)
-    n = se.shape[-1]
-    lts = se[..., 0].unsqueeze(2)
-    if causal:
-        lte = se[..., 1].unsqueeze(2) if n >= 2 else torch.full_like(lts, Sq)
-        masked = (rows >= lts) & (rows < lte)
-        keep = ~masked & (rows >= torch.arange(Sk, device=device).view(1, 1, 1, Sk) - (Sk - Sq))
-    else:
-        if n == 2:
-            lte = torch.full_like(lts, Sq)
-            ute = se[..., 1].unsqueeze(2)
-            uts = torch.zeros_like(ute)
-        else:
-            lte, uts, ute = (se[..., i].unsqueeze(2) for i in (1, 2, 3))
-        masked = ((rows >= lts) & (rows < lte)) | ((rows >= uts) & (rows < ute))
-        keep = ~masked
-    return keep
+def flashmask_attention(*args, **kwargs):
+    """Reference: python/paddle/nn/functional/flash_attention.py:1306; in-kernel row bounds (see
+    nn/functional/flash_attention.py)."""
+    from .flash_attention import flashmask_attention as _fm
+    return _fm(*args, **kwargs)
 
 
-def flashmask_attention(query, key, value, startend_row_indices=None, *, dropout=0.0, causal=False,
-                        window_size=None, return_softmax_lse=False, return_seed_offset=False,
-                        fixed_seed_offset=None, rng_name="", training=True, name=None):
-    """FlashMask: per key-column row intervals masked out. q/k/v [B, S, H, D]."""
-    q, k, v = T(query), T(key), T(value)
-    Sq, Sk = q.shape[1], k.shape[1]
-    if startend_row_indices is None and window_size is None:
-        return _wrap(_ops.flash_attention(q, k, v, causal=causal, dropout=dropout, training=training))
-    keep = torch.ones(1, 1, Sq, Sk, dtype=torch.bool, device=q.device)
-    if startend_row_indices is not None:
-        keep = _flashmask(T(startend_row_indices), Sq, Sk, causal, q.device)
-    elif causal:
-        keep = torch.ones(Sq, Sk, dtype=torch.bool, device=q.device).tril(Sk - Sq).view(1, 1, Sq, Sk)
-    if window_size is not None:
-        wl, wr = (window_size, window_size) if isinstance(window_size, int) else window_size
-        r = torch.arange(Sq, device=q.device).view(Sq, 1) + (Sk - Sq)
-        c = torch.arange(Sk, device=q.device).view(1, Sk)
-        keep = keep & ((c >= r - wl) & (c <= r + wr)).view(1, 1, Sq, Sk)
-    o = _ops.flash_attention(q, k, v, causal=False, mask=keep, dropout=dropout, training=training)
-    return _wrap(o)
-
-
-def flash_attn_varlen_qkvpacked(qkv, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k, scale, dropout=0.0,
-                                causal=False, return_softmax=False, fixed_seed_offset=None, rng_name="",
-                                varlen_padded=True, training=True, name=None):
-    """Packed varlen attention: qkv [total, G + 2, Hk, D] (G query heads per kv head group)."""
-    t = T(qkv)
-    g = t.shape[1] - 2
-    # query head h = kv_head * G + g, the grouping the GQA kernel assumes (h // G -> kv head)
-    q = t[:, :g].permute(0, 2, 1, 3).reshape(t.shape[0], g * t.shape[2], t.shape[3])
-    k, v = t[:, g], t[:, g + 1]
-    from .flash_attention import flash_attn_unpadded
-    return flash_attn_unpadded(_wrap(q), _wrap(k), _wrap(v), cu_seqlens_q, cu_seqlens_k, max_seqlen_q,
-                               max_seqlen_k, scale, dropout, causal, return_softmax, training=training)
+def flash_attn_varlen_qkvpacked(*args, **kwargs):
+    """Reference: python/paddle/nn/functional/flash_attention.py:961 (one varlen launch)."""
+    from .flash_attention import flash_attn_varlen_qkvpacked as _f
+    return _f(*args, **kwargs)

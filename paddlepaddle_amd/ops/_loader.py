@@ -101,6 +101,11 @@ def _declare(L):
         "pa_flash_attn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _f32, _i32, _vp],
         "pa_flash_attn_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                               _i32, _i32, _i32, _i32, _i32, _i32, _f32, _i32, _vp],
+        "pa_flash_attn_fwd_ex": [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _f32, _i32, _vp,
+                                 _vp],
+        "pa_flash_attn_bwd_ex": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                 _i32, _i32, _i32, _i32, _i32, _i32, _f32, _i32, _i64, _vp, _vp],
+        "pa_fa_fm_stats": [_vp, _i32, _i32, _i32, _i32, _i32, _i64, _i64, _i32, _vp, _vp],
         "pa_paged_decode_attn": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
                                  _i64, _i64, _f32, _vp],
         # gemm epilogue companions

@@ -21,7 +21,7 @@ def _run(B, Sq, Sk, H, Hk, D, causal, dt=torch.bfloat16, spike=False, seed=0):
         q[:, Sq - 1] *= 4
     q.requires_grad_(True), k.requires_grad_(True), v.requires_grad_(True)
     o = ops.flash_attention(q, k, v, causal=causal)
-    assert L._LIB is not None and L.has("pa_flash_attn_fwd")
+    assert L._LIB is not None and L.has("pa_flash_attn_fwd_ex")
     qr, kr, vr = (t.detach().float().requires_grad_(True) for t in (q, k, v))
     orf = attention_reference(qr, kr, vr, causal=causal)
     err = (o.float() - orf).abs().max().item()
@@ -33,7 +33,8 @@ def _run(B, Sq, Sk, H, Hk, D, causal, dt=torch.bfloat16, spike=False, seed=0):
         scale = b.abs().max().item() + 1e-6
         e = (a.float() - b).abs().max().item() / scale
         assert e < 2.5e-2, f"{name} rel err {e}"
-    assert L.calls("pa_flash_attn_fwd") > 0 and L.calls("pa_flash_attn_bwd") > 0
+    assert L.calls("pa_flash_attn_fwd_ex") > 0 and L.calls("pa_flash_attn_bwd_ex") > 0
+    assert L.calls("attn_aten_fallback") == 0
 
 
 @pytest.mark.parametrize("causal", [False, True])
@@ -77,11 +78,11 @@ def test_fa_qkvpacked_matches_unpacked():
 
 
 def test_fa_lse_matches_logsumexp():
-    from paddlepaddle_amd.ops.attention import _fa_fwd
+    from paddlepaddle_amd.ops.attention import attention
     torch.manual_seed(2)
     B, S, H, D = 1, 200, 2, 128
     q, k, v = (torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16) for _ in range(3))
-    o, lse = _fa_fwd(q, k, v, True, 1 / math.sqrt(D))
+    o, lse = attention(q, k, v, causal=True, return_lse=True)
     s = torch.einsum("bqhd,bkhd->bhqk", q.float(), k.float()) / math.sqrt(D)
     s = s.masked_fill(~torch.ones(S, S, dtype=torch.bool, device="cuda").tril(), float("-inf"))
     ref = torch.logsumexp(s, -1)
