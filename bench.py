@@ -352,6 +352,10 @@ def main():
                           "per_gpu_batch": args.resnet_batch},
         }
         print(json.dumps(line), flush=True)
+    dump = os.environ.get("PADDLE_AMD_TUNING_DUMP")
+    if dump and int(os.environ.get("RANK", "0")) == 0:  # refresh paddlepaddle_amd/ops/tuning/<arch>.json
+        from paddlepaddle_amd.ops import gemm as _G
+        _G.dump_tuning_table(dump)
     if dist_on:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()

@@ -96,7 +96,7 @@ def conv1x1_nhwc(x, w, b, stride, fallback):
                 y = fn(xx, ww)
                 y.backward(torch.ones_like(y))
         return run
-    if key not in G._CHOICE and not G._capturing() and L.flag("FLAGS_gemm_backend", "auto") == "auto":
+    if not G.known(key) and not G._capturing() and L.flag("FLAGS_gemm_backend", "auto") == "auto":
         G.choose(key, {"hip": _fb_bench(lambda xx, ww: _Conv1x1.apply(xx, ww, b, stride)),
                        "blas": _fb_bench(lambda xx, ww: fallback(xx, ww))})
     ch = G.choose(key, {"hip": hip, "blas": lambda: None})
@@ -243,7 +243,7 @@ def conv_implicit_nhwc(x, w, b, stride, pad, dil, fallback):
                 if y.requires_grad:
                     y.backward(torch.ones_like(y))
         return go
-    if key not in G._CHOICE and not G._capturing() and L.flag("FLAGS_gemm_backend", "auto") == "auto":
+    if not G.known(key) and not G._capturing() and L.flag("FLAGS_gemm_backend", "auto") == "auto":
         G.choose(key, {"hip": bench(run), "blas": bench(fallback)})
     if G.choose(key, {"hip": None, "blas": None}) == "hip":
         return run(x, w)

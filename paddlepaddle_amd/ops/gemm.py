@@ -9,6 +9,9 @@ into an existing output (fp32 or bf16) into the GEMM epilogue.
 """
 from __future__ import annotations
 
+import json
+import os
+
 import torch
 
 from . import _loader as L
@@ -122,7 +125,94 @@ def _pick_bn(M, N, b_kmajor, cus=256):
 # on scratch outputs and keeps the faster one — our own TunableOp. Inside a hipGraph capture no
 # timing happens (hipBLASLt is used until the key has been tuned eagerly).
 # FLAGS_gemm_backend = "auto" (default) | "hip" | "blas" forces a side.
+#
+# Decisions persist: paddlepaddle_amd/ops/tuning/<arch>.json (committed, measured on MI355X) is read first,
+# so every process makes the same choice for a known shape without timing it (and a captured graph uses the
+# tuned kernel); shapes it does not hold are timed once and appended to the per-user overlay
+# $PADDLE_AMD_TUNING_FILE (default ~/.cache/paddlepaddle_amd/tuning_<arch>.json), read on later starts.
 _CHOICE = {}
+_TABLE_LOADED = False
+_TUNING_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning")
+
+
+def _arch():
+    try:
+        return torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName.split(":")[0]
+    except Exception:  # pragma: no cover
+        return "unknown"
+
+
+def _canon(key):
+    """Decision keys as JSON-stable tuples (dtypes and other objects by their str; nested tuples flattened
+    to lists and back)."""
+    def c(v):
+        if isinstance(v, (bool, int, float, str)) or v is None:
+            return v
+        if isinstance(v, (tuple, list)):
+            return tuple(c(x) for x in v)
+        return str(v)
+    return tuple(c(v) for v in key)
+
+
+def _key_str(key):
+    def j(v):
+        return [j(x) for x in v] if isinstance(v, tuple) else v
+    return json.dumps([j(v) for v in key])
+
+
+def known(key):
+    """Whether a decision for ``key`` exists (committed table, overlay or measured in this process)."""
+    load_tuning_table()
+    return _canon(key) in _CHOICE
+
+
+def _overlay_path():
+    return os.environ.get("PADDLE_AMD_TUNING_FILE") or os.path.join(
+        os.path.expanduser("~"), ".cache", "paddlepaddle_amd", f"tuning_{_arch()}.json")
+
+
+def _read_table(path):
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return {_canon(json.loads(k)): v for k, v in d.get("choices", {}).items()}
+    except (OSError, ValueError):
+        return {}
+
+
+def load_tuning_table():
+    """Merge the committed table and the overlay into the in-process decisions (once per process)."""
+    global _TABLE_LOADED
+    if _TABLE_LOADED:
+        return
+    _TABLE_LOADED = True
+    for path in (os.path.join(_TUNING_DIR, f"{_arch()}.json"), _overlay_path()):
+        for k, v in _read_table(path).items():
+            _CHOICE.setdefault(k, v)
+
+
+def _persist(key, choice):
+    path = _overlay_path()
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        cur = {}
+        if os.path.exists(path):
+            with open(path) as f:
+                cur = json.load(f).get("choices", {})
+        cur[_key_str(key)] = choice
+        tmp = f"{path}.{os.getpid()}.tmp"
+        with open(tmp, "w") as f:
+            json.dump({"arch": _arch(), "choices": cur}, f, indent=0, sort_keys=True)
+        os.replace(tmp, path)
+    except OSError:  # read-only home: the decision still holds for this process
+        pass
+
+
+def dump_tuning_table(path):
+    """Write every decision of this process (committed-table format)."""
+    with open(path, "w") as f:
+        json.dump({"arch": _arch(), "choices": {_key_str(k): v for k, v in sorted(_CHOICE.items(), key=str)}}, f,
+                  indent=0, sort_keys=True)
 
 
 def _capturing():
@@ -151,8 +241,10 @@ def choose(key, candidates, cold=False):
     mode = L.flag("FLAGS_gemm_backend", "auto")
     if mode in candidates:
         return mode
+    load_tuning_table()
+    key = _canon(key)
     ch = _CHOICE.get(key)
-    if ch is not None:
+    if ch is not None and ch in candidates:
         return ch
     if _capturing():
         return "blas"
@@ -172,6 +264,7 @@ def choose(key, candidates, cold=False):
             times[n].append(s.elapsed_time(e))
     ch = min(times, key=lambda n: min(times[n]))
     _CHOICE[key] = ch
+    _persist(key, ch)
     return ch
 
 

@@ -90,6 +90,25 @@ def test_semi_auto_parallel_and_dist_checkpoint(tmp_path):
         ref.append(float(loss))
     for _, out in res:
         np.testing.assert_allclose(out["losses"], ref, rtol=1e-5, atol=1e-6)
+    # the checkpoint is in the reference layout and reshards onto a single process
+    ck = os.environ["CKPT_DIR"]
+    assert sorted(os.listdir(ck)) == ["0.metadata", "0_0.distcp", "1_0.distcp"]
+    with open(os.path.join(ck, "0.metadata"), "rb") as f:
+        assert b"paddle.distributed.checkpoint.metadata" in f.read()
+    md = paddle.load(os.path.join(ck, "0.metadata"))
+    assert [m.global_offset for m in md.state_dict_metadata["t"]] == [(0, 0), (2, 0)]
+    assert md.state_dict_metadata["t"][0].dtype == "float32"
+    part0 = paddle.load(os.path.join(ck, "0_0.distcp"), return_numpy=True)
+    part1 = paddle.load(os.path.join(ck, "1_0.distcp"), return_numpy=True)
+    np.testing.assert_array_equal(part0["t"], a[:2])
+    np.testing.assert_array_equal(part1["t"], a[2:])
+    whole = paddle.zeros([4, 6])
+    paddle.distributed.load_state_dict({"t": whole}, ck)
+    np.testing.assert_array_equal(whole.numpy(), a)
+    w = part0["w"] if "w" in part0 else part1["w"]  # replicated: stored once
+    assert ("w" in part0) != ("w" in part1)
+    np.testing.assert_allclose(w, res[0][1]["w"], rtol=1e-6)
+    for _, out in res:
         np.testing.assert_allclose(out["w"], net[0].weight.numpy(), rtol=1e-5, atol=1e-6)
 
 
