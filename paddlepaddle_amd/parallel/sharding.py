@@ -20,6 +20,12 @@ MI355X-native design (one process per GPU, flat buffers, no per-parameter collec
   RCCL's stream while the current unit computes. With 288 GB HBM per GPU, units are whole
   transformer blocks (a 13B block is 630 MB in bf16) — few, large collectives that keep the xGMI
   rings in their bandwidth-bound regime.
+* ``offload=True`` (reference group_sharded_stage3.py:98-127 keeps fp32 master weights and the optimizer
+  update on the CPU): here the optimizer state of the local shards (fp32 master weights, moments) lives in
+  pinned host memory between steps and is streamed through the GPU one unit at a time — H2D of unit i+1 on
+  a copy stream overlaps the fused AdamW update of unit i, whose state goes back D2H behind it — so HBM
+  holds the state of at most two units (instead of 12 bytes per local parameter) and the update still runs
+  on the MFMA-free, bandwidth-bound HIP kernel rather than on host cores.
 """
 from __future__ import annotations
 
@@ -151,8 +157,10 @@ class GroupShardedEngine:
     """Implements stage 1/2/3 over a model + inner optimizer."""
 
     def __init__(self, model, optimizer, stage, group=None, decay_fn=None, mp_group=None, dp_group=None,
-                 keep_params=None, pp_group=None):
+                 keep_params=None, pp_group=None, offload=False):
         self.model = model
+        self.offload = bool(offload)
+        self._copy_stream = None
         self.stage = stage
         self.group = group
         self.pg = C._pg(group)
@@ -453,7 +461,10 @@ class GroupShardedEngine:
                     dp_work.append(dist.all_reduce(g, group=self.dp_group.process_group, async_op=True))
         for w in dp_work:
             w.wait()
-        self.inner_opt.step()
+        if self.offload:
+            self._offload_step()
+        else:
+            self.inner_opt.step()
         if self.world == 1:
             return  # shard aliases the full buffer: nothing to publish
         for u in self.units:
@@ -463,6 +474,95 @@ class GroupShardedEngine:
                 continue
             for f in u.flats:
                 dist.all_gather_into_tensor(f.gbuf, f.shard._t.detach().to(f.full.dtype), group=self.pg)
+
+    # ------------------------------------------------------------------ offload
+    def _state_slots(self, p):
+        """(dict, key) of every optimizer-state tensor of shard ``p`` (accumulators + master weight)."""
+        opt = self.inner_opt
+        out = [(d, id(p)) for d in opt._accumulators.values() if id(p) in d]
+        if id(p) in opt._master_weights:
+            out.append((opt._master_weights, id(p)))
+        return out
+
+    @staticmethod
+    def _host_copy(t):
+        return torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+
+    def _swap_in(self, shards, dev):
+        """Start the H2D copies of ``shards``' host state on the copy stream; returns the ready event."""
+        if dev.type != "cuda":  # CPU tensors: the state already lives in host memory
+            return None
+        cs = self._copy_stream
+        cs.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(cs):
+            for p in shards:
+                for d, k in self._state_slots(p):
+                    h = d[k]
+                    if h.device.type == "cpu":
+                        g = torch.empty(h.shape, dtype=h.dtype, device=dev)
+                        g.copy_(h, non_blocking=True)
+                        g._pa_host = h
+                        d[k] = g
+        ev = torch.cuda.Event()
+        ev.record(cs)
+        return ev
+
+    def _swap_out(self, shards, dev):
+        """Queue the D2H copies of the updated state behind the update, then point the optimizer at the host
+        tensors; the device buffers go back to the allocator once the copy stream has read them."""
+        if dev.type != "cuda":
+            return
+        cs = self._copy_stream
+        cs.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(cs):
+            for p in shards:
+                for d, k in self._state_slots(p):
+                    g = d[k]
+                    if g.device.type == "cpu":
+                        continue
+                    h = getattr(g, "_pa_host", None)
+                    if h is None:
+                        h = self._host_copy(g)
+                    h.copy_(g, non_blocking=True)
+                    g.record_stream(cs)
+                    d[k] = h
+
+    @torch.no_grad()
+    def _offload_step(self):
+        """Optimizer.step (optimizer.py:189) unit by unit with the state streamed from pinned host memory."""
+        from ..ops.linear import bump_weight_epoch
+        opt = self.inner_opt
+        bump_weight_epoch()
+        opt._step_count += 1
+        opt._apply_clip()
+        group = opt._param_groups[0]
+        chunks = [[f.shard for f in u.flats if f.shard._t.grad is not None] for u in self.units]
+        chunks = [c for c in chunks if c]
+        if not chunks:
+            return
+        dev = chunks[0][0]._t.device
+        if dev.type == "cuda" and self._copy_stream is None:
+            self._copy_stream = torch.cuda.Stream(dev)
+        ev = self._swap_in(chunks[0], dev)
+        for i, ps in enumerate(chunks):
+            nxt = self._swap_in(chunks[i + 1], dev) if i + 1 < len(chunks) else None
+            if ev is not None:
+                torch.cuda.current_stream(dev).wait_event(ev)
+            opt._update_group(group, ps)
+            self._swap_out(ps, dev)
+            ev = nxt
+        if dev.type == "cuda":
+            torch.cuda.current_stream(dev).wait_stream(self._copy_stream)
+
+    def offloaded_bytes(self):
+        """Bytes of optimizer state currently held in host memory."""
+        tot = 0
+        for u in self.units:
+            for f in u.flats:
+                for d, k in self._state_slots(f.shard):
+                    if d[k].device.type == "cpu":
+                        tot += d[k].numel() * d[k].element_size()
+        return tot
 
     def clear_grad(self, set_to_zero=True):
         for u in self.units:
@@ -578,9 +678,8 @@ def group_sharded_parallel(model, optimizer, level, scaler=None, group=None, off
         mp_group = hcg.get_model_parallel_group()
         if group is None and hcg.get_sharding_parallel_world_size() > 1:
             group = hcg.get_sharding_parallel_group()
-    if offload:
-        raise NotImplementedError("group_sharded_parallel(offload=True) is not supported yet")
-    eng = GroupShardedEngine(model, optimizer, stage, group, mp_group=mp_group, dp_group=dp_group)
+    eng = GroupShardedEngine(model, optimizer, stage, group, mp_group=mp_group, dp_group=dp_group,
+                             offload=offload)
     return GroupShardedModel(eng), GroupShardedOptimizer(eng), scaler
 
 

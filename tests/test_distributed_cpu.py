@@ -87,8 +87,11 @@ def _dp_worker(rank, world, port, mode, q):
         model = paddle.DataParallel(model)
     else:
         from paddlepaddle_amd.distributed.sharding import group_sharded_parallel
-        model, opt, _ = group_sharded_parallel(model, opt, level=mode)
+        level, _, off = mode.partition("+")
+        model, opt, _ = group_sharded_parallel(model, opt, level=level, offload=off == "offload")
     losses = _train(paddle, model, crit, opt, paddle.Tensor(local))
+    if mode.endswith("+offload"):
+        assert model._engine.offloaded_bytes() > 0
     sd = {k: v.numpy() for k, v in model.state_dict().items()}
     q.put((rank, losses, sd))
     paddle.distributed.barrier()
@@ -154,7 +157,7 @@ def _reference():
     return losses, {k: v.numpy() for k, v in model.state_dict().items()}
 
 
-@pytest.mark.parametrize("mode", ["dp", "os", "os_g", "p_g_os"])
+@pytest.mark.parametrize("mode", ["dp", "os", "os_g", "p_g_os", "p_g_os+offload"])
 def test_data_parallel_and_sharding_match_single_process(mode):
     ref_losses, ref_sd = _reference()
     res = _spawn(_dp_worker, mode)
