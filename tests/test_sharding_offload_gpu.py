@@ -38,6 +38,7 @@ def _run(offload):
         opt.clear_grad()
         losses.append(float(loss))
     torch.cuda.synchronize()
+    torch.empty(1, device="cuda")  # lets the allocator retire blocks freed behind the copy stream
     mem = torch.cuda.memory_allocated()
     eng = model._engine
     return losses, mem, eng.offloaded_bytes(), (model, opt)
