@@ -1,3 +1,3 @@
 """paddle.incubate.distributed.models.moe (re-export of parallel/moe.py)."""
-from ....parallel.moe import (MoELayer, BaseGate, NaiveGate, GShardGate, SwitchGate,  # noqa: F401
+from ....parallel.moe import (MoELayer, BaseGate, NaiveGate, GShardGate, SwitchGate, GroupedExperts,  # noqa: F401
                               ClipGradForMOEByGlobalNorm)

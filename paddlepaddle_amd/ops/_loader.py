@@ -130,6 +130,10 @@ def _declare(L):
         # pooling
         "pa_maxpool_nhwc_fwd": [_vp, _vp, _vp] + [_i32] * 10 + [_vp],
         "pa_maxpool_nhwc_bwd": [_vp, _vp, _vp] + [_i32] * 10 + [_vp],
+        # MoE
+        "pa_grouped_gemm": [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _i64, _i64, _i64, _i32,
+                            _vp],
+        "pa_moe_route": [_vp, _i32, _i32, _vp, _vp, _vp, _vp],
         "pa_version": [],
     }
     for name, args in sigs.items():

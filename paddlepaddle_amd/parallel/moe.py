@@ -7,9 +7,14 @@ MoEGather PyLayers, prepare_forward), gate/{naive_gate,gshard_gate,switch_gate}.
 Dispatch on MI355X: tokens are sorted by destination expert once (stable argsort on the device),
 per-rank counts are exchanged with a tiny all-to-all, then ONE variable-split all-to-all moves the
 tokens (each rank pair has its own xGMI link on an 8-GPU node, so an 8-way EP all-to-all is a single
-hop per pair). Local experts run on contiguous slices (grouped GEMMs), the reverse all-to-all brings
+hop per pair). Local experts run on contiguous slices, the reverse all-to-all brings
 results home, and the weighted combine is one index_add. Backward is the mirror image (the
 all-to-all autograd node swaps the split vectors).
+
+Experts given as ``GroupedExperts`` (E same-shape FFNs with stacked weights) run as ONE grouped GEMM per
+projection over all experts (csrc/kernels/grouped_gemm.hip via ops.moe), with routing offsets computed on the
+device: without expert parallelism that layer never synchronises with the host and can be captured in a
+hipGraph. ``fused_moe`` takes the same path.
 """
 from __future__ import annotations
 
@@ -148,6 +153,55 @@ class SwitchGate(NaiveGate):
         return _wrap(val), _wrap(idx)
 
 
+# ------------------------------------------------------------------------------------- experts
+class GroupedExperts(nn.Layer):
+    """``num_experts`` FFN experts (fc1 [d, h] -> activation -> fc2 [h, d]) with stacked weights
+    ``w1`` [E, d, h], ``w2`` [E, h, d] (+ biases [E, h], [E, d]). ``activation``: "gelu", "relu", "silu" or
+    "swiglu" (then w1 is [E, d, 2h] and the two halves are the value / gate inputs)."""
+
+    def __init__(self, num_experts, d_model, d_hidden, activation="gelu", bias=True, weight_attr=None):
+        super().__init__()
+        self.num_experts, self.d_model, self.d_hidden = num_experts, d_model, d_hidden
+        self.activation = activation
+        h1 = 2 * d_hidden if activation == "swiglu" else d_hidden
+        init = I.XavierUniform() if weight_attr is None else None
+        self.w1 = self.create_parameter([num_experts, d_model, h1], attr=weight_attr, default_initializer=init)
+        self.w2 = self.create_parameter([num_experts, d_hidden, d_model], attr=weight_attr,
+                                        default_initializer=init)
+        self.b1 = self.create_parameter([num_experts, h1], is_bias=True) if bias else None
+        self.b2 = self.create_parameter([num_experts, d_model], is_bias=True) if bias else None
+
+    def __len__(self):
+        return self.num_experts
+
+    def forward_sorted(self, xs, offs):
+        """xs [n, d] rows sorted by expert (offs [E + 1]) -> [n, d]; rows past offs[E] come out 0."""
+        from ..ops import moe as M
+        t = lambda p: None if p is None else p._t
+        h = M.grouped_linear(xs, self.w1._t, offs, t(self.b1))
+        if self.activation == "swiglu":
+            from .. import ops as _ops
+            a, g = h.chunk(2, -1)
+            h = _ops.swiglu(a.contiguous(), g.contiguous())
+        elif self.activation == "gelu":
+            h = TF.gelu(h)
+        elif self.activation == "relu":
+            h = TF.relu(h)
+        elif self.activation == "silu":
+            h = TF.silu(h)
+        return M.grouped_linear(h, self.w2._t, offs, t(self.b2))
+
+    def forward(self, x, expert_index):
+        """Dense helper: run every row of ``x`` through expert ``expert_index[row]``."""
+        from ..ops import moe as M
+        xt = x._t if isinstance(x, Tensor) else x
+        ei = expert_index._t if isinstance(expert_index, Tensor) else expert_index
+        offs, perm = M.route(ei, self.num_experts)
+        y = self.forward_sorted(xt[perm], offs)
+        out = torch.zeros_like(y).index_copy(0, perm, y)
+        return _wrap(out)
+
+
 # ------------------------------------------------------------------------------------- layer
 class MoELayer(nn.Layer):
     """Experts ``experts`` are this rank's local experts; global expert e lives on rank
@@ -179,7 +233,25 @@ class MoELayer(nn.Layer):
         for p in self.experts.parameters():
             p.is_distributed = self.world_size > 1  # expert params differ per rank (not DP-replicated)
 
+    def _grouped_local(self, x, val, idx):
+        """Experts on this rank only, as grouped GEMMs with device-side routing (no host sync)."""
+        from ..ops import moe as M
+        N, K = idx.shape
+        E = self.num_expert
+        offs, perm = M.route(idx.reshape(-1), E)
+        tok = perm // K
+        n = perm.numel()
+        valid = torch.arange(n, device=x.device, dtype=torch.int32) < offs[E]
+        wts = torch.where(valid, val.reshape(-1)[perm], torch.zeros((), dtype=val.dtype, device=val.device))
+        y = self.experts.forward_sorted(x[tok], offs)
+        out = torch.zeros_like(x, dtype=y.dtype)
+        return out.index_add(0, tok, y * wts[:, None].to(y.dtype))
+
     def _run_experts(self, x, counts):
+        if isinstance(self.experts, GroupedExperts):
+            offs = torch.zeros(len(counts) + 1, dtype=torch.int32)
+            offs[1:] = torch.cumsum(torch.tensor(counts, dtype=torch.int64), 0).to(torch.int32)
+            return self.experts.forward_sorted(x, offs.to(x.device))
         outs, off = [], 0
         for i, c in enumerate(counts):
             if c:
@@ -197,6 +269,8 @@ class MoELayer(nn.Layer):
         x = inp._t.reshape(-1, self.d_model)
         val, idx = self.gate(_wrap(x))
         val, idx = val._t, idx._t
+        if self.world_size == 1 and isinstance(self.experts, GroupedExperts):
+            return _wrap(self._grouped_local(x, val, idx).reshape(shape))
         N, K = idx.shape
         E = self.num_expert * self.world_size
         flat_e = idx.reshape(-1)
@@ -262,7 +336,8 @@ class ClipGradForMOEByGlobalNorm(nn.ClipGradByGlobalNorm):
 def fused_moe(x, gate_weight, ffn1_weight, ffn2_weight, ffn1_bias=None, ffn1_scale=None, ffn2_bias=None,
               ffn2_scale=None, quant_method="None", moe_topk=2, norm_topk_prob=True):
     """All experts local: route with the gate *logits* ``gate_weight`` [.., E], SwiGLU FFN per expert
-    (ffn1 [E, d, 2f] -> swiglu -> ffn2 [E, f, d]); experts run as grouped GEMMs over sorted tokens."""
+    (ffn1 [E, d, 2f] -> swiglu -> ffn2 [E, f, d]); routing and both projections run on the device as grouped
+    GEMMs over the expert-sorted tokens (no host sync)."""
     from .. import ops as _ops
     xt = x._t
     d = xt.shape[-1]
@@ -272,25 +347,17 @@ def fused_moe(x, gate_weight, ffn1_weight, ffn2_weight, ffn1_bias=None, ffn1_sca
     val, idx = probs.topk(moe_topk, -1)
     if norm_topk_prob:
         val = val / val.sum(-1, keepdim=True)
+    from ..ops import moe as M
     N, K = idx.shape
-    fe = idx.reshape(-1)
-    tok = torch.arange(N, device=xf.device).repeat_interleave(K)
-    order = torch.argsort(fe, stable=True)
-    fe, tok, wts = fe[order], tok[order], val.reshape(-1)[order]
-    counts = torch.bincount(fe, minlength=ffn1_weight.shape[0]).tolist()
-    w1, w2 = ffn1_weight._t, ffn2_weight._t
-    b1 = ffn1_bias._t if ffn1_bias is not None else None
-    b2 = ffn2_bias._t if ffn2_bias is not None else None
-    xs = xf[tok]
-    outs, off = [], 0
-    for e, c in enumerate(counts):
-        if c == 0:
-            continue
-        h = _ops.fused_linear(xs[off:off + c], w1[e], None if b1 is None else b1[e].reshape(-1))
-        a, bgate = h.chunk(2, -1)
-        h = _ops.swiglu(a, bgate)
-        outs.append(_ops.fused_linear(h, w2[e], None if b2 is None else b2[e].reshape(-1)))
-        off += c
-    y = torch.cat(outs, 0)
+    E = ffn1_weight.shape[0]
+    offs, perm = M.route(idx.reshape(-1), E)
+    tok = perm // K
+    wts = val.reshape(-1)[perm]
+    b1 = ffn1_bias._t.reshape(E, -1) if ffn1_bias is not None else None
+    b2 = ffn2_bias._t.reshape(E, -1) if ffn2_bias is not None else None
+    h = M.grouped_linear(xf[tok], ffn1_weight._t, offs, b1)
+    a, bgate = h.chunk(2, -1)
+    h = _ops.swiglu(a.contiguous(), bgate.contiguous())
+    y = M.grouped_linear(h, ffn2_weight._t, offs, b2)
     out = torch.zeros_like(xf).index_add(0, tok, (y * wts[:, None].to(y.dtype)).to(xf.dtype))
     return _wrap(out.reshape(xt.shape))

@@ -22,6 +22,10 @@ class _Net(paddle.nn.Layer):
 
 
 def _run(offload):
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
     paddle.seed(7)
     net = _Net()
     opt = paddle.optimizer.AdamW(1e-3, parameters=net.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0))
@@ -39,7 +43,7 @@ def _run(offload):
         losses.append(float(loss))
     torch.cuda.synchronize()
     torch.empty(1, device="cuda")  # lets the allocator retire blocks freed behind the copy stream
-    mem = torch.cuda.memory_allocated()
+    mem = torch.cuda.memory_allocated() - base  # what this run keeps resident between steps
     eng = model._engine
     return losses, mem, eng.offloaded_bytes(), (model, opt)
 
