@@ -178,15 +178,29 @@ class _Fleet:
             self.init()
             hcg = self._hcg
         mode = hcg.get_parallel_mode()
+        if mode == ParallelMode.SEGMENT_PARALLEL:
+            if hcg.get_sharding_parallel_world_size() > 1:
+                raise NotImplementedError("segment parallel combined with sharding is not supported")
+            from ...parallel.segment_parallel import SegmentParallel
+            return SegmentParallel(model, hcg, self._strategy)
         if hcg.get_sharding_parallel_world_size() > 1 and mode != ParallelMode.PIPELINE_PARALLEL:
             # sharding (x mp) (x dp): the sharding engine built by distributed_optimizer partitions the
             # parameters / grads / optimizer state over hcg's sharding group
             self._sharded_model = ShardingHybridModel(model, hcg, self._strategy)
             return self._sharded_model
         if mode == ParallelMode.PIPELINE_PARALLEL:
-            from ...parallel.pipeline import PipelineParallel, PipelineParallelWithInterleave
+            from ...parallel.pipeline import (PipelineParallel, PipelineParallelWithInterleave,
+                                              PipelineParallelWithInterleaveFthenB)
             if getattr(model, "get_num_virtual_stages", lambda: 1)() > 1:
-                return PipelineParallelWithInterleave(model, hcg, self._strategy)
+                # reference fleet/model.py:160-178: interleaved 1F1B when accumulate_steps >= 2 * pp,
+                # all-forward-then-all-backward when pp <= accumulate_steps < 2 * pp
+                acc = int((self._strategy.pipeline_configs or {}).get("accumulate_steps", 1))
+                pp = hcg.get_pipe_parallel_world_size()
+                if acc >= 2 * pp:
+                    return PipelineParallelWithInterleave(model, hcg, self._strategy)
+                if pp <= acc:
+                    return PipelineParallelWithInterleaveFthenB(model, hcg, self._strategy)
+                raise ValueError(f"The accumulate_steps({acc}) should be greater than or equal to pp_degree({pp})")
             return PipelineParallel(model, hcg, self._strategy)
         if mode == ParallelMode.TENSOR_PARALLEL:
             return TensorParallel(model, hcg, self._strategy)

@@ -70,6 +70,15 @@ class CommunicateTopology:
             out.append(grp)
         return out
 
+    def get_fused_ranks(self, fused_axes):
+        """Rank groups that vary only along the axes in ``fused_axes`` (reference create_fuse_group)."""
+        idx = [self._parallel_names.index(a) for a in fused_axes]
+        groups = {}
+        for c, r in self._coord2rank.items():
+            key = tuple(v for i, v in enumerate(c) if i not in idx)
+            groups.setdefault(key, []).append(r)
+        return [sorted(g) for _, g in sorted(groups.items())]
+
     def get_rank_from_stage(self, global_rank, **kwargs):
         coord = self.get_coord(global_rank)._asdict()
         coord.update(kwargs)
@@ -89,6 +98,9 @@ class HybridCommunicateGroup:
         self._groups = {}
         for axis in ("data", "pipe", "sharding", "sep", "model"):
             self._groups[axis] = self._build(axis)
+        self._fused = {}
+        if self._sep_degree > 1:
+            self._fused[("data", "sep")] = self._build_fused(("data", "sep"))
         self.stage_id = self._topo.get_coord(self.global_rank).pipe
         # check group for global grad-norm (all ranks that hold distinct param shards)
         self._check_group = None
@@ -105,15 +117,24 @@ class HybridCommunicateGroup:
                 mine = g if g is not None else C.Group(ranks.index(self.global_rank), -1, ranks, None)
         return mine
 
+    def _build_fused(self, axes):
+        mine = None
+        for ranks in self._topo.get_fused_ranks(axes):
+            g = C.new_group(ranks) if (C.is_initialized() and len(ranks) > 1) else None
+            if self.global_rank in ranks:
+                mine = g if g is not None else C.Group(ranks.index(self.global_rank), -1, ranks, None)
+        return mine
+
     def get_parallel_mode(self):
+        # reference order: pp -> mp -> sep -> sharding -> dp
         if self._pp_degree > 1:
             return ParallelMode.PIPELINE_PARALLEL
         if self._mp_degree > 1:
             return ParallelMode.TENSOR_PARALLEL
-        if self._sharding_degree > 1:
-            return ParallelMode.SHARDING_PARALLEL
         if self._sep_degree > 1:
             return ParallelMode.SEGMENT_PARALLEL
+        if self._sharding_degree > 1:
+            return ParallelMode.SHARDING_PARALLEL
         return ParallelMode.DATA_PARALLEL
 
     def topology(self):
@@ -186,6 +207,15 @@ class HybridCommunicateGroup:
 
     def get_sep_parallel_group(self):
         return self._groups["sep"]
+
+    def get_sep_parallel_group_src_rank(self):
+        return self._groups["sep"].ranks[0]
+
+    def get_dp_sep_parallel_group(self):
+        """data x sep fused group (gradients of sep-parallel training are reduced over it)."""
+        if self._sep_degree <= 1:
+            return self._groups["data"]
+        return self._fused[("data", "sep")]
 
     def get_check_parallel_group(self, sharding=False):
         return None

@@ -42,6 +42,7 @@ class LlamaConfig:
     tie_word_embeddings: bool = False
     use_recompute: bool = False
     tensor_parallel_degree: int = 1
+    sep_parallel_degree: int = 1  # segment parallelism: each rank of hcg's sep group holds S / sep tokens
     pad_token_id: int = 0
     bos_token_id: int = 1
     eos_token_id: int = 2
@@ -154,6 +155,8 @@ class LlamaAttention(nn.Layer):
             return self._decode_step(x, cache, pos)
         q, k, v = self._qkv(x)
         B, S = q.shape[0], q.shape[1]
+        if cache is None and self.cfg.sep_parallel_degree > 1:
+            return self._forward_sep(q, k, v, B, S)
         cos, sin = self.rope.tables(pos + S, q.device)
         q = _ops.apply_rotary(q, cos[pos:pos + S], sin[pos:pos + S])
         k = _ops.apply_rotary(k, cos[pos:pos + S], sin[pos:pos + S])
@@ -168,6 +171,20 @@ class LlamaAttention(nn.Layer):
         else:
             causal = True
         o = _ops.flash_attention(q, k, v, causal=causal)
+        return self.o_proj(_wrap(o.reshape(B, S, self.H * self.D)))
+
+    def _forward_sep(self, q, k, v, B, S):
+        """Segment-parallel training step: this rank holds tokens [r * S, (r + 1) * S) of every sequence;
+        RoPE uses the global positions and attention runs over the full sequence after a head / sequence
+        all-to-all (parallel/segment_parallel.py)."""
+        from ..distributed.fleet.topology import _get_hcg
+        from ..parallel.segment_parallel import segment_attention
+        g = _get_hcg().get_sep_parallel_group()
+        off = g.rank * S
+        cos, sin = self.rope.tables(off + S, q.device)
+        q = _ops.apply_rotary(q, cos[off:off + S], sin[off:off + S])
+        k = _ops.apply_rotary(k, cos[off:off + S], sin[off:off + S])
+        o = segment_attention(q, k, v, g, causal=True)
         return self.o_proj(_wrap(o.reshape(B, S, self.H * self.D)))
 
     def _decode_step(self, x, cache, pos_t):

@@ -411,3 +411,42 @@ class PipelineParallelWithInterleave(PipelineParallel):
         if self.stage_id == self.num_stages - 1 and compute_loss:
             return _wrap(torch.stack([l._t.float().mean() for l in losses]).mean())
         return [l._t for l in losses]
+
+
+class PipelineParallelWithInterleaveFthenB(PipelineParallelWithInterleave):
+    """Virtual pipeline that runs every forward micro-step first, then every backward (reference
+    pipeline_parallel.py:2261 PipelineParallelWithInterleaveFthenB, chosen by fleet when
+    pp <= accumulate_steps < 2 * pp). Micro-step k runs chunk (k // accumulate_steps) on micro-batch
+    k % accumulate_steps; backward walks the chunks in reverse. Messages are keyed by (chunk, micro-batch),
+    so the all-forward order needs no extra synchronisation."""
+
+    def __init__(self, layers, hcg, strategy):
+        PipelineParallel.__init__(self, layers, hcg, strategy)
+        self.V = layers.get_num_virtual_stages()
+        if self.V < 2:
+            raise ValueError("PipelineParallelWithInterleaveFthenB needs num_virtual_pipeline_stages >= 2")
+        S = self.num_stages
+        self.prev_rank = self.group.ranks[(self.stage_id - 1) % S]
+        self.next_rank = self.group.ranks[(self.stage_id + 1) % S]
+        if self.accumulate_steps < S:
+            raise ValueError(f"accumulate_steps ({self.accumulate_steps}) must be >= pp degree ({S})")
+
+    def _chunk_of(self, k, forward):
+        v = (k // self.accumulate_steps) % self.V
+        return v if forward else self.V - 1 - v
+
+    def _mb_of(self, k):
+        return k % self.accumulate_steps
+
+    def forward_backward_pipeline(self, data, scaler=None):
+        inputs, labels = (data if isinstance(data, (list, tuple)) and len(data) == 2 else (data, None))
+        n = self.accumulate_steps
+        mb_in = self._split(inputs) if self.stage_id == 0 else [None] * n
+        mb_lb = self._split(labels) if (self.stage_id == self.num_stages - 1 and labels is not None) else [None] * n
+        store, losses = {}, []
+        for k in range(n * self.V):
+            self._vforward(k, mb_in, mb_lb, store, losses)
+        for k in range(n * self.V):
+            self._vbackward(k, store)
+        self.is_last = self.stage_id == self.num_stages - 1
+        return self._finish(losses)

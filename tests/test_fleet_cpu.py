@@ -6,6 +6,7 @@ import os
 import sys
 
 import numpy as np
+import pytest
 import torch
 
 from test_distributed_cpu import ROOT, _data, _setup, _spawn
@@ -274,12 +275,13 @@ def _vpp_descs(paddle):
             LayerDesc(nn.Linear, 32, 32), LayerDesc(nn.Tanh), LayerDesc(nn.Linear, 32, 8), LayerDesc(nn.Tanh)]
 
 
-def _vpp_worker(rank, world, port, q):
+def _vpp_worker(rank, world, port, acc, q):
     paddle = _setup(rank, world, port)
-    from paddlepaddle_amd.parallel.pipeline import PipelineLayer, PipelineParallelWithInterleave
+    from paddlepaddle_amd.parallel.pipeline import (PipelineLayer, PipelineParallelWithInterleave,
+                                                    PipelineParallelWithInterleaveFthenB)
     paddle.seed(11)
     full = [d.build_layer() for d in _vpp_descs(paddle)]
-    fleet = _fleet_init(paddle, acc=4, pp_degree=2)
+    fleet = _fleet_init(paddle, acc=acc, pp_degree=2)
     pl = PipelineLayer(_vpp_descs(paddle), num_stages=2, loss_fn=_mse, num_virtual_pipeline_stages=2)
     # chunks: segments of 2 layers; stage s holds segments s and 2 + s
     idx = {}
@@ -293,7 +295,8 @@ def _vpp_worker(rank, world, port, q):
                 v._t.copy_(fv._t)
     opt = paddle.optimizer.SGD(0.1, parameters=pl.parameters())
     model = fleet.distributed_model(pl)
-    assert isinstance(model, PipelineParallelWithInterleave)
+    # fleet picks the schedule like the reference: interleaved 1F1B for acc >= 2 pp, FThenB for pp <= acc < 2 pp
+    assert type(model) is (PipelineParallelWithInterleave if acc >= 4 else PipelineParallelWithInterleaveFthenB)
     x, y = _pp_data()
     losses = [float(model.train_batch([paddle.Tensor(x), paddle.Tensor(y)], opt)) for _ in range(2)]
     params = {f"{i}.{k}": v.numpy() for i, f in idx.items() for k, v in f.state_dict().items()}
@@ -301,7 +304,8 @@ def _vpp_worker(rank, world, port, q):
     paddle.distributed.barrier()
 
 
-def test_pipeline_interleaved_matches_single_process():
+@pytest.mark.parametrize("acc", [4, 2])
+def test_pipeline_interleaved_matches_single_process(acc):
     sys.path.insert(0, ROOT)
     os.environ["PADDLE_AMD_FORCE_CPU"] = "1"
     import paddlepaddle_amd as paddle
@@ -323,7 +327,7 @@ def test_pipeline_interleaved_matches_single_process():
         opt.clear_grad()
         ref.append(float(loss))
     ref_params = {f"{i}.{k}": v.numpy() for i, l in enumerate(layers) for k, v in l.state_dict().items()}
-    res = _spawn(_vpp_worker)
+    res = _spawn(_vpp_worker, acc)
     (_, l0, p0, _), (_, l1, p1, _) = res
     np.testing.assert_allclose(l0, ref, rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(l1, ref, rtol=1e-5, atol=1e-6)
@@ -446,3 +450,57 @@ def test_sharding_stage3_x_tensor_parallel_gpt_four_ranks():
 
 def test_sharding_stage2_x_data_parallel_gpt_four_ranks():
     _check_hybrid(_spawn(_hybrid_sharding_worker, 1, 2, world=4), 1)
+
+
+# ----------------------------------------------------------------------------- segment parallel (sep)
+def _sep_worker(rank, world, port, q):
+    paddle = _setup(rank, world, port)
+    from paddlepaddle_amd.models.llama import LlamaConfig, LlamaForCausalLM, LlamaPretrainingCriterion
+    from paddlepaddle_amd.parallel.segment_parallel import SegmentParallel, split_sequence
+    fleet = _fleet_init(paddle, sep_degree=2)
+    hcg = fleet.get_hybrid_communicate_group()
+    paddle.seed(4)
+    cfg = LlamaConfig.tiny(sep_parallel_degree=2)
+    model, crit = LlamaForCausalLM(cfg), LlamaPretrainingCriterion(cfg)
+    opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    model = fleet.distributed_model(model)
+    assert isinstance(model, SegmentParallel)
+    opt = fleet.distributed_optimizer(opt)
+    g = hcg.get_sep_parallel_group()
+    ids = _data(cfg)
+    x = split_sequence(paddle.Tensor(ids[:, :-1]), g)
+    y = split_sequence(paddle.Tensor(ids[:, 1:]), g)
+    losses = []
+    for _ in range(3):
+        # segment losses are summed over the sep group (reference: sep gradients are not scaled)
+        loss = crit(model(x), y) * 0.5
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        t = loss._t.detach().clone()
+        paddle.distributed.all_reduce(paddle.Tensor(t), group=g)
+        losses.append(float(t))
+    q.put((rank, losses))
+    paddle.distributed.barrier()
+
+
+def test_llama_segment_parallel_matches_single_process():
+    sys.path.insert(0, ROOT)
+    os.environ["PADDLE_AMD_FORCE_CPU"] = "1"
+    import paddlepaddle_amd as paddle
+    from paddlepaddle_amd.models.llama import LlamaConfig, LlamaForCausalLM, LlamaPretrainingCriterion
+    paddle.seed(4)
+    cfg = LlamaConfig.tiny()
+    model, crit = LlamaForCausalLM(cfg), LlamaPretrainingCriterion(cfg)
+    opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    ref = _train(paddle, model, crit, opt, _data(cfg))
+    res = _spawn(_sep_worker)
+    for _, l in res:
+        np.testing.assert_allclose(l, ref, rtol=1e-4, atol=1e-5)
+
+
+def test_segment_all_to_all_roundtrip_single_process():
+    """seq_to_head / head_to_seq are inverse layouts (checked with a fake 1-rank group: identity)."""
+    from paddlepaddle_amd.parallel.segment_parallel import head_to_seq, seq_to_head
+    x = torch.randn(2, 8, 4, 16)
+    assert torch.equal(head_to_seq(seq_to_head(x, None), None), x)
