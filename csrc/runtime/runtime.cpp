@@ -71,9 +71,12 @@ std::vector<std::vector<int64_t>> plan_buckets(const std::vector<int64_t>& sizes
   return out;
 }
 
-// Kahn topological order (stable: smallest ready id first, i.e. program order when possible)
-// plus a last-use table: last[v] = position in `order` after which node v's output is dead.
-py::tuple schedule(int64_t n, const std::vector<std::pair<int64_t, int64_t>>& edges, const std::vector<int64_t>& keep) {
+// Kahn topological order (stable: among ready nodes the lowest priority class first, then the smallest id,
+// i.e. program order when possible; the executor gives collectives class 0 so they are issued as soon as
+// their inputs exist and overlap the independent compute) plus a last-use table: last[v] = position in
+// `order` after which node v's output is dead.
+py::tuple schedule(int64_t n, const std::vector<std::pair<int64_t, int64_t>>& edges, const std::vector<int64_t>& keep,
+                   const std::vector<int64_t>& prio) {
   std::vector<std::vector<int64_t>> succ(n);
   std::vector<int64_t> indeg(n, 0);
   for (auto& e : edges) {
@@ -81,17 +84,19 @@ py::tuple schedule(int64_t n, const std::vector<std::pair<int64_t, int64_t>>& ed
     succ[e.first].push_back(e.second);
     indeg[e.second]++;
   }
-  std::priority_queue<int64_t, std::vector<int64_t>, std::greater<int64_t>> ready;
+  auto cls = [&](int64_t v) -> int64_t { return static_cast<int64_t>(prio.size()) == n ? prio[v] : 0; };
+  using Item = std::pair<int64_t, int64_t>;  // (class, id)
+  std::priority_queue<Item, std::vector<Item>, std::greater<Item>> ready;
   for (int64_t i = 0; i < n; ++i)
-    if (indeg[i] == 0) ready.push(i);
+    if (indeg[i] == 0) ready.push({cls(i), i});
   std::vector<int64_t> order;
   order.reserve(n);
   while (!ready.empty()) {
-    int64_t v = ready.top();
+    int64_t v = ready.top().second;
     ready.pop();
     order.push_back(v);
     for (int64_t w : succ[v])
-      if (--indeg[w] == 0) ready.push(w);
+      if (--indeg[w] == 0) ready.push({cls(w), w});
   }
   if (static_cast<int64_t>(order.size()) != n) throw std::runtime_error("schedule: graph has a cycle");
   std::vector<int64_t> pos(n);
@@ -168,7 +173,8 @@ PYBIND11_MODULE(_C_runtime, m) {
   register_ps_table(m);
   m.def("stack_into", &stack_into, py::arg("arrays"), py::arg("out"));
   m.def("plan_buckets", &plan_buckets, py::arg("sizes"), py::arg("bucket_bytes"));
-  m.def("schedule", &schedule, py::arg("n"), py::arg("edges"), py::arg("keep"));
+  m.def("schedule", &schedule, py::arg("n"), py::arg("edges"), py::arg("keep"),
+        py::arg("prio") = std::vector<int64_t>());
   m.def("levels", &levels, py::arg("n"), py::arg("edges"));
   m.def("write_blobs", &write_blobs, py::arg("path"), py::arg("header"), py::arg("blobs"));
 }

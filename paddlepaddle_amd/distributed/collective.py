@@ -251,7 +251,27 @@ def _all_reduce_raw(t, op=ReduceOp.SUM, group=None, async_op=False):
     return dist.all_reduce(t, op=_TORCH_OP[op], group=_pg(group), async_op=async_op)
 
 
+def _static_comm(tensor, name, fn):
+    """Inside a static program being built: record the collective as one in-place "comm" node (replayed on
+    the executor's communication stream, static/program.py _Streams). Returns True when recorded."""
+    from ..framework.trace_hook import _active_program
+    prog = _active_program()
+    t = tensor._t if hasattr(tensor, "_t") else tensor
+    if prog is None or not prog._is_traced(t):
+        return False
+    from ..static.program import OpNode
+
+    def run(x):
+        fn(x)
+        return None
+    prog._append(OpNode(run, (prog._template(t),), {}, None, kind="comm", name="c:" + name))
+    return True
+
+
 def all_reduce(tensor, op=ReduceOp.SUM, group=None, sync_op=True, use_calc_stream=False):
+    if is_initialized() and get_world_size(group) > 1 and _static_comm(
+            tensor, "all_reduce", lambda x: dist.all_reduce(x, op=_TORCH_OP[op], group=_pg(group))):
+        return _ret(None, sync_op)
     if not is_initialized() or get_world_size(group) == 1:
         return _ret(None, sync_op)
     w = dist.all_reduce(tensor._t, op=_TORCH_OP[op], group=_pg(group), async_op=not sync_op)
@@ -295,6 +315,9 @@ def all_gather_object(object_list, obj, group=None):
 
 
 def broadcast(tensor, src, group=None, sync_op=True):
+    if is_initialized() and get_world_size(group) > 1 and _static_comm(
+            tensor, "broadcast", lambda x: dist.broadcast(x, src=src, group=_pg(group))):
+        return _ret(None, sync_op)
     if not is_initialized() or get_world_size(group) == 1:
         return _ret(None, sync_op)
     w = dist.broadcast(tensor._t, src=src, group=_pg(group), async_op=not sync_op)

@@ -7,11 +7,13 @@ sparse_embedding), static/nn/sequence_lod.py.
 
 Design: in dygraph (and under jit.to_static, which traces with concrete values) the predicates are
 concrete, so control flow is plain Python. Inside a static program the tensors are meta tensors
-(shape/dtype only, see static/program.py), so a branch cannot be chosen at build time: ``cond`` /
-``case`` / ``switch_case`` then record BOTH branches and select the result with ``where`` on the
-predicate — identical results for side-effect-free branches, the usual requirement of the reference's
-conditional_block as well. ``while_loop`` needs a data-dependent trip count and is only supported
-where the predicate is concrete.
+(shape/dtype only, see static/program.py): ``cond`` records each branch into its own sub-block and
+``while_loop`` records the condition and the body into two sub-blocks over loop-variable slots; the
+program gets ONE control-flow node (program.CFNode) whose replay evaluates the predicate on the device
+values and runs only the chosen block / iterates the body (reference: conditional_block and while ops
+executing sub-blocks, static/nn/control_flow.py:755,1620). ``case`` / ``switch_case`` nest ``cond``.
+Gradients flow through whatever the replay executed (autograd records the taken branch / every
+iteration).
 """
 from __future__ import annotations
 
@@ -39,13 +41,65 @@ def _map2(fn, a, b):
     return fn(a, b)
 
 
-def _select(pred, a, b):
-    def sel(x, y):
-        if isinstance(x, Tensor):
-            p = pred._t.reshape([])
-            return _wrap(torch.where(p, x._t, y._t if isinstance(y, Tensor) else torch.as_tensor(y)))
+def _prog():
+    from ..framework.trace_hook import _active_program
+    prog = _active_program()
+    if prog is None:
+        raise RuntimeError("static control flow outside of a program being built")
+    return prog
+
+
+def _tensors_of(x):
+    return x._t if isinstance(x, Tensor) else x
+
+
+def _leaves_to_t(x):
+    if isinstance(x, Tensor):
+        return x._t
+    if isinstance(x, (list, tuple)):
+        return type(x)(_leaves_to_t(v) for v in x)
+    if isinstance(x, dict):
+        return {k: _leaves_to_t(v) for k, v in x.items()}
+    return x
+
+
+def _out_like(a, b):
+    """Output structure of a cond: fresh meta values for tensor leaves (shapes / dtypes must agree)."""
+    def leaf(x, y):
+        if isinstance(x, Tensor) or isinstance(y, Tensor):
+            if not (isinstance(x, Tensor) and isinstance(y, Tensor)):
+                raise ValueError("cond branches must both return a Tensor at the same position")
+            if list(x.shape) != list(y.shape) or x._t.dtype != y._t.dtype:
+                raise ValueError(f"cond branches return different shapes / dtypes: {list(x.shape)} {x._t.dtype} vs "
+                                 f"{list(y.shape)} {y._t.dtype}")
+            with torch._C.DisableTorchFunction():
+                return _wrap(torch.empty(x._t.shape, dtype=x._t.dtype, device="meta"))
+        if x != y:
+            raise ValueError(f"cond branches return different non-tensor values {x!r} / {y!r}")
         return x
-    return _map2(sel, a, b)
+    return _map2(leaf, a, b)
+
+
+def _static_cond(pred, true_fn, false_fn):
+    from .program import CFNode, _SubBlock
+    from ..framework.trace_hook import _active_program
+    prog = _active_program()
+    if prog is None:  # meta tensors outside any program: shape inference only
+        t = true_fn() if true_fn is not None else None
+        f = false_fn() if false_fn is not None else None
+        return _out_like(t, f) if t is not None else None
+    with prog._sub_block() as tb:
+        t = true_fn() if true_fn is not None else None
+    with prog._sub_block() as fb:
+        f = false_fn() if false_fn is not None else None
+    if (t is None) != (f is None):
+        raise ValueError("cond: both branches must return values (or both None)")
+    res = [prog._template(_leaves_to_t(t)), prog._template(_leaves_to_t(f))]
+    out = _out_like(t, f) if t is not None else None
+    outs = prog._out_template(_leaves_to_t(out)) if out is not None else None
+    node = CFNode("cond", (prog._template(pred._t),), outs, [_SubBlock(tb), _SubBlock(fb)], res)
+    prog._append(node)
+    return out
 
 
 def cond(pred, true_fn=None, false_fn=None, name=None, return_names=None):
@@ -53,11 +107,7 @@ def cond(pred, true_fn=None, false_fn=None, name=None, return_names=None):
         p = bool(pred._t.reshape([]).item()) if isinstance(pred, Tensor) else bool(pred)
         fn = true_fn if p else false_fn
         return fn() if fn is not None else None
-    t = true_fn() if true_fn is not None else None
-    f = false_fn() if false_fn is not None else None
-    if t is None or f is None:
-        return None
-    return _select(pred, t, f)
+    return _static_cond(pred, true_fn, false_fn)
 
 
 def case(pred_fn_pairs, default=None, name=None):
@@ -88,24 +138,50 @@ def switch_case(branch_index, branch_fns, default=None, name=None):
             if k == i:
                 return fn()
         return default()
-    out = default()
+    out_fn = default
     for k, fn in reversed(items):
-        out = _select(_wrap(branch_index._t == k), fn(), out)
-    return out
+        out_fn = (lambda k_, f_, o_: (lambda: cond(_wrap(branch_index._t == k_), f_, o_)))(k, fn, out_fn)
+    return out_fn()
+
+
+def _static_while(cond_fn, body, loop_vars):
+    from .program import CFNode, _SubBlock
+    prog = _prog()
+    init = [v if isinstance(v, Tensor) else _wrap(torch.as_tensor(v)) for v in loop_vars]
+    ph = [_wrap(prog._new_like(v._t)) for v in init]
+    slots = [prog._slot_of[id(p._t)] for p in ph]
+    with prog._sub_block() as cb:
+        c = cond_fn(*ph)
+    with prog._sub_block() as bb:
+        out = body(*ph)
+    out = list(out) if isinstance(out, (list, tuple)) else [out]
+    if len(out) != len(ph):
+        raise ValueError(f"while_loop body returned {len(out)} values for {len(ph)} loop variables")
+    for o, p in zip(out, ph):
+        if list(o.shape) != list(p.shape):
+            raise ValueError(f"while_loop variable changes shape {list(p.shape)} -> {list(o.shape)} (loop "
+                             "variables must keep their shapes)")
+    res = [prog._template(_tensors_of(c)), prog._template([_tensors_of(o) for o in out])]
+    with torch._C.DisableTorchFunction():
+        metas = [torch.empty(p._t.shape, dtype=p._t.dtype, device="meta") for p in ph]
+    outs = prog._out_template(metas)
+    node = CFNode("while", prog._template([v._t for v in init]), outs, [_SubBlock(cb), _SubBlock(bb)], res, slots)
+    prog._append(node)
+    return [_wrap(m) for m in metas]
 
 
 def while_loop(cond, body, loop_vars, is_test=False, name=None):
     loop_vars = list(loop_vars)
+    first = cond(*loop_vars)
+    if _is_meta(first) or any(_is_meta(v) for v in loop_vars):
+        return _static_while(cond, body, loop_vars)
+    c = first
     while True:
-        c = cond(*loop_vars)
-        if _is_meta(c):
-            raise NotImplementedError(
-                "while_loop inside a static program needs a data-dependent trip count; build the loop in "
-                "dygraph or under paddle.jit.to_static (traced with concrete values)")
         if not bool(c._t.reshape([]).item() if isinstance(c, Tensor) else c):
             break
         out = body(*loop_vars)
         loop_vars = list(out) if isinstance(out, (list, tuple)) else [out]
+        c = cond(*loop_vars)
     return loop_vars
 
 

@@ -154,6 +154,7 @@ class Program:
         self._id = next(Program._ids)
         self._is_test = False
         self._dyn = False        # saved program with an affine dynamic dim
+        self._cur = self.nodes   # node list being recorded into (a control-flow sub-block while tracing one)
 
     # ------------------------------------------------------------ slots / values
     def _new_slot(self, meta):
@@ -254,9 +255,29 @@ class Program:
         return out
 
     def _append(self, node):
-        self.nodes.append(node)
+        self._cur.append(node)
         self._version += 1
         self._plans.clear()
+
+    @contextlib.contextmanager
+    def _sub_block(self):
+        """Record into a fresh node list (a control-flow sub-block) sharing this program's value slots."""
+        old = self._cur
+        blk = []
+        self._cur = blk
+        try:
+            yield blk
+        finally:
+            self._cur = old
+
+    def _new_like(self, meta):
+        """A fresh traced value with the shape / dtype of ``meta`` (control-flow outputs, loop variables)."""
+        with torch._C.DisableTorchFunction():
+            m = torch.empty(meta.shape, dtype=meta.dtype, device=_META)
+            if meta.requires_grad and m.is_floating_point():
+                m.requires_grad_(True)
+        self._new_slot(m)
+        return m
 
     # ------------------------------------------------------------ user API
     def global_block(self):
@@ -267,7 +288,7 @@ class Program:
 
     @property
     def num_blocks(self):
-        return 1
+        return 1 + sum(_count_blocks(n) for n in self.nodes)
 
     def current_block(self):
         return _Block(self)
@@ -285,6 +306,7 @@ class Program:
         p = Program.__new__(Program)
         p.__dict__.update(self.__dict__)
         p.nodes = list(self.nodes)
+        p._cur = p.nodes
         p._plans = {}
         p._id = next(Program._ids)
         if for_test:
@@ -315,7 +337,7 @@ class Program:
     # ------------------------------------------------------------ (de)serialization
     def to_dict(self, fetch_slots, const_names):
         enc = _Encoder(const_names)
-        nodes = [{"f": n.name, "a": enc(n.args), "k": enc(n.kwargs), "o": enc(n.outs)} for n in self.nodes]
+        nodes = [_encode_node(n, enc) for n in self.nodes]
         return {"format": "paddlepaddle_amd.program", "version": 1,
                 "n_slots": len(self._metas),
                 "slot_meta": [[list(m.shape), str(m.dtype).replace("torch.", "")] for m in self._metas],
@@ -331,7 +353,7 @@ class Program:
             p._new_slot(torch.empty(shape, dtype=getattr(torch, dt), device=_META))
         dec = _Decoder(p, consts_by_name)
         for nd in d["nodes"]:
-            p.nodes.append(OpNode(_resolve(nd["f"]), dec(nd["a"]), dec(nd["k"]), dec(nd["o"]), name=nd["f"]))
+            p.nodes.append(_decode_node(nd, dec))
         for f in d["feeds"]:
             p.feeds[f["name"]] = (f["slot"], tuple(f["shape"]), f["dtype"])
             p._names[f["name"]] = f["slot"]
@@ -450,14 +472,8 @@ def build_plan(program, fetch_slots, keep_slots=()):
     last uses (reference: new_executor dependency builder + GC)."""
     from ..utils import native
     nodes = program.nodes
-    reads = [set(_refs((n.args, n.kwargs), [])) for n in nodes]
-    writes = []
-    for n in nodes:
-        w = set(_refs(n.outs, []))
-        if n.name == "m:__setitem__" or (n.name.startswith("m:") and n.name.endswith("_")
-                                         and not n.name.endswith("__")):
-            w |= set(_refs(n.args[:1], []))  # in-place: the receiver is written
-        writes.append(w)
+    reads = [_node_reads(n) for n in nodes]
+    writes = [_node_writes(n) for n in nodes]
     # liveness pruning (backwards from the fetches)
     need = set(fetch_slots) | set(keep_slots)
     live = [False] * len(nodes)
@@ -485,7 +501,10 @@ def build_plan(program, fetch_slots, keep_slots=()):
             creator.setdefault(s, i)
             last_writer[s] = i
     keep_nodes = {pos_of[creator[s]] for s in set(fetch_slots) | set(keep_slots) if s in creator}
-    order, last = native.schedule(len(idx), sorted(edges), sorted(keep_nodes))
+    # collectives are issued as soon as their inputs exist (they run on the comm stream and overlap the
+    # compute that does not depend on them)
+    prio = [0 if nodes[i].kind == "comm" else 1 for i in idx]
+    order, last = native.schedule(len(idx), sorted(edges), sorted(keep_nodes), prio)
     pos = {v: p for p, v in enumerate(order)}
     free_after = {}
     feeds = {s for (s, _, _) in program.feeds.values()}
@@ -529,18 +548,205 @@ def _assign(tmpl, val, env):
             _assign(t, v, env)
 
 
+def _is_inplace(n):
+    return n.kind == "comm" or n.name == "m:__setitem__" or (
+        n.name.startswith("m:") and n.name.endswith("_") and not n.name.endswith("__"))
+
+
+def _node_reads(n):
+    if isinstance(n, CFNode):
+        return n.reads()
+    return set(_refs((n.args, n.kwargs), []))
+
+
+def _node_writes(n):
+    w = set(_refs(n.outs, []))
+    if _is_inplace(n):
+        w |= set(_refs(n.args[:1], []))  # in-place: the receiver is written
+    return w
+
+
+def _exec_node(n, env, consts, dev, sym_n):
+    if isinstance(n, CFNode):
+        n.execute(env, consts, dev, sym_n)
+        return
+    args = _materialize(n.args, env, consts, dev, sym_n)
+    kw = _materialize(n.kwargs, env, consts, dev, sym_n)
+    out = n.func(*args, **kw)
+    if n.outs is not None:
+        _assign(n.outs, out, env)
+
+
+class _Streams:
+    """Compute + communication HIP streams of one plan run. A collective waits for the compute issued
+    before it (its input is ready), runs on the comm stream and records an event; a later node reading
+    what the collective wrote waits for that event. Compute that does not depend on the collective keeps
+    running on the compute stream meanwhile."""
+
+    def __init__(self, dev):
+        self.comp = torch.cuda.current_stream(dev)
+        self.comm = _comm_stream(dev)
+        self.pending = {}  # slot -> event recorded on the comm stream after the collective that wrote it
+
+    def before(self, n, reads):
+        if n.kind == "comm":
+            self.comm.wait_stream(self.comp)
+            return self.comm
+        for s in reads:
+            ev = self.pending.pop(s, None)
+            if ev is not None:
+                self.comp.wait_event(ev)
+        return self.comp
+
+    def after(self, n, writes, env):
+        if n.kind != "comm":
+            return
+        ev = torch.cuda.Event()
+        ev.record(self.comm)
+        for s in writes:
+            self.pending[s] = ev
+            t = env.get(s)
+            if isinstance(t, torch.Tensor) and t.is_cuda:
+                t.record_stream(self.comm)
+
+    def finish(self):
+        if self.pending:
+            self.comp.wait_stream(self.comm)
+
+
+_COMM_STREAMS = {}
+
+
+def _comm_stream(dev):
+    s = _COMM_STREAMS.get(dev)
+    if s is None:
+        s = _COMM_STREAMS[dev] = torch.cuda.Stream(dev)
+    return s
+
+
 def run_plan(program, plan, env, dev, consts=None, sym_n=None):
     fa = plan.free_after
+    multi = dev is not None and getattr(dev, "type", None) == "cuda" and any(
+        plan.nodes[i].kind == "comm" for i in plan.order)
+    st = _Streams(dev) if multi else None
     for p, ni in enumerate(plan.order):
         n = plan.nodes[ni]
-        args = _materialize(n.args, env, consts, dev, sym_n)
-        kw = _materialize(n.kwargs, env, consts, dev, sym_n)
-        out = n.func(*args, **kw)
-        if n.outs is not None:
-            _assign(n.outs, out, env)
+        if st is None:
+            _exec_node(n, env, consts, dev, sym_n)
+        else:
+            stream = st.before(n, _node_reads(n))
+            with torch.cuda.stream(stream):
+                _exec_node(n, env, consts, dev, sym_n)
+            st.after(n, _node_writes(n), env)
         for s in fa.get(p, ()):
             env.pop(s, None)
+    if st is not None:
+        st.finish()
     return env
+
+
+# ---------------------------------------------------------------------------------- control flow
+class _SubBlock:
+    """Ops recorded for one branch / loop body: executed in recording order on the parent's value slots;
+    values created inside are dropped when the block finishes (reference: conditional_block /
+    while sub-blocks run by the interpreter)."""
+
+    def __init__(self, nodes):
+        self.nodes = nodes
+        self._inner = None
+
+    def inner(self):
+        """Values created in the block (not outer values it updates in place)."""
+        if self._inner is None:
+            w = set()
+            for n in self.nodes:
+                w |= set(_refs(n.outs, []))
+            self._inner = w
+        return self._inner
+
+    def free_reads(self):
+        r, made = set(), set()
+        for n in self.nodes:
+            r |= _node_reads(n) - made
+            made |= set(_refs(n.outs, []))
+        return r
+
+    def run(self, env, consts, dev, sym_n):
+        for n in self.nodes:
+            _exec_node(n, env, consts, dev, sym_n)
+
+    def drop(self, env, keep=()):
+        for sl in self.inner():
+            if sl not in keep:
+                env.pop(sl, None)
+
+
+class CFNode(OpNode):
+    """A control-flow op owning sub-blocks (kind "cond" or "while")."""
+    __slots__ = ("blocks", "res", "loop_slots")
+
+    def __init__(self, kind, args, outs, blocks, res, loop_slots=()):
+        super().__init__(None, args, {}, outs, kind=kind, name="cf:" + kind)
+        self.blocks = blocks          # [_SubBlock]
+        self.res = res                # per block: template of its result (cond: branch value; while: pred, body)
+        self.loop_slots = tuple(loop_slots)
+
+    def reads(self):
+        r = set(_refs(self.args, []))
+        for b, res in zip(self.blocks, self.res):
+            r |= b.free_reads() | (set(_refs(res, [])) - b.inner())
+        return r - set(self.loop_slots)
+
+    def execute(self, env, consts, dev, sym_n):
+        m = lambda t: _materialize(t, env, consts, dev, sym_n)  # noqa: E731
+        if self.kind == "cond":
+            pred = m(self.args[0])
+            take = bool(pred.reshape(()).item()) if isinstance(pred, torch.Tensor) else bool(pred)
+            i = 0 if take else 1
+            blk = self.blocks[i]
+            blk.run(env, consts, dev, sym_n)
+            val = m(self.res[i])
+            blk.drop(env)
+            _assign(self.outs, val, env)
+            return
+        # while: loop variables live in loop_slots; blocks = (cond block, body block)
+        cblk, bblk = self.blocks
+        for sl, v in zip(self.loop_slots, m(self.args)):
+            env[sl] = v
+        while True:
+            cblk.run(env, consts, dev, sym_n)
+            pred = m(self.res[0])
+            cblk.drop(env, keep=self.loop_slots)
+            if not (bool(pred.reshape(()).item()) if isinstance(pred, torch.Tensor) else bool(pred)):
+                break
+            bblk.run(env, consts, dev, sym_n)
+            new = m(self.res[1])
+            bblk.drop(env, keep=self.loop_slots)
+            for sl, v in zip(self.loop_slots, new):
+                env[sl] = v
+        _assign(self.outs, [env.pop(sl) for sl in self.loop_slots], env)
+
+
+def _count_blocks(n):
+    if not isinstance(n, CFNode):
+        return 0
+    return sum(1 + sum(_count_blocks(x) for x in b.nodes) for b in n.blocks)
+
+
+def _encode_node(n, enc):
+    if isinstance(n, CFNode):
+        return {"f": n.name, "a": enc(n.args), "o": enc(n.outs), "loop": list(n.loop_slots),
+                "blocks": [[_encode_node(x, enc) for x in b.nodes] for b in n.blocks],
+                "res": [enc(r) for r in n.res]}
+    return {"f": n.name, "a": enc(n.args), "k": enc(n.kwargs), "o": enc(n.outs)}
+
+
+def _decode_node(nd, dec):
+    if nd["f"].startswith("cf:"):
+        blocks = [_SubBlock([_decode_node(x, dec) for x in b]) for b in nd["blocks"]]
+        return CFNode(nd["f"][3:], dec(nd["a"]), dec(nd["o"]), blocks, [dec(r) for r in nd["res"]],
+                      nd.get("loop", ()))
+    return OpNode(_resolve(nd["f"]), dec(nd["a"]), dec(nd["k"]), dec(nd["o"]), name=nd["f"])
 
 
 def _grad_node_fn(n_targets, retain):

@@ -62,28 +62,32 @@ def plan_buckets(sizes_bytes, bucket_bytes):
     return buckets
 
 
-def schedule(n_nodes, edges, outputs_keep):
-    """Topological schedule of a DAG. edges: list of (src, dst). Returns (order, last_use) where
-    last_use[v] is the position in ``order`` after which value v can be freed (-1 = keep)."""
+def schedule(n_nodes, edges, outputs_keep, prio=None):
+    """Topological schedule of a DAG. edges: list of (src, dst). Among ready nodes the lowest ``prio`` class
+    goes first, then the smallest id. Returns (order, last_use) where last_use[v] is the position in
+    ``order`` after which value v can be freed (-1 = keep)."""
     m = module()
+    prio = list(prio) if prio is not None else []
     if m is not None:
-        return m.schedule(int(n_nodes), [(int(a), int(b)) for a, b in edges], list(int(k) for k in outputs_keep))
+        return m.schedule(int(n_nodes), [(int(a), int(b)) for a, b in edges], list(int(k) for k in outputs_keep),
+                          [int(x) for x in prio])
+    cls = (lambda v: prio[v]) if len(prio) == n_nodes else (lambda v: 0)
     indeg = [0] * n_nodes
     succ = [[] for _ in range(n_nodes)]
     for a, b in edges:
         succ[a].append(b)
         indeg[b] += 1
     import heapq
-    ready = [i for i in range(n_nodes) if indeg[i] == 0]
+    ready = [(cls(i), i) for i in range(n_nodes) if indeg[i] == 0]
     heapq.heapify(ready)
     order = []
     while ready:
-        v = heapq.heappop(ready)
+        _, v = heapq.heappop(ready)
         order.append(v)
         for w in succ[v]:
             indeg[w] -= 1
             if indeg[w] == 0:
-                heapq.heappush(ready, w)
+                heapq.heappush(ready, (cls(w), w))
     if len(order) != n_nodes:
         raise ValueError("graph has a cycle")
     pos = {v: i for i, v in enumerate(order)}
