@@ -68,6 +68,10 @@ def _check_placements(mesh, placements):
 def shard_tensor(data, mesh, placements, dtype=None, place=None, stop_gradient=None):
     """Every rank passes the same global value; each keeps its shard (reference semantics)."""
     _check_placements(mesh, placements)
+    if isinstance(data, Tensor) and not isinstance(data, Parameter):
+        rec = _traced_reshard(data._t, mesh, placements)
+        if rec is not None:
+            return rec
     if isinstance(data, Tensor):
         t = data._t
         sg = data.stop_gradient if stop_gradient is None else stop_gradient
@@ -96,11 +100,13 @@ def shard_tensor(data, mesh, placements, dtype=None, place=None, stop_gradient=N
     out._pa_mesh = mesh
     if isinstance(data, Parameter):
         data._t = out.detach().requires_grad_(not sg)
+        data._t._pa_mesh = mesh
         from ...framework.tensor import _PARAM_OF
         _PARAM_OF[id(data._t)] = data
         return data
     if not sg and out.is_floating_point():
         out = out.detach().requires_grad_(True)
+        out._pa_mesh = mesh
     return _wrap(out)
 
 
@@ -120,9 +126,29 @@ def dtensor_from_fn(fn, mesh, placements, *args, **kwargs):
     return shard_tensor(fn(*args, **kwargs), mesh, placements)
 
 
+def _traced_reshard(t, mesh, placements):
+    """Inside a program being traced (static auto-parallel): record the reshard as an annotation node."""
+    from ...framework.trace_hook import _active_program
+    prog = _active_program()
+    if prog is None or not prog._is_traced(t) or not hasattr(prog, "_pa_reshard"):
+        return None
+    from ...static.program import OpNode
+    from .static_engine import StaticEngine
+    with torch._C.DisableTorchFunction():
+        out = torch.empty(t.shape, dtype=t.dtype, device="meta").requires_grad_(t.requires_grad)
+    node = OpNode(lambda x: x, (prog._template(t),), {}, None, kind="reshard", name="ap:reshard")
+    node.outs = prog._out_template(out)
+    prog._append(node)
+    prog._pa_reshard[id(node)] = (mesh, [StaticEngine._pl_of(p) for p in placements])
+    return _wrap(out)
+
+
 def reshard(dist_tensor, mesh, placements):
     _check_placements(mesh, placements)
     t = dist_tensor._t
+    rec = _traced_reshard(t, mesh, placements)
+    if rec is not None:
+        return rec
     if not _is_dist(t):
         return shard_tensor(dist_tensor, mesh, placements)
     if mesh != dist_tensor.process_mesh:
@@ -322,10 +348,21 @@ class Strategy:
 
 
 class DistModel:
-    """Reference: DistModel — callable train/eval/predict step over a (semi-auto) distributed layer."""
+    """Reference: DistModel — callable train/eval/predict step over a (semi-auto) distributed layer.
+
+    Training with a loss and an optimizer runs through the static engine (static_engine.StaticEngine:
+    traced program, SPMD placement propagation, per-rank partition with explicit collectives, pipeline
+    schedule from ``strategy.pipeline``) whenever the layer holds distributed parameters; otherwise, and for
+    eval / predict, the layer runs eagerly on the distributed tensors."""
 
     def __init__(self, layer, loader, loss=None, optimizer=None, strategy=None, metrics=None, input_spec=None):
         self.network = layer
+        self._engine = None
+        strategy = strategy or Strategy()
+        if loss is not None and optimizer is not None and getattr(strategy, "full_graph", True) and any(
+                _is_dist(p._t) for p in layer.parameters()):
+            from .static_engine import StaticEngine
+            self._engine = StaticEngine(layer, loss, getattr(optimizer, "_inner_opt", optimizer), strategy)
         self._loader = loader
         self._loss = loss
         self._opt = optimizer
@@ -353,6 +390,8 @@ class DistModel:
             with no_grad():
                 return self.network(*args)
         inputs, labels = args[:-1], args[-1]
+        if self._engine is not None and self._mode == "train":
+            return self._engine.step(inputs, labels)
         if self._mode == "eval":
             from ...framework.grad_mode import no_grad
             with no_grad():

@@ -1,0 +1,950 @@
+"""Static semi-auto parallel engine: trace -> placement propagation -> per-rank partition -> pipeline run.
+
+Reference: python/paddle/distributed/auto_parallel/static/engine.py:99 (Engine: build the serial program,
+plan, partition, reshard, run with a pipeline schedule), static/completion.py (placement propagation),
+static/partitioner.py, static/reshard.py, paddle/phi/infermeta/spmd_rules/ (per-op SPMD rules),
+pipeline scheduler passes (1F1B / FThenB), api.py:2167 DistModel, :2776 to_static.
+
+How it works here:
+  1. Trace: the model + loss run ONCE on meta tensors with GLOBAL shapes (static/program.py tracer).
+     Every distributed parameter becomes a program input carrying its ProcessMesh + placements; every
+     ``dist.reshard`` on a traced value becomes an annotation node (the pipeline stage hand-offs of the
+     reference semi-auto LLaMA are exactly these).
+  2. Propagate: each value gets (mesh, placement per mesh dim) — Replicate, Shard(d) or Partial(sum|avg) —
+     from per-op SPMD rules (linear, reshape / view, element-wise with broadcasting, transpose, row-wise
+     ops such as norms / softmax / cross-entropy, embedding, reductions, attention, RoPE). An op without
+     a rule gets all its inputs replicated (always correct, never silent).
+  3. Partition: for this rank, keep the ops of its pipeline stage (the stage = the mesh of the op's
+     output), rewrite shape arguments to LOCAL shapes, and insert the collectives the placements need,
+     each an autograd function with the conjugate backward:
+        Partial -> Replicate   all-reduce        (backward: identity)
+        Shard   -> Replicate   all-gather        (backward: slice)
+        Replicate -> Shard     slice             (backward: all-gather)
+        Replicate input of a split computation   identity (backward: all-reduce)   e.g. column-parallel
+                                                 x, data-parallel weights (= the dp gradient all-reduce)
+     Values crossing stages become point-to-point transfers between ranks with the same coordinate in the
+     two stage meshes.
+  4. Run: micro-batches through a 1F1B (or FThenB) schedule, each stage replaying its local op list;
+     backward is autograd over what ran, seeded with the gradients received from the next stage. The
+     optimizer then steps on the local shards.
+
+One process per GPU; collectives are RCCL over xGMI groups, one group per mesh dim (all created up front).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ...framework.tensor import Parameter, Tensor, _wrap
+from ...static import program as P
+from .. import collective as C
+from .placement_type import from_torch_placements
+
+R = ("R",)
+
+
+def S(d):
+    return ("S", int(d))
+
+
+def PSUM():
+    return ("P", "sum")
+
+
+def _is_s(p):
+    return p[0] == "S"
+
+
+def _is_p(p):
+    return p[0] == "P"
+
+
+class _Info:
+    __slots__ = ("mesh", "pl", "shape")
+
+    def __init__(self, mesh, pl, shape):
+        self.mesh, self.pl, self.shape = mesh, tuple(pl), tuple(shape)
+
+    def __repr__(self):
+        return f"_Info({None if self.mesh is None else self.mesh.process_ids}, {self.pl}, {self.shape})"
+
+
+# ------------------------------------------------------------------------------------ collectives
+class _Groups:
+    """Process groups along every dim of every stage mesh (created collectively, same order everywhere)."""
+
+    def __init__(self, meshes):
+        self.g = {}
+        rank = C.get_rank()
+        for mi, m in enumerate(meshes):
+            arr = m.mesh
+            for d in range(arr.ndim):
+                moved = np.moveaxis(arr, d, -1).reshape(-1, arr.shape[d])
+                for row in moved:
+                    ranks = [int(x) for x in row]
+                    grp = dist.new_group(ranks) if len(ranks) > 1 else None
+                    if rank in ranks:
+                        self.g[(mi, d)] = (grp, ranks)
+
+    def get(self, mi, d):
+        return self.g.get((mi, d), (None, None))
+
+
+def _nranks(gr):
+    return 1 if gr[1] is None else len(gr[1])
+
+
+def _my(gr):
+    return 0 if gr[1] is None else gr[1].index(C.get_rank())
+
+
+class _AllReduce(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gr, avg):
+        ctx.scale = 1.0 / _nranks(gr) if avg else 1.0
+        y = x.clone()
+        if gr[0] is not None:
+            dist.all_reduce(y, group=gr[0])
+        if avg:
+            y.mul_(ctx.scale)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        return (g * ctx.scale if ctx.scale != 1.0 else g), None, None
+
+
+def _gather(x, gr, dim):
+    n = _nranks(gr)
+    if n == 1:
+        return x
+    parts = [torch.empty_like(x) for _ in range(n)]
+    dist.all_gather(parts, x.contiguous(), group=gr[0])
+    return torch.cat(parts, dim)
+
+
+class _AllGather(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gr, dim):
+        ctx.gr, ctx.dim = gr, dim
+        return _gather(x, gr, dim)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.chunk(_nranks(ctx.gr), ctx.dim)[_my(ctx.gr)].contiguous(), None, None
+
+
+class _Slice(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gr, dim):
+        ctx.gr, ctx.dim = gr, dim
+        return x.chunk(_nranks(gr), dim)[_my(gr)].contiguous()
+
+    @staticmethod
+    def backward(ctx, g):
+        return _gather(g, ctx.gr, ctx.dim), None, None
+
+
+class _CopyToParallel(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gr):
+        ctx.gr = gr
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.clone()
+        if ctx.gr[0] is not None:
+            dist.all_reduce(g, group=ctx.gr[0])
+        return g, None
+
+
+# ------------------------------------------------------------------------------------ rules
+_ELEMENTWISE = {
+    "add", "sub", "mul", "div", "true_divide", "neg", "exp", "log", "sqrt", "rsqrt", "tanh", "sigmoid", "silu",
+    "gelu", "relu", "pow", "abs", "square", "clamp", "where", "maximum", "minimum", "float", "half", "bfloat16",
+    "to", "type_as", "__add__", "__radd__", "__sub__", "__rsub__", "__mul__", "__rmul__", "__truediv__",
+    "__rtruediv__", "__neg__", "__pow__", "add_", "mul_", "swiglu", "dropout", "contiguous", "clone", "detach",
+    "masked_fill", "erf", "sin", "cos", "reciprocal", "sign", "__eq__", "__ne__", "__lt__", "__gt__", "__le__",
+    "__ge__", "logical_not", "cast", "astype", "bias_gelu", "gelu_tanh", "requires_grad_",
+}
+_ROWWISE = {"rms_norm", "layer_norm", "softmax", "log_softmax", "softmax_cross_entropy", "fused_softmax"}
+_RESHAPE = {"view", "reshape", "flatten", "unflatten"}
+_TRANSPOSE = {"transpose", "permute", "t"}
+_REDUCE = {"sum", "mean"}
+
+
+def _short(name):
+    return name.split(":")[-1]
+
+
+def _flat_tensor_refs(tmpl, acc):
+    if isinstance(tmpl, P._Ref):
+        acc.append(tmpl)
+    elif isinstance(tmpl, (list, tuple)):
+        for v in tmpl:
+            _flat_tensor_refs(v, acc)
+    elif isinstance(tmpl, dict):
+        for v in tmpl.values():
+            _flat_tensor_refs(v, acc)
+    return acc
+
+
+def _shape_args(args):
+    """The target shape of a view / reshape call (ints, possibly one -1)."""
+    rest = args[1:]
+    if len(rest) == 1 and isinstance(rest[0], (list, tuple)):
+        return list(rest[0])
+    return list(rest)
+
+
+def _resolve_shape(shape, numel):
+    shape = list(shape)
+    if -1 in shape:
+        known = int(np.prod([s for s in shape if s != -1])) or 1
+        shape[shape.index(-1)] = numel // known
+    return shape
+
+
+def _map_shard_through_reshape(in_shape, out_shape, d):
+    """Output dim that carries input dim ``d``'s sharding (contiguous chunks stay contiguous), or None."""
+    pre = int(np.prod(in_shape[:d])) if d > 0 else 1
+    acc = 1
+    for j, s in enumerate(out_shape):
+        if acc == pre:
+            # dim j starts where input dim d starts; the chunking of d maps onto j if j's extent divides evenly
+            tail_in = int(np.prod(in_shape[d:]))
+            tail_out = int(np.prod(out_shape[j:]))
+            if tail_in == tail_out and (s % in_shape[d] == 0 or in_shape[d] % s == 0 or s == in_shape[d]):
+                return j
+            if s >= in_shape[d] and s % in_shape[d] == 0:
+                return j
+            return j if s == in_shape[d] else None
+        acc *= s
+        if acc > pre:
+            return None
+    return None
+
+
+# ------------------------------------------------------------------------------------ engine
+class _LNode:
+    """A local op: ``fn(*materialized args, **kw)`` with outputs assigned to ``outs`` template."""
+    __slots__ = ("fn", "args", "kwargs", "outs", "name")
+
+    def __init__(self, fn, args, kwargs, outs, name):
+        self.fn, self.args, self.kwargs, self.outs, self.name = fn, args, kwargs, outs, name
+
+
+class StaticEngine:
+    def __init__(self, layer, loss_fn, optimizer, strategy):
+        self.layer, self.loss_fn, self.opt, self.strategy = layer, loss_fn, optimizer, strategy
+        pp = strategy.pipeline
+        self.acc = max(1, int(pp.accumulate_steps)) if pp.enable else 1
+        self.schedule = str(pp.schedule_mode).upper() if pp.enable else "1F1B"
+        self.built = False
+        self.rank = C.get_rank()
+        self._consts = {}
+
+    # ---------------------------------------------------------------- build
+    def _stage_meshes(self, params):
+        from .process_mesh import get_mesh
+        gm = get_mesh()
+        if gm is not None and "pp" in gm.dim_names:
+            return [gm.get_mesh_with_dim("pp", i) for i in range(gm.get_dim_size("pp"))]
+        meshes = []
+        for p in params:
+            m = getattr(p._t, "_pa_mesh", None)
+            if m is not None and m not in meshes:
+                meshes.append(m)
+        return meshes[:1] or [gm]
+
+    def build(self, inputs, labels):
+        params = [p for p in self.layer.parameters()]
+        self.params = params
+        self.meshes = self._stage_meshes(params)
+        self.stage_of_mesh = {m: i for i, m in enumerate(self.meshes)}
+        self.my_stage = next((i for i, m in enumerate(self.meshes) if self.rank in m), None)
+        self.groups = _Groups(self.meshes)
+        prog = P.Program()
+        self.prog = prog
+        self.info = {}
+        # feeds: micro-batch global shapes; batch dim sharded on a "dp" mesh dim
+        self.feed_slots = []
+        for i, t in enumerate(list(inputs) + [labels]):
+            full = t._t if isinstance(t, Tensor) else torch.as_tensor(np.asarray(t))
+            shp = [full.shape[0] // self.acc] + list(full.shape[1:])
+            ph = P.placeholder(prog, f"feed{i}", shp, str(full.dtype).replace("torch.", ""))
+            slot = prog._slot_of[id(ph._t)]
+            self.feed_slots.append(slot)
+            self.info[slot] = _Info(None, self._batch_pl(), shp)
+        # parameters: global meta stand-ins carrying their annotations
+        self.param_slots = {}
+        saved = {}
+        for p in params:
+            if id(p) in saved:
+                continue
+            t = p._t
+            mesh = getattr(t, "_pa_mesh", None)
+            if mesh is None and hasattr(t, "device_mesh"):
+                from .process_mesh import ProcessMesh
+                dm = t.device_mesh
+                mesh = ProcessMesh(dm.mesh.cpu().numpy(), list(dm.mesh_dim_names or []) or None)
+            pl = [self._pl_of(x) for x in from_torch_placements(t.placements)] if mesh is not None else None
+            with torch._C.DisableTorchFunction():
+                meta = torch.empty(tuple(t.shape), dtype=t.dtype, device="meta").requires_grad_(not p.stop_gradient)
+            slot = prog._new_slot(meta)
+            saved[id(p)] = t
+            self.param_slots[id(p)] = slot
+            if mesh is None:
+                mesh, pl = self.meshes[0], [R] * self.meshes[0].ndim
+            self.info[slot] = _Info(mesh, pl, tuple(t.shape))
+            p._t = meta
+        self.reshard_ann = {}
+        prog._pa_reshard = self.reshard_ann
+        try:
+            with P.trace_into(prog):
+                xs = [_wrap(prog._metas[s]) for s in self.feed_slots[:-1]]
+                out = self.layer(*xs)
+                loss = self.loss_fn(out, _wrap(prog._metas[self.feed_slots[-1]]))
+        finally:
+            for p in params:
+                if id(p) in saved:
+                    p._t = saved[id(p)]
+        self.loss_slot = prog._slot_of[id(loss._t)]
+        self._propagate_and_partition()
+        self._localize_params()
+        self.built = True
+
+    def _batch_pl(self):
+        m = self.meshes[0]
+        return [S(0) if n == "dp" and m.get_dim_size(n) > 1 else R for n in m.dim_names]
+
+    @staticmethod
+    def _pl_of(p):
+        if p.is_shard():
+            return S(p.dim)
+        if p.is_partial():
+            return PSUM()
+        return R
+
+    # ---------------------------------------------------------------- propagation + partition
+    def _propagate_and_partition(self):
+        prog = self.prog
+        nstage = len(self.meshes)
+        self.stage_nodes = [[] for _ in range(nstage)]
+        self.stage_inputs = [set() for _ in range(nstage)]     # slots received from earlier stages
+        self.sends = [dict() for _ in range(nstage)]           # slot -> set(dst stages)
+        self.slot_stage = {}                                   # slot -> producing stage
+        self.local_alias = [dict() for _ in range(nstage)]     # (slot, pl) -> converted local slot
+        self._next = len(prog._metas) + 1
+        for s in self.feed_slots:
+            self.slot_stage[s] = None  # available everywhere
+        for s in self.param_slots.values():
+            self.slot_stage[s] = self.stage_of_mesh.get(self.info[s].mesh, 0)
+        for n in prog.nodes:
+            if isinstance(n, P.CFNode):
+                raise NotImplementedError("control flow inside an auto-parallel program")
+            self._partition_node(n)
+
+    def _new(self):
+        self._next += 1
+        return self._next
+
+    def _stage_for(self, node, in_refs):
+        if node.kind == "reshard":
+            mesh, _ = self.reshard_ann[id(node)]
+            return self.stage_of_mesh.get(mesh, 0)
+        st = [self.slot_stage.get(r.i) for r in in_refs if self.slot_stage.get(r.i) is not None]
+        return max(st) if st else 0
+
+    def _avail(self, slot, stage):
+        """Make ``slot`` usable in ``stage`` (cross-stage: point-to-point transfer)."""
+        src = self.slot_stage.get(slot)
+        if src is None or src == stage:
+            return
+        self.sends[src].setdefault(slot, set()).add(stage)
+        self.stage_inputs[stage].add(slot)
+
+    def _convert(self, stage, slot, want):
+        """Local slot holding ``slot`` with placement ``want`` (per mesh dim) in ``stage``."""
+        have = self.info[slot].pl
+        if tuple(have) == tuple(want):
+            return slot
+        key = (slot, tuple(want))
+        al = self.local_alias[stage]
+        if key in al:
+            return al[key]
+        cur = slot
+        pl = list(have)
+        shape = self.info[slot].shape
+        for d in range(len(want)):
+            h, w = pl[d], want[d]
+            if h == w:
+                continue
+            gr = ("G", stage, d)
+            if _is_p(h):
+                out = self._new()
+                self._emit(stage, "allreduce", _AllReduce.apply, (P._Ref(cur), gr, h[1] == "avg"), out)
+                cur, pl[d] = out, R
+                h = R
+            if _is_s(h) and w == R:
+                out = self._new()
+                self._emit(stage, "allgather", _AllGather.apply, (P._Ref(cur), gr, h[1]), out)
+                cur, pl[d] = out, R
+            elif _is_s(h) and _is_s(w):
+                out = self._new()
+                self._emit(stage, "allgather", _AllGather.apply, (P._Ref(cur), gr, h[1]), out)
+                out2 = self._new()
+                self._emit(stage, "slice", _Slice.apply, (P._Ref(out), gr, w[1]), out2)
+                cur, pl[d] = out2, w
+            elif h == R and _is_s(w):
+                out = self._new()
+                self._emit(stage, "slice", _Slice.apply, (P._Ref(cur), gr, w[1]), out)
+                cur, pl[d] = out, w
+            elif _is_p(w):
+                raise NotImplementedError(f"conversion to a Partial placement ({h} -> {w})")
+        self.info[cur] = _Info(self.meshes[stage], pl, shape)
+        al[key] = cur
+        return cur
+
+    def _copy_to_parallel(self, stage, slot, dims):
+        key = (slot, ("ctp",) + tuple(dims))
+        al = self.local_alias[stage]
+        if key in al:
+            return al[key]
+        cur = slot
+        for d in dims:
+            out = self._new()
+            self._emit(stage, "copy_to_parallel", _CopyToParallel.apply, (P._Ref(cur), ("G", stage, d)), out)
+            cur = out
+        self.info[cur] = self.info[slot]
+        al[key] = cur
+        return cur
+
+    def _emit(self, stage, name, fn, args, out_slot):
+        self.stage_nodes[stage].append(_LNode(fn, args, {}, P._Ref(out_slot), name))
+        self.slot_stage[out_slot] = stage
+
+    def _partition_node(self, n):
+        prog = self.prog
+        refs = _flat_tensor_refs((n.args, n.kwargs), [])
+        stage = self._stage_for(n, refs)
+        for r in refs:
+            self._avail(r.i, stage)
+        mesh = self.meshes[stage]
+        nd = mesh.ndim
+        for r in refs:
+            inf = self.info.get(r.i)
+            if inf is None:
+                self.info[r.i] = _Info(mesh, [R] * nd, tuple(prog._metas[r.i].shape))
+            elif inf.mesh is None:
+                inf.mesh = mesh
+        out_refs = _flat_tensor_refs(n.outs, []) if n.outs is not None else []
+        name = _short(n.name)
+        if n.kind == "reshard":
+            _, want = self.reshard_ann[id(n)]
+            src = refs[0].i
+            loc = self._convert(stage, src, want)
+            for o in out_refs:
+                self._alias(stage, o.i, loc, want)
+            return
+        want, out_pl, ctp = self._rule(n, name, refs, nd)
+        # inputs: convert to the wanted placements, wrap replicated inputs of split computations
+        sub = {}
+        for r, w in zip(refs, want):
+            loc = self._convert(stage, r.i, w)
+            dims = [d for d in range(nd) if d in ctp.get(r.i, ())]
+            if dims and prog._metas[r.i].requires_grad:
+                loc = self._copy_to_parallel(stage, loc, dims)
+            sub[r.i] = loc
+        args = self._subst(n.args, sub)
+        kwargs = self._subst(n.kwargs, sub)
+        if name in _RESHAPE and refs:
+            args = self._local_reshape_args(n, refs[0].i, args, out_pl)
+        for o in out_refs:
+            m = prog._metas[o.i]
+            self.info[o.i] = _Info(mesh, out_pl, tuple(m.shape))
+            self.slot_stage[o.i] = stage
+        self.stage_nodes[stage].append(_LNode(n.func, args, kwargs, n.outs, n.name))
+        if n.outs is None:  # in-place op on its first argument
+            for r in refs[:1]:
+                self.slot_stage[r.i] = stage
+
+    def _alias(self, stage, out_slot, src_slot, pl):
+        self._emit(stage, "alias", lambda x: x, (P._Ref(src_slot),), out_slot)
+        self.info[out_slot] = _Info(self.meshes[stage], pl, self.info[src_slot].shape)
+
+    @staticmethod
+    def _subst(tmpl, sub):
+        if isinstance(tmpl, P._Ref):
+            return P._Ref(sub.get(tmpl.i, tmpl.i))
+        if isinstance(tmpl, list):
+            return [StaticEngine._subst(v, sub) for v in tmpl]
+        if isinstance(tmpl, tuple):
+            return tuple(StaticEngine._subst(v, sub) for v in tmpl)
+        if isinstance(tmpl, dict):
+            return {k: StaticEngine._subst(v, sub) for k, v in tmpl.items()}
+        return tmpl
+
+    # ---------------------------------------------------------------- SPMD rules
+    def _rule(self, n, name, refs, nd):
+        """-> (wanted input placements per ref, output placement, {slot: dims needing copy-to-parallel})."""
+        prog = self.prog
+        ins = [self.info[r.i] for r in refs]
+        out_refs = _flat_tensor_refs(n.outs, []) if n.outs is not None else []
+        out_rank = prog._metas[out_refs[0].i].dim() if out_refs else 0
+        rep = [R] * nd
+        if not refs:
+            return [], rep, {}
+        if name == "fused_linear" and len(refs) >= 2:
+            return self._rule_linear(refs, ins, nd)
+        if name == "embedding" and len(refs) >= 2:
+            return self._rule_embedding(refs, ins, nd)
+        want = [list(i.pl) for i in ins]
+        out = [R] * nd
+        ctp = {}
+        for d in range(nd):
+            pls = [i.pl[d] for i in ins]
+            if name in _ELEMENTWISE or name in ("apply_rotary", "flash_attention", "attention", "embedding"):
+                self._rule_elementwise(name, refs, ins, d, want, out, ctp, out_rank)
+            elif name in _ROWWISE:
+                x = ins[0]
+                p0 = pls[0]
+                if _is_s(p0) and p0[1] % len(x.shape) != len(x.shape) - 1:
+                    out[d] = S(p0[1] % len(x.shape))
+                    for k in range(1, len(refs)):  # weights / labels
+                        wd = ins[k]
+                        if len(wd.shape) == len(x.shape) - 1 and name == "softmax_cross_entropy":
+                            want[k][d] = S(p0[1] % len(x.shape))
+                        else:
+                            want[k][d] = R
+                            ctp.setdefault(refs[k].i, set()).add(d)
+                else:
+                    for k in range(len(refs)):
+                        want[k][d] = R
+            elif name in _RESHAPE:
+                p0 = pls[0]
+                x = ins[0]
+                if _is_s(p0):
+                    oshape = _resolve_shape(list(prog._metas[out_refs[0].i].shape), int(np.prod(x.shape)))
+                    j = _map_shard_through_reshape(list(x.shape), oshape, p0[1] % len(x.shape))
+                    if j is not None and oshape[j] % self.meshes[0].shape[d] == 0:
+                        out[d] = S(j)
+                    else:
+                        want[0][d] = R
+                elif _is_p(p0):
+                    out[d] = p0
+                for k in range(1, len(refs)):
+                    want[k][d] = R
+            elif name in _TRANSPOSE:
+                p0 = pls[0]
+                if _is_s(p0):
+                    out[d] = S(self._transpose_dim(n, p0[1] % len(ins[0].shape), len(ins[0].shape)))
+                elif _is_p(p0):
+                    out[d] = p0
+            elif name in _REDUCE:
+                p0 = pls[0]
+                dims = self._reduce_dims(n, len(ins[0].shape))
+                if _is_s(p0):
+                    sd = p0[1] % len(ins[0].shape)
+                    if sd in dims:
+                        out[d] = ("P", "avg" if name == "mean" else "sum")
+                    else:
+                        keep = self._keepdim(n)
+                        out[d] = S(sd if keep else sd - sum(1 for x in dims if x < sd))
+                elif _is_p(p0) and name == "sum":
+                    out[d] = p0
+                elif _is_p(p0):
+                    want[0][d] = R
+            else:
+                for k in range(len(refs)):
+                    want[k][d] = R
+        return [tuple(w) for w in want], out, ctp
+
+    def _rule_elementwise(self, name, refs, ins, d, want, out, ctp, out_rank):
+        pls = [i.pl[d] for i in ins]
+        if any(_is_p(p) for p in pls):
+            if name in ("add", "__add__", "__radd__", "sub", "__sub__") and all(_is_p(p) for p in pls):
+                out[d] = pls[0]
+                return
+            for k, p in enumerate(pls):
+                if _is_p(p):
+                    want[k][d] = R
+            pls = [want[k][d] for k in range(len(pls))]
+        shards = set()
+        for k, p in enumerate(pls):
+            if _is_s(p):
+                rank_k = len(ins[k].shape)
+                shards.add(out_rank - rank_k + (p[1] % rank_k))  # right-aligned output dim
+        if len(shards) > 1 or (name == "embedding" and any(_is_s(p) for p in pls[1:])):
+            for k in range(len(pls)):
+                want[k][d] = R
+            return
+        if not shards:
+            return
+        od = shards.pop()
+        if name in ("flash_attention", "attention", "apply_rotary") and od not in (0, 2):
+            for k in range(len(pls)):
+                want[k][d] = R
+            return
+        out[d] = S(od)
+        for k, p in enumerate(pls):
+            if p == R or (isinstance(p, tuple) and p == R):
+                rank_k = len(ins[k].shape)
+                ad = od - (out_rank - rank_k)
+                if name == "embedding" and k == 1:
+                    ctp.setdefault(refs[k].i, set()).add(d)  # weight: gradient is partial over the shards
+                elif 0 <= ad < rank_k and ins[k].shape[ad] > 1:
+                    if name in ("apply_rotary",) and k > 0:
+                        continue  # RoPE tables are per position, shared by every head / batch shard
+                    want[k][d] = S(ad)
+                else:
+                    ctp.setdefault(refs[k].i, set()).add(d)
+
+    def _rule_embedding(self, refs, ins, nd):
+        """ids [..] x table [V, h] -> [.., h]: ids placements carry over (left-aligned); a table sharded on h
+        gives a hidden-sharded output; a vocab-sharded table is gathered."""
+        ids, w = ins[0], ins[1]
+        want = [list(i.pl) for i in ins]
+        out = [R] * nd
+        ctp = {}
+        for d in range(nd):
+            pi, pw = ids.pl[d], w.pl[d]
+            if _is_p(pi):
+                want[0][d] = pi = R
+            if pw == R:
+                out[d] = pi
+                if _is_s(pi):
+                    ctp.setdefault(refs[1].i, set()).add(d)
+            elif _is_s(pw) and pw[1] % 2 == 1 and pi == R:
+                out[d] = S(len(ids.shape))
+            else:
+                want[1][d] = R
+                out[d] = pi
+                if _is_s(pi):
+                    ctp.setdefault(refs[1].i, set()).add(d)
+        return [tuple(v) for v in want], out, ctp
+
+    def _rule_linear(self, refs, ins, nd):
+        x, w = ins[0], ins[1]
+        xr = len(x.shape)
+        want = [list(i.pl) for i in ins]
+        out = [R] * nd
+        ctp = {}
+        for d in range(nd):
+            px, pw = x.pl[d], w.pl[d]
+            if _is_p(px):
+                px = want[0][d] = R
+            if pw == R:
+                if _is_s(px) and px[1] % xr == xr - 1:
+                    want[0][d] = R
+                    px = R
+                out[d] = px if _is_s(px) else R
+                if _is_s(px):
+                    ctp.setdefault(refs[1].i, set()).add(d)  # replicated weight, split rows: dW partial
+                    if len(refs) > 2:
+                        ctp.setdefault(refs[2].i, set()).add(d)
+            elif pw == S(1) or pw == S(-1):
+                if _is_s(px):
+                    want[0][d] = R
+                ctp.setdefault(refs[0].i, set()).add(d)  # column parallel: dx partial
+                out[d] = S(xr - 1)
+                if len(refs) > 2:
+                    want[2][d] = S(0)
+            elif pw == S(0):
+                want[0][d] = S(xr - 1)
+                out[d] = PSUM()
+                if len(refs) > 2:
+                    raise NotImplementedError("row-parallel linear with a bias")
+            else:
+                want[1][d] = R
+                want[0][d] = R
+        return [tuple(v) for v in want], out, ctp
+
+    def _transpose_dim(self, n, d, rank):
+        name = _short(n.name)
+        a = n.args[1:]
+        if name == "t":
+            return 1 - d
+        if name == "transpose":
+            i, j = (x % rank for x in a[:2])
+            return j if d == i else (i if d == j else d)
+        perm = list(a[0]) if len(a) == 1 and isinstance(a[0], (list, tuple)) else list(a)
+        perm = [p % rank for p in perm]
+        return perm.index(d)
+
+    @staticmethod
+    def _reduce_dims(n, rank):
+        a = n.args[1:]
+        dims = n.kwargs.get("dim", n.kwargs.get("axis", a[0] if a and not isinstance(a[0], bool) else None))
+        if dims is None:
+            return set(range(rank))
+        dims = dims if isinstance(dims, (list, tuple)) else [dims]
+        return {x % rank for x in dims}
+
+    @staticmethod
+    def _keepdim(n):
+        if "keepdim" in n.kwargs:
+            return bool(n.kwargs["keepdim"])
+        a = n.args[1:]
+        return len(a) >= 2 and isinstance(a[1], bool) and a[1]
+
+    def _local_reshape_args(self, n, src, args, out_pl):
+        """Rewrite the global target shape to this rank's local shape."""
+        ins = self.info[src]
+        shape = _resolve_shape(_shape_args(n.args), int(np.prod(ins.shape)))
+        mesh_shape = self.meshes[0].shape
+        for d, p in enumerate(out_pl):
+            if _is_s(p):
+                shape[p[1]] //= mesh_shape[d]
+        head = list(args[:1])
+        rest = n.args[1:]
+        if len(rest) == 1 and isinstance(rest[0], (list, tuple)):
+            return tuple(head + [type(rest[0])(shape)])
+        return tuple(head + shape)
+
+    # ---------------------------------------------------------------- parameters
+    def _localize_params(self):
+        """Each rank keeps only its stage's shards, as plain leaf tensors the optimizer updates."""
+        self.local_params = {}
+        for p in self.params:
+            slot = self.param_slots[id(p)]
+            st = self.slot_stage.get(slot)
+            t = p._t
+            if type(t) is not torch.Tensor and hasattr(t, "to_local"):
+                loc = t.to_local() if self.rank in self.info[slot].mesh else torch.empty(0, dtype=t.dtype)
+            else:
+                loc = t
+            loc = loc.detach().clone().requires_grad_(not p.stop_gradient and st == self.my_stage)
+            p._t = loc
+            from ...framework.tensor import _PARAM_OF
+            _PARAM_OF[id(loc)] = p
+            self.local_params[slot] = p
+        clip = getattr(self.opt, "_grad_clip", None)
+        if clip is not None and hasattr(clip, "_extra_sq_norm_fn"):
+            clip._param_sq_fn = self._param_sq
+
+    def _param_sq(self, params):
+        """Global grad-norm^2: sharded params summed over their mesh dims, replicated ones counted once,
+        stages summed over the pipeline."""
+        dev = params[0]._t.device if params else torch.device("cpu")
+        tot = torch.zeros(1, dtype=torch.float32, device=dev)
+        by_id = {id(p): s for s, p in self.local_params.items()}
+        for p in params:
+            g = p._t.grad
+            if g is None:
+                continue
+            slot = by_id.get(id(p))
+            sq = g.float().pow(2).sum().reshape(1)
+            if slot is not None:
+                inf = self.info[slot]
+                for d, pl in enumerate(inf.pl):
+                    if _is_s(pl):
+                        gr = self.groups.get(self.my_stage, d)
+                        if gr[0] is not None:
+                            dist.all_reduce(sq, group=gr[0])
+            tot += sq
+        if len(self.meshes) > 1 and dist.is_initialized():
+            # sum over the stages: ranks with the same coordinate in every stage mesh
+            dist.all_reduce(tot, group=self._pp_group())
+        return tot[0]
+
+    def _pp_group(self):
+        if not hasattr(self, "_ppg"):
+            arrs = [m.mesh.reshape(-1) for m in self.meshes]
+            groups = None
+            for k in range(arrs[0].size):
+                ranks = [int(a[k]) for a in arrs]
+                g = dist.new_group(ranks)
+                if self.rank in ranks:
+                    groups = g
+            self._ppg = groups
+        return self._ppg
+
+    # ---------------------------------------------------------------- run
+    def _peer(self, dst_stage):
+        src_mesh = self.meshes[self.my_stage].mesh
+        idx = np.argwhere(src_mesh == self.rank)[0]
+        return int(self.meshes[dst_stage].mesh[tuple(idx)])
+
+    def _feeds_local(self, inputs, labels, mb):
+        vals = []
+        for t, slot in zip(list(inputs) + [labels], self.feed_slots):
+            full = t._t if isinstance(t, Tensor) else torch.as_tensor(np.asarray(t))
+            part = full.chunk(self.acc, 0)[mb]
+            inf = self.info[slot]
+            for d, pl in enumerate(inf.pl):
+                if _is_s(pl):
+                    gr = self.groups.get(self.my_stage, d)
+                    part = part.chunk(_nranks(gr), pl[1])[_my(gr)]
+            vals.append(part.contiguous())
+        return vals
+
+    def _materialize(self, tmpl, env):
+        if isinstance(tmpl, tuple) and len(tmpl) == 3 and tmpl[0] == "G":
+            return self.groups.get(self.my_stage, tmpl[2])
+        if isinstance(tmpl, P._Ref):
+            return env[tmpl.i]
+        if isinstance(tmpl, P._Const):
+            t = tmpl.t
+            if isinstance(t, torch.Tensor) and t.device != self.dev and t.device.type != "meta":
+                c = self._consts.get(tmpl.idx)
+                if c is None:
+                    c = self._consts[tmpl.idx] = t.to(self.dev)
+                return c
+            return t
+        if tmpl is P._RUN_DEV:
+            return self.dev
+        if isinstance(tmpl, list):
+            return [self._materialize(v, env) for v in tmpl]
+        if isinstance(tmpl, tuple):
+            return tuple(self._materialize(v, env) for v in tmpl)
+        if isinstance(tmpl, dict):
+            return {k: self._materialize(v, env) for k, v in tmpl.items()}
+        if isinstance(tmpl, slice):
+            return slice(self._materialize(tmpl.start, env), self._materialize(tmpl.stop, env),
+                         self._materialize(tmpl.step, env))
+        return tmpl
+
+    def _forward_mb(self, mb, inputs, labels, p2p):
+        s = self.my_stage
+        env = {}
+        for slot, p in self.local_params.items():
+            env[slot] = p._t
+        for slot, v in zip(self.feed_slots, self._feeds_local(inputs, labels, mb)):
+            env[slot] = v.to(self.dev)
+        received = []
+        for slot in sorted(self.stage_inputs[s]):
+            t = p2p.recv(self._peer(self.slot_stage[slot]), ("F", slot, mb))
+            if t.is_floating_point():
+                t.requires_grad_(True)
+            env[slot] = t
+            received.append((slot, t))
+        for nd in self.stage_nodes[s]:
+            args = self._materialize(nd.args, env)
+            kw = self._materialize(nd.kwargs, env)
+            out = nd.fn(*args, **kw)
+            if nd.outs is not None:
+                P._assign(nd.outs, out, env)
+        sent = []
+        for slot, dsts in sorted(self.sends[s].items()):
+            t = env[slot]
+            for dst in sorted(dsts):
+                p2p.send(t.detach(), self._peer(dst), ("F", slot, mb))
+            sent.append((slot, t, sorted(dsts)))
+        loss = env.get(self.loss_slot) if self.slot_stage.get(self.loss_slot) == s else None
+        return received, sent, loss
+
+    def _backward_mb(self, mb, state, p2p):
+        received, sent, loss = state
+        outs, grads = [], []
+        for slot, t, dsts in sent:
+            if not t.requires_grad:
+                continue
+            g = None
+            for dst in dsts:
+                gi = p2p.recv(self._peer(dst), ("B", slot, mb))
+                g = gi if g is None else g + gi
+            outs.append(t)
+            grads.append(g)
+        if loss is not None:
+            outs.append(loss / self.acc)
+            grads.append(None)
+        if outs:
+            torch.autograd.backward(outs, grads)
+        for slot, t in received:
+            if t.requires_grad:
+                g = t.grad if t.grad is not None else torch.zeros_like(t)
+                p2p.send(g, self._peer(self.slot_stage[slot]), ("B", slot, mb))
+
+    def step(self, inputs, labels):
+        if not self.built:
+            self.build(inputs, labels)
+        from ...framework.place import _get_torch_device
+        self.dev = _get_torch_device()
+        p2p = _P2P(self.dev)
+        nst = len(self.meshes)
+        s = self.my_stage
+        n = self.acc
+        states, losses = {}, []
+
+        def fwd(mb):
+            st = self._forward_mb(mb, inputs, labels, p2p)
+            if st[2] is not None:
+                losses.append(st[2].detach().float().reshape(()))
+            states[mb] = st
+        if self.schedule == "FTHENB" or nst == 1:
+            for mb in range(n):
+                fwd(mb)
+            for mb in range(n):
+                self._backward_mb(mb, states.pop(mb), p2p)
+        else:  # 1F1B: warm-up forwards, then one forward / one backward, then the cool-down backwards
+            warm = min(nst - s - 1, n)
+            fi = bi = 0
+            for _ in range(warm):
+                fwd(fi)
+                fi += 1
+            while fi < n:
+                fwd(fi)
+                fi += 1
+                self._backward_mb(bi, states.pop(bi), p2p)
+                bi += 1
+            while bi < n:
+                self._backward_mb(bi, states.pop(bi), p2p)
+                bi += 1
+        p2p.join()
+        loss = torch.stack(losses).mean() if losses else torch.zeros((), device=self.dev)
+        if nst > 1:  # every rank reports the loss of the last stage
+            loss = loss.clone()
+            dist.all_reduce(loss, group=self._pp_group())
+        self.opt.step()
+        self.opt.clear_grad()
+        return _wrap(loss)
+
+
+def _key(key):
+    kind, slot, mb = key
+    return ((0 if kind == "F" else 1) << 40) | (int(slot) << 20) | int(mb)
+
+
+class _P2P:
+    """Keyed point-to-point messages between pipeline stage ranks (non-blocking sends)."""
+
+    def __init__(self, dev):
+        self.dev = dev
+        self.pending = []
+        self.stash = {}
+
+    def send(self, t, dst, key):
+        t = t.contiguous()
+        hdr = torch.tensor([t.dim()] + list(t.shape) + [0] * (8 - t.dim()) + [_DT[t.dtype], _key(key)],
+                           dtype=torch.int64, device=t.device)
+        self.pending.append((dist.isend(hdr, dst), hdr))
+        self.pending.append((dist.isend(t, dst), t))
+
+    def recv(self, src, key):
+        st = self.stash.setdefault(src, {})
+        want = _key(key)
+        if want in st:
+            return st.pop(want)
+        while True:
+            hdr = torch.empty(11, dtype=torch.int64, device=self.dev)
+            dist.recv(hdr, src)
+            h = [int(v) for v in hdr.tolist()]
+            t = torch.empty(h[1:1 + h[0]], dtype=_CODE[h[9]], device=self.dev)
+            dist.recv(t, src)
+            if h[10] == want:
+                return t
+            st[h[10]] = t
+
+    def join(self):
+        for w, _ in self.pending:
+            w.wait()
+        self.pending = []
+
+
+_DT = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2, torch.int64: 3, torch.int32: 4, torch.bool: 5}
+_CODE = {v: k for k, v in _DT.items()}

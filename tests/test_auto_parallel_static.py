@@ -1,0 +1,91 @@
+"""Static semi-auto parallel engine (dist.to_static): LLaMA annotated with placements on a ["pp", "dp", "mp"]
+mesh trains through traced programs partitioned per rank (TP collectives, DP gradient reduction, pipeline
+p2p) and must reproduce single-process training. Reference: test/auto_parallel/hybrid_strategy/
+semi_auto_llama.py (semi-auto LLaMA PP x TP x DP), static/engine.py."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from test_distributed_cpu import ROOT, _setup, _spawn
+
+STEPS = 3
+
+
+def _data():
+    g = torch.Generator().manual_seed(5)
+    return torch.randint(0, 512, (4, 17), generator=g)
+
+
+def _cfg():
+    from paddlepaddle_amd.models.llama_auto import LlamaConfig
+    return LlamaConfig.tiny(num_hidden_layers=4, num_attention_heads=4, num_key_value_heads=2)
+
+
+def _worker(rank, world, port, shape, acc, schedule, q):
+    paddle = _setup(rank, world, port)
+    import paddlepaddle_amd.distributed as dist
+    from paddlepaddle_amd.models.llama_auto import LlamaForCausalLMAuto, LlamaPretrainingCriterionAuto
+    pp, dp, mp = shape
+    mesh = dist.ProcessMesh(np.arange(pp * dp * mp).reshape(pp, dp, mp), dim_names=["pp", "dp", "mp"])
+    dist.auto_parallel.set_mesh(mesh)
+    paddle.seed(4)
+    cfg = _cfg()
+    model, crit = LlamaForCausalLMAuto(cfg), LlamaPretrainingCriterionAuto(cfg)
+    opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    strategy = dist.Strategy()
+    strategy.pipeline.enable = pp > 1 or acc > 1
+    strategy.pipeline.accumulate_steps = acc
+    strategy.pipeline.schedule_mode = schedule
+    dm = dist.to_static(model, None, crit, opt, strategy)
+    assert dm._engine is not None
+    ids = _data()
+    losses = []
+    for _ in range(STEPS):
+        loss = dm(paddle.Tensor(ids[:, :-1]), paddle.Tensor(ids[:, 1:]))
+        losses.append(float(loss))
+    eng = dm._engine
+    kinds = sorted({n.name for nodes in eng.stage_nodes for n in nodes if n.name in (
+        "allreduce", "allgather", "slice", "copy_to_parallel")})
+    q.put((rank, losses, kinds, eng.my_stage))
+    paddle.distributed.barrier()
+
+
+def _reference():
+    sys.path.insert(0, ROOT)
+    os.environ["PADDLE_AMD_FORCE_CPU"] = "1"
+    import paddlepaddle_amd as paddle
+    from paddlepaddle_amd.models.llama_auto import LlamaForCausalLMAuto, LlamaPretrainingCriterionAuto
+    paddle.distributed.auto_parallel.set_mesh(None)
+    paddle.seed(4)
+    cfg = _cfg()
+    model, crit = LlamaForCausalLMAuto(cfg), LlamaPretrainingCriterionAuto(cfg)
+    opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    ids = _data()
+    out = []
+    for _ in range(STEPS):
+        loss = crit(model(paddle.Tensor(ids[:, :-1])), paddle.Tensor(ids[:, 1:]))
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        out.append(float(loss))
+    return out
+
+
+@pytest.mark.parametrize("shape,acc,schedule", [
+    ((1, 1, 2), 1, "1F1B"),     # tensor parallel
+    ((1, 2, 2), 1, "1F1B"),     # data x tensor parallel
+    ((2, 1, 2), 2, "1F1B"),     # pipeline x tensor parallel
+    ((4, 1, 2), 4, "1F1B"),     # the reference's PP4 x TP2 configuration, 8 ranks
+    ((2, 2, 2), 2, "FThenB"),   # pipeline x data x tensor parallel, 8 ranks
+])
+def test_static_auto_parallel_llama_matches_single_process(shape, acc, schedule):
+    ref = _reference()
+    world = int(np.prod(shape))
+    res = _spawn(_worker, shape, acc, schedule, world=world)
+    for rank, losses, kinds, stage in res:
+        np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-5, err_msg=f"rank {rank} stage {stage}")
+        if shape[2] > 1:
+            assert "allreduce" in kinds and "copy_to_parallel" in kinds
