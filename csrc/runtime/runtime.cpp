@@ -20,6 +20,8 @@
 #include <thread>
 #include <vector>
 
+#include "allocator.h"
+
 namespace py = pybind11;
 
 namespace {
@@ -160,6 +162,36 @@ int64_t write_blobs(const std::string& path, const std::string& header, const st
   return off;
 }
 
+// Host-memory backend of the device allocator core (allocator.h) for CPU unit tests: "streams" are plain
+// integers, cross-stream waits are counted.
+void* host_raw_alloc(size_t n, int) { return std::aligned_alloc(4096, (n + 4095) / 4096 * 4096); }
+void host_raw_free(void* p, int) { std::free(p); }
+void host_wait(uintptr_t, uintptr_t, int) {}
+void host_sync(int) {}
+
+class HostAllocator {
+ public:
+  explicit HostAllocator(size_t min_chunk)
+      : a_({host_raw_alloc, host_raw_free, host_wait, host_sync}, 0, min_chunk) {}
+  uintptr_t allocate(size_t n, uintptr_t stream) { return reinterpret_cast<uintptr_t>(a_.allocate(n, stream)); }
+  bool free(uintptr_t p) { return a_.deallocate(reinterpret_cast<void*>(p)); }
+  size_t release() { return a_.release_free_chunks(); }
+  size_t block_size(uintptr_t p) { return a_.block_size(reinterpret_cast<void*>(p)); }
+  size_t free_blocks() { return a_.free_blocks(); }
+  py::dict stats() {
+    pa_alloc::Stats s = a_.stats();
+    py::dict d;
+    d["allocated"] = s.allocated; d["reserved"] = s.reserved; d["peak_allocated"] = s.peak_allocated;
+    d["peak_reserved"] = s.peak_reserved; d["n_alloc"] = s.n_alloc; d["n_free"] = s.n_free;
+    d["n_chunks"] = s.n_chunks; d["n_raw_alloc"] = s.n_raw_alloc; d["n_raw_free"] = s.n_raw_free;
+    d["n_cross_stream"] = s.n_cross_stream; d["n_oom_release"] = s.n_oom_release;
+    return d;
+  }
+
+ private:
+  pa_alloc::BestFitAllocator a_;
+};
+
 }  // namespace
 
 void register_pinned_pool(py::module& m);    // pinned_pool.cpp
@@ -171,6 +203,14 @@ PYBIND11_MODULE(_C_runtime, m) {
   register_pinned_pool(m);
   register_comm_watchdog(m);
   register_ps_table(m);
+  py::class_<HostAllocator>(m, "HostAllocator")
+      .def(py::init<size_t>(), py::arg("min_chunk") = size_t(64) << 20)
+      .def("allocate", &HostAllocator::allocate, py::arg("nbytes"), py::arg("stream") = 0)
+      .def("free", &HostAllocator::free)
+      .def("release", &HostAllocator::release)
+      .def("block_size", &HostAllocator::block_size)
+      .def("free_blocks", &HostAllocator::free_blocks)
+      .def("stats", &HostAllocator::stats);
   m.def("stack_into", &stack_into, py::arg("arrays"), py::arg("out"));
   m.def("plan_buckets", &plan_buckets, py::arg("sizes"), py::arg("bucket_bytes"));
   m.def("schedule", &schedule, py::arg("n"), py::arg("edges"), py::arg("keep"),

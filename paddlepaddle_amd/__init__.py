@@ -190,3 +190,16 @@ from . import sysconfig, hub, reader, dataset, base, _C_ops, _legacy_C_ops  # no
 from .tensor import _bind_reference_extras as _bre  # noqa: E402
 from .tensor.search import top_p_sampling  # noqa: F401,E402
 _bre()
+
+
+def _maybe_native_allocator():
+    """FLAGS_allocator_strategy=auto_growth_best_fit / PADDLE_AMD_ALLOCATOR=auto_growth: install the native
+    device allocator (device/allocator.py) before anything touches device memory."""
+    from .device import allocator as _al
+    if _al._env_requested() and _torch.cuda.is_available():
+        _al.enable(int(_os_env.get("PADDLE_AMD_ALLOC_MIN_CHUNK_MB", "64")))
+
+
+from os import environ as _os_env  # noqa: E402
+
+_maybe_native_allocator()

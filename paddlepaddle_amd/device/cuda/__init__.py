@@ -96,27 +96,59 @@ def set_stream(stream):
     return stream
 
 
+def _native():
+    from .. import allocator as A
+    return A if A.is_enabled() else None
+
+
+def _idx(device):
+    d = _dev(device)
+    return d.index if isinstance(d, torch.device) and d.index is not None else (
+        d if isinstance(d, int) else torch.cuda.current_device())
+
+
 def max_memory_allocated(device=None):
+    A = _native()
+    if A is not None:
+        return A.stats(_idx(device))["peak_allocated"]
     return torch.cuda.max_memory_allocated(_dev(device))
 
 
 def max_memory_reserved(device=None):
+    A = _native()
+    if A is not None:
+        return A.stats(_idx(device))["peak_reserved"]
     return torch.cuda.max_memory_reserved(_dev(device))
 
 
 def memory_allocated(device=None):
+    A = _native()
+    if A is not None:
+        return A.stats(_idx(device))["allocated"]
     return torch.cuda.memory_allocated(_dev(device))
 
 
 def memory_reserved(device=None):
+    A = _native()
+    if A is not None:
+        return A.stats(_idx(device))["reserved"]
     return torch.cuda.memory_reserved(_dev(device))
 
 
 def reset_max_memory_allocated(device=None):
+    A = _native()
+    if A is not None:
+        A.reset_peak(_idx(device))
+        return
     torch.cuda.reset_peak_memory_stats(_dev(device))
 
 
 def empty_cache():
+    A = _native()
+    if A is not None:
+        for i in range(torch.cuda.device_count()):
+            A.empty_cache(i)
+        return
     torch.cuda.empty_cache()
 
 

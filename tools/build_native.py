@@ -68,13 +68,28 @@ def build_hip(verbose=False, jobs=None):
 
 def build_runtime(verbose=False):
     import pybind11
-    srcs = sorted(glob.glob(os.path.join(ROOT, "csrc", "runtime", "*.cpp")))
+    srcs = sorted(s for s in glob.glob(os.path.join(ROOT, "csrc", "runtime", "*.cpp")) if not s.endswith("_hip.cpp"))
+    hdrs = glob.glob(os.path.join(ROOT, "csrc", "runtime", "*.h"))
     suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
     out = os.path.join(PKG, "_C_runtime" + suffix)
-    if not _newer(srcs, out):
+    if not _newer(srcs + hdrs, out):
         return out
     inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
     _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", *inc, *srcs, "-o", out, "-ldl"])
+    if verbose:
+        print(f"built {out}")
+    return out
+
+
+def build_alloc(verbose=False):
+    """The HIP device allocator (host code, hipMalloc / events) as a PyTorch pluggable allocator library."""
+    srcs = sorted(glob.glob(os.path.join(ROOT, "csrc", "runtime", "*_hip.cpp")))
+    hdrs = glob.glob(os.path.join(ROOT, "csrc", "runtime", "*.h"))
+    out = os.path.join(PKG, "_C_alloc.so")
+    if not _newer(srcs + hdrs, out):
+        return out
+    hipcc = os.path.join(ROCM, "bin", "hipcc")
+    _run([hipcc, "-O3", "-std=c++17", "-fPIC", "-shared", *srcs, "-o", out, f"-L{ROCM}/lib", "-lamdhip64"])
     if verbose:
         print(f"built {out}")
     return out
@@ -84,6 +99,7 @@ def main():
     verbose = "-v" in sys.argv or True
     build_hip(verbose)
     build_runtime(verbose)
+    build_alloc(verbose)
 
 
 if __name__ == "__main__":
