@@ -52,6 +52,8 @@ def parse():
     p.add_argument("--resnet-batch", type=int, default=256, help="per-GPU ResNet-50 batch")
     p.add_argument("--resnet-steps", type=int, default=10)
     p.add_argument("--skip-gpt", type=int, default=0)
+    p.add_argument("--allocator", default="native", choices=["native", "torch"],
+                   help="device allocator: the framework's auto-growth best-fit allocator or PyTorch's")
     return p.parse_args()
 
 
@@ -166,7 +168,7 @@ def gpt_bench(args, paddle, world, dist_on):
     tps = tokens / dt
     fpt = cfg.flops_per_token(S, recompute=False)
     mfu = tps * fpt / (PEAK_BF16 * world)
-    mem = torch.cuda.max_memory_allocated() / 2**30 if dev.type == "cuda" else 0.0
+    mem = paddle.device.cuda.max_memory_allocated() / 2**30 if dev.type == "cuda" else 0.0
     log(f"[gpt] loss={float(state['loss']):.4f} step={dt / args.steps * 1000:.1f}ms tokens/s={tps:.0f} "
         f"MFU(6N model flops)={mfu * 100:.1f}% mem={mem:.1f}GiB")
     try:
@@ -179,7 +181,7 @@ def gpt_bench(args, paddle, world, dist_on):
         pass
     del model, opt, ids, lbl
     if dev.type == "cuda":
-        torch.cuda.empty_cache()
+        paddle.device.cuda.empty_cache()
     gpt_bench.keep_params = keep
     return tps, dt / args.steps * 1000, B * args.accum * n_shard, mfu
 
@@ -293,6 +295,14 @@ def _relaunch(args):
     sys.exit(subprocess.call(cmd, env=env))
 
 
+def _native_alloc_on():
+    try:
+        from paddlepaddle_amd.device import allocator as A
+        return A.is_enabled()
+    except Exception:  # pragma: no cover
+        return False
+
+
 def main():
     args = parse()
     if args.tp is None:
@@ -302,6 +312,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
+    if args.allocator == "native":
+        os.environ.setdefault("PADDLE_AMD_ALLOCATOR", "auto_growth")  # installed at package import
     import paddlepaddle_amd as paddle
     dist_on = world > 1
     if dist_on:
@@ -343,6 +355,7 @@ def main():
                        "global_batch": gb, "seq_len": args.seq_len, "micro_batch": args.micro_batch,
                        "accum_steps": args.accum, "parallelism": par, "recompute": bool(args.recompute),
                        "optimizer": "AdamW fp32-master fused HIP", "amp": "O2 bf16",
+                       "allocator": ("native auto-growth best-fit" if _native_alloc_on() else "torch caching"),
                        **({"stage3_params": ("gathered once per step, resident until the optimizer step"
                                              if getattr(gpt_bench, "keep_params", None) else
                                              "released after each block, re-gathered per micro-batch")}

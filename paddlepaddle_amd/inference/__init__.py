@@ -251,7 +251,8 @@ class Predictor:
 
     def try_shrink_memory(self):
         if torch.cuda.is_available():
-            torch.cuda.empty_cache()
+            from ..device.cuda import empty_cache as _ec
+            _ec()
 
 
 def create_predictor(config):

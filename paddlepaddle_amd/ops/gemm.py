@@ -243,6 +243,7 @@ def choose(key, candidates, cold=False):
         return mode
     load_tuning_table()
     key = _canon(key)
+    _USED.add(key)
     ch = _CHOICE.get(key)
     if ch is not None and ch in candidates:
         return ch
@@ -268,8 +269,13 @@ def choose(key, candidates, cold=False):
     return ch
 
 
-def choices():
-    """The tuned decisions so far: {key: backend} (for logs / profiles)."""
+_USED = set()
+
+
+def choices(used_only=True):
+    """Decisions {key: backend} (for logs / profiles): by default only the keys this process dispatched."""
+    if used_only:
+        return {k: v for k, v in _CHOICE.items() if k in _USED}
     return dict(_CHOICE)
 
 
