@@ -46,6 +46,9 @@ def enable(min_chunk_mb=64):
         return True
     lib = _lib()
     lib.pa_alloc_set_min_chunk(int(min_chunk_mb) << 20)
+    # a pluggable allocator gets no record_stream calls: let the process groups keep their tensors alive
+    # until the collective is waited on instead (stream-ordered reuse stays safe)
+    os.environ.setdefault("TORCH_NCCL_AVOID_RECORD_STREAMS", "1")
     alloc = torch.cuda.memory.CUDAPluggableAllocator(_PATH, "pa_malloc", "pa_free")
     torch.cuda.memory.change_current_allocator(alloc)
     _ACTIVE = True
