@@ -525,6 +525,7 @@ class GroupShardedEngine:
                         h = self._host_copy(g)
                     h.copy_(g, non_blocking=True)
                     g.record_stream(cs)
+                    self._inflight.append(g)  # released once the compute stream has waited for the copies
                     d[k] = h
 
     @torch.no_grad()
@@ -543,6 +544,7 @@ class GroupShardedEngine:
         dev = chunks[0][0]._t.device
         if dev.type == "cuda" and self._copy_stream is None:
             self._copy_stream = torch.cuda.Stream(dev)
+        self._inflight = []
         ev = self._swap_in(chunks[0], dev)
         for i, ps in enumerate(chunks):
             nxt = self._swap_in(chunks[i + 1], dev) if i + 1 < len(chunks) else None
@@ -553,6 +555,7 @@ class GroupShardedEngine:
             ev = nxt
         if dev.type == "cuda":
             torch.cuda.current_stream(dev).wait_stream(self._copy_stream)
+        self._inflight = []
 
     def offloaded_bytes(self):
         """Bytes of optimizer state currently held in host memory."""

@@ -587,6 +587,8 @@ class _Streams:
         self.comp = torch.cuda.current_stream(dev)
         self.comm = _comm_stream(dev)
         self.pending = {}  # slot -> event recorded on the comm stream after the collective that wrote it
+        self.keep = []     # tensors the comm stream touched: alive until finish() (allocators without
+                           # record_stream would otherwise hand their memory to the compute stream early)
 
     def before(self, n, reads):
         if n.kind == "comm":
@@ -608,10 +610,12 @@ class _Streams:
             t = env.get(s)
             if isinstance(t, torch.Tensor) and t.is_cuda:
                 t.record_stream(self.comm)
+                self.keep.append(t)
 
     def finish(self):
-        if self.pending:
+        if self.pending or self.keep:
             self.comp.wait_stream(self.comm)
+        self.keep = []
 
 
 _COMM_STREAMS = {}
