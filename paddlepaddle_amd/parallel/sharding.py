@@ -514,6 +514,7 @@ class GroupShardedEngine:
             return
         cs = self._copy_stream
         cs.wait_stream(torch.cuda.current_stream(dev))
+        bufs = []
         with torch.cuda.stream(cs):
             for p in shards:
                 for d, k in self._state_slots(p):
@@ -525,8 +526,16 @@ class GroupShardedEngine:
                         h = self._host_copy(g)
                     h.copy_(g, non_blocking=True)
                     g.record_stream(cs)
-                    self._inflight.append(g)  # released once the compute stream has waited for the copies
+                    bufs.append(g)
                     d[k] = h
+        ev = torch.cuda.Event()
+        ev.record(cs)
+        # the device buffers are released one unit later, after the compute stream has waited for their
+        # copies (allocators that ignore record_stream stay safe; at most ~2 units of state stay in HBM)
+        if self._inflight:
+            pev, _ = self._inflight.pop(0)
+            torch.cuda.current_stream(dev).wait_event(pev)
+        self._inflight.append((ev, bufs))
 
     @torch.no_grad()
     def _offload_step(self):
