@@ -42,17 +42,57 @@ struct Stats {
 class BestFitAllocator {
  public:
   static constexpr size_t kAlign = 512;
+  static constexpr uintptr_t kPoolBit = uintptr_t(1) << 63;
 
   BestFitAllocator(Backend be, int device, size_t min_chunk = size_t(64) << 20)
       : be_(be), device_(device), min_chunk_(min_chunk) {}
 
   ~BestFitAllocator() { release_all(); }
 
-  void* allocate(size_t bytes, uintptr_t stream) {
+  // Graph capture: while `stream` is being captured its allocations come from the private pool
+  // `pool_id`, whose free blocks are never handed to other streams / pools, so the addresses a captured
+  // graph uses stay reserved for its replays (reference: CUDA graph memory pools). end_pool stops the
+  // redirection; release_pool returns the pool's blocks to ordinary use once the graph is gone.
+  void begin_pool(uintptr_t stream, uint64_t pool_id) {
+    std::lock_guard<std::mutex> g(mu_);
+    const uintptr_t pkey = kPoolBit | static_cast<uintptr_t>(pool_id);
+    capture_[stream] = pkey;
+    pool_origin_[pkey] = stream;
+  }
+
+  void end_pool(uintptr_t stream) {
+    std::lock_guard<std::mutex> g(mu_);
+    capture_.erase(stream);
+  }
+
+  void release_pool(uint64_t pool_id) {
+    std::lock_guard<std::mutex> g(mu_);
+    const uintptr_t pkey = kPoolBit | static_cast<uintptr_t>(pool_id);
+    auto o = pool_origin_.find(pkey);
+    if (o == pool_origin_.end()) return;
+    const uintptr_t dst = o->second;
+    released_[pkey] = dst;
+    auto pit = pools_.find(pkey);
+    if (pit != pools_.end()) {
+      std::vector<Key> keys(pit->second.begin(), pit->second.end());
+      pools_.erase(pit);
+      for (const Key& k : keys) {
+        Block* b = lookup(k);
+        b->stream = dst;
+        b = coalesce(b);
+        pools_[dst].insert(key(b));
+      }
+    }
+    pool_origin_.erase(o);
+  }
+
+  void* allocate(size_t bytes, uintptr_t stream_in) {
     std::lock_guard<std::mutex> g(mu_);
     const size_t need = round(bytes ? bytes : 1);
+    auto cap = capture_.find(stream_in);
+    const uintptr_t stream = cap == capture_.end() ? stream_in : cap->second;
     Block* b = take(need, stream);
-    if (b == nullptr) b = take_other_stream(need, stream);
+    if (b == nullptr && cap == capture_.end()) b = take_other_stream(need, stream);
     if (b == nullptr) {
       Chunk* c = grow(need, stream);
       if (c == nullptr) {
@@ -83,6 +123,8 @@ class BestFitAllocator {
     st_.allocated -= static_cast<int64_t>(b->size);
     ++st_.n_free;
     b->free = true;
+    auto rel = released_.find(b->stream);
+    if (rel != released_.end()) b->stream = rel->second;  // its graph pool is gone: back to the stream
     b = coalesce(b);
     pools_[b->stream].insert(key(b));
     return true;
@@ -181,7 +223,7 @@ class BestFitAllocator {
     Block* best = nullptr;
     uintptr_t owner = 0;
     for (auto& kv : pools_) {
-      if (kv.first == stream) continue;
+      if (kv.first == stream || (kv.first & kPoolBit)) continue;  // graph pools are never shared
       auto it = kv.second.lower_bound({need, nullptr});
       if (it == kv.second.end()) continue;
       if (best == nullptr || it->first < best->size) {
@@ -278,6 +320,9 @@ class BestFitAllocator {
   std::unordered_map<uintptr_t, std::set<Key>> pools_;
   std::unordered_map<char*, Block*> live_;    // allocated blocks
   std::unordered_map<char*, Block*> blocks_;  // every block (free or not) by address
+  std::unordered_map<uintptr_t, uintptr_t> capture_;      // capturing stream -> graph pool key
+  std::unordered_map<uintptr_t, uintptr_t> pool_origin_;  // graph pool key -> its capturing stream
+  std::unordered_map<uintptr_t, uintptr_t> released_;     // released pool key -> stream its blocks rejoin
   Stats st_;
 };
 

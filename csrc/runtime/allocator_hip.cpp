@@ -113,3 +113,61 @@ extern "C" __attribute__((visibility("default"))) void pa_alloc_reset_peak(int d
 }
 
 extern "C" __attribute__((visibility("default"))) void pa_alloc_set_min_chunk(int64_t bytes) { g_min_chunk = bytes; }
+
+// ---- graph-capture memory pools
+extern "C" __attribute__((visibility("default"))) void pa_alloc_begin_pool(int device, hipStream_t stream,
+                                                                          uint64_t pool) {
+  pa_alloc::BestFitAllocator* a = get(device);
+  if (a != nullptr) a->begin_pool(reinterpret_cast<uintptr_t>(stream), pool);
+}
+
+extern "C" __attribute__((visibility("default"))) void pa_alloc_end_pool(int device, hipStream_t stream) {
+  pa_alloc::BestFitAllocator* a = get(device);
+  if (a != nullptr) a->end_pool(reinterpret_cast<uintptr_t>(stream));
+}
+
+extern "C" __attribute__((visibility("default"))) void pa_alloc_release_pool(int device, uint64_t pool) {
+  pa_alloc::BestFitAllocator* a = get(device);
+  if (a != nullptr) a->release_pool(pool);
+}
+
+// ---- hipGraph capture / instantiate / launch (paddlepaddle_amd/device/cuda/graphs.py)
+// mode: 0 global, 1 thread-local, 2 relaxed (hipStreamCaptureMode)
+extern "C" __attribute__((visibility("default"))) int pa_graph_begin(hipStream_t stream, int mode) {
+  const hipStreamCaptureMode m = mode == 0 ? hipStreamCaptureModeGlobal
+                                           : (mode == 1 ? hipStreamCaptureModeThreadLocal : hipStreamCaptureModeRelaxed);
+  return static_cast<int>(hipStreamBeginCapture(stream, m));
+}
+
+extern "C" __attribute__((visibility("default"))) int pa_graph_end(hipStream_t stream, void** graph_out,
+                                                                  void** exec_out) {
+  hipGraph_t g = nullptr;
+  hipError_t e = hipStreamEndCapture(stream, &g);
+  if (e != hipSuccess) return static_cast<int>(e);
+  hipGraphExec_t x = nullptr;
+  e = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+  if (e != hipSuccess) {
+    (void)hipGraphDestroy(g);
+    return static_cast<int>(e);
+  }
+  *graph_out = g;
+  *exec_out = x;
+  return 0;
+}
+
+extern "C" __attribute__((visibility("default"))) int pa_graph_launch(void* exec, hipStream_t stream) {
+  return static_cast<int>(hipGraphLaunch(static_cast<hipGraphExec_t>(exec), stream));
+}
+
+extern "C" __attribute__((visibility("default"))) int pa_graph_num_nodes(void* graph, size_t* n) {
+  return static_cast<int>(hipGraphGetNodes(static_cast<hipGraph_t>(graph), nullptr, n));
+}
+
+extern "C" __attribute__((visibility("default"))) int pa_graph_dot(void* graph, const char* path) {
+  return static_cast<int>(hipGraphDebugDotPrint(static_cast<hipGraph_t>(graph), path, 0));
+}
+
+extern "C" __attribute__((visibility("default"))) void pa_graph_destroy(void* graph, void* exec) {
+  if (exec != nullptr) (void)hipGraphExecDestroy(static_cast<hipGraphExec_t>(exec));
+  if (graph != nullptr) (void)hipGraphDestroy(static_cast<hipGraph_t>(graph));
+}

@@ -178,6 +178,9 @@ class HostAllocator {
   size_t release() { return a_.release_free_chunks(); }
   size_t block_size(uintptr_t p) { return a_.block_size(reinterpret_cast<void*>(p)); }
   size_t free_blocks() { return a_.free_blocks(); }
+  void begin_pool(uintptr_t stream, uint64_t pool) { a_.begin_pool(stream, pool); }
+  void end_pool(uintptr_t stream) { a_.end_pool(stream); }
+  void release_pool(uint64_t pool) { a_.release_pool(pool); }
   py::dict stats() {
     pa_alloc::Stats s = a_.stats();
     py::dict d;
@@ -210,6 +213,9 @@ PYBIND11_MODULE(_C_runtime, m) {
       .def("release", &HostAllocator::release)
       .def("block_size", &HostAllocator::block_size)
       .def("free_blocks", &HostAllocator::free_blocks)
+      .def("begin_pool", &HostAllocator::begin_pool)
+      .def("end_pool", &HostAllocator::end_pool)
+      .def("release_pool", &HostAllocator::release_pool)
       .def("stats", &HostAllocator::stats);
   m.def("stack_into", &stack_into, py::arg("arrays"), py::arg("out"));
   m.def("plan_buckets", &plan_buckets, py::arg("sizes"), py::arg("bucket_bytes"));

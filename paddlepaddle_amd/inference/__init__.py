@@ -233,8 +233,9 @@ class Predictor:
             with torch.cuda.stream(s):
                 self._replay(dict(env))
             torch.cuda.current_stream().wait_stream(s)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            from ..device.cuda.graphs import CUDAGraph, capture
+            g = CUDAGraph()
+            with capture(g):
                 outs = self._replay(dict(env))
             ent = self._graphs[key] = (g, static_in, outs)
         g, static_in, outs = ent

@@ -258,8 +258,9 @@ class StaticFunction:
             with torch.cuda.stream(s):
                 cp.run(static_in, dev)  # warm-up (allocator, library handles)
             torch.cuda.current_stream().wait_stream(s)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            from ..device.cuda.graphs import CUDAGraph, capture
+            g = CUDAGraph()
+            with capture(g):
                 out = cp.run(static_in, dev)
             cp.graph = (g, static_in, out)
         g, static_in, out = cp.graph

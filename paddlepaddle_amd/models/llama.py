@@ -405,8 +405,9 @@ class LlamaForCausalLM(nn.Layer):
             with torch.cuda.stream(s):
                 self._decode_logits(tok, caches, pos_t)
             torch.cuda.current_stream().wait_stream(s)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            from ..device.cuda.graphs import CUDAGraph, capture
+            g = CUDAGraph()
+            with capture(g):
                 static_logits = self._decode_logits(tok, caches, pos_t)
             for t in range(1, max_new_tokens):
                 tok.copy_(nxt[:, None])

@@ -114,3 +114,21 @@ def test_native_allocator_drives_training_gpu():
     assert s["n_alloc"] > 50 and s["n_chunks"] >= 1 and s["reserved"] >= s["peak_allocated"] > 0
     assert s["api_allocated"] == s["allocated"] and s["api_peak"] == s["peak_allocated"]
     assert s["losses"][-1] < s["losses"][0]
+
+
+def test_graph_pool_isolation_and_release():
+    a = _alloc(min_chunk=1 * MB)
+    a.begin_pool(5, 1)                 # stream 5 is being captured into graph pool 1
+    p = a.allocate(4096, stream=5)
+    a.free(p)                          # freed during capture: stays in the graph's pool
+    a.end_pool(5)
+    q = a.allocate(4096, stream=5)     # after capture: ordinary allocations never reuse graph memory
+    assert q != p
+    r = a.allocate(4096, stream=9)
+    assert r != p
+    a.release_pool(1)                  # graph destroyed: its blocks rejoin stream 5's pool
+    s = a.allocate(4096, stream=5)
+    assert s == p
+    for t in (q, r, s):
+        a.free(t)
+    assert a.stats()["allocated"] == 0
