@@ -95,6 +95,7 @@ class BestFitAllocator {
     if (b == nullptr && cap == capture_.end()) b = take_other_stream(need, stream);
     if (b == nullptr) {
       Chunk* c = grow(need, stream);
+      if (c == nullptr && cap != capture_.end()) return nullptr;  // no device sync inside a capture
       if (c == nullptr) {
         release_locked();
         ++st_.n_oom_release;

@@ -81,7 +81,9 @@ class CUDAGraph:
             if self._pool is None:
                 self._pool = torch.cuda.graph_pool_handle()
             torch._C._cuda_beginAllocateCurrentStreamToPool(self._dev, self._pool)
-        rc = _lib().pa_graph_begin(sp, self._mode)
+        # the native allocator may grow its graph pool with hipMalloc during the capture, which only the
+        # relaxed capture mode permits
+        rc = _lib().pa_graph_begin(sp, 2 if self._native else self._mode)
         if rc != 0:
             self._end_pool()
             self._ctx.__exit__(None, None, None)
