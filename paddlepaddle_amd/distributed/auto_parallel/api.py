@@ -214,11 +214,36 @@ class ShardingStage1(_ShardingStageBase):
 
 
 class ShardingStage2(ShardingStage1):
-    """+ gradients reduce-scattered to the optimizer-state sharding."""
+    """+ gradients kept only as the shard the optimizer state uses: after backward each replicated gradient is
+    redistributed to Shard(0) over the sharding mesh dim (ZeRO-2), so the update reads / writes 1/N of it."""
+
+    def _shard_grad(self, param):
+        g = param._t.grad
+        if g is None or not _is_dist(g) or g.dim() == 0:
+            return
+        pls = list(g.placements)
+        if isinstance(pls[self._dim], _dtm.Replicate) and g.shape[0] % g.device_mesh.size(self._dim) == 0:
+            pls[self._dim] = _dtm.Shard(0)
+            param._t.grad = g.redistribute(g.device_mesh, pls)
 
 
 class ShardingStage3(ShardingStage2):
-    """+ parameters sharded, gathered on use by sharding propagation."""
+    """+ parameters themselves stored as Shard(0) over the sharding mesh dim (ZeRO-3): each rank holds 1/N of
+    every weight; an op that needs the full weight all-gathers it through sharding propagation and the
+    gathered copy is dropped after use."""
+
+    def _shard_param(self, param):
+        t = param._t
+        if not _is_dist(t) or t.dim() == 0:
+            return
+        pls = list(t.placements)
+        if isinstance(pls[self._dim], _dtm.Replicate) and t.shape[0] % t.device_mesh.size(self._dim) == 0:
+            pls[self._dim] = _dtm.Shard(0)
+            sharded = t.detach().redistribute(t.device_mesh, pls).requires_grad_(t.requires_grad)
+            sharded._pa_mesh = getattr(t, "_pa_mesh", None)
+            param._t = sharded
+            from ...framework.tensor import _PARAM_OF
+            _PARAM_OF[id(param._t)] = param
 
 
 class _ShardOptimizer:
@@ -239,9 +264,15 @@ class _ShardOptimizer:
                     d[id(p)] = t
                 return t
             optimizer._acc = _acc
+        if isinstance(shard_fn, ShardingStage3):
+            for p in optimizer._parameter_list:
+                shard_fn._shard_param(p)
 
     def step(self):
         # state sharded differently from the param: compute in the state layout, write back replicated
+        if isinstance(self._shard_fn, ShardingStage2):
+            for p in self._inner_opt._parameter_list:
+                self._shard_fn._shard_grad(p)
         self._inner_opt.step()
 
     def clear_grad(self, set_to_zero=True):
@@ -264,6 +295,36 @@ def shard_optimizer(optimizer, shard_fn=None, gradient_accumulation_steps=1):
 
 
 def shard_scaler(scaler):
+    """Make a GradScaler distributed-aware (reference api.py shard_scaler): the inf/nan check runs on each
+    rank's local gradient shards and the found-inf flag is max-reduced over all ranks, so every rank skips
+    (or takes) the same optimizer step."""
+    import torch.distributed as tdist
+    from ...amp.grad_scaler import OptimizerState
+
+    def unscale_(optimizer):
+        if not scaler._enable:
+            return
+        inner = getattr(optimizer, "_inner_opt", optimizer)
+        if scaler._opt_states.get(id(inner), OptimizerState.INIT) == OptimizerState.UNSCALED:
+            return
+        grads = []
+        for p in inner._parameter_list:
+            g = p._t.grad
+            if g is not None:
+                grads.append(g.to_local() if _is_dist(g) else g)  # local shards share the DTensor storage
+        dev = grads[0].device if grads else torch.device("cpu")
+        found = torch.zeros(1, dtype=torch.float32, device=dev)
+        inv = torch.full((1,), 1.0 / scaler._scale, dtype=torch.float32, device=dev)
+        by = {}
+        for g in grads:
+            by.setdefault((g.device, g.dtype), []).append(g)
+        for gs in by.values():
+            torch._amp_foreach_non_finite_check_and_unscale_(gs, found, inv)
+        if tdist.is_available() and tdist.is_initialized():
+            tdist.all_reduce(found, op=tdist.ReduceOp.MAX)
+        scaler._found_inf = found
+        scaler._opt_states[id(inner)] = OptimizerState.UNSCALED
+    scaler.unscale_ = unscale_
     return scaler
 
 
