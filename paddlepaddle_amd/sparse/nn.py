@@ -10,11 +10,11 @@ import torch.nn.functional as TF
 from .. import nn as _nn
 from ..framework.tensor import Tensor, _wrap
 from ..nn import initializer as I
+from . import _core as K
 
 
 def _vals(x, fn):
-    t = x._t.coalesce()
-    return _wrap(torch.sparse_coo_tensor(t.indices(), fn(t.values()), t.shape))
+    return _wrap(K.map_values(x._t, fn))
 
 
 class functional:  # namespace object: paddle.sparse.nn.functional.*
@@ -32,35 +32,24 @@ class functional:  # namespace object: paddle.sparse.nn.functional.*
 
     @staticmethod
     def softmax(x, axis=-1, name=None):
-        t = x._t
-        if t.layout == torch.sparse_csr:
-            return _wrap(torch.sparse.softmax(t.to_sparse_coo(), axis).to_sparse_csr())
-        return _wrap(torch.sparse.softmax(t.coalesce(), axis))
+        out = K.softmax(x._t, axis)
+        return _wrap(K.same_layout(out, x._t))
 
     @staticmethod
     def _conv(x, weight, bias, stride, padding, dilation, groups, subm, nd):
-        t = x._t.coalesce()
-        dense = t.to_dense()  # [N, *spatial, C]
-        perm_in = [0, nd + 1] + list(range(1, nd + 1))
-        d = dense.permute(perm_in)
-        w = weight._t  # [*k, Cin, Cout]
-        wk = w.permute([nd + 1, nd] + list(range(nd)))  # [Cout, Cin, *k]
-        conv = TF.conv3d if nd == 3 else TF.conv2d
+        """Rulebook convolution on the active sites (sparse/_core.py sparse_conv); submanifold convs keep
+        the input's active set with a centred kernel."""
+        def lst(v):
+            return [int(v)] * nd if isinstance(v, int) else [int(a) for a in v]
+        w = weight._t  # [*k, Cin / groups, Cout]
+        dil = lst(dilation)
         if subm:
-            k = w.shape[:nd]
-            padding = [(kk - 1) // 2 * (dilation if isinstance(dilation, int) else dilation[i])
-                       for i, kk in enumerate(k)]
-            stride = 1
-        out = conv(d, wk, None if bias is None else bias._t, stride, padding, dilation, groups)
-        perm_out = [0] + list(range(2, nd + 2)) + [1]
-        out = out.permute(perm_out)
-        if subm:  # keep the input's active sites
-            idx = t.indices()[:nd + 1]
-            vals = out[tuple(idx)]
-            return _wrap(torch.sparse_coo_tensor(idx, vals, tuple(out.shape)).coalesce())
-        active = out.abs().sum(-1) != 0
-        idx = active.nonzero().t()
-        return _wrap(torch.sparse_coo_tensor(idx, out[tuple(idx)], tuple(out.shape)).coalesce())
+            st = [1] * nd
+            pad = [(int(kk) - 1) // 2 * dil[i] for i, kk in enumerate(w.shape[:nd])]
+        else:
+            st, pad = lst(stride), lst(padding)
+        out = K.sparse_conv(x._t, w, None if bias is None else bias._t, st, pad, dil, groups, subm)
+        return _wrap(out)
 
     @staticmethod
     def conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NDHWC", name=None):
@@ -82,31 +71,20 @@ class functional:  # namespace object: paddle.sparse.nn.functional.*
 
     @staticmethod
     def max_pool3d(x, kernel_size, stride=None, padding=0, ceil_mode=False, data_format="NDHWC", name=None):
-        t = x._t.coalesce()
-        d = t.to_dense().permute(0, 4, 1, 2, 3)
-        mask = (t.to_dense().abs().sum(-1) != 0).float()[:, None]
-        big = torch.where(mask.bool().expand_as(d), d, torch.full_like(d, float("-inf")))
-        o = TF.max_pool3d(big, kernel_size, stride, padding, ceil_mode=ceil_mode)
-        o = torch.where(torch.isinf(o), torch.zeros_like(o), o).permute(0, 2, 3, 4, 1)
-        active = TF.max_pool3d(mask, kernel_size, stride, padding, ceil_mode=ceil_mode)[:, 0] > 0
-        idx = active.nonzero().t()
-        return _wrap(torch.sparse_coo_tensor(idx, o[tuple(idx)], tuple(o.shape)).coalesce())
+        """Max over the active sites of each window (rulebook), output sites = windows with any active input."""
+        def lst(v):
+            return [int(v)] * 3 if isinstance(v, int) else [int(a) for a in v]
+        ks = lst(kernel_size)
+        st = lst(stride if stride is not None else kernel_size)
+        return _wrap(K.sparse_max_pool(x._t, ks, st, lst(padding)))
 
     @staticmethod
     def attention(query, key, value, sparse_mask, key_padding_mask=None, attn_mask=None, name=None):
-        """Attention whose score matrix is evaluated only at sparse_mask's nonzeros (CSR [B*H, S, S])."""
-        q, k, v = query._t, key._t, value._t  # [B, H, S, D]
-        B, H, S, D = q.shape
-        m = sparse_mask._t
-        dense_mask = m.to_dense().reshape(B, H, S, S) != 0
-        s = torch.matmul(q, k.transpose(-1, -2)) / math.sqrt(D)
-        if key_padding_mask is not None:
-            s = s + key_padding_mask._t[:, None, None, :]
-        if attn_mask is not None:
-            s = s + attn_mask._t
-        s = s.masked_fill(~dense_mask, float("-inf"))
-        p = torch.nan_to_num(torch.softmax(s, -1))
-        return _wrap(torch.matmul(p, v))
+        """Attention whose score matrix is evaluated only at sparse_mask's nonzeros (CSR [B*H, S, S]):
+        SDDMM -> per-row softmax over the stored scores -> SpMM (no dense S x S matrix)."""
+        return _wrap(K.sparse_attention(query._t, key._t, value._t, sparse_mask._t,
+                                        None if key_padding_mask is None else key_padding_mask._t,
+                                        None if attn_mask is None else attn_mask._t))
 
 
 class ReLU(_nn.Layer):
@@ -150,8 +128,7 @@ class BatchNorm(_nn.Layer):
         self.momentum, self.eps = momentum, epsilon
 
     def forward(self, x):
-        t = x._t.coalesce()
-        v = t.values()
+        i, v, shape, _ = K.coo_parts(K.to_coo(x._t))
         if self.training:
             mean, var = v.mean(0), v.var(0, unbiased=False)
             with torch.no_grad():
@@ -161,7 +138,7 @@ class BatchNorm(_nn.Layer):
         else:
             mean, var = self._mean._t, self._variance._t
         y = (v - mean) / torch.sqrt(var + self.eps) * self.weight._t + self.bias._t
-        return _wrap(torch.sparse_coo_tensor(t.indices(), y, t.shape))
+        return _wrap(K.make_coo(i, y, shape))
 
 
 SyncBatchNorm = BatchNorm

@@ -63,7 +63,7 @@ def test_sparse_coo_csr_ops():
     np.testing.assert_allclose(mm.to_dense().numpy(), (a @ b) * (dense != 0), rtol=1e-5, atol=1e-6)
     tr = paddle.sparse.transpose(coo, [1, 0])
     np.testing.assert_array_equal(tr.to_dense().numpy(), dense.T)
-    np.testing.assert_allclose(float(paddle.sparse.sum(coo).numpy()), dense.sum())
+    np.testing.assert_allclose(float(paddle.sparse.sum(coo).to_dense().numpy()[0]), dense.sum())  # sparse [1]
     np.testing.assert_array_equal(paddle.sparse.add(coo, coo).to_dense().numpy(), 2 * dense)
     # submanifold conv keeps the active set
     x = np.zeros((1, 4, 4, 4, 2), dtype="float32")
