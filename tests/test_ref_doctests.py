@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = "/root/reference"
 
 MODULES = ["tensor", "nn/functional", "nn/layer", "fft.py", "signal.py", "geometric", "autograd",
-           "audio/functional", "distribution"]
+           "audio/functional", "distribution", "sparse"]
 
 
 @pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "python", "paddle")), reason="reference tree not present")
