@@ -2,7 +2,9 @@
 load_inference_model:777, save/load:1467/1540, serialize_program, deserialize_program...).
 
 On-disk format (ours, not protobuf): ``<prefix>.pdmodel`` is a JSON program (see
-``Program.to_dict``) and ``<prefix>.pdiparams`` is a ``paddle.save`` dict name -> ndarray of every
+``Program.to_dict``) and ``<prefix>.pdiparams`` holds the parameters in the reference save_combine binary
+layout (framework/combine_io.py; names in the program's "params" list, sorted) — previously a ``paddle.save``
+dict name -> ndarray of every
 parameter / captured constant. Both load without executing anything from the files.
 """
 from __future__ import annotations
@@ -92,16 +94,26 @@ def write_program(path_prefix, prog, fetch_slots):
         os.makedirs(d, exist_ok=True)
     names = _const_names(prog)
     used = _used_consts(prog, prog.nodes)
+    order = sorted(used, key=lambda i: names[i])  # the reference writes persistables sorted by name
+    d = prog.to_dict(fetch_slots, names)
+    d["params"] = [names[i] for i in order]
     with open(path_prefix + ".pdmodel", "w") as f:
-        json.dump(prog.to_dict(fetch_slots, names), f)
-    _io.save({names[i]: _wrap(prog._consts[i].detach()) for i in sorted(used)}, path_prefix + ".pdiparams")
+        json.dump(d, f)
+    # parameters in the reference save_combine layout (framework/combine_io.py)
+    from ..framework.combine_io import write_combined
+    write_combined(path_prefix + ".pdiparams", [prog._consts[i].detach() for i in order])
 
 
 def read_program(path_prefix, device=None, params_file=None):
     with open(path_prefix + ".pdmodel" if not path_prefix.endswith(".pdmodel") else path_prefix) as f:
         d = json.load(f)
     base = path_prefix[:-len(".pdmodel")] if path_prefix.endswith(".pdmodel") else path_prefix
-    sd = _io.load(params_file or base + ".pdiparams")
+    pfile = params_file or base + ".pdiparams"
+    from ..framework.combine_io import is_combined, read_combined
+    if is_combined(pfile):
+        sd = dict(zip(d.get("params", []), read_combined(pfile)))
+    else:  # files written before the save_combine layout: a restricted-unpickler paddle.save dict
+        sd = _io.load(pfile)
     consts = {}
     for k, v in sd.items():
         t = v._t if isinstance(v, Tensor) else torch.as_tensor(np.asarray(v))
