@@ -116,7 +116,7 @@ def read_program(path_prefix, device=None, params_file=None):
         sd = _io.load(pfile)
     consts = {}
     for k, v in sd.items():
-        t = v._t if isinstance(v, Tensor) else torch.as_tensor(np.asarray(v))
+        t = v._t if isinstance(v, Tensor) else v if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v))
         if device is not None:
             t = t.to(device)
         consts[k] = t

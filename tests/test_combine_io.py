@@ -59,3 +59,23 @@ def test_inference_model_uses_the_combined_layout(tmp_path):
         np.testing.assert_allclose(got, ref, rtol=1e-6)
     finally:
         paddle.disable_static()
+
+
+def test_bf16_model_jit_save_and_predictor(tmp_path):
+    """bf16 parameters come back from the combined file as bf16 torch tensors (no numpy hop)."""
+    from paddlepaddle_amd.static import InputSpec
+    paddle.seed(0)
+    paddle.set_default_dtype("bfloat16")
+    try:
+        net = paddle.nn.Linear(8, 4)
+        x = paddle.randn([2, 8]).astype("bfloat16")
+        ref = net(x)
+        prefix = str(tmp_path / "lin")
+        paddle.jit.save(net, prefix, input_spec=[InputSpec([None, 8], "bfloat16", "x")])
+    finally:
+        paddle.set_default_dtype("float32")
+    cfg = paddle.inference.Config(prefix + ".pdmodel", prefix + ".pdiparams")
+    cfg.disable_gpu()
+    pred = paddle.inference.create_predictor(cfg)
+    out, = pred.run([x])
+    np.testing.assert_allclose(out.astype("float32").numpy(), ref.astype("float32").numpy(), rtol=0, atol=0)
