@@ -74,6 +74,11 @@ struct GemmArgs {
   // p = (n, ho, wo), k = (kh * KW + kw) * C + c; out-of-image taps read the 128-byte zero page
   const uint16_t* zero;
   int cH, cW, cC, cHo, cWo, cKW, cStride, cPadH, cPadW, cDil;
+  // balanced tail (ping-pong kernel): tiles [full_tiles, tiles) are split over K into tail_split slices
+  // (workgroups full_tiles + u, u = local tile * tail_split + slice) that write fp32 256x256 partials to
+  // tail_ws; gemm_tail_reduce_k sums them and applies the epilogue. tail_split == 0: no tail.
+  int full_tiles, tail_split;
+  float* tail_ws;
 };
 
 // split-K view: slice blockIdx.y of K (p.K elements each) and its own fp32 output slab
@@ -391,9 +396,30 @@ __device__ __forceinline__ void vm_wait(int n) {
   }
 }
 
+// grouped tile order (8 m-tiles per group, so neighbouring workgroups share B panels)
+__device__ __forceinline__ void tile_coords(int pid, int tiles_m, int tiles_n, int* tm, int* tn) {
+  constexpr int GM = 8;
+  const int per_group = GM * tiles_n;
+  const int first_m = (pid / per_group) * GM;
+  const int gsz = min(tiles_m - first_m, GM);
+  *tm = first_m + (pid % per_group) % gsz;
+  *tn = (pid % per_group) / gsz;
+}
+
+template <int V>
+struct IntC {
+  static constexpr int value = V;
+};
+using H0_ = IntC<0>;
+using H1_ = IntC<1>;
+using H2_ = IntC<2>;
+using H3_ = IntC<3>;
+using True_ = IntC<1>;
+using False_ = IntC<0>;
+
 template <bool AK, bool BKM>
 __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p0) {
-  const GemmArgs p = split_view<AK, BKM>(p0);
+  GemmArgs p = split_view<AK, BKM>(p0);
   constexpr int HALF = 128 * kBK * 2;  // 16 KiB
   constexpr int STAGE = 4 * HALF;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -401,15 +427,25 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p0) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 2, wn = wave & 3;
 
-  const int nwg = p.tiles_m * p.tiles_n;
-  const int pid = xcd_remap((int)blockIdx.x, nwg);
-  constexpr int GM = 8;
-  const int per_group = GM * p.tiles_n;
-  const int gid = pid / per_group;
-  const int first_m = gid * GM;
-  const int gsz = min(p.tiles_m - first_m, GM);
-  const int tm = first_m + (pid % per_group) % gsz;
-  const int tn = (pid % per_group) / gsz;
+  // Balanced tail: the first full_tiles workgroups (a whole number of waves over the CUs) own whole
+  // tiles; the remaining tiles are cut along K so the last wave is as wide as the chip (320 tiles of a
+  // 4096 x 5120 output on 256 CUs: 256 whole + 64 x 4 quarter tiles = 1.25 tile-times instead of 2).
+  const int bid = (int)blockIdx.x;
+  int pid;
+  float* tail_out = nullptr;
+  if (p.tail_split > 0 && bid >= p.full_tiles) {
+    const int u = bid - p.full_tiles;
+    const int ks = u % p.tail_split;
+    pid = p.full_tiles + u / p.tail_split;
+    p.K /= p.tail_split;
+    p.a += (int64_t)ks * p.K * (AK ? 1 : p.lda);
+    p.b += (int64_t)ks * p.K * (BKM ? 1 : p.ldb);
+    tail_out = p.tail_ws + (int64_t)u * 65536;
+  } else {
+    pid = xcd_remap(bid, p.tail_split > 0 ? p.full_tiles : p.tiles_m * p.tiles_n);
+  }
+  int tm, tn;
+  tile_coords(pid, p.tiles_m, p.tiles_n, &tm, &tn);
   const int m0 = tm * 256, n0 = tn * 256;
   const int nk = p.K / kBK;
 
@@ -420,6 +456,15 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p0) {
     if (h == 0) stage<128, AK>(p.a, p.lda, m0, p.M, t * kBK, dst, wave, lane);
     else if (h == 2) stage<128, AK>(p.a, p.lda, m0 + 128, p.M, t * kBK, dst, wave, lane);
     else if (h == 1) stage<128, BKM>(p.b, p.ldb, n0, p.N, t * kBK, dst, wave, lane);
+    else stage<128, BKM>(p.b, p.ldb, n0 + 128, p.N, t * kBK, dst, wave, lane);
+  };
+  // the same with the half known at compile time (steady-state body: no branch on h)
+  auto issue_h = [&](int t, auto hc) {
+    constexpr int h = decltype(hc)::value;
+    char* dst = smem + (t & 1) * STAGE + h * HALF;
+    if constexpr (h == 0) stage<128, AK>(p.a, p.lda, m0, p.M, t * kBK, dst, wave, lane);
+    else if constexpr (h == 2) stage<128, AK>(p.a, p.lda, m0 + 128, p.M, t * kBK, dst, wave, lane);
+    else if constexpr (h == 1) stage<128, BKM>(p.b, p.ldb, n0, p.N, t * kBK, dst, wave, lane);
     else stage<128, BKM>(p.b, p.ldb, n0 + 128, p.N, t * kBK, dst, wave, lane);
   };
 
@@ -454,20 +499,29 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p0) {
   bf16x8_t af[4][2], bl[2][2], br[2][2];
   const int ar = wm * 64, bc = wn * 32;
 
-#pragma unroll 1
-  for (int t = 0; t < nk; ++t) {
+  // One K-tile = 4 phases. STEADY (t <= nk - 3): every issue happens and every wait count is the
+  // constant of the formula above (issued - jstar = 3, 5, 4 half-tiles -> vmcnt 6, 10, 8), so the body
+  // has no branches; the last two tiles run the generic body with clamped counts.
+  auto ktile = [&](int t, auto steady) {
+    constexpr bool S = decltype(steady)::value;
     const char* buf = smem + (t & 1) * STAGE;
     const int ph = 4 * t;
     // ---- phase 0: read A-top + B-left; issue j = ph + 6; MFMA (top, L)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int j = 0; j < 2; ++j) bl[j][ks] = frag<128, BKM>(buf + HALF, bc + j * 16, ks, lane);
 #pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
       for (int i = 0; i < 4; ++i) af[i][ks] = frag<128, AK>(buf, ar + i * 16, ks, lane);
+    if (S) {
+      issue_h(t + 1, H2_{});
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // B-right of this tile, read in phase 1
+    } else {
+      if (ph + 6 <= last_j) issue(ph + 6);
+      wait_for(ph, ph + 3);
     }
-    if (ph + 6 <= last_j) issue(ph + 6);
-    wait_for(ph, ph + 3);  // B-right of this tile, read in phase 1
     bar();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -484,8 +538,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p0) {
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int j = 0; j < 2; ++j) br[j][ks] = frag<128, BKM>(buf + 3 * HALF, bc + j * 16, ks, lane);
-    if (ph + 7 <= last_j) issue(ph + 7);
-    wait_for(ph + 1, ph + 2);  // A-bottom of this tile, read in phase 2
+    if (S) {
+      issue_h(t + 1, H3_{});
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // A-bottom of this tile, read in phase 2
+    } else {
+      if (ph + 7 <= last_j) issue(ph + 7);
+      wait_for(ph + 1, ph + 2);
+    }
     bar();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -502,7 +561,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p0) {
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int i = 0; i < 4; ++i) af[i][ks] = frag<128, AK>(buf + 2 * HALF, ar + i * 16, ks, lane);
-    if (ph + 8 <= last_j) issue(ph + 8);
+    if (S) issue_h(t + 2, H0_{});
+    else if (ph + 8 <= last_j) issue(ph + 8);
     bar();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -515,8 +575,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p0) {
     __builtin_amdgcn_s_setprio(0);
     bar();
     // ---- phase 3: issue j = ph + 9; wait for H0/H1 of tile t+1; MFMA (bottom, R)
-    if (ph + 9 <= last_j) issue(ph + 9);
-    if (t + 1 < nk) wait_for(ph + 3, ph + 5);
+    if (S) {
+      issue_h(t + 2, H1_{});
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      if (ph + 9 <= last_j) issue(ph + 9);
+      if (t + 1 < nk) wait_for(ph + 3, ph + 5);
+    }
     bar();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -528,8 +593,31 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p0) {
           acc[1][i][1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(br[j][ks], af[i][ks], acc[1][i][1][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     bar();
-  }
+  };
+  const int nsteady = max(nk - 2, 0);
+  int t = 0;
+#pragma unroll 1
+  for (; t < nsteady; ++t) ktile(t, True_{});
+#pragma unroll 1
+  for (; t < nk; ++t) ktile(t, False_{});
   if (!lag) bar();
+
+  if (tail_out) {  // K-slice of a tail tile: raw fp32 partial, row-major 256 x 256
+#pragma unroll
+    for (int bh = 0; bh < 2; ++bh)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ah = 0; ah < 2; ++ah)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = ah * 128 + ar + i * 16 + (lane & 15);
+            const int c = bh * 128 + bc + j * 16 + 4 * (lane >> 4);
+            const f32x4 v = acc[ah][i][bh][j];
+            *reinterpret_cast<float4*>(tail_out + r * 256 + c) = make_float4(v[0], v[1], v[2], v[3]);
+          }
+    return;
+  }
 
   // ---- epilogue
   const int flags = p.flags;
@@ -815,17 +903,21 @@ int launch3s(const GemmArgs& a0, int splits, hipStream_t st) {
 }
 
 template <bool AK, bool BKM>
-int launch256(const GemmArgs& a0, int splits, hipStream_t st) {
+int launch256(const GemmArgs& a0, int splits, hipStream_t st, int grid = 0) {
   GemmArgs a = a0;
   a.tiles_m = (a.M + 255) / 256;
   a.tiles_n = (a.N + 255) / 256;
+  if (!grid) {
+    grid = a.tiles_m * a.tiles_n;
+    a.tail_split = 0;
+  }
   const int smem = 2 * 4 * 128 * kBK * 2;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKM>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr_set = true;
   }
-  hipLaunchKernelGGL((gemm256_kernel<AK, BKM>), dim3(a.tiles_m * a.tiles_n, splits), dim3(kThreads), smem, st, a);
+  hipLaunchKernelGGL((gemm256_kernel<AK, BKM>), dim3(grid, splits), dim3(kThreads), smem, st, a);
   return (int)hipGetLastError();
 }
 
@@ -979,7 +1071,126 @@ __global__ __launch_bounds__(256) void gemm_small_m_reduce_k(const float* __rest
   *reinterpret_cast<uint2*>(c + (int64_t)m * ldc + n) = make_uint2(pack_bf16(acc.x, acc.y), pack_bf16(acc.z, acc.w));
 }
 
+// Balanced-tail reduction: tail tile b (blockIdx.x) = tile full_tiles + b; each thread sums the
+// tail_split fp32 partials of 4 consecutive columns and applies the epilogue of the main kernel.
+__global__ __launch_bounds__(256) void gemm_tail_reduce_k(GemmArgs p) {
+  const int b = blockIdx.x;
+  int tm, tn;
+  tile_coords(p.full_tiles + b, p.tiles_m, p.tiles_n, &tm, &tn);
+  const int e = (blockIdx.y * 256 + threadIdx.x) * 4;  // element of the 256 x 256 tile
+  const int r = e >> 8, c = e & 255;
+  const int m = tm * 256 + r, n = tn * 256 + c;
+  if (m >= p.M || n >= p.N) return;
+  const float* src = p.tail_ws + (int64_t)b * p.tail_split * 65536 + e;
+  float4 a = *reinterpret_cast<const float4*>(src);
+  for (int k = 1; k < p.tail_split; ++k) {
+    const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)k * 65536);
+    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+  }
+  const int flags = p.flags;
+  float bv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (flags & kEpiBias) {
+    const uint2 braw = *reinterpret_cast<const uint2*>(p.bias + n);
+    bv[0] = lo_bf16(braw.x); bv[1] = hi_bf16(braw.x); bv[2] = lo_bf16(braw.y); bv[3] = hi_bf16(braw.y);
+  }
+  float v[4] = {a.x * p.alpha + bv[0], a.y * p.alpha + bv[1], a.z * p.alpha + bv[2], a.w * p.alpha + bv[3]};
+  const int64_t off = (int64_t)m * p.ldc + n;
+  if (flags & kEpiAux)
+    *reinterpret_cast<uint2*>(p.aux + off) = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
+  if (flags & kEpiGelu) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = gelu_tanh(v[q]);
+  }
+  if (flags & kEpiOutF32) {
+    float4* cp = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.c) + off);
+    if (flags & kEpiAccum) {
+      const float4 o = *cp;
+      v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+    }
+    *cp = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    uint2* cp = reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.c) + off);
+    if (flags & kEpiAccum) {
+      const uint2 o = *cp;
+      v[0] += lo_bf16(o.x); v[1] += hi_bf16(o.x); v[2] += lo_bf16(o.y); v[3] += hi_bf16(o.y);
+    }
+    *cp = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
+  }
+}
+
+int device_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  return cus;
+}
+
+// Tail plan of the ping-pong kernel: tiles beyond the last whole wave are split along K so the last wave
+// has about one workgroup per CU. Only when the remainder covers at most half the chip and every slice
+// keeps at least 4 K-tiles.
+void pp_plan(int64_t M, int64_t N, int64_t K, int cus, int* full, int* split) {
+  const int64_t T = ((M + 255) / 256) * ((N + 255) / 256);
+  const int64_t nk = K / kBK;
+  *full = (int)T;
+  *split = 0;
+  if (T <= cus) return;
+  const int64_t r = T % cus;
+  if (r == 0 || 2 * r > cus) return;
+  int sp = 1;
+  while (r * sp * 2 <= cus && nk % (sp * 2) == 0 && nk / (sp * 2) >= 4) sp *= 2;
+  if (sp == 1) return;
+  *full = (int)(T - r);
+  *split = sp;
+}
+
 }  // namespace
+
+// Workspace (bytes) the ping-pong GEMM needs for its balanced tail (0: none).
+PA_EXPORT int64_t pa_gemm_pp_ws_bytes(int64_t M, int64_t N, int64_t K) {
+  int full, split;
+  pp_plan(M, N, K, device_cus(), &full, &split);
+  if (!split) return 0;
+  const int64_t T = ((M + 255) / 256) * ((N + 255) / 256);
+  return (T - full) * split * 65536 * 4;
+}
+
+// Ping-pong 256x256 GEMM (same operands / flags as pa_gemm_bf16, no split-K) with the balanced tail;
+// ws: pa_gemm_pp_ws_bytes(M, N, K) bytes (may be null when that is 0).
+PA_EXPORT int pa_gemm_bf16_pp(const void* a, const void* b, void* c, const void* bias, void* aux, int64_t M, int64_t N,
+                              int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor, int b_kmajor, int flags,
+                              float alpha, void* ws, hipStream_t st) {
+  if (K % kBK != 0 || N % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || ldc % 4 != 0) return 1;
+  if (!a_kmajor && M % 8 != 0) return 1;
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  GemmArgs g{};
+  g.a = (const uint16_t*)a; g.b = (const uint16_t*)b; g.c = c;
+  g.bias = (const uint16_t*)bias; g.aux = (uint16_t*)aux;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.flags = flags; g.alpha = alpha;
+  g.c_split = M * ldc;
+  int full, split;
+  pp_plan(M, N, K, device_cus(), &full, &split);
+  if (split && !ws) split = 0;
+  g.tiles_m = (int)((M + 255) / 256);
+  g.tiles_n = (int)((N + 255) / 256);
+  const int T = g.tiles_m * g.tiles_n;
+  g.full_tiles = split ? full : T;
+  g.tail_split = split;
+  g.tail_ws = (float*)ws;
+  const int grid = split ? full + (T - full) * split : T;
+  int rc;
+  if (a_kmajor && !b_kmajor) rc = launch256<true, false>(g, 1, st, grid);
+  else if (a_kmajor && b_kmajor) rc = launch256<true, true>(g, 1, st, grid);
+  else if (!a_kmajor && !b_kmajor) rc = launch256<false, false>(g, 1, st, grid);
+  else rc = launch256<false, true>(g, 1, st, grid);
+  if (rc || !split) return rc;
+  hipLaunchKernelGGL(gemm_tail_reduce_k, dim3(T - full, 64), dim3(256), 0, st, g);
+  return (int)hipGetLastError();
+}
 
 // C = epi(alpha * A.B). A: [M][K] (a_kmajor) or [K][M]; B: [N][K] (b_kmajor) or [K][N].
 // Requirements (checked by the Python wrapper too): K % 64 == 0, 16-byte aligned rows

@@ -112,6 +112,9 @@ def _declare(L):
         "pa_colsum": [_vp, _vp, _vp, _i64, _i64, _i32, _vp],
         "pa_gemm_bf16": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _f32,
                          _i32, _i32, _vp],
+        "pa_gemm_bf16_pp": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _f32,
+                            _vp, _vp],
+        "pa_gemm_pp_ws_bytes": [_i64, _i64, _i64],
         "pa_gemm_small_m": [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp],
         "pa_conv2d_nhwc_fwd": [_vp, _vp, _vp, _vp, _vp] + [_i32] * 13 + [_vp],
         "pa_conv2d_nhwc_wgrad": [_vp, _vp, _vp, _vp] + [_i32] * 15 + [_vp],
@@ -141,7 +144,10 @@ def _declare(L):
         if fn is None:
             continue
         fn.argtypes = args
-        fn.restype = _i32
+        fn.restype = _i64 if name in _RET_I64 else _i32
+
+
+_RET_I64 = {"pa_gemm_pp_ws_bytes"}
 
 
 def has(name):

@@ -76,6 +76,12 @@ def gemm(a, b, bias=None, gelu=False, aux=None, out=None, accumulate=False, alph
         flags |= EPI_OUT_F32
     if bn is None:
         bn = _pick_bn(M, N, bk)
+    if bn == 1 and L.has("pa_gemm_bf16_pp"):  # ping-pong 256x256 with the balanced K-split tail
+        nb = int(L.lib().pa_gemm_pp_ws_bytes(M, N, K))
+        ws = torch.empty(nb // 4, dtype=torch.float32, device=a.device) if nb else None
+        L.call("pa_gemm_bf16_pp", L.ptr(a), L.ptr(b), L.ptr(out), L.ptr(bias), L.ptr(aux), M, N, K, lda, ldb,
+               out.stride(0), int(ak), int(bk), flags, float(alpha), L.ptr(ws), L.stream_ptr())
+        return out
     L.call("pa_gemm_bf16", L.ptr(a), L.ptr(b), L.ptr(out), L.ptr(bias), L.ptr(aux), M, N, K, lda, ldb, out.stride(0),
            int(ak), int(bk), flags, float(alpha), int(bn), 1, L.stream_ptr())
     return out
@@ -106,9 +112,13 @@ def pick_splits(M, N, K, bn=256, cus=256, max_ws_bytes=256 << 20):
 
 
 def _pick_bn(M, N, b_kmajor, cus=256):
-    """Kernel variant. Measured on MI355X (profiles/gemm_mfma_vs_hipblaslt.log): the 3-stage 256x160
-    kernel is the fastest whenever B is K-major (its 160-column MN-major image would read unaligned
-    320-B rows); otherwise the 2-stage 256x256 kernel, or 256x128 when that fills the CUs better."""
+    """Kernel variant. Measured on MI355X (profiles/gemm_mfma_vs_hipblaslt.log): the 4-phase ping-pong
+    256x256 kernel (code 1, with the balanced K-split tail) is the fastest of ours on every layout once the
+    output fills a wave of 256x256 tiles with M, N >= 1024. Below that: the 3-stage 256x160 kernel
+    whenever B is K-major (its 160-column MN-major image would read unaligned 320-B rows); otherwise the
+    2-stage 256x256 kernel, or 256x128 when that fills the CUs better."""
+    if M >= 1024 and N >= 1024 and -(-M // 256) * -(-N // 256) >= cus:
+        return 1
     if b_kmajor:
         return 160
 
@@ -166,15 +176,22 @@ def known(key):
     return _canon(key) in _CHOICE
 
 
+# bumped whenever what "hip" runs for a key changes (v2: the ping-pong kernel for large GEMMs), so
+# decisions timed against an older kernel set are not reused
+_TABLE_VERSION = 2
+
+
 def _overlay_path():
     return os.environ.get("PADDLE_AMD_TUNING_FILE") or os.path.join(
-        os.path.expanduser("~"), ".cache", "paddlepaddle_amd", f"tuning_{_arch()}.json")
+        os.path.expanduser("~"), ".cache", "paddlepaddle_amd", f"tuning_{_arch()}_v{_TABLE_VERSION}.json")
 
 
 def _read_table(path):
     try:
         with open(path) as f:
             d = json.load(f)
+        if d.get("version", 1) != _TABLE_VERSION:
+            return {}
         return {_canon(json.loads(k)): v for k, v in d.get("choices", {}).items()}
     except (OSError, ValueError):
         return {}
@@ -202,7 +219,7 @@ def _persist(key, choice):
         cur[_key_str(key)] = choice
         tmp = f"{path}.{os.getpid()}.tmp"
         with open(tmp, "w") as f:
-            json.dump({"arch": _arch(), "choices": cur}, f, indent=0, sort_keys=True)
+            json.dump({"arch": _arch(), "version": _TABLE_VERSION, "choices": cur}, f, indent=0, sort_keys=True)
         os.replace(tmp, path)
     except OSError:  # read-only home: the decision still holds for this process
         pass
@@ -211,8 +228,9 @@ def _persist(key, choice):
 def dump_tuning_table(path):
     """Write every decision of this process (committed-table format)."""
     with open(path, "w") as f:
-        json.dump({"arch": _arch(), "choices": {_key_str(k): v for k, v in sorted(_CHOICE.items(), key=str)}}, f,
-                  indent=0, sort_keys=True)
+        json.dump({"arch": _arch(), "version": _TABLE_VERSION,
+                   "choices": {_key_str(k): v for k, v in sorted(_CHOICE.items(), key=str)}}, f, indent=0,
+                  sort_keys=True)
 
 
 def _capturing():

@@ -1,7 +1,6 @@
 #!/bin/bash
-# measure the per-shape GEMM / conv backend choices for the bench models and dump them (committed table source)
+# re-time every per-shape backend decision of the default bench (GPT-3 13B + ResNet-50) and dump the table
 source "$(dirname "$0")/gpu_steps.sh"
-export PADDLE_AMD_TUNING_FILE=/tmp/tuning_overlay.json
-PADDLE_AMD_TUNING_DUMP=gpurun_out/tuning_gpt_resnet.json step tune_bench 900 python bench.py --steps 2 --warmup 1
-PADDLE_AMD_TUNING_DUMP=gpurun_out/tuning_llama.json step tune_llama 900 python bench.py --model llama2-7b --seq-len 4096 --accum 2 --steps 1 --warmup 1
-step bench_tuned 600 python bench.py
+export PADDLE_AMD_TUNING_FILE=$R/gpurun_out/overlay.json
+TAIL=12 PADDLE_AMD_TUNING_DUMP=$R/gpurun_out/gfx950.json step bench_tune 900 python bench.py
+TAIL=12 step bench_tuned 900 python bench.py
