@@ -1,112 +1,306 @@
 """paddle.linalg. Reference: python/paddle/tensor/linalg.py, python/paddle/linalg.py.
-Dense factorizations run on rocSOLVER through ATen's HIP backend."""
+
+Design: seven LAPACK-class primitives run on rocSOLVER through ATen's HIP backend — LU with partial
+pivoting (``_lu``), Householder QR, SVD, the general and the symmetric eigensolver, Cholesky and the
+triangular solve. Everything else is composed here from those primitives and our own reductions / GEMMs,
+with the reference's semantics (defaults, tolerances, output dtypes, batching):
+  * norms: own reductions per order (vector p-norms, fro / nuc / 1 / inf / 2 matrix norms);
+  * det / slogdet from the LU diagonal and the pivot parity; solve / inverse / cholesky_solve /
+    cholesky_inverse as pivot gathers + two triangular solves;
+  * lu_unpack builds P from LAPACK's sequential row swaps;
+  * matrix_rank / pinv / cond / lstsq from singular (or symmetric eigen) values with the reference's
+    cut-offs; lstsq's 'gels' driver from QR, the others from the SVD;
+  * matrix_power by binary exponentiation; matrix_exp by scaling and squaring with the degree-13 Pade
+    approximant (Higham 2005); multi_dot with the optimal matrix-chain order (dynamic programme);
+  * householder_product / ormqr apply the elementary reflectors; cov / corrcoef with frequency and
+    analytic weights; svd_lowrank / pca_lowrank as the randomized range finder (Halko et al.).
+"""
 from __future__ import annotations
+
+import math
 
 import torch
 
-from ..framework.tensor import Tensor, _wrap
+from ..framework.tensor import Tensor, _wrap  # noqa: F401
 from ._helpers import T, axis_arg
-from .math import matmul, bmm, dot, mv, cross, inverse as inv  # noqa: F401
+from .math import matmul, bmm, dot, mv, cross  # noqa: F401
+
+_INF = float("inf")
+
+
+# ------------------------------------------------------------------ primitives (rocSOLVER)
+def _lu(a, pivot=True):
+    return torch.linalg.lu_factor_ex(a, pivot=pivot)
+
+
+def _tri(a, b, upper, left=True, unit=False):
+    return torch.linalg.solve_triangular(a, b, upper=upper, left=left, unitriangular=unit)
+
+
+def _svdvals(a):
+    return torch.linalg.svdvals(a)
+
+
+def _eye_like(a, n=None, m=None):
+    n = a.shape[-1] if n is None else n
+    m = n if m is None else m
+    return torch.eye(n, m, dtype=a.dtype, device=a.device).expand(*a.shape[:-2], n, m)
+
+
+def _real_dtype(t):
+    return t.real.dtype if t.is_complex() else t.dtype
+
+
+# ------------------------------------------------------------------ norms
+def _vnorm(t, p, dim, keepdim):
+    p = float(p)
+    a = t.abs()
+    if dim is None:
+        dims = tuple(range(t.dim()))
+    else:
+        dims = (dim,) if isinstance(dim, int) else tuple(dim)
+    if p == _INF:
+        r = a.amax(dim=dims, keepdim=keepdim) if t.dim() else a
+    elif p == -_INF:
+        r = a.amin(dim=dims, keepdim=keepdim) if t.dim() else a
+    elif p == 0:
+        r = (t != 0).sum(dim=dims, keepdim=keepdim).to(_real_dtype(t))
+    elif p == 1:
+        r = a.sum(dim=dims, keepdim=keepdim)
+    elif p == 2:
+        r = (a * a).sum(dim=dims, keepdim=keepdim).sqrt()
+    else:
+        r = a.pow(p).sum(dim=dims, keepdim=keepdim).pow(1.0 / p)
+    return r
+
+
+def _mnorm(t, p, dims, keepdim):
+    d0, d1 = (d % t.dim() for d in dims)
+    if p == "fro":
+        r = (t.abs() ** 2).sum(dim=(d0, d1), keepdim=True).sqrt()
+    elif p in ("nuc", 2, -2, 2.0, -2.0):
+        s = _svdvals(t.movedim((d0, d1), (-2, -1)))
+        v = s.sum(-1) if p == "nuc" else (s.amax(-1) if float(p) > 0 else s.amin(-1))
+        r = v[..., None, None].movedim((-2, -1), (d0, d1))
+    elif p in (1, -1, _INF, -_INF):
+        # 1: max column abs-sum; inf: max row abs-sum
+        col = float(p) in (1.0, -1.0)
+        s = t.abs().sum(dim=d0 if col else d1, keepdim=True)
+        r = s.amax(dim=d1 if col else d0, keepdim=True) if float(p) > 0 else s.amin(dim=d1 if col else d0,
+                                                                                     keepdim=True)
+    else:
+        raise ValueError(f"unsupported matrix norm order {p!r}")
+    return r if keepdim else r.squeeze(max(d0, d1)).squeeze(min(d0, d1))
 
 
 def norm(x, p=None, axis=None, keepdim=False, name=None):
     t = T(x)
     ax = axis_arg(axis)
+    if isinstance(ax, list):
+        ax = tuple(ax)
     if p is None or p == "fro":
         if ax is None:
-            return _wrap(torch.linalg.vector_norm(t.flatten(), 2) if t.dim() != 2 or p is None
-                         else torch.linalg.matrix_norm(t, "fro", keepdim=keepdim))
+            if t.dim() == 2 and p == "fro":
+                return _wrap(_mnorm(t, "fro", (0, 1), keepdim))
+            return _wrap(_vnorm(t.flatten(), 2, None, False).reshape([1] * t.dim() if keepdim else []))
         if isinstance(ax, tuple) and len(ax) == 2:
-            return _wrap(torch.linalg.matrix_norm(t, "fro", dim=ax, keepdim=keepdim))
-        return _wrap(torch.linalg.vector_norm(t, 2, dim=ax, keepdim=keepdim))
+            return _wrap(_mnorm(t, "fro", ax, keepdim))
+        return _wrap(_vnorm(t, 2, ax, keepdim))
     if p == "nuc":
-        return _wrap(torch.linalg.matrix_norm(t, "nuc", dim=ax or (-2, -1), keepdim=keepdim))
+        return _wrap(_mnorm(t, "nuc", ax or (-2, -1), keepdim))
     if isinstance(ax, tuple) and len(ax) == 2:
-        return _wrap(torch.linalg.matrix_norm(t, p, dim=ax, keepdim=keepdim))
+        return _wrap(_mnorm(t, p, ax, keepdim))
     if ax is None:
-        t = t.flatten()
-    return _wrap(torch.linalg.vector_norm(t, float(p), dim=ax, keepdim=keepdim))
+        r = _vnorm(t.flatten(), p, None, False)
+        return _wrap(r.reshape([1] * t.dim()) if keepdim else r)
+    return _wrap(_vnorm(t, p, ax, keepdim))
 
 
 def vector_norm(x, p=2.0, axis=None, keepdim=False, name=None):
-    return _wrap(torch.linalg.vector_norm(T(x), p, dim=axis_arg(axis), keepdim=keepdim))
+    ax = axis_arg(axis)
+    return _wrap(_vnorm(T(x), p, tuple(ax) if isinstance(ax, list) else ax, keepdim))
 
 
 def matrix_norm(x, p="fro", axis=[-2, -1], keepdim=False, name=None):
-    return _wrap(torch.linalg.matrix_norm(T(x), p, dim=tuple(axis), keepdim=keepdim))
+    return _wrap(_mnorm(T(x), p, tuple(axis), keepdim))
 
 
-def cond(x, p=None, name=None):
-    return _wrap(torch.linalg.cond(T(x), p))
+# ------------------------------------------------------------------ LU-based: det, slogdet, solve, inverse
+def _perm_from_pivots(piv, m):
+    """Row permutation of LAPACK's sequential swaps (1-based): row i of LU is row perm[i] of A."""
+    k = piv.shape[-1]
+    perm = torch.arange(m, device=piv.device).expand(*piv.shape[:-1], m).clone()
+    p = piv.long() - 1
+    for i in range(k):
+        j = p[..., i:i + 1]
+        pi = perm[..., i:i + 1].clone()
+        pj = perm.gather(-1, j)
+        perm[..., i:i + 1] = pj
+        perm.scatter_(-1, j, pi)
+    return perm
+
+
+def _pivot_sign(piv, dtype):
+    k = piv.shape[-1]
+    swaps = (piv.long() != torch.arange(1, k + 1, device=piv.device)).sum(-1)
+    return (1 - 2 * (swaps % 2)).to(dtype)
 
 
 def det(x, name=None):
-    return _wrap(torch.linalg.det(T(x)))
+    a = T(x)
+    lu_, piv, _ = _lu(a)
+    d = lu_.diagonal(dim1=-2, dim2=-1)
+    return _wrap(d.prod(-1) * _pivot_sign(piv, a.dtype))
 
 
 def slogdet(x, name=None):
-    s, l = torch.linalg.slogdet(T(x))
-    return _wrap(torch.stack([s, l]))
+    a = T(x)
+    lu_, piv, _ = _lu(a)
+    d = lu_.diagonal(dim1=-2, dim2=-1)
+    if a.is_complex():
+        sign = (d / d.abs()).prod(-1) * _pivot_sign(piv, a.dtype)
+    else:
+        sign = torch.sign(d).prod(-1) * _pivot_sign(piv, a.dtype)
+    logabs = d.abs().log().sum(-1)
+    return _wrap(torch.stack([sign.to(logabs.dtype) if not a.is_complex() else sign, logabs.to(sign.dtype)]))
 
 
-def matrix_rank(x, tol=None, hermitian=False, atol=None, rtol=None, name=None):
-    # phi's matrix_rank kernel returns int32 (reference docstring: dtype=int32)
-    return _wrap(torch.linalg.matrix_rank(T(x), atol=atol if tol is None else tol, rtol=rtol,
-                                          hermitian=hermitian).to(torch.int32))
+def _lu_solve(lu_, piv, b):
+    """A X = B with A = P L U (LU factors + pivots of A)."""
+    m = lu_.shape[-1]
+    perm = _perm_from_pivots(piv, m)
+    pb = b.gather(-2, perm.unsqueeze(-1).expand(*perm.shape, b.shape[-1])) if b.dim() == perm.dim() + 1 else \
+        torch.take_along_dim(b, perm.unsqueeze(-1), dim=-2)
+    z = _tri(lu_, pb, upper=False, unit=True)
+    return _tri(lu_, z, upper=True)
 
 
-def matrix_power(x, n, name=None):
-    return _wrap(torch.linalg.matrix_power(T(x), n))
+def solve(x, y, left=True, name=None):
+    a, b = T(x), T(y)
+    vec = b.dim() == a.dim() - 1 or (b.dim() == 1)
+    if vec:
+        b = b.unsqueeze(-1)
+    if not left:  # X A = B  <=>  A^T X^T = B^T
+        a, b = a.transpose(-1, -2), b.transpose(-1, -2)
+    batch = torch.broadcast_shapes(a.shape[:-2], b.shape[:-2])
+    a = a.expand(*batch, *a.shape[-2:])
+    b = b.expand(*batch, *b.shape[-2:])
+    lu_, piv, _ = _lu(a)
+    out = _lu_solve(lu_, piv, b)
+    if not left:
+        out = out.transpose(-1, -2)
+    return _wrap(out.squeeze(-1) if vec else out)
 
 
-def matrix_exp(x, name=None):
-    return _wrap(torch.linalg.matrix_exp(T(x)))
+def _inv(a):
+    lu_, piv, _ = _lu(a)
+    return _lu_solve(lu_, piv, _eye_like(a).contiguous())
 
 
+def inv(x, name=None):
+    return _wrap(_inv(T(x)))
+
+
+def triangular_solve(x, y, upper=True, transpose=False, unitriangular=False, name=None):
+    a = T(x)
+    if transpose:
+        a = a.transpose(-1, -2)
+        upper = not upper
+    return _wrap(_tri(a, T(y), upper=upper, unit=unitriangular))
+
+
+# ------------------------------------------------------------------ Cholesky-based
 def cholesky(x, upper=False, name=None):
     return _wrap(torch.linalg.cholesky(T(x), upper=upper))
 
 
+def _chol_solve(b, u, upper):
+    if upper:  # A = U^H U
+        z = _tri(u.mH, b, upper=False)
+        return _tri(u, z, upper=True)
+    z = _tri(u, b, upper=False)  # A = L L^H
+    return _tri(u.mH, z, upper=True)
+
+
 def cholesky_solve(x, y, upper=False, name=None):
-    return _wrap(torch.cholesky_solve(T(x), T(y), upper))
+    return _wrap(_chol_solve(T(x), T(y), upper))
 
 
 def cholesky_inverse(x, upper=False, name=None):
-    return _wrap(torch.cholesky_inverse(T(x), upper))
+    u = T(x)
+    return _wrap(_chol_solve(_eye_like(u).contiguous(), u, upper))
 
 
+# ------------------------------------------------------------------ QR / LU factor outputs
 def qr(x, mode="reduced", name=None):
     q, r = torch.linalg.qr(T(x), mode)
     return (_wrap(r) if mode == "r" else (_wrap(q), _wrap(r)))
 
 
 def lu(x, pivot=True, get_infos=False, name=None):
-    lu_, piv, info = torch.linalg.lu_factor_ex(T(x), pivot=pivot)
+    lu_, piv, info = _lu(T(x), pivot=pivot)
     res = (_wrap(lu_), _wrap(piv.to(torch.int32)))
     return res + (_wrap(info.to(torch.int32)),) if get_infos else res
 
 
 def lu_unpack(x, y, unpack_ludata=True, unpack_pivots=True, name=None):
-    p, l, u = torch.lu_unpack(T(x), T(y))
-    return _wrap(p), _wrap(l), _wrap(u)
+    a, piv = T(x), T(y)
+    m, n = a.shape[-2:]
+    k = min(m, n)
+    L = U = P = None
+    if unpack_ludata:
+        L = a[..., :, :k].tril(-1) + torch.eye(m, k, dtype=a.dtype, device=a.device)
+        U = a[..., :k, :].triu()
+    if unpack_pivots:
+        perm = _perm_from_pivots(piv, m)
+        eye = torch.eye(m, dtype=a.dtype, device=a.device)
+        P = eye[perm].transpose(-1, -2)  # A = P L U
+    empty = torch.empty(0, dtype=a.dtype, device=a.device)
+    return (_wrap(P if P is not None else empty), _wrap(L if L is not None else empty),
+            _wrap(U if U is not None else empty))
 
 
+# ------------------------------------------------------------------ SVD / eigen
 def svd(x, full_matrices=False, name=None):
     u, s, vh = torch.linalg.svd(T(x), full_matrices=full_matrices)
     return _wrap(u), _wrap(s), _wrap(vh)
 
 
 def svdvals(x, name=None):
-    return _wrap(torch.linalg.svdvals(T(x)))
+    return _wrap(_svdvals(T(x)))
+
+
+def _svd_lowrank(a, q, niter, m_sub=None):
+    if m_sub is not None:
+        a = a - m_sub
+    m, n = a.shape[-2:]
+    tall = m >= n
+    if not tall:  # work on A^H so the range finder runs on the short side
+        a = a.mH
+        m, n = n, m
+    omega = torch.randn(*a.shape[:-2], n, q, dtype=a.dtype, device=a.device)
+    qm = torch.linalg.qr(a @ omega).Q
+    for _ in range(niter):
+        qz = torch.linalg.qr(a.mH @ qm).Q
+        qm = torch.linalg.qr(a @ qz).Q
+    ub, s, vh = torch.linalg.svd(qm.mH @ a, full_matrices=False)
+    u, v = qm @ ub, vh.mH
+    return (u, s, v) if tall else (v, s, u)
 
 
 def svd_lowrank(x, q=None, niter=2, M=None, name=None):
-    u, s, v = torch.svd_lowrank(T(x), q=q or 6, niter=niter, M=T(M))
+    a = T(x)
+    q = 6 if q is None else q
+    u, s, v = _svd_lowrank(a, q, niter, T(M) if M is not None else None)
     return _wrap(u), _wrap(s), _wrap(v)
 
 
 def pca_lowrank(x, q=None, center=True, niter=2, name=None):
-    u, s, v = torch.pca_lowrank(T(x), q=q, center=center, niter=niter)
+    a = T(x)
+    m, n = a.shape[-2:]
+    q = min(6, m, n) if q is None else q
+    mean = a.mean(-2, keepdim=True) if center else None
+    u, s, v = _svd_lowrank(a, q, niter, mean)
     return _wrap(u), _wrap(s), _wrap(v)
 
 
@@ -128,52 +322,253 @@ def eigvalsh(x, UPLO="L", name=None):
     return _wrap(torch.linalg.eigvalsh(T(x), UPLO))
 
 
-def solve(x, y, left=True, name=None):
-    return _wrap(torch.linalg.solve(T(x), T(y), left=left))
-
-
-def triangular_solve(x, y, upper=True, transpose=False, unitriangular=False, name=None):
+# ------------------------------------------------------------------ spectrum-derived
+def cond(x, p=None, name=None):
     a = T(x)
-    if transpose:
-        a = a.transpose(-1, -2)
-        upper = not upper
-    return _wrap(torch.linalg.solve_triangular(a, T(y), upper=upper, unitriangular=unitriangular))
+    if p is None or p in (2, -2):
+        s = _svdvals(a)
+        r = s.amax(-1) / s.amin(-1) if p in (None, 2) else s.amin(-1) / s.amax(-1)
+        return _wrap(r)
+    return _wrap(_mnorm(a, p, (-2, -1), False) * _mnorm(_inv(a), p, (-2, -1), False))
 
 
-def lstsq(x, y, rcond=None, driver=None, name=None):
-    r = torch.linalg.lstsq(T(x), T(y), rcond=rcond, driver=driver)
-    return _wrap(r.solution), _wrap(r.residuals), _wrap(r.rank.to(torch.int32)), _wrap(r.singular_values)
+def matrix_rank(x, tol=None, hermitian=False, atol=None, rtol=None, name=None):
+    a = T(x)
+    s = torch.linalg.eigvalsh(a).abs() if hermitian else _svdvals(a)
+    smax = s.amax(-1, keepdim=True) if s.shape[-1] else torch.zeros_like(s[..., :1])
+    if tol is not None:
+        thr = T(tol).unsqueeze(-1) if isinstance(T(tol), torch.Tensor) and T(tol).dim() else T(tol)
+    else:
+        eps = torch.finfo(s.dtype).eps * max(a.shape[-2:])
+        at = 0.0 if atol is None else (T(atol).unsqueeze(-1) if isinstance(T(atol), torch.Tensor) else atol)
+        if rtol is None:
+            rt = eps if atol is None else 0.0
+        else:
+            rt = T(rtol).unsqueeze(-1) if isinstance(T(rtol), torch.Tensor) else rtol
+        thr = torch.maximum(torch.as_tensor(at, dtype=s.dtype, device=s.device), rt * smax)
+    # phi's matrix_rank kernel returns int32 (reference docstring: dtype=int32)
+    return _wrap((s > thr).sum(-1).to(torch.int32))
 
 
 def pinv(x, rcond=1e-15, hermitian=False, name=None):
-    return _wrap(torch.linalg.pinv(T(x), rtol=rcond, hermitian=hermitian))
+    a = T(x)
+    if hermitian:
+        w, v = torch.linalg.eigh(a)
+        cut = rcond * w.abs().amax(-1, keepdim=True)
+        winv = torch.where(w.abs() > cut, 1.0 / w, torch.zeros_like(w))
+        return _wrap((v * winv.unsqueeze(-2).to(v.dtype)) @ v.mH)
+    u, s, vh = torch.linalg.svd(a, full_matrices=False)
+    cut = rcond * s.amax(-1, keepdim=True)
+    sinv = torch.where(s > cut, 1.0 / s, torch.zeros_like(s))
+    return _wrap((vh.mH * sinv.unsqueeze(-2).to(vh.dtype)) @ u.mH)
+
+
+def lstsq(x, y, rcond=None, driver=None, name=None):
+    """min ||A X - B||. 'gels' (the reference's GPU driver): QR (full-rank A); 'gelsy' / 'gelsd' / 'gelss':
+    SVD pseudo-inverse with the rcond cut-off (rank and, for gelsd / gelss, singular values reported).
+    Residuals (sum of squares per column) only for tall full-rank problems, like LAPACK."""
+    a, b = T(x), T(y)
+    if driver is None:
+        driver = "gels" if a.is_cuda else "gelsy"
+    m, n = a.shape[-2:]
+    vec = b.dim() == a.dim() - 1
+    if vec:
+        b = b.unsqueeze(-1)
+    empty = torch.empty(0, dtype=a.dtype, device=a.device)
+    sv = empty
+    if driver == "gels":
+        if m >= n:
+            q, r = torch.linalg.qr(a, "reduced")
+            sol = _tri(r, q.mH @ b, upper=True)
+        else:  # minimum-norm solution through A^H = Q R
+            q, r = torch.linalg.qr(a.mH, "reduced")
+            sol = q @ _tri(r.mH, b, upper=False)
+        rank = torch.full(a.shape[:-2], min(m, n), dtype=torch.int32, device=a.device)
+        full = True
+    else:
+        u, s, vh = torch.linalg.svd(a, full_matrices=False)
+        rc = torch.finfo(s.dtype).eps * max(m, n) if rcond is None else rcond
+        keep = s > rc * s.amax(-1, keepdim=True)
+        sinv = torch.where(keep, 1.0 / s, torch.zeros_like(s))
+        sol = vh.mH @ (sinv.unsqueeze(-1).to(u.dtype) * (u.mH @ b))
+        rank = keep.sum(-1).to(torch.int32)
+        full = bool((rank == n).all()) if rank.numel() else True
+        if driver in ("gelsd", "gelss"):
+            sv = s
+    if m > n and full:
+        res = ((a @ sol - b).abs() ** 2).sum(-2)
+    else:
+        res = empty
+    if driver == "gels":
+        rank = torch.empty(0, dtype=torch.int32, device=a.device)
+    if vec:
+        sol = sol.squeeze(-1)
+        if res.numel():
+            res = res.squeeze(-1)
+    return _wrap(sol), _wrap(res), _wrap(rank), _wrap(sv)
+
+
+# ------------------------------------------------------------------ matrix functions / products
+def matrix_power(x, n, name=None):
+    a = T(x)
+    n = int(n)
+    if n == 0:
+        return _wrap(_eye_like(a).clone())
+    if n < 0:
+        a, n = _inv(a), -n
+    result = None
+    base = a
+    while n:
+        if n & 1:
+            result = base if result is None else result @ base
+        n >>= 1
+        if n:
+            base = base @ base
+    return _wrap(result)
+
+
+_PADE13 = (64764752532480000., 32382376266240000., 7771770303897600., 1187353796428800., 129060195264000.,
+           10559470521600., 670442572800., 33522128640., 1323241920., 40840800., 960960., 16380., 182., 1.)
+_THETA13 = 5.371920351148152
+
+
+def matrix_exp(x, name=None):
+    """Scaling and squaring: A / 2^s has 1-norm <= theta_13, exp of it by the [13/13] Pade approximant
+    r = (V - U)^-1 (V + U), then s squarings (per matrix of a batch)."""
+    a = T(x)
+    if a.shape[-1] == 0:
+        return _wrap(a.clone())
+    nrm = a.abs().sum(-2).amax(-1)
+    s = torch.clamp(torch.ceil(torch.log2(nrm / _THETA13)), min=0).nan_to_num(0)
+    A = a / (2.0 ** s).to(a.dtype)[..., None, None]
+    b = _PADE13
+    eye = _eye_like(A)
+    A2 = A @ A
+    A4 = A2 @ A2
+    A6 = A4 @ A2
+    U = A @ (A6 @ (b[13] * A6 + b[11] * A4 + b[9] * A2) + b[7] * A6 + b[5] * A4 + b[3] * A2 + b[1] * eye)
+    V = A6 @ (b[12] * A6 + b[10] * A4 + b[8] * A2) + b[6] * A6 + b[4] * A4 + b[2] * A2 + b[0] * eye
+    lu_, piv, _ = _lu(V - U)
+    R = _lu_solve(lu_, piv, V + U)
+    smax = int(s.max().item()) if s.numel() else 0
+    for k in range(smax):
+        sq = R @ R
+        R = torch.where((k < s)[..., None, None], sq, R)
+    return _wrap(R)
 
 
 def multi_dot(x, name=None):
-    return _wrap(torch.linalg.multi_dot([T(v) for v in x]))
+    """Product of a matrix chain in the order that minimises scalar multiplications (O(n^3) programme);
+    a 1-D first / last operand is a row / column vector and its dimension is dropped from the result."""
+    ts = [T(v) for v in x]
+    if len(ts) < 2:
+        raise ValueError("multi_dot expects at least two tensors")
+    first_vec, last_vec = ts[0].dim() == 1, ts[-1].dim() == 1
+    if first_vec:
+        ts[0] = ts[0].unsqueeze(0)
+    if last_vec:
+        ts[-1] = ts[-1].unsqueeze(-1)
+    n = len(ts)
+    dims = [ts[0].shape[0]] + [t.shape[1] for t in ts]
+    cost = [[0] * n for _ in range(n)]
+    split = [[0] * n for _ in range(n)]
+    for ln in range(1, n):
+        for i in range(n - ln):
+            j = i + ln
+            cost[i][j] = None
+            for k in range(i, j):
+                c = cost[i][k] + cost[k + 1][j] + dims[i] * dims[k + 1] * dims[j + 1]
+                if cost[i][j] is None or c < cost[i][j]:
+                    cost[i][j], split[i][j] = c, k
+
+    def prod(i, j):
+        if i == j:
+            return ts[i]
+        k = split[i][j]
+        return prod(i, k) @ prod(k + 1, j)
+    out = prod(0, n - 1)
+    if first_vec:
+        out = out.squeeze(0)
+    if last_vec:
+        out = out.squeeze(-1)
+    return _wrap(out)
+
+
+def _reflectors(x, tau, ncols):
+    """H_1 H_2 ... H_k applied to the first ``ncols`` columns of the identity (m x ncols)."""
+    m = x.shape[-2]
+    k = tau.shape[-1]
+    q = torch.eye(m, ncols, dtype=x.dtype, device=x.device).expand(*x.shape[:-2], m, ncols)
+    for i in reversed(range(k)):
+        v = torch.cat([torch.zeros(*x.shape[:-2], i, dtype=x.dtype, device=x.device),
+                       torch.ones(*x.shape[:-2], 1, dtype=x.dtype, device=x.device), x[..., i + 1:, i]], -1)
+        q = q - tau[..., i, None, None] * v.unsqueeze(-1) @ (v.conj().unsqueeze(-2) @ q)
+    return q
 
 
 def householder_product(x, tau, name=None):
-    return _wrap(torch.linalg.householder_product(T(x), T(tau)))
+    a, t = T(x), T(tau)
+    return _wrap(_reflectors(a, t, a.shape[-1]))
 
 
-def corrcoef(x, rowvar=True, name=None):
-    t = T(x)
-    return _wrap(torch.corrcoef(t if rowvar else t.T))
+def ormqr(x, tau, y, left=True, transpose=False, name=None):
+    a, t, c = T(x), T(tau), T(y)
+    q = _reflectors(a, t, a.shape[-2])  # the full m x m Q
+    if transpose:
+        q = q.mH
+    return _wrap(q @ c if left else c @ q)
 
 
 def cov(x, rowvar=True, ddof=True, fweights=None, aweights=None, name=None):
     t = T(x)
-    return _wrap(torch.cov(t if rowvar else t.T, correction=1 if ddof else 0,
-                           fweights=T(fweights), aweights=T(aweights)))
+    X = t if t.dim() > 1 else t.unsqueeze(0)
+    if not rowvar and t.dim() > 1:
+        X = X.t()
+    nobs = X.shape[1]
+    fw = T(fweights) if fweights is not None else None
+    aw = T(aweights) if aweights is not None else None
+    w = None
+    if fw is not None:
+        w = fw.to(X.dtype if X.is_floating_point() else torch.float32)
+    if aw is not None:
+        w = aw.to(X.dtype if X.is_floating_point() else torch.float32) if w is None else w * aw
+    Xf = X if X.is_floating_point() or X.is_complex() else X.float()
+    corr = 1 if ddof else 0
+    if w is None:
+        avg = Xf.mean(1, keepdim=True)
+        fact = nobs - corr
+        Xc = Xf - avg
+        c = Xc @ Xc.mH
+    else:
+        wsum = w.sum()
+        avg = (Xf * w).sum(1, keepdim=True) / wsum
+        if corr == 0:
+            fact = wsum
+        elif aw is None:
+            fact = wsum - corr
+        else:
+            fact = wsum - corr * (w * aw).sum() / wsum
+        Xc = Xf - avg
+        c = (Xc * w) @ Xc.mH
+    c = c / fact
+    return _wrap(c.squeeze() if c.shape[0] == 1 else c)
 
 
-def ormqr(x, tau, y, left=True, transpose=False, name=None):
-    return _wrap(torch.ormqr(T(x), T(tau), T(y), left, transpose))
+def corrcoef(x, rowvar=True, name=None):
+    c = T(cov(x, rowvar))
+    if c.dim() == 0:
+        return _wrap(c / c)
+    d = c.diagonal()
+    sd = d.sqrt()
+    r = c / sd.unsqueeze(1) / sd.unsqueeze(0)
+    if r.is_complex():
+        return _wrap(torch.complex(r.real.clamp(-1, 1), r.imag.clamp(-1, 1)))
+    return _wrap(r.clamp(-1, 1))
 
 
 def vecdot(x, y, axis=-1, name=None):
-    return _wrap(torch.linalg.vecdot(T(x), T(y), dim=axis))
+    a, b = T(x), T(y)
+    return _wrap((a.conj() * b).sum(axis))
 
 
 def histogramdd(*a, **k):

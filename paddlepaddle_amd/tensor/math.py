@@ -694,7 +694,8 @@ def broadcast_shape(x_shape, y_shape):
 
 
 def inverse(x, name=None):
-    return _wrap(torch.linalg.inv(T(x)))
+    from .linalg import _inv  # LU factor + pivot gather + two triangular solves
+    return _wrap(_inv(T(x)))
 
 
 def isclose(x, y, rtol=1e-05, atol=1e-08, equal_nan=False, name=None):
