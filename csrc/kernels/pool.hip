@@ -2,8 +2,11 @@
 // Reference behaviour: paddle/phi/kernels/funcs/pooling.cu (max pool with padding as -inf, the first maximum
 // of the window wins) and the mask-based backward of max_pool2d_with_index.
 //
-// Forward: a thread owns 8 channels of one output pixel (16-byte loads / stores), keeps the running max and
-// the window offset of the first maximum (uint8, kernel <= 15x15). Backward is a gather, not a scatter: a
+// Forward: a thread owns 8 channels of one output pixel (16-byte loads / stores); the value follows the
+// reference's compare order (y = y > x ? y : x, so NaN behaves as in paddle/phi/kernels/funcs/pooling.h
+// MaxPool), and the gradient slot is the first in-bounds element equal to the output (pooling.cu
+// KernelMaxPool2DGrad's ele == input test; a NaN output gets no gradient), stored as a uint8 window offset
+// (kernel <= 15x15, 255 = none). Backward is a gather, not a scatter: a
 // thread owns 8 channels of one INPUT pixel, visits the <= ceil(K/s)^2 outputs whose windows contain it and
 // adds dy where the stored offset points at this pixel — every dx element is written once, no atomics and
 // no zero-fill pass (ATen's NHWC max_pool backward scatters into a zeroed dx).
@@ -12,6 +15,8 @@
 using namespace pa;
 
 namespace {
+
+constexpr int kNoGrad = 255;  // window offsets are < 15 * 15
 
 template <typename T>
 __global__ __launch_bounds__(256) void maxpool_nhwc_fwd_k(const T* __restrict__ x, T* __restrict__ y,
@@ -28,8 +33,24 @@ __global__ __launch_bounds__(256) void maxpool_nhwc_fwd_k(const T* __restrict__ 
     float best[8];
     int bi[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = kNoGrad; }
     const int h0 = oh * s - p, w0 = ow * s - p;
+    // value: the reference's running compare y = y > x ? y : x over the in-bounds window (a NaN is taken
+    // when met and replaced by any later element)
+    for (int kh = 0; kh < K; ++kh) {
+      const int h = h0 + kh;
+      if (h < 0 || h >= H) continue;
+      for (int kw = 0; kw < K; ++kw) {
+        const int w = w0 + kw;
+        if (w < 0 || w >= W) continue;
+        float v[8];
+        load8<T>(x + (((int64_t)n * H + h) * W + w) * C + c8 * 8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) best[j] = best[j] > v[j] ? best[j] : v[j];
+      }
+    }
+    // gradient slot: the first in-bounds element equal to the output (the reference's ele == input test);
+    // none for a NaN output (kNoGrad)
     for (int kh = 0; kh < K; ++kh) {
       const int h = h0 + kh;
       if (h < 0 || h >= H) continue;
@@ -40,7 +61,7 @@ __global__ __launch_bounds__(256) void maxpool_nhwc_fwd_k(const T* __restrict__ 
         load8<T>(x + (((int64_t)n * H + h) * W + w) * C + c8 * 8, v);
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          if (v[j] > best[j] || (v[j] != v[j] && best[j] == best[j])) { best[j] = v[j]; bi[j] = kh * K + kw; }
+          if (bi[j] == kNoGrad && v[j] == best[j]) bi[j] = kh * K + kw;
       }
     }
     store8<T>(y + i * 8, best);

@@ -22,17 +22,43 @@ def _back(t, cl):
     return t
 
 
-def _pad_arg(padding, n):
+def _pad_arg(padding, n, data_format=None):
+    """Spatial padding as "same", an int / per-dim tuple (symmetric), or ("asym", [before0, after0, ...]).
+    Accepts paddle's forms: int, [p] * n, [before0, after0, ...] and the nested per-axis pairs
+    ([[0, 0], [0, 0], [ph0, ph1], [pw0, pw1]] NCHW, [[0, 0], [ph0, ph1], [pw0, pw1], [0, 0]] NHWC)."""
     if isinstance(padding, str):
         return 0 if padding.upper() == "VALID" else "same"
-    if isinstance(padding, (list, tuple)) and len(padding) == 2 * n:
-        return tuple(padding[2 * i] for i in range(n))
-    return padding
+    if isinstance(padding, (list, tuple)) and padding and isinstance(padding[0], (list, tuple)):
+        cl = data_format in ("NHWC", "NLC", "NDHWC")
+        pairs = padding[1:1 + n] if cl else padding[2:2 + n]
+        flat = [int(a) for pr in pairs for a in pr]
+    elif isinstance(padding, (list, tuple)) and len(padding) == 2 * n:
+        flat = [int(a) for a in padding]
+    else:
+        return padding
+    if all(flat[2 * i] == flat[2 * i + 1] for i in range(n)):
+        return tuple(flat[2 * i] for i in range(n))
+    return ("asym", flat)
+
+
+def _explicit_pad(t, flat, value):
+    """Pad the trailing spatial dims of a channels-first tensor ([before0, after0, before1, ...] in dim order)."""
+    n = len(flat) // 2
+    spec = []
+    for i in reversed(range(n)):
+        spec += [flat[2 * i], flat[2 * i + 1]]
+    return F.pad(t, spec, value=value)
 
 
 def _scalar(v):
+    """The single value of an int / uniform list (None otherwise). Paddle's nested padding form
+    ([[0, 0], [ph, ph], [pw, pw], [0, 0]] for NHWC) is read through its spatial pairs."""
     if isinstance(v, (list, tuple)):
-        return v[0] if len(set(v)) == 1 else None
+        if any(isinstance(e, (list, tuple)) for e in v):
+            if len(v) != 4 or list(v[0]) != [0, 0] or list(v[3]) != [0, 0]:
+                return None
+            v = [int(a) for pair in v[1:3] for a in pair]
+        return v[0] if len(v) and len(set(v)) == 1 else None
     return v
 
 
@@ -47,7 +73,9 @@ def _maxpool(n, x, kernel_size, stride, padding, return_mask, ceil_mode, data_fo
             return _wrap(_pool.maxpool2d_nhwc(xt, k, s, p))
     t, cl = _cf(T(x), data_format)
     fn = {1: F.max_pool1d, 2: F.max_pool2d, 3: F.max_pool3d}[n]
-    pad = _pad_arg(padding, n)
+    pad = _pad_arg(padding, n, data_format)
+    if isinstance(pad, tuple) and pad and pad[0] == "asym":
+        t, pad = _explicit_pad(t, pad[1], float("-inf")), 0
     if pad == "same":
         pad = tuple(k // 2 for k in ((kernel_size,) * n if isinstance(kernel_size, int) else kernel_size))
     r = fn(t, kernel_size, stride, pad, 1, ceil_mode, return_mask)
@@ -72,7 +100,11 @@ def max_pool3d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_m
 
 def _avgpool(n, x, kernel_size, stride, padding, ceil_mode, exclusive, divisor_override, data_format):
     t, cl = _cf(T(x), data_format)
-    pad = _pad_arg(padding, n)
+    pad = _pad_arg(padding, n, data_format)
+    if isinstance(pad, tuple) and pad and pad[0] == "asym":
+        if exclusive:
+            raise NotImplementedError("avg pooling with asymmetric padding and exclusive=True")
+        t, pad = _explicit_pad(t, pad[1], 0.0), 0
     if pad == "same":
         pad = tuple(k // 2 for k in ((kernel_size,) * n if isinstance(kernel_size, int) else kernel_size))
     if n == 1:

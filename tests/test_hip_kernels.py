@@ -294,3 +294,66 @@ def test_maxpool_nhwc_matches_torch(shape, k, s, p):
     yr.backward(gy.to(torch.bfloat16).float())
     torch.testing.assert_close(x.grad.float(), xr.grad.permute(0, 2, 3, 1), atol=2e-2, rtol=1e-2)
     _lib_loaded("pa_maxpool_nhwc_fwd", "pa_maxpool_nhwc_bwd")
+
+
+def _maxpool_paddle_ref(x, k, s, p, gy):
+    """numpy max pool with the reference's semantics (pooling.h MaxPool / pooling.cu KernelMaxPool2DGrad): the
+    in-bounds window only, y = y > x ? y : x from the type's lowest value, gradient to the first x == y."""
+    import numpy as np
+    N, H, W, C = x.shape
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    y = np.full((N, Ho, Wo, C), -np.inf, dtype=np.float64)
+    dx = np.zeros_like(x, dtype=np.float64)
+    for n in range(N):
+        for i in range(Ho):
+            for j in range(Wo):
+                hs, ws = i * s - p, j * s - p
+                hh = range(max(hs, 0), min(hs + k, H))
+                ww = range(max(ws, 0), min(ws + k, W))
+                for c in range(C):
+                    best = -np.inf
+                    for a in hh:
+                        for b in ww:
+                            v = x[n, a, b, c]
+                            best = best if best > v else v
+                    y[n, i, j, c] = best
+                    done = False
+                    for a in hh:
+                        for b in ww:
+                            if not done and x[n, a, b, c] == best:
+                                dx[n, a, b, c] += gy[n, i, j, c]
+                                done = True
+    return y, dx
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("k,s,p", [(3, 2, 1), (2, 3, 0), (3, 1, 1)])
+def test_maxpool_nhwc_through_functional(dtype, k, s, p):
+    """paddle.nn.functional.max_pool2d(data_format='NHWC') (the path ResNet takes) against the reference's
+    semantics, with border windows whose in-bounds inputs are all -inf and a NaN input; tuple kernel sizes and
+    ceil_mode take the fallback and must agree with the NCHW path."""
+    import numpy as np
+    import paddlepaddle_amd as paddle
+    from paddlepaddle_amd.ops import _loader as L
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(2, 9, 10, 8, generator=g).to(dtype)
+    x[0, 0, :, :] = -float("inf")
+    x[0, 0:2, 0:2, 3] = -float("inf")
+    x[1, 4, 4, 5] = float("nan")
+    xt = paddle.Tensor(x.to("cuda").requires_grad_(True))
+    xt.stop_gradient = False
+    before = L.calls("pa_maxpool_nhwc_fwd")
+    y = paddle.nn.functional.max_pool2d(xt, k, s, p, data_format="NHWC")
+    assert L.calls("pa_maxpool_nhwc_fwd") > before, "the NHWC HIP kernel must serve int kernel / stride"
+    gy = torch.randn(tuple(y.shape), generator=g).to(dtype)
+    y.backward(paddle.Tensor(gy.to("cuda")))
+    want_y, want_dx = _maxpool_paddle_ref(x.float().numpy(), k, s, p, gy.float().numpy())
+    np.testing.assert_array_equal(y._t.detach().float().cpu().numpy(), want_y.astype(np.float32))
+    np.testing.assert_allclose(xt.grad._t.float().cpu().numpy(), want_dx, atol=2e-2, rtol=1e-2)
+    # fallback forms agree with the NCHW path on finite data
+    xf = paddle.Tensor(torch.randn(2, 9, 10, 8, generator=g).to("cuda", dtype))
+    for kk, ss, cm in (((2, 3), (2, 2), False), (3, 2, True)):
+        a = paddle.nn.functional.max_pool2d(xf, kk, ss, 0, ceil_mode=cm, data_format="NHWC")
+        b = paddle.nn.functional.max_pool2d(xf.transpose([0, 3, 1, 2]), kk, ss, 0, ceil_mode=cm)
+        assert torch.equal(a._t, b._t.permute(0, 2, 3, 1))

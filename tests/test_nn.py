@@ -253,3 +253,21 @@ def test_gpt_tiny_trains_with_recompute():
         opt.clear_grad()
         losses.append(float(loss))
     assert losses[-1] < losses[0] - 1.0
+
+
+def test_max_pool_padding_forms():
+    """paddle's int / flat / nested padding forms on both layouts, incl. asymmetric (explicit -inf pad)."""
+    import numpy as np
+    x = paddle.to_tensor(np.random.RandomState(3).randn(2, 3, 7, 6).astype("float32"))
+    F = paddle.nn.functional
+    ref = F.max_pool2d(x, 3, 2, 1)
+    np.testing.assert_array_equal(F.max_pool2d(x, 3, 2, [1, 1, 1, 1]).numpy(), ref.numpy())
+    np.testing.assert_array_equal(F.max_pool2d(x, 3, 2, [[0, 0], [0, 0], [1, 1], [1, 1]]).numpy(), ref.numpy())
+    xh = x.transpose([0, 2, 3, 1])
+    got = F.max_pool2d(xh, 3, 2, [[0, 0], [1, 1], [1, 1], [0, 0]], data_format="NHWC")
+    np.testing.assert_array_equal(got.numpy(), ref.numpy().transpose(0, 2, 3, 1))
+    asym = F.max_pool2d(x, 3, 2, [[0, 0], [0, 0], [0, 2], [1, 0]]).numpy()
+    xp = np.pad(x.numpy(), ((0, 0), (0, 0), (0, 2), (1, 0)), constant_values=-np.inf)
+    want = np.stack([[[[xp[b, c, i * 2:i * 2 + 3, j * 2:j * 2 + 3].max() for j in range((xp.shape[3] - 3) // 2 + 1)]
+                       for i in range((xp.shape[2] - 3) // 2 + 1)] for c in range(3)] for b in range(2)])
+    np.testing.assert_array_equal(asym, want)
