@@ -406,6 +406,8 @@ __device__ __forceinline__ void tile_coords(int pid, int tiles_m, int tiles_n, i
   *tn = (pid % per_group) / gsz;
 }
 
+constexpr int kEpiRowStride = 260;  // fp32 per row of the epilogue image (256 + 4 padding)
+
 template <int V>
 struct IntC {
   static constexpr int value = V;
@@ -619,52 +621,77 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p0) {
     return;
   }
 
-  // ---- epilogue
+  // ---- epilogue, staged through LDS in two 128-row halves: the accumulators go to a row-major fp32 image
+  // (1040-byte rows: the 16 rows of a ds_write_b128 lane group land on distinct banks), then every thread
+  // owns 8 consecutive columns and walks 8 row steps of 16 rows, so each wave instruction moves whole
+  // 512-byte (bf16) / 1 KiB (fp32) row segments — bias / alpha / pre-activation / GELU / accumulate are
+  // applied in that coalesced phase. The scattered 8-byte fragment stores left the tile wave's final burst
+  // (aux / accumulate read-modify-write) far below the HBM rate.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int flags = p.flags;
+  float* img = reinterpret_cast<float*>(smem);
+  constexpr int RS = kEpiRowStride;  // floats per image row
+  const int ec = (tid & 31) * 8;     // this thread's 8 columns of the tile
+  const int er = tid >> 5;           // first row (of 16 per step)
+  const int n = n0 + ec;
+  const bool n_ok = n < p.N;
+  float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if ((flags & kEpiBias) && n_ok) load8<bf16>(reinterpret_cast<const bf16*>(p.bias + n), bv);
 #pragma unroll
-  for (int bh = 0; bh < 2; ++bh)
+  for (int ah = 0; ah < 2; ++ah) {
+    bar();
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + bh * 128 + bc + j * 16 + 4 * (lane >> 4);
-      if (n >= p.N) continue;
-      float bv[4] = {0.f, 0.f, 0.f, 0.f};
-      if (flags & kEpiBias) {
-        const uint2 braw = *reinterpret_cast<const uint2*>(p.bias + n);
-        bv[0] = lo_bf16(braw.x); bv[1] = hi_bf16(braw.x); bv[2] = lo_bf16(braw.y); bv[3] = hi_bf16(braw.y);
-      }
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int ah = 0; ah < 2; ++ah)
+      for (int bh = 0; bh < 2; ++bh)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = m0 + ah * 128 + ar + i * 16 + (lane & 15);
-          if (m >= p.M) continue;
-          float v[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = acc[ah][i][bh][j][e] * p.alpha + bv[e];
-          const int64_t off = (int64_t)m * p.ldc + n;
-          if (flags & kEpiAux)
-            *reinterpret_cast<uint2*>(p.aux + off) = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
-          if (flags & kEpiGelu) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = gelu_tanh(v[e]);
-          }
-          if (flags & kEpiOutF32) {
-            float4* cp = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.c) + off);
-            if (flags & kEpiAccum) {
-              const float4 o = *cp;
-              v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
-            }
-            *cp = make_float4(v[0], v[1], v[2], v[3]);
-          } else {
-            uint2* cp = reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.c) + off);
-            if (flags & kEpiAccum) {
-              const uint2 o = *cp;
-              v[0] += lo_bf16(o.x); v[1] += hi_bf16(o.x); v[2] += lo_bf16(o.y); v[3] += hi_bf16(o.y);
-            }
-            *cp = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
-          }
+        for (int j = 0; j < 2; ++j) {
+          const int r = ar + i * 16 + (lane & 15);
+          const int c = bh * 128 + bc + j * 16 + 4 * (lane >> 4);
+          *reinterpret_cast<f32x4*>(img + r * RS + c) = acc[ah][i][bh][j];
         }
+    bar();
+    if (!n_ok) continue;
+#pragma unroll 2
+    for (int step = 0; step < 8; ++step) {
+      const int r = step * 16 + er;
+      const int m = m0 + ah * 128 + r;
+      if (m >= p.M) break;
+      float v[8];
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(img + r * RS + ec);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(img + r * RS + ec + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = lo[e] * p.alpha + bv[e];
+        v[4 + e] = hi[e] * p.alpha + bv[4 + e];
+      }
+      const int64_t off = (int64_t)m * p.ldc + n;
+      if (flags & kEpiAux) store8<bf16>(reinterpret_cast<bf16*>(p.aux + off), v);
+      if (flags & kEpiGelu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
+      }
+      if (flags & kEpiOutF32) {
+        float* cp = reinterpret_cast<float*>(p.c) + off;
+        if (flags & kEpiAccum) {
+          float o[8];
+          load8<float>(cp, o);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += o[e];
+        }
+        store8<float>(cp, v);
+      } else {
+        bf16* cp = reinterpret_cast<bf16*>(reinterpret_cast<uint16_t*>(p.c) + off);
+        if (flags & kEpiAccum) {
+          float o[8];
+          load8<bf16>(cp, o);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += o[e];
+        }
+        store8<bf16>(cp, v);
+      }
     }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -911,10 +938,12 @@ int launch256(const GemmArgs& a0, int splits, hipStream_t st, int grid = 0) {
     grid = a.tiles_m * a.tiles_n;
     a.tail_split = 0;
   }
-  const int smem = 2 * 4 * 128 * kBK * 2;
+  constexpr int kLoop = 2 * 4 * 128 * kBK * 2, kEpi = 128 * kEpiRowStride * 4;
+  const int smem = kLoop > kEpi ? kLoop : kEpi;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKM>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    (void)hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKM>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              smem);
     attr_set = true;
   }
   hipLaunchKernelGGL((gemm256_kernel<AK, BKM>), dim3(grid, splits), dim3(kThreads), smem, st, a);

@@ -6,9 +6,18 @@ jit/dy2static/program_translator.py (StaticFunction, concrete programs), jit/tra
 No bytecode translation and no tracing compiler: ``to_static`` records the function once per input
 signature into a static ``Program`` (static/program.py: meta-tensor tracing, whole-op nodes for the
 HIP kernels) and replays it; autograd flows through the replay, so training works unchanged.
-Functions whose Python control flow depends on tensor *values* cannot be recorded; they fall back
-to eager execution (like the reference's ``full_graph=False`` fallback). Optionally the replay of an
-inference-only signature is captured into a hipGraph (``to_static(..., backend="hipgraph")``).
+
+Graph breaks (the reference's SOT, jit/sot/translate.py:31, splits the bytecode where Python needs a
+tensor's *value*): when the meta trace hits bool(t) / t.item() / t.tolist() / ..., the function is traced
+again in *guarded* mode — every op also runs on the real inputs (shadow values), each such conversion
+returns the real value and is recorded as a GuardNode, so the trace follows the branch / trip count the
+data selects. Replay re-evaluates the guards as early as their inputs exist; a mismatch raises
+GuardFailure and the next recorded variant for that signature is tried, or a new one is traced (up to
+``_MAX_VARIANTS`` per signature, then eager). So data-dependent control flow keeps running as replayed
+programs (one per observed path) instead of falling back to eager. Caveat: a variant that fails a guard
+after an in-place update of a parameter / buffer has applied that update once already.
+Optionally the replay of an inference-only signature is captured into a hipGraph
+(``to_static(..., backend="hipgraph")``; not for guarded programs — a guard reads data on the host).
 ``jit.save`` writes the JSON program + params; dynamic (None) dims are supported when every shape
 argument in the program is an affine function of them (checked by tracing at three sizes).
 """
@@ -91,8 +100,12 @@ def _rebuild(tmpl, vals):
     return tmpl
 
 
+_MAX_VARIANTS = 8
+
+
 class ConcreteProgram:
-    """One recorded signature: program + feed slots + output template."""
+    """One recorded signature (one data-dependent path when guarded): program + feed slots + output
+    template."""
 
     def __init__(self, program, feed_slots, out_tmpl, fetch_slots):
         self.main_program = program
@@ -102,6 +115,11 @@ class ConcreteProgram:
         self.fetch_slots = fetch_slots
         self.plan = P.build_plan(program, fetch_slots)
         self.graph = None
+        self.guarded = any(n.kind == "guard" for n in program.nodes)
+
+    @property
+    def guards(self):
+        return [n for n in self.program.nodes if n.kind == "guard"]
 
     @property
     def parameters(self):
@@ -141,9 +159,10 @@ def _rebuild_out(t, outs):
     return v
 
 
-def trace_program(fn, args, kwargs, names=None, dyn_size=None):
+def trace_program(fn, args, kwargs, names=None, dyn_size=None, guarded=False):
     """Record ``fn(*args, **kwargs)`` into a fresh Program. Tensor leaves of the inputs become feeds;
-    for InputSpec leaves a placeholder of that spec is created (-1 dims -> ``dyn_size``)."""
+    for InputSpec leaves a placeholder of that spec is created (-1 dims -> ``dyn_size``). ``guarded``:
+    dual tracing on the real tensor leaves (data-dependent Python values become guards)."""
     prog = P.Program()
     leaves = []
     struct = _flatten((args, kwargs), leaves)
@@ -187,8 +206,14 @@ def trace_program(fn, args, kwargs, names=None, dyn_size=None):
             return {k: fill(v) for k, v in x.items()}
         return x
     a, k = fill(struct)
-    with P.trace_into(prog):
-        out = fn(*a, **k)
+    if guarded:
+        prog._shadow = {s: x._t for s, x in zip(feed_slots, leaves)}
+        prog._shadow_dev = leaves[0]._t.device if leaves else torch.device("cpu")
+    try:
+        with P.trace_into(prog):
+            out = fn(*a, **k)
+    finally:
+        prog._shadow = None
     fetch = []
     tmpl = _out_template(prog, out, fetch)
     return prog, feed_slots, tmpl, fetch
@@ -200,7 +225,8 @@ class StaticFunction:
         self._dygraph_function = function
         self._input_spec = input_spec
         self._instance = instance
-        self._cache = {}
+        self._cache = {}        # signature -> the most recently used program
+        self._variants = {}     # signature -> guarded variants (most recently used first)
         self._backend = backend
         self._eager_keys = set()
         functools.update_wrapper(self, function)
@@ -233,21 +259,60 @@ class StaticFunction:
         key, leaves = self._signature(args, kwargs)
         if key in self._eager_keys:
             return self._call_eager(*args, **kwargs)
+        dev = leaves[0]._t.device if leaves else torch.device("cpu")
         cp = self._cache.get(key)
         if cp is None:
-            fn = self._call_eager
             try:
-                prog, feed_slots, tmpl, fetch = trace_program(fn, args, kwargs)
-            except Exception as e:  # value-dependent control flow etc.
-                warnings.warn(f"to_static: falling back to eager for {self._dygraph_function.__name__}: {e}")
-                self._eager_keys.add(key)
-                return self._call_eager(*args, **kwargs)
-            cp = ConcreteProgram(prog, feed_slots, tmpl, fetch)
+                cp = self._trace(args, kwargs, guarded=False)
+            except Exception:  # a Python conversion of tensor data (graph break): trace with guards
+                try:
+                    cp = self._trace(args, kwargs, guarded=True)
+                except Exception as e:
+                    warnings.warn(f"to_static: falling back to eager for {self._dygraph_function.__name__}: {e}")
+                    self._eager_keys.add(key)
+                    return self._call_eager(*args, **kwargs)
             self._cache[key] = cp
-        dev = leaves[0]._t.device if leaves else torch.device("cpu")
+            self._variants[key] = [cp]
+        if cp.guarded:
+            return self._run_guarded(key, args, kwargs, leaves, dev)
         if self._backend in ("hipgraph", "cudagraph") and dev.type == "cuda" and not torch.is_grad_enabled():
             return self._graph_call(cp, leaves, dev)
         return cp.run(leaves, dev)
+
+    def _trace(self, args, kwargs, guarded):
+        prog, feed_slots, tmpl, fetch = trace_program(self._call_eager, args, kwargs, guarded=guarded)
+        return ConcreteProgram(prog, feed_slots, tmpl, fetch)
+
+    def _run_guarded(self, key, args, kwargs, leaves, dev):
+        vs = self._variants[key]
+        for i, cp in enumerate(vs):
+            try:
+                out = cp.run(leaves, dev)
+            except P.GuardFailure:
+                continue
+            if i:
+                vs.insert(0, vs.pop(i))
+                self._cache[key] = cp
+            return out
+        if len(vs) >= _MAX_VARIANTS:
+            warnings.warn(f"to_static: {self._dygraph_function.__name__} took more than {_MAX_VARIANTS} "
+                          "data-dependent paths for one signature; running it eagerly")
+            self._eager_keys.add(key)
+            return self._call_eager(*args, **kwargs)
+        try:
+            cp = self._trace(args, kwargs, guarded=True)
+        except Exception as e:
+            warnings.warn(f"to_static: falling back to eager for {self._dygraph_function.__name__}: {e}")
+            self._eager_keys.add(key)
+            return self._call_eager(*args, **kwargs)
+        vs.insert(0, cp)
+        self._cache[key] = cp
+        return cp.run(leaves, dev)
+
+    def variants(self, *args, **kwargs):
+        """Programs recorded for the signature of these arguments (one per observed data-dependent path)."""
+        key, _ = self._signature(args, kwargs)
+        return list(self._variants.get(key, []))
 
     def _graph_call(self, cp, leaves, dev):
         """Capture the replay once into a hipGraph with static input/output buffers."""

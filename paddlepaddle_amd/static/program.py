@@ -96,6 +96,39 @@ class OpNode:
         return f"{self.outs} = {self.name}{self.args}"
 
 
+class GuardFailure(RuntimeError):
+    """A guard of a dual-traced program saw a different Python value than at trace time."""
+
+
+class GuardNode(OpNode):
+    """A Python conversion of a traced value (bool(t), t.item(), t.tolist(), ...) seen while dual-tracing:
+    replay recomputes it and raises GuardFailure when it differs from the traced value, because the
+    Python code after it (a branch, a loop trip count, a shape) was specialised to that value."""
+    __slots__ = ("expected",)
+
+    def __init__(self, func, args, kwargs, expected, name=None):
+        super().__init__(func, args, kwargs, None, "guard", name)
+        self.expected = expected
+
+    def check(self, val):
+        e = self.expected
+        if isinstance(e, np.ndarray) or isinstance(val, np.ndarray):
+            ok = isinstance(val, np.ndarray) and isinstance(e, np.ndarray) and val.shape == e.shape and \
+                val.dtype == e.dtype and bool(np.array_equal(val, e, equal_nan=val.dtype.kind in "fc"))
+        else:
+            ok = type(val) is type(e) and (val == e or (val != val and e != e))
+        if not ok:
+            raise GuardFailure(f"guard {self.name} expected {e!r}, got {val!r}")
+
+    def __repr__(self):
+        return f"guard {self.name}{self.args} == {self.expected!r}"
+
+
+# Python conversions of a tensor's data (graph breaks of the reference's SOT; guards here)
+_BREAK_FUNCS = frozenset({"m:__bool__", "m:item", "m:tolist", "m:__int__", "m:__float__", "m:__index__",
+                          "m:__complex__", "m:numpy", "m:__array__"})
+
+
 def _func_name(func):
     q = getattr(func, "__qualname__", "") or ""
     if q == "getset_descriptor.__get__" or q.endswith(".__get__"):
@@ -155,6 +188,11 @@ class Program:
         self._is_test = False
         self._dyn = False        # saved program with an affine dynamic dim
         self._cur = self.nodes   # node list being recorded into (a control-flow sub-block while tracing one)
+        # guarded (dual) tracing: real values of the slots, computed next to the meta trace so a Python
+        # conversion of a traced value (bool / item / tolist ...) yields the actual value and is recorded as
+        # a GuardNode instead of ending the trace (jit.to_static's graph-break path)
+        self._shadow = None
+        self._shadow_dev = None
 
     # ------------------------------------------------------------ slots / values
     def _new_slot(self, meta):
@@ -235,6 +273,10 @@ class Program:
     def _record(self, func, args, kwargs, kind="torch"):
         traced = self._any((args, kwargs), self._is_traced)
         name = _func_name(func)
+        if traced and name in _BREAK_FUNCS:
+            if self._shadow is None:
+                raise RuntimeError(f"{name[2:]}() of a traced value: the Python result depends on tensor data")
+            return self._guard(func, args, kwargs, name)
         if not traced:
             out = func(*args, **kwargs)
             # factories creating tensors on the trace device (torch.arange(..., device=x.device))
@@ -248,7 +290,13 @@ class Program:
             return func(*self._to_meta(args), **self._to_meta(kwargs))
         targs, tkw = self._template(args), self._template(kwargs)
         margs, mkw = self._to_meta(args), self._to_meta(kwargs)
-        out = func(*margs, **mkw)
+        if name == "m:cpu" and self._shadow is not None:
+            # a host copy of a traced value (ahead of .numpy() / .tolist()): traced as a meta value of the
+            # same shape, the shadow holds the real host tensor
+            with torch._C.DisableTorchFunction():
+                out = torch.empty(margs[0].shape, dtype=margs[0].dtype, device=_META)
+        else:
+            out = func(*margs, **mkw)
         node = OpNode(func, targs, tkw, None, kind, name)
         node.outs = self._out_template(out)
         self._append(node)
@@ -258,6 +306,21 @@ class Program:
         self._cur.append(node)
         self._version += 1
         self._plans.clear()
+        if self._shadow is not None and self._cur is self.nodes and not isinstance(node, GuardNode):
+            self._shadow_exec(node)
+
+    def _shadow_exec(self, node):
+        """Run a freshly recorded top-level node on the shadow values (no recording, no autograd)."""
+        with torch._C.DisableTorchFunction(), torch.no_grad():
+            _exec_node(node, self._shadow, None, self._shadow_dev, None)
+
+    def _guard(self, func, args, kwargs, name):
+        targs, tkw = self._template(args), self._template(kwargs)
+        with torch._C.DisableTorchFunction(), torch.no_grad():
+            val = func(*_materialize(targs, self._shadow, None, self._shadow_dev),
+                       **_materialize(tkw, self._shadow, None, self._shadow_dev))
+        self._append(GuardNode(func, targs, tkw, val, name))
+        return val
 
     @contextlib.contextmanager
     def _sub_block(self):
@@ -478,7 +541,7 @@ def build_plan(program, fetch_slots, keep_slots=()):
     need = set(fetch_slots) | set(keep_slots)
     live = [False] * len(nodes)
     for i in range(len(nodes) - 1, -1, -1):
-        if writes[i] & need:
+        if writes[i] & need or nodes[i].kind == "guard":
             live[i] = True
             need |= reads[i]
     idx = [i for i in range(len(nodes)) if live[i]]
@@ -501,9 +564,10 @@ def build_plan(program, fetch_slots, keep_slots=()):
             creator.setdefault(s, i)
             last_writer[s] = i
     keep_nodes = {pos_of[creator[s]] for s in set(fetch_slots) | set(keep_slots) if s in creator}
+    keep_nodes |= {k for k, i in enumerate(idx) if nodes[i].kind == "guard"}
     # collectives are issued as soon as their inputs exist (they run on the comm stream and overlap the
     # compute that does not depend on them)
-    prio = [0 if nodes[i].kind == "comm" else 1 for i in idx]
+    prio = [0 if nodes[i].kind in ("comm", "guard") else 1 for i in idx]
     order, last = native.schedule(len(idx), sorted(edges), sorted(keep_nodes), prio)
     pos = {v: p for p, v in enumerate(order)}
     free_after = {}
@@ -572,6 +636,10 @@ def _exec_node(n, env, consts, dev, sym_n):
         return
     args = _materialize(n.args, env, consts, dev, sym_n)
     kw = _materialize(n.kwargs, env, consts, dev, sym_n)
+    if n.kind == "guard":
+        with torch.no_grad():
+            n.check(n.func(*args, **kw))
+        return
     out = n.func(*args, **kw)
     if n.outs is not None:
         _assign(n.outs, out, env)
@@ -738,6 +806,9 @@ def _count_blocks(n):
 
 
 def _encode_node(n, enc):
+    if n.kind == "guard":
+        raise ValueError("a program specialised by data guards (jit.to_static graph breaks) cannot be saved; "
+                         "save with an input_spec instead")
     if isinstance(n, CFNode):
         return {"f": n.name, "a": enc(n.args), "o": enc(n.outs), "loop": list(n.loop_slots),
                 "blocks": [[_encode_node(x, enc) for x in b.nodes] for b in n.blocks],

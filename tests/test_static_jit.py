@@ -162,15 +162,22 @@ def test_to_static_forward_backward_and_jit_save_load_dynamic_batch(tmp_path):
     np.testing.assert_array_equal(out, out2)
 
 
-def test_to_static_falls_back_on_value_dependent_control_flow():
+def test_to_static_value_dependent_control_flow_is_guarded():
+    """float(x.sum()) is a graph break: the function is traced with a guard on that value instead of
+    falling back to eager (tests/test_jit_guards.py covers the variants)."""
     @paddle.jit.to_static
     def f(x):
         if float(x.sum()) > 0:
             return x * 2
         return x * 3
-    with pytest.warns(UserWarning):
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")  # no eager-fallback warning
         y = f(paddle.ones([3]))
+        z = f(-paddle.ones([3]))
     np.testing.assert_array_equal(y.numpy(), [2, 2, 2])
+    np.testing.assert_array_equal(z.numpy(), [-3, -3, -3])
+    assert all(cp.guarded for cp in f.variants(paddle.ones([3])))
 
 
 def test_native_scheduler_frees_intermediates():
