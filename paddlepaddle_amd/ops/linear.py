@@ -190,8 +190,12 @@ def _wgrad(x2, dy2, acc=None):
     return acc.addmm_(xt, dy2)
 
 
-def _mm_grads(x2, w, dy2, need_x, need_w):
+def _mm_grads(x2, w, dy2, need_x, need_w, dx_hook=None):
+    """dX first, then dW. ``dx_hook(dx)`` (tensor parallelism: the column-parallel layer's dX all-reduce)
+    starts an asynchronous collective on dX right after its GEMM and returns a finisher, called once the
+    weight-gradient GEMM has been issued — the collective runs beside the dW GEMM instead of after it."""
     dx = _dgrad(dy2, w) if need_x else None
+    fin = dx_hook(dx) if (dx_hook is not None and dx is not None) else None
     dw = None
     if need_w:
         ent = _main_grad_of(w)
@@ -201,18 +205,39 @@ def _mm_grads(x2, w, dy2, need_x, need_w):
             on_ready(w)
         else:
             dw = _wgrad(x2, dy2)
+    if fin is not None:
+        fin()
     return dx, dw
+
+
+class _GradHook(torch.autograd.Function):
+    """Identity whose backward runs ``hook(grad)`` (and its finisher) — the dX hook for linears that are not
+    on the HIP path."""
+
+    @staticmethod
+    def forward(ctx, x, hook):
+        ctx.hook = hook
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        fin = ctx.hook(g)
+        if fin is not None:
+            fin()
+        return g, None
 
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, dx_hook=None):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
         y = _fwd_mm(x2, w, b)
         ctx.save_for_backward(x2, w)
         ctx.has_b = b is not None
         ctx.shape = shape
+        ctx.dx_hook = dx_hook
         return y.view(*shape[:-1], w.shape[1])
 
     @staticmethod
@@ -223,21 +248,22 @@ class _LinearFn(torch.autograd.Function):
             dy2 = dy2.to(x2.dtype)
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
-        dx, dw = _mm_grads(x2, w, dy2, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        dx, dw = _mm_grads(x2, w, dy2, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.dx_hook)
         db = colsum(dy2) if ctx.has_b and ctx.needs_input_grad[2] else None
         if dx is not None:
             dx = dx.view(ctx.shape)
-        return dx, dw, db
+        return dx, dw, db, None
 
 
 class _LinearBiasGeluFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, dx_hook=None):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
         y, h, bb = _fwd_bias_gelu(x2, w, b)
         ctx.save_for_backward(x2, w, bb, h)
         ctx.shape = shape
+        ctx.dx_hook = dx_hook
         return y.view(*shape[:-1], w.shape[1])
 
     @staticmethod
@@ -250,10 +276,10 @@ class _LinearBiasGeluFn(torch.autograd.Function):
         ws = torch.empty(256 * cols, dtype=torch.float32, device=h.device)
         L.call("pa_bias_gelu_bwd", L.ptr(h), L.ptr(b), L.ptr(dy2), L.ptr(dh), L.ptr(db), L.ptr(ws), rows, cols,
                L.dcode(h), L.stream_ptr())
-        dx, dw = _mm_grads(x2, w, dh, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        dx, dw = _mm_grads(x2, w, dh, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.dx_hook)
         if dx is not None:
             dx = dx.view(ctx.shape)
-        return dx, dw, db
+        return dx, dw, db, None
 
 
 def _hip_linear_ok(x, w, b):
@@ -262,11 +288,16 @@ def _hip_linear_ok(x, w, b):
 
 
 @static_op
-def fused_linear(x, w, b=None, act=None):
+def fused_linear(x, w, b=None, act=None, dx_hook=None):
+    """y = act(x @ w + b). ``dx_hook``: see _mm_grads (runs on the input gradient in backward)."""
     hip = _hip_linear_ok(x, w, b)
+    if dx_hook is not None and not (hip and (act is None or (act in ("gelu", "gelu_tanh", "gelu_approximate")
+                                                             and b is not None))):
+        x = _GradHook.apply(x, dx_hook)  # not a HIP linear: the hook runs on the incoming gradient
+        dx_hook = None
     if act is None:
         if hip:
-            return _LinearFn.apply(x, w, b)
+            return _LinearFn.apply(x, w, b, dx_hook)
         if b is None:
             return torch.matmul(x, w)
         if x.dim() == 2:
@@ -274,7 +305,7 @@ def fused_linear(x, w, b=None, act=None):
         return torch.addmm(b, x.reshape(-1, x.shape[-1]), w).view(*x.shape[:-1], w.shape[-1])
     if act in ("gelu", "gelu_tanh", "gelu_approximate"):
         if hip and b is not None:
-            return _LinearBiasGeluFn.apply(x, w, b)
+            return _LinearBiasGeluFn.apply(x, w, b, dx_hook)
         h = torch.matmul(x, w)
         if b is not None:
             return bias_gelu(h, b)

@@ -118,6 +118,15 @@ class _Concat(torch.autograd.Function):
         return g.chunk(n, -1)[_rank(ctx.group)].contiguous(), None
 
 
+def _async_allreduce_hook(group):
+    """dX hook of a column-parallel linear: all-reduce over the mp group on the collective stream, waited
+    for (a stream dependency, no host block) after the dW GEMM has been issued."""
+    def hook(dx):
+        work = dist.all_reduce(dx, group=group.process_group, async_op=True)
+        return work.wait
+    return hook
+
+
 def c_identity(t, group=None):
     g = group or _mp_group()
     return _Identity.apply(t, g) if _ws(g) > 1 else t
@@ -174,11 +183,14 @@ class ColumnParallelLinear(nn.Layer):
             self.bias.is_distributed = self.world > 1
 
     def forward(self, x):
-        t = c_identity(x._t, self.group)
+        t = x._t
         w = self.weight._t
         if t.dtype != w.dtype:
             t = t.to(w.dtype)
-        y = _ops.fused_linear(t, w, None if self.bias is None else self.bias._t, act=self.act)
+        # c_identity's backward all-reduce, issued asynchronously right after the dX GEMM so it overlaps the
+        # weight-gradient GEMM (reference: mp_layers.py ColumnParallelLinear + mp_async_allreduce)
+        hook = _async_allreduce_hook(self.group) if self.world > 1 else None
+        y = _ops.fused_linear(t, w, None if self.bias is None else self.bias._t, act=self.act, dx_hook=hook)
         if self.gather_output:
             y = c_concat(y, self.group)
         return _wrap(y)

@@ -357,3 +357,30 @@ def test_maxpool_nhwc_through_functional(dtype, k, s, p):
         a = paddle.nn.functional.max_pool2d(xf, kk, ss, 0, ceil_mode=cm, data_format="NHWC")
         b = paddle.nn.functional.max_pool2d(xf.transpose([0, 3, 1, 2]), kk, ss, 0, ceil_mode=cm)
         assert torch.equal(a._t, b._t.permute(0, 2, 3, 1))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("act", [None, "gelu"])
+def test_fused_linear_dx_hook_runs_between_dgrad_and_wgrad(act):
+    """The column-parallel dX hook (tensor_parallel._async_allreduce_hook) sees dX right after its GEMM; the
+    finisher runs after the dW GEMM was issued; dW is unaffected by what the hook does to dX."""
+    from paddlepaddle_amd.ops import linear as Lin
+    torch.manual_seed(0)
+    x = torch.randn(256, 128, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.randn(128, 192, device="cuda") * 0.05).to(torch.bfloat16).requires_grad_(True)
+    b = torch.randn(192, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    events = []
+
+    def hook(dx):
+        events.append("hook")
+        dx.mul_(2.0)
+        return lambda: events.append("finish")
+    y = Lin.fused_linear(x, w, b, act=act, dx_hook=hook)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr, wr, br = (t.detach().clone().requires_grad_(True) for t in (x, w, b))
+    yr = Lin.fused_linear(xr, wr, br, act=act)
+    yr.backward(g)
+    assert events == ["hook", "finish"]
+    torch.testing.assert_close(x.grad, 2 * xr.grad)
+    torch.testing.assert_close(w.grad, wr.grad)

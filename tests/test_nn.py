@@ -271,3 +271,15 @@ def test_max_pool_padding_forms():
     want = np.stack([[[[xp[b, c, i * 2:i * 2 + 3, j * 2:j * 2 + 3].max() for j in range((xp.shape[3] - 3) // 2 + 1)]
                        for i in range((xp.shape[2] - 3) // 2 + 1)] for c in range(3)] for b in range(2)])
     np.testing.assert_array_equal(asym, want)
+
+
+def test_fused_linear_dx_hook_on_the_generic_path():
+    import torch
+    from paddlepaddle_amd.ops import linear as Lin
+    x = torch.randn(4, 3, requires_grad=True)
+    w = torch.randn(3, 5, requires_grad=True)
+    seen = []
+    y = Lin.fused_linear(x, w, None, dx_hook=lambda g: (seen.append(g.shape), g.mul_(3))[0] and None)
+    y.sum().backward()
+    assert seen == [torch.Size([4, 3])]
+    torch.testing.assert_close(x.grad, 3 * torch.ones(4, 5) @ w.detach().t())
