@@ -204,6 +204,17 @@ __global__ __launch_bounds__(256) void momentum_multi_k(const int64_t* __restric
   }
 }
 
+// Values carried as kernel arguments (copied into the launch / the captured graph node at launch time), so a
+// pointer table written inside a hipGraph capture does not reference any host buffer on replay.
+constexpr int kArgVals = 248;
+struct ArgVals {
+  int64_t v[kArgVals];
+};
+
+__global__ __launch_bounds__(256) void write_i64_k(int64_t* __restrict__ dst, ArgVals a, int n) {
+  if ((int)threadIdx.x < n) dst[threadIdx.x] = a.v[threadIdx.x];
+}
+
 }  // namespace
 
 PA_EXPORT int pa_adamw_multi(const int64_t* table, const int64_t* items, int64_t n_items, const float* inv_scale,
@@ -235,5 +246,17 @@ PA_EXPORT int pa_momentum_multi(const int64_t* table, const int64_t* items, int6
   hipLaunchKernelGGL(momentum_multi_k, dim3((unsigned)g), dim3(256), 0, st, table, items, n_items, inv_scale, lr, mu,
                      rescale, nesterov);
   PA_CHECK_LAUNCH();
+  return 0;
+}
+
+// dst[0:n] (device) = src[0:n] (host int64), as kernel-argument payloads of <= 248 values per launch.
+PA_EXPORT int pa_write_i64(int64_t* dst, const int64_t* src, int64_t n, hipStream_t st) {
+  for (int64_t o = 0; o < n; o += kArgVals) {
+    ArgVals a;
+    const int m = (int)(n - o < kArgVals ? n - o : kArgVals);
+    for (int i = 0; i < m; ++i) a.v[i] = src[o + i];
+    hipLaunchKernelGGL(write_i64_k, dim3(1), dim3(256), 0, st, dst + o, a, m);
+    PA_CHECK_LAUNCH();
+  }
   return 0;
 }

@@ -18,6 +18,20 @@ from . import _loader as L
 _CHUNK = 16384  # elements per work item
 
 
+def device_table(rows, dev):
+    """int64 pointer / work-item table on ``dev`` (and the host buffer it came from). Eager: a pinned
+    non-blocking copy. Inside a hipGraph capture (a captured optimizer step) the values are written by kernels
+    that carry them as launch arguments (pa_write_i64), so the graph holds no reference to host memory."""
+    host = torch.tensor(rows, dtype=torch.int64)
+    if dev.type == "cuda":
+        if torch.cuda.is_current_stream_capturing() and L.has("pa_write_i64"):
+            out = torch.empty(host.shape, dtype=torch.int64, device=dev)
+            L.call("pa_write_i64", L.ptr(out), ctypes.c_void_p(host.data_ptr()), host.numel(), L.stream_ptr())
+            return out, host
+        host = host.pin_memory()
+    return host.to(dev, non_blocking=True), host
+
+
 class AdamWTable:
     """Device-resident pointer table for one parameter group (rebuilt when buffers change)."""
 

@@ -129,11 +129,13 @@ class Adam(Optimizer):
                 for s in range(0, n, _opt._CHUNK):
                     items.append([i, s])
             dev = fp32[0].device
-            t_rows = torch.tensor(rows, dtype=torch.int64).to(dev, non_blocking=True)
-            t_items = torch.tensor(items, dtype=torch.int64).to(dev, non_blocking=True)
-            tab = (key, t_rows, t_items, len(items), fp32, grads)
+            t_rows, h_rows = _opt.device_table(rows, dev)
+            t_items, h_items = _opt.device_table(items, dev)
+            tab = (key, t_rows, t_items, len(items), fp32, grads, (h_rows, h_items))
             self._tables[id(group)] = tab
-        _, t_rows, t_items, n_items, _, _ = tab
+            if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+                self.__dict__.setdefault("_graph_hosts", []).append(tab[6])  # read by every replay
+        _, t_rows, t_items, n_items = tab[:4]
         bc1 = 1 - b1 ** step
         bc2 = 1 - b2 ** step
         inv_scale = getattr(self, "_inv_scale_tensor", None)

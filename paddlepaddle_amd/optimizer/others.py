@@ -87,10 +87,13 @@ class Momentum(_PerParam):
                 for s0 in range(0, w.numel(), _opt._CHUNK):
                     items.append([i, s0])
             dev = fp32[0].device
-            tab = (key, torch.tensor(rows, dtype=torch.int64).to(dev, non_blocking=True),
-                   torch.tensor(items, dtype=torch.int64).to(dev, non_blocking=True), len(items), fp32, grads)
+            t_rows, h_rows = _opt.device_table(rows, dev)
+            t_items, h_items = _opt.device_table(items, dev)
+            tab = (key, t_rows, t_items, len(items), fp32, grads, (h_rows, h_items))
             tabs[id(group)] = tab
-        _, t_rows, t_items, n_items, _, _ = tab
+            if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+                self.__dict__.setdefault("_graph_hosts", []).append(tab[6])  # read by every replay
+        _, t_rows, t_items, n_items = tab[:4]
         lr = self._group_lr(group, None)
         mu = group.get("momentum", self._momentum)
         L.call("pa_momentum_multi", L.ptr(t_rows), L.ptr(t_items), n_items,
