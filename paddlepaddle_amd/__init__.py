@@ -113,13 +113,18 @@ def disable_signal_handler():
 
 
 class LazyGuard:
-    """Parameters created inside are materialised normally (lazy init is unnecessary with 288 GB HBM
-    per GPU; sharding slices parameters right after construction)."""
+    """Parameters created inside get no memory (meta tensors) until ``param.initialize()`` allocates them on
+    their device and runs their initializer (reference: nn/initializer/lazy_init.py) — build a model larger
+    than one device, then materialise only the shards a rank keeps."""
 
     def __enter__(self):
+        from .nn.layer import layers as _layers
+        _layers._LAZY.depth += 1
         return self
 
     def __exit__(self, *a):
+        from .nn.layer import layers as _layers
+        _layers._LAZY.depth -= 1
         return False
 
 

@@ -175,3 +175,6 @@ class iinfo:
         self.bits = ii.bits
         self.min = ii.min
         self.max = ii.max
+
+    def __repr__(self):
+        return f"paddle.iinfo(min={self.min}, max={self.max}, bits={self.bits}, dtype={self.dtype})"

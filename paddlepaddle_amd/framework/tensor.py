@@ -593,6 +593,24 @@ class Parameter(Tensor):
         self.is_distributed = attrs.get("is_distributed", False)
         self.do_model_average = attrs.get("do_model_average", None)
 
+    def initialize(self):
+        """Materialise a parameter created under paddle.LazyGuard: allocate it on its device and run its
+        initializer (no-op for an ordinary parameter)."""
+        lazy = self.__dict__.pop("_lazy_init", None)
+        if lazy is None:
+            return self
+        init, dev = lazy
+        old = self._t
+        t = torch.empty(old.shape, dtype=old.dtype, device=dev)
+        with torch.no_grad():
+            init._init(t)
+        if old.requires_grad:
+            t.requires_grad_(True)
+        _PARAM_OF.pop(id(old), None)
+        self._t = t
+        _PARAM_OF[id(t)] = self
+        return self
+
     @property
     def trainable(self):
         return self.__dict__.get("_trainable", True)

@@ -18,6 +18,9 @@ def linear(x, weight, bias=None, name=None):
     b = T(bias)
     if b is not None and b.dtype != w.dtype:
         b = b.to(w.dtype)
+    if w.dim() == 1:  # a vector weight (e.g. set by the Assign initializer): matmul semantics
+        y = torch.matmul(a, w)
+        return _wrap(y + b if b is not None else y)
     return _wrap(_ops.fused_linear(a, w, b))
 
 

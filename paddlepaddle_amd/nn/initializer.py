@@ -160,7 +160,11 @@ class Assign(Initializer):
 
     def _init(self, t):
         v = self.value._t if isinstance(self.value, Tensor) else torch.as_tensor(np.asarray(self.value))
-        t.copy_(v.reshape(t.shape).to(t.dtype))
+        if v.numel() == t.numel():
+            t.copy_(v.reshape(t.shape).to(t.dtype))
+        else:  # the reference's assign_value_ gives the parameter the value's shape
+            with torch.no_grad():
+                t.data = v.detach().to(device=t.device, dtype=t.dtype).clone()
 
 
 NumpyArrayInitializer = Assign

@@ -8,6 +8,8 @@ import re
 import weakref
 
 import numpy as np
+import threading
+
 import torch
 
 from ...framework import dtype as _dt
@@ -73,21 +75,30 @@ class HookRemoveHelper:
             del hooks[self._hook_id]
 
 
+class _LazyState(threading.local):
+    depth = 0
+
+
+_LAZY = _LazyState()  # > 0 inside paddle.LazyGuard
+
+
 def create_parameter_tensor(shape, dtype, attr=None, is_bias=False, default_initializer=None, device=None):
     attr = ParamAttr._to_attr(attr)
     if attr is False:
         return None
     td = _dt.to_torch_dtype(dtype) if dtype is not None else _dt.default_dtype().torch_dtype
     dev = to_torch_device(device)
-    t = torch.empty([int(s) for s in shape], dtype=td, device=dev)
+    lazy = _LAZY.depth > 0
+    t = torch.empty([int(s) for s in shape], dtype=td, device="meta" if lazy else dev)
     init = attr.initializer or default_initializer
     if init is None:
         if is_bias:
             init = I._global_bias_init or I.Constant(0.0)
         else:
             init = I._global_weight_init or I.XavierUniform()
-    with torch.no_grad():
-        init._init(t)
+    if not lazy:
+        with torch.no_grad():
+            init._init(t)
     name = attr.name
     if name is None:
         name = f"create_parameter_{next(_param_name_counters['create_parameter'])}.{'b' if is_bias else 'w'}_0"
@@ -95,6 +106,8 @@ def create_parameter_tensor(shape, dtype, attr=None, is_bias=False, default_init
                   optimize_attr={"learning_rate": attr.learning_rate},
                   regularizer=attr.regularizer, need_clip=attr.need_clip,
                   do_model_average=attr.do_model_average)
+    if lazy:
+        p.__dict__["_lazy_init"] = (init, dev)
     return p
 
 

@@ -53,3 +53,11 @@ class Stub(_Layer):
 
     def forward(self, input):
         return input
+
+
+from . import quant_layers  # noqa: E402,F401
+from .format import (ConvertibleQuantedLayer, LinearDequanter, LinearQuanter,  # noqa: E402,F401
+                     LinearQuanterDequanter)
+from .quant_layers import (FakeQuantAbsMax, FakeQuantChannelWiseAbsMax,  # noqa: E402,F401
+                           FakeQuantMovingAverageAbsMax, MovingAverageAbsMaxScale, QuantizedConv2D,
+                           QuantizedConv2DTranspose, QuantizedLinear)

@@ -21,14 +21,23 @@ def vector_to_parameters(vec, parameters, name=None):
             off += n
 
 
+def _norm_except(v, dim):
+    """2-norm over every axis but ``dim`` (all axes when dim is None), shaped to broadcast against v."""
+    if dim is None:
+        return (v * v).sum().sqrt()
+    red = [i for i in range(v.dim()) if i != dim]
+    return (v * v).sum(dim=red, keepdim=True).sqrt() if red else v.abs()
+
+
 def weight_norm(layer, name="weight", dim=0):
+    """w = g * v / ||v|| (reference nn/utils/weight_norm_hook.py): weight_g has the shape of the kept axis
+    (``[out]`` for dim 0), weight_v the weight's."""
     w = getattr(layer, name)
     t = w._t.detach()
-    if dim is None:
-        g = t.norm()
-    else:
-        red = [i for i in range(t.dim()) if i != dim]
-        g = t.norm(dim=red, keepdim=True) if red else t.abs()
+    if dim is not None and dim < 0:
+        dim += t.dim()
+    n = _norm_except(t, dim)
+    g = n.reshape(t.shape[dim]) if dim is not None else n.reshape([])
     g_p = Parameter(g.clone())
     v_p = Parameter(t.clone())
     del layer._parameters[name]
@@ -38,11 +47,8 @@ def weight_norm(layer, name="weight", dim=0):
     def _compute(l, inputs):
         v = l._parameters[name + "_v"]._t
         gg = l._parameters[name + "_g"]._t
-        if dim is None:
-            wv = v * (gg / v.norm())
-        else:
-            red = [i for i in range(v.dim()) if i != dim]
-            wv = v * (gg / v.norm(dim=red, keepdim=True))
+        nv = _norm_except(v, dim)
+        wv = v * (gg.reshape(nv.shape) / nv)
         object.__setattr__(l, name, _wrap(wv))
     h = layer.register_forward_pre_hook(_compute)
     layer.__dict__["_weight_norm_hook"] = (h, name, dim)

@@ -360,3 +360,105 @@ class ConstantLR(LRScheduler):
 
     def get_lr(self):
         return self.base_lr * (self.factor if self.last_epoch < self.total_steps else 1.0)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# Legacy step-based decay functions (reference: python/paddle/optimizer/lr.py:2636-3150, the fluid-era API).
+# The reference builds a global-step counter variable in static mode and returns an LRScheduler in dygraph
+# (where its decay_steps / staircase arguments are dropped). Here every mode gets a scheduler that evaluates the
+# legacy formula of the global step exactly (decay_steps, staircase, cycle honoured); optimizers step it like any
+# other LRScheduler.
+class _LegacyStepDecay(LRScheduler):
+    def __init__(self, fn, learning_rate=1.0):
+        self._fn = fn
+        super().__init__(learning_rate, -1, False)
+
+    def get_lr(self):
+        return float(self._fn(max(self.last_epoch, 0)))
+
+
+class _StepCounter:
+    """autoincreased_step_counter: value = begin + step * (number of increments)."""
+
+    def __init__(self, name, begin, step):
+        self.name, self.begin, self.step_size, self.n = name, begin, step, 0
+
+    def increment(self):
+        self.n += 1
+        return self.value
+
+    @property
+    def value(self):
+        return self.begin + self.step_size * self.n
+
+    def __int__(self):
+        return int(self.value)
+
+    def __repr__(self):
+        return f"StepCounter({self.name}={self.value})"
+
+
+_COUNTERS = {}
+
+
+def autoincreased_step_counter(counter_name=None, begin=1, step=1):
+    name = counter_name or "@STEP_COUNTER@"
+    c = _COUNTERS.get(name)
+    if c is None:
+        c = _COUNTERS[name] = _StepCounter(name, begin, step)
+    return c
+
+
+def noam_decay(d_model, warmup_steps, learning_rate=1.0):
+    return NoamDecay(d_model, warmup_steps, learning_rate)
+
+
+def _div(step, decay_steps, staircase):
+    d = step / decay_steps
+    return math.floor(d) if staircase else d
+
+
+def exponential_decay(learning_rate, decay_steps, decay_rate, staircase=False):
+    return _LegacyStepDecay(lambda s: learning_rate * decay_rate ** _div(s, decay_steps, staircase), learning_rate)
+
+
+def natural_exp_decay(learning_rate, decay_steps, decay_rate, staircase=False):
+    return _LegacyStepDecay(lambda s: learning_rate * math.exp(-decay_rate * _div(s, decay_steps, staircase)),
+                            learning_rate)
+
+
+def inverse_time_decay(learning_rate, decay_steps, decay_rate, staircase=False):
+    return _LegacyStepDecay(lambda s: learning_rate / (1 + decay_rate * _div(s, decay_steps, staircase)),
+                            learning_rate)
+
+
+def polynomial_decay(learning_rate, decay_steps, end_learning_rate=0.0001, power=1.0, cycle=False):
+    def f(s):
+        ds = decay_steps
+        if cycle:
+            ds = decay_steps * max(math.ceil(s / decay_steps), 1)
+        else:
+            s = min(s, decay_steps)
+        return (learning_rate - end_learning_rate) * (1 - s / ds) ** power + end_learning_rate
+    return _LegacyStepDecay(f, learning_rate)
+
+
+def piecewise_decay(boundaries, values):
+    return PiecewiseDecay(boundaries, values)
+
+
+def cosine_decay(learning_rate, step_each_epoch, epochs):
+    return _LegacyStepDecay(
+        lambda s: learning_rate * 0.5 * (math.cos(math.floor(s / step_each_epoch) * math.pi / epochs) + 1),
+        learning_rate)
+
+
+def linear_lr_warmup(learning_rate, warmup_steps, start_lr, end_lr):
+    if isinstance(learning_rate, LRScheduler):
+        return LinearWarmup(learning_rate, warmup_steps, start_lr, end_lr)
+
+    def f(s):
+        if s < warmup_steps:
+            return start_lr + (end_lr - start_lr) * (s / warmup_steps)
+        return learning_rate
+    return _LegacyStepDecay(f, learning_rate)

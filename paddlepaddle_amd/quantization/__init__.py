@@ -372,3 +372,9 @@ class PTQ(QAT):
     def convert(self, model, inplace=False, remain_weight=False):
         m = super().convert(model, inplace, remain_weight)
         return m
+
+
+import sys as _sys  # noqa: E402
+# `from paddle.quantization.quanters import ...` / `.observers import ...` work like the reference packages
+_sys.modules[__name__ + ".quanters"] = quanters
+_sys.modules[__name__ + ".observers"] = observers
