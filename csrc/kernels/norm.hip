@@ -128,7 +128,7 @@ template <typename T, int VPL, bool LN>
 __global__ __launch_bounds__(256) void norm_bwd_dx_rows(const T* __restrict__ dy, const T* __restrict__ x,
                                                         const T* __restrict__ w, const float* __restrict__ mean,
                                                         const float* __restrict__ rstd, T* __restrict__ dx,
-                                                        int64_t rows, int64_t cols) {
+                                                        int64_t rows, int64_t cols, const T* __restrict__ res) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -166,6 +166,12 @@ __global__ __launch_bounds__(256) void norm_bwd_dx_rows(const T* __restrict__ dy
       float o[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = rs * (g[k][j] - sg - xh[k][j] * sgx);
+      if (res) {  // + the residual branch's gradient of the same input (fused residual add)
+        float rv[8];
+        load8<T>(res + row * cols + e, rv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += rv[j];
+      }
       store8<T>(dx + row * cols + e, o);
     }
   }
@@ -175,7 +181,7 @@ template <typename T, bool LN>
 __global__ __launch_bounds__(256) void norm_bwd_dx_wide(const T* __restrict__ dy, const T* __restrict__ x,
                                                         const T* __restrict__ w, const float* __restrict__ mean,
                                                         const float* __restrict__ rstd, T* __restrict__ dx,
-                                                        int64_t rows, int64_t cols) {
+                                                        int64_t rows, int64_t cols, const T* __restrict__ res) {
   __shared__ float red[4];
   const int64_t row = blockIdx.x;
   const float mu = LN ? mean[row] : 0.f;
@@ -199,6 +205,12 @@ __global__ __launch_bounds__(256) void norm_bwd_dx_wide(const T* __restrict__ dy
     if (w) load8<T>(w + e, wv); else for (int j = 0; j < 8; ++j) wv[j] = 1.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = rs * (dv[j] * wv[j] - sg - (xv[j] - mu) * rs * sgx);
+    if (res) {
+      float rv[8];
+      load8<T>(res + row * cols + e, rv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] += rv[j];
+    }
     store8<T>(dx + row * cols + e, o);
   }
 }
@@ -250,11 +262,12 @@ int launch_fwd(const void* x, const void* w, const void* b, void* y, float* mean
 
 template <typename T, bool LN>
 int launch_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, void* dx,
-               float* dw_part, float* db_part, int64_t rows, int64_t cols, int nparts, hipStream_t st) {
+               float* dw_part, float* db_part, int64_t rows, int64_t cols, int nparts, hipStream_t st,
+               const void* res = nullptr) {
   const int64_t vpl = cdiv(cols, 512);
   dim3 grid((unsigned)cdiv(rows, 4)), block(256);
-  auto DY = (const T*)dy; auto X = (const T*)x; auto W = (const T*)w; auto DX = (T*)dx;
-#define PA_BWD(V) hipLaunchKernelGGL((norm_bwd_dx_rows<T, V, LN>), grid, block, 0, st, DY, X, W, mean, rstd, DX, rows, cols)
+  auto DY = (const T*)dy; auto X = (const T*)x; auto W = (const T*)w; auto DX = (T*)dx; auto RES = (const T*)res;
+#define PA_BWD(V) hipLaunchKernelGGL((norm_bwd_dx_rows<T, V, LN>), grid, block, 0, st, DY, X, W, mean, rstd, DX, rows, cols, RES)
   if (vpl <= 1) PA_BWD(1);
   else if (vpl <= 2) PA_BWD(2);
   else if (vpl <= 3) PA_BWD(3);
@@ -262,7 +275,8 @@ int launch_bwd(const void* dy, const void* x, const void* w, const float* mean, 
   else if (vpl <= 6) PA_BWD(6);
   else if (vpl <= 8) PA_BWD(8);
   else if (vpl <= 10) PA_BWD(10);
-  else hipLaunchKernelGGL((norm_bwd_dx_wide<T, LN>), dim3((unsigned)rows), block, 0, st, DY, X, W, mean, rstd, DX, rows, cols);
+  else hipLaunchKernelGGL((norm_bwd_dx_wide<T, LN>), dim3((unsigned)rows), block, 0, st, DY, X, W, mean, rstd, DX, rows, cols,
+                          RES);
 #undef PA_BWD
   PA_CHECK_LAUNCH();
   if (dw_part) {
@@ -296,13 +310,14 @@ PA_EXPORT int pa_layer_norm_fwd(const void* x, const void* w, const void* b, voi
   return 0;
 }
 
+// res (nullable): [rows, cols] gradient of the same input from a residual branch, added into dx in the pass.
 PA_EXPORT int pa_layer_norm_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd,
-                                void* dx, float* dw_part, float* db_part, void* unused, int64_t rows, int64_t cols,
+                                void* dx, float* dw_part, float* db_part, void* res, int64_t rows, int64_t cols,
                                 int dtype_np, hipStream_t st) {
   const int dtype = dtype_np & 0xff, nparts = dtype_np >> 8;
   PA_DISPATCH_DTYPE(dtype, T,
                     return (launch_bwd<T, true>(dy, x, w, mean, rstd, dx, dw_part, db_part, rows, cols,
-                                                nparts > 0 ? nparts : 1, st)));
+                                                nparts > 0 ? nparts : 1, st, res)));
   return 0;
 }
 

@@ -188,11 +188,19 @@ class GPTDecoderLayer(nn.Layer):
         self.dropout1 = nn.Dropout(cfg.hidden_dropout_prob)
         self.dropout2 = nn.Dropout(cfg.hidden_dropout_prob)
 
+    def _ln(self, norm, x):
+        """(residual, LN(x)): the residual's gradient is summed into the LN input gradient by the LN backward
+        kernel (ops.layer_norm_residual) instead of a separate add."""
+        r, h = _ops.layer_norm_residual(x._t, norm.weight._t, norm.bias._t, norm._epsilon)
+        return r, _wrap(h)
+
     def forward(self, x):
         # residual + dropout fused in one HIP pass (mask regenerated from a seed in backward)
         p = self.dropout1.p if self.training else 0.0
-        x = _wrap(_ops.dropout_add(self.self_attn(self.norm1(x))._t, x._t, p, self.training))
-        x = _wrap(_ops.dropout_add(self.mlp(self.norm2(x))._t, x._t, p, self.training))
+        r, h = self._ln(self.norm1, x)
+        x = _wrap(_ops.dropout_add(self.self_attn(h)._t, r, p, self.training))
+        r, h = self._ln(self.norm2, x)
+        x = _wrap(_ops.dropout_add(self.mlp(h)._t, r, p, self.training))
         return x
 
 

@@ -117,6 +117,43 @@ def rms_norm(x, w, eps=1e-6):
     return _rms_ref(x, w, eps)
 
 
+class _LayerNormResidualHIP(torch.autograd.Function):
+    """(x, layer_norm(x)) where the first output is the residual branch's use of x: its gradient is added into
+    dx inside the LN backward kernel (pa_layer_norm_bwd `res`), replacing the separate residual-gradient add
+    of a pre-LN transformer block (x feeds both the LN and the residual)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        y = _LayerNormHIP.forward(ctx, x, w, b, eps)
+        return x.view_as(x), y
+
+    @staticmethod
+    def backward(ctx, g_res, dy):
+        x2, wc, mean, rstd = ctx.saved_tensors
+        rows, cols = x2.shape
+        res = None if g_res is None else g_res.contiguous().view(rows, cols).to(x2.dtype)
+        if dy is None:
+            return (None if res is None else res.view(ctx.shape)), None, None, None
+        dy2 = dy.contiguous().view(rows, cols).to(x2.dtype)
+        dx = torch.empty_like(x2)
+        nparts = min(max((rows + 15) // 16, 1), 512)
+        dw_part = torch.empty(nparts, cols, dtype=torch.float32, device=x2.device)
+        db_part = torch.empty(nparts, cols, dtype=torch.float32, device=x2.device)
+        L.call("pa_layer_norm_bwd", L.ptr(dy2), L.ptr(x2), L.ptr(wc), L.ptr(mean), L.ptr(rstd), L.ptr(dx),
+               L.ptr(dw_part), L.ptr(db_part), L.ptr(res), rows, cols, L.dcode(x2) | (nparts << 8), L.stream_ptr())
+        dw, db = _finalize_parts(dw_part if wc is not None else None, db_part if ctx.has_b else None, ctx.w_dtype,
+                                 ctx.b_dtype, nparts, cols)
+        return dx.view(ctx.shape), dw, db, None
+
+
+def layer_norm_residual(x, w, b, eps=1e-5):
+    """(x_residual, layer_norm(x)): use x_residual for the block's residual connection; on the HIP path its
+    gradient is summed into the LN input gradient by the LN backward kernel (no separate add)."""
+    if L.hip_enabled_for(x) and x.dtype in L._DT and x.shape[-1] % 8 == 0 and torch.is_grad_enabled():
+        return _LayerNormResidualHIP.apply(x, w, b, eps)
+    return x, layer_norm(x, w, b, eps)
+
+
 @static_op
 def layer_norm(x, w, b, eps=1e-5):
     if L.hip_enabled_for(x) and x.dtype in L._DT and x.shape[-1] % 8 == 0:

@@ -384,3 +384,24 @@ def test_fused_linear_dx_hook_runs_between_dgrad_and_wgrad(act):
     assert events == ["hook", "finish"]
     torch.testing.assert_close(x.grad, 2 * xr.grad)
     torch.testing.assert_close(w.grad, wr.grad)
+
+
+@pytest.mark.gpu
+def test_layer_norm_residual_grad_fused():
+    """(r, LN(x)) with r's gradient summed into dx by the LN backward kernel == LN + separate residual add."""
+    from paddlepaddle_amd.ops import norm as N
+    torch.manual_seed(0)
+    x = torch.randn(64, 1024, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(1024, device="cuda")).to(torch.bfloat16).requires_grad_(True)
+    b = (0.1 * torch.randn(1024, device="cuda")).to(torch.bfloat16).requires_grad_(True)
+    gr, gy = torch.randn_like(x), torch.randn_like(x)
+    before = L.calls("pa_layer_norm_bwd")
+    r, y = N.layer_norm_residual(x, w, b, 1e-5)
+    torch.autograd.backward([r, y], [gr, gy])
+    assert L.calls("pa_layer_norm_bwd") == before + 1
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    yr = torch.nn.functional.layer_norm(xr, (1024,), wr, br, 1e-5)
+    torch.autograd.backward([xr, yr], [gr.float(), gy.float()])
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=5e-2, rtol=2e-2)
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=5e-1, rtol=2e-2)
+    torch.testing.assert_close(b.grad.float(), br.grad, atol=5e-1, rtol=2e-2)
