@@ -290,11 +290,13 @@ int pick_cb(int C) {
 
 // row chunking: ~512 workgroups over the chip (2 per CU, each lane with two 16-byte loads in
 // flight per tensor), each at least 8 row-iterations deep; fewer chunks keep the fold cheap
+int g_target_wgs = 512;  // reduction workgroups over the chip (pa_bn_set_target_wgs)
+
 void plan(int64_t R, int C, int* CB, int* chunks, int64_t* rows_per_chunk) {
   *CB = pick_cb(C);
   const int rpi = kThreads / (*CB / 8);
   const int gx = C / *CB;
-  int64_t want = 512 / gx;
+  int64_t want = g_target_wgs / gx;
   if (want < 1) want = 1;
   int64_t rpc = (R + want - 1) / want;
   const int64_t min_rows = 8 * rpi;
@@ -311,6 +313,13 @@ unsigned apply_grid(int64_t nvec) {
 }
 
 }  // namespace
+
+// Tuning knob for the reduction grid (microbenchmarks); returns the previous value.
+PA_EXPORT int pa_bn_set_target_wgs(int n) {
+  const int old = g_target_wgs;
+  if (n > 0) g_target_wgs = n;
+  return old;
+}
 
 // Number of row chunks (partial workspace = 2 * chunks * C floats) for a reduction over [R, C].
 PA_EXPORT int pa_bn_chunks(int64_t R, int C) {

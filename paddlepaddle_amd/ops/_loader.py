@@ -97,6 +97,7 @@ def _declare(L):
         "pa_sq_norm_multi": [_vp, _vp, _i64, _vp, _vp],
         "pa_scale_multi": [_vp, _i64, _vp, _vp],
         "pa_write_i64": [_vp, _vp, _i64, _vp],
+        "pa_bn_set_target_wgs": [_i32],
         "pa_momentum_multi": [_vp, _vp, _i64, _vp, _f32, _f32, _f32, _i32, _vp],
         # attention
         "pa_flash_attn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _f32, _i32, _vp],
