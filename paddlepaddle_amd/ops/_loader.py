@@ -16,6 +16,7 @@ import os
 import torch
 
 from ..framework.flags import flag
+from ._sigs import RET_I64, SIGS
 
 _LIB = None
 _LIB_ERR = None
@@ -37,7 +38,42 @@ def _load():
         _LIB_ERR = str(e)
         return None
     _declare(_LIB)
+    _load_native()
     return _LIB
+
+
+class _CurrentStream:
+    """Sentinel pointer argument: the native launch path substitutes the current HIP stream."""
+    __slots__ = ()
+
+    def __repr__(self):
+        return "<current HIP stream>"
+
+
+CURRENT_STREAM = _CurrentStream()
+_NATIVE = False   # True once _C_dispatch is loaded: launches skip ctypes
+_ENTRY: dict = {}  # launcher name -> METH_FASTCALL entry point of _C_dispatch
+
+
+def _load_native():
+    """Load the generated native entry points (csrc/dispatch). They take tensors, None, ints and the
+    CURRENT_STREAM sentinel directly, so ``ptr`` / ``stream_ptr`` hand over the objects unconverted.
+    ``PADDLE_AMD_CTYPES_LAUNCH=1`` keeps the ctypes path (A/B timing, debugging)."""
+    global _NATIVE
+    if os.environ.get("PADDLE_AMD_CTYPES_LAUNCH", "0") == "1":
+        return
+    try:
+        from .. import _C_dispatch as D
+    except ImportError:
+        return
+    D.set_stream_sentinel(CURRENT_STREAM)
+    _ENTRY.update({n: getattr(D, n) for n in SIGS if hasattr(D, n)})
+    _NATIVE = True
+
+
+def native_launch() -> bool:
+    _load()
+    return _NATIVE
 
 
 def lib():
@@ -61,95 +97,19 @@ def hip_enabled_for(t: torch.Tensor) -> bool:
 
 
 def stream_ptr(device=None):
+    if _NATIVE and device is None:
+        return CURRENT_STREAM
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
-_vp = ctypes.c_void_p
-_i64 = ctypes.c_int64
-_i32 = ctypes.c_int
-_f32 = ctypes.c_float
-
-
 def _declare(L):
-    """Argument types of every exported launcher (see csrc/kernels/*.hip)."""
-    sigs = {
-        # norms
-        "pa_rms_norm_fwd": [_vp, _vp, _vp, _vp, _i64, _i64, _f32, _i32, _vp],
-        "pa_rms_norm_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp],
-        "pa_layer_norm_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _f32, _i32, _vp],
-        "pa_layer_norm_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp],
-        "pa_reduce_parts": [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp],
-        # softmax / cross entropy
-        "pa_softmax_fwd": [_vp, _vp, _i64, _i64, _i32, _vp],
-        "pa_softmax_bwd": [_vp, _vp, _vp, _i64, _i64, _i32, _vp],
-        "pa_softmax_ce_fwd": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp],
-        "pa_softmax_ce_bwd": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp],
-        # activations
-        "pa_gelu_fwd": [_vp, _vp, _i64, _i32, _i32, _vp],
-        "pa_gelu_bwd": [_vp, _vp, _vp, _i64, _i32, _i32, _vp],
-        "pa_swiglu_fwd": [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp],
-        "pa_swiglu_bwd": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp],
-        "pa_bias_gelu_fwd": [_vp, _vp, _vp, _i64, _i64, _i32, _vp],
-        # rope
-        "pa_rope_fwd": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _i32, _vp],
-        # optimizer
-        "pa_adamw_multi": [_vp, _vp, _i64, _vp, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _vp, _vp],
-        "pa_sq_norm_multi": [_vp, _vp, _i64, _vp, _vp],
-        "pa_scale_multi": [_vp, _i64, _vp, _vp],
-        "pa_write_i64": [_vp, _vp, _i64, _vp],
-        "pa_bn_set_target_wgs": [_i32],
-        "pa_momentum_multi": [_vp, _vp, _i64, _vp, _f32, _f32, _f32, _i32, _vp],
-        # attention
-        "pa_flash_attn_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _f32, _i32, _vp],
-        "pa_flash_attn_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                              _i32, _i32, _i32, _i32, _i32, _i32, _f32, _i32, _vp],
-        "pa_flash_attn_fwd_ex": [_vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _f32, _i32, _vp,
-                                 _vp],
-        "pa_flash_attn_bwd_ex": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                 _i32, _i32, _i32, _i32, _i32, _i32, _f32, _i32, _i64, _vp, _vp],
-        "pa_fa_fm_stats": [_vp, _i32, _i32, _i32, _i32, _i32, _i64, _i64, _i32, _vp, _vp],
-        "pa_paged_decode_attn": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
-                                 _i64, _i64, _f32, _vp],
-        # gemm epilogue companions
-        "pa_colsum": [_vp, _vp, _vp, _i64, _i64, _i32, _vp],
-        "pa_gemm_bf16": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _f32,
-                         _i32, _i32, _vp],
-        "pa_gemm_bf16_pp": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _f32,
-                            _vp, _vp],
-        "pa_gemm_pp_ws_bytes": [_i64, _i64, _i64],
-        "pa_gemm_small_m": [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp],
-        "pa_conv2d_nhwc_fwd": [_vp, _vp, _vp, _vp, _vp] + [_i32] * 13 + [_vp],
-        "pa_conv2d_nhwc_wgrad": [_vp, _vp, _vp, _vp] + [_i32] * 15 + [_vp],
-        "pa_bias_gelu_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp],
-        "pa_dropout_add_fwd": [_vp, _vp, _vp, _i64, _f32, ctypes.c_uint64, _i32, _vp],
-        "pa_dropout_bwd": [_vp, _vp, _i64, _f32, ctypes.c_uint64, _i32, _vp],
-        # batch norm (NHWC)
-        "pa_bn_chunks": [_i64, _i32],
-        "pa_bn_fwd_nhwc": [_vp] * 11 + [_i64, _i32, _f32, _f32, _i32, _i32, _vp],
-        "pa_bn_bwd_nhwc": [_vp] * 12 + [_i64, _i32, _i32, _i32, _vp, _vp],
-        "pa_bn_reduce_nhwc": [_i32] + [_vp] * 7 + [_i64, _i32, _i32, _vp],
-        "pa_bn_bwd_apply_nhwc": [_vp] * 6 + [_i64, _i32, _i32, _vp, _vp],
-        # fused decode step
-        "pa_add_rms_norm_fwd": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _f32, _i32, _vp],
-        "pa_decode_rope_cache": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i64, _i32, _vp],
-        # pooling
-        "pa_maxpool_nhwc_fwd": [_vp, _vp, _vp] + [_i32] * 10 + [_vp],
-        "pa_maxpool_nhwc_bwd": [_vp, _vp, _vp] + [_i32] * 10 + [_vp],
-        # MoE
-        "pa_grouped_gemm": [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _i64, _i64, _i64, _i32,
-                            _vp],
-        "pa_moe_route": [_vp, _i32, _i32, _vp, _vp, _vp, _vp],
-        "pa_version": [],
-    }
-    for name, args in sigs.items():
+    """ctypes argument types of every exported launcher (table in ``_sigs``)."""
+    for name, args in SIGS.items():
         fn = getattr(L, name, None)
         if fn is None:
             continue
         fn.argtypes = args
-        fn.restype = _i64 if name in _RET_I64 else _i32
-
-
-_RET_I64 = {"pa_gemm_pp_ws_bytes"}
+        fn.restype = ctypes.c_int64 if name in RET_I64 else ctypes.c_int
 
 
 def has(name):
@@ -171,12 +131,15 @@ def reset_calls():
 
 def call(name, *args):
     CALLS[name] = CALLS.get(name, 0) + 1
-    rc = getattr(lib(), name)(*args)
+    fn = _ENTRY.get(name)
+    rc = fn(*args) if fn is not None else getattr(lib(), name)(*args)
     if rc != 0:
         raise RuntimeError(f"HIP kernel {name} failed with code {rc}")
 
 
 def ptr(t):
+    if _NATIVE:
+        return t  # unpacked to data_ptr() in C++
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 
 

@@ -203,7 +203,7 @@ def _fa_fwd(q, k, v, job):
     lse = torch.empty(job.lse_shape(), dtype=torch.float32, device=q.device)
     st = _i64arr(_strides(q) + _strides(k) + _strides(v) + _strides(o))
     L.call("pa_flash_attn_fwd_ex", L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(o), L.ptr(lse), st, job.B, job.Sq, job.Sk,
-           job.H, job.Hk, job.D, job.scale, int(job.causal), ctypes.byref(job.ex), L.stream_ptr())
+           job.H, job.Hk, job.D, job.scale, int(job.causal), ctypes.addressof(job.ex), L.stream_ptr())
     return o, lse
 
 
@@ -214,7 +214,7 @@ def _fa_bwd(q, k, v, o, lse, do, dq, dk, dv, job):
                  + _strides(dk) + _strides(dv))
     L.call("pa_flash_attn_bwd_ex", L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(o), L.ptr(do), L.ptr(lse), L.ptr(dq),
            L.ptr(dk), L.ptr(dv), L.ptr(dq_acc), L.ptr(delta), st, job.B, job.Sq, job.Sk, job.H, job.Hk, job.D,
-           job.scale, int(job.causal), int(job.q_rows), ctypes.byref(job.ex), L.stream_ptr())
+           job.scale, int(job.causal), int(job.q_rows), ctypes.addressof(job.ex), L.stream_ptr())
 
 
 def _lastdim_contig(t):
