@@ -200,12 +200,14 @@ class HostAllocator {
 void register_pinned_pool(py::module& m);    // pinned_pool.cpp
 void register_comm_watchdog(py::module& m);  // comm_watchdog.cpp
 void register_ps_table(py::module& m);       // ps_table.cpp
+void register_autograd_engine(py::module& m);  // autograd_engine.cpp
 
 PYBIND11_MODULE(_C_runtime, m) {
   m.doc() = "paddlepaddle_amd native runtime (collate, scheduler, bucket planner, tensor files, pinned pool)";
   register_pinned_pool(m);
   register_comm_watchdog(m);
   register_ps_table(m);
+  register_autograd_engine(m);
   py::class_<HostAllocator>(m, "HostAllocator")
       .def(py::init<size_t>(), py::arg("min_chunk") = size_t(64) << 20)
       .def("allocate", &HostAllocator::allocate, py::arg("nbytes"), py::arg("stream") = 0)

@@ -131,6 +131,10 @@ def backward(tensors, grad_tensors=None, retain_graph=False):
             raise ValueError("The length of grad_tensors must be equal to the length of tensors")
         gs = [None if g is None else _u(g) for g in gl]
     gs = [torch.ones_like(t._t) if g is None else g for t, g in zip(ts, gs)]
+    from . import engine as _eng
+    if _eng.use_native():
+        _eng.backward([t._t for t in ts], gs, retain_graph=retain_graph)
+        return
     torch.autograd.backward([t._t for t in ts], gs, retain_graph=retain_graph)
 
 
@@ -143,6 +147,12 @@ def grad(outputs, inputs, grad_outputs=None, retain_graph=None, create_graph=Fal
         gos = [grad_outputs] if isinstance(grad_outputs, Tensor) else list(grad_outputs)
         gos = [None if g is None else _u(g) for g in gos]
     rg = create_graph if retain_graph is None else retain_graph
+    from . import engine as _eng
+    if _eng.use_native():
+        gl = [torch.ones_like(o._t) if (gos is None or gos[k] is None) else gos[k] for k, o in enumerate(outs)]
+        res = _eng.grad([o._t for o in outs], [i._t for i in ins], gl, create_graph=create_graph,
+                        allow_unused=allow_unused)
+        return [None if r is None else _wrap(r) for r in res]
     res = torch.autograd.grad([o._t for o in outs], [i._t for i in ins], gos, retain_graph=rg,
                               create_graph=create_graph, allow_unused=allow_unused)
     return [None if r is None else _wrap(r) for r in res]

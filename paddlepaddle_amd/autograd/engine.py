@@ -1,0 +1,143 @@
+"""Eager backward engine selection and the Python half of the native engine.
+
+``FLAGS_eager_backward_engine``:
+  * ``native`` — backward()/paddle.grad run through ``_C_runtime.run_backward``
+    (csrc/runtime/autograd_engine.cpp): in-degree map over the reachable grad-node graph, ready queue,
+    per-slot gradient sums, gradient hooks applied to the summed slot, paddle.grad pruning + capture.
+    Reference: paddle/fluid/eager/backward.cc:105 (RunBackward), general_grad.h (paddle.grad).
+  * ``torch`` (default) — PyTorch-ROCm's C++ autograd engine runs the same grad nodes (multi-threaded device
+    queues, node-level hooks registered by DataParallel / sharding for comm overlap).
+
+Grad nodes are the per-op backward functions: the autograd functions of the hand-written HIP kernels
+(ops/*.py) and ATen's derivative formulas. Gradient hooks registered with ``Tensor.register_hook`` go into a
+table keyed by the tensor's gradient edge (node, slot) that this engine applies; tensors' post-accumulate hooks
+(DataParallel / sharding grad-ready hooks) run inside the leaf accumulation node under both engines.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..framework.flags import get_flags
+
+_HOOKS: dict = {}     # (node, slot) -> [fn(torch grad) -> torch grad | None]
+
+
+def engine_name():
+    try:
+        return str(get_flags("FLAGS_eager_backward_engine")["FLAGS_eager_backward_engine"])
+    except Exception:  # pragma: no cover
+        return "torch"
+
+
+def use_native():
+    if engine_name() != "native":
+        return False
+    from ..utils import native
+    m = native.module()
+    return m is not None and hasattr(m, "run_backward")
+
+
+def _edge(t):
+    e = torch.autograd.graph.get_gradient_edge(t)
+    return e.node, e.output_nr
+
+
+def add_hook(t, fn):
+    """Register a gradient hook for ``t`` in the native engine's table; returns a remover."""
+    key = _edge(t)
+    lst = _HOOKS.setdefault(key, [])
+    lst.append(fn)
+
+    def remove():
+        if fn in lst:
+            lst.remove(fn)
+        if not lst:
+            _HOOKS.pop(key, None)
+    return remove
+
+
+def retain(t):
+    """Tensor.retain_grads under the native engine: store the summed slot gradient into ``t.grad``."""
+    import weakref
+    if t.is_leaf:
+        return
+    t.retain_grad()  # marks .grad readable on the non-leaf; the value is written by the hook below
+    ref = weakref.ref(t)
+
+    def h(g):
+        x = ref()
+        if x is not None:
+            x.grad = g.detach() if x.grad is None else x.grad + g.detach()
+        return None
+    key = _edge(t)
+    _HOOKS.setdefault(key, []).insert(0, h)
+
+
+def _zeros_for(node, slot):
+    m = node._input_metadata[slot]
+    return torch.zeros(tuple(m.shape), dtype=m.dtype, device=m.device)
+
+
+def _fix(g, node, slot):
+    """validate_outputs: a gradient flowing into a node's slot takes that slot's dtype and shape
+    (sum over broadcast dims)."""
+    try:
+        m = node._input_metadata[slot]
+    except (IndexError, AttributeError, RuntimeError):
+        return g
+    if g.dtype != m.dtype and (m.dtype.is_floating_point or m.dtype.is_complex):
+        g = g.to(m.dtype)
+    shp = tuple(m.shape)
+    if tuple(g.shape) != shp and len(shp) <= g.dim():
+        try:
+            g = g.sum_to_size(shp)
+        except RuntimeError:
+            pass
+    return g
+
+
+def _is_py(node):
+    return isinstance(node, torch.autograd.function.BackwardCFunction)
+
+
+_HELPERS = (_zeros_for, _fix, _is_py)
+
+
+def _run(outs, grads, captures, create_graph):
+    from ..utils import native
+    roots = []
+    for t, g in zip(outs, grads):
+        if not t.requires_grad:
+            raise RuntimeError("backward: the output tensor has stop_gradient=True (no grad node to start from)")
+        node, slot = _edge(t)
+        roots.append((node, slot, g))
+    with torch.set_grad_enabled(create_graph):
+        return native.module().run_backward(roots, captures, _HOOKS, _HELPERS)
+
+
+def backward(outs, grads, retain_graph=False):
+    """Run backward from ``outs`` (torch tensors) seeded with ``grads``; leaves accumulate into ``.grad``.
+    Hooks of non-leaf tensors belong to this graph and are dropped afterwards unless ``retain_graph``."""
+    _run(outs, grads, [], False)
+    if not retain_graph:
+        for k in [k for k in _HOOKS if not isinstance(k[0], _ACC)]:
+            del _HOOKS[k]
+
+
+_ACC = type(torch.autograd.graph.get_gradient_edge(torch.zeros(1, requires_grad=True)).node)
+
+
+def grad(outs, ins, grads, create_graph=False, allow_unused=False):
+    caps = []
+    for t in ins:
+        if not t.requires_grad:
+            raise RuntimeError("paddle.grad: an input tensor has stop_gradient=True")
+        caps.append(_edge(t))
+    res = _run(outs, grads, caps, create_graph)
+    for r in res:
+        if r is None and not allow_unused:
+            raise RuntimeError("paddle.grad: one of the inputs is not reachable from the outputs; "
+                               "set allow_unused=True to return None for it")
+    if not create_graph:
+        res = [None if r is None else r.detach() for r in res]
+    return res

@@ -58,6 +58,11 @@ def _wrap_nested(x):
     return x
 
 
+class _FnRemover:
+    def __init__(self, fn):
+        self.remove = fn
+
+
 class _HookHandle:
     def __init__(self, h):
         self._h = h
@@ -408,6 +413,10 @@ class Tensor:
         g = _unwrap(grad_tensor)
         if g is None:
             g = torch.ones_like(self._t)
+        from ..autograd import engine as _eng
+        if _eng.use_native():
+            _eng.backward([self._t], [g], retain_graph=retain_graph)
+            return
         self._t.backward(g, retain_graph=retain_graph)
 
     def clear_grad(self, set_to_zero=True):
@@ -428,9 +437,16 @@ class Tensor:
         def _h(g):
             r = hook(_wrap(g))
             return None if r is None else _unwrap(r)
+        from ..autograd import engine as _eng
+        if _eng.use_native():  # the native engine applies hooks from its (node, slot) table
+            return _HookHandle(_FnRemover(_eng.add_hook(self._t, _h)))
         return _HookHandle(self._t.register_hook(_h))
 
     def retain_grads(self):
+        from ..autograd import engine as _eng
+        if _eng.use_native():
+            _eng.retain(self._t)
+            return
         self._t.retain_grad()
 
     def detach(self):

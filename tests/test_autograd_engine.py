@@ -1,0 +1,201 @@
+"""Native eager backward engine (csrc/runtime/autograd_engine.cpp, FLAGS_eager_backward_engine=native) against
+PyTorch's engine on the same grad nodes. Reference semantics: paddle/fluid/eager/backward.cc:105 (RunBackward),
+python/paddle/autograd/backward_mode.py, general_grad.h (paddle.grad)."""
+import contextlib
+
+import numpy as np
+import pytest
+import torch
+
+import paddlepaddle_amd as paddle
+from paddlepaddle_amd.autograd import engine
+from paddlepaddle_amd.utils import native
+
+pytestmark = pytest.mark.skipif(not native.available(), reason="_C_runtime not built")
+
+
+@contextlib.contextmanager
+def eng(name):
+    old = paddle.get_flags("FLAGS_eager_backward_engine")["FLAGS_eager_backward_engine"]
+    paddle.set_flags({"FLAGS_eager_backward_engine": name})
+    try:
+        yield
+    finally:
+        paddle.set_flags({"FLAGS_eager_backward_engine": old})
+
+
+def _grads_both(build, params_fn, device="cpu"):
+    out = {}
+    for name in ("torch", "native"):
+        with eng(name):
+            paddle.seed(5)
+            model, inputs = build()
+            loss = model(*inputs)
+            loss.backward()
+            out[name] = [None if p.grad is None else p.grad.numpy().astype("float64") for p in params_fn(model)]
+    return out["torch"], out["native"]
+
+
+def test_native_engine_selected():
+    with eng("native"):
+        assert engine.use_native()
+    with eng("torch"):
+        assert not engine.use_native()
+
+
+def test_mlp_parity():
+    def build():
+        net = paddle.nn.Sequential(paddle.nn.Linear(8, 16), paddle.nn.GELU(), paddle.nn.Linear(16, 4))
+        x = paddle.randn([5, 8])
+        return (lambda a: (net(a) ** 2).mean()), [x]
+    # the same weights in both runs (seeded build); compare all parameter gradients
+    res = {}
+    for name in ("torch", "native"):
+        with eng(name):
+            paddle.seed(11)
+            net = paddle.nn.Sequential(paddle.nn.Linear(8, 16), paddle.nn.GELU(), paddle.nn.Linear(16, 4))
+            x = paddle.randn([5, 8])
+            (net(x) ** 2).mean().backward()
+            res[name] = [p.grad.numpy() for p in net.parameters()]
+    for a, b in zip(res["torch"], res["native"]):
+        np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-7)
+
+
+def test_conv_bn_parity():
+    res = {}
+    for name in ("torch", "native"):
+        with eng(name):
+            paddle.seed(3)
+            net = paddle.nn.Sequential(paddle.nn.Conv2D(3, 8, 3, padding=1), paddle.nn.BatchNorm2D(8),
+                                       paddle.nn.ReLU(), paddle.nn.AdaptiveAvgPool2D(1), paddle.nn.Flatten(),
+                                       paddle.nn.Linear(8, 10))
+            x = paddle.randn([4, 3, 8, 8])
+            y = paddle.randint(0, 10, [4])
+            paddle.nn.functional.cross_entropy(net(x), y).backward()
+            res[name] = [p.grad.numpy() for p in net.parameters() if p.grad is not None]
+    assert len(res["torch"]) == len(res["native"])
+    for a, b in zip(res["torch"], res["native"]):
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_gpt_tiny_parity_and_accumulation():
+    from paddlepaddle_amd.models.gpt import GPTConfig, GPTForPretraining, GPTPretrainingCriterion
+    res = {}
+    for name in ("torch", "native"):
+        with eng(name):
+            paddle.seed(7)
+            cfg = GPTConfig.tiny(hidden_size=64, num_attention_heads=4, intermediate_size=128, num_hidden_layers=2,
+                                 vocab_size=97, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+            model = GPTForPretraining(cfg)
+            crit = GPTPretrainingCriterion(cfg)
+            ids = paddle.randint(0, 97, [2, 17])
+            for _ in range(2):  # two micro-batches: leaf gradients accumulate
+                crit(model(ids[:, :-1]), ids[:, 1:]).backward()
+            res[name] = {n: p.grad.numpy() for n, p in model.named_parameters() if p.grad is not None}
+    assert res["torch"].keys() == res["native"].keys() and len(res["torch"]) > 10
+    for k in res["torch"]:
+        np.testing.assert_allclose(res["torch"][k], res["native"][k], rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+def test_hooks_retain_grads_and_multi_output():
+    with eng("native"):
+        x = paddle.to_tensor(np.arange(6, dtype="float32"), stop_gradient=False)
+        a, b = paddle.split(x * 1.0, 2)
+        a.retain_grads()
+        calls = []
+        h = a.register_hook(lambda g: (calls.append(1), g * 10)[1])
+        loss = (a * 2).sum() + (b * b).sum() * 0  # b's slot contributes a zero gradient
+        loss.backward()
+        np.testing.assert_allclose(x.grad.numpy(), [20, 20, 20, 0, 0, 0])
+        np.testing.assert_allclose(a.grad.numpy(), [2, 2, 2])  # retained before the hook ran, like paddle
+        assert calls == [1]
+        assert h.remove()
+        # leaf hook: applied to the leaf's summed gradient before accumulation
+        w = paddle.to_tensor([1.0, 2.0], stop_gradient=False)
+        w.register_hook(lambda g: g + 1)
+        ((w * 3).sum() + (w * 4).sum()).backward()
+        np.testing.assert_allclose(w.grad.numpy(), [8, 8])
+
+
+def test_pylayer_and_unused_slot_zero_fill():
+    class TwoOut(paddle.autograd.PyLayer):
+        @staticmethod
+        def forward(ctx, x):
+            return x * 2, x * 3
+
+        @staticmethod
+        def backward(ctx, g1, g2):
+            return g1 * 2 + g2 * 3
+
+    with eng("native"):
+        x = paddle.to_tensor([1.0, -1.0], stop_gradient=False)
+        p, q = TwoOut.apply(x)
+        p.sum().backward()  # q's gradient slot is undefined -> zeros for the Python backward
+        np.testing.assert_allclose(x.grad.numpy(), [2, 2])
+
+
+def test_paddle_grad_prune_capture_and_double_backward():
+    with eng("native"):
+        a = paddle.to_tensor([1.0, 2.0, 3.0], stop_gradient=False)
+        c = paddle.to_tensor([5.0], stop_gradient=False)
+        u = paddle.to_tensor([1.0], stop_gradient=False)
+        out = (a ** 3).sum() + c.sum() * 2
+        ga, gc, gu = paddle.grad(out, [a, c, u], create_graph=True, allow_unused=True)
+        np.testing.assert_allclose(ga.numpy(), [3, 12, 27])
+        np.testing.assert_allclose(gc.numpy(), [2])
+        assert gu is None
+        assert a.grad is None and c.grad is None  # paddle.grad captures, does not accumulate
+        (gga,) = paddle.grad(ga.sum(), a)
+        np.testing.assert_allclose(gga.numpy(), [6, 12, 18])
+        with pytest.raises(RuntimeError):
+            paddle.grad((a * 2).sum(), [u])
+
+
+def test_amp_dtype_mixing():
+    res = {}
+    for name in ("torch", "native"):
+        with eng(name):
+            paddle.seed(2)
+            lin = paddle.nn.Linear(8, 8)
+            x = paddle.randn([4, 8])
+            y = lin(x).astype("bfloat16")
+            (y.astype("float32") * 3).sum().backward()
+            res[name] = lin.weight.grad.numpy()
+    np.testing.assert_allclose(res["torch"], res["native"], rtol=1e-6)
+
+
+def test_post_accumulate_hooks_fire():
+    # DataParallel / sharding grad-ready hooks ride on the leaf accumulation node
+    with eng("native"):
+        w = paddle.to_tensor([1.0, 2.0], stop_gradient=False)
+        seen = []
+        w._t.register_post_accumulate_grad_hook(lambda t: seen.append(t.grad.clone()))
+        (w * w).sum().backward()
+        assert len(seen) == 1
+        np.testing.assert_allclose(seen[0].numpy(), [2, 4])
+
+
+@pytest.mark.gpu
+def test_gpt_tiny_hip_kernels_native_engine():
+    from paddlepaddle_amd.models.gpt import GPTConfig, GPTForPretraining, GPTPretrainingCriterion
+    from paddlepaddle_amd.ops import _loader
+    assert torch.cuda.is_available() and _loader._LIB is not None
+    paddle.set_device("gpu:0")
+    res = {}
+    for name in ("torch", "native"):
+        with eng(name):
+            paddle.seed(7)
+            cfg = GPTConfig.tiny(hidden_size=256, num_attention_heads=2, intermediate_size=1024,
+                                 hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+            paddle.set_default_dtype("bfloat16")
+            model = GPTForPretraining(cfg)
+            paddle.set_default_dtype("float32")
+            crit = GPTPretrainingCriterion(cfg)
+            ids = paddle.randint(0, cfg.vocab_size, [2, 129])
+            crit(model(ids[:, :-1]), ids[:, 1:]).backward()
+            torch.cuda.synchronize()
+            res[name] = {n: p.grad.astype("float32").numpy() for n, p in model.named_parameters()
+                         if p.grad is not None}
+    assert res["torch"].keys() == res["native"].keys()
+    for k in res["torch"]:
+        np.testing.assert_allclose(res["torch"][k], res["native"][k], rtol=2e-2, atol=2e-3, err_msg=k)
