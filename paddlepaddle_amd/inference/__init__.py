@@ -10,6 +10,8 @@ from __future__ import annotations
 
 import enum
 
+import os
+
 import numpy as np
 import torch
 
@@ -167,6 +169,15 @@ class Predictor:
         dev = torch.device(f"cuda:{config._device_id}") if (config._use_gpu and torch.cuda.is_available()) \
             else torch.device("cpu")
         self._dev = dev
+        self._runner = None
+        from ..framework import program_desc as _pd
+        if os.path.exists(config._prefix + ".pdmodel") and _pd.is_program_desc(config._prefix + ".pdmodel"):
+            # reference-format ProgramDesc: run op by op over this framework's kernels
+            self._runner = _pd.load(config._prefix, dev)
+            self._in_names = list(self._runner.program.feed_names)
+            self._out_names = list(self._runner.program.fetch_names)
+            self._inputs, self._outputs, self._graphs = {}, {}, {}
+            return
         prog, fetch, _ = _sio.read_program(config._prefix, dev, config._params)
         self._prog = prog
         self._fetch = fetch
@@ -210,6 +221,14 @@ class Predictor:
         if inputs is not None:  # new-style API: list in, list out
             for n, v in zip(self._in_names, inputs):
                 self._inputs[n] = v
+        if self._runner is not None:
+            def _t(v):
+                v = v._t if hasattr(v, "_t") else v
+                return (v if isinstance(v, torch.Tensor) else torch.from_numpy(np.asarray(v))).to(self._dev)
+            feeds = {n: _wrap(_t(self._inputs[n])) for n in self._in_names}
+            outs = [o._t for o in self._runner.run(feeds)]
+            self._outputs = dict(zip(self._out_names, outs))
+            return [_wrap(o) for o in outs] if inputs is not None else True
         tens = {n: self._to_dev(n, self._inputs[n]) for n in self._in_names}
         with torch.no_grad():
             if self._config._hip_graph and self._dev.type == "cuda":

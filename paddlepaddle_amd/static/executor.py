@@ -252,6 +252,10 @@ class Executor:
         prog = program if program is not None else _main
         if isinstance(prog, CompiledProgram):
             prog = prog._program
+        from ..framework.program_desc import ProgramDescRunner
+        if isinstance(prog, ProgramDescRunner):  # a reference-format .pdmodel from load_inference_model
+            outs = prog.run(feed or {})
+            return [o.numpy() for o in outs] if return_numpy else outs
         if not prog.nodes and not prog.feeds:
             return []  # startup program: parameters are initialised eagerly at creation
         fetch_list = [] if fetch_list is None else (fetch_list if isinstance(fetch_list, (list, tuple))

@@ -125,10 +125,18 @@ def read_program(path_prefix, device=None, params_file=None):
 
 
 def load_inference_model(path_prefix, executor=None, **kwargs):
+    """Loads either format: a reference ProgramDesc protobuf ``.pdmodel`` (run by
+    framework/program_desc.ProgramDescRunner over this framework's ops; Executor.run accepts it as the
+    program) or this framework's JSON program."""
     dev = None
     if executor is not None and executor.place is not None:
         from ..framework.place import to_torch_device
         dev = to_torch_device(executor.place)
+    from ..framework import program_desc as _pd
+    base = path_prefix[:-len(".pdmodel")] if path_prefix.endswith(".pdmodel") else path_prefix
+    if os.path.exists(base + ".pdmodel") and _pd.is_program_desc(base + ".pdmodel"):
+        runner = _pd.load(base, dev)
+        return [runner, list(runner.program.feed_names), list(runner.program.fetch_names)]
     prog, fetch, _ = read_program(path_prefix, dev)
     feed_names = list(prog.feeds)
     fetch_vars = [P._Var(prog, s, f"fetch_{i}") for i, s in enumerate(fetch)]
