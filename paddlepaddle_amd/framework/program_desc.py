@@ -624,3 +624,228 @@ class ProgramDescBuilder:
             f.write(self.to_bytes())
         names = sorted(self.params)
         write_combined(path_prefix + ".pdiparams", [self.params[n] for n in names])
+
+
+# ------------------------------------------------------------------------------------------------ exporter
+class _Exporter:
+    """Lowers this framework's recorded static Program (static/program.py OpNodes) to reference operators."""
+
+    def __init__(self, prog, const_names):
+        self.prog, self.cn = prog, const_names
+        self.b = ProgramDescBuilder()
+        self.n_tmp = 0
+        self.alias = {}  # slot -> feed name
+
+    def name(self, a):
+        from ..static import program as P
+        if isinstance(a, P._Ref):
+            return self.alias.get(a.i, f"t{a.i}")
+        if isinstance(a, P._Const):
+            n = self.cn[a.idx]
+            if n not in self.b.params:
+                self.b.param(n, self.prog._consts[a.idx])
+            return n
+        return None
+
+    def ndim(self, a):
+        from ..static import program as P
+        if isinstance(a, P._Ref):
+            return len(self.prog._metas[a.i].shape)
+        return self.prog._consts[a.idx].dim()
+
+    def tmp(self):
+        self.n_tmp += 1
+        return f"tmp_{self.n_tmp}"
+
+    def declare(self, slot):
+        slot = getattr(slot, "i", slot)
+        m = self.prog._metas[slot]
+        name = self.alias.get(slot, f"t{slot}")
+        self.b.var(name, list(m.shape), m.dtype)
+        return name
+
+    def emit(self, node):
+        outs = node.outs if isinstance(node.outs, (list, tuple)) else [node.outs]
+        out = [self.declare(s) for s in outs]
+        key = node.name.split(":")[-1]
+        fn = getattr(self, "op_" + key, None)
+        if fn is None:
+            raise NotImplementedError(f"no reference operator lowering for recorded op {node.name!r}")
+        fn(out, list(node.args), dict(node.kwargs))
+
+    def op(self, ty, ins, outs, **attrs):
+        self.b.op(ty, ins, outs, **attrs)
+
+    # --- lowerings (reference operator definitions: paddle/phi/ops/yaml/op_compat.yaml names / attributes)
+    def op_fused_linear(self, out, a, k):
+        x, w, bias, act = (a + [None, None])[:4]
+        act = act or k.get("act")
+        cur = out[0] if bias is None and act is None else self.tmp()
+        self.op("matmul_v2", {"X": [self.name(x)], "Y": [self.name(w)]}, {"Out": [cur]}, trans_x=False, trans_y=False)
+        if bias is not None:
+            nxt = out[0] if act is None else self.tmp()
+            self.op("elementwise_add", {"X": [cur], "Y": [self.name(bias)]}, {"Out": [nxt]}, axis=-1)
+            cur = nxt
+        if act is not None:
+            if act.startswith("gelu"):
+                self.op("gelu", {"X": [cur]}, {"Out": [out[0]]}, approximate=act != "gelu")
+            else:
+                self.op({"swish": "silu"}.get(act, act), {"X": [cur]}, {"Out": [out[0]]})
+
+    def op_layer_norm(self, out, a, k):
+        x, w, b, eps = a[:4]
+        ins = {"X": [self.name(x)]}
+        if w is not None:
+            ins["Scale"] = [self.name(w)]
+        if b is not None:
+            ins["Bias"] = [self.name(b)]
+        nd = self.ndim(w) if w is not None else 1
+        self.op("layer_norm", ins, {"Y": [out[0]], "Mean": [self.tmp()], "Variance": [self.tmp()]},
+                epsilon=float(eps), begin_norm_axis=self.ndim(x) - nd)
+
+    def op_gelu(self, out, a, k):
+        approx = a[1] if len(a) > 1 else k.get("approximate", False)
+        self.op("gelu", {"X": [self.name(a[0])]}, {"Out": out},
+                approximate=bool(approx) and approx != "none")
+
+    def _unary(ty):
+        return lambda self, out, a, k: self.op(ty, {"X": [self.name(a[0])]}, {"Out": out})
+    op_relu = _unary("relu")
+    op_sigmoid = _unary("sigmoid")
+    op_tanh = _unary("tanh")
+    op_silu = _unary("silu")
+    op_exp = _unary("exp")
+    op_sqrt = _unary("sqrt")
+    op_rsqrt = _unary("rsqrt")
+    op_abs = _unary("abs")
+    op_log = _unary("log")
+
+    def op_softmax(self, out, a, k):
+        axis = a[1] if len(a) > 1 else k.get("dim", k.get("axis", -1))
+        self.op("softmax", {"X": [self.name(a[0])]}, {"Out": out}, axis=int(axis))
+
+    def _binary(ty, scale_of):
+        def run(self, out, a, k):
+            x, y = a[0], a[1]
+            if isinstance(y, (int, float)):
+                s, bias = scale_of(float(y))
+                self.op("scale", {"X": [self.name(x)]}, {"Out": out}, scale=s, bias=bias, bias_after_scale=True)
+            else:
+                self.op(ty, {"X": [self.name(x)], "Y": [self.name(y)]}, {"Out": out}, axis=-1)
+        return run
+    op_add = _binary("elementwise_add", lambda v: (1.0, v))
+    op_sub = _binary("elementwise_sub", lambda v: (1.0, -v))
+    op_mul = _binary("elementwise_mul", lambda v: (v, 0.0))
+    op_div = _binary("elementwise_div", lambda v: (1.0 / v, 0.0))
+    op_true_divide = op_div
+
+    def op_matmul(self, out, a, k):
+        self.op("matmul_v2", {"X": [self.name(a[0])], "Y": [self.name(a[1])]}, {"Out": out}, trans_x=False,
+                trans_y=False)
+
+    def op_unsqueeze(self, out, a, k):
+        d = a[1] if len(a) > 1 else k["dim"]
+        self.op("unsqueeze2", {"X": [self.name(a[0])]}, {"Out": out, "XShape": [self.tmp()]},
+                axes=[int(v) for v in (d if isinstance(d, (list, tuple)) else [d])])
+
+    def op_permute(self, out, a, k):
+        perm = list(a[1]) if len(a) == 2 and isinstance(a[1], (list, tuple)) else [int(v) for v in a[1:]]
+        self.op("transpose2", {"X": [self.name(a[0])]}, {"Out": out, "XShape": [self.tmp()]}, axis=perm)
+
+    def op_transpose(self, out, a, k):
+        nd = self.ndim(a[0])
+        d0, d1 = a[1] % nd, a[2] % nd
+        perm = list(range(nd))
+        perm[d0], perm[d1] = perm[d1], perm[d0]
+        self.op("transpose2", {"X": [self.name(a[0])]}, {"Out": out, "XShape": [self.tmp()]}, axis=perm)
+
+    def op_reshape(self, out, a, k):
+        shape = list(a[1]) if len(a) == 2 and isinstance(a[1], (list, tuple)) else [int(v) for v in a[1:]]
+        self.op("reshape2", {"X": [self.name(a[0])]}, {"Out": out, "XShape": [self.tmp()]},
+                shape=[int(v) for v in shape])
+    op_view = op_reshape
+
+    def op_to(self, out, a, k):
+        dt = next((v for v in list(a[1:]) + list(k.values()) if isinstance(v, torch.dtype)), None)
+        src = self.name(a[0])
+        if dt is None or src == out[0]:
+            if src != out[0]:
+                self.op("assign", {"X": [src]}, {"Out": out})
+            if dt is None or self.prog._metas[a[0].i].dtype == dt:
+                return
+        self.op("cast", {"X": [src]}, {"Out": out}, in_dtype=_PROTO[self.prog._metas[a[0].i].dtype],
+                out_dtype=_PROTO[dt])
+
+    def op_cat(self, out, a, k):
+        axis = a[1] if len(a) > 1 else k.get("dim", 0)
+        self.op("concat", {"X": [self.name(t) for t in a[0]]}, {"Out": out}, axis=int(axis))
+
+    def op_batch_norm(self, out, a, k):
+        x, mean, var = a[:3]
+        self.op("batch_norm", {"X": [self.name(x)], "Scale": [self.name(k["weight"])], "Bias": [self.name(k["bias"])],
+                               "Mean": [self.name(mean)], "Variance": [self.name(var)]},
+                {"Y": out}, epsilon=float(k.get("eps", 1e-5)), is_test=True, data_layout="NCHW")
+
+    @staticmethod
+    def _pair(v):
+        return [int(v), int(v)] if isinstance(v, int) else [int(x) for x in v]
+
+    def op_avg_pool2d(self, out, a, k):
+        x, ks = a[0], a[1]
+        stride = a[2] if len(a) > 2 and a[2] is not None else ks
+        pad = a[3] if len(a) > 3 else 0
+        ceil = bool(a[4]) if len(a) > 4 else False
+        incl = bool(a[5]) if len(a) > 5 else True
+        self.op("pool2d", {"X": [self.name(x)]}, {"Out": out}, pooling_type="avg", ksize=self._pair(ks),
+                strides=self._pair(stride), paddings=self._pair(pad), global_pooling=False, adaptive=False,
+                ceil_mode=ceil, exclusive=not incl, data_format="NCHW", padding_algorithm="EXPLICIT")
+
+    def op_max_pool2d(self, out, a, k):
+        x, ks = a[0], a[1]
+        stride = k.get("stride", a[2] if len(a) > 2 else None) or ks
+        pad = k.get("padding", a[3] if len(a) > 3 else 0)
+        self.op("pool2d", {"X": [self.name(x)]}, {"Out": out}, pooling_type="max", ksize=self._pair(ks),
+                strides=self._pair(stride), paddings=self._pair(pad), global_pooling=False, adaptive=False,
+                ceil_mode=bool(k.get("ceil_mode", False)), exclusive=True, data_format="NCHW",
+                padding_algorithm="EXPLICIT")
+
+    def op_mean(self, out, a, k):
+        dims = a[1] if len(a) > 1 else k.get("dim")
+        keep = bool(k.get("keepdim", a[2] if len(a) > 2 else False))
+        if dims is None:
+            self.op("reduce_mean", {"X": [self.name(a[0])]}, {"Out": out}, dim=[0], keep_dim=keep, reduce_all=True)
+        else:
+            dims = [int(d) for d in (dims if isinstance(dims, (list, tuple)) else [dims])]
+            self.op("reduce_mean", {"X": [self.name(a[0])]}, {"Out": out}, dim=dims, keep_dim=keep,
+                    reduce_all=False)
+
+    def op_conv2d(self, out, a, k):
+        x, w, b = a[0], a[1], (a[2] if len(a) > 2 else None)
+        stride, pad, dil, groups = (list(a[3:7]) + [1, 0, 1, 1][len(a[3:7]):])
+        cur = out[0] if b is None else self.tmp()
+        self.op("conv2d", {"Input": [self.name(x)], "Filter": [self.name(w)]}, {"Output": [cur]},
+                strides=self._pair(stride), paddings=self._pair(pad), dilations=self._pair(dil), groups=int(groups),
+                padding_algorithm="EXPLICIT", data_format="NCHW")
+        if b is not None:
+            self.op("elementwise_add", {"X": [cur], "Y": [self.name(b)]}, {"Out": out}, axis=1)
+
+    def op_flatten(self, out, a, k):
+        s = a[1] if len(a) > 1 else k.get("start_dim", 0)
+        e = a[2] if len(a) > 2 else k.get("end_dim", -1)
+        self.op("flatten_contiguous_range", {"X": [self.name(a[0])]}, {"Out": out, "XShape": [self.tmp()]},
+                start_axis=int(s), stop_axis=int(e))
+
+
+def export(prog, fetch_slots, feed_names, const_names):
+    """A recorded static Program (pruned to the fetch targets) as a reference ProgramDescBuilder."""
+    ex = _Exporter(prog, const_names)
+    b = ex.b
+    for name in feed_names:
+        slot, shape, dtype = prog.feeds[name]
+        ex.alias[slot] = name
+        b.feed(name, list(shape), getattr(torch, dtype))
+    for n in prog.nodes:
+        ex.emit(n)
+    for s in fetch_slots:
+        b.fetch(ex.alias.get(s, f"t{s}"))
+    return b

@@ -85,6 +85,11 @@ def save_inference_model(path_prefix, feed_vars, fetch_vars, executor=None, prog
     q = _prune(prog, fetch)
     feeds = [v if isinstance(v, str) else v.name for v in feed_vars]
     q.feeds = {k: prog.feeds[k] for k in feeds}
+    if kwargs.get("program_format", "json") == "protobuf":
+        # the reference's ProgramDesc .pdmodel + save_combine .pdiparams (framework/program_desc.py)
+        from ..framework import program_desc as _pd
+        _pd.export(q, fetch, feeds, _const_names(q)).save(path_prefix)
+        return
     write_program(path_prefix, q, fetch)
 
 

@@ -173,3 +173,59 @@ def test_unmapped_operator_is_reported(tmp_path):
     b.save(str(tmp_path / "bad"))
     with pytest.raises(NotImplementedError, match="some_custom_op"):
         pd.load(str(tmp_path / "bad"), torch.device("cpu"))
+
+
+def _static_models():
+    paddle.seed(4)
+    x = paddle.static.data("x", [-1, 8], "float32")
+    lin, ln = paddle.nn.Linear(8, 6), paddle.nn.LayerNorm(6)
+    y = paddle.nn.functional.gelu(ln(lin(x)))
+    y = paddle.nn.functional.sigmoid(y) * 2.0 - paddle.tanh(y) / 3.0
+    y = paddle.reshape(paddle.transpose(paddle.unsqueeze(y, 1), [0, 2, 1]), [-1, 6])
+    y = paddle.concat([y, y + 1.0], axis=1)
+    y = paddle.nn.functional.softmax(paddle.matmul(y, y, transpose_y=True), axis=-1)
+    im = paddle.static.data("im", [-1, 3, 8, 8], "float32")
+    conv = paddle.nn.Conv2D(3, 4, 3, padding=1)
+    bn = paddle.nn.BatchNorm2D(4)
+    bn.eval()
+    h = paddle.nn.functional.relu(bn(conv(im)))
+    h = paddle.nn.functional.max_pool2d(h, 2, 2)
+    h = paddle.nn.functional.avg_pool2d(h, 2)
+    q = paddle.flatten(h, 1)
+    return (x, im), (y, q)
+
+
+def test_static_program_exports_to_reference_format(tmp_path):
+    rng = np.random.RandomState(5)
+    xs = {"x": rng.randn(3, 8).astype("float32"), "im": rng.randn(2, 3, 8, 8).astype("float32")}
+    paddle.enable_static()
+    try:
+        main, startup = paddle.static.Program(), paddle.static.Program()
+        with paddle.static.program_guard(main, startup):
+            feeds, fetches = _static_models()
+        exe = paddle.static.Executor(paddle.CPUPlace())
+        exe.run(startup)
+        ref = exe.run(main, feed=xs, fetch_list=list(fetches))
+        prefix = str(tmp_path / "exported")
+        paddle.static.save_inference_model(prefix, list(feeds), list(fetches), exe, program=main,
+                                           program_format="protobuf")
+        assert pd.is_program_desc(prefix + ".pdmodel")
+        prog, feed_names, fetch_names = paddle.static.load_inference_model(prefix, exe)
+        assert feed_names == ["x", "im"]
+        got = exe.run(prog, feed=xs, fetch_list=fetch_names)
+    finally:
+        paddle.disable_static()
+    types = {o["type"] for o in prog.program.ops}
+    assert {"matmul_v2", "layer_norm", "gelu", "conv2d", "batch_norm", "pool2d", "transpose2", "reshape2",
+            "concat", "softmax", "scale", "flatten_contiguous_range"} <= types
+    for a, b in zip(ref, got):
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_reference_program_runs_on_gpu(tmp_path):
+    prefix, x, ref = _mlp(tmp_path)
+    runner = pd.load(prefix, torch.device("cuda:0"))
+    (out,) = runner.run({"x": paddle.Tensor(torch.from_numpy(x).cuda())})
+    assert out._t.is_cuda
+    np.testing.assert_allclose(out.numpy(), ref, rtol=1e-4, atol=1e-5)
