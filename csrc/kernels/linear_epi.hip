@@ -47,7 +47,7 @@ __global__ __launch_bounds__(256) void colsum_partial_k(const T* __restrict__ x,
 // serial 256-deep loop per thread (which left all but ~10 CUs idle on a 20480-column bias).
 template <typename T>
 __global__ __launch_bounds__(256) void fold_partials_k(const float* __restrict__ part, T* __restrict__ out,
-                                                       int64_t cols, int nparts) {
+                                                       int64_t cols, int nparts, int accumulate) {
   __shared__ float red[32][65];
   const int cv = threadIdx.x & 7, rg = threadIdx.x >> 3;
   const int64_t c = (int64_t)blockIdx.x * 64 + cv * 8;
@@ -74,6 +74,12 @@ __global__ __launch_bounds__(256) void fold_partials_k(const float* __restrict__
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = red[0][cv * 8 + j];
+    if (accumulate) {  // gradient-accumulation fusion: out += column sums (the parameter's .grad buffer)
+      float o[8];
+      load8<T>(out + c, o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += o[j];
+    }
     store8<T>(out + c, v);
   }
 }
@@ -149,25 +155,29 @@ inline unsigned grid_ew(int64_t nvec) {
 }  // namespace
 
 // workspace: fp32 [256 * cols] (caller-provided, reused)
-PA_EXPORT int pa_colsum(const void* x, void* out, float* ws, int64_t rows, int64_t cols, int dtype, hipStream_t st) {
+// dtype bit 8: accumulate into `out` instead of overwriting it
+PA_EXPORT int pa_colsum(const void* x, void* out, float* ws, int64_t rows, int64_t cols, int dtype_acc, hipStream_t st) {
+  const int dtype = dtype_acc & 0xff, acc = (dtype_acc >> 8) & 1;
   const int np = nparts_for(rows);
   dim3 g1((unsigned)cdiv(cols, 2048), (unsigned)np), g2((unsigned)cdiv(cols, 64));
   PA_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL((colsum_partial_k<T>), g1, dim3(256), 0, st, (const T*)x, ws, rows, cols, np);
-    hipLaunchKernelGGL((fold_partials_k<T>), g2, dim3(256), 0, st, ws, (T*)out, cols, np);
+    hipLaunchKernelGGL((fold_partials_k<T>), g2, dim3(256), 0, st, ws, (T*)out, cols, np, acc);
   });
   PA_CHECK_LAUNCH();
   return 0;
 }
 
+// dtype bit 8: accumulate the bias gradient into `db`
 PA_EXPORT int pa_bias_gelu_bwd(const void* h, const void* b, const void* dy, void* dh, void* db, float* ws,
-                               int64_t rows, int64_t cols, int dtype, hipStream_t st) {
+                               int64_t rows, int64_t cols, int dtype_acc, hipStream_t st) {
+  const int dtype = dtype_acc & 0xff, acc = (dtype_acc >> 8) & 1;
   const int np = nparts_for(rows);
   dim3 g1((unsigned)cdiv(cols, 2048), (unsigned)np), g2((unsigned)cdiv(cols, 64));
   PA_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL((bias_gelu_bwd_k<T>), g1, dim3(256), 0, st, (const T*)h, (const T*)b, (const T*)dy, (T*)dh,
                        ws, rows, cols, np);
-    hipLaunchKernelGGL((fold_partials_k<T>), g2, dim3(256), 0, st, ws, (T*)db, cols, np);
+    hipLaunchKernelGGL((fold_partials_k<T>), g2, dim3(256), 0, st, ws, (T*)db, cols, np, acc);
   });
   PA_CHECK_LAUNCH();
   return 0;

@@ -322,13 +322,16 @@ PA_EXPORT int pa_layer_norm_bwd(const void* dy, const void* x, const void* w, co
 }
 
 // Weight / bias gradient finalize of the norm backwards in one launch: out_a[c] = sum_p part_a[p][c],
-// out_b[c] = sum_p part_b[p][c] (part_b / out_b may be null), written in the parameters' dtypes.
+// out_b[c] = sum_p part_b[p][c] (part_b / out_b may be null), written in the parameters' dtypes. Bit 8 of a
+// dtype code accumulates into that output (out += sum: the parameter's .grad buffer) instead of overwriting it.
 // Block = 64 columns x 4 part groups, folded through LDS; grid (cols / 64, 2).
 __global__ __launch_bounds__(256) void reduce_parts_k(const float* __restrict__ pa, const float* __restrict__ pb,
                                                       void* oa, void* ob, int nparts, int64_t cols, int dta, int dtb) {
   const float* part = blockIdx.y == 0 ? pa : pb;
   void* out = blockIdx.y == 0 ? oa : ob;
-  const int dt = blockIdx.y == 0 ? dta : dtb;
+  const int dtc = blockIdx.y == 0 ? dta : dtb;
+  const int dt = dtc & 0xff;
+  const bool accum = (dtc >> 8) & 1;
   if (part == nullptr || out == nullptr) return;
   const int cx = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int64_t c = (int64_t)blockIdx.x * 64 + cx;
@@ -341,10 +344,17 @@ __global__ __launch_bounds__(256) void reduce_parts_k(const float* __restrict__ 
   sm[g][cx] = acc;
   __syncthreads();
   if (g == 0 && c < cols) {
-    const float v = sm[0][cx] + sm[1][cx] + sm[2][cx] + sm[3][cx];
-    if (dt == kF32) reinterpret_cast<float*>(out)[c] = v;
-    else if (dt == kBF16) reinterpret_cast<bf16*>(out)[c] = from_f<bf16>(v);
-    else reinterpret_cast<f16*>(out)[c] = from_f<f16>(v);
+    float v = sm[0][cx] + sm[1][cx] + sm[2][cx] + sm[3][cx];
+    if (dt == kF32) {
+      float* o = reinterpret_cast<float*>(out);
+      o[c] = accum ? o[c] + v : v;
+    } else if (dt == kBF16) {
+      bf16* o = reinterpret_cast<bf16*>(out);
+      o[c] = from_f<bf16>(accum ? to_f(o[c]) + v : v);
+    } else {
+      f16* o = reinterpret_cast<f16*>(out);
+      o[c] = from_f<f16>(accum ? to_f(o[c]) + v : v);
+    }
   }
 }
 

@@ -26,15 +26,26 @@ from .activation import bias_gelu, gelu
 from ..framework.trace_hook import static_op
 
 
-def colsum(x2d):
-    """Column sums of a [rows, cols] tensor (bias gradient)."""
+def colsum(x2d, acc=None):
+    """Column sums of a [rows, cols] tensor (bias gradient); added in place into ``acc`` when given."""
     rows, cols = x2d.shape
     if L.hip_enabled_for(x2d) and x2d.dtype in L._DT and cols % 8 == 0 and x2d.is_contiguous():
-        out = torch.empty(cols, dtype=x2d.dtype, device=x2d.device)
+        out = acc if acc is not None else torch.empty(cols, dtype=x2d.dtype, device=x2d.device)
         ws = torch.empty(256 * cols, dtype=torch.float32, device=x2d.device)
-        L.call("pa_colsum", L.ptr(x2d), L.ptr(out), L.ptr(ws), rows, cols, L.dcode(x2d), L.stream_ptr())
+        L.call("pa_colsum", L.ptr(x2d), L.ptr(out), L.ptr(ws), rows, cols,
+               L.dcode(x2d) | ((acc is not None) << 8), L.stream_ptr())
         return out
-    return x2d.float().sum(0).to(x2d.dtype)
+    s = x2d.float().sum(0).to(x2d.dtype)
+    return s if acc is None else acc.add_(s)
+
+
+def _vector_main_grad(p, dtype):
+    """(buffer, ready handler) when ``p``'s gradient accumulates in place (main-grad fusion for biases / norm
+    parameters: the finalize kernels add into the buffer), else None."""
+    ent = _main_grad_of(p) if p is not None else None
+    if ent is None or ent[1].dtype != dtype or not ent[1].is_contiguous():
+        return None
+    return ent[1], ent[2]
 
 
 # ---------------------------------------------------------------------------------------------
@@ -236,6 +247,7 @@ class _LinearFn(torch.autograd.Function):
         y = _fwd_mm(x2, w, b)
         ctx.save_for_backward(x2, w)
         ctx.has_b = b is not None
+        ctx.bias = b
         ctx.shape = shape
         ctx.dx_hook = dx_hook
         return y.view(*shape[:-1], w.shape[1])
@@ -249,7 +261,14 @@ class _LinearFn(torch.autograd.Function):
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         dx, dw = _mm_grads(x2, w, dy2, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.dx_hook)
-        db = colsum(dy2) if ctx.has_b and ctx.needs_input_grad[2] else None
+        db = None
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            mg = _vector_main_grad(ctx.bias, dy2.dtype)
+            if mg is not None:  # bias gradient added straight into its .grad buffer
+                colsum(dy2, acc=mg[0])
+                mg[1](ctx.bias)
+            else:
+                db = colsum(dy2)
         if dx is not None:
             dx = dx.view(ctx.shape)
         return dx, dw, db, None
@@ -262,6 +281,7 @@ class _LinearBiasGeluFn(torch.autograd.Function):
         x2 = x.reshape(-1, shape[-1])
         y, h, bb = _fwd_bias_gelu(x2, w, b)
         ctx.save_for_backward(x2, w, bb, h)
+        ctx.bias = b
         ctx.shape = shape
         ctx.dx_hook = dx_hook
         return y.view(*shape[:-1], w.shape[1])
@@ -272,10 +292,14 @@ class _LinearBiasGeluFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1]).to(h.dtype).contiguous()
         rows, cols = h.shape
         dh = torch.empty_like(h)
-        db = torch.empty(cols, dtype=b.dtype, device=b.device)
+        mg = _vector_main_grad(ctx.bias, b.dtype) if ctx.needs_input_grad[2] else None
+        db = mg[0] if mg is not None else torch.empty(cols, dtype=b.dtype, device=b.device)
         ws = torch.empty(256 * cols, dtype=torch.float32, device=h.device)
         L.call("pa_bias_gelu_bwd", L.ptr(h), L.ptr(b), L.ptr(dy2), L.ptr(dh), L.ptr(db), L.ptr(ws), rows, cols,
-               L.dcode(h), L.stream_ptr())
+               L.dcode(h) | ((mg is not None) << 8), L.stream_ptr())
+        if mg is not None:  # bias gradient added straight into its .grad buffer
+            mg[1](ctx.bias)
+            db = None
         dx, dw = _mm_grads(x2, w, dh, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.dx_hook)
         if dx is not None:
             dx = dx.view(ctx.shape)

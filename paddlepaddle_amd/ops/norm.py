@@ -13,16 +13,25 @@ from . import _loader as L
 from ..framework.trace_hook import static_op
 
 
-def _finalize_parts(pa, pb, dta, dtb, nparts, cols):
+def _finalize_parts(pa, pb, dta, dtb, nparts, cols, params=(None, None)):
     """Sum the [nparts, cols] fp32 partials of the weight (and bias) gradient into the parameters' dtypes:
-    one HIP launch for both instead of a reduction + a cast each."""
+    one HIP launch for both instead of a reduction + a cast each. A parameter whose gradient buffer is
+    registered for in-place accumulation (ops.linear.register_main_grad) gets the sum added straight into
+    that buffer (no separate autograd accumulation pass); None is returned for it."""
     dev = (pa if pa is not None else pb).device
     if L.has("pa_reduce_parts") and all(d in L._DT for d in (dta, dtb) if d is not None):
-        oa = torch.empty(cols, dtype=dta, device=dev) if pa is not None else None
-        ob = torch.empty(cols, dtype=dtb, device=dev) if pb is not None else None
+        from .linear import _vector_main_grad
+        mga = _vector_main_grad(params[0], dta) if pa is not None else None
+        mgb = _vector_main_grad(params[1], dtb) if pb is not None else None
+        oa = (mga[0] if mga else torch.empty(cols, dtype=dta, device=dev)) if pa is not None else None
+        ob = (mgb[0] if mgb else torch.empty(cols, dtype=dtb, device=dev)) if pb is not None else None
         L.call("pa_reduce_parts", L.ptr(pa), L.ptr(pb), L.ptr(oa), L.ptr(ob), nparts, cols,
-               L._DT[dta] if dta is not None else 0, L._DT[dtb] if dtb is not None else 0, L.stream_ptr())
-        return oa, ob
+               (L._DT[dta] | (bool(mga) << 8)) if dta is not None else 0,
+               (L._DT[dtb] | (bool(mgb) << 8)) if dtb is not None else 0, L.stream_ptr())
+        for mg, prm in ((mga, params[0]), (mgb, params[1])):
+            if mg:
+                mg[1](prm)
+        return (None if mga else oa), (None if mgb else ob)
     return (pa.sum(0).to(dta) if pa is not None else None), (pb.sum(0).to(dtb) if pb is not None else None)
 
 
@@ -91,6 +100,7 @@ class _LayerNormHIP(torch.autograd.Function):
         ctx.has_b = b is not None
         ctx.w_dtype = None if w is None else w.dtype
         ctx.b_dtype = None if b is None else b.dtype
+        ctx.params = (w, b)
         ctx.shape = x.shape
         return y.view(x.shape)
 
@@ -106,7 +116,7 @@ class _LayerNormHIP(torch.autograd.Function):
         L.call("pa_layer_norm_bwd", L.ptr(dy2), L.ptr(x2), L.ptr(wc), L.ptr(mean), L.ptr(rstd), L.ptr(dx),
                L.ptr(dw_part), L.ptr(db_part), L.ptr(None), rows, cols, L.dcode(x2) | (nparts << 8), L.stream_ptr())
         dw, db = _finalize_parts(dw_part if wc is not None else None, db_part if ctx.has_b else None, ctx.w_dtype,
-                                 ctx.b_dtype, nparts, cols)
+                                 ctx.b_dtype, nparts, cols, getattr(ctx, "params", (None, None)))
         return dx.view(ctx.shape), dw, db, None
 
 
@@ -142,7 +152,7 @@ class _LayerNormResidualHIP(torch.autograd.Function):
         L.call("pa_layer_norm_bwd", L.ptr(dy2), L.ptr(x2), L.ptr(wc), L.ptr(mean), L.ptr(rstd), L.ptr(dx),
                L.ptr(dw_part), L.ptr(db_part), L.ptr(res), rows, cols, L.dcode(x2) | (nparts << 8), L.stream_ptr())
         dw, db = _finalize_parts(dw_part if wc is not None else None, db_part if ctx.has_b else None, ctx.w_dtype,
-                                 ctx.b_dtype, nparts, cols)
+                                 ctx.b_dtype, nparts, cols, getattr(ctx, "params", (None, None)))
         return dx.view(ctx.shape), dw, db, None
 
 

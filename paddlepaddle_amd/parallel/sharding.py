@@ -31,6 +31,8 @@ from __future__ import annotations
 
 import contextlib
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -42,6 +44,10 @@ from ..nn.layer.layers import Layer
 
 def _is_nccl(pg):
     return dist.get_backend(pg) == "nccl"
+
+
+# biases / norm parameters accumulate in the HIP finalize kernels too (PADDLE_AMD_VECTOR_MAIN_GRAD=0: through autograd)
+_VECTOR_MAIN_GRAD = os.environ.get("PADDLE_AMD_VECTOR_MAIN_GRAD", "1") != "0"
 
 
 class _Flat:
@@ -98,8 +104,9 @@ class _Flat:
             for p, o, n in zip(self.params, self.offsets, self.numels):
                 view = self.full_grad[o:o + n].view(p._t.shape)
                 p._t.grad = view
-                if p._t.dim() == 2 and self.ready_fn is not None:
-                    # linear weights: the wgrad GEMM accumulates into this view directly
+                if self.ready_fn is not None and (p._t.dim() == 2 or _VECTOR_MAIN_GRAD):
+                    # linear weights: the wgrad GEMM accumulates into this view directly; biases and norm
+                    # parameters: the HIP gradient-finalize kernels add into it (no autograd accumulation pass)
                     register_main_grad(p._t, view, self.ready_fn)
         return self.full_grad
 

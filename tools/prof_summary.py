@@ -14,7 +14,9 @@ CATS = [
     ("bn/bn+relu(+add) (HIP)", re.compile(r"bn_(reduce|apply|bwd_apply|fwd_finalize|bwd_finalize)_k")),
     ("maxpool NHWC (HIP)", re.compile(r"maxpool_nhwc_(fwd|bwd)_k")),
     ("miopen/ck(conv/bn)", re.compile(r"miopen|igemm|naive_conv|batchnorm|grouped_conv|SubTensorOp|MIOpen", re.I)),
-    ("gemm(hipBLASLt/rocBLAS)", re.compile(r"^Cijk_|^Custom_Cijk|gemm|Gemm|rocblas")),
+    ("GEMM hipBLASLt/rocBLAS (vendor)", re.compile(r"^Cijk_|^Custom_Cijk|rocblas|hipblaslt", re.I)),
+    ("GEMM/conv hand-written (HIP)", re.compile(r"gemm256_kernel|gemm_bf16_kernel|gemm3s_kernel|gemm_tail_reduce|"
+                                                r"grouped_gemm|gemm_smallm|conv_|implicit_gemm|gemm")),
     ("flash_attn(HIP)", re.compile(r"fa_(fwd|bwd)|fa_delta|dq_convert")),
     ("norm(HIP)", re.compile(r"norm_(fwd|bwd)|layer_?norm|rms_?norm")),
     ("softmax/CE(HIP)", re.compile(r"softmax|xent|\bce_|_ce_")),
