@@ -64,6 +64,7 @@ class _RMSNormHIP(torch.autograd.Function):
                L.dcode(x2), L.stream_ptr())
         ctx.save_for_backward(x2, wc, rstd)
         ctx.w_dtype = None if w is None else w.dtype
+        ctx.params = (w, None)
         ctx.shape = x.shape
         return y.view(x.shape)
 
@@ -79,7 +80,8 @@ class _RMSNormHIP(torch.autograd.Function):
         dw_part = torch.empty(nparts, cols, dtype=torch.float32, device=x2.device) if wc is not None else None
         L.call("pa_rms_norm_bwd", L.ptr(dy2), L.ptr(x2), L.ptr(wc), L.ptr(rstd), L.ptr(dx), L.ptr(dw_part),
                rows, cols, L.dcode(x2) | (nparts << 8), L.stream_ptr())
-        dw, _ = _finalize_parts(dw_part, None, ctx.w_dtype, None, nparts, cols) if wc is not None else (None, None)
+        dw, _ = _finalize_parts(dw_part, None, ctx.w_dtype, None, nparts, cols, ctx.params) if wc is not None \
+            else (None, None)
         return dx.view(ctx.shape), dw, None
 
 

@@ -69,3 +69,21 @@ def test_layer_norm_params_accumulate_in_place():
     finally:
         LIN.unregister_main_grad(w)
         LIN.unregister_main_grad(b)
+
+
+def test_rms_norm_weight_accumulates_in_place():
+    torch.manual_seed(2)
+    x = torch.randn(384, 256, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(256, device="cuda")).to(torch.bfloat16).requires_grad_()
+    wbuf, wseen = _reg(w)
+    try:
+        y = NORM.rms_norm(x, w, 1e-6)
+        dy = torch.randn_like(y)
+        y.backward(dy)
+        torch.cuda.synchronize()
+        xr, wr = (t.detach().float().requires_grad_() for t in (x, w))
+        (xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * wr).backward(dy.float())
+        assert w.grad is None and wseen == [w]
+        torch.testing.assert_close(wbuf.float(), 0.5 + wr.grad, rtol=2e-2, atol=2e-1)
+    finally:
+        LIN.unregister_main_grad(w)
