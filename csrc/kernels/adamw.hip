@@ -32,8 +32,14 @@ __device__ __forceinline__ void st_any(void* p, int64_t i, int dt, float x) {
 
 __global__ __launch_bounds__(256) void adamw_multi_k(const int64_t* __restrict__ table, const int64_t* __restrict__ items,
                                                      int64_t n_items, const float* __restrict__ inv_scale_p, float lr,
-                                                     float b1, float b2, float eps, float bc1, float bc2) {
+                                                     float b1, float b2, float eps, float bc1, float bc2,
+                                                     const float* __restrict__ hyper) {
   const float inv_scale = inv_scale_p ? *inv_scale_p : 1.f;
+  if (hyper) {  // device-resident {lr, beta1^t, beta2^t}: a captured step keeps following the schedule on replay
+    lr = hyper[0];
+    bc1 = 1.f - hyper[1];
+    bc2 = 1.f - hyper[2];
+  }
   const float rbc2 = 1.f / bc2;
   for (int64_t it = blockIdx.x; it < n_items; it += gridDim.x) {
     const int64_t ti = items[it * 2], s = items[it * 2 + 1];
@@ -219,11 +225,27 @@ __global__ __launch_bounds__(256) void write_i64_k(int64_t* __restrict__ dst, Ar
 
 PA_EXPORT int pa_adamw_multi(const int64_t* table, const int64_t* items, int64_t n_items, const float* inv_scale,
                              float lr, float b1, float b2, float eps, float wd_unused, float bc1, float bc2,
-                             void* found_inf_unused, hipStream_t st) {
+                             const float* hyper, hipStream_t st) {
   if (n_items <= 0) return 0;
   int64_t g = n_items < 4096 ? n_items : 4096;
   hipLaunchKernelGGL(adamw_multi_k, dim3((unsigned)g), dim3(256), 0, st, table, items, n_items, inv_scale, lr, b1, b2,
-                     eps, bc1, bc2);
+                     eps, bc1, bc2, hyper);
+  PA_CHECK_LAUNCH();
+  return 0;
+}
+
+// One optimizer step of the device-resident Adam hyper-parameters {lr, beta1^t, beta2^t}: the beta powers advance
+// on the device (reference: the beta1_pow / beta2_pow accumulators updated inside adam_kernel), so a hipGraph that
+// captured the step applies the right bias correction on every replay; lr is written by the LR scheduler.
+__global__ void adam_hyper_step_k(float* hyper, float b1, float b2) {
+  if (threadIdx.x == 0) {
+    hyper[1] *= b1;
+    hyper[2] *= b2;
+  }
+}
+
+PA_EXPORT int pa_adam_hyper_step(float* hyper, float b1, float b2, hipStream_t st) {
+  hipLaunchKernelGGL(adam_hyper_step_k, dim3(1), dim3(64), 0, st, hyper, b1, b2);
   PA_CHECK_LAUNCH();
   return 0;
 }

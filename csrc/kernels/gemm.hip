@@ -695,6 +695,298 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p0) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// 256x256 tile, 4 waves (one per SIMD), 128x128 outputs per wave held in the accumulator file.
+// The 8-wave ping-pong kernel above hides latency by pairing two waves on each SIMD; PMC showed 31 % of its
+// wave cycles parked (barriers every phase, each wave reading its fragments from LDS while its partner
+// computes). This form keeps one wave per SIMD and hides latency inside the wave instead:
+//   * 8 x 8 MFMA 16x16x32 fragments per wave = 256 fp32 accumulators -> AGPRs (launch bounds 256 x 1 give the
+//     wave the whole 512-entry register file); a third less LDS read traffic per MFMA than 128x64 wave tiles.
+//   * K-tiles of 32 in a 4-slot LDS ring (4 x 32 KiB): tile t+1 is read into the second fragment register set
+//     while the 64 MFMAs of tile t run; tiles t+2, t+3 (+ t+4 issued after the barrier) stay in flight, so a
+//     glds has three K-tiles (~3k cycles) to land. One barrier per K-tile.
+//   * K-major images [256][32] (64-B rows) with the chunk swizzle c ^ 2*((row >> 3) & 1): the 16 rows x 4 chunks
+//     of one fragment ds_read_b128 hit 16 distinct 16-B bank slots in each lane group. MN-major images [32][256]
+//     (512-B rows) use the mn_swz swizzle and ds_read_b64_tr_b16 like the kernels above.
+__device__ __forceinline__ int k32_swz(int row) { return ((row >> 3) & 1) << 1; }
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// LDS-DMA staging of one operand's 256 x 32 tile through buffer_load_dwordx4 ... lds: the buffer descriptor
+// holds the tile's base address (advanced by scalar adds per K-tile), each lane's byte offset inside the tile
+// window is loop-invariant (4 pieces per wave), M0 the wave-uniform LDS destination: no VALU per load.
+template <bool KMAJ>
+struct Loader32 {
+  uint64_t base;    // wave-uniform address of (first row / column of the tile, k = 0)
+  uint64_t kstep;   // bytes per K-tile of 32
+  int voff[4];      // per-lane byte offsets of this wave's 4 pieces
+
+  __device__ __forceinline__ void init(const uint16_t* g, int64_t ld, int r0, int rmax, int wave, int lane) {
+    base = reinterpret_cast<uint64_t>(g) + (KMAJ ? (uint64_t)r0 * ld * 2 : (uint64_t)r0 * 2);
+    kstep = KMAJ ? 64 : (uint64_t)ld * 64;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = i * 4 + wave;  // 1-KiB piece of the 16-KiB operand image
+      if constexpr (KMAJ) {
+        const int row = q * 16 + (lane >> 2);
+        const int c = (lane & 3) ^ k32_swz(row);
+        const int gr = min(r0 + row, rmax - 1) - r0;
+        voff[i] = gr * (int)ld * 2 + c * 16;
+      } else {
+        const int lin = q * 64 + lane;
+        const int row = lin >> 5;  // k
+        const int lc = (lin & 31) ^ mn_swz(row);
+        const int gc = min(r0 + lc * 8, rmax - 8) - r0;
+        voff[i] = row * (int)ld * 2 + gc * 2;
+      }
+    }
+  }
+  // piece i of K-tile t into the operand image at LDS byte address img (wave-uniform)
+  __device__ __forceinline__ void load(int t, int i, uint32_t img, int wave) const {
+    const uint64_t b = base + (uint64_t)t * kstep;
+    i32x4 srd;
+    srd[0] = (int)(uint32_t)b;
+    srd[1] = (int)((uint32_t)(b >> 32) & 0xffff);
+    srd[2] = -1;
+    srd[3] = 0x00020000;
+    const uint32_t m0 = img + (uint32_t)(i * 4 + wave) * 1024u;
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff[i]), "s"(srd),
+                 "s"(m0)
+                 : "memory");
+  }
+};
+
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8_t frag32(const char* img, int rbase, int lane) {
+  if constexpr (KMAJ) {
+    const int row = rbase + (lane & 15);
+    const int c = (lane >> 4) ^ k32_swz(row);
+    Frag8 f;
+    f.u = *reinterpret_cast<const uint4*>(img + row * 64 + (c << 4));
+    return f.v;
+  } else {
+    return frag<256, false>(img, rbase, 0, lane);
+  }
+}
+
+// acc += a . b with the accumulator pinned to the AGPR file ("+a"): the builtin lets the register allocator
+// move accumulators between the AGPR and VGPR halves of the unified file across the unrolled K-loop (hundreds
+// of v_accvgpr moves per K-tile). Operands come straight from ds_read (the compiler's lgkmcnt covers them); the
+// accumulator is re-read by the next MFMA on it 64 MFMAs later, so no MFMA->MFMA hazard arises.
+__device__ __forceinline__ void mfma_acc(f32x4& acc, const bf16x8_t& a, const bf16x8_t& b) {
+  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+// vmcnt for "tile t+1 has landed" at the top of K-iteration t: the tiles issued after it stay in flight
+__device__ __forceinline__ void wait_tiles_after(int n_after) {
+  if (n_after >= 3) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else if (n_after == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (n_after == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Coalesced epilogue pass over 128 rows of a 256-column tile from the fp32 LDS image (kEpiRowStride floats per
+// row): each thread owns 8 consecutive columns and walks the rows NT / 32 at a time.
+template <int NT>
+__device__ __forceinline__ void epi_rows(const GemmArgs& p, const float* img, int m_base, int n0, int tid,
+                                         const float* bv) {
+  constexpr int RS = kEpiRowStride;
+  constexpr int RSTEP = NT / 32;
+  const int ec = (tid & 31) * 8, er = tid / 32;
+  const int n = n0 + ec;
+  if (n >= p.N) return;
+  const int flags = p.flags;
+#pragma unroll 2
+  for (int step = 0; step < 128 / RSTEP; ++step) {
+    const int r = step * RSTEP + er;
+    const int m = m_base + r;
+    if (m >= p.M) break;
+    float v[8];
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(img + r * RS + ec);
+    const f32x4 hi = *reinterpret_cast<const f32x4*>(img + r * RS + ec + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = lo[e] * p.alpha + bv[e];
+      v[4 + e] = hi[e] * p.alpha + bv[4 + e];
+    }
+    const int64_t off = (int64_t)m * p.ldc + n;
+    if (flags & kEpiAux) store8<bf16>(reinterpret_cast<bf16*>(p.aux + off), v);
+    if (flags & kEpiGelu) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
+    }
+    if (flags & kEpiOutF32) {
+      float* cp = reinterpret_cast<float*>(p.c) + off;
+      if (flags & kEpiAccum) {
+        float o[8];
+        load8<float>(cp, o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += o[e];
+      }
+      store8<float>(cp, v);
+    } else {
+      bf16* cp = reinterpret_cast<bf16*>(reinterpret_cast<uint16_t*>(p.c) + off);
+      if (flags & kEpiAccum) {
+        float o[8];
+        load8<bf16>(cp, o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += o[e];
+      }
+      store8<bf16>(cp, v);
+    }
+  }
+}
+
+// ABL (diagnostic ablations, timing only, wrong results): 1 = no global loads in the K-loop, 2 = no global
+// loads and no fragment reads, 3 = 2 without the per-tile barrier
+template <bool AK, bool BKM, int ABL = 0, int NSLOT = 4>
+__global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
+  constexpr int BK = 32;
+  constexpr int OPB = 256 * BK * 2;  // 16 KiB per operand image
+  constexpr int SLOT = 2 * OPB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // balanced tail as in gemm256_kernel
+  const int bid = (int)blockIdx.x;
+  int pid;
+  float* tail_out = nullptr;
+  if (p.tail_split > 0 && bid >= p.full_tiles) {
+    const int u = bid - p.full_tiles;
+    const int ks = u % p.tail_split;
+    pid = p.full_tiles + u / p.tail_split;
+    p.K /= p.tail_split;
+    p.a += (int64_t)ks * p.K * (AK ? 1 : p.lda);
+    p.b += (int64_t)ks * p.K * (BKM ? 1 : p.ldb);
+    tail_out = p.tail_ws + (int64_t)u * 65536;
+  } else {
+    pid = xcd_remap(bid, p.tail_split > 0 ? p.full_tiles : p.tiles_m * p.tiles_n);
+  }
+  int tm, tn;
+  tile_coords(pid, p.tiles_m, p.tiles_n, &tm, &tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int nk = p.K / BK;
+
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  Loader32<AK> la;
+  Loader32<BKM> lb;
+  la.init(p.a, p.lda, m0, p.M, wv, lane);
+  lb.init(p.b, p.ldb, n0, p.N, wv, lane);
+  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>(smem);
+  // piece g (0..3: A, 4..7: B) of this wave's share of K-tile t
+  auto piece = [&](int t, int g) {
+    const uint32_t slot = lds0 + (uint32_t)(t % NSLOT) * SLOT;
+    if (g < 4) la.load(t, g, slot, wv);
+    else lb.load(t, g - 4, slot + OPB, wv);
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  asm volatile("s_nop 4" ::: "memory");  // v_accvgpr_write of the zeros -> first MFMA reading them as C
+  bf16x8_t fa0[8], fb0[8], fa1[8], fb1[8];
+  const int ar = wm * 128, bc = wn * 128;
+  // K-iteration t: F(t) = (fc, gc) is in registers. Wait for tile t+1, barrier (every wave has read F(t) out of
+  // slot t % 4, and tile t+1 is visible), then 8 groups of {one LDS-DMA piece of tile t+4 into slot t % 4,
+  // two fragment reads of F(t+1), the 8 MFMAs of fragment row g}: the loads issue in the MFMA gaps.
+  auto step = [&](int t, const bf16x8_t(&fc)[8], const bf16x8_t(&gc)[8], bf16x8_t(&fn)[8], bf16x8_t(&gn)[8],
+                  auto full) {
+    constexpr bool F = decltype(full)::value;
+    if (F) wait_tiles_after(NSLOT - 2);
+    else if (t + 1 < nk) wait_tiles_after(min(t + NSLOT - 1, nk - 1) - (t + 1));
+    if (ABL < 3) bar();
+    const bool iss = (F || t + NSLOT < nk) && ABL == 0;
+    const bool rd = (F || t + 1 < nk) && ABL < 2;
+    const char* nb = smem + ((t + 1) % NSLOT) * SLOT;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      // fillers spread over the MFMA gaps (a wave alone on its SIMD issues nothing else while an MFMA holds the
+      // issue port, so fillers bunched ahead of the MFMAs would all be exposed): after MFMA 0 the LDS-DMA piece;
+      // the 16 fragment reads of F(t+1) early in the step (groups 0..5), so the next step's first MFMAs never
+      // wait on a read issued a few MFMAs before them (lgkmcnt counts in order)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        mfma_acc(acc[g][k], gc[k], fc[g]);
+        if (k == 0 && iss) piece(t + NSLOT, g);
+        const int r = 3 * g + (k - 1) / 2;  // fragment read r of F(t+1) after MFMAs 1, 3, 5 of groups 0..5
+        if ((k & 1) && k < 6 && r < 16 && rd) {
+          if (r < 8) gn[r] = frag32<BKM>(nb + OPB, bc + r * 16, lane);
+          else fn[r - 8] = frag32<AK>(nb, ar + (r - 8) * 16, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+
+  const int npro = min(NSLOT, nk);
+#pragma unroll 1
+  for (int t = 0; t < npro; ++t)
+#pragma unroll
+    for (int g = 0; g < 8; ++g) piece(t, g);
+  if (npro == 5) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");  // tile 0 landed, tiles 1.. in flight
+  else wait_tiles_after(npro - 1);
+  bar();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) fb0[j] = frag32<BKM>(smem + OPB, bc + j * 16, lane);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) fa0[i] = frag32<AK>(smem, ar + i * 16, lane);
+  int t = 0;
+#pragma unroll 1
+  for (; t + 1 + NSLOT < nk; t += 2) {  // steady state: every load is issued, constant wait counts
+    step(t, fa0, fb0, fa1, fb1, True_{});
+    step(t + 1, fa1, fb1, fa0, fb0, True_{});
+  }
+#pragma unroll 1
+  for (; t + 1 < nk; t += 2) {
+    step(t, fa0, fb0, fa1, fb1, False_{});
+    step(t + 1, fa1, fb1, fa0, fb0, False_{});
+  }
+  if (t < nk) step(t, fa0, fb0, fa1, fb1, False_{});
+  // the last MFMAs' results -> v_accvgpr_read by compiler code (hipcc pads nothing after an asm MFMA)
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 7" ::: "memory");
+
+  if (tail_out) {  // K-slice of a tail tile: raw fp32 partial, row-major 256 x 256
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = ar + i * 16 + (lane & 15);
+        const int c = bc + j * 16 + 4 * (lane >> 4);
+        const f32x4 v = acc[i][j];
+        *reinterpret_cast<float4*>(tail_out + r * 256 + c) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    return;
+  }
+
+  // epilogue through LDS, one 128-row half at a time (the two waves with wm == half write their accumulators)
+  float* img = reinterpret_cast<float*>(smem);
+  float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  {
+    const int n = n0 + (tid & 31) * 8;
+    if ((p.flags & kEpiBias) && n < p.N) load8<bf16>(reinterpret_cast<const bf16*>(p.bias + n), bv);
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    bar();
+    if (wm == h) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int r = i * 16 + (lane & 15);
+          const int c = bc + j * 16 + 4 * (lane >> 4);
+          *reinterpret_cast<f32x4*>(img + r * kEpiRowStride + c) = acc[i][j];
+        }
+    }
+    bar();
+    epi_rows<256>(p, img, m0 + h * 128, n0, tid, bv);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // 256 x 160 x 64 tiles in a 3-stage LDS ring (3 x 52 KiB = 156 KiB of the 160 KiB LDS): two K-tiles
 // of glds stay in flight while one is consumed, so the global->LDS latency is hidden by two K-tiles of
 // MFMA work instead of one (PMC on the 256x256 two-stage kernel: 36 % of wave cycles waiting on
@@ -1218,6 +1510,80 @@ PA_EXPORT int pa_gemm_bf16_pp(const void* a, const void* b, void* c, const void*
   else rc = launch256<false, true>(g, 1, st, grid);
   if (rc || !split) return rc;
   hipLaunchKernelGGL(gemm_tail_reduce_k, dim3(T - full, 64), dim3(256), 0, st, g);
+  return (int)hipGetLastError();
+}
+
+// 4-wave 256x256 GEMM (gemm4w_kernel; same operands / flags / workspace as pa_gemm_bf16_pp).
+PA_EXPORT int pa_gemm_bf16_4w(const void* a, const void* b, void* c, const void* bias, void* aux, int64_t M, int64_t N,
+                              int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor, int b_kmajor, int flags,
+                              float alpha, void* ws, hipStream_t st) {
+  if (K % kBK != 0 || N % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || ldc % 4 != 0) return 1;
+  if (!a_kmajor && M % 8 != 0) return 1;
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  GemmArgs g{};
+  g.a = (const uint16_t*)a; g.b = (const uint16_t*)b; g.c = c;
+  g.bias = (const uint16_t*)bias; g.aux = (uint16_t*)aux;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.flags = flags; g.alpha = alpha;
+  int full, split;
+  pp_plan(M, N, K, device_cus(), &full, &split);
+  if (split && !ws) split = 0;
+  g.tiles_m = (int)((M + 255) / 256);
+  g.tiles_n = (int)((N + 255) / 256);
+  const int T = g.tiles_m * g.tiles_n;
+  g.full_tiles = split ? full : T;
+  g.tail_split = split;
+  g.tail_ws = (float*)ws;
+  const int grid = split ? full + (T - full) * split : T;
+  constexpr int kLoop = 4 * 2 * 256 * 32 * 2, kEpi = 128 * kEpiRowStride * 4;
+  constexpr int smem = kLoop > kEpi ? kLoop : kEpi;
+  static bool attr_set[4] = {false, false, false, false};
+#define PA_G4(AKV, BKV, I)                                                                                      \
+  do {                                                                                                          \
+    if (!attr_set[I]) {                                                                                         \
+      (void)hipFuncSetAttribute((const void*)gemm4w_kernel<AKV, BKV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                smem);                                                                          \
+      attr_set[I] = true;                                                                                       \
+    }                                                                                                           \
+    hipLaunchKernelGGL((gemm4w_kernel<AKV, BKV>), dim3(grid), dim3(256), smem, st, g);                          \
+  } while (0)
+  if (a_kmajor && !b_kmajor) PA_G4(true, false, 0);
+  else if (a_kmajor && b_kmajor) PA_G4(true, true, 1);
+  else if (!a_kmajor && !b_kmajor) PA_G4(false, false, 2);
+  else PA_G4(false, true, 3);
+#undef PA_G4
+  int rc = (int)hipGetLastError();
+  if (rc || !split) return rc;
+  hipLaunchKernelGGL(gemm_tail_reduce_k, dim3(T - full, 64), dim3(256), 0, st, g);
+  return (int)hipGetLastError();
+}
+
+// Diagnostic ablations of gemm4w_kernel (A K-major, B MN-major, no tail): timing only.
+PA_EXPORT int pa_gemm_bf16_4w_abl(const void* a, const void* b, void* c, int64_t M, int64_t N, int64_t K, int abl,
+                                  hipStream_t st) {
+  if (K % kBK || N % 256 || M % 256) return 1;
+  GemmArgs g{};
+  g.a = (const uint16_t*)a; g.b = (const uint16_t*)b; g.c = c;
+  g.lda = K; g.ldb = N; g.ldc = N; g.M = (int)M; g.N = (int)N; g.K = (int)K; g.alpha = 1.f;
+  g.tiles_m = (int)(M / 256); g.tiles_n = (int)(N / 256);
+  g.full_tiles = g.tiles_m * g.tiles_n;
+  constexpr int smem = 128 * kEpiRowStride * 4;
+#define PA_G4A(V)                                                                                              \
+  do {                                                                                                         \
+    (void)hipFuncSetAttribute((const void*)gemm4w_kernel<true, false, V>,                                      \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);                               \
+    hipLaunchKernelGGL((gemm4w_kernel<true, false, V>), dim3(g.full_tiles), dim3(256), smem, st, g);           \
+  } while (0)
+  if (abl == 1) PA_G4A(1);
+  else if (abl == 2) PA_G4A(2);
+  else if (abl == 3) PA_G4A(3);
+  else if (abl == 4) {
+    (void)hipFuncSetAttribute((const void*)gemm4w_kernel<true, false, 0, 5>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              5 * 32768);
+    hipLaunchKernelGGL((gemm4w_kernel<true, false, 0, 5>), dim3(g.full_tiles), dim3(256), 5 * 32768, st, g);
+  } else PA_G4A(0);
+#undef PA_G4A
   return (int)hipGetLastError();
 }
 

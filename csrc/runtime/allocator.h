@@ -53,11 +53,15 @@ class BestFitAllocator {
   // `pool_id`, whose free blocks are never handed to other streams / pools, so the addresses a captured
   // graph uses stay reserved for its replays (reference: CUDA graph memory pools). end_pool stops the
   // redirection; release_pool returns the pool's blocks to ordinary use once the graph is gone.
+  // A pool may be shared by several graphs: every begin_pool takes a reference that release_pool drops, and
+  // the pool's memory returns to ordinary use only when the last graph using it is gone.
   void begin_pool(uintptr_t stream, uint64_t pool_id) {
     std::lock_guard<std::mutex> g(mu_);
     const uintptr_t pkey = kPoolBit | static_cast<uintptr_t>(pool_id);
     capture_[stream] = pkey;
-    pool_origin_[pkey] = stream;
+    if (pool_origin_.find(pkey) == pool_origin_.end()) pool_origin_[pkey] = stream;
+    ++pool_refs_[pkey];
+    released_.erase(pkey);  // a reused pool id: frees during this capture stay in the pool
   }
 
   void end_pool(uintptr_t stream) {
@@ -70,6 +74,9 @@ class BestFitAllocator {
     const uintptr_t pkey = kPoolBit | static_cast<uintptr_t>(pool_id);
     auto o = pool_origin_.find(pkey);
     if (o == pool_origin_.end()) return;
+    auto rc = pool_refs_.find(pkey);
+    if (rc != pool_refs_.end() && --rc->second > 0) return;  // another graph still replays into this pool
+    pool_refs_.erase(pkey);
     const uintptr_t dst = o->second;
     released_[pkey] = dst;
     auto pit = pools_.find(pkey);
@@ -169,7 +176,9 @@ class BestFitAllocator {
     for (auto it = chunks_.begin(); it != chunks_.end();) {
       Chunk* c = it->second;
       Block* h = c->head;
-      if (h->free && h->next == nullptr && h->size == c->size) {
+      // a free chunk of a live graph pool is not idle: the graph's replays still read and write it
+      const bool live_pool = (h->stream & kPoolBit) && pool_origin_.count(h->stream);
+      if (h->free && h->next == nullptr && h->size == c->size && !live_pool) {
         pools_[h->stream].erase(key(h));
         be_.raw_free(c->base, device_);
         freed += c->size;
@@ -324,6 +333,7 @@ class BestFitAllocator {
   std::unordered_map<uintptr_t, uintptr_t> capture_;      // capturing stream -> graph pool key
   std::unordered_map<uintptr_t, uintptr_t> pool_origin_;  // graph pool key -> its capturing stream
   std::unordered_map<uintptr_t, uintptr_t> released_;     // released pool key -> stream its blocks rejoin
+  std::unordered_map<uintptr_t, int> pool_refs_;          // graph pool key -> graphs captured into it
   Stats st_;
 };
 

@@ -413,6 +413,14 @@ class DataLoader:
         side = torch.cuda.Stream(dev)
 
         def stage(b):
+            # The staged batch is allocated on the side stream. A batch the caller has dropped went back to the
+            # allocator while compute kernels queued on the current stream may still read it; record_stream
+            # covers that for PyTorch's caching allocator, but a pluggable allocator (the native auto-growth
+            # allocator, csrc/runtime/allocator.h) never sees record_stream and returns the block to the side
+            # stream's pool at once. Ordering the side stream behind the compute stream's queued work before
+            # allocating makes reuse safe under any allocator; batch i+1's copy still overlaps batch i's compute
+            # (only work queued before this call, i.e. up to batch i-1, is waited for).
+            side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
                 out = _stage_batch(b, dev, side, _pinned)
                 ev = torch.cuda.Event()

@@ -34,6 +34,7 @@ SIGS = {
     "pa_rope_fwd": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _i32, _vp],
     # optimizer
     "pa_adamw_multi": [_vp, _vp, _i64, _vp, _f32, _f32, _f32, _f32, _f32, _f32, _f32, _vp, _vp],
+    "pa_adam_hyper_step": [_vp, _f32, _f32, _vp],
     "pa_sq_norm_multi": [_vp, _vp, _i64, _vp, _vp],
     "pa_scale_multi": [_vp, _i64, _vp, _vp],
     "pa_write_i64": [_vp, _vp, _i64, _vp],
@@ -56,7 +57,10 @@ SIGS = {
                      _i32, _i32, _vp],
     "pa_gemm_bf16_pp": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _f32,
                         _vp, _vp],
+    "pa_gemm_bf16_4w": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _f32,
+                        _vp, _vp],
     "pa_gemm_pp_ws_bytes": [_i64, _i64, _i64],
+    "pa_gemm_bf16_4w_abl": [_vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp],
     "pa_gemm_small_m": [_vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp],
     "pa_conv2d_nhwc_fwd": [_vp, _vp, _vp, _vp, _vp] + [_i32] * 13 + [_vp],
     "pa_conv2d_nhwc_wgrad": [_vp, _vp, _vp, _vp] + [_i32] * 15 + [_vp],

@@ -76,11 +76,12 @@ def gemm(a, b, bias=None, gelu=False, aux=None, out=None, accumulate=False, alph
         flags |= EPI_OUT_F32
     if bn is None:
         bn = _pick_bn(M, N, bk)
-    if bn == 1 and L.has("pa_gemm_bf16_pp"):  # ping-pong 256x256 with the balanced K-split tail
+    if bn in (1, 2) and L.has("pa_gemm_bf16_pp"):  # 256x256 (1: 8-wave ping-pong, 2: 4-wave) + balanced tail
         nb = int(L.lib().pa_gemm_pp_ws_bytes(M, N, K))
         ws = torch.empty(nb // 4, dtype=torch.float32, device=a.device) if nb else None
-        L.call("pa_gemm_bf16_pp", L.ptr(a), L.ptr(b), L.ptr(out), L.ptr(bias), L.ptr(aux), M, N, K, lda, ldb,
-               out.stride(0), int(ak), int(bk), flags, float(alpha), L.ptr(ws), L.stream_ptr())
+        L.call("pa_gemm_bf16_pp" if bn == 1 else "pa_gemm_bf16_4w", L.ptr(a), L.ptr(b), L.ptr(out), L.ptr(bias),
+               L.ptr(aux), M, N, K, lda, ldb, out.stride(0), int(ak), int(bk), flags, float(alpha), L.ptr(ws),
+               L.stream_ptr())
         return out
     L.call("pa_gemm_bf16", L.ptr(a), L.ptr(b), L.ptr(out), L.ptr(bias), L.ptr(aux), M, N, K, lda, ldb, out.stride(0),
            int(ak), int(bk), flags, float(alpha), int(bn), 1, L.stream_ptr())

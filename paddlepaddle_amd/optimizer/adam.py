@@ -11,6 +11,8 @@ import struct
 
 import torch
 
+from .lr import LRScheduler
+
 from ..ops import _loader as L
 from ..ops import optim as _opt
 from .optimizer import Optimizer
@@ -142,9 +144,31 @@ class Adam(Optimizer):
         coef = getattr(self, "_clip_coef", None)
         if coef is not None:
             inv_scale = coef if inv_scale is None else (coef * inv_scale.reshape(())).reshape(())
+        hyper = None
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            hyper = self._graph_hyper(group, fp32[0].device, lr, b1, b2, step)
+            L.call("pa_adam_hyper_step", L.ptr(hyper), float(b1), float(b2), L.stream_ptr())
         L.call("pa_adamw_multi", L.ptr(t_rows), L.ptr(t_items), n_items, L.ptr(inv_scale), float(lr), float(b1),
-               float(b2), float(eps), 0.0, float(bc1), float(bc2), L.ptr(None), L.stream_ptr())
+               float(b2), float(eps), 0.0, float(bc1), float(bc2), L.ptr(hyper), L.stream_ptr())
         self._last_step = step
+
+    def _graph_hyper(self, group, dev, lr, b1, b2, step):
+        """Device-resident {lr, beta1^t, beta2^t} of a group whose step is being captured into a hipGraph.
+        The captured step advances the beta powers on the device before the update (like the reference's
+        beta1_pow / beta2_pow accumulators), so every replay applies its own bias correction; the learning rate
+        lives in hyper[0], which the LR scheduler rewrites on each scheduler.step() (and set_lr does too)."""
+        hs = self.__dict__.setdefault("_graph_hypers", {})
+        h = hs.get(id(group))
+        if h is None:
+            h = torch.tensor([float(lr), float(b1) ** (step - 1), float(b2) ** (step - 1)], dtype=torch.float32,
+                             device=dev)
+            hs[id(group)] = h
+            base = self.get_lr()
+            ratio = float(lr) / base if base else 1.0
+            if isinstance(self._learning_rate, LRScheduler):
+                self._learning_rate._register_device_lr(h, ratio)
+            self.__dict__.setdefault("_graph_lr_sinks", []).append((h, ratio))
+        return h
 
     def state_dict(self):
         # materialise beta-pow accumulators paddle-style

@@ -17,6 +17,31 @@ class LRScheduler:
     def __call__(self):
         return self.last_lr
 
+    def _register_device_lr(self, t, ratio=1.0):
+        """A device scalar (hyper[0] of a hipGraph-captured optimizer step) that follows this schedule: every
+        step() writes last_lr * ratio into it, outside the graph, before the next replay reads it."""
+        import weakref
+        self.__dict__.setdefault("_device_lrs", []).append((weakref.ref(t), float(ratio)))
+
+    @property
+    def last_lr(self):
+        return self.__dict__.get("_last_lr")
+
+    @last_lr.setter
+    def last_lr(self, v):
+        # every schedule (including subclasses with their own step()) sets last_lr: push it to the device
+        # scalars of captured optimizer steps
+        self.__dict__["_last_lr"] = v
+        sinks = self.__dict__.get("_device_lrs")
+        if sinks:
+            live = []
+            for ref, ratio in sinks:
+                t = ref()
+                if t is not None:
+                    t[0].fill_(float(v) * ratio)
+                    live.append((ref, ratio))
+            self._device_lrs = live
+
     def step(self, epoch=None):
         if epoch is None:
             self.last_epoch += 1

@@ -75,7 +75,10 @@ class Optimizer:
     def set_lr(self, value):
         if isinstance(self._learning_rate, LRScheduler):
             raise RuntimeError("cannot set_lr when an LRScheduler is used")
+        old = float(self._learning_rate)
         self._learning_rate = float(value)
+        for h, ratio in self.__dict__.get("_graph_lr_sinks", ()):  # captured steps read lr from the device
+            h[0].fill_(float(value) * ratio if old else float(value))
 
     def set_lr_scheduler(self, scheduler):
         self._learning_rate = scheduler

@@ -132,3 +132,79 @@ def test_graph_pool_isolation_and_release():
     for t in (q, r, s):
         a.free(t)
     assert a.stats()["allocated"] == 0
+
+
+def test_graph_pool_chunks_survive_release_free_chunks():
+    """empty_cache / OOM release must not hand a live graph pool's memory back to the driver."""
+    a = _alloc(min_chunk=1 * MB)
+    a.begin_pool(5, 7)
+    p = a.allocate(4096, stream=5)     # the pool grows its own chunk during the capture
+    a.free(p)                          # graph intermediates are freed once the capture ends
+    a.end_pool(5)
+    before = a.stats()["reserved"]
+    a.release()                        # release_free_chunks: the pool chunk is free but still in use by replays
+    assert a.stats()["reserved"] == before
+    a.release_pool(7)                  # graph gone: now the chunk is idle and can go
+    a.release()
+    assert a.stats()["reserved"] == 0
+
+
+def test_graph_pool_shared_by_two_graphs_is_refcounted():
+    a = _alloc(min_chunk=1 * MB)
+    a.begin_pool(5, 3)                 # graph A captures into pool 3
+    p = a.allocate(4096, stream=5)
+    a.free(p)
+    a.end_pool(5)
+    a.begin_pool(6, 3)                 # graph B shares pool 3
+    q = a.allocate(4096, stream=6)
+    a.free(q)
+    a.end_pool(6)
+    a.release_pool(3)                  # graph A reset: B still replays into the pool
+    r = a.allocate(4096, stream=5)
+    assert r not in (p, q)
+    a.release_pool(3)                  # graph B reset: the pool's memory is ordinary again
+    a.free(r)
+    a.begin_pool(5, 3)                 # the id reused by a new capture: frees stay reserved for it
+    s = a.allocate(4096, stream=5)
+    a.free(s)
+    a.end_pool(5)
+    t = a.allocate(4096, stream=5)
+    assert t != s
+    a.free(t)
+
+
+_CHILD_LOADER = r"""
+import os, sys
+sys.path.insert(0, os.environ["REPO"])
+import numpy as np
+import torch
+import paddlepaddle_amd as paddle
+from paddlepaddle_amd.device import allocator as A
+assert A.is_enabled()
+
+class DS(paddle.io.Dataset):
+    def __len__(self):
+        return 64
+    def __getitem__(self, i):
+        return np.full([1 << 16], float(i), dtype="float32")
+
+loader = paddle.io.DataLoader(DS(), batch_size=4, shuffle=False)
+sums = []
+for b in loader:
+    torch.cuda._sleep(5_000_000)          # a slow consumer: the batch is read long after it was yielded
+    sums.append(b._t.sum())
+    del b
+got = torch.stack(sums).cpu().numpy()
+want = np.array([sum(range(4 * k, 4 * k + 4)) * (1 << 16) for k in range(16)], dtype="float64")
+assert np.allclose(got, want), (got, want)
+print("LOADER_OK")
+"""
+
+
+@pytest.mark.gpu
+def test_dataloader_slow_consumer_native_allocator_gpu():
+    """Batches staged on the DataLoader's side stream are never overwritten while the compute stream still reads
+    them, under the native allocator (which receives no record_stream calls)."""
+    env = dict(os.environ, PADDLE_AMD_ALLOCATOR="auto_growth", REPO=ROOT)
+    r = subprocess.run([sys.executable, "-c", _CHILD_LOADER], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "LOADER_OK" in r.stdout, r.stderr[-3000:]

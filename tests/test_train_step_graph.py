@@ -56,3 +56,45 @@ def test_captured_resnet_step_matches_eager():
     worst = max((a - b).abs().max().item() for a, b in zip(*runs))
     assert worst < 0.3, worst
     assert all(torch.isfinite(b).all() for b in runs[1])
+
+
+def test_captured_adamw_follows_lr_schedule_and_bias_correction():
+    """A captured AdamW step reads lr and the beta powers from device memory: replays advance the bias
+    correction in-graph and follow the LR scheduler (frozen host floats ignored the schedule)."""
+    import paddlepaddle_amd as paddle
+    from paddlepaddle_amd.device.cuda.graphs import CUDAGraph
+    paddle.set_device("gpu")
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = paddle.Tensor(torch.randn(32, 64, device="cuda", generator=g))
+    runs = []
+    for use_graph in (False, True):
+        paddle.seed(11)
+        net = paddle.nn.Sequential(paddle.nn.Linear(64, 128), paddle.nn.Tanh(), paddle.nn.Linear(128, 64))
+        sched = paddle.optimizer.lr.StepDecay(learning_rate=1e-2, step_size=1, gamma=0.5)
+        opt = paddle.optimizer.AdamW(learning_rate=sched, parameters=net.parameters(), weight_decay=0.01)
+
+        def step():
+            loss = (net(x) ** 2).mean()
+            loss.backward()
+            opt.step()
+            opt.clear_grad(set_to_zero=False)
+        for _ in range(3):
+            step()
+            sched.step()
+        torch.cuda.synchronize()
+        if use_graph:
+            cg = CUDAGraph()
+            cg.capture_begin()
+            step()
+            cg.capture_end()
+            for _ in range(3):
+                cg.replay()
+                sched.step()
+        else:
+            for _ in range(3):
+                step()
+                sched.step()
+        torch.cuda.synchronize()
+        runs.append([p._t.detach().clone() for p in net.parameters()])
+    worst = max((a - b).abs().max().item() for a, b in zip(*runs))
+    assert worst < 1e-5, worst

@@ -20,7 +20,7 @@ def timeit(fn, iters=20):
     return s.elapsed_time(e) / iters
 
 
-VARIANTS = {1: "pp-256", 4: "4w-256", 256: "2st-256"}
+VARIANTS = {1: "pp-256", 2: "4w-agpr"}
 
 
 def main():
