@@ -45,6 +45,9 @@ def parse():
     p.add_argument("--tp", type=int, default=None,
                    help="tensor-parallel degree (GPT: sharding over world/tp ranks). Default: the BASELINE config "
                         "'GPT-3 13B sharding stage-3 + TP=2' -> 2 on any multi-GPU run of GPT, 1 on one GPU")
+    p.add_argument("--sp", type=int, default=1,
+                   help="GPT with tp > 1: sequence parallel (token shards between the TP regions; all-gather / "
+                        "reduce-scatter overlapped with the GEMMs, parallel/sequence_parallel.py)")
     p.add_argument("--stage3-keep-params", default="auto",
                    help="sharding stage 3: auto | 1 (keep gathered params resident from first use until the "
                         "optimizer step) | 0 (release after each unit's forward/backward, re-gather per micro-batch)")
@@ -116,7 +119,7 @@ def gpt_bench(args, paddle, world, dist_on):
         data_rank = hcg.get_sharding_parallel_rank()
         shard_group = hcg.get_sharding_parallel_group()
     cfg = cfgs[args.model](max_position_embeddings=max(args.seq_len, 128), use_recompute=bool(args.recompute),
-                           tensor_parallel_degree=tp)
+                           tensor_parallel_degree=tp, sequence_parallel=bool(args.sp) and tp > 1)
     paddle.set_default_dtype("bfloat16")
     paddle.seed(1234)
     t0 = time.time()
@@ -352,7 +355,7 @@ def main():
     if int(os.environ.get("RANK", "0")) == 0:
         ns = world // max(args.tp, 1)
         par = (f"sharding_stage{args.sharding_stage}_degree{ns}" if args.sharding_stage else f"dp{ns}") + \
-              (f"_tp{args.tp}" if args.tp > 1 else "")
+              (f"_tp{args.tp}" if args.tp > 1 else "") + ("_sp" if (args.tp > 1 and args.sp) else "")
         if is_llama:
             par = f"pp{args.pp}_tp{args.tp}_dp{world // (args.pp * args.tp)}" + (f"_vpp{args.vpp}" if args.vpp > 1 else "")
         metric = BASELINE_METRIC if args.model == "gpt3-13b" else \

@@ -144,6 +144,51 @@ __global__ __launch_bounds__(256) void softmax_ce_bwd_k(const T* __restrict__ lo
   }
 }
 
+// ---- vocabulary-slice cross entropy (vocab-parallel CE over the mp group, vocab-chunked fused LM head):
+// the kernels see columns [v0, v0 + cols) of the full vocabulary.
+// fwd: lse_out[row] = logsumexp of the slice, tgt_out[row] = logit of the row's label when it falls in the slice
+//      (else 0); the caller combines the slices (one small collective / torch op).
+// bwd: dlogits = (exp(x - lse[row]) - [label == v0 + j]) * dloss[row] with the GLOBAL lse; a label outside the slice
+//      only drops the one-hot term, rows whose label is ignore_index get 0. May run in place (dlogits == logits).
+template <typename T>
+__global__ __launch_bounds__(256) void ce_slice_fwd_k(const T* __restrict__ logits, const int64_t* __restrict__ labels,
+                                                      float* __restrict__ lse_out, float* __restrict__ tgt_out,
+                                                      int64_t cols, int64_t v0) {
+  __shared__ float sm[4], ss[4];
+  const int64_t row = blockIdx.x;
+  const T* xr = logits + row * cols;
+  MS st = block_ms(row_stats<T>(xr, cols), sm, ss);
+  if (threadIdx.x == 0) {
+    lse_out[row] = st.m + __logf(st.s);
+    const int64_t lb = labels[row] - v0;
+    tgt_out[row] = (lb >= 0 && lb < cols) ? to_f(xr[lb]) : 0.f;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void ce_slice_bwd_k(const T* logits, const int64_t* __restrict__ labels,
+                                                      const float* __restrict__ lse, const float* __restrict__ dloss,
+                                                      T* dlogits, int64_t cols, int64_t v0, int64_t ignore_index) {
+  const int64_t row = blockIdx.x;
+  const int64_t lab = labels[row];
+  const float g = lab == ignore_index ? 0.f : dloss[row];
+  const int64_t lb = lab - v0;
+  const float l = lse[row];
+  const T* xr = logits + row * cols;
+  T* dr = dlogits + row * cols;
+  for (int64_t e = (int64_t)threadIdx.x * 8; e < cols; e += 2048) {
+    float v[8];
+    load8<T>(xr + e, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float pr = __expf(v[j] - l);
+      if (e + j == lb) pr -= 1.f;
+      v[j] = pr * g;
+    }
+    store8<T>(dr + e, v);
+  }
+}
+
 }  // namespace
 
 PA_EXPORT int pa_softmax_fwd(const void* x, void* y, int64_t rows, int64_t cols, int dtype, hipStream_t st) {
@@ -174,6 +219,26 @@ PA_EXPORT int pa_softmax_ce_bwd(const void* logits, const int64_t* labels, const
                                 hipStream_t st) {
   PA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((softmax_ce_bwd_k<T>), dim3((unsigned)rows), dim3(256), 0, st,
                                                  (const T*)logits, labels, lse, dloss, (T*)dlogits, cols,
+                                                 ignore_index));
+  PA_CHECK_LAUNCH();
+  return 0;
+}
+
+PA_EXPORT int pa_ce_slice_fwd(const void* logits, const int64_t* labels, float* lse, float* tgt, int64_t rows,
+                              int64_t cols, int64_t v0, int dtype, hipStream_t st) {
+  if (rows <= 0) return 0;
+  PA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((ce_slice_fwd_k<T>), dim3((unsigned)rows), dim3(256), 0, st,
+                                                 (const T*)logits, labels, lse, tgt, cols, v0));
+  PA_CHECK_LAUNCH();
+  return 0;
+}
+
+PA_EXPORT int pa_ce_slice_bwd(const void* logits, const int64_t* labels, const float* lse, const float* dloss,
+                              void* dlogits, int64_t rows, int64_t cols, int64_t v0, int64_t ignore_index, int dtype,
+                              hipStream_t st) {
+  if (rows <= 0) return 0;
+  PA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((ce_slice_bwd_k<T>), dim3((unsigned)rows), dim3(256), 0, st,
+                                                 (const T*)logits, labels, lse, dloss, (T*)dlogits, cols, v0,
                                                  ignore_index));
   PA_CHECK_LAUNCH();
   return 0;

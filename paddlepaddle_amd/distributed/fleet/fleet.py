@@ -387,6 +387,10 @@ class HybridParallelOptimizer:
             self._sharding = "stage1"
 
     def step(self):
+        if self._hcg is not None:
+            # sequence-parallel parameters saw only this rank's token block: one flat all-reduce per step
+            from ...parallel.sequence_parallel import allreduce_sequence_parallel_grads
+            allreduce_sequence_parallel_grads(self._inner_opt._parameter_list, self._hcg.get_model_parallel_group())
         self._inner_opt.step()
 
     def clear_grad(self, set_to_zero=True):

@@ -126,6 +126,11 @@ def mark_as_sequence_parallel_parameter(parameter):
     parameter.sequence_parallel = True
 
 
+# the overlapped sequence-parallel linears and token-block collectives (parallel/sequence_parallel.py)
+from ....parallel.sequence_parallel import (column_sp_linear, row_sp_linear, gather_tokens,  # noqa: E402,F401
+                                            reduce_scatter_tokens, allreduce_sequence_parallel_grads)
+
+
 def is_sequence_parallel_parameter(parameter):
     return getattr(parameter, "sequence_parallel", False)
 
@@ -140,6 +145,7 @@ def register_sequence_parallel_allreduce_hooks(model, accumulation_steps=1, fuse
             def hook(t, _g=g):
                 dist.all_reduce(t.grad, group=_g.process_group)
             p._t.register_post_accumulate_grad_hook(hook)
+            p._sp_hooked = True  # the optimizer-side flat all-reduce skips it
 
 
 class ColumnSequenceParallelLinear(nn.Layer):
@@ -155,8 +161,9 @@ class ColumnSequenceParallelLinear(nn.Layer):
         self.bias = self.create_parameter([out_features // n], is_bias=True) if has_bias in (None, True) else None
 
     def forward(self, x):
-        t = _AllGather.apply(x._t, self.group)
-        return _wrap(_ops.fused_linear(t, self.weight._t, None if self.bias is None else self.bias._t))
+        # all-gather of the sequence blocks overlapped with the GEMM of this rank's own block
+        return _wrap(column_sp_linear(x._t, self.weight._t, None if self.bias is None else self.bias._t,
+                                      group=self.group))
 
 
 class RowSequenceParallelLinear(nn.Layer):
@@ -174,8 +181,7 @@ class RowSequenceParallelLinear(nn.Layer):
             mark_as_sequence_parallel_parameter(self.bias)
 
     def forward(self, x):
-        y = _ops.fused_linear(x._t, self.weight._t, None)
-        y = _ReduceScatter.apply(y, self.group)
+        y = row_sp_linear(x._t, self.weight._t, group=self.group)  # GEMM pipelined with the block reduces
         if self.bias is not None:
             y = y + self.bias._t
         return _wrap(y)

@@ -9,7 +9,9 @@ MI355X-native layer (per decoder block):
   [B,S,H,D] views of the QKV buffer (HIP MFMA kernel, causal) → out-proj GEMM → dropout+residual
   → LN → FFN1 GEMM + fused bias-GELU (HIP) → FFN2 GEMM → dropout+residual.
 Tensor parallel (mp_degree>1): QKV/FFN1 column-parallel, out-proj/FFN2 row-parallel, vocab-parallel
-embedding + parallel cross-entropy (parallel/tensor_parallel.py). Activation recompute per block.
+embedding + parallel cross-entropy (parallel/tensor_parallel.py). With ``sequence_parallel`` the hidden states
+between the TP regions are token shards [B*S/mp, H]: LayerNorm / dropout / residual on the shard, all-gather /
+reduce-scatter overlapped with the GEMMs (parallel/sequence_parallel.py). Activation recompute per block.
 """
 from __future__ import annotations
 
@@ -80,9 +82,10 @@ class GPTConfig:
         return L * per_layer + V * h + P * h + 2 * h
 
     def flops_per_token(self, seq_len, recompute=False):
-        """Training FLOPs per token: 6N (fwd+bwd GEMMs) + attention scores; +2N with full recompute."""
+        """Training FLOPs per token: 6N (fwd+bwd GEMMs) + causal attention scores; +2N with full recompute."""
         n = self.num_params() - self.max_position_embeddings * self.hidden_size
-        attn = 12 * self.num_hidden_layers * self.hidden_size * seq_len  # QK^T + PV fwd+bwd (causal halves it; count dense)
+        # QK^T + PV, forward + backward = 12 L h S per token for full attention; a causal mask does half of it
+        attn = 6 * self.num_hidden_layers * self.hidden_size * seq_len
         f = 6 * n + attn
         if recompute:
             f += 2 * n + attn / 3
@@ -92,6 +95,15 @@ class GPTConfig:
 def _tp():
     from ..parallel import tensor_parallel as tp
     return tp
+
+
+def _sp():
+    from ..parallel import sequence_parallel as sp
+    return sp
+
+
+def _use_sp(cfg):
+    return cfg.sequence_parallel and cfg.tensor_parallel_degree > 1
 
 
 class GPTEmbeddings(nn.Layer):
@@ -108,12 +120,35 @@ class GPTEmbeddings(nn.Layer):
                                                 weight_attr=nn.ParamAttr(initializer=init))
         self.dropout = nn.Dropout(cfg.hidden_dropout_prob)
 
+        self.sp = _use_sp(cfg)
+        if self.sp:
+            _sp().mark_sequence_parallel(self.position_embeddings.weight)
+
     def forward(self, input_ids, position_ids=None):
+        if self.sp:
+            return self._forward_sp(input_ids, position_ids)
         if position_ids is None:
             S = input_ids.shape[-1]
             position_ids = _wrap(torch.arange(S, device=input_ids._t.device).unsqueeze(0))
         x = self.word_embeddings(input_ids)._t
         pe = self.position_embeddings(position_ids)._t
+        p = self.dropout.p if self.training else 0.0
+        return _wrap(_ops.dropout_add(x + pe, None, p, self.training))
+
+    def _forward_sp(self, input_ids, position_ids):
+        """This rank's token block [B*S/mp, H]: the vocab-parallel partial embeddings are reduce-scattered over
+        tokens (half the bytes of the all-reduce), positions are looked up for the block's own tokens."""
+        sp = _sp()
+        ids = input_ids._t
+        B, S = ids.shape[0], ids.shape[-1]
+        emb = self.word_embeddings.local_lookup(ids).reshape(B * S, -1)
+        x = sp.reduce_scatter_tokens(emb)
+        r0, r1 = sp.token_block_range(B * S)
+        if position_ids is None:
+            pos = torch.arange(r0, r1, device=ids.device) % S
+        else:
+            pos = position_ids._t.expand(B, S).reshape(-1)[r0:r1]
+        pe = torch.nn.functional.embedding(pos, self.position_embeddings.weight._t)
         p = self.dropout.p if self.training else 0.0
         return _wrap(_ops.dropout_add(x + pe, None, p, self.training))
 
@@ -139,14 +174,32 @@ class GPTAttention(nn.Layer):
             self.out_proj = nn.Linear(h, h, weight_attr=nn.ParamAttr(initializer=out_init))
             self.local_heads = self.num_heads
         self.attn_dropout = cfg.attention_probs_dropout_prob
+        self.sp = _use_sp(cfg)
+        self.bs = None  # (B, S) of the current micro-batch (sequence parallel: x is a token block)
+        if self.sp:
+            _sp().mark_sequence_parallel(self.out_proj.bias)
 
     def forward(self, x):
+        if self.sp:
+            return self._forward_sp(x)
         qkv = self.qkv_proj(x)._t  # [B, S, 3*h_local]
         B, S = qkv.shape[0], qkv.shape[1]
         qkv = qkv.view(B, S, self.local_heads, 3, self.head_dim)
         o = _ops.flash_attention_qkvpacked(qkv, causal=True, dropout=self.attn_dropout, training=self.training)
         o = o.reshape(B, S, self.local_heads * self.head_dim)
         return self.out_proj(_wrap(o))
+
+    def _forward_sp(self, x):
+        sp = _sp()
+        B, S = self.bs
+        w, b = self.qkv_proj.weight._t, self.qkv_proj.bias._t
+        t = x._t if x._t.dtype == w.dtype else x._t.to(w.dtype)
+        qkv = sp.column_sp_linear(t, w, b)  # [B*S, 3*h_local]: all-gather overlapped with the GEMM
+        qkv = qkv.view(B, S, self.local_heads, 3, self.head_dim)
+        o = _ops.flash_attention_qkvpacked(qkv, causal=True, dropout=self.attn_dropout, training=self.training)
+        o = o.reshape(B * S, self.local_heads * self.head_dim)
+        y = sp.row_sp_linear(o, self.out_proj.weight._t)  # GEMM pipelined with the reduce-scatter
+        return _wrap(y + self.out_proj.bias._t)
 
 
 class GPTMLP(nn.Layer):
@@ -165,8 +218,18 @@ class GPTMLP(nn.Layer):
         else:
             self.linear1 = nn.Linear(h, f, weight_attr=nn.ParamAttr(initializer=init))
             self.linear2 = nn.Linear(f, h, weight_attr=nn.ParamAttr(initializer=out_init))
+        self.sp = _use_sp(cfg)
+        if self.sp:
+            _sp().mark_sequence_parallel(self.linear2.bias)
 
     def forward(self, x):
+        if self.sp:
+            sp = _sp()
+            w1 = self.linear1.weight._t
+            t = x._t if x._t.dtype == w1.dtype else x._t.to(w1.dtype)
+            h = sp.column_sp_linear(t, w1, self.linear1.bias._t, act="gelu")
+            y = sp.row_sp_linear(h, self.linear2.weight._t)
+            return _wrap(y + self.linear2.bias._t)
         if self.tp > 1:
             h = self.linear1(x)
         else:
@@ -187,6 +250,8 @@ class GPTDecoderLayer(nn.Layer):
         self.mlp = GPTMLP(cfg)
         self.dropout1 = nn.Dropout(cfg.hidden_dropout_prob)
         self.dropout2 = nn.Dropout(cfg.hidden_dropout_prob)
+        if _use_sp(cfg):
+            _sp().mark_sequence_parallel(self.norm1.weight, self.norm1.bias, self.norm2.weight, self.norm2.bias)
 
     def _ln(self, norm, x):
         """(residual, LN(x)): the residual's gradient is summed into the LN input gradient by the LN backward
@@ -211,8 +276,14 @@ class GPTModel(nn.Layer):
         self.embeddings = GPTEmbeddings(cfg)
         self.layers = nn.LayerList([GPTDecoderLayer(cfg) for _ in range(cfg.num_hidden_layers)])
         self.norm = nn.LayerNorm(cfg.hidden_size, epsilon=cfg.layer_norm_eps)
+        if _use_sp(cfg):
+            _sp().mark_sequence_parallel(self.norm.weight, self.norm.bias)
 
     def forward(self, input_ids, position_ids=None):
+        if _use_sp(self.config):
+            bs = (input_ids.shape[0], input_ids.shape[-1])
+            for layer in self.layers:
+                layer.self_attn.bs = bs
         x = self.embeddings(input_ids, position_ids)
         rc = self.config.use_recompute and self.training
         if rc:
@@ -238,9 +309,14 @@ class GPTForPretraining(nn.Layer):
         ht, wt = h._t, w._t
         if ht.dtype != wt.dtype:
             ht = ht.to(wt.dtype)
+        if _use_sp(self.config):
+            # token blocks -> vocab-parallel logits of all tokens: the token all-gather overlaps the GEMM of this
+            # rank's own block, the backward's dX reduce-scatter overlaps the dW GEMM
+            B, S = input_ids.shape[0], input_ids.shape[-1]
+            return _wrap(_sp().column_sp_linear_nt(ht, wt).view(B, S, -1))
         if self.config.tensor_parallel_degree > 1:
             ht = _tp().c_identity(ht)
-        logits = torch.matmul(ht, wt.t())  # [B, S, V(_local)]
+        logits = _ops.linear_nt(ht, wt)  # [B, S, V(_local)]: hand-written GEMM or hipBLASLt per shape
         return _wrap(logits)
 
 

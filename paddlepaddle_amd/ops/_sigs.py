@@ -24,6 +24,8 @@ SIGS = {
     "pa_softmax_bwd": [_vp, _vp, _vp, _i64, _i64, _i32, _vp],
     "pa_softmax_ce_fwd": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp],
     "pa_softmax_ce_bwd": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp],
+    "pa_ce_slice_fwd": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i32, _vp],
+    "pa_ce_slice_bwd": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp],
     # activations
     "pa_gelu_fwd": [_vp, _vp, _i64, _i32, _i32, _vp],
     "pa_gelu_bwd": [_vp, _vp, _vp, _i64, _i32, _i32, _vp],

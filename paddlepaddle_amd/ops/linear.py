@@ -341,3 +341,68 @@ def fused_linear(x, w, b=None, act=None, dx_hook=None):
         h = fused_linear(x, w, b)
         return F.relu(h)
     raise ValueError(f"unsupported activation {act}")
+
+
+# ---------------------------------------------------------------------------------------------
+# y = x @ W^T with W stored [out, in] (the tied LM head: the embedding table is [vocab, hidden]).
+# forward  y  = x  . W^T : both operands K-major (the dgrad layout of an ordinary linear)
+# dgrad    dx = dy . W   : B MN-major
+# wgrad    dW = dy^T . x : both MN-major (dW comes out [out, in], W's own layout; no transposes)
+# Each product takes the per-shape choice between the hand-written GEMM and hipBLASLt (ops/gemm.py
+# choose()), so the 3 vocabulary GEMMs of a GPT step are in the same tuning table as every other GEMM.
+def _nt_fwd(x2, w):
+    wt = w.t()
+    if G.supported(x2, wt):
+        key = ("fwd_nt", x2.shape[0], w.shape[0], x2.shape[1])
+        if G.choose(key, {"blas": lambda: torch.mm(x2, wt), "hip": lambda: G.gemm(x2, wt)}) == "hip":
+            return G.gemm(x2, wt)
+    return torch.mm(x2, wt)
+
+
+def _nt_dgrad(dy2, w):
+    if G.supported(dy2, w):
+        key = ("dgrad_nt", dy2.shape[0], w.shape[1], dy2.shape[1])
+        if G.choose(key, {"blas": lambda: torch.mm(dy2, w), "hip": lambda: G.gemm(dy2, w)}) == "hip":
+            return G.gemm(dy2, w)
+    return torch.mm(dy2, w)
+
+
+def _nt_wgrad(dy2, x2):
+    dyt = dy2.t()
+    if G.supported(dyt, x2):
+        key = ("wgrad_nt", dyt.shape[0], x2.shape[1], dyt.shape[1])
+        if G.choose(key, {"blas": lambda: torch.mm(dyt, x2), "hip": lambda: G.gemm(dyt, x2)}) == "hip":
+            return G.gemm(dyt, x2)
+    return torch.mm(dyt, x2)
+
+
+class _LinearNTFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        ctx.save_for_backward(x2, w)
+        ctx.shape = shape
+        return _nt_fwd(x2, w).view(*shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if dy2.dtype != x2.dtype:
+            dy2 = dy2.to(x2.dtype)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        dx = _nt_dgrad(dy2, w).view(ctx.shape) if ctx.needs_input_grad[0] else None
+        dw = _nt_wgrad(dy2, x2) if ctx.needs_input_grad[1] else None
+        return dx, dw
+
+
+@static_op
+def linear_nt(x, w):
+    """x @ w.T for w stored [out, in] (LM head over a tied embedding table)."""
+    if _hip_linear_ok(x, w.t(), None):
+        return _LinearNTFn.apply(x, w)
+    return torch.matmul(x, w.t())

@@ -147,10 +147,13 @@ class _Unit:
         self.flats = []
         groups = {}
         for p in params:
-            key = (p._t.dtype, bool(decay_fn(p)), bool(getattr(p, "is_distributed", False)))
+            key = (p._t.dtype, bool(decay_fn(p)), bool(getattr(p, "is_distributed", False)),
+                   bool(getattr(p, "sequence_parallel", False)))
             groups.setdefault(key, []).append(p)
-        for (dt, dec, dist_), ps in groups.items():
-            self.flats.append(_Flat(ps, world, rank, dec, dist_))
+        for (dt, dec, dist_, sp), ps in groups.items():
+            f = _Flat(ps, world, rank, dec, dist_)
+            f.sequence_parallel = sp  # grads partial over the mp group (token-block inputs)
+            self.flats.append(f)
         self.n_params = len(params)
         self.ready = set()
         self.gathered = True
@@ -466,8 +469,19 @@ class GroupShardedEngine:
                     g = f.shard._t.grad
                     g.mul_(1.0 / self.dp_group.nranks)
                     dp_work.append(dist.all_reduce(g, group=self.dp_group.process_group, async_op=True))
+        sp = [f.shard._t.grad for u in self.units for f in u.flats if getattr(f, "sequence_parallel", False)]
+        if sp and self.mp_group is not None:
+            # sequence-parallel flats (LayerNorm / row-parallel bias / position table): each mp rank holds the
+            # gradient of its own token blocks; one flat all-reduce over the mp group per optimizer step
+            flat = torch.cat([g.reshape(-1).float() for g in sp])
+            dp_work.append(dist.all_reduce(flat, group=self.mp_group.process_group, async_op=True))
         for w in dp_work:
             w.wait()
+        if sp and self.mp_group is not None:
+            off = 0
+            for g in sp:
+                g.copy_(flat[off:off + g.numel()].view_as(g))
+                off += g.numel()
         if self.offload:
             self._offload_step()
         else:

@@ -240,6 +240,14 @@ class VocabParallelEmbedding(nn.Layer):
                                                 default_initializer=I.XavierNormal())
         self.weight.is_distributed = self.world > 1
 
+    def local_lookup(self, ids):
+        """This rank's partial embedding (rows of other ranks' vocab slices are 0), before the mp sum."""
+        local = ids - self.start
+        mask = (local < 0) | (local >= self.per)
+        local = local.masked_fill(mask, 0)
+        emb = torch.nn.functional.embedding(local, self.weight._t)
+        return emb.masked_fill(mask.unsqueeze(-1), 0.0)
+
     def forward(self, x):
         ids = x._t
         if self.world == 1:
@@ -253,37 +261,38 @@ class VocabParallelEmbedding(nn.Layer):
 
 
 class _ParallelCE(torch.autograd.Function):
+    """Vocab-parallel softmax cross entropy with ONE collective. Each rank reduces its vocabulary slice to
+    (logsumexp, label logit) per token (HIP slice kernel), the [N, 2] pairs are all-gathered over the mp group
+    and combined locally (lse = logsumexp over ranks, label logit = sum: only the owning rank's is non-zero).
+    The backward needs no collective: (exp(x - lse) - onehot) * g on the local slice with the global lse.
+    Reference (3 all-reduces: max, sum-exp, label logit): mp_layers.py:744 ParallelCrossEntropy,
+    c_softmax_with_cross_entropy."""
+
     @staticmethod
     def forward(ctx, logits, labels, group, ignore_index):
         # logits [N, V/mp] (any dtype), labels [N] global ids
-        lf = logits.float()
+        from ..ops.loss import ce_slice_stats
         n = _ws(group)
-        per = lf.shape[-1]
+        per = logits.shape[-1]
         start = _rank(group) * per
-        m = lf.max(-1).values
-        dist.all_reduce(m, op=dist.ReduceOp.MAX, group=group.process_group)
-        e = torch.exp(lf - m.unsqueeze(-1))
-        s = e.sum(-1)
-        dist.all_reduce(s, group=group.process_group)
-        local = labels - start
-        inr = (local >= 0) & (local < per)
-        tgt = torch.where(inr, lf.gather(-1, local.clamp(0, per - 1).unsqueeze(-1)).squeeze(-1), torch.zeros_like(m))
-        dist.all_reduce(tgt, group=group.process_group)
-        loss = torch.log(s) + m - tgt
-        ign = labels == ignore_index
-        loss = loss.masked_fill(ign, 0.0)
-        ctx.save_for_backward(e, s, local, inr, ign)
-        ctx.dtype = logits.dtype
+        lg = logits.contiguous()
+        lse_r, tgt_r = ce_slice_stats(lg, labels, start)
+        mine = torch.stack([lse_r, tgt_r], -1).contiguous()       # [N, 2]
+        allp = torch.empty((n,) + tuple(mine.shape), dtype=mine.dtype, device=mine.device)
+        dist.all_gather_into_tensor(allp.view(-1), mine.view(-1), group=group.process_group)
+        lse = torch.logsumexp(allp[..., 0], 0)
+        tgt = allp[..., 1].sum(0)
+        loss = (lse - tgt).masked_fill(labels == ignore_index, 0.0)
+        ctx.save_for_backward(lg, labels, lse)
+        ctx.start = start
+        ctx.ignore_index = ignore_index
         return loss
 
     @staticmethod
     def backward(ctx, g):
-        e, s, local, inr, ign = ctx.saved_tensors
-        p = e / s.unsqueeze(-1)
-        onehot = torch.zeros_like(p)
-        onehot.scatter_(-1, local.clamp(0, p.shape[-1] - 1).unsqueeze(-1), inr.float().unsqueeze(-1))
-        gg = g.masked_fill(ign, 0.0).unsqueeze(-1)
-        return ((p - onehot) * gg).to(ctx.dtype), None, None, None
+        from ..ops.loss import ce_slice_grad
+        lg, labels, lse = ctx.saved_tensors
+        return ce_slice_grad(lg, labels, ctx.start, lse, g, ctx.ignore_index), None, None, None
 
 
 def parallel_cross_entropy_raw(logits, labels, ignore_index=-100, group=None):

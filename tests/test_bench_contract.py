@@ -64,8 +64,26 @@ def test_bench_self_launch_sharding_x_tp_four_ranks():
     assert len(lines) == 1
     d = json.loads(lines[0])
     assert d["n_gpus"] == 4 and d["value"] > 0
-    assert d["config"]["parallelism"] == "sharding_stage3_degree2_tp2"
+    assert d["config"]["parallelism"] == "sharding_stage3_degree2_tp2_sp"
     assert d["config"]["global_batch"] == 2 * 2 * 2
+
+
+def test_bench_eight_ranks_sharding4_x_tp2_sp():
+    """The 8-GPU flagship layout on 8 gloo ranks: `bench.py --gpus 8 --tp 2` (sharding stage 3 over 4 ranks x
+    tensor parallel 2 with sequence parallelism), self-launched."""
+    env = dict(os.environ, PADDLE_AMD_FORCE_CPU="1", PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--tp", "2", "--model", "tiny",
+           "--steps", "2", "--warmup", "1", "--seq-len", "64", "--micro-batch", "2", "--accum", "2", "--resnet", "0"]
+    r = subprocess.run(cmd, env=env, capture_output=True, timeout=900, cwd="/tmp")
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    lines = [l for l in r.stdout.decode().splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["value"] > 0
+    assert d["config"]["parallelism"] == "sharding_stage3_degree4_tp2_sp"
+    assert d["config"]["global_batch"] == 2 * 2 * 4
 
 
 def test_bench_rejects_world_mismatch():

@@ -504,3 +504,98 @@ def test_segment_all_to_all_roundtrip_single_process():
     from paddlepaddle_amd.parallel.segment_parallel import head_to_seq, seq_to_head
     x = torch.randn(2, 8, 4, 16)
     assert torch.equal(head_to_seq(seq_to_head(x, None), None), x)
+
+
+# ----------------------------------------------------------------------------- sequence parallel GPT
+def _sp_gpt_worker(rank, world, port, q):
+    """GPT with tensor parallel + sequence parallel (token shards between the TP regions, overlapped
+    all-gather / reduce-scatter linears) reproduces single-process training; rank 0 records the order of
+    collectives and GEMMs of one step."""
+    paddle = _setup(rank, world, port)
+    from paddlepaddle_amd.models.gpt import GPTConfig, GPTForPretraining, GPTPretrainingCriterion
+    from paddlepaddle_amd.parallel import sequence_parallel as SP
+    _, full, _ = _gpt_full(paddle)
+    full_sd = {k: v._t.detach().clone() for k, v in full.state_dict().items()}
+    fleet = _fleet_init(paddle, mp_degree=2)
+    cfg = GPTConfig.tiny(num_hidden_layers=2, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0,
+                         tensor_parallel_degree=2, sequence_parallel=True)
+    model, crit = GPTForPretraining(cfg), GPTPretrainingCriterion(cfg)
+    with torch.no_grad():
+        for k, v in model.state_dict().items():
+            v._t.copy_(_shard_like(full_sd[k], v._t, rank, world))
+    sp_names = sorted(n for n, p in model.named_parameters() if getattr(p, "sequence_parallel", False))
+    opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    model = fleet.distributed_model(model)
+    opt = fleet.distributed_optimizer(opt)
+    ids = _data(cfg)
+    SP.TRACE = []
+    losses = _train(paddle, model, crit, opt, ids, steps=1)
+    trace = list(SP.TRACE)
+    SP.TRACE = None
+    losses += _train(paddle, model, crit, opt, ids, steps=2)
+    sd = {k: v.numpy() for k, v in model.state_dict().items()}
+    q.put((rank, losses, sd, trace if rank == 0 else None, sp_names))
+    paddle.distributed.barrier()
+
+
+def test_sequence_parallel_gpt_matches_single_process():
+    ref_losses, ref_sd = _single_gpt()
+    res = sorted(_spawn(_sp_gpt_worker), key=lambda r: r[0])
+    (_, l0, sd0, trace, sp_names), (_, l1, sd1, _, _) = res
+    np.testing.assert_allclose(l0, ref_losses, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(l1, l0, rtol=0, atol=0)
+    for k, full in ref_sd.items():
+        t = torch.from_numpy(full)
+        for r, sd in enumerate((sd0, sd1)):
+            exp = _shard_like(t, torch.from_numpy(sd[k]), r, 2).numpy()
+            np.testing.assert_allclose(sd[k], exp, rtol=2e-3, atol=2e-4, err_msg=f"rank{r}:{k}")
+    # every LayerNorm, row-parallel bias and the position table see token shards
+    assert "gpt.embeddings.position_embeddings.weight" in sp_names
+    assert "gpt.norm.weight" in sp_names and "gpt.layers.0.mlp.linear2.bias" in sp_names
+    assert not any("qkv_proj.weight" in n for n in sp_names)
+    # overlap structure: every all-gather is issued asynchronously and waited only after the GEMM of this rank's
+    # own token block; every dX reduce-scatter of a column-SP backward is waited after the dW GEMM
+    for i, ev in enumerate(trace):
+        if ev == ("issue", "all_gather"):
+            j = trace.index(("wait", "all_gather"), i)
+            between = [e for e in trace[i + 1:j] if e[0] == "gemm"]
+            assert between, f"all-gather at {i} waited with no GEMM in flight: {trace[i:j + 1]}"
+    rs_issues = [i for i, e in enumerate(trace) if e == ("issue", "reduce_scatter") and i > 0
+                 and trace[i - 1] == ("gemm", "dgrad")]
+    assert len(rs_issues) >= 4  # QKV + FFN1 of two layers
+    for i in rs_issues:
+        j = trace.index(("wait", "reduce_scatter"), i)
+        assert ("gemm", "wgrad") in trace[i + 1:j], trace[i:j + 1]
+    assert ("issue", "reduce") in trace  # row-SP forward: reduces pipelined with the next block's GEMM
+
+
+def _sp_sharding_worker(rank, world, port, q):
+    paddle = _setup(rank, world, port)
+    from paddlepaddle_amd.models.gpt import GPTConfig, GPTForPretraining, GPTPretrainingCriterion
+    _, full, _ = _gpt_full(paddle)
+    full_sd = {k: v._t.detach().clone() for k, v in full.state_dict().items()}
+    fleet = _fleet_init(paddle, mp_degree=2, sharding_degree=2, dp_degree=1)
+    fleet.fleet._strategy.sharding_configs["stage"] = 3
+    hcg = fleet.get_hybrid_communicate_group()
+    mp_rank = hcg.get_model_parallel_rank()
+    data_rank = hcg.get_sharding_parallel_rank()
+    cfg = GPTConfig.tiny(num_hidden_layers=2, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0,
+                         tensor_parallel_degree=2, sequence_parallel=True)
+    model, crit = GPTForPretraining(cfg), GPTPretrainingCriterion(cfg)
+    with torch.no_grad():
+        for k, v in model.state_dict().items():
+            v._t.copy_(_shard_like(full_sd[k], v._t, mp_rank, 2))
+    opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    model = fleet.distributed_model(model)
+    opt = fleet.distributed_optimizer(opt)
+    ids = _data(cfg)
+    per = ids.shape[0] // 2
+    losses = _train(paddle, model, crit, opt, ids[data_rank * per:(data_rank + 1) * per])
+    sd = {k: v.numpy() for k, v in model.state_dict().items()}
+    q.put((rank, mp_rank, losses, sd))
+    paddle.distributed.barrier()
+
+
+def test_sharding_stage3_x_tensor_parallel_sequence_parallel_gpt_four_ranks():
+    """sharding-2 (stage 3) x TP-2 + sequence parallel: losses and weights match single-process training."""
+    _check_hybrid(_spawn(_sp_sharding_worker, world=4), 2)
