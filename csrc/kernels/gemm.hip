@@ -837,7 +837,8 @@ __device__ __forceinline__ void epi_rows(const GemmArgs& p, const float* img, in
 }
 
 // ABL (diagnostic ablations, timing only, wrong results): 1 = no global loads in the K-loop, 2 = no global
-// loads and no fragment reads, 3 = 2 without the per-tile barrier
+// loads and no fragment reads, 3 = 2 without the per-tile barrier, 5 = loads issued but never waited for in the
+// K-loop (load latency taken out, issue cost and bandwidth kept)
 template <bool AK, bool BKM, int ABL = 0, int NSLOT = 4>
 __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
   constexpr int BK = 32;
@@ -895,9 +896,11 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
   auto step = [&](int t, const bf16x8_t(&fc)[8], const bf16x8_t(&gc)[8], bf16x8_t(&fn)[8], bf16x8_t(&gn)[8],
                   auto full) {
     constexpr bool F = decltype(full)::value;
-    if (F) wait_tiles_after(NSLOT - 2);
-    else if (t + 1 < nk) wait_tiles_after(min(t + NSLOT - 1, nk - 1) - (t + 1));
-    if (ABL < 3) bar();
+    if (ABL != 5) {
+      if (F) wait_tiles_after(NSLOT - 2);
+      else if (t + 1 < nk) wait_tiles_after(min(t + NSLOT - 1, nk - 1) - (t + 1));
+    }
+    if (ABL < 3 || ABL == 5) bar();
     const bool iss = (F || t + NSLOT < nk) && ABL == 0;
     const bool rd = (F || t + 1 < nk) && ABL < 2;
     const char* nb = smem + ((t + 1) % NSLOT) * SLOT;
@@ -1578,6 +1581,12 @@ PA_EXPORT int pa_gemm_bf16_4w_abl(const void* a, const void* b, void* c, int64_t
   if (abl == 1) PA_G4A(1);
   else if (abl == 2) PA_G4A(2);
   else if (abl == 3) PA_G4A(3);
+  else if (abl == 5) PA_G4A(5);
+  else if (abl >= 6 && abl <= 8) {  // operand footprint ablations: 6 both, 7 B, 8 A read from one L2-resident row
+    if (abl != 7) g.lda = 0;
+    if (abl != 8) g.ldb = 0;
+    PA_G4A(0);
+  }
   else if (abl == 4) {
     (void)hipFuncSetAttribute((const void*)gemm4w_kernel<true, false, 0, 5>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               5 * 32768);

@@ -92,22 +92,34 @@ def _raw(t):
     return t.numpy().tobytes()
 
 
+def combined_bytes(tensors):
+    """The save_combine byte stream of ``tensors`` (in order)."""
+    out = bytearray()
+    for t in tensors:
+        out += struct.pack("<IQ", 0, 0)
+        desc = tensor_desc(t.dtype, list(t.shape))
+        out += struct.pack("<Ii", 0, len(desc))
+        out += desc
+        out += _raw(t)
+    return bytes(out)
+
+
 def write_combined(path, tensors):
     """tensors: iterable of torch tensors, written in order."""
     with open(path, "wb") as f:
         for t in tensors:
-            f.write(struct.pack("<IQ", 0, 0))
-            desc = tensor_desc(t.dtype, list(t.shape))
-            f.write(struct.pack("<Ii", 0, len(desc)))
-            f.write(desc)
-            f.write(_raw(t))
+            f.write(combined_bytes([t]))
 
 
 def read_combined(path):
     """-> list of torch tensors in file order."""
-    out = []
     with open(path, "rb") as f:
-        data = f.read()
+        return parse_combined(f.read())
+
+
+def parse_combined(data):
+    """save_combine byte stream -> list of torch tensors."""
+    out = []
     pos = 0
     while pos < len(data):
         _ver, lod_level = struct.unpack_from("<IQ", data, pos)

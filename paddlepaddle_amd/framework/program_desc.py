@@ -653,9 +653,14 @@ class _Exporter:
             return len(self.prog._metas[a.i].shape)
         return self.prog._consts[a.idx].dim()
 
-    def tmp(self):
+    def tmp(self, like=None):
+        """A temporary; ``like``: an already declared variable whose dtype / shape it shares (the intermediate
+        of a lowered op chain, e.g. the conv output before its bias add)."""
         self.n_tmp += 1
-        return f"tmp_{self.n_tmp}"
+        name = f"tmp_{self.n_tmp}"
+        if like is not None and like in self.b.vars:
+            self.b.vars[name] = dict(self.b.vars[like], name=name)
+        return name
 
     def declare(self, slot):
         slot = getattr(slot, "i", slot)
@@ -680,10 +685,10 @@ class _Exporter:
     def op_fused_linear(self, out, a, k):
         x, w, bias, act = (a + [None, None])[:4]
         act = act or k.get("act")
-        cur = out[0] if bias is None and act is None else self.tmp()
+        cur = out[0] if bias is None and act is None else self.tmp(like=out[0])
         self.op("matmul_v2", {"X": [self.name(x)], "Y": [self.name(w)]}, {"Out": [cur]}, trans_x=False, trans_y=False)
         if bias is not None:
-            nxt = out[0] if act is None else self.tmp()
+            nxt = out[0] if act is None else self.tmp(like=out[0])
             self.op("elementwise_add", {"X": [cur], "Y": [self.name(bias)]}, {"Out": [nxt]}, axis=-1)
             cur = nxt
         if act is not None:
@@ -822,7 +827,7 @@ class _Exporter:
     def op_conv2d(self, out, a, k):
         x, w, b = a[0], a[1], (a[2] if len(a) > 2 else None)
         stride, pad, dil, groups = (list(a[3:7]) + [1, 0, 1, 1][len(a[3:7]):])
-        cur = out[0] if b is None else self.tmp()
+        cur = out[0] if b is None else self.tmp(like=out[0])
         self.op("conv2d", {"Input": [self.name(x)], "Filter": [self.name(w)]}, {"Output": [cur]},
                 strides=self._pair(stride), paddings=self._pair(pad), dilations=self._pair(dil), groups=int(groups),
                 padding_algorithm="EXPLICIT", data_format="NCHW")

@@ -170,7 +170,15 @@ class Predictor:
             else torch.device("cpu")
         self._dev = dev
         self._runner = None
-        from ..framework import program_desc as _pd
+        from ..framework import program_desc as _pd, pir_json as _pir
+        pre = config._prefix
+        if not os.path.exists(pre + ".pdmodel") and os.path.exists(pre + ".json") and _pir.is_pir_json(pre + ".json"):
+            # Paddle 3.x PIR program (.json): run op by op over this framework's kernels
+            self._runner = _pir.load(pre, dev)
+            self._in_names = list(self._runner.feed_names)
+            self._out_names = list(self._runner.fetch_names)
+            self._inputs, self._outputs, self._graphs = {}, {}, {}
+            return
         if os.path.exists(config._prefix + ".pdmodel") and _pd.is_program_desc(config._prefix + ".pdmodel"):
             # reference-format ProgramDesc: run op by op over this framework's kernels
             self._runner = _pd.load(config._prefix, dev)

@@ -10,6 +10,9 @@ from .io import (save_inference_model, load_inference_model, save, load, load_pr
                  save_to_file, load_from_file, normalize_program, save_persistables, load_persistables)
 from . import nn  # noqa: F401
 from .extras import *  # noqa: F401,F403
+from .io import (deserialize_persistables, save_vars, load_vars, get_program_persistable_vars,  # noqa: F401,E402
+                 get_program_parameter, is_persistable, is_parameter)
+from . import io, log_helper  # noqa: F401,E402
 from ..framework.tensor import Tensor as Variable  # noqa: F401
 
 ParallelExecutor = Executor

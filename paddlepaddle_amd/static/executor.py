@@ -100,13 +100,26 @@ class InputSpec:
         return cls(ndarray.shape, str(ndarray.dtype), name)
 
     def batch(self, batch_size):
-        return InputSpec((batch_size,) + self.shape, self.dtype, self.name)
+        """Insert ``batch_size`` in front of the shape, in place (reference input.py: returns self)."""
+        if isinstance(batch_size, (list, tuple)):
+            if len(batch_size) != 1:
+                raise ValueError(f"Length of batch_size: {batch_size} shall be 1, but received {len(batch_size)}.")
+            batch_size = batch_size[0]
+        elif not isinstance(batch_size, int):
+            raise TypeError(f"type(batch_size) shall be `int`, but received {type(batch_size).__name__}.")
+        self.shape = (int(batch_size),) + tuple(self.shape)
+        return self
 
     def unbatch(self):
-        return InputSpec(self.shape[1:], self.dtype, self.name)
+        """Remove the first dim of the shape, in place."""
+        if len(self.shape) == 0:
+            raise ValueError("Not support to unbatch a InputSpec when len(shape) == 0.")
+        self.shape = tuple(self.shape[1:])
+        return self
 
     def __repr__(self):
-        return f"InputSpec(shape={self.shape}, dtype={self.dtype}, name={self.name})"
+        return (f"{type(self).__name__}(shape={self.shape}, dtype={self.dtype}, name={self.name}, "
+                f"stop_gradient={self.stop_gradient})")
 
     def __eq__(self, o):
         return isinstance(o, InputSpec) and (self.shape, self.dtype, self.name) == (o.shape, o.dtype, o.name)
@@ -253,7 +266,8 @@ class Executor:
         if isinstance(prog, CompiledProgram):
             prog = prog._program
         from ..framework.program_desc import ProgramDescRunner
-        if isinstance(prog, ProgramDescRunner):  # a reference-format .pdmodel from load_inference_model
+        from ..framework.pir_json import PirRunner
+        if isinstance(prog, (ProgramDescRunner, PirRunner)):  # a reference-format model from load_inference_model
             outs = prog.run(feed or {})
             return [o.numpy() for o in outs] if return_numpy else outs
         if not prog.nodes and not prog.feeds:

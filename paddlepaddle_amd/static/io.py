@@ -24,9 +24,10 @@ from .executor import _slot_of, default_main_program
 def _const_names(prog):
     names, used = [], set()
     params = {id(p._t): p for p in prog.all_parameters()}
+    alias = prog.__dict__.get("_const_alias", {})  # names of a deserialized / loaded program's persistables
     for i, t in enumerate(prog._consts):
         p = params.get(id(t))
-        n = p.name if p is not None else f"__const_{i}"
+        n = p.name if p is not None else alias.get(i, f"__const_{i}")
         while n in used:
             n = n + "_"
         used.add(n)
@@ -61,20 +62,43 @@ def _prune(prog, fetch_slots):
     return q
 
 
-def serialize_program(feed_vars, fetch_vars, program=None, **kw):
+def _pruned(feed_vars, fetch_vars, program):
     prog = program or default_main_program()
     fetch = [_slot_of(prog, v) for v in (fetch_vars if isinstance(fetch_vars, (list, tuple)) else [fetch_vars])]
     q = _prune(prog, fetch)
     feeds = [v if isinstance(v, str) else v.name for v in (feed_vars if isinstance(feed_vars, (list, tuple))
                                                             else [feed_vars])]
     q.feeds = {k: v for k, v in prog.feeds.items() if k in feeds}
-    return json.dumps(q.to_dict(fetch, _const_names(q))).encode()
+    return q, fetch
+
+
+def _persistable_order(prog):
+    """(names, const indices) of the persistables a program uses, sorted by name (the reference's order)."""
+    names = _const_names(prog)
+    used = _used_consts(prog, prog.nodes)
+    order = sorted(used, key=lambda i: names[i])
+    return [names[i] for i in order], order
+
+
+def serialize_program(feed_vars, fetch_vars, program=None, **kw):
+    """The pruned program as bytes (this framework's program JSON; persistables travel separately through
+    serialize_persistables, as in the reference)."""
+    q, fetch = _pruned(feed_vars, fetch_vars, program)
+    d = q.to_dict(fetch, _const_names(q))
+    names, order = _persistable_order(q)
+    d["params"] = names
+    d["param_meta"] = {n: [list(q._consts[i].shape), str(q._consts[i].dtype).replace("torch.", "")]
+                       for n, i in zip(names, order)}
+    return json.dumps(d).encode()
 
 
 def serialize_persistables(feed_vars, fetch_vars, executor=None, program=None, **kw):
-    prog = program or default_main_program()
-    names = _const_names(prog)
-    return {n: _wrap(t.detach()) for n, t in zip(names, prog._consts)}
+    """The persistables the pruned program reads, as bytes in the reference save_combine layout (sorted by
+    name) — what save_to_file writes and deserialize_persistables reads back."""
+    from ..framework.combine_io import combined_bytes
+    q, _ = _pruned(feed_vars, fetch_vars, program)
+    _, order = _persistable_order(q)
+    return combined_bytes([q._consts[i].detach() for i in order])
 
 
 def save_inference_model(path_prefix, feed_vars, fetch_vars, executor=None, program=None, **kwargs):
@@ -85,12 +109,31 @@ def save_inference_model(path_prefix, feed_vars, fetch_vars, executor=None, prog
     q = _prune(prog, fetch)
     feeds = [v if isinstance(v, str) else v.name for v in feed_vars]
     q.feeds = {k: prog.feeds[k] for k in feeds}
-    if kwargs.get("program_format", "json") == "protobuf":
+    fmt = kwargs.get("program_format", "json")
+    if fmt == "protobuf":
         # the reference's ProgramDesc .pdmodel + save_combine .pdiparams (framework/program_desc.py)
         from ..framework import program_desc as _pd
         _pd.export(q, fetch, feeds, _const_names(q)).save(path_prefix)
         return
-    write_program(path_prefix, q, fetch)
+    if fmt == "pir":  # the reference's Paddle 3.x format only: <prefix>.json (PIR) + .pdiparams
+        _pir_writer(q, fetch, feeds, kwargs).save(path_prefix)
+        return
+    # default: this framework's program (<prefix>.pdmodel, every recorded op, hipGraph replay in the Predictor)
+    # plus, when every op lowers to reference operations, the PIR <prefix>.json over the same .pdiparams — the
+    # file Paddle 3.x's load_inference_model / paddle.inference read
+    order = write_program(path_prefix, q, fetch)
+    try:
+        w = _pir_writer(q, fetch, feeds, kwargs)
+    except NotImplementedError:
+        return
+    if sorted(w.params) == order:
+        with open(path_prefix + ".json", "w") as f:
+            json.dump(w.to_json(), f)
+
+
+def _pir_writer(q, fetch, feeds, kwargs):
+    from ..framework import program_desc as _pd, pir_json as _pir
+    return _pir.from_builder(_pd.export(q, fetch, feeds, _const_names(q)), trainable=kwargs.get("trainable", False))
 
 
 def write_program(path_prefix, prog, fetch_slots):
@@ -107,6 +150,7 @@ def write_program(path_prefix, prog, fetch_slots):
     # parameters in the reference save_combine layout (framework/combine_io.py)
     from ..framework.combine_io import write_combined
     write_combined(path_prefix + ".pdiparams", [prog._consts[i].detach() for i in order])
+    return [names[i] for i in order]
 
 
 def read_program(path_prefix, device=None, params_file=None):
@@ -137,11 +181,19 @@ def load_inference_model(path_prefix, executor=None, **kwargs):
     if executor is not None and executor.place is not None:
         from ..framework.place import to_torch_device
         dev = to_torch_device(executor.place)
-    from ..framework import program_desc as _pd
-    base = path_prefix[:-len(".pdmodel")] if path_prefix.endswith(".pdmodel") else path_prefix
+    from ..framework import program_desc as _pd, pir_json as _pir
+    base = path_prefix
+    for ext in (".pdmodel", ".json"):
+        if base.endswith(ext):
+            base = base[:-len(ext)]
+    own = os.path.exists(base + ".pdmodel") and not _pd.is_program_desc(base + ".pdmodel")
+    if not own and os.path.exists(base + ".json") and _pir.is_pir_json(base + ".json"):
+        runner = _pir.load(base, dev)  # a Paddle 3.x PIR program: run op by op over this framework's ops
+        return [runner, list(runner.feed_names), list(runner.fetch_names)]
     if os.path.exists(base + ".pdmodel") and _pd.is_program_desc(base + ".pdmodel"):
         runner = _pd.load(base, dev)
         return [runner, list(runner.program.feed_names), list(runner.program.fetch_names)]
+    path_prefix = base
     prog, fetch, _ = read_program(path_prefix, dev)
     feed_names = list(prog.feeds)
     fetch_vars = [P._Var(prog, s, f"fetch_{i}") for i, s in enumerate(fetch)]
@@ -191,9 +243,99 @@ def load_from_file(path):
 
 
 def deserialize_program(data):
+    """A Program from serialize_program bytes. Its persistables are zero-filled placeholders of the recorded
+    shape / dtype until deserialize_persistables (or load_vars / set_program_state) fills them."""
     d = json.loads(data.decode() if isinstance(data, (bytes, bytearray)) else data)
-    prog, _ = P.Program.from_dict(d, {})
+    consts = {n: torch.zeros(shape, dtype=getattr(torch, dt)) for n, (shape, dt) in d.get("param_meta", {}).items()}
+    prog, fetch = P.Program.from_dict(d, consts)
+    prog._serialized_params = list(d.get("params", []))
+    prog._serialized_fetch = fetch
     return prog
+
+
+def deserialize_persistables(program, data, executor=None):
+    """Fill ``program``'s persistables from serialize_persistables bytes (save_combine layout, sorted names)."""
+    from ..framework.combine_io import parse_combined
+    tensors = parse_combined(bytes(data))
+    names = getattr(program, "_serialized_params", None)
+    if names is None:
+        names, _ = _persistable_order(program)
+    if len(names) != len(tensors):
+        raise ValueError(f"{len(tensors)} serialized tensors for {len(names)} persistables of the program")
+    by_name = dict(zip(names, tensors))
+    cn = _const_names(program)
+    with torch.no_grad():
+        for i, n in enumerate(cn):
+            if n in by_name:
+                program._consts[i].copy_(by_name[n].to(program._consts[i].dtype))
+    return program
+
+
+def get_program_persistable_vars(program):
+    """The persistable variables (parameters and captured persistable tensors) of ``program``."""
+    return list(program.all_parameters())
+
+
+def get_program_parameter(program):
+    return list(program.all_parameters())
+
+
+def is_persistable(var):
+    return bool(getattr(var, "persistable", False)) or isinstance(var, Parameter)
+
+
+def is_parameter(var):
+    return isinstance(var, Parameter)
+
+
+def _select_vars(main_program, vars, predicate):
+    if vars is not None:
+        return list(vars)
+    prog = main_program or default_main_program()
+    pool = list(prog.all_parameters())
+    return [v for v in pool if predicate is None or predicate(v)]
+
+
+def save_vars(executor=None, dirname=None, main_program=None, vars=None, predicate=None, filename=None):
+    """Save variables: one file per variable named after it in ``dirname``, or all of them in ``filename`` (the
+    reference save_combine layout, in the given order); with neither ``dirname`` nor ``filename`` the combined
+    bytes are returned. Reference: static/io.py:1049 save_vars."""
+    from ..framework.combine_io import combined_bytes
+    vs = _select_vars(main_program, vars, predicate)
+    ts = [v._t.detach() if isinstance(v, Tensor) else torch.as_tensor(np.asarray(v)) for v in vs]
+    if dirname is None and filename is None:
+        return combined_bytes(ts)
+    if dirname:
+        os.makedirs(dirname, exist_ok=True)
+    if filename is not None:
+        with open(os.path.join(dirname or "", filename), "wb") as f:
+            f.write(combined_bytes(ts))
+        return None
+    for v, t in zip(vs, ts):
+        with open(os.path.join(dirname, v.name), "wb") as f:
+            f.write(combined_bytes([t]))
+    return None
+
+
+def load_vars(executor=None, dirname=None, main_program=None, vars=None, predicate=None, filename=None):
+    """Inverse of save_vars: fill the variables in place (shapes must match). Reference: static/io.py:1236."""
+    from ..framework.combine_io import parse_combined
+    vs = _select_vars(main_program, vars, predicate)
+    if filename is not None:
+        with open(os.path.join(dirname or "", filename), "rb") as f:
+            ts = parse_combined(f.read())
+        if len(ts) != len(vs):
+            raise ValueError(f"{filename} holds {len(ts)} tensors, {len(vs)} variables requested")
+    else:
+        ts = []
+        for v in vs:
+            with open(os.path.join(dirname, v.name), "rb") as f:
+                ts.append(parse_combined(f.read())[0])
+    with torch.no_grad():
+        for v, t in zip(vs, ts):
+            if tuple(t.shape) != tuple(v._t.shape):
+                raise ValueError(f"variable {v.name}: file shape {tuple(t.shape)} != {tuple(v._t.shape)}")
+            v._t.copy_(t.to(v._t.dtype))
 
 
 def normalize_program(program, feed_vars, fetch_vars, **kw):

@@ -22,7 +22,9 @@ def fc(x, size, num_flatten_dims=1, weight_attr=None, bias_attr=None, activation
     for i, xi in enumerate(xs):
         in_f = int(np.prod(xi.shape[num_flatten_dims:]))
         lin = _nn.Linear(in_f, size, weight_attr=weight_attr, bias_attr=bias_attr if i == 0 else False)
-        h = xi.reshape(list(xi.shape[:num_flatten_dims]) + [in_f]) if xi.ndim != num_flatten_dims + 1 else xi
+        # leading dims from the data (shape-generic: a None batch dim stays dynamic), the rest flattened
+        lead = list(xi.shape[1:num_flatten_dims])
+        h = xi.reshape([-1] + lead + [in_f]) if xi.ndim != num_flatten_dims + 1 else xi
         y = lin(h)
         out = y if out is None else out + y
     return _act(out, activation)

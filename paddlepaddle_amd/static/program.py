@@ -884,7 +884,9 @@ class _Decoder:
         if "r" in x:
             return _Ref(x["r"])
         if "c" in x:
-            return self.prog._const(self.consts[x["c"]])
+            c = self.prog._const(self.consts[x["c"]])
+            self.prog.__dict__.setdefault("_const_alias", {})[c.idx] = x["c"]  # keep the saved name
+            return c
         if "dev" in x:
             return _RUN_DEV
         if "sym" in x:

@@ -1,0 +1,113 @@
+"""PIR program JSON (Paddle 3.x model format): a static program saved by save_inference_model is written in the
+reference schema (paddle/fluid/pir/serialize_deserialize: base_code / regions / blocks / ops, compressed dialect
+ids, "p" parameter ops, t_dtensor types, a_* attributes, mutable attributes as full / full_int_array operands)
+and loads back through the PIR runner with the same outputs. Parity with the reference's own reader is unpinned:
+no reference-exported .json model ships in the reference tree; the schema checks below follow schema.h /
+ir_serialize.cc / serialize_utils.h key for key."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import paddlepaddle_amd as paddle
+from paddlepaddle_amd.framework import pir_json as pir
+
+from test_program_desc import _static_models
+
+
+def _save(tmp_path, fmt="json"):
+    rng = np.random.RandomState(5)
+    xs = {"x": rng.randn(3, 8).astype("float32"), "im": rng.randn(2, 3, 8, 8).astype("float32")}
+    paddle.enable_static()
+    try:
+        main, startup = paddle.static.Program(), paddle.static.Program()
+        with paddle.static.program_guard(main, startup):
+            feeds, fetches = _static_models()
+        exe = paddle.static.Executor(paddle.CPUPlace())
+        exe.run(startup)
+        ref = exe.run(main, feed=xs, fetch_list=list(fetches))
+        prefix = str(tmp_path / "m")
+        paddle.static.save_inference_model(prefix, list(feeds), list(fetches), exe, program=main,
+                                           program_format=fmt)
+    finally:
+        paddle.disable_static()
+    return prefix, xs, ref
+
+
+def test_default_save_writes_reference_pir_json(tmp_path):
+    prefix, xs, ref = _save(tmp_path)
+    assert os.path.exists(prefix + ".pdmodel") and os.path.exists(prefix + ".json")
+    with open(prefix + ".json") as f:
+        d = json.load(f)
+    assert d["base_code"] == {"magic": "pir", "version": 1, "trainable": False}
+    region = d["program"]["regions"][0]
+    assert region["#"] == "region_0" and region["blocks"][0]["#"] == "block_0"
+    ops = region["blocks"][0]["ops"]
+    names = [o["#"] for o in ops]
+    # dialect-compressed op names, parameter ops, feeds first, fetches last
+    assert "p" in names and "1.data" in names and names[-1] == "1.fetch"
+    assert {"1.matmul", "1.layer_norm", "1.gelu", "1.conv2d", "1.batch_norm_", "1.pool2d", "1.reshape",
+            "1.transpose", "1.concat", "1.softmax", "1.scale", "1.flatten", "1.full_int_array", "0.combine"} <= set(names)
+    # value ids: results count up from 1 and every operand refers to an earlier result
+    seen = set()
+    for o in ops:
+        for i in o.get("I", []):
+            assert i["%"] in seen
+        outs = [o["O"]] if isinstance(o["O"], dict) else o["O"]
+        for r in outs:
+            assert r["%"] not in seen and r["%"] >= 1
+            seen.add(r["%"])
+            assert r["TT"]["#"] in ("0.t_dtensor", "0.t_vec")
+    p = next(o for o in ops if o["#"] == "p")
+    assert len(p["A"]) == 4 and isinstance(p["A"][3], str)
+    data = next(o for o in ops if o["#"] == "1.data")
+    attrs = {a["N"]: a["AT"] for a in data["A"]}
+    assert attrs["name"] == {"#": "0.a_str", "D": "x"} and attrs["dtype"] == {"#": "1.a_dtype", "D": "float32"}
+    assert attrs["shape"]["#"] == "1.a_intarray" and attrs["place"]["#"] == "1.a_place"
+    # mutable attributes are operands: reshape (x, shape), pool2d (x, kernel_size), concat (combine, axis)
+    for op, n in (("1.reshape", 2), ("1.pool2d", 2), ("1.concat", 2), ("1.scale", 2)):
+        assert all(len(o["I"]) == n for o in ops if o["#"] == op), op
+    mm = next(o for o in ops if o["#"] == "1.matmul")
+    assert {a["N"] for a in mm["A"]} == {"transpose_x", "transpose_y"}
+
+
+def test_pir_json_round_trip_runs(tmp_path):
+    prefix, xs, ref = _save(tmp_path, fmt="pir")
+    assert not os.path.exists(prefix + ".pdmodel") and pir.is_pir_json(prefix + ".json")
+    paddle.enable_static()
+    try:
+        exe = paddle.static.Executor(paddle.CPUPlace())
+        prog, feed_names, fetch_names = paddle.static.load_inference_model(prefix, exe)
+        assert isinstance(prog, pir.PirRunner) and feed_names == ["x", "im"]
+        got = exe.run(prog, feed=xs, fetch_list=fetch_names)
+    finally:
+        paddle.disable_static()
+    for a, b in zip(ref, got):
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-5)
+
+
+def test_predictor_reads_pir_json(tmp_path):
+    prefix, xs, ref = _save(tmp_path, fmt="pir")
+    from paddlepaddle_amd import inference
+    cfg = inference.Config(prefix + ".json", prefix + ".pdiparams")
+    pred = inference.create_predictor(cfg)
+    for n in pred.get_input_names():
+        pred.get_input_handle(n).copy_from_cpu(xs[n])
+    pred.run()
+    outs = [pred.get_output_handle(n).copy_to_cpu() for n in pred.get_output_names()]
+    for a, b in zip(ref, outs):
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-5)
+
+
+def test_attribute_and_type_codec():
+    assert pir.a_f32(float("nan")) == {"#": "0.a_f32", "VD": "NaN"}
+    assert pir.a_f64(float("-inf")) == {"#": "0.a_f64", "VD": "-INF"}
+    for a in (pir.a_bool(True), pir.a_i32(3), pir.a_i64(1 << 40), pir.a_str("s"), pir.a_intarray([1, -1]),
+              pir.a_array([pir.a_i32(1), pir.a_i32(2)]), pir.a_dtype("bfloat16")):
+        pir.decode_attr(a)
+    assert pir.decode_attr(pir.a_array([pir.a_i32(1), pir.a_i32(2)])) == [1, 2]
+    assert pir.decode_attr({"#": "1.a_scalar", "D": ["float32", 2.5]}) == 2.5
+    assert pir.decode_type(pir.dtensor("bfloat16", [2, -1])) == ("bfloat16", [2, -1])
+    with pytest.raises(ValueError):
+        pir.PirProgram({"program": {}})
