@@ -10,4 +10,12 @@ from ..framework.place import CPUPlace, CUDAPlace, CUDAPinnedPlace  # noqa: F401
 from ..framework import in_dynamic_mode as in_dygraph_mode  # noqa: F401
 from ..framework.tensor import Tensor as Variable  # noqa: F401
 from ..framework.flags import set_flags, get_flags  # noqa: F401,E402
-from . import core, framework, dygraph  # noqa: F401,E402
+from . import core, framework, dygraph, io  # noqa: F401,E402
+
+
+def enable_dygraph(place=None):
+    _static.disable_static(place)
+
+
+def disable_dygraph():
+    _static.enable_static()

@@ -21,6 +21,11 @@ _FLAGS = {
     "FLAGS_eager_backward_engine": "torch",  # torch | native (csrc/runtime/autograd_engine.cpp RunBackward)
     "FLAGS_gemm_backend": "auto",         # per-shape GEMM / conv backend: auto (timed) | hip | blas
     "FLAGS_sharding_stage3_keep_params": "auto",  # stage 3: keep gathered params until the optimizer step
+    "FLAGS_use_autotune": True,           # time GEMM backends for shapes the tuning table does not hold
+    "FLAGS_autotune_range_begin": 0,      # incubate.autotune kernel tuning_range (optimizer-step window)
+    "FLAGS_autotune_range_end": 1 << 30,
+    "FLAGS_layout_autotune": False,
+    "FLAGS_dataloader_autotune": False,
     "FLAGS_linear_wt_cache_mb": 0,        # [out,in] weight copies for TN-form forward GEMMs (0 = off;
                                           # measured no net gain on the 13B step, see ops/linear.py)
 }

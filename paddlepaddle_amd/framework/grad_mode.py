@@ -55,14 +55,41 @@ class enable_grad(_GradMode):
     _mode = True
 
 
-class set_grad_enabled(_GradMode):
+class set_grad_enabled:
+    """Sets the mode on construction, so both ``paddle.set_grad_enabled(False)`` (a plain call) and
+    ``with paddle.set_grad_enabled(False):`` (restores the previous mode on exit) work."""
+
     def __init__(self, mode):
-        super().__init__()
+        self._prev = torch.is_grad_enabled()
         self._mode = bool(mode)
+        torch.set_grad_enabled(self._mode)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        torch.set_grad_enabled(self._prev)
+        return False
+
+    def __call__(self, func):
+        torch.set_grad_enabled(self._prev)  # as a decorator the mode applies only inside func
+        mode = self._mode
+
+        @functools.wraps(func)
+        def wrapper(*a, **k):
+            prev = torch.is_grad_enabled()
+            torch.set_grad_enabled(mode)
+            try:
+                return func(*a, **k)
+            finally:
+                torch.set_grad_enabled(prev)
+        return wrapper
 
 
 def is_grad_enabled():
-    return torch.is_grad_enabled()
+    """False in static-graph mode (gradients come from append_backward there), else the dygraph mode."""
+    from ..static.executor import _static_mode
+    return False if _static_mode.enabled else torch.is_grad_enabled()
 
 
 no_grad_ = no_grad

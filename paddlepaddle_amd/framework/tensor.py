@@ -419,6 +419,11 @@ class Tensor:
             return
         self._t.backward(g, retain_graph=retain_graph)
 
+    def gradient(self):
+        """The accumulated gradient as a numpy array (None before backward) — legacy dygraph API."""
+        g = self._t.grad
+        return None if g is None else g.detach().cpu().numpy()
+
     def clear_grad(self, set_to_zero=True):
         g = self._t.grad
         if g is None:

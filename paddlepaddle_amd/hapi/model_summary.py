@@ -35,42 +35,108 @@ def _shape_of(o):
     return []
 
 
+def _layer_key(layer, n_rows):
+    """`<Class>-<k>`: k is the per-class instance counter of the layer's full name plus one, so the
+    n-th Conv2D built in the process is Conv2D-n (reference model_summary.py numbering)."""
+    try:
+        idx = int(layer.full_name().split("_")[-1])
+    except ValueError:
+        idx = n_rows
+    return f"{type(layer).__name__}-{idx + 1}"
+
+
+def _input_mb(sizes):
+    if isinstance(sizes, (list, tuple)) and all(isinstance(v, (int, np.integer)) for v in sizes):
+        return abs(float(np.prod(sizes)) * 4.0 / 1024 ** 2)
+    return sum(_input_mb(v) for v in sizes)
+
+
+def _summary_table(rows, input_sizes):
+    """The reference's text table: centred columns at least 15/20/20/15 wide (grown to fit), a rule
+    at least 75 wide, then parameter totals and a float32 memory estimate."""
+    w = {"layer": 15, "in": 20, "out": 20, "params": 15}
+    for key, r in rows.items():
+        w["layer"] = max(w["layer"], len(key))
+        w["in"] = max(w["in"], len(str(r["input_shape"])))
+        w["out"] = max(w["out"], len(str(r["output_shape"])))
+        w["params"] = max(w["params"], len(str(r["nb_params"])))
+    width = max(75, sum(w.values()) + 5)
+
+    def line(a, b, c, d):
+        return f"{a:^{w['layer']}} {b:^{w['in']}} {c:^{w['out']}} {d:^{w['params']}}"
+
+    out = ["-" * width, line("Layer (type)", "Input Shape", "Output Shape", "Param #"), "=" * width]
+    total = trainable = 0
+    n_out = 0.0
+    for key, r in rows.items():
+        out.append(line(key, str(r["input_shape"]), str(r["output_shape"]), f"{r['nb_params']:,}"))
+        total += r["nb_params"]
+        trainable += r["trainable_params"]
+        shp = r["output_shape"]
+        if shp and isinstance(shp[0], list):
+            n_out += sum(float(np.prod(o)) for o in shp if o and not isinstance(o[0], list))
+        elif shp:
+            n_out += float(np.prod(shp))
+    in_mb = _input_mb(input_sizes)
+    act_mb = abs(2.0 * n_out * 4.0 / 1024 ** 2)  # x2: activations and their gradients
+    par_mb = abs(total * 4.0 / 1024 ** 2)
+    out += ["=" * width, f"Total params: {total:,}", f"Trainable params: {trainable:,}",
+            f"Non-trainable params: {total - trainable:,}", "-" * width,
+            f"Input size (MB): {in_mb:0.2f}", f"Forward/backward pass size (MB): {act_mb:0.2f}",
+            f"Params size (MB): {par_mb:0.2f}", f"Estimated Total Size (MB): {par_mb + act_mb + in_mb:0.2f}",
+            "-" * width]
+    return "\n".join(out) + "\n", total, trainable
+
+
 def summary(net, input_size=None, dtypes=None, input=None):
-    rows = []
+    """Per-layer input/output shapes and parameter counts from one forward pass (reference
+    hapi/model_summary.py:summary). Every sublayer except Sequential / LayerList containers is
+    hooked; each row counts the layer's own parameters."""
+    from .. import nn
+    if input_size is None and input is None:
+        raise ValueError("summary needs input_size or input")
+    rows = {}
     hooks = []
 
-    def make_hook(name, layer):
-        def hook(l, inp, out):
-            n_params = sum(int(np.prod(p.shape)) for p in l.parameters(include_sublayers=False))
-            trainable = sum(int(np.prod(p.shape)) for p in l.parameters(include_sublayers=False)
-                            if not p.stop_gradient)
-            rows.append((f"{type(l).__name__}-{len(rows) + 1}", _shape_of(inp[0]) if inp else [], _shape_of(out),
-                         n_params, trainable))
-        return hook
+    def hook(l, inp, out):
+        own = [p for p in l._parameters.values() if p is not None]
+        rows[_layer_key(l, len(rows))] = {
+            "input_shape": _shape_of(list(inp)),
+            "output_shape": _shape_of(out),
+            "nb_params": sum(int(np.prod(p.shape)) for p in own),
+            "trainable_params": sum(int(np.prod(p.shape)) for p in own
+                                    if not p.stop_gradient and getattr(p, "trainable", True)),
+        }
 
-    for name, layer in net.named_sublayers():
-        if _is_leaf(layer):
-            hooks.append(layer.register_forward_post_hook(make_hook(name, layer)))
+    subs = net.sublayers()
+    for layer in net.sublayers(include_self=True):
+        if isinstance(layer, (nn.Sequential, nn.LayerList)) or (layer is net and subs):
+            continue
+        hooks.append(layer.register_forward_post_hook(hook))
+    if isinstance(input_size, tuple):
+        input_size = [input_size]
+    if input is not None:
+        flat = list(input.values()) if isinstance(input, dict) else \
+            (list(input) if isinstance(input, (list, tuple)) else [input])
+        sizes = [list(t.shape) for t in flat if isinstance(t, Tensor)]
+    else:
+        inputs, sizes = _make_inputs(input_size, dtypes, None), input_size
     was_training = net.training
     net.eval()
     from ..framework.grad_mode import no_grad
     try:
         with no_grad():
-            net(*_make_inputs(input_size, dtypes, input))
+            if input is not None:
+                net(input)  # passed through as the single forward argument, as the reference does
+            else:
+                net(*inputs)
     finally:
         for h in hooks:
             h.remove()
         if was_training:
             net.train()
-    total = sum(int(np.prod(p.shape)) for p in net.parameters())
-    trainable = sum(int(np.prod(p.shape)) for p in net.parameters() if not p.stop_gradient)
-    w = 100
-    lines = ["-" * w, f"{'Layer (type)':<28}{'Input Shape':<26}{'Output Shape':<26}{'Param #':>14}", "=" * w]
-    for name, i, o, n, _ in rows:
-        lines.append(f"{name:<28}{str(i):<26}{str(o):<26}{n:>14,}")
-    lines += ["=" * w, f"Total params: {total:,}", f"Trainable params: {trainable:,}",
-              f"Non-trainable params: {total - trainable:,}", "-" * w]
-    print("\n".join(lines))
+    text, total, trainable = _summary_table(rows, sizes)
+    print(text)
     return {"total_params": total, "trainable_params": trainable}
 
 

@@ -8,7 +8,7 @@ import torch
 from ..framework.tensor import Tensor, _wrap
 from . import nn  # noqa: F401
 from .optimizer import LookAhead, ModelAverage  # noqa: F401
-from . import optimizer, asp, autograd  # noqa: F401
+from . import optimizer, asp, autograd, autotune  # noqa: F401
 from ..geometric import (segment_sum, segment_mean, segment_max, segment_min,  # noqa: F401
                          sample_neighbors as graph_sample_neighbors, reindex_graph as graph_reindex)
 from ..geometric import send_u_recv as _send_u_recv

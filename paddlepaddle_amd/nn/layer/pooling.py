@@ -11,7 +11,12 @@ class _Pool(Layer):
         self._kw = kw
 
     def extra_repr(self):
-        return ", ".join(f"{k}={v}" for k, v in self._kw.items())
+        kw = self._kw
+        if "kernel_size" not in kw:  # adaptive pools
+            keys = ["output_size"] + (["return_mask"] if "return_mask" in kw else [])
+            return ", ".join(f"{k}={kw[k]}" for k in keys)
+        head = f"norm_type={kw['norm_type']}, " if "norm_type" in kw else ""
+        return head + f"kernel_size={kw['kernel_size']}, stride={kw.get('stride')}, padding={kw.get('padding', 0)}"
 
 
 class MaxPool1D(_Pool):

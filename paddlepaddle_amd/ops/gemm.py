@@ -277,6 +277,8 @@ def choose(key, candidates, cold=False):
         return ch
     if _capturing():
         return "blas"
+    if not L.flag("FLAGS_use_autotune", True):  # incubate.autotune kernel tuning off: no timing, vendor GEMM
+        return "blas" if "blas" in candidates else next(iter(candidates))
     times = {n: [] for n in candidates}
     for fn in candidates.values():
         fn()

@@ -11,6 +11,7 @@ straight-through estimator so QAT trains through the rounding."""
 from __future__ import annotations
 
 import copy
+import inspect
 
 import torch
 
@@ -81,23 +82,34 @@ class BaseQuanter(BaseObserver):
 
 
 class _Factory:
-    """quanter/observer factory: holds the class + kwargs, instantiated per layer."""
+    """quanter/observer factory: holds the layer class + its arguments, instantiated per layer
+    (reference factory.py QuanterFactory / ObserverFactory). Printing lists every argument with the
+    defaults filled in, `name` first, as the reference's factories do."""
 
-    def __init__(self, cls, **kwargs):
-        self.cls, self.kwargs = cls, kwargs
+    def __init__(self, cls, display, args=(), kwargs=None):
+        self.cls, self._display = cls, display
+        sig = [p for p in inspect.signature(cls.__init__).parameters.values() if p.name != "self"]
+        bound = {p.name: p.default for p in sig if p.default is not inspect.Parameter.empty}
+        for p, v in zip(sig, args):
+            bound[p.name] = v
+        bound.update(kwargs or {})
+        order = (["name"] if "name" in bound else []) + [p.name for p in sig if p.name != "name"]
+        self.kwargs = {k: bound[k] for k in order if k in bound}
 
     def _instance(self, layer=None):
         return self.cls(**self.kwargs)
 
-    def __repr__(self):
-        return f"{self.cls.__name__}Factory({self.kwargs})"
+    def __str__(self):
+        return f"{self._display}(" + ",".join(f"{k}={v}" for k, v in self.kwargs.items()) + ")"
+
+    __repr__ = __str__
 
 
 def quanter(class_name):
     """Decorator registering a quanter class; the decorated name becomes a factory."""
     def deco(cls):
-        def factory(**kwargs):
-            return _Factory(cls, **kwargs)
+        def factory(*args, **kwargs):
+            return _Factory(cls, class_name, args, kwargs)
         factory._cls = cls
         factory.__name__ = class_name
         return factory
@@ -105,7 +117,7 @@ def quanter(class_name):
 
 
 # ------------------------------------------------------------------------------ observers / quanters
-class _AbsmaxObserverImpl(BaseObserver):
+class AbsmaxObserverLayer(BaseObserver):
     def __init__(self, quant_bits=8):
         super().__init__()
         self._bits = quant_bits
@@ -119,7 +131,7 @@ class _AbsmaxObserverImpl(BaseObserver):
         return self._absmax
 
 
-class _GroupWiseObserverImpl(BaseObserver):
+class GroupWiseWeightObserverLayer(BaseObserver):
     def __init__(self, quant_bits=4, group_size=128):
         super().__init__()
         self._bits, self.group_size = quant_bits, group_size
@@ -133,8 +145,8 @@ class _GroupWiseObserverImpl(BaseObserver):
         return _wrap(self._scales)
 
 
-class _FakeQuanterWithAbsMaxObserverImpl(BaseQuanter):
-    def __init__(self, moving_rate=0.9, bit_length=8, dtype="float32", name=None):
+class FakeQuanterWithAbsMaxObserverLayer(BaseQuanter):
+    def __init__(self, name=None, moving_rate=0.9, bit_length=8, dtype="float32"):
         super().__init__()
         self._bits = bit_length
         self.moving_rate = moving_rate
@@ -157,7 +169,7 @@ class _FakeQuanterWithAbsMaxObserverImpl(BaseQuanter):
         return self._scale
 
 
-class _FakeQuanterChannelWiseAbsMaxImpl(BaseQuanter):
+class FakeQuanterChannelWiseAbsMaxObserverLayer(BaseQuanter):
     def __init__(self, bit_length=8, quant_axis=-1, dtype="float32", name=None):
         super().__init__()
         self._bits, self._axis = bit_length, quant_axis
@@ -178,11 +190,19 @@ class _FakeQuanterChannelWiseAbsMaxImpl(BaseQuanter):
         return self._axis
 
 
-AbsmaxObserver = quanter("AbsmaxObserver")(_AbsmaxObserverImpl)
-GroupWiseWeightObserver = quanter("GroupWiseWeightObserver")(_GroupWiseObserverImpl)
-FakeQuanterWithAbsMaxObserver = quanter("FakeQuanterWithAbsMaxObserver")(_FakeQuanterWithAbsMaxObserverImpl)
+AbsmaxObserver = quanter("AbsmaxObserver")(AbsmaxObserverLayer)
+GroupWiseWeightObserver = quanter("GroupWiseWeightObserver")(GroupWiseWeightObserverLayer)
+
+
+def FakeQuanterWithAbsMaxObserver(moving_rate=0.9, bit_length=8, dtype="float32", name=None):
+    """factory; positional order is the reference's (moving_rate, bit_length, dtype, name)"""
+    return _Factory(FakeQuanterWithAbsMaxObserverLayer, "FakeQuanterWithAbsMaxObserver",
+                    kwargs=dict(name=name, moving_rate=moving_rate, bit_length=bit_length, dtype=dtype))
+
+
+FakeQuanterWithAbsMaxObserver._cls = FakeQuanterWithAbsMaxObserverLayer
 FakeQuanterChannelWiseAbsMaxObserver = quanter("FakeQuanterChannelWiseAbsMaxObserver")(
-    _FakeQuanterChannelWiseAbsMaxImpl)
+    FakeQuanterChannelWiseAbsMaxObserverLayer)
 
 
 class observers:  # paddle.quantization.observers namespace
@@ -196,61 +216,171 @@ class quanters:  # paddle.quantization.quanters namespace
 
 
 # ------------------------------------------------------------------------------ config
-class QuantConfig:
-    def __init__(self, activation=None, weight=None):
-        self._global = (activation, weight)
-        self._by_layer = {}
-        self._by_name = {}
-        self._by_type = {}
-        self._qat_layer_mapping = {nn.Linear: QuantedLinear, nn.Conv2D: QuantedConv2D}
+class SingleLayerConfig:
+    """activation + weight quanter factories of one layer (reference config.py SingleLayerConfig)."""
 
+    def __init__(self, activation=None, weight=None):
+        self._activation, self._weight = activation, weight
+
+    @property
+    def activation(self):
+        return self._activation
+
+    @property
+    def weight(self):
+        return self._weight
+
+    def __str__(self):
+        return f"activation: {self._activation}\nweight: {self._weight}"
+
+
+_DEFAULT_LEAVES = (nn.ReLU, nn.AvgPool2D)
+
+
+class QuantConfig:
+    """Maps every sublayer of a model to a SingleLayerConfig (reference config.py QuantConfig).
+
+    Precedence when `_specify` walks the model: global config < parent's config < config by layer
+    type < config by layer full name (`add_layer_config` keys by `layer.full_name()`, so it survives
+    the deep copy QAT/PTQ make of a non-inplace model)."""
+
+    def __init__(self, activation=None, weight=None):
+        self._global_config = None if activation is None and weight is None else \
+            SingleLayerConfig(activation, weight)
+        self._layer2config = {}
+        self._prefix2config = {}
+        self._type2config = {}
+        self._model = None
+        self._qat_layer_mapping = {nn.Linear: QuantedLinear, nn.Conv2D: QuantedConv2D}
+        self._customized_qat_layer_mapping = {}
+        self._customized_leaves = []
+
+    # ------------------------------------------------------------------ configuration
     def add_layer_config(self, layer, activation=None, weight=None):
         for l in (layer if isinstance(layer, (list, tuple)) else [layer]):
-            self._by_layer[id(l)] = (activation, weight)
+            self.add_name_config(l.full_name(), activation=activation, weight=weight)
 
     def add_name_config(self, layer_name, activation=None, weight=None):
         for n in (layer_name if isinstance(layer_name, (list, tuple)) else [layer_name]):
-            self._by_name[n] = (activation, weight)
+            self._prefix2config[n] = SingleLayerConfig(activation, weight)
 
     def add_type_config(self, layer_type, activation=None, weight=None):
         for t in (layer_type if isinstance(layer_type, (list, tuple)) else [layer_type]):
-            self._by_type[t] = (activation, weight)
+            if not (isinstance(t, type) and issubclass(t, nn.Layer)):
+                raise TypeError("add_type_config expects subclasses of paddle.nn.Layer")
+            self._type2config[t] = SingleLayerConfig(activation, weight)
 
     def add_qat_layer_mapping(self, source, target):
+        if not (isinstance(source, type) and isinstance(target, type) and issubclass(target, nn.Layer)):
+            raise TypeError("add_qat_layer_mapping expects two Layer classes")
         self._qat_layer_mapping[source] = target
+        self._customized_qat_layer_mapping[source] = target
 
-    def _config_for(self, name, layer):
-        if id(layer) in self._by_layer:
-            return self._by_layer[id(layer)]
-        if name in self._by_name:
-            return self._by_name[name]
-        for t, c in self._by_type.items():
-            if isinstance(layer, t):
-                return c
-        return self._global
+    def add_customized_leaf(self, layer_type):
+        self._customized_leaves.append(layer_type)
 
-    def __repr__(self):
-        return f"QuantConfig(global={self._global})"
+    @property
+    def customized_leaves(self):
+        return self._customized_leaves
+
+    @property
+    def qat_layer_mappings(self):
+        return self._qat_layer_mapping
+
+    @property
+    def default_qat_layer_mapping(self):
+        return {nn.Linear: QuantedLinear, nn.Conv2D: QuantedConv2D}
+
+    @property
+    def global_config(self):
+        return self._global_config
+
+    # ------------------------------------------------------------------ resolution
+    def _specify(self, model):
+        self._model = model
+        self._specify_helper(model)
+        return self
+
+    def _specify_helper(self, model):
+        for child in model.children():
+            cfg = self._layer2config.get(model, self._global_config)
+            cfg = self._type2config.get(type(child), cfg)
+            cfg = self._prefix2config.get(child.full_name(), cfg)
+            if cfg is not None:
+                self._layer2config[child] = cfg
+            self._specify_helper(child)
+        return self
+
+    def _get_config_by_layer(self, layer):
+        return self._layer2config.get(layer)
+
+    def _is_quantifiable(self, layer):
+        return layer in self._layer2config
+
+    def _is_leaf(self, layer):
+        return (type(layer) in _DEFAULT_LEAVES or not layer._sub_layers
+                or type(layer) in self._customized_leaves)
+
+    def _has_observer_config(self, layer):
+        cfg = self._get_config_by_layer(layer)
+        return cfg is not None and cfg.activation is not None
+
+    def _need_observe(self, layer):
+        return self._is_leaf(layer) and self._has_observer_config(layer)
+
+    def _get_qat_layer(self, layer):
+        target = self._customized_qat_layer_mapping.get(type(layer), self._qat_layer_mapping.get(type(layer)))
+        return target(layer, self._get_config_by_layer(layer))
+
+    def _get_observe_wrapper(self, layer):
+        return ObserveWrapper(_make(self._get_config_by_layer(layer).activation, layer), layer)
+
+    # ------------------------------------------------------------------ printing
+    def details(self):
+        return str(self) if self._model is None else self._details_helper(self._model)
+
+    def _details_helper(self, layer):
+        lines = []
+        for name, sub in layer.named_children():
+            if sub in self._layer2config:
+                body = self._details_helper(sub).replace("\n", "\n  ")
+                cfg = str(self._layer2config[sub]).replace("\n", "\n  ")
+                lines.append(f"({name}): {body}, {cfg}")
+        out = layer.__class__.__name__ + "("
+        if lines:
+            out += "\n  " + "\n  ".join(lines) + "\n"
+        return out + ")"
+
+    def __str__(self):
+        out = f"Global config:\n{self._global_config}\n"
+        if self._type2config:
+            out += f"Layer type config:\n{self._type2config}\n"
+        if self._prefix2config:
+            out += f"Layer prefix config: \n{self._prefix2config}\n"
+        return out
+
+    __repr__ = __str__
 
 
-def _make(f):
+def _make(f, layer=None):
     if f is None:
         return None
     if isinstance(f, _Factory):
-        return f._instance()
+        return f._instance(layer)
     if isinstance(f, type):
         return f()
     return copy.deepcopy(f)
 
 
 class QuantedLinear(nn.Layer):
+    """Linear whose weight (and input activation) go through fake quant (reference nn/quant/qat/linear.py)."""
+
     def __init__(self, layer, q_config):
         super().__init__()
         self.weight = layer.weight
         self.bias = layer.bias
-        act, wq = q_config
-        self.activation_quanter = _make(act)
-        self.weight_quanter = _make(wq)
+        self.weight_quanter = _make(q_config.weight, layer)
+        self.activation_quanter = _make(q_config.activation, layer)
 
     def forward(self, x):
         if self.activation_quanter is not None:
@@ -260,29 +390,34 @@ class QuantedLinear(nn.Layer):
 
 
 class QuantedConv2D(nn.Layer):
+    """Conv2D with fake-quantised weight / input (reference nn/quant/qat/conv.py); the conv's parameters
+    and geometry move here so the quantised weight feeds the same conv kernel."""
+
     def __init__(self, layer, q_config):
         super().__init__()
-        self._conv = layer
-        act, wq = q_config
-        self.activation_quanter = _make(act)
-        self.weight_quanter = _make(wq)
+        self.weight, self.bias = layer.weight, layer.bias
+        self._stride, self._padding, self._dilation = layer._stride, layer._padding, layer._dilation
+        self._groups, self._data_format = layer._groups, layer._data_format
+        self._padding_mode = layer._padding_mode
+        self.weight_quanter = _make(q_config.weight, layer)
+        self.activation_quanter = _make(q_config.activation, layer)
 
     def forward(self, x):
         if self.activation_quanter is not None:
             x = self.activation_quanter(x)
-        w = self._conv.weight
-        if self.weight_quanter is not None:
-            qw = self.weight_quanter(w)
-            saved = w._t
-            w._t = qw._t
-            try:
-                return self._conv(x)
-            finally:
-                w._t = saved
-        return self._conv(x)
+        w = self.weight_quanter(self.weight) if self.weight_quanter is not None else self.weight
+        p = self._padding
+        if self._padding_mode != "zeros":
+            pads = [p] * 4 if isinstance(p, int) else list(p)
+            x = nn.functional.pad(x, pads, mode=self._padding_mode, data_format=self._data_format)
+            p = 0
+        return nn.functional.conv2d(x, w, self.bias, self._stride, p, self._dilation, self._groups,
+                                    self._data_format)
 
 
 class ObserveWrapper(nn.Layer):
+    """Puts an observer / quanter in front of (or behind) a leaf layer (reference quantization/wrapper.py)."""
+
     def __init__(self, observer, observed, observe_input=True):
         super().__init__()
         self._observer = observer
@@ -291,63 +426,83 @@ class ObserveWrapper(nn.Layer):
 
     def forward(self, *inputs, **kw):
         if self._observe_input:
-            self._observer(inputs[0])
-            return self._observed(*inputs, **kw)
-        out = self._observed(*inputs, **kw)
-        self._observer(out)
-        return out
+            return self._observed(self._observer(*inputs), **kw)
+        return self._observer(self._observed(*inputs, **kw))
 
 
-def _replace(model, config, mapping, inplace):
-    m = model if inplace else copy.deepcopy(model)
-    for name, sub in list(m.named_sublayers()):
-        cfg = config._config_for(name, sub)
-        if cfg == (None, None):
-            continue
-        for src, dst in mapping.items():
-            if type(sub) is src:
-                parent = m
-                parts = name.split(".")
-                for p in parts[:-1]:
-                    parent = getattr(parent, p) if not p.isdigit() else parent[int(p)]
-                new = dst(sub, cfg)
-                if parts[-1].isdigit():
-                    parent[int(parts[-1])] = new
-                else:
-                    setattr(parent, parts[-1], new)
-                break
-    return m
+class _Quantization:
+    """Shared QAT / PTQ passes (reference quantization/quantize.py Quantization)."""
 
-
-class QAT:
     def __init__(self, config):
-        self._config = config
+        self._config = copy.deepcopy(config)
 
-    def quantize(self, model, inplace=False):
-        return _replace(model, self._config, self._config._qat_layer_mapping, inplace)
+    def _convert_to_quant_layers(self, model):
+        cfg = self._config
+        for name, child in list(model.named_children()):
+            if cfg._is_quantifiable(child) and type(child) in cfg.qat_layer_mappings:
+                model._sub_layers[name] = cfg._get_qat_layer(child)
+            else:
+                self._convert_to_quant_layers(child)
+
+    def _insert_activation_observers(self, model):
+        cfg = self._config
+        quanted = set(cfg._qat_layer_mapping.values()) | set(cfg._customized_qat_layer_mapping.values())
+        for name, child in list(model.named_children()):
+            if cfg._need_observe(child):
+                model._sub_layers[name] = cfg._get_observe_wrapper(child)
+            elif type(child) not in quanted:
+                self._insert_activation_observers(child)
+
+    def _prepare(self, model, inplace):
+        m = model if inplace else copy.deepcopy(model)
+        self._config._specify(m)
+        self._convert_to_quant_layers(m)
+        self._insert_activation_observers(m)
+        return m
 
     def convert(self, model, inplace=False, remain_weight=False):
-        """Freeze: weights are replaced by their quantised-dequantised values; quanters become
-        fixed-scale (eval) fake quant nodes."""
+        """Freeze: weights are replaced by their quantised-dequantised values (unless remain_weight);
+        activation observers / quanters become fixed-scale quant-dequant nodes."""
         m = model if inplace else copy.deepcopy(model)
         m.eval()
         with torch.no_grad():
-            for _, sub in m.named_sublayers(include_self=True):
-                if not isinstance(sub, (QuantedLinear, QuantedConv2D)):
-                    continue
-                w = sub.weight if isinstance(sub, QuantedLinear) else sub._conv.weight
-                q = sub.weight_quanter
-                if q is not None and not remain_weight:
-                    if isinstance(q, BaseQuanter):
-                        w._t.copy_(q(w)._t)
-                    else:  # observer: quantise with the observed range
-                        q(w)
-                        w._t.copy_(fake_quant(w._t, q.scales()._t.to(w._t.dtype), q.bit_length()))
-                    sub.weight_quanter = None
-                a = sub.activation_quanter
-                if a is not None and not isinstance(a, BaseQuanter):
-                    sub.activation_quanter = _FixedQuant(a.scales()._t.clone(), a.bit_length())
+            for sub in m.sublayers(include_self=True):
+                if isinstance(sub, (QuantedLinear, QuantedConv2D)):
+                    q = sub.weight_quanter
+                    if q is not None and not remain_weight:
+                        w = sub.weight
+                        if isinstance(q, BaseQuanter):
+                            w._t.copy_(q(w)._t)
+                        else:  # observer: quantise with the observed range
+                            q(w)
+                            w._t.copy_(fake_quant(w._t, q.scales()._t.to(w._t.dtype), q.bit_length()))
+                        sub.weight_quanter = None
+                    a = sub.activation_quanter
+                    if a is not None and not isinstance(a, BaseQuanter):
+                        sub.activation_quanter = _FixedQuant(a.scales()._t.clone(), a.bit_length())
+                elif isinstance(sub, ObserveWrapper):
+                    o = sub._observer
+                    if isinstance(o, BaseObserver) and not isinstance(o, BaseQuanter) and o.scales() is not None:
+                        sub._observer = _FixedQuant(o.scales()._t.clone(), o.bit_length())
         return m
+
+    def _details(self):
+        return self._config.details()
+
+    def __str__(self):
+        return self._details()
+
+    __repr__ = __str__
+
+
+class QAT(_Quantization):
+    """Quantization-aware training: fake quanters on weights + activations, trained through an STE
+    (reference quantization/qat.py)."""
+
+    def quantize(self, model, inplace=False):
+        if not model.training:
+            raise ValueError("QAT works on training models: call model.train() first")
+        return self._prepare(model, inplace)
 
 
 class _FixedQuant(nn.Layer):
@@ -363,14 +518,13 @@ class _FixedQuant(nn.Layer):
         return _wrap(fake_quant(t, self.scale._t.to(t.device, t.dtype), self.bits))
 
 
-class PTQ(QAT):
-    """Observers record activation / weight ranges on calibration batches; convert() bakes scales."""
+class PTQ(_Quantization):
+    """Post-training quantization: observers record activation / weight ranges on calibration batches;
+    convert() bakes the scales (reference quantization/ptq.py)."""
 
     def quantize(self, model, inplace=False):
-        return _replace(model, self._config, self._config._qat_layer_mapping, inplace)
-
-    def convert(self, model, inplace=False, remain_weight=False):
-        m = super().convert(model, inplace, remain_weight)
+        m = self._prepare(model, inplace)
+        m.eval()
         return m
 
 

@@ -162,3 +162,9 @@ def multiprocess_reader(readers, use_pipe=True, queue_size=1000):
             else:
                 yield s
     return reader
+
+
+import sys as _sys  # noqa: E402
+# `paddle.reader.decorator.<fn>` is the reference's spelling of the same functions
+decorator = _sys.modules[__name__]
+_sys.modules[__name__ + ".decorator"] = decorator

@@ -14,5 +14,6 @@ from .io import (deserialize_persistables, save_vars, load_vars, get_program_per
                  get_program_parameter, is_persistable, is_parameter)
 from . import io, log_helper  # noqa: F401,E402
 from ..framework.tensor import Tensor as Variable  # noqa: F401
+from ..framework.place import CPUPlace, CUDAPlace  # noqa: F401,E402
 
 ParallelExecutor = Executor

@@ -34,6 +34,13 @@ def default_startup_program():
     return _startup
 
 
+def _reset_default_programs():
+    """Fresh default main / startup programs (what a new process starts with)."""
+    global _main, _startup
+    _main, _startup = P.Program(), P.Program()
+    _retarget_tracer()
+
+
 def _retarget_tracer():
     global _global_tracer
     if _global_tracer is not None:

@@ -2,6 +2,42 @@
 from . import models  # noqa: F401
 from .models import *  # noqa: F401,F403
 from . import transforms, datasets, ops  # noqa: F401
+from .datasets import (MNIST, VOC2012, Cifar10, Cifar100, DatasetFolder, FashionMNIST,  # noqa: F401
+                       Flowers, ImageFolder)
+from .transforms import (  # noqa: F401
+    BaseTransform,
+    BrightnessTransform,
+    CenterCrop,
+    ColorJitter,
+    Compose,
+    ContrastTransform,
+    Grayscale,
+    HueTransform,
+    Normalize,
+    Pad,
+    RandomCrop,
+    RandomHorizontalFlip,
+    RandomResizedCrop,
+    RandomRotation,
+    RandomVerticalFlip,
+    Resize,
+    SaturationTransform,
+    ToTensor,
+    Transpose,
+    adjust_brightness,
+    adjust_contrast,
+    adjust_hue,
+    center_crop,
+    crop,
+    hflip,
+    normalize,
+    pad,
+    resize,
+    rotate,
+    to_grayscale,
+    to_tensor,
+    vflip,
+)
 
 _image_backend = "pil"
 

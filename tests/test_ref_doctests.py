@@ -13,17 +13,32 @@ REF = "/root/reference"
 
 MODULES = ["tensor", "nn/functional", "nn/layer", "fft.py", "signal.py", "geometric", "autograd",
            "audio/functional", "distribution", "sparse"]
+# framework-level APIs: static graph + io, jit, optimizers / LR schedules, vision, quantization, hapi
+MODULES_FRAMEWORK = ["static", "jit", "optimizer", "vision", "incubate", "quantization", "linalg.py", "hapi",
+                     "base/dygraph", "nn/initializer", "nn/utils", "metric", "framework"]
+
+
+def _run(tmp_path, modules):
+    out = tmp_path / "res.json"
+    env = dict(os.environ, PADDLE_AMD_FORCE_CPU="1", OMP_NUM_THREADS="4")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "ref_doctests.py"), "--ref", REF, "--modules",
+                        *modules, "--json", str(out)], env=env, capture_output=True, timeout=1500, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    print(r.stdout.decode().strip().splitlines()[-1])
+    return json.loads(out.read_text())
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "python", "paddle")), reason="reference tree not present")
+def test_reference_framework_doc_examples_pass_rate(tmp_path):
+    res = _run(tmp_path, MODULES_FRAMEWORK)
+    assert res["deterministic"] > 100
+    bad = [f"{f['status']} {f['where']}: {f['source'][:80]}" for f in res["failures"]]
+    assert res["pass_rate"] >= 0.95, "\n".join(bad[:40])
 
 
 @pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "python", "paddle")), reason="reference tree not present")
 def test_reference_doc_examples_pass_rate(tmp_path):
-    out = tmp_path / "res.json"
-    env = dict(os.environ, PADDLE_AMD_FORCE_CPU="1", OMP_NUM_THREADS="4")
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "ref_doctests.py"), "--ref", REF, "--modules",
-                        *MODULES, "--json", str(out)], env=env, capture_output=True, timeout=1500, cwd=str(tmp_path))
-    assert r.returncode == 0, r.stderr.decode()[-3000:]
-    res = json.loads(out.read_text())
-    print(r.stdout.decode().strip().splitlines()[-1])
+    res = _run(tmp_path, MODULES)
     assert res["deterministic"] > 1000
     bad = [f"{f['status']} {f['where']}: {f['source'][:80]}" for f in res["failures"]]
     assert res["pass_rate"] >= 0.97, "\n".join(bad[:40])

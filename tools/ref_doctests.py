@@ -117,7 +117,7 @@ def _close(a, b, rtol=1e-5, atol=1e-6):
 def _split_tensors(s):
     """[(shape, dtype, stop_gradient, values)] for every Tensor repr in s, plus the text outside them."""
     tensors, rest, pos = [], [], 0
-    for m in re.finditer(r"Tensor\(shape=\[([^\]]*)\],\s*dtype=([\w.]+),\s*place=Place\([^)]*\),\s*"
+    for m in re.finditer(r"Tensor\(shape=\[([^\]]*)\],\s*dtype=([\w.]+),\s*place=(?:Place\([^)]*\)|\w*Place(?:\([^)]*\))?),\s*"
                          r"stop_gradient=(True|False),", s):
         rest.append(s[pos:m.start()])
         # the payload runs to the matching close paren of "Tensor("
@@ -222,7 +222,37 @@ def _merge_continuations(examples):
     return out
 
 
-def run_docstring(doc, name, timeout=20):
+def _drop_text_blocks(doc):
+    """Remove ``.. code-block:: text`` bodies: prompts inside them are pseudo-code, not examples."""
+    out, skip_indent = [], None
+    for line in doc.splitlines():
+        stripped = line.lstrip()
+        ind = len(line) - len(stripped)
+        if skip_indent is not None:
+            if not stripped or ind > skip_indent:
+                continue
+            skip_indent = None
+        if re.match(r"\.\.\s+code-block::\s*(text|none|bash|shell|console)\s*$", stripped):
+            skip_indent = ind
+            continue
+        out.append(line)
+    return "\n".join(out)
+
+
+def module_namespace(rel):
+    """Names of our module matching a reference file, like xdoctest's default of running a docstring's
+    examples in its module's globals (``jit/utils.py`` -> ``paddle.jit.utils``)."""
+    mod = "paddle." + rel[:-3].replace("/", ".") if rel.endswith(".py") else None
+    if mod is None:
+        return {}
+    try:
+        m = importlib.import_module(mod)
+    except Exception:
+        return {}
+    return {k: v for k, v in vars(m).items() if not k.startswith("_")}
+
+
+def run_docstring(doc, name, timeout=20, base_globs=None):
     """[(status, source, want, got)] for each checked example of one docstring, executed in one namespace.
 
     xdoctest semantics: the output of statements without an expected output accumulates and is checked at
@@ -230,12 +260,14 @@ def run_docstring(doc, name, timeout=20):
     if _REQUIRES.search(doc):
         return [("skip", "", "", "requires device")]
     parser = doctest.DocTestParser()
+    doc = _drop_text_blocks(doc)
     try:
         examples = parser.get_examples(_sentinelize(doc), name)
     except ValueError as e:
         return [("error", "<parse>", "", f"unparsable docstring: {e}")]
     examples = _merge_continuations(examples)
-    globs = {"__name__": "__doctest__", "__doctest_directive__": lambda *a: None}
+    globs = dict(base_globs or {})
+    globs.update({"__name__": "__doctest__", "__doctest_directive__": lambda *a: None})
     results, skipping, skipped_any, random_seen = [], False, False, False
     pending = ""
     for ex in examples:
@@ -278,6 +310,12 @@ def run_docstring(doc, name, timeout=20):
                 status = "pass"
             elif isinstance(e, NameError) and skipped_any:
                 status = "skip"
+            elif re.search(r"no network|needs network access", str(e)):
+                # a dataset / hub download the offline image cannot make: environment-bound
+                status, skipped_any = "skip", True
+            elif isinstance(e, ModuleNotFoundError) and not str(e.name or "").startswith("paddle"):
+                # a third-party package the image lacks (cv2, astor): environment-bound, like a device
+                status, skipped_any = "skip", True
             else:
                 status, got = "error", f"{type(e).__name__}: {e}"[:300]
         finally:
@@ -318,14 +356,24 @@ def run(ref="/root/reference", modules=None, verbose=False):
     failures = []
     for rel, path in iter_files(ref, modules or DEFAULT_MODULES):
         counts = {"pass": 0, "fail": 0, "error": 0, "skip": 0}
+        base = module_namespace(rel)
         for name, doc in _docstrings(path):
             np.set_printoptions(precision=8, threshold=1000, edgeitems=3, linewidth=75, suppress=False)
             import torch
             torch.set_printoptions(profile="default")
+            torch.set_grad_enabled(True)
             paddle.set_default_dtype("float32")
             if hasattr(paddle, "disable_static"):
                 paddle.disable_static()
-            for status, src, want, got in run_docstring(doc, f"{rel}:{name}"):
+            # each reference example runs in a fresh process: reset the process-wide state examples set
+            from paddlepaddle_amd.static import executor as _sx
+            _sx._reset_default_programs()
+            from paddlepaddle_amd.nn.layer import layers as _ly
+            _ly._layer_name_counters.clear()
+            _ly._param_name_counters.clear()
+            if hasattr(paddle, "vision"):
+                paddle.vision.set_image_backend("pil")
+            for status, src, want, got in run_docstring(doc, f"{rel}:{name}", base_globs=base):
                 counts[status] += 1
                 if status in ("fail", "error"):
                     failures.append({"where": f"{rel}:{name}", "status": status, "source": src.strip()[:400],
