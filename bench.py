@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--tp", type=int, default=None,
                    help="tensor-parallel degree (GPT: sharding over world/tp ranks). Default: the BASELINE config "
                         "'GPT-3 13B sharding stage-3 + TP=2' -> 2 on any multi-GPU run of GPT, 1 on one GPU")
+    p.add_argument("--fused-head-ce", type=int, default=0,
+                   help="LM head + cross-entropy over vocabulary slices, logits never materialised (ops/lm_head.py)")
     p.add_argument("--sp", type=int, default=1,
                    help="GPT with tp > 1: sequence parallel (token shards between the TP regions; all-gather / "
                         "reduce-scatter overlapped with the GEMMs, parallel/sequence_parallel.py)")
@@ -119,7 +121,8 @@ def gpt_bench(args, paddle, world, dist_on):
         data_rank = hcg.get_sharding_parallel_rank()
         shard_group = hcg.get_sharding_parallel_group()
     cfg = cfgs[args.model](max_position_embeddings=max(args.seq_len, 128), use_recompute=bool(args.recompute),
-                           tensor_parallel_degree=tp, sequence_parallel=bool(args.sp) and tp > 1)
+                           tensor_parallel_degree=tp, sequence_parallel=bool(args.sp) and tp > 1,
+                           fused_head_ce=bool(args.fused_head_ce))
     paddle.set_default_dtype("bfloat16")
     paddle.seed(1234)
     t0 = time.time()
@@ -160,8 +163,10 @@ def gpt_bench(args, paddle, world, dist_on):
             ctx = no_sync() if (no_sync is not None and n_shard > 1 and a < args.accum - 1) else \
                 contextlib.nullcontext()
             with ctx:
-                logits = model(ids[a])
-                loss = crit(logits, lbl[a])
+                if cfg.fused_head_ce and tp == 1:
+                    loss = model(ids[a], labels=lbl[a])
+                else:
+                    loss = crit(model(ids[a]), lbl[a])
                 if args.accum > 1:
                     loss = loss * (1.0 / args.accum)
                 loss.backward()
@@ -378,6 +383,7 @@ def main():
                        if is_llama else args.model,
                        "global_batch": gb, "seq_len": args.seq_len, "micro_batch": args.micro_batch,
                        "accum_steps": args.accum, "parallelism": par, "recompute": bool(args.recompute),
+                       "fused_head_ce": bool(args.fused_head_ce),
                        "optimizer": "AdamW fp32-master fused HIP", "amp": "O2 bf16",
                        "allocator": ("native auto-growth best-fit" if _native_alloc_on() else "torch caching"),
                        **({"stage3_params": ("gathered once per step, resident until the optimizer step"

@@ -120,16 +120,74 @@ class FusedTransformerEncoderLayer(_nn.Layer):
 
 
 class FusedMultiTransformer(_nn.Layer):
-    def __init__(self, embed_dim, num_heads, dim_feedforward, dropout_rate=0.0, activation="gelu",
-                 normalize_before=True, num_layers=1, epsilon=1e-5, name=None, **kw):
-        super().__init__()
-        self.layers = _nn.LayerList([FusedTransformerEncoderLayer(embed_dim, num_heads, dim_feedforward,
-                                                                  dropout_rate, activation,
-                                                                  normalize_before=normalize_before)
-                                     for _ in range(num_layers)])
+    """Stack of generation decoder layers over F.fused_multi_transformer (reference
+    incubate/nn/layer/fused_transformer.py FusedMultiTransformer): per-layer parameter lists, qkv weight
+    [3, H, D, E] (or [E, 3, H, D] without trans_qkvw; [H + 2*kv, D, E] with gqa_group_size = kv heads),
+    heads / ffn width split over nranks tensor-parallel ranks (ring_id selects the mp all-reduce)."""
 
-    def forward(self, src, attn_mask=None, caches=None, time_step=None, **kw):
-        h = src
-        for l in self.layers:
-            h = l(h, attn_mask)
-        return h
+    def __init__(self, embed_dim, num_heads, dim_feedforward, dropout_rate=0.0, activation="gelu",
+                 normalize_before=True, ln_scale_attrs=None, ln_bias_attrs=None, qkv_weight_attrs=None,
+                 qkv_bias_attrs=None, linear_weight_attrs=None, linear_bias_attrs=None, ffn_ln_scale_attrs=None,
+                 ffn_ln_bias_attrs=None, ffn1_weight_attrs=None, ffn1_bias_attrs=None, ffn2_weight_attrs=None,
+                 ffn2_bias_attrs=None, epsilon=1e-5, residual_alpha=1.0, num_layers=-1, nranks=1, trans_qkvw=True,
+                 ring_id=-1, norm_type="layernorm", use_neox_rotary_style=False, gqa_group_size=-1, name=None):
+        super().__init__()
+        if embed_dim <= 0 or num_heads <= 0 or dim_feedforward <= 0:
+            raise ValueError("embed_dim, num_heads and dim_feedforward must be positive")
+        if num_heads % nranks or dim_feedforward % nranks:
+            raise ValueError("num_heads and dim_feedforward must divide by nranks")
+        if num_layers < 0:
+            num_layers = len(qkv_weight_attrs) if isinstance(qkv_weight_attrs, (list, tuple)) else 1
+        self.normalize_before, self.dropout_rate, self.activation = normalize_before, dropout_rate, activation
+        self._epsilon, self._residual_alpha, self._trans_qkvw = epsilon, residual_alpha, trans_qkvw
+        self._ring_id, self._norm_type = ring_id, norm_type
+        self._use_neox_rotary_style, self._gqa_group_size = use_neox_rotary_style, gqa_group_size
+        self.head_dim = embed_dim // num_heads
+        H = num_heads // nranks
+        kv = (gqa_group_size // nranks) if gqa_group_size and gqa_group_size > 0 else None
+        ffn = dim_feedforward // nranks
+        heads_shape = [3, H] if kv is None else [H + 2 * kv]
+
+        def attr(a, i):
+            return a[i] if isinstance(a, (list, tuple)) else a
+
+        names = ["ln_scales", "ln_biases", "qkv_weights", "qkv_biases", "linear_weights", "linear_biases",
+                 "ffn_ln_scales", "ffn_ln_biases", "ffn1_weights", "ffn1_biases", "ffn2_weights", "ffn2_biases"]
+        for n in names:
+            setattr(self, n, _nn.ParameterList())
+        one, zero = _I.Constant(1.0), _I.Constant(0.0)
+        for i in range(num_layers):
+            self.ln_scales.append(self.create_parameter([embed_dim], attr=attr(ln_scale_attrs, i),
+                                                        default_initializer=one))
+            self.ln_biases.append(self.create_parameter([embed_dim], attr=attr(ln_bias_attrs, i), is_bias=True))
+            qkv_shape = ([*heads_shape, self.head_dim, embed_dim] if trans_qkvw
+                         else [embed_dim, *heads_shape, self.head_dim])
+            self.qkv_weights.append(self.create_parameter(qkv_shape, attr=attr(qkv_weight_attrs, i)))
+            self.qkv_biases.append(self.create_parameter([*heads_shape, self.head_dim],
+                                                         attr=attr(qkv_bias_attrs, i), is_bias=True))
+            self.linear_weights.append(self.create_parameter([H * self.head_dim, embed_dim],
+                                                             attr=attr(linear_weight_attrs, i)))
+            self.linear_biases.append(self.create_parameter([embed_dim], attr=attr(linear_bias_attrs, i),
+                                                            is_bias=True))
+            self.ffn_ln_scales.append(self.create_parameter([embed_dim], attr=attr(ffn_ln_scale_attrs, i),
+                                                            default_initializer=one))
+            self.ffn_ln_biases.append(self.create_parameter([embed_dim], attr=attr(ffn_ln_bias_attrs, i),
+                                                            is_bias=True))
+            self.ffn1_weights.append(self.create_parameter([embed_dim, ffn], attr=attr(ffn1_weight_attrs, i)))
+            self.ffn1_biases.append(self.create_parameter([ffn], attr=attr(ffn1_bias_attrs, i), is_bias=True))
+            self.ffn2_weights.append(self.create_parameter([ffn, embed_dim], attr=attr(ffn2_weight_attrs, i)))
+            self.ffn2_biases.append(self.create_parameter([embed_dim], attr=attr(ffn2_bias_attrs, i), is_bias=True))
+        del zero
+
+    def forward(self, src, attn_mask=None, caches=None, pre_caches=None, rotary_embs=None, rotary_emb_dims=0,
+                beam_offset=None, seq_lens=None, time_step=None):
+        return F.fused_multi_transformer(
+            src, list(self.ln_scales), list(self.ln_biases), list(self.qkv_weights), list(self.qkv_biases),
+            list(self.linear_weights), list(self.linear_biases), list(self.ffn_ln_scales),
+            list(self.ffn_ln_biases), list(self.ffn1_weights), list(self.ffn1_biases), list(self.ffn2_weights),
+            list(self.ffn2_biases), pre_layer_norm=self.normalize_before, epsilon=self._epsilon,
+            residual_alpha=self._residual_alpha, cache_kvs=caches, beam_offset=beam_offset, pre_caches=pre_caches,
+            seq_lens=seq_lens, rotary_embs=rotary_embs, time_step=time_step, attn_mask=attn_mask,
+            dropout_rate=self.dropout_rate, rotary_emb_dims=rotary_emb_dims, activation=self.activation,
+            training=self.training, trans_qkvw=self._trans_qkvw, ring_id=self._ring_id, norm_type=self._norm_type,
+            use_neox_rotary_style=self._use_neox_rotary_style, gqa_group_size=self._gqa_group_size)

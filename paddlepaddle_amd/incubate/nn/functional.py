@@ -260,47 +260,184 @@ def fused_multi_head_attention(x, qkv_weight, linear_weight, pre_layer_norm=Fals
     return _wrap(out)
 
 
+def _fmt_norm(t, w, b, eps, norm_type):
+    if norm_type == "rmsnorm":
+        return _ops.rms_norm(t, _t(w), eps)
+    d = t.shape[-1]
+    ww = _t(w) if w is not None else torch.ones(d, dtype=t.dtype, device=t.device)
+    bb = _t(b) if b is not None else torch.zeros(d, dtype=t.dtype, device=t.device)
+    return _ops.layer_norm(t, ww, bb, eps)
+
+
+def _mp_allreduce(t, ring_id):
+    """ring_id >= 0: tensor-parallel layers; the row-parallel outputs are summed over the mp group."""
+    if ring_id is None or ring_id < 0:
+        return t
+    from ...parallel import tensor_parallel as _tp
+    g = _tp._mp_group()
+    if _tp._ws(g) > 1:
+        torch.distributed.all_reduce(t, group=g.process_group)
+    return t
+
+
 def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, linear_weights, linear_biases,
                             ffn_ln_scales, ffn_ln_biases, ffn1_weights, ffn1_biases, ffn2_weights, ffn2_biases,
-                            pre_layer_norm=True, epsilon=1e-05, cache_kvs=None, time_step=None, attn_mask=None,
-                            dropout_rate=0.0, activation="gelu", training=False, mode="upscale_in_train",
-                            trans_qkvw=True, ring_id=-1, name=None, **kw):
-    """Stack of pre-LN decoder layers (inference)."""
-    h = x
+                            pre_layer_norm=True, epsilon=1e-05, residual_alpha=1.0, cache_kvs=None, beam_offset=None,
+                            pre_caches=None, seq_lens=None, rotary_embs=None, time_step=None, attn_mask=None,
+                            dropout_rate=0.0, rotary_emb_dims=0, activation="gelu", training=False,
+                            mode="upscale_in_train", trans_qkvw=True, ring_id=-1, norm_type="layernorm",
+                            use_neox_rotary_style=False, gqa_group_size=-1, name=None):
+    """Stack of decoder layers for generation (reference incubate/nn/functional/fused_transformer.py:1015).
+
+    Three modes, by (cache_kvs, time_step):
+    - no cache: every layer is attention over the S tokens (+ attn_mask), LN/FFN, residuals.
+    - cache_kvs, time_step None (context / prefill): K/V of the S tokens (after pre_caches, if any)
+      are written into cache_kvs[i][:, :, :, P:P+S] (cache layout [2, B, kv_heads, max_len, D]).
+    - cache_kvs and time_step (decode, S == 1): K/V are written at position time_step (or seq_lens[b]
+      per sequence) and the token attends over positions [0, step] of the cache with the HIP
+      flash-decoding kernel (ops.dense_decode_attention), or the math path when attn_mask is given.
+    Returns out, or (out, cache_kvs) when cache_kvs is given (the caches are updated in place).
+    qkv_weights: [3, H, D, E] (trans_qkvw) or [E, 3, H, D]; with gqa_group_size = kv heads,
+    [H + 2*kv_heads, D, E] / [E, H + 2*kv_heads, D]."""
+    if beam_offset is not None:
+        raise NotImplementedError("fused_multi_transformer: beam_offset (beam-search cache reorder) is not supported")
+    if mode != "upscale_in_train" and training and dropout_rate > 0:
+        raise NotImplementedError("fused_multi_transformer: only mode='upscale_in_train' dropout is supported")
+    xt = _t(x)
+    B, S, E = xt.shape
+    decode = cache_kvs is not None and time_step is not None
+    if decode and S != 1:
+        raise ValueError("fused_multi_transformer decode (time_step given) takes one token per sequence")
+    if decode:
+        if seq_lens is not None:
+            steps = _t(seq_lens).reshape(-1).to(device=xt.device, dtype=torch.long)
+        else:  # time_step lives on the host (CPUPlace in the reference): no device sync
+            ts = _t(time_step)
+            steps = torch.full((B,), int(ts.reshape(-1)[0]), dtype=torch.long, device=xt.device)
+    rot = None
+    if rotary_embs is not None and rotary_emb_dims > 0:
+        r = _t(rotary_embs)  # [2, B|1, 1, L, D]
+        rot = (r[0, :, 0], r[1, :, 0])  # [B|1, L, D]
+    mask = _t(attn_mask)
+    act = "gelu" if activation == "gelu" else ("relu" if activation == "relu" else None)
+    if act is None:
+        raise ValueError(f"fused_multi_transformer: unsupported activation {activation}")
+    h = xt
     for i in range(len(qkv_weights)):
-        h = fused_multi_head_attention(h, qkv_weights[i], linear_weights[i], pre_layer_norm=pre_layer_norm,
-                                       pre_ln_scale=ln_scales[i], pre_ln_bias=ln_biases[i],
-                                       pre_ln_epsilon=epsilon, qkv_bias=qkv_biases[i], linear_bias=linear_biases[i],
-                                       attn_mask=attn_mask, dropout_rate=dropout_rate, attn_dropout_rate=0.0,
-                                       training=training, transpose_qkv_wb=not trans_qkvw and False)
-        h = fused_feedforward(h, ffn1_weights[i], ffn2_weights[i], ffn1_biases[i], ffn2_biases[i],
-                              ln1_scale=ffn_ln_scales[i], ln1_bias=ffn_ln_biases[i], dropout1_rate=0.0,
-                              dropout2_rate=dropout_rate, activation=activation, ln1_epsilon=epsilon,
-                              pre_layer_norm=pre_layer_norm, training=training)
-    return h
+        w = _t(qkv_weights[i])
+        if trans_qkvw:
+            Dh = w.shape[-2]
+            w2 = w.reshape(-1, E)  # [(3|H+2Hk) * Dh, E]
+            nh = w2.shape[0] // Dh
+        else:
+            Dh = w.shape[-1]
+            w2 = w.reshape(E, -1).t()
+            nh = w2.shape[0] // Dh
+        Hk = gqa_group_size if gqa_group_size and gqa_group_size > 0 else nh // 3
+        H = nh - 2 * Hk
+        residual = h
+        t = _fmt_norm(h, ln_scales[i], ln_biases[i], epsilon, norm_type) if pre_layer_norm else h
+        qkv = torch.matmul(t, w2.t())
+        if qkv_biases is not None and qkv_biases[i] is not None:
+            qkv = qkv + _t(qkv_biases[i]).reshape(-1)
+        qkv = qkv.view(B, S, nh, Dh)
+        q, k, v = qkv[:, :, :H], qkv[:, :, H:H + Hk], qkv[:, :, H + Hk:]
+        cache = _t(cache_kvs[i]) if cache_kvs is not None else None
+        if decode:
+            q, k, v = q[:, 0], k[:, 0], v[:, 0]  # [B, heads, Dh]
+            if rot is not None:
+                bi = torch.arange(B, device=xt.device) % rot[0].shape[0]
+                cs, sn = rot[0][bi, steps], rot[1][bi, steps]
+                q = _rotate_rows(q, cs, sn, use_neox_rotary_style)
+                k = _rotate_rows(k, cs, sn, use_neox_rotary_style)
+            bi = torch.arange(B, device=xt.device)
+            cache[0][bi, :, steps] = k.to(cache.dtype)
+            cache[1][bi, :, steps] = v.to(cache.dtype)
+            if mask is None:
+                o = _ops.dense_decode_attention(q.to(cache.dtype), cache[0], cache[1], steps + 1).to(q.dtype)
+            else:  # additive [B, 1, 1, step + 1] mask: math path over the cache prefix
+                Lc = cache.shape[3]
+                G = H // Hk
+                s = torch.einsum("bkgd,bkld->bkgl", q.float().view(B, Hk, G, Dh), cache[0].float()) / math.sqrt(Dh)
+                m = mask.float().reshape(B, 1, 1, -1)
+                s[..., :m.shape[-1]] += m
+                valid = torch.arange(Lc, device=xt.device)[None] <= steps[:, None]
+                s = s.masked_fill(~valid[:, None, None], float("-inf"))
+                o = torch.einsum("bkgl,bkld->bkgd", torch.softmax(s, -1), cache[1].float()).reshape(B, H, Dh)
+            o = o.to(h.dtype).reshape(B, 1, H * Dh)
+        else:
+            if rot is not None:
+                pos = torch.arange(S, device=xt.device)
+                cs = rot[0][:, pos].expand(B, S, -1).reshape(B * S, -1)
+                sn = rot[1][:, pos].expand(B, S, -1).reshape(B * S, -1)
+                q = _rotate_rows(q.reshape(B * S, H, Dh), cs, sn, use_neox_rotary_style).view(B, S, H, Dh)
+                k = _rotate_rows(k.reshape(B * S, Hk, Dh), cs, sn, use_neox_rotary_style).view(B, S, Hk, Dh)
+            kk, vv = k, v
+            P = 0
+            if pre_caches is not None and pre_caches[i] is not None:
+                pc = _t(pre_caches[i])  # [2, B, Hk, P, Dh]
+                P = pc.shape[3]
+                kk = torch.cat([pc[0].transpose(1, 2).to(k.dtype), k], 1)
+                vv = torch.cat([pc[1].transpose(1, 2).to(v.dtype), v], 1)
+            if cache is not None:
+                cache[0][:, :, :P + S] = kk.transpose(1, 2).to(cache.dtype)
+                cache[1][:, :, :P + S] = vv.transpose(1, 2).to(cache.dtype)
+            o = _ops.flash_attention(q, kk, vv, causal=False, mask=mask,
+                                     dropout=0.0, training=False).reshape(B, S, H * Dh)
+        out = torch.matmul(o, _t(linear_weights[i]))
+        out = _mp_allreduce(out, ring_id)
+        if linear_biases is not None and linear_biases[i] is not None:
+            out = out + _t(linear_biases[i])
+        out = _ops.dropout_add(out, residual * residual_alpha if residual_alpha != 1.0 else residual,
+                               dropout_rate if training else 0.0, training)
+        if not pre_layer_norm:
+            out = _fmt_norm(out, ln_scales[i], ln_biases[i], epsilon, norm_type)
+        residual = out
+        t = _fmt_norm(out, ffn_ln_scales[i], ffn_ln_biases[i], epsilon, norm_type) if pre_layer_norm else out
+        f = _ops.fused_linear(t, _t(ffn1_weights[i]), _t(ffn1_biases[i]) if ffn1_biases is not None else None,
+                              act=act)
+        f = torch.matmul(f, _t(ffn2_weights[i]))
+        f = _mp_allreduce(f, ring_id)
+        if ffn2_biases is not None and ffn2_biases[i] is not None:
+            f = f + _t(ffn2_biases[i])
+        h = _ops.dropout_add(f, residual * residual_alpha if residual_alpha != 1.0 else residual,
+                             dropout_rate if training else 0.0, training)
+        if not pre_layer_norm:
+            h = _fmt_norm(h, ffn_ln_scales[i], ffn_ln_biases[i], epsilon, norm_type)
+    return (_wrap(h), cache_kvs) if cache_kvs is not None else _wrap(h)
 
 
 # --------------------------------------------------------------------------------------- attention
 def variable_length_memory_efficient_attention(query, key, value, seq_lens, kv_seq_lens, mask=None, scale=None,
                                                causal=False, pre_cache_length=0):
-    """query [B, H, Sq, D], key/value [B, Hk, Sk, D]; per-batch valid lengths."""
+    """query [B, H, Sq, D], key/value [B, Hk, Sk, D] padded; row i of batch b is valid for i < seq_lens[b] and
+    attends to keys j < kv_seq_lens[b] + pre_cache_length (and, when causal, j <= i + pre_cache_length).
+    One flash-attention launch with the lengths folded into a dense keep-mask built on the device (no host
+    sync; capturable); rows past seq_lens[b] come out zero. Reference:
+    incubate/nn/functional/variable_length_memory_efficient_attention.py:33."""
     q, k, v = _t(query), _t(key), _t(value)
     B, H, Sq, D = q.shape
-    sl = _t(seq_lens).reshape(-1).tolist()
-    kl = _t(kv_seq_lens).reshape(-1).tolist()
-    out = torch.zeros_like(q)
+    Sk = k.shape[2]
+    dev = q.device
+    sl = _t(seq_lens).reshape(-1).to(dev)
+    kl = _t(kv_seq_lens).reshape(-1).to(dev) + int(pre_cache_length)
+    rows = torch.arange(Sq, device=dev)
+    cols = torch.arange(Sk, device=dev)
+    keep = cols.view(1, 1, 1, Sk) < kl.view(B, 1, 1, 1)
+    if causal:
+        keep = keep & (cols.view(1, 1, 1, Sk) <= rows.view(1, 1, Sq, 1) + int(pre_cache_length))
+    row_ok = rows.view(1, Sq) < sl.view(B, 1)
+    keep = keep | ~row_ok.view(B, 1, Sq, 1)  # padded rows see every key (finite softmax), zeroed below
     m = _t(mask)
-    for b in range(B):
-        n, nk = int(sl[b]), int(kl[b]) + pre_cache_length
-        if n == 0:
-            continue
-        qb = q[b:b + 1, :, :n].transpose(1, 2)
-        kb = k[b:b + 1, :, :nk].transpose(1, 2)
-        vb = v[b:b + 1, :, :nk].transpose(1, 2)
-        mb = m[b:b + 1, :, :n, :nk] if m is not None else None
-        o = _ops.flash_attention(qb, kb, vb, causal=causal, scale=scale, mask=mb, training=False)
-        out[b, :, :n] = o[0].transpose(0, 1)
-    return _wrap(out)
+    if m is not None:
+        full = m.float().expand(B, 1, Sq, Sk) if m.dim() == 4 else m.float()
+        attn_mask = full.masked_fill(~keep, float("-inf"))
+    else:
+        attn_mask = keep
+    o = _ops.flash_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), causal=False, scale=scale,
+                             mask=attn_mask, training=False)  # [B, Sq, H, D]
+    o = o.transpose(1, 2)
+    return _wrap(torch.where(row_ok.view(B, 1, Sq, 1), o, torch.zeros((), dtype=o.dtype, device=dev)))
 
 
 def masked_multihead_attention(x, cache_kv=None, bias=None, src_mask=None, cum_offsets=None, sequence_lengths=None,
@@ -377,68 +514,82 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
                               tgt_mask=None, max_seq_len=-1, block_size=64, use_neox_style=False,
                               use_dynamic_cachekv_quant=False, quant_round_type=1, quant_max_bound=127.0,
                               quant_min_bound=-127.0, out_scale=-1, compute_dtype="default", rope_theta=10000.0):
-    """Paged-KV attention for a mixed prefill/decode batch.
-    qkv [tokens, 3*H*D] (unpadded, sequences back to back per cu_seqlens_q); key/value_cache
-    [num_blocks, H, block_size, D]; block_tables [B, max_blocks]. Prefill sequences (encoder len > 0)
-    write their K/V into their blocks and run causal flash attention; decode sequences append one
-    position at seq_lens_decoder[b] and attend over the cached prefix (one batched gather)."""
+    """Paged-KV attention for a mixed prefill/decode batch, entirely on the device (no host reads of the
+    length tensors, so a decode step can be captured in a hipGraph and replayed with new lengths).
+    Reference: incubate/nn/functional/block_multihead_attention.py:33.
+
+    qkv [tokens, (H + 2*Hk) * D]: the step's tokens back to back per cu_seqlens_q; key/value_cache
+    [num_blocks, Hk, block_size, D]; block_tables [B, max_blocks]. Token t of sequence b sits at cache
+    position pos = t - cu_seqlens_q[b] + seq_lens_decoder[b]; its rotated K/V are scattered to
+    block_tables[b, pos // bs] row pos % bs. Prefill tokens (seq_lens_encoder[b] > 0) attend causally
+    within their sequence through the varlen flash-attention kernel; decode tokens attend over cache
+    positions [0, pos] through the paged flash-decoding kernel. max_enc_len_this_time /
+    max_dec_len_this_time (host tensors from blha_get_max_len) skip a phase that has no tokens; without
+    them both run and the per-token result is selected on the device.
+    Quantized caches, pre-caches, dense masks and quantized outputs raise NotImplementedError."""
+    unsupported = {"pre_key_cache": pre_key_cache, "pre_value_cache": pre_value_cache,
+                   "cache_k_quant_scales": cache_k_quant_scales, "cache_v_quant_scales": cache_v_quant_scales,
+                   "cache_k_dequant_scales": cache_k_dequant_scales,
+                   "cache_v_dequant_scales": cache_v_dequant_scales, "mask": mask, "tgt_mask": tgt_mask}
+    for n, val in unsupported.items():
+        if val is not None:
+            raise NotImplementedError(f"block_multihead_attention: `{n}` is not supported on this backend")
+    if use_dynamic_cachekv_quant or (out_scale is not None and out_scale > 0):
+        raise NotImplementedError("block_multihead_attention: int8 cache / output quantization is not supported")
     q_all = _t(qkv)
     kc, vc = _t(key_cache), _t(value_cache)
-    nb, H, bs, D = kc.shape
+    nb, Hk, bs, D = kc.shape
+    if qkv_out_scale is not None:  # int32 GEMM output -> real values
+        cdt = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(compute_dtype, kc.dtype)
+        q_all = (q_all.float() * _t(qkv_out_scale).float().reshape(-1)).to(cdt)
     if qkv_bias is not None:
-        q_all = q_all + _t(qkv_bias)
-    x = q_all.view(-1, 3, H, D)
-    enc = _t(seq_lens_encoder).reshape(-1).tolist()
-    dec = _t(seq_lens_decoder).reshape(-1).tolist()
-    this = _t(seq_lens_this_time).reshape(-1).tolist()
-    bt = _t(block_tables).long()
-    cu = _t(cu_seqlens_q).reshape(-1).tolist()
-    out = torch.zeros(x.shape[0], H, D, dtype=x.dtype, device=x.device)
+        q_all = q_all + _t(qkv_bias).reshape(-1)
+    T = q_all.shape[0]
+    H = q_all.shape[1] // D - 2 * Hk
+    x = q_all.view(T, H + 2 * Hk, D)
+    q, k, v = x[:, :H], x[:, H:H + Hk], x[:, H + Hk:]
+    dev = x.device
+    cu = _t(cu_seqlens_q).reshape(-1).to(device=dev, dtype=torch.long)
+    B = cu.numel() - 1
+    tok = torch.arange(T, device=dev)
+    bid = torch.searchsorted(cu[1:].contiguous(), tok, right=True).clamp_(max=B - 1)
+    dec = _t(seq_lens_decoder).reshape(-1).to(device=dev, dtype=torch.long)
+    enc = _t(seq_lens_encoder).reshape(-1).to(device=dev, dtype=torch.long)
+    pos = tok - cu[bid] + dec[bid]
     rope = _t(rope_emb)
-
-    def rot(t, pos):  # t [n, H, D]; positions [n]
-        if rope is None:
-            return t
-        cos = rope[0].reshape(rope.shape[1], -1, rope.shape[-1])[0][pos] if rope.dim() >= 3 else None
-        sin = rope[1].reshape(rope.shape[1], -1, rope.shape[-1])[0][pos]
-        cos = torch.cat([cos, cos], -1) if cos.shape[-1] * 2 == D else cos
-        sin = torch.cat([sin, sin], -1) if sin.shape[-1] * 2 == D else sin
-        return _rotate_rows(t, cos, sin, True if use_neox_style else False)
-
-    dec_b = []
-    for b in range(len(this)):
-        n = int(this[b])
-        if n == 0:
-            continue
-        s0 = int(cu[b])
-        if enc[b] > 0:  # prefill
-            pos = torch.arange(n, device=x.device)
-            q = rot(x[s0:s0 + n, 0], pos)
-            k = rot(x[s0:s0 + n, 1], pos)
-            v = x[s0:s0 + n, 2]
-            blk = bt[b, pos // bs]
-            kc[blk, :, pos % bs] = k.to(kc.dtype)
-            vc[blk, :, pos % bs] = v.to(vc.dtype)
-            o = _ops.flash_attention(q[None], k[None], v[None], causal=True, training=False)
-            out[s0:s0 + n] = o[0]
-        else:
-            dec_b.append((b, s0))
-    if dec_b:  # all decode sequences of the step together
-        bidx = torch.as_tensor([b for b, _ in dec_b], device=x.device)
-        toks = torch.as_tensor([s for _, s in dec_b], device=x.device)
-        steps = torch.as_tensor([int(dec[b]) for b, _ in dec_b], device=x.device)
-        q = rot(x[toks, 0], steps)
-        k = rot(x[toks, 1], steps)
-        v = x[toks, 2]
-        blk = bt[bidx, steps // bs]
-        kc[blk, :, steps % bs] = k.to(kc.dtype)
-        vc[blk, :, steps % bs] = v.to(vc.dtype)
-        L = max(int(dec[b]) for b, _ in dec_b) + 1
-        nblk = (L + bs - 1) // bs
-        # HIP flash-decoding kernel (ops.paged_decode_attention) streams each sequence's blocks
-        o = _ops.paged_decode_attention(q.to(kc.dtype), kc, vc, bt[bidx, :nblk], steps + 1, max_len=L)
-        out[toks] = o.to(out.dtype)
-    res = out.reshape(x.shape[0], H * D)
+    if rope is not None:  # [2, B|1, max_len, 1, D//2 | D] (cos, sin)
+        cos = rope[0].reshape(rope.shape[1], rope.shape[2], -1)
+        sin = rope[1].reshape(rope.shape[1], rope.shape[2], -1)
+        rb = bid % cos.shape[0]
+        cs, sn = cos[rb, pos], sin[rb, pos]
+        if cs.shape[-1] * 2 == D:
+            cs, sn = torch.cat([cs, cs], -1), torch.cat([sn, sn], -1)
+        q = _rotate_rows(q, cs, sn, bool(use_neox_style))
+        k = _rotate_rows(k, cs, sn, bool(use_neox_style))
+    bt = _t(block_tables).to(device=dev, dtype=torch.long)
+    blk = bt[bid, pos // bs]
+    kc[blk, :, pos % bs] = k.to(kc.dtype)
+    vc[blk, :, pos % bs] = v.to(vc.dtype)
+    host = lambda t: None if t is None else int(_t(t).reshape(-1)[0])  # noqa: E731  (CPU tensors: no sync)
+    max_enc, max_dec = host(max_enc_len_this_time), host(max_dec_len_this_time)
+    run_prefill = max_enc is None or max_enc > 0
+    run_decode = max_dec is None or max_dec > 0
+    prefill_tok = enc[bid] > 0
+    o = None
+    if run_prefill:
+        mq = max_enc if max_enc else T
+        o_p = _ops.attention.attention(q.to(kc.dtype), k.to(kc.dtype), v.to(kc.dtype), causal=True, cu_seqlens_q=cu,
+                                       cu_seqlens_k=cu, max_seqlen_q=mq, max_seqlen_k=mq, training=False)
+        o = o_p
+    if run_decode:
+        # prefill tokens ride along reading one position; their rows are replaced by o_p below
+        lens = torch.where(prefill_tok, torch.ones_like(pos), pos + 1) if run_prefill else pos + 1
+        ml = None
+        if max_dec is not None:
+            ml = max_dec + 1
+        o_d = _ops.paged_decode_attention(q.to(kc.dtype), kc, vc, bt[bid], lens, max_len=ml)
+        o = o_d if o is None else torch.where(prefill_tok.view(T, 1, 1), o, o_d)
+    res = o.to(q_all.dtype).reshape(T, H * D)
     if out_shift is not None:
         res = res + _t(out_shift)
     if out_smooth is not None:

@@ -45,6 +45,8 @@ class GPTConfig:
     tensor_parallel_degree: int = 1
     sequence_parallel: bool = False
     fuse_attention_qkv: bool = True
+    # LM head + CE over vocabulary slices (ops/lm_head.py): the [tokens, vocab] logits are never materialised
+    fused_head_ce: bool = False
 
     @staticmethod
     def gpt3_13b(**kw):
@@ -303,12 +305,20 @@ class GPTForPretraining(nn.Layer):
                                                          cfg.hidden_size],
                                                         default_initializer=I.Normal(0.0, cfg.initializer_range))
 
-    def forward(self, input_ids, position_ids=None):
+    def forward(self, input_ids, position_ids=None, labels=None, loss_mask=None, ignore_index=-100):
+        """Logits [B, S, V(_local)]; with ``labels``, the mean token loss instead (through the vocab-sliced
+        fused head + CE when config.fused_head_ce and no tensor parallelism, else logits + criterion)."""
         h = self.gpt(input_ids, position_ids)
         w = self.gpt.embeddings.word_embeddings.weight if self.config.tie_word_embeddings else self.lm_head_weight
         ht, wt = h._t, w._t
         if ht.dtype != wt.dtype:
             ht = ht.to(wt.dtype)
+        if labels is not None:
+            if self.config.fused_head_ce and self.config.tensor_parallel_degree <= 1:
+                per_tok = _ops.lm_head_cross_entropy(ht, wt, labels._t, ignore_index)
+                return _mean_loss(per_tok, labels._t, loss_mask, ignore_index)
+            logits = self.forward(input_ids, position_ids)
+            return GPTPretrainingCriterion(self.config, ignore_index)(logits, labels, loss_mask)
         if _use_sp(self.config):
             # token blocks -> vocab-parallel logits of all tokens: the token all-gather overlaps the GEMM of this
             # rank's own block, the backward's dX reduce-scatter overlaps the dW GEMM
@@ -334,8 +344,12 @@ class GPTPretrainingCriterion(nn.Layer):
             per_tok = _tp().parallel_cross_entropy_raw(lt, labels._t, self.ignore_index)
         else:
             per_tok = _ops.softmax_cross_entropy(lt, labels._t, self.ignore_index)
-        if loss_mask is not None:
-            m = loss_mask._t.reshape(per_tok.shape).float()
-            return _wrap((per_tok * m).sum() / m.sum().clamp_min(1.0))
-        valid = (labels._t != self.ignore_index).sum().clamp_min(1)
-        return _wrap(per_tok.sum() / valid)
+        return _mean_loss(per_tok, labels._t, loss_mask, self.ignore_index)
+
+
+def _mean_loss(per_tok, labels, loss_mask, ignore_index):
+    if loss_mask is not None:
+        m = loss_mask._t.reshape(per_tok.shape).float()
+        return _wrap((per_tok * m).sum() / m.sum().clamp_min(1.0))
+    valid = (labels != ignore_index).sum().clamp_min(1)
+    return _wrap(per_tok.sum() / valid)

@@ -1,0 +1,325 @@
+"""Serving ops against plain fp32 math: fused_multi_transformer (no cache / prefill into cache_kvs /
+decode at time_step, GQA, rotary, rmsnorm), variable_length_memory_efficient_attention (device-side
+length masking) and block_multihead_attention (mixed prefill + decode batch over a paged cache, with and
+without the host max-length hints). GPU tests run the bf16 HIP paths (varlen flash attention, paged /
+dense flash-decoding) and replay a captured decode step with new lengths.
+
+Reference semantics: python/paddle/incubate/nn/functional/fused_transformer.py:1015 (fused_multi_transformer),
+block_multihead_attention.py:33, variable_length_memory_efficient_attention.py:33."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import paddlepaddle_amd as paddle
+import paddlepaddle_amd.incubate.nn.functional as IF
+
+
+def _T(a, dev="cpu", dt=torch.float32):
+    return paddle.to_tensor(torch.as_tensor(a).to(dev, dt))
+
+
+# ------------------------------------------------------------------------------------ references
+def _rot(x, cos, sin):
+    """x [..., D] interleaved-pair rotation (use_neox_rotary_style=False)."""
+    x1, x2 = x[..., 0::2], x[..., 1::2]
+    r = torch.stack([-x2, x1], -1).flatten(-2)
+    return x * cos + r * sin
+
+
+def _ref_attention(q, k, v, mask):
+    """q [B,S,H,D], k/v [B,L,Hk,D] fp32; mask additive [B,1,S,L] or None."""
+    H, Hk = q.shape[2], k.shape[2]
+    k = k.repeat_interleave(H // Hk, 2)
+    v = v.repeat_interleave(H // Hk, 2)
+    s = torch.einsum("bshd,blhd->bhsl", q, k) / math.sqrt(q.shape[-1])
+    if mask is not None:
+        s = s + mask
+    return torch.einsum("bhsl,blhd->bshd", torch.softmax(s, -1), v)
+
+
+def _ref_stack(x, P, mask, H, Hk, rot=None, norm="layernorm", eps=1e-5):
+    """Pre-LN decoder stack over all positions of x [B,S,E] (fp32), relu FFN."""
+    B, S, E = x.shape
+    Dh = E // H
+
+    def nrm(t, w, b):
+        if norm == "rmsnorm":
+            return t * torch.rsqrt(t.pow(2).mean(-1, keepdim=True) + eps) * w
+        return torch.nn.functional.layer_norm(t, (E,), w, b, eps)
+    h = x
+    for p in P:
+        t = nrm(h, p["ln_s"], p["ln_b"])
+        qkv = t @ p["qkv_w"].reshape(-1, E).t() + p["qkv_b"].reshape(-1)
+        qkv = qkv.view(B, S, H + 2 * Hk, Dh)
+        q, k, v = qkv[:, :, :H], qkv[:, :, H:H + Hk], qkv[:, :, H + Hk:]
+        if rot is not None:
+            cos, sin = rot[0][:, :S][:, :, None], rot[1][:, :S][:, :, None]
+            q, k = _rot(q, cos, sin), _rot(k, cos, sin)
+        o = _ref_attention(q, k, v, mask).reshape(B, S, H * Dh)
+        h = h + o @ p["lin_w"] + p["lin_b"]
+        t = nrm(h, p["ffn_ln_s"], p["ffn_ln_b"])
+        h = h + torch.relu(t @ p["ffn1_w"] + p["ffn1_b"]) @ p["ffn2_w"] + p["ffn2_b"]
+    return h
+
+
+def _params(nl, E, H, Hk, F, gen, gqa):
+    P = []
+    for _ in range(nl):
+        heads = (H + 2 * Hk)
+        P.append({
+            "ln_s": 1 + 0.1 * torch.randn(E, generator=gen), "ln_b": 0.1 * torch.randn(E, generator=gen),
+            "qkv_w": torch.randn((heads, E // H, E) if gqa else (3, H, E // H, E), generator=gen) / math.sqrt(E),
+            "qkv_b": 0.1 * torch.randn((heads, E // H) if gqa else (3, H, E // H), generator=gen),
+            "lin_w": torch.randn(E, E, generator=gen) / math.sqrt(E), "lin_b": 0.1 * torch.randn(E, generator=gen),
+            "ffn_ln_s": 1 + 0.1 * torch.randn(E, generator=gen), "ffn_ln_b": 0.1 * torch.randn(E, generator=gen),
+            "ffn1_w": torch.randn(E, F, generator=gen) / math.sqrt(E), "ffn1_b": 0.1 * torch.randn(F, generator=gen),
+            "ffn2_w": torch.randn(F, E, generator=gen) / math.sqrt(F), "ffn2_b": 0.1 * torch.randn(E, generator=gen),
+        })
+    return P
+
+
+def _fmt(x, P, dev, dt, **kw):
+    g = lambda k: [_T(p[k], dev, dt) for p in P]  # noqa: E731
+    return IF.fused_multi_transformer(
+        x, g("ln_s"), g("ln_b"), g("qkv_w"), g("qkv_b"), g("lin_w"), g("lin_b"), g("ffn_ln_s"), g("ffn_ln_b"),
+        g("ffn1_w"), g("ffn1_b"), g("ffn2_w"), g("ffn2_b"), activation="relu", **kw)
+
+
+def _causal(B, S, L, off, dev):
+    keep = torch.arange(L, device=dev)[None] <= (torch.arange(S, device=dev)[:, None] + off)
+    return torch.zeros(B, 1, S, L, device=dev).masked_fill(~keep, float("-inf"))
+
+
+def _run_fmt_prefill_decode(dev, dt, E, H, Hk, norm="layernorm", rotary=False, tol=1e-4):
+    gen = torch.Generator().manual_seed(0)
+    B, S, steps, Lmax, F = 2, 5, 3, 16, 2 * E
+    gqa = Hk != H
+    P = _params(2, E, H, Hk, F, gen, gqa)
+    xs = torch.randn(B, S + steps, E, generator=gen)
+    Dh = E // H
+    rot = None
+    kw = {}
+    if rotary:
+        pos = torch.arange(Lmax)[:, None].float()
+        inv = 1.0 / (10000 ** (torch.arange(0, Dh, 2).float() / Dh))
+        ang = (pos * inv).repeat_interleave(2, -1)  # interleaved pairs share an angle
+        rot = (ang.cos()[None].expand(B, -1, -1), ang.sin()[None].expand(B, -1, -1))
+        kw = dict(rotary_embs=_T(torch.stack([rot[0], rot[1]])[:, :, None], dev, torch.float32), rotary_emb_dims=1)
+    if gqa:
+        kw["gqa_group_size"] = Hk
+    full = _ref_stack(xs, P, _causal(B, S + steps, S + steps, 0, "cpu"), H, Hk, rot, norm)
+    caches = [paddle.to_tensor(torch.zeros(2, B, Hk, Lmax, Dh, device=dev, dtype=dt)) for _ in P]
+    out, caches = _fmt(_T(xs[:, :S], dev, dt), P, dev, dt, cache_kvs=caches,
+                       attn_mask=_T(_causal(B, S, S, 0, "cpu"), dev, dt), norm_type=norm, **kw)
+    got = out._t.float().cpu()
+    np.testing.assert_allclose(got.numpy(), full[:, :S].numpy(), rtol=tol, atol=tol)
+    for t in range(steps):
+        step = S + t
+        out, caches = _fmt(_T(xs[:, step:step + 1], dev, dt), P, dev, dt, cache_kvs=caches,
+                           time_step=paddle.to_tensor(np.array([step], "int32")), norm_type=norm, **kw)
+        np.testing.assert_allclose(out._t.float().cpu().numpy(), full[:, step:step + 1].numpy(), rtol=tol,
+                                   atol=tol)
+
+
+def test_fused_multi_transformer_no_cache_matches_math():
+    gen = torch.Generator().manual_seed(1)
+    B, S, E, H = 2, 6, 32, 4
+    P = _params(2, E, H, H, 64, gen, False)
+    x = torch.randn(B, S, E, generator=gen)
+    mask = torch.randn(B, 1, S, S, generator=gen)
+    out = _fmt(_T(x), P, "cpu", torch.float32, attn_mask=_T(mask))
+    np.testing.assert_allclose(out.numpy(), _ref_stack(x, P, mask, H, H).numpy(), rtol=1e-4, atol=1e-4)
+
+
+def test_fused_multi_transformer_prefill_then_decode_cpu():
+    _run_fmt_prefill_decode("cpu", torch.float32, 32, 4, 4)
+
+
+def test_fused_multi_transformer_gqa_rotary_rmsnorm_cpu():
+    _run_fmt_prefill_decode("cpu", torch.float32, 32, 4, 2, norm="rmsnorm", rotary=True)
+
+
+def test_fused_multi_transformer_layer_returns_caches():
+    m = paddle.incubate.nn.FusedMultiTransformer(32, 4, 64, num_layers=2)
+    m.eval()
+    x = paddle.randn([2, 3, 32])
+    caches = [paddle.zeros([2, 2, 4, 8, 8]) for _ in range(2)]
+    out, c2 = m(x, caches=caches)
+    assert out.shape == [2, 3, 32] and c2 is caches
+    assert float(caches[0]._t[:, :, :, :3].abs().sum()) > 0 and float(caches[0]._t[:, :, :, 3:].abs().sum()) == 0
+
+
+def _ref_varlen(q, k, v, sl, kl, mask, causal, pre):
+    B, H, Sq, D = q.shape
+    out = torch.zeros_like(q)
+    for b in range(B):
+        n, nk = int(sl[b]), int(kl[b]) + pre
+        if n == 0:
+            continue
+        s = torch.einsum("hqd,hkd->hqk", q[b, :, :n], k[b, :, :nk]) / math.sqrt(D)
+        if mask is not None:
+            s = s + mask[b, :, :n, :nk]
+        if causal:
+            keep = torch.arange(nk)[None] <= torch.arange(n)[:, None] + pre
+            s = s.masked_fill(~keep, float("-inf"))
+        out[b, :, :n] = torch.einsum("hqk,hkd->hqd", torch.softmax(s, -1), v[b, :, :nk])
+    return out
+
+
+@pytest.mark.parametrize("causal,with_mask,pre", [(False, False, 0), (True, False, 0), (True, True, 2)])
+def test_variable_length_attention_cpu(causal, with_mask, pre):
+    gen = torch.Generator().manual_seed(2)
+    B, H, S, D = 3, 2, 7, 16
+    q, k, v = (torch.randn(B, H, S, D, generator=gen) for _ in range(3))
+    sl, kl = torch.tensor([7, 4, 1]), torch.tensor([5, 4, 1])
+    mask = torch.randn(B, 1, S, S, generator=gen) if with_mask else None
+    out = IF.variable_length_memory_efficient_attention(
+        _T(q), _T(k), _T(v), _T(sl, dt=torch.int32), _T(kl, dt=torch.int32),
+        mask=None if mask is None else _T(mask), causal=causal, pre_cache_length=pre)
+    np.testing.assert_allclose(out.numpy(), _ref_varlen(q, k, v, sl, kl, mask, causal, pre).numpy(),
+                               rtol=1e-4, atol=1e-5)
+
+
+def _blha_case(dev, dt, H, Hk, D, hints):
+    """Step 1: sequences 0 and 1 prefill (5 and 3 tokens). Step 2 (mixed): sequence 0 decodes one token,
+    sequence 1 decodes one token, sequence 2 prefills 4 tokens. Every output row is checked against
+    causal attention over that sequence's whole history."""
+    gen = torch.Generator().manual_seed(3)
+    bs, nblocks = 4, 12
+    kc = torch.zeros(nblocks, Hk, bs, D, device=dev, dtype=dt)
+    vc = torch.zeros_like(kc)
+    tables = torch.tensor([[0, 1, 2], [3, 4, 5], [6, 7, 8]], dtype=torch.int32)
+    W = (H + 2 * Hk) * D
+    hist = {0: [], 1: [], 2: []}
+
+    def call(per_seq):  # per_seq: [(enc, dec, tokens [n, W])]
+        toks = torch.cat([t for _, _, t in per_seq])
+        lens = [t.shape[0] for _, _, t in per_seq]
+        cu = torch.tensor(np.concatenate([[0], np.cumsum(lens)]), dtype=torch.int32)
+        enc = torch.tensor([e for e, _, _ in per_seq], dtype=torch.int32)
+        dec = torch.tensor([d for _, d, _ in per_seq], dtype=torch.int32)
+        extra = {}
+        if hints:
+            extra = dict(max_enc_len_this_time=paddle.to_tensor(np.array([int(enc.max())], "int32")),
+                         max_dec_len_this_time=paddle.to_tensor(np.array([int(dec.max())], "int32")))
+        out, _, _, _ = IF.block_multihead_attention(
+            _T(toks, dev, dt), paddle.to_tensor(kc), paddle.to_tensor(vc), _T(enc, dev, torch.int32),
+            _T(dec, dev, torch.int32), _T(torch.tensor(lens), dev, torch.int32), None, None,
+            _T(cu, dev, torch.int32), _T(cu, dev, torch.int32), _T(tables[:len(per_seq)], dev, torch.int32),
+            block_size=bs, **extra)
+        return out._t.float().cpu()
+
+    def check(out, per_seq, tol):
+        r = 0
+        for b, (_, _, t) in enumerate(per_seq):
+            hist[b].append(t)
+            full = torch.cat(hist[b]).view(-1, H + 2 * Hk, D).float()
+            n = t.shape[0]
+            q, k, v = full[-n:, :H][None], full[:, H:H + Hk][None], full[:, H + Hk:][None]
+            Ltot = full.shape[0]
+            ref = _ref_attention(q, k, v, _causal(1, n, Ltot, Ltot - n, "cpu"))[0].reshape(n, H * D)
+            np.testing.assert_allclose(out[r:r + n].numpy(), ref.numpy(), rtol=tol, atol=tol)
+            r += n
+
+    tol = 1e-4 if dt == torch.float32 else 3e-2
+    rnd = lambda n: (torch.randn(n, W, generator=gen) * 0.5).to(dt).float()  # noqa: E731
+    s1 = [(5, 0, rnd(5)), (3, 0, rnd(3))]
+    check(call(s1), s1, tol)
+    s2 = [(0, 5, rnd(1)), (0, 3, rnd(1)), (4, 0, rnd(4))]
+    check(call(s2), s2, tol)
+    return kc
+
+
+@pytest.mark.parametrize("hints", [False, True])
+def test_block_mha_mixed_prefill_decode_cpu(hints):
+    _blha_case("cpu", torch.float32, 4, 2, 16, hints)
+
+
+def test_block_mha_rejects_unsupported_args():
+    z = paddle.zeros([1], dtype="int32")
+    with pytest.raises(NotImplementedError):
+        IF.block_multihead_attention(paddle.zeros([1, 48]), paddle.zeros([2, 1, 4, 16]), paddle.zeros([2, 1, 4, 16]),
+                                     z, z, z + 1, None, None, paddle.to_tensor(np.array([0, 1], "int32")),
+                                     paddle.to_tensor(np.array([0, 1], "int32")), paddle.zeros([1, 2], "int32"),
+                                     cache_k_quant_scales=paddle.ones([1]))
+
+
+# ------------------------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+def test_fused_multi_transformer_prefill_decode_gpu_bf16():
+    _run_fmt_prefill_decode("cuda", torch.bfloat16, 256, 2, 2, tol=6e-2)
+    _run_fmt_prefill_decode("cuda", torch.bfloat16, 512, 4, 2, norm="rmsnorm", rotary=True, tol=6e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hints", [False, True])
+def test_block_mha_mixed_prefill_decode_gpu_bf16(hints):
+    _blha_case("cuda", torch.bfloat16, 8, 2, 128, hints)
+
+
+@pytest.mark.gpu
+def test_variable_length_attention_gpu_bf16():
+    gen = torch.Generator().manual_seed(4)
+    B, H, S, D = 3, 4, 96, 128
+    q, k, v = ((torch.randn(B, H, S, D, generator=gen) * 0.5).bfloat16().float() for _ in range(3))
+    sl, kl = torch.tensor([96, 40, 1]), torch.tensor([80, 40, 3])
+    out = IF.variable_length_memory_efficient_attention(
+        _T(q, "cuda", torch.bfloat16), _T(k, "cuda", torch.bfloat16), _T(v, "cuda", torch.bfloat16),
+        _T(sl, "cuda", torch.int32), _T(kl, "cuda", torch.int32), causal=True)
+    ref = _ref_varlen(q, k, v, sl, kl, None, True, 0)
+    np.testing.assert_allclose(out._t.float().cpu().numpy(), ref.numpy(), rtol=3e-2, atol=3e-2)
+
+
+@pytest.mark.gpu
+def test_block_mha_decode_step_graph_replay_gpu():
+    """One decode step of 4 sequences captured once, replayed at three later steps with new tokens and
+    lengths written into the captured input buffers; each replay matches the fp32 reference."""
+    H, Hk, D, bs, B = 8, 2, 128, 64, 4
+    W = (H + 2 * Hk) * D
+    gen = torch.Generator().manual_seed(5)
+    dev = "cuda"
+    nblk = 4
+    kc = torch.zeros(B * nblk, Hk, bs, D, device=dev, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    tables = torch.arange(B * nblk, dtype=torch.int32, device=dev).view(B, nblk)
+    prompt = [37, 64, 5, 100]
+    hist = [(torch.randn(n, W, generator=gen) * 0.5).bfloat16().float() for n in prompt]
+    for b in range(B):  # prompts straight into the cache
+        full = hist[b].view(-1, H + 2 * Hk, D)
+        for p in range(prompt[b]):
+            kc[tables[b, p // bs], :, p % bs] = full[p, H:H + Hk].to(dev, torch.bfloat16)
+            vc[tables[b, p // bs], :, p % bs] = full[p, H + Hk:].to(dev, torch.bfloat16)
+    x = torch.zeros(B, W, device=dev, dtype=torch.bfloat16)
+    dec = torch.tensor(prompt, dtype=torch.int32, device=dev)
+    zeros = torch.zeros(B, dtype=torch.int32, device=dev)
+    ones = torch.ones(B, dtype=torch.int32, device=dev)
+    cu = torch.arange(B + 1, dtype=torch.int32, device=dev)
+    hint_e = paddle.to_tensor(np.array([0], "int32"))
+    hint_d = paddle.to_tensor(np.array([nblk * bs - 1], "int32"))
+    P = lambda t: paddle.to_tensor(t)  # noqa: E731
+
+    def step():
+        return IF.block_multihead_attention(P(x), P(kc), P(vc), P(zeros), P(dec), P(ones), None, None, P(cu), P(cu),
+                                            P(tables), block_size=bs, max_enc_len_this_time=hint_e,
+                                            max_dec_len_this_time=hint_d)[0]._t
+    step()  # warm-up (lazy init) writes a throw-away token at the prompt position, overwritten below
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = step()
+    for _ in range(3):
+        new = (torch.randn(B, W, generator=gen) * 0.5).bfloat16().float()
+        x.copy_(new.to(dev, torch.bfloat16))
+        g.replay()
+        torch.cuda.synchronize()
+        got = out.float().cpu()
+        for b in range(B):
+            hist[b] = torch.cat([hist[b], new[b:b + 1]])
+            full = hist[b].view(-1, H + 2 * Hk, D)
+            Ltot = full.shape[0]
+            ref = _ref_attention(full[-1:, :H][None], full[:, H:H + Hk][None], full[:, H + Hk:][None], None)
+            np.testing.assert_allclose(got[b].numpy(), ref[0, 0].reshape(-1).numpy(), rtol=3e-2, atol=3e-2)
+            assert Ltot == int(dec[b]) + 1
+        dec += 1
