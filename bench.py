@@ -45,6 +45,9 @@ def parse():
     p.add_argument("--tp", type=int, default=None,
                    help="tensor-parallel degree (GPT: sharding over world/tp ranks). Default: the BASELINE config "
                         "'GPT-3 13B sharding stage-3 + TP=2' -> 2 on any multi-GPU run of GPT, 1 on one GPU")
+    p.add_argument("--llama-engine", default="static", choices=["static", "fleet"],
+                   help="LLaMA: static-graph auto-parallel (dist.parallelize + dist.to_static, the BASELINE config) "
+                        "or the dygraph fleet pipeline")
     p.add_argument("--fused-head-ce", type=int, default=0,
                    help="LM head + cross-entropy over vocabulary slices, logits never materialised (ops/lm_head.py)")
     p.add_argument("--sp", type=int, default=1,
@@ -195,6 +198,65 @@ def gpt_bench(args, paddle, world, dist_on):
         paddle.device.cuda.empty_cache()
     gpt_bench.keep_params = keep
     return tps, dt / args.steps * 1000, B * args.accum * n_shard, mfu
+
+
+LLAMA_TP_PLAN = {
+    "layers.*.self_attn.q_proj": "col", "layers.*.self_attn.k_proj": "col", "layers.*.self_attn.v_proj": "col",
+    "layers.*.self_attn.o_proj": "row", "layers.*.mlp.gate_proj": "col", "layers.*.mlp.up_proj": "col",
+    "layers.*.mlp.down_proj": "row", "lm_head": "col"}
+
+
+def llama_static_bench(args, paddle, world, dist_on):
+    """LLaMA-2 pre-training the BASELINE way: static-graph semi-auto parallel. A plain single-card LLaMA is
+    distributed by plan (dist.parallelize: pipeline split over the decoder layers, ColWise / RowWise tensor
+    parallel), then dist.to_static traces it once, propagates placements, partitions the program per rank
+    (explicit RCCL collectives + stage-to-stage p2p) and runs a 1F1B schedule over the micro-batches;
+    bf16 weights, AdamW with fp32 master weights."""
+    import numpy as np
+    import paddlepaddle_amd.distributed as dist
+    from paddlepaddle_amd.models.llama_auto import LlamaConfig, LlamaForCausalLMAuto, LlamaPretrainingCriterionAuto
+    pp, tp = args.pp, args.tp
+    if world % (pp * tp):
+        raise SystemExit(f"world {world} is not a multiple of pp*tp = {pp * tp}")
+    dp = world // (pp * tp)
+    presets = {"llama2-70b": LlamaConfig.llama2_70b, "llama2-13b": LlamaConfig.llama2_13b,
+               "llama2-7b": LlamaConfig.llama2_7b, "llama-tiny": LlamaConfig.tiny}
+    extra = {"num_hidden_layers": max(2, 2 * pp)} if args.model == "llama-tiny" else {}
+    cfg = presets[args.model](max_position_embeddings=max(args.seq_len, 128), **extra)
+    dist.auto_parallel.set_mesh(None)
+    paddle.set_default_dtype("bfloat16")
+    paddle.seed(1234)
+    model, crit = LlamaForCausalLMAuto(cfg), LlamaPretrainingCriterionAuto(cfg)
+    paddle.set_default_dtype("float32")
+    opt = paddle.optimizer.AdamW(learning_rate=1e-4, parameters=model.parameters(), weight_decay=0.01,
+                                 multi_precision=True, grad_clip=paddle.nn.ClipGradByGlobalNorm(1.0))
+    mesh = dist.ProcessMesh(np.arange(world).reshape(pp, dp, tp), dim_names=["pp", "dp", "mp"])
+    plan = {k: (dist.ColWiseParallel() if v == "col" else dist.RowWiseParallel()) for k, v in LLAMA_TP_PLAN.items()}
+    model, opt = dist.parallelize(model, opt, mesh, dp_config={"sharding_level": 0},
+                                  mp_config={"parallelize_plan": plan}, pp_config={"split_spec": "layers"})
+    strategy = dist.Strategy()
+    strategy.pipeline.enable = True
+    strategy.pipeline.schedule_mode = "1F1B"
+    strategy.pipeline.accumulate_steps = args.accum
+    strategy.pipeline.micro_batch_size = args.micro_batch
+    dm = dist.to_static(model, None, crit, opt, strategy)
+    dev = _dev()
+    gb = args.micro_batch * args.accum * dp
+    gen = torch.Generator(device=dev).manual_seed(7)
+    data = torch.randint(0, cfg.vocab_size, (gb, args.seq_len + 1), device=dev, generator=gen)
+    x, y = paddle.Tensor(data[:, :-1].contiguous()), paddle.Tensor(data[:, 1:].contiguous())
+    state = {}
+
+    def step():
+        state["loss"] = dm(x, y)
+
+    dt = timed(step, args.steps, args.warmup, dist_on)
+    tokens = args.steps * gb * args.seq_len
+    tps = tokens / dt
+    mfu = tps * cfg.flops_per_token(args.seq_len) / (PEAK_BF16 * world)
+    log(f"[llama-static] {args.model} pp{pp} tp{tp} dp{dp}: loss={float(state['loss']):.4f} "
+        f"step={dt / args.steps * 1000:.1f}ms tokens/s={tps:.0f} MFU={mfu * 100:.1f}%")
+    return tps, dt / args.steps * 1000, gb, mfu
 
 
 def llama_bench(args, paddle, world, dist_on):
@@ -352,7 +414,8 @@ def main():
     tps = step_ms = gb = mfu = None
     is_llama = args.model.startswith("llama")
     if is_llama:
-        tps, step_ms, gb, mfu = llama_bench(args, paddle, world, dist_on)
+        fn = llama_static_bench if args.llama_engine == "static" else llama_bench
+        tps, step_ms, gb, mfu = fn(args, paddle, world, dist_on)
         args.resnet = 0
     elif not args.skip_gpt:
         tps, step_ms, gb, mfu = gpt_bench(args, paddle, world, dist_on)
@@ -363,6 +426,8 @@ def main():
               (f"_tp{args.tp}" if args.tp > 1 else "") + ("_sp" if (args.tp > 1 and args.sp) else "")
         if is_llama:
             par = f"pp{args.pp}_tp{args.tp}_dp{world // (args.pp * args.tp)}" + (f"_vpp{args.vpp}" if args.vpp > 1 else "")
+            if args.llama_engine == "static":
+                par += "_static_auto_parallel"
         metric = BASELINE_METRIC if args.model == "gpt3-13b" else \
             f"tokens/sec {args.model} training ({par})"
         line = {

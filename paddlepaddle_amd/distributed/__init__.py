@@ -10,6 +10,10 @@ from .auto_parallel import (ProcessMesh, Shard, Replicate, Partial, Placement, R
                             shard_optimizer, shard_scaler, ShardingStage1, ShardingStage2, ShardingStage3,
                             shard_dataloader, Strategy, DistModel, to_static, get_mesh, set_mesh)
 from . import auto_parallel  # noqa: F401
+from .auto_parallel.intermediate import (parallelize, ColWiseParallel, RowWiseParallel,  # noqa: F401,E402
+                                         PrepareLayerInput, PrepareLayerOutput, SequenceParallelBegin,
+                                         SequenceParallelEnd, SequenceParallelEnable, SequenceParallelDisable,
+                                         SplitPoint)
 from ..parallel.data_parallel import DataParallel  # noqa: F401,E402
 from .extras import *  # noqa: F401,F403,E402
 from .watchdog import enable_comm_watchdog, disable_comm_watchdog  # noqa: F401,E402

@@ -5,3 +5,6 @@ from .api import (shard_tensor, dtensor_from_local, dtensor_to_local, dtensor_fr
                   unshard_dtensor, shard_layer, shard_optimizer, shard_scaler, ShardingStage1, ShardingStage2,
                   ShardingStage3, shard_dataloader, ShardDataloader, Strategy, DistModel, to_static,
                   in_auto_parallel_align_mode)
+from .intermediate import (parallelize, parallelize_model, parallelize_optimizer, ColWiseParallel,  # noqa: F401,E402
+                           RowWiseParallel, PrepareLayerInput, PrepareLayerOutput, SequenceParallelBegin,
+                           SequenceParallelEnd, SequenceParallelEnable, SequenceParallelDisable, SplitPoint)

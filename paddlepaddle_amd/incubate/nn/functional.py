@@ -570,7 +570,13 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
     blk = bt[bid, pos // bs]
     kc[blk, :, pos % bs] = k.to(kc.dtype)
     vc[blk, :, pos % bs] = v.to(vc.dtype)
-    host = lambda t: None if t is None else int(_t(t).reshape(-1)[0])  # noqa: E731  (CPU tensors: no sync)
+    def host(t):  # the hints are host tensors (blha_get_max_len on CPU): reading them never syncs the device
+        if t is None:
+            return None
+        tt = _t(t)
+        if tt.is_cuda and torch.cuda.is_current_stream_capturing():
+            return None  # a device-resident hint cannot be read inside a captured graph: run both phases
+        return int(tt.reshape(-1)[0])
     max_enc, max_dec = host(max_enc_len_this_time), host(max_dec_len_this_time)
     run_prefill = max_enc is None or max_enc > 0
     run_decode = max_dec is None or max_dec > 0

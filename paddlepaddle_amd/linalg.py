@@ -10,32 +10,26 @@ from .tensor.manipulation import matrix_transpose  # noqa: F401
 
 def fp8_fp8_half_gemm_fused(x, y, transpose_x=False, transpose_y=False, bias=None, scale=1.0,
                             output_dtype="float16", act="identity", name=None):
-    """out = act(scale * op(x) @ op(y) + bias) for OCP fp8 (e4m3fn / e5m2) x, y and a half-precision
-    output (reference: python/paddle/tensor/linalg.py fp8_fp8_half_gemm_fused). On the HIP device the
-    product runs as a scaled fp8 GEMM (hipBLASLt fp8 MFMA through torch._scaled_mm) when available, else
-    as an fp32-accumulated dequantised GEMM."""
+    """out = act(scale * op(x) @ op(y) + bias) for OCP fp8 (e4m3fn / e5m2) x, y and an fp16 / bf16 output
+    (reference: python/paddle/tensor/linalg.py fp8_fp8_half_gemm_fused). On the device it is the
+    hand-written block-scaled-MFMA fp8 GEMM of csrc/kernels/gemm_fp8.hip (ops/fp8.py): both operands are
+    fed K-major, so transpose_y=True (weight stored [N, K]) needs no copy; leading batch dims of x fold
+    into M when y is 2-D, and batched y runs per batch."""
     import torch as _torch
     from .framework.tensor import _wrap as _w
+    from .ops.fp8 import gemm_fp8
+    odt = {"float16": _torch.float16, "bfloat16": _torch.bfloat16}.get(str(output_dtype))
+    if odt is None:
+        raise ValueError("The output_dtype must be float16 or bfloat16")
     a, b = x._t, y._t
     if transpose_x:
         a = a.transpose(-1, -2)
-    if transpose_y:
-        b = b.transpose(-1, -2)
-    odt = {"float16": _torch.float16, "bfloat16": _torch.bfloat16}[str(output_dtype)]
-    out = None
-    if a.is_cuda and a.dim() == 2 and hasattr(_torch, "_scaled_mm"):
-        try:
-            one = _torch.ones((), device=a.device)
-            out = _torch._scaled_mm(a.contiguous(), b.t().contiguous().t(), scale_a=one * float(scale),
-                                    scale_b=one, out_dtype=odt)
-        except (RuntimeError, TypeError):
-            out = None
-    if out is None:
-        out = (float(scale) * _torch.matmul(a.float(), b.float())).to(odt)
-    if bias is not None:
-        out = out + bias._t.to(odt)
-    if act in ("gelu",):
-        out = _torch.nn.functional.gelu(out.float(), approximate="tanh").to(odt)
-    elif act == "relu":
-        out = _torch.relu(out)
-    return _w(out)
+    b_nk = b if transpose_y else b.transpose(-1, -2)  # [.., N, K]
+    bt = None if bias is None else bias._t
+    if b_nk.dim() == 2:
+        lead = a.shape[:-1]
+        a2 = a.reshape(-1, a.shape[-1])
+        out = gemm_fp8(a2, b_nk, bt, float(scale), act, odt)
+        return _w(out.view(*lead, out.shape[-1]))
+    outs = [gemm_fp8(a[i], b_nk[i], bt, float(scale), act, odt) for i in range(b_nk.shape[0])]
+    return _w(_torch.stack(outs))

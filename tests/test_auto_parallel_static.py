@@ -53,6 +53,41 @@ def _worker(rank, world, port, shape, acc, schedule, q):
     paddle.distributed.barrier()
 
 
+LLAMA_PLAN = {
+    "layers.*.self_attn.q_proj": "col", "layers.*.self_attn.k_proj": "col", "layers.*.self_attn.v_proj": "col",
+    "layers.*.self_attn.o_proj": "row", "layers.*.mlp.gate_proj": "col", "layers.*.mlp.up_proj": "col",
+    "layers.*.mlp.down_proj": "row", "lm_head": "col"}
+
+
+def _worker_parallelize(rank, world, port, shape, acc, q):
+    """Plain single-card LLaMA built without a mesh, then distributed by dist.parallelize plans."""
+    paddle = _setup(rank, world, port)
+    import paddlepaddle_amd.distributed as dist
+    from paddlepaddle_amd.models.llama_auto import LlamaForCausalLMAuto, LlamaPretrainingCriterionAuto
+    pp, dp, mp = shape
+    dist.auto_parallel.set_mesh(None)
+    paddle.seed(4)
+    cfg = _cfg()
+    model, crit = LlamaForCausalLMAuto(cfg), LlamaPretrainingCriterionAuto(cfg)
+    opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    mesh = dist.ProcessMesh(np.arange(pp * dp * mp).reshape(pp, dp, mp), dim_names=["pp", "dp", "mp"])
+    plan = {k: (dist.ColWiseParallel() if v == "col" else dist.RowWiseParallel()) for k, v in LLAMA_PLAN.items()}
+    model, opt = dist.parallelize(model, opt, mesh, dp_config={"sharding_level": 0},
+                                  mp_config={"parallelize_plan": plan}, pp_config={"split_spec": "layers"})
+    strategy = dist.Strategy()
+    strategy.pipeline.enable = pp > 1 or acc > 1
+    strategy.pipeline.accumulate_steps = acc
+    dm = dist.to_static(model, None, crit, opt, strategy)
+    assert dm._engine is not None
+    ids = _data()
+    losses = [float(dm(paddle.Tensor(ids[:, :-1]), paddle.Tensor(ids[:, 1:]))) for _ in range(STEPS)]
+    eng = dm._engine
+    kinds = sorted({n.name for nodes in eng.stage_nodes for n in nodes if n.name in (
+        "allreduce", "allgather", "slice", "copy_to_parallel")})
+    q.put((rank, losses, kinds, eng.my_stage))
+    paddle.distributed.barrier()
+
+
 def _reference():
     sys.path.insert(0, ROOT)
     os.environ["PADDLE_AMD_FORCE_CPU"] = "1"
@@ -89,3 +124,17 @@ def test_static_auto_parallel_llama_matches_single_process(shape, acc, schedule)
         np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-5, err_msg=f"rank {rank} stage {stage}")
         if shape[2] > 1:
             assert "allreduce" in kinds and "copy_to_parallel" in kinds
+
+
+@pytest.mark.parametrize("shape,acc", [((1, 1, 2), 1), ((4, 1, 2), 4)])
+def test_parallelize_plan_llama_matches_single_process(shape, acc):
+    """dist.parallelize (pipeline split_spec + ColWise / RowWise plan) then dist.to_static: same losses as
+    single-process training; at PP4 x TP2 every stage holds its own layers."""
+    ref = _reference()
+    res = _spawn(_worker_parallelize, shape, acc, world=int(np.prod(shape)))
+    stages = set()
+    for rank, losses, kinds, stage in res:
+        np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-5, err_msg=f"rank {rank} stage {stage}")
+        assert "allreduce" in kinds and "copy_to_parallel" in kinds
+        stages.add(stage)
+    assert stages == set(range(shape[0]))

@@ -41,13 +41,32 @@ def test_bench_llama_pipeline_x_tp_four_ranks():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr",
            "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "4", "--model",
            "llama-tiny", "--pp", "2", "--tp", "2", "--steps", "2", "--warmup", "1", "--seq-len", "32",
-           "--micro-batch", "1", "--accum", "4"]
+           "--micro-batch", "1", "--accum", "4", "--llama-engine", "fleet"]
     r = subprocess.run(cmd, env=env, capture_output=True, timeout=600, cwd="/tmp")
     assert r.returncode == 0, r.stderr.decode()[-3000:]
     lines = [l for l in r.stdout.decode().splitlines() if l.startswith("{")]
     assert len(lines) == 1
     d = json.loads(lines[0])
     assert d["n_gpus"] == 4 and d["value"] > 0 and d["config"]["parallelism"] == "pp2_tp2_dp1"
+
+
+def test_bench_llama_static_auto_parallel_pp4_tp2_eight_ranks():
+    """The BASELINE LLaMA-2 layout (PP4 x TP2, static-graph auto-parallel) on 8 gloo ranks: `bench.py --model
+    llama-tiny --pp 4 --tp 2` distributes a plain LLaMA with dist.parallelize and trains it through
+    dist.to_static (traced program, per-rank partition, 1F1B)."""
+    env = dict(os.environ, PADDLE_AMD_FORCE_CPU="1", PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "8", "--model",
+           "llama-tiny", "--pp", "4", "--tp", "2", "--steps", "2", "--warmup", "1", "--seq-len", "32",
+           "--micro-batch", "1", "--accum", "4"]
+    r = subprocess.run(cmd, env=env, capture_output=True, timeout=900, cwd="/tmp")
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    lines = [l for l in r.stdout.decode().splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["value"] > 0
+    assert d["config"]["parallelism"] == "pp4_tp2_dp1_static_auto_parallel"
+    assert "[llama-static]" in r.stderr.decode() + r.stdout.decode()
 
 
 def test_bench_self_launch_sharding_x_tp_four_ranks():

@@ -202,8 +202,10 @@ def _blha_case(dev, dt, H, Hk, D, hints):
         dec = torch.tensor([d for _, d, _ in per_seq], dtype=torch.int32)
         extra = {}
         if hints:
-            extra = dict(max_enc_len_this_time=paddle.to_tensor(np.array([int(enc.max())], "int32")),
-                         max_dec_len_this_time=paddle.to_tensor(np.array([int(dec.max())], "int32")))
+            extra = dict(max_enc_len_this_time=paddle.to_tensor(np.array([int(enc.max())], "int32"),
+                                                                place=paddle.CPUPlace()),
+                         max_dec_len_this_time=paddle.to_tensor(np.array([int(dec.max())], "int32"),
+                                                                place=paddle.CPUPlace()))
         out, _, _, _ = IF.block_multihead_attention(
             _T(toks, dev, dt), paddle.to_tensor(kc), paddle.to_tensor(vc), _T(enc, dev, torch.int32),
             _T(dec, dev, torch.int32), _T(torch.tensor(lens), dev, torch.int32), None, None,
@@ -296,8 +298,8 @@ def test_block_mha_decode_step_graph_replay_gpu():
     zeros = torch.zeros(B, dtype=torch.int32, device=dev)
     ones = torch.ones(B, dtype=torch.int32, device=dev)
     cu = torch.arange(B + 1, dtype=torch.int32, device=dev)
-    hint_e = paddle.to_tensor(np.array([0], "int32"))
-    hint_d = paddle.to_tensor(np.array([nblk * bs - 1], "int32"))
+    hint_e = paddle.to_tensor(np.array([0], "int32"), place=paddle.CPUPlace())  # host hints, as blha_get_max_len
+    hint_d = paddle.to_tensor(np.array([nblk * bs - 1], "int32"), place=paddle.CPUPlace())
     P = lambda t: paddle.to_tensor(t)  # noqa: E731
 
     def step():
