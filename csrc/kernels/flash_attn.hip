@@ -3,6 +3,7 @@
 #include "flash_attn_kernels.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 // heads per dispatch group for block_map: all of an XCD's heads at once (global heaviest-first) while that
 // is at most 512 workgroups per XCD, else groups that keep ~`inflight` workgroups (2 per CU forward, 1
@@ -136,6 +137,8 @@ PA_EXPORT int pa_flash_attn_bwd_ex(const void* q, const void* k, const void* v, 
     a.qs[i] = qs[i]; a.ks[i] = ks[i]; a.vs[i] = vs[i]; a.dos[i] = dos[i]; a.dks[i] = dks[i]; a.dvs[i] = dvs[i];
   }
   a.scale = scale; a.scale_log2 = scale * kLog2e; a.inv_scale = 1.f / scale; a.causal = causal;
+  const char* abl_env = getenv("PA_FA_BWD_ABL");  // measurement ablations only (tools/bench_fa_bwd_abl.py)
+  a.abl = abl_env ? atoi(abl_env) : 0;
   const int BK = D == 256 ? 64 : 128;
   const int nkb = (Sk + BK - 1) / BK;
   a.grp = fa_group(B * Hk, nkb, 32);

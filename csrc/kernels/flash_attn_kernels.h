@@ -589,6 +589,7 @@ struct BwdArgs {
   const int* fm_stats; int64_t fmst[2];
   int dropout; uint32_t keep16; float rkeep; uint32_t seed0, seed1;
   int64_t lse_s[2];
+  int abl;  // measurement ablations (0 in normal runs): 1 dQ atomics dropped, 2 dQ step skipped, 4 dK/dV GEMMs skipped
 };
 
 // delta[b,h,q] = sum_d dO * O   (delta / lse index = b * lse_s0 + h * lse_s1 + q)
@@ -819,7 +820,7 @@ __global__ __launch_bounds__(NW * 64, 1) void fa_bwd_kernel(BwdArgs p) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int qr = (i & 3) + 8 * (i >> 2) + 4 * hf;
-        const int off = (qb0 + qr < Sq) ? base + qr * rs : 0x7ffffff0;
+        const int off = (qb0 + qr < Sq && !(p.abl & 1)) ? base + qr * rs : 0x7ffffff0;
         __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(qacc[i] * p.scale, dq_rsrc, off, 0, 0);
       }
     }
@@ -878,7 +879,7 @@ __global__ __launch_bounds__(NW * 64, 1) void fa_bwd_kernel(BwdArgs p) {
       lds_barrier();
       if (kMask) mask_load(h, q0);
       if (it + 1 < n_qb) prefetch(h, q0 + BM);
-      if (it > 0) dq_step(ds_lds + (((it - 1) & 1) * DST_BYTES), h, q0 - BM);
+      if (it > 0 && !(p.abl & 2)) dq_step(ds_lds + (((it - 1) & 1) * DST_BYTES), h, q0 - BM);
       const bool dq_ran = it > 0 && has_atomics;
 
       // S' and dP' : rows q (registers), cols = this lane's key.
@@ -967,6 +968,7 @@ __global__ __launch_bounds__(NW * 64, 1) void fa_bwd_kernel(BwdArgs p) {
       // dV^T += dO^T P ; dK^T += Q^T dS  (A via transposed reads of the dO / Q images)
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
+        if (p.abl & 4) break;
         const int cch = (dt * 32 + 16 * G1) / 8 + (pp >> 1);
         const int cb = 8 * (pp & 1);
 #pragma unroll
@@ -999,7 +1001,7 @@ __global__ __launch_bounds__(NW * 64, 1) void fa_bwd_kernel(BwdArgs p) {
     }
     // dQ of the head's last block
     lds_barrier();
-    dq_step(ds_lds + (((n_qb - 1) & 1) * DST_BYTES), h, qa + (n_qb - 1) * BM);
+    if (!(p.abl & 2)) dq_step(ds_lds + (((n_qb - 1) & 1) * DST_BYTES), h, qa + (n_qb - 1) * BM);
   }
 
   // write dK = scale * (dK^T)^T, dV = (dV^T)^T : lane = key, 4 consecutive d per 8-byte store

@@ -20,6 +20,22 @@ import torch
 from ..framework.flags import get_flags
 
 _HOOKS: dict = {}     # (node, slot) -> [fn(torch grad) -> torch grad | None]
+_FINAL: list = []     # callbacks queued during a native backward, run once it has finished
+_ACTIVE = [0]         # depth of native backward passes in flight
+
+
+def queue_callback(fn):
+    """Run ``fn`` once the current backward pass has finished, under either engine (the gradient-ready
+    hooks of DataParallel / sharding / segment parallel use it to flush their last bucket)."""
+    if _ACTIVE[0]:
+        _FINAL.append(fn)
+    else:
+        torch.autograd.Variable._execution_engine.queue_callback(fn)
+
+
+def _drain():
+    while _FINAL:
+        _FINAL.pop(0)()
 
 
 def engine_name():
@@ -54,6 +70,15 @@ def add_hook(t, fn):
         if not lst:
             _HOOKS.pop(key, None)
     return remove
+
+
+def register_grad_hook(t, fn):
+    """Gradient hook on a torch tensor under whichever engine will run its backward (torch's hook list, or
+    this engine's (node, slot) table)."""
+    if use_native():
+        return add_hook(t, fn)
+    h = t.register_hook(fn)
+    return h.remove
 
 
 def retain(t):
@@ -111,8 +136,15 @@ def _run(outs, grads, captures, create_graph):
             raise RuntimeError("backward: the output tensor has stop_gradient=True (no grad node to start from)")
         node, slot = _edge(t)
         roots.append((node, slot, g))
-    with torch.set_grad_enabled(create_graph):
-        return native.module().run_backward(roots, captures, _HOOKS, _HELPERS)
+    _ACTIVE[0] += 1
+    try:
+        with torch.set_grad_enabled(create_graph):
+            res = native.module().run_backward(roots, captures, _HOOKS, _HELPERS)
+    finally:
+        _ACTIVE[0] -= 1
+    if not _ACTIVE[0]:
+        _drain()
+    return res
 
 
 def backward(outs, grads, retain_graph=False):

@@ -21,6 +21,7 @@ import contextlib
 import torch
 import torch.distributed as dist
 
+from ..autograd.engine import queue_callback as _queue_callback
 from ..distributed import collective as C
 from ..framework.flags import flag
 from ..framework.tensor import Tensor, _wrap
@@ -123,7 +124,7 @@ class DataParallel(Layer):
             p._t.grad = v
         if not self._queued:
             self._queued = True
-            torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+            _queue_callback(self._finalize)
         if j in b.ready:
             return
         b.ready.add(j)

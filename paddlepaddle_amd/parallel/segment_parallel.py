@@ -17,6 +17,7 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from ..autograd.engine import queue_callback as _queue_callback
 from .. import nn
 from ..distributed import collective as C
 from ..framework.tensor import Tensor, _wrap
@@ -122,7 +123,7 @@ class SegmentParallel(nn.Layer):
     def _on_grad(self, t):
         if not self._queued:
             self._queued = True
-            torch.autograd.Variable._execution_engine.queue_callback(self._sync)
+            _queue_callback(self._sync)
 
     @torch.no_grad()
     def _sync(self):

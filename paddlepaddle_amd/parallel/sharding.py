@@ -36,6 +36,7 @@ import os
 import torch
 import torch.distributed as dist
 
+from ..autograd.engine import queue_callback as _queue_callback, register_grad_hook as _register_grad_hook
 from ..distributed import collective as C
 from ..framework.tensor import Parameter, Tensor, _wrap
 from ..nn.layer.common import LayerList
@@ -342,7 +343,7 @@ class GroupShardedEngine:
             if torch.is_grad_enabled():
                 t = out._t if isinstance(out, Tensor) else None
                 if t is not None and t.requires_grad:
-                    t.register_hook(self._make_pre_backward(ui))
+                    _register_grad_hook(t, self._make_pre_backward(ui))
             if self.stage == 3 and not self._in_backward and not self.keep_params:
                 self._release(u)
             return None
@@ -378,7 +379,7 @@ class GroupShardedEngine:
     def _queue_finalize(self):
         if not self._queued:
             self._queued = True
-            torch.autograd.Variable._execution_engine.queue_callback(self._finalize_backward)
+            _queue_callback(self._finalize_backward)
 
     # ------------------------------------------------------------------ collectives
     def _gather(self, u):

@@ -299,3 +299,38 @@ def test_sync_batch_norm_matches_full_batch(fmt):
     for t in res:
         np.testing.assert_allclose(t[5], rm, rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(t[6], rv, rtol=1e-5, atol=1e-6)
+
+
+def _native_engine_worker(rank, world, port, mode, q):
+    """DataParallel / sharding gradient-ready hooks under FLAGS_eager_backward_engine=native: their final
+    bucket flush goes through autograd.engine.queue_callback, which runs after the native backward."""
+    paddle = _setup(rank, world, port)
+    paddle.set_flags({"FLAGS_eager_backward_engine": "native"})
+    from paddlepaddle_amd.autograd import engine
+    assert engine.use_native()
+    cfg, model, crit = _make_model(paddle)
+    ids = _data(cfg)
+    local = ids[rank * 2:(rank + 1) * 2]
+    opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    if mode == "dp":
+        model = paddle.DataParallel(model)
+    else:
+        from paddlepaddle_amd.distributed.sharding import group_sharded_parallel
+        model, opt, _ = group_sharded_parallel(model, opt, level=mode)
+    losses = _train(paddle, model, crit, opt, paddle.Tensor(local))
+    sd = {k: v.numpy() for k, v in model.state_dict().items()}
+    q.put((rank, losses, sd))
+    paddle.distributed.barrier()
+
+
+@pytest.mark.parametrize("mode", ["dp", "os_g", "p_g_os"])
+def test_data_parallel_and_sharding_under_native_autograd_engine(mode):
+    from paddlepaddle_amd.utils import native
+    if native.module() is None or not hasattr(native.module(), "run_backward"):
+        pytest.skip("native runtime extension not built")
+    ref_losses, ref_sd = _reference()
+    (_, l0, sd0), (_, l1, sd1) = _spawn(_native_engine_worker, mode)
+    np.testing.assert_allclose((np.array(l0) + np.array(l1)) / 2, ref_losses, rtol=1e-4, atol=1e-5)
+    for k in ref_sd:
+        np.testing.assert_allclose(sd0[k], ref_sd[k], rtol=2e-3, atol=2e-4, err_msg=f"{mode}:{k}")
+        np.testing.assert_allclose(sd1[k], sd0[k], rtol=0, atol=0, err_msg=f"{mode}:{k} replicas differ")
