@@ -27,6 +27,10 @@ def __getattr__(name):
         mod = importlib.import_module(f".{name}", __name__)
         globals()[name] = mod
         return mod
+    if name == "stream":  # paddle.distributed.stream: collectives with sync_op / use_calc_stream semantics
+        from . import communication
+        globals()["stream"] = communication.stream
+        return communication.stream
     if name in ("save_state_dict", "load_state_dict"):
         from . import checkpoint
         return getattr(checkpoint, name)

@@ -5,16 +5,7 @@ from .collective import (all_reduce, all_gather, broadcast, reduce, reduce_scatt
                          alltoall, alltoall_single, send, recv, isend, irecv, ReduceOp)
 
 
-class stream:
-    """communication.stream.*: same collectives; ``sync_op=False`` returns the async task."""
-    all_reduce = staticmethod(all_reduce)
-    all_gather = staticmethod(all_gather)
-    broadcast = staticmethod(broadcast)
-    reduce = staticmethod(reduce)
-    reduce_scatter = staticmethod(reduce_scatter)
-    scatter = staticmethod(scatter)
-    gather = staticmethod(gather)
-    alltoall = staticmethod(alltoall)
-    alltoall_single = staticmethod(alltoall_single)
-    send = staticmethod(send)
-    recv = staticmethod(recv)
+from . import comm_stream as stream  # noqa: E402  (explicit sync_op / use_calc_stream semantics)
+
+import sys as _sys  # noqa: E402
+_sys.modules[__name__ + ".stream"] = stream

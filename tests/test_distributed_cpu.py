@@ -334,3 +334,42 @@ def test_data_parallel_and_sharding_under_native_autograd_engine(mode):
     for k in ref_sd:
         np.testing.assert_allclose(sd0[k], ref_sd[k], rtol=2e-3, atol=2e-4, err_msg=f"{mode}:{k}")
         np.testing.assert_allclose(sd1[k], sd0[k], rtol=0, atol=0, err_msg=f"{mode}:{k} replicas differ")
+
+
+def _stream_worker(rank, world, port, q):
+    paddle = _setup(rank, world, port)
+    import paddlepaddle_amd.distributed as dist
+    from paddlepaddle_amd.distributed.communication import stream as S
+    assert dist.stream is S
+    out = {}
+    x = paddle.to_tensor([1.0 + rank, 2.0])
+    task = dist.stream.all_reduce(x, sync_op=False)
+    task.wait()
+    out["ar_async"] = x.numpy().tolist()
+    y = paddle.to_tensor([float(rank)])
+    out["ar_calc"] = dist.stream.all_reduce(y, sync_op=True, use_calc_stream=True)  # None on the calc stream
+    out["ar_calc_val"] = y.numpy().tolist()
+    try:
+        dist.stream.all_reduce(y, sync_op=False, use_calc_stream=True)
+        out["bad"] = "accepted"
+    except RuntimeError:
+        out["bad"] = "rejected"
+    g = paddle.zeros([2 * 2])
+    t2 = dist.stream.all_gather(g, paddle.to_tensor([rank * 10.0, rank * 10.0 + 1]), sync_op=True)
+    out["ag_tensor"] = g.numpy().tolist()
+    out["ag_task_done"] = t2.is_completed()
+    rs = paddle.zeros([2])
+    dist.stream.reduce_scatter(rs, paddle.to_tensor([1.0, 2.0, 3.0, 4.0]), sync_op=True)
+    out["rs"] = rs.numpy().tolist()
+    q.put((rank, out))
+    dist.barrier()
+
+
+def test_stream_collectives_semantics_gloo():
+    res = _spawn(_stream_worker)
+    for rank, out in res:
+        assert out["ar_async"] == [3.0, 4.0]
+        assert out["ar_calc"] is None and out["ar_calc_val"] == [1.0]
+        assert out["bad"] == "rejected"
+        assert out["ag_tensor"] == [0.0, 1.0, 10.0, 11.0] and out["ag_task_done"]
+    assert res[0][1]["rs"] == [2.0, 4.0] and res[1][1]["rs"] == [6.0, 8.0]
