@@ -57,5 +57,7 @@ def test_lm_head_ce_bf16_gpu_matches_fp32_and_saves_memory():
 
     fused = peak(lambda: ops.lm_head_cross_entropy(h, w, labels, -100, 4))
     plain = peak(lambda: ops.softmax_cross_entropy(ops.linear_nt(h, w), labels))
+    # the plain path holds the [T, V] logits and their gradient at its peak; the fused one a vocabulary slice of
+    # each (plus dW, which both produce)
     logits_bytes = T * V * 2
-    assert fused < plain - logits_bytes, (fused, plain, logits_bytes)
+    assert plain - fused > 0.8 * logits_bytes, (fused, plain, logits_bytes)
