@@ -617,3 +617,51 @@ def fused_dot_product_attention(query, key, value, attn_mask=None, dropout_p=0.0
 
 def memory_efficient_attention(query, key, value, attn_bias=None, p=0.0, scale=None, training=True):
     return fused_dot_product_attention(query, key, value, attn_bias, p, False, scale, training)
+
+
+def fused_gate_attention(query, key=None, query_weight=None, key_weight=None, value_weight=None, qkv_weight=None,
+                         gate_linear_weight=None, gate_linear_bias=None, out_linear_weight=None, out_linear_bias=None,
+                         nonbatched_bias=None, attn_mask=None, has_gating=True, merge_qkv=True, use_flash_attn=False):
+    """AlphaFold-style gated self / cross attention over MSA rows (reference
+    incubate/nn/functional/fused_gate_attention.py:26). query [B, M, R, q_dim]; merge_qkv: qkv_weight
+    [3, H, c, q_dim], else key [B, M, K, kv_dim] with query / key / value weights [dim, H, c]. The attention
+    runs as one flash-attention launch over the B*M rows with attn_mask [B, M, 1, 1, K] and nonbatched_bias
+    [B, 1, H, R, K] folded into one additive mask; gating = sigmoid(query . gate_w + gate_b) multiplies the
+    heads' outputs, then out = avg . out_w [H, c, q_dim] + out_b."""
+    q_in = _t(query)
+    B, M, R, Dq = q_in.shape
+    if merge_qkv:
+        w = _t(qkv_weight)  # [3, H, c, q_dim]
+        H, c = w.shape[1], w.shape[2]
+        qkv = torch.matmul(q_in, w.reshape(3 * H * c, Dq).t()).view(B, M, R, 3, H, c)
+        q, k, v = qkv[..., 0, :, :], qkv[..., 1, :, :], qkv[..., 2, :, :]
+    else:
+        kin = _t(key)
+        wq, wk, wv = _t(query_weight), _t(key_weight), _t(value_weight)
+        H, c = wq.shape[1], wq.shape[2]
+        q = torch.matmul(q_in, wq.reshape(Dq, H * c)).view(B, M, R, H, c)
+        k = torch.matmul(kin, wk.reshape(kin.shape[-1], H * c)).view(B, M, kin.shape[2], H, c)
+        v = torch.matmul(kin, wv.reshape(kin.shape[-1], H * c)).view(B, M, kin.shape[2], H, c)
+    K = k.shape[2]
+    bias = None
+    if attn_mask is not None:
+        bias = _t(attn_mask).to(q.dtype).reshape(B, M, 1, 1, K)
+    if nonbatched_bias is not None:
+        nb = _t(nonbatched_bias).to(q.dtype).reshape(B, 1, H, R, K)
+        bias = nb if bias is None else bias + nb
+    if bias is not None:
+        bias = bias.expand(B, M, H, R, K).reshape(B * M, H, R, K)
+    o = _ops.flash_attention(q.reshape(B * M, R, H, c), k.reshape(B * M, K, H, c), v.reshape(B * M, K, H, c),
+                             causal=False, scale=c ** -0.5, mask=bias, training=False)
+    o = o.reshape(B, M, R, H, c)
+    if has_gating:
+        gw = _t(gate_linear_weight)  # [q_dim, H, c]
+        g = torch.matmul(q_in, gw.reshape(Dq, H * c)).view(B, M, R, H, c)
+        if gate_linear_bias is not None:
+            g = g + _t(gate_linear_bias)
+        o = o * torch.sigmoid(g)
+    ow = _t(out_linear_weight)  # [H, c, q_dim]
+    out = torch.matmul(o.reshape(B, M, R, H * c), ow.reshape(H * c, ow.shape[-1]))
+    if out_linear_bias is not None:
+        out = out + _t(out_linear_bias)
+    return _wrap(out)

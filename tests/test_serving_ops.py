@@ -325,3 +325,36 @@ def test_block_mha_decode_step_graph_replay_gpu():
             np.testing.assert_allclose(got[b].numpy(), ref[0, 0].reshape(-1).numpy(), rtol=3e-2, atol=3e-2)
             assert Ltot == int(dec[b]) + 1
         dec += 1
+
+
+def _ref_gate_attention(q_data, m_data, wq, wk, wv, gw, gb, ow, ob, nb, mask):
+    c = wq.shape[-1]
+    q = torch.einsum("nbqa,ahc->nbqhc", q_data, wq) * c ** -0.5
+    k = torch.einsum("nbka,ahc->nbkhc", m_data, wk)
+    v = torch.einsum("nbka,ahc->nbkhc", m_data, wv)
+    logits = torch.einsum("nbqhc,nbkhc->nbhqk", q, k) + mask
+    if nb is not None:
+        logits = logits + nb
+    avg = torch.einsum("nbhqk,nbkhc->nbqhc", torch.softmax(logits, -1), v)
+    avg = avg * torch.sigmoid(torch.einsum("nbqc,chv->nbqhv", q_data, gw) + gb)
+    return torch.einsum("nbqhc,hco->nbqo", avg, ow) + ob
+
+
+@pytest.mark.parametrize("merge", [True, False])
+def test_fused_gate_attention_matches_einsum(merge):
+    g = torch.Generator().manual_seed(6)
+    B, M, R, Dq, H, c = 2, 3, 5, 16, 4, 8
+    r = lambda *s: torch.randn(*s, generator=g) * 0.5  # noqa: E731
+    q_data = r(B, M, R, Dq)
+    wq, wk, wv = r(Dq, H, c), r(Dq, H, c), r(Dq, H, c)
+    gw, gb, ow, ob = r(Dq, H, c), r(H, c), r(H, c, Dq), r(Dq)
+    nb, mask = r(B, 1, H, R, R), r(B, M, 1, 1, R)
+    ref = _ref_gate_attention(q_data, q_data, wq, wk, wv, gw, gb, ow, ob, nb, mask)
+    kw = dict(gate_linear_weight=_T(gw), gate_linear_bias=_T(gb), out_linear_weight=_T(ow), out_linear_bias=_T(ob),
+              nonbatched_bias=_T(nb), attn_mask=_T(mask))
+    if merge:
+        qkv = torch.stack([wq.permute(1, 2, 0), wk.permute(1, 2, 0), wv.permute(1, 2, 0)])  # [3, H, c, q_dim]
+        out = IF.fused_gate_attention(_T(q_data), qkv_weight=_T(qkv), merge_qkv=True, **kw)
+    else:
+        out = IF.fused_gate_attention(_T(q_data), _T(q_data), _T(wq), _T(wk), _T(wv), merge_qkv=False, **kw)
+    np.testing.assert_allclose(out.numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
