@@ -37,7 +37,7 @@ def batch_norm(x, running_mean, running_var, weight=None, bias=None, training=Fa
 
 
 def fused_bn_act(x, running_mean, running_var, weight=None, bias=None, training=False, momentum=0.9,
-                 epsilon=1e-05, data_format="NCHW", use_global_stats=None, act=None, residual=None):
+                 epsilon=1e-05, data_format="NCHW", use_global_stats=None, act=None, residual=None, _grad_sink=None):
     """act(batch_norm(x) [+ residual]) — batch_norm with the fused_bn_add_activation epilogue
     (reference: python/paddle/incubate/layers/nn.py:1092). Channels-last bf16 input runs the HIP
     kernels of csrc/kernels/bn.hip (ops.batch_norm_act_nhwc); other layouts / dtypes run torch.
@@ -49,7 +49,7 @@ def fused_bn_act(x, running_mean, running_var, weight=None, bias=None, training=
     w, b = T(weight), T(bias)
     r = T(residual)
     if cl and t.dim() >= 2:
-        return _wrap(_ops.batch_norm_act_nhwc(t, w, b, rm, rv, use_batch, momentum, epsilon, act, r))
+        return _wrap(_ops.batch_norm_act_nhwc(t, w, b, rm, rv, use_batch, momentum, epsilon, act, r, _grad_sink))
     nd = t.dim()
     if t.dtype in (torch.float16, torch.bfloat16) and w is not None and w.dtype != torch.float32:
         w, b = w.float(), b.float() if b is not None else None

@@ -38,14 +38,14 @@ class _BatchNormBase(Layer):
         return F.batch_norm(x, self._mean, self._variance, self.weight, self.bias, self.training, self._momentum,
                             self._epsilon, self._data_format, self._use_global_stats)
 
-    def fused_forward(self, x, act=None, residual=None):
+    def fused_forward(self, x, act=None, residual=None, _grad_sink=None):
         """act(self(x) [+ residual]) in one fused pass where the layer is a plain batch norm
         (fused_bn_add_activation, F.fused_bn_act); layers that override forward (SyncBatchNorm,
         legacy BatchNorm with its own act) compose the ops instead."""
         if type(self).forward is _BatchNormBase.forward:
             return F.fused_bn_act(x, self._mean, self._variance, self.weight, self.bias, self.training,
                                   self._momentum, self._epsilon, self._data_format, self._use_global_stats, act,
-                                  residual)
+                                  residual, _grad_sink)
         y = self(x)
         if residual is not None:
             y = y + residual

@@ -49,7 +49,9 @@ def _chunks(R, C):
 
 class _BNActHIP(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x2, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu):
+    def forward(ctx, x2, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu,
+                sink=None):
+        ctx.sink = sink
         R, C = x2.shape
         dev = x2.device
         y = torch.empty_like(x2)
@@ -85,7 +87,9 @@ class _BNActHIP(torch.autograd.Function):
         dev = x2.device
         dy = dy.contiguous()
         dx = torch.empty_like(x2)
-        dres = torch.empty_like(x2) if has_res and ctx.needs_input_grad[3] else None
+        sink = ctx.sink
+        to_sink = sink is not None and has_res
+        dres = torch.empty_like(x2) if has_res and (ctx.needs_input_grad[3] or to_sink) else None
         dw = torch.empty(C, dtype=torch.float32, device=dev) if has_w else None
         db = torch.empty(C, dtype=torch.float32, device=dev) if has_b else None
         partial = torch.empty(2 * _chunks(R, C) * C, dtype=torch.float32, device=dev)
@@ -95,7 +99,10 @@ class _BNActHIP(torch.autograd.Function):
                L.ptr(ss), L.stream_ptr())
         if dw is not None and dw.dtype != weight.dtype:
             dw = dw.to(weight.dtype)
-        return dx, dw, db, dres, None, None, None, None, None, None
+        if to_sink:  # the block's first conv adds it to its data gradient (ops/conv.py ResidualGradSink)
+            sink.dres = dres
+            dres = None
+        return dx, dw, db, dres, None, None, None, None, None, None, None
 
 
 def _hip_ok(x, weight, bias, residual, running_mean, running_var):
@@ -119,7 +126,7 @@ def _hip_ok(x, weight, bias, residual, running_mean, running_var):
 
 @static_op
 def batch_norm_act_nhwc(x, weight, bias, running_mean, running_var, training=True, momentum=0.9, eps=1e-5,
-                        act=None, residual=None):
+                        act=None, residual=None, grad_sink=None):
     """y = act(batch_norm(x) [+ residual]) over the last (channel) dim of a channels-last tensor."""
     if act not in (None, "relu"):
         raise ValueError(f"unsupported fused activation {act}")
@@ -127,8 +134,11 @@ def batch_norm_act_nhwc(x, weight, bias, running_mean, running_var, training=Tru
     if _hip_ok(x, weight, bias, residual, running_mean, running_var):
         x2 = x.view(-1, C)
         r2 = residual.view(-1, C) if residual is not None else None
+        sink = grad_sink if (grad_sink is not None and grad_sink.armed and r2 is not None) else None
+        if sink is not None:
+            r2 = r2.detach()  # its gradient travels through the sink, not autograd
         y = _BNActHIP.apply(x2, weight, bias, r2, running_mean, running_var, bool(training), float(momentum),
-                            float(eps), act == "relu")
+                            float(eps), act == "relu", sink)
         return y.view(x.shape)
     x2 = x.reshape(-1, C)
     r2 = residual.reshape(-1, C) if residual is not None else None

@@ -23,13 +23,43 @@ from . import _loader as L
 from . import gemm as G
 
 
+class ResidualGradSink:
+    """Hand-off of a residual-branch gradient between two ops of one ResNet bottleneck (identity shortcut):
+    the block's last BN (which adds the block input x as its residual) writes d(residual) here instead of
+    returning it to autograd, and the block's first 1x1 conv — the other consumer of x — accumulates its data
+    gradient onto it in the GEMM epilogue (kEpiAccum) and returns the sum as dx. That removes the separate
+    elementwise add autograd would run to sum the two gradients of x (one read + one write of an activation
+    per block). ``armed`` is set only when the conv really ran the hand-written GEMM path."""
+
+    def __init__(self):
+        self.armed = False
+        self.dres = None
+
+
+_SINK = [None]
+
+
+class residual_grad_sink:
+    """``with residual_grad_sink() as s: y = conv1(x)`` — a 1x1 conv on the HIP path inside the block arms s."""
+
+    def __enter__(self):
+        self.sink = ResidualGradSink()
+        _SINK[0] = self.sink
+        return self.sink
+
+    def __exit__(self, *exc):
+        _SINK[0] = None
+        return False
+
+
 def _splits(M, N, K):
     return G.pick_splits(M, N, K, bn=G._pick_bn(M, N, False))
 
 
 class _Conv1x1(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, stride):
+    def forward(ctx, x, w, b, stride, sink=None):
+        ctx.sink = sink
         N, H, W, Cin = x.shape
         Cout = w.shape[0]
         xs = x[:, ::stride, ::stride, :].contiguous() if stride > 1 else x
@@ -49,8 +79,15 @@ class _Conv1x1(torch.autograd.Function):
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         dx = dw = db = None
+        sink = ctx.sink
         if ctx.needs_input_grad[0]:
-            dx2 = G.gemm(dy2, w2)
+            if sink is not None and sink.dres is not None and stride == 1:
+                # dx = d(residual) + dy . W in one epilogue (see ResidualGradSink)
+                acc = sink.dres
+                sink.dres = None
+                dx2 = G.gemm(dy2, w2, out=acc.view(-1, Cin), accumulate=True)
+            else:
+                dx2 = G.gemm(dy2, w2)
             dx = dx2.view(N, Ho, Wo, Cin)
             if stride > 1:
                 full = torch.zeros(N, H, W, Cin, dtype=dx.dtype, device=dx.device)
@@ -65,7 +102,7 @@ class _Conv1x1(torch.autograd.Function):
             dw = dw.view(Cout, Cin, 1, 1)
         if has_b and ctx.needs_input_grad[2]:
             db = dy2.float().sum(0).to(dy2.dtype)
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
 def eligible(x_nhwc, w, groups, padding_is_zero, dilation_ok=True):
@@ -85,8 +122,12 @@ def conv1x1_nhwc(x, w, b, stride, fallback):
     returns the NHWC result. Picks the faster per shape (forward + backward timed once)."""
     key = ("conv1x1", tuple(x.shape), w.shape[0], stride, b is not None, x.requires_grad or w.requires_grad)
 
+    sink = _SINK[0] if stride == 1 else None
+
     def hip():
-        return _Conv1x1.apply(x, w, b, stride)
+        if sink is not None:
+            sink.armed = True
+        return _Conv1x1.apply(x, w, b, stride, sink)
 
     def _fb_bench(fn):
         def run():

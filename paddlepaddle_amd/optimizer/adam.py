@@ -145,9 +145,14 @@ class Adam(Optimizer):
         if coef is not None:
             inv_scale = coef if inv_scale is None else (coef * inv_scale.reshape(())).reshape(())
         hyper = None
-        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
-            hyper = self._graph_hyper(group, fp32[0].device, lr, b1, b2, step)
-            L.call("pa_adam_hyper_step", L.ptr(hyper), float(b1), float(b2), L.stream_ptr())
+        if fp32[0].is_cuda:
+            # the device copy of {lr, beta1^t, beta2^t} is created on the first (eager) step and advanced by every
+            # step, so a step captured later into a hipGraph starts from the right powers; eager steps still pass
+            # host floats, captured ones read the device copy
+            h = self._graph_hyper(group, fp32[0].device, lr, b1, b2, step)
+            L.call("pa_adam_hyper_step", L.ptr(h), float(b1), float(b2), L.stream_ptr())
+            if torch.cuda.is_current_stream_capturing():
+                hyper = h
         L.call("pa_adamw_multi", L.ptr(t_rows), L.ptr(t_items), n_items, L.ptr(inv_scale), float(lr), float(b1),
                float(b2), float(eps), 0.0, float(bc1), float(bc2), L.ptr(hyper), L.stream_ptr())
         self._last_step = step
@@ -160,6 +165,9 @@ class Adam(Optimizer):
         hs = self.__dict__.setdefault("_graph_hypers", {})
         h = hs.get(id(group))
         if h is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("capture an optimizer step only after an eager warm-up step (the device "
+                                   "hyper-parameter copy is created there)")
             h = torch.tensor([float(lr), float(b1) ** (step - 1), float(b2) ** (step - 1)], dtype=torch.float32,
                              device=dev)
             hs[id(group)] = h

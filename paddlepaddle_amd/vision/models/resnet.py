@@ -8,12 +8,12 @@ from __future__ import annotations
 from ... import nn
 
 
-def _bn_act(bn, x, act="relu", residual=None):
+def _bn_act(bn, x, act="relu", residual=None, grad_sink=None):
     """bn(x) [+ residual] -> act as one fused pass (fused_bn_add_activation) when the norm layer
     supports it; any other norm layer composes the ops."""
     f = getattr(bn, "fused_forward", None)
     if f is not None:
-        return f(x, act, residual)
+        return f(x, act, residual, grad_sink) if grad_sink is not None else f(x, act, residual)
     y = bn(x)
     if residual is not None:
         y = y + residual
@@ -65,11 +65,19 @@ class BottleneckBlock(nn.Layer):
 
     def forward(self, x):
         identity = x
-        out = _bn_act(self.bn1, self.conv1(x))
+        sink = None
+        if self.downsample is None:
+            # identity shortcut: x's two gradients (residual, conv1) are summed in conv1's GEMM epilogue
+            from ...ops.conv import residual_grad_sink
+            with residual_grad_sink() as sink:
+                h = self.conv1(x)
+        else:
+            h = self.conv1(x)
+        out = _bn_act(self.bn1, h)
         out = _bn_act(self.bn2, self.conv2(out))
         if self.downsample is not None:
             identity = self.downsample(x)
-        return _bn_act(self.bn3, self.conv3(out), "relu", identity)
+        return _bn_act(self.bn3, self.conv3(out), "relu", identity, grad_sink=sink)
 
 
 class ResNet(nn.Layer):

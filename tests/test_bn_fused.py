@@ -126,3 +126,54 @@ def test_momentum_multi_tensor_hip_matches_fp32(nesterov):
     for p, m in zip(params, masters):
         torch.testing.assert_close(opt._master(p), m, rtol=1e-5, atol=1e-5)
         torch.testing.assert_close(p._t.float(), m.bfloat16().float(), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.gpu
+def test_bottleneck_residual_grad_sink_matches_autograd_sum_gpu():
+    """Identity-shortcut bottleneck on the HIP path: bn3 hands d(residual) to conv1, whose dgrad GEMM adds it in
+    its epilogue (ops/conv.py ResidualGradSink). Gradients match the same block with the hand-off disabled
+    (autograd sums the two gradients of x with an elementwise add)."""
+    from paddlepaddle_amd.ops import conv as C
+    from paddlepaddle_amd.vision.models import resnet as RN
+    paddle.set_device("gpu")
+    paddle.seed(3)
+    paddle.set_default_dtype("bfloat16")
+    try:
+        blk = RN.BottleneckBlock(256, 64, data_format="NHWC")
+    finally:
+        paddle.set_default_dtype("float32")
+    g = torch.Generator(device="cuda").manual_seed(0)
+    xt = torch.randn(8, 14, 14, 256, device="cuda", generator=g, dtype=torch.bfloat16)
+    dy = torch.randn(8, 14, 14, 256, device="cuda", generator=g, dtype=torch.bfloat16)
+    seen = []
+    orig = C.residual_grad_sink
+
+    class spy(orig):
+        def __exit__(self, *exc):
+            seen.append(self.sink.armed)
+            return super().__exit__(*exc)
+
+    def run(ctx_factory):
+        C.residual_grad_sink = ctx_factory
+        try:
+            x = paddle.Tensor(xt.clone().requires_grad_(True))
+            for p in blk.parameters():
+                p.clear_gradient(set_to_zero=False)
+            blk(x)._t.backward(dy)
+            return x._t.grad.float(), [p.grad._t.float().clone() for p in blk.parameters()]
+        finally:
+            C.residual_grad_sink = orig
+
+    class off:
+        def __enter__(self):
+            return C.ResidualGradSink()
+
+        def __exit__(self, *exc):
+            return False
+    gx_s, gp_s = run(spy)
+    gx_r, gp_r = run(off)
+    assert seen and all(seen), "conv1 did not run the hand-written GEMM path"
+    scale = gx_r.abs().max().item()
+    assert (gx_s - gx_r).abs().max().item() < 2e-2 * scale
+    for a, b in zip(gp_s, gp_r):
+        assert (a - b).abs().max().item() <= 2e-2 * max(b.abs().max().item(), 1e-3)
