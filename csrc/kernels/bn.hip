@@ -29,11 +29,14 @@ __device__ __forceinline__ void st8(uint16_t* p, const float* f) { store8<bf16>(
 // MASKX (with RELU, no residual in the forward): the relu mask is recomputed from x as
 // x * scale + shift > 0 with the forward's scale / shift (ss), the same expression the forward applied,
 // so y is not read (one tensor fewer in both backward passes).
-template <int MODE, bool RELU, bool MASKX = false>
+// MASKB (with RELU): the relu mask comes from the forward's bit mask (one byte per 8 channels of a row,
+// bn_apply_k WMASK) instead of y: 1/16 of y's bytes.
+template <int MODE, bool RELU, bool MASKX = false, bool MASKB = false>
 __global__ __launch_bounds__(kThreads) void bn_reduce_k(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
                                                         const uint16_t* __restrict__ y, const float* __restrict__ mean,
                                                         float* __restrict__ partial, int64_t R, int C, int CB,
-                                                        int64_t rows_per_chunk, const float* __restrict__ ss = nullptr) {
+                                                        int64_t rows_per_chunk, const float* __restrict__ ss = nullptr,
+                                                        const uint8_t* __restrict__ mbits = nullptr) {
   const int tcx = CB >> 3;               // lanes along channels
   const int rpi = kThreads / tcx;        // rows per iteration
   const int tx = threadIdx.x % tcx, ty = threadIdx.x / tcx;
@@ -66,6 +69,14 @@ __global__ __launch_bounds__(kThreads) void bn_reduce_k(const uint16_t* __restri
         for (int u = 0; u < U; ++u)
 #pragma unroll
           for (int j = 0; j < 8; ++j) gs[u][j] = xs[u][j] * sc[j] + sh[j] > 0.f ? gs[u][j] : 0.f;
+      } else if (RELU && MASKB) {
+        uint32_t mb[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) mb[u] = mbits[((r + u * rpi) * C + c0) >> 3];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) gs[u][j] = (mb[u] >> j) & 1u ? gs[u][j] : 0.f;
       } else if (RELU) {
         float ys[U][8];
 #pragma unroll
@@ -101,6 +112,10 @@ __global__ __launch_bounds__(kThreads) void bn_reduce_k(const uint16_t* __restri
       if (RELU && MASKX) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) ga[j] = xa[j] * sc[j] + sh[j] > 0.f ? ga[j] : 0.f;
+      } else if (RELU && MASKB) {
+        const uint32_t mb = mbits[(r * C + c0) >> 3];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ga[j] = (mb >> j) & 1u ? ga[j] : 0.f;
       } else if (RELU) {
         float ya[8];
         ld8(y + r * C + c0, ya);
@@ -217,11 +232,11 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float* __restric
   coef[2 * C + c] = d0;
 }
 
-// y = act(x * scale + shift [+ res])
-template <bool RELU, bool RES>
+// y = act(x * scale + shift [+ res]); WMASK: also the relu mask, bit j of byte i = (y[8i + j] > 0)
+template <bool RELU, bool RES, bool WMASK = false>
 __global__ __launch_bounds__(kThreads) void bn_apply_k(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                        const float* __restrict__ ss, uint16_t* __restrict__ y,
-                                                       int64_t nvec, int C) {
+                                                       int64_t nvec, int C, uint8_t* __restrict__ mbits = nullptr) {
   const int cv = C >> 3;
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * kThreads) {
     const int c0 = (int)(i % cv) * 8;
@@ -232,6 +247,7 @@ __global__ __launch_bounds__(kThreads) void bn_apply_k(const uint16_t* __restric
     const float4 h0 = *reinterpret_cast<const float4*>(ss + C + c0), h1 = *reinterpret_cast<const float4*>(ss + C + c0 + 4);
     const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
     const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    uint32_t bits = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float v = f[j] * sc[j] + sh[j];
@@ -240,15 +256,27 @@ __global__ __launch_bounds__(kThreads) void bn_apply_k(const uint16_t* __restric
       f[j] = v;
     }
     st8(y + i * 8, f);
+    if (WMASK) {
+      // the mask of the stored (bf16-rounded) value, the same test the y-reading backward applies
+      const uint4 w = *reinterpret_cast<const uint4*>(y + i * 8);
+      const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bits |= (lo_bf16(ww[j]) > 0.f ? 1u : 0u) << (2 * j);
+        bits |= (hi_bf16(ww[j]) > 0.f ? 1u : 0u) << (2 * j + 1);
+      }
+      mbits[i] = (uint8_t)bits;
+    }
   }
 }
 
 // dx = a * dyp - bc * x + d0; dres = dyp   (MASKX: relu mask from x * scale + shift, see bn_reduce_k)
-template <bool RELU, bool DRES, bool MASKX = false>
+template <bool RELU, bool DRES, bool MASKX = false, bool MASKB = false>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply_k(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
                                                            const uint16_t* __restrict__ y, const float* __restrict__ coef,
                                                            uint16_t* __restrict__ dx, uint16_t* __restrict__ dres,
-                                                           int64_t nvec, int C, const float* __restrict__ ss = nullptr) {
+                                                           int64_t nvec, int C, const float* __restrict__ ss = nullptr,
+                                                           const uint8_t* __restrict__ mbits = nullptr) {
   const int cv = C >> 3;
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * kThreads) {
     const int c0 = (int)(i % cv) * 8;
@@ -261,6 +289,10 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_k(const uint16_t* __res
       load8<float>(ss + C + c0, sh);
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = f[j] * sc[j] + sh[j] > 0.f ? g[j] : 0.f;
+    } else if (RELU && MASKB) {
+      const uint32_t mb = mbits[i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = (mb >> j) & 1u ? g[j] : 0.f;
     } else if (RELU) {
       float yy[8];
       ld8(y + i * 8, yy);
@@ -398,6 +430,62 @@ PA_EXPORT int pa_bn_bwd_nhwc(const void* dy, const void* x, const void* y, void*
   else if (dres) PA_BN_BWD(false, true);
   else PA_BN_BWD(false, false);
 #undef PA_BN_BWD
+  PA_CHECK_LAUNCH();
+  return 0;
+}
+
+// Residual + relu variants that keep a bit mask of the relu instead of re-reading y in the backward
+// (mbits: R * C / 8 bytes). Forward: bn_apply writes y and the mask; backward: both passes read the mask.
+PA_EXPORT int pa_bn_fwd_nhwc_mask(const void* x, const void* res, void* y, const float* w, const float* b,
+                                  float* run_mean, float* run_var, float* save_mean, float* save_rstd, float* partial,
+                                  float* ss, void* mbits, int64_t R, int C, float momentum, float eps, int training,
+                                  hipStream_t st) {
+  if (C % 8 != 0 || R < 1 || !mbits) return 3;
+  int CB, chunks;
+  int64_t rpc;
+  plan(R, C, &CB, &chunks, &rpc);
+  if (training) {
+    hipLaunchKernelGGL((bn_reduce_k<0, false>), dim3(C / CB, chunks), dim3(kThreads), 0, st, (const uint16_t*)x,
+                       nullptr, nullptr, nullptr, partial, R, C, CB, rpc);
+    PA_CHECK_LAUNCH();
+    hipLaunchKernelGGL(bn_fwd_finalize_k, dim3((C + 63) / 64), dim3(1024), 0, st, partial, chunks, C, R, w, b,
+                       run_mean, run_var, momentum, eps, save_mean, save_rstd, ss);
+    PA_CHECK_LAUNCH();
+  }
+  const int64_t nvec = R * C / 8;
+  if (res)
+    hipLaunchKernelGGL((bn_apply_k<true, true, true>), dim3(apply_grid(nvec)), dim3(kThreads), 0, st,
+                       (const uint16_t*)x, (const uint16_t*)res, ss, (uint16_t*)y, nvec, C, (uint8_t*)mbits);
+  else
+    hipLaunchKernelGGL((bn_apply_k<true, false, true>), dim3(apply_grid(nvec)), dim3(kThreads), 0, st,
+                       (const uint16_t*)x, nullptr, ss, (uint16_t*)y, nvec, C, (uint8_t*)mbits);
+  PA_CHECK_LAUNCH();
+  return 0;
+}
+
+PA_EXPORT int pa_bn_bwd_nhwc_mask(const void* dy, const void* x, const void* mbits, void* dx, void* dres,
+                                  const float* w, const float* mean, const float* rstd, float* dw, float* db,
+                                  float* partial, float* coef, int64_t R, int C, int global_stats, hipStream_t st) {
+  if (C % 8 != 0 || R < 1 || !mbits) return 3;
+  int CB, chunks;
+  int64_t rpc;
+  plan(R, C, &CB, &chunks, &rpc);
+  const uint8_t* mb = (const uint8_t*)mbits;
+  hipLaunchKernelGGL((bn_reduce_k<1, true, false, true>), dim3(C / CB, chunks), dim3(kThreads), 0, st,
+                     (const uint16_t*)x, (const uint16_t*)dy, nullptr, mean, partial, R, C, CB, rpc, nullptr, mb);
+  PA_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_bwd_finalize_k, dim3((C + 63) / 64), dim3(1024), 0, st, partial, chunks, C, R, w, mean, rstd,
+                     dw, db, coef, global_stats);
+  PA_CHECK_LAUNCH();
+  const int64_t nvec = R * C / 8;
+  const unsigned g = apply_grid(nvec);
+  if (dres)
+    hipLaunchKernelGGL((bn_bwd_apply_k<true, true, false, true>), dim3(g), dim3(kThreads), 0, st, (const uint16_t*)dy,
+                       (const uint16_t*)x, nullptr, coef, (uint16_t*)dx, (uint16_t*)dres, nvec, C, nullptr, mb);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_k<true, false, false, true>), dim3(g), dim3(kThreads), 0, st,
+                       (const uint16_t*)dy, (const uint16_t*)x, nullptr, coef, (uint16_t*)dx, nullptr, nvec, C,
+                       nullptr, mb);
   PA_CHECK_LAUNCH();
   return 0;
 }

@@ -75,6 +75,8 @@ SIGS = {
     "pa_bn_fwd_nhwc": [_vp] * 11 + [_i64, _i32, _f32, _f32, _i32, _i32, _vp],
     "pa_bn_bwd_nhwc": [_vp] * 12 + [_i64, _i32, _i32, _i32, _vp, _vp],
     "pa_bn_reduce_nhwc": [_i32] + [_vp] * 7 + [_i64, _i32, _i32, _vp],
+    "pa_bn_fwd_nhwc_mask": [_vp] * 12 + [_i64, _i32, _f32, _f32, _i32, _vp],
+    "pa_bn_bwd_nhwc_mask": [_vp] * 12 + [_i64, _i32, _i32, _vp],
     "pa_bn_bwd_apply_nhwc": [_vp] * 6 + [_i64, _i32, _i32, _vp, _vp],
     # fused decode step
     "pa_add_rms_norm_fwd": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _f32, _i32, _vp],

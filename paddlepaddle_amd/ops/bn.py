@@ -68,14 +68,25 @@ class _BNActHIP(torch.autograd.Function):
             ss[0].copy_(w * rstd)
             ss[1].copy_(b - mean * w * rstd)
             partial = None
-        L.call("pa_bn_fwd_nhwc", L.ptr(x2), L.ptr(residual), L.ptr(y), L.ptr(weight), L.ptr(bias),
-               L.ptr(running_mean if training else None), L.ptr(running_var if training else None), L.ptr(mean),
-               L.ptr(rstd), L.ptr(partial), L.ptr(ss), R, C, float(momentum), float(eps), int(relu), int(training),
-               L.stream_ptr())
         # relu without residual: the backward recomputes the mask from x with scale / shift (ss) instead of
-        # reading y; with a residual the mask needs y
+        # reading y; relu with a residual: the forward writes a bit mask of the relu (R * C / 8 bytes) that the
+        # backward reads instead of y
         mask_x = bool(relu) and residual is None
-        ctx.save_for_backward(x2, y if relu and not mask_x else None, weight, mean, rstd, ss if mask_x else None)
+        mbits = None
+        if relu and residual is not None and L.has("pa_bn_fwd_nhwc_mask"):
+            mbits = torch.empty(R * C // 8, dtype=torch.uint8, device=dev)
+            L.call("pa_bn_fwd_nhwc_mask", L.ptr(x2), L.ptr(residual), L.ptr(y), L.ptr(weight), L.ptr(bias),
+                   L.ptr(running_mean if training else None), L.ptr(running_var if training else None), L.ptr(mean),
+                   L.ptr(rstd), L.ptr(partial), L.ptr(ss), L.ptr(mbits), R, C, float(momentum), float(eps),
+                   int(training), L.stream_ptr())
+        else:
+            L.call("pa_bn_fwd_nhwc", L.ptr(x2), L.ptr(residual), L.ptr(y), L.ptr(weight), L.ptr(bias),
+                   L.ptr(running_mean if training else None), L.ptr(running_var if training else None), L.ptr(mean),
+                   L.ptr(rstd), L.ptr(partial), L.ptr(ss), R, C, float(momentum), float(eps), int(relu),
+                   int(training), L.stream_ptr())
+        keep = mbits if mbits is not None else (y if relu and not mask_x else None)
+        ctx.save_for_backward(x2, keep, weight, mean, rstd, ss if mask_x else None)
+        ctx.bitmask = mbits is not None
         ctx.flags = (bool(relu), bool(training), residual is not None, weight is not None, bias is not None)
         return y
 
@@ -94,9 +105,14 @@ class _BNActHIP(torch.autograd.Function):
         db = torch.empty(C, dtype=torch.float32, device=dev) if has_b else None
         partial = torch.empty(2 * _chunks(R, C) * C, dtype=torch.float32, device=dev)
         coef = torch.empty(3, C, dtype=torch.float32, device=dev)
-        L.call("pa_bn_bwd_nhwc", L.ptr(dy), L.ptr(x2), L.ptr(y), L.ptr(dx), L.ptr(dres), L.ptr(weight), L.ptr(mean),
-               L.ptr(rstd), L.ptr(dw), L.ptr(db), L.ptr(partial), L.ptr(coef), R, C, int(relu), int(not training),
-               L.ptr(ss), L.stream_ptr())
+        if ctx.bitmask:  # `y` holds the relu bit mask
+            L.call("pa_bn_bwd_nhwc_mask", L.ptr(dy), L.ptr(x2), L.ptr(y), L.ptr(dx), L.ptr(dres), L.ptr(weight),
+                   L.ptr(mean), L.ptr(rstd), L.ptr(dw), L.ptr(db), L.ptr(partial), L.ptr(coef), R, C,
+                   int(not training), L.stream_ptr())
+        else:
+            L.call("pa_bn_bwd_nhwc", L.ptr(dy), L.ptr(x2), L.ptr(y), L.ptr(dx), L.ptr(dres), L.ptr(weight),
+                   L.ptr(mean), L.ptr(rstd), L.ptr(dw), L.ptr(db), L.ptr(partial), L.ptr(coef), R, C, int(relu),
+                   int(not training), L.ptr(ss), L.stream_ptr())
         if dw is not None and dw.dtype != weight.dtype:
             dw = dw.to(weight.dtype)
         if to_sink:  # the block's first conv adds it to its data gradient (ops/conv.py ResidualGradSink)
