@@ -62,6 +62,9 @@ def parse_args(argv=None):
     p.add_argument("--np", default=None, help="worker count MIN or MIN:MAX (elastic)")
     p.add_argument("--elastic_level", type=int, default=-1)
     p.add_argument("--elastic_timeout", type=int, default=30)
+    # auto tuner (reference launch/main.py --auto_tuner_json): search the parallel configuration by trials
+    p.add_argument("--auto_tuner_json", default=None, help="auto tuner config (json): run trials, keep the best")
+    p.add_argument("--max_time_per_task", type=float, default=None, help="seconds before a job is stopped")
     p.add_argument("training_script")
     p.add_argument("training_script_args", nargs=argparse.REMAINDER)
     return p.parse_args(argv)
@@ -90,6 +93,8 @@ def _tail(path, n=20):
 
 def launch(argv=None):
     a = parse_args(argv)
+    if a.auto_tuner_json:
+        return _launch_auto_tuner(a)
     if a.run_mode == "ps" or a.server_num or a.servers:
         return _launch_ps(a)
     if a.elastic_server:
@@ -282,9 +287,74 @@ def _terminate(procs):
                 pass
 
 
+def _launch_auto_tuner(a):
+    """Trial loop of the auto tuner (distributed/auto_tuner): each configuration runs as an ordinary collective
+    job (its own log dir ``<log_dir>/trial_<k>``, the config as ``PADDLE_AUTO_TUNER_CFG`` json in the workers'
+    environment and as script flags through the tuner's ``run_cmd``), the metric is read from rank 0's log,
+    failures / out-of-memory runs are recorded as such (and prune the configs they dominate), ``history.csv``
+    is rewritten after every trial and ``best_cfg.json`` names the winner."""
+    import json
+    from ..auto_tuner import AutoTuner, HistoryRecorder, gen_new_args, parse_metric
+    with open(a.auto_tuner_json) as f:
+        cfg = json.load(f)
+    devs = _devices(a)
+    cfg.setdefault("num_gpus", len(devs) * int(str(a.nnodes).split(":")[0]))
+    cfg.setdefault("gpus_per_node", len(devs))
+    tuner, rec = AutoTuner(cfg), HistoryRecorder(cfg)
+    metric = cfg.setdefault("metric_cfg", {"name": "tokens/s", "OptimizationDirection": "Maximize"})
+    per_task = a.max_time_per_task or cfg.get("max_time_per_task")
+    base = a.log_dir
+    os.makedirs(base, exist_ok=True)
+    job = 0
+    while True:
+        c = tuner.search_once()
+        if c is None:
+            break
+        job += 1
+        trial_dir = os.path.join(base, f"trial_{job}")
+        argv = ["--devices", ",".join(devs), "--log_dir", trial_dir, "--job_id", f"{a.job_id}_t{job}"]
+        if per_task:
+            argv += ["--max_time_per_task", str(per_task)]
+        argv += [a.training_script] + gen_new_args(a.training_script_args, c, cfg)
+        os.environ["PADDLE_AUTO_TUNER_CFG"] = json.dumps(c)
+        print(f"[auto_tuner] trial {job}: {c}", file=sys.stderr)
+        t0 = time.time()
+        rc = launch(argv)
+        os.environ.pop("PADDLE_AUTO_TUNER_CFG", None)
+        text = ""
+        try:
+            with open(os.path.join(trial_dir, "workerlog.0"), errors="replace") as f:
+                text = f.read()
+        except OSError:
+            pass
+        value = parse_metric(text, metric)
+        low = text.lower()
+        entry = dict(c, job_id=job, time=round(time.time() - t0, 1), exit_code=rc)
+        entry[metric["name"]] = value
+        entry["oom"] = "out of memory" in low or "outofmemory" in low
+        entry["error"] = rc != 0 or value is None
+        rec.add_cfg(**entry)
+        tuner.add_cfg(entry)
+        rec.store_history(os.path.join(base, "history.csv"))
+    best, none = rec.get_best()
+    if none:
+        print("[auto_tuner] no trial produced the metric", file=sys.stderr)
+        return 1
+    with open(os.path.join(base, "best_cfg.json"), "w") as f:
+        json.dump(best, f, indent=1, default=str)
+    print(f"[auto_tuner] best of {job} trials: {best}", file=sys.stderr)
+    return 0
+
+
 def _watch(procs, a):
+    deadline = time.time() + a.max_time_per_task if getattr(a, "max_time_per_task", None) else None
     try:
         while True:
+            if deadline is not None and time.time() > deadline:
+                print(f"[launch] job exceeded --max_time_per_task ({a.max_time_per_task} s); stopping it.",
+                      file=sys.stderr)
+                _terminate(procs)
+                return 124
             alive = 0
             for rank, p, log in procs:
                 rc = p.poll()
