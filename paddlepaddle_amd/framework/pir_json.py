@@ -639,4 +639,11 @@ def load(path_prefix, device=None):
         from .place import _get_torch_device
         device = _get_torch_device()
     params = {n: Tensor(t.to(device)) for n, t in zip(names, tensors)}
+    from ..framework.flags import flag
+    if flag("FLAGS_pir_native_interpreter", True):
+        from .native_interp import compile_program
+        native = compile_program(prog, params, device if isinstance(device, torch.device) else
+                                 torch.device(device))
+        if native is not None:
+            return native
     return PirRunner(prog, params)

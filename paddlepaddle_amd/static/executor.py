@@ -274,7 +274,8 @@ class Executor:
             prog = prog._program
         from ..framework.program_desc import ProgramDescRunner
         from ..framework.pir_json import PirRunner
-        if isinstance(prog, (ProgramDescRunner, PirRunner)):  # a reference-format model from load_inference_model
+        from ..framework.native_interp import NativeRunner
+        if isinstance(prog, (ProgramDescRunner, PirRunner, NativeRunner)):  # a reference-format model from load_inference_model
             outs = prog.run(feed or {})
             return [o.numpy() for o in outs] if return_numpy else outs
         if not prog.nodes and not prog.feeds:

@@ -79,7 +79,8 @@ def test_pir_json_round_trip_runs(tmp_path):
     try:
         exe = paddle.static.Executor(paddle.CPUPlace())
         prog, feed_names, fetch_names = paddle.static.load_inference_model(prefix, exe)
-        assert isinstance(prog, pir.PirRunner) and feed_names == ["x", "im"]
+        from paddlepaddle_amd.framework.native_interp import NativeRunner
+        assert isinstance(prog, (pir.PirRunner, NativeRunner)) and feed_names == ["x", "im"]
         got = exe.run(prog, feed=xs, fetch_list=fetch_names)
     finally:
         paddle.disable_static()
@@ -111,3 +112,29 @@ def test_attribute_and_type_codec():
     assert pir.decode_type(pir.dtensor("bfloat16", [2, -1])) == ("bfloat16", [2, -1])
     with pytest.raises(ValueError):
         pir.PirProgram({"program": {}})
+
+
+def test_native_interpreter_matches_python_replay(tmp_path):
+    """The C++ interpreter (csrc/interpreter, instruction list + last-use release) runs the saved PIR program
+    with the Python replay's outputs; mutable attributes are folded, intermediates are released."""
+    from paddlepaddle_amd.framework import native_interp as ni
+    if not ni.available():
+        pytest.skip("_C_interp not built")
+    prefix, xs, ref = _save(tmp_path, fmt="pir")
+    paddle.set_flags({"FLAGS_pir_native_interpreter": True})
+    native = pir.load(prefix)
+    assert isinstance(native, ni.NativeRunner)
+    paddle.set_flags({"FLAGS_pir_native_interpreter": False})
+    try:
+        py = pir.load(prefix)
+    finally:
+        paddle.set_flags({"FLAGS_pir_native_interpreter": True})
+    assert isinstance(py, pir.PirRunner)
+    feeds = {k: paddle.to_tensor(v) for k, v in xs.items()}
+    a = [t.numpy() for t in native.run(feeds)]
+    b = [t.numpy() for t in py.run(feeds)]
+    for x, y, r in zip(a, b, ref):
+        np.testing.assert_allclose(x, y, rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(x, r, rtol=1e-5, atol=1e-5)
+    it = native.interp
+    assert it.num_instructions > 10 and it.releases > 0 and it.peak_live < it.num_instructions
