@@ -104,3 +104,8 @@ class ModelAverage:
         self.step()
 
 from ..optimizer import LBFGS  # noqa: F401,E402  (reference keeps an incubate alias)
+
+
+import sys as _sys  # noqa: E402
+from . import optimizer_functional as functional  # noqa: E402
+_sys.modules[__name__ + ".functional"] = functional
