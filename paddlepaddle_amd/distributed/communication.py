@@ -9,3 +9,4 @@ from . import comm_stream as stream  # noqa: E402  (explicit sync_op / use_calc_
 
 import sys as _sys  # noqa: E402
 _sys.modules[__name__ + ".stream"] = stream
+__path__ = []  # submodules above are importable by dotted name

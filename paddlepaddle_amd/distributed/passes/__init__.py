@@ -1,0 +1,8 @@
+"""paddle.distributed.passes: pass framework + registered program passes (reference
+python/paddle/distributed/passes/__init__.py). See pass_base.py and program_passes.py."""
+from .pass_base import PassBase, PassContext, PassManager, PassType, new_pass, register_pass  # noqa: F401
+from .program_passes import (  # noqa: F401
+    AMPPass, DeadCodeEliminationPass, FP16Pass, FuseGemmEpiloguePass, GradientMergePass,
+)
+
+__all__ = ["new_pass", "PassManager", "PassContext"]

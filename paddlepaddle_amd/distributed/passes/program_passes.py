@@ -1,0 +1,280 @@
+"""Registered program passes over the traced static Program (static/program.py).
+
+* ``fuse_gemm_epilogue`` (reference passes/cpp_pass.py FuseGemmEpiloguePass, a C++ IR fusion there):
+  ``matmul(x, W) + b`` and ``fused_linear(x, W, b)`` followed by relu / gelu become ONE
+  ``ops.linear.fused_linear(x, W, b, act)`` node, so replay runs the hand-written MFMA GEMM with the bias +
+  GELU epilogue (ops/linear.py _LinearBiasGeluFn) instead of three kernels and two [M, N] round trips.
+* ``dead_code_elimination``: drops nodes that no fetch, the optimizer loss, a guard, a collective or an
+  in-place write to a parameter depends on (the Executor already prunes per fetch list; this shrinks the
+  program itself, e.g. before save_inference_model).
+* ``auto_parallel_amp`` / ``auto_parallel_fp16`` (reference auto_parallel_amp.py / auto_parallel_fp16.py):
+  insert casts so white-list ops (GEMMs, convolutions, attention) run in bf16/fp16 and black-list ops
+  (softmax, norms, losses, reductions) in fp32; parameters stay fp32 masters. Output dtypes are propagated
+  by re-running each op on meta tensors, the same way the program was traced.
+* ``auto_parallel_gradient_merge`` (reference auto_parallel_gradient_merge.py): the Executor accumulates
+  gradients over ``k_steps`` runs and applies the optimizer on the last one (``avg`` scales by 1/k).
+"""
+from __future__ import annotations
+
+import torch
+
+from .pass_base import PassBase, PassType, register_pass
+from ...static import program as P
+
+__all__ = ["FuseGemmEpiloguePass", "DeadCodeEliminationPass", "AMPPass", "FP16Pass", "GradientMergePass"]
+
+_RELU = {"f:torch.nn.functional:relu", "f:torch:relu", "m:relu"}
+_GELU = {"o:paddlepaddle_amd.ops.activation:gelu", "f:torch.nn.functional:gelu"}
+_ADD = {"m:add", "f:torch:add", "m:__add__", "m:__radd__"}
+_MATMUL = {"f:torch:matmul", "m:matmul", "f:torch:mm", "m:mm", "m:__matmul__"}
+_LINEAR = "o:paddlepaddle_amd.ops.linear:fused_linear"
+
+
+def _slot(t):
+    return t.i if isinstance(t, P._Ref) else None
+
+
+def _vars_to_slots(prog, vs):
+    out = set()
+    for v in vs or ():
+        if isinstance(v, str):
+            if v in prog._names:
+                out.add(prog._names[v])
+            continue
+        t = getattr(v, "_t", v)
+        s = prog._slot_of.get(id(t))
+        if s is not None:
+            out.add(s)
+    return out
+
+
+def _protected(prog, attrs_fetch):
+    keep = _vars_to_slots(prog, attrs_fetch)
+    keep |= set(prog._names.values())
+    if prog._optimize is not None:
+        keep.add(prog._optimize[1])
+    return keep
+
+
+def _use_counts(nodes):
+    cnt = {}
+    for n in nodes:
+        for s in P._node_reads(n):
+            cnt[s] = cnt.get(s, 0) + 1
+    return cnt
+
+
+def _shape_of(prog, t):
+    if isinstance(t, P._Ref):
+        return tuple(prog._metas[t.i].shape)
+    if isinstance(t, P._Const):
+        return tuple(t.t.shape)
+    return None
+
+
+def _act_of(n):
+    """fused_linear activation name for an activation node, or None."""
+    if n.name in _RELU and len(n.args) == 1 and not n.kwargs.get("inplace", False):
+        return "relu"
+    if n.name in _GELU:
+        approx = n.args[1] if len(n.args) > 1 else n.kwargs.get("approximate", False)
+        if isinstance(approx, str):
+            approx = approx == "tanh"
+        return "gelu" if approx else "gelu_erf"
+    return None
+
+
+@register_pass("fuse_gemm_epilogue")
+class FuseGemmEpiloguePass(PassBase):
+    _after = ("auto_parallel_amp", "auto_parallel_fp16")
+
+    def _type(self):
+        return PassType.FUSION_OPT
+
+    def _apply_single_impl(self, prog, startup, context):
+        lin = P._resolve(_LINEAR)
+        keep = _protected(prog, self.get_attr("fetch_vars"))
+        nodes = prog.nodes
+        fused = 0
+        changed = True
+        while changed:
+            changed = False
+            uses = _use_counts(nodes)
+            producer = {}
+            for i, n in enumerate(nodes):
+                if not isinstance(n, P.CFNode):
+                    for s in P._node_writes(n):
+                        producer.setdefault(s, i)
+
+            def single(s):
+                return s is not None and uses.get(s, 0) == 1 and s not in keep
+
+            for j, n in enumerate(nodes):
+                if isinstance(n, P.CFNode) or n.kind == "guard":
+                    continue
+                # matmul(x, W) + b  ->  fused_linear(x, W, b)
+                if n.name in _ADD and len(n.args) == 2 and not n.kwargs:
+                    a, b = n.args
+                    if _slot(a) is None or not isinstance(n.outs, P._Ref):
+                        a, b = b, a
+                    i = producer.get(_slot(a))
+                    if i is None or not single(_slot(a)):
+                        continue
+                    m = nodes[i]
+                    if m.name not in _MATMUL or len(m.args) != 2 or m.kwargs:
+                        continue
+                    ws, bs = _shape_of(prog, m.args[1]), _shape_of(prog, b)
+                    if ws is None or bs is None or len(ws) != 2 or bs != (ws[1],):
+                        continue
+                    nodes[j] = P.OpNode(lin, (m.args[0], m.args[1], b), {}, n.outs, "op", _LINEAR)
+                    del nodes[i]
+                    fused += 1
+                    changed = True
+                    break
+                # fused_linear(x, W, b) -> act  ->  fused_linear(x, W, b, act)
+                act = _act_of(n)
+                if act is not None:
+                    s = _slot(n.args[0])
+                    i = producer.get(s)
+                    if i is None or not single(s):
+                        continue
+                    m = nodes[i]
+                    if m.name != _LINEAR or m.kwargs or len(m.args) != 3 or not isinstance(m.outs, P._Ref):
+                        continue
+                    nodes[j] = P.OpNode(lin, tuple(m.args) + (act,), {}, n.outs, "op", _LINEAR)
+                    del nodes[i]
+                    fused += 1
+                    changed = True
+                    break
+        context.set_attr("fuse_gemm_epilogue.fused", context.get_attr("fuse_gemm_epilogue.fused", 0) + fused)
+
+
+@register_pass("dead_code_elimination")
+class DeadCodeEliminationPass(PassBase):
+    def _apply_single_impl(self, prog, startup, context):
+        need = _vars_to_slots(prog, self.get_attr("fetch_vars"))
+        if not need:
+            need = set(prog._names.values())
+        if prog._optimize is not None:
+            need.add(prog._optimize[1])
+        consts_written = lambda n: P._is_inplace(n) and n.args and isinstance(n.args[0], P._Const)  # noqa: E731
+        live = []
+        for n in reversed(prog.nodes):
+            w = P._node_writes(n)
+            if (w & need or isinstance(n, P.CFNode) or n.kind in ("guard", "comm", "grad")
+                    or consts_written(n)):
+                live.append(n)
+                need |= P._node_reads(n)
+        removed = len(prog.nodes) - len(live)
+        prog.nodes[:] = live[::-1]
+        context.set_attr("dead_code_elimination.removed", removed)
+
+
+_WHITE = {"f:torch:matmul", "m:matmul", "f:torch:mm", "m:mm", "f:torch:bmm", "f:torch:addmm", "m:__matmul__",
+          "f:torch.nn.functional:linear", "f:torch.nn.functional:conv1d", "f:torch.nn.functional:conv2d",
+          "f:torch.nn.functional:conv3d", "f:torch.nn.functional:scaled_dot_product_attention", _LINEAR,
+          "f:torch:einsum"}
+_BLACK = {"f:torch:softmax", "m:softmax", "f:torch.nn.functional:softmax", "f:torch.nn.functional:log_softmax",
+          "f:torch.nn.functional:layer_norm", "f:torch.nn.functional:batch_norm", "f:torch.nn.functional:group_norm",
+          "f:torch.nn.functional:cross_entropy", "f:torch.nn.functional:nll_loss", "f:torch:exp", "m:exp",
+          "f:torch:log", "m:log", "m:mean", "f:torch:mean", "m:sum", "f:torch:sum", "f:torch:logsumexp",
+          "f:torch.nn.functional:mse_loss", "f:torch:pow", "m:pow", "f:torch:sqrt", "f:torch:rsqrt"}
+
+
+def _is_float(t):
+    return isinstance(t, torch.Tensor) and t.is_floating_point()
+
+
+@register_pass("auto_parallel_amp")
+class AMPPass(PassBase):
+    """attrs: dtype ('bfloat16' | 'float16'), level ('o1' | 'o2'), custom_white_list, custom_black_list
+    (op names as in the program listing, e.g. 'f:torch:matmul', or bare 'matmul')."""
+
+    def _type(self):
+        return PassType.CALC_OPT
+
+    def _check_self(self):
+        return str(self.get_attr("level", "o1")).lower() in ("o1", "o2")
+
+    def _lists(self):
+        def norm(xs):
+            return {x for x in xs or ()}
+        white = set(_WHITE) | norm(self.get_attr("custom_white_list"))
+        black = (set(_BLACK) | norm(self.get_attr("custom_black_list"))) - norm(self.get_attr("custom_white_list"))
+        white -= norm(self.get_attr("custom_black_list"))
+        return white, black
+
+    @staticmethod
+    def _listed(name, lst):
+        return name in lst or name.rsplit(":", 1)[-1] in lst
+
+    def _apply_single_impl(self, prog, startup, context):
+        if any(isinstance(n, P.CFNode) for n in prog.nodes) or prog._dyn:
+            raise NotImplementedError("auto_parallel_amp: programs with control-flow blocks or dynamic dims "
+                                      "are not rewritten; use paddle.amp.auto_cast while building them")
+        from ...framework import dtype as _dt
+        low = _dt.to_torch_dtype(self.get_attr("dtype", "bfloat16"))
+        o2 = str(self.get_attr("level", "o1")).lower() == "o2"
+        white, black = self._lists()
+        meta_dev = torch.device("meta")
+        env = dict(enumerate(prog._metas))  # slot -> meta with the dtype it has after the rewrite
+        consts = [c.detach().to(meta_dev) if isinstance(c, torch.Tensor) else c for c in prog._consts]
+        new_nodes, casts = [], 0
+        to = torch.Tensor.to
+
+        def cast_arg(a, dt):
+            nonlocal casts
+            if isinstance(a, (list, tuple)):
+                return type(a)(cast_arg(v, dt) for v in a)
+            if not isinstance(a, (P._Ref, P._Const)):
+                return a
+            m = env[a.i] if isinstance(a, P._Ref) else consts[a.idx]
+            if not _is_float(m) or m.dtype == dt or m.dtype == torch.float64:
+                return a
+            with torch._C.DisableTorchFunction():
+                cm = torch.empty(m.shape, dtype=dt, device=meta_dev)
+            s = prog._new_slot(cm)
+            env[s] = cm
+            new_nodes.append(P.OpNode(to, (a, dt), {}, P._Ref(s), "torch", "m:to"))
+            casts += 1
+            return P._Ref(s)
+
+        for n in prog.nodes:
+            if n.kind in ("op", "torch") and n.outs is not None:
+                if self._listed(n.name, black):
+                    n.args = cast_arg(n.args, torch.float32)
+                elif self._listed(n.name, white) or o2:
+                    n.args = cast_arg(n.args, low)
+            new_nodes.append(n)
+            if n.outs is not None and n.kind in ("op", "torch"):
+                with torch._C.DisableTorchFunction(), torch.no_grad():
+                    out = n.func(*P._materialize(n.args, env, consts, meta_dev),
+                                 **P._materialize(n.kwargs, env, consts, meta_dev))
+                P._assign(n.outs, out, env)
+        prog.nodes[:] = new_nodes
+        context.set_attr("auto_parallel_amp.casts", casts)
+
+
+@register_pass("auto_parallel_fp16")
+class FP16Pass(AMPPass):
+    """The reference's pure-fp16 (O2) pass: every op that is not black-listed runs in the low dtype."""
+
+    def _apply_single_impl(self, prog, startup, context):
+        self._attrs.setdefault("level", "o2")
+        self._attrs.setdefault("dtype", "float16")
+        super()._apply_single_impl(prog, startup, context)
+
+
+@register_pass("auto_parallel_gradient_merge")
+class GradientMergePass(PassBase):
+    def _type(self):
+        return PassType.CALC_OPT
+
+    def _check_self(self):
+        return int(self.get_attr("k_steps", 1)) >= 1
+
+    def _apply_single_impl(self, prog, startup, context):
+        if prog._optimize is None:
+            raise ValueError("auto_parallel_gradient_merge needs a program with optimizer.minimize(loss)")
+        prog._grad_merge = (int(self.get_attr("k_steps", 1)), bool(self.get_attr("avg", True)))
+        prog._gm_count = 0

@@ -12,6 +12,29 @@ from ..framework.tensor import Tensor
 
 _excluded = set()
 _masks = {}
+# layer-type name -> pruning function (weight ndarray, m, n, mask_algo, param_name) -> (pruned, mask);
+# None = the default n:m mask of create_mask (reference supported_layer_list.py)
+_supported = {"linear": None, "conv2d": None}
+
+
+def _snake(name):
+    import re
+    return re.sub(r"(?<!^)(?=[A-Z])", "_", name).lower()
+
+
+def add_supported_layer(layer, pruning_func=None):
+    """Register a layer type (name, class or instance) whose weights prune_model should sparsify, optionally with
+    its own pruning function ``(weight, m, n, mask_algo, param_name) -> (pruned_weight, mask)``."""
+    from ..nn import Layer
+    if isinstance(layer, str):
+        name = layer
+    elif isinstance(layer, Layer):
+        name = _snake(type(layer).__name__)
+    elif isinstance(layer, type) and issubclass(layer, Layer):
+        name = _snake(layer.__name__)
+    else:
+        raise TypeError(f"add_supported_layer expects a name, Layer subclass or instance, got {type(layer)}")
+    _supported[name] = pruning_func
 
 
 def calculate_density(x):
@@ -54,19 +77,29 @@ def reset_excluded_layers(main_program=None):
 
 
 def _prunable(layer):
-    from .. import nn
     out = []
     for name, sub in layer.named_sublayers(include_self=True):
-        if isinstance(sub, (nn.Linear, nn.Conv2D)) and sub.weight.name not in _excluded and name not in _excluded:
-            out.append(sub.weight)
+        kind = _snake(type(sub).__name__)
+        w = getattr(sub, "weight", None)
+        if kind in _supported and w is not None and w.name not in _excluded and name not in _excluded:
+            out.append((w, _supported[kind]))
     return out
 
 
 @no_grad()
 def prune_model(model, n=2, m=4, mask_algo="mask_1d", with_mask=True):
     res = {}
-    for w in _prunable(model):
+    for w, fn in _prunable(model):
         t = w._t
+        if fn is not None:  # user pruning function on the host copy
+            import numpy as np
+            pruned, mk = fn(t.detach().float().cpu().numpy(), m, n, mask_algo, w.name)
+            t.copy_(torch.as_tensor(np.asarray(pruned), dtype=t.dtype, device=t.device))
+            mk = torch.as_tensor(np.asarray(mk) != 0, device=t.device)
+            if with_mask:
+                _masks[id(w)] = (w, mk)
+            res[w.name] = mk
+            continue
         if t.dim() == 4:  # conv [out, in, kh, kw] -> group along in
             mk = create_mask(t.permute(1, 2, 3, 0).reshape(t.shape[1] * t.shape[2] * t.shape[3], t.shape[0]), n, m)
             mk = mk.reshape(t.shape[1], t.shape[2], t.shape[3], t.shape[0]).permute(3, 0, 1, 2)

@@ -109,3 +109,4 @@ from ..optimizer import LBFGS  # noqa: F401,E402  (reference keeps an incubate a
 import sys as _sys  # noqa: E402
 from . import optimizer_functional as functional  # noqa: E402
 _sys.modules[__name__ + ".functional"] = functional
+__path__ = []  # submodules above are importable by dotted name

@@ -196,3 +196,4 @@ functional.subm_conv3d_igemm = functional.subm_conv3d
 import sys as _sys  # noqa: E402
 # `import paddle.sparse.nn.functional as F` works like in the reference (a namespace object as module)
 _sys.modules[__name__ + ".functional"] = functional
+__path__ = []  # submodules above are importable by dotted name

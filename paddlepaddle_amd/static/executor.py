@@ -299,9 +299,19 @@ class Executor:
             P.run_plan(prog, plan, env, dev, sym_n=sym_n)
         if opt is not None:
             optimizer, ls = opt
-            optimizer.clear_grad(set_to_zero=False)
-            env[ls].backward()
-            optimizer.step()
+            gm = getattr(prog, "_grad_merge", None)  # (k_steps, avg) from auto_parallel_gradient_merge
+            if gm is None:
+                optimizer.clear_grad(set_to_zero=False)
+                env[ls].backward()
+                optimizer.step()
+            else:
+                k, avg = gm
+                if prog._gm_count % k == 0:
+                    optimizer.clear_grad(set_to_zero=False)
+                (env[ls] / k if avg else env[ls]).backward()
+                prog._gm_count += 1
+                if prog._gm_count % k == 0:
+                    optimizer.step()
         outs = []
         for s in fetch:
             t = env[s]

@@ -183,3 +183,46 @@ def test_minimize_bfgs_and_lbfgs_match_scipy():
     ok, _, x, _, _, H = minimize_bfgs(quad, paddle.zeros([6], dtype="float64"), dtype="float64")
     np.testing.assert_allclose(x.numpy(), np.linalg.solve(A, b), atol=1e-6)
     np.testing.assert_allclose(H.numpy(), np.linalg.inv(A), atol=5e-2)
+
+
+def test_asp_add_supported_layer_custom_pruning():
+    import numpy as np
+    import paddlepaddle_amd as paddle
+    from paddlepaddle_amd.incubate import asp
+
+    class MyLayer(paddle.nn.Layer):
+        def __init__(self):
+            super().__init__()
+            self.weight = self.create_parameter([8, 8])
+
+        def forward(self, x):
+            return x @ self.weight
+
+    calls = []
+
+    def prune(w, m, n, algo, name):  # keep the first n of every m along rows (a custom pattern)
+        calls.append(name)
+        mask = np.zeros_like(w)
+        mask[:, ::m] = 1
+        return w * mask, mask
+
+    net = paddle.nn.Sequential(MyLayer(), paddle.nn.Linear(8, 8))
+    assert len(asp._prunable(net)) == 1  # only the Linear before registration
+    asp.add_supported_layer(MyLayer, prune)
+    try:
+        assert asp._snake("MyLayer") == "my_layer" and len(asp._prunable(net)) == 2
+        masks = asp.prune_model(net, n=2, m=4)
+        assert calls == [net[0].weight.name]
+        w = net[0].weight.numpy()
+        assert (w[:, 1::4] == 0).all() and (w[:, ::4] != 0).any()
+        assert asp.check_sparsity(net[1].weight, 2, 4)
+        assert len(masks) == 2
+    finally:
+        asp._supported.pop("my_layer", None)
+
+
+def test_incubate_distributed_fleet_recompute_exports():
+    import importlib
+    mod = importlib.import_module("paddlepaddle_amd.incubate.distributed.fleet")
+    from paddlepaddle_amd.distributed.fleet.recompute import recompute_sequential
+    assert mod.recompute_sequential is recompute_sequential and callable(mod.recompute_hybrid)
