@@ -876,25 +876,25 @@ class StaticEngine:
             if st[2] is not None:
                 losses.append(st[2].detach().float().reshape(()))
             states[mb] = st
-        if self.schedule == "FTHENB" or nst == 1:
-            for mb in range(n):
-                fwd(mb)
-            for mb in range(n):
+        from ...ops import linear as LIN
+        from ...parallel.pp_schedules import schedule as _schedule
+        mode = "FTHENB" if nst == 1 and self.schedule != "ZBH1" else self.schedule
+        wq = {}
+        for kind, mb in _schedule(mode, nst, s, n):  # 1F1B / FThenB / ZBH1 job list of this stage
+            if kind == "F":
+                if mode == "ZBH1":
+                    with LIN.zero_bubble_forward():
+                        fwd(mb)
+                else:
+                    fwd(mb)
+            elif kind == "B" and mode == "ZBH1":
+                q = wq[mb] = []
+                with LIN.defer_weight_grads(q):
+                    self._backward_mb(mb, states.pop(mb), p2p)
+            elif kind == "B":
                 self._backward_mb(mb, states.pop(mb), p2p)
-        else:  # 1F1B: warm-up forwards, then one forward / one backward, then the cool-down backwards
-            warm = min(nst - s - 1, n)
-            fi = bi = 0
-            for _ in range(warm):
-                fwd(fi)
-                fi += 1
-            while fi < n:
-                fwd(fi)
-                fi += 1
-                self._backward_mb(bi, states.pop(bi), p2p)
-                bi += 1
-            while bi < n:
-                self._backward_mb(bi, states.pop(bi), p2p)
-                bi += 1
+            else:
+                LIN.apply_weight_grads(wq.pop(mb))
         p2p.join()
         loss = torch.stack(losses).mean() if losses else torch.zeros((), device=self.dev)
         if nst > 1:  # every rank reports the loss of the last stage

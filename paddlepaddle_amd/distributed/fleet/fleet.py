@@ -190,7 +190,7 @@ class _Fleet:
             return self._sharded_model
         if mode == ParallelMode.PIPELINE_PARALLEL:
             from ...parallel.pipeline import (PipelineParallel, PipelineParallelWithInterleave,
-                                              PipelineParallelWithInterleaveFthenB)
+                                              PipelineParallelWithInterleaveFthenB, PipelineParallelZeroBubble)
             if getattr(model, "get_num_virtual_stages", lambda: 1)() > 1:
                 # reference fleet/model.py:160-178: interleaved 1F1B when accumulate_steps >= 2 * pp,
                 # all-forward-then-all-backward when pp <= accumulate_steps < 2 * pp
@@ -201,6 +201,8 @@ class _Fleet:
                 if pp <= acc:
                     return PipelineParallelWithInterleaveFthenB(model, hcg, self._strategy)
                 raise ValueError(f"The accumulate_steps({acc}) should be greater than or equal to pp_degree({pp})")
+            if str((self._strategy.pipeline_configs or {}).get("schedule_mode", "1F1B")).upper() == "ZBH1":
+                return PipelineParallelZeroBubble(model, hcg, self._strategy)
             return PipelineParallel(model, hcg, self._strategy)
         if mode == ParallelMode.TENSOR_PARALLEL:
             return TensorParallel(model, hcg, self._strategy)

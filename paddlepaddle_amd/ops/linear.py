@@ -201,6 +201,64 @@ def _wgrad(x2, dy2, acc=None):
     return acc.addmm_(xt, dy2)
 
 
+# ---------------------------------------------------------------------------------------------
+# Zero-bubble pipelining (parallel/pp_schedules.py ZBH1): the backward of a micro-batch is split into B
+# (input gradients: on the critical path to the previous stage) and W (weight gradients: deferrable into
+# the pipeline's cool-down bubbles). Inside ``defer_weight_grads(q)`` a linear's backward computes dX and
+# the bias gradient and appends (weight, x, dY) to ``q`` instead of running the dW GEMM;
+# ``apply_weight_grads(q)`` runs those GEMMs later (same main-grad / accumulate paths, then the weight's
+# post-accumulate hooks). ``zero_bubble_forward()`` routes every linear through the deferrable autograd
+# function for the forwards of such a schedule (off the HIP path a linear is otherwise a plain addmm).
+import contextlib  # noqa: E402
+import threading  # noqa: E402
+
+_ZB = threading.local()
+
+
+@contextlib.contextmanager
+def defer_weight_grads(queue):
+    prev = getattr(_ZB, "queue", None)
+    _ZB.queue = queue
+    try:
+        yield queue
+    finally:
+        _ZB.queue = prev
+
+
+@contextlib.contextmanager
+def zero_bubble_forward(enable=True):
+    prev = getattr(_ZB, "route", False)
+    _ZB.route = enable
+    try:
+        yield
+    finally:
+        _ZB.route = prev
+
+
+def apply_weight_grads(queue):
+    """Run the deferred weight-gradient GEMMs of ``queue`` (in order) and clear it."""
+    for w, x2, dy2 in queue:
+        ent = _main_grad_of(w)
+        if ent is not None and ent[1].dtype == dy2.dtype:
+            _wgrad(x2, dy2, acc=ent[1])
+            ent[2](w)
+            continue
+        if w.grad_fn is not None:
+            # the linear read a derived weight (a cast / TP slice recorded in the program): dW flows back
+            # through that chain to the parameter (B never entered it, so its saved tensors are intact)
+            torch.autograd.backward(w, _wgrad(x2, dy2))
+            continue
+        if w.grad is None:
+            w.grad = _wgrad(x2, dy2).to(w.dtype)
+        elif w.grad.dtype == dy2.dtype and w.grad.is_contiguous():
+            _wgrad(x2, dy2, acc=w.grad)
+        else:
+            w.grad.add_(_wgrad(x2, dy2))
+        for h in (getattr(w, "_post_accumulate_grad_hooks", None) or {}).values():
+            h(w)
+    queue.clear()
+
+
 def _mm_grads(x2, w, dy2, need_x, need_w, dx_hook=None):
     """dX first, then dW. ``dx_hook(dx)`` (tensor parallelism: the column-parallel layer's dX all-reduce)
     starts an asynchronous collective on dX right after its GEMM and returns a finisher, called once the
@@ -208,6 +266,10 @@ def _mm_grads(x2, w, dy2, need_x, need_w, dx_hook=None):
     dx = _dgrad(dy2, w) if need_x else None
     fin = dx_hook(dx) if (dx_hook is not None and dx is not None) else None
     dw = None
+    q = getattr(_ZB, "queue", None)
+    if need_w and q is not None:  # zero-bubble B step: the dW GEMM runs later, in a W step
+        q.append((w, x2, dy2))
+        need_w = False
     if need_w:
         ent = _main_grad_of(w)
         if ent is not None and ent[1].dtype == dy2.dtype:
@@ -315,6 +377,18 @@ def _hip_linear_ok(x, w, b):
 def fused_linear(x, w, b=None, act=None, dx_hook=None):
     """y = act(x @ w + b). ``dx_hook``: see _mm_grads (runs on the input gradient in backward)."""
     hip = _hip_linear_ok(x, w, b)
+    if not hip and getattr(_ZB, "route", False) and w.dim() == 2 and torch.is_grad_enabled():
+        # zero-bubble forward off the HIP path: the deferrable autograd function, activation applied after
+        y = _LinearFn.apply(x, w, b, dx_hook)
+        if act is None:
+            return y
+        if act in ("gelu", "gelu_tanh", "gelu_approximate"):
+            return gelu(y, approximate=True)
+        if act == "gelu_erf":
+            return gelu(y, approximate=False)
+        if act == "relu":
+            return F.relu(y)
+        raise ValueError(f"unsupported activation {act}")
     if dx_hook is not None and not (hip and (act is None or (act in ("gelu", "gelu_tanh", "gelu_approximate")
                                                              and b is not None))):
         x = _GradHook.apply(x, dx_hook)  # not a HIP linear: the hook runs on the incoming gradient

@@ -314,6 +314,40 @@ class PipelineParallel(nn.Layer):
         return self._layers.parameters(include_sublayers)
 
 
+class PipelineParallelZeroBubble(PipelineParallel):
+    """1F1B with the backward split into input-gradient (B) and deferred weight-gradient (W) jobs — the
+    reference's ZBH1 schedule (distributed/passes/pipeline_scheduler_pass/pipeline_zero_bubble.py:61), picked
+    by fleet for ``pipeline_configs["schedule_mode"] = "ZBH1"``. Job order: parallel/pp_schedules.py zbh1;
+    the W jobs run the linears' dW GEMMs recorded during B (ops/linear.py defer_weight_grads)."""
+
+    def forward_backward_pipeline(self, data, scaler=None):
+        from ..ops import linear as LIN
+        from .pp_schedules import zbh1
+        inputs, labels = (data if isinstance(data, (list, tuple)) and len(data) == 2 else (data, None))
+        n = self.accumulate_steps
+        mb_in = self._split(inputs) if self.is_first else [None] * n
+        mb_lb = self._split(labels) if (self.is_last and labels is not None) else [None] * n
+        store, wq, losses = {}, {}, []
+        self.jobs = zbh1(self.num_stages, self.stage_id, n)
+        self.deferred_wgrads = 0
+        for kind, mb in self.jobs:
+            if kind == "F":
+                with LIN.zero_bubble_forward():
+                    x, y = self._forward_step(mb_in[mb], mb_lb[mb], mb)
+                store[mb] = (x, y)
+                if self.is_last:
+                    losses.append(y)
+            elif kind == "B":
+                q = []
+                with LIN.defer_weight_grads(q):
+                    self._backward_step(*store.pop(mb), mb)
+                wq[mb] = q
+                self.deferred_wgrads += len(q)
+            else:
+                LIN.apply_weight_grads(wq.pop(mb))
+        return self._finish(losses)
+
+
 _DT_CODE = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2, torch.int64: 3, torch.int32: 4, torch.bool: 5}
 _CODE_DT = {v: k for k, v in _DT_CODE.items()}
 

@@ -1,0 +1,83 @@
+"""Pipeline schedules as per-stage job lists (reference: distributed/passes/pipeline_scheduler_pass/
+pipeline_1f1b.py, pipeline_fthenb.py, pipeline_zero_bubble.py:61 ZBH1 — job lists of forward / backward /
+backward_b / backward_w per stage).
+
+A job is (kind, micro_batch) with kind "F" (forward), "B" (backward: input gradients, and weight gradients
+too unless the schedule splits them) or "W" (the deferred weight-gradient GEMMs of a micro-batch; see
+ops/linear.py defer_weight_grads). Both pipeline engines (parallel/pipeline.py dygraph PipelineParallel and
+distributed/auto_parallel/static_engine.py) execute these lists.
+
+ZBH1 (zero bubble, "handcrafted 1"): 1F1B order for F and B, with W split off. During the steady phase a
+stage keeps at most ``warm = stages - stage - 1`` W jobs pending (the same activation bound as 1F1B: each
+pending W holds one micro-batch's linear inputs and output gradients); in the cool-down every B is followed
+by one W, and the remaining W jobs run after the last B. The cool-down bubbles of 1F1B — a stage waiting
+for the next output gradient from downstream — are filled with weight-gradient GEMMs, and the gradient
+reaches the previous stage one W earlier per hop than with a fused backward.
+"""
+from __future__ import annotations
+
+__all__ = ["schedule", "fthenb", "one_f_one_b", "zbh1", "SCHEDULES"]
+
+
+def fthenb(n_stages, stage, n_mb):
+    return [("F", i) for i in range(n_mb)] + [("B", i) for i in range(n_mb)]
+
+
+def one_f_one_b(n_stages, stage, n_mb):
+    warm = min(n_stages - stage - 1, n_mb)
+    out = [("F", i) for i in range(warm)]
+    fi, bi = warm, 0
+    while fi < n_mb:
+        out += [("F", fi), ("B", bi)]
+        fi += 1
+        bi += 1
+    out += [("B", i) for i in range(bi, n_mb)]
+    return out
+
+
+def zbh1(n_stages, stage, n_mb):
+    warm = min(n_stages - stage - 1, n_mb)
+    out = [("F", i) for i in range(warm)]
+    pending = []
+    fi, bi = warm, 0
+    while fi < n_mb:
+        out += [("F", fi), ("B", bi)]
+        pending.append(bi)
+        fi += 1
+        bi += 1
+        if len(pending) > warm:
+            out.append(("W", pending.pop(0)))
+    while bi < n_mb:
+        out.append(("B", bi))
+        pending.append(bi)
+        bi += 1
+        out.append(("W", pending.pop(0)))
+    out += [("W", i) for i in pending]
+    return out
+
+
+SCHEDULES = {"FTHENB": fthenb, "1F1B": one_f_one_b, "ZBH1": zbh1}
+
+
+def schedule(mode, n_stages, stage, n_mb):
+    fn = SCHEDULES.get(str(mode).upper())
+    if fn is None:
+        raise ValueError(f"unknown pipeline schedule {mode!r}; one of {sorted(SCHEDULES)}")
+    return fn(n_stages, stage, n_mb)
+
+
+def check(jobs, n_mb, split_w):
+    """Validity of one stage's job list: every micro-batch forwarded once, backward after its forward, W after
+    its B (and present exactly when the schedule splits weight gradients)."""
+    seen = {}
+    for pos, (k, mb) in enumerate(jobs):
+        if (k, mb) in seen:
+            raise AssertionError(f"duplicate job {(k, mb)}")
+        seen[(k, mb)] = pos
+    for mb in range(n_mb):
+        assert seen[("F", mb)] < seen[("B", mb)], mb
+        if split_w:
+            assert seen[("B", mb)] < seen[("W", mb)], mb
+        else:
+            assert ("W", mb) not in seen
+    return True

@@ -115,6 +115,7 @@ def _reference():
     ((2, 1, 2), 2, "1F1B"),     # pipeline x tensor parallel
     ((4, 1, 2), 4, "1F1B"),     # the reference's PP4 x TP2 configuration, 8 ranks
     ((2, 2, 2), 2, "FThenB"),   # pipeline x data x tensor parallel, 8 ranks
+    ((2, 1, 2), 4, "ZBH1"),     # zero-bubble: weight gradients deferred into the cool-down
 ])
 def test_static_auto_parallel_llama_matches_single_process(shape, acc, schedule):
     ref = _reference()

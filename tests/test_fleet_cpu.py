@@ -12,13 +12,13 @@ import torch
 from test_distributed_cpu import ROOT, _data, _setup, _spawn
 
 
-def _fleet_init(paddle, acc=2, **hc):
+def _fleet_init(paddle, acc=2, schedule="1F1B", **hc):
     from paddlepaddle_amd.distributed import fleet
     s = fleet.DistributedStrategy()
     cfg = dict(dp_degree=1, mp_degree=1, pp_degree=1)
     cfg.update(hc)
     s.hybrid_configs = cfg
-    s.pipeline_configs = {"accumulate_steps": acc, "micro_batch_size": 2}
+    s.pipeline_configs = {"accumulate_steps": acc, "micro_batch_size": 2, "schedule_mode": schedule}
     fleet.init(is_collective=True, strategy=s)
     return fleet
 
@@ -119,11 +119,11 @@ def _pp_full_params(paddle):
     return layers
 
 
-def _pp_worker(rank, world, port, q):
+def _pp_worker(rank, world, port, q, schedule="1F1B"):
     paddle = _setup(rank, world, port)
     from paddlepaddle_amd.parallel.pipeline import PipelineLayer
     full = _pp_full_params(paddle)
-    fleet = _fleet_init(paddle, pp_degree=2)
+    fleet = _fleet_init(paddle, pp_degree=2, schedule=schedule)
     pl = PipelineLayer(_mlp_descs(paddle), num_stages=2, loss_fn=_mse)
     lo = pl.segment_parts[pl._stage_id]
     with torch.no_grad():
@@ -137,11 +137,16 @@ def _pp_worker(rank, world, port, q):
     losses = [float(model.train_batch([paddle.Tensor(x), paddle.Tensor(y)], opt)) for _ in range(3)]
     ev = model.eval_batch([paddle.Tensor(x), paddle.Tensor(y)], compute_loss=True)
     params = {f"{lo + i}.{k}": v.numpy() for i, f in enumerate(pl.run_function) for k, v in f.state_dict().items()}
+    if schedule == "ZBH1":  # weight gradients really were deferred into W jobs
+        from paddlepaddle_amd.parallel.pipeline import PipelineParallelZeroBubble
+        assert type(model) is PipelineParallelZeroBubble and model.deferred_wgrads > 0
+        assert any(k == "W" for k, _ in model.jobs)
     q.put((rank, losses, params, None if isinstance(ev, list) else float(ev)))
     paddle.distributed.barrier()
 
 
-def test_pipeline_1f1b_matches_single_process():
+@pytest.mark.parametrize("schedule", ["1F1B", "ZBH1"])
+def test_pipeline_1f1b_matches_single_process(schedule):
     sys.path.insert(0, ROOT)
     os.environ["PADDLE_AMD_FORCE_CPU"] = "1"
     import paddlepaddle_amd as paddle
@@ -169,7 +174,8 @@ def test_pipeline_1f1b_matches_single_process():
         ref_eval = 0.5 * (float(_mse(fwd(paddle.Tensor(x[:4])), paddle.Tensor(y[:4]))) +
                           float(_mse(fwd(paddle.Tensor(x[4:])), paddle.Tensor(y[4:]))))
 
-    res = _spawn(_pp_worker)
+    import functools
+    res = _spawn(functools.partial(_pp_worker, schedule=schedule))
     (_, l0, p0, _), (_, l1, p1, ev1) = res
     np.testing.assert_allclose(l0, ref, rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(l1, ref, rtol=1e-5, atol=1e-6)
