@@ -367,8 +367,14 @@ class StaticFunction:
 
 
 def to_static(function=None, input_spec=None, build_strategy=None, backend=None, full_graph=True, **kwargs):
+    """``full_graph=True`` (default here): whole-function trace into one Program (graph breaks become guarded
+    variants). ``full_graph=False``: the bytecode translator (jit/sot: guards on Python-level inputs, replayed
+    side effects, graph breaks at print / not_to_static calls)."""
     def deco(fn):
         from ..nn.layer.layers import Layer
+        if not full_graph and input_spec is None:
+            from .sot import symbolic_translate
+            return symbolic_translate(fn)
         if isinstance(fn, Layer):
             sf = StaticFunction(type(fn).forward, input_spec, build_strategy, backend, full_graph, instance=fn)
             fn.__dict__["forward"] = sf
@@ -590,3 +596,5 @@ def set_code_level(level=100, also_to_stdout=False):
 
 def set_verbosity(level=0, also_to_stdout=False):
     pass
+
+from . import sot  # noqa: E402,F401  (bytecode translator: paddle.jit.sot.symbolic_translate)

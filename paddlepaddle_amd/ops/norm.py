@@ -18,6 +18,8 @@ def _finalize_parts(pa, pb, dta, dtb, nparts, cols, params=(None, None)):
     one HIP launch for both instead of a reduction + a cast each. A parameter whose gradient buffer is
     registered for in-place accumulation (ops.linear.register_main_grad) gets the sum added straight into
     that buffer (no separate autograd accumulation pass); None is returned for it."""
+    if pa is None and pb is None:  # a norm without affine weight and bias
+        return None, None
     dev = (pa if pa is not None else pb).device
     if L.has("pa_reduce_parts") and all(d in L._DT for d in (dta, dtb) if d is not None):
         from .linear import _vector_main_grad

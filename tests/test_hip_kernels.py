@@ -70,6 +70,24 @@ def test_layer_norm(dt, cols):
     torch.testing.assert_close(b.grad.float(), br.grad, atol=_tol(dt) * 60, rtol=_tol(dt) * 4)
 
 
+@pytest.mark.parametrize("op", ["layer_norm", "rms_norm"])
+def test_norm_without_affine_params(op):
+    """weight = bias = None (paddle.nn.functional.layer_norm(x, shape)): the kernels take null pointers and
+    the backward produces no parameter gradients."""
+    torch.manual_seed(2)
+    x = torch.randn(33, 512, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = ops.layer_norm(x, None, None, 1e-5) if op == "layer_norm" else ops.rms_norm(x, None, 1e-6)
+    xr = x.detach().float().requires_grad_(True)
+    yr = F.layer_norm(xr, (512,), None, None, 1e-5) if op == "layer_norm" else \
+        xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6)
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    _lib_loaded(f"pa_{op}_fwd", f"pa_{op}_bwd")
+    torch.testing.assert_close(y.float(), yr, atol=0.05, rtol=0.02)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=0.1, rtol=0.04)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("cols", [8, 128, 4096, 50304])
 def test_softmax(dt, cols):

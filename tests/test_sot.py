@@ -1,0 +1,243 @@
+"""Bytecode-level dy2static (paddle.jit.sot; reference python/paddle/jit/sot/ and test/sot/): every translated
+function must give the eager result, replay side effects and graph breaks on every call, re-translate when a
+guarded Python input changes, and train (gradients through the replayed program)."""
+import warnings
+
+import numpy as np
+import pytest
+
+import paddlepaddle_amd as paddle
+from paddlepaddle_amd.jit import sot
+
+COUNTER = 0
+SCALE = 2.0
+
+
+def _x(seed=0, shape=(3, 4)):
+    return paddle.to_tensor(np.random.RandomState(seed).randn(*shape).astype("float32"))
+
+
+class Block(paddle.nn.Layer):
+    def __init__(self):
+        super().__init__()
+        self.fc = paddle.nn.Linear(4, 4)
+        self.act = "relu"
+
+    def forward(self, x):
+        y = self.fc(x)
+        return paddle.nn.functional.relu(y) if self.act == "relu" else paddle.tanh(y)
+
+
+class Base(paddle.nn.Layer):
+    def forward(self, x):
+        return x * 2
+
+
+class Net(Base):
+    def __init__(self):
+        super().__init__()
+        self.blocks = paddle.nn.LayerList([Block(), Block()])
+        self.hist = []
+
+    def helper(self, x, k=1):
+        return [x + i for i in range(k)]
+
+    def forward(self, x, k=2):
+        for b in self.blocks:
+            x = b(x)
+        parts = self.helper(x, k=k)
+        head, *rest = parts
+        out = super().forward(head) + sum(rest)
+        self.hist.append(len(rest))
+        self.last = out
+        return {"out": out, "tag": f"k={k}"}
+
+
+def test_layer_translation_matches_eager_and_replays_effects():
+    paddle.seed(0)
+    net = Net()
+    ref = Net()
+    ref.set_state_dict(net.state_dict())
+    f = sot.symbolic_translate(net)
+    for it in range(3):
+        x = _x(it)
+        got = f(x)
+        want = ref(x)
+        np.testing.assert_allclose(got["out"].numpy(), want["out"].numpy(), rtol=1e-6)
+        assert got["tag"] == "k=2"
+    info = net.forward.last_info
+    assert info["inlined_frames"] >= 5 and info["side_effects"] == 2 and info["breaks"] == 0
+    assert net.hist == [1, 1, 1]
+    np.testing.assert_allclose(net.last.numpy(), got["out"].numpy())  # setattr replayed with the new value
+    assert len(net.forward.translations) == 1
+
+
+def test_guards_retranslate_on_python_input_changes():
+    paddle.seed(1)
+    net = Net()
+    ref = Net()
+    ref.set_state_dict(net.state_dict())
+    f = sot.symbolic_translate(net)
+    x = _x(3)
+    f(x)
+    net.blocks[1].act = ref.blocks[1].act = "tanh"  # attribute of an inlined sub-layer
+    np.testing.assert_allclose(f(x)["out"].numpy(), ref(x)["out"].numpy(), rtol=1e-6)
+    np.testing.assert_allclose(f(x, k=3)["out"].numpy(), ref(x, k=3)["out"].numpy(), rtol=1e-6)
+    assert len(net.forward.translations) == 3
+    assert any("act" in g for g in net.forward.last_info["guards"])
+
+
+def test_globals_closures_and_global_side_effects():
+    global SCALE, COUNTER
+    COUNTER = 0
+    bias = [1.0]
+
+    def make(c):
+        def fn(x):
+            global COUNTER
+            COUNTER += 1
+            return x * SCALE + c
+        return fn
+    f = sot.symbolic_translate(make(bias[0]))
+    x = _x(4)
+    np.testing.assert_allclose(f(x).numpy(), x.numpy() * 2 + 1, rtol=1e-6)
+    np.testing.assert_allclose(f(x).numpy(), x.numpy() * 2 + 1, rtol=1e-6)
+    assert COUNTER == 2
+    SCALE = 5.0
+    try:
+        np.testing.assert_allclose(f(x).numpy(), x.numpy() * 5 + 1, rtol=1e-6)  # global guard
+    finally:
+        SCALE = 2.0
+    assert COUNTER == 3
+
+
+def test_counter_attribute_is_guarded_and_stays_correct():
+    class C(paddle.nn.Layer):
+        def __init__(self):
+            super().__init__()
+            self.calls = 0
+
+        def forward(self, x):
+            self.calls += 1  # read (guarded by value) then written: re-translated per value, never stale
+            return x * self.calls
+
+    c = C()
+    f = sot.symbolic_translate(c)
+    x = _x(9)
+    for i in range(1, 4):
+        np.testing.assert_allclose(f(x).numpy(), x.numpy() * i, rtol=1e-6)
+    assert c.calls == 3
+
+
+def test_graph_breaks_run_on_real_values_every_call(capsys):
+    @paddle.jit.not_to_static
+    def host_square(t):
+        return paddle.to_tensor(t.numpy() ** 2)
+
+    def fn(x):
+        y = x + 1
+        print("mean", float(y.mean().numpy()) > -100)
+        z = host_square(y)  # graph break: tensors flow out and back in
+        return z * 2
+
+    f = sot.symbolic_translate(fn)
+    for seed in range(3):
+        x = _x(10 + seed)
+        np.testing.assert_allclose(f(x).numpy(), ((x.numpy() + 1) ** 2) * 2, rtol=1e-5)
+    out = capsys.readouterr().out
+    assert out.count("mean True") == 3
+    assert fn.__name__ == f.__name__ and f.last_info["breaks"] == 3  # .numpy(), print, host_square
+    assert len(f.translations) == 1  # new data did not re-translate: the break is not specialised
+
+
+def test_data_dependent_branch_and_loops():
+    def fn(x, n):
+        acc = paddle.zeros_like(x)
+        for i in range(n):
+            acc = acc + x * i
+        if acc.mean() > 0:
+            return acc - 1
+        return acc + 1
+
+    f = sot.symbolic_translate(fn)
+    for seed, n in [(0, 3), (1, 3), (2, 4)]:
+        x = _x(seed)
+        exp = sum(x.numpy() * i for i in range(n))
+        exp = exp - 1 if exp.mean() > 0 else exp + 1
+        np.testing.assert_allclose(f(x, n).numpy(), exp, rtol=1e-5, atol=1e-6)
+
+
+def test_no_grad_block_and_training_gradients():
+    paddle.seed(2)
+    lin = paddle.nn.Linear(4, 2)
+    lin2 = paddle.nn.Linear(4, 2)
+    lin2.set_state_dict(lin.state_dict())
+
+    def loss_fn(layer, x):
+        with paddle.no_grad():
+            ref = layer(x)
+        out = layer(x)
+        return ((out - ref.detach() - 1.0) ** 2).mean(), ref
+
+    f = sot.symbolic_translate(loss_fn)
+    x = _x(5)
+    loss, ref = f(lin, x)
+    assert ref.stop_gradient and f.last_info is not None  # translated, the no_grad block replayed
+    loss.backward()
+    l2, _ = loss_fn(lin2, x)
+    l2.backward()
+    np.testing.assert_allclose(float(loss), float(l2), rtol=1e-6)
+    np.testing.assert_allclose(lin.weight.grad.numpy(), lin2.weight.grad.numpy(), rtol=1e-5)
+    lin.clear_gradients()
+    loss, _ = f(lin, x)  # replayed
+    loss.backward()
+    np.testing.assert_allclose(lin.weight.grad.numpy(), lin2.weight.grad.numpy(), rtol=1e-5)
+
+
+def test_unsupported_constructs_fall_back_to_eager():
+    def fn(x):
+        return sum(v for v in (x, x * 2))  # generator expression: inlined frame unsupported -> native call
+
+    f = sot.symbolic_translate(fn)
+    x = _x(6)
+    np.testing.assert_allclose(f(x).numpy(), x.numpy() * 3, rtol=1e-6)
+
+    def gen(x):
+        yield x
+
+    g = sot.symbolic_translate(gen)
+    with warnings.catch_warnings(record=True):
+        warnings.simplefilter("always")
+        assert next(iter(g(x))) is not None
+
+
+def test_to_static_full_graph_false_uses_bytecode_translator():
+    @paddle.jit.to_static(full_graph=False)
+    def fn(x):
+        return x * 3
+
+    assert isinstance(fn, sot.SOTFunction)
+    x = _x(7)
+    np.testing.assert_allclose(fn(x).numpy(), x.numpy() * 3, rtol=1e-6)
+
+
+def test_gpt_tiny_forward_and_grads_match_eager():
+    from paddlepaddle_amd.models.gpt import GPTConfig, GPTForPretraining
+    paddle.seed(3)
+    cfg = GPTConfig.tiny(num_hidden_layers=2, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    m = GPTForPretraining(cfg)
+    ids = paddle.to_tensor(np.random.RandomState(0).randint(0, cfg.vocab_size, (2, 16)))
+    ref = m(ids)
+    ref.mean().backward()
+    g_ref = {n: p.grad.numpy().copy() for n, p in m.named_parameters() if p.grad is not None}
+    m.clear_gradients()
+    f = sot.symbolic_translate(m)
+    for _ in range(2):
+        out = f(ids)
+        np.testing.assert_allclose(out.numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
+        m.clear_gradients()
+        out.mean().backward()
+        for n, p in m.named_parameters():
+            if n in g_ref:
+                np.testing.assert_allclose(p.grad.numpy(), g_ref[n], rtol=1e-4, atol=1e-6, err_msg=n)
+    assert m.forward.last_info is not None and len(m.forward.translations) == 1

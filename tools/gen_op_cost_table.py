@@ -135,8 +135,8 @@ def measure(dtypes=("float32", "bfloat16"), small=False, warmup=3, reps=10, devi
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                                                  "paddlepaddle_amd", "cost_model", "mi355x_op_benchmark.json"))
+    ap.add_argument("--out", default="gpurun_out/mi355x_op_benchmark.json",
+                    help="copy the result to paddlepaddle_amd/cost_model/mi355x_op_benchmark.json to ship it")
     ap.add_argument("--small", action="store_true")
     ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
