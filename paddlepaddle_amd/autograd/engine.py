@@ -1,8 +1,10 @@
 """Eager backward engine selection and the Python half of the native engine.
 
 ``FLAGS_eager_backward_engine``:
-  * ``native`` — backward()/paddle.grad run through ``_C_runtime.run_backward``
-    (csrc/runtime/autograd_engine.cpp): in-degree map over the reachable grad-node graph, ready queue,
+  * ``native`` — backward()/paddle.grad run through ``_C_autograd.run_backward``
+    (csrc/autograd/autograd_exec.cpp: C++ over the Node interface, saved tensors released as nodes run; the
+    pybind traversal csrc/runtime/autograd_engine.cpp when that extension is absent): in-degree map over the
+    reachable grad-node graph, ready queue,
     per-slot gradient sums, gradient hooks applied to the summed slot, paddle.grad pruning + capture.
     Reference: paddle/fluid/eager/backward.cc:105 (RunBackward), general_grad.h (paddle.grad).
   * ``torch`` (default) — PyTorch-ROCm's C++ autograd engine runs the same grad nodes (multi-threaded device
@@ -128,18 +130,36 @@ def _is_py(node):
 _HELPERS = (_zeros_for, _fix, _is_py)
 
 
-def _run(outs, grads, captures, create_graph):
+_EXEC = []
+
+
+def _executor():
+    """``_C_autograd`` (csrc/autograd/autograd_exec.cpp): the executor over the C++ Node interface; None when the
+    extension is not built (the pybind traversal in _C_runtime is used then)."""
+    if not _EXEC:
+        try:
+            from .. import _C_autograd
+            _EXEC.append(_C_autograd)
+        except ImportError:
+            _EXEC.append(None)
+    return _EXEC[0]
+
+
+def _run(outs, grads, ins, create_graph, retain_graph=None):
     from ..utils import native
-    roots = []
-    for t, g in zip(outs, grads):
+    for t in outs:
         if not t.requires_grad:
             raise RuntimeError("backward: the output tensor has stop_gradient=True (no grad node to start from)")
-        node, slot = _edge(t)
-        roots.append((node, slot, g))
+    keep = create_graph if retain_graph is None else bool(retain_graph)
+    ex = _executor()
     _ACTIVE[0] += 1
     try:
-        with torch.set_grad_enabled(create_graph):
-            res = native.module().run_backward(roots, captures, _HOOKS, _HELPERS)
+        if ex is not None:
+            res = ex.run_backward(list(zip(outs, grads)), list(ins), _HOOKS, keep, create_graph)
+        else:
+            roots = [(*_edge(t), g) for t, g in zip(outs, grads)]
+            with torch.set_grad_enabled(create_graph):
+                res = native.module().run_backward(roots, [_edge(t) for t in ins], _HOOKS, _HELPERS)
     finally:
         _ACTIVE[0] -= 1
     if not _ACTIVE[0]:
@@ -150,7 +170,7 @@ def _run(outs, grads, captures, create_graph):
 def backward(outs, grads, retain_graph=False):
     """Run backward from ``outs`` (torch tensors) seeded with ``grads``; leaves accumulate into ``.grad``.
     Hooks of non-leaf tensors belong to this graph and are dropped afterwards unless ``retain_graph``."""
-    _run(outs, grads, [], False)
+    _run(outs, grads, [], False, retain_graph)
     if not retain_graph:
         for k in [k for k in _HOOKS if not isinstance(k[0], _ACC)]:
             del _HOOKS[k]
@@ -159,13 +179,11 @@ def backward(outs, grads, retain_graph=False):
 _ACC = type(torch.autograd.graph.get_gradient_edge(torch.zeros(1, requires_grad=True)).node)
 
 
-def grad(outs, ins, grads, create_graph=False, allow_unused=False):
-    caps = []
+def grad(outs, ins, grads, create_graph=False, allow_unused=False, retain_graph=None):
     for t in ins:
         if not t.requires_grad:
             raise RuntimeError("paddle.grad: an input tensor has stop_gradient=True")
-        caps.append(_edge(t))
-    res = _run(outs, grads, caps, create_graph)
+    res = _run(outs, grads, ins, create_graph, retain_graph)
     for r in res:
         if r is None and not allow_unused:
             raise RuntimeError("paddle.grad: one of the inputs is not reachable from the outputs; "
