@@ -154,7 +154,20 @@ class Optimizer:
 
     # ------------------------------------------------------------------ step
     def clear_grad(self, set_to_zero=True):
+        zeroed = set()
         for p in self._parameter_list:
+            loc = getattr(p, "_dp_bucket", None)
+            if loc is not None:
+                # DataParallel's flat all-reduce bucket: the grad stays a view of it (releasing it would make
+                # the next backward allocate a fresh gradient that has to be copied back); one memset per bucket
+                bucket, j = loc
+                if id(bucket) not in zeroed:
+                    zeroed.add(id(bucket))
+                    bucket.flat.zero_()
+                v = bucket.view(j)
+                if p._t.grad is None or p._t.grad.data_ptr() != v.data_ptr():
+                    p._t.grad = v
+                continue
             if set_to_zero:
                 if p._t.grad is not None:
                     p._t.grad.zero_()

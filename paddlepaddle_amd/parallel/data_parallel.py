@@ -102,6 +102,7 @@ class DataParallel(Layer):
                 for j, p in enumerate(b.params):
                     self._param_loc[id(p)] = (bi, j)
                     p._t.grad = b.view(j)
+                    p._dp_bucket = (b, j)  # Optimizer.clear_grad keeps the bucket views (one memset per bucket)
                     p._t.register_post_accumulate_grad_hook(self._make_hook(p))
 
     def _make_hook(self, p):
