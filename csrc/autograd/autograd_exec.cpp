@@ -10,7 +10,9 @@
 // operator() to run a node (Python-defined functions re-enter Python only inside their own apply), the input
 // metadata to validate each produced gradient (dtype cast, sum-reduction of broadcast dims), release_variables()
 // right after a node ran when the graph is not retained (saved activations are freed as the backward proceeds),
-// and the node's tensor pre-hooks / node hooks (retain_grads is the framework's own hook: engine.py retain). It runs on the calling thread and the
+// and the node-level pre / post hooks. Tensor hooks are the framework's own table (engine.py register_grad_hook /
+// retain: they are also registered with torch for backward passes that go through torch's engine, so torch's
+// tensor hook lists are not run here). It runs on the calling thread and the
 // current HIP stream: no device-thread hand-off per backward pass.
 //
 // Python side: paddlepaddle_amd/autograd/engine.py (FLAGS_eager_backward_engine=native) passes the root tensors
@@ -77,8 +79,10 @@ at::Tensor fix(at::Tensor g, const Node& nx, uint32_t slot) {
   if (!g.defined() || slot >= nx.num_inputs()) return g;
   const auto& m = nx.input_metadata(slot);
   if (m.was_default_constructed()) return g;
-  if (!m.is_nested_tensor() && !m.is_tensor_subclass() && !m.is_same_shape(g)) {
-    if (m.is_expandable_to_shape(g)) g = m.reduce_grad(g);
+  if (!m.is_same_shape(g)) {
+    if (!m.is_expandable_to_shape(g))
+      throw std::runtime_error(m.incompatible_shape_error_message(slot, g).str());
+    g = m.reduce_grad(g);
   }
   auto want = m.grad_dtype();
   at::ScalarType st = want.has_value() ? *want : c10::typeMetaToScalarType(m.dtype());
@@ -192,7 +196,6 @@ py::list run_backward(py::list roots, py::list captures, py::dict hooks, bool ke
       for (auto& b : nd.buf) any = any || b.defined();
       if (any) {
         variable_list inputs = std::move(nd.buf);
-        for (const auto& h : fn.tensor_pre_hooks()) inputs = (*h)(inputs);
         for (const auto& h : fn.pre_hooks()) inputs = (*h)(inputs);
         if (!keep_graph) fn.will_release_variables();
         outs = fn(std::move(inputs));

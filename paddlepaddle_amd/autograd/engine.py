@@ -7,8 +7,9 @@
     reachable grad-node graph, ready queue,
     per-slot gradient sums, gradient hooks applied to the summed slot, paddle.grad pruning + capture.
     Reference: paddle/fluid/eager/backward.cc:105 (RunBackward), general_grad.h (paddle.grad).
-  * ``torch`` (default) — PyTorch-ROCm's C++ autograd engine runs the same grad nodes (multi-threaded device
-    queues, node-level hooks registered by DataParallel / sharding for comm overlap).
+  * ``torch`` — PyTorch-ROCm's C++ autograd engine runs the same grad nodes (multi-threaded device queues).
+``native`` is the default (same 13B throughput as torch's engine, faster when launch-bound:
+profiles/r3_passes_costmodel.md).
 
 Grad nodes are the per-op backward functions: the autograd functions of the hand-written HIP kernels
 (ops/*.py) and ATen's derivative formulas. Gradient hooks registered with ``Tensor.register_hook`` go into a
@@ -78,7 +79,16 @@ def register_grad_hook(t, fn):
     """Gradient hook on a torch tensor under whichever engine will run its backward (torch's hook list, or
     this engine's (node, slot) table)."""
     if use_native():
-        return add_hook(t, fn)
+        # both tables: this engine applies its own (node, slot) table; a backward that some code starts through
+        # torch's engine directly (torch.autograd.backward inside recompute / pipeline schedules) runs torch's
+        # hook list. The native executor does not run torch's tensor hooks, so nothing fires twice.
+        rm = add_hook(t, fn)
+        h = t.register_hook(fn)
+
+        def remove():
+            rm()
+            h.remove()
+        return remove
     h = t.register_hook(fn)
     return h.remove
 

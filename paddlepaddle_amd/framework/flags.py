@@ -19,7 +19,7 @@ _FLAGS = {
     "FLAGS_dp_bucket_mb": 128,            # DataParallel fused all-reduce bucket (xGMI ring friendly)
     "FLAGS_sharding_bucket_mb": 256,
     "FLAGS_pir_native_interpreter": True,  # PIR programs run on the C++ interpreter (_C_interp) when every op maps
-    "FLAGS_eager_backward_engine": "torch",  # torch | native (csrc/runtime/autograd_engine.cpp RunBackward)
+    "FLAGS_eager_backward_engine": "native",  # native (csrc/autograd/autograd_exec.cpp RunBackward) | torch
     "FLAGS_gemm_backend": "auto",         # per-shape GEMM / conv backend: auto (timed) | hip | blas
     "FLAGS_sharding_stage3_keep_params": "auto",  # stage 3: keep gathered params until the optimizer step
     "FLAGS_use_autotune": True,           # time GEMM backends for shapes the tuning table does not hold

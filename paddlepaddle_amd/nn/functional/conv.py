@@ -96,6 +96,16 @@ def _convnd(n, x, weight, bias, stride, padding, dilation, groups, data_format):
             ww = ww.contiguous(memory_format=torch.channels_last)
         return fn(tt, ww, b, stride, pad, dilation, groups)
 
+    # NHWC depthwise convolutions: direct HIP kernels (ops/dwconv.py) when they measured faster than MIOpen
+    if cl and n == 2 and pre is None and groups > 1:
+        from ... import ops as _ops
+        if _ops.dwconv.eligible(x_raw, w, groups):
+            pd = (pad, pad) if isinstance(pad, int) else tuple(pad)
+            y = _ops.dwconv.depthwise_conv2d_nhwc(
+                x_raw, w, b, stride, pd, dilation,
+                lambda xx, ww: _from_cf(miopen(_to_cf(xx, data_format, n)[0], ww), cl, n))
+            if y is not None:
+                return _wrap(y)
     # NHWC 1x1 convolutions: hand-written MFMA GEMM (ops/conv.py) when it measured faster than MIOpen
     if cl and n == 2 and pre is None and stride[0] == stride[1]:
         from ... import ops as _ops
@@ -147,6 +157,15 @@ def _conv_transpose_nd(n, x, weight, bias, stride, padding, output_padding, dila
         osz = _tuple(output_size, n) if not isinstance(output_size, Tensor) else tuple(output_size._t.tolist())
         op = tuple(o - ((i - 1) * s - 2 * p + d * (k - 1) + 1) for o, i, s, p, d, k in
                    zip(osz, t.shape[2:], stride, pad, dilation, w.shape[2:]))
+    if (cl and n == 2 and groups == 1 and stride == (1, 1) and dilation == (1, 1) and op == (0, 0)
+            and all(k - 1 - q >= 0 for k, q in zip(w.shape[2:], pad)) and w.shape[2] == w.shape[3]
+            and pad[0] == pad[1] and t.is_cuda):
+        # stride-1 transposed convolution == convolution with the flipped, in/out-swapped filter and padding
+        # K-1-p: the NHWC convolution path (hand-written implicit GEMM / 1x1 GEMM kernels when they measured
+        # faster than MIOpen); the filter transform is part of the autograd graph, so dW flows back to `weight`
+        w2 = w.flip(2, 3).transpose(0, 1)
+        return _convnd(2, _wrap(_from_cf(t, cl, n)), _wrap(w2), None if b is None else _wrap(b), 1,
+                       w.shape[2] - 1 - pad[0], 1, 1, data_format)
     fn = {1: F.conv_transpose1d, 2: F.conv_transpose2d, 3: F.conv_transpose3d}[n]
     out = fn(t, w, b, stride, pad, op, groups, dilation)
     return _wrap(_from_cf(out, cl, n))
