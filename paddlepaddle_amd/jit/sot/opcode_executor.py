@@ -455,6 +455,7 @@ class Frame:
     def _getattr(self, obj, name):
         if obj.slot is not None:
             return self.tr.rt_call(getattr, [obj, V(name)], {}, "getattr")
+        obj = _anchor(obj)
         o = obj.v
         ov = self.tr.overlay.get((id(o), name))
         if ov is not None:
@@ -476,7 +477,7 @@ class Frame:
         return V(val, src)
 
     def op_STORE_ATTR(self, ins):
-        obj = self.pop()
+        obj = _anchor(self.pop())
         val = self.pop()
         if obj.src is not None:  # an object that outlives the call: replay the write
             self.tr.record_py(functools.partial(setattr, obj.v, ins.argval), [val], {}, f"setattr {ins.argval}")
@@ -940,7 +941,7 @@ class Frame:
             fwd = type(f).forward
             if "forward" in f.__dict__ or not _is_user_function(fwd) or _has_hooks(f):
                 return None
-            return fwd, V(f, fv.src)
+            return fwd, _anchor(V(f, fv.src))
         if isinstance(f, types.MethodType) and _is_user_function(f.__func__):
             self_src = fv.recv.src if fv.recv is not None else None
             return f.__func__, V(f.__self__, self_src)
@@ -992,6 +993,17 @@ for _n in Frame._BIN:
     setattr(Frame, "op_" + _n, Frame._binary)
 for _n in Frame._UN:
     setattr(Frame, "op_" + _n, Frame._unary)
+
+
+def _anchor(v):
+    """A Layer reached without a source path (e.g. through enumerate / zip of a sub-layer list) is anchored as a
+    constant source: guards on its attributes are re-read from that very object at call time, and writes to it
+    are replayed side effects, like for layers reached from the arguments."""
+    if v.src is None and v.slot is None:
+        from ...nn.layer.layers import Layer
+        if isinstance(v.v, Layer):
+            return V(v.v, Source("const", v.v), v.recv)
+    return v
 
 
 def _has_hooks(layer):

@@ -268,3 +268,24 @@ def test_sot_gpt_tiny_on_gpu_matches_eager():
                 np.testing.assert_allclose(p.grad.astype("float32").numpy(), g_ref[n], rtol=5e-2, atol=5e-3,
                                            err_msg=n)
     assert len(m.forward.translations) == 1
+
+
+def test_layers_reached_through_enumerate_are_guarded():
+    class Stack(paddle.nn.Layer):
+        def __init__(self):
+            super().__init__()
+            self.blocks = paddle.nn.LayerList([Block(), Block()])
+
+        def forward(self, x):
+            for i, b in enumerate(self.blocks):  # no source path: the layers are anchored as constants
+                x = b(x) + i
+            return x
+
+    paddle.seed(6)
+    net = Stack()
+    f = sot.symbolic_translate(net)
+    x = _x(11)
+    np.testing.assert_allclose(f(x).numpy(), Stack.forward(net, x).numpy(), rtol=1e-6)
+    net.blocks[0].act = "tanh"
+    np.testing.assert_allclose(f(x).numpy(), Stack.forward(net, x).numpy(), rtol=1e-6)
+    assert len(net.forward.translations) == 2
