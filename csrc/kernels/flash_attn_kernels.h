@@ -590,6 +590,7 @@ struct BwdArgs {
   int dropout; uint32_t keep16; float rkeep; uint32_t seed0, seed1;
   int64_t lse_s[2];
   int abl;  // measurement ablations (0 in normal runs): 1 dQ atomics dropped, 2 dQ step skipped, 4 dK/dV GEMMs skipped
+  int k16;  // 1: the 8-wave 16-keys-per-wave kernel (fa_bwd16_kernel) for D = 128 without mask / dropout
 };
 
 // delta[b,h,q] = sum_d dO * O   (delta / lse index = b * lse_s0 + h * lse_s1 + q)
@@ -1028,6 +1029,293 @@ __global__ __launch_bounds__(NW * 64, 1) void fa_bwd_kernel(BwdArgs p) {
 }
 
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// Backward, 16 keys per wave (D = 128, no mask / flashmask / dropout): 8 waves x 16 keys = the same 128-key block
+// per workgroup as fa_bwd_kernel<128, .., 4, ..>, but on v_mfma_f32_16x16x32 tiles, so a wave's dK^T / dV^T
+// accumulators are 2 x 8 x 4 fp32 registers (not 2 x 4 x 16) and its cached K / V fragments 2 x 16: the kernel fits
+// 256 registers and runs 2 waves per SIMD (the 4-wave kernel holds one, and its S / dP / softmax / LDS phases
+// serialise on it). Same math and pipeline:
+//   S = Q K^T and dP = dO V^T as [16 q][16 key] tiles (2 query tiles of a 32-query block), initialised with the
+//   row constants (-LSE/scale, -delta); P = exp2(scale*log2e*S), dS = P dP. A 16x16x32 accumulator is the B operand
+//   of the next product with the k (query) index permuted: element j of lane group g is query 4g+j (j < 4) of tile 0
+//   and 16+4g+j-4 of tile 1 — so P / dS feed dV^T += dO^T P and dK^T += Q^T dS with no lane movement; the A operands
+//   dO^T / Q^T come from ds_read_b64_tr_b16 reads of the row images at those query rows.
+//   dQ += dS K over the workgroup's 128 keys through a dS^T LDS image (rows = key, 64-byte rows), wave w owning
+//   d columns 16w..16w+15, fp32 atomics into dq_acc; software-pipelined one block behind like the 4-wave kernel.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <bool F16>
+__device__ __forceinline__ f32x4 mfma16(const Frag& a, const Frag& b, f32x4 c) {
+  if constexpr (F16) return __builtin_amdgcn_mfma_f32_16x16x32_f16(a.f, b.f, c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, c, 0, 0, 0);
+}
+
+// [rows][128 x 16-bit] image as 8-row x 32-column subtiles of 512 B (cdna_hip_programming.md T10 image (a)): row
+// reads and transposed reads of every operand above are conflict-free, and the reads of one loop are a per-lane base
+// plus immediates (a chunk step of 4 or a row step of 8 is a constant), so few address registers stay live.
+__device__ __forceinline__ int img_a(int row, int ch) {
+  return 2048 * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
+}
+
+// byte offset of the 8-byte unit (row, col4) of a [rows][32 x 16-bit] image with 64-byte rows (col4 = column / 4)
+__device__ __forceinline__ int dst_off(int row, int col4) {
+  return row * 64 + ((col4 * 8) ^ (((row >> 2) & 3) << 3));
+}
+
+template <bool F16>
+__global__ __launch_bounds__(512, 1) void fa_bwd16_kernel(BwdArgs p) {
+  constexpr int D = 128, NCH = 16, NW = 8, NT = NW * 64, BK = 128, BM = 32;
+  constexpr int KT_BYTES = BK * D * 2;
+  constexpr int QT_BYTES = BM * D * 2;
+  constexpr int DST_BYTES = BK * BM * 2;
+  constexpr int ATOMICS = 8;  // fire-and-forget dQ atomics per lane per block
+  __shared__ __attribute__((aligned(16))) char smem[2 * KT_BYTES + 2 * QT_BYTES + 2 * DST_BYTES + 2 * BM * 4];
+  char* k_lds = smem;
+  char* v_lds = smem + KT_BYTES;
+  char* q_lds = v_lds + KT_BYTES;
+  char* do_lds = q_lds + QT_BYTES;
+  char* ds_lds = do_lds + QT_BYTES;
+  float* lse_s = reinterpret_cast<float*>(ds_lds + 2 * DST_BYTES);
+  float* dlt_s = lse_s + BM;
+
+  const int nkb0 = (p.Sk + BK - 1) / BK;
+  int kb, bhk;
+  block_map((int)blockIdx.x, p.B * p.Hk, nkb0, p.grp, bhk, kb);
+  const int b = bhk / p.Hk, hk = bhk % p.Hk;
+  const int G = p.H / p.Hk;
+  int q_start = 0, k_start = 0, Sq = p.Sq, Sk = p.Sk;
+  const bool varlen = p.cu_q != nullptr;
+  if (varlen) {
+    q_start = p.cu_q[b];
+    Sq = p.cu_q[b + 1] - q_start;
+    k_start = p.cu_k[b];
+    Sk = p.cu_k[b + 1] - k_start;
+  }
+  if (kb * BK >= Sk) return;  // uniform exit
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r16 = lane & 15, kg = lane >> 4;
+  const int tq = r16 >> 2, tp = r16 & 3;  // transposed reads: block row and column quad this lane addresses
+  const int shift = Sk - Sq;
+  const int kj = kb * BK + w * 16 + r16;  // this lane's key (MFMA column of S / dP, of dK^T / dV^T)
+
+  const uint16_t* kbase = p.k + (varlen ? (int64_t)k_start * p.ks[1] : (int64_t)b * p.ks[0]) + (int64_t)hk * p.ks[2];
+  const uint16_t* vbase = p.v + (varlen ? (int64_t)k_start * p.vs[1] : (int64_t)b * p.vs[0]) + (int64_t)hk * p.vs[2];
+#pragma unroll
+  for (int i = 0; i < BK * NCH / NT; ++i) {
+    const int idx = tid + NT * i;
+    const int row = idx / NCH, ch = idx % NCH;
+    const int key = kb * BK + row;
+    uint4 val = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+    if (key < Sk) {
+      val = *reinterpret_cast<const uint4*>(kbase + (int64_t)key * p.ks[1] + ch * 8);
+      vv = *reinterpret_cast<const uint4*>(vbase + (int64_t)key * p.vs[1] + ch * 8);
+    }
+    *reinterpret_cast<uint4*>(k_lds + img_a(row, ch)) = val;
+    *reinterpret_cast<uint4*>(v_lds + img_a(row, ch)) = vv;
+  }
+  f32x4 dk_acc[8], dv_acc[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { dk_acc[dt][i] = 0.f; dv_acc[dt][i] = 0.f; }
+  __syncthreads();
+  // K^T / V^T B fragments of this wave's 16 keys: element j of group kg = d 32ks + 8kg + j
+  Frag kfr[4], vfr[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    kfr[ks].u = lds_b128(k_lds, img_a(w * 16 + r16, 4 * ks + kg));
+    vfr[ks].u = lds_b128(v_lds, img_a(w * 16 + r16, 4 * ks + kg));
+  }
+
+  int q_begin0 = 0;
+  if (p.causal) q_begin0 = max(0, kb * BK - shift);
+  q_begin0 = (q_begin0 / BM) * BM;
+  const int h0 = hk * G;
+  const int64_t dq_row0 = varlen ? (int64_t)q_start : (int64_t)b * p.Sq;
+
+  u32x4 qreg, dreg;
+  float lse_raw = 0.f, dlt_raw = 0.f;
+  bool row_ok = false, q_ok = false;
+  auto prefetch = [&](int h, int q0) {
+    const uint16_t* qbase = p.q + (varlen ? (int64_t)q_start * p.qs[1] : (int64_t)b * p.qs[0]) + (int64_t)h * p.qs[2];
+    const uint16_t* dobase =
+        p.dout + (varlen ? (int64_t)q_start * p.dos[1] : (int64_t)b * p.dos[0]) + (int64_t)h * p.dos[2];
+    const int row = tid / NCH, ch = tid % NCH;
+    const int qx = q0 + row;
+    q_ok = qx < Sq;
+    const int qc = q_ok ? qx : Sq - 1;
+    qreg = gload16_async(qbase + (int64_t)qc * p.qs[1] + ch * 8);
+    dreg = gload16_async(dobase + (int64_t)qc * p.dos[1] + ch * 8);
+    const int qr = q0 + (tid & (BM - 1));
+    row_ok = qr < Sq;
+    const int qrc = row_ok ? qr : Sq - 1;
+    const int64_t lrow = (int64_t)b * p.lse_s[0] + (int64_t)h * p.lse_s[1] + q_start + qrc;
+    lse_raw = __uint_as_float(gload4_async(p.lse + lrow));
+    dlt_raw = __uint_as_float(gload4_async(p.delta + lrow));
+  };
+  const float inv_scale = 1.f / p.scale;
+
+  auto dq_step = [&](const char* dsb, int h, int qb0) {
+    float* dqb = p.dq_acc + dq_row0 * p.H * D + (int64_t)h * D;
+    const __amdgpu_buffer_rsrc_t dq_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        dqb, 0, (int)((int64_t)(Sq - 1) * p.H * D * 4 + D * 4), 0x00020000);
+    f32x4 qacc[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) qacc[qt][i] = 0.f;
+    // per-lane bases; the key block 32ks is +8192 (K image) / +2048 (dS^T image) and query tile 1 is +32 bytes
+    const int kb0 = img_a(8 * kg + tq, 2 * w + (tp >> 1)) + 8 * (tp & 1);
+    const int kb4 = img_a(8 * kg + 4 + tq, 2 * w + (tp >> 1)) + 8 * (tp & 1);
+    const int sb0 = dst_off(8 * kg + tq, tp), sb4 = dst_off(8 * kg + 4 + tq, tp);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      Frag bb;  // K[key 32ks + 8kg + j][d 16w + r16]
+      bb.h[0] = lds_tr(k_lds, kb0 + 8192 * ks);
+      bb.h[1] = lds_tr(k_lds, kb4 + 8192 * ks);
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        Frag a;  // dS[q 16qt + r16][key 32ks + 8kg + j] from the dS^T image
+        a.h[0] = lds_tr(dsb, sb0 + 2048 * ks + 32 * qt);
+        a.h[1] = lds_tr(dsb, sb4 + 2048 * ks + 32 * qt);
+        qacc[qt] = mfma16<F16>(a, bb, qacc[qt]);
+      }
+      if (ks & 1) __builtin_amdgcn_sched_barrier(0);
+    }
+    const int rs = p.H * D * 4;
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int qr = 16 * qt + 4 * kg + i;
+        const int off = (qb0 + qr < Sq) ? (qb0 + qr) * rs + (16 * w + r16) * 4 : 0x7ffffff0;
+        __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(qacc[qt][i] * p.scale, dq_rsrc, off, 0, 0);
+      }
+  };
+
+  for (int hi = 0; hi < G; ++hi) {
+    const int h = h0 + hi;
+    const int qa = q_begin0;
+    const int n_qb = qa < Sq ? (Sq - qa + BM - 1) / BM : 0;
+    if (n_qb == 0) continue;
+    prefetch(h, qa);
+    // n_qb + 1 passes: the last one only runs the pipelined dQ step of the last block (one dq_step call site:
+    // a second inlined copy after the loop pushed the kernel past 256 registers)
+    for (int it = 0; it <= n_qb; ++it) {
+      const int q0 = qa + it * BM;
+      const bool last = it == n_qb;
+      if (last) {
+        lds_barrier();
+      } else {
+      if (it == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(qreg), "+v"(dreg), "+v"(lse_raw), "+v"(dlt_raw)::"memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(%4)" : "+v"(qreg), "+v"(dreg), "+v"(lse_raw), "+v"(dlt_raw)
+                     : "n"(ATOMICS) : "memory");
+      }
+      if (!q_ok) {
+        qreg = u32x4{0u, 0u, 0u, 0u};
+        dreg = u32x4{0u, 0u, 0u, 0u};
+      }
+      const float lse_r = row_ok ? -lse_raw * inv_scale : -INFINITY;
+      const float dlt_r = row_ok ? -dlt_raw : 0.f;
+      lds_barrier();  // previous iteration's LDS reads done
+      {
+        const int row = tid / NCH, ch = tid % NCH;
+        *reinterpret_cast<u32x4*>(q_lds + img_a(row, ch)) = qreg;
+        *reinterpret_cast<u32x4*>(do_lds + img_a(row, ch)) = dreg;
+      }
+      if (tid < BM) {
+        lse_s[tid] = lse_r;
+        dlt_s[tid] = dlt_r;
+      }
+      lds_barrier();
+      if (it + 1 < n_qb) prefetch(h, q0 + BM);
+      }
+      if (it > 0) dq_step(ds_lds + (((it - 1) & 1) * DST_BYTES), h, q0 - BM);
+      if (last) break;
+
+      // S' and dP' tiles: rows = queries 16qt + 4kg + i, column = this lane's key
+      f32x4 sacc[2], pacc[2];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        const float4 l4 = *reinterpret_cast<const float4*>(lse_s + 16 * qt + 4 * kg);
+        const float4 d4 = *reinterpret_cast<const float4*>(dlt_s + 16 * qt + 4 * kg);
+        sacc[qt][0] = l4.x; sacc[qt][1] = l4.y; sacc[qt][2] = l4.z; sacc[qt][3] = l4.w;
+        pacc[qt][0] = d4.x; pacc[qt][1] = d4.y; pacc[qt][2] = d4.z; pacc[qt][3] = d4.w;
+      }
+      const int rb = img_a(r16, kg);  // query tile qt: +4096, d block 32ks: +512
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          Frag qf, df;
+          qf.u = lds_b128(q_lds, rb + 4096 * qt + 512 * ks);
+          df.u = lds_b128(do_lds, rb + 4096 * qt + 512 * ks);
+          sacc[qt] = mfma16<F16>(qf, kfr[ks], sacc[qt]);
+          pacc[qt] = mfma16<F16>(df, vfr[ks], pacc[qt]);
+        }
+        if (ks & 1) __builtin_amdgcn_sched_barrier(0);
+      }
+      const bool need_mask = kj >= Sk || (p.causal && kb * BK + BK - 1 > q0 + shift);
+      float pv[8], sv[8];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int qr = 16 * qt + 4 * kg + i;
+          float pr = __builtin_amdgcn_exp2f(sacc[qt][i] * p.scale_log2);
+          if (need_mask && (kj >= Sk || (p.causal && kj > q0 + qr + shift))) pr = 0.f;
+          pv[4 * qt + i] = pr;
+          sv[4 * qt + i] = pr * pacc[qt][i];
+        }
+      const Frag pf = pack8<F16>(pv), sf = pack8<F16>(sv);
+
+      // dV^T += dO^T P ; dK^T += Q^T dS  (A: transposed reads at query rows 4kg+tq and 16+4kg+tq)
+      // transposed-read bases for even / odd d tiles; d tiles 2m, 2m+1: +512m; query rows 16..: +4096
+      const int tb0 = img_a(4 * kg + tq, tp >> 1) + 8 * (tp & 1);
+      const int tb1 = img_a(4 * kg + tq, 2 + (tp >> 1)) + 8 * (tp & 1);
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        const int tb = ((dt & 1) ? tb1 : tb0) + 512 * (dt >> 1);
+        Frag a, c;
+        a.h[0] = lds_tr(do_lds, tb);
+        a.h[1] = lds_tr(do_lds, tb + 4096);
+        dv_acc[dt] = mfma16<F16>(a, pf, dv_acc[dt]);
+        c.h[0] = lds_tr(q_lds, tb);
+        c.h[1] = lds_tr(q_lds, tb + 4096);
+        dk_acc[dt] = mfma16<F16>(c, sf, dk_acc[dt]);
+        if (dt & 1) __builtin_amdgcn_sched_barrier(0);  // bound the reads in flight (register budget: 2 waves/SIMD)
+      }
+      // dS^T [128 keys][32 q]: this lane's key row, queries 4kg..4kg+3 and 16+4kg..16+4kg+3
+      {
+        char* dsb = ds_lds + (it & 1) * DST_BYTES;
+        const int row = w * 16 + r16;
+        *reinterpret_cast<uint2*>(dsb + dst_off(row, kg)) = make_uint2(sf.u.x, sf.u.y);
+        *reinterpret_cast<uint2*>(dsb + dst_off(row, 4 + kg)) = make_uint2(sf.u.z, sf.u.w);
+      }
+    }
+  }
+
+  if (kj < Sk) {
+    uint16_t* dkrow = p.dk + (varlen ? (int64_t)k_start * p.dks[1] : (int64_t)b * p.dks[0]) + (int64_t)kj * p.dks[1] +
+                      (int64_t)hk * p.dks[2];
+    uint16_t* dvrow = p.dv + (varlen ? (int64_t)k_start * p.dvs[1] : (int64_t)b * p.dvs[0]) + (int64_t)kj * p.dvs[1] +
+                      (int64_t)hk * p.dvs[2];
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      const int d0 = 16 * dt + 4 * kg;
+      uint2 a, cc;
+      a.x = pack2<F16>(dk_acc[dt][0] * p.scale, dk_acc[dt][1] * p.scale);
+      a.y = pack2<F16>(dk_acc[dt][2] * p.scale, dk_acc[dt][3] * p.scale);
+      cc.x = pack2<F16>(dv_acc[dt][0], dv_acc[dt][1]);
+      cc.y = pack2<F16>(dv_acc[dt][2], dv_acc[dt][3]);
+      *reinterpret_cast<uint2*>(dkrow + d0) = a;
+      *reinterpret_cast<uint2*>(dvrow + d0) = cc;
+    }
+  }
+}
+
 // ---- launch helpers (one instantiation set per 16-bit type: flash_attn.hip = bf16, flash_attn_f16.hip = fp16)
 template <int D, bool F16, int MW>
 void fa_fwd_feat(const FwdArgs& a, int feat, dim3 grid, hipStream_t st) {
@@ -1072,6 +1360,10 @@ void fa_bwd_feat(const BwdArgs& a, int feat, dim3 grid, hipStream_t st) {
 
 template <bool F16>
 void fa_bwd_dispatch(const BwdArgs& a, int D, int feat, dim3 grid, hipStream_t st) {
+  if (D == 128 && feat == 0 && a.k16 && a.abl == 0) {
+    hipLaunchKernelGGL((fa_bwd16_kernel<F16>), grid, dim3(512), 0, st, a);
+    return;
+  }
   if (D == 128) fa_bwd_feat<128, F16, 4, true>(a, feat, grid, st);
   else if (D == 64) fa_bwd_feat<64, F16, 4, true>(a, feat, grid, st);
   else fa_bwd_feat<256, F16, 2, false>(a, feat, grid, st);
