@@ -151,6 +151,11 @@ __device__ __forceinline__ void glds16_fa(const void* g, const char* lds) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
 }
 
+__device__ __forceinline__ void glds4_fa(const void* g, const char* lds) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(lds));
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
+}
+
 __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -1069,15 +1074,15 @@ __global__ __launch_bounds__(512, 1) void fa_bwd16_kernel(BwdArgs p) {
   constexpr int KT_BYTES = BK * D * 2;
   constexpr int QT_BYTES = BM * D * 2;
   constexpr int DST_BYTES = BK * BM * 2;
-  constexpr int ATOMICS = 8;  // fire-and-forget dQ atomics per lane per block
-  __shared__ __attribute__((aligned(16))) char smem[2 * KT_BYTES + 2 * QT_BYTES + 2 * DST_BYTES + 2 * BM * 4];
+  // K, V | Q, dO (two stages each, filled by global_load_lds) | dS^T (two stages) | row constants (two stages:
+  // 32 LSE then 32 delta values)
+  __shared__ __attribute__((aligned(16))) char smem[2 * KT_BYTES + 4 * QT_BYTES + 2 * DST_BYTES + 2 * 2 * BM * 4];
   char* k_lds = smem;
   char* v_lds = smem + KT_BYTES;
-  char* q_lds = v_lds + KT_BYTES;
-  char* do_lds = q_lds + QT_BYTES;
-  char* ds_lds = do_lds + QT_BYTES;
-  float* lse_s = reinterpret_cast<float*>(ds_lds + 2 * DST_BYTES);
-  float* dlt_s = lse_s + BM;
+  char* q_st = v_lds + KT_BYTES;          // stage s: q_st + s * QT_BYTES
+  char* do_st = q_st + 2 * QT_BYTES;
+  char* ds_lds = do_st + 2 * QT_BYTES;
+  char* rc_st = ds_lds + 2 * DST_BYTES;   // stage s: rc_st + s * 256
 
   const int nkb0 = (p.Sk + BK - 1) / BK;
   int kb, bhk;
@@ -1133,25 +1138,27 @@ __global__ __launch_bounds__(512, 1) void fa_bwd16_kernel(BwdArgs p) {
   const int h0 = hk * G;
   const int64_t dq_row0 = varlen ? (int64_t)q_start : (int64_t)b * p.Sq;
 
-  u32x4 qreg, dreg;
-  float lse_raw = 0.f, dlt_raw = 0.f;
-  bool row_ok = false, q_ok = false;
-  auto prefetch = [&](int h, int q0) {
+  // Q / dO block q0 of head h -> stage sl by global_load_lds (no registers in flight: at 254 VGPRs an asm load's
+  // destination could be moved by the allocator before the data lands). The LDS write is lane-linear (wave w:
+  // bytes 1024w .. 1024w + 1023 of the tile), so each lane fetches the chunk (row, ch) that img_a puts at its
+  // destination. Wave 0 also fetches the 32 LSE (lanes 0..31) and delta (lanes 32..63) values of the block.
+  const int o_dst = 1024 * w + 16 * lane;
+  const int pf_row = 8 * (o_dst >> 11) + ((o_dst & 511) >> 6);
+  const int pf_ch = 4 * ((o_dst & 2047) >> 9) + (((o_dst & 63) >> 4) ^ ((pf_row >> 2) & 3));
+  auto prefetch = [&](int h, int q0, int sl) {
     const uint16_t* qbase = p.q + (varlen ? (int64_t)q_start * p.qs[1] : (int64_t)b * p.qs[0]) + (int64_t)h * p.qs[2];
     const uint16_t* dobase =
         p.dout + (varlen ? (int64_t)q_start * p.dos[1] : (int64_t)b * p.dos[0]) + (int64_t)h * p.dos[2];
-    const int row = tid / NCH, ch = tid % NCH;
-    const int qx = q0 + row;
-    q_ok = qx < Sq;
-    const int qc = q_ok ? qx : Sq - 1;
-    qreg = gload16_async(qbase + (int64_t)qc * p.qs[1] + ch * 8);
-    dreg = gload16_async(dobase + (int64_t)qc * p.dos[1] + ch * 8);
-    const int qr = q0 + (tid & (BM - 1));
-    row_ok = qr < Sq;
-    const int qrc = row_ok ? qr : Sq - 1;
-    const int64_t lrow = (int64_t)b * p.lse_s[0] + (int64_t)h * p.lse_s[1] + q_start + qrc;
-    lse_raw = __uint_as_float(gload4_async(p.lse + lrow));
-    dlt_raw = __uint_as_float(gload4_async(p.delta + lrow));
+    const int qx = q0 + pf_row;
+    const int qc = qx < Sq ? qx : Sq - 1;
+    glds16_fa(qbase + (int64_t)qc * p.qs[1] + pf_ch * 8, q_st + sl * QT_BYTES + 1024 * w);
+    glds16_fa(dobase + (int64_t)qc * p.dos[1] + pf_ch * 8, do_st + sl * QT_BYTES + 1024 * w);
+    if (w == 0) {
+      const int qr = q0 + (lane & 31);
+      const int qrc = qr < Sq ? qr : Sq - 1;
+      const int64_t lrow = (int64_t)b * p.lse_s[0] + (int64_t)h * p.lse_s[1] + q_start + qrc;
+      glds4_fa(lane < 32 ? (const void*)(p.lse + lrow) : (const void*)(p.delta + lrow), rc_st + sl * 256);
+    }
   };
   const float inv_scale = 1.f / p.scale;
 
@@ -1198,51 +1205,41 @@ __global__ __launch_bounds__(512, 1) void fa_bwd16_kernel(BwdArgs p) {
     const int qa = q_begin0;
     const int n_qb = qa < Sq ? (Sq - qa + BM - 1) / BM : 0;
     if (n_qb == 0) continue;
-    prefetch(h, qa);
+    prefetch(h, qa, 0);
     // n_qb + 1 passes: the last one only runs the pipelined dQ step of the last block (one dq_step call site:
     // a second inlined copy after the loop pushed the kernel past 256 registers)
     for (int it = 0; it <= n_qb; ++it) {
       const int q0 = qa + it * BM;
       const bool last = it == n_qb;
-      if (last) {
-        lds_barrier();
-      } else {
-      if (it == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(qreg), "+v"(dreg), "+v"(lse_raw), "+v"(dlt_raw)::"memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(%4)" : "+v"(qreg), "+v"(dreg), "+v"(lse_raw), "+v"(dlt_raw)
-                     : "n"(ATOMICS) : "memory");
+      const int sl = it & 1;
+      // this block's stage has landed: the loads were issued in the previous pass, before its 8 dQ atomics
+      if (!last) {
+        if (it >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      if (!q_ok) {
-        qreg = u32x4{0u, 0u, 0u, 0u};
-        dreg = u32x4{0u, 0u, 0u, 0u};
-      }
-      const float lse_r = row_ok ? -lse_raw * inv_scale : -INFINITY;
-      const float dlt_r = row_ok ? -dlt_raw : 0.f;
-      lds_barrier();  // previous iteration's LDS reads done
-      {
-        const int row = tid / NCH, ch = tid % NCH;
-        *reinterpret_cast<u32x4*>(q_lds + img_a(row, ch)) = qreg;
-        *reinterpret_cast<u32x4*>(do_lds + img_a(row, ch)) = dreg;
-      }
-      if (tid < BM) {
-        lse_s[tid] = lse_r;
-        dlt_s[tid] = dlt_r;
-      }
-      lds_barrier();
-      if (it + 1 < n_qb) prefetch(h, q0 + BM);
-      }
-      if (it > 0) dq_step(ds_lds + (((it - 1) & 1) * DST_BYTES), h, q0 - BM);
+      lds_barrier();  // every wave's stage data visible; the previous pass's reads of the other stage done
+      if (!last && it + 1 < n_qb) prefetch(h, q0 + BM, sl ^ 1);
+      if (it > 0 && p.k16 == 1) dq_step(ds_lds + (((it - 1) & 1) * DST_BYTES), h, q0 - BM);
       if (last) break;
 
-      // S' and dP' tiles: rows = queries 16qt + 4kg + i, column = this lane's key
+      const char* q_lds = q_st + sl * QT_BYTES;
+      const char* do_lds = do_st + sl * QT_BYTES;
+      const float* lse_s = reinterpret_cast<const float*>(rc_st + sl * 256);
+      const float* dlt_s = lse_s + BM;
+      // S' and dP' tiles: rows = queries 16qt + 4kg + i, column = this lane's key; the row constants enter as the
+      // accumulators' initial values (-LSE/scale, -delta; rows past Sq: -inf, 0)
       f32x4 sacc[2], pacc[2];
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
         const float4 l4 = *reinterpret_cast<const float4*>(lse_s + 16 * qt + 4 * kg);
         const float4 d4 = *reinterpret_cast<const float4*>(dlt_s + 16 * qt + 4 * kg);
-        sacc[qt][0] = l4.x; sacc[qt][1] = l4.y; sacc[qt][2] = l4.z; sacc[qt][3] = l4.w;
-        pacc[qt][0] = d4.x; pacc[qt][1] = d4.y; pacc[qt][2] = d4.z; pacc[qt][3] = d4.w;
+        const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool ok = q0 + 16 * qt + 4 * kg + i < Sq;
+          sacc[qt][i] = ok ? -lv[i] * inv_scale : -INFINITY;
+          pacc[qt][i] = ok ? -dv4[i] : 0.f;
+        }
       }
       const int rb = img_a(r16, kg);  // query tile qt: +4096, d block 32ks: +512
 #pragma unroll
@@ -1268,6 +1265,10 @@ __global__ __launch_bounds__(512, 1) void fa_bwd16_kernel(BwdArgs p) {
           if (need_mask && (kj >= Sk || (p.causal && kj > q0 + qr + shift))) pr = 0.f;
           pv[4 * qt + i] = pr;
           sv[4 * qt + i] = pr * pacc[qt][i];
+          if (p.k16 >= 3) {  // debug levels (tools/fa16_diag.py): 3 = P := 1, 4 = P := S' (raw accumulator)
+            pv[4 * qt + i] = p.k16 == 3 ? 1.f : sacc[qt][i];
+            sv[4 * qt + i] = pacc[qt][i];
+          }
         }
       const Frag pf = pack8<F16>(pv), sf = pack8<F16>(sv);
 
