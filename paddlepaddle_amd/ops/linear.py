@@ -210,9 +210,11 @@ def _wgrad(x2, dy2, acc=None):
 # post-accumulate hooks). ``zero_bubble_forward()`` routes every linear through the deferrable autograd
 # function for the forwards of such a schedule (off the HIP path a linear is otherwise a plain addmm).
 import contextlib  # noqa: E402
-import threading  # noqa: E402
+import types  # noqa: E402
 
-_ZB = threading.local()
+# Process-wide, not thread-local: the backward of cuda tensors may run on an autograd worker thread (torch's
+# engine executes device nodes on a per-device thread), which must still see the queue of the B step.
+_ZB = types.SimpleNamespace(queue=None, route=False)
 
 
 @contextlib.contextmanager
