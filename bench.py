@@ -362,9 +362,12 @@ def resnet_bench(args, paddle, world, dist_on):
         (" (hipGraph replay of the whole step)" if resnet_bench.graph else ""))
     try:
         from paddlepaddle_amd.ops import gemm as _G
-        for kind in ("conv1x1", "convKxK"):
+        names = {"convf": "forward", "convd": "data grad", "convw": "weight grad"}
+        for kind, what in names.items():
             cv = {k: v for k, v in _G.choices().items() if k[0] == kind}
-            log(f"[resnet50] {kind} backend per shape: {sum(v == 'hip' for v in cv.values())} hand-written MFMA / "
+            own = sum(v != "blas" for v in cv.values())
+            log(f"[resnet50] conv {what} backend per shape: {own} hand-written "
+                f"({sum(v == 'skinny' for v in cv.values())} on the memory-bound skinny kernel) / "
                 f"{sum(v == 'blas' for v in cv.values())} MIOpen")
     except Exception:  # pragma: no cover
         pass

@@ -109,6 +109,13 @@ def _convnd(n, x, weight, bias, stride, padding, dilation, groups, data_format):
     # NHWC 1x1 convolutions: hand-written MFMA GEMM (ops/conv.py) when it measured faster than MIOpen
     if cl and n == 2 and pre is None and stride[0] == stride[1]:
         from ... import ops as _ops
+        pd = pad if isinstance(pad, int) else (pad[0] if pad[0] == pad[1] else None)
+        one = tuple(w.shape[2:]) == (1, 1)
+        if (_ops._loader.flag("FLAGS_conv_per_direction", True) and pd is not None
+                and dilation[0] == dilation[1] and (not one or (pd == 0 and dilation[0] == 1))
+                and _ops.conv.eligible_nhwc(x_raw, w, groups)):
+            # each of forward / data gradient / weight gradient on the faster of ours and MIOpen (ops/conv.py)
+            return _wrap(_ops.conv.conv2d_nhwc(x_raw, w, b, stride[0], pd, dilation[0]))
         if (pad == 0 or pad == (0, 0)) and _ops.conv.eligible(x_raw, w, groups, True):
             y = _ops.conv.conv1x1_nhwc(x_raw, w, b, stride[0],
                                        lambda xx, ww: _from_cf(miopen(_to_cf(xx, data_format, n)[0], ww), cl, n))

@@ -257,6 +257,196 @@ class _ConvImplicit(torch.autograd.Function):
         return dx, gw, gb, None, None, None
 
 
+# ---------------------------------------------------------------------------------------------
+# Per-direction backend choice. A convolution is three products (forward, data gradient, weight gradient)
+# and the hand-written kernel and MIOpen win different ones on the same layer: e.g. on the 56x56 stage of
+# ResNet-50 our 1x1 data gradient (a K=64 GEMM) beats MIOpen while its forward does not. _ConvNHWC picks
+# each direction separately (keys convf / convd / convw, timed once on first use like every GEMM key,
+# tools/bench_conv_dir.py), so a layer never pays for the losing direction of the winning side.
+def _mi_weight(w):
+    return w if w.is_contiguous(memory_format=torch.channels_last) else w.contiguous(memory_format=torch.channels_last)
+
+
+def _mi_fwd(x, w, b, stride, pad, dil):
+    y = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2), _mi_weight(w), b, stride, pad, dil)
+    y = y.permute(0, 2, 3, 1)
+    return y if y.is_contiguous() else y.contiguous()
+
+
+def _mi_bwd(x, w, dy, stride, pad, dil, mask):
+    gi, gw, _ = torch.ops.aten.convolution_backward(dy.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2), _mi_weight(w),
+                                                    None, [stride] * 2, [pad] * 2, [dil] * 2, False, [0, 0], 1,
+                                                    mask + [False])
+    if gi is not None:
+        gi = gi.permute(0, 2, 3, 1)
+        gi = gi if gi.is_contiguous() else gi.contiguous()
+    return gi, gw
+
+
+def _skinny_ok(x, w, stride, dgrad):
+    """1x1 products the memory-bound kernel (ops/gemm.py gemm_skinny) takes: N, K in {32..256}, tall M."""
+    if not (w.shape[2] == 1 and w.shape[3] == 1) or not L.has("pa_gemm_skinny"):
+        return False
+    C, Cout = x.shape[3], w.shape[0]
+    M = x.shape[0] * (-(-x.shape[1] // stride)) * (-(-x.shape[2] // stride))
+    n, k = (C, Cout) if dgrad else (Cout, C)
+    return M >= 1024 and bool(L.lib().pa_gemm_skinny_ok(n, k))
+
+
+def _own_fwd(x, w, b, stride, pad, dil, skinny=False):
+    N, H, W, C = x.shape
+    Cout, _, KH, KW = w.shape
+    if KH == 1 and KW == 1:
+        xs = x[:, ::stride, ::stride, :].contiguous() if stride > 1 else x
+        if skinny:
+            y2 = G.gemm_skinny(xs.reshape(-1, C), w.reshape(Cout, C).t(), bias=b)
+        else:
+            y2 = G.gemm(xs.reshape(-1, C), w.reshape(Cout, C).t(), bias=b)
+        return y2.view(N, xs.shape[1], xs.shape[2], Cout)
+    wk = w.permute(0, 2, 3, 1)
+    if not wk.is_contiguous():
+        wk = wk.contiguous()
+    return _implicit_fwd(x, wk, b, N, H, W, C, Cout, KH, KW, stride, pad, dil)
+
+
+def _own_dgrad_ok(x, w, stride, pad, dil):
+    C, (Cout, _, KH, KW) = x.shape[3], w.shape
+    if KH == 1 and KW == 1:
+        return True
+    return stride == 1 and dil == 1 and Cout % 64 == 0 and C % 8 == 0 and 2 * pad <= KH - 1 + pad and KH == KW
+
+
+def _own_dgrad(x, w, dy, stride, pad, dil, acc=None, skinny=False):
+    """dX on the hand-written kernels; ``acc`` (1x1, stride 1): NHWC gradient dX is added onto in the epilogue."""
+    N, H, W, C = x.shape
+    Cout, _, KH, KW = w.shape
+    if KH == 1 and KW == 1:
+        dy2 = dy.reshape(-1, Cout)
+        w2 = w.reshape(Cout, C)
+        mm = G.gemm_skinny if skinny else G.gemm
+        if acc is not None and stride == 1:
+            return mm(dy2, w2, out=acc.view(-1, C), accumulate=True).view(N, H, W, C)
+        dx = mm(dy2, w2).view(N, dy.shape[1], dy.shape[2], C)
+        if stride > 1:
+            full = torch.zeros(N, H, W, C, dtype=dx.dtype, device=dx.device)
+            full[:, ::stride, ::stride, :] = dx
+            dx = full
+        return dx
+    # transposed convolution = convolution of dY with the flipped, in/out-swapped filter [C, KH, KW, Cout]
+    wt = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()
+    return _implicit_fwd(dy, wt, None, N, dy.shape[1], dy.shape[2], Cout, C, KH, KW, 1, KH - 1 - pad, 1)
+
+
+def _own_wgrad_ok(x, w, dy):
+    C, Cout = x.shape[3], w.shape[0]
+    P = dy.shape[0] * dy.shape[1] * dy.shape[2]
+    if w.shape[2] == 1 and w.shape[3] == 1:
+        return P % 64 == 0
+    return L.has("pa_conv2d_nhwc_wgrad") and C % 8 == 0 and Cout % 8 == 0 and P % 64 == 0
+
+
+def _own_wgrad(x, w, dy, stride, pad, dil):
+    N, H, W, C = x.shape
+    Cout, _, KH, KW = w.shape
+    if KH == 1 and KW == 1:
+        xs = x[:, ::stride, ::stride, :].contiguous() if stride > 1 else x
+        x2 = xs.reshape(-1, C)
+        dy2 = dy.reshape(-1, Cout)
+        dw = G.gemm_splitk(dy2.t(), x2, _splits(Cout, C, dy2.shape[0]), out_dtype=w.dtype)
+        return dw.view(Cout, C, 1, 1)
+    return _implicit_wgrad(x, dy, w, N, H, W, C, Cout, KH, KW, stride, pad, dil, dy.shape[1], dy.shape[2])
+
+
+def _pick(key, own, mi, skinny=None):
+    """'hip' | 'skinny' | 'blas' for one direction (ops/gemm.py choose(): timed once, persisted). 'skinny' is the
+    memory-bound 1x1 kernel, offered when the shape fits it."""
+    if L.flag("FLAGS_gemm_backend", "auto") != "auto":
+        return G.choose(key, {"hip": None, "blas": None})
+    cands = {"hip": own, "blas": mi}
+    if skinny is not None:
+        cands["skinny"] = skinny
+    return G.choose(key, cands)
+
+
+class _ConvNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad, dil, sink=None):
+        key = (tuple(x.shape), tuple(w.shape), stride, pad, dil)
+        sk = (lambda: _own_fwd(x, w, b, stride, pad, dil, skinny=True)) if _skinny_ok(x, w, stride, False) else None
+        ch = _pick(("convf",) + key + (b is not None,), lambda: _own_fwd(x, w, b, stride, pad, dil),
+                   lambda: _mi_fwd(x, w, b, stride, pad, dil), sk)
+        y = _mi_fwd(x, w, b, stride, pad, dil) if ch == "blas" else \
+            _own_fwd(x, w, b, stride, pad, dil, skinny=ch == "skinny")
+        ctx.save_for_backward(x, w)
+        ctx.cfg = (stride, pad, dil, b is not None, key)
+        ctx.sink = sink
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        stride, pad, dil, has_b, key = ctx.cfg
+        dy = dy if dy.is_contiguous() else dy.contiguous()
+        dres = None
+        if ctx.sink is not None:
+            dres, ctx.sink.dres = ctx.sink.dres, None
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            ch = "blas"
+            if _own_dgrad_ok(x, w, stride, pad, dil):
+                sk = (lambda: _own_dgrad(x, w, dy, stride, pad, dil, skinny=True)) \
+                    if _skinny_ok(x, w, stride, True) else None
+                ch = _pick(("convd",) + key, lambda: _own_dgrad(x, w, dy, stride, pad, dil),
+                           lambda: _mi_bwd(x, w, dy, stride, pad, dil, [True, False]), sk)
+            if ch != "blas":
+                dx = _own_dgrad(x, w, dy, stride, pad, dil, acc=dres, skinny=ch == "skinny")
+                if dres is not None and not (w.shape[2] == 1 and w.shape[3] == 1 and stride == 1):
+                    dx = dx + dres
+            else:
+                dx = _mi_bwd(x, w, dy, stride, pad, dil, [True, False])[0]
+                if dres is not None:
+                    dx = dx.add_(dres)
+        elif dres is not None:
+            dx = dres
+        if ctx.needs_input_grad[1]:
+            own = _own_wgrad_ok(x, w, dy)
+            if own:
+                own = _pick(("convw",) + key, lambda: _own_wgrad(x, w, dy, stride, pad, dil),
+                            lambda: _mi_bwd(x, w, dy, stride, pad, dil, [False, True])) == "hip"
+            dw = _own_wgrad(x, w, dy, stride, pad, dil) if own else _mi_bwd(x, w, dy, stride, pad, dil,
+                                                                            [False, True])[1]
+            if dw.dtype != w.dtype:
+                dw = dw.to(w.dtype)
+        if has_b and ctx.needs_input_grad[2]:
+            db = dy.reshape(-1, dy.shape[-1]).float().sum(0).to(dy.dtype)
+        return dx, dw, db, None, None, None, None
+
+
+def conv2d_nhwc(x, w, b, stride, pad, dil):
+    """NHWC 2-D convolution (groups 1, symmetric padding) with each of its three products on the hand-written
+    kernel or MIOpen, whichever measured faster for the shape. A stride-1 1x1 convolution inside
+    ``residual_grad_sink()`` takes over the block's residual gradient (ResidualGradSink)."""
+    sink = _SINK[0] if (w.shape[2] == 1 and w.shape[3] == 1 and stride == 1) else None
+    if sink is not None:
+        sink.armed = True
+    return _ConvNHWC.apply(x, w, b, stride, pad, dil, sink)
+
+
+def eligible_nhwc(x_nhwc, w, groups):
+    """Shape / layout conditions of _ConvNHWC (the per-direction choice needs the hand-written side to exist
+    for at least the forward)."""
+    if not (x_nhwc.is_cuda and x_nhwc.dtype == torch.bfloat16 and w.dtype == torch.bfloat16):
+        return False
+    if x_nhwc.dim() != 4 or w.dim() != 4 or groups != 1 or not x_nhwc.is_contiguous() or x_nhwc.numel() == 0:
+        return False
+    if not L.hip_enabled_for(x_nhwc):
+        return False
+    cin, cout = x_nhwc.shape[3], w.shape[0]
+    if tuple(w.shape[2:]) == (1, 1):
+        return L.has("pa_gemm_bf16") and cin % 64 == 0 and cout % 64 == 0
+    return L.has("pa_conv2d_nhwc_fwd") and cin % 64 == 0 and cout % 8 == 0
+
+
 def eligible_implicit(x_nhwc, w, groups):
     if not (x_nhwc.is_cuda and x_nhwc.dtype == torch.bfloat16 and w.dtype == torch.bfloat16):
         return False

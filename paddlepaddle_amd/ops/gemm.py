@@ -103,6 +103,35 @@ def gemm_splitk(a, b, splits, out_dtype=torch.bfloat16, bn=None):
     return ws.sum(0, dtype=torch.float32).to(out_dtype) if splits > 1 else ws[0].to(out_dtype)
 
 
+def skinny_supported(a, b):
+    """gemm_skinny's conditions: bf16, A row-major, tall M, N and K in {32, 64, 128, 256}, 16-byte rows."""
+    if not (L.has("pa_gemm_skinny") and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.is_cuda):
+        return False
+    M, K = a.shape
+    N = b.shape[1]
+    if a.stride(1) != 1 or a.stride(0) % 8 or M < 1024 or not L.lib().pa_gemm_skinny_ok(N, K):
+        return False
+    return (b.stride(0) == 1 and b.stride(1) % 8 == 0) or (b.stride(1) == 1 and b.stride(0) % 8 == 0)
+
+
+def gemm_skinny(a, b, bias=None, out=None, accumulate=False, relu=False):
+    """C = a @ b (+ bias) (relu), or C += a @ b with ``accumulate``: the memory-bound kernel for a tall M and a
+    small N x K (csrc/kernels/gemm_skinny.hip; the 1x1 convolutions of ResNet's early stages)."""
+    M, K = a.shape
+    N = b.shape[1]
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    assert out.stride(1) == 1 and out.stride(0) % 8 == 0 and out.dtype == torch.bfloat16
+    bk = b.stride(0) == 1  # b = B^T row-major viewed transposed
+    ldb = b.stride(1) if bk else b.stride(0)
+    flags = (1 if bias is not None else 0) | (2 if accumulate else 0) | (4 if relu else 0)
+    rc = L.call("pa_gemm_skinny", L.ptr(a), L.ptr(b), L.ptr(out), L.ptr(bias), M, N, K, a.stride(0), ldb,
+                out.stride(0), int(bk), flags, L.stream_ptr())
+    if rc:
+        raise RuntimeError(f"pa_gemm_skinny failed ({rc}) for M={M} N={N} K={K}")
+    return out
+
+
 def pick_splits(M, N, K, bn=256, cus=256, max_ws_bytes=256 << 20):
     """Largest power-of-two split keeping K-slices a multiple of 64 that brings the grid to ~2 waves."""
     tiles = -(-M // 256) * -(-N // bn)

@@ -12,6 +12,7 @@ DEV = "cuda"
 
 # launchers each test must have dispatched (ops._loader.CALLS, reset per test by conftest)
 _EXPECT = {
+    "test_gemm_skinny": ["pa_gemm_skinny"],
     "test_gemm_small_m": ["pa_gemm_small_m"],
     "test_conv_implicit_gemm_fwd": ["pa_conv2d_nhwc_fwd"],
     "test_conv_implicit_gemm_dgrad": ["pa_conv2d_nhwc_fwd"],
@@ -222,3 +223,24 @@ def test_gemm_pp_tail_epilogues():
     out = base.clone()
     G.gemm(a, b, out=out, accumulate=True, alpha=0.5, bn=1)
     torch.testing.assert_close(out, base + 0.5 * _ref(a, b), atol=0.1, rtol=1e-2)
+
+
+@pytest.mark.parametrize("N,K", [(64, 64), (256, 64), (64, 256), (128, 128), (32, 32), (256, 256)])
+@pytest.mark.parametrize("b_kmaj", [True, False])
+@pytest.mark.parametrize("epi", ["none", "bias_relu", "accum"])
+def test_gemm_skinny(N, K, b_kmaj, epi):
+    """Memory-bound tall-M kernel (csrc/kernels/gemm_skinny.hip) incl. a ragged last 16-row block."""
+    M = 4104
+    a, b = _operands(M, N, K, True, b_kmaj, seed=N + K)
+    assert G.skinny_supported(a, b)
+    ref = _ref(a, b)
+    bias = None
+    out = None
+    if epi == "bias_relu":
+        bias = torch.randn(N, device=DEV).bfloat16()
+        ref = torch.relu(ref + bias.float())
+    if epi == "accum":
+        out = torch.randn(M, N, device=DEV).bfloat16()
+        ref = ref + out.float()
+    got = G.gemm_skinny(a, b, bias=bias, out=out, accumulate=epi == "accum", relu=epi == "bias_relu")
+    torch.testing.assert_close(got.float(), ref, rtol=2e-2, atol=2e-2 * (K ** 0.5))
