@@ -13,6 +13,8 @@
 // Reference role: the cuDNN 1x1-convolution kernels behind paddle/phi/kernels/gpu/conv_kernel.cu.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 using namespace pa;
 
@@ -40,7 +42,7 @@ struct SkArgs {
   int flags;
 };
 
-template <int NT, int KS>
+template <int NT, int KS, int R>
 __global__ __launch_bounds__(256) void skinny_gemm_k(SkArgs p) {
   constexpr int N = 16 * NT, K = 32 * KS, LDK = K + 8;  // LDS row of B^T padded by 16 bytes
   extern __shared__ __attribute__((aligned(16))) uint16_t bt[];
@@ -67,7 +69,8 @@ __global__ __launch_bounds__(256) void skinny_gemm_k(SkArgs p) {
   __syncthreads();
 
   const int wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
-  const int64_t nb = (p.M + 15) / 16;
+  // a wave iteration covers R 16-row blocks: every B^T fragment read from LDS feeds R MFMAs
+  const int64_t nb = (p.M + 16 * R - 1) / (16 * R);
   const int64_t stride = (int64_t)gridDim.x * 4;
   int64_t blk = (int64_t)blockIdx.x * 4 + wave;
   if (blk >= nb) return;  // wave-uniform; no barrier follows
@@ -80,94 +83,110 @@ __global__ __launch_bounds__(256) void skinny_gemm_k(SkArgs p) {
     f.u = *reinterpret_cast<const uint4*>(bt + (32 * (t >> 1) + 4 * (t & 1) + brow) * LDK + 32 * ks + 8 * g);
     return f;
   };
-  auto load_a = [&](int64_t b, Frag8* fr) {
-    int64_t row = b * 16 + r;
-    row = row < p.M ? row : p.M - 1;
-    const uint16_t* src = p.a + row * p.lda + 8 * g;
+  auto load_a = [&](int64_t b, Frag8 (&fr)[R][KS]) {
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) fr[ks].w = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + 32 * ks));
+    for (int i = 0; i < R; ++i) {
+      int64_t row = b * 16 * R + 16 * i + r;
+      row = row < p.M ? row : p.M - 1;
+      const uint16_t* src = p.a + row * p.lda + 8 * g;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        fr[i][ks].w = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + 32 * ks));
+    }
   };
 
-  Frag8 acur[KS], anext[KS];
+  Frag8 acur[R][KS], anext[R][KS];
   load_a(blk, acur);
   for (; blk < nb; blk += stride) {
     const bool more = blk + stride < nb;
     if (more) load_a(blk + stride, anext);
-    f32x4 acc[NT];
+    f32x4 acc[R][NT];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfrag(t, ks).v, acur[ks].v, acc[t], 0, 0, 0);
-        if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound the B^T reads in flight (registers)
+        const Frag8 bf = bfrag(t, ks);
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf.v, acur[i][ks].v, acc[i][t], 0, 0, 0);
+        if ((t & 1) == 1) __builtin_amdgcn_sched_barrier(0);  // bound the B^T reads in flight (registers)
       }
-    // lane: output row blk*16 + r, columns 32q + 8g .. +7 of tile pair q
-    const int64_t row = blk * 16 + r;
-    if (row < p.M) {
-      uint16_t* dst = p.c + row * p.ldc;
 #pragma unroll
-      for (int q = 0; q < NT / 2; ++q) {
-        const int c0 = 32 * q + 8 * g;
-        float v[8];
+    for (int i = 0; i < R; ++i) {
+      // lane: output row (blk*R + i)*16 + r, columns 32q + 8g .. +7 of tile pair q
+      const int64_t row = blk * 16 * R + 16 * i + r;
+      if (row < p.M) {
+        uint16_t* dst = p.c + row * p.ldc;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          v[i] = acc[2 * q][i];
-          v[4 + i] = acc[2 * q + 1][i];
-        }
-        if (p.flags & kSkEpiBias) {
-          const uint4 bb = *reinterpret_cast<const uint4*>(p.bias + c0);
-          const uint32_t w[4] = {bb.x, bb.y, bb.z, bb.w};
+        for (int q = 0; q < NT / 2; ++q) {
+          const int c0 = 32 * q + 8 * g;
+          float v[8];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            v[2 * j] += lo_bf16(w[j]);
-            v[2 * j + 1] += hi_bf16(w[j]);
+            v[j] = acc[i][2 * q][j];
+            v[4 + j] = acc[i][2 * q + 1][j];
           }
-        }
-        if (p.flags & kSkEpiAccum) {
-          const uint4 cc = *reinterpret_cast<const uint4*>(dst + c0);
-          const uint32_t w[4] = {cc.x, cc.y, cc.z, cc.w};
+          if (p.flags & kSkEpiBias) {
+            const uint4 bb = *reinterpret_cast<const uint4*>(p.bias + c0);
+            const uint32_t w[4] = {bb.x, bb.y, bb.z, bb.w};
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            v[2 * j] += lo_bf16(w[j]);
-            v[2 * j + 1] += hi_bf16(w[j]);
+            for (int j = 0; j < 4; ++j) {
+              v[2 * j] += lo_bf16(w[j]);
+              v[2 * j + 1] += hi_bf16(w[j]);
+            }
           }
-        }
-        if (p.flags & kSkEpiRelu) {
+          if (p.flags & kSkEpiAccum) {
+            const uint4 cc = *reinterpret_cast<const uint4*>(dst + c0);
+            const uint32_t w[4] = {cc.x, cc.y, cc.z, cc.w};
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+            for (int j = 0; j < 4; ++j) {
+              v[2 * j] += lo_bf16(w[j]);
+              v[2 * j + 1] += hi_bf16(w[j]);
+            }
+          }
+          if (p.flags & kSkEpiRelu) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+          }
+          uint4 o;
+          o.x = pack_bf16(v[0], v[1]);
+          o.y = pack_bf16(v[2], v[3]);
+          o.z = pack_bf16(v[4], v[5]);
+          o.w = pack_bf16(v[6], v[7]);
+          *reinterpret_cast<uint4*>(dst + c0) = o;
         }
-        uint4 o;
-        o.x = pack_bf16(v[0], v[1]);
-        o.y = pack_bf16(v[2], v[3]);
-        o.z = pack_bf16(v[4], v[5]);
-        o.w = pack_bf16(v[6], v[7]);
-        *reinterpret_cast<uint4*>(dst + c0) = o;
       }
     }
     if (more) {
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) acur[ks] = anext[ks];
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) acur[i][ks] = anext[i][ks];
     }
   }
 }
 
 template <int NT, int KS>
 int launch_sk(const SkArgs& a, hipStream_t st) {
+  // two 16-row blocks per wave iteration, except N = 256 (its 128 accumulators would leave one wave per SIMD)
+  constexpr int R = NT <= 8 ? 2 : 1;
   constexpr int N = 16 * NT, K = 32 * KS;
   const size_t lds = (size_t)N * (K + 8) * 2;
   if (lds > 160 * 1024) return 2;
   const int per_cu = (int)std::min<size_t>(8, (160 * 1024) / lds);
-  const int64_t nb = (a.M + 15) / 16;
+  const int64_t nb = (a.M + 16 * R - 1) / (16 * R);
   const int64_t grid = std::min<int64_t>((nb + 3) / 4, (int64_t)256 * per_cu);
   static bool attr_set = false;  // dynamic LDS above 64 KB needs the attribute
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_k<NT, KS>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_k<NT, KS, R>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
-  hipLaunchKernelGGL((skinny_gemm_k<NT, KS>), dim3((unsigned)grid), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((skinny_gemm_k<NT, KS, R>), dim3((unsigned)grid), dim3(256), lds, st, a);
   PA_CHECK_LAUNCH();
   return 0;
 }
@@ -181,6 +200,166 @@ int launch_sk_k(const SkArgs& a, int64_t K, hipStream_t st) {
     case 256: return launch_sk<NT, 8>(a, st);
     default: return 2;
   }
+}
+
+// ---- implicit-GEMM convolution on the same scheme: Y[p, co] = sum_{tap, c} X[pixel(p, tap), c] . W[co, tap, c] for the
+// small-channel KxK layers (C = 64, Cout = 64: ResNet-50's 56x56 3x3, forward and — with the flipped, in/out-swapped
+// filter — stride-1 data gradient), where the 256-wide tile of the general implicit kernel wastes 3/4 of its MFMAs.
+// The filter [Cout][KH][KW][C] is B^T (K = KH*KW*C = 576: 74 KB of LDS, 2 workgroups per CU); a lane's A fragment of
+// K step (tap, 32-channel slice) is 16 B of one input pixel, fetched by a raw buffer load whose offset is pushed past
+// the buffer's end for taps in the padding (the hardware returns zeros: no branches, no zero page). Neighbouring
+// output pixels re-read the same input pixels across taps from L1 / L2; HBM sees X about once.
+struct SkConvArgs {
+  const uint16_t* x;
+  const uint16_t* w;  // [Cout][KH][KW][C]
+  uint16_t* y;
+  const uint16_t* bias;
+  int64_t M;  // N * Ho * Wo
+  int H, W, Ho, Wo, stride, pad;
+  uint32_t x_bytes;
+  int flags;
+};
+
+// Per wave iteration: a super-block of R x 16 output pixels, so every B^T fragment read from LDS feeds R MFMAs
+// (LDS traffic / R); A moves through a ring of S tap-groups of fragments, the loads of tap g + S - 1 issued while
+// tap g's MFMAs run (crossing into the next super-block at the end), so the loop never waits on a whole block.
+template <int NT, int C, int KH, int KW, int R, int NW>
+__global__ __launch_bounds__(NW * 64) void skinny_conv_k(SkConvArgs p) {
+  constexpr int NOUT = 16 * NT, KG = KH * KW, CS = C / 32, K = KG * C, LDK = K + 8, S = 3;
+  static_assert(KG % S == 0, "tap count must be a multiple of the ring depth");
+  extern __shared__ __attribute__((aligned(16))) uint16_t bt[];
+  const int tid = threadIdx.x;
+  for (int idx = tid; idx < NOUT * (K / 8); idx += NW * 64) {
+    const int n = idx / (K / 8), kc = idx % (K / 8);
+    *reinterpret_cast<uint4*>(bt + n * LDK + kc * 8) = *reinterpret_cast<const uint4*>(p.w + (int64_t)n * K + kc * 8);
+  }
+  __syncthreads();
+  const int wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
+  const int64_t nsb = (p.M + 16 * R - 1) / (16 * R);
+  const int64_t stride = (int64_t)gridDim.x * NW;
+  int64_t sb = (int64_t)blockIdx.x * NW + wave;
+  if (sb >= nsb) return;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(p.x), 0, (int)p.x_bytes,
+                                                                       0x00020000);
+  const int brow = 8 * (r >> 2) + (r & 3);
+  // lane's output pixel of block i of super-block s: image base (n*H*W), top-left input row / column of its window
+  auto rows = [&](int64_t s, int* rb, int* rh, int* rw) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      int64_t row = s * 16 * R + 16 * i + r;
+      row = row < p.M ? row : p.M - 1;
+      const int wo = (int)(row % p.Wo);
+      const int64_t t1 = row / p.Wo;
+      const int ho = (int)(t1 % p.Ho);
+      rb[i] = (int)(t1 / p.Ho) * p.H * p.W;
+      rh[i] = ho * p.stride - p.pad;
+      rw[i] = wo * p.stride - p.pad;
+    }
+  };
+  auto load_tap = [&](const int* rb, const int* rh, const int* rw, int tap, Frag8 (&dst)[R][CS]) {
+    const int kh = tap / KW, kw = tap % KW;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int hi = rh[i] + kh, wi = rw[i] + kw;
+      const bool ok = (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W;
+      const int off = ok ? ((rb[i] + hi * p.W + wi) * C + 8 * g) * 2 : 0x7ff00000;
+#pragma unroll
+      for (int cs = 0; cs < CS; ++cs)
+        dst[i][cs].w = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, off + 64 * cs, 0, 0));
+    }
+  };
+  Frag8 ring[S][R][CS];
+  int cb[R], ch[R], cw[R], nbs[R], nh[R], nw[R];
+  rows(sb, cb, ch, cw);
+#pragma unroll
+  for (int j = 0; j < S - 1; ++j) load_tap(cb, ch, cw, j, ring[j]);
+  for (; sb < nsb; sb += stride) {
+    const bool more = sb + stride < nsb;
+    if (more) rows(sb + stride, nbs, nh, nw);
+    f32x4 acc[R][NT];
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kg = 0; kg < KG; ++kg) {
+      const int g2 = kg + S - 1;
+      if (g2 < KG) load_tap(cb, ch, cw, g2, ring[g2 % S]);
+      else if (more) load_tap(nbs, nh, nw, g2 - KG, ring[g2 % S]);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        Frag8 bf[CS];
+#pragma unroll
+        for (int cs = 0; cs < CS; ++cs)
+          bf[cs].u = *reinterpret_cast<const uint4*>(bt + (32 * (t >> 1) + 4 * (t & 1) + brow) * LDK +
+                                                     kg * C + 32 * cs + 8 * g);
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+#pragma unroll
+          for (int cs = 0; cs < CS; ++cs)
+            acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[cs].v, ring[kg % S][i][cs].v, acc[i][t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);  // one tile's B^T fragments live at a time (register budget)
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int64_t row = sb * 16 * R + 16 * i + r;
+      if (row < p.M) {
+        uint16_t* dst = p.y + row * NOUT;
+#pragma unroll
+        for (int q = 0; q < NT / 2; ++q) {
+          const int c0 = 32 * q + 8 * g;
+          float v[8];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[j] = acc[i][2 * q][j];
+            v[4 + j] = acc[i][2 * q + 1][j];
+          }
+          if (p.flags & kSkEpiBias) {
+            const uint4 bb = *reinterpret_cast<const uint4*>(p.bias + c0);
+            const uint32_t w[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              v[2 * j] += lo_bf16(w[j]);
+              v[2 * j + 1] += hi_bf16(w[j]);
+            }
+          }
+          uint4 o;
+          o.x = pack_bf16(v[0], v[1]);
+          o.y = pack_bf16(v[2], v[3]);
+          o.z = pack_bf16(v[4], v[5]);
+          o.w = pack_bf16(v[6], v[7]);
+          *reinterpret_cast<uint4*>(dst + c0) = o;
+        }
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        cb[i] = nbs[i];
+        ch[i] = nh[i];
+        cw[i] = nw[i];
+      }
+    }
+  }
+}
+
+template <int NT, int C, int KH, int KW, int R, int NW>
+int launch_skconv(const SkConvArgs& a, hipStream_t st) {
+  constexpr int K = KH * KW * C;
+  const size_t lds = (size_t)16 * NT * (K + 8) * 2;
+  const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / lds));
+  const int64_t nb = (a.M + 16 * R - 1) / (16 * R);
+  const int64_t grid = std::min<int64_t>((nb + NW - 1) / NW, (int64_t)256 * per_cu);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_conv_k<NT, C, KH, KW, R, NW>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((skinny_conv_k<NT, C, KH, KW, R, NW>), dim3((unsigned)grid), dim3(NW * 64), lds, st, a);
+  PA_CHECK_LAUNCH();
+  return 0;
 }
 
 }  // namespace
@@ -206,5 +385,36 @@ PA_EXPORT int pa_gemm_skinny(const void* a, const void* b, void* c, const void* 
     case 128: return launch_sk_k<8>(g, K, st);
     case 256: return launch_sk_k<16>(g, K, st);
     default: return 2;
+  }
+}
+
+// 1 if the skinny implicit convolution has an instantiation for (C, Cout, KH, KW).
+PA_EXPORT int pa_conv_skinny_ok(int64_t C, int64_t Cout, int64_t KH, int64_t KW) {
+  return C == 64 && Cout == 64 && KH == 3 && KW == 3;
+}
+
+// NHWC convolution y[N, Ho, Wo, Cout] = conv(x[N, H, W, C], w[Cout][KH][KW][C]) (+ bias), symmetric padding, no
+// dilation, on the skinny implicit-GEMM kernel. x must be below 2 GB (32-bit buffer offsets). Returns 2 if the
+// shape has no instantiation.
+PA_EXPORT int pa_conv_skinny(const void* x, const void* w, const void* bias, void* y, int64_t N, int64_t H, int64_t W,
+                             int64_t C, int64_t Cout, int64_t KH, int64_t KW, int64_t stride, int64_t pad, int64_t Ho,
+                             int64_t Wo, void* stream) {
+  if (!pa_conv_skinny_ok(C, Cout, KH, KW)) return 2;
+  const int64_t xb = N * H * W * C * 2;
+  if (xb >= ((int64_t)1 << 31) - (1 << 21)) return 2;
+  SkConvArgs a{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w), static_cast<uint16_t*>(y),
+               static_cast<const uint16_t*>(bias), N * Ho * Wo, (int)H, (int)W, (int)Ho, (int)Wo, (int)stride, (int)pad,
+               (uint32_t)xb, bias ? kSkEpiBias : 0};
+  if (a.M <= 0) return 0;
+  static const int cfg = [] {  // PA_SKCONV_CFG (measurement): 0 = R2 x 4 waves, 1 = R1 x 8, 2 = R2 x 8, 3 = R1 x 4
+    const char* e = getenv("PA_SKCONV_CFG");
+    return e ? atoi(e) : 0;
+  }();
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  switch (cfg) {
+    case 1: return launch_skconv<4, 64, 3, 3, 1, 8>(a, st);
+    case 2: return launch_skconv<4, 64, 3, 3, 2, 8>(a, st);
+    case 3: return launch_skconv<4, 64, 3, 3, 1, 4>(a, st);
+    default: return launch_skconv<4, 64, 3, 3, 2, 4>(a, st);
   }
 }

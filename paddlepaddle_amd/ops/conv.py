@@ -34,9 +34,29 @@ class ResidualGradSink:
     def __init__(self):
         self.armed = False
         self.dres = None
+        self.consumed = False  # the consuming conv ran before any producer (producers then return dx normally)
 
 
 _SINK = [None]
+_PRODUCER = [None]
+
+
+class residual_grad_producer:
+    """``with residual_grad_producer(sink): identity = downsample(x)`` — projection-shortcut blocks: the
+    shortcut's convolution hands its data gradient to ``sink`` (returning none to autograd) and the block's first
+    1x1 conv, the other consumer of x, adds it in its GEMM epilogue, so autograd never sums x's two gradients with
+    a separate elementwise add. Order-safe: if the consumer already ran, the producer returns dx normally."""
+
+    def __init__(self, sink):
+        self.sink = sink
+
+    def __enter__(self):
+        _PRODUCER[0] = self.sink if (self.sink is not None and self.sink.armed) else None
+        return self.sink
+
+    def __exit__(self, *exc):
+        _PRODUCER[0] = None
+        return False
 
 
 class residual_grad_sink:
@@ -283,11 +303,28 @@ def _mi_bwd(x, w, dy, stride, pad, dil, mask):
     return gi, gw
 
 
-def _skinny_ok(x, w, stride, dgrad):
-    """1x1 products the memory-bound kernel (ops/gemm.py gemm_skinny) takes: N, K in {32..256}, tall M."""
-    if not (w.shape[2] == 1 and w.shape[3] == 1) or not L.has("pa_gemm_skinny"):
-        return False
+def _skinny_conv(x, wk, b, N, H, W, C, Cout, KH, KW, stride, pad):
+    """KxK convolution on the skinny implicit-GEMM kernel (csrc/kernels/gemm_skinny.hip pa_conv_skinny);
+    wk: filter [Cout, KH, KW, C] contiguous."""
+    Ho = (H + 2 * pad - KH) // stride + 1
+    Wo = (W + 2 * pad - KW) // stride + 1
+    out = torch.empty(N, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
+    L.call("pa_conv_skinny", L.ptr(x), L.ptr(wk), L.ptr(b), L.ptr(out), N, H, W, C, Cout, KH, KW, stride, pad, Ho, Wo,
+           L.stream_ptr())
+    return out
+
+
+def _skinny_ok(x, w, stride, dgrad, pad=0, dil=1):
+    """Products the memory-bound skinny kernels take: 1x1 (ops/gemm.py gemm_skinny: N, K in {32..256}, tall M)
+    and KxK (pa_conv_skinny: C = Cout = 64, 3x3; the data gradient only at stride 1)."""
     C, Cout = x.shape[3], w.shape[0]
+    if not (w.shape[2] == 1 and w.shape[3] == 1):
+        if not L.has("pa_conv_skinny") or dil != 1 or (dgrad and stride != 1) or x.numel() * 2 >= (1 << 31) - (1 << 21):
+            return False
+        ci, co = (Cout, C) if dgrad else (C, Cout)
+        return bool(L.lib().pa_conv_skinny_ok(ci, co, w.shape[2], w.shape[3]))
+    if not L.has("pa_gemm_skinny"):
+        return False
     M = x.shape[0] * (-(-x.shape[1] // stride)) * (-(-x.shape[2] // stride))
     n, k = (C, Cout) if dgrad else (Cout, C)
     return M >= 1024 and bool(L.lib().pa_gemm_skinny_ok(n, k))
@@ -306,6 +343,8 @@ def _own_fwd(x, w, b, stride, pad, dil, skinny=False):
     wk = w.permute(0, 2, 3, 1)
     if not wk.is_contiguous():
         wk = wk.contiguous()
+    if skinny:
+        return _skinny_conv(x, wk, b, N, H, W, C, Cout, KH, KW, stride, pad)
     return _implicit_fwd(x, wk, b, N, H, W, C, Cout, KH, KW, stride, pad, dil)
 
 
@@ -334,6 +373,8 @@ def _own_dgrad(x, w, dy, stride, pad, dil, acc=None, skinny=False):
         return dx
     # transposed convolution = convolution of dY with the flipped, in/out-swapped filter [C, KH, KW, Cout]
     wt = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()
+    if skinny:
+        return _skinny_conv(dy, wt, None, N, dy.shape[1], dy.shape[2], Cout, C, KH, KW, 1, KH - 1 - pad)
     return _implicit_fwd(dy, wt, None, N, dy.shape[1], dy.shape[2], Cout, C, KH, KW, 1, KH - 1 - pad, 1)
 
 
@@ -370,9 +411,10 @@ def _pick(key, own, mi, skinny=None):
 
 class _ConvNHWC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, stride, pad, dil, sink=None):
+    def forward(ctx, x, w, b, stride, pad, dil, sink=None, produce=None):
         key = (tuple(x.shape), tuple(w.shape), stride, pad, dil)
-        sk = (lambda: _own_fwd(x, w, b, stride, pad, dil, skinny=True)) if _skinny_ok(x, w, stride, False) else None
+        sk = (lambda: _own_fwd(x, w, b, stride, pad, dil, skinny=True)) \
+            if _skinny_ok(x, w, stride, False, pad, dil) else None
         ch = _pick(("convf",) + key + (b is not None,), lambda: _own_fwd(x, w, b, stride, pad, dil),
                    lambda: _mi_fwd(x, w, b, stride, pad, dil), sk)
         y = _mi_fwd(x, w, b, stride, pad, dil) if ch == "blas" else \
@@ -380,6 +422,7 @@ class _ConvNHWC(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.cfg = (stride, pad, dil, b is not None, key)
         ctx.sink = sink
+        ctx.produce = produce
         return y
 
     @staticmethod
@@ -390,12 +433,14 @@ class _ConvNHWC(torch.autograd.Function):
         dres = None
         if ctx.sink is not None:
             dres, ctx.sink.dres = ctx.sink.dres, None
+            if dres is None:
+                ctx.sink.consumed = True
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             ch = "blas"
             if _own_dgrad_ok(x, w, stride, pad, dil):
                 sk = (lambda: _own_dgrad(x, w, dy, stride, pad, dil, skinny=True)) \
-                    if _skinny_ok(x, w, stride, True) else None
+                    if _skinny_ok(x, w, stride, True, pad, dil) else None
                 ch = _pick(("convd",) + key, lambda: _own_dgrad(x, w, dy, stride, pad, dil),
                            lambda: _mi_bwd(x, w, dy, stride, pad, dil, [True, False]), sk)
             if ch != "blas":
@@ -419,7 +464,12 @@ class _ConvNHWC(torch.autograd.Function):
                 dw = dw.to(w.dtype)
         if has_b and ctx.needs_input_grad[2]:
             db = dy.reshape(-1, dy.shape[-1]).float().sum(0).to(dy.dtype)
-        return dx, dw, db, None, None, None, None
+        prod = ctx.produce
+        if prod is not None and dx is not None and not prod.consumed:
+            dx = dx if dx.is_contiguous() else dx.contiguous()
+            prod.dres = dx if prod.dres is None else prod.dres.add_(dx)
+            dx = None  # the block's first conv adds it (residual_grad_producer)
+        return dx, dw, db, None, None, None, None, None
 
 
 def conv2d_nhwc(x, w, b, stride, pad, dil):
@@ -429,7 +479,10 @@ def conv2d_nhwc(x, w, b, stride, pad, dil):
     sink = _SINK[0] if (w.shape[2] == 1 and w.shape[3] == 1 and stride == 1) else None
     if sink is not None:
         sink.armed = True
-    return _ConvNHWC.apply(x, w, b, stride, pad, dil, sink)
+    produce, _PRODUCER[0] = _PRODUCER[0], None
+    if produce is not None and produce is sink:
+        produce = None
+    return _ConvNHWC.apply(x, w, b, stride, pad, dil, sink, produce)
 
 
 def eligible_nhwc(x_nhwc, w, groups):

@@ -66,17 +66,17 @@ class BottleneckBlock(nn.Layer):
     def forward(self, x):
         identity = x
         sink = None
-        if self.downsample is None:
-            # identity shortcut: x's two gradients (residual, conv1) are summed in conv1's GEMM epilogue
-            from ...ops.conv import residual_grad_sink
-            with residual_grad_sink() as sink:
-                h = self.conv1(x)
-        else:
+        from ...ops.conv import residual_grad_producer, residual_grad_sink
+        # x's two gradients are summed in conv1's GEMM epilogue: the other one comes from bn3 (identity shortcut)
+        # or from the shortcut convolution (projection shortcut, residual_grad_producer)
+        with residual_grad_sink() as sink:
             h = self.conv1(x)
         out = _bn_act(self.bn1, h)
         out = _bn_act(self.bn2, self.conv2(out))
         if self.downsample is not None:
-            identity = self.downsample(x)
+            with residual_grad_producer(sink):
+                identity = self.downsample(x)
+            sink = None
         return _bn_act(self.bn3, self.conv3(out), "relu", identity, grad_sink=sink)
 
 

@@ -186,3 +186,67 @@ def test_bottleneck_residual_grad_sink_matches_autograd_sum_gpu():
     assert (gx_s - gx_r).abs().max().item() < 2e-2 * scale
     for a, b in zip(gp_s, gp_r):
         assert (a - b).abs().max().item() <= 2e-2 * max(b.abs().max().item(), 1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stride", [1, 2])
+def test_projection_block_residual_grad_producer_gpu(stride):
+    """Projection-shortcut bottleneck: the shortcut conv hands dx to conv1's epilogue (residual_grad_producer);
+    gradients match the same block with the hand-off disabled (autograd sums the two gradients of x)."""
+    from paddlepaddle_amd.ops import _loader as L
+    from paddlepaddle_amd.ops import conv as C
+    from paddlepaddle_amd.vision.models import resnet as RN
+    paddle.set_device("gpu")
+    paddle.seed(4)
+    paddle.set_default_dtype("bfloat16")
+    try:
+        ds = paddle.nn.Sequential(paddle.nn.Conv2D(128, 256, 1, stride=stride, bias_attr=False, data_format="NHWC"),
+                                  paddle.nn.BatchNorm2D(256, data_format="NHWC"))
+        blk = RN.BottleneckBlock(128, 64, stride=stride, downsample=ds, data_format="NHWC")
+    finally:
+        paddle.set_default_dtype("float32")
+    g = torch.Generator(device="cuda").manual_seed(1)
+    xt = torch.randn(8, 14, 14, 128, device="cuda", generator=g, dtype=torch.bfloat16)
+    ho = 14 // stride
+    dy = torch.randn(8, ho, ho, 256, device="cuda", generator=g, dtype=torch.bfloat16)
+    orig = C.residual_grad_producer
+    produced = []
+
+    class spy(orig):
+        def __exit__(self, *exc):
+            produced.append(self.sink is not None and self.sink.armed)
+            return super().__exit__(*exc)
+
+    class off:
+        def __init__(self, sink):
+            pass
+
+        def __enter__(self):
+            return None
+
+        def __exit__(self, *exc):
+            return False
+
+    def run(factory):
+        C.residual_grad_producer = factory
+        try:
+            x = paddle.Tensor(xt.clone().requires_grad_(True))
+            for p in blk.parameters():
+                p.clear_gradient(set_to_zero=False)
+            blk(x)._t.backward(dy)
+            return x._t.grad.float(), [p.grad._t.float().clone() for p in blk.parameters()]
+        finally:
+            C.residual_grad_producer = orig
+    old = paddle.get_flags("FLAGS_gemm_backend")["FLAGS_gemm_backend"]
+    paddle.set_flags({"FLAGS_gemm_backend": "hip"})
+    try:
+        L.CALLS.clear()
+        gx_s, gp_s = run(spy)
+        gx_r, gp_r = run(off)
+    finally:
+        paddle.set_flags({"FLAGS_gemm_backend": old})
+    assert produced and all(produced), "conv1 did not arm the sink on the hand-written path"
+    scale = gx_r.abs().max().item()
+    assert (gx_s - gx_r).abs().max().item() < 2e-2 * scale
+    for a, b in zip(gp_s, gp_r):
+        assert (a - b).abs().max().item() <= 2e-2 * max(b.abs().max().item(), 1e-3)

@@ -97,3 +97,27 @@ def test_conv_nhwc_skinny_1x1(monkeypatch, cin, cout):
     _close(y, yr, "y")
     _close(xx.grad, dxr + dres.float(), "dx + dres")
     _close(ww.grad, dwr, "dw")
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_conv_nhwc_skinny_3x3(monkeypatch, stride):
+    """3x3 C=Cout=64 forward (stride 1 / 2) and stride-1 data gradient on the skinny implicit-GEMM kernel, padding
+    taps read as zeros past the buffer end."""
+    forced = {"convf": "skinny", "convd": "skinny", "convw": "hip"}
+    monkeypatch.setattr(C, "_pick", lambda key, own, mi, skinny=None: forced[key[0]] if skinny is not None or
+                        forced[key[0]] != "skinny" else "hip")
+    g = torch.Generator(device="cuda").manual_seed(7 + stride)
+    x = torch.randn(3, 15, 13, 64, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(64, 64, 3, 3, device="cuda", generator=g) * 0.05).bfloat16()
+    assert C._skinny_ok(x, w, stride, False, 1, 1) and C._skinny_ok(x, w, 1, True, 1, 1)
+    xx = x.clone().requires_grad_(True)
+    ww = w.clone().requires_grad_(True)
+    L.CALLS.clear()
+    y = C.conv2d_nhwc(xx, ww, None, stride, 1, 1)
+    dy = torch.randn(y.shape, device="cuda", generator=g).bfloat16()
+    y.backward(dy)
+    assert L.calls("pa_conv_skinny") == (2 if stride == 1 else 1)
+    yr, dxr, dwr = _ref(x, w, None, stride, 1, dy)
+    _close(y, yr, "y")
+    _close(xx.grad, dxr, "dx")
+    _close(ww.grad, dwr, "dw")

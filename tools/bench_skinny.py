@@ -51,5 +51,27 @@ def main():
         print(line, flush=True)
 
 
+def conv3x3():
+    from paddlepaddle_amd.ops import conv as C
+    for (H, Cc, s) in [(56, 64, 1), (56, 64, 2)]:
+        x = torch.randn(256, H, H, Cc, device="cuda").bfloat16()
+        w = (torch.randn(Cc, Cc, 3, 3, device="cuda") * 0.05).bfloat16()
+        wk = w.permute(0, 2, 3, 1).contiguous()
+        t_sk = timeit(lambda: C._skinny_conv(x, wk, None, 256, H, H, Cc, Cc, 3, 3, s, 1))
+        if len(sys.argv) > 1:  # one PA_SKCONV_CFG per process (the launcher reads it once)
+            print(f"cfg {os.environ.get('PA_SKCONV_CFG', '0')} H{H} s{s}: {t_sk:.1f} us", flush=True)
+            continue
+        t_im = timeit(lambda: C._implicit_fwd(x, wk, None, 256, H, H, Cc, Cc, 3, 3, s, 1, 1))
+        t_mi = timeit(lambda: C._mi_fwd(x, w, None, s, 1, 1))
+        ref = C._mi_fwd(x, w, None, s, 1, 1).float()
+        err = (C._skinny_conv(x, wk, None, 256, H, H, Cc, Cc, 3, 3, s, 1).float() - ref).abs().max().item()
+        fl = 2 * ref.numel() * Cc * 9
+        print(f"conv3x3 H{H} C{Cc} s{s}: skinny {t_sk:6.1f} us ({fl / t_sk / 1e6:5.0f} TF) | implicit {t_im:6.1f} | "
+              f"MIOpen {t_mi:6.1f} | max err {err:.3g} (max |y| {ref.abs().max().item():.3g})", flush=True)
+
+
 if __name__ == "__main__":
+    conv3x3()
+    if len(sys.argv) > 1:
+        sys.exit(0)
     main()
