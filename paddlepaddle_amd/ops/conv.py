@@ -398,15 +398,44 @@ def _own_wgrad(x, w, dy, stride, pad, dil):
     return _implicit_wgrad(x, dy, w, N, H, W, C, Cout, KH, KW, stride, pad, dil, dy.shape[1], dy.shape[2])
 
 
-def _pick(key, own, mi, skinny=None):
-    """'hip' | 'skinny' | 'blas' for one direction (ops/gemm.py choose(): timed once, persisted). 'skinny' is the
-    memory-bound 1x1 kernel, offered when the shape fits it."""
+def _pick(key, own, mi, skinny=None, mm=None):
+    """'hip' | 'skinny' | 'mm' | 'blas' for one direction (ops/gemm.py choose(): timed once, persisted). 'skinny'
+    is the memory-bound kernel, offered when the shape fits it; 'mm' a 1x1 product as a hipBLASLt GEMM. Timed
+    with cold caches: in a training step every activation streams from HBM, while a repeated call would find a
+    100 MB input in the 256 MB MALL and favour the kernels that profit most from that."""
     if L.flag("FLAGS_gemm_backend", "auto") != "auto":
         return G.choose(key, {"hip": None, "blas": None})
     cands = {"hip": own, "blas": mi}
     if skinny is not None:
         cands["skinny"] = skinny
-    return G.choose(key, cands)
+    if mm is not None:
+        cands["mm"] = mm
+    return G.choose(key, cands, cold=True)
+
+
+def _mm_fwd(x, w, b, stride):
+    """1x1 forward as a hipBLASLt GEMM (the 'mm' candidate)."""
+    N, C, Cout = x.shape[0], x.shape[3], w.shape[0]
+    xs = x[:, ::stride, ::stride, :].contiguous() if stride > 1 else x
+    x2 = xs.reshape(-1, C)
+    w2 = w.reshape(Cout, C)
+    y2 = torch.mm(x2, w2.t()) if b is None else torch.addmm(b, x2, w2.t())
+    return y2.view(N, xs.shape[1], xs.shape[2], Cout)
+
+
+def _mm_dgrad(x, w, dy, stride, acc=None):
+    N, H, W, C = x.shape
+    Cout = w.shape[0]
+    dy2 = dy.reshape(-1, Cout)
+    w2 = w.reshape(Cout, C)
+    if acc is not None and stride == 1:
+        return acc.view(-1, C).addmm_(dy2, w2).view(N, H, W, C)
+    dx = torch.mm(dy2, w2).view(N, dy.shape[1], dy.shape[2], C)
+    if stride > 1:
+        full = torch.zeros(N, H, W, C, dtype=dx.dtype, device=dx.device)
+        full[:, ::stride, ::stride, :] = dx
+        dx = full
+    return dx
 
 
 class _ConvNHWC(torch.autograd.Function):
@@ -415,10 +444,15 @@ class _ConvNHWC(torch.autograd.Function):
         key = (tuple(x.shape), tuple(w.shape), stride, pad, dil)
         sk = (lambda: _own_fwd(x, w, b, stride, pad, dil, skinny=True)) \
             if _skinny_ok(x, w, stride, False, pad, dil) else None
+        one = w.shape[2] == 1 and w.shape[3] == 1
         ch = _pick(("convf",) + key + (b is not None,), lambda: _own_fwd(x, w, b, stride, pad, dil),
-                   lambda: _mi_fwd(x, w, b, stride, pad, dil), sk)
-        y = _mi_fwd(x, w, b, stride, pad, dil) if ch == "blas" else \
-            _own_fwd(x, w, b, stride, pad, dil, skinny=ch == "skinny")
+                   lambda: _mi_fwd(x, w, b, stride, pad, dil), sk, (lambda: _mm_fwd(x, w, b, stride)) if one else None)
+        if ch == "blas":
+            y = _mi_fwd(x, w, b, stride, pad, dil)
+        elif ch == "mm":
+            y = _mm_fwd(x, w, b, stride)
+        else:
+            y = _own_fwd(x, w, b, stride, pad, dil, skinny=ch == "skinny")
         ctx.save_for_backward(x, w)
         ctx.cfg = (stride, pad, dil, b is not None, key)
         ctx.sink = sink
@@ -441,9 +475,15 @@ class _ConvNHWC(torch.autograd.Function):
             if _own_dgrad_ok(x, w, stride, pad, dil):
                 sk = (lambda: _own_dgrad(x, w, dy, stride, pad, dil, skinny=True)) \
                     if _skinny_ok(x, w, stride, True, pad, dil) else None
+                one = w.shape[2] == 1 and w.shape[3] == 1
                 ch = _pick(("convd",) + key, lambda: _own_dgrad(x, w, dy, stride, pad, dil),
-                           lambda: _mi_bwd(x, w, dy, stride, pad, dil, [True, False]), sk)
-            if ch != "blas":
+                           lambda: _mi_bwd(x, w, dy, stride, pad, dil, [True, False]), sk,
+                           (lambda: _mm_dgrad(x, w, dy, stride)) if one else None)
+            if ch == "mm":
+                dx = _mm_dgrad(x, w, dy, stride, acc=dres)
+                if dres is not None and stride != 1:
+                    dx = dx + dres
+            elif ch != "blas":
                 dx = _own_dgrad(x, w, dy, stride, pad, dil, acc=dres, skinny=ch == "skinny")
                 if dres is not None and not (w.shape[2] == 1 and w.shape[3] == 1 and stride == 1):
                     dx = dx + dres

@@ -31,7 +31,7 @@ def _close(got, exp, what):
 @pytest.mark.parametrize("combo", list(itertools.product(["hip", "blas"], repeat=3)))
 def test_conv_nhwc_per_direction(monkeypatch, k, stride, cin, cout, hw, combo):
     forced = dict(zip(("convf", "convd", "convw"), combo))
-    monkeypatch.setattr(C, "_pick", lambda key, own, mi, skinny=None: forced[key[0]])
+    monkeypatch.setattr(C, "_pick", lambda key, own, mi, skinny=None, mm=None: forced[key[0]])
     g = torch.Generator(device="cuda").manual_seed(k * 10 + stride)
     x = torch.randn(4, hw, hw, cin, device="cuda", generator=g).bfloat16()
     w = (torch.randn(cout, cin, k, k, device="cuda", generator=g) * 0.1).bfloat16()
@@ -58,7 +58,7 @@ def test_conv_nhwc_per_direction(monkeypatch, k, stride, cin, cout, hw, combo):
 def test_conv_nhwc_residual_sink(monkeypatch, dgrad):
     """A d(residual) parked in the sink is added to dx whichever backend computes the data gradient."""
     forced = {"convf": "hip", "convd": dgrad, "convw": "hip"}
-    monkeypatch.setattr(C, "_pick", lambda key, own, mi, skinny=None: forced[key[0]])
+    monkeypatch.setattr(C, "_pick", lambda key, own, mi, skinny=None, mm=None: forced[key[0]])
     g = torch.Generator(device="cuda").manual_seed(5)
     x = torch.randn(2, 8, 8, 128, device="cuda", generator=g).bfloat16()
     w = (torch.randn(64, 128, 1, 1, device="cuda", generator=g) * 0.1).bfloat16()
@@ -78,7 +78,7 @@ def test_conv_nhwc_residual_sink(monkeypatch, dgrad):
 def test_conv_nhwc_skinny_1x1(monkeypatch, cin, cout):
     """1x1 forward and data gradient on the memory-bound kernel (gemm_skinny), with the residual sink."""
     forced = {"convf": "skinny", "convd": "skinny", "convw": "hip"}
-    monkeypatch.setattr(C, "_pick", lambda key, own, mi, skinny=None: forced[key[0]])
+    monkeypatch.setattr(C, "_pick", lambda key, own, mi, skinny=None, mm=None: forced[key[0]])
     g = torch.Generator(device="cuda").manual_seed(cin + cout)
     x = torch.randn(4, 16, 16, cin, device="cuda", generator=g).bfloat16()
     w = (torch.randn(cout, cin, 1, 1, device="cuda", generator=g) * 0.1).bfloat16()
@@ -104,7 +104,7 @@ def test_conv_nhwc_skinny_3x3(monkeypatch, stride):
     """3x3 C=Cout=64 forward (stride 1 / 2) and stride-1 data gradient on the skinny implicit-GEMM kernel, padding
     taps read as zeros past the buffer end."""
     forced = {"convf": "skinny", "convd": "skinny", "convw": "hip"}
-    monkeypatch.setattr(C, "_pick", lambda key, own, mi, skinny=None: forced[key[0]] if skinny is not None or
+    monkeypatch.setattr(C, "_pick", lambda key, own, mi, skinny=None, mm=None: forced[key[0]] if skinny is not None or
                         forced[key[0]] != "skinny" else "hip")
     g = torch.Generator(device="cuda").manual_seed(7 + stride)
     x = torch.randn(3, 15, 13, 64, device="cuda", generator=g).bfloat16()
@@ -120,4 +120,28 @@ def test_conv_nhwc_skinny_3x3(monkeypatch, stride):
     yr, dxr, dwr = _ref(x, w, None, stride, 1, dy)
     _close(y, yr, "y")
     _close(xx.grad, dxr, "dx")
+    _close(ww.grad, dwr, "dw")
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_conv_nhwc_mm_1x1(monkeypatch, stride):
+    """1x1 forward / data gradient as hipBLASLt GEMMs (the 'mm' candidate), incl. the residual sink at stride 1."""
+    forced = {"convf": "mm", "convd": "mm", "convw": "hip"}
+    monkeypatch.setattr(C, "_pick", lambda key, own, mi, skinny=None, mm=None: forced[key[0]] if mm is not None
+                        else "hip")
+    g = torch.Generator(device="cuda").manual_seed(11 + stride)
+    x = torch.randn(4, 16, 16, 128, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(64, 128, 1, 1, device="cuda", generator=g) * 0.1).bfloat16()
+    dres = torch.randn(x.shape, device="cuda", generator=g).bfloat16()
+    xx = x.clone().requires_grad_(True)
+    ww = w.clone().requires_grad_(True)
+    with C.residual_grad_sink() as s:
+        y = C.conv2d_nhwc(xx, ww, None, stride, 0, 1)
+    if stride == 1:
+        s.dres = dres.clone()
+    dy = torch.randn(y.shape, device="cuda", generator=g).bfloat16()
+    y.backward(dy)
+    yr, dxr, dwr = _ref(x, w, None, stride, 0, dy)
+    _close(y, yr, "y")
+    _close(xx.grad, dxr + (dres.float() if stride == 1 else 0), "dx")
     _close(ww.grad, dwr, "dw")
