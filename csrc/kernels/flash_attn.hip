@@ -139,8 +139,10 @@ PA_EXPORT int pa_flash_attn_bwd_ex(const void* q, const void* k, const void* v, 
   a.scale = scale; a.scale_log2 = scale * kLog2e; a.inv_scale = 1.f / scale; a.causal = causal;
   const char* abl_env = getenv("PA_FA_BWD_ABL");  // measurement ablations only (tools/bench_fa_bwd_abl.py)
   a.abl = abl_env ? atoi(abl_env) : 0;
-  const char* k16_env = getenv("PA_FA_BWD16");  // 16-keys-per-wave backward (D = 128, no mask / dropout)
-  a.k16 = k16_env ? atoi(k16_env) : 0;
+  // 16-keys-per-wave backward (D = 128, no mask / dropout): the default (1.04-1.06x the 4-wave kernel,
+  // profiles/flash_attn_bwd_ablations_r3.md); PA_FA_BWD16=0 selects the 4-wave kernel
+  const char* k16_env = getenv("PA_FA_BWD16");
+  a.k16 = k16_env ? atoi(k16_env) : 1;
   const int BK = D == 256 ? 64 : 128;
   const int nkb = (Sk + BK - 1) / BK;
   a.grp = fa_group(B * Hk, nkb, 32);

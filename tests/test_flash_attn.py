@@ -87,3 +87,14 @@ def test_fa_lse_matches_logsumexp():
     s = s.masked_fill(~torch.ones(S, S, dtype=torch.bool, device="cuda").tril(), float("-inf"))
     ref = torch.logsumexp(s, -1)
     torch.testing.assert_close(lse, ref, atol=2e-2, rtol=1e-3)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("shape", [(2, 256, 256, 4, 4), (1, 300, 300, 2, 2), (2, 192, 192, 8, 2), (1, 128, 320, 2, 2)])
+@pytest.mark.parametrize("k16", ["1", "0"])
+def test_fa_bwd16_kernel(monkeypatch, causal, shape, k16):
+    """Both D = 128 backward kernels — the 8-wave 16-keys-per-wave one (default) and the 4-wave one
+    (PA_FA_BWD16=0) — against the fp32 reference."""
+    monkeypatch.setenv("PA_FA_BWD16", k16)
+    B, Sq, Sk, H, Hk = shape
+    _run(B, Sq, Sk, H, Hk, 128, causal)
