@@ -362,6 +362,150 @@ int launch_skconv(const SkConvArgs& a, hipStream_t st) {
   return 0;
 }
 
+// ---- 3x3, stride 1, pad 1, C = Cout = 64 on a per-wave LDS halo tile. A wave owns a segment of 16 output pixels of
+// one image row; its input window (3 rows x 18 pixels x 64 channels = 6.75 KB) arrives in 7 LDS-DMA instructions
+// (global_load_lds_dwordx4, padding pixels fetched from a zero page), so the 9 taps' A fragments are LDS reads
+// instead of 18 per-tap HBM / L2 gathers. The 16-byte channel chunks of a pixel are XOR-swizzled by the pixel
+// index (conflict-free 16-lane row reads). All 18 A fragments are read into registers before the MFMAs, and the
+// next segment's DMA is issued right then, so the window load overlaps this segment's 72 MFMAs.
+__device__ __forceinline__ void sk_glds16(const void* g, char* lds_wave_base) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(lds_wave_base));
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
+}
+
+struct SkHaloArgs {
+  const uint16_t* x;
+  const uint16_t* w;   // [64][3][3][64]
+  const uint16_t* zero;  // >= 128 zero bytes
+  uint16_t* y;
+  const uint16_t* bias;
+  int N, H, W;  // output = input size (stride 1, pad 1)
+  int flags;
+};
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void skinny_conv_halo_k(SkHaloArgs p) {
+  constexpr int C = 64, NT = 4, K = 9 * C, LDK = K + 8, TILE = 7 * 1024;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* bt = smem;
+  char* tiles = reinterpret_cast<char*>(smem + 16 * NT * LDK);
+  const int tid = threadIdx.x;
+  for (int idx = tid; idx < 16 * NT * (K / 8); idx += NW * 64) {
+    const int n = idx / (K / 8), kc = idx % (K / 8);
+    *reinterpret_cast<uint4*>(bt + n * LDK + kc * 8) = *reinterpret_cast<const uint4*>(p.w + (int64_t)n * K + kc * 8);
+  }
+  __syncthreads();
+  const int wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
+  char* tile = tiles + wave * TILE;
+  const int segs_row = (p.W + 15) / 16;
+  const int64_t nseg = (int64_t)p.N * p.H * segs_row;
+  const int64_t stride = (int64_t)gridDim.x * NW;
+  int64_t sg = (int64_t)blockIdx.x * NW + wave;
+  if (sg >= nseg) return;
+  // DMA of segment s's window: slot q = 64 i + lane (q < 432) -> LDS byte 16 q = (row, px, swizzled chunk)
+  auto load_window = [&](int64_t s) {
+    const int seg = (int)(s % segs_row);
+    const int64_t t1 = s / segs_row;
+    const int ho = (int)(t1 % p.H);
+    const int n = (int)(t1 / p.H);
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int q = 64 * i + lane;
+      const int row = q / 144, px = (q % 144) >> 3, chs = q & 7;
+      const int hi = ho - 1 + row, wi = 16 * seg - 1 + px;
+      const int ch = chs ^ (px & 7);
+      const bool ok = q < 432 && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W;
+      const uint16_t* src = ok ? p.x + (((int64_t)n * p.H + hi) * p.W + wi) * C + 8 * ch : p.zero + 8 * (q & 7);
+      sk_glds16(src, tile + 1024 * i);
+    }
+  };
+  const int brow = 8 * (r >> 2) + (r & 3);
+  load_window(sg);
+  for (; sg < nseg; sg += stride) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's window has landed (its own DMA only)
+    Frag8 af[9][2];
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int kh = tap / 3, kw = tap % 3, px = r + kw;
+#pragma unroll
+      for (int cs = 0; cs < 2; ++cs) {
+        const int ch = (4 * cs + g) ^ (px & 7);
+        af[tap][cs].u = *reinterpret_cast<const uint4*>(tile + ((kh * 18 + px) * 8 + ch) * 16);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // window consumed: the next DMA may overwrite it
+    const int64_t cur = sg;
+    if (sg + stride < nseg) load_window(sg + stride);
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+#pragma unroll
+        for (int cs = 0; cs < 2; ++cs) {
+          Frag8 bf;
+          bf.u = *reinterpret_cast<const uint4*>(bt + (32 * (t >> 1) + 4 * (t & 1) + brow) * LDK + tap * C + 32 * cs +
+                                                 8 * g);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf.v, af[tap][cs].v, acc[t], 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const int seg = (int)(cur % segs_row);
+    const int wo = 16 * seg + r;
+    if (wo < p.W) {
+      const int64_t t1 = cur / segs_row;  // n * H + ho
+      uint16_t* dst = p.y + (t1 * p.W + wo) * (16 * NT);
+#pragma unroll
+      for (int q = 0; q < NT / 2; ++q) {
+        const int c0 = 32 * q + 8 * g;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[j] = acc[2 * q][j];
+          v[4 + j] = acc[2 * q + 1][j];
+        }
+        if (p.flags & kSkEpiBias) {
+          const uint4 bb = *reinterpret_cast<const uint4*>(p.bias + c0);
+          const uint32_t w[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[2 * j] += lo_bf16(w[j]);
+            v[2 * j + 1] += hi_bf16(w[j]);
+          }
+        }
+        uint4 o;
+        o.x = pack_bf16(v[0], v[1]);
+        o.y = pack_bf16(v[2], v[3]);
+        o.z = pack_bf16(v[4], v[5]);
+        o.w = pack_bf16(v[6], v[7]);
+        *reinterpret_cast<uint4*>(dst + c0) = o;
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int NW>
+int launch_halo(const SkHaloArgs& a, hipStream_t st) {
+  const size_t lds = (size_t)64 * (9 * 64 + 8) * 2 + (size_t)NW * 7 * 1024;
+  if (lds > 160 * 1024) return 2;
+  const int64_t nseg = (int64_t)a.N * a.H * ((a.W + 15) / 16);
+  const int per_cu = (int)std::max<size_t>(1, (160 * 1024) / lds);
+  const int64_t grid = std::min<int64_t>((nseg + NW - 1) / NW, (int64_t)256 * per_cu);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_conv_halo_k<NW>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((skinny_conv_halo_k<NW>), dim3((unsigned)grid), dim3(NW * 64), lds, st, a);
+  PA_CHECK_LAUNCH();
+  return 0;
+}
+
 }  // namespace
 
 // 1 if (N, K) has an instantiation (N in {32, 64, 128, 256}, K in {32, 64, 128, 256}).
@@ -394,11 +538,12 @@ PA_EXPORT int pa_conv_skinny_ok(int64_t C, int64_t Cout, int64_t KH, int64_t KW)
 }
 
 // NHWC convolution y[N, Ho, Wo, Cout] = conv(x[N, H, W, C], w[Cout][KH][KW][C]) (+ bias), symmetric padding, no
-// dilation, on the skinny implicit-GEMM kernel. x must be below 2 GB (32-bit buffer offsets). Returns 2 if the
+// dilation, on the skinny implicit-GEMM kernels (stride 1 / pad 1: the LDS halo-tile kernel; zero_page: >= 128 zero
+// bytes it reads for padding pixels). x must be below 2 GB (32-bit buffer offsets). Returns 2 if the
 // shape has no instantiation.
-PA_EXPORT int pa_conv_skinny(const void* x, const void* w, const void* bias, void* y, int64_t N, int64_t H, int64_t W,
-                             int64_t C, int64_t Cout, int64_t KH, int64_t KW, int64_t stride, int64_t pad, int64_t Ho,
-                             int64_t Wo, void* stream) {
+PA_EXPORT int pa_conv_skinny(const void* x, const void* w, const void* bias, void* y, const void* zero_page, int64_t N,
+                             int64_t H, int64_t W, int64_t C, int64_t Cout, int64_t KH, int64_t KW, int64_t stride,
+                             int64_t pad, int64_t Ho, int64_t Wo, void* stream) {
   if (!pa_conv_skinny_ok(C, Cout, KH, KW)) return 2;
   const int64_t xb = N * H * W * C * 2;
   if (xb >= ((int64_t)1 << 31) - (1 << 21)) return 2;
@@ -406,6 +551,19 @@ PA_EXPORT int pa_conv_skinny(const void* x, const void* w, const void* bias, voi
                static_cast<const uint16_t*>(bias), N * Ho * Wo, (int)H, (int)W, (int)Ho, (int)Wo, (int)stride, (int)pad,
                (uint32_t)xb, bias ? kSkEpiBias : 0};
   if (a.M <= 0) return 0;
+  if (stride == 1 && pad == 1 && Ho == H && Wo == W && zero_page != nullptr) {
+    static const int halo = [] {  // PA_SKCONV_HALO: 0 = the per-tap gather kernel below, 12 = 12 waves (measurement)
+      const char* e = getenv("PA_SKCONV_HALO");
+      return e ? atoi(e) : 1;
+    }();
+    if (halo) {
+      SkHaloArgs h{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w),
+                   static_cast<const uint16_t*>(zero_page), static_cast<uint16_t*>(y),
+                   static_cast<const uint16_t*>(bias), (int)N, (int)H, (int)W, bias ? kSkEpiBias : 0};
+      return halo == 12 ? launch_halo<12>(h, static_cast<hipStream_t>(stream))
+                        : launch_halo<8>(h, static_cast<hipStream_t>(stream));
+    }
+  }
   static const int cfg = [] {  // PA_SKCONV_CFG (measurement): 0 = R2 x 4 waves, 1 = R1 x 8, 2 = R2 x 8, 3 = R1 x 4
     const char* e = getenv("PA_SKCONV_CFG");
     return e ? atoi(e) : 0;

@@ -309,8 +309,8 @@ def _skinny_conv(x, wk, b, N, H, W, C, Cout, KH, KW, stride, pad):
     Ho = (H + 2 * pad - KH) // stride + 1
     Wo = (W + 2 * pad - KW) // stride + 1
     out = torch.empty(N, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
-    L.call("pa_conv_skinny", L.ptr(x), L.ptr(wk), L.ptr(b), L.ptr(out), N, H, W, C, Cout, KH, KW, stride, pad, Ho, Wo,
-           L.stream_ptr())
+    L.call("pa_conv_skinny", L.ptr(x), L.ptr(wk), L.ptr(b), L.ptr(out), L.ptr(_zero_page(x.device)), N, H, W, C, Cout,
+           KH, KW, stride, pad, Ho, Wo, L.stream_ptr())
     return out
 
 
