@@ -552,16 +552,18 @@ PA_EXPORT int pa_conv_skinny(const void* x, const void* w, const void* bias, voi
                (uint32_t)xb, bias ? kSkEpiBias : 0};
   if (a.M <= 0) return 0;
   if (stride == 1 && pad == 1 && Ho == H && Wo == W && zero_page != nullptr) {
-    static const int halo = [] {  // PA_SKCONV_HALO: 0 = the per-tap gather kernel below, 12 = 12 waves (measurement)
+    // PA_SKCONV_HALO (measurement): 0 = the per-tap gather kernel below, 8 = 8 waves per workgroup; default 12 waves
+    // (3 per SIMD, 160 KB of LDS: 89.7 vs 96.3 us with 8, profiles/conv3x3_skinny_sweep_r3.log)
+    static const int halo = [] {
       const char* e = getenv("PA_SKCONV_HALO");
-      return e ? atoi(e) : 1;
+      return e ? atoi(e) : 12;
     }();
     if (halo) {
       SkHaloArgs h{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w),
                    static_cast<const uint16_t*>(zero_page), static_cast<uint16_t*>(y),
                    static_cast<const uint16_t*>(bias), (int)N, (int)H, (int)W, bias ? kSkEpiBias : 0};
-      return halo == 12 ? launch_halo<12>(h, static_cast<hipStream_t>(stream))
-                        : launch_halo<8>(h, static_cast<hipStream_t>(stream));
+      return halo == 8 ? launch_halo<8>(h, static_cast<hipStream_t>(stream))
+                       : launch_halo<12>(h, static_cast<hipStream_t>(stream));
     }
   }
   static const int cfg = [] {  // PA_SKCONV_CFG (measurement): 0 = R2 x 4 waves, 1 = R1 x 8, 2 = R2 x 8, 3 = R1 x 4
