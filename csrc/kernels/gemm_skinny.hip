@@ -506,6 +506,123 @@ int launch_halo(const SkHaloArgs& a, hipStream_t st) {
   return 0;
 }
 
+// ---- 3x3 stride-1 pad-1 weight gradient, C = Cout = 64: dW[co][kh][kw][c] = sum_px dY[px][co] X[px + tap][c].
+// A workgroup of 9 waves (one per tap) walks 32-pixel row pieces of its share of the image rows: the piece's dY tile
+// [32 px][64 co] and input window [3 rows][34 px][64 c] (16.75 KB) arrive by LDS-DMA into a double buffer; both MFMA
+// operands are pixel-contiguous columns of those row-major tiles, read with ds_read_b64_tr_b16 (the hardware
+// transpose). Each wave accumulates its tap's 64 x 64 block (16 tiles of 16x16) over the pieces and writes an fp32
+// slab per workgroup; the slabs are summed afterwards (split over pixels).
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ s16x4_t sk_lds_tr(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4_t*)(reinterpret_cast<uintptr_t>(p)));
+}
+
+// 16-byte chunk swizzle of a 128-byte pixel row of the weight-gradient tiles: pixels 4 apart (the rows of one
+// transposed read) and 8 apart (the two 16-lane groups of a half-wave) land on different banks
+__device__ __forceinline__ int wg_swz(int px) { return (px & 3) ^ (((px >> 3) & 1) << 2); }  // conflict-free (bank model)
+
+struct SkWgArgs {
+  const uint16_t* x;
+  const uint16_t* dy;
+  const uint16_t* zero;
+  float* ws;  // [gridDim.x][64][9][64]
+  int N, H, W;
+};
+
+__global__ __launch_bounds__(576) void skinny_wgrad3_k(SkWgArgs p) {
+  // 1152 DMA slots of 16 B per stage; NST stages: pieces s+1 .. s+NST-1 are in flight while piece s is multiplied
+  // (the DMA latency under load, ~2 us, is several pieces' worth of MFMA work)
+  constexpr int C = 64, DY_B = 32 * 128, WIN_B = 3 * 34 * 128, STAGE = 18 * 1024, NST = 4;
+  __shared__ __attribute__((aligned(16))) char lds[NST * STAGE];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int l16 = lane & 15, g = lane >> 4, q = l16 >> 2, pp = l16 & 3;
+  const int pieces_row = (p.W + 31) / 32;
+  const int64_t npieces = (int64_t)p.N * p.H * pieces_row;
+  const int64_t per = (npieces + gridDim.x - 1) / gridDim.x;
+  const int64_t p0 = (int64_t)blockIdx.x * per;
+  const int64_t p1 = p0 + per < npieces ? p0 + per : npieces;
+  // DMA of piece s into stage st: slots 0..255 = dY tile (px, chunk), 256..1071 = window (row, px, chunk); the
+  // remaining slots load the zero page into the stage's tail
+  auto load_piece = [&](int64_t s, int st) {
+    const int pc = (int)(s % pieces_row);
+    const int64_t t1 = s / pieces_row;
+    const int ho = (int)(t1 % p.H);
+    const int n = (int)(t1 / p.H);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int slot = 576 * i + tid;  // wave-contiguous 1 KB pieces: slot = 64 * (9 i + wave) + lane
+      const uint16_t* src = p.zero + 8 * (slot & 7);
+      if (slot < 256) {
+        const int px = slot >> 3, ch = (slot & 7) ^ wg_swz(px), wo = 32 * pc + px;
+        if (wo < p.W) src = p.dy + (((int64_t)n * p.H + ho) * p.W + wo) * C + 8 * ch;
+      } else if (slot < 256 + 816) {
+        const int u = slot - 256, row = u / 272, px = (u % 272) >> 3, ch = (u & 7) ^ wg_swz(px);
+        const int hi = ho - 1 + row, wi = 32 * pc - 1 + px;
+        if ((unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
+          src = p.x + (((int64_t)n * p.H + hi) * p.W + wi) * C + 8 * ch;
+      }
+      sk_glds16(src, lds + st * STAGE + 1024 * (9 * i + wave));
+    }
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kh = wave / 3, kw = wave % 3;
+#pragma unroll
+  for (int j = 0; j < NST - 1; ++j)
+    if (p0 + j < p1) load_piece(p0 + j, j);
+  for (int64_t s = p0; s < p1; ++s) {
+    const int st = (int)((s - p0) % NST);
+    // this wave's DMA of piece s has landed once at most 2 per younger piece in flight remain outstanding
+    const int64_t younger = p1 - 1 - s < NST - 2 ? p1 - 1 - s : NST - 2;
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave's DMA of piece s landed; stage (s - 1) % NST was read in the last step
+    if (s + NST - 1 < p1) load_piece(s + NST - 1, (int)((s + NST - 1 - p0) % NST));
+    const char* dyt = lds + st * STAGE;
+    const char* win = dyt + DY_B;
+    // k (pixel) = 8 g + 4 h + element; A = dY^T (row co), B = window pixels (column c)
+    Frag8 af[4], bfr[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int pa = 8 * g + 4 * h + q, pb = pa + kw;  // dY tile pixel, window pixel of this lane's row
+        const s16x4_t va = sk_lds_tr(dyt + pa * 128 + (((2 * t + (pp >> 1)) ^ wg_swz(pa)) << 4) + 8 * (pp & 1));
+        const s16x4_t vb = sk_lds_tr(win + (kh * 34 + pb) * 128 + (((2 * t + (pp >> 1)) ^ wg_swz(pb)) << 4) +
+                                     8 * (pp & 1));
+        af[t].u = h == 0 ? make_uint4(__builtin_bit_cast(uint2, va).x, __builtin_bit_cast(uint2, va).y, af[t].u.z,
+                                      af[t].u.w)
+                         : make_uint4(af[t].u.x, af[t].u.y, __builtin_bit_cast(uint2, va).x,
+                                      __builtin_bit_cast(uint2, va).y);
+        bfr[t].u = h == 0 ? make_uint4(__builtin_bit_cast(uint2, vb).x, __builtin_bit_cast(uint2, vb).y, bfr[t].u.z,
+                                       bfr[t].u.w)
+                          : make_uint4(bfr[t].u.x, bfr[t].u.y, __builtin_bit_cast(uint2, vb).x,
+                                       __builtin_bit_cast(uint2, vb).y);
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a].v, bfr[b].v, acc[a][b], 0, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // slab [64 co][9 taps][64 c]: lane holds rows co = 16 a + 4 g + i, column c = 16 b + l16
+  float* slab = p.ws + (int64_t)blockIdx.x * (64 * 9 * 64);
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        slab[((16 * a + 4 * g + i) * 9 + wave) * 64 + 16 * b + l16] = acc[a][b][i];
+}
+
 }  // namespace
 
 // 1 if (N, K) has an instantiation (N in {32, 64, 128, 256}, K in {32, 64, 128, 256}).
@@ -577,4 +694,16 @@ PA_EXPORT int pa_conv_skinny(const void* x, const void* w, const void* bias, voi
     case 3: return launch_skconv<4, 64, 3, 3, 1, 4>(a, st);
     default: return launch_skconv<4, 64, 3, 3, 2, 4>(a, st);
   }
+}
+
+// dW partial slabs of the 3x3 stride-1 pad-1 C = Cout = 64 weight gradient (skinny_wgrad3_k): ws holds `splits`
+// fp32 [64][3][3][64] slabs (sum them for dW in [Cout][KH][KW][C]). Returns 2 for other shapes.
+PA_EXPORT int pa_conv_skinny_wgrad(const void* x, const void* dy, const void* zero_page, float* ws, int64_t N, int64_t H,
+                                   int64_t W, int64_t C, int64_t Cout, int64_t splits, void* stream) {
+  if (C != 64 || Cout != 64 || splits < 1 || zero_page == nullptr) return 2;
+  SkWgArgs a{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(zero_page),
+             ws, (int)N, (int)H, (int)W};
+  hipLaunchKernelGGL(skinny_wgrad3_k, dim3((unsigned)splits), dim3(576), 0, static_cast<hipStream_t>(stream), a);
+  PA_CHECK_LAUNCH();
+  return 0;
 }

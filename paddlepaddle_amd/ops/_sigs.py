@@ -73,6 +73,7 @@ SIGS = {
     "pa_gemm_skinny_ok": [_i64, _i64],
     "pa_conv_skinny": [_vp, _vp, _vp, _vp, _vp] + [_i64] * 11 + [_vp],
     "pa_conv_skinny_ok": [_i64, _i64, _i64, _i64],
+    "pa_conv_skinny_wgrad": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp],
     "pa_conv2d_nhwc_fwd": [_vp, _vp, _vp, _vp, _vp] + [_i32] * 13 + [_vp],
     "pa_conv2d_nhwc_wgrad": [_vp, _vp, _vp, _vp] + [_i32] * 15 + [_vp],
     "pa_bias_gelu_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp],

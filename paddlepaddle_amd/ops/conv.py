@@ -398,6 +398,24 @@ def _own_wgrad(x, w, dy, stride, pad, dil):
     return _implicit_wgrad(x, dy, w, N, H, W, C, Cout, KH, KW, stride, pad, dil, dy.shape[1], dy.shape[2])
 
 
+def _skinny_wgrad_ok(x, w, dy, stride, pad, dil):
+    """3x3 stride-1 pad-1 C = Cout = 64 weight gradient on the halo-tile kernel (pa_conv_skinny_wgrad)."""
+    return (L.has("pa_conv_skinny_wgrad") and tuple(w.shape) == (64, 64, 3, 3) and x.shape[3] == 64 and stride == 1
+            and pad == 1 and dil == 1 and tuple(dy.shape[1:3]) == tuple(x.shape[1:3]))
+
+
+def _skinny_wgrad(x, dy, w):
+    N, H, W, C = x.shape
+    npieces = N * H * (-(-W // 32))
+    splits = max(1, min(256, npieces))
+    ws = torch.empty(splits, 64 * 9 * 64, dtype=torch.float32, device=x.device)
+    L.call("pa_conv_skinny_wgrad", L.ptr(x), L.ptr(dy), L.ptr(_zero_page(x.device)), L.ptr(ws), N, H, W, C, 64,
+           splits, L.stream_ptr())
+    dw = ws.sum(0).view(64, 3, 3, 64).permute(0, 3, 1, 2).to(w.dtype)
+    return dw.contiguous(memory_format=torch.channels_last) \
+        if w.is_contiguous(memory_format=torch.channels_last) and not w.is_contiguous() else dw.contiguous()
+
+
 def _pick(key, own, mi, skinny=None, mm=None):
     """'hip' | 'skinny' | 'mm' | 'blas' for one direction (ops/gemm.py choose(): timed once, persisted). 'skinny'
     is the memory-bound kernel, offered when the shape fits it; 'mm' a 1x1 product as a hipBLASLt GEMM. Timed
@@ -494,12 +512,17 @@ class _ConvNHWC(torch.autograd.Function):
         elif dres is not None:
             dx = dres
         if ctx.needs_input_grad[1]:
-            own = _own_wgrad_ok(x, w, dy)
-            if own:
-                own = _pick(("convw",) + key, lambda: _own_wgrad(x, w, dy, stride, pad, dil),
-                            lambda: _mi_bwd(x, w, dy, stride, pad, dil, [False, True])) == "hip"
-            dw = _own_wgrad(x, w, dy, stride, pad, dil) if own else _mi_bwd(x, w, dy, stride, pad, dil,
-                                                                            [False, True])[1]
+            ch = "blas"
+            if _own_wgrad_ok(x, w, dy):
+                sk = (lambda: _skinny_wgrad(x, dy, w)) if _skinny_wgrad_ok(x, w, dy, stride, pad, dil) else None
+                ch = _pick(("convw",) + key, lambda: _own_wgrad(x, w, dy, stride, pad, dil),
+                           lambda: _mi_bwd(x, w, dy, stride, pad, dil, [False, True]), sk)
+            if ch == "skinny":
+                dw = _skinny_wgrad(x, dy, w)
+            elif ch == "hip":
+                dw = _own_wgrad(x, w, dy, stride, pad, dil)
+            else:
+                dw = _mi_bwd(x, w, dy, stride, pad, dil, [False, True])[1]
             if dw.dtype != w.dtype:
                 dw = dw.to(w.dtype)
         if has_b and ctx.needs_input_grad[2]:

@@ -145,3 +145,25 @@ def test_conv_nhwc_mm_1x1(monkeypatch, stride):
     _close(y, yr, "y")
     _close(xx.grad, dxr + (dres.float() if stride == 1 else 0), "dx")
     _close(ww.grad, dwr, "dw")
+
+
+@pytest.mark.parametrize("hw", [(15, 16), (12, 40), (8, 64)])
+def test_conv_nhwc_skinny_wgrad_3x3(monkeypatch, hw):
+    """3x3 C=Cout=64 weight gradient on the halo-tile kernel (transposed LDS reads of dY and the input window,
+    fp32 slabs per workgroup) against the fp32 reference, incl. rows wider than one 32-pixel piece."""
+    forced = {"convf": "hip", "convd": "hip", "convw": "skinny"}
+    monkeypatch.setattr(C, "_pick", lambda key, own, mi, skinny=None, mm=None:
+                        forced[key[0]] if (skinny is not None or forced[key[0]] != "skinny") else "hip")
+    g = torch.Generator(device="cuda").manual_seed(hw[1])
+    x = torch.randn(4, hw[0], hw[1], 64, device="cuda", generator=g).bfloat16()  # 4 * H * W pixels: multiple of 64
+    w = (torch.randn(64, 64, 3, 3, device="cuda", generator=g) * 0.05).bfloat16()
+    xx = x.clone().requires_grad_(True)
+    ww = w.clone().requires_grad_(True)
+    L.CALLS.clear()
+    y = C.conv2d_nhwc(xx, ww, None, 1, 1, 1)
+    dy = torch.randn(y.shape, device="cuda", generator=g).bfloat16()
+    y.backward(dy)
+    assert L.calls("pa_conv_skinny_wgrad") == 1
+    _, dxr, dwr = _ref(x, w, None, 1, 1, dy)
+    _close(ww.grad, dwr, "dw")
+    _close(xx.grad, dxr, "dx")

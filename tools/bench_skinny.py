@@ -58,6 +58,15 @@ def conv3x3():
         w = (torch.randn(Cc, Cc, 3, 3, device="cuda") * 0.05).bfloat16()
         wk = w.permute(0, 2, 3, 1).contiguous()
         t_sk = timeit(lambda: C._skinny_conv(x, wk, None, 256, H, H, Cc, Cc, 3, 3, s, 1))
+        if s == 1:
+            dy = torch.randn(256, H, H, Cc, device="cuda").bfloat16()
+            t_wsk = timeit(lambda: C._skinny_wgrad(x, dy, w))
+            t_wim = timeit(lambda: C._implicit_wgrad(x, dy, w, 256, H, H, Cc, Cc, 3, 3, 1, 1, 1, H, H))
+            t_wmi = timeit(lambda: C._mi_bwd(x, w, dy, 1, 1, 1, [False, True]))
+            ref = C._mi_bwd(x, w, dy, 1, 1, 1, [False, True])[1].float()
+            err = (C._skinny_wgrad(x, dy, w).float() - ref).abs().max().item() / ref.abs().max().item()
+            print(f"wgrad3x3 H{H} C{Cc}: skinny {t_wsk:6.1f} us | implicit {t_wim:6.1f} | MIOpen {t_wmi:6.1f} | "
+                  f"rel err {err:.3g}", flush=True)
         if len(sys.argv) > 1:  # one PA_SKCONV_CFG per process (the launcher reads it once)
             print(f"cfg {os.environ.get('PA_SKCONV_CFG', '0')} H{H} s{s}: {t_sk:.1f} us", flush=True)
             continue
