@@ -170,6 +170,17 @@ __global__ __launch_bounds__(256) void skinny_gemm_k(SkArgs p) {
   }
 }
 
+// Opt a kernel into 160 KB of dynamic LDS once per device (the attribute is per device; one process may drive
+// several GPUs). Bit d of `done` marks device d.
+__host__ inline void sk_lds_attr(const void* fn, unsigned long long& done) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const unsigned long long bit = 1ull << (dev & 63);
+  if (done & bit) return;
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  done |= bit;
+}
+
 template <int NT, int KS>
 int launch_sk(const SkArgs& a, hipStream_t st) {
   // two 16-row blocks per wave iteration, except N = 256 (its 128 accumulators would leave one wave per SIMD)
@@ -180,12 +191,8 @@ int launch_sk(const SkArgs& a, hipStream_t st) {
   const int per_cu = (int)std::min<size_t>(8, (160 * 1024) / lds);
   const int64_t nb = (a.M + 16 * R - 1) / (16 * R);
   const int64_t grid = std::min<int64_t>((nb + 3) / 4, (int64_t)256 * per_cu);
-  static bool attr_set = false;  // dynamic LDS above 64 KB needs the attribute
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_k<NT, KS, R>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
+  static unsigned long long attr_done = 0;  // devices whose LDS limit this instantiation raised
+  sk_lds_attr(reinterpret_cast<const void*>(&skinny_gemm_k<NT, KS, R>), attr_done);
   hipLaunchKernelGGL((skinny_gemm_k<NT, KS, R>), dim3((unsigned)grid), dim3(256), lds, st, a);
   PA_CHECK_LAUNCH();
   return 0;
@@ -351,12 +358,8 @@ int launch_skconv(const SkConvArgs& a, hipStream_t st) {
   const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / lds));
   const int64_t nb = (a.M + 16 * R - 1) / (16 * R);
   const int64_t grid = std::min<int64_t>((nb + NW - 1) / NW, (int64_t)256 * per_cu);
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_conv_k<NT, C, KH, KW, R, NW>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
+  static unsigned long long attr_done = 0;  // devices whose LDS limit this instantiation raised
+  sk_lds_attr(reinterpret_cast<const void*>(&skinny_conv_k<NT, C, KH, KW, R, NW>), attr_done);
   hipLaunchKernelGGL((skinny_conv_k<NT, C, KH, KW, R, NW>), dim3((unsigned)grid), dim3(NW * 64), lds, st, a);
   PA_CHECK_LAUNCH();
   return 0;
@@ -495,12 +498,8 @@ int launch_halo(const SkHaloArgs& a, hipStream_t st) {
   const int64_t nseg = (int64_t)a.N * a.H * ((a.W + 15) / 16);
   const int per_cu = (int)std::max<size_t>(1, (160 * 1024) / lds);
   const int64_t grid = std::min<int64_t>((nseg + NW - 1) / NW, (int64_t)256 * per_cu);
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_conv_halo_k<NW>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
+  static unsigned long long attr_done = 0;  // devices whose LDS limit this instantiation raised
+  sk_lds_attr(reinterpret_cast<const void*>(&skinny_conv_halo_k<NW>), attr_done);
   hipLaunchKernelGGL((skinny_conv_halo_k<NW>), dim3((unsigned)grid), dim3(NW * 64), lds, st, a);
   PA_CHECK_LAUNCH();
   return 0;
