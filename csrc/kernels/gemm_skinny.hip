@@ -386,9 +386,11 @@ struct SkHaloArgs {
   int flags;
 };
 
-template <int NW>
+template <int NW, int R>
 __global__ __launch_bounds__(NW * 64) void skinny_conv_halo_k(SkHaloArgs p) {
-  constexpr int C = 64, NT = 4, K = 9 * C, LDK = K + 8, TILE = 7 * 1024;
+  // R: segments of 16 R output pixels (R = 2: every B^T fragment read feeds 2 MFMAs, half the LDS B traffic)
+  constexpr int C = 64, NT = 4, K = 9 * C, LDK = K + 8, WPX = 16 * R + 2, SLOTS = 3 * WPX * 8;
+  constexpr int NI = (SLOTS + 63) / 64, TILE = NI * 1024;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* bt = smem;
   char* tiles = reinterpret_cast<char*>(smem + 16 * NT * LDK);
@@ -400,24 +402,24 @@ __global__ __launch_bounds__(NW * 64) void skinny_conv_halo_k(SkHaloArgs p) {
   __syncthreads();
   const int wave = tid >> 6, lane = tid & 63, r = lane & 15, g = lane >> 4;
   char* tile = tiles + wave * TILE;
-  const int segs_row = (p.W + 15) / 16;
+  const int segs_row = (p.W + 16 * R - 1) / (16 * R);
   const int64_t nseg = (int64_t)p.N * p.H * segs_row;
   const int64_t stride = (int64_t)gridDim.x * NW;
   int64_t sg = (int64_t)blockIdx.x * NW + wave;
   if (sg >= nseg) return;
-  // DMA of segment s's window: slot q = 64 i + lane (q < 432) -> LDS byte 16 q = (row, px, swizzled chunk)
+  // DMA of segment s's window: slot q = 64 i + lane (q < SLOTS) -> LDS byte 16 q = (row, px, swizzled chunk)
   auto load_window = [&](int64_t s) {
     const int seg = (int)(s % segs_row);
     const int64_t t1 = s / segs_row;
     const int ho = (int)(t1 % p.H);
     const int n = (int)(t1 / p.H);
 #pragma unroll
-    for (int i = 0; i < 7; ++i) {
+    for (int i = 0; i < NI; ++i) {
       const int q = 64 * i + lane;
-      const int row = q / 144, px = (q % 144) >> 3, chs = q & 7;
-      const int hi = ho - 1 + row, wi = 16 * seg - 1 + px;
+      const int row = q / (8 * WPX), px = (q % (8 * WPX)) >> 3, chs = q & 7;
+      const int hi = ho - 1 + row, wi = 16 * R * seg - 1 + px;
       const int ch = chs ^ (px & 7);
-      const bool ok = q < 432 && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W;
+      const bool ok = q < SLOTS && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W;
       const uint16_t* src = ok ? p.x + (((int64_t)n * p.H + hi) * p.W + wi) * C + 8 * ch : p.zero + 8 * (q & 7);
       sk_glds16(src, tile + 1024 * i);
     }
@@ -426,22 +428,26 @@ __global__ __launch_bounds__(NW * 64) void skinny_conv_halo_k(SkHaloArgs p) {
   load_window(sg);
   for (; sg < nseg; sg += stride) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's window has landed (its own DMA only)
-    Frag8 af[9][2];
+    Frag8 af[R][9][2];
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int kh = tap / 3, kw = tap % 3, px = r + kw;
+    for (int i = 0; i < R; ++i)
 #pragma unroll
-      for (int cs = 0; cs < 2; ++cs) {
-        const int ch = (4 * cs + g) ^ (px & 7);
-        af[tap][cs].u = *reinterpret_cast<const uint4*>(tile + ((kh * 18 + px) * 8 + ch) * 16);
+      for (int tap = 0; tap < 9; ++tap) {
+        const int kh = tap / 3, kw = tap % 3, px = 16 * i + r + kw;
+#pragma unroll
+        for (int cs = 0; cs < 2; ++cs) {
+          const int ch = (4 * cs + g) ^ (px & 7);
+          af[i][tap][cs].u = *reinterpret_cast<const uint4*>(tile + ((kh * WPX + px) * 8 + ch) * 16);
+        }
       }
-    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // window consumed: the next DMA may overwrite it
     const int64_t cur = sg;
     if (sg + stride < nseg) load_window(sg + stride);
-    f32x4 acc[NT];
+    f32x4 acc[R][NT];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
 #pragma unroll
@@ -451,56 +457,62 @@ __global__ __launch_bounds__(NW * 64) void skinny_conv_halo_k(SkHaloArgs p) {
           Frag8 bf;
           bf.u = *reinterpret_cast<const uint4*>(bt + (32 * (t >> 1) + 4 * (t & 1) + brow) * LDK + tap * C + 32 * cs +
                                                  8 * g);
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf.v, af[tap][cs].v, acc[t], 0, 0, 0);
+#pragma unroll
+          for (int i = 0; i < R; ++i)
+            acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf.v, af[i][tap][cs].v, acc[i][t], 0, 0, 0);
         }
       }
       __builtin_amdgcn_sched_barrier(0);
     }
     const int seg = (int)(cur % segs_row);
-    const int wo = 16 * seg + r;
-    if (wo < p.W) {
-      const int64_t t1 = cur / segs_row;  // n * H + ho
-      uint16_t* dst = p.y + (t1 * p.W + wo) * (16 * NT);
+    const int64_t t1 = cur / segs_row;  // n * H + ho
 #pragma unroll
-      for (int q = 0; q < NT / 2; ++q) {
-        const int c0 = 32 * q + 8 * g;
-        float v[8];
+    for (int i = 0; i < R; ++i) {
+      const int wo = 16 * R * seg + 16 * i + r;
+      if (wo < p.W) {
+        uint16_t* dst = p.y + (t1 * p.W + wo) * (16 * NT);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          v[j] = acc[2 * q][j];
-          v[4 + j] = acc[2 * q + 1][j];
-        }
-        if (p.flags & kSkEpiBias) {
-          const uint4 bb = *reinterpret_cast<const uint4*>(p.bias + c0);
-          const uint32_t w[4] = {bb.x, bb.y, bb.z, bb.w};
+        for (int q = 0; q < NT / 2; ++q) {
+          const int c0 = 32 * q + 8 * g;
+          float v[8];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            v[2 * j] += lo_bf16(w[j]);
-            v[2 * j + 1] += hi_bf16(w[j]);
+            v[j] = acc[i][2 * q][j];
+            v[4 + j] = acc[i][2 * q + 1][j];
           }
+          if (p.flags & kSkEpiBias) {
+            const uint4 bb = *reinterpret_cast<const uint4*>(p.bias + c0);
+            const uint32_t w[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              v[2 * j] += lo_bf16(w[j]);
+              v[2 * j + 1] += hi_bf16(w[j]);
+            }
+          }
+          uint4 o;
+          o.x = pack_bf16(v[0], v[1]);
+          o.y = pack_bf16(v[2], v[3]);
+          o.z = pack_bf16(v[4], v[5]);
+          o.w = pack_bf16(v[6], v[7]);
+          *reinterpret_cast<uint4*>(dst + c0) = o;
         }
-        uint4 o;
-        o.x = pack_bf16(v[0], v[1]);
-        o.y = pack_bf16(v[2], v[3]);
-        o.z = pack_bf16(v[4], v[5]);
-        o.w = pack_bf16(v[6], v[7]);
-        *reinterpret_cast<uint4*>(dst + c0) = o;
       }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int NW>
+template <int NW, int R>
 int launch_halo(const SkHaloArgs& a, hipStream_t st) {
-  const size_t lds = (size_t)64 * (9 * 64 + 8) * 2 + (size_t)NW * 7 * 1024;
+  constexpr int NI = (3 * (16 * R + 2) * 8 + 63) / 64;
+  const size_t lds = (size_t)64 * (9 * 64 + 8) * 2 + (size_t)NW * NI * 1024;
   if (lds > 160 * 1024) return 2;
-  const int64_t nseg = (int64_t)a.N * a.H * ((a.W + 15) / 16);
+  const int64_t nseg = (int64_t)a.N * a.H * ((a.W + 16 * R - 1) / (16 * R));
   const int per_cu = (int)std::max<size_t>(1, (160 * 1024) / lds);
   const int64_t grid = std::min<int64_t>((nseg + NW - 1) / NW, (int64_t)256 * per_cu);
-  static unsigned long long attr_done = 0;  // devices whose LDS limit this instantiation raised
-  sk_lds_attr(reinterpret_cast<const void*>(&skinny_conv_halo_k<NW>), attr_done);
-  hipLaunchKernelGGL((skinny_conv_halo_k<NW>), dim3((unsigned)grid), dim3(NW * 64), lds, st, a);
+  static unsigned long long attr_done = 0;
+  sk_lds_attr(reinterpret_cast<const void*>(&skinny_conv_halo_k<NW, R>), attr_done);
+  hipLaunchKernelGGL((skinny_conv_halo_k<NW, R>), dim3((unsigned)grid), dim3(NW * 64), lds, st, a);
   PA_CHECK_LAUNCH();
   return 0;
 }
@@ -678,8 +690,10 @@ PA_EXPORT int pa_conv_skinny(const void* x, const void* w, const void* bias, voi
       SkHaloArgs h{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w),
                    static_cast<const uint16_t*>(zero_page), static_cast<uint16_t*>(y),
                    static_cast<const uint16_t*>(bias), (int)N, (int)H, (int)W, bias ? kSkEpiBias : 0};
-      return halo == 8 ? launch_halo<8>(h, static_cast<hipStream_t>(stream))
-                       : launch_halo<12>(h, static_cast<hipStream_t>(stream));
+      hipStream_t hs = static_cast<hipStream_t>(stream);
+      if (halo == 8) return launch_halo<8, 1>(h, hs);
+      if (halo == 2) return launch_halo<6, 2>(h, hs);  // 32-pixel segments, 6 waves (measurement)
+      return launch_halo<12, 1>(h, hs);
     }
   }
   static const int cfg = [] {  // PA_SKCONV_CFG (measurement): 0 = R2 x 4 waves, 1 = R1 x 8, 2 = R2 x 8, 3 = R1 x 4
