@@ -10,10 +10,12 @@
 // operator() to run a node (Python-defined functions re-enter Python only inside their own apply), the input
 // metadata to validate each produced gradient (dtype cast, sum-reduction of broadcast dims), release_variables()
 // right after a node ran when the graph is not retained (saved activations are freed as the backward proceeds),
-// and the node-level pre / post hooks. Tensor hooks are the framework's own table (engine.py register_grad_hook /
-// retain: they are also registered with torch for backward passes that go through torch's engine, so torch's
-// tensor hook lists are not run here). It runs on the calling thread and the
-// current HIP stream: no device-thread hand-off per backward pass.
+// and the hooks in torch's order: tensor pre-hooks and retains-grad hooks (Tensor.register_hook / retain_grad
+// through either framework's API, Module full-backward hooks), node pre-hooks, the node, node post-hooks. The
+// framework's own (node, slot) table is only filled when hooks are registered for the pybind fallback.
+// It runs on the calling thread; each node runs on the stream its forward ran on (Node::stream(), as torch's
+// engine does), gradients crossing streams are ordered by an event (producer -> consumer), and the caller's
+// current stream waits for every stream the backward used before it returns: no device-thread hand-off.
 //
 // Python side: paddlepaddle_amd/autograd/engine.py (FLAGS_eager_backward_engine=native) passes the root tensors
 // and seeds, the paddle.grad inputs, and the framework's gradient-hook table keyed by (grad node, slot).
@@ -22,6 +24,9 @@
 #include <torch/csrc/autograd/grad_mode.h>
 #include <torch/csrc/autograd/python_variable.h>
 #include <torch/csrc/autograd/variable.h>
+#include <c10/core/Event.h>
+#include <c10/core/StreamGuard.h>
+#include <c10/core/impl/VirtualGuardImpl.h>
 
 #include <deque>
 #include <string>
@@ -63,6 +68,26 @@ struct XGraph {
     return it == ids.end() ? -1 : it->second;
   }
 };
+
+// consumer stream waits for the producer stream (InputBuffer::add's cross-stream rule)
+void order_streams(const std::optional<c10::Stream>& producer, const std::optional<c10::Stream>& consumer) {
+  if (!producer || !consumer || *producer == *consumer) return;
+  c10::Event ev{producer->device_type()};
+  ev.record(*producer);
+  consumer->wait(ev);
+}
+
+c10::Stream current_stream(const c10::Stream& like) {
+  c10::impl::VirtualGuardImpl impl(like.device_type());
+  return impl.getStream(like.device());
+}
+
+// torch's call_tensor_pre_hooks: Tensor.register_hook hooks, then retain_grad hooks, over the summed inputs
+variable_list tensor_pre_hooks(Node& fn, variable_list inputs) {
+  for (const auto& h : fn.tensor_pre_hooks()) inputs = (*h)(inputs);
+  for (const auto& kv : fn.retains_grad_hooks()) inputs = (*kv.second)(inputs);
+  return inputs;
+}
 
 at::Tensor unpack(py::handle h) {
   if (!THPVariable_Check(h.ptr())) throw std::invalid_argument("expected a torch.Tensor");
@@ -167,6 +192,20 @@ py::list run_backward(py::list roots, py::list captures, py::dict hooks, bool ke
   }
 
   at::AutoGradMode grad_mode(create_graph);
+  // streams: the seeds were produced on the caller's current stream; every stream a node runs on is recorded
+  // so the caller's stream can wait for all of them at the end
+  std::vector<c10::Stream> used;
+  auto note_stream = [&](const std::optional<c10::Stream>& s) {
+    if (!s) return;
+    for (const auto& u : used)
+      if (u == *s) return;
+    used.push_back(*s);
+  };
+  for (int64_t i = 0; i < n; ++i) {
+    if (g.nodes[i].indeg != 0) continue;
+    auto s = g.nodes[i].fn->stream();
+    if (s) order_streams(current_stream(*s), s);
+  }
   std::vector<at::Tensor> captured(cap.size());
   std::deque<int64_t> ready;
   for (int64_t i = 0; i < n; ++i)
@@ -176,6 +215,10 @@ py::list run_backward(py::list roots, py::list captures, py::dict hooks, bool ke
     ready.pop_front();
     auto& nd = g.nodes[id];
     Node& fn = *nd.fn;
+    const std::optional<c10::Stream> stream = fn.stream();
+    note_stream(stream);
+    c10::OptionalStreamGuard guard(stream);
+    if (!fn.tensor_pre_hooks().empty() || !fn.retains_grad_hooks().empty()) nd.buf = tensor_pre_hooks(fn, std::move(nd.buf));
     auto hk = node_hooks.empty() || fn.pyobj() == nullptr ? node_hooks.end() : node_hooks.find(fn.pyobj());
     if (hk != node_hooks.end()) {
       for (auto& sh : hk->second) {
@@ -198,8 +241,13 @@ py::list run_backward(py::list roots, py::list captures, py::dict hooks, bool ke
         variable_list inputs = std::move(nd.buf);
         for (const auto& h : fn.pre_hooks()) inputs = (*h)(inputs);
         if (!keep_graph) fn.will_release_variables();
-        outs = fn(std::move(inputs));
-        for (const auto& h : fn.post_hooks()) outs = (*h)(outs, variable_list());
+        if (fn.post_hooks().empty()) {
+          outs = fn(std::move(inputs));
+        } else {  // post-hooks see (grad outputs, grad inputs), as in torch's call_post_hooks
+          variable_list copy = inputs;
+          outs = fn(std::move(copy));
+          for (const auto& h : fn.post_hooks()) outs = (*h)(outs, inputs);
+        }
         if (!keep_graph) fn.release_variables();
         ran = true;
       }
@@ -212,11 +260,13 @@ py::list run_backward(py::list roots, py::list captures, py::dict hooks, bool ke
       auto& nx = g.nodes[e.first];
       if (ran && k < outs.size() && outs[k].defined()) {
         if (e.second >= nx.buf.size()) nx.buf.resize(e.second + 1);
+        order_streams(stream, nx.fn->stream());
         accumulate(nx.buf[e.second], fix(outs[k], *nx.fn, e.second));
       }
       if (--nx.indeg == 0) ready.push_back(e.first);
     }
   }
+  for (const auto& s : used) order_streams(s, current_stream(s));  // the caller's stream sees every gradient
   py::list res;
   for (auto& c : captured) {
     if (c.defined()) res.append(py::reinterpret_steal<py::object>(THPVariable_Wrap(c)));

@@ -75,13 +75,18 @@ def add_hook(t, fn):
     return remove
 
 
+def runs_tensor_hooks():
+    """True when native backward runs torch's tensor hook lists itself (the C++ executor does, like torch's
+    engine); the pybind fallback traversal applies only the (node, slot) table."""
+    return _executor() is not None
+
+
 def register_grad_hook(t, fn):
     """Gradient hook on a torch tensor under whichever engine will run its backward (torch's hook list, or
     this engine's (node, slot) table)."""
-    if use_native():
-        # both tables: this engine applies its own (node, slot) table; a backward that some code starts through
-        # torch's engine directly (torch.autograd.backward inside recompute / pipeline schedules) runs torch's
-        # hook list. The native executor does not run torch's tensor hooks, so nothing fires twice.
+    if use_native() and not runs_tensor_hooks():
+        # pybind fallback: both tables. It applies its own (node, slot) table; a backward that some code starts
+        # through torch's engine directly (recompute / pipeline schedules) runs torch's hook list.
         rm = add_hook(t, fn)
         h = t.register_hook(fn)
 
@@ -95,17 +100,26 @@ def register_grad_hook(t, fn):
 
 def retain(t):
     """Tensor.retain_grads under the native engine: store the summed slot gradient into ``t.grad``."""
+    import warnings
     import weakref
     if t.is_leaf:
         return
-    t.retain_grad()  # marks .grad readable on the non-leaf; the value is written by the hook below
     ref = weakref.ref(t)
 
     def h(g):
         x = ref()
         if x is not None:
-            x.grad = g.detach() if x.grad is None else x.grad + g.detach()
+            with warnings.catch_warnings():  # reading .grad of a non-leaf without torch's retain flag warns
+                warnings.simplefilter("ignore")
+                cur = x.grad
+            x.grad = g.detach() if cur is None else cur + g.detach()
         return None
+    if runs_tensor_hooks():
+        # a tensor pre-hook in registration order (Paddle: retain_grads is a gradient hook like any other, so
+        # a hook registered after it does not change the retained value)
+        t.register_hook(h)
+        return
+    t.retain_grad()  # marks .grad readable on the non-leaf; the value is written by the hook below
     key = _edge(t)
     _HOOKS.setdefault(key, []).insert(0, h)
 
@@ -163,6 +177,7 @@ def _run(outs, grads, ins, create_graph, retain_graph=None):
     keep = create_graph if retain_graph is None else bool(retain_graph)
     ex = _executor()
     _ACTIVE[0] += 1
+    ok = False
     try:
         if ex is not None:
             res = ex.run_backward(list(zip(outs, grads)), list(ins), _HOOKS, keep, create_graph)
@@ -170,8 +185,17 @@ def _run(outs, grads, ins, create_graph, retain_graph=None):
             roots = [(*_edge(t), g) for t, g in zip(outs, grads)]
             with torch.set_grad_enabled(create_graph):
                 res = native.module().run_backward(roots, [_edge(t) for t in ins], _HOOKS, _HELPERS)
+        ok = True
     finally:
         _ACTIVE[0] -= 1
+        if not _ACTIVE[0] and not ok:
+            # a failed backward must not leave its flush callbacks (DataParallel / sharding finalizers) to fire
+            # at the end of the next, unrelated backward; their owners may queue again on the next pass
+            for fn in _FINAL:
+                owner = getattr(fn, "__self__", None)
+                if owner is not None and getattr(owner, "_queued", False):
+                    owner._queued = False
+            _FINAL.clear()
     if not _ACTIVE[0]:
         _drain()
     return res

@@ -443,14 +443,16 @@ class Tensor:
             r = hook(_wrap(g))
             return None if r is None else _unwrap(r)
         from ..autograd import engine as _eng
-        if _eng.use_native():  # the native engine applies hooks from its (node, slot) table
+        if _eng.use_native() and not _eng.runs_tensor_hooks():
+            # pybind fallback traversal: it applies hooks from the (node, slot) table only
             return _HookHandle(_FnRemover(_eng.add_hook(self._t, _h)))
+        # torch's tensor hook list: run by torch's engine and by the native executor alike
         return _HookHandle(self._t.register_hook(_h))
 
     def retain_grads(self):
         from ..autograd import engine as _eng
         if _eng.use_native():
-            _eng.retain(self._t)
+            _eng.retain(self._t)  # paddle order: the retained value is the slot gradient at registration order
             return
         self._t.retain_grad()
 

@@ -199,6 +199,17 @@ class Adam(Optimizer):
                 if 0 < v < 1 and 0 < b1 < 1:
                     self._param_step[id(p)] = int(round(math.log(v) / math.log(b1)))
         self._tables.clear()
+        # re-seed the device {lr, beta1^t, beta2^t} copies of a later hipGraph-captured step from the restored
+        # step counts (they are otherwise only ever advanced by pa_adam_hyper_step)
+        hs = self.__dict__.get("_graph_hypers") or {}
+        for group in self._param_groups:
+            h = hs.get(id(group))
+            if h is None:
+                continue
+            b1, b2, _ = self._hyper(group)
+            st = max((self._param_step.get(id(p), 0) for p in group["params"]), default=0)
+            with torch.no_grad():
+                h[1:].copy_(torch.tensor([float(b1) ** st, float(b2) ** st], dtype=torch.float32))
 
 
 class AdamW(Adam):

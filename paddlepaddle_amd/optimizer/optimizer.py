@@ -154,19 +154,34 @@ class Optimizer:
 
     # ------------------------------------------------------------------ step
     def clear_grad(self, set_to_zero=True):
+        # DataParallel's flat all-reduce buckets: a bucket may hold parameters of several optimizers (e.g. the
+        # generator and discriminator of one wrapped GAN), so a whole-bucket memset is only legal when every
+        # parameter in it is ours; otherwise only our own slices are zeroed
+        own = {id(p) for p in self._parameter_list}
+        whole = {}
+        for p in self._parameter_list:
+            loc = getattr(p, "_dp_bucket", None)
+            if loc is not None and id(loc[0]) not in whole:
+                whole[id(loc[0])] = all(id(q) in own for q in loc[0].params)
         zeroed = set()
         for p in self._parameter_list:
             loc = getattr(p, "_dp_bucket", None)
             if loc is not None:
-                # DataParallel's flat all-reduce bucket: the grad stays a view of it (releasing it would make
-                # the next backward allocate a fresh gradient that has to be copied back); one memset per bucket
                 bucket, j = loc
-                if id(bucket) not in zeroed:
-                    zeroed.add(id(bucket))
-                    bucket.flat.zero_()
                 v = bucket.view(j)
-                if p._t.grad is None or p._t.grad.data_ptr() != v.data_ptr():
-                    p._t.grad = v
+                if set_to_zero and whole[id(bucket)]:
+                    # the grad stays a view of the bucket (releasing it would make the next backward allocate a
+                    # fresh gradient that has to be copied back); one memset per bucket
+                    if id(bucket) not in zeroed:
+                        zeroed.add(id(bucket))
+                        bucket.flat.zero_()
+                else:
+                    v.zero_()  # an unused parameter contributes zeros to the next all-reduce
+                if set_to_zero:
+                    if p._t.grad is None or p._t.grad.data_ptr() != v.data_ptr():
+                        p._t.grad = v
+                else:
+                    p._t.grad = None  # DataParallel's ready hook folds the next fresh grad back into the bucket
                 continue
             if set_to_zero:
                 if p._t.grad is not None:

@@ -460,25 +460,34 @@ class GroupShardedEngine:
     @torch.no_grad()
     def step(self):
         dp_work = []
+        sp_mp = self.mp_group is not None
+        sp = []
         for u in self.units:
             for f in u.flats:
                 if self.world == 1:
                     f.shard._t.grad = f.alloc_full_grad()
                 else:
                     f.shard._t.grad = f.shard_grad
+                if sp_mp and getattr(f, "sequence_parallel", False):
+                    sp.append(f.shard._t.grad)  # reduced below as one flat over mp, then dp
+                    continue
                 if self.dp_group is not None:  # replicas of this shard: average across the outer dp group
                     g = f.shard._t.grad
                     g.mul_(1.0 / self.dp_group.nranks)
                     dp_work.append(dist.all_reduce(g, group=self.dp_group.process_group, async_op=True))
-        sp = [f.shard._t.grad for u in self.units for f in u.flats if getattr(f, "sequence_parallel", False)]
-        if sp and self.mp_group is not None:
+        if sp:
             # sequence-parallel flats (LayerNorm / row-parallel bias / position table): each mp rank holds the
-            # gradient of its own token blocks; one flat all-reduce over the mp group per optimizer step
+            # gradient of its own token blocks. One flat holds all of them: summed over the mp group first, then
+            # averaged over the dp replicas; the per-flat dp all-reduces above skip these grads, so no collective
+            # ever reads a buffer another one is still writing.
             flat = torch.cat([g.reshape(-1).float() for g in sp])
-            dp_work.append(dist.all_reduce(flat, group=self.mp_group.process_group, async_op=True))
+            dist.all_reduce(flat, group=self.mp_group.process_group)
+            if self.dp_group is not None:
+                flat.mul_(1.0 / self.dp_group.nranks)
+                dp_work.append(dist.all_reduce(flat, group=self.dp_group.process_group, async_op=True))
         for w in dp_work:
             w.wait()
-        if sp and self.mp_group is not None:
+        if sp:
             off = 0
             for g in sp:
                 g.copy_(flat[off:off + g.numel()].view_as(g))

@@ -184,3 +184,83 @@ def test_gpt_tiny_hip_kernels_native_engine():
     assert res["torch"].keys() == res["native"].keys()
     for k in res["torch"]:
         np.testing.assert_allclose(res["torch"][k], res["native"][k], rtol=2e-2, atol=2e-3, err_msg=k)
+
+
+def test_torch_api_hooks_fire_once_under_native_engine():
+    """hooks registered through torch's own API (Tensor.register_hook on the torch tensor, Module
+    full-backward hooks) fire under the native executor; hooks registered through paddle fire exactly once."""
+    with eng("native"):
+        assert engine.runs_tensor_hooks()
+        x = paddle.to_tensor([1.0, 2.0, 3.0], stop_gradient=False)
+        y = x * 2
+        seen_t, seen_p = [], []
+        y._t.register_hook(lambda g: seen_t.append(g.clone()))
+        y.register_hook(lambda g: (seen_p.append(1), g * 3)[1])
+        x._t.register_hook(lambda g: g + 1)  # leaf hook through torch
+        y.sum().backward()
+        assert len(seen_t) == 1 and seen_p == [1]
+        np.testing.assert_allclose(x.grad.numpy(), [7, 7, 7])
+        # torch.nn.Module full-backward hooks are tensor pre-hooks on the module's output grad nodes
+        lin = torch.nn.Linear(4, 2)
+        got = []
+        lin.register_full_backward_hook(lambda m, gi, go: got.append((gi[0].shape, go[0].shape)))
+        inp = paddle.to_tensor(np.ones((3, 4), "float32"), stop_gradient=False)
+        out = paddle.Tensor(lin(inp._t))
+        out.sum().backward()
+        assert got == [(torch.Size([3, 4]), torch.Size([3, 2]))]
+        # torch retain_grad on a non-leaf
+        z = x * 5
+        z._t.retain_grad()
+        (z * z).sum().backward()
+        np.testing.assert_allclose(z._t.grad.numpy(), (2 * z).numpy())
+
+
+def test_failed_backward_drops_queued_callbacks():
+    with eng("native"):
+        class Owner:
+            _queued = True
+
+            def cb(self):
+                raise AssertionError("stale callback fired")
+        o = Owner()
+
+        class Boom(paddle.autograd.PyLayer):
+            @staticmethod
+            def forward(ctx, x):
+                return x * 1
+
+            @staticmethod
+            def backward(ctx, g):
+                engine.queue_callback(o.cb)
+                raise ValueError("boom")
+        x = paddle.to_tensor([1.0], stop_gradient=False)
+        with pytest.raises(Exception):
+            Boom.apply(x).sum().backward()
+        assert not o._queued and not engine._FINAL
+        (x * 2).sum().backward()  # an unrelated backward runs no stale callback
+
+
+@pytest.mark.gpu
+def test_side_stream_forward_native_engine():
+    """A forward run on a side stream: each grad node runs on its forward's stream, gradients crossing streams
+    are event-ordered and the caller's stream waits for the backward."""
+    assert torch.cuda.is_available()
+    paddle.set_device("gpu:0")
+    res = {}
+    for name in ("torch", "native"):
+        with eng(name):
+            torch.manual_seed(0)
+            w = torch.randn(2048, 2048, device="cuda", requires_grad=True)
+            x = torch.randn(4096, 2048, device="cuda")
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                h = x
+                for _ in range(6):
+                    h = torch.tanh(h @ w)
+            torch.cuda.current_stream().wait_stream(side)
+            loss = paddle.Tensor(h).square().sum()
+            loss.backward()
+            res[name] = w.grad.clone()  # read on the caller's stream right after backward
+    torch.cuda.synchronize()
+    torch.testing.assert_close(res["native"], res["torch"], rtol=1e-3, atol=1e-3)

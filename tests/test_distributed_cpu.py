@@ -373,3 +373,52 @@ def test_stream_collectives_semantics_gloo():
         assert out["bad"] == "rejected"
         assert out["ag_tensor"] == [0.0, 1.0, 10.0, 11.0] and out["ag_task_done"]
     assert res[0][1]["rs"] == [2.0, 4.0] and res[1][1]["rs"] == [6.0, 8.0]
+
+
+def _two_opt_worker(rank, world, port, q):
+    """One DataParallel model, two optimizers over disjoint halves of it (GAN generator / discriminator):
+    clearing one optimizer's grads must not wipe the other's before it steps, and
+    clear_grad(set_to_zero=False) leaves .grad None."""
+    paddle = _setup(rank, world, port)
+    paddle.seed(3)
+    net = paddle.nn.Sequential(paddle.nn.Linear(8, 8), paddle.nn.Linear(8, 4))
+    dp = paddle.DataParallel(net, comm_buffer_size=1, last_comm_buffer_size=1)
+    opt_a = paddle.optimizer.SGD(0.1, parameters=net[0].parameters())
+    opt_b = paddle.optimizer.SGD(0.1, parameters=net[1].parameters())
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(4, 8, generator=g)
+    out = []
+    for step in range(2):
+        loss = dp(paddle.Tensor(x[rank * 2:(rank + 1) * 2])).square().mean()
+        loss.backward()
+        opt_a.step()
+        opt_a.clear_grad(set_to_zero=(step == 0))
+        if step == 1:
+            out.append([p.grad is None for p in net[0].parameters()])
+        opt_b.step()
+        opt_b.clear_grad()
+    q.put((rank, {k: v.numpy() for k, v in net.state_dict().items()}, out))
+    paddle.distributed.barrier()
+
+
+def test_data_parallel_two_optimizers_clear_grad_keeps_other_grads():
+    sys.path.insert(0, ROOT)
+    os.environ["PADDLE_AMD_FORCE_CPU"] = "1"
+    import paddlepaddle_amd as paddle
+    paddle.seed(3)
+    net = paddle.nn.Sequential(paddle.nn.Linear(8, 8), paddle.nn.Linear(8, 4))
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(4, 8, generator=g)
+    opt = paddle.optimizer.SGD(0.1, parameters=net.parameters())
+    for _ in range(2):
+        # mean over the two half-batch losses == the DP average of the per-rank gradients
+        loss = (net(paddle.Tensor(x[:2])).square().mean() + net(paddle.Tensor(x[2:])).square().mean()) * 0.5
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+    ref = {k: v.numpy() for k, v in net.state_dict().items()}
+    res = _spawn(_two_opt_worker)
+    for _, sd, out in res:
+        assert out == [[True, True]]
+        for k in ref:
+            np.testing.assert_allclose(sd[k], ref[k], rtol=1e-5, atol=1e-6, err_msg=k)

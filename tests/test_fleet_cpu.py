@@ -575,16 +575,16 @@ def test_sequence_parallel_gpt_matches_single_process():
     assert ("issue", "reduce") in trace  # row-SP forward: reduces pipelined with the next block's GEMM
 
 
-def _sp_sharding_worker(rank, world, port, q):
+def _sp_sharding_worker(rank, world, port, q, dp_deg=1):
     paddle = _setup(rank, world, port)
     from paddlepaddle_amd.models.gpt import GPTConfig, GPTForPretraining, GPTPretrainingCriterion
     _, full, _ = _gpt_full(paddle)
     full_sd = {k: v._t.detach().clone() for k, v in full.state_dict().items()}
-    fleet = _fleet_init(paddle, mp_degree=2, sharding_degree=2, dp_degree=1)
+    fleet = _fleet_init(paddle, mp_degree=2, sharding_degree=2, dp_degree=dp_deg)
     fleet.fleet._strategy.sharding_configs["stage"] = 3
     hcg = fleet.get_hybrid_communicate_group()
     mp_rank = hcg.get_model_parallel_rank()
-    data_rank = hcg.get_sharding_parallel_rank()
+    data_rank = hcg.get_data_parallel_rank() * 2 + hcg.get_sharding_parallel_rank()
     cfg = GPTConfig.tiny(num_hidden_layers=2, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0,
                          tensor_parallel_degree=2, sequence_parallel=True)
     model, crit = GPTForPretraining(cfg), GPTPretrainingCriterion(cfg)
@@ -595,11 +595,22 @@ def _sp_sharding_worker(rank, world, port, q):
     model = fleet.distributed_model(model)
     opt = fleet.distributed_optimizer(opt)
     ids = _data(cfg)
-    per = ids.shape[0] // 2
+    per = ids.shape[0] // (2 * dp_deg)
     losses = _train(paddle, model, crit, opt, ids[data_rank * per:(data_rank + 1) * per])
     sd = {k: v.numpy() for k, v in model.state_dict().items()}
     q.put((rank, mp_rank, losses, sd))
     paddle.distributed.barrier()
+
+
+def _sp_sharding_dp2_worker(rank, world, port, q):
+    _sp_sharding_worker(rank, world, port, q, dp_deg=2)
+
+
+def test_dp2_x_sharding_stage3_x_tensor_parallel_sequence_parallel_gpt_eight_ranks():
+    """dp-2 x sharding-2 (stage 3) x TP-2 + sequence parallel on 8 gloo ranks: the sequence-parallel grads
+    (LayerNorm, row-parallel bias, position table) are summed over mp AND averaged over the dp replicas, so
+    every rank's weights match single-process training (the dp all-reduce raced the mp flat)."""
+    _check_hybrid(_spawn(_sp_sharding_dp2_worker, world=8), 2)
 
 
 def test_sharding_stage3_x_tensor_parallel_sequence_parallel_gpt_four_ranks():
