@@ -10,7 +10,8 @@ from ..framework.place import CPUPlace, CUDAPlace, CUDAPinnedPlace  # noqa: F401
 from ..framework import in_dynamic_mode as in_dygraph_mode  # noqa: F401
 from ..framework.tensor import Tensor as Variable  # noqa: F401
 from ..framework.flags import set_flags, get_flags  # noqa: F401,E402
-from . import core, framework, dygraph, io  # noqa: F401,E402
+from . import core, framework, dygraph, io, layers  # noqa: F401,E402
+from .data_feeder import DataFeeder  # noqa: F401,E402
 
 
 def enable_dygraph(place=None):

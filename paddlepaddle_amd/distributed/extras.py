@@ -105,9 +105,15 @@ class _IO:
         return bool(getattr(var, "persistable", False))
 
     @staticmethod
-    def load_inference_model_distributed(path_prefix, executor, **kw):
-        from ..static.io import load_inference_model
-        return load_inference_model(path_prefix, executor, **kw)
+    def load_inference_model_distributed(dirname=None, executor=None, model_filename=None, params_filename=None,
+                                         pserver_endpoints=None, path_prefix=None, **kw):
+        """A program saved by (fluid) save_inference_model under ``dirname``; ``pserver_endpoints`` name the
+        servers of distributed lookup tables, which this framework's programs read through their own PS
+        runtime (distributed/ps), so they need no rewrite here."""
+        from ..base.io import load_inference_model
+        if path_prefix is not None:
+            return load_inference_model(path_prefix, executor, **kw)
+        return load_inference_model(executor=executor, dirname=dirname, model_filename=model_filename, **kw)
 
 
 io = _IO()

@@ -214,9 +214,23 @@ def trace_program(fn, args, kwargs, names=None, dyn_size=None, guarded=False):
             out = fn(*a, **k)
     finally:
         prog._shadow = None
+    _check_defined(out)
     fetch = []
     tmpl = _out_template(prog, out, fetch)
     return prog, feed_slots, tmpl, fetch
+
+
+def _check_defined(x):
+    """A converted program must not return a name bound on only one path (dy2static UndefinedVar)."""
+    from .dy2static.convert_operators import UndefinedVar
+    if isinstance(x, UndefinedVar):
+        x._fail()
+    if isinstance(x, (list, tuple)):
+        for v in x:
+            _check_defined(v)
+    elif isinstance(x, dict):
+        for v in x.values():
+            _check_defined(v)
 
 
 class StaticFunction:
@@ -279,7 +293,33 @@ class StaticFunction:
             return self._graph_call(cp, leaves, dev)
         return cp.run(leaves, dev)
 
+    def _converted(self):
+        """The dy2static (AST) conversion of the wrapped function: tensor-dependent if / while / for-range
+        become control-flow nodes of the program (jit/dy2static); None when nothing was rewritten."""
+        conv = self.__dict__.get("_conv")
+        if conv is None:
+            from .dy2static import convert_to_static
+            conv = convert_to_static(self._dygraph_function)
+            self._conv = conv
+        return None if conv is self._dygraph_function else conv
+
+    def _call_converted(self, *args, **kwargs):
+        conv = self._converted() or self._dygraph_function
+        if self._instance is not None:
+            return conv(self._instance, *args, **kwargs)
+        return conv(*args, **kwargs)
+
     def _trace(self, args, kwargs, guarded):
+        from .dy2static import conversion_scope
+        if not guarded:
+            # converted source first: data-dependent branches / loops become one program with control-flow nodes
+            try:
+                with conversion_scope():
+                    prog, feed_slots, tmpl, fetch = trace_program(self._call_converted, args, kwargs)
+                return ConcreteProgram(prog, feed_slots, tmpl, fetch)
+            except Exception:
+                if self._converted() is None:
+                    raise
         prog, feed_slots, tmpl, fetch = trace_program(self._call_eager, args, kwargs, guarded=guarded)
         return ConcreteProgram(prog, feed_slots, tmpl, fetch)
 
@@ -452,18 +492,46 @@ def _fit_affine(t2, t3, t5, n=(2, 3, 5)):
 
 
 def _trace_layer(layer, specs, dyn):
+    from .dy2static import conversion_scope, convert_to_static
     names = [s.name for s in specs]
     fwd = layer.__dict__.get("forward")
-    fn = fwd._call_eager if isinstance(fwd, StaticFunction) else layer.forward
-    return trace_program(fn, tuple(specs), {}, names=names, dyn_size=dyn)
+    if isinstance(fwd, StaticFunction):
+        fn = fwd._call_converted
+    elif isinstance(layer, StaticFunction):
+        fn = layer._call_converted
+    else:
+        fn = convert_to_static(layer.forward)
+    with conversion_scope():
+        return trace_program(fn, tuple(specs), {}, names=names, dyn_size=dyn)
+
+
+class _FunctionHolder:
+    """jit.save of a to_static function (reference: jit/api.py:1110-1115 saves a StaticFunction's concrete
+    program): the Layer-shaped view save() works on."""
+    training = False
+
+    def __init__(self, sf):
+        self._sf = sf
+        self.__dict__["forward"] = sf
+
+    def eval(self):
+        pass
+
+    def train(self):
+        pass
 
 
 def save(layer, path, input_spec=None, **configs):
     from ..nn.layer.layers import Layer
-    if not isinstance(layer, Layer):
-        if isinstance(layer, StaticFunction):
-            raise NotImplementedError("jit.save of a bare function: wrap it in a Layer")
-        raise TypeError("jit.save expects a Layer")
+    if isinstance(layer, StaticFunction) and layer._instance is None:
+        layer = _FunctionHolder(layer)
+    elif isinstance(layer, StaticFunction):
+        layer = layer._instance
+    elif not isinstance(layer, Layer):
+        if callable(layer):
+            layer = _FunctionHolder(StaticFunction(layer))
+        else:
+            raise TypeError("jit.save expects a Layer or a (to_static) function")
     specs = _specs_for(layer, input_spec)
     was_training = layer.training
     layer.eval()

@@ -111,6 +111,9 @@ def create_parameter_tensor(shape, dtype, attr=None, is_bias=False, default_init
     return p
 
 
+from ...framework.dy2static_state import ACTIVE as _D2S_ACTIVE  # noqa: E402
+
+
 class Layer:
     """Base class of all layers (see module docstring)."""
 
@@ -147,7 +150,12 @@ class Layer:
                 r = hook(self, inputs)
                 if r is not None:
                     inputs = r if isinstance(r, tuple) else (r,)
-        out = self.forward(*inputs, **kwargs)
+        if _D2S_ACTIVE[0] and "forward" not in self.__dict__:
+            # recording a converted program: user sublayers' tensor-dependent control flow is converted too
+            from ...jit.dy2static import convert_to_static
+            out = convert_to_static(self.forward)(*inputs, **kwargs)
+        else:
+            out = self.forward(*inputs, **kwargs)
         if self._forward_post_hooks:
             for hook in list(self._forward_post_hooks.values()):
                 r = hook(self, inputs, out)

@@ -82,10 +82,13 @@ def program_guard(main_program, startup_program=None):
         _retarget_tracer()
 
 
-def data(name, shape, dtype=None, lod_level=0):
+def data(name, shape, dtype=None, lod_level=0, append_batch_size=False):
     """Feed variable. Unknown dims (None / -1) are traced with a placeholder size; shape-generic code
-    (reshape(-1, ...)) runs at any size, code that reads the traced size keeps it fixed."""
+    (reshape(-1, ...)) runs at any size, code that reads the traced size keeps it fixed.
+    ``append_batch_size`` (legacy fluid.layers.data): prepend a -1 batch dimension."""
     dtype = dtype or _dt.get_default_dtype()
+    if append_batch_size:
+        shape = [-1] + list(shape)
     return P.placeholder(_main, name, shape, dtype)
 
 

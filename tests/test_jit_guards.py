@@ -37,10 +37,32 @@ def test_branch_on_tensor_value_records_one_variant_per_path(monkeypatch):
     np.testing.assert_allclose(sf(pos * 5).numpy(), f(pos * 5).numpy())
     np.testing.assert_allclose(sf(neg * 2).numpy(), f(neg * 2).numpy())
     vs = sf.variants(pos)
+    # the AST conversion (jit/dy2static) turns the tensor-dependent if into one control-flow node: a single
+    # unguarded program serves both paths, recorded once
+    assert len(vs) == 1 and not vs[0].guarded
+    assert [n.name for n in vs[0].program.nodes].count("cf:cond") == 1
+    assert calls == [False]
+
+
+def test_branch_on_host_value_records_one_variant_per_path(monkeypatch):
+    """A branch on a host conversion (.numpy()) cannot be a program node: guarded variants, one per path."""
+    calls = _count_traces(monkeypatch)
+
+    def f(x):
+        if (x.sum() > 0).numpy():
+            return x * 2 + 1
+        return x - 3
+
+    sf = paddle.jit.to_static(f)
+    pos = paddle.to_tensor(np.ones([4], "float32"))
+    neg = paddle.to_tensor(-np.ones([4], "float32"))
+    for v in (pos, neg, pos * 5, neg * 2):
+        np.testing.assert_allclose(sf(v).numpy(), f(v).numpy())
+    vs = sf.variants(pos)
     assert len(vs) == 2 and all(cp.guarded for cp in vs)
     assert [g.expected for g in vs[0].guards] in ([True], [False])
-    # plain meta trace failed once, then exactly two guarded traces (one per path); no retrace afterwards
-    assert calls == [False, True, True]
+    # converted and plain meta traces fail once, then exactly two guarded traces (one per path)
+    assert calls == [False, False, True, True]
 
 
 def test_item_as_loop_trip_count_and_tolist():
