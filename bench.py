@@ -62,6 +62,9 @@ def parse():
     p.add_argument("--resnet-graph", type=int, default=0,
                    help="capture the ResNet-50 training step into a hipGraph and replay it (1 GPU; measured "
                         "+0.8%%: the eager step already keeps the GPU ~97%% busy)")
+    p.add_argument("--resnet-layout", default="nhwc", choices=["nhwc", "nchw-autotune"],
+                   help="nhwc: channels-last model; nchw-autotune: Paddle's default NCHW model with "
+                        "FLAGS_layout_autotune (NHWC kernels on channels-last views)")
     p.add_argument("--skip-gpt", type=int, default=0)
     p.add_argument("--allocator", default="native", choices=["native", "torch"],
                    help="device allocator: the framework's auto-growth best-fit allocator or PyTorch's")
@@ -319,14 +322,18 @@ def llama_bench(args, paddle, world, dist_on):
 def resnet_bench(args, paddle, world, dist_on):
     from paddlepaddle_amd.vision.models import resnet50
     paddle.seed(99)
-    model = resnet50(num_classes=1000, data_format="NHWC")
+    nchw = getattr(args, "resnet_layout", "nhwc") == "nchw-autotune"
+    if nchw:
+        paddle.set_flags({"FLAGS_layout_autotune": True})
+    model = resnet50(num_classes=1000, data_format="NCHW" if nchw else "NHWC")
     opt = paddle.optimizer.Momentum(learning_rate=0.1, momentum=0.9, parameters=model.parameters(),
                                     weight_decay=1e-4, multi_precision=True)
     model, opt = paddle.amp.decorate(model, opt, level="O2", dtype="bfloat16")
     if world > 1:
         model = paddle.DataParallel(model)
     B = args.resnet_batch
-    x = paddle.Tensor(torch.randn(B, 224, 224, 3, device=_dev(), dtype=torch.bfloat16))
+    x = paddle.Tensor(torch.randn(*((B, 3, 224, 224) if nchw else (B, 224, 224, 3)), device=_dev(),
+                                  dtype=torch.bfloat16))
     y = paddle.Tensor(torch.randint(0, 1000, (B,), device=_dev()))
 
     def step():

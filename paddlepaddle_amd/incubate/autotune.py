@@ -4,8 +4,12 @@ What the switches drive here:
   kernel     -> the per-shape GEMM backend choice (ops/gemm.py choose(): hand-written MFMA kernels vs hipBLASLt,
                 timed on first use, persisted in the tuning table). Disabled: shapes not in the table are not timed
                 and take hipBLASLt; ``tuning_range`` bounds the step window in which new shapes may be timed.
-  layout     -> FLAGS_layout_autotune (channels-last preference of the conv / BN kernels, which are NHWC-native).
-  dataloader -> FLAGS_dataloader_autotune (io.DataLoader picks num_workers itself when set).
+  layout     -> FLAGS_layout_autotune: NCHW conv / batch-norm / max-pool calls on device tensors run the NHWC HIP
+                kernels on channels-last views (framework/layout_autotune.py, read by nn/functional conv / norm /
+                pooling).
+  dataloader -> FLAGS_dataloader_autotune: io.DataLoader built with num_workers=0 times its first
+                ``tuning_steps`` batches at 0, 2, 4, ... workers and keeps the cheapest (io/__init__.py
+                _tune_num_workers).
 """
 from __future__ import annotations
 
@@ -62,3 +66,10 @@ def set_config(config=None):
         _bool_switch(cfg["layout"], "FLAGS_layout_autotune", "layout")
     if "dataloader" in cfg:
         _bool_switch(cfg["dataloader"], "FLAGS_dataloader_autotune", "dataloader")
+        if "tuning_steps" in cfg["dataloader"]:
+            ts = cfg["dataloader"]["tuning_steps"]
+            if isinstance(ts, int) and ts > 0:
+                set_flags({"FLAGS_dataloader_tuning_steps": ts})
+            else:
+                warnings.warn("The auto-tuning configuration of the dataloader is incorrect. The `tuning_steps` "
+                              "should be int. Use default parameter instead.")

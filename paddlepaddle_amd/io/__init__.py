@@ -358,6 +358,45 @@ def get_worker_info():
     return wi
 
 
+def _dataloader_autotune_on():
+    from ..framework.flags import get_flags
+    try:
+        return bool(get_flags("FLAGS_dataloader_autotune")["FLAGS_dataloader_autotune"])
+    except Exception:  # pragma: no cover
+        return False
+
+
+def _tune_num_workers(dataset, batch_sampler, collate, worker_init_fn):
+    """Worker count with the lowest per-batch load time over the first ``FLAGS_dataloader_tuning_steps`` batches
+    (at least 2 per candidate): candidates 0, 2, 4, ... up to half the visible CPUs (at most 16); a larger count
+    must beat the best so far by 20 % to be taken, and the search stops at the first one that does not."""
+    import os as _os
+    import time as _time
+    from ..framework.flags import get_flags
+    try:
+        steps = int(get_flags("FLAGS_dataloader_tuning_steps")["FLAGS_dataloader_tuning_steps"])
+    except Exception:  # pragma: no cover
+        steps = 8
+    bs = getattr(batch_sampler, "batch_size", 1) or 1
+    n = min(len(dataset), max(2, steps) * bs)
+    sub = Subset(dataset, list(range(n)))
+    sampler = BatchSampler(sub, batch_size=bs, drop_last=False)
+    max_w = min(16, max(0, (len(_os.sched_getaffinity(0)) if hasattr(_os, "sched_getaffinity") else
+                            (_os.cpu_count() or 2)) // 2))
+    best, best_cost = 0, None
+    for w in range(0, max_w + 1, 2):
+        loader = _tud.DataLoader(_TorchDS(sub), batch_sampler=_BS(sampler), collate_fn=collate, num_workers=w,
+                                 worker_init_fn=worker_init_fn)
+        t0 = _time.perf_counter()
+        cnt = sum(1 for _ in loader)
+        cost = (_time.perf_counter() - t0) / max(cnt, 1)
+        if best_cost is None or cost < 0.8 * best_cost:
+            best, best_cost = w, cost
+        elif w > best:
+            break
+    return best
+
+
 class DataLoader:
     def __init__(self, dataset, feed_list=None, places=None, return_list=True, batch_sampler=None, batch_size=1,
                  shuffle=False, drop_last=False, collate_fn=None, num_workers=0, use_buffer_reader=True,
@@ -377,6 +416,13 @@ class DataLoader:
         self.drop_last = drop_last
         self._device = _get_torch_device()
         self._pin = self._device.type == "cuda" and use_buffer_reader
+        self.autotuned_num_workers = None
+        if num_workers == 0 and not self._iterable and _dataloader_autotune_on():
+            # FLAGS_dataloader_autotune (incubate.autotune.set_config({"dataloader": ...})): time the loader on a
+            # prefix of the dataset at growing worker counts and keep the cheapest (reference io/reader.py AuToTune)
+            num_workers = self.autotuned_num_workers = _tune_num_workers(
+                dataset, self.batch_sampler, self._collate_np, worker_init_fn)
+            self.num_workers = num_workers
         if self._iterable:
             tds = _TorchIterDS(dataset)
             self._loader = _tud.DataLoader(tds, batch_size=batch_size, drop_last=drop_last,

@@ -10,6 +10,7 @@ import torch
 import torch.nn.functional as F
 
 from ...amp.state import maybe_cast
+from ...framework import layout_autotune as _lat
 from ...framework.tensor import Tensor, _wrap
 from ...tensor._helpers import T
 
@@ -76,6 +77,10 @@ def _from_cf(t, cl, n):
 
 
 def _convnd(n, x, weight, bias, stride, padding, dilation, groups, data_format):
+    if n == 2 and data_format == "NCHW" and _lat.applies(T(x)):
+        # layout autotune: the NHWC kernels on the channels-last view, result handed back as logical NCHW
+        y = _convnd(2, _wrap(_lat.to_nhwc_view(T(x))), weight, bias, stride, padding, dilation, groups, "NHWC")
+        return _wrap(_lat.to_nchw_view(T(y)))
     t = T(x)
     w = T(weight)
     t, w = maybe_cast("conv2d", t, w)

@@ -6,6 +6,7 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from ...framework import layout_autotune as _lat
 from ...framework.tensor import Tensor, _wrap
 from ...tensor._helpers import T
 from ... import ops as _ops
@@ -44,6 +45,13 @@ def fused_bn_act(x, running_mean, running_var, weight=None, bias=None, training=
     Running statistics follow the reference: biased batch variance, factor 1 - momentum."""
     t = T(x)
     cl = data_format in ("NHWC", "NLC", "NDHWC")
+    if data_format == "NCHW" and _lat.applies(t):
+        # layout autotune: the channels-last HIP kernels on the NHWC view (framework/layout_autotune.py)
+        r = T(residual)
+        y = _ops.batch_norm_act_nhwc(_lat.to_nhwc_view(t), T(weight), T(bias), T(running_mean), T(running_var),
+                                     training and not use_global_stats, momentum, epsilon, act,
+                                     None if r is None else _lat.to_nhwc_view(r), _grad_sink)
+        return _wrap(_lat.to_nchw_view(y))
     use_batch = training and not use_global_stats
     rm, rv = T(running_mean), T(running_var)
     w, b = T(weight), T(bias)

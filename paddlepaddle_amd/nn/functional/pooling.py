@@ -4,6 +4,7 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
+from ...framework import layout_autotune as _lat
 from ...framework.tensor import _wrap
 from ...tensor._helpers import T
 
@@ -63,6 +64,10 @@ def _scalar(v):
 
 
 def _maxpool(n, x, kernel_size, stride, padding, return_mask, ceil_mode, data_format):
+    if n == 2 and data_format == "NCHW" and not return_mask and _lat.applies(T(x)) \
+            and not isinstance(padding, str) and _scalar(padding) is not None:
+        y = _maxpool(2, _wrap(_lat.to_nhwc_view(T(x))), kernel_size, stride, padding, False, ceil_mode, "NHWC")
+        return _wrap(_lat.to_nchw_view(T(y)))
     if n == 2 and data_format == "NHWC" and not isinstance(padding, str):
         # channels-last HIP kernel (ops/pool.py): first-max mask kept as uint8, gather backward
         from ...ops import pool as _pool
