@@ -865,7 +865,9 @@ class StaticEngine:
             self.build(inputs, labels)
         from ...framework.place import _get_torch_device
         self.dev = _get_torch_device()
-        p2p = _P2P(self.dev)
+        if getattr(self, "_p2p", None) is None:
+            self._p2p = _P2P(self.dev)  # built once on every rank (its host twin is a collective group creation)
+        p2p = self._p2p
         nst = len(self.meshes)
         s = self.my_stage
         n = self.acc
@@ -905,46 +907,29 @@ class StaticEngine:
         return _wrap(loss)
 
 
-def _key(key):
-    kind, slot, mb = key
-    return ((0 if kind == "F" else 1) << 40) | (int(slot) << 20) | int(mb)
-
-
 class _P2P:
-    """Keyed point-to-point messages between pipeline stage ranks (non-blocking sends)."""
+    """Keyed point-to-point messages between pipeline stage ranks: the tagged endpoint of parallel/p2p.py (tags and
+    meta on a gloo twin of the world, meta once per (channel, shape), payloads on RCCL), kept across steps so
+    the meta cache persists. Keys are ("F" | "B", slot, micro-batch)."""
 
     def __init__(self, dev):
-        self.dev = dev
-        self.pending = []
-        self.stash = {}
+        from ...parallel.p2p import P2P, host_twin
+        ws = dist.get_world_size() if dist.is_initialized() else 1
+        host = host_twin([list(range(ws))], dist.get_rank()) if ws > 1 else None
+        self.ep = P2P(dev, None, host)
+
+    @staticmethod
+    def _tag(key):
+        kind, slot, mb = key
+        return (0 if kind == "F" else 1, int(slot), int(mb))
 
     def send(self, t, dst, key):
-        t = t.contiguous()
-        hdr = torch.tensor([t.dim()] + list(t.shape) + [0] * (8 - t.dim()) + [_DT[t.dtype], _key(key)],
-                           dtype=torch.int64, device=t.device)
-        self.pending.append((dist.isend(hdr, dst), hdr))
-        self.pending.append((dist.isend(t, dst), t))
+        self.ep.send(t, dst, self._tag(key))
 
     def recv(self, src, key):
-        st = self.stash.setdefault(src, {})
-        want = _key(key)
-        if want in st:
-            return st.pop(want)
-        while True:
-            hdr = torch.empty(11, dtype=torch.int64, device=self.dev)
-            dist.recv(hdr, src)
-            h = [int(v) for v in hdr.tolist()]
-            t = torch.empty(h[1:1 + h[0]], dtype=_CODE[h[9]], device=self.dev)
-            dist.recv(t, src)
-            if h[10] == want:
-                return t
-            st[h[10]] = t
+        return self.ep.recv(src, self._tag(key))
 
     def join(self):
-        for w, _ in self.pending:
-            w.wait()
-        self.pending = []
+        self.ep.join()
 
 
-_DT = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2, torch.int64: 3, torch.int32: 4, torch.bool: 5}
-_CODE = {v: k for k, v in _DT.items()}

@@ -102,6 +102,11 @@ class HybridCommunicateGroup:
         if self._sep_degree > 1:
             self._fused[("data", "sep")] = self._build_fused(("data", "sep"))
         self.stage_id = self._topo.get_coord(self.global_rank).pipe
+        # host-side (gloo) twin of the pipe groups: pipeline p2p tags / meta travel there (parallel/p2p.py)
+        self._pipe_host = None
+        if self._pp_degree > 1 and C.is_initialized():
+            from ...parallel.p2p import host_twin
+            self._pipe_host = host_twin(self._topo.get_comm_list("pipe"), self.global_rank)
         # check group for global grad-norm (all ranks that hold distinct param shards)
         self._check_group = None
 
@@ -178,6 +183,10 @@ class HybridCommunicateGroup:
 
     def get_pipe_parallel_group(self):
         return self._groups["pipe"]
+
+    def get_pipe_parallel_host_group(self):
+        """gloo twin of this rank's pipe group (None on gloo worlds, where the group itself carries host tensors)."""
+        return self._pipe_host
 
     def is_first_stage(self):
         return self.stage_id == 0

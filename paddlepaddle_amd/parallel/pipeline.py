@@ -28,8 +28,9 @@ from .. import nn
 from ..distributed import collective as C
 from ..framework.tensor import Tensor, _wrap
 
+from .p2p import P2P  # noqa: E402
+
 _FWD, _BWD = 0, 1
-_HDR = 13  # ndim, shape[8], dtype, kind, chunk, micro-batch
 
 
 class LayerDesc:
@@ -162,47 +163,34 @@ class PipelineParallel(nn.Layer):
         self.prev_rank = self.group.ranks[self.stage_id - 1] if not self.is_first else None
         self.next_rank = self.group.ranks[self.stage_id + 1] if not self.is_last else None
         self._dp_sync = hcg.get_data_parallel_world_size() > 1
-        self._pending = []
-        self._stash = {}
+        self._p2p = None
 
     # --------------------------------------------------------------- p2p
     def _dev(self):
         p = next(iter(self._layers.parameters()), None)
         return p._t.device if p is not None else torch.device("cpu")
 
+    def _p2p_chan(self):
+        """The stage's tagged p2p endpoint (parallel/p2p.py: tags + meta on the host twin of the pipe group, meta
+        once per shape, payloads on the pipe group's RCCL communicator)."""
+        if self._p2p is None:
+            host = self._hcg.get_pipe_parallel_host_group() if hasattr(self._hcg, "get_pipe_parallel_host_group") \
+                else None
+            self._p2p = P2P(self._dev(), self.group.process_group, host)
+        return self._p2p
+
     def _send(self, t, dst, kind=_FWD, key=(0, 0)):
         # non-blocking: a stage may send its next activation before the neighbour has posted the
         # receive (1F1B would dead-lock on rendezvous sends); buffers are kept alive until joined
-        t = t.contiguous()
-        hdr = torch.tensor([t.dim()] + list(t.shape) + [0] * (8 - t.dim()) + [_DT_CODE[t.dtype], kind, key[0], key[1]],
-                           dtype=torch.int64, device=t.device)
-        pg = self.group.process_group
-        self._pending.append((dist.isend(hdr, dst, group=pg), hdr))
-        self._pending.append((dist.isend(t, dst, group=pg), t))
+        self._p2p_chan().send(t, dst, (kind, key[0], key[1]))
 
     def _join_sends(self):
-        for w, _ in self._pending:
-            w.wait()
-        self._pending = []
+        if self._p2p is not None:
+            self._p2p.join()
 
     def _recv(self, src, kind=_FWD, key=(0, 0)):
-        """The (kind, key) message from ``src``: the peer's stream is read in send order and messages
-        that are not the one asked for are stashed for a later call."""
-        stash = self._stash.setdefault(src, {})
-        want = (kind, tuple(key))
-        if want in stash:
-            return stash.pop(want)
-        while True:
-            hdr = torch.empty(_HDR, dtype=torch.int64, device=self._dev())
-            dist.recv(hdr, src, group=self.group.process_group)
-            h = [int(v) for v in hdr.tolist()]
-            nd = h[0]
-            t = torch.empty(h[1:1 + nd], dtype=_CODE_DT[h[9]], device=self._dev())
-            dist.recv(t, src, group=self.group.process_group)
-            got = (h[10], (h[11], h[12]))
-            if got == want:
-                return t
-            stash[got] = t
+        """The (kind, key) message from ``src`` (messages that arrive ahead of it are stashed)."""
+        return self._p2p_chan().recv(src, (kind, key[0], key[1]))
 
     # --------------------------------------------------------------- schedule
     def _split(self, data):
@@ -348,8 +336,6 @@ class PipelineParallelZeroBubble(PipelineParallel):
         return self._finish(losses)
 
 
-_DT_CODE = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2, torch.int64: 3, torch.int32: 4, torch.bool: 5}
-_CODE_DT = {v: k for k, v in _DT_CODE.items()}
 
 
 class PipelineParallelWithInterleave(PipelineParallel):

@@ -49,6 +49,11 @@ def _worker(rank, world, port, shape, acc, schedule, q):
     eng = dm._engine
     kinds = sorted({n.name for nodes in eng.stage_nodes for n in nodes if n.name in (
         "allreduce", "allgather", "slice", "copy_to_parallel")})
+    if pp > 1:
+        # pipeline p2p (parallel/p2p.py): the meta of each (peer, direction, slot) crossed once in the whole run
+        ep = eng._p2p.ep
+        assert ep.meta_exchanges == len(ep.sent_meta) and ep.messages == STEPS * acc * len(ep.sent_meta), (
+            ep.meta_exchanges, len(ep.sent_meta), ep.messages)
     q.put((rank, losses, kinds, eng.my_stage))
     paddle.distributed.barrier()
 

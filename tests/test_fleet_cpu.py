@@ -141,6 +141,10 @@ def _pp_worker(rank, world, port, q, schedule="1F1B"):
         from paddlepaddle_amd.parallel.pipeline import PipelineParallelZeroBubble
         assert type(model) is PipelineParallelZeroBubble and model.deferred_wgrads > 0
         assert any(k == "W" for k, _ in model.jobs)
+    # p2p meta (shape / dtype) crossed each directed channel once; every later message carried only its tag
+    ep = model._p2p
+    assert ep.meta_exchanges == 1 and ep.messages == 3 * 2 + (2 if rank == 0 else 0), (ep.meta_exchanges,
+                                                                                          ep.messages)
     q.put((rank, losses, params, None if isinstance(ev, list) else float(ev)))
     paddle.distributed.barrier()
 
