@@ -2,6 +2,7 @@
 
 Reference: paddle/fluid/framework/new_executor/program_interpreter.cc — the program becomes a flat instruction
 list executed in C++ with last-use garbage collection. Lowering here:
+  * matmul + bias add (+ GELU) is fused into one ``fused_linear`` instruction (the GEMM epilogue);
   * every PIR value gets a slot; parameters are bound once (persistent), feeds per run, fetch targets kept;
   * ``builtin.combine`` / ``builtin.split`` disappear (their slot lists are spliced into the consumers /
     producers);
@@ -73,6 +74,48 @@ class NativeRunner:
         return [_wrap(t) for t in self.interp.run(items)]
 
 
+def _fuse_linear(ops):
+    """Peephole: ``matmul(x, W)`` whose only reader is ``add(., bias)`` with a 1-D parameter bias (and, when that
+    sum's only reader is ``gelu``, the activation too) becomes one ``fused_linear`` instruction: the MFMA GEMM
+    with its bias / GELU epilogue (reference: the fused_gemm_epilogue pass, fuse_gemm_epilogue_pass.cc)."""
+    from .pir_json import decode_type
+    uses, producer = {}, {}
+    for i, (name, operands, results, attrs, types) in enumerate(ops):
+        for v in operands:
+            uses.setdefault(v, []).append(i)
+        for k, r in enumerate(results):
+            producer[r] = (i, k)
+    param_shape = {}
+    for name, operands, results, attrs, types in ops:
+        if name == "builtin.parameter":
+            t = decode_type(types[0]) if types and types[0] else None
+            param_shape[results[0]] = t[1] if isinstance(t, tuple) else None
+    out = list(ops)
+    dead = set()
+    for i, (name, operands, results, attrs, types) in enumerate(ops):
+        if name != "pd_op.matmul" or attrs.get("transpose_x") or len(uses.get(results[0], [])) != 1:
+            continue
+        j = uses[results[0]][0]
+        an, aops, ares, _, atypes = ops[j]
+        if an != "pd_op.add" or len(aops) != 2:
+            continue
+        bias = aops[1] if aops[0] == results[0] else aops[0]
+        if len(param_shape.get(bias) or []) != 1 or (len(param_shape.get(operands[1]) or []) != 2):
+            continue
+        fa = {"transpose_y": bool(attrs.get("transpose_y", False)), "activation": "none"}
+        res, tys, at = ares, atypes, j
+        users = uses.get(ares[0], [])
+        if len(users) == 1 and ops[users[0]][0] == "pd_op.gelu":
+            g = users[0]
+            fa["activation"] = "gelu"
+            fa["approximate"] = bool(ops[g][3].get("approximate", False))
+            res, tys, at = ops[g][2], ops[g][4], g
+            dead.add(j)
+        dead.add(i)
+        out[at] = ("pd_op.fused_linear", [operands[0], operands[1], bias], res, fa, tys)
+    return [op for k, op in enumerate(out) if k not in dead]
+
+
 def compile_program(program, params, device):
     """PirProgram + {name: Tensor} -> NativeRunner, or None when an op has no native kernel."""
     m = _module()
@@ -90,7 +133,7 @@ def compile_program(program, params, device):
 
     plan = []        # (op, in_slots, out_slots, attrs)
     feed_slots, fetch_slots, bound = [], [], []
-    for name, operands, results, attrs, _types in program.ops:
+    for name, operands, results, attrs, _types in _fuse_linear(program.ops):
         dialect, _, short = name.partition(".")
         if name == "builtin.parameter":
             bound.append((slot(results[0]), params[attrs["parameter_name"]]._t))
@@ -154,3 +197,15 @@ def compile_program(program, params, device):
     r = NativeRunner(program, interp, feed_slots, fetch_slots)
     r.device = device
     return r
+
+
+def kernel_calls():
+    """Launches of the hand-written HIP kernels made by native interpreters in this process, per kind."""
+    m = _module()
+    return dict(m.kernel_calls()) if m is not None and hasattr(m, "kernel_calls") else {}
+
+
+def reset_kernel_calls():
+    m = _module()
+    if m is not None and hasattr(m, "reset_kernel_calls"):
+        m.reset_kernel_calls()

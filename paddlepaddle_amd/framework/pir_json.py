@@ -348,6 +348,17 @@ def from_builder(b, trainable=False):
                          "global_pooling": a_bool(at.get("global_pooling", False)),
                          "adaptive": a_bool(at.get("adaptive", False)),
                          "padding_algorithm": a_str(at.get("padding_algorithm", "EXPLICIT"))}, [ty(o[0])]))
+        elif t == "lookup_table_v2":
+            put(o, w.op("embedding", [X("Ids"), X("W")], {"padding_idx": a_i64(at.get("padding_idx", -1)),
+                                                           "sparse": a_bool(at.get("is_sparse", False))}, [ty(o[0])]))
+        elif t == "flash_attn_qkvpacked":
+            res = outs["out"]
+            f32 = dtensor("float32", [])
+            r = w.op("flash_attn_qkvpacked", [X("qkv"), None, None],
+                     {"dropout": a_f32(at.get("dropout", 0.0)), "causal": a_bool(at.get("causal", False)),
+                      "return_softmax": a_bool(False), "is_test": a_bool(True), "rng_name": a_str("")},
+                     [ty(res[0]), f32, f32, dtensor("int64", [2])])
+            env[res[0]] = r[0]
         elif t == "reduce_mean":
             axis = [] if at.get("reduce_all") else list(at.get("dim") or [])
             put(o, w.op("mean", [X()], {"axis": a_intarray(axis), "keepdim": a_bool(at.get("keep_dim", False))},
@@ -503,7 +514,22 @@ def _un(fn):
     return lambda ins, a: [fn(ins[0])]
 
 
+def _flash_attn(ins, a):
+    from .program_desc import _qkvpacked
+    from ..ops import attention as _att
+    from .tensor import _wrap
+    if len(ins) > 4 and ins[4] is not None:
+        raise NotImplementedError("flash_attn with attn_mask")
+    q, k, v = ins[0], ins[1], ins[2]
+    return [_wrap(_att.flash_attention(q._t, k._t, v._t, causal=bool(a.get("causal", False)), dropout=0.0,
+                                       training=False))]
+
+
 _RUN = {
+    "pd_op.embedding": lambda ins, a: [_F().embedding(ins[0], ins[1])],
+    "pd_op.flash_attn": _flash_attn,
+    "pd_op.flash_attn_qkvpacked": lambda ins, a: [__import__(
+        "paddlepaddle_amd.framework.program_desc", fromlist=["_qkvpacked"])._qkvpacked(ins[0], a)],
     "pd_op.full": _full, "pd_op.full_int_array": _full_int_array,
     "pd_op.full_like": lambda ins, a: [_P().full_like(ins[0], _scalar(ins[1]), dtype=a.get("dtype") or None)],
     "pd_op.assign": lambda ins, a: [ins[0]],

@@ -476,6 +476,7 @@ OPS = {
     "sum": lambda ins, a: {"Out": [_P().add_n(ins["X"])]},
     "assign": lambda ins, a: {"Out": [ins["X"][0]]},
     "lookup_table_v2": lambda ins, a: {"Out": [_F().embedding(ins["Ids"][0], ins["W"][0])]},
+    "flash_attn_qkvpacked": lambda ins, a: {"out": [_qkvpacked(ins["qkv"][0], a)]},
     "fill_constant": _fill_constant, "cast": _cast,
     "shape": lambda ins, a: {"Out": [_P().to_tensor(list(ins["Input"][0].shape), dtype="int32")]},
     "reduce_mean": _reduce("mean"), "reduce_sum": _reduce("sum"), "reduce_max": _reduce("max"),
@@ -489,6 +490,17 @@ OPS = {
     "where": lambda ins, a: {"Out": [_P().where(ins["Condition"][0], ins["X"][0], ins["Y"][0])]},
     "bilinear_interp_v2": _interp("bilinear"), "nearest_interp_v2": _interp("nearest"),
 }
+
+
+def _qkvpacked(qkv, a):
+    """Reference flash_attn_qkvpacked: qkv [B, S, G + 2, Hk, D] (query groups, then K and V) -> [B, S, G*Hk, D]."""
+    from ..framework.tensor import _wrap
+    from ..ops import attention as _att
+    t = qkv._t
+    g = t.shape[2] - 2
+    q = t[:, :, :g].transpose(2, 3).flatten(2, 3) if g > 1 else t[:, :, 0]
+    return _wrap(_att.flash_attention(q, t[:, :, g], t[:, :, g + 1], causal=bool(a.get("causal", False)),
+                                      dropout=0.0, training=False))
 
 
 class ProgramDescRunner:
@@ -833,6 +845,51 @@ class _Exporter:
                 padding_algorithm="EXPLICIT", data_format="NCHW")
         if b is not None:
             self.op("elementwise_add", {"X": [cur], "Y": [self.name(b)]}, {"Out": out}, axis=1)
+
+    def op_embedding(self, out, a, k):
+        if k.get("max_norm") is not None:
+            raise NotImplementedError("embedding with max_norm has no reference operator")
+        pad = k.get("padding_idx")
+        self.op("lookup_table_v2", {"Ids": [self.name(a[0])], "W": [self.name(a[1])]}, {"Out": out},
+                padding_idx=-1 if pad is None else int(pad), is_sparse=bool(k.get("sparse", False)))
+
+    def op_dropout_add(self, out, a, k):
+        x, res = a[0], (a[1] if len(a) > 1 else None)
+        p = float(a[2]) if len(a) > 2 else 0.0
+        training = bool(a[3]) if len(a) > 3 else False
+        if training and p > 0:
+            raise NotImplementedError("a training-mode dropout_add cannot be exported (inference programs only)")
+        if res is None:
+            self.op("assign", {"X": [self.name(x)]}, {"Out": out})
+        else:
+            self.op("elementwise_add", {"X": [self.name(x)], "Y": [self.name(res)]}, {"Out": out}, axis=-1)
+
+    def op_flash_attention_qkvpacked(self, out, a, k):
+        """Our packing is [B, S, H, 3, D]; the reference op takes [B, S, G + 2, Hk, D] (G = H / Hk = 1 here)."""
+        if k.get("training") and float(k.get("dropout", 0.0)) > 0:
+            raise NotImplementedError("attention dropout cannot be exported (inference programs only)")
+        x = self.name(a[0])
+        t = self.tmp()
+        m = self.prog._metas[a[0].i]
+        B, S, H, _, D = m.shape
+        self.b.var(t, [B, S, 3, H, D], m.dtype)
+        self.op("transpose2", {"X": [x]}, {"Out": [t], "XShape": [self.tmp()]}, axis=[0, 1, 3, 2, 4])
+        self.op("flash_attn_qkvpacked", {"qkv": [t]},
+                {"out": out, "softmax": [self.tmp()], "softmax_lse": [self.tmp()], "seed_offset": [self.tmp()]},
+                dropout=0.0, causal=bool(k.get("causal", a[1] if len(a) > 1 else True)), return_softmax=False,
+                is_test=True, rng_name="")
+
+    def op_linear_nt(self, out, a, k):
+        self.op("matmul_v2", {"X": [self.name(a[0])], "Y": [self.name(a[1])]}, {"Out": out}, trans_x=False,
+                trans_y=True)
+
+    def op_arange(self, out, a, k):
+        """A shape-only value (positions of a fixed-length program): a persistable constant."""
+        vals = torch.arange(*[int(v) for v in a if isinstance(v, (int, float))])
+        n = f"__arange_{'_'.join(str(int(v)) for v in a if isinstance(v, (int, float)))}"
+        if n not in self.b.params:
+            self.b.param(n, vals)
+        self.op("assign", {"X": [n]}, {"Out": out})
 
     def op_flatten(self, out, a, k):
         s = a[1] if len(a) > 1 else k.get("start_dim", 0)

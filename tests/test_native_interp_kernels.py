@@ -1,0 +1,78 @@
+"""The native program interpreter (csrc/interpreter/interpreter.cpp) runs a saved PIR program on this
+framework's hand-written kernels: a GPT program exported with save_inference_model(program_format="pir") and
+loaded by the inference Predictor executes its matmuls / fused linears on the MFMA GEMM, layer norms on the row
+kernel and attention on the flash-attention forward (reference: new_executor/program_interpreter.cc:142,231)."""
+import numpy as np
+import pytest
+import torch
+
+import paddlepaddle_amd as paddle
+from paddlepaddle_amd.framework import native_interp as NI
+
+pytestmark = pytest.mark.skipif(not NI.available(), reason="_C_interp not built")
+
+
+def _export_gpt(tmp_path, cfg, ids, dtype="float32"):
+    from paddlepaddle_amd.models.gpt import GPTForPretraining
+    paddle.seed(3)
+    paddle.set_default_dtype(dtype)
+    try:
+        m = GPTForPretraining(cfg)
+    finally:
+        paddle.set_default_dtype("float32")
+    m.eval()
+    ref = m(paddle.to_tensor(ids)).astype("float32").numpy()
+    paddle.enable_static()
+    try:
+        main, start = paddle.static.Program(), paddle.static.Program()
+        with paddle.static.program_guard(main, start):
+            x = paddle.static.data("ids", list(ids.shape), "int64")
+            logits = m(x)
+        exe = paddle.static.Executor(paddle.CPUPlace())
+        prefix = str(tmp_path / "gpt")
+        paddle.static.save_inference_model(prefix, [x], [logits], exe, program=main, program_format="pir")
+    finally:
+        paddle.disable_static()
+    return prefix, ref
+
+
+def test_gpt_pir_program_runs_on_the_native_interpreter_with_fused_linears(tmp_path):
+    from paddlepaddle_amd.models.gpt import GPTConfig
+    from paddlepaddle_amd.framework import pir_json
+    cfg = GPTConfig.tiny(hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    ids = np.random.RandomState(0).randint(0, cfg.vocab_size, (2, 16)).astype("int64")
+    prefix, ref = _export_gpt(tmp_path, cfg, ids)
+    cfgi = paddle.inference.Config(prefix + ".json", prefix + ".pdiparams")
+    cfgi.disable_gpu()
+    pred = paddle.inference.create_predictor(cfgi)
+    assert type(pred._runner).__name__ == "NativeRunner"
+    np.testing.assert_allclose(pred.run([ids])[0].numpy(), ref, rtol=1e-4, atol=1e-4)
+    # matmul + bias (+ GELU) pairs of every block became one fused_linear instruction
+    prog = pir_json.PirProgram(__import__("json").load(open(prefix + ".json")))
+    names = [o[0] for o in NI._fuse_linear(prog.ops)]
+    assert names.count("pd_op.fused_linear") == 4 * cfg.num_hidden_layers
+    assert "pd_op.flash_attn_qkvpacked" in names and "pd_op.gelu" not in names
+
+
+@pytest.mark.gpu
+def test_gpt_pir_predictor_launches_the_hip_kernels(tmp_path):
+    from paddlepaddle_amd.models.gpt import GPTConfig
+    paddle.set_device("gpu:0")
+    cfg = GPTConfig.tiny(hidden_size=256, num_attention_heads=2, intermediate_size=1024, hidden_dropout_prob=0.0,
+                         attention_probs_dropout_prob=0.0)
+    ids = np.random.RandomState(1).randint(0, cfg.vocab_size, (2, 128)).astype("int64")
+    prefix, ref = _export_gpt(tmp_path, cfg, ids, dtype="bfloat16")
+    cfgi = paddle.inference.Config(prefix + ".json", prefix + ".pdiparams")
+    cfgi.enable_use_gpu(100, 0)
+    pred = paddle.inference.create_predictor(cfgi)
+    assert type(pred._runner).__name__ == "NativeRunner"
+    NI.reset_kernel_calls()
+    out = pred.run([ids])[0].astype("float32").numpy()
+    torch.cuda.synchronize()
+    calls = NI.kernel_calls()
+    L = cfg.num_hidden_layers
+    assert calls.get("gemm", 0) >= 4 * L + 1, calls        # QKV / out-proj / FFN x2 per block + tied LM head
+    assert calls.get("layer_norm", 0) == 2 * L + 1, calls
+    assert calls.get("flash_attn", 0) == L, calls
+    scale = np.abs(ref).max()
+    assert np.abs(out - ref).max() / scale < 3e-2
