@@ -26,10 +26,40 @@ def _t(x):
 
 
 # --------------------------------------------------------------------------------------- norms
+def _quant_out(y, quant_scale, round_type, max_bound, min_bound):
+    """int8 output of a quantising norm (reference fused_layernorm_kernel.cu QuantHelperFunc): q =
+    clip(round(max_bound * quant_scale * y), min_bound, max_bound); round_type 0 rounds half to even (rint),
+    1 half away from zero (round)."""
+    v = y.float() * (float(max_bound) * float(quant_scale))
+    v = torch.round(v) if int(round_type) == 0 else torch.sign(v) * torch.floor(v.abs() + 0.5)
+    return v.clamp(float(min_bound), float(max_bound)).to(torch.int8)
+
+
+def _with_quant(fn):
+    """quant_scale > 0 turns the normalised output into int8 (residual_out stays in the input dtype)."""
+    def run(*a, quant_scale=-1, quant_round_type=0, quant_max_bound=0, quant_min_bound=0, **k):
+        out = fn(*a, **k)
+        if quant_scale is None or float(quant_scale) <= 0:
+            return out
+        if float(quant_max_bound) <= 0:
+            raise ValueError("quant_scale > 0 needs quant_max_bound > 0 (e.g. 127) and quant_min_bound (e.g. -127)")
+        y = out[0] if isinstance(out, tuple) else out
+        q = _wrap(_quant_out(_t(y), quant_scale, quant_round_type, quant_max_bound, quant_min_bound))
+        return (q, out[1]) if isinstance(out, tuple) else q
+    return run
+
+
 def fused_rms_norm(x, norm_weight, norm_bias, epsilon, begin_norm_axis, bias=None, residual=None, quant_scale=-1,
                    quant_round_type=0, quant_max_bound=0, quant_min_bound=0):
     """out = rms_norm(x + bias + residual); returns (out, residual_out) when residual is given. Residual without
-    bias: the add and the norm are one HIP pass (ops.add_rms_norm) when no gradient is needed."""
+    bias: the add and the norm are one HIP pass (ops.add_rms_norm) when no gradient is needed. ``quant_scale`` > 0:
+    ``out`` is int8 (reference fused_rms_norm quantised output, see _quant_out)."""
+    return _with_quant(_fused_rms_norm)(x, norm_weight, norm_bias, epsilon, begin_norm_axis, bias, residual,
+                                        quant_scale=quant_scale, quant_round_type=quant_round_type,
+                                        quant_max_bound=quant_max_bound, quant_min_bound=quant_min_bound)
+
+
+def _fused_rms_norm(x, norm_weight, norm_bias, epsilon, begin_norm_axis, bias=None, residual=None):
     if residual is not None and bias is None and norm_weight is not None:
         xt, rt = _t(x), _t(residual)
         shape = xt.shape
@@ -58,6 +88,15 @@ def fused_rms_norm(x, norm_weight, norm_bias, epsilon, begin_norm_axis, bias=Non
 
 def fused_layer_norm(x, norm_weight, norm_bias, epsilon, residual_alpha=1.0, begin_norm_axis=1, bias=None,
                      residual=None, quant_scale=-1, quant_round_type=0, quant_max_bound=0, quant_min_bound=0):
+    """out = layer_norm(x + bias + residual_alpha * residual); (out, residual_out) with a residual; int8 ``out``
+    when ``quant_scale`` > 0 (reference fused_layernorm_kernel.cu:996)."""
+    return _with_quant(_fused_layer_norm)(x, norm_weight, norm_bias, epsilon, residual_alpha, begin_norm_axis, bias,
+                                          residual, quant_scale=quant_scale, quant_round_type=quant_round_type,
+                                          quant_max_bound=quant_max_bound, quant_min_bound=quant_min_bound)
+
+
+def _fused_layer_norm(x, norm_weight, norm_bias, epsilon, residual_alpha=1.0, begin_norm_axis=1, bias=None,
+                      residual=None):
     xt = _t(x)
     if bias is not None:
         xt = xt + _t(bias)
@@ -446,12 +485,26 @@ def masked_multihead_attention(x, cache_kv=None, bias=None, src_mask=None, cum_o
                                compute_dtype="default", out_scale=-1, quant_round_type=1, quant_max_bound=127.0,
                                quant_min_bound=-127.0):
     """One decode step. x [B, 3*H*D]; cache_kv [2, B, H, max_len, D] updated in place at the step.
-    The step index is sequence_lengths[b] (per batch) or src_mask's width - 1."""
+    The step index is sequence_lengths[b] (per batch) or src_mask's width - 1. ``qkv_out_scale``: x is the int32
+    output of an int8 QKV GEMM, dequantised by these per-column scales; ``out_scale`` > 0: int8 output
+    (reference QuantHelperFunc rounding / bounds). Beam-search cache indirection (``beam_cache_offset``) and the
+    reference's ``cum_offsets`` padding removal are not implemented and raise."""
+    if beam_cache_offset is not None:
+        raise NotImplementedError("masked_multihead_attention: beam_cache_offset (beam-search KV indirection) is "
+                                  "not implemented")
+    if cum_offsets is not None:
+        raise NotImplementedError("masked_multihead_attention: cum_offsets is not implemented")
+    if compute_dtype not in ("default", "bf16", "fp16", "fp32"):
+        raise ValueError(f"compute_dtype must be default / bf16 / fp16 / fp32, got {compute_dtype!r}")
     xt = _t(x)
     cache = _t(cache_kv)
     _, B, H, L, D = cache.shape
+    if qkv_out_scale is not None:
+        xt = (xt.float() * _t(qkv_out_scale).float().reshape(-1)).to(cache.dtype)
+    elif not xt.is_floating_point():
+        raise ValueError("masked_multihead_attention: an integer x needs qkv_out_scale")
     if bias is not None:
-        xt = xt + _t(bias)
+        xt = xt + _t(bias).to(xt.dtype)
     qkv = xt.view(B, 3, H, D)
     q, k, v = qkv[:, 0], qkv[:, 1], qkv[:, 2]
     if sequence_lengths is not None:
@@ -484,6 +537,8 @@ def masked_multihead_attention(x, cache_kv=None, bias=None, src_mask=None, cum_o
         out = out + _t(out_shift)
     if out_smooth is not None:
         out = out * _t(out_smooth)
+    if out_scale is not None and float(out_scale) > 0:
+        out = _quant_out(out, out_scale, quant_round_type, quant_max_bound, quant_min_bound)
     return _wrap(out), _wrap(cache)
 
 

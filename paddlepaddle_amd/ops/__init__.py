@@ -17,4 +17,4 @@ from .dropout import dropout_add  # noqa: F401
 from . import optim  # noqa: F401
 from ._loader import has as has_kernel, hip_enabled_for, LIB_PATH  # noqa: F401
 from .bn import batch_norm_act_nhwc  # noqa: F401
-from . import conv, gemm, dwconv  # noqa: F401,E402
+from . import conv, gemm, dwconv, quant  # noqa: F401,E402
