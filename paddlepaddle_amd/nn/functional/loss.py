@@ -18,6 +18,11 @@ def _reduce(l, reduction):
     return l
 
 
+def _acc_dt(x):
+    """Loss accumulation dtype: fp32 for 16-bit logits, float64 kept."""
+    return torch.float64 if x.dtype == torch.float64 else torch.float32
+
+
 def cross_entropy(input, label, weight=None, ignore_index=-100, reduction="mean", soft_label=False, axis=-1,
                   use_softmax=True, label_smoothing=0.0, name=None):
     x = T(input)
@@ -31,12 +36,12 @@ def cross_entropy(input, label, weight=None, ignore_index=-100, reduction="mean"
     C = x.shape[-1]
     w = T(weight)
     if soft_label or (y.is_floating_point() and y.shape == x.shape):
-        logp = F.log_softmax(x.float(), -1) if use_softmax else torch.log(x.float())
-        yt = y.float()
+        logp = F.log_softmax(x.to(_acc_dt(x)), -1) if use_softmax else torch.log(x.to(_acc_dt(x)))
+        yt = y.to(_acc_dt(x))
         if label_smoothing:
             yt = yt * (1 - label_smoothing) + label_smoothing / C
         if w is not None:
-            logp = logp * w.float()
+            logp = logp * w.to(_acc_dt(x))
         l = -(yt * logp).sum(-1, keepdim=True)
         if reduction == "none":
             return _wrap(l)
@@ -53,13 +58,13 @@ def cross_entropy(input, label, weight=None, ignore_index=-100, reduction="mean"
             return _wrap(l.sum())
         valid = (y != ignore_index).sum()
         return _wrap(l.sum() / valid.clamp_min(1).to(l.dtype))
-    logp = F.log_softmax(x.float(), -1) if use_softmax else torch.log(x.float())
+    logp = F.log_softmax(x.to(_acc_dt(x)), -1) if use_softmax else torch.log(x.to(_acc_dt(x)))
     flat = logp.reshape(-1, C)
     yl = y.reshape(-1)
-    l = F.nll_loss(flat, yl, weight=None if w is None else w.float(), ignore_index=ignore_index,
+    l = F.nll_loss(flat, yl, weight=None if w is None else w.to(_acc_dt(x)), ignore_index=ignore_index,
                    reduction="none")
     if label_smoothing:
-        smooth = -flat.mean(-1) if w is None else -(flat * w.float()).sum(-1) / C
+        smooth = -flat.mean(-1) if w is None else -(flat * w.to(_acc_dt(x))).sum(-1) / C
         l = (1 - label_smoothing) * l + label_smoothing * smooth * (yl != ignore_index)
     l = l.reshape(y.shape)
     if reduction == "none":
@@ -67,7 +72,7 @@ def cross_entropy(input, label, weight=None, ignore_index=-100, reduction="mean"
     if reduction == "sum":
         return _wrap(l.sum())
     if w is not None:
-        wsum = (w.float()[yl.clamp_min(0)] * (yl != ignore_index)).sum()
+        wsum = (w.to(_acc_dt(x))[yl.clamp_min(0)] * (yl != ignore_index)).sum()
         return _wrap(l.sum() / wsum)
     return _wrap(l.sum() / (yl != ignore_index).sum().clamp_min(1))
 

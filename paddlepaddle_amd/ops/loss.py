@@ -48,7 +48,8 @@ def softmax_cross_entropy(logits, labels, ignore_index=-100):
     if L.hip_enabled_for(logits) and logits.dtype in L._DT and logits.shape[-1] % 8 == 0:
         return _SoftmaxCEHIP.apply(logits, labels, ignore_index)
     V = logits.shape[-1]
-    lf = logits.reshape(-1, V).float()
+    lf = logits.reshape(-1, V)
+    lf = lf.float() if lf.dtype in (torch.float16, torch.bfloat16) else lf  # float64 stays float64
     lb = labels.reshape(-1).long()
     loss = F.cross_entropy(lf, lb, ignore_index=ignore_index, reduction="none")
     return loss.view(logits.shape[:-1])

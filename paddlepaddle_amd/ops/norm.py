@@ -37,18 +37,25 @@ def _finalize_parts(pa, pb, dta, dtb, nparts, cols, params=(None, None)):
     return (pa.sum(0).to(dta) if pa is not None else None), (pb.sum(0).to(dtb) if pb is not None else None)
 
 
+def _acc(t):
+    """Accumulation dtype of the reference paths: fp32 for 16-bit inputs, the input's own dtype otherwise (a
+    float64 norm stays float64)."""
+    return t.float() if t.dtype in (torch.float16, torch.bfloat16) else t
+
+
 def _rms_ref(x, w, eps):
-    xf = x.float()
+    xf = _acc(x)
     r = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
     y = xf * r
     if w is not None:
-        y = y * w.float()
+        y = y * w.to(y.dtype)
     return y.to(x.dtype)
 
 
 def _ln_ref(x, w, b, eps):
-    return torch.nn.functional.layer_norm(x.float(), (x.shape[-1],), None if w is None else w.float(),
-                                          None if b is None else b.float(), eps).to(x.dtype)
+    xf = _acc(x)
+    return torch.nn.functional.layer_norm(xf, (x.shape[-1],), None if w is None else w.to(xf.dtype),
+                                          None if b is None else b.to(xf.dtype), eps).to(x.dtype)
 
 
 class _RMSNormHIP(torch.autograd.Function):
