@@ -7,9 +7,10 @@
 //
 // y[M, N] = x[M, K] . dequant(Wq)^T (+ bias). Decode GEMMs are bound by the weight bytes, so the kernel is
 // built to stream Wq once at full width:
-//   * a workgroup = 4 waves owns 16 output channels and every activation row (M <= 64: up to four 16-row MFMA
-//     tiles); its waves take interleaved 64-deep K chunks (adjacent waves read adjacent weight bytes), and the
-//     K range may be split over gridDim.y workgroups as well so that narrow layers still fill the chip;
+//   * a workgroup = 4 waves owns 16 x NT output channels (NT = 1 / 2 / 4 for M <= 16 / 32 / 64: each activation
+//     fragment then feeds NT weight fragments) and every activation row (M <= 64: up to four 16-row MFMA tiles);
+//     its waves take interleaved 64-deep K chunks (adjacent waves read adjacent weight bytes), and the K range
+//     may be split over gridDim.y workgroups as well so that narrow layers still fill the chip;
 //   * per chunk each lane loads 16 weight bytes of one channel (one 16-byte load: 16 int8 k-values, or for int4
 //     the byte pair-row shared by channels 2j / 2j+1) and 16 activations per row tile, converts the integers to
 //     exact bf16 integers and runs two v_mfma_f32_16x16x32_bf16 per row tile. A and B use the same permuted
@@ -23,6 +24,8 @@
 //   * the four waves' sums meet in LDS; without a K split the workgroup writes bf16 (+ bias), with one it adds
 //     fp32 partials into a zeroed slab that pa_wo_finalize turns into bf16 (+ bias).
 #include "common.h"
+
+#include <algorithm>
 
 namespace {
 
@@ -75,80 +78,99 @@ __device__ __forceinline__ void load_x16(const uint16_t* row, bool ok, bf16x8& l
   }
 }
 
-// BITS: 8 / 4; G: 0 = per-channel scale, else group size (64 / 128); MT: 16-row tiles (ceil(M / 16)); LLM: int8 mode
-template <int BITS, int G, int MT, bool LLM>
+// BITS: 8 / 4; G: 0 = per-channel scale, else group size (64 / 128); MT: 16-row tiles (ceil(M / 16)); NT: 16-column
+// tiles per wave (the workgroup covers 16 * NT channels: more rows re-read the activations more often, so larger M
+// gives each activation fragment more channels to feed); LLM: int8 mode
+template <int BITS, int G, int MT, int NT, bool LLM>
 __global__ __launch_bounds__(256) void wo_gemm_k(WoArgs p) {
-  __shared__ float red[4][MT * 16 * 16 * (LLM ? 2 : 1)];
+  constexpr int TILE = MT * 256;                       // floats of one 16-column tile's partial sums
+  __shared__ float red[4][NT * TILE * (LLM ? 2 : 1)];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int col = lane & 15, q = lane >> 4;
-  const int n0 = blockIdx.x * 16;
-  const int n = n0 + col;
+  const int n0 = blockIdx.x * 16 * NT;
   const int chunk0 = blockIdx.y * p.kchunks_per_split;
   const int nch = min(p.kchunks_per_split, p.K / 64 - chunk0);
-  // weight row of this lane's channel
-  const int8_t* wrow = BITS == 8 ? p.w + (int64_t)n * p.K : p.w + (int64_t)(n >> 1) * p.K;
-  const int nib = n & 1;
-  f32x4 acc[MT], acco[MT];
+  const int8_t* wrow[NT];
+  int nib[NT];
 #pragma unroll
-  for (int t = 0; t < MT; ++t) {
-    acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    acco[t] = acc[t];
+  for (int j = 0; j < NT; ++j) {
+    const int n = n0 + j * 16 + col;
+    wrow[j] = BITS == 8 ? p.w + (int64_t)n * p.K : p.w + (int64_t)(n >> 1) * p.K;
+    nib[j] = n & 1;
   }
+  f32x4 acc[MT][NT], acco[MT][NT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      acc[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acco[t][j] = acc[t][j];
+    }
   // weight stream two chunks ahead of the MFMAs (the only HBM operand; activations are L2-resident)
-  auto wload = [&](int c) -> uint4 {
-    return c < nch ? *reinterpret_cast<const uint4*>(wrow + (chunk0 + c) * 64 + q * 16) : make_uint4(0, 0, 0, 0);
-  };
-  uint4 raw0 = wload(wave), raw1 = wload(wave + 4);
+  uint4 raw0[NT], raw1[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    raw0[j] = wave < nch ? *reinterpret_cast<const uint4*>(wrow[j] + (chunk0 + wave) * 64 + q * 16)
+                         : make_uint4(0, 0, 0, 0);
+    raw1[j] = wave + 4 < nch ? *reinterpret_cast<const uint4*>(wrow[j] + (chunk0 + wave + 4) * 64 + q * 16)
+                             : make_uint4(0, 0, 0, 0);
+  }
   for (int c = wave; c < nch; c += 4) {
     const int kc = (chunk0 + c) * 64 + q * 16;
-    const uint4 raw = raw0;
-    raw0 = raw1;
-    raw1 = wload(c + 8);
-    bf16x8 blo, bhi;
-    dequant16<BITS>(raw, nib, blo, bhi);
-    f32x4 part[MT];
+    bf16x8 blo[NT], bhi[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      dequant16<BITS>(raw0[j], nib[j], blo[j], bhi[j]);
+      raw0[j] = raw1[j];
+      raw1[j] = c + 8 < nch ? *reinterpret_cast<const uint4*>(wrow[j] + (chunk0 + c + 8) * 64 + q * 16)
+                            : make_uint4(0, 0, 0, 0);
+    }
+    float s[NT];
+    if constexpr (G != 0) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j) s[j] = p.scale[(int64_t)(((chunk0 + c) * 64) / G) * p.N + n0 + j * 16 + col];
+    }
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
       const int m = t * 16 + col;
       const bool ok = m < p.M;
       bf16x8 alo, ahi;
       load_x16(p.x + (int64_t)(ok ? m : 0) * p.ldx + kc, ok, alo, ahi);
-      f32x4 z = G ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[t];
-      z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, blo, z, 0, 0, 0);
-      z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bhi, z, 0, 0, 0);
-      part[t] = z;
-      if constexpr (LLM) {
-        bf16x8 olo, ohi;
-        load_x16(p.xo + (int64_t)(ok ? m : 0) * p.ldx + kc, ok, olo, ohi);
-        acco[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(olo, blo, acco[t], 0, 0, 0);
-        acco[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ohi, bhi, acco[t], 0, 0, 0);
+      bf16x8 olo, ohi;
+      if constexpr (LLM) load_x16(p.xo + (int64_t)(ok ? m : 0) * p.ldx + kc, ok, olo, ohi);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        f32x4 z = G ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[t][j];
+        z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, blo[j], z, 0, 0, 0);
+        z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bhi[j], z, 0, 0, 0);
+        if constexpr (G != 0) acc[t][j] += z * s[j];
+        else acc[t][j] = z;
+        if constexpr (LLM) {
+          acco[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(olo, blo[j], acco[t][j], 0, 0, 0);
+          acco[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ohi, bhi[j], acco[t][j], 0, 0, 0);
+        }
       }
-    }
-    if constexpr (G != 0) {
-      const float s = p.scale[(int64_t)(((chunk0 + c) * 64) / G) * p.N + n];
-#pragma unroll
-      for (int t = 0; t < MT; ++t) acc[t] += part[t] * s;
-    } else {
-#pragma unroll
-      for (int t = 0; t < MT; ++t) acc[t] = part[t];
     }
   }
   // D layout: col = lane & 15 (the channel), rows (lane >> 4) * 4 + r of each 16-row tile
 #pragma unroll
-  for (int t = 0; t < MT; ++t) {
+  for (int j = 0; j < NT; ++j)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      red[wave][(t * 16 + q * 4 + r) * 16 + col] = acc[t][r];
-      if constexpr (LLM) red[wave][MT * 256 + (t * 16 + q * 4 + r) * 16 + col] = acco[t][r];
-    }
-  }
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        red[wave][j * TILE + (t * 16 + q * 4 + r) * 16 + col] = acc[t][j][r];
+        if constexpr (LLM) red[wave][NT * TILE + j * TILE + (t * 16 + q * 4 + r) * 16 + col] = acco[t][j][r];
+      }
   __syncthreads();
-  for (int e = tid; e < MT * 256; e += 256) {
-    const int m = e >> 4, cc = e & 15, nn = n0 + cc;
+  for (int e = tid; e < NT * TILE; e += 256) {
+    const int j = e / TILE, w = e % TILE;
+    const int m = w >> 4, nn = n0 + j * 16 + (w & 15);
     if (m >= p.M) continue;
     float v = red[0][e] + red[1][e] + red[2][e] + red[3][e];
     if constexpr (LLM) {
-      const float o = red[0][MT * 256 + e] + red[1][MT * 256 + e] + red[2][MT * 256 + e] + red[3][MT * 256 + e];
+      const int eo = NT * TILE + e;
+      const float o = red[0][eo] + red[1][eo] + red[2][eo] + red[3][eo];
       v = (v * p.sx[m] + o) * p.scale[nn];
     } else if constexpr (G == 0) {
       v *= p.scale[nn];
@@ -199,25 +221,39 @@ __global__ void wo_dequant_k(const int8_t* w, const float* scale, uint16_t* out,
   *reinterpret_cast<uint4*>(out + i) = make_uint4(packed[0], packed[1], packed[2], packed[3]);
 }
 
-template <int BITS, int G, bool LLM>
-int launch_mt(const WoArgs& a, dim3 grid, hipStream_t st) {
+// column tiles per wave by row count (more rows: more channels per activation fragment)
+inline int nt_for(int M) { return M <= 16 ? 1 : (M <= 32 ? 2 : 4); }
+
+template <int BITS, int G, bool LLM, int NT>
+int launch_nt(const WoArgs& a, dim3 grid, hipStream_t st) {
   const int mt = (a.M + 15) / 16;
   switch (mt) {
-    case 1: hipLaunchKernelGGL((wo_gemm_k<BITS, G, 1, LLM>), grid, dim3(256), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((wo_gemm_k<BITS, G, 2, LLM>), grid, dim3(256), 0, st, a); break;
-    case 3: hipLaunchKernelGGL((wo_gemm_k<BITS, G, 3, LLM>), grid, dim3(256), 0, st, a); break;
-    case 4: hipLaunchKernelGGL((wo_gemm_k<BITS, G, 4, LLM>), grid, dim3(256), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((wo_gemm_k<BITS, G, 1, NT, LLM>), grid, dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((wo_gemm_k<BITS, G, 2, NT, LLM>), grid, dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((wo_gemm_k<BITS, G, 3, NT, LLM>), grid, dim3(256), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((wo_gemm_k<BITS, G, 4, NT, LLM>), grid, dim3(256), 0, st, a); break;
     default: return 1;
   }
   return 0;
 }
 
+template <int BITS, int G, bool LLM>
+int launch_mt(const WoArgs& a, dim3 grid, hipStream_t st) {
+  const int nt = LLM ? std::min(nt_for(a.M), 2) : nt_for(a.M);
+  if (nt == 1) return launch_nt<BITS, G, LLM, 1>(a, grid, st);
+  if (nt == 2) return launch_nt<BITS, G, LLM, 2>(a, grid, st);
+  if constexpr (!LLM) return launch_nt<BITS, G, LLM, 4>(a, grid, st);
+  return 1;
+}
+
 }  // namespace
 
-// Splits of K so that (N / 16) x splits workgroups fill the chip (>= 2 per CU), each split a multiple of
+// Splits of K so that (N / (16 * NT)) x splits workgroups fill the chip (>= 2 per CU), each split a multiple of
 // 4 chunks of 64.
-PA_EXPORT int pa_wo_gemm_splits(int64_t N, int64_t K) {
-  const int64_t wgs = N / 16, chunks = K / 64;
+PA_EXPORT int pa_wo_gemm_splits(int64_t M, int64_t N, int64_t K, int llm) {
+  int nt = nt_for((int)M);
+  if (llm && nt > 2) nt = 2;
+  const int64_t wgs = N / (16 * nt), chunks = K / 64;
   int s = 1;
   while (wgs * s < 512 && chunks % (s * 2 * 4) == 0) s *= 2;
   return s;
@@ -229,7 +265,9 @@ PA_EXPORT int pa_wo_gemm_splits(int64_t N, int64_t K) {
 PA_EXPORT int pa_wo_gemm(const void* x, const void* xo, const float* sx, const void* w, const float* scale,
                          const void* bias, void* y, float* ws, int M, int N, int K, int ldx, int ldy, int bits,
                          int group, int splits, hipStream_t st) {
-  if (M <= 0 || M > 64 || K % 64 != 0 || N % 16 != 0 || ldx % 8 != 0) return 1;
+  if (M <= 0 || M > 64 || K % 64 != 0 || ldx % 8 != 0) return 1;
+  const int nt_req = xo != nullptr ? std::min(nt_for(M), 2) : nt_for(M);
+  if (N % (16 * nt_req) != 0) return 1;
   if (bits != 8 && bits != 4) return 2;
   if (group != -1 && group != 64 && group != 128) return 3;
   const bool llm = xo != nullptr;
@@ -241,7 +279,7 @@ PA_EXPORT int pa_wo_gemm(const void* x, const void* xo, const float* sx, const v
   a.bias = (const uint16_t*)bias; a.y = (uint16_t*)y; a.ws = ws;
   a.M = M; a.N = N; a.K = K; a.ldx = ldx; a.ldy = ldy; a.split = splits; a.kchunks_per_split = K / 64 / splits;
   if (splits > 1 && hipMemsetAsync(ws, 0, sizeof(float) * (size_t)M * N, st) != hipSuccess) return 7;
-  dim3 grid((unsigned)(N / 16), (unsigned)splits);
+  dim3 grid((unsigned)(N / (16 * nt_req)), (unsigned)splits);
   int rc;
   if (llm) rc = launch_mt<8, 0, true>(a, grid, st);
   else if (bits == 8 && group == -1) rc = launch_mt<8, 0, false>(a, grid, st);

@@ -72,7 +72,7 @@ SIGS = {
     "pa_gemm_skinny": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _vp],
     # weight-only int8 / int4 GEMM and LLM.int8 (csrc/kernels/wo_gemm.hip)
     "pa_wo_gemm": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp],
-    "pa_wo_gemm_splits": [_i64, _i64],
+    "pa_wo_gemm_splits": [_i64, _i64, _i64, _i32],
     "pa_wo_dequant": [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp],
     "pa_gemm_skinny_ok": [_i64, _i64],
     "pa_conv_skinny": [_vp, _vp, _vp, _vp, _vp] + [_i64] * 11 + [_vp],

@@ -46,7 +46,10 @@ def wo_linear(x, w, scale, bias, bits, group, llm=None):
     b = None if bias is None else bias.to(torch.bfloat16).contiguous()
     if M <= DECODE_MAX_M:
         y = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
-        splits = int(L.lib().pa_wo_gemm_splits(N, K))
+        nt = 1 if M <= 16 else (2 if M <= 32 else (2 if llm is not None else 4))
+        if N % (16 * nt):
+            raise ValueError(f"weight-only decode GEMM needs N % {16 * nt} == 0 at M = {M} (N={N})")
+        splits = int(L.lib().pa_wo_gemm_splits(M, N, K, int(llm is not None)))
         ws = torch.empty(M * N, dtype=torch.float32, device=x.device) if splits > 1 else None
         if llm is not None:
             xq, xo, sx = llm

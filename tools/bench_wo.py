@@ -44,7 +44,7 @@ def main():
             line = f"K={K:5d} N={N:5d} M={M:2d}: " + "  ".join(f"{k} {v:7.1f}us" for k, v in res.items())
             line += f"  | int8 {best_bf16 / res['int8']:.2f}x  int4 {best_bf16 / res['int4']:.2f}x of best bf16"
             wb = K * N
-            line += f"  | int8 {wb / res['int8'] / 1e3:.2f} TB/s weight stream"
+            line += f"  | int8 weight stream {wb / res['int8'] / 1e6:.2f} TB/s"
             print(line, flush=True)
 
 
