@@ -490,6 +490,105 @@ PA_EXPORT int pa_bn_bwd_nhwc_mask(const void* dy, const void* x, const void* mbi
   return 0;
 }
 
+// ---- conv -> BN fusion: the producing convolution wrote the forward partials (csrc/kernels/gemm.hip
+// kEpiStats: stats[2][chunks][C], one chunk per 64/128 output rows), so the statistics pass over x is skipped.
+
+namespace {
+// first-level fold of a long chunk list: block (cx, g) folds chunks [g * per, (g + 1) * per) of 64 channels
+// into out[2][gridDim.y][C] (fp64 lane sums, as fold_chunks)
+__global__ __launch_bounds__(1024) void bn_fold_range_k(const float* __restrict__ partial, int chunks, int C, int per,
+                                                        float* __restrict__ out) {
+  __shared__ double sm1[kFoldLanes][64], sm2[kFoldLanes][64];
+  const int cl = threadIdx.x & 63, k = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int j0 = blockIdx.y * per, j1 = min(chunks, j0 + per);
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    const float* p1 = partial + c;
+    const float* p2 = partial + (int64_t)chunks * C + c;
+    int j = j0 + k;
+    for (; j + 3 * kFoldLanes < j1; j += 4 * kFoldLanes) {
+      float u[4], v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        u[q] = p1[(int64_t)(j + q * kFoldLanes) * C];
+        v[q] = p2[(int64_t)(j + q * kFoldLanes) * C];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { a += u[q]; b += v[q]; }
+    }
+    for (; j < j1; j += kFoldLanes) {
+      a += p1[(int64_t)j * C];
+      b += p2[(int64_t)j * C];
+    }
+  }
+  sm1[k][cl] = a;
+  sm2[k][cl] = b;
+  __syncthreads();
+  if (k == 0 && c < C) {
+    double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+    for (int q = 0; q < kFoldLanes; ++q) { t1 += sm1[q][cl]; t2 += sm2[q][cl]; }
+    out[(int64_t)blockIdx.y * C + c] = (float)t1;
+    out[((int64_t)gridDim.y + blockIdx.y) * C + c] = (float)t2;
+  }
+}
+constexpr int kFoldPer = 256;  // chunks per first-level block
+}  // namespace
+
+// Workspace floats pa_bn_fwd_nhwc_pre needs for `chunks` producer chunks (0: folded directly).
+PA_EXPORT int64_t pa_bn_pre_ws(int chunks, int C) {
+  if (chunks <= kFoldPer) return 0;
+  return 2 * (int64_t)((chunks + kFoldPer - 1) / kFoldPer) * C;
+}
+
+// Training forward from precomputed partials (stats[2][chunks][C] written by the convolution): fold ->
+// finalize (mean / rstd / running stats / scale-shift) -> apply, as pa_bn_fwd_nhwc / _mask without the
+// statistics pass. mbits (relu only): also the relu bit mask. ws: pa_bn_pre_ws floats (may be null if 0).
+PA_EXPORT int pa_bn_fwd_nhwc_pre(const void* x, const void* res, void* y, const float* w, const float* b,
+                                 float* run_mean, float* run_var, float* save_mean, float* save_rstd,
+                                 const float* stats, int chunks, float* ws, float* ss, void* mbits, int64_t R, int C,
+                                 float momentum, float eps, int relu, hipStream_t st) {
+  if (C % 8 != 0 || R < 1 || chunks < 1 || !stats) return 3;
+  if (mbits && !relu) return 3;
+  const float* part = stats;
+  int nch = chunks;
+  if (chunks > kFoldPer) {
+    if (!ws) return 3;
+    const int groups = (chunks + kFoldPer - 1) / kFoldPer;
+    hipLaunchKernelGGL(bn_fold_range_k, dim3((C + 63) / 64, groups), dim3(1024), 0, st, stats, chunks, C, kFoldPer,
+                       ws);
+    PA_CHECK_LAUNCH();
+    part = ws;
+    nch = groups;
+  }
+  hipLaunchKernelGGL(bn_fwd_finalize_k, dim3((C + 63) / 64), dim3(1024), 0, st, part, nch, C, R, w, b, run_mean,
+                     run_var, momentum, eps, save_mean, save_rstd, ss);
+  PA_CHECK_LAUNCH();
+  const int64_t nvec = R * C / 8;
+  const unsigned g = apply_grid(nvec);
+  const uint16_t* xp = (const uint16_t*)x;
+  const uint16_t* rp = (const uint16_t*)res;
+  uint16_t* yp = (uint16_t*)y;
+  if (mbits && res)
+    hipLaunchKernelGGL((bn_apply_k<true, true, true>), dim3(g), dim3(kThreads), 0, st, xp, rp, ss, yp, nvec, C,
+                       (uint8_t*)mbits);
+  else if (mbits)
+    hipLaunchKernelGGL((bn_apply_k<true, false, true>), dim3(g), dim3(kThreads), 0, st, xp, nullptr, ss, yp, nvec, C,
+                       (uint8_t*)mbits);
+  else if (relu && res)
+    hipLaunchKernelGGL((bn_apply_k<true, true>), dim3(g), dim3(kThreads), 0, st, xp, rp, ss, yp, nvec, C, nullptr);
+  else if (relu)
+    hipLaunchKernelGGL((bn_apply_k<true, false>), dim3(g), dim3(kThreads), 0, st, xp, nullptr, ss, yp, nvec, C, nullptr);
+  else if (res)
+    hipLaunchKernelGGL((bn_apply_k<false, true>), dim3(g), dim3(kThreads), 0, st, xp, rp, ss, yp, nvec, C, nullptr);
+  else
+    hipLaunchKernelGGL((bn_apply_k<false, false>), dim3(g), dim3(kThreads), 0, st, xp, nullptr, ss, yp, nvec, C,
+                       nullptr);
+  PA_CHECK_LAUNCH();
+  return 0;
+}
+
 // ---- split-phase entry points (cross-rank SyncBatchNorm: the per-channel sums are all-reduced between
 // the reduction and the apply; reference: sync_batch_norm_utils.h:575 all-reduces the backward stats)
 

@@ -56,6 +56,7 @@ enum EpiFlags : int {
   kEpiAux = 4,        // store the pre-activation (x.W + b) to aux (bf16, ldc)
   kEpiAccum = 8,      // C += result (read-modify-write)
   kEpiOutF32 = 16,    // C is fp32
+  kEpiStats = 32,     // per-column batch-norm partials of the stored C (sum, sum of squares) to stats
 };
 
 struct GemmArgs {
@@ -79,6 +80,9 @@ struct GemmArgs {
   // tail_ws; gemm_tail_reduce_k sums them and applies the epilogue. tail_split == 0: no tail.
   int full_tiles, tail_split;
   float* tail_ws;
+  // kEpiStats: stats[2][chunks][N] fp32, chunk = m-tile * (waves along M) + wave row; each (chunk, column) is
+  // written by exactly one lane (no atomics, deterministic), folded by bn.hip (pa_bn_fwd_nhwc_pre)
+  float* stats;
 };
 
 // split-K view: slice blockIdx.y of K (p.K elements each) and its own fp32 output slab
@@ -95,6 +99,30 @@ __device__ __forceinline__ GemmArgs split_view(const GemmArgs& p0) {
 }
 
 __device__ __forceinline__ float gelu_tanh(float x) { return gelu_tanh_fast(x); }
+
+// Batch-norm statistics of the fragment epilogue (conv -> BN fusion, reference:
+// fusion/gpu/fused_scale_bias_relu_conv_bn_kernel.cu computes the BN sums of the conv output in the conv):
+// s1 / s2 are a lane's sums of its rows for 4 consecutive columns n..n+3; the 16 lanes of the DPP row are
+// folded and lane 0 of the row writes chunk `chunk` of stats[2][chunks][N].
+__device__ __forceinline__ void stats_store(const GemmArgs& p, int chunk, int chunks, int n, int lane, float* s1,
+                                            float* s2) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    s1[e] = row16_sum(s1[e]);
+    s2[e] = row16_sum(s2[e]);
+  }
+  if ((lane & 15) == 0) {
+    *reinterpret_cast<float4*>(p.stats + (int64_t)chunk * p.N + n) = make_float4(s1[0], s1[1], s1[2], s1[3]);
+    *reinterpret_cast<float4*>(p.stats + ((int64_t)chunks + chunk) * p.N + n) = make_float4(s2[0], s2[1], s2[2], s2[3]);
+  }
+}
+
+// stored bf16 pair -> the two rounded values accumulated into the statistics
+__device__ __forceinline__ void stats_add2(uint32_t packed, float* s1, float* s2, int e) {
+  const float a = lo_bf16(packed), b = hi_bf16(packed);
+  s1[e] += a; s2[e] += a * a;
+  s1[e + 1] += b; s2[e + 1] += b * b;
+}
 
 // global_load_lds_dwordx4 issued from inline asm: hipcc treats a builtin LDS-DMA as a pending write to
 // every LDS object and puts s_waitcnt vmcnt(0) in front of the next ds_read, which would drain the
@@ -324,6 +352,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmArgs p0) {
   for (int j = 0; j < NR; ++j) {
     const int n = ncol0 + j * 16;
     if (n >= p.N) continue;  // N % 4 == 0 is required by the launcher
+    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
     if (flags & kEpiBias) {
       const uint2 braw = *reinterpret_cast<const uint2*>(p.bias + n);
@@ -357,9 +386,15 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmArgs p0) {
           const uint2 o = *cp;
           v[0] += lo_bf16(o.x); v[1] += hi_bf16(o.x); v[2] += lo_bf16(o.y); v[3] += hi_bf16(o.y);
         }
-        *cp = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
+        const uint2 o = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
+        *cp = o;
+        if (flags & kEpiStats) {
+          stats_add2(o.x, s1, s2, 0);
+          stats_add2(o.y, s1, s2, 2);
+        }
       }
     }
+    if (flags & kEpiStats) stats_store(p, tm * 2 + wm, p.tiles_m * 2, n, lane, s1, s2);
   }
 }
 
@@ -1169,6 +1204,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm3s_kernel(GemmArgs p0) {
   for (int j = 0; j < NR; ++j) {
     const int n = ncol0 + j * 16;
     if (n >= p.N) continue;
+    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
     if (flags & kEpiBias) {
       const uint2 braw = *reinterpret_cast<const uint2*>(p.bias + n);
@@ -1201,9 +1237,15 @@ __global__ __launch_bounds__(kThreads, 1) void gemm3s_kernel(GemmArgs p0) {
           const uint2 o = *cp;
           v[0] += lo_bf16(o.x); v[1] += hi_bf16(o.x); v[2] += lo_bf16(o.y); v[3] += hi_bf16(o.y);
         }
-        *cp = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
+        const uint2 o = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
+        *cp = o;
+        if (flags & kEpiStats) {
+          stats_add2(o.x, s1, s2, 0);
+          stats_add2(o.y, s1, s2, 2);
+        }
       }
     }
+    if (flags & kEpiStats) stats_store(p, tm * 4 + wm, p.tiles_m * 4, n, lane, s1, s2);
   }
 }
 
@@ -1628,6 +1670,34 @@ PA_EXPORT int pa_gemm_bf16(const void* a, const void* b, void* c, const void* bi
   return dispatch_layout<256>(g, a_kmajor, b_kmajor, splits, st);
 }
 
+// Statistics chunks of a kEpiStats launch (stats: [2][chunks][N] fp32): 256-row tiles x waves along M
+// (4 for the 256x160 kernel, 2 for the two-stage kernels).
+PA_EXPORT int pa_gemm_stats_chunks(int64_t M, int bn) { return (int)((M + kBM - 1) / kBM) * (bn == 160 ? 4 : 2); }
+
+// pa_gemm_bf16 (bf16 output, no split) that also writes the per-column batch-norm partials of the stored C
+// (sum, sum of squares of the bf16-rounded values) to stats. bn: 160, 256, 128 or 4 (two-stage 4-wave).
+PA_EXPORT int pa_gemm_bf16_stats(const void* a, const void* b, void* c, const void* bias, int64_t M, int64_t N,
+                                 int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor, int b_kmajor,
+                                 int flags, int bn, float* stats, hipStream_t st) {
+  if (K % kBK != 0 || N % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || ldc % 4 != 0 || !stats) return 1;
+  if (!a_kmajor && M % 8 != 0) return 1;
+  if (flags & (kEpiOutF32 | kEpiGelu | kEpiAux)) return 1;
+  if (bn != 160 && bn != 256 && bn != 128 && bn != 4) return 1;
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  GemmArgs g{};
+  g.a = (const uint16_t*)a; g.b = (const uint16_t*)b; g.c = c;
+  g.bias = (const uint16_t*)bias;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.flags = flags | kEpiStats; g.alpha = 1.f;
+  g.c_split = M * ldc;
+  g.stats = stats;
+  if (bn == 160) return dispatch_layout<160>(g, a_kmajor, b_kmajor, 1, st);
+  if (bn == 128) return dispatch_layout<128>(g, a_kmajor, b_kmajor, 1, st);
+  if (bn == 4) return dispatch_layout<4>(g, a_kmajor, b_kmajor, 1, st);
+  return dispatch_layout<256>(g, a_kmajor, b_kmajor, 1, st);
+}
+
 // Implicit-GEMM NHWC convolution forward: out[N*Ho*Wo, Cout] = im2col(x) . W^T (+ bias), with
 // x [N, H, W, C] bf16 (C % 64 == 0), w [Cout, KH, KW, C] bf16 (channels-last filter), out NHWC bf16.
 // Runs on the 3-stage 256x160 kernel; `zero` is a >= 128-byte zeroed device buffer for padding taps.
@@ -1640,6 +1710,24 @@ PA_EXPORT int pa_conv2d_nhwc_fwd(const void* x, const void* w, const void* bias,
   g.M = N * Ho * Wo; g.N = Cout; g.K = KH * KW * C;
   g.lda = C; g.ldb = (int64_t)KH * KW * C; g.ldc = Cout;
   g.flags = bias ? kEpiBias : 0; g.alpha = 1.f;
+  g.zero = (const uint16_t*)zero;
+  g.cH = H; g.cW = W; g.cC = C; g.cHo = Ho; g.cWo = Wo; g.cKW = KW; g.cStride = stride; g.cPadH = pad_h;
+  g.cPadW = pad_w; g.cDil = dil;
+  return launch3s<true, true, true>(g, 1, st);
+}
+
+// pa_conv2d_nhwc_fwd that also writes the batch-norm partials of the output (stats: [2][chunks][Cout],
+// chunks = pa_gemm_stats_chunks(N * Ho * Wo, 160)) for the following BN layer (conv -> BN fusion).
+PA_EXPORT int pa_conv2d_nhwc_fwd_stats(const void* x, const void* w, const void* bias, void* out, const void* zero,
+                                       int N, int H, int W, int C, int Cout, int KH, int KW, int stride, int pad_h,
+                                       int pad_w, int dil, int Ho, int Wo, float* stats, hipStream_t st) {
+  if (C % kBK != 0 || Cout % 8 != 0 || N <= 0 || !stats) return 1;
+  GemmArgs g{};
+  g.a = (const uint16_t*)x; g.b = (const uint16_t*)w; g.c = out; g.bias = (const uint16_t*)bias;
+  g.M = N * Ho * Wo; g.N = Cout; g.K = KH * KW * C;
+  g.lda = C; g.ldb = (int64_t)KH * KW * C; g.ldc = Cout;
+  g.flags = (bias ? kEpiBias : 0) | kEpiStats; g.alpha = 1.f;
+  g.stats = stats;
   g.zero = (const uint16_t*)zero;
   g.cH = H; g.cW = W; g.cC = C; g.cHo = Ho; g.cWo = Wo; g.cKW = KW; g.cStride = stride; g.cPadH = pad_h;
   g.cPadW = pad_w; g.cDil = dil;

@@ -40,9 +40,46 @@ struct SkArgs {
   int64_t M, lda, ldb, ldc;
   int b_kmajor;  // 1: B^T given row-major [N][K] (ldb = its row stride); 0: B row-major [K][N]
   int flags;
+  float* stats;  // STATS: batch-norm partials [2][chunks][N] of the stored C, chunk = global wave id (conv -> BN)
 };
 
-template <int NT, int KS, int R>
+// Batch-norm partials of a wave (conv -> BN fusion): s1 / s2 hold a lane's sums over its rows of the 8 consecutive
+// columns c0 = 32 q + 8 g; the 16 lanes of a DPP row (same g) are folded and lane r = 0 stores the wave's chunk.
+template <int NQ>
+__device__ __forceinline__ void sk_stats_store(float* stats, int64_t chunk, int64_t chunks, int ncols, int lane,
+                                               float (&s1)[NQ][8], float (&s2)[NQ][8]) {
+  const int g = lane >> 4;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s1[q][j] = row16_sum(s1[q][j]);
+      s2[q][j] = row16_sum(s2[q][j]);
+    }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      float* d1 = stats + chunk * ncols + 32 * q + 8 * g;
+      float* d2 = stats + (chunks + chunk) * ncols + 32 * q + 8 * g;
+      *reinterpret_cast<float4*>(d1) = make_float4(s1[q][0], s1[q][1], s1[q][2], s1[q][3]);
+      *reinterpret_cast<float4*>(d1 + 4) = make_float4(s1[q][4], s1[q][5], s1[q][6], s1[q][7]);
+      *reinterpret_cast<float4*>(d2) = make_float4(s2[q][0], s2[q][1], s2[q][2], s2[q][3]);
+      *reinterpret_cast<float4*>(d2 + 4) = make_float4(s2[q][4], s2[q][5], s2[q][6], s2[q][7]);
+    }
+  }
+}
+
+__device__ __forceinline__ void sk_stats_add(const uint4& o, float* s1, float* s2) {
+  const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float a = lo_bf16(w[j]), b = hi_bf16(w[j]);
+    s1[2 * j] += a; s2[2 * j] += a * a;
+    s1[2 * j + 1] += b; s2[2 * j + 1] += b * b;
+  }
+}
+
+template <int NT, int KS, int R, bool STATS = false>
 __global__ __launch_bounds__(256) void skinny_gemm_k(SkArgs p) {
   constexpr int N = 16 * NT, K = 32 * KS, LDK = K + 8;  // LDS row of B^T padded by 16 bytes
   extern __shared__ __attribute__((aligned(16))) uint16_t bt[];
@@ -73,7 +110,16 @@ __global__ __launch_bounds__(256) void skinny_gemm_k(SkArgs p) {
   const int64_t nb = (p.M + 16 * R - 1) / (16 * R);
   const int64_t stride = (int64_t)gridDim.x * 4;
   int64_t blk = (int64_t)blockIdx.x * 4 + wave;
-  if (blk >= nb) return;  // wave-uniform; no barrier follows
+  constexpr int NQ = STATS ? NT / 2 : 1;
+  float s1[NQ][8], s2[NQ][8];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s1[q][j] = 0.f; s2[q][j] = 0.f; }
+  if (blk >= nb) {  // wave-uniform; no barrier follows
+    if constexpr (STATS) sk_stats_store<NQ>(p.stats, (int64_t)blockIdx.x * 4 + wave, stride, N, lane, s1, s2);
+    return;
+  }
 
   // B^T operand of tile t, K step ks: MFMA row r of tile t is output column 32(t/2) + 8(r/4) + 4(t%2) + r%4
   // (two tiles interleaved so a lane's 8 results are 8 consecutive columns)
@@ -158,6 +204,7 @@ __global__ __launch_bounds__(256) void skinny_gemm_k(SkArgs p) {
           o.z = pack_bf16(v[4], v[5]);
           o.w = pack_bf16(v[6], v[7]);
           *reinterpret_cast<uint4*>(dst + c0) = o;
+          if constexpr (STATS) sk_stats_add(o, s1[q], s2[q]);
         }
       }
     }
@@ -168,6 +215,7 @@ __global__ __launch_bounds__(256) void skinny_gemm_k(SkArgs p) {
         for (int ks = 0; ks < KS; ++ks) acur[i][ks] = anext[i][ks];
     }
   }
+  if constexpr (STATS) sk_stats_store<NQ>(p.stats, (int64_t)blockIdx.x * 4 + wave, stride, N, lane, s1, s2);
 }
 
 // Opt a kernel into 160 KB of dynamic LDS once per device (the attribute is per device; one process may drive
@@ -181,30 +229,37 @@ __host__ inline void sk_lds_attr(const void* fn, unsigned long long& done) {
   done |= bit;
 }
 
-template <int NT, int KS>
+// workgroups of a skinny_gemm_k launch (the statistics variant writes 4 chunks per workgroup)
+inline int64_t sk_grid(int64_t M, int64_t N, int64_t K) {
+  const int R = N <= 128 ? 2 : 1;
+  const size_t lds = (size_t)N * (K + 8) * 2;
+  const int per_cu = (int)std::min<size_t>(8, (160 * 1024) / lds);
+  const int64_t nb = (M + 16 * R - 1) / (16 * R);
+  return std::min<int64_t>((nb + 3) / 4, (int64_t)256 * per_cu);
+}
+
+template <int NT, int KS, bool STATS = false>
 int launch_sk(const SkArgs& a, hipStream_t st) {
   // two 16-row blocks per wave iteration, except N = 256 (its 128 accumulators would leave one wave per SIMD)
   constexpr int R = NT <= 8 ? 2 : 1;
   constexpr int N = 16 * NT, K = 32 * KS;
   const size_t lds = (size_t)N * (K + 8) * 2;
   if (lds > 160 * 1024) return 2;
-  const int per_cu = (int)std::min<size_t>(8, (160 * 1024) / lds);
-  const int64_t nb = (a.M + 16 * R - 1) / (16 * R);
-  const int64_t grid = std::min<int64_t>((nb + 3) / 4, (int64_t)256 * per_cu);
+  const int64_t grid = sk_grid(a.M, N, K);
   static unsigned long long attr_done = 0;  // devices whose LDS limit this instantiation raised
-  sk_lds_attr(reinterpret_cast<const void*>(&skinny_gemm_k<NT, KS, R>), attr_done);
-  hipLaunchKernelGGL((skinny_gemm_k<NT, KS, R>), dim3((unsigned)grid), dim3(256), lds, st, a);
+  sk_lds_attr(reinterpret_cast<const void*>(&skinny_gemm_k<NT, KS, R, STATS>), attr_done);
+  hipLaunchKernelGGL((skinny_gemm_k<NT, KS, R, STATS>), dim3((unsigned)grid), dim3(256), lds, st, a);
   PA_CHECK_LAUNCH();
   return 0;
 }
 
-template <int NT>
+template <int NT, bool STATS = false>
 int launch_sk_k(const SkArgs& a, int64_t K, hipStream_t st) {
   switch (K) {
-    case 32: return launch_sk<NT, 1>(a, st);
-    case 64: return launch_sk<NT, 2>(a, st);
-    case 128: return launch_sk<NT, 4>(a, st);
-    case 256: return launch_sk<NT, 8>(a, st);
+    case 32: return launch_sk<NT, 1, STATS>(a, st);
+    case 64: return launch_sk<NT, 2, STATS>(a, st);
+    case 128: return launch_sk<NT, 4, STATS>(a, st);
+    case 256: return launch_sk<NT, 8, STATS>(a, st);
     default: return 2;
   }
 }
@@ -384,9 +439,10 @@ struct SkHaloArgs {
   const uint16_t* bias;
   int N, H, W;  // output = input size (stride 1, pad 1)
   int flags;
+  float* stats;  // STATS: batch-norm partials [2][gridDim.x * NW][64] of y (conv -> BN fusion)
 };
 
-template <int NW, int R>
+template <int NW, int R, bool STATS = false>
 __global__ __launch_bounds__(NW * 64) void skinny_conv_halo_k(SkHaloArgs p) {
   // R: segments of 16 R output pixels (R = 2: every B^T fragment read feeds 2 MFMAs, half the LDS B traffic)
   constexpr int C = 64, NT = 4, K = 9 * C, LDK = K + 8, WPX = 16 * R + 2, SLOTS = 3 * WPX * 8;
@@ -406,7 +462,16 @@ __global__ __launch_bounds__(NW * 64) void skinny_conv_halo_k(SkHaloArgs p) {
   const int64_t nseg = (int64_t)p.N * p.H * segs_row;
   const int64_t stride = (int64_t)gridDim.x * NW;
   int64_t sg = (int64_t)blockIdx.x * NW + wave;
-  if (sg >= nseg) return;
+  constexpr int NQ = STATS ? NT / 2 : 1;
+  float s1[NQ][8], s2[NQ][8];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s1[q][j] = 0.f; s2[q][j] = 0.f; }
+  if (sg >= nseg) {
+    if constexpr (STATS) sk_stats_store<NQ>(p.stats, (int64_t)blockIdx.x * NW + wave, stride, 16 * NT, lane, s1, s2);
+    return;
+  }
   // DMA of segment s's window: slot q = 64 i + lane (q < SLOTS) -> LDS byte 16 q = (row, px, swizzled chunk)
   auto load_window = [&](int64_t s) {
     const int seg = (int)(s % segs_row);
@@ -495,24 +560,33 @@ __global__ __launch_bounds__(NW * 64) void skinny_conv_halo_k(SkHaloArgs p) {
           o.z = pack_bf16(v[4], v[5]);
           o.w = pack_bf16(v[6], v[7]);
           *reinterpret_cast<uint4*>(dst + c0) = o;
+          if constexpr (STATS) sk_stats_add(o, s1[q], s2[q]);
         }
       }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (STATS) sk_stats_store<NQ>(p.stats, (int64_t)blockIdx.x * NW + wave, stride, 16 * NT, lane, s1, s2);
 }
 
 template <int NW, int R>
+int64_t halo_grid(int64_t N, int64_t H, int64_t W) {
+  constexpr int NI = (3 * (16 * R + 2) * 8 + 63) / 64;
+  const size_t lds = (size_t)64 * (9 * 64 + 8) * 2 + (size_t)NW * NI * 1024;
+  const int64_t nseg = N * H * ((W + 16 * R - 1) / (16 * R));
+  const int per_cu = (int)std::max<size_t>(1, (160 * 1024) / lds);
+  return std::min<int64_t>((nseg + NW - 1) / NW, (int64_t)256 * per_cu);
+}
+
+template <int NW, int R, bool STATS = false>
 int launch_halo(const SkHaloArgs& a, hipStream_t st) {
   constexpr int NI = (3 * (16 * R + 2) * 8 + 63) / 64;
   const size_t lds = (size_t)64 * (9 * 64 + 8) * 2 + (size_t)NW * NI * 1024;
   if (lds > 160 * 1024) return 2;
-  const int64_t nseg = (int64_t)a.N * a.H * ((a.W + 16 * R - 1) / (16 * R));
-  const int per_cu = (int)std::max<size_t>(1, (160 * 1024) / lds);
-  const int64_t grid = std::min<int64_t>((nseg + NW - 1) / NW, (int64_t)256 * per_cu);
+  const int64_t grid = halo_grid<NW, R>(a.N, a.H, a.W);
   static unsigned long long attr_done = 0;
-  sk_lds_attr(reinterpret_cast<const void*>(&skinny_conv_halo_k<NW, R>), attr_done);
-  hipLaunchKernelGGL((skinny_conv_halo_k<NW, R>), dim3((unsigned)grid), dim3(NW * 64), lds, st, a);
+  sk_lds_attr(reinterpret_cast<const void*>(&skinny_conv_halo_k<NW, R, STATS>), attr_done);
+  hipLaunchKernelGGL((skinny_conv_halo_k<NW, R, STATS>), dim3((unsigned)grid), dim3(NW * 64), lds, st, a);
   PA_CHECK_LAUNCH();
   return 0;
 }
@@ -660,6 +734,30 @@ PA_EXPORT int pa_gemm_skinny(const void* a, const void* b, void* c, const void* 
   }
 }
 
+// Statistics chunks of pa_gemm_skinny_stats for (M, N, K) (0: no statistics variant, N > 128).
+PA_EXPORT int64_t pa_gemm_skinny_stats_chunks(int64_t M, int64_t N, int64_t K) {
+  if (!pa_gemm_skinny_ok(N, K) || N > 128 || M <= 0) return 0;
+  return sk_grid(M, N, K) * 4;
+}
+
+// pa_gemm_skinny (no accumulate / relu) that also writes the batch-norm partials of the stored C to stats
+// ([2][chunks][N] fp32, chunks = pa_gemm_skinny_stats_chunks) for the following BN (conv -> BN fusion).
+PA_EXPORT int pa_gemm_skinny_stats(const void* a, const void* b, void* c, const void* bias, int64_t M, int64_t N,
+                                   int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int b_kmajor, float* stats,
+                                   void* stream) {
+  if (M <= 0) return 0;
+  if (!pa_gemm_skinny_ok(N, K) || N > 128 || !stats) return 2;
+  SkArgs g{static_cast<const uint16_t*>(a), static_cast<const uint16_t*>(b), static_cast<uint16_t*>(c),
+           static_cast<const uint16_t*>(bias), M, lda, ldb, ldc, b_kmajor, bias ? kSkEpiBias : 0, stats};
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  switch (N) {
+    case 32: return launch_sk_k<2, true>(g, K, st);
+    case 64: return launch_sk_k<4, true>(g, K, st);
+    case 128: return launch_sk_k<8, true>(g, K, st);
+    default: return 2;
+  }
+}
+
 // 1 if the skinny implicit convolution has an instantiation for (C, Cout, KH, KW).
 PA_EXPORT int pa_conv_skinny_ok(int64_t C, int64_t Cout, int64_t KH, int64_t KW) {
   return C == 64 && Cout == 64 && KH == 3 && KW == 3;
@@ -707,6 +805,21 @@ PA_EXPORT int pa_conv_skinny(const void* x, const void* w, const void* bias, voi
     case 3: return launch_skconv<4, 64, 3, 3, 1, 4>(a, st);
     default: return launch_skconv<4, 64, 3, 3, 2, 4>(a, st);
   }
+}
+
+// Statistics chunks of pa_conv_skinny_stats (the 3x3 stride-1 pad-1 halo kernel, 12 waves per workgroup).
+PA_EXPORT int64_t pa_conv_skinny_stats_chunks(int64_t N, int64_t H, int64_t W) { return halo_grid<12, 1>(N, H, W) * 12; }
+
+// 3x3 stride-1 pad-1 C = Cout = 64 convolution on the halo kernel that also writes the batch-norm partials of y
+// ([2][chunks][64], chunks = pa_conv_skinny_stats_chunks) for the following BN (conv -> BN fusion).
+PA_EXPORT int pa_conv_skinny_stats(const void* x, const void* w, const void* bias, void* y, const void* zero_page,
+                                   int64_t N, int64_t H, int64_t W, float* stats, void* stream) {
+  if (!zero_page || !stats || N <= 0) return 2;
+  if (N * H * W * 64 * 2 >= ((int64_t)1 << 31) - (1 << 21)) return 2;
+  SkHaloArgs h{static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w),
+               static_cast<const uint16_t*>(zero_page), static_cast<uint16_t*>(y),
+               static_cast<const uint16_t*>(bias), (int)N, (int)H, (int)W, bias ? kSkEpiBias : 0, stats};
+  return launch_halo<12, 1, true>(h, static_cast<hipStream_t>(stream));
 }
 
 // dW partial slabs of the 3x3 stride-1 pad-1 C = Cout = 64 weight gradient (skinny_wgrad3_k): ws holds `splits`

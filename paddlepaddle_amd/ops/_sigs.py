@@ -75,10 +75,18 @@ SIGS = {
     "pa_wo_gemm_splits": [_i64, _i64, _i64, _i32],
     "pa_wo_dequant": [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp],
     "pa_gemm_skinny_ok": [_i64, _i64],
+    "pa_gemm_skinny_stats_chunks": [_i64, _i64, _i64],
+    "pa_gemm_skinny_stats": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _vp, _vp],
+    "pa_conv_skinny_stats_chunks": [_i64, _i64, _i64],
+    "pa_conv_skinny_stats": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp],
     "pa_conv_skinny": [_vp, _vp, _vp, _vp, _vp] + [_i64] * 11 + [_vp],
     "pa_conv_skinny_ok": [_i64, _i64, _i64, _i64],
     "pa_conv_skinny_wgrad": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp],
     "pa_conv2d_nhwc_fwd": [_vp, _vp, _vp, _vp, _vp] + [_i32] * 13 + [_vp],
+    "pa_conv2d_nhwc_fwd_stats": [_vp, _vp, _vp, _vp, _vp] + [_i32] * 13 + [_vp, _vp],
+    "pa_gemm_stats_chunks": [_i64, _i32],
+    "pa_gemm_bf16_stats": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _vp,
+                           _vp],
     "pa_conv2d_nhwc_wgrad": [_vp, _vp, _vp, _vp] + [_i32] * 15 + [_vp],
     "pa_bias_gelu_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp],
     "pa_dropout_add_fwd": [_vp, _vp, _vp, _i64, _f32, _u64, _i32, _vp],
@@ -91,6 +99,8 @@ SIGS = {
     "pa_bn_fwd_nhwc_mask": [_vp] * 12 + [_i64, _i32, _f32, _f32, _i32, _vp],
     "pa_bn_bwd_nhwc_mask": [_vp] * 12 + [_i64, _i32, _i32, _vp],
     "pa_bn_bwd_apply_nhwc": [_vp] * 6 + [_i64, _i32, _i32, _vp, _vp],
+    "pa_bn_pre_ws": [_i32, _i32],
+    "pa_bn_fwd_nhwc_pre": [_vp] * 10 + [_i32, _vp, _vp, _vp, _i64, _i32, _f32, _f32, _i32, _vp],
     # fused decode step
     "pa_add_rms_norm_fwd": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _f32, _i32, _vp],
     "pa_decode_rope_cache": [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i64, _i32, _vp],
@@ -104,4 +114,4 @@ SIGS = {
     "pa_version": [],
 }
 
-RET_I64 = {"pa_gemm_pp_ws_bytes"}
+RET_I64 = {"pa_gemm_pp_ws_bytes", "pa_bn_pre_ws", "pa_gemm_skinny_stats_chunks", "pa_conv_skinny_stats_chunks"}

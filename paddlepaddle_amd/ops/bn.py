@@ -13,6 +13,7 @@ from __future__ import annotations
 import torch
 
 from . import _loader as L
+from . import _conv_bn as _CB
 from ..framework.trace_hook import static_op
 
 
@@ -50,7 +51,7 @@ def _chunks(R, C):
 class _BNActHIP(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x2, weight, bias, residual, running_mean, running_var, training, momentum, eps, relu,
-                sink=None):
+                sink=None, pre=None):
         ctx.sink = sink
         R, C = x2.shape
         dev = x2.device
@@ -59,7 +60,7 @@ class _BNActHIP(torch.autograd.Function):
         if training:
             mean = torch.empty(C, dtype=torch.float32, device=dev)
             rstd = torch.empty(C, dtype=torch.float32, device=dev)
-            partial = torch.empty(2 * _chunks(R, C) * C, dtype=torch.float32, device=dev)
+            partial = torch.empty(2 * _chunks(R, C) * C, dtype=torch.float32, device=dev) if pre is None else None
         else:
             mean = running_mean.float().contiguous()
             rstd = torch.rsqrt(running_var.float() + eps)
@@ -73,7 +74,17 @@ class _BNActHIP(torch.autograd.Function):
         # backward reads instead of y
         mask_x = bool(relu) and residual is None
         mbits = None
-        if relu and residual is not None and L.has("pa_bn_fwd_nhwc_mask"):
+        if training and pre is not None:
+            # conv -> BN fusion: the producing convolution wrote the partial sums (ops/_conv_bn.py)
+            stats, chunks = pre
+            if relu and residual is not None:
+                mbits = torch.empty(R * C // 8, dtype=torch.uint8, device=dev)
+            nws = int(L.lib().pa_bn_pre_ws(chunks, C))
+            ws = torch.empty(nws, dtype=torch.float32, device=dev) if nws else None
+            L.call("pa_bn_fwd_nhwc_pre", L.ptr(x2), L.ptr(residual), L.ptr(y), L.ptr(weight), L.ptr(bias),
+                   L.ptr(running_mean), L.ptr(running_var), L.ptr(mean), L.ptr(rstd), L.ptr(stats), chunks, L.ptr(ws),
+                   L.ptr(ss), L.ptr(mbits), R, C, float(momentum), float(eps), int(bool(relu)), L.stream_ptr())
+        elif relu and residual is not None and L.has("pa_bn_fwd_nhwc_mask"):
             mbits = torch.empty(R * C // 8, dtype=torch.uint8, device=dev)
             L.call("pa_bn_fwd_nhwc_mask", L.ptr(x2), L.ptr(residual), L.ptr(y), L.ptr(weight), L.ptr(bias),
                    L.ptr(running_mean if training else None), L.ptr(running_var if training else None), L.ptr(mean),
@@ -118,7 +129,7 @@ class _BNActHIP(torch.autograd.Function):
         if to_sink:  # the block's first conv adds it to its data gradient (ops/conv.py ResidualGradSink)
             sink.dres = dres
             dres = None
-        return dx, dw, db, dres, None, None, None, None, None, None, None
+        return dx, dw, db, dres, None, None, None, None, None, None, None, None
 
 
 def _hip_ok(x, weight, bias, residual, running_mean, running_var):
@@ -153,8 +164,9 @@ def batch_norm_act_nhwc(x, weight, bias, running_mean, running_var, training=Tru
         sink = grad_sink if (grad_sink is not None and grad_sink.armed and r2 is not None) else None
         if sink is not None:
             r2 = r2.detach()  # its gradient travels through the sink, not autograd
+        pre = _CB.take(x) if training else None
         y = _BNActHIP.apply(x2, weight, bias, r2, running_mean, running_var, bool(training), float(momentum),
-                            float(eps), act == "relu", sink)
+                            float(eps), act == "relu", sink, pre)
         return y.view(x.shape)
     x2 = x.reshape(-1, C)
     r2 = residual.reshape(-1, C) if residual is not None else None

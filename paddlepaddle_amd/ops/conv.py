@@ -20,6 +20,7 @@ from __future__ import annotations
 import torch
 
 from . import _loader as L
+from . import _conv_bn as _CB
 from . import gemm as G
 
 
@@ -330,6 +331,44 @@ def _skinny_ok(x, w, stride, dgrad, pad=0, dil=1):
     return M >= 1024 and bool(L.lib().pa_gemm_skinny_ok(n, k))
 
 
+def _skinny_stats_ok(x, w, stride, pad, dil):
+    """The skinny kernels with a statistics epilogue: 1x1 with Cout <= 128, the 3x3 stride-1 pad-1 halo kernel."""
+    Cout, _, KH, KW = w.shape
+    if KH == 1 and KW == 1:
+        return L.has("pa_gemm_skinny_stats") and Cout <= 128
+    return L.has("pa_conv_skinny_stats") and stride == 1 and pad == 1 and dil == 1
+
+
+def _own_fwd_stats(x, w, b, stride, pad, dil, skinny=False):
+    """The hand-written forward that also writes the following BN's partials (conv -> BN fusion, ops/_conv_bn.py):
+    (y, (stats, chunks))."""
+    N, H, W, C = x.shape
+    Cout, _, KH, KW = w.shape
+    if KH == 1 and KW == 1:
+        xs = x[:, ::stride, ::stride, :].contiguous() if stride > 1 else x
+        mm = G.gemm_skinny_bn_stats if skinny else G.gemm_bn_stats
+        y2, stats, chunks = mm(xs.reshape(-1, C), w.reshape(Cout, C).t(), bias=b)
+        return y2.view(N, xs.shape[1], xs.shape[2], Cout), (stats, chunks)
+    wk = w.permute(0, 2, 3, 1)
+    if not wk.is_contiguous():
+        wk = wk.contiguous()
+    if skinny:
+        out = torch.empty(N, H, W, Cout, dtype=x.dtype, device=x.device)
+        chunks = int(L.lib().pa_conv_skinny_stats_chunks(N, H, W))
+        stats = torch.empty(2 * chunks * Cout, dtype=torch.float32, device=x.device)
+        L.call("pa_conv_skinny_stats", L.ptr(x), L.ptr(wk), L.ptr(b), L.ptr(out), L.ptr(_zero_page(x.device)), N, H, W,
+               L.ptr(stats), L.stream_ptr())
+        return out, (stats, chunks)
+    Ho = (H + 2 * pad - dil * (KH - 1) - 1) // stride + 1
+    Wo = (W + 2 * pad - dil * (KW - 1) - 1) // stride + 1
+    out = torch.empty(N, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
+    chunks = int(L.lib().pa_gemm_stats_chunks(N * Ho * Wo, 160))
+    stats = torch.empty(2 * chunks * Cout, dtype=torch.float32, device=x.device)
+    L.call("pa_conv2d_nhwc_fwd_stats", L.ptr(x), L.ptr(wk), L.ptr(b), L.ptr(out), L.ptr(_zero_page(x.device)), N, H,
+           W, C, Cout, KH, KW, stride, pad, pad, dil, Ho, Wo, L.ptr(stats), L.stream_ptr())
+    return out, (stats, chunks)
+
+
 def _own_fwd(x, w, b, stride, pad, dil, skinny=False):
     N, H, W, C = x.shape
     Cout, _, KH, KW = w.shape
@@ -458,17 +497,38 @@ def _mm_dgrad(x, w, dy, stride, acc=None):
 
 class _ConvNHWC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, stride, pad, dil, sink=None, produce=None):
+    def forward(ctx, x, w, b, stride, pad, dil, sink=None, produce=None, bn_stats=False):
         key = (tuple(x.shape), tuple(w.shape), stride, pad, dil)
-        sk = (lambda: _own_fwd(x, w, b, stride, pad, dil, skinny=True)) \
-            if _skinny_ok(x, w, stride, False, pad, dil) else None
         one = w.shape[2] == 1 and w.shape[3] == 1
-        ch = _pick(("convf",) + key + (b is not None,), lambda: _own_fwd(x, w, b, stride, pad, dil),
-                   lambda: _mi_fwd(x, w, b, stride, pad, dil), sk, (lambda: _mm_fwd(x, w, b, stride)) if one else None)
+        _CB._PENDING[0] = None
+        sk_stats = False
+        if bn_stats:
+            # a training BN consumes the output: the hand-written kernels write its statistics in the epilogue;
+            # the other candidates are timed with the statistics pass the BN then runs itself
+            red = _CB.reduce_cost
+            sk = None
+            sk_stats = _skinny_ok(x, w, stride, False, pad, dil) and _skinny_stats_ok(x, w, stride, pad, dil)
+            if sk_stats:
+                sk = lambda: _own_fwd_stats(x, w, b, stride, pad, dil, skinny=True)  # noqa: E731
+            elif _skinny_ok(x, w, stride, False, pad, dil):
+                sk = lambda: red(_own_fwd(x, w, b, stride, pad, dil, skinny=True))  # noqa: E731
+            ch = _pick(("convf",) + key + (b is not None, "bn"), lambda: _own_fwd_stats(x, w, b, stride, pad, dil),
+                       lambda: red(_mi_fwd(x, w, b, stride, pad, dil)), sk,
+                       (lambda: red(_mm_fwd(x, w, b, stride))) if one else None)
+        else:
+            sk = (lambda: _own_fwd(x, w, b, stride, pad, dil, skinny=True)) \
+                if _skinny_ok(x, w, stride, False, pad, dil) else None
+            ch = _pick(("convf",) + key + (b is not None,), lambda: _own_fwd(x, w, b, stride, pad, dil),
+                       lambda: _mi_fwd(x, w, b, stride, pad, dil), sk,
+                       (lambda: _mm_fwd(x, w, b, stride)) if one else None)
         if ch == "blas":
             y = _mi_fwd(x, w, b, stride, pad, dil)
         elif ch == "mm":
             y = _mm_fwd(x, w, b, stride)
+        elif ch == "hip" and bn_stats:
+            y, _CB._PENDING[0] = _own_fwd_stats(x, w, b, stride, pad, dil)
+        elif ch == "skinny" and bn_stats and sk_stats:
+            y, _CB._PENDING[0] = _own_fwd_stats(x, w, b, stride, pad, dil, skinny=True)
         else:
             y = _own_fwd(x, w, b, stride, pad, dil, skinny=ch == "skinny")
         ctx.save_for_backward(x, w)
@@ -532,7 +592,7 @@ class _ConvNHWC(torch.autograd.Function):
             dx = dx if dx.is_contiguous() else dx.contiguous()
             prod.dres = dx if prod.dres is None else prod.dres.add_(dx)
             dx = None  # the block's first conv adds it (residual_grad_producer)
-        return dx, dw, db, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None
 
 
 def conv2d_nhwc(x, w, b, stride, pad, dil):
@@ -545,7 +605,11 @@ def conv2d_nhwc(x, w, b, stride, pad, dil):
     produce, _PRODUCER[0] = _PRODUCER[0], None
     if produce is not None and produce is sink:
         produce = None
-    return _ConvNHWC.apply(x, w, b, stride, pad, dil, sink, produce)
+    key = (tuple(x.shape), tuple(w.shape), stride, pad, dil)
+    y = _ConvNHWC.apply(x, w, b, stride, pad, dil, sink, produce, _CB.wanted(key))
+    pre, _CB._PENDING[0] = _CB._PENDING[0], None
+    _CB.tag(y, key, pre)
+    return y
 
 
 def eligible_nhwc(x_nhwc, w, groups):

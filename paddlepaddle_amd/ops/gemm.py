@@ -88,6 +88,22 @@ def gemm(a, b, bias=None, gelu=False, aux=None, out=None, accumulate=False, alph
     return out
 
 
+def gemm_bn_stats(a, b, bias=None):
+    """C = a @ b (+ bias) in bf16 plus the batch-norm partials of C's columns, written by the GEMM epilogue
+    (kEpiStats): returns (C, stats [2 * chunks * N] fp32, chunks) for ops/bn.py (conv -> BN fusion)."""
+    M, K = a.shape
+    N = b.shape[1]
+    lda, ak = _layout(a, 0)
+    ldb, bk = _layout(b, 1)
+    bn = 160 if bk else (256 if _pick_bn(M, N, bk) == 256 else 128)
+    chunks = int(L.lib().pa_gemm_stats_chunks(M, bn))
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    stats = torch.empty(2 * chunks * N, dtype=torch.float32, device=a.device)
+    L.call("pa_gemm_bf16_stats", L.ptr(a), L.ptr(b), L.ptr(out), L.ptr(bias), M, N, K, lda, ldb, N, int(ak),
+           int(bk), EPI_BIAS if bias is not None else 0, bn, L.ptr(stats), L.stream_ptr())
+    return out, stats, chunks
+
+
 def gemm_splitk(a, b, splits, out_dtype=torch.bfloat16, bn=None):
     """C = a @ b with K split over ``splits`` slices computed by separate workgroups (fp32 slabs, summed
     here): fills the chip when M x N has few tiles but K is long (weight gradients of convolutions)."""
@@ -130,6 +146,23 @@ def gemm_skinny(a, b, bias=None, out=None, accumulate=False, relu=False):
     if rc:
         raise RuntimeError(f"pa_gemm_skinny failed ({rc}) for M={M} N={N} K={K}")
     return out
+
+
+def gemm_skinny_bn_stats(a, b, bias=None):
+    """gemm_skinny plus the batch-norm partials of C's columns (N <= 128): (C, stats, chunks), or None when the
+    shape has no statistics variant."""
+    M, K = a.shape
+    N = b.shape[1]
+    chunks = int(L.lib().pa_gemm_skinny_stats_chunks(M, N, K))
+    if chunks <= 0:
+        return None
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    stats = torch.empty(2 * chunks * N, dtype=torch.float32, device=a.device)
+    bk = b.stride(0) == 1
+    ldb = b.stride(1) if bk else b.stride(0)
+    L.call("pa_gemm_skinny_stats", L.ptr(a), L.ptr(b), L.ptr(out), L.ptr(bias), M, N, K, a.stride(0), ldb, N, int(bk),
+           L.ptr(stats), L.stream_ptr())
+    return out, stats, chunks
 
 
 def pick_splits(M, N, K, bn=256, cus=256, max_ws_bytes=256 << 20):

@@ -1,0 +1,140 @@
+"""Conv -> BN fusion (ops/_conv_bn.py): the convolution's GEMM epilogue writes the batch-norm partial sums of its
+bf16 output (csrc/kernels/gemm.hip kEpiStats) and the BN forward starts from them (bn.hip pa_bn_fwd_nhwc_pre)
+instead of re-reading the activation. Reference: paddle/phi/kernels/fusion/gpu/fused_scale_bias_relu_conv_bn_kernel.cu.
+Each check compares against plain PyTorch fp64/fp32 math of the same op, or against the unfused path."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from paddlepaddle_amd.ops import _loader as L  # noqa: E402
+from paddlepaddle_amd.ops import gemm as G  # noqa: E402
+from paddlepaddle_amd.ops import conv as C  # noqa: E402
+from paddlepaddle_amd.ops import _conv_bn as CB  # noqa: E402
+
+
+def _fold(stats, chunks, n):
+    s = stats.view(2, chunks, n).double().sum(1)
+    return s[0], s[1]
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 64, 64), (4096, 192, 256), (25088, 128, 576), (300, 512, 128)])
+def test_gemm_epilogue_bn_partials(M, N, K):
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    y, stats, chunks = G.gemm_bn_stats(a, w.t())
+    torch.cuda.synchronize()
+    ref = a.float() @ w.float().t()
+    assert (y.float() - ref).abs().max().item() < 3e-2 * ref.abs().max().item()
+    s1, s2 = _fold(stats, chunks, N)
+    yd = y.double()
+    torch.testing.assert_close(s1, yd.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(s2, (yd * yd).sum(0), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("n,hw,cin,cout,k,stride", [(4, 28, 64, 64, 3, 1), (8, 28, 128, 128, 3, 2),
+                                                    (2, 14, 64, 256, 1, 1), (32, 28, 128, 128, 3, 1)])
+def test_conv_epilogue_bn_partials(n, hw, cin, cout, k, stride):
+    g = torch.Generator(device="cuda").manual_seed(n * hw + cin)
+    x = torch.randn(n, hw, hw, cin, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(cout, cin, k, k, device="cuda", generator=g) / (cin * k * k) ** 0.5).bfloat16()
+    L.reset_calls()
+    y, (stats, chunks) = C._own_fwd_stats(x, w, None, stride, k // 2, 1)
+    torch.cuda.synchronize()
+    assert L.calls("pa_conv2d_nhwc_fwd_stats") + L.calls("pa_gemm_bf16_stats") == 1
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float(), None, stride, k // 2)
+    ref = ref.permute(0, 2, 3, 1)
+    assert (y.float() - ref).abs().max().item() < 3e-2 * ref.abs().max().item()
+    s1, s2 = _fold(stats, chunks, cout)
+    yd = y.double().reshape(-1, cout)
+    torch.testing.assert_close(s1, yd.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(s2, (yd * yd).sum(0), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(5000, 64, 256), (20000, 128, 64), (3136, 64, 64)])
+def test_skinny_gemm_epilogue_bn_partials(M, N, K):
+    g = torch.Generator(device="cuda").manual_seed(M + K)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    r = G.gemm_skinny_bn_stats(a, w.t())
+    assert r is not None
+    y, stats, chunks = r
+    torch.cuda.synchronize()
+    ref = a.float() @ w.float().t()
+    assert (y.float() - ref).abs().max().item() < 3e-2 * ref.abs().max().item()
+    s1, s2 = _fold(stats, chunks, N)
+    yd = y.double()
+    torch.testing.assert_close(s1, yd.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(s2, (yd * yd).sum(0), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("n,hw", [(2, 56), (8, 20)])
+def test_skinny_halo_conv_epilogue_bn_partials(n, hw):
+    g = torch.Generator(device="cuda").manual_seed(n + hw)
+    x = torch.randn(n, hw, hw, 64, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(64, 64, 3, 3, device="cuda", generator=g) / 24.0).bfloat16()
+    L.reset_calls()
+    y, (stats, chunks) = C._own_fwd_stats(x, w, None, 1, 1, 1, skinny=True)
+    torch.cuda.synchronize()
+    assert L.calls("pa_conv_skinny_stats") == 1
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float(), None, 1, 1).permute(0, 2, 3, 1)
+    assert (y.float() - ref).abs().max().item() < 3e-2 * ref.abs().max().item()
+    s1, s2 = _fold(stats, chunks, 64)
+    yd = y.double().reshape(-1, 64)
+    torch.testing.assert_close(s1, yd.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(s2, (yd * yd).sum(0), rtol=1e-4, atol=1e-2)
+
+
+def _block(fused, x0, params, steps=2):
+    """conv(3x3) -> BN+relu -> conv(1x1) -> BN (+ residual) + relu on the paddle NHWC layers."""
+    import paddlepaddle_amd as paddle
+    from paddlepaddle_amd.framework import flags
+    flags.set_flags({"FLAGS_conv_bn_fusion": fused})
+    CB._FEEDS_BN.clear()
+    paddle.seed(0)
+    nn = paddle.nn
+    conv1 = nn.Conv2D(64, 64, 3, padding=1, bias_attr=False, data_format="NHWC")
+    bn1 = nn.BatchNorm2D(64, data_format="NHWC")
+    conv2 = nn.Conv2D(64, 64, 1, bias_attr=False, data_format="NHWC")
+    bn2 = nn.BatchNorm2D(64, data_format="NHWC")
+    conv1.weight.set_value(params[0])
+    conv2.weight.set_value(params[1])
+    for m in (conv1, conv2):
+        m.weight._t.data = m.weight._t.data.bfloat16()
+    outs = []
+    for _ in range(steps):
+        x = paddle.Tensor(x0.clone().requires_grad_(True))
+        x.stop_gradient = False
+        h = bn1.fused_forward(conv1(x), "relu", None)
+        y = bn2.fused_forward(conv2(h), "relu", x)
+        y.astype("float32").sum().backward()
+        outs.append((y._t.float().clone(), x.grad._t.float().clone(), conv1.weight.grad._t.float().clone()))
+        conv1.weight.clear_gradient()
+        conv2.weight.clear_gradient()
+    torch.cuda.synchronize()
+    return outs, bn1._mean._t.clone(), bn2._variance._t.clone()
+
+
+def test_fused_block_matches_unfused():
+    import paddlepaddle_amd as paddle
+    from paddlepaddle_amd.framework import flags
+    paddle.set_device("gpu:0")
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x0 = torch.randn(16, 28, 28, 64, device="cuda", generator=g).bfloat16()
+    params = [torch.randn(64, 64, 3, 3, device="cuda", generator=g) * 0.05,
+              torch.randn(64, 64, 1, 1, device="cuda", generator=g) * 0.1]
+    try:
+        ref, rm_ref, rv_ref = _block(False, x0, params)
+        L.reset_calls()
+        got, rm, rv = _block(True, x0, params)
+        # step 1 learns the conv -> BN pairs, step 2 runs fused
+        assert L.calls("pa_bn_fwd_nhwc_pre") >= 1, dict(L.CALLS)
+    finally:
+        flags.set_flags({"FLAGS_conv_bn_fusion": True})
+    for (y, dx, dw), (yr, dxr, dwr) in zip(got, ref):
+        assert (y - yr).abs().max().item() <= 0.02 * yr.abs().max().item() + 1e-3
+        assert (dx - dxr).abs().max().item() <= 0.02 * dxr.abs().max().item() + 1e-3
+        assert (dw - dwr).abs().max().item() <= 0.02 * dwr.abs().max().item() + 1e-3
+    torch.testing.assert_close(rm, rm_ref, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(rv, rv_ref, rtol=1e-3, atol=1e-4)
