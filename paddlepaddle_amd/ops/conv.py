@@ -595,10 +595,11 @@ class _ConvNHWC(torch.autograd.Function):
         return dx, dw, db, None, None, None, None, None, None
 
 
-def conv2d_nhwc(x, w, b, stride, pad, dil):
+def conv2d_nhwc(x, w, b, stride, pad, dil, bn_stats=None):
     """NHWC 2-D convolution (groups 1, symmetric padding) with each of its three products on the hand-written
     kernel or MIOpen, whichever measured faster for the shape. A stride-1 1x1 convolution inside
-    ``residual_grad_sink()`` takes over the block's residual gradient (ResidualGradSink)."""
+    ``residual_grad_sink()`` takes over the block's residual gradient (ResidualGradSink). ``bn_stats``: True when
+    the caller knows a training BN consumes the output (fused units), None to learn it (ops/_conv_bn.py)."""
     sink = _SINK[0] if (w.shape[2] == 1 and w.shape[3] == 1 and stride == 1) else None
     if sink is not None:
         sink.armed = True
@@ -606,7 +607,8 @@ def conv2d_nhwc(x, w, b, stride, pad, dil):
     if produce is not None and produce is sink:
         produce = None
     key = (tuple(x.shape), tuple(w.shape), stride, pad, dil)
-    y = _ConvNHWC.apply(x, w, b, stride, pad, dil, sink, produce, _CB.wanted(key))
+    want = _CB.wanted(key) if bn_stats is None else (bool(bn_stats) and torch.is_grad_enabled() and _CB.enabled())
+    y = _ConvNHWC.apply(x, w, b, stride, pad, dil, sink, produce, want)
     pre, _CB._PENDING[0] = _CB._PENDING[0], None
     _CB.tag(y, key, pre)
     return y

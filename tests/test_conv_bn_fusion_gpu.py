@@ -98,17 +98,16 @@ def _block(fused, x0, params, steps=2):
     bn1 = nn.BatchNorm2D(64, data_format="NHWC")
     conv2 = nn.Conv2D(64, 64, 1, bias_attr=False, data_format="NHWC")
     bn2 = nn.BatchNorm2D(64, data_format="NHWC")
-    conv1.weight.set_value(params[0])
-    conv2.weight.set_value(params[1])
-    for m in (conv1, conv2):
-        m.weight._t.data = m.weight._t.data.bfloat16()
+    conv1.weight._t.data = params[0].bfloat16()
+    conv2.weight._t.data = params[1].bfloat16()
     outs = []
     for _ in range(steps):
         x = paddle.Tensor(x0.clone().requires_grad_(True))
         x.stop_gradient = False
         h = bn1.fused_forward(conv1(x), "relu", None)
         y = bn2.fused_forward(conv2(h), "relu", x)
-        y.astype("float32").sum().backward()
+        gy = torch.randn(y.shape, device="cuda", generator=torch.Generator(device="cuda").manual_seed(9))
+        y.astype("float32").backward(paddle.Tensor(gy))
         outs.append((y._t.float().clone(), x.grad._t.float().clone(), conv1.weight.grad._t.float().clone()))
         conv1.weight.clear_gradient()
         conv2.weight.clear_gradient()

@@ -80,14 +80,17 @@ def test_resnet50_layer1_stack_bf16_hip_vs_fp32():
     xb.stop_gradient = False
     L.reset_calls()
     y = stage(xb)
-    y.astype("float32").sum().backward()
+    # a random cotangent: d sum(y) / dx through training-mode BN is a near-total cancellation (the batch mean
+    # removes it), which no bf16 pipeline reproduces to a few percent of its tiny magnitude
+    gy = torch.randn(y.shape, device="cuda", generator=g)
+    y.astype("float32").backward(paddle.Tensor(gy))
     torch.cuda.synchronize()
     assert sum(v for k, v in L.CALLS.items() if k.startswith("pa_bn_")) > 0
     assert sum(v for k, v in L.CALLS.items() if "gemm" in k or "conv" in k) > 0
     xf = paddle.Tensor(x.clone().requires_grad_(True))
     xf.stop_gradient = False
     yf = ref(xf)
-    yf.sum().backward()
+    yf.backward(paddle.Tensor(gy))
     assert _rel(y._t, yf._t.detach()) < 5e-2
     assert _rel(xb.grad._t, xf.grad._t) < 8e-2
 
