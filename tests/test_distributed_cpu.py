@@ -422,3 +422,30 @@ def test_data_parallel_two_optimizers_clear_grad_keeps_other_grads():
         assert out == [[True, True]]
         for k in ref:
             np.testing.assert_allclose(sd[k], ref[k], rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+def _moe_exchange_worker(rank, world, port, q):
+    paddle = _setup(rank, world, port)
+    from paddlepaddle_amd.distributed.utils import global_gather, global_scatter
+    # 2 experts per card; rank r sends local_count[j * 2 + e] rows to expert e of card j
+    local = {0: [1, 2, 0, 1], 1: [2, 0, 1, 1]}
+    lc = local[rank]
+    # global_count[j * 2 + e] = rows card j sends to my expert e
+    gc = [local[j][rank * 2 + e] for j in range(world) for e in range(2)]
+    rows = sum(lc)
+    x = paddle.to_tensor(np.arange(rows, dtype="float32").reshape(rows, 1) + 100 * rank)
+    y = global_scatter(x, paddle.to_tensor(lc, dtype="int64"), paddle.to_tensor(gc, dtype="int64"))
+    # expected: expert-major, then source card
+    exp = []
+    for e in range(2):
+        for j in range(world):
+            off = sum(local[j][:rank * 2 + e])
+            exp += [100 * j + off + k for k in range(local[j][rank * 2 + e])]
+    np.testing.assert_array_equal(y.numpy().ravel(), np.array(exp, "float32"))
+    z = global_gather(y, paddle.to_tensor(lc, dtype="int64"), paddle.to_tensor(gc, dtype="int64"))
+    np.testing.assert_array_equal(z.numpy(), x.numpy())
+    q.put((rank, True))
+
+
+def test_moe_global_scatter_gather_two_ranks():
+    _spawn(_moe_exchange_worker)
