@@ -203,14 +203,16 @@ class HistQuantizer(BaseHistQuantizer):
 
 def _kl_threshold(hist, bin_width, bits):
     """Threshold minimising KL(P || Q): P = the histogram clipped at bin i (outliers folded into the last bin),
-    Q = P quantised to 2^(bits-1) levels and expanded back over the non-zero bins of each level."""
-    levels = 2 ** (bits - 1)
+    Q = the clipped histogram quantised to 2^(bits-1) - 1 levels and expanded back over the non-zero bins of
+    each level; candidates i run from half the histogram range to its end."""
+    levels = 2 ** (bits - 1) - 1
     n = hist.shape[0]
     if n <= levels:
         return n * bin_width
     best, best_i = float("inf"), n
     total = hist.sum()
-    for i in range(levels, n + 1):
+    # like the reference search (static/quantization/cal_kl_threshold.py), candidates start at half the range
+    for i in range(max(levels, (n - 1) // 2), n + 1):
         p = hist[:i].astype(np.float64).copy()
         p[i - 1] += hist[i:].sum()
         nz = p > 0
@@ -220,7 +222,7 @@ def _kl_threshold(hist, bin_width, bits):
         for k in range(levels):
             a, b = int(math.floor(edges[k])), max(int(math.floor(edges[k + 1])), int(math.floor(edges[k])) + 1)
             b = min(b, i)
-            seg = hist[a:b] if k < levels - 1 else p[a:b]
+            seg = hist[a:b]  # the candidate quantisation sees the clipped range only (no outlier mass)
             cnt = np.count_nonzero(seg)
             if cnt:
                 q[a:b] = np.where(seg > 0, seg.sum() / cnt, 0.0)
