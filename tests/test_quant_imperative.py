@@ -65,7 +65,12 @@ def test_hist_and_kl_thresholds():
         q.sample_data(None, (torch.from_numpy(data[10000:] * 1.5),))   # second batch has a larger range
         q.cal_thresholds()
     assert 2.0 < h.thresholds[0] < 10.0, h.thresholds
-    assert 1.0 < k.thresholds[0] < 20.0, k.thresholds
+    # the KL search runs over the upper half of the range (reference cal_kl_threshold starting_iter)
+    assert 20.0 <= k.thresholds[0] <= 40.1, k.thresholds
+    g = Q.KLQuantizer()
+    g.sample_data(None, (torch.from_numpy(np.random.RandomState(1).randn(50000).astype("float32")),))
+    g.cal_thresholds()
+    assert 0.5 * g.abs_max_vals[0] <= g.thresholds[0] < g.abs_max_vals[0], (g.thresholds, g.abs_max_vals)
     a = Q.AbsmaxQuantizer()
     a.sample_data(None, (torch.from_numpy(data),))
     a.cal_thresholds()
