@@ -455,7 +455,7 @@ def _skinny_wgrad(x, dy, w):
         if w.is_contiguous(memory_format=torch.channels_last) and not w.is_contiguous() else dw.contiguous()
 
 
-def _pick(key, own, mi, skinny=None, mm=None):
+def _pick(key, own, mi, skinny=None, mm=None, extra=None):
     """'hip' | 'skinny' | 'mm' | 'blas' for one direction (ops/gemm.py choose(): timed once, persisted). 'skinny'
     is the memory-bound kernel, offered when the shape fits it; 'mm' a 1x1 product as a hipBLASLt GEMM. Timed
     with cold caches: in a training step every activation streams from HBM, while a repeated call would find a
@@ -467,6 +467,7 @@ def _pick(key, own, mi, skinny=None, mm=None):
         cands["skinny"] = skinny
     if mm is not None:
         cands["mm"] = mm
+    cands.update(extra or {})
     return G.choose(key, cands, cold=True)
 
 
@@ -512,9 +513,12 @@ class _ConvNHWC(torch.autograd.Function):
                 sk = lambda: _own_fwd_stats(x, w, b, stride, pad, dil, skinny=True)  # noqa: E731
             elif _skinny_ok(x, w, stride, False, pad, dil):
                 sk = lambda: red(_own_fwd(x, w, b, stride, pad, dil, skinny=True))  # noqa: E731
+            # 'hipu': the hand-written kernel without the statistics epilogue (e.g. the ping-pong 256x256 GEMM
+            # of a large 1x1 convolution, which has no statistics variant) plus the BN's own statistics pass
             ch = _pick(("convf",) + key + (b is not None, "bn"), lambda: _own_fwd_stats(x, w, b, stride, pad, dil),
                        lambda: red(_mi_fwd(x, w, b, stride, pad, dil)), sk,
-                       (lambda: red(_mm_fwd(x, w, b, stride))) if one else None)
+                       (lambda: red(_mm_fwd(x, w, b, stride))) if one else None,
+                       {"hipu": lambda: red(_own_fwd(x, w, b, stride, pad, dil))})
         else:
             sk = (lambda: _own_fwd(x, w, b, stride, pad, dil, skinny=True)) \
                 if _skinny_ok(x, w, stride, False, pad, dil) else None
@@ -525,6 +529,8 @@ class _ConvNHWC(torch.autograd.Function):
             y = _mi_fwd(x, w, b, stride, pad, dil)
         elif ch == "mm":
             y = _mm_fwd(x, w, b, stride)
+        elif ch == "hipu":
+            y = _own_fwd(x, w, b, stride, pad, dil)
         elif ch == "hip" and bn_stats:
             y, _CB._PENDING[0] = _own_fwd_stats(x, w, b, stride, pad, dil)
         elif ch == "skinny" and bn_stats and sk_stats:
