@@ -234,6 +234,9 @@ class BuildStrategy:
         self.memory_optimize = True
         self.fuse_all_reduce_ops = True
         self.enable_addto = False
+        # reference base/executor.py:993: the new executor captures the program into a CUDA graph; here the
+        # whole run (forward, backward, optimizer update) is captured into a hipGraph and replayed (_GraphRun)
+        self.allow_cuda_graph_capture = False
         self.build_cuda_graph = False
 
 
@@ -252,11 +255,31 @@ class CompiledProgram:
         return self
 
 
+class _GraphRun:
+    """One captured Executor.run of a fixed-shape program: static feed buffers, the hipGraph of plan replay +
+    backward + optimizer step, and the fetch tensors it writes. Captured on the third run with these shapes
+    (the first runs pick kernels, grow the allocator and create optimizer state eagerly); a run is
+    replayed after copying the new feed values into the static buffers."""
+
+    WARMUP = 2
+
+    def __init__(self):
+        self.runs = 0
+        self.graph = None
+        self.feeds = None
+        self.fetch = None
+        self.failed = None
+
+
+_GRAPH_STATS = {"captured": 0, "replayed": 0}
+
+
 class Executor:
     """Replays a Program: feeds -> native-scheduled op list -> fetches (+ backward/optimizer)."""
 
     def __init__(self, place=None):
         self.place = place
+        self._graphs = {}
 
     def _device(self, prog):
         for p in prog.all_parameters():
@@ -273,7 +296,10 @@ class Executor:
     def run(self, program=None, feed=None, fetch_list=None, feed_var_name="feed", fetch_var_name="fetch",
             scope=None, return_numpy=True, use_program_cache=False, use_prune=False):
         prog = program if program is not None else _main
+        use_graph = False
         if isinstance(prog, CompiledProgram):
+            bs = prog._build_strategy
+            use_graph = bool(getattr(bs, "allow_cuda_graph_capture", False) or getattr(bs, "build_cuda_graph", False))
             prog = prog._program
         from ..framework.program_desc import ProgramDescRunner
         from ..framework.pir_json import PirRunner
@@ -294,6 +320,10 @@ class Executor:
             plan = P.build_plan(prog, fetch, keep)
             prog._plans[key] = plan
         dev = self._device(prog)
+        if use_graph and dev.type == "cuda" and self._graph_ok(prog):
+            outs = self._run_graph(prog, plan, fetch, feed or {}, dev, key)
+            if outs is not None:
+                return [(_wrap(t).numpy() if return_numpy else _wrap(t.clone())) for t in outs]
         env = self._feed(prog, feed or {}, dev)
         grad_on = opt is not None or any(prog.nodes[i].kind == "grad" for i in plan.order)
         from .. import amp as _amp
@@ -321,6 +351,67 @@ class Executor:
             t = t.detach() if isinstance(t, torch.Tensor) else t
             outs.append(_wrap(t).numpy() if return_numpy else _wrap(t))
         return outs
+
+    # ------------------------------------------------------------------ hipGraph execution
+    @staticmethod
+    def _graph_ok(prog):
+        """Programs whose run is one fixed launch sequence: no guard nodes (data-dependent Python decisions),
+        no dynamic dims, no gradient merge (host-side step counting)."""
+        if prog._dyn or getattr(prog, "_grad_merge", None) is not None:
+            return False
+        return not any(isinstance(n, P.GuardNode) for n in prog.nodes)
+
+    def _step(self, prog, plan, env, dev):
+        opt = prog._optimize
+        grad_on = opt is not None or any(prog.nodes[i].kind == "grad" for i in plan.order)
+        with torch.set_grad_enabled(grad_on):
+            P.run_plan(prog, plan, env, dev)
+        if opt is not None:
+            optimizer, ls = opt
+            optimizer.clear_grad(set_to_zero=False)
+            env[ls].backward()
+            optimizer.step()
+
+    def _run_graph(self, prog, plan, fetch, feed, dev, key):
+        sig = tuple(sorted((k, tuple(v.shape) if isinstance(v, (Tensor, torch.Tensor)) else np.shape(v))
+                           for k, v in feed.items()))
+        gkey = (id(prog), key, sig)
+        st = self._graphs.get(gkey)
+        if st is None:
+            st = self._graphs[gkey] = _GraphRun()
+        if st.failed:
+            return None
+        env = self._feed(prog, feed, dev)
+        if st.graph is None:
+            st.runs += 1
+            if st.runs <= _GraphRun.WARMUP:
+                return None  # eager warm-up runs (the caller continues with this env's feeds)
+            from ..device.cuda.graphs import CUDAGraph
+            st.feeds = {s: (t.detach().clone().requires_grad_(t.requires_grad) if t.is_floating_point() else
+                            t.clone()) for s, t in env.items()}
+            cap_env = dict(st.feeds)
+            torch.cuda.synchronize(dev)
+            g = CUDAGraph()
+            try:
+                g.capture_begin()
+                try:
+                    self._step(prog, plan, cap_env, dev)
+                finally:
+                    g.capture_end()
+            except Exception as e:  # noqa: BLE001 - a host sync / allocation inside the program: run eagerly
+                st.failed = repr(e)
+                g.reset()
+                return None
+            st.graph = g
+            st.fetch = [cap_env[s] for s in fetch]
+            _GRAPH_STATS["captured"] += 1
+        else:
+            for s, t in env.items():
+                st.feeds[s].data.copy_(t, non_blocking=True) if st.feeds[s].requires_grad else \
+                    st.feeds[s].copy_(t, non_blocking=True)
+        st.graph.replay()
+        _GRAPH_STATS["replayed"] += 1
+        return [t.detach() if isinstance(t, torch.Tensor) else t for t in st.fetch]
 
     @staticmethod
     def _sym_n(prog, feed):

@@ -1,0 +1,68 @@
+"""Static Executor with BuildStrategy.allow_cuda_graph_capture (reference base/executor.py:993): after two eager
+warm-up runs the whole run — program replay, backward, optimizer update — is captured into one hipGraph and
+replayed; training must follow the eager run step for step."""
+import numpy as np
+import pytest
+
+import paddlepaddle_amd as paddle
+
+
+def _train(use_graph, steps=8):
+    paddle.enable_static()
+    try:
+        main, start = paddle.static.Program(), paddle.static.Program()
+        with paddle.static.program_guard(main, start):
+            paddle.seed(3)
+            x = paddle.static.data("x", [32, 16], "float32")
+            t = paddle.static.data("t", [32, 1], "float32")
+            h = paddle.nn.functional.gelu(paddle.nn.Linear(16, 64)(x))
+            y = paddle.nn.Linear(64, 1)(h)
+            loss = ((y - t) ** 2).mean()
+            paddle.optimizer.AdamW(learning_rate=0.01, weight_decay=0.01).minimize(loss)
+        exe = paddle.static.Executor(paddle.CUDAPlace(0))
+        prog = main
+        if use_graph:
+            bs = paddle.static.BuildStrategy()
+            bs.allow_cuda_graph_capture = True
+            prog = paddle.static.CompiledProgram(main, build_strategy=bs)
+        rng = np.random.RandomState(0)
+        losses = []
+        for _ in range(steps):
+            xs = rng.rand(32, 16).astype("float32")
+            ts = xs.sum(1, keepdims=True).astype("float32") * 0.1
+            losses.append(float(exe.run(prog, feed={"x": xs, "t": ts}, fetch_list=[loss])[0]))
+        return losses
+    finally:
+        paddle.disable_static()
+
+
+@pytest.mark.gpu
+def test_captured_static_training_matches_eager():
+    from paddlepaddle_amd.static import executor as E
+    paddle.set_device("gpu:0")
+    eager = _train(False)
+    before = dict(E._GRAPH_STATS)
+    graph = _train(True)
+    assert E._GRAPH_STATS["captured"] == before["captured"] + 1
+    assert E._GRAPH_STATS["replayed"] >= before["replayed"] + 6
+    np.testing.assert_allclose(graph, eager, rtol=2e-4, atol=1e-6)
+    assert graph[-1] < graph[0]
+
+
+def test_cpu_program_with_capture_flag_runs_eagerly():
+    """CPU place: the flag is accepted and the program runs eagerly (no hipGraph on the host)."""
+    paddle.set_device("cpu")
+    paddle.enable_static()
+    try:
+        main, start = paddle.static.Program(), paddle.static.Program()
+        with paddle.static.program_guard(main, start):
+            x = paddle.static.data("x", [4, 2], "float32")
+            y = paddle.nn.Linear(2, 1)(x)
+        bs = paddle.static.BuildStrategy()
+        bs.allow_cuda_graph_capture = True
+        exe = paddle.static.Executor(paddle.CPUPlace())
+        out = exe.run(paddle.static.CompiledProgram(main, build_strategy=bs), feed={"x": np.ones((4, 2), "float32")},
+                      fetch_list=[y])
+        assert out[0].shape == (4, 1)
+    finally:
+        paddle.disable_static()
