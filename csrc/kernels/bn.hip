@@ -589,6 +589,34 @@ PA_EXPORT int pa_bn_fwd_nhwc_pre(const void* x, const void* res, void* y, const 
   return 0;
 }
 
+// Backward from precomputed partials ([sum dyp, sum dyp * (x - mean)] written by the producing data-gradient
+// convolution, gemm.hip kEpiStatsBwd) for the relu-without-residual form (mask from x * ss[0] + ss[1]):
+// fold -> finalize (dweight / dbias / dx coefficients) -> apply.
+PA_EXPORT int pa_bn_bwd_nhwc_pre(const void* dy, const void* x, void* dx, const float* w, const float* mean,
+                                 const float* rstd, float* dw, float* db, const float* stats, int chunks, float* ws,
+                                 float* coef, int64_t R, int C, int global_stats, const float* ss, hipStream_t st) {
+  if (C % 8 != 0 || R < 1 || chunks < 1 || !stats || !ss) return 3;
+  const float* part = stats;
+  int nch = chunks;
+  if (chunks > kFoldPer) {
+    if (!ws) return 3;
+    const int groups = (chunks + kFoldPer - 1) / kFoldPer;
+    hipLaunchKernelGGL(bn_fold_range_k, dim3((C + 63) / 64, groups), dim3(1024), 0, st, stats, chunks, C, kFoldPer,
+                       ws);
+    PA_CHECK_LAUNCH();
+    part = ws;
+    nch = groups;
+  }
+  hipLaunchKernelGGL(bn_bwd_finalize_k, dim3((C + 63) / 64), dim3(1024), 0, st, part, nch, C, R, w, mean, rstd, dw, db,
+                     coef, global_stats);
+  PA_CHECK_LAUNCH();
+  const int64_t nvec = R * C / 8;
+  hipLaunchKernelGGL((bn_bwd_apply_k<true, false, true>), dim3(apply_grid(nvec)), dim3(kThreads), 0, st,
+                     (const uint16_t*)dy, (const uint16_t*)x, nullptr, coef, (uint16_t*)dx, nullptr, nvec, C, ss);
+  PA_CHECK_LAUNCH();
+  return 0;
+}
+
 // ---- split-phase entry points (cross-rank SyncBatchNorm: the per-channel sums are all-reduced between
 // the reduction and the apply; reference: sync_batch_norm_utils.h:575 all-reduces the backward stats)
 

@@ -57,6 +57,8 @@ enum EpiFlags : int {
   kEpiAccum = 8,      // C += result (read-modify-write)
   kEpiOutF32 = 16,    // C is fp32
   kEpiStats = 32,     // per-column batch-norm partials of the stored C (sum, sum of squares) to stats
+  kEpiStatsBwd = 64,  // with kEpiStats: BN-backward partials instead (C is the BN's output gradient):
+                      // sum dyp, sum dyp * (x - mean), dyp = relu mask (x * scale + shift > 0) of the stored C
 };
 
 struct GemmArgs {
@@ -83,6 +85,10 @@ struct GemmArgs {
   // kEpiStats: stats[2][chunks][N] fp32, chunk = m-tile * (waves along M) + wave row; each (chunk, column) is
   // written by exactly one lane (no atomics, deterministic), folded by bn.hip (pa_bn_fwd_nhwc_pre)
   float* stats;
+  // kEpiStatsBwd: the BN's input x ([M][ldc] bf16), its forward scale / shift ss [2][N] and batch mean [N]
+  const uint16_t* bn_x;
+  const float* bn_ss;
+  const float* bn_mean;
 };
 
 // split-K view: slice blockIdx.y of K (p.K elements each) and its own fp32 output slab
@@ -115,6 +121,31 @@ __device__ __forceinline__ void stats_store(const GemmArgs& p, int chunk, int ch
     *reinterpret_cast<float4*>(p.stats + (int64_t)chunk * p.N + n) = make_float4(s1[0], s1[1], s1[2], s1[3]);
     *reinterpret_cast<float4*>(p.stats + ((int64_t)chunks + chunk) * p.N + n) = make_float4(s2[0], s2[1], s2[2], s2[3]);
   }
+}
+
+// BN-backward partials of 4 stored gradient values (packed pair o.x, o.y) against the BN input at the same
+// element (conv dgrad -> relu' -> BN backward, reference fusion/gpu/fused_dconv_drelu_dbn_kernel.cu)
+__device__ __forceinline__ void stats_add_bwd(const GemmArgs& p, int64_t off, uint2 o, const float* sc,
+                                              const float* sh, const float* mu, float* s1, float* s2) {
+  const uint2 xr = *reinterpret_cast<const uint2*>(p.bn_x + off);
+  const float g[4] = {lo_bf16(o.x), hi_bf16(o.x), lo_bf16(o.y), hi_bf16(o.y)};
+  const float x[4] = {lo_bf16(xr.x), hi_bf16(xr.x), lo_bf16(xr.y), hi_bf16(xr.y)};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float d = x[e] * sc[e] + sh[e] > 0.f ? g[e] : 0.f;
+    s1[e] += d;
+    s2[e] += d * (x[e] - mu[e]);
+  }
+}
+
+// per-column BN constants of the backward statistics for columns n..n+3
+__device__ __forceinline__ void bn_cols(const GemmArgs& p, int n, float* sc, float* sh, float* mu) {
+  const float4 a = *reinterpret_cast<const float4*>(p.bn_ss + n);
+  const float4 b = *reinterpret_cast<const float4*>(p.bn_ss + p.N + n);
+  const float4 m = *reinterpret_cast<const float4*>(p.bn_mean + n);
+  sc[0] = a.x; sc[1] = a.y; sc[2] = a.z; sc[3] = a.w;
+  sh[0] = b.x; sh[1] = b.y; sh[2] = b.z; sh[3] = b.w;
+  mu[0] = m.x; mu[1] = m.y; mu[2] = m.z; mu[3] = m.w;
 }
 
 // stored bf16 pair -> the two rounded values accumulated into the statistics
@@ -353,6 +384,8 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmArgs p0) {
     const int n = ncol0 + j * 16;
     if (n >= p.N) continue;  // N % 4 == 0 is required by the launcher
     float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+    float bsc[4] = {0.f, 0.f, 0.f, 0.f}, bsh[4] = {0.f, 0.f, 0.f, 0.f}, bmu[4] = {0.f, 0.f, 0.f, 0.f};
+    if (flags & kEpiStatsBwd) bn_cols(p, n, bsc, bsh, bmu);
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
     if (flags & kEpiBias) {
       const uint2 braw = *reinterpret_cast<const uint2*>(p.bias + n);
@@ -388,7 +421,9 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmArgs p0) {
         }
         const uint2 o = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
         *cp = o;
-        if (flags & kEpiStats) {
+        if (flags & kEpiStatsBwd) {
+          stats_add_bwd(p, off, o, bsc, bsh, bmu, s1, s2);
+        } else if (flags & kEpiStats) {
           stats_add2(o.x, s1, s2, 0);
           stats_add2(o.y, s1, s2, 2);
         }
@@ -1205,6 +1240,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm3s_kernel(GemmArgs p0) {
     const int n = ncol0 + j * 16;
     if (n >= p.N) continue;
     float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+    float bsc[4] = {0.f, 0.f, 0.f, 0.f}, bsh[4] = {0.f, 0.f, 0.f, 0.f}, bmu[4] = {0.f, 0.f, 0.f, 0.f};
+    if (flags & kEpiStatsBwd) bn_cols(p, n, bsc, bsh, bmu);
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
     if (flags & kEpiBias) {
       const uint2 braw = *reinterpret_cast<const uint2*>(p.bias + n);
@@ -1239,7 +1276,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm3s_kernel(GemmArgs p0) {
         }
         const uint2 o = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
         *cp = o;
-        if (flags & kEpiStats) {
+        if (flags & kEpiStatsBwd) {
+          stats_add_bwd(p, off, o, bsc, bsh, bmu, s1, s2);
+        } else if (flags & kEpiStats) {
           stats_add2(o.x, s1, s2, 0);
           stats_add2(o.y, s1, s2, 2);
         }
@@ -1698,6 +1737,31 @@ PA_EXPORT int pa_gemm_bf16_stats(const void* a, const void* b, void* c, const vo
   return dispatch_layout<256>(g, a_kmajor, b_kmajor, 1, st);
 }
 
+// pa_gemm_bf16_stats in BN-backward form: C is the gradient of a relu'd BN's output (a 1x1 convolution's data
+// gradient); stats receives [sum dyp, sum dyp * (x - mean)] per column with x / ss / mean the BN's forward input,
+// scale-shift and batch mean (bn.hip pa_bn_bwd_nhwc_pre consumes them).
+PA_EXPORT int pa_gemm_bf16_bnbwd(const void* a, const void* b, void* c, int64_t M, int64_t N, int64_t K, int64_t lda,
+                                 int64_t ldb, int64_t ldc, int a_kmajor, int b_kmajor, int bn, const void* bn_x,
+                                 const float* bn_ss, const float* bn_mean, float* stats, hipStream_t st) {
+  if (K % kBK != 0 || N % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || ldc % 4 != 0 || !stats) return 1;
+  if (!bn_x || !bn_ss || !bn_mean) return 1;
+  if (!a_kmajor && M % 8 != 0) return 1;
+  if (bn != 160 && bn != 256 && bn != 128 && bn != 4) return 1;
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  GemmArgs g{};
+  g.a = (const uint16_t*)a; g.b = (const uint16_t*)b; g.c = c;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.flags = kEpiStats | kEpiStatsBwd; g.alpha = 1.f;
+  g.c_split = M * ldc;
+  g.stats = stats;
+  g.bn_x = (const uint16_t*)bn_x; g.bn_ss = bn_ss; g.bn_mean = bn_mean;
+  if (bn == 160) return dispatch_layout<160>(g, a_kmajor, b_kmajor, 1, st);
+  if (bn == 128) return dispatch_layout<128>(g, a_kmajor, b_kmajor, 1, st);
+  if (bn == 4) return dispatch_layout<4>(g, a_kmajor, b_kmajor, 1, st);
+  return dispatch_layout<256>(g, a_kmajor, b_kmajor, 1, st);
+}
+
 // Implicit-GEMM NHWC convolution forward: out[N*Ho*Wo, Cout] = im2col(x) . W^T (+ bias), with
 // x [N, H, W, C] bf16 (C % 64 == 0), w [Cout, KH, KW, C] bf16 (channels-last filter), out NHWC bf16.
 // Runs on the 3-stage 256x160 kernel; `zero` is a >= 128-byte zeroed device buffer for padding taps.
@@ -1728,6 +1792,26 @@ PA_EXPORT int pa_conv2d_nhwc_fwd_stats(const void* x, const void* w, const void*
   g.lda = C; g.ldb = (int64_t)KH * KW * C; g.ldc = Cout;
   g.flags = (bias ? kEpiBias : 0) | kEpiStats; g.alpha = 1.f;
   g.stats = stats;
+  g.zero = (const uint16_t*)zero;
+  g.cH = H; g.cW = W; g.cC = C; g.cHo = Ho; g.cWo = Wo; g.cKW = KW; g.cStride = stride; g.cPadH = pad_h;
+  g.cPadW = pad_w; g.cDil = dil;
+  return launch3s<true, true, true>(g, 1, st);
+}
+
+// pa_conv2d_nhwc_fwd in BN-backward form (the stride-1 data gradient of a KxK convolution, run as the convolution
+// of dY with the flipped filter): out is the gradient of a relu'd BN's output, stats as pa_gemm_bf16_bnbwd.
+PA_EXPORT int pa_conv2d_nhwc_fwd_bnbwd(const void* x, const void* w, void* out, const void* zero, int N, int H, int W,
+                                       int C, int Cout, int KH, int KW, int stride, int pad_h, int pad_w, int dil,
+                                       int Ho, int Wo, const void* bn_x, const float* bn_ss, const float* bn_mean,
+                                       float* stats, hipStream_t st) {
+  if (C % kBK != 0 || Cout % 8 != 0 || N <= 0 || !stats || !bn_x || !bn_ss || !bn_mean) return 1;
+  GemmArgs g{};
+  g.a = (const uint16_t*)x; g.b = (const uint16_t*)w; g.c = out;
+  g.M = N * Ho * Wo; g.N = Cout; g.K = KH * KW * C;
+  g.lda = C; g.ldb = (int64_t)KH * KW * C; g.ldc = Cout;
+  g.flags = kEpiStats | kEpiStatsBwd; g.alpha = 1.f;
+  g.stats = stats;
+  g.bn_x = (const uint16_t*)bn_x; g.bn_ss = bn_ss; g.bn_mean = bn_mean;
   g.zero = (const uint16_t*)zero;
   g.cH = H; g.cW = W; g.cC = C; g.cHo = Ho; g.cWo = Wo; g.cKW = KW; g.cStride = stride; g.cPadH = pad_h;
   g.cPadW = pad_w; g.cDil = dil;

@@ -85,6 +85,9 @@ SIGS = {
     "pa_conv2d_nhwc_fwd": [_vp, _vp, _vp, _vp, _vp] + [_i32] * 13 + [_vp],
     "pa_conv2d_nhwc_fwd_stats": [_vp, _vp, _vp, _vp, _vp] + [_i32] * 13 + [_vp, _vp],
     "pa_gemm_stats_chunks": [_i64, _i32],
+    "pa_gemm_bf16_bnbwd": [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp,
+                           _vp],
+    "pa_conv2d_nhwc_fwd_bnbwd": [_vp, _vp, _vp, _vp] + [_i32] * 13 + [_vp, _vp, _vp, _vp, _vp],
     "pa_gemm_bf16_stats": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _vp,
                            _vp],
     "pa_conv2d_nhwc_wgrad": [_vp, _vp, _vp, _vp] + [_i32] * 15 + [_vp],
@@ -100,6 +103,7 @@ SIGS = {
     "pa_bn_bwd_nhwc_mask": [_vp] * 12 + [_i64, _i32, _i32, _vp],
     "pa_bn_bwd_apply_nhwc": [_vp] * 6 + [_i64, _i32, _i32, _vp, _vp],
     "pa_bn_pre_ws": [_i32, _i32],
+    "pa_bn_bwd_nhwc_pre": [_vp] * 9 + [_i32, _vp, _vp, _i64, _i32, _i32, _vp, _vp],
     "pa_bn_fwd_nhwc_pre": [_vp] * 10 + [_i32, _vp, _vp, _vp, _i64, _i32, _f32, _f32, _i32, _vp],
     # fused decode step
     "pa_add_rms_norm_fwd": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _f32, _i32, _vp],

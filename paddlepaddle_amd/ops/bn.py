@@ -97,6 +97,8 @@ class _BNActHIP(torch.autograd.Function):
                    int(training), L.stream_ptr())
         keep = mbits if mbits is not None else (y if relu and not mask_x else None)
         ctx.save_for_backward(x2, keep, weight, mean, rstd, ss if mask_x else None)
+        if mask_x and training:
+            _CB._PENDING_BN[0] = (x2, mean, ss)  # the consuming convolution may fuse this BN's backward reduction
         ctx.bitmask = mbits is not None
         ctx.flags = (bool(relu), bool(training), residual is not None, weight is not None, bias is not None)
         return y
@@ -121,9 +123,18 @@ class _BNActHIP(torch.autograd.Function):
                    L.ptr(mean), L.ptr(rstd), L.ptr(dw), L.ptr(db), L.ptr(partial), L.ptr(coef), R, C,
                    int(not training), L.stream_ptr())
         else:
-            L.call("pa_bn_bwd_nhwc", L.ptr(dy), L.ptr(x2), L.ptr(y), L.ptr(dx), L.ptr(dres), L.ptr(weight),
-                   L.ptr(mean), L.ptr(rstd), L.ptr(dw), L.ptr(db), L.ptr(partial), L.ptr(coef), R, C, int(relu),
-                   int(not training), L.ptr(ss), L.stream_ptr())
+            pre = _CB.take_bwd(dy, x2) if (ss is not None and training and dres is None) else None
+            if pre is not None:  # the data-gradient convolution wrote [sum dyp, sum dyp * (x - mean)]
+                stats, chunks = pre
+                nws = int(L.lib().pa_bn_pre_ws(chunks, C))
+                ws = torch.empty(nws, dtype=torch.float32, device=dev) if nws else None
+                L.call("pa_bn_bwd_nhwc_pre", L.ptr(dy), L.ptr(x2), L.ptr(dx), L.ptr(weight), L.ptr(mean), L.ptr(rstd),
+                       L.ptr(dw), L.ptr(db), L.ptr(stats), chunks, L.ptr(ws), L.ptr(coef), R, C, 0, L.ptr(ss),
+                       L.stream_ptr())
+            else:
+                L.call("pa_bn_bwd_nhwc", L.ptr(dy), L.ptr(x2), L.ptr(y), L.ptr(dx), L.ptr(dres), L.ptr(weight),
+                       L.ptr(mean), L.ptr(rstd), L.ptr(dw), L.ptr(db), L.ptr(partial), L.ptr(coef), R, C, int(relu),
+                       int(not training), L.ptr(ss), L.stream_ptr())
         if dw is not None and dw.dtype != weight.dtype:
             dw = dw.to(weight.dtype)
         if to_sink:  # the block's first conv adds it to its data gradient (ops/conv.py ResidualGradSink)
@@ -165,8 +176,12 @@ def batch_norm_act_nhwc(x, weight, bias, running_mean, running_var, training=Tru
         if sink is not None:
             r2 = r2.detach()  # its gradient travels through the sink, not autograd
         pre = _CB.take(x) if training else None
+        _CB._PENDING_BN[0] = None
         y = _BNActHIP.apply(x2, weight, bias, r2, running_mean, running_var, bool(training), float(momentum),
                             float(eps), act == "relu", sink, pre)
+        src, _CB._PENDING_BN[0] = _CB._PENDING_BN[0], None
+        if src is not None and torch.is_grad_enabled():
+            _CB.tag_bn_output(y, src)
         return y.view(x.shape)
     x2 = x.reshape(-1, C)
     r2 = residual.reshape(-1, C) if residual is not None else None

@@ -417,6 +417,46 @@ def _own_dgrad(x, w, dy, stride, pad, dil, acc=None, skinny=False):
     return _implicit_fwd(dy, wt, None, N, dy.shape[1], dy.shape[2], Cout, C, KH, KW, 1, KH - 1 - pad, 1)
 
 
+def _bnbwd_ok(x, w, stride, pad, dil):
+    """Data gradients with the BN-backward statistics epilogue: stride-1 1x1 (GEMM) and stride-1 KxK
+    (implicit GEMM of the flipped filter) on the hand-written kernels."""
+    if not (L.has("pa_gemm_bf16_bnbwd") and stride == 1 and _own_dgrad_ok(x, w, stride, pad, dil)):
+        return False
+    return x.shape[3] % 8 == 0 and w.shape[1] == x.shape[3]
+
+
+def _own_dgrad_bnbwd(x, w, dy, pad, src):
+    """dX of a stride-1 convolution whose input is a relu BN's output, with the BN-backward partials of dX
+    ([sum dyp, sum dyp * (x_bn - mean)]) written by the epilogue: (dX, (stats, chunks))."""
+    bx, mean, ss = src
+    N, H, W, C = x.shape
+    Cout, _, KH, KW = w.shape
+    if KH == 1 and KW == 1:
+        dy2 = dy.reshape(-1, Cout)
+        w2 = w.reshape(Cout, C)
+        M = dy2.shape[0]
+        lda, ak = G._layout(dy2, 0)
+        ldb, bk = G._layout(w2, 1)
+        bn = 160 if bk else (256 if G._pick_bn(M, C, bk) == 256 else 128)
+        chunks = int(L.lib().pa_gemm_stats_chunks(M, bn))
+        dx = torch.empty(N, H, W, C, dtype=dy.dtype, device=dy.device)
+        stats = torch.empty(2 * chunks * C, dtype=torch.float32, device=dy.device)
+        L.call("pa_gemm_bf16_bnbwd", L.ptr(dy2), L.ptr(w2), L.ptr(dx), M, C, Cout, lda, ldb, C, int(ak), int(bk), bn,
+               L.ptr(bx), L.ptr(ss), L.ptr(mean), L.ptr(stats), L.stream_ptr())
+        return dx, (stats, chunks)
+    wt = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()
+    Ho, Wo = dy.shape[1], dy.shape[2]
+    pd = KH - 1 - pad
+    Hx = (Ho + 2 * pd - (KH - 1) - 1) + 1
+    Wx = (Wo + 2 * pd - (KW - 1) - 1) + 1
+    dx = torch.empty(N, Hx, Wx, C, dtype=dy.dtype, device=dy.device)
+    chunks = int(L.lib().pa_gemm_stats_chunks(N * Hx * Wx, 160))
+    stats = torch.empty(2 * chunks * C, dtype=torch.float32, device=dy.device)
+    L.call("pa_conv2d_nhwc_fwd_bnbwd", L.ptr(dy), L.ptr(wt), L.ptr(dx), L.ptr(_zero_page(dy.device)), N, Ho, Wo, Cout,
+           C, KH, KW, 1, pd, pd, 1, Hx, Wx, L.ptr(bx), L.ptr(ss), L.ptr(mean), L.ptr(stats), L.stream_ptr())
+    return dx, (stats, chunks)
+
+
 def _own_wgrad_ok(x, w, dy):
     C, Cout = x.shape[3], w.shape[0]
     P = dy.shape[0] * dy.shape[1] * dy.shape[2]
@@ -498,7 +538,7 @@ def _mm_dgrad(x, w, dy, stride, acc=None):
 
 class _ConvNHWC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, stride, pad, dil, sink=None, produce=None, bn_stats=False):
+    def forward(ctx, x, w, b, stride, pad, dil, sink=None, produce=None, bn_stats=False, bn_src=None):
         key = (tuple(x.shape), tuple(w.shape), stride, pad, dil)
         one = w.shape[2] == 1 and w.shape[3] == 1
         _CB._PENDING[0] = None
@@ -541,6 +581,7 @@ class _ConvNHWC(torch.autograd.Function):
         ctx.cfg = (stride, pad, dil, b is not None, key)
         ctx.sink = sink
         ctx.produce = produce
+        ctx.bn_src = bn_src  # (x, mean, scale-shift) of the relu BN that produced x: fused backward statistics
         return y
 
     @staticmethod
@@ -554,7 +595,28 @@ class _ConvNHWC(torch.autograd.Function):
             if dres is None:
                 ctx.sink.consumed = True
         dx = dw = db = None
-        if ctx.needs_input_grad[0]:
+        src = ctx.bn_src if dres is None and ctx.needs_input_grad[0] else None
+        if src is not None and _bnbwd_ok(x, w, stride, pad, dil):
+            red = _CB.reduce_cost_bwd
+            sk = (lambda: red(_own_dgrad(x, w, dy, stride, pad, dil, skinny=True), src)) \
+                if _skinny_ok(x, w, stride, True, pad, dil) else None
+            one = w.shape[2] == 1 and w.shape[3] == 1
+            ch = _pick(("convd",) + key + ("bnbwd",), lambda: _own_dgrad_bnbwd(x, w, dy, pad, src),
+                       lambda: red(_mi_bwd(x, w, dy, stride, pad, dil, [True, False])[0], src), sk,
+                       (lambda: red(_mm_dgrad(x, w, dy, stride), src)) if one else None,
+                       {"hipu": lambda: red(_own_dgrad(x, w, dy, stride, pad, dil), src)})
+            if ch == "hip":
+                dx, (stats, chunks) = _own_dgrad_bnbwd(x, w, dy, pad, src)
+                _CB.put_bwd(dx, stats, chunks, src[0])
+            elif ch == "hipu":
+                dx = _own_dgrad(x, w, dy, stride, pad, dil)
+            elif ch == "skinny":
+                dx = _own_dgrad(x, w, dy, stride, pad, dil, skinny=True)
+            elif ch == "mm":
+                dx = _mm_dgrad(x, w, dy, stride)
+            else:
+                dx = _mi_bwd(x, w, dy, stride, pad, dil, [True, False])[0]
+        elif ctx.needs_input_grad[0]:
             ch = "blas"
             if _own_dgrad_ok(x, w, stride, pad, dil):
                 sk = (lambda: _own_dgrad(x, w, dy, stride, pad, dil, skinny=True)) \
@@ -598,7 +660,7 @@ class _ConvNHWC(torch.autograd.Function):
             dx = dx if dx.is_contiguous() else dx.contiguous()
             prod.dres = dx if prod.dres is None else prod.dres.add_(dx)
             dx = None  # the block's first conv adds it (residual_grad_producer)
-        return dx, dw, db, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None
 
 
 def conv2d_nhwc(x, w, b, stride, pad, dil, bn_stats=None):
@@ -614,7 +676,8 @@ def conv2d_nhwc(x, w, b, stride, pad, dil, bn_stats=None):
         produce = None
     key = (tuple(x.shape), tuple(w.shape), stride, pad, dil)
     want = _CB.wanted(key) if bn_stats is None else (bool(bn_stats) and torch.is_grad_enabled() and _CB.enabled())
-    y = _ConvNHWC.apply(x, w, b, stride, pad, dil, sink, produce, want)
+    src = _CB.bn_source(x) if torch.is_grad_enabled() else None
+    y = _ConvNHWC.apply(x, w, b, stride, pad, dil, sink, produce, want, src)
     pre, _CB._PENDING[0] = _CB._PENDING[0], None
     _CB.tag(y, key, pre)
     return y

@@ -137,3 +137,55 @@ def test_fused_block_matches_unfused():
         assert (dw - dwr).abs().max().item() <= 0.02 * dwr.abs().max().item() + 1e-3
     torch.testing.assert_close(rm, rm_ref, rtol=1e-3, atol=1e-4)
     torch.testing.assert_close(rv, rv_ref, rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("k,cin,cout,hw", [(1, 64, 128, 28), (3, 64, 64, 20), (1, 256, 64, 14)])
+def test_dgrad_epilogue_bn_backward_partials(k, cin, cout, hw):
+    g = torch.Generator(device="cuda").manual_seed(k + cin + hw)
+    n = 4
+    bx = torch.randn(n, hw, hw, cin, device="cuda", generator=g).bfloat16()      # BN input (= conv input shape)
+    mean = torch.randn(cin, device="cuda", generator=g) * 0.1
+    ss = torch.stack([torch.rand(cin, device="cuda", generator=g) + 0.5,
+                      torch.randn(cin, device="cuda", generator=g) * 0.2]).contiguous()
+    w = (torch.randn(cout, cin, k, k, device="cuda", generator=g) / (cin * k * k) ** 0.5).bfloat16()
+    x = torch.empty(n, hw, hw, cin, device="cuda", dtype=torch.bfloat16)     # only its shape is used
+    dy = torch.randn(n, hw, hw, cout, device="cuda", generator=g).bfloat16()
+    L.reset_calls()
+    dx, (stats, chunks) = C._own_dgrad_bnbwd(x, w, dy, k // 2, (bx.view(-1, cin), mean, ss))
+    torch.cuda.synchronize()
+    assert L.calls("pa_gemm_bf16_bnbwd") + L.calls("pa_conv2d_nhwc_fwd_bnbwd") == 1
+    ref = torch.nn.grad.conv2d_input((n, cin, hw, hw), w.float(), dy.float().permute(0, 3, 1, 2), 1, k // 2)
+    ref = ref.permute(0, 2, 3, 1)
+    assert (dx.float() - ref).abs().max().item() < 3e-2 * ref.abs().max().item()
+    xf = bx.float().reshape(-1, cin)
+    g2 = dx.float().reshape(-1, cin)
+    dyp = torch.where(xf * ss[0] + ss[1] > 0, g2, torch.zeros_like(g2)).double()
+    s1, s2 = _fold(stats, chunks, cin)
+    torch.testing.assert_close(s1, dyp.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(s2, (dyp * (xf.double() - mean.double())).sum(0), rtol=1e-4, atol=1e-2)
+
+
+def test_fused_block_forward_and_backward_paths_forced_hip(monkeypatch):
+    """With the hand-written kernels forced, both halves of the fusion run: conv epilogue -> BN forward
+    statistics, and dgrad epilogue -> BN backward reduction (bn1 feeds the second convolution)."""
+    import paddlepaddle_amd as paddle
+    from paddlepaddle_amd.framework import flags
+    paddle.set_device("gpu:0")
+    g = torch.Generator(device="cuda").manual_seed(6)
+    x0 = torch.randn(8, 28, 28, 64, device="cuda", generator=g).bfloat16()
+    params = [torch.randn(64, 64, 3, 3, device="cuda", generator=g) * 0.05,
+              torch.randn(64, 64, 1, 1, device="cuda", generator=g) * 0.1]
+    flags.set_flags({"FLAGS_gemm_backend": "hip"})
+    try:
+        ref, rm_ref, rv_ref = _block(False, x0, params)
+        L.reset_calls()
+        got, rm, rv = _block(True, x0, params)
+        assert L.calls("pa_bn_fwd_nhwc_pre") >= 2, dict(L.CALLS)
+        assert L.calls("pa_bn_bwd_nhwc_pre") >= 1, dict(L.CALLS)
+    finally:
+        flags.set_flags({"FLAGS_gemm_backend": "auto", "FLAGS_conv_bn_fusion": True})
+    for (y, dx, dw), (yr, dxr, dwr) in zip(got, ref):
+        assert (y - yr).abs().max().item() <= 0.02 * yr.abs().max().item() + 1e-3
+        assert (dx - dxr).abs().max().item() <= 0.03 * dxr.abs().max().item() + 1e-3
+        assert (dw - dwr).abs().max().item() <= 0.03 * dwr.abs().max().item() + 1e-3
+    torch.testing.assert_close(rm, rm_ref, rtol=1e-3, atol=1e-4)
