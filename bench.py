@@ -372,7 +372,7 @@ def resnet_bench(args, paddle, world, dist_on):
         names = {"convf": "forward", "convd": "data grad", "convw": "weight grad"}
         for kind, what in names.items():
             cv = {k: v for k, v in _G.choices().items() if k[0] == kind}
-            own = sum(v in ("hip", "hipu", "skinny") for v in cv.values())
+            own = sum(v in ("hip", "hipu", "hip128", "skinny") for v in cv.values())
             log(f"[resnet50] conv {what} backend per shape: {own} hand-written "
                 f"({sum(v == 'skinny' for v in cv.values())} on the memory-bound skinny kernel) / "
                 f"{sum(v == 'mm' for v in cv.values())} hipBLASLt / {sum(v == 'blas' for v in cv.values())} MIOpen")

@@ -339,15 +339,17 @@ def _skinny_stats_ok(x, w, stride, pad, dil):
     return L.has("pa_conv_skinny_stats") and stride == 1 and pad == 1 and dil == 1
 
 
-def _own_fwd_stats(x, w, b, stride, pad, dil, skinny=False):
+def _own_fwd_stats(x, w, b, stride, pad, dil, skinny=False, bn=None):
     """The hand-written forward that also writes the following BN's partials (conv -> BN fusion, ops/_conv_bn.py):
-    (y, (stats, chunks))."""
+    (y, (stats, chunks)). bn: GEMM tile width of a 1x1 convolution (160 / 128)."""
     N, H, W, C = x.shape
     Cout, _, KH, KW = w.shape
     if KH == 1 and KW == 1:
         xs = x[:, ::stride, ::stride, :].contiguous() if stride > 1 else x
-        mm = G.gemm_skinny_bn_stats if skinny else G.gemm_bn_stats
-        y2, stats, chunks = mm(xs.reshape(-1, C), w.reshape(Cout, C).t(), bias=b)
+        if skinny:
+            y2, stats, chunks = G.gemm_skinny_bn_stats(xs.reshape(-1, C), w.reshape(Cout, C).t(), bias=b)
+        else:
+            y2, stats, chunks = G.gemm_bn_stats(xs.reshape(-1, C), w.reshape(Cout, C).t(), bias=b, bn=bn)
         return y2.view(N, xs.shape[1], xs.shape[2], Cout), (stats, chunks)
     wk = w.permute(0, 2, 3, 1)
     if not wk.is_contiguous():
@@ -558,7 +560,9 @@ class _ConvNHWC(torch.autograd.Function):
             ch = _pick(("convf",) + key + (b is not None, "bn"), lambda: _own_fwd_stats(x, w, b, stride, pad, dil),
                        lambda: red(_mi_fwd(x, w, b, stride, pad, dil)), sk,
                        (lambda: red(_mm_fwd(x, w, b, stride))) if one else None,
-                       {"hipu": lambda: red(_own_fwd(x, w, b, stride, pad, dil))})
+                       dict({"hipu": lambda: red(_own_fwd(x, w, b, stride, pad, dil))},
+                            **({"hip128": lambda: _own_fwd_stats(x, w, b, stride, pad, dil, bn=128)}
+                               if one and w.shape[0] <= 128 else {})))
         else:
             sk = (lambda: _own_fwd(x, w, b, stride, pad, dil, skinny=True)) \
                 if _skinny_ok(x, w, stride, False, pad, dil) else None
@@ -571,6 +575,8 @@ class _ConvNHWC(torch.autograd.Function):
             y = _mm_fwd(x, w, b, stride)
         elif ch == "hipu":
             y = _own_fwd(x, w, b, stride, pad, dil)
+        elif ch == "hip128":
+            y, _CB._PENDING[0] = _own_fwd_stats(x, w, b, stride, pad, dil, bn=128)
         elif ch == "hip" and bn_stats:
             y, _CB._PENDING[0] = _own_fwd_stats(x, w, b, stride, pad, dil)
         elif ch == "skinny" and bn_stats and sk_stats:

@@ -88,14 +88,16 @@ def gemm(a, b, bias=None, gelu=False, aux=None, out=None, accumulate=False, alph
     return out
 
 
-def gemm_bn_stats(a, b, bias=None):
+def gemm_bn_stats(a, b, bias=None, bn=None):
     """C = a @ b (+ bias) in bf16 plus the batch-norm partials of C's columns, written by the GEMM epilogue
-    (kEpiStats): returns (C, stats [2 * chunks * N] fp32, chunks) for ops/bn.py (conv -> BN fusion)."""
+    (kEpiStats): returns (C, stats [2 * chunks * N] fp32, chunks) for ops/bn.py (conv -> BN fusion).
+    bn: tile width (160: three-stage kernel; 128 / 256: two-stage kernel), default by layout."""
     M, K = a.shape
     N = b.shape[1]
     lda, ak = _layout(a, 0)
     ldb, bk = _layout(b, 1)
-    bn = 160 if bk else (256 if _pick_bn(M, N, bk) == 256 else 128)
+    if bn is None:
+        bn = 160 if bk else (256 if _pick_bn(M, N, bk) == 256 else 128)
     chunks = int(L.lib().pa_gemm_stats_chunks(M, bn))
     out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
     stats = torch.empty(2 * chunks * N, dtype=torch.float32, device=a.device)
