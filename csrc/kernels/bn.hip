@@ -232,45 +232,101 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_k(const float* __restric
   coef[2 * C + c] = d0;
 }
 
+// The apply passes are grid-strided over 16-byte vectors (8 channels of one row). With the grid stride a multiple
+// of C / 8 — kThreads = 256 is, for every C / 8 that divides 256 (C <= 2048, power of two) — a thread keeps the
+// same 8 channels for its whole loop: the per-channel constants are loaded once into registers instead of with
+// every vector (they were half the memory instructions of the loop), and two vectors per trip keep two 16-byte
+// loads per stream in flight. Other C take the general loop.
+
 // y = act(x * scale + shift [+ res]); WMASK: also the relu mask, bit j of byte i = (y[8i + j] > 0)
+template <bool RELU, bool RES, bool WMASK>
+__device__ __forceinline__ void bn_apply_vec(const float* f, const float* r, const float* sc, const float* sh,
+                                             uint16_t* __restrict__ y, uint8_t* __restrict__ mbits, int64_t i) {
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float t = f[j] * sc[j] + sh[j];
+    if (RES) t += r[j];
+    if (RELU) t = fmaxf(t, 0.f);
+    v[j] = t;
+  }
+  uint4 o;
+  o.x = pack_bf16(v[0], v[1]); o.y = pack_bf16(v[2], v[3]); o.z = pack_bf16(v[4], v[5]); o.w = pack_bf16(v[6], v[7]);
+  *reinterpret_cast<uint4*>(y + i * 8) = o;
+  if (WMASK) {
+    // the mask of the stored (bf16-rounded) value, the same test the y-reading backward applies
+    const uint32_t ww[4] = {o.x, o.y, o.z, o.w};
+    uint32_t bits = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bits |= (lo_bf16(ww[j]) > 0.f ? 1u : 0u) << (2 * j);
+      bits |= (hi_bf16(ww[j]) > 0.f ? 1u : 0u) << (2 * j + 1);
+    }
+    mbits[i] = (uint8_t)bits;
+  }
+}
+
 template <bool RELU, bool RES, bool WMASK = false>
 __global__ __launch_bounds__(kThreads) void bn_apply_k(const uint16_t* __restrict__ x, const uint16_t* __restrict__ res,
                                                        const float* __restrict__ ss, uint16_t* __restrict__ y,
                                                        int64_t nvec, int C, uint8_t* __restrict__ mbits = nullptr) {
   const int cv = C >> 3;
-  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * kThreads) {
-    const int c0 = (int)(i % cv) * 8;
-    float f[8], r[8];
-    ld8(x + i * 8, f);
-    if (RES) ld8(res + i * 8, r);
-    const float4 s0 = *reinterpret_cast<const float4*>(ss + c0), s1 = *reinterpret_cast<const float4*>(ss + c0 + 4);
-    const float4 h0 = *reinterpret_cast<const float4*>(ss + C + c0), h1 = *reinterpret_cast<const float4*>(ss + C + c0 + 4);
-    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-    uint32_t bits = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v = f[j] * sc[j] + sh[j];
-      if (RES) v += r[j];
-      if (RELU) v = fmaxf(v, 0.f);
-      f[j] = v;
-    }
-    st8(y + i * 8, f);
-    if (WMASK) {
-      // the mask of the stored (bf16-rounded) value, the same test the y-reading backward applies
-      const uint4 w = *reinterpret_cast<const uint4*>(y + i * 8);
-      const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        bits |= (lo_bf16(ww[j]) > 0.f ? 1u : 0u) << (2 * j);
-        bits |= (hi_bf16(ww[j]) > 0.f ? 1u : 0u) << (2 * j + 1);
+  const int64_t T = (int64_t)gridDim.x * kThreads;
+  const int64_t i0 = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  float sc[8], sh[8], f0[8], f1[8], r0[8], r1[8];
+  if (T % cv == 0) {
+    const int c0 = (int)(i0 % cv) * 8;
+    load8<float>(ss + c0, sc);
+    load8<float>(ss + C + c0, sh);
+    for (int64_t i = i0; i < nvec; i += 2 * T) {
+      const bool two = i + T < nvec;
+      ld8(x + i * 8, f0);
+      if (two) ld8(x + (i + T) * 8, f1);
+      if (RES) {
+        ld8(res + i * 8, r0);
+        if (two) ld8(res + (i + T) * 8, r1);
       }
-      mbits[i] = (uint8_t)bits;
+      bn_apply_vec<RELU, RES, WMASK>(f0, r0, sc, sh, y, mbits, i);
+      if (two) bn_apply_vec<RELU, RES, WMASK>(f1, r1, sc, sh, y, mbits, i + T);
     }
+    return;
+  }
+  for (int64_t i = i0; i < nvec; i += T) {
+    const int c0 = (int)(i % cv) * 8;
+    ld8(x + i * 8, f0);
+    if (RES) ld8(res + i * 8, r0);
+    load8<float>(ss + c0, sc);
+    load8<float>(ss + C + c0, sh);
+    bn_apply_vec<RELU, RES, WMASK>(f0, r0, sc, sh, y, mbits, i);
   }
 }
 
 // dx = a * dyp - bc * x + d0; dres = dyp   (MASKX: relu mask from x * scale + shift, see bn_reduce_k)
+template <bool RELU, bool DRES, bool MASKX, bool MASKB>
+__device__ __forceinline__ void bn_bwd_vec(float* g, const float* f, const uint16_t* __restrict__ y,
+                                           const uint8_t* __restrict__ mbits, const float* sc, const float* sh,
+                                           const float* a, const float* bc, const float* d0,
+                                           uint16_t* __restrict__ dx, uint16_t* __restrict__ dres, int64_t i) {
+  if (RELU && MASKX) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = f[j] * sc[j] + sh[j] > 0.f ? g[j] : 0.f;
+  } else if (RELU && MASKB) {
+    const uint32_t mb = mbits[i];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = (mb >> j) & 1u ? g[j] : 0.f;
+  } else if (RELU) {
+    float yy[8];
+    ld8(y + i * 8, yy);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = yy[j] > 0.f ? g[j] : 0.f;
+  }
+  if (DRES) st8(dres + i * 8, g);
+  float o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = a[j] * g[j] - bc[j] * f[j] + d0[j];
+  st8(dx + i * 8, o);
+}
+
 template <bool RELU, bool DRES, bool MASKX = false, bool MASKB = false>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply_k(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
                                                            const uint16_t* __restrict__ y, const float* __restrict__ coef,
@@ -278,35 +334,45 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_k(const uint16_t* __res
                                                            int64_t nvec, int C, const float* __restrict__ ss = nullptr,
                                                            const uint8_t* __restrict__ mbits = nullptr) {
   const int cv = C >> 3;
-  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * kThreads) {
-    const int c0 = (int)(i % cv) * 8;
-    float g[8], f[8];
-    ld8(dy + i * 8, g);
-    ld8(x + i * 8, f);
+  const int64_t T = (int64_t)gridDim.x * kThreads;
+  const int64_t i0 = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  float sc[8], sh[8], a[8], bc[8], d0[8], g0[8], g1[8], f0[8], f1[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sc[j] = 0.f; sh[j] = 0.f; }
+  if (T % cv == 0) {
+    const int c0 = (int)(i0 % cv) * 8;
     if (RELU && MASKX) {
-      float sc[8], sh[8];
       load8<float>(ss + c0, sc);
       load8<float>(ss + C + c0, sh);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = f[j] * sc[j] + sh[j] > 0.f ? g[j] : 0.f;
-    } else if (RELU && MASKB) {
-      const uint32_t mb = mbits[i];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = (mb >> j) & 1u ? g[j] : 0.f;
-    } else if (RELU) {
-      float yy[8];
-      ld8(y + i * 8, yy);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = yy[j] > 0.f ? g[j] : 0.f;
     }
-    if (DRES) st8(dres + i * 8, g);
-    float a[8], bc[8], d0[8], o[8];
     load8<float>(coef + c0, a);
     load8<float>(coef + C + c0, bc);
     load8<float>(coef + 2 * C + c0, d0);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = a[j] * g[j] - bc[j] * f[j] + d0[j];
-    st8(dx + i * 8, o);
+    for (int64_t i = i0; i < nvec; i += 2 * T) {
+      const bool two = i + T < nvec;
+      ld8(dy + i * 8, g0);
+      ld8(x + i * 8, f0);
+      if (two) {
+        ld8(dy + (i + T) * 8, g1);
+        ld8(x + (i + T) * 8, f1);
+      }
+      bn_bwd_vec<RELU, DRES, MASKX, MASKB>(g0, f0, y, mbits, sc, sh, a, bc, d0, dx, dres, i);
+      if (two) bn_bwd_vec<RELU, DRES, MASKX, MASKB>(g1, f1, y, mbits, sc, sh, a, bc, d0, dx, dres, i + T);
+    }
+    return;
+  }
+  for (int64_t i = i0; i < nvec; i += T) {
+    const int c0 = (int)(i % cv) * 8;
+    ld8(dy + i * 8, g0);
+    ld8(x + i * 8, f0);
+    if (RELU && MASKX) {
+      load8<float>(ss + c0, sc);
+      load8<float>(ss + C + c0, sh);
+    }
+    load8<float>(coef + c0, a);
+    load8<float>(coef + C + c0, bc);
+    load8<float>(coef + 2 * C + c0, d0);
+    bn_bwd_vec<RELU, DRES, MASKX, MASKB>(g0, f0, y, mbits, sc, sh, a, bc, d0, dx, dres, i);
   }
 }
 
