@@ -1886,3 +1886,14 @@ PA_EXPORT int pa_gemm_small_m(const void* a, int64_t lda, const void* b, int64_t
                      (const uint16_t*)bias, (uint16_t*)c, ldc, M, N, splits);
   return (int)hipGetLastError();
 }
+
+// Sum of `splits` fp32 slabs [splits][M][N] (split-K partials) into bf16 C [M][ldc] in one pass (the weight
+// gradients of convolutions: replaces a separate reduction and cast). N % 4 == 0.
+PA_EXPORT int pa_slab_reduce_bf16(const float* ws, void* c, int64_t ldc, int64_t M, int64_t N, int splits,
+                                  hipStream_t st) {
+  if (N % 4 != 0 || ldc % 4 != 0 || splits < 1 || M <= 0) return 1;
+  const int64_t n4 = M * N / 4;
+  hipLaunchKernelGGL(gemm_small_m_reduce_k, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, ws, nullptr,
+                     (uint16_t*)c, ldc, (int)M, (int)N, splits);
+  return (int)hipGetLastError();
+}

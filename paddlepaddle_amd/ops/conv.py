@@ -205,7 +205,7 @@ def _implicit_wgrad(x, dy, w, N, H, W, C, Cout, KH, KW, stride, pad, dil, Ho, Wo
     ws = torch.empty(splits, M, Cout, dtype=torch.float32, device=x.device)
     L.call("pa_conv2d_nhwc_wgrad", L.ptr(x), L.ptr(dy), L.ptr(ws), L.ptr(_zero_page(x.device)), N, H, W, C, Cout, KH,
            KW, stride, pad, pad, dil, Ho, Wo, splits, bn, L.stream_ptr())
-    dwt = ws.sum(0) if splits > 1 else ws[0]
+    dwt = G.reduce_slabs(ws, w.dtype)
     return dwt.view(KH, KW, C, Cout).permute(3, 2, 0, 1).to(w.dtype).contiguous(memory_format=torch.channels_last) \
         if w.is_contiguous(memory_format=torch.channels_last) and not w.is_contiguous() else \
         dwt.view(KH, KW, C, Cout).permute(3, 2, 0, 1).to(w.dtype).contiguous()
@@ -492,7 +492,7 @@ def _skinny_wgrad(x, dy, w):
     ws = torch.empty(splits, 64 * 9 * 64, dtype=torch.float32, device=x.device)
     L.call("pa_conv_skinny_wgrad", L.ptr(x), L.ptr(dy), L.ptr(_zero_page(x.device)), L.ptr(ws), N, H, W, C, 64,
            splits, L.stream_ptr())
-    dw = ws.sum(0).view(64, 3, 3, 64).permute(0, 3, 1, 2).to(w.dtype)
+    dw = G.reduce_slabs(ws.view(splits, 1, -1), w.dtype).view(64, 3, 3, 64).permute(0, 3, 1, 2).to(w.dtype)
     return dw.contiguous(memory_format=torch.channels_last) \
         if w.is_contiguous(memory_format=torch.channels_last) and not w.is_contiguous() else dw.contiguous()
 

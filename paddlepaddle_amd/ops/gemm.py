@@ -118,6 +118,16 @@ def gemm_splitk(a, b, splits, out_dtype=torch.bfloat16, bn=None):
         bn = _pick_bn(M, N, bk)
     L.call("pa_gemm_bf16", L.ptr(a), L.ptr(b), L.ptr(ws), L.ptr(None), L.ptr(None), M, N, K, lda, ldb, N,
            int(ak), int(bk), EPI_OUT_F32, 1.0, int(bn), int(splits), L.stream_ptr())
+    return reduce_slabs(ws, out_dtype)
+
+
+def reduce_slabs(ws, out_dtype):
+    """[splits, M, N] fp32 split-K partials -> [M, N] out_dtype; bf16 in one HIP pass (sum + cast)."""
+    splits, M, N = ws.shape
+    if out_dtype == torch.bfloat16 and N % 4 == 0 and L.has("pa_slab_reduce_bf16"):
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=ws.device)
+        L.call("pa_slab_reduce_bf16", L.ptr(ws), L.ptr(out), N, M, N, int(splits), L.stream_ptr())
+        return out
     return ws.sum(0, dtype=torch.float32).to(out_dtype) if splits > 1 else ws[0].to(out_dtype)
 
 
