@@ -133,6 +133,17 @@ def _convnd(n, x, weight, bias, stride, padding, dilation, groups, data_format):
                                              lambda xx, ww: _from_cf(miopen(_to_cf(xx, data_format, n)[0], ww), cl, n))
             if y is not None:
                 return _wrap(y)
+    # NLC 1-D convolutions: the NHWC kernels on a 1 x L image with a 1 x K filter (padding (0, p)); each of the
+    # three products again on the faster of ours and MIOpen (the data gradient of a 1 x K filter: MIOpen)
+    if cl and n == 1 and pre is None and groups == 1 and t.is_cuda:
+        from ... import ops as _ops
+        pd = pad if isinstance(pad, int) else (pad[0] if len(pad) == 1 else None)
+        if pd is not None and _ops._loader.flag("FLAGS_conv_per_direction", True):
+            x4, w4 = x_raw.unsqueeze(1), w.unsqueeze(2)
+            one = w4.shape[3] == 1
+            if (not one or (pd == 0 and dilation[0] == 1)) and _ops.conv.eligible_nhwc(x4, w4, 1):
+                y = _ops.conv.conv2d_nhwc(x4, w4, b, stride[0], 0 if one else (0, pd), dilation[0])
+                return _wrap(y.squeeze(1))
     out = miopen(t, w)
     return _wrap(_from_cf(out, cl, n))
 

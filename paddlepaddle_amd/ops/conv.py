@@ -177,12 +177,18 @@ def _zero_page(dev):
     return z
 
 
+def _ph_pw(pad):
+    """(pad_h, pad_w) of an int or (h, w) padding (1-D convolutions run as 1 x K with padding (0, p))."""
+    return (pad, pad) if isinstance(pad, int) else (int(pad[0]), int(pad[1]))
+
+
 def _implicit_fwd(x, wk, b, N, H, W, C, Cout, KH, KW, stride, pad, dil):
-    Ho = (H + 2 * pad - dil * (KH - 1) - 1) // stride + 1
-    Wo = (W + 2 * pad - dil * (KW - 1) - 1) // stride + 1
+    ph, pw = _ph_pw(pad)
+    Ho = (H + 2 * ph - dil * (KH - 1) - 1) // stride + 1
+    Wo = (W + 2 * pw - dil * (KW - 1) - 1) // stride + 1
     out = torch.empty(N, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
     L.call("pa_conv2d_nhwc_fwd", L.ptr(x), L.ptr(wk), L.ptr(b), L.ptr(out), L.ptr(_zero_page(x.device)), N, H, W,
-           C, Cout, KH, KW, stride, pad, pad, dil, Ho, Wo, L.stream_ptr())
+           C, Cout, KH, KW, stride, ph, pw, dil, Ho, Wo, L.stream_ptr())
     return out
 
 
@@ -203,8 +209,9 @@ def _implicit_wgrad(x, dy, w, N, H, W, C, Cout, KH, KW, stride, pad, dil, Ho, Wo
     bn = 256 if Cout % 256 == 0 else (64 if Cout <= 64 else 128)
     splits = _wgrad_splits(N * Ho * Wo, M, Cout, bn)
     ws = torch.empty(splits, M, Cout, dtype=torch.float32, device=x.device)
+    ph, pw = _ph_pw(pad)
     L.call("pa_conv2d_nhwc_wgrad", L.ptr(x), L.ptr(dy), L.ptr(ws), L.ptr(_zero_page(x.device)), N, H, W, C, Cout, KH,
-           KW, stride, pad, pad, dil, Ho, Wo, splits, bn, L.stream_ptr())
+           KW, stride, ph, pw, dil, Ho, Wo, splits, bn, L.stream_ptr())
     dwt = G.reduce_slabs(ws, w.dtype)
     return dwt.view(KH, KW, C, Cout).permute(3, 2, 0, 1).to(w.dtype).contiguous(memory_format=torch.channels_last) \
         if w.is_contiguous(memory_format=torch.channels_last) and not w.is_contiguous() else \
@@ -295,8 +302,9 @@ def _mi_fwd(x, w, b, stride, pad, dil):
 
 
 def _mi_bwd(x, w, dy, stride, pad, dil, mask):
+    pad = _ph_pw(pad)
     gi, gw, _ = torch.ops.aten.convolution_backward(dy.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2), _mi_weight(w),
-                                                    None, [stride] * 2, [pad] * 2, [dil] * 2, False, [0, 0], 1,
+                                                    None, [stride] * 2, list(pad), [dil] * 2, False, [0, 0], 1,
                                                     mask + [False])
     if gi is not None:
         gi = gi.permute(0, 2, 3, 1)
@@ -318,6 +326,8 @@ def _skinny_conv(x, wk, b, N, H, W, C, Cout, KH, KW, stride, pad):
 def _skinny_ok(x, w, stride, dgrad, pad=0, dil=1):
     """Products the memory-bound skinny kernels take: 1x1 (ops/gemm.py gemm_skinny: N, K in {32..256}, tall M)
     and KxK (pa_conv_skinny: C = Cout = 64, 3x3; the data gradient only at stride 1)."""
+    if not isinstance(pad, int):
+        return False
     C, Cout = x.shape[3], w.shape[0]
     if not (w.shape[2] == 1 and w.shape[3] == 1):
         if not L.has("pa_conv_skinny") or dil != 1 or (dgrad and stride != 1) or x.numel() * 2 >= (1 << 31) - (1 << 21):
@@ -361,13 +371,14 @@ def _own_fwd_stats(x, w, b, stride, pad, dil, skinny=False, bn=None):
         L.call("pa_conv_skinny_stats", L.ptr(x), L.ptr(wk), L.ptr(b), L.ptr(out), L.ptr(_zero_page(x.device)), N, H, W,
                L.ptr(stats), L.stream_ptr())
         return out, (stats, chunks)
-    Ho = (H + 2 * pad - dil * (KH - 1) - 1) // stride + 1
-    Wo = (W + 2 * pad - dil * (KW - 1) - 1) // stride + 1
+    ph, pw = _ph_pw(pad)
+    Ho = (H + 2 * ph - dil * (KH - 1) - 1) // stride + 1
+    Wo = (W + 2 * pw - dil * (KW - 1) - 1) // stride + 1
     out = torch.empty(N, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
     chunks = int(L.lib().pa_gemm_stats_chunks(N * Ho * Wo, 160))
     stats = torch.empty(2 * chunks * Cout, dtype=torch.float32, device=x.device)
     L.call("pa_conv2d_nhwc_fwd_stats", L.ptr(x), L.ptr(wk), L.ptr(b), L.ptr(out), L.ptr(_zero_page(x.device)), N, H,
-           W, C, Cout, KH, KW, stride, pad, pad, dil, Ho, Wo, L.ptr(stats), L.stream_ptr())
+           W, C, Cout, KH, KW, stride, ph, pw, dil, Ho, Wo, L.ptr(stats), L.stream_ptr())
     return out, (stats, chunks)
 
 
@@ -391,6 +402,8 @@ def _own_fwd(x, w, b, stride, pad, dil, skinny=False):
 
 def _own_dgrad_ok(x, w, stride, pad, dil):
     C, (Cout, _, KH, KW) = x.shape[3], w.shape
+    if not isinstance(pad, int):
+        return False  # asymmetric (1-D) padding: MIOpen
     if KH == 1 and KW == 1:
         return True
     return stride == 1 and dil == 1 and Cout % 64 == 0 and C % 8 == 0 and 2 * pad <= KH - 1 + pad and KH == KW
@@ -670,6 +683,8 @@ class _ConvNHWC(torch.autograd.Function):
 
 
 def conv2d_nhwc(x, w, b, stride, pad, dil, bn_stats=None):
+    if not isinstance(pad, int):
+        pad = int(pad[0]) if pad[0] == pad[1] else (int(pad[0]), int(pad[1]))
     """NHWC 2-D convolution (groups 1, symmetric padding) with each of its three products on the hand-written
     kernel or MIOpen, whichever measured faster for the shape. A stride-1 1x1 convolution inside
     ``residual_grad_sink()`` takes over the block's residual gradient (ResidualGradSink). ``bn_stats``: True when
