@@ -77,6 +77,8 @@ struct GemmArgs {
   // p = (n, ho, wo), k = (kh * KW + kw) * C + c; out-of-image taps read the 128-byte zero page
   const uint16_t* zero;
   int cH, cW, cC, cHo, cWo, cKW, cStride, cPadH, cPadW, cDil;
+  // 3-D (NDHWC) forward: depth, output depth, taps per depth slice (KH * KW) and depth padding; 2-D: 1, 1, KH*KW, 0
+  int cD, cDo, cKHW, cPadD;
   // balanced tail (ping-pong kernel): tiles [full_tiles, tiles) are split over K into tail_split slices
   // (workgroups full_tiles + u, u = local tile * tail_split + slice) that write fp32 256x256 partials to
   // tail_ws; gemm_tail_reduce_k sums them and applies the epilogue. tail_split == 0: no tail.
@@ -1117,8 +1119,8 @@ __device__ __forceinline__ bf16x8_t frag_r(const char* img, int rbase, int s, in
 
 // Per-thread precomputed output pixels of the 4 A rows this thread stages (implicit-GEMM conv).
 struct ConvRows {
-  int pix[4];  // n * H * W (first pixel of the image), or -1 for rows past M
-  int hb[4], wb[4];
+  int pix[4];  // n * D * H * W (first pixel of the image), or -1 for rows past M
+  int db[4], hb[4], wb[4];
 };
 
 __device__ __forceinline__ ConvRows conv_rows(const GemmArgs& p, int m0, int wave, int lane) {
@@ -1128,14 +1130,16 @@ __device__ __forceinline__ ConvRows conv_rows(const GemmArgs& p, int m0, int wav
     const int row = (i * 8 + wave) * 8 + (lane >> 3);
     const int m = m0 + row;
     if (m < p.M) {
-      const int hw = p.cHo * p.cWo;
-      const int n = m / hw, rem = m - n * hw;
+      const int hw = p.cHo * p.cWo, dhw = p.cDo * hw;
+      const int n = m / dhw, r1 = m - n * dhw;
+      const int dd = r1 / hw, rem = r1 - dd * hw;
       const int ho = rem / p.cWo, wo = rem - ho * p.cWo;
-      r.pix[i] = n * p.cH * p.cW;
+      r.pix[i] = n * p.cD * p.cH * p.cW;
+      r.db[i] = dd * p.cStride - p.cPadD;
       r.hb[i] = ho * p.cStride - p.cPadH;
       r.wb[i] = wo * p.cStride - p.cPadW;
     } else {
-      r.pix[i] = -1; r.hb[i] = 0; r.wb[i] = 0;
+      r.pix[i] = -1; r.db[i] = 0; r.hb[i] = 0; r.wb[i] = 0;
     }
   }
   return r;
@@ -1145,15 +1149,17 @@ __device__ __forceinline__ ConvRows conv_rows(const GemmArgs& p, int m0, int wav
 __device__ __forceinline__ void stage_conv(const GemmArgs& p, const ConvRows& cr, int k0, char* img, int wave,
                                            int lane) {
   const int tap = k0 / p.cC, c0 = k0 - tap * p.cC;
-  const int kh = tap / p.cKW, kw = tap - kh * p.cKW;
+  const int kd = tap / p.cKHW, t2 = tap - kd * p.cKHW;
+  const int kh = t2 / p.cKW, kw = t2 - kh * p.cKW;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int q = i * 8 + wave;
     const int row = q * 8 + (lane >> 3);
     const int lc = (lane & 7) ^ ((row >> 1) & 7);
-    const int hi = cr.hb[i] + kh * p.cDil, wi = cr.wb[i] + kw * p.cDil;
-    const bool ok = cr.pix[i] >= 0 && hi >= 0 && hi < p.cH && wi >= 0 && wi < p.cW;
-    const uint16_t* src = ok ? p.a + ((int64_t)(cr.pix[i] + hi * p.cW + wi) * p.cC + c0 + lc * 8) : p.zero + lc * 8;
+    const int di = cr.db[i] + kd * p.cDil, hi = cr.hb[i] + kh * p.cDil, wi = cr.wb[i] + kw * p.cDil;
+    const bool ok = cr.pix[i] >= 0 && di >= 0 && di < p.cD && hi >= 0 && hi < p.cH && wi >= 0 && wi < p.cW;
+    const uint16_t* src =
+        ok ? p.a + ((int64_t)(cr.pix[i] + (di * p.cH + hi) * p.cW + wi) * p.cC + c0 + lc * 8) : p.zero + lc * 8;
     glds16(src, img + q * 1024);
   }
 }
@@ -1709,6 +1715,25 @@ PA_EXPORT int pa_gemm_bf16(const void* a, const void* b, void* c, const void* bi
   return dispatch_layout<256>(g, a_kmajor, b_kmajor, splits, st);
 }
 
+// Implicit-GEMM NDHWC 3-D convolution forward: out[N*Do*Ho*Wo, Cout] = im2col3d(x) . W^T (+ bias), x [N, D, H, W, C]
+// bf16 (C % 64 == 0), w [Cout, KD, KH, KW, C] (channels-last filter); every 64-deep K tile is one (kd, kh, kw) tap.
+// Same 256x160 kernel as the 2-D forward (a 2-D convolution is the D = KD = 1 case).
+PA_EXPORT int pa_conv3d_ndhwc_fwd(const void* x, const void* w, const void* bias, void* out, const void* zero, int N,
+                                  int D, int H, int W, int C, int Cout, int KD, int KH, int KW, int stride, int pad_d,
+                                  int pad_h, int pad_w, int dil, int Do, int Ho, int Wo, hipStream_t st) {
+  if (C % kBK != 0 || Cout % 8 != 0 || N <= 0) return 1;
+  GemmArgs g{};
+  g.a = (const uint16_t*)x; g.b = (const uint16_t*)w; g.c = out; g.bias = (const uint16_t*)bias;
+  g.M = N * Do * Ho * Wo; g.N = Cout; g.K = KD * KH * KW * C;
+  g.lda = C; g.ldb = (int64_t)KD * KH * KW * C; g.ldc = Cout;
+  g.flags = bias ? kEpiBias : 0; g.alpha = 1.f;
+  g.zero = (const uint16_t*)zero;
+  g.cD = D; g.cDo = Do; g.cKHW = KH * KW; g.cPadD = pad_d;
+  g.cH = H; g.cW = W; g.cC = C; g.cHo = Ho; g.cWo = Wo; g.cKW = KW; g.cStride = stride; g.cPadH = pad_h;
+  g.cPadW = pad_w; g.cDil = dil;
+  return launch3s<true, true, true>(g, 1, st);
+}
+
 // Statistics chunks of a kEpiStats launch (stats: [2][chunks][N] fp32): 256-row tiles x waves along M
 // (4 for the 256x160 kernel, 2 for the two-stage kernels).
 PA_EXPORT int pa_gemm_stats_chunks(int64_t M, int bn) { return (int)((M + kBM - 1) / kBM) * (bn == 160 ? 4 : 2); }
@@ -1775,6 +1800,7 @@ PA_EXPORT int pa_conv2d_nhwc_fwd(const void* x, const void* w, const void* bias,
   g.lda = C; g.ldb = (int64_t)KH * KW * C; g.ldc = Cout;
   g.flags = bias ? kEpiBias : 0; g.alpha = 1.f;
   g.zero = (const uint16_t*)zero;
+  g.cD = 1; g.cDo = 1; g.cKHW = KH * KW; g.cPadD = 0;
   g.cH = H; g.cW = W; g.cC = C; g.cHo = Ho; g.cWo = Wo; g.cKW = KW; g.cStride = stride; g.cPadH = pad_h;
   g.cPadW = pad_w; g.cDil = dil;
   return launch3s<true, true, true>(g, 1, st);
@@ -1793,6 +1819,7 @@ PA_EXPORT int pa_conv2d_nhwc_fwd_stats(const void* x, const void* w, const void*
   g.flags = (bias ? kEpiBias : 0) | kEpiStats; g.alpha = 1.f;
   g.stats = stats;
   g.zero = (const uint16_t*)zero;
+  g.cD = 1; g.cDo = 1; g.cKHW = KH * KW; g.cPadD = 0;
   g.cH = H; g.cW = W; g.cC = C; g.cHo = Ho; g.cWo = Wo; g.cKW = KW; g.cStride = stride; g.cPadH = pad_h;
   g.cPadW = pad_w; g.cDil = dil;
   return launch3s<true, true, true>(g, 1, st);
@@ -1813,6 +1840,7 @@ PA_EXPORT int pa_conv2d_nhwc_fwd_bnbwd(const void* x, const void* w, void* out, 
   g.stats = stats;
   g.bn_x = (const uint16_t*)bn_x; g.bn_ss = bn_ss; g.bn_mean = bn_mean;
   g.zero = (const uint16_t*)zero;
+  g.cD = 1; g.cDo = 1; g.cKHW = KH * KW; g.cPadD = 0;
   g.cH = H; g.cW = W; g.cC = C; g.cHo = Ho; g.cWo = Wo; g.cKW = KW; g.cStride = stride; g.cPadH = pad_h;
   g.cPadW = pad_w; g.cDil = dil;
   return launch3s<true, true, true>(g, 1, st);
@@ -1834,6 +1862,7 @@ PA_EXPORT int pa_conv2d_nhwc_wgrad(const void* x, const void* dy, float* ws, con
   g.flags = kEpiOutF32; g.alpha = 1.f;
   g.c_split = (int64_t)g.M * Cout;
   g.zero = (const uint16_t*)zero;
+  g.cD = 1; g.cDo = 1; g.cKHW = KH * KW; g.cPadD = 0;
   g.cH = H; g.cW = W; g.cC = C; g.cHo = Ho; g.cWo = Wo; g.cKW = KW; g.cStride = stride; g.cPadH = pad_h;
   g.cPadW = pad_w; g.cDil = dil;
   g.tiles_m = (g.M + kBM - 1) / kBM;

@@ -133,6 +133,13 @@ def _convnd(n, x, weight, bias, stride, padding, dilation, groups, data_format):
                                              lambda xx, ww: _from_cf(miopen(_to_cf(xx, data_format, n)[0], ww), cl, n))
             if y is not None:
                 return _wrap(y)
+    # NDHWC 3-D convolutions: forward on the 3-D implicit GEMM when it measured faster than MIOpen
+    if cl and n == 3 and pre is None and groups == 1 and t.is_cuda and len(set(stride)) == 1 and \
+            len(set(dilation)) == 1:
+        from ... import ops as _ops
+        pads = (pad,) * 3 if isinstance(pad, int) else tuple(pad)
+        if len(pads) == 3 and _ops.conv.conv3d_ndhwc_ok(x_raw, w, groups, stride[0], pads, dilation[0]):
+            return _wrap(_ops.conv.conv3d_ndhwc(x_raw, w, b, stride[0], pads, dilation[0]))
     # NLC 1-D convolutions: the NHWC kernels on a 1 x L image with a 1 x K filter (padding (0, p)); each of the
     # three products again on the faster of ours and MIOpen (the data gradient of a 1 x K filter: MIOpen)
     if cl and n == 1 and pre is None and groups == 1 and t.is_cuda:

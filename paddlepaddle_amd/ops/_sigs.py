@@ -83,6 +83,7 @@ SIGS = {
     "pa_conv_skinny_ok": [_i64, _i64, _i64, _i64],
     "pa_conv_skinny_wgrad": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp],
     "pa_conv2d_nhwc_fwd": [_vp, _vp, _vp, _vp, _vp] + [_i32] * 13 + [_vp],
+    "pa_conv3d_ndhwc_fwd": [_vp, _vp, _vp, _vp, _vp] + [_i32] * 17 + [_vp],
     "pa_conv2d_nhwc_fwd_stats": [_vp, _vp, _vp, _vp, _vp] + [_i32] * 13 + [_vp, _vp],
     "pa_gemm_stats_chunks": [_i64, _i32],
     "pa_slab_reduce_bf16": [_vp, _vp, _i64, _i64, _i64, _i32, _vp],

@@ -751,3 +751,62 @@ def conv_implicit_nhwc(x, w, b, stride, pad, dil, fallback):
     if G.choose(key, {"hip": None, "blas": None}) == "hip":
         return run(x, w)
     return None
+
+
+# ---------------------------------------------------------------------------------------------------- 3-D (NDHWC)
+def _conv3d_own(x, w, b, stride, pads, dil):
+    """Forward on the implicit GEMM (pa_conv3d_ndhwc_fwd): x [N, D, H, W, C], w [Cout, C, KD, KH, KW]."""
+    N, D, H, W, C = x.shape
+    Cout, _, KD, KH, KW = w.shape
+    pd, ph, pw = pads
+    Do = (D + 2 * pd - dil * (KD - 1) - 1) // stride + 1
+    Ho = (H + 2 * ph - dil * (KH - 1) - 1) // stride + 1
+    Wo = (W + 2 * pw - dil * (KW - 1) - 1) // stride + 1
+    wk = w.permute(0, 2, 3, 4, 1).contiguous()
+    out = torch.empty(N, Do, Ho, Wo, Cout, dtype=x.dtype, device=x.device)
+    L.call("pa_conv3d_ndhwc_fwd", L.ptr(x), L.ptr(wk), L.ptr(b), L.ptr(out), L.ptr(_zero_page(x.device)), N, D, H, W,
+           C, Cout, KD, KH, KW, stride, pd, ph, pw, dil, Do, Ho, Wo, L.stream_ptr())
+    return out
+
+
+def _conv3d_mi(x, w, b, stride, pads, dil):
+    y = torch.nn.functional.conv3d(x.permute(0, 4, 1, 2, 3), w, b, stride, pads, dil)
+    return y.permute(0, 2, 3, 4, 1).contiguous()
+
+
+class _Conv3dNDHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pads, dil):
+        key = ("conv3f", tuple(x.shape), tuple(w.shape), stride, pads, dil, b is not None)
+        ch = _pick(key, lambda: _conv3d_own(x, w, b, stride, pads, dil), lambda: _conv3d_mi(x, w, b, stride, pads, dil))
+        y = _conv3d_own(x, w, b, stride, pads, dil) if ch == "hip" else _conv3d_mi(x, w, b, stride, pads, dil)
+        ctx.save_for_backward(x, w)
+        ctx.cfg = (stride, pads, dil, b is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        stride, pads, dil, has_b = ctx.cfg
+        mask = [ctx.needs_input_grad[0], ctx.needs_input_grad[1], has_b and ctx.needs_input_grad[2]]
+        gi, gw, gb = torch.ops.aten.convolution_backward(
+            dy.permute(0, 4, 1, 2, 3), x.permute(0, 4, 1, 2, 3), w, [w.shape[0]] if has_b else None, [stride] * 3,
+            list(pads), [dil] * 3, False, [0, 0, 0], 1, mask)
+        if gi is not None:
+            gi = gi.permute(0, 2, 3, 4, 1).contiguous()
+        return gi, gw, gb, None, None, None
+
+
+def conv3d_ndhwc_ok(x, w, groups, stride, pads, dil):
+    """Conditions of the 3-D implicit GEMM forward: bf16 NDHWC, groups 1, C % 64, Cout % 8, cubic stride."""
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 5 and groups == 1):
+        return False
+    if not x.is_contiguous() or not L.hip_enabled_for(x) or not L.has("pa_conv3d_ndhwc_fwd"):
+        return False
+    return x.shape[4] % 64 == 0 and w.shape[0] % 8 == 0 and x.numel() < (1 << 31)
+
+
+def conv3d_ndhwc(x, w, b, stride, pads, dil):
+    """NDHWC 3-D convolution: forward on the faster of the hand-written implicit GEMM and MIOpen (timed per shape),
+    both gradients on MIOpen."""
+    return _Conv3dNDHWC.apply(x, w, b, int(stride), tuple(int(p) for p in pads), int(dil))
