@@ -14,6 +14,7 @@ import torch
 from ..framework import dtype as _dt
 from ..framework.tensor import Tensor, Parameter, _wrap
 from . import program as P
+from ..framework.trace_hook import static_op
 
 
 class _StaticMode:
@@ -469,9 +470,44 @@ def name_scope(prefix=None):
     yield
 
 
+_PRINT_COUNTS: dict = {}
+
+
+@static_op
+def print_tensor(x, key, first_n, message, summarize, name, show_type, show_shape, show_layout):
+    """The Print op (reference: operators/print_op.cc): prints ``x`` when executed (at most first_n times per
+    op) and returns it (a view). Recorded as one node of a static program, so it prints on every run."""
+    if x.device.type == "meta":  # being traced
+        return x.view_as(x)
+    n = _PRINT_COUNTS.get(key, 0)
+    if first_n < 0 or n < first_n:
+        _PRINT_COUNTS[key] = n + 1
+        parts = [message] if message else []
+        if name:
+            parts.append(f"Variable: {name}")
+        if show_type:
+            parts.append(f"  - dtype: {str(x.dtype).replace('torch.', '')}")
+        if show_shape:
+            parts.append(f"  - shape: {list(x.shape)}")
+        if show_layout:
+            parts.append("  - layout: NCHW")
+        flat = x.detach().reshape(-1)
+        vals = flat[:summarize] if summarize >= 0 else flat
+        parts.append(f"  - data: {vals.float().cpu().tolist()}")
+        print("\n".join(parts), flush=True)
+    return x.view_as(x)
+
+
 def Print(input, first_n=-1, message=None, summarize=20, print_tensor_name=True, print_tensor_type=True,
           print_tensor_shape=True, print_tensor_layout=True, print_tensor_lod=True, print_phase="both"):
-    return input
+    """Prints the tensor when the program runs (static: recorded as an op of the program; dygraph: now).
+    Reference: python/paddle/static/nn/control_flow.py Print."""
+    t = input._t if isinstance(input, Tensor) else input
+    name = getattr(input, "name", None) if print_tensor_name else None
+    key = f"print:{id(input)}:{message}"
+    out = print_tensor(t, key, int(first_n), message, int(summarize), name, bool(print_tensor_type),
+                       bool(print_tensor_shape), bool(print_tensor_layout))
+    return _wrap(out) if isinstance(input, Tensor) else out
 
 
 def create_global_var(shape, value, dtype, persistable=False, force_cpu=False, name=None):

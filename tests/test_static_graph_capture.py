@@ -66,3 +66,25 @@ def test_cpu_program_with_capture_flag_runs_eagerly():
         assert out[0].shape == (4, 1)
     finally:
         paddle.disable_static()
+
+
+def test_static_print_is_an_op_of_the_program(capsys):
+    """paddle.static.Print prints when the program runs (every run, first_n bounded), not at build time."""
+    import numpy as np
+    paddle.set_device("cpu")
+    paddle.enable_static()
+    try:
+        main, start = paddle.static.Program(), paddle.static.Program()
+        with paddle.static.program_guard(main, start):
+            x = paddle.static.data("x", [2, 2], "float32")
+            y = paddle.static.Print(x * 3, message="tripled", first_n=2)
+            z = y + 1
+        assert capsys.readouterr().out == ""          # nothing printed while building
+        exe = paddle.static.Executor(paddle.CPUPlace())
+        for _ in range(3):
+            out = exe.run(main, feed={"x": np.ones((2, 2), "float32")}, fetch_list=[z])[0]
+        np.testing.assert_array_equal(out, np.full((2, 2), 4.0, "float32"))
+        printed = capsys.readouterr().out
+        assert printed.count("tripled") == 2 and "[3.0, 3.0, 3.0, 3.0]" in printed
+    finally:
+        paddle.disable_static()
