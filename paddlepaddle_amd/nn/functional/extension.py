@@ -181,32 +181,9 @@ def rnnt_loss(input, label, input_lengths, label_lengths, blank=0, fastemit_lamb
 
 # ----------------------------------------------------------------------------------- adaptive softmax
 def adaptive_log_softmax_with_loss(input, label, head_weight, tail_weights, cutoffs, head_bias=None, name=None):
-    """(output, loss): log-probability of the target class per row and the mean NLL.
-    head_weight [in, shortlist + n_clusters]; tail_weights[i] = [proj [in, hsz], out [hsz, osz]]."""
-    x, y = T(input), T(label).to(torch.int64).reshape(-1)
-    hw = T(head_weight)
-    hb = T(head_bias)
-    cutoffs = list(cutoffs)
-    shortlist = cutoffs[0]
-    head = x @ hw
-    if hb is not None:
-        head = head + hb
-    head_lp = head.log_softmax(-1)
-    out = torch.zeros(x.shape[0], dtype=head_lp.dtype, device=x.device)
-    in_short = y < shortlist
-    out = torch.where(in_short, head_lp.gather(1, y.clamp_max(shortlist - 1).unsqueeze(1)).squeeze(1), out)
-    for i in range(len(cutoffs) - 1):
-        lo, hi = cutoffs[i], cutoffs[i + 1]
-        m = (y >= lo) & (y < hi)
-        if not bool(m.any()):
-            continue
-        proj, o = (T(w) for w in tail_weights[i])
-        tail_lp = ((x[m] @ proj) @ o).log_softmax(-1)
-        rel = (y[m] - lo).unsqueeze(1)
-        val = head_lp[m, shortlist + i] + tail_lp.gather(1, rel).squeeze(1)
-        out = out.masked_scatter(m, val)
-    loss = (-out).mean()
-    return _wrap(out), _wrap(loss)
+    """(output, loss): log-probability of the target class per row and the mean NLL (nn/functional/loss.py)."""
+    from .loss import adaptive_log_softmax_with_loss as _alsm
+    return _alsm(input, label, head_weight, tail_weights, cutoffs, head_bias, name)
 
 
 # ----------------------------------------------------------------------------------- attention variants

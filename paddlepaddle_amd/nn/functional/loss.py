@@ -274,4 +274,43 @@ def edit_distance(input, label, normalized=True, ignored_tokens=None, input_leng
 
 
 def adaptive_log_softmax_with_loss(input, label, head_weight, tail_weights, cutoffs, head_bias=None, name=None):
-    raise NotImplementedError("adaptive_log_softmax_with_loss: use nn.AdaptiveLogSoftmaxWithLoss")
+    """Adaptive softmax (Grave et al.; reference nn/functional/loss.py:4461): the head scores the shortlist
+    [0, cutoffs[0]) plus one logit per tail cluster; a target in cluster i ([cutoffs[i-1], cutoffs[i])) scores
+    head_logprob[shortlist + i - 1] + log_softmax((x @ proj_i) @ out_i)[target - cutoffs[i-1]].
+    ``cutoffs`` ends with the class count. Returns (per-sample target log-probabilities, mean NLL)."""
+    x, y = T(input), T(label)
+    if y.dim() > 1:
+        raise ValueError("0D or 1D label tensor expected, multi-label not supported")
+    batched = y.dim() == 1
+    if batched and (x.dim() != 2 or x.shape[0] != y.shape[0]):
+        raise ValueError("1D label tensor expects 2D input tensors with the same batch size")
+    if not batched:
+        if x.dim() != 1:
+            raise ValueError("0D label tensor expects 1D input tensors")
+        x, y = x.unsqueeze(0), y.unsqueeze(0)
+    y = y.long()
+    cut = [int(T(c).item()) if isinstance(c, (Tensor, torch.Tensor)) else int(c) for c in cutoffs]
+    short = cut[0]
+    head = x @ T(head_weight)
+    if head_bias is not None:
+        head = head + T(head_bias)
+    head_lp = head.float().log_softmax(-1).to(x.dtype)
+    out = torch.zeros(y.shape[0], dtype=x.dtype, device=x.device)
+    m0 = y < short
+    if bool(m0.any()):
+        rows = m0.nonzero().squeeze(1)
+        out = out.index_put((rows,), head_lp[rows].gather(1, y[rows].unsqueeze(1)).squeeze(1))
+    for i in range(1, len(cut)):
+        lo, hi = cut[i - 1], cut[i]
+        m = (y >= lo) & (y < hi)
+        if not bool(m.any()):
+            continue
+        rows = m.nonzero().squeeze(1)
+        proj, o = tail_weights[i - 1]
+        tail = ((x[rows] @ T(proj)) @ T(o)).float().log_softmax(-1).to(x.dtype)
+        val = head_lp[rows, short + i - 1] + tail.gather(1, (y[rows] - lo).unsqueeze(1)).squeeze(1)
+        out = out.index_put((rows,), val)
+    if bool(((y < 0) | (y >= cut[-1])).any()):
+        raise ValueError(f"target values should be in [0, {cut[-1] - 1}]")
+    loss = (-out).mean()
+    return _wrap(out if batched else out.squeeze(0)), _wrap(loss)

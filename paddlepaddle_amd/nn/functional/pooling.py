@@ -108,7 +108,14 @@ def _avgpool(n, x, kernel_size, stride, padding, ceil_mode, exclusive, divisor_o
     pad = _pad_arg(padding, n, data_format)
     if isinstance(pad, tuple) and pad and pad[0] == "asym":
         if exclusive:
-            raise NotImplementedError("avg pooling with asymmetric padding and exclusive=True")
+            # average over the real elements of each window: window sums of the zero-padded input divided by
+            # the window counts of a zero-padded ones map (both pooled with the same divisor, which cancels)
+            tp = _explicit_pad(t, pad[1], 0.0)
+            ones = _explicit_pad(torch.ones_like(t[:, :1]), pad[1], 0.0)
+            fn = {1: F.avg_pool1d, 2: F.avg_pool2d, 3: F.avg_pool3d}[n]
+            s_ = fn(tp, kernel_size, stride, 0, ceil_mode, True)
+            c_ = fn(ones, kernel_size, stride, 0, ceil_mode, True)
+            return _wrap(_back(s_ / c_.clamp_min(1e-12), cl))
         t, pad = _explicit_pad(t, pad[1], 0.0), 0
     if pad == "same":
         pad = tuple(k // 2 for k in ((kernel_size,) * n if isinstance(kernel_size, int) else kernel_size))
