@@ -1916,13 +1916,51 @@ PA_EXPORT int pa_gemm_small_m(const void* a, int64_t lda, const void* b, int64_t
   return (int)hipGetLastError();
 }
 
+namespace {
+// Slab sum with the split dimension spread over the block: 16 lanes of float4 columns x 16 split groups; each
+// thread sums every 16th slab of its 4 columns (several loads in flight), the 16 groups fold through LDS. A
+// weight gradient has few outputs and many slabs (64 x 64 x 128 splits), which a one-thread-per-output loop
+// walks serially.
+__global__ __launch_bounds__(256) void slab_reduce_k(const float* __restrict__ ws, uint16_t* __restrict__ c,
+                                                     int64_t ldc, int64_t M, int64_t N, int splits) {
+  __shared__ float4 red[16][16];
+  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int64_t i4 = ((int64_t)blockIdx.x * 16 + cl) * 4;
+  const int64_t MN = M * N;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i4 < MN) {
+    int s = g;
+    for (; s + 48 < splits; s += 64) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(ws + (int64_t)(s + 16 * u) * MN + i4);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
+    }
+    for (; s < splits; s += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(ws + (int64_t)s * MN + i4);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  red[g][cl] = acc;
+  __syncthreads();
+  if (g == 0 && i4 < MN) {
+    float4 t = red[0][cl];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) { t.x += red[q][cl].x; t.y += red[q][cl].y; t.z += red[q][cl].z; t.w += red[q][cl].w; }
+    const int64_t m = i4 / N, n = i4 % N;
+    *reinterpret_cast<uint2*>(c + m * ldc + n) = make_uint2(pack_bf16(t.x, t.y), pack_bf16(t.z, t.w));
+  }
+}
+}  // namespace
+
 // Sum of `splits` fp32 slabs [splits][M][N] (split-K partials) into bf16 C [M][ldc] in one pass (the weight
 // gradients of convolutions: replaces a separate reduction and cast). N % 4 == 0.
 PA_EXPORT int pa_slab_reduce_bf16(const float* ws, void* c, int64_t ldc, int64_t M, int64_t N, int splits,
                                   hipStream_t st) {
   if (N % 4 != 0 || ldc % 4 != 0 || splits < 1 || M <= 0) return 1;
   const int64_t n4 = M * N / 4;
-  hipLaunchKernelGGL(gemm_small_m_reduce_k, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, ws, nullptr,
-                     (uint16_t*)c, ldc, (int)M, (int)N, splits);
+  hipLaunchKernelGGL(slab_reduce_k, dim3((unsigned)((n4 + 15) / 16)), dim3(256), 0, st, ws, (uint16_t*)c, ldc, M, N,
+                     splits);
   return (int)hipGetLastError();
 }
