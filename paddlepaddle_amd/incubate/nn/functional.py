@@ -336,10 +336,10 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
       per sequence) and the token attends over positions [0, step] of the cache with the HIP
       flash-decoding kernel (ops.dense_decode_attention), or the math path when attn_mask is given.
     Returns out, or (out, cache_kvs) when cache_kvs is given (the caches are updated in place).
+    beam_offset [batch, beam, max_len] (decode): beam-search cache indirection, as masked_multihead_attention's
+    beam_cache_offset (math path over the re-gathered cache).
     qkv_weights: [3, H, D, E] (trans_qkvw) or [E, 3, H, D]; with gqa_group_size = kv heads,
     [H + 2*kv_heads, D, E] / [E, H + 2*kv_heads, D]."""
-    if beam_offset is not None:
-        raise NotImplementedError("fused_multi_transformer: beam_offset (beam-search cache reorder) is not supported")
     if mode != "upscale_in_train" and training and dropout_rate > 0:
         raise NotImplementedError("fused_multi_transformer: only mode='upscale_in_train' dropout is supported")
     xt = _t(x)
@@ -392,17 +392,19 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
             bi = torch.arange(B, device=xt.device)
             cache[0][bi, :, steps] = k.to(cache.dtype)
             cache[1][bi, :, steps] = v.to(cache.dtype)
-            if mask is None:
+            if mask is None and beam_offset is None:
                 o = _ops.dense_decode_attention(q.to(cache.dtype), cache[0], cache[1], steps + 1).to(q.dtype)
-            else:  # additive [B, 1, 1, step + 1] mask: math path over the cache prefix
+            else:  # additive [B, 1, 1, step + 1] mask / beam indirection: math path over the cache prefix
                 Lc = cache.shape[3]
                 G = H // Hk
-                s = torch.einsum("bkgd,bkld->bkgl", q.float().view(B, Hk, G, Dh), cache[0].float()) / math.sqrt(Dh)
-                m = mask.float().reshape(B, 1, 1, -1)
-                s[..., :m.shape[-1]] += m
+                kc, vc = _beam_kv(cache, beam_offset, steps) if beam_offset is not None else (cache[0], cache[1])
+                s = torch.einsum("bkgd,bkld->bkgl", q.float().view(B, Hk, G, Dh), kc.float()) / math.sqrt(Dh)
+                if mask is not None:
+                    m = mask.float().reshape(B, 1, 1, -1)
+                    s[..., :m.shape[-1]] += m
                 valid = torch.arange(Lc, device=xt.device)[None] <= steps[:, None]
                 s = s.masked_fill(~valid[:, None, None], float("-inf"))
-                o = torch.einsum("bkgl,bkld->bkgd", torch.softmax(s, -1), cache[1].float()).reshape(B, H, Dh)
+                o = torch.einsum("bkgl,bkld->bkgd", torch.softmax(s, -1), vc.float()).reshape(B, H, Dh)
             o = o.to(h.dtype).reshape(B, 1, H * Dh)
         else:
             if rot is not None:
@@ -487,11 +489,11 @@ def masked_multihead_attention(x, cache_kv=None, bias=None, src_mask=None, cum_o
     """One decode step. x [B, 3*H*D]; cache_kv [2, B, H, max_len, D] updated in place at the step.
     The step index is sequence_lengths[b] (per batch) or src_mask's width - 1. ``qkv_out_scale``: x is the int32
     output of an int8 QKV GEMM, dequantised by these per-column scales; ``out_scale`` > 0: int8 output
-    (reference QuantHelperFunc rounding / bounds). Beam-search cache indirection (``beam_cache_offset``) and the
-    reference's ``cum_offsets`` padding removal are not implemented and raise."""
-    if beam_cache_offset is not None:
-        raise NotImplementedError("masked_multihead_attention: beam_cache_offset (beam-search KV indirection) is "
-                                  "not implemented")
+    (reference QuantHelperFunc rounding / bounds). ``beam_cache_offset`` [batch, beam, max_len]: beam-search KV
+    indirection — key / value of step t of row b are read from beam ``beam_cache_offset[b, t]`` of b's batch
+    entry (an entry of 0 reads b's own cache, as the reference kernel does, masked_multihead_attention_kernel.cu
+    :423); the result is then (out, cache_kv, beam_cache_offset). The reference's ``cum_offsets`` padding removal
+    is not implemented and raises."""
     if cum_offsets is not None:
         raise NotImplementedError("masked_multihead_attention: cum_offsets is not implemented")
     if compute_dtype not in ("default", "bf16", "fp16", "fp32"):
@@ -521,7 +523,17 @@ def masked_multihead_attention(x, cache_kv=None, bias=None, src_mask=None, cum_o
     bi = torch.arange(B, device=xt.device)
     cache[0][bi, :, steps] = k.to(cache.dtype)
     cache[1][bi, :, steps] = v.to(cache.dtype)
-    if src_mask is None:  # HIP flash-decoding over the dense cache (ops.dense_decode_attention)
+    if beam_cache_offset is not None:
+        kc, vc = _beam_kv(cache, beam_cache_offset, steps)                          # [B, H, L, D]
+        pos = torch.arange(L, device=xt.device)
+        valid = pos[None, :] <= steps[:, None]
+        s_ = torch.einsum("bhd,bhld->bhl", q.float(), kc.float()) / math.sqrt(D)
+        if src_mask is not None:
+            sm = _t(src_mask).float().reshape(B, 1, -1)
+            s_[..., :sm.shape[-1]] = s_[..., :sm.shape[-1]] + sm
+        s_ = s_.masked_fill(~valid[:, None], float("-inf"))
+        o = torch.einsum("bhl,bhld->bhd", torch.softmax(s_, -1), vc.float()).to(xt.dtype)
+    elif src_mask is None:  # HIP flash-decoding over the dense cache (ops.dense_decode_attention)
         o = _ops.dense_decode_attention(q, cache[0], cache[1], steps + 1).to(xt.dtype)
     else:
         pos = torch.arange(L, device=xt.device)
@@ -539,7 +551,26 @@ def masked_multihead_attention(x, cache_kv=None, bias=None, src_mask=None, cum_o
         out = out * _t(out_smooth)
     if out_scale is not None and float(out_scale) > 0:
         out = _quant_out(out, out_scale, quant_round_type, quant_max_bound, quant_min_bound)
+    if beam_cache_offset is not None:
+        return _wrap(out), _wrap(cache), beam_cache_offset
     return _wrap(out), _wrap(cache)
+
+
+def _beam_kv(cache, beam_cache_offset, steps):
+    """Key / value caches [B, heads, L, D] as seen through beam-search indirection: position t of row b comes
+    from beam ``off[b, t]`` of b's batch entry (0: b's own row); the current step is always the row's own
+    (reference masked_multihead_attention_kernel.cu beam_offsets)."""
+    _, B, Hk, L, D = cache.shape
+    dev = cache.device
+    off = _t(beam_cache_offset)
+    W = off.shape[1] if off.dim() == 3 else 1
+    off = off.reshape(B, -1)[:, :L].long()
+    off = off.masked_fill(torch.arange(L, device=dev)[None, :] >= steps[:, None], 0)
+    bi = torch.arange(B, device=dev)
+    src = (bi // W).view(B, 1) * W + torch.where(off != 0, off, (bi % W).view(B, 1))  # [B, L] source row
+    hh = torch.arange(Hk, device=dev).view(1, Hk, 1)
+    tt = torch.arange(L, device=dev).view(1, 1, L)
+    return cache[0][src.view(B, 1, L), hh, tt], cache[1][src.view(B, 1, L), hh, tt]
 
 
 def _rotate_rows(x, cos, sin, neox):

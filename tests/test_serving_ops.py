@@ -141,6 +141,31 @@ def test_fused_multi_transformer_gqa_rotary_rmsnorm_cpu():
     _run_fmt_prefill_decode("cpu", torch.float32, 32, 4, 2, norm="rmsnorm", rotary=True)
 
 
+def test_fused_multi_transformer_beam_offset_equals_reordered_cache():
+    """beam_offset indirection == physically copying each position from the parent beam's cache row."""
+    gen = torch.Generator().manual_seed(3)
+    bsz, W, E, H, Lmax, step = 2, 2, 32, 4, 8, 4
+    B, Dh = bsz * W, E // H
+    P = _params(2, E, H, H, 64, gen, False)
+    x = torch.randn(B, 1, E, generator=gen)
+    base = [torch.randn(2, B, H, Lmax, Dh, generator=gen) for _ in P]
+    off = torch.randint(0, W, (bsz, W, Lmax), generator=gen).int()
+    ts = paddle.to_tensor(np.array([step], "int32"))
+    out_b, _ = _fmt(_T(x), P, "cpu", torch.float32, cache_kvs=[paddle.to_tensor(c.clone()) for c in base],
+                    time_step=ts, beam_offset=paddle.to_tensor(off))
+    phys = []
+    for c in base:
+        r = c.clone()
+        for b in range(B):
+            for t in range(step):
+                o = int(off[b // W, b % W, t])
+                if o:
+                    r[:, b, :, t] = c[:, (b // W) * W + o, :, t]
+        phys.append(paddle.to_tensor(r))
+    out_p, _ = _fmt(_T(x), P, "cpu", torch.float32, cache_kvs=phys, time_step=ts)
+    np.testing.assert_allclose(out_b.numpy(), out_p.numpy(), rtol=1e-4, atol=1e-4)
+
+
 def test_fused_multi_transformer_layer_returns_caches():
     m = paddle.incubate.nn.FusedMultiTransformer(32, 4, 64, num_layers=2)
     m.eval()

@@ -109,10 +109,42 @@ def test_masked_mha_unsupported_arguments_raise():
     x = paddle.randn([2, 3 * 2 * 16])
     cache = paddle.zeros([2, 2, 2, 8, 16])
     with pytest.raises(NotImplementedError):
-        IF.masked_multihead_attention(x, cache, beam_cache_offset=paddle.zeros([2, 1, 8], dtype="int32"))
+        IF.masked_multihead_attention(x, cache, cum_offsets=paddle.zeros([2], dtype="int32"))
     out, _ = IF.masked_multihead_attention(x, cache, sequence_lengths=paddle.to_tensor([0, 0]), out_scale=0.1,
                                            quant_round_type=1, quant_max_bound=127.0, quant_min_bound=-127.0)
     assert out.dtype == paddle.int8
+
+
+def test_masked_mha_beam_cache_offset_reads_parent_beams():
+    """beam_cache_offset[b, t] = w (non-zero) reads key / value t from beam w of b's batch entry; the current step
+    is the row's own (reference masked_multihead_attention_kernel.cu beam_offsets)."""
+    from paddlepaddle_amd.incubate.nn import functional as IF
+    torch.manual_seed(0)
+    bsz, W, H, D, Lmax, step = 2, 3, 2, 16, 8, 5
+    B = bsz * W
+    x = torch.randn(B, 3 * H * D)
+    cache = torch.randn(2, B, H, Lmax, D)
+    off = torch.randint(0, W, (bsz, W, Lmax), dtype=torch.int32)
+    ref_cache = cache.clone()
+    out, cache_out, off_out = IF.masked_multihead_attention(
+        paddle.to_tensor(x), paddle.to_tensor(cache), sequence_lengths=paddle.to_tensor([step] * B),
+        beam_cache_offset=paddle.to_tensor(off))
+    q, k, v = x.view(B, 3, H, D).unbind(1)
+    ref_cache[0][:, :, step] = k
+    ref_cache[1][:, :, step] = v
+    for b in range(B):
+        ks, vs = [], []
+        for t in range(step + 1):
+            o = int(off[b // W, b % W, t])
+            r = (b // W) * W + o if (o != 0 and t < step) else b
+            ks.append(ref_cache[0][r, :, t])
+            vs.append(ref_cache[1][r, :, t])
+        K, V = torch.stack(ks, 1), torch.stack(vs, 1)        # [H, T, D]
+        p = torch.softmax(torch.einsum("hd,htd->ht", q[b], K) / D ** 0.5, -1)
+        ref = torch.einsum("ht,htd->hd", p, V).reshape(-1)
+        np.testing.assert_allclose(out.numpy()[b], ref.numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(cache_out.numpy(), ref_cache.numpy())
+    assert off_out is not None
 
 
 # ------------------------------------------------------------------------------------------------ GPU kernels
