@@ -1,0 +1,70 @@
+"""Per-tile fixed cost of the 256x256 GEMM: time C[M, N] = A[M, K] . B[K, N] over a K sweep at fixed M, N and fit
+t = t0 + k1 * K. t0 / (tiles / CUs) is the per-tile cost that does not scale with K (workgroup launch, prologue
+load latency, epilogue stores) — what a persistent kernel that overlaps the next tile's prologue with the current
+tile's epilogue could recover. Training-like operands (N(0,1) activations, N(0,0.02) weights).
+
+    python tools/bench_gemm_k_sweep.py
+"""
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+from paddlepaddle_amd.ops import gemm as G  # noqa: E402
+
+
+def timed(fn, iters):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters
+
+
+def main():
+    dev = "cuda"
+    torch.manual_seed(0)
+    # chip warm-up: sustained load so the clock settles before any timing
+    w = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
+    t_end = time.time() + 2.0
+    while time.time() < t_end:
+        torch.mm(w, w)
+    torch.cuda.synchronize()
+    for (M, N, kmaj_b) in [(4096, 20480, False), (4096, 20480, True), (4096, 5120, False)]:
+        tiles = (M // 256) * (N // 256)
+        rows = []
+        for K in (512, 1024, 2048, 3072, 5120, 10240):
+            a = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+            if kmaj_b:
+                b = (torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02).t()
+            else:
+                b = torch.randn(K, N, device=dev, dtype=torch.bfloat16) * 0.02
+            out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            f_ours = lambda: G.gemm(a, b, out=out, bn=1)  # noqa: E731
+            f_blas = lambda: torch.mm(a, b, out=out)  # noqa: E731
+            iters = max(5, int(0.4 / (2 * M * N * K / 1.3e15)))
+            best = {}
+            for _ in range(2):
+                for name, fn in (("ours", f_ours), ("blas", f_blas)):
+                    fn()
+                    t = timed(fn, iters)
+                    best[name] = min(best.get(name, 1e9), t)
+            rows.append((K, best["ours"], best["blas"]))
+            print(f"M={M} N={N} K={K:5d} B{'kmaj' if kmaj_b else 'mnmaj'} tiles={tiles}: ours {best['ours'] * 1e6:8.1f} us "
+                  f"({2 * M * N * K / best['ours'] / 1e12:6.0f} TF)  blas {best['blas'] * 1e6:8.1f} us "
+                  f"({2 * M * N * K / best['blas'] / 1e12:6.0f} TF)", flush=True)
+            del a, b, out
+        Ks = np.array([r[0] for r in rows], dtype=np.float64)
+        for j, name in ((1, "ours"), (2, "blas")):
+            ts = np.array([r[j] for r in rows])
+            k1, t0 = np.polyfit(Ks, ts, 1)
+            rounds = tiles / 256.0
+            print(f"  fit {name}: t0 = {t0 * 1e6:7.1f} us, per-tile-round fixed = {t0 / rounds * 1e6:6.2f} us, "
+                  f"slope = {k1 * 1e9:7.2f} ns/K  (asymptotic {2 * M * N / k1 / 1e12:6.0f} TF)", flush=True)
+
+
+if __name__ == "__main__":
+    main()
