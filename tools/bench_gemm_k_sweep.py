@@ -33,7 +33,10 @@ def main():
     while time.time() < t_end:
         torch.mm(w, w)
     torch.cuda.synchronize()
-    for (M, N, kmaj_b) in [(4096, 20480, False), (4096, 20480, True), (4096, 5120, False)]:
+    shapes = [(4096, 20480, False), (4096, 20480, True), (4096, 5120, False)]
+    if len(sys.argv) > 1:
+        shapes = shapes[:int(sys.argv[1])]
+    for (M, N, kmaj_b) in shapes:
         tiles = (M // 256) * (N // 256)
         rows = []
         for K in (512, 1024, 2048, 3072, 5120, 10240):
@@ -52,6 +55,9 @@ def main():
                     fn()
                     t = timed(fn, iters)
                     best[name] = min(best.get(name, 1e9), t)
+            ref = torch.mm(a, b).float()
+            err = (G.gemm(a, b, bn=1).float() - ref).abs().max().item() / ref.abs().max().item()
+            assert err < 2e-2, err
             rows.append((K, best["ours"], best["blas"]))
             print(f"M={M} N={N} K={K:5d} B{'kmaj' if kmaj_b else 'mnmaj'} tiles={tiles}: ours {best['ours'] * 1e6:8.1f} us "
                   f"({2 * M * N * K / best['ours'] / 1e12:6.0f} TF)  blas {best['blas'] * 1e6:8.1f} us "
