@@ -138,6 +138,30 @@ __global__ __launch_bounds__(256) void dropout_bwd_k(const T* __restrict__ dy, T
   }
 }
 
+// dropout backward of a [rows, cols] gradient that also writes the column partials of dx (the bias gradient of the
+// linear whose output was dropped out: out-proj / FFN2 of a transformer block), laid out like colsum_partial_k's.
+// The keep mask is indexed by the flat element index r * cols + c, as in dropout_add_k.
+template <typename T>
+__global__ __launch_bounds__(256) void dropout_bwd_colsum_k(const T* __restrict__ dy, T* __restrict__ dx,
+                                                            float* __restrict__ part, int64_t rows, int64_t cols,
+                                                            int nparts, uint64_t seed, uint32_t thresh, float scale) {
+  const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c >= cols) return;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t r = blockIdx.y; r < rows; r += nparts) {
+    float g[8];
+    const int64_t e = r * cols + c;
+    load8<T>(dy + e, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      g[j] = keep(seed, e + j, thresh) ? g[j] * scale : 0.f;
+      acc[j] += g[j];
+    }
+    store8<T>(dx + e, g);
+  }
+  store8<float>(part + (int64_t)blockIdx.y * cols + c, acc);
+}
+
 inline int nparts_for(int64_t rows) {
   int64_t p = rows / 32;
   if (p < 1) p = 1;
@@ -200,6 +224,34 @@ PA_EXPORT int pa_dropout_bwd(const void* dy, void* dx, int64_t n, float p, uint6
   const float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
   PA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((dropout_bwd_k<T>), dim3(grid_ew(nvec)), dim3(256), 0, st,
                                                  (const T*)dy, (T*)dx, nvec, seed, thresh, scale));
+  PA_CHECK_LAUNCH();
+  return 0;
+}
+
+// dropout backward over a [rows, cols] gradient + the column partials of dx into ws [nparts, cols] (fp32, nparts =
+// pa_colsum_nparts(rows)); pa_fold_partials turns them into the column sums later (bias gradient)
+PA_EXPORT int pa_dropout_bwd_colsum(const void* dy, void* dx, float* ws, int64_t rows, int64_t cols, float p,
+                                    uint64_t seed, int dtype, hipStream_t st) {
+  if (cols % 8) return 1;
+  const uint32_t thresh = (uint32_t)fminf(p * 4294967296.0f, 4294967295.0f);
+  const float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  const int np = nparts_for(rows);
+  dim3 g1((unsigned)cdiv(cols, 2048), (unsigned)np);
+  PA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((dropout_bwd_colsum_k<T>), g1, dim3(256), 0, st, (const T*)dy, (T*)dx,
+                                                 ws, rows, cols, np, seed, thresh, scale));
+  PA_CHECK_LAUNCH();
+  return 0;
+}
+
+PA_EXPORT int64_t pa_colsum_nparts(int64_t rows) { return nparts_for(rows); }
+
+// dtype bit 8: accumulate into `out`
+PA_EXPORT int pa_fold_partials(const float* ws, void* out, int64_t cols, int64_t nparts, int dtype_acc,
+                               hipStream_t st) {
+  const int dtype = dtype_acc & 0xff, acc = (dtype_acc >> 8) & 1;
+  dim3 g2((unsigned)cdiv(cols, 64));
+  PA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((fold_partials_k<T>), g2, dim3(256), 0, st, ws, (T*)out, cols,
+                                                 (int)nparts, acc));
   PA_CHECK_LAUNCH();
   return 0;
 }

@@ -96,6 +96,9 @@ SIGS = {
     "pa_bias_gelu_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp],
     "pa_dropout_add_fwd": [_vp, _vp, _vp, _i64, _f32, _u64, _i32, _vp],
     "pa_dropout_bwd": [_vp, _vp, _i64, _f32, _u64, _i32, _vp],
+    "pa_dropout_bwd_colsum": [_vp, _vp, _vp, _i64, _i64, _f32, _u64, _i32, _vp],
+    "pa_colsum_nparts": [_i64],
+    "pa_fold_partials": [_vp, _vp, _i64, _i64, _i32, _vp],
     # batch norm (NHWC)
     "pa_bn_chunks": [_i64, _i32],
     "pa_bn_fwd_nhwc": [_vp] * 11 + [_i64, _i32, _f32, _f32, _i32, _i32, _vp],
@@ -120,4 +123,5 @@ SIGS = {
     "pa_version": [],
 }
 
-RET_I64 = {"pa_gemm_pp_ws_bytes", "pa_bn_pre_ws", "pa_gemm_skinny_stats_chunks", "pa_conv_skinny_stats_chunks"}
+RET_I64 = {"pa_gemm_pp_ws_bytes", "pa_bn_pre_ws", "pa_gemm_skinny_stats_chunks", "pa_conv_skinny_stats_chunks",
+           "pa_colsum_nparts"}

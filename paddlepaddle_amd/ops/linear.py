@@ -21,14 +21,22 @@ import torch
 import torch.nn.functional as F
 
 from . import _loader as L
+from . import dropout as _dropout
 from . import gemm as G
 from .activation import bias_gelu, gelu
 from ..framework.trace_hook import static_op
 
 
 def colsum(x2d, acc=None):
-    """Column sums of a [rows, cols] tensor (bias gradient); added in place into ``acc`` when given."""
+    """Column sums of a [rows, cols] tensor (bias gradient); added in place into ``acc`` when given. A gradient
+    whose producer (a dropout backward) already wrote its column partials only has them folded."""
     rows, cols = x2d.shape
+    pre = _dropout.take_colsum(x2d) if x2d.is_cuda else None
+    if pre is not None:
+        out = acc if acc is not None else torch.empty(cols, dtype=x2d.dtype, device=x2d.device)
+        L.call("pa_fold_partials", L.ptr(pre[0]), L.ptr(out), cols, pre[1], L.dcode(x2d) | ((acc is not None) << 8),
+               L.stream_ptr())
+        return out
     if L.hip_enabled_for(x2d) and x2d.dtype in L._DT and cols % 8 == 0 and x2d.is_contiguous():
         out = acc if acc is not None else torch.empty(cols, dtype=x2d.dtype, device=x2d.device)
         ws = torch.empty(256 * cols, dtype=torch.float32, device=x2d.device)

@@ -296,6 +296,38 @@ def test_dropout_add_statistics_and_grad():
     assert torch.equal(a, b)
 
 
+def test_dropout_backward_writes_linear_bias_grad_partials():
+    """linear(+bias) -> dropout_add: after the first backward the dropout backward writes the column partials of
+    its gradient and the linear only folds them; the bias gradient equals the plain column sum, and the dropout
+    mask matches the unfused kernel (same seed)."""
+    from paddlepaddle_amd.ops import dropout as D
+    torch.manual_seed(0)
+    rows, k, n = 1000, 64, 96
+    x = torch.randn(rows, k, device=DEV, dtype=torch.bfloat16)
+    w = (torch.randn(k, n, device=DEV) / 8).to(torch.bfloat16).requires_grad_(True)
+    b = torch.zeros(n, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    gy = torch.randn(rows, n, device=DEV, dtype=torch.bfloat16)
+    D._WANT_CS.discard((rows, n, torch.bfloat16))
+    grads = []
+    for it in range(2):
+        torch.manual_seed(11)
+        lin = ops.fused_linear(x, w, b)
+        y = ops.dropout_add(lin, None, 0.25, True)
+        w.grad, b.grad = None, None
+        L.CALLS.clear()
+        y.backward(gy)
+        grads.append((w.grad.clone(), b.grad.clone()))
+        if it == 0:
+            assert (rows, n, torch.bfloat16) in D._WANT_CS and L.calls("pa_dropout_bwd") > 0
+        else:
+            _lib_loaded("pa_dropout_bwd_colsum", "pa_fold_partials")
+    mask = (y.detach() != 0) | (lin.detach() == 0)
+    dx_ref = gy.float() * mask.float() / 0.75
+    torch.testing.assert_close(grads[1][1].float(), dx_ref.sum(0), atol=0.25, rtol=1e-2)
+    assert torch.equal(grads[0][0], grads[1][0])  # same mask / dX as the unfused kernel
+    torch.testing.assert_close(grads[0][1].float(), grads[1][1].float(), atol=0.25, rtol=1e-2)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("shape,k,s,p", [((2, 17, 15, 64), 3, 2, 1), ((3, 12, 12, 32), 2, 2, 0), ((1, 9, 11, 16), 3, 1, 1)])
 def test_maxpool_nhwc_matches_torch(shape, k, s, p):
