@@ -22,8 +22,8 @@ _FLAGS = {
     "FLAGS_eager_backward_engine": "native",  # native (csrc/autograd/autograd_exec.cpp RunBackward) | torch
     "FLAGS_gemm_backend": "auto",         # per-shape GEMM / conv backend: auto (timed) | hip | blas
     "FLAGS_sharding_stage3_keep_params": "auto",  # stage 3: keep gathered params until the optimizer step
-    "FLAGS_conv_per_direction": True,
-    "FLAGS_conv_bn_fusion": True,         # convs feeding a training BN write its statistics in their epilogue     # NHWC conv: forward / dgrad / wgrad each on the faster of ours and MIOpen
+    "FLAGS_conv_per_direction": True,     # NHWC conv: forward / dgrad / wgrad each on the faster of ours and MIOpen
+    "FLAGS_conv_bn_fusion": True,         # convs feeding a training BN write its statistics in their epilogue
     "FLAGS_use_autotune": True,           # time GEMM backends for shapes the tuning table does not hold
     "FLAGS_autotune_range_begin": 0,      # incubate.autotune kernel tuning_range (optimizer-step window)
     "FLAGS_autotune_range_end": 1 << 30,
