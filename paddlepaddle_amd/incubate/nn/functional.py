@@ -612,21 +612,31 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
     positions [0, pos] through the paged flash-decoding kernel. max_enc_len_this_time /
     max_dec_len_this_time (host tensors from blha_get_max_len) skip a phase that has no tokens; without
     them both run and the per-token result is selected on the device.
-    Quantized caches, pre-caches, dense masks and quantized outputs raise NotImplementedError."""
-    unsupported = {"pre_key_cache": pre_key_cache, "pre_value_cache": pre_value_cache,
-                   "cache_k_quant_scales": cache_k_quant_scales, "cache_v_quant_scales": cache_v_quant_scales,
-                   "cache_k_dequant_scales": cache_k_dequant_scales,
-                   "cache_v_dequant_scales": cache_v_dequant_scales, "mask": mask, "tgt_mask": tgt_mask}
+    Static int8 cache quantisation (cache_k/v_quant_scales, cache_k/v_dequant_scales [kv_heads], uint8 caches): the
+    step's K / V are stored as clip(round(scale * x), min_bound, max_bound) + 128 and read back as
+    (u - 128) * dequant_scale, the current token's own K / V unquantised (reference block_attn.h CacheKernel /
+    mul_pointer_v2); out_scale > 0 gives an int8 output (QuantHelperFunc rounding / bounds). Dynamic cache
+    quantisation, pre-caches and dense masks raise NotImplementedError."""
+    unsupported = {"pre_key_cache": pre_key_cache, "pre_value_cache": pre_value_cache, "mask": mask,
+                   "tgt_mask": tgt_mask}
     for n, val in unsupported.items():
         if val is not None:
             raise NotImplementedError(f"block_multihead_attention: `{n}` is not supported on this backend")
-    if use_dynamic_cachekv_quant or (out_scale is not None and out_scale > 0):
-        raise NotImplementedError("block_multihead_attention: int8 cache / output quantization is not supported")
+    quant_cache = cache_k_quant_scales is not None
+    if use_dynamic_cachekv_quant:
+        raise NotImplementedError("block_multihead_attention: dynamic cache-KV quantisation is not supported")
+    if quant_cache and any(t is None for t in (cache_v_quant_scales, cache_k_dequant_scales,
+                                               cache_v_dequant_scales)):
+        raise ValueError("block_multihead_attention: int8 caches need cache_k/v_quant_scales and "
+                         "cache_k/v_dequant_scales")
     q_all = _t(qkv)
     kc, vc = _t(key_cache), _t(value_cache)
     nb, Hk, bs, D = kc.shape
+    if quant_cache and kc.dtype != torch.uint8:
+        raise ValueError("block_multihead_attention: quantised caches are uint8 (int8 value + 128)")
     if qkv_out_scale is not None:  # int32 GEMM output -> real values
-        cdt = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(compute_dtype, kc.dtype)
+        cdt = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(
+            compute_dtype, kc.dtype if kc.is_floating_point() else torch.bfloat16)
         q_all = (q_all.float() * _t(qkv_out_scale).float().reshape(-1)).to(cdt)
     if qkv_bias is not None:
         q_all = q_all + _t(qkv_bias).reshape(-1)
@@ -654,8 +664,17 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
         k = _rotate_rows(k, cs, sn, bool(use_neox_style))
     bt = _t(block_tables).to(device=dev, dtype=torch.long)
     blk = bt[bid, pos // bs]
-    kc[blk, :, pos % bs] = k.to(kc.dtype)
-    vc[blk, :, pos % bs] = v.to(vc.dtype)
+    adt = kc.dtype if not quant_cache else (q_all.dtype if q_all.is_floating_point() else torch.bfloat16)
+    if quant_cache:
+        def qz(t, sc):  # [T, Hk, D] -> uint8 with a per-kv-head scale
+            z = t.float() * _t(sc).float().reshape(1, -1, 1).to(dev)
+            z = torch.round(z) if int(quant_round_type) == 0 else torch.sign(z) * torch.floor(z.abs() + 0.5)
+            return (z.clamp(float(quant_min_bound), float(quant_max_bound)) + 128.0).to(torch.uint8)
+        kc[blk, :, pos % bs] = qz(k, cache_k_quant_scales)
+        vc[blk, :, pos % bs] = qz(v, cache_v_quant_scales)
+    else:
+        kc[blk, :, pos % bs] = k.to(kc.dtype)
+        vc[blk, :, pos % bs] = v.to(vc.dtype)
     def host(t):  # the hints are host tensors (blha_get_max_len on CPU): reading them never syncs the device
         if t is None:
             return None
@@ -670,7 +689,7 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
     o = None
     if run_prefill:
         mq = max_enc if max_enc else T
-        o_p = _ops.attention.attention(q.to(kc.dtype), k.to(kc.dtype), v.to(kc.dtype), causal=True, cu_seqlens_q=cu,
+        o_p = _ops.attention.attention(q.to(adt), k.to(adt), v.to(adt), causal=True, cu_seqlens_q=cu,
                                        cu_seqlens_k=cu, max_seqlen_q=mq, max_seqlen_k=mq, training=False)
         o = o_p
     if run_decode:
@@ -679,13 +698,21 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
         ml = None
         if max_dec is not None:
             ml = max_dec + 1
-        o_d = _ops.paged_decode_attention(q.to(kc.dtype), kc, vc, bt[bid], lens, max_len=ml)
+        kd, vd = kc, vc
+        if quant_cache:  # dequantised view of the cache; the step's own rows stay exact
+            kd = ((kc.float() - 128.0) * _t(cache_k_dequant_scales).float().reshape(1, -1, 1, 1).to(dev)).to(adt)
+            vd = ((vc.float() - 128.0) * _t(cache_v_dequant_scales).float().reshape(1, -1, 1, 1).to(dev)).to(adt)
+            kd[blk, :, pos % bs] = k.to(adt)
+            vd[blk, :, pos % bs] = v.to(adt)
+        o_d = _ops.paged_decode_attention(q.to(adt), kd, vd, bt[bid], lens, max_len=ml)
         o = o_d if o is None else torch.where(prefill_tok.view(T, 1, 1), o, o_d)
     res = o.to(q_all.dtype).reshape(T, H * D)
     if out_shift is not None:
         res = res + _t(out_shift)
     if out_smooth is not None:
         res = res * _t(out_smooth)
+    if out_scale is not None and float(out_scale) > 0:
+        res = _quant_out(res, out_scale, quant_round_type, quant_max_bound, quant_min_bound)
     return _wrap(res), _wrap(q_all), _wrap(kc), _wrap(vc)
 
 
