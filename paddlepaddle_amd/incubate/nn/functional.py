@@ -492,10 +492,11 @@ def masked_multihead_attention(x, cache_kv=None, bias=None, src_mask=None, cum_o
     (reference QuantHelperFunc rounding / bounds). ``beam_cache_offset`` [batch, beam, max_len]: beam-search KV
     indirection — key / value of step t of row b are read from beam ``beam_cache_offset[b, t]`` of b's batch
     entry (an entry of 0 reads b's own cache, as the reference kernel does, masked_multihead_attention_kernel.cu
-    :423); the result is then (out, cache_kv, beam_cache_offset). The reference's ``cum_offsets`` padding removal
-    is not implemented and raises."""
+    :423); the result is then (out, cache_kv, beam_cache_offset). ``cum_offsets`` raises, as in the reference
+    kernel (masked_multihead_attention_kernel.cu:1061 "does not support cum_offsets")."""
     if cum_offsets is not None:
-        raise NotImplementedError("masked_multihead_attention: cum_offsets is not implemented")
+        raise NotImplementedError("masked_multihead_attention: cum_offsets is not supported (as in the reference "
+                                  "kernel)")
     if compute_dtype not in ("default", "bf16", "fp16", "fp32"):
         raise ValueError(f"compute_dtype must be default / bf16 / fp16 / fp32, got {compute_dtype!r}")
     xt = _t(x)
