@@ -280,51 +280,63 @@ def test_block_mha_rejects_unsupported_args():
 
 
 def test_block_mha_static_int8_cache_and_int8_output():
+    _blha_int8("cpu", torch.float32, 16, 1e-5)
+
+
+@pytest.mark.gpu
+def test_block_mha_static_int8_cache_gpu_bf16():
+    _blha_int8("cuda", torch.bfloat16, 128, 3e-2)
+
+
+def _blha_int8(dev, dt, D, tol):
     """uint8 caches with per-kv-head static scales: stored = clip(round(scale * x)) + 128, read back as
     (u - 128) * dequant_scale (reference block_attn.h); a prefill step then a decode step, compared with the same
     steps over float caches holding the dequantised history, and an int8 output for out_scale > 0."""
     gen = torch.Generator().manual_seed(9)
-    H, Hk, D, bs = 4, 2, 16, 4
+    H, Hk, bs = 4, 2, 4
     W = (H + 2 * Hk) * D
     ksc = torch.tensor([40.0, 60.0])
     vsc = torch.tensor([50.0, 30.0])
     kdq, vdq = 1.0 / ksc, 1.0 / vsc
-    tables = torch.tensor([[0, 1, 2]], dtype=torch.int32)
-    kq = torch.zeros(3, Hk, bs, D, dtype=torch.uint8)
+    tables = torch.tensor([[0, 1, 2]], dtype=torch.int32, device=dev)
+    kq = torch.zeros(3, Hk, bs, D, dtype=torch.uint8, device=dev)
     vq = torch.zeros_like(kq)
-    kf = torch.zeros(3, Hk, bs, D)
+    kf = torch.zeros(3, Hk, bs, D, device=dev, dtype=dt)
     vf = torch.zeros_like(kf)
+    ksc, vsc, kdq, vdq = (t.to(dev) for t in (ksc, vsc, kdq, vdq))
     P = paddle.to_tensor
 
     def step(x, enc, dec, quant, out_scale=-1):
         n = x.shape[0]
-        cu = torch.tensor([0, n], dtype=torch.int32)
+        x = x.to(dev, dt)
+        cu = torch.tensor([0, n], dtype=torch.int32, device=dev)
         kc, vc = (kq, vq) if quant else (kf, vf)
         extra = dict(cache_k_quant_scales=P(ksc), cache_v_quant_scales=P(vsc), cache_k_dequant_scales=P(kdq),
                      cache_v_dequant_scales=P(vdq)) if quant else {}
         out, _, _, _ = IF.block_multihead_attention(
-            P(x), P(kc), P(vc), P(torch.tensor([enc], dtype=torch.int32)), P(torch.tensor([dec], dtype=torch.int32)),
-            P(torch.tensor([n], dtype=torch.int32)), None, None, P(cu), P(cu), P(tables), block_size=bs,
-            out_scale=out_scale, **extra)
-        return out._t
+            P(x), P(kc), P(vc), P(torch.tensor([enc], dtype=torch.int32, device=dev)),
+            P(torch.tensor([dec], dtype=torch.int32, device=dev)), P(torch.tensor([n], dtype=torch.int32, device=dev)),
+            None, None, P(cu), P(cu), P(tables), block_size=bs, out_scale=out_scale, **extra)
+        return out._t.cpu()
 
-    x1 = torch.randn(5, W, generator=gen) * 0.5
+    x1 = (torch.randn(5, W, generator=gen) * 0.5).to(dt)
     o_q = step(x1, 5, 0, True)
     o_f = step(x1, 5, 0, False)
-    np.testing.assert_allclose(o_q.numpy(), o_f.numpy(), rtol=1e-5, atol=1e-5)  # prefill reads no cache
-    k1 = x1.view(5, H + 2 * Hk, D)[:, H:H + Hk]
-    exp = (torch.sign(k1 * ksc.view(1, -1, 1)) * torch.floor((k1 * ksc.view(1, -1, 1)).abs() + 0.5)).clamp(-127, 127)
-    got = kq.view(-1, Hk, bs, D)[torch.tensor([0, 0, 0, 0, 1]), :, torch.tensor([0, 1, 2, 3, 0])].float() - 128
+    np.testing.assert_allclose(o_q.float().numpy(), o_f.float().numpy(), rtol=tol, atol=tol)  # prefill: no cache read
+    k1 = x1.float().view(5, H + 2 * Hk, D)[:, H:H + Hk]
+    ks = ksc.cpu().view(1, -1, 1)
+    exp = (torch.sign(k1 * ks) * torch.floor((k1 * ks).abs() + 0.5)).clamp(-127, 127)
+    got = kq.cpu().view(-1, Hk, bs, D)[torch.tensor([0, 0, 0, 0, 1]), :, torch.tensor([0, 1, 2, 3, 0])].float() - 128
     np.testing.assert_array_equal(got.numpy(), exp.numpy())
     # float caches holding what the quantised ones hold, then one decode step on each
     kf.copy_((kq.float() - 128) * kdq.view(1, -1, 1, 1))
     vf.copy_((vq.float() - 128) * vdq.view(1, -1, 1, 1))
-    x2 = torch.randn(1, W, generator=gen) * 0.5
+    x2 = (torch.randn(1, W, generator=gen) * 0.5).to(dt)
     o_q = step(x2, 0, 5, True)
     o_f = step(x2, 0, 5, False)
-    np.testing.assert_allclose(o_q.numpy(), o_f.numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(o_q.float().numpy(), o_f.float().numpy(), rtol=tol, atol=tol)
     # int8 output
-    x3 = torch.randn(1, W, generator=gen) * 0.5
+    x3 = (torch.randn(1, W, generator=gen) * 0.5).to(dt)
     o_i8 = step(x3, 0, 6, True, out_scale=0.5)
     assert o_i8.dtype == torch.int8
 
