@@ -616,16 +616,18 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
     Static int8 cache quantisation (cache_k/v_quant_scales, cache_k/v_dequant_scales [kv_heads], uint8 caches): the
     step's K / V are stored as clip(round(scale * x), min_bound, max_bound) + 128 and read back as
     (u - 128) * dequant_scale, the current token's own K / V unquantised (reference block_attn.h CacheKernel /
-    mul_pointer_v2); out_scale > 0 gives an int8 output (QuantHelperFunc rounding / bounds). Dynamic cache
-    quantisation, pre-caches and dense masks raise NotImplementedError."""
+    mul_pointer_v2); ``use_dynamic_cachekv_quant``: the scales are computed from the step (127 / max|x| per kv head
+    over its tokens) into the [batch, kv_heads] rows of the prefilling sequences, decode reads row 0
+    (quant_write_cache_int8_kernel). out_scale > 0 gives an int8 output (QuantHelperFunc rounding / bounds).
+    Pre-caches and dense masks raise NotImplementedError."""
     unsupported = {"pre_key_cache": pre_key_cache, "pre_value_cache": pre_value_cache, "mask": mask,
                    "tgt_mask": tgt_mask}
     for n, val in unsupported.items():
         if val is not None:
             raise NotImplementedError(f"block_multihead_attention: `{n}` is not supported on this backend")
     quant_cache = cache_k_quant_scales is not None
-    if use_dynamic_cachekv_quant:
-        raise NotImplementedError("block_multihead_attention: dynamic cache-KV quantisation is not supported")
+    if use_dynamic_cachekv_quant and not quant_cache:
+        raise ValueError("block_multihead_attention: dynamic cache-KV quantisation needs the scale tensors")
     if quant_cache and any(t is None for t in (cache_v_quant_scales, cache_k_dequant_scales,
                                                cache_v_dequant_scales)):
         raise ValueError("block_multihead_attention: int8 caches need cache_k/v_quant_scales and "
@@ -667,12 +669,32 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
     blk = bt[bid, pos // bs]
     adt = kc.dtype if not quant_cache else (q_all.dtype if q_all.is_floating_point() else torch.bfloat16)
     if quant_cache:
-        def qz(t, sc):  # [T, Hk, D] -> uint8 with a per-kv-head scale
-            z = t.float() * _t(sc).float().reshape(1, -1, 1).to(dev)
+        def qz(t, sc):  # [T, Hk, D] -> uint8 with per-token per-kv-head scales sc [T, Hk]
+            z = t.float() * sc.unsqueeze(-1)
             z = torch.round(z) if int(quant_round_type) == 0 else torch.sign(z) * torch.floor(z.abs() + 0.5)
             return (z.clamp(float(quant_min_bound), float(quant_max_bound)) + 128.0).to(torch.uint8)
-        kc[blk, :, pos % bs] = qz(k, cache_k_quant_scales)
-        vc[blk, :, pos % bs] = qz(v, cache_v_quant_scales)
+        sk, sv = _t(cache_k_quant_scales), _t(cache_v_quant_scales)
+        if use_dynamic_cachekv_quant:
+            # reference block_attn.h quant_write_cache_int8_kernel: per kv head, scale = 127 / max|x| over the
+            # step's tokens, stored (with 1 / scale) in the [batch, kv_heads] rows of the prefilling sequences;
+            # prefill tokens use their sequence's row, decode tokens (and the decode reads) row 0
+            dk, dv = _t(cache_k_dequant_scales), _t(cache_v_dequant_scales)
+            pre = enc > 0
+            for t, s_, d_ in ((k, sk, dk), (v, sv, dv)):
+                amax = t.float().abs().amax(dim=(0, 2)).clamp_min(1e-20)        # [Hk]
+                rows = s_.view(-1, Hk)
+                upd = pre.view(-1, 1)[:rows.shape[0]]
+                rows.copy_(torch.where(upd, (127.0 / amax).to(rows.dtype).view(1, -1), rows))
+                dr = d_.view(-1, Hk)
+                dr.copy_(torch.where(upd, (amax / 127.0).to(dr.dtype).view(1, -1), dr))
+            tok_pre = pre[bid].view(T, 1)
+            ksc_t = torch.where(tok_pre, sk.view(-1, Hk).float()[bid], sk.view(-1, Hk).float()[0].view(1, -1))
+            vsc_t = torch.where(tok_pre, sv.view(-1, Hk).float()[bid], sv.view(-1, Hk).float()[0].view(1, -1))
+        else:
+            ksc_t = sk.float().reshape(1, -1).to(dev).expand(T, Hk)
+            vsc_t = sv.float().reshape(1, -1).to(dev).expand(T, Hk)
+        kc[blk, :, pos % bs] = qz(k, ksc_t)
+        vc[blk, :, pos % bs] = qz(v, vsc_t)
     else:
         kc[blk, :, pos % bs] = k.to(kc.dtype)
         vc[blk, :, pos % bs] = v.to(vc.dtype)
@@ -701,8 +723,10 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
             ml = max_dec + 1
         kd, vd = kc, vc
         if quant_cache:  # dequantised view of the cache; the step's own rows stay exact
-            kd = ((kc.float() - 128.0) * _t(cache_k_dequant_scales).float().reshape(1, -1, 1, 1).to(dev)).to(adt)
-            vd = ((vc.float() - 128.0) * _t(cache_v_dequant_scales).float().reshape(1, -1, 1, 1).to(dev)).to(adt)
+            kdq = _t(cache_k_dequant_scales).float().reshape(-1, Hk)[0].to(dev)  # dynamic: row 0, as the reference
+            vdq = _t(cache_v_dequant_scales).float().reshape(-1, Hk)[0].to(dev)
+            kd = ((kc.float() - 128.0) * kdq.view(1, -1, 1, 1)).to(adt)
+            vd = ((vc.float() - 128.0) * vdq.view(1, -1, 1, 1)).to(adt)
             kd[blk, :, pos % bs] = k.to(adt)
             vd[blk, :, pos % bs] = v.to(adt)
         o_d = _ops.paged_decode_attention(q.to(adt), kd, vd, bt[bid], lens, max_len=ml)

@@ -271,12 +271,53 @@ def test_block_mha_rejects_unsupported_args():
                                      z, z, z + 1, None, None, paddle.to_tensor(np.array([0, 1], "int32")),
                                      paddle.to_tensor(np.array([0, 1], "int32")), paddle.zeros([1, 2], "int32"),
                                      pre_key_cache=paddle.zeros([1, 1, 2, 16]))
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(ValueError):
         IF.block_multihead_attention(paddle.zeros([1, 48]), paddle.zeros([2, 1, 4, 16], "uint8"),
                                      paddle.zeros([2, 1, 4, 16], "uint8"), z, z, z + 1, None, None,
                                      paddle.to_tensor(np.array([0, 1], "int32")),
                                      paddle.to_tensor(np.array([0, 1], "int32")), paddle.zeros([1, 2], "int32"),
                                      cache_k_quant_scales=paddle.ones([1]), use_dynamic_cachekv_quant=True)
+
+
+def test_block_mha_dynamic_int8_cache():
+    """use_dynamic_cachekv_quant: the prefill step sets scale = 127 / max|k| per kv head (over the step's tokens)
+    in the [batch, kv_heads] scale rows, stores round(scale * k) + 128, and the decode step reads the cache with
+    row 0's dequant scales (reference quant_write_cache_int8_kernel / blha)."""
+    gen = torch.Generator().manual_seed(5)
+    H, Hk, D, bs = 4, 2, 16, 4
+    W = (H + 2 * Hk) * D
+    kq = torch.zeros(3, Hk, bs, D, dtype=torch.uint8)
+    vq = torch.zeros_like(kq)
+    sk, sv, dk, dv = (torch.zeros(1, Hk) for _ in range(4))
+    P = paddle.to_tensor
+    tables = torch.tensor([[0, 1, 2]], dtype=torch.int32)
+
+    def step(x, enc, dec, kc, vc, quant):
+        n = x.shape[0]
+        cu = torch.tensor([0, n], dtype=torch.int32)
+        extra = dict(cache_k_quant_scales=P(sk), cache_v_quant_scales=P(sv), cache_k_dequant_scales=P(dk),
+                     cache_v_dequant_scales=P(dv), use_dynamic_cachekv_quant=True) if quant else {}
+        out, _, _, _ = IF.block_multihead_attention(
+            P(x), P(kc), P(vc), P(torch.tensor([enc], dtype=torch.int32)), P(torch.tensor([dec], dtype=torch.int32)),
+            P(torch.tensor([n], dtype=torch.int32)), None, None, P(cu), P(cu), P(tables), block_size=bs, **extra)
+        return out._t
+
+    x1 = torch.randn(5, W, generator=gen)
+    step(x1, 5, 0, kq, vq, True)
+    k1 = x1.view(5, H + 2 * Hk, D)[:, H:H + Hk]
+    amax = k1.abs().amax(dim=(0, 2))
+    np.testing.assert_allclose(sk[0].numpy(), (127.0 / amax).numpy(), rtol=1e-6)
+    np.testing.assert_allclose(dk[0].numpy(), (amax / 127.0).numpy(), rtol=1e-6)
+    z = k1 * sk.view(1, -1, 1)
+    exp = (torch.sign(z) * torch.floor(z.abs() + 0.5)).clamp(-127, 127)
+    got = kq[torch.tensor([0, 0, 0, 0, 1]), :, torch.tensor([0, 1, 2, 3, 0])].float() - 128
+    np.testing.assert_array_equal(got.numpy(), exp.numpy())
+    kf = (kq.float() - 128) * dk.view(1, -1, 1, 1)
+    vf = (vq.float() - 128) * dv.view(1, -1, 1, 1)
+    x2 = torch.randn(1, W, generator=gen)
+    o_q = step(x2, 0, 5, kq, vq, True)
+    o_f = step(x2, 0, 5, kf, vf, False)
+    np.testing.assert_allclose(o_q.numpy(), o_f.numpy(), rtol=1e-5, atol=1e-5)
 
 
 def test_block_mha_static_int8_cache_and_int8_output():
