@@ -619,12 +619,13 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
     mul_pointer_v2); ``use_dynamic_cachekv_quant``: the scales are computed from the step (127 / max|x| per kv head
     over its tokens) into the [batch, kv_heads] rows of the prefilling sequences, decode reads row 0
     (quant_write_cache_int8_kernel). out_scale > 0 gives an int8 output (QuantHelperFunc rounding / bounds).
-    Pre-caches and dense masks raise NotImplementedError."""
-    unsupported = {"pre_key_cache": pre_key_cache, "pre_value_cache": pre_value_cache, "mask": mask,
-                   "tgt_mask": tgt_mask}
-    for n, val in unsupported.items():
-        if val is not None:
-            raise NotImplementedError(f"block_multihead_attention: `{n}` is not supported on this backend")
+    pre_key_cache / pre_value_cache [B, kv_heads, P, D] (prefix caches): a prefilling sequence's cache positions
+    0 .. P-1 receive them and its tokens start at P; its attention covers the prefix plus its tokens, causal
+    (bottom-right) or through the additive ``mask`` [B, 1, S, P + S] when given; decode tokens with ``tgt_mask``
+    [B, 1, 1, L] add it over their cache positions. The masked / prefixed phases run a math path (per-sequence
+    lengths read on the host), the others the HIP kernels."""
+    if (pre_key_cache is None) != (pre_value_cache is None):
+        raise ValueError("block_multihead_attention: pre_key_cache and pre_value_cache go together")
     quant_cache = cache_k_quant_scales is not None
     if use_dynamic_cachekv_quant and not quant_cache:
         raise ValueError("block_multihead_attention: dynamic cache-KV quantisation needs the scale tensors")
@@ -654,7 +655,9 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
     bid = torch.searchsorted(cu[1:].contiguous(), tok, right=True).clamp_(max=B - 1)
     dec = _t(seq_lens_decoder).reshape(-1).to(device=dev, dtype=torch.long)
     enc = _t(seq_lens_encoder).reshape(-1).to(device=dev, dtype=torch.long)
-    pos = tok - cu[bid] + dec[bid]
+    pk, pv = _t(pre_key_cache), _t(pre_value_cache)
+    P = pk.shape[2] if pk is not None else 0
+    pos = tok - cu[bid] + dec[bid] + P
     rope = _t(rope_emb)
     if rope is not None:  # [2, B|1, max_len, 1, D//2 | D] (cos, sin)
         cos = rope[0].reshape(rope.shape[1], rope.shape[2], -1)
@@ -667,6 +670,14 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
         k = _rotate_rows(k, cs, sn, bool(use_neox_style))
     bt = _t(block_tables).to(device=dev, dtype=torch.long)
     blk = bt[bid, pos // bs]
+    if P:  # prefix caches into positions 0 .. P-1 of the prefilling sequences
+        pb = torch.nonzero(enc > 0).reshape(-1)
+        pp = torch.arange(P, device=dev)
+        pblk = bt[pb.view(-1, 1), (pp // bs).view(1, -1)]                      # [nb_pre, P]
+        for cache, src in ((kc, pk), (vc, pv)):
+            vals = src[pb].permute(0, 2, 1, 3).to(dev)                             # [nb_pre, P, Hk, D]
+            if not quant_cache:
+                cache[pblk, :, (pp % bs).view(1, -1)] = vals.to(cache.dtype)
     adt = kc.dtype if not quant_cache else (q_all.dtype if q_all.is_floating_point() else torch.bfloat16)
     if quant_cache:
         def qz(t, sc):  # [T, Hk, D] -> uint8 with per-token per-kv-head scales sc [T, Hk]
@@ -695,6 +706,13 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
             vsc_t = sv.float().reshape(1, -1).to(dev).expand(T, Hk)
         kc[blk, :, pos % bs] = qz(k, ksc_t)
         vc[blk, :, pos % bs] = qz(v, vsc_t)
+        if P:
+            for cache, src, sc in ((kc, pk, sk), (vc, pv, sv)):
+                rows = sc.float().reshape(-1, Hk).to(dev)
+                srow = rows[pb] if rows.shape[0] > 1 else rows.expand(pb.numel(), Hk)  # [nb_pre, Hk]
+                vals = src[pb].permute(0, 2, 1, 3).to(dev)                                 # [nb_pre, P, Hk, D]
+                cache[pblk, :, (pp % bs).view(1, -1)] = qz(vals.reshape(-1, Hk, D),
+                                                           srow.repeat_interleave(P, 0)).view(vals.shape)
     else:
         kc[blk, :, pos % bs] = k.to(kc.dtype)
         vc[blk, :, pos % bs] = v.to(vc.dtype)
@@ -710,7 +728,9 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
     run_decode = max_dec is None or max_dec > 0
     prefill_tok = enc[bid] > 0
     o = None
-    if run_prefill:
+    if run_prefill and (P or mask is not None):
+        o = _blha_prefill_math(q.to(adt), k.to(adt), v.to(adt), cu, enc, pk, pv, _t(mask))
+    elif run_prefill:
         mq = max_enc if max_enc else T
         o_p = _ops.attention.attention(q.to(adt), k.to(adt), v.to(adt), causal=True, cu_seqlens_q=cu,
                                        cu_seqlens_k=cu, max_seqlen_q=mq, max_seqlen_k=mq, training=False)
@@ -729,7 +749,10 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
             vd = ((vc.float() - 128.0) * vdq.view(1, -1, 1, 1)).to(adt)
             kd[blk, :, pos % bs] = k.to(adt)
             vd[blk, :, pos % bs] = v.to(adt)
-        o_d = _ops.paged_decode_attention(q.to(adt), kd, vd, bt[bid], lens, max_len=ml)
+        if tgt_mask is not None:
+            o_d = _blha_decode_math(q.to(adt), kd, vd, bt[bid], lens, _t(tgt_mask)[bid])
+        else:
+            o_d = _ops.paged_decode_attention(q.to(adt), kd, vd, bt[bid], lens, max_len=ml)
         o = o_d if o is None else torch.where(prefill_tok.view(T, 1, 1), o, o_d)
     res = o.to(q_all.dtype).reshape(T, H * D)
     if out_shift is not None:
@@ -739,6 +762,54 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
     if out_scale is not None and float(out_scale) > 0:
         res = _quant_out(res, out_scale, quant_round_type, quant_max_bound, quant_min_bound)
     return _wrap(res), _wrap(q_all), _wrap(kc), _wrap(vc)
+
+
+def _blha_prefill_math(q, k, v, cu, enc, pk, pv, mask):
+    """Prefill attention of the prefilling sequences with prefix caches and / or an additive mask (math path;
+    per-sequence lengths on the host). q [T, H, D], k / v [T, Hk, D]; rows of other sequences stay zero."""
+    T, H, D = q.shape
+    Hk = k.shape[1]
+    o = torch.zeros_like(q)
+    cuh, ench = cu.tolist(), enc.tolist()
+    for b in range(len(cuh) - 1):
+        if ench[b] <= 0:
+            continue
+        s0, s1 = cuh[b], cuh[b + 1]
+        n = s1 - s0
+        kk, vv = k[s0:s1].transpose(0, 1).float(), v[s0:s1].transpose(0, 1).float()    # [Hk, n, D]
+        if pk is not None:
+            kk = torch.cat([pk[b].to(kk.device).float(), kk], 1)
+            vv = torch.cat([pv[b].to(vv.device).float(), vv], 1)
+        L_ = kk.shape[1]
+        P = L_ - n
+        qq = q[s0:s1].transpose(0, 1).float().view(Hk, H // Hk, n, D)
+        sc = torch.einsum("kgnd,kld->kgnl", qq, kk) / math.sqrt(D)
+        if mask is not None:
+            sc = sc + mask[b, 0, :n, :L_].float().to(sc.device)
+        else:
+            keep = torch.arange(L_, device=sc.device)[None] <= (torch.arange(n, device=sc.device)[:, None] + P)
+            sc = sc.masked_fill(~keep, float("-inf"))
+        ob = torch.einsum("kgnl,kld->kgnd", torch.softmax(sc, -1), vv).reshape(H, n, D)
+        o[s0:s1] = ob.transpose(0, 1).to(o.dtype)
+    return o
+
+
+def _blha_decode_math(q, kc, vc, tables, lens, tmask):
+    """Decode attention over the paged cache with an additive [T, 1, 1, L] mask (math path). q [T, H, D]."""
+    T, H, D = q.shape
+    nb, Hk, bs, _ = kc.shape
+    Lmax = tables.shape[1] * bs
+    posi = torch.arange(Lmax, device=q.device)
+    blk = tables[:, posi // bs]                                         # [T, Lmax]
+    kk = kc[blk, :, (posi % bs).view(1, -1)].float()                    # [T, Lmax, Hk, D]
+    vv = vc[blk, :, (posi % bs).view(1, -1)].float()
+    qq = q.float().view(T, Hk, H // Hk, D)
+    sc = torch.einsum("tkgd,tlkd->tkgl", qq, kk) / math.sqrt(D)
+    m = tmask.float().reshape(T, 1, 1, -1)
+    w = min(m.shape[-1], Lmax)
+    sc[..., :w] = sc[..., :w] + m[..., :w]
+    sc = sc.masked_fill(~(posi.view(1, 1, 1, -1) < lens.view(-1, 1, 1, 1)), float("-inf"))
+    return torch.einsum("tkgl,tlkd->tkgd", torch.softmax(sc, -1), vv).reshape(T, H, D).to(q.dtype)
 
 
 def fused_moe(*a, **k):

@@ -266,17 +266,68 @@ def test_block_mha_mixed_prefill_decode_cpu(hints):
 
 def test_block_mha_rejects_unsupported_args():
     z = paddle.zeros([1], dtype="int32")
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(ValueError):
         IF.block_multihead_attention(paddle.zeros([1, 48]), paddle.zeros([2, 1, 4, 16]), paddle.zeros([2, 1, 4, 16]),
                                      z, z, z + 1, None, None, paddle.to_tensor(np.array([0, 1], "int32")),
                                      paddle.to_tensor(np.array([0, 1], "int32")), paddle.zeros([1, 2], "int32"),
-                                     pre_key_cache=paddle.zeros([1, 1, 2, 16]))
+                                     pre_key_cache=paddle.zeros([1, 1, 2, 16]))  # without pre_value_cache
     with pytest.raises(ValueError):
         IF.block_multihead_attention(paddle.zeros([1, 48]), paddle.zeros([2, 1, 4, 16], "uint8"),
                                      paddle.zeros([2, 1, 4, 16], "uint8"), z, z, z + 1, None, None,
                                      paddle.to_tensor(np.array([0, 1], "int32")),
                                      paddle.to_tensor(np.array([0, 1], "int32")), paddle.zeros([1, 2], "int32"),
                                      cache_k_quant_scales=paddle.ones([1]), use_dynamic_cachekv_quant=True)
+
+
+@pytest.mark.parametrize("use_mask", [False, True])
+def test_block_mha_prefix_cache_and_masks(use_mask):
+    """pre_key_cache / pre_value_cache: the prefilling sequence's cache positions 0..P-1 hold the prefix and its
+    tokens attend to prefix + causal tokens (or through an additive mask that says the same); a decode step then
+    attends over prefix + history (+ tgt_mask). Checked against explicit attention."""
+    gen = torch.Generator().manual_seed(13)
+    H, Hk, D, bs, P, n = 4, 2, 16, 4, 3, 5
+    W = (H + 2 * Hk) * D
+    kc = torch.zeros(4, Hk, bs, D)
+    vc = torch.zeros_like(kc)
+    pk, pv = torch.randn(1, Hk, P, D, generator=gen), torch.randn(1, Hk, P, D, generator=gen)
+    tables = torch.tensor([[0, 1, 2, 3]], dtype=torch.int32)
+    Pt = paddle.to_tensor
+
+    def ref(xs, q_rows):
+        full = xs.view(-1, H + 2 * Hk, D)
+        kk = torch.cat([pk[0].transpose(0, 1), full[:, H:H + Hk]], 0)          # [P + L, Hk, D]
+        vv = torch.cat([pv[0].transpose(0, 1), full[:, H + Hk:]], 0)
+        q = full[q_rows, :H]                                                   # [m, H, D]
+        Ltot = kk.shape[0]
+        out = []
+        for i, r in enumerate(q_rows):
+            sc = torch.einsum("hd,lhd->hl", q[i], kk.repeat_interleave(H // Hk, 1)) / D ** 0.5
+            sc[:, P + r + 1:] = float("-inf")
+            out.append(torch.einsum("hl,lhd->hd", torch.softmax(sc, -1), vv.repeat_interleave(H // Hk, 1)))
+        return torch.stack(out).reshape(len(q_rows), H * D)
+
+    x1 = torch.randn(n, W, generator=gen) * 0.5
+    mask = None
+    if use_mask:
+        keep = torch.arange(P + n)[None] <= (torch.arange(n)[:, None] + P)
+        mask = Pt(torch.zeros(1, 1, n, P + n).masked_fill(~keep, -1e4))
+    cu = torch.tensor([0, n], dtype=torch.int32)
+    out, _, _, _ = IF.block_multihead_attention(
+        Pt(x1), Pt(kc), Pt(vc), Pt(torch.tensor([n], dtype=torch.int32)), Pt(torch.tensor([0], dtype=torch.int32)),
+        Pt(torch.tensor([n], dtype=torch.int32)), None, None, Pt(cu), Pt(cu), Pt(tables), pre_key_cache=Pt(pk),
+        pre_value_cache=Pt(pv), mask=mask, block_size=bs)
+    np.testing.assert_allclose(out.numpy(), ref(x1, list(range(n))).numpy(), rtol=1e-4, atol=1e-4)
+    # the prefix sits at cache positions 0..P-1
+    np.testing.assert_allclose(kc[0, :, :P].numpy(), pk[0].numpy(), rtol=0, atol=0)
+    # decode one token at position P + n (dec = n: tokens so far, the prefix offset is added inside)
+    x2 = torch.randn(1, W, generator=gen) * 0.5
+    tgt = Pt(torch.zeros(1, 1, 1, 16)) if use_mask else None
+    cu1 = torch.tensor([0, 1], dtype=torch.int32)
+    out2, _, _, _ = IF.block_multihead_attention(
+        Pt(x2), Pt(kc), Pt(vc), Pt(torch.tensor([0], dtype=torch.int32)), Pt(torch.tensor([n], dtype=torch.int32)),
+        Pt(torch.tensor([1], dtype=torch.int32)), None, None, Pt(cu1), Pt(cu1), Pt(tables), pre_key_cache=Pt(pk),
+        pre_value_cache=Pt(pv), tgt_mask=tgt, block_size=bs)
+    np.testing.assert_allclose(out2.numpy(), ref(torch.cat([x1, x2]), [n]).numpy(), rtol=1e-4, atol=1e-4)
 
 
 def test_block_mha_dynamic_int8_cache():
