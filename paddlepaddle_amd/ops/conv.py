@@ -683,12 +683,13 @@ class _ConvNHWC(torch.autograd.Function):
 
 
 def conv2d_nhwc(x, w, b, stride, pad, dil, bn_stats=None):
+    """NHWC 2-D convolution (groups 1; ``pad`` an int or a per-dimension (ph, pw) pair) with each of its three
+    products on the hand-written kernel or MIOpen, whichever measured faster for the shape. A stride-1 1x1
+    convolution inside ``residual_grad_sink()`` takes over the block's residual gradient (ResidualGradSink).
+    ``bn_stats``: True when the caller knows a training BN consumes the output (fused units), None to learn it
+    (ops/_conv_bn.py)."""
     if not isinstance(pad, int):
         pad = int(pad[0]) if pad[0] == pad[1] else (int(pad[0]), int(pad[1]))
-    """NHWC 2-D convolution (groups 1, symmetric padding) with each of its three products on the hand-written
-    kernel or MIOpen, whichever measured faster for the shape. A stride-1 1x1 convolution inside
-    ``residual_grad_sink()`` takes over the block's residual gradient (ResidualGradSink). ``bn_stats``: True when
-    the caller knows a training BN consumes the output (fused units), None to learn it (ops/_conv_bn.py)."""
     sink = _SINK[0] if (w.shape[2] == 1 and w.shape[3] == 1 and stride == 1) else None
     if sink is not None:
         sink.armed = True
