@@ -4,7 +4,7 @@
 // Layout: x [rows, cols] row-major, cols % 8 == 0. fp32 statistics (mean / rstd per row).
 // Row kernels: one 64-lane wave per row, 4 rows per 256-thread workgroup, each lane keeps VPL
 // 16-byte vectors of its row in registers (so the row is read from HBM exactly once);
-// rows > 8192 wide use a workgroup-per-row two-pass kernel.
+// rows of more than 3072 columns use a workgroup-per-row two-pass kernel (faster in the step, see norm_fwd_wide).
 // Weight/bias gradients are column reductions done by a separate coalesced kernel that writes
 // fp32 partials [nparts, cols] (summed on the host side by one tiny reduction) — no atomics.
 #include "common.h"
@@ -22,6 +22,8 @@ __global__ __launch_bounds__(256) void norm_fwd_rows(const T* __restrict__ x, co
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const T* xr = x + row * cols;
+  // LayerNorm: the mean is summed about the row's first element, so rows with a large mean keep their digits
+  const float sh = LN ? to_f(xr[0]) : 0.f;
   float v[VPL][8];
   float s = 0.f;
 #pragma unroll
@@ -31,16 +33,16 @@ __global__ __launch_bounds__(256) void norm_fwd_rows(const T* __restrict__ x, co
       load8<T>(xr + e, v[k]);
     } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[k][j] = 0.f;
+      for (int j = 0; j < 8; ++j) v[k][j] = LN ? sh : 0.f;
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s += LN ? v[k][j] : v[k][j] * v[k][j];
+    for (int j = 0; j < 8; ++j) s += LN ? v[k][j] - sh : v[k][j] * v[k][j];
   }
   s = wave_sum(s);
   const float inv_n = 1.0f / (float)cols;
   float mu = 0.f, rstd;
   if (LN) {
-    mu = s * inv_n;
+    mu = sh + s * inv_n;
     float s2 = 0.f;
 #pragma unroll
     for (int k = 0; k < VPL; ++k) {
@@ -80,7 +82,11 @@ __global__ __launch_bounds__(256) void norm_fwd_rows(const T* __restrict__ x, co
   }
 }
 
-// wide rows: one 256-thread workgroup per row, two passes over global (second pass hits L2)
+// wide rows (>= 4096 columns): one 256-thread workgroup per row, two passes over global (the second hits L2).
+// Measured in the GPT-3 13B step (5120 columns, operands from HBM): forward 19.5 vs 22.5 us, data gradient 38.8 vs
+// 48.0 us for the wave-per-row kernels (`profiles/norm_rows_vs_wide_r4.md`): a whole workgroup's loads per row in
+// flight instead of one wave's. LayerNorm sums are taken about the row's first element (shifted moments) so the
+// one-pass variance does not cancel for rows with a large mean.
 template <typename T, bool LN>
 __global__ __launch_bounds__(256) void norm_fwd_wide(const T* __restrict__ x, const T* __restrict__ w,
                                                      const T* __restrict__ b, T* __restrict__ y,
@@ -89,20 +95,22 @@ __global__ __launch_bounds__(256) void norm_fwd_wide(const T* __restrict__ x, co
   __shared__ float red[4];
   const int64_t row = blockIdx.x;
   const T* xr = x + row * cols;
+  const float sh = LN ? to_f(xr[0]) : 0.f;
   float s = 0.f, s2 = 0.f;
   for (int64_t e = (int64_t)threadIdx.x * 8; e < cols; e += 256 * 8) {
     float v[8];
     load8<T>(xr + e, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { s += v[j]; s2 += v[j] * v[j]; }
+    for (int j = 0; j < 8; ++j) { const float d = v[j] - sh; s += d; s2 += d * d; }
   }
   const float inv_n = 1.0f / (float)cols;
   float mu = 0.f, rstd;
   if (LN) {
     s = block_sum<256>(s, red);
     s2 = block_sum<256>(s2, red);
-    mu = s * inv_n;
-    rstd = rsqrtf(fmaxf(s2 * inv_n - mu * mu, 0.f) + eps);
+    const float md = s * inv_n;
+    mu = sh + md;
+    rstd = rsqrtf(fmaxf(s2 * inv_n - md * md, 0.f) + eps);
   } else {
     s2 = block_sum<256>(s2, red);
     rstd = rsqrtf(s2 * inv_n + eps);
@@ -250,10 +258,6 @@ int launch_fwd(const void* x, const void* w, const void* b, void* y, float* mean
   else if (vpl <= 3) PA_FWD(3);
   else if (vpl <= 4) PA_FWD(4);
   else if (vpl <= 6) PA_FWD(6);
-  else if (vpl <= 8) PA_FWD(8);
-  else if (vpl <= 10) PA_FWD(10);
-  else if (vpl <= 12) PA_FWD(12);
-  else if (vpl <= 16) PA_FWD(16);
   else hipLaunchKernelGGL((norm_fwd_wide<T, LN>), dim3((unsigned)rows), block, 0, st, X, W, B, Y, mean, rstd, rows, cols, eps);
 #undef PA_FWD
   PA_CHECK_LAUNCH();
@@ -273,8 +277,6 @@ int launch_bwd(const void* dy, const void* x, const void* w, const float* mean, 
   else if (vpl <= 3) PA_BWD(3);
   else if (vpl <= 4) PA_BWD(4);
   else if (vpl <= 6) PA_BWD(6);
-  else if (vpl <= 8) PA_BWD(8);
-  else if (vpl <= 10) PA_BWD(10);
   else hipLaunchKernelGGL((norm_bwd_dx_wide<T, LN>), dim3((unsigned)rows), block, 0, st, DY, X, W, mean, rstd, DX, rows, cols,
                           RES);
 #undef PA_BWD

@@ -50,17 +50,22 @@ def test_rms_norm(dt, cols):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("cols", [256, 5120, 16384])
-def test_layer_norm(dt, cols):
+@pytest.mark.parametrize("cols,shift", [(256, 1.0), (3072, 1.0), (4096, 1.0), (5120, 1.0), (16384, 1.0),
+                                        (5120, 300.0), (3072, 300.0)])
+def test_layer_norm(dt, cols, shift):
+    """Wave-per-row kernels up to 3072 columns, workgroup-per-row kernels above; shift = 300: rows whose mean is
+    large against their spread (the wide kernel's shifted moments must not cancel)."""
     torch.manual_seed(1)
-    x = (torch.randn(29, cols, device=DEV) * 3 + 1).to(dt).requires_grad_(True)
+    x = (torch.randn(29, cols, device=DEV) * 3 + shift).to(dt).requires_grad_(True)
     w = torch.randn(cols, device=DEV).to(dt).requires_grad_(True)
     b = torch.randn(cols, device=DEV).to(dt).requires_grad_(True)
     y = ops.layer_norm(x, w, b, 1e-5)
     _lib_loaded("pa_layer_norm_fwd")
     xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
     yr = F.layer_norm(xr, (cols,), wr, br, 1e-5)
-    torch.testing.assert_close(y.float(), yr, atol=_tol(dt) * 8, rtol=_tol(dt))
+    # forward against a float64 reference (an fp32 LayerNorm of rows with mean 300 is itself ~1e-4 off)
+    y64 = F.layer_norm(xr.detach().double(), (cols,), wr.detach().double(), br.detach().double(), 1e-5)
+    torch.testing.assert_close(y.double(), y64, atol=_tol(dt) * 8, rtol=_tol(dt))
     g = torch.randn_like(yr)
     y.backward(g.to(dt))
     yr.backward(g)
