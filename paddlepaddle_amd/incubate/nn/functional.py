@@ -740,7 +740,7 @@ def block_multihead_attention(qkv, key_cache, value_cache, seq_lens_encoder, seq
         lens = torch.where(prefill_tok, torch.ones_like(pos), pos + 1) if run_prefill else pos + 1
         ml = None
         if max_dec is not None:
-            ml = max_dec + 1
+            ml = max_dec + 1 + P
         kd, vd = kc, vc
         if quant_cache:  # dequantised view of the cache; the step's own rows stay exact
             kdq = _t(cache_k_dequant_scales).float().reshape(-1, Hk)[0].to(dev)  # dynamic: row 0, as the reference

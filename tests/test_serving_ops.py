@@ -323,10 +323,12 @@ def test_block_mha_prefix_cache_and_masks(use_mask):
     x2 = torch.randn(1, W, generator=gen) * 0.5
     tgt = Pt(torch.zeros(1, 1, 1, 16)) if use_mask else None
     cu1 = torch.tensor([0, 1], dtype=torch.int32)
+    hints = dict(max_enc_len_this_time=paddle.to_tensor(np.array([0], "int32"), place=paddle.CPUPlace()),
+                 max_dec_len_this_time=paddle.to_tensor(np.array([n], "int32"), place=paddle.CPUPlace()))
     out2, _, _, _ = IF.block_multihead_attention(
         Pt(x2), Pt(kc), Pt(vc), Pt(torch.tensor([0], dtype=torch.int32)), Pt(torch.tensor([n], dtype=torch.int32)),
         Pt(torch.tensor([1], dtype=torch.int32)), None, None, Pt(cu1), Pt(cu1), Pt(tables), pre_key_cache=Pt(pk),
-        pre_value_cache=Pt(pv), tgt_mask=tgt, block_size=bs)
+        pre_value_cache=Pt(pv), tgt_mask=tgt, block_size=bs, **hints)
     np.testing.assert_allclose(out2.numpy(), ref(torch.cat([x1, x2]), [n]).numpy(), rtol=1e-4, atol=1e-4)
 
 
