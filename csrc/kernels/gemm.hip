@@ -478,7 +478,8 @@ __device__ __forceinline__ void tile_coords(int pid, int tiles_m, int tiles_n, i
   *tn = (pid % per_group) / gsz;
 }
 
-constexpr int kEpiRowStride = 260;  // fp32 per row of the epilogue image (256 + 4 padding)
+constexpr int kEpiRowStride = 260;      // fp32 per row of the epilogue image (256 + 4 padding)
+constexpr int kEpiRowStrideBf16 = 264;  // bf16 per row of the one-pass bf16 epilogue image (528-byte rows)
 
 template <int V>
 struct IntC {
@@ -701,6 +702,51 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p0) {
   // (aux / accumulate read-modify-write) far below the HBM rate.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int flags = p.flags;
+  if (!(flags & (kEpiAux | kEpiAccum | kEpiOutF32))) {
+    // bf16 output without aux / accumulate: alpha, bias and GELU applied in registers, the finished bf16 tile
+    // staged through LDS in one pass ([256][264] bf16, 528-byte rows) instead of two fp32 halves
+    uint16_t* im = reinterpret_cast<uint16_t*>(smem);
+    constexpr int RSB = kEpiRowStrideBf16;
+    bar();
+#pragma unroll
+    for (int bh = 0; bh < 2; ++bh)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = bh * 128 + bc + j * 16 + 4 * (lane >> 4);
+        float bq[4] = {0.f, 0.f, 0.f, 0.f};
+        if ((flags & kEpiBias) && n0 + c < p.N) {
+          const uint2 braw = *reinterpret_cast<const uint2*>(p.bias + n0 + c);
+          bq[0] = lo_bf16(braw.x); bq[1] = hi_bf16(braw.x); bq[2] = lo_bf16(braw.y); bq[3] = hi_bf16(braw.y);
+        }
+#pragma unroll
+        for (int ah = 0; ah < 2; ++ah)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = ah * 128 + ar + i * 16 + (lane & 15);
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[e] = acc[ah][i][bh][j][e] * p.alpha + bq[e];
+              if (flags & kEpiGelu) v[e] = gelu_tanh(v[e]);
+            }
+            *reinterpret_cast<uint2*>(im + r * RSB + c) = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
+          }
+      }
+    bar();
+    const int ecb = (tid & 31) * 8, erb = tid >> 5;
+    const int nb_ = n0 + ecb;
+    if (nb_ < p.N) {
+#pragma unroll 4
+      for (int step = 0; step < 16; ++step) {
+        const int r = step * 16 + erb;
+        const int m = m0 + r;
+        if (m >= p.M) break;
+        *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(p.c) + (int64_t)m * p.ldc + nb_) =
+            *reinterpret_cast<const uint4*>(im + r * RSB + ecb);
+      }
+    }
+    return;
+  }
   float* img = reinterpret_cast<float*>(smem);
   constexpr int RS = kEpiRowStride;  // floats per image row
   const int ec = (tid & 31) * 8;     // this thread's 8 columns of the tile
@@ -1320,7 +1366,8 @@ int launch256(const GemmArgs& a0, int splits, hipStream_t st, int grid = 0) {
     grid = a.tiles_m * a.tiles_n;
     a.tail_split = 0;
   }
-  constexpr int kLoop = 2 * 4 * 128 * kBK * 2, kEpi = 128 * kEpiRowStride * 4;
+  constexpr int kLoop = 2 * 4 * 128 * kBK * 2, kEpi0 = 128 * kEpiRowStride * 4, kEpi1 = 256 * kEpiRowStrideBf16 * 2;
+  constexpr int kEpi = kEpi0 > kEpi1 ? kEpi0 : kEpi1;
   const int smem = kLoop > kEpi ? kLoop : kEpi;
   static bool attr_set = false;
   if (!attr_set) {

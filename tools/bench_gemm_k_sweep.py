@@ -33,9 +33,9 @@ def main():
     while time.time() < t_end:
         torch.mm(w, w)
     torch.cuda.synchronize()
-    shapes = [(4096, 20480, False), (4096, 20480, True), (4096, 5120, False)]
+    shapes = [(4096, 20480, False), (4096, 20480, True), (4096, 5120, False), (32768, 2048, False)]
     if len(sys.argv) > 1:
-        shapes = shapes[:int(sys.argv[1])]
+        shapes = [shapes[int(i)] for i in sys.argv[1].split(",")]
     for (M, N, kmaj_b) in shapes:
         tiles = (M // 256) * (N // 256)
         rows = []
