@@ -340,8 +340,14 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
     beam_cache_offset (math path over the re-gathered cache).
     qkv_weights: [3, H, D, E] (trans_qkvw) or [E, 3, H, D]; with gqa_group_size = kv heads,
     [H + 2*kv_heads, D, E] / [E, H + 2*kv_heads, D]."""
-    if mode != "upscale_in_train" and training and dropout_rate > 0:
-        raise NotImplementedError("fused_multi_transformer: only mode='upscale_in_train' dropout is supported")
+    if mode not in ("upscale_in_train", "downscale_in_infer"):
+        raise ValueError(f"fused_multi_transformer: mode must be upscale_in_train or downscale_in_infer, got {mode!r}")
+
+    def drop_add(t, res):  # residual + dropout(t) in the requested mode
+        if mode == "downscale_in_infer" and dropout_rate > 0:
+            # training: keep mask without rescale (= the upscaling kernel applied to t * (1 - p)); inference: t * (1 - p)
+            return _ops.dropout_add(t * (1.0 - dropout_rate), res, dropout_rate if training else 0.0, training)
+        return _ops.dropout_add(t, res, dropout_rate if training else 0.0, training)
     xt = _t(x)
     B, S, E = xt.shape
     decode = cache_kvs is not None and time_step is not None
@@ -429,8 +435,7 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
         out = _mp_allreduce(out, ring_id)
         if linear_biases is not None and linear_biases[i] is not None:
             out = out + _t(linear_biases[i])
-        out = _ops.dropout_add(out, residual * residual_alpha if residual_alpha != 1.0 else residual,
-                               dropout_rate if training else 0.0, training)
+        out = drop_add(out, residual * residual_alpha if residual_alpha != 1.0 else residual)
         if not pre_layer_norm:
             out = _fmt_norm(out, ln_scales[i], ln_biases[i], epsilon, norm_type)
         residual = out
@@ -441,8 +446,7 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
         f = _mp_allreduce(f, ring_id)
         if ffn2_biases is not None and ffn2_biases[i] is not None:
             f = f + _t(ffn2_biases[i])
-        h = _ops.dropout_add(f, residual * residual_alpha if residual_alpha != 1.0 else residual,
-                             dropout_rate if training else 0.0, training)
+        h = drop_add(f, residual * residual_alpha if residual_alpha != 1.0 else residual)
         if not pre_layer_norm:
             h = _fmt_norm(h, ffn_ln_scales[i], ffn_ln_biases[i], epsilon, norm_type)
     return (_wrap(h), cache_kvs) if cache_kvs is not None else _wrap(h)

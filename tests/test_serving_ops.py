@@ -166,6 +166,28 @@ def test_fused_multi_transformer_beam_offset_equals_reordered_cache():
     np.testing.assert_allclose(out_b.numpy(), out_p.numpy(), rtol=1e-4, atol=1e-4)
 
 
+def test_fused_multi_transformer_downscale_in_infer_mode():
+    """mode='downscale_in_infer': inference scales the dropped branches by (1 - p); training keeps them unscaled
+    where kept (reference fused_transformer.py dropout modes)."""
+    gen = torch.Generator().manual_seed(2)
+    B, S, E, H = 2, 4, 32, 4
+    P = _params(1, E, H, H, 64, gen, False)
+    x = torch.randn(B, S, E, generator=gen)
+    base = _fmt(_T(x), P, "cpu", torch.float32, attn_mask=_T(torch.zeros(B, 1, S, S)))
+    scaled = _fmt(_T(x), P, "cpu", torch.float32, attn_mask=_T(torch.zeros(B, 1, S, S)), dropout_rate=0.25,
+                  mode="downscale_in_infer", training=False)
+    assert not np.allclose(base.numpy(), scaled.numpy())
+    P2 = [dict(p, lin_w=p["lin_w"] * 0.75, lin_b=p["lin_b"] * 0.75, ffn2_w=p["ffn2_w"] * 0.75,
+               ffn2_b=p["ffn2_b"] * 0.75) for p in P]  # (1 - p) on both dropped branches
+    np.testing.assert_allclose(scaled.numpy(), _ref_stack(x, P2, torch.zeros(B, 1, S, S), H, H).numpy(), rtol=1e-4,
+                               atol=1e-4)
+    out = _fmt(_T(x), P, "cpu", torch.float32, attn_mask=_T(torch.zeros(B, 1, S, S)), dropout_rate=0.25,
+               mode="downscale_in_infer", training=True)
+    assert np.isfinite(out.numpy()).all()
+    with pytest.raises(ValueError):
+        _fmt(_T(x), P, "cpu", torch.float32, dropout_rate=0.25, mode="bogus")
+
+
 def test_fused_multi_transformer_layer_returns_caches():
     m = paddle.incubate.nn.FusedMultiTransformer(32, 4, 64, num_layers=2)
     m.eval()
