@@ -148,6 +148,20 @@ class _Slice(torch.autograd.Function):
         return _gather(g, ctx.gr, ctx.dim), None, None
 
 
+class _ToPartial(torch.autograd.Function):
+    """Replicate -> Partial(sum): the group's rank 0 keeps the value, the others contribute zeros (the sum of the
+    parts is the value, exactly). Backward is the identity: the logical tensor's gradient is the (replicated)
+    gradient of the sum."""
+
+    @staticmethod
+    def forward(ctx, x, gr):
+        return x.clone() if _my(gr) == 0 else torch.zeros_like(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
 class _CopyToParallel(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gr):
@@ -404,6 +418,10 @@ class StaticEngine:
                 out = self._new()
                 self._emit(stage, "slice", _Slice.apply, (P._Ref(cur), gr, w[1]), out)
                 cur, pl[d] = out, w
+            elif _is_p(w) and w[1] == "sum" and h == R:
+                out = self._new()
+                self._emit(stage, "to_partial", _ToPartial.apply, (P._Ref(cur), gr), out)
+                cur, pl[d] = out, w
             elif _is_p(w):
                 raise NotImplementedError(f"conversion to a Partial placement ({h} -> {w})")
         self.info[cur] = _Info(self.meshes[stage], pl, shape)
@@ -657,8 +675,8 @@ class StaticEngine:
             elif pw == S(0):
                 want[0][d] = S(xr - 1)
                 out[d] = PSUM()
-                if len(refs) > 2:
-                    raise NotImplementedError("row-parallel linear with a bias")
+                if len(refs) > 2:  # the bias joins the partial sum once (rank 0 of the group)
+                    want[2][d] = PSUM()
             else:
                 want[1][d] = R
                 want[0][d] = R
