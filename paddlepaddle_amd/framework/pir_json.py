@@ -518,11 +518,10 @@ def _flash_attn(ins, a):
     from .program_desc import _qkvpacked
     from ..ops import attention as _att
     from .tensor import _wrap
-    if len(ins) > 4 and ins[4] is not None:
-        raise NotImplementedError("flash_attn with attn_mask")
+    mask = ins[4]._t if len(ins) > 4 and ins[4] is not None else None  # additive / boolean [B|1, H|1, Sq, Sk]
     q, k, v = ins[0], ins[1], ins[2]
-    return [_wrap(_att.flash_attention(q._t, k._t, v._t, causal=bool(a.get("causal", False)), dropout=0.0,
-                                       training=False))]
+    return [_wrap(_att.flash_attention(q._t, k._t, v._t, causal=bool(a.get("causal", False)), mask=mask,
+                                       dropout=0.0, training=False))]
 
 
 _RUN = {

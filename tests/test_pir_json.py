@@ -138,3 +138,18 @@ def test_native_interpreter_matches_python_replay(tmp_path):
         np.testing.assert_allclose(x, r, rtol=1e-5, atol=1e-5)
     it = native.interp
     assert it.num_instructions > 10 and it.releases > 0 and it.peak_live < it.num_instructions
+
+
+def test_pir_flash_attn_with_attn_mask_replays():
+    """pd_op.flash_attn with its attn_mask input (5th operand) replays through the masked attention kernel."""
+    import torch
+    import paddlepaddle_amd as paddle
+    from paddlepaddle_amd.framework import pir_json as PJ
+    g = torch.Generator().manual_seed(0)
+    q, k, v = (torch.randn(2, 5, 2, 8, generator=g) for _ in range(3))
+    m = torch.randn(2, 1, 5, 5, generator=g)
+    out = PJ._flash_attn([paddle.to_tensor(q), paddle.to_tensor(k), paddle.to_tensor(v), None, paddle.to_tensor(m)],
+                         {"causal": False})[0]
+    s = torch.einsum("bqhd,bkhd->bhqk", q, k) / 8 ** 0.5 + m
+    ref = torch.einsum("bhqk,bkhd->bqhd", torch.softmax(s, -1), v)
+    assert (out._t - ref).abs().max().item() < 1e-5
