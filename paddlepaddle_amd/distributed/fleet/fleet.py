@@ -178,9 +178,12 @@ class _Fleet:
             self.init()
             hcg = self._hcg
         mode = hcg.get_parallel_mode()
+        if mode == ParallelMode.SEGMENT_PARALLEL and hcg.get_sharding_parallel_world_size() > 1:
+            # sep x sharding: the sharding engine partitions the state and also sums the shard gradients over
+            # the sep group (ShardingHybridModel.build_engine)
+            self._sharded_model = ShardingHybridModel(model, hcg, self._strategy)
+            return self._sharded_model
         if mode == ParallelMode.SEGMENT_PARALLEL:
-            if hcg.get_sharding_parallel_world_size() > 1:
-                raise NotImplementedError("segment parallel combined with sharding is not supported")
             from ...parallel.segment_parallel import SegmentParallel
             return SegmentParallel(model, hcg, self._strategy)
         if hcg.get_sharding_parallel_world_size() > 1 and mode != ParallelMode.PIPELINE_PARALLEL:
@@ -313,9 +316,10 @@ class ShardingHybridModel(_Layer):
     def build_engine(self, optimizer, stage=None):
         from ...parallel.sharding import GroupShardedEngine, GroupShardedOptimizer
         hcg = self._hcg
+        sep = hcg.get_sep_parallel_group() if hasattr(hcg, "get_sep_parallel_group") else None
         eng = GroupShardedEngine(self._layers, optimizer, stage or _sharding_stage(self._strategy),
                                  hcg.get_sharding_parallel_group(), mp_group=hcg.get_model_parallel_group(),
-                                 dp_group=hcg.get_data_parallel_group())
+                                 dp_group=hcg.get_data_parallel_group(), sep_group=sep)
         object.__setattr__(self, "_engine", eng)
         return GroupShardedOptimizer(eng)
 

@@ -168,7 +168,7 @@ class GroupShardedEngine:
     """Implements stage 1/2/3 over a model + inner optimizer."""
 
     def __init__(self, model, optimizer, stage, group=None, decay_fn=None, mp_group=None, dp_group=None,
-                 keep_params=None, pp_group=None, offload=False):
+                 keep_params=None, pp_group=None, offload=False, sep_group=None):
         self.model = model
         self.offload = bool(offload)
         self._copy_stream = None
@@ -181,6 +181,9 @@ class GroupShardedEngine:
         self.mp_group = mp_group if (mp_group is not None and getattr(mp_group, "nranks", 1) > 1) else None
         self.dp_group = dp_group if (dp_group is not None and getattr(dp_group, "nranks", 1) > 1) else None
         self.pp_group = pp_group if (pp_group is not None and getattr(pp_group, "nranks", 1) > 1) else None
+        # segment parallel (sep): the sep ranks hold the same shards for different sequence segments, so their
+        # shard gradients are summed over the sep group (reference: sep gradients are not averaged)
+        self.sep_group = sep_group if (sep_group is not None and getattr(sep_group, "nranks", 1) > 1) else None
         self._keep_override = keep_params
         self.world = C.get_world_size(group)
         self.rank = C.get_rank(group) if group is not None else (dist.get_rank() if dist.is_initialized() else 0)
@@ -244,9 +247,10 @@ class GroupShardedEngine:
                 src = self.group.ranks[0] if self.group is not None else 0
                 for p in self.model.parameters():
                     dist.broadcast(p._t.data, src=src, group=self.pg)
-            if self.dp_group is not None:  # replicas of the sharded state start identical
-                for p in self.model.parameters():
-                    dist.broadcast(p._t.data, src=self.dp_group.ranks[0], group=self.dp_group.process_group)
+            for og in (self.dp_group, self.sep_group):  # replicas of the sharded state start identical
+                if og is not None:
+                    for p in self.model.parameters():
+                        dist.broadcast(p._t.data, src=og.ranks[0], group=og.process_group)
 
     def _build_units(self, decay_fn):
         unit_layers = []
@@ -471,6 +475,8 @@ class GroupShardedEngine:
                 if sp_mp and getattr(f, "sequence_parallel", False):
                     sp.append(f.shard._t.grad)  # reduced below as one flat over mp, then dp
                     continue
+                if self.sep_group is not None:  # summed over the sequence segments before the dp average
+                    dist.all_reduce(f.shard._t.grad, group=self.sep_group.process_group)
                 if self.dp_group is not None:  # replicas of this shard: average across the outer dp group
                     g = f.shard._t.grad
                     g.mul_(1.0 / self.dp_group.nranks)
@@ -482,6 +488,8 @@ class GroupShardedEngine:
             # ever reads a buffer another one is still writing.
             flat = torch.cat([g.reshape(-1).float() for g in sp])
             dist.all_reduce(flat, group=self.mp_group.process_group)
+            if self.sep_group is not None:
+                dist.all_reduce(flat, group=self.sep_group.process_group)
             if self.dp_group is not None:
                 flat.mul_(1.0 / self.dp_group.nranks)
                 dp_work.append(dist.all_reduce(flat, group=self.dp_group.process_group, async_op=True))

@@ -509,6 +509,56 @@ def test_llama_segment_parallel_matches_single_process():
         np.testing.assert_allclose(l, ref, rtol=1e-4, atol=1e-5)
 
 
+def _sep_sharding_worker(rank, world, port, q):
+    """sep 2 x sharding 2 (stage 2): the batch split over the sharding ranks, the sequence over the sep ranks;
+    the sharding engine sums the shard gradients over sep and averages them over sharding."""
+    paddle = _setup(rank, world, port)
+    from paddlepaddle_amd.models.llama import LlamaConfig, LlamaForCausalLM, LlamaPretrainingCriterion
+    from paddlepaddle_amd.parallel.segment_parallel import split_sequence
+    fleet = _fleet_init(paddle, sep_degree=2, sharding_degree=2)
+    fleet.fleet._strategy.sharding_configs["stage"] = 2
+    hcg = fleet.get_hybrid_communicate_group()
+    paddle.seed(4)
+    cfg = LlamaConfig.tiny(sep_parallel_degree=2)
+    model, crit = LlamaForCausalLM(cfg), LlamaPretrainingCriterion(cfg)
+    opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    model = fleet.distributed_model(model)
+    opt = fleet.distributed_optimizer(opt)
+    g = hcg.get_sep_parallel_group()
+    ids = _data(cfg)
+    per = ids.shape[0] // 2
+    sr = hcg.get_sharding_parallel_rank()
+    part = ids[sr * per:(sr + 1) * per]
+    x = split_sequence(paddle.Tensor(part[:, :-1]), g)
+    y = split_sequence(paddle.Tensor(part[:, 1:]), g)
+    losses = []
+    for _ in range(3):
+        loss = crit(model(x), y) * 0.5
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        t = loss._t.detach().clone()
+        paddle.distributed.all_reduce(paddle.Tensor(t), group=g)
+        losses.append(float(t))
+    q.put((rank, losses))
+    paddle.distributed.barrier()
+
+
+def test_llama_segment_parallel_x_sharding_matches_single_process():
+    sys.path.insert(0, ROOT)
+    os.environ["PADDLE_AMD_FORCE_CPU"] = "1"
+    import paddlepaddle_amd as paddle
+    from paddlepaddle_amd.models.llama import LlamaConfig, LlamaForCausalLM, LlamaPretrainingCriterion
+    paddle.seed(4)
+    cfg = LlamaConfig.tiny()
+    model, crit = LlamaForCausalLM(cfg), LlamaPretrainingCriterion(cfg)
+    opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    ref = _train(paddle, model, crit, opt, _data(cfg))
+    res = _spawn(_sep_sharding_worker, world=4)
+    mean = np.mean([l for _, l in res], axis=0)  # the two sharding ranks' halves of the batch
+    np.testing.assert_allclose(mean, ref, rtol=1e-4, atol=1e-5)
+
+
 def test_segment_all_to_all_roundtrip_single_process():
     """seq_to_head / head_to_seq are inverse layouts (checked with a fake 1-rank group: identity)."""
     from paddlepaddle_amd.parallel.segment_parallel import head_to_seq, seq_to_head
