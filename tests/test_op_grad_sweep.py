@@ -277,6 +277,43 @@ def _table():
         ("sigmoid_focal", lambda x: F.sigmoid_focal_loss(x, paddle.to_tensor(BIN34)),
          [u(3, 4)], {}, None),
         ("huber", lambda a, b: paddle.nn.functional.smooth_l1_loss(a, b, delta=0.5), [u(3, 4), u(3, 4) * 2], {}, None),
+        # round 4 additions: linear algebra compositions, scans, pooling variants, shape ops
+        ("addmm", lambda c, a, b: paddle.addmm(c, a, b, beta=0.5, alpha=2.0), [u(3, 5), u(3, 4), u(4, 5)], {},
+         lambda c, a, b: 0.5 * c + 2.0 * a @ b),
+        ("einsum", lambda a, b: paddle.einsum("ij,jk->ik", a, b), [u(3, 4), u(4, 2)], {}, lambda a, b: a @ b),
+        ("tensordot", lambda a, b: paddle.tensordot(a, b, axes=1), [u(3, 4), u(4, 2)], {}, lambda a, b: a @ b),
+        ("diff", lambda x: paddle.diff(x, axis=1), [u(3, 5)], {}, lambda x: np.diff(x, axis=1)),
+        ("trapezoid", lambda x: paddle.trapezoid(x, dx=0.5, axis=1), [u(3, 5)], {}, None),
+        ("cumulative_trapezoid", lambda x: paddle.cumulative_trapezoid(x, dx=0.5, axis=1), [u(3, 5)], {}, None),
+        ("nansum", lambda x: paddle.nansum(x, axis=1), [u(3, 4)], {}, lambda x: np.nansum(x, 1)),
+        ("nanmean", lambda x: paddle.nanmean(x, axis=0), [u(3, 4)], {}, lambda x: np.nanmean(x, 0)),
+        ("renorm", lambda x: paddle.renorm(x, 2.0, 0, 0.5), [u(3, 4) * 2], {}, None),
+        ("diag_embed", lambda x: paddle.diag_embed(x), [u(2, 3)], {}, None),
+        ("hstack", lambda a, b: paddle.hstack([a, b]), [u(3, 2), u(3, 4)], {}, lambda a, b: np.hstack([a, b])),
+        ("vstack", lambda a, b: paddle.vstack([a, b]), [u(2, 4), u(3, 4)], {}, lambda a, b: np.vstack([a, b])),
+        ("index_fill", lambda x: paddle.index_fill(x, paddle.to_tensor([0, 2]), 1, 0.5), [u(3, 4)], {}, None),
+        ("copysign", lambda a: paddle.copysign(a, paddle.to_tensor(SIGN34)), [away(3, 4)], {},
+         lambda a: np.copysign(a, SIGN34)),
+        ("frac", lambda x: paddle.frac(x * 0.9), [pos(3, 4, lo=0.1, hi=0.9)], {}, None),
+        ("i0", paddle.i0, [u(3, 4)], {}, None),
+        ("i1", paddle.i1, [u(3, 4)], {}, None),
+        ("erfinv", lambda x: paddle.erfinv(x * 0.8), [u(3, 4)], {}, None),
+        ("polygamma", lambda x: paddle.polygamma(x, 1), [pos(3, 4)], {}, None),
+        ("avg_pool1d", lambda x: F.avg_pool1d(x, 2, 2), [u(2, 3, 8)], {}, None),
+        ("max_pool1d", lambda x: F.max_pool1d(x, 2, 2), [distinct(2, 3, 8)], {}, None),
+        ("avg_pool3d", lambda x: F.avg_pool3d(x, 2, 2), [u(1, 2, 4, 4, 4)], {}, None),
+        ("adaptive_avg_pool1d", lambda x: F.adaptive_avg_pool1d(x, 3), [u(2, 3, 7)], {}, None),
+        ("pixel_unshuffle", lambda x: F.pixel_unshuffle(x, 2), [u(1, 2, 4, 4)], {}, None),
+        ("channel_shuffle", lambda x: F.channel_shuffle(x, 2), [u(1, 4, 3, 3)], {}, None),
+        ("fold", lambda x: F.fold(x, [4, 4], [2, 2]), [u(1, 8, 9)], {}, None),
+        ("affine_grid", lambda t: F.affine_grid(t, [1, 1, 3, 3], align_corners=False), [u(1, 2, 3)], {}, None),
+        ("pad_constant", lambda x: F.pad(x, [1, 2, 0, 1], value=0.3), [u(1, 2, 3, 3)], {}, None),
+        ("interp_trilinear", lambda x: F.interpolate(x, size=[3, 5, 5], mode="trilinear", data_format="NCDHW"),
+         [u(1, 1, 2, 3, 3)], {}, None),
+        ("square_error_cost", lambda a, b: F.square_error_cost(a, b), [u(3, 4), u(3, 4)], {},
+         lambda a, b: (a - b) ** 2),
+        ("npair_loss", lambda a, p_: F.npair_loss(a, p_, paddle.to_tensor(np.array([0.0, 1.0, 2.0]))),
+         [u(3, 4), u(3, 4)], {}, None),
     ]
     return t
 
@@ -294,4 +331,4 @@ def test_op(name, fn, inputs, kw, ref):
 
 
 def test_sweep_covers_the_api_breadth():
-    assert len(TABLE) >= 180, len(TABLE)
+    assert len(TABLE) >= 230, len(TABLE)
