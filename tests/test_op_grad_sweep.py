@@ -314,6 +314,36 @@ def _table():
          lambda a, b: (a - b) ** 2),
         ("npair_loss", lambda a, p_: F.npair_loss(a, p_, paddle.to_tensor(np.array([0.0, 1.0, 2.0]))),
          [u(3, 4), u(3, 4)], {}, None),
+        ("max_pool3d", lambda x: F.max_pool3d(x, 2, 2), [u(1, 2, 4, 4, 4)], {}, None),
+        ("adaptive_max_pool1d", lambda x: F.adaptive_max_pool1d(x, 3), [u(2, 3, 7)], {}, None),
+        ("adaptive_avg_pool3d", lambda x: F.adaptive_avg_pool3d(x, 2), [u(1, 2, 4, 5, 3)], {}, None),
+        ("conv1d_transpose", lambda x, w: F.conv1d_transpose(x, w, stride=2, padding=1), [u(2, 3, 5), u(3, 2, 3)],
+         {}, None),
+        ("conv3d_transpose", lambda x, w: F.conv3d_transpose(x, w, stride=1), [u(1, 2, 3, 3, 3), u(2, 2, 2, 2, 2)],
+         {}, None),
+        ("prelu", lambda x, w: F.prelu(x, w), [u(2, 3, 4), u(3) * 0.5], {}, None),
+        ("maxout", lambda x: F.maxout(x, 2, axis=1), [u(2, 4, 3, 3)], {}, None),
+        ("rrelu_eval", lambda x: F.rrelu(x, training=False), [u(3, 4)], {}, None),
+        ("dice_loss", lambda x: F.dice_loss(F.softmax(x), paddle.to_tensor(np.array([[0], [2], [1]], np.int64))),
+         [u(3, 3)], {}, None),
+        ("label_smooth", lambda x: F.label_smooth(F.softmax(x), epsilon=0.1), [u(3, 4)], {}, None),
+        ("multi_margin", lambda x: F.multi_margin_loss(x, paddle.to_tensor(np.array([0, 2, 1], np.int64))),
+         [u(3, 4)], {}, None),
+        ("cdist", lambda a, b: paddle.cdist(a, b), [u(3, 4), u(5, 4) + 1.0], {}, None),
+        ("vector_norm", lambda x: paddle.linalg.vector_norm(x, p=3.0, axis=1), [u(3, 4) + 2.0], {}, None),
+        ("matrix_norm_nuc", lambda x: paddle.linalg.matrix_norm(x, p="nuc"), [u(3, 3)], {}, None),
+        ("cummax", lambda x: paddle.cummax(x, axis=1)[0], [u(3, 5)], {}, None),
+        ("temporal_shift", lambda x: F.temporal_shift(x, seg_num=2, shift_ratio=0.25), [u(4, 4, 2, 2)], {}, None),
+        ("zeropad2d", lambda x: F.zeropad2d(x, [1, 0, 2, 1]), [u(1, 2, 3, 3)], {}, None),
+        ("interp_nearest", lambda x: F.interpolate(x, scale_factor=2, mode="nearest"), [u(1, 2, 3, 3)], {}, None),
+        ("softmax_with_ce", lambda x: F.softmax_with_cross_entropy(x, paddle.to_tensor(np.array([[1], [0], [3]],
+                                                                                               np.int64))),
+         [u(3, 4)], {}, None),
+        ("max_unpool2d", lambda x: F.max_unpool2d(*F.max_pool2d(x, 2, 2, return_mask=True), 2, 2),
+         [u(1, 2, 4, 4)], {}, None),
+        ("triplet_margin_dist", lambda a, p_, n: F.triplet_margin_with_distance_loss(a, p_, n),
+         [u(3, 4), u(3, 4), u(3, 4) + 2.0], {}, None),
+        ("bilinear_tensor", lambda a, b, w: F.bilinear(a, b, w), [u(2, 3), u(2, 4), u(5, 3, 4)], {}, None),
     ]
     return t
 
