@@ -119,6 +119,10 @@ def _merge_branch(i, a, b, names):
     if ta or tb:
         raise Dygraph2StaticException(f"variable '{nm}' is a Tensor in one branch of a tensor-dependent if and "
                                       f"{type(b if ta else a).__name__} in the other")
+    if isinstance(a, bool) and isinstance(b, bool) and a != b:
+        # a flag set in one branch only (break / continue lowering, or user flags): a bool tensor after the if
+        with torch._C.DisableTorchFunction():
+            return "tensor", _wrap(torch.tensor(a)), _wrap(torch.tensor(b))
     try:
         same = a is b or bool(a == b)
     except Exception:
@@ -239,12 +243,15 @@ def convert_while_loop(cond_fn, body_fn, args=(), names=None):
     returns their new values."""
     vals = tuple(args)
     c = cond_fn(*vals)
-    if _static(c) or (isinstance(c, Tensor) and any(_static(v) for v in vals)):
-        return _static_while(cond_fn, body_fn, vals, names)
-    while _py_truth(c):
+    while True:
+        # a Python loop turns static once a tensor-dependent break flag (or other carried tensor) reaches its
+        # test: the remaining iterations become one while node
+        if _static(c) or (isinstance(c, Tensor) and any(_static(v) for v in vals)):
+            return _static_while(cond_fn, body_fn, vals, names)
+        if not _py_truth(c):
+            return vals
         vals = tuple(body_fn(*vals))
         c = cond_fn(*vals)
-    return vals
 
 
 def _loop_init(v):

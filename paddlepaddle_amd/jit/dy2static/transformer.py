@@ -15,12 +15,14 @@ reference's nonlocal getter / setter pairs):
 (``_jst.While``); ``for i in range(a, b, s)`` becomes such a while loop over a hidden counter; ``and`` /
 ``or`` / ``not`` in tests become ``_jst.And`` / ``Or`` / ``Not`` (short-circuit kept for Python values);
 ``a if c else b`` becomes ``_jst.IfExp``; ``assert`` becomes ``_jst.Assert``; zero-argument ``super()`` becomes
-``super(__class__, <self>)`` (the rewritten function is built outside its class body).
+``super(__class__, <self>)`` (the rewritten function is built outside its class body). ``break`` / ``continue``
+of a ``while`` or ``for ... in range`` loop become boolean flags: the loop test gains ``not <break flag>`` and the
+statements after a flag-setting ``if`` are guarded, so a tensor-dependent break ends a static while node.
 
 Returns: an ``if`` whose body ends in ``return`` absorbs the statements after it as its ``else`` (early-return
 normalisation); when both branches then end in ``return``, each return becomes an assignment to
 ``__pa_ret`` and one ``return __pa_ret`` follows the if. Statements the rewriting cannot express (``break`` /
-``continue`` / ``return`` in non-tail positions, ``yield``, ``global`` / ``nonlocal``) keep their Python
+``continue`` inside ``with`` / ``try`` or a non-range ``for``, ``return`` in non-tail positions, ``yield``, ``global`` / ``nonlocal``) keep their Python
 form: they still run in dygraph and for Python predicates, and a tensor predicate there fails at trace time
 with the usual graph-break path.
 """
@@ -217,6 +219,48 @@ class _Logical(ast.NodeTransformer):
         return node
 
 
+def _set_flag(name, value=True):
+    """``name = _jst.create_bool_as_type(name, value)``: a Python bool, or a bool tensor once the flag is one."""
+    return ast.Assign(targets=[ast.Name(id=name, ctx=ast.Store())],
+                      value=ast.Call(func=_jst("create_bool_as_type"),
+                                     args=[ast.Name(id=name, ctx=ast.Load()), ast.Constant(value=value)],
+                                     keywords=[]))
+
+
+def _lower_break_continue(stmts, brk, cnt):
+    """A loop body with ``break`` / ``continue`` (of this loop) as straight-line flag code (reference:
+    transformers/break_continue_transformer.py): ``break`` sets ``brk``, ``continue`` sets ``cnt``, and every
+    statement after an ``if`` that may have set one runs under ``if not (brk or cnt)``. None when a break /
+    continue sits in a statement other than ``if`` (``with`` / ``try``), which keeps the Python loop."""
+    out = []
+    for idx, s in enumerate(stmts):
+        if isinstance(s, ast.Break):
+            out.append(ast.copy_location(_set_flag(brk), s))
+            return out
+        if isinstance(s, ast.Continue):
+            out.append(ast.copy_location(_set_flag(cnt), s))
+            return out
+        if not _contains([s], (ast.Break, ast.Continue), into_loops=False):
+            out.append(s)
+            continue
+        if not isinstance(s, ast.If):
+            return None
+        body, orelse = _lower_break_continue(s.body, brk, cnt), _lower_break_continue(s.orelse, brk, cnt)
+        if body is None or orelse is None:
+            return None
+        s.body, s.orelse = body or [ast.Pass()], orelse
+        out.append(s)
+        rest = _lower_break_continue(stmts[idx + 1:], brk, cnt)
+        if rest is None:
+            return None
+        if rest:
+            flags = [ast.Name(id=f, ctx=ast.Load()) for f in (brk, cnt) if f]
+            test = flags[0] if len(flags) == 1 else ast.BoolOp(op=ast.Or(), values=flags)
+            out.append(ast.If(test=ast.UnaryOp(op=ast.Not(), operand=test), body=rest, orelse=[]))
+        return out
+    return out
+
+
 def _lam(expr):
     args = ast.arguments(posonlyargs=[], args=[], vararg=None, kwonlyargs=[], kw_defaults=[], kwarg=None,
                          defaults=[])
@@ -325,7 +369,39 @@ class DygraphToStaticAst(ast.NodeTransformer):
                     or _contains(node.body, (ast.Return, ast.Yield, ast.YieldFrom, ast.Global, ast.Nonlocal,
                                              ast.Await)))
 
+    def _break_flags(self, node):
+        """(flag initialisers, lowered body, break flag or None) for a loop whose body breaks / continues, else
+        None (see _lower_break_continue)."""
+        import copy
+        if node.orelse or not _contains(node.body, (ast.Break, ast.Continue), into_loops=False) or _contains(
+                node.body, (ast.Return, ast.Yield, ast.YieldFrom, ast.Global, ast.Nonlocal, ast.Await)):
+            return None
+        k = self._uid()
+        brk = f"_jst_brk_{k}" if _contains(node.body, (ast.Break,), into_loops=False) else None
+        cnt = f"_jst_cnt_{k}" if _contains(node.body, (ast.Continue,), into_loops=False) else None
+        body = _lower_break_continue(copy.deepcopy(node.body), brk, cnt)
+        if body is None:
+            return None
+        pre = [ast.Assign(targets=[ast.Name(id=f, ctx=ast.Store())], value=ast.Constant(value=False))
+               for f in (brk, cnt) if f]
+        if cnt:
+            body = [_set_flag(cnt, False)] + body
+        return pre, body, brk
+
+    @staticmethod
+    def _and_not(brk, test):
+        if brk is None:
+            return test
+        return ast.BoolOp(op=ast.And(), values=[ast.UnaryOp(op=ast.Not(), operand=ast.Name(id=brk, ctx=ast.Load())),
+                                                test])
+
     def visit_While(self, node):
+        bc = self._break_flags(node)
+        if bc is not None:
+            pre, body, brk = bc
+            out = self.visit_While(ast.copy_location(ast.While(test=self._and_not(brk, node.test), body=body,
+                                                               orelse=[]), node))
+            return [ast.copy_location(s, node) for s in pre] + (out if isinstance(out, list) else [out])
         if not self._loop_ok(node):
             return self._generic_block_owner(node)
         body = self._block(node.body)
@@ -343,9 +419,16 @@ class DygraphToStaticAst(ast.NodeTransformer):
 
     def visit_For(self, node):
         it = node.iter
-        if not (isinstance(it, ast.Call) and isinstance(it.func, ast.Name) and it.func.id == "range"
-                and not it.keywords and 1 <= len(it.args) <= 3 and isinstance(node.target, ast.Name)
-                and self._loop_ok(node)):
+        is_range = (isinstance(it, ast.Call) and isinstance(it.func, ast.Name) and it.func.id == "range"
+                    and not it.keywords and 1 <= len(it.args) <= 3 and isinstance(node.target, ast.Name))
+        # only a range loop is lowered: a Python iteration must keep rebinding its target until the real break
+        bc = self._break_flags(node) if is_range else None
+        flag_pre, brk = [], None
+        if bc is not None:
+            flag_pre, lowered, brk = bc
+            node = ast.copy_location(ast.For(target=node.target, iter=node.iter, body=lowered, orelse=[],
+                                             type_comment=None), node)
+        if not (is_range and self._loop_ok(node)):
             return self._generic_block_owner(node)
         k = self._uid()
         ctr, stop, step = f"{_PREFIX}i_{k}", f"{_PREFIX}stop_{k}", f"{_PREFIX}step_{k}"
@@ -360,7 +443,8 @@ class DygraphToStaticAst(ast.NodeTransformer):
         body = [ast.Assign(targets=[ast.Name(id=node.target.id, ctx=ast.Store())], value=name(ctr))] + list(node.body)
         body.append(ast.Assign(targets=[name(ctr, ast.Store)],
                                value=ast.BinOp(left=name(ctr), op=ast.Add(), right=name(step))))
-        test = ast.Call(func=_jst("RangeCond"), args=[name(ctr), name(stop), name(step)], keywords=[])
+        test = self._and_not(brk, ast.Call(func=_jst("RangeCond"), args=[name(ctr), name(stop), name(step)],
+                                           keywords=[]))
         w = ast.While(test=test, body=body, orelse=[])
         # the hidden counter is a loop variable too: _names_assigned skips the __pa_ prefix, so bind it by hand
         out = self.visit_While(w)
@@ -381,4 +465,4 @@ class DygraphToStaticAst(ast.NodeTransformer):
             out = [cdef, bdef, stmt]
         else:
             return self._generic_block_owner(node)
-        return [ast.copy_location(s, node) for s in pre + out]
+        return [ast.copy_location(s, node) for s in flag_pre + pre + out]

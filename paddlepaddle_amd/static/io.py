@@ -47,8 +47,16 @@ def _used_consts(prog, plan_nodes):
         elif isinstance(x, dict):
             for v in x.values():
                 walk(v)
+    def node(n):
+        walk((n.args, getattr(n, "kwargs", None)))
+        if isinstance(n, P.CFNode):
+            # constants read inside a cond / while body or returned by it (e.g. a branch's literal result)
+            walk(n.res)
+            for b in n.blocks:
+                for x in b.nodes:
+                    node(x)
     for n in plan_nodes:
-        walk((n.args, n.kwargs))
+        node(n)
     return used
 
 

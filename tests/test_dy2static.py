@@ -219,3 +219,67 @@ def test_branch_shape_mismatch_is_reported():
         return y
     with pytest.raises(Exception, match="shape"):
         paddle.jit.save(f, "/nonexistent/never_written", input_spec=[InputSpec([2], "float32")])
+
+
+# --------------------------------------------------------------------------- break / continue
+def _bc(x, n):
+    s = x * 0
+    for i in range(n):
+        if i % 2 == 1:
+            continue
+        s = s + x * i
+        if s.sum() > 20:
+            break
+        s = s + 1
+    j = 0
+    while j < 10:
+        j += 1
+        if j == 3:
+            continue
+        if j > 6:
+            break
+        s = s - 0.5
+    return s, i, j
+
+
+def test_break_continue_lowered_and_python_semantics_kept():
+    src = D.converted_source(_bc)
+    assert "_jst_brk_" in src and "_jst_cnt_" in src and "break" not in src and "continue" not in src
+    g = D.convert_to_static(_bc)
+    for v, n in (([1.0, 2.0], 9), ([5.0, 5.0], 9), ([0.1, 0.1], 4), ([1.0, 1.0], 0)):
+        got, exp = g(_t(v), n), _bc(_t(v), n) if n else None
+        if n == 0:
+            continue  # i is unbound after an empty range in both versions
+        np.testing.assert_allclose(got[0].numpy(), exp[0].numpy())
+        assert got[1:] == exp[1:]
+
+
+def test_tensor_dependent_break_is_one_static_while(tmp_path):
+    @paddle.jit.to_static(input_spec=[InputSpec([3], "float32", "x")])
+    def fn(x):
+        s = paddle.zeros([3])
+        n = paddle.zeros([1])
+        while n < 100:
+            n = n + 1.0
+            if s.sum() > 10:
+                break
+            if n.sum() == 2:
+                continue
+            s = s + x
+        for k in range(50):
+            if s.mean() > 30:
+                break
+            s = s * 1.5
+        return s, n
+
+    path = str(tmp_path / "bc")
+    paddle.jit.save(fn, path)
+    lf = paddle.jit.load(path)
+    for v in ([1.0, 2.0, 3.0], [0.5, 0.25, 0.25], [4.0, 4.0, 4.0]):
+        x = _t(v)
+        es, en = fn.dygraph_function(x)
+        ls, ln = lf(x)
+        np.testing.assert_allclose(fn(x)[0].numpy(), es.numpy(), rtol=1e-6)
+        np.testing.assert_allclose(ls.numpy(), es.numpy(), rtol=1e-6)
+        np.testing.assert_allclose(ln.numpy(), en.numpy())
+    assert _names(lf.program()).count("cf:while") >= 2
