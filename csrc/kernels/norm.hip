@@ -306,6 +306,18 @@ PA_EXPORT int pa_rms_norm_bwd(const void* dy, const void* x, const void* w, cons
   return 0;
 }
 
+// RMSNorm backward with the residual branch's gradient summed into dx (dx = d rms_norm / dx + res): the pre-norm
+// block's x feeds both the norm and the residual add, so this replaces autograd's separate accumulation add.
+PA_EXPORT int pa_rms_norm_bwd_res(const void* dy, const void* x, const void* w, const float* rstd, void* dx,
+                                  float* dw_part, void* res, int64_t rows, int64_t cols, int dtype_np,
+                                  hipStream_t st) {
+  const int dtype = dtype_np & 0xff, nparts = dtype_np >> 8;
+  PA_DISPATCH_DTYPE(dtype, T,
+                    return (launch_bwd<T, false>(dy, x, w, nullptr, rstd, dx, w ? dw_part : nullptr, nullptr, rows,
+                                                 cols, nparts > 0 ? nparts : 1, st, res)));
+  return 0;
+}
+
 PA_EXPORT int pa_layer_norm_fwd(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd,
                                 int64_t rows, int64_t cols, float eps, int dtype, hipStream_t st) {
   PA_DISPATCH_DTYPE(dtype, T, return (launch_fwd<T, true>(x, w, b, y, mean, rstd, rows, cols, eps, st)));

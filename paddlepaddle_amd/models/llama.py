@@ -245,6 +245,15 @@ class LlamaDecoderLayer(nn.Layer):
         self.mlp = LlamaMLP(cfg)
 
     def forward(self, x, cache=None, pos=0):
+        from ..framework.trace_hook import _active_program
+        if cache is None and torch.is_grad_enabled() and _active_program() is None:
+            # training: each residual branch's gradient is summed into the RMSNorm input gradient by the norm's
+            # backward kernel (ops.rms_norm_residual) instead of autograd's separate accumulation add
+            n1, n2 = self.input_layernorm, self.post_attention_layernorm
+            r, h = _ops.rms_norm_residual(x._t, n1.weight._t, n1.eps)
+            t = r + self.self_attn(_wrap(h), cache, pos)._t
+            r, h = _ops.rms_norm_residual(t, n2.weight._t, n2.eps)
+            return _wrap(r + self.mlp(_wrap(h))._t)
         h = self.self_attn(self.input_layernorm(x), cache, pos)
         x = _wrap(x._t + h._t)
         h = self.mlp(self.post_attention_layernorm(x))

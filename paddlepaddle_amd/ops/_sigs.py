@@ -16,6 +16,7 @@ SIGS = {
     # norms
     "pa_rms_norm_fwd": [_vp, _vp, _vp, _vp, _i64, _i64, _f32, _i32, _vp],
     "pa_rms_norm_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp],
+    "pa_rms_norm_bwd_res": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp],
     "pa_layer_norm_fwd": [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _f32, _i32, _vp],
     "pa_layer_norm_bwd": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _vp],
     "pa_reduce_parts": [_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _vp],

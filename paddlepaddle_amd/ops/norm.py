@@ -167,6 +167,42 @@ class _LayerNormResidualHIP(torch.autograd.Function):
         return dx.view(ctx.shape), dw, db, None
 
 
+class _RMSNormResidualHIP(torch.autograd.Function):
+    """(x, rms_norm(x)) with the residual branch's gradient summed into dx by the RMSNorm backward kernel
+    (pa_rms_norm_bwd_res), the RMSNorm twin of _LayerNormResidualHIP for pre-norm LLaMA blocks."""
+
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        y = _RMSNormHIP.forward(ctx, x, w, eps)
+        return x.view_as(x), y
+
+    @staticmethod
+    def backward(ctx, g_res, dy):
+        x2, wc, rstd = ctx.saved_tensors
+        rows, cols = x2.shape
+        res = None if g_res is None else g_res.contiguous().view(rows, cols).to(x2.dtype)
+        if dy is None:
+            return (None if res is None else res.view(ctx.shape)), None, None
+        dy2 = dy.contiguous().view(rows, cols).to(x2.dtype)
+        dx = torch.empty_like(x2)
+        nparts = min(max((rows + 15) // 16, 1), 512)
+        dw_part = torch.empty(nparts, cols, dtype=torch.float32, device=x2.device) if wc is not None else None
+        L.call("pa_rms_norm_bwd_res", L.ptr(dy2), L.ptr(x2), L.ptr(wc), L.ptr(rstd), L.ptr(dx), L.ptr(dw_part),
+               L.ptr(res), rows, cols, L.dcode(x2) | (nparts << 8), L.stream_ptr())
+        dw, _ = _finalize_parts(dw_part, None, ctx.w_dtype, None, nparts, cols, ctx.params) if wc is not None \
+            else (None, None)
+        return dx.view(ctx.shape), dw, None
+
+
+def rms_norm_residual(x, w, eps=1e-6):
+    """(x_residual, rms_norm(x)): on the HIP path the residual branch's gradient is summed into the norm's input
+    gradient inside the backward kernel (no separate add)."""
+    if (L.hip_enabled_for(x) and x.dtype in L._DT and x.shape[-1] % 8 == 0 and torch.is_grad_enabled()
+            and L.has("pa_rms_norm_bwd_res")):
+        return _RMSNormResidualHIP.apply(x, w, eps)
+    return x, rms_norm(x, w, eps)
+
+
 def layer_norm_residual(x, w, b, eps=1e-5):
     """(x_residual, layer_norm(x)): use x_residual for the block's residual connection; on the HIP path its
     gradient is summed into the LN input gradient by the LN backward kernel (no separate add)."""
