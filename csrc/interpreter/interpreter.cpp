@@ -59,6 +59,20 @@ int kdtype(const at::Tensor& t) {
 
 bool aligned16(const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0; }
 
+// One guard for every hand-written kernel launched from the interpreter (the Python paths enforce the same:
+// ops/activation.py softmax, ops/attention.py _lastdim_contig, ops/gemm.py supported): the kernels use 16-byte
+// vector loads / stores, so each operand pointer must be 16-byte aligned and every leading stride (elements) a
+// multiple of 8 (16 bytes of bf16). Optional operands (nullptr) are skipped. Failing it means "use ATen".
+bool vec16_ok(std::initializer_list<const at::Tensor*> ts) {
+  for (const at::Tensor* t : ts) {
+    if (t == nullptr || !t->defined()) continue;
+    if (!aligned16(*t)) return false;
+    for (int64_t d = 0; d + 1 < t->dim(); ++d)
+      if (t->size(d) > 1 && t->stride(d) % 8 != 0) return false;
+  }
+  return true;
+}
+
 void check_launch(int rc, const char* what) {
   if (rc != 0) throw std::runtime_error(std::string("interpreter: ") + what + " kernel launch failed (" +
                                         std::to_string(rc) + ")");
@@ -76,7 +90,7 @@ at::Tensor hip_linear(const at::Tensor& x_in, const at::Tensor& w, const at::Ten
   const int64_t N = trans_w ? w.size(0) : w.size(1);
   if ((trans_w ? w.size(1) : w.size(0)) != K || K % 64 != 0 || N % 8 != 0) return at::Tensor();
   at::Tensor x = x_in.reshape({-1, K});
-  if (!x.is_contiguous() || !w.is_contiguous() || !aligned16(x) || !aligned16(w)) return at::Tensor();
+  if (!x.is_contiguous() || !w.is_contiguous() || !vec16_ok({&x, &w, bias})) return at::Tensor();
   const int64_t M = x.size(0);
   std::vector<int64_t> oshape(x_in.sizes().begin(), x_in.sizes().end());
   oshape.back() = N;
@@ -104,7 +118,7 @@ at::Tensor hip_linear(const at::Tensor& x_in, const at::Tensor& w, const at::Ten
 at::Tensor hip_norm(const at::Tensor& x, const at::Tensor* w, const at::Tensor* b, int64_t begin, double eps,
                     bool rms) {
   const int dt = kdtype(x);
-  if (!x.is_cuda() || dt < 0 || !x.is_contiguous() || !aligned16(x)) return at::Tensor();
+  if (!x.is_cuda() || dt < 0 || !x.is_contiguous() || !vec16_ok({&x, w, b})) return at::Tensor();
   int64_t cols = 1;
   for (int64_t d = begin; d < x.dim(); ++d) cols *= x.size(d);
   if (cols % 8 != 0) return at::Tensor();
@@ -133,7 +147,11 @@ at::Tensor hip_softmax_lastdim(const at::Tensor& x) {
   const int dt = kdtype(x);
   if (!x.is_cuda() || dt < 0 || !x.is_contiguous() || x.dim() < 1) return at::Tensor();
   const int64_t cols = x.size(-1);
+  // softmax.hip reads / writes rows in 8-element vectors and keeps a row in one workgroup: cols % 8 == 0,
+  // 0 < cols <= 65536, 16-byte aligned rows (ops/activation.py applies the same conditions)
+  if (cols <= 0 || cols % 8 != 0 || cols > 65536 || !vec16_ok({&x})) return at::Tensor();
   at::Tensor y = at::empty_like(x);
+  if (!aligned16(y)) return at::Tensor();
   check_launch(pa_softmax_fwd(x.data_ptr(), y.data_ptr(), x.numel() / cols, cols, dt, cur_stream()), "softmax");
   ++g_kernel_calls["softmax"];
   return y;
@@ -147,6 +165,7 @@ at::Tensor hip_flash_attn(const at::Tensor& q, const at::Tensor& k, const at::Te
   const int64_t B = q.size(0), Sq = q.size(1), H = q.size(2), D = q.size(3), Sk = k.size(1), Hk = k.size(2);
   if ((D != 64 && D != 128 && D != 256) || q.stride(3) != 1 || k.stride(3) != 1 || v.stride(3) != 1 || H % Hk != 0)
     return at::Tensor();
+  if (!vec16_ok({&q, &k, &v})) return at::Tensor();
   at::Tensor o = at::empty({B, Sq, H, D}, q.options());
   at::Tensor lse = at::empty({B, H, Sq}, q.options().dtype(at::kFloat));
   const int64_t st[12] = {q.stride(0), q.stride(1), q.stride(2), k.stride(0), k.stride(1), k.stride(2),

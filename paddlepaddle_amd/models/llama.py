@@ -105,8 +105,20 @@ class LlamaRMSNorm(nn.Layer):
         self.weight = self.create_parameter([cfg.hidden_size], default_initializer=I.Constant(1.0))
         self.eps = cfg.rms_norm_eps
 
-    def forward(self, x):
+    def forward(self, x, residual=False):
+        """``residual=True`` (pre-norm training blocks): returns (x_residual, rms_norm(x)) — use x_residual for the
+        block's skip connection; on the HIP path its gradient is summed into this norm's input gradient by the
+        backward kernel (ops.rms_norm_residual: no separate autograd accumulation add)."""
+        if residual:
+            r, h = _ops.rms_norm_residual(x._t, self.weight._t, self.eps)
+            return _wrap(r), _wrap(h)
         return _wrap(_ops.rms_norm(x._t, self.weight._t, self.eps))
+
+    def fuses_residual(self):
+        """Whether forward(x, residual=True) is this layer's own math with nothing observing its output
+        (subclasses overriding forward and layers with forward hooks keep the plain call)."""
+        return (type(self).forward is LlamaRMSNorm.forward and not getattr(self, "_forward_pre_hooks", None)
+                and not getattr(self, "_forward_post_hooks", None))
 
 
 class _Rope:
@@ -245,15 +257,16 @@ class LlamaDecoderLayer(nn.Layer):
         self.mlp = LlamaMLP(cfg)
 
     def forward(self, x, cache=None, pos=0):
-        from ..framework.trace_hook import _active_program
-        if cache is None and torch.is_grad_enabled() and _active_program() is None:
+        n1, n2 = self.input_layernorm, self.post_attention_layernorm
+        if (cache is None and torch.is_grad_enabled() and isinstance(n1, LlamaRMSNorm) and n1.fuses_residual()
+                and isinstance(n2, LlamaRMSNorm) and n2.fuses_residual()):
             # training: each residual branch's gradient is summed into the RMSNorm input gradient by the norm's
-            # backward kernel (ops.rms_norm_residual) instead of autograd's separate accumulation add
-            n1, n2 = self.input_layernorm, self.post_attention_layernorm
-            r, h = _ops.rms_norm_residual(x._t, n1.weight._t, n1.eps)
-            t = r + self.self_attn(_wrap(h), cache, pos)._t
-            r, h = _ops.rms_norm_residual(t, n2.weight._t, n2.eps)
-            return _wrap(r + self.mlp(_wrap(h))._t)
+            # backward kernel (LlamaRMSNorm(residual=True) -> ops.rms_norm_residual, a recorded static op, so a
+            # captured program keeps it) instead of autograd's separate accumulation add
+            r, h = n1(x, residual=True)
+            t = r._t + self.self_attn(h, cache, pos)._t
+            r, h = n2(_wrap(t), residual=True)
+            return _wrap(r._t + self.mlp(h)._t)
         h = self.self_attn(self.input_layernorm(x), cache, pos)
         x = _wrap(x._t + h._t)
         h = self.mlp(self.post_attention_layernorm(x))

@@ -194,6 +194,7 @@ class _RMSNormResidualHIP(torch.autograd.Function):
         return dx.view(ctx.shape), dw, None
 
 
+@static_op
 def rms_norm_residual(x, w, eps=1e-6):
     """(x_residual, rms_norm(x)): on the HIP path the residual branch's gradient is summed into the norm's input
     gradient inside the backward kernel (no separate add)."""

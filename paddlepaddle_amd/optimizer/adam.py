@@ -71,6 +71,7 @@ class Adam(Optimizer):
         if dev_ok and same_step and (self._decoupled or not self._has_l2(group, params)):
             self._fused(group, params, lr, b1, b2, eps, steps[0])
             return
+        self._host_path = True  # bias correction / lr passed as host floats: not replayable from a graph
         coef = getattr(self, "_clip_coef", None)
         if coef is not None:  # deferred clip, but this group takes the per-tensor path
             torch._foreach_mul_([p._t.grad for p in params], coef)
@@ -177,6 +178,33 @@ class Adam(Optimizer):
                 self._learning_rate._register_device_lr(h, ratio)
             self.__dict__.setdefault("_graph_lr_sinks", []).append((h, ratio))
         return h
+
+    # hipGraph capture: the fused update reads lr and the beta powers from a device copy that the captured step
+    # advances itself (_graph_hyper), so replays are exact; the host step counters are advanced per replay here
+    # so state_dict() / a later eager step see the true step.
+    def _graph_capturable(self):
+        return not self._amsgrad and not getattr(self, "_host_path", False)
+
+    def _graph_host_state(self):
+        st = super()._graph_host_state()
+        st["_param_step"] = dict(self._param_step)
+        st["_last_step"] = getattr(self, "_last_step", None)
+        return st
+
+    def _graph_restore_host_state(self, state):
+        super()._graph_restore_host_state(state)
+        self._param_step = dict(state["_param_step"])
+        self._last_step = state["_last_step"]
+
+    def _graph_replayed(self, before, after):
+        super()._graph_replayed(before, after)
+        b, a = before["_param_step"], after["_param_step"]
+        for k, s in a.items():
+            d = s - b.get(k, 0)
+            if d:
+                self._param_step[k] = self._param_step.get(k, 0) + d
+        if after["_last_step"] is not None:
+            self._last_step = (self._last_step or 0) + (after["_last_step"] - (before["_last_step"] or 0))
 
     def state_dict(self):
         # materialise beta-pow accumulators paddle-style

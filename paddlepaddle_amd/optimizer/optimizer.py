@@ -231,6 +231,31 @@ class Optimizer:
         for p in params:
             self._update_param(group, p)
 
+    # ------------------------------------------------------------------ hipGraph capture of a step
+    # A captured training step (static.Executor with BuildStrategy.allow_cuda_graph_capture) replays only device
+    # work: host-side state that the update reads (a learning rate passed as a kernel argument, step counters
+    # used for bias correction) is frozen at its capture-time value. An optimizer therefore says whether its
+    # step may be captured, and keeps its host bookkeeping in step with the replays.
+    def _graph_capturable(self):
+        """Whether a step of this optimizer stays correct when replayed from a hipGraph. Default: no."""
+        return False
+
+    def _graph_host_state(self):
+        """Snapshot of the host-side state a step mutates (restored when a capture fails part-way)."""
+        return {"_step_count": self._step_count}
+
+    def _graph_restore_host_state(self, state):
+        self._step_count = state["_step_count"]
+
+    def _graph_replayed(self, before, after):
+        """Called after every replay of a step captured between host states ``before`` and ``after``: advance
+        the host bookkeeping by what the captured step did."""
+        self._step_count += after["_step_count"] - before["_step_count"]
+
+    def _graph_replay_valid(self, captured_lr):
+        """False when a replay would apply a stale host hyper-parameter (the graph must be re-captured)."""
+        return True
+
     def _update_param(self, group, p):
         raise NotImplementedError
 

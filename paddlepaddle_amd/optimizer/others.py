@@ -26,7 +26,21 @@ class _PerParam(Optimizer):
             p._t.detach().copy_(master)
 
 
-class SGD(_PerParam):
+class _HostLrCapture:
+    """SGD / Momentum steps keep no step counters; their learning rate is a kernel argument, so a captured step
+    is valid while the learning rate is a constant float and unchanged since the capture (an LRScheduler, or a
+    set_lr() after capture, makes the Executor re-run eagerly / re-capture)."""
+
+    def _graph_capturable(self):
+        from .lr import LRScheduler
+        return not isinstance(self._learning_rate, LRScheduler) and \
+            not any(isinstance(g.get("learning_rate"), LRScheduler) for g in self._param_groups)
+
+    def _graph_replay_valid(self, captured_lr):
+        return self.get_lr() == captured_lr
+
+
+class SGD(_HostLrCapture, _PerParam):
     def __init__(self, learning_rate=0.001, parameters=None, weight_decay=None, grad_clip=None,
                  multi_precision=False, name=None):
         super().__init__(learning_rate, parameters, weight_decay, grad_clip, name, multi_precision)
@@ -37,7 +51,7 @@ class SGD(_PerParam):
         self._fin(p, master)
 
 
-class Momentum(_PerParam):
+class Momentum(_HostLrCapture, _PerParam):
     _acc_names = ("velocity",)
 
     def __init__(self, learning_rate=0.001, momentum=0.9, parameters=None, use_nesterov=False, weight_decay=None,

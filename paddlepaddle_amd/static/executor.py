@@ -270,6 +270,8 @@ class _GraphRun:
         self.feeds = None
         self.fetch = None
         self.failed = None
+        self.host_before = self.host_after = None  # optimizer host state around the captured step
+        self.lr = None
 
 
 _GRAPH_STATS = {"captured": 0, "replayed": 0}
@@ -382,6 +384,15 @@ class Executor:
             st = self._graphs[gkey] = _GraphRun()
         if st.failed:
             return None
+        optimizer = prog._optimize[0] if prog._optimize is not None else None
+        if optimizer is not None and not optimizer._graph_capturable():
+            # the update reads host-side hyper-parameters / step counters a replay would freeze
+            st.failed = f"{type(optimizer).__name__} step is not replayable from a hipGraph"
+            return None
+        if st.graph is not None and optimizer is not None and not optimizer._graph_replay_valid(st.lr):
+            st.graph.reset()  # the learning rate baked into the captured launch changed: capture again
+            st = self._graphs[gkey] = _GraphRun()
+            st.runs = _GraphRun.WARMUP
         env = self._feed(prog, feed, dev)
         if st.graph is None:
             st.runs += 1
@@ -393,6 +404,7 @@ class Executor:
             cap_env = dict(st.feeds)
             torch.cuda.synchronize(dev)
             g = CUDAGraph()
+            before = optimizer._graph_host_state() if optimizer is not None else None
             try:
                 g.capture_begin()
                 try:
@@ -402,7 +414,12 @@ class Executor:
             except Exception as e:  # noqa: BLE001 - a host sync / allocation inside the program: run eagerly
                 st.failed = repr(e)
                 g.reset()
+                if optimizer is not None:  # the partial capture advanced host counters no device work matched
+                    optimizer._graph_restore_host_state(before)
                 return None
+            if optimizer is not None:
+                st.host_before, st.host_after = before, optimizer._graph_host_state()
+                st.lr = optimizer.get_lr()
             st.graph = g
             st.fetch = [cap_env[s] for s in fetch]
             _GRAPH_STATS["captured"] += 1
@@ -410,6 +427,8 @@ class Executor:
             for s, t in env.items():
                 st.feeds[s].data.copy_(t, non_blocking=True) if st.feeds[s].requires_grad else \
                     st.feeds[s].copy_(t, non_blocking=True)
+            if optimizer is not None:  # the capture run's host update stands for its own (first) replay
+                optimizer._graph_replayed(st.host_before, st.host_after)
         st.graph.replay()
         _GRAPH_STATS["replayed"] += 1
         return [t.detach() if isinstance(t, torch.Tensor) else t for t in st.fetch]

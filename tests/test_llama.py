@@ -146,3 +146,94 @@ def test_llama_fused_inference_forward_matches_training_path():
         got = model(ids)._t.float()
     err = (got - ref).abs().max().item() / ref.abs().max().item()
     assert err < 2e-2, err
+
+
+def _llama_grads(model, ids):
+    crit = LlamaPretrainingCriterion(model.config if hasattr(model, "config") else LlamaConfig.tiny())
+    loss = crit(model(paddle.Tensor(ids[:, :-1])), paddle.Tensor(ids[:, 1:]))
+    loss.backward()
+    g = {n: p.grad.numpy().copy() for n, p in model.named_parameters() if p.grad is not None}
+    model.clear_gradients()
+    return float(loss), g
+
+
+def test_llama_norm_hooks_fire_in_training_and_fused_path_matches():
+    """the residual-gradient fusion lives in LlamaRMSNorm (forward(residual=True)); the decoder layer
+    still calls its norm sublayers, a forward hook on input_layernorm fires in training (that layer then takes the
+    plain path) and both paths give the same loss and gradients."""
+    paddle.seed(0)
+    cfg = LlamaConfig.tiny()
+    model = LlamaForCausalLM(cfg)
+    ids = torch.randint(0, cfg.vocab_size, (2, 17), generator=torch.Generator().manual_seed(4))
+    l0, g0 = _llama_grads(model, ids)
+    calls = []
+    n1 = model.llama.layers[0].input_layernorm
+    assert n1.fuses_residual()
+    h = n1.register_forward_post_hook(lambda layer, inp, out: calls.append(tuple(out.shape)))
+    assert not n1.fuses_residual()
+    l1, g1 = _llama_grads(model, ids)
+    h.remove()
+    assert calls and calls[0][-1] == cfg.hidden_size
+    assert abs(l0 - l1) < 1e-6
+    for k in g0:
+        np.testing.assert_allclose(g1[k], g0[k], rtol=1e-5, atol=1e-6)
+
+
+def test_llama_subclassed_norm_is_called():
+    from paddlepaddle_amd.models import llama as LM
+
+    class ScaledNorm(LM.LlamaRMSNorm):
+        def forward(self, x, residual=False):
+            return super().forward(x) * 2.0
+
+    paddle.seed(0)
+    cfg = LlamaConfig.tiny()
+    model = LlamaForCausalLM(cfg)
+    for layer in model.llama.layers:
+        sn = ScaledNorm(cfg)
+        sn.weight.set_value(layer.input_layernorm.weight)
+        layer.input_layernorm = sn
+    ids = torch.randint(0, cfg.vocab_size, (2, 9), generator=torch.Generator().manual_seed(2))
+    sd = {k: v.numpy() for k, v in model.state_dict().items()}
+    for k in list(sd):
+        if k.endswith("input_layernorm.weight"):
+            sd[k] = sd[k] * 2.0  # the subclass doubles the norm output = a doubled weight in the reference
+    ref = _torch_llama(sd, cfg, ids)
+    with paddle.enable_grad() if hasattr(paddle, "enable_grad") else torch.enable_grad():
+        got = model(paddle.Tensor(ids)).numpy()
+    np.testing.assert_allclose(got, ref.numpy(), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("use", ["both", "residual_only", "norm_only"])
+def test_rms_norm_residual_hip_gradients_vs_fp32(use):
+    """ops.rms_norm_residual's backward branches (dy None, g_res None) against an fp32 autograd reference."""
+    from paddlepaddle_amd import ops
+    torch.manual_seed(0)
+    dev = "cuda"
+    x = torch.randn(64, 512, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(512, device=dev)).to(torch.bfloat16).requires_grad_(True)
+    gr, gn = torch.randn(64, 512, device=dev), torch.randn(64, 512, device=dev)
+
+    def run(fn, xx, ww):
+        r, h = fn(xx, ww)
+        loss = 0.0
+        if use in ("both", "residual_only"):
+            loss = loss + (r.float() * gr).sum()
+        if use in ("both", "norm_only"):
+            loss = loss + (h.float() * gn).sum()
+        gx, gw = torch.autograd.grad(loss, (xx, ww), allow_unused=True)
+        return gx, gw
+
+    def ref(xx, ww):
+        xf = xx.float()
+        h = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-6) * ww.float()
+        return xf, h
+    gx, gw = run(lambda a, b: ops.rms_norm_residual(a, b, 1e-6), x, w)
+    xr, wr = x.detach().float().requires_grad_(True), w.detach().float().requires_grad_(True)
+    rx, rw = run(ref, xr, wr)
+    assert (gx.float() - rx).abs().max() <= 2e-2 * rx.abs().max()
+    if use == "residual_only":
+        assert gw is None or float(gw.float().abs().max()) == 0.0
+    else:
+        assert (gw.float() - rw).abs().max() <= 2e-2 * rw.abs().max()

@@ -76,3 +76,41 @@ def test_gpt_pir_predictor_launches_the_hip_kernels(tmp_path):
     assert calls.get("flash_attn", 0) == L, calls
     scale = np.abs(ref).max()
     assert np.abs(out - ref).max() / scale < 3e-2
+
+
+def _one_op_interp(op, attrs, device):
+    m = NI._module()
+    it = m.Interpreter(2, str(device))
+    it.add(op, [0], [1], attrs)
+    it.finalize([], [1])
+    return it
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cols", [10, 77, 64, 1000])
+def test_interp_softmax_guards_rows_the_kernel_cannot_take(cols):
+    # softmax.hip needs cols % 8 == 0 and 16-byte rows: 10 / 77 / 1000-wide rows must fall back to
+    # ATen, multiples of 8 run the HIP kernel; every row is checked against the fp32 softmax
+    dev = torch.device("cuda:0")
+    x = torch.randn(33, cols, device=dev, dtype=torch.float32) * 3
+    it = _one_op_interp("softmax", {"axis": -1}, dev)
+    NI.reset_kernel_calls()
+    y = it.run([(0, x)])[0]
+    torch.cuda.synchronize()
+    ref = torch.softmax(x.double(), -1).float()
+    assert torch.allclose(y, ref, atol=1e-5, rtol=1e-4)
+    launched = NI.kernel_calls().get("softmax", 0)
+    assert launched == (1 if cols % 8 == 0 else 0)
+
+
+@pytest.mark.gpu
+def test_interp_softmax_misaligned_view_falls_back():
+    dev = torch.device("cuda:0")
+    base = torch.randn(17 * 64 + 4, device=dev)
+    x = base[4:].view(17, 64)  # 16-byte misaligned start
+    it = _one_op_interp("softmax", {"axis": -1}, dev)
+    NI.reset_kernel_calls()
+    y = it.run([(0, x)])[0]
+    torch.cuda.synchronize()
+    assert torch.allclose(y, torch.softmax(x, -1), atol=1e-6)
+    assert NI.kernel_calls().get("softmax", 0) == 0
