@@ -18,6 +18,8 @@ from ..parallel.data_parallel import DataParallel  # noqa: F401,E402
 from .extras import *  # noqa: F401,F403,E402
 from . import communicator  # noqa: F401,E402
 from .watchdog import enable_comm_watchdog, disable_comm_watchdog  # noqa: F401,E402
+from .collective_check import (enable_collective_check, disable_collective_check, check_collectives,  # noqa: F401,E402
+                               CollectiveMismatchError)
 
 
 def __getattr__(name):

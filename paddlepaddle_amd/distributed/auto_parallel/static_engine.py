@@ -886,6 +886,7 @@ class StaticEngine:
         if getattr(self, "_p2p", None) is None:
             self._p2p = _P2P(self.dev)  # built once on every rank (its host twin is a collective group creation)
         p2p = self._p2p
+        p2p.begin_run()
         nst = len(self.meshes)
         s = self.my_stage
         n = self.acc
@@ -922,6 +923,9 @@ class StaticEngine:
             dist.all_reduce(loss, group=self._pp_group())
         self.opt.step()
         self.opt.clear_grad()
+        from .. import collective_check as _cc
+        if _cc.enabled():
+            _cc.check_collectives("static engine step")
         return _wrap(loss)
 
 
@@ -934,7 +938,9 @@ class _P2P:
         from ...parallel.p2p import P2P, host_twin
         ws = dist.get_world_size() if dist.is_initialized() else 1
         host = host_twin([list(range(ws))], dist.get_rank()) if ws > 1 else None
-        self.ep = P2P(dev, None, host)
+        # ordered: every stage walks its 1F1B / FThenB / ZBH1 job list and its slots in sorted order, so each
+        # directed channel is consumed in production order (no per-message header, parallel/p2p.py)
+        self.ep = P2P(dev, None, host, ordered=True)
 
     @staticmethod
     def _tag(key):
@@ -949,5 +955,8 @@ class _P2P:
 
     def join(self):
         self.ep.join()
+
+    def begin_run(self):
+        self.ep.begin_run()
 
 

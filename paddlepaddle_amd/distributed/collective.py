@@ -176,6 +176,8 @@ def init_parallel_env(backend=None, timeout_s=1800):
         if wd:
             from .watchdog import enable_comm_watchdog
             enable_comm_watchdog(timeout_s=float(wd), report_dir=os.environ.get("PADDLE_AMD_COMM_WATCHDOG_DIR"))
+        from .collective_check import maybe_enable_from_env
+        maybe_enable_from_env()
     ws = dist.get_world_size()
     _default_group = Group(dist.get_rank(), 0, list(range(ws)), None, "_default_pg")
     _groups[0] = _default_group

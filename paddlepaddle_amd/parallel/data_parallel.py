@@ -12,6 +12,10 @@ MI355X design:
   is latency-bound below a few MB and bandwidth-bound above;
 - collectives are issued async (RCCL runs them on its own HIP stream ordered after the producing
   compute) and are all joined at the end of backward, before ``optimizer.step``;
+- buckets are launched strictly in bucket-index order (reference reducer.cc:955 MarkGroupReady /
+  next_group_): a bucket that fills early waits for its predecessors, so every rank issues the same
+  collective sequence on the RCCL communicator even when grads become ready in a different order on
+  different ranks (unused parameters, stream timing) — out-of-order all-reduces would hang RCCL;
 - ReduceOp.AVG on RCCL (no extra scaling kernel); SUM + scale on gloo.
 """
 from __future__ import annotations
@@ -30,7 +34,7 @@ from ..utils import native
 
 
 class _Bucket:
-    __slots__ = ("params", "flat", "offsets", "pending", "work", "ready")
+    __slots__ = ("params", "flat", "offsets", "pending", "work", "ready", "id")
 
     def __init__(self, params, dtype, device):
         self.params = params
@@ -52,7 +56,7 @@ class _Bucket:
 
 
 class DataParallel(Layer):
-    def __init__(self, layers, strategy=None, comm_buffer_size=64, last_comm_buffer_size=8,
+    def __init__(self, layers, strategy=None, comm_buffer_size=None, last_comm_buffer_size=8,
                  find_unused_parameters=False, group=None):
         super().__init__()
         self._layers = layers
@@ -63,6 +67,7 @@ class DataParallel(Layer):
         self._buckets = []
         self._param_loc = {}
         self._queued = False
+        self._next_launch = 0  # index of the next bucket to all-reduce (launch order = bucket order)
         if self._world > 1:
             self._broadcast_params()
             self._build_buckets(comm_buffer_size, last_comm_buffer_size)
@@ -82,7 +87,8 @@ class DataParallel(Layer):
         by_key = {}
         for p in params:
             by_key.setdefault((p._t.dtype, p._t.device), []).append(p)
-        mb = flag("FLAGS_dp_bucket_mb", comm_mb) or comm_mb
+        # an explicit comm_buffer_size wins; otherwise FLAGS_dp_bucket_mb (sized for xGMI rings)
+        mb = comm_mb if comm_mb is not None else flag("FLAGS_dp_bucket_mb", 128)
         for (dt, dev), ps in by_key.items():
             sizes = [p._t.numel() * p._t.element_size() for p in ps]
             # first-ready (last registered) bucket small, the rest large
@@ -98,6 +104,7 @@ class DataParallel(Layer):
                     continue
                 b = _Bucket([ps[i] for i in idxs], dt, dev)
                 bi = len(self._buckets)
+                b.id = bi  # planned identity (the collective checker labels its all-reduce with it)
                 self._buckets.append(b)
                 for j, p in enumerate(b.params):
                     self._param_loc[id(p)] = (bi, j)
@@ -130,28 +137,42 @@ class DataParallel(Layer):
             return
         b.ready.add(j)
         if len(b.ready) == len(b.params):
+            self._launch_ready()
+
+    def _launch_ready(self):
+        """Launch every full bucket at the head of the launch order (bucket-index order)."""
+        while self._next_launch < len(self._buckets):
+            b = self._buckets[self._next_launch]
+            if b.work is not None or len(b.ready) < len(b.params):
+                break
             self._launch(b)
+            self._next_launch += 1
 
     def _launch(self, b):
+        from ..distributed import collective_check as _cc
         pg = C._pg(self.group)
-        if dist.get_backend(pg) == "nccl":
-            b.work = dist.all_reduce(b.flat, op=dist.ReduceOp.AVG, group=pg, async_op=True)
-        else:
-            b.flat.mul_(1.0 / self._world)
-            b.work = dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=pg, async_op=True)
+        with _cc.label(f"dp bucket {b.id}") if _cc.enabled() else contextlib.nullcontext():
+            if dist.get_backend(pg) == "nccl":
+                b.work = dist.all_reduce(b.flat, op=dist.ReduceOp.AVG, group=pg, async_op=True)
+            else:
+                b.flat.mul_(1.0 / self._world)
+                b.work = dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=pg, async_op=True)
 
     def _finalize(self):
+        # the rest in bucket order; buckets with unused params keep those slices as they are (zero after
+        # clear_grad) and are reduced like the others
+        while self._next_launch < len(self._buckets):
+            self._launch(self._buckets[self._next_launch])
+            self._next_launch += 1
         for b in self._buckets:
-            if b.work is None:
-                if len(b.ready) < len(b.params):
-                    if not self.find_unused_parameters and b.ready:
-                        pass
-                    # unused params: their slice stays whatever it was (zero after clear_grad)
-                self._launch(b)
             b.work.wait()
             b.work = None
             b.ready = set()
+        self._next_launch = 0
         self._queued = False
+        from ..distributed import collective_check as _cc
+        if _cc.enabled():
+            _cc.check_collectives("DataParallel backward")
 
     # ------------------------------------------------------------------ api
     def forward(self, *inputs, **kwargs):

@@ -164,6 +164,7 @@ class PipelineParallel(nn.Layer):
         self.next_rank = self.group.ranks[self.stage_id + 1] if not self.is_last else None
         self._dp_sync = hcg.get_data_parallel_world_size() > 1
         self._p2p = None
+        self._p2p_ordered = True  # 1F1B / FThenB / ZBH1 consume each directed channel in production order
 
     # --------------------------------------------------------------- p2p
     def _dev(self):
@@ -176,7 +177,8 @@ class PipelineParallel(nn.Layer):
         if self._p2p is None:
             host = self._hcg.get_pipe_parallel_host_group() if hasattr(self._hcg, "get_pipe_parallel_host_group") \
                 else None
-            self._p2p = P2P(self._dev(), self.group.process_group, host)
+            # ordered (no per-message header) unless the schedule consumes a channel out of production order
+            self._p2p = P2P(self._dev(), self.group.process_group, host, ordered=self._p2p_ordered)
         return self._p2p
 
     def _send(self, t, dst, kind=_FWD, key=(0, 0)):
@@ -224,6 +226,7 @@ class PipelineParallel(nn.Layer):
             self._send(inp._t.grad, self.prev_rank, _BWD, (0, mb))
 
     def forward_backward_pipeline(self, data, scaler=None):
+        self._p2p_chan().begin_run()
         inputs, labels = (data if isinstance(data, (list, tuple)) and len(data) == 2 else (data, None))
         mb_in = self._split(inputs) if self.is_first else [None] * self.accumulate_steps
         mb_lb = self._split(labels) if (self.is_last and labels is not None) else [None] * self.accumulate_steps
@@ -277,11 +280,15 @@ class PipelineParallel(nn.Layer):
         optimizer.clear_grad()
         if lr_scheduler is not None:
             lr_scheduler.step()
+        from ..distributed import collective_check as _cc
+        if _cc.enabled():
+            _cc.check_collectives("pipeline train_batch")
         return loss
 
     @torch.no_grad()
     def eval_batch(self, data, compute_loss=True):
         self._layers.eval()
+        self._p2p_chan().begin_run()
         inputs, labels = (data if isinstance(data, (list, tuple)) and len(data) == 2 else (data, None))
         mb_in = self._split(inputs) if self.is_first else [None] * self.accumulate_steps
         mb_lb = self._split(labels) if (self.is_last and labels is not None) else [None] * self.accumulate_steps
@@ -311,6 +318,7 @@ class PipelineParallelZeroBubble(PipelineParallel):
     def forward_backward_pipeline(self, data, scaler=None):
         from ..ops import linear as LIN
         from .pp_schedules import zbh1
+        self._p2p_chan().begin_run()
         inputs, labels = (data if isinstance(data, (list, tuple)) and len(data) == 2 else (data, None))
         n = self.accumulate_steps
         mb_in = self._split(inputs) if self.is_first else [None] * n
@@ -351,6 +359,7 @@ class PipelineParallelWithInterleave(PipelineParallel):
         S = self.num_stages
         self.prev_rank = self.group.ranks[(self.stage_id - 1) % S]
         self.next_rank = self.group.ranks[(self.stage_id + 1) % S]
+        self._p2p_ordered = False  # chunks of a ring channel are consumed out of production order: tagged + stash
         if self.accumulate_steps % S:
             raise ValueError(f"accumulate_steps ({self.accumulate_steps}) must be a multiple of the "
                              f"pipeline degree ({S}) for the interleaved schedule")
@@ -448,6 +457,7 @@ class PipelineParallelWithInterleaveFthenB(PipelineParallelWithInterleave):
         S = self.num_stages
         self.prev_rank = self.group.ranks[(self.stage_id - 1) % S]
         self.next_rank = self.group.ranks[(self.stage_id + 1) % S]
+        self._p2p_ordered = False  # chunks of a ring channel are consumed out of production order: tagged + stash
         if self.accumulate_steps < S:
             raise ValueError(f"accumulate_steps ({self.accumulate_steps}) must be >= pp degree ({S})")
 

@@ -387,6 +387,13 @@ class GroupShardedEngine:
 
     # ------------------------------------------------------------------ collectives
     def _gather(self, u):
+        from ..distributed import collective_check as _cc
+        if _cc.enabled() and not (u.gathered or self.world == 1):
+            with _cc.label(f"ag unit {self.units.index(u)}"):
+                return self._gather_impl(u)
+        return self._gather_impl(u)
+
+    def _gather_impl(self, u):
         if u.gathered or self.world == 1:
             u.gathered = True
             return
@@ -413,6 +420,13 @@ class GroupShardedEngine:
         u.gathered = False
 
     def _reduce_scatter(self, u):
+        from ..distributed import collective_check as _cc
+        if _cc.enabled():
+            with _cc.label(f"rs unit {self.units.index(u)}"):
+                return self._reduce_scatter_impl(u)
+        return self._reduce_scatter_impl(u)
+
+    def _reduce_scatter_impl(self, u):
         for f in u.flats:
             f.fold_param_grads()
             fg = f.full_grad
@@ -463,6 +477,9 @@ class GroupShardedEngine:
     # ------------------------------------------------------------------ optimizer
     @torch.no_grad()
     def step(self):
+        from ..distributed import collective_check as _cc
+        if _cc.enabled():
+            _cc.check_collectives("sharding step")
         dp_work = []
         sp_mp = self.mp_group is not None
         sp = []

@@ -54,6 +54,7 @@ def _worker(rank, world, port, shape, acc, schedule, q):
         ep = eng._p2p.ep
         assert ep.meta_exchanges == len(ep.sent_meta) and ep.messages == STEPS * acc * len(ep.sent_meta), (
             ep.meta_exchanges, len(ep.sent_meta), ep.messages)
+        assert ep.ordered and ep.headers == STEPS * len(ep.sent_meta), ep.headers  # one header per class per run
     q.put((rank, losses, kinds, eng.my_stage))
     paddle.distributed.barrier()
 

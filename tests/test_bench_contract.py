@@ -50,11 +50,12 @@ def test_bench_llama_pipeline_x_tp_four_ranks():
     assert d["n_gpus"] == 4 and d["value"] > 0 and d["config"]["parallelism"] == "pp2_tp2_dp1"
 
 
-def test_bench_llama_static_auto_parallel_pp4_tp2_eight_ranks():
+def test_bench_llama_static_auto_parallel_pp4_tp2_eight_ranks():  # collective-sequence checker on
     """The BASELINE LLaMA-2 layout (PP4 x TP2, static-graph auto-parallel) on 8 gloo ranks: `bench.py --model
     llama-tiny --pp 4 --tp 2` distributes a plain LLaMA with dist.parallelize and trains it through
     dist.to_static (traced program, per-rank partition, 1F1B)."""
-    env = dict(os.environ, PADDLE_AMD_FORCE_CPU="1", PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    env = dict(os.environ, PADDLE_AMD_FORCE_CPU="1", PYTHONPATH=ROOT, OMP_NUM_THREADS="1",
+               PADDLE_AMD_CHECK_COLLECTIVES="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8", "--master-addr",
            "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "8", "--model",
            "llama-tiny", "--pp", "4", "--tp", "2", "--steps", "2", "--warmup", "1", "--seq-len", "32",
@@ -67,6 +68,7 @@ def test_bench_llama_static_auto_parallel_pp4_tp2_eight_ranks():
     assert d["n_gpus"] == 8 and d["value"] > 0
     assert d["config"]["parallelism"] == "pp4_tp2_dp1_static_auto_parallel"
     assert "[llama-static]" in r.stderr.decode() + r.stdout.decode()
+    assert "sequence checks passed" in r.stderr.decode()  # every rank's collective sequence matched its peers' 
 
 
 def test_bench_self_launch_sharding_x_tp_four_ranks():
@@ -89,8 +91,9 @@ def test_bench_self_launch_sharding_x_tp_four_ranks():
 
 def test_bench_eight_ranks_sharding4_x_tp2_sp():
     """The 8-GPU flagship layout on 8 gloo ranks: `bench.py --gpus 8 --tp 2` (sharding stage 3 over 4 ranks x
-    tensor parallel 2 with sequence parallelism), self-launched."""
-    env = dict(os.environ, PADDLE_AMD_FORCE_CPU="1", PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    tensor parallel 2 with sequence parallelism), self-launched, with the collective-sequence checker on."""
+    env = dict(os.environ, PADDLE_AMD_FORCE_CPU="1", PYTHONPATH=ROOT, OMP_NUM_THREADS="1",
+               PADDLE_AMD_CHECK_COLLECTIVES="1")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--tp", "2", "--model", "tiny",
@@ -103,6 +106,7 @@ def test_bench_eight_ranks_sharding4_x_tp2_sp():
     assert d["n_gpus"] == 8 and d["value"] > 0
     assert d["config"]["parallelism"] == "sharding_stage3_degree4_tp2_sp"
     assert d["config"]["global_batch"] == 2 * 2 * 4
+    assert "sequence checks passed" in r.stderr.decode()
 
 
 def test_bench_rejects_world_mismatch():

@@ -145,6 +145,9 @@ def _pp_worker(rank, world, port, q, schedule="1F1B"):
     ep = model._p2p
     assert ep.meta_exchanges == 1 and ep.messages == 3 * 2 + (2 if rank == 0 else 0), (ep.meta_exchanges,
                                                                                           ep.messages)
+    # ordered channels: a host-side header only for the first message of each run (3 train runs + 1 eval run on
+    # the forward channel, 3 on the backward one), every other payload receive posted from the cached meta
+    assert ep.ordered and ep.headers == (4 if rank == 0 else 3), ep.headers
     q.put((rank, losses, params, None if isinstance(ev, list) else float(ev)))
     paddle.distributed.barrier()
 
