@@ -42,6 +42,9 @@ def parse():
     p.add_argument("--seq-len", type=int, default=2048)
     p.add_argument("--recompute", type=int, default=0)
     p.add_argument("--sharding-stage", type=int, default=3)
+    p.add_argument("--pair-wgrad", type=int, default=1,
+                   help="GPT: pair the weight-gradient GEMMs of consecutive accumulation micro-batches into one "
+                        "K = 2T product (ops/linear.py pair_weight_grads)")
     p.add_argument("--tp", type=int, default=None,
                    help="tensor-parallel degree (GPT: sharding over world/tp ranks). Default: the BASELINE config "
                         "'GPT-3 13B sharding stage-3 + TP=2' -> 2 on any multi-GPU run of GPT, 1 on one GPU")
@@ -162,13 +165,20 @@ def gpt_bench(args, paddle, world, dist_on):
     import contextlib
     no_sync = getattr(model, "no_sync", None)
 
+    from paddlepaddle_amd.ops import linear as LIN
+
     def step():
         for a in range(args.accum):
             # accumulation micro-batches skip the gradient reduce-scatter / all-reduce; the last one
             # reduces (overlapped with its backward)
             ctx = no_sync() if (no_sync is not None and n_shard > 1 and a < args.accum - 1) else \
                 contextlib.nullcontext()
-            with ctx:
+            # weight-gradient pairing (ops/linear.py): even micro-batches queue their dW GEMMs, the next one runs
+            # each weight's pair as one K = 2T product into the main grad (every queued job is done inside it)
+            pair = None
+            if args.pair_wgrad and args.accum > 1:
+                pair = "defer" if (a % 2 == 0 and a + 1 < args.accum) else "merge"
+            with ctx, LIN.pair_weight_grads(pair):
                 if cfg.fused_head_ce and tp == 1:
                     loss = model(ids[a], labels=lbl[a])
                 else:
@@ -223,7 +233,13 @@ def llama_static_bench(args, paddle, world, dist_on):
         raise SystemExit(f"world {world} is not a multiple of pp*tp = {pp * tp}")
     dp = world // (pp * tp)
     presets = {"llama2-70b": LlamaConfig.llama2_70b, "llama2-13b": LlamaConfig.llama2_13b,
-               "llama2-7b": LlamaConfig.llama2_7b, "llama-tiny": LlamaConfig.tiny}
+               "llama2-7b": LlamaConfig.llama2_7b, "llama-tiny": LlamaConfig.tiny,
+               # one rank of the BASELINE LLaMA-2 70B PP4 x TP2 layout on one GPU: a pipeline stage's 20 layers at
+               # the tensor-parallel-local widths (hidden 8192, 32 of the 64 query heads, 4 of the 8 KV heads,
+               # ffn 28672 / 2), embedding and LM head included (the first / last stage's extra weights)
+               "llama2-70b-stage": lambda **kw: LlamaConfig.llama2_70b(
+                   num_hidden_layers=20, num_attention_heads=32, num_key_value_heads=4, intermediate_size=14336,
+                   attention_head_dim=128, **kw)}
     extra = {"num_hidden_layers": max(2, 2 * pp)} if args.model == "llama-tiny" else {}
     cfg = presets[args.model](max_position_embeddings=max(args.seq_len, 128), **extra)
     dist.auto_parallel.set_mesh(None)
@@ -257,8 +273,11 @@ def llama_static_bench(args, paddle, world, dist_on):
     tokens = args.steps * gb * args.seq_len
     tps = tokens / dt
     mfu = tps * cfg.flops_per_token(args.seq_len) / (PEAK_BF16 * world)
+    mem = paddle.device.cuda.max_memory_allocated() / 2**30 if dev.type == "cuda" else 0.0
+    eng = dm._engine
     log(f"[llama-static] {args.model} pp{pp} tp{tp} dp{dp}: loss={float(state['loss']):.4f} "
-        f"step={dt / args.steps * 1000:.1f}ms tokens/s={tps:.0f} MFU={mfu * 100:.1f}%")
+        f"step={dt / args.steps * 1000:.1f}ms tokens/s={tps:.0f} MFU={mfu * 100:.1f}% peak_mem={mem:.1f}GiB "
+        f"params={cfg.num_params() / 1e9:.2f}B passes={getattr(eng, 'pass_stats', {})}")
     return tps, dt / args.steps * 1000, gb, mfu
 
 
@@ -459,6 +478,7 @@ def main():
                        "global_batch": gb, "seq_len": args.seq_len, "micro_batch": args.micro_batch,
                        "accum_steps": args.accum, "parallelism": par, "recompute": bool(args.recompute),
                        "fused_head_ce": bool(args.fused_head_ce),
+                       **({"paired_wgrad": bool(args.pair_wgrad and args.accum > 1)} if not is_llama else {}),
                        "optimizer": "AdamW fp32-master fused HIP", "amp": "O2 bf16",
                        "allocator": ("native auto-growth best-fit" if _native_alloc_on() else "torch caching"),
                        **({"stage3_params": ("gathered once per step, resident until the optimizer step"

@@ -84,6 +84,17 @@ struct GemmArgs {
   // tail_ws; gemm_tail_reduce_k sums them and applies the epilogue. tail_split == 0: no tail.
   int full_tiles, tail_split;
   float* tail_ws;
+  // operand segments (ping-pong kernel), nseg = 0 / 1: none. seg_k = 1: the K range is split, K-tiles
+  // [seg_end[s-1], seg_end[s]) read A = seg_a[s] (lda seg_lda[s]) and B = seg_b[s] (ldb seg_ldb[s]) from their own
+  // k = 0: C = sum_s A_s . B_s in one launch (the data gradient of sibling linears, the weight gradient of two
+  // accumulation micro-batches) without concatenated copies. seg_k = 0: the N range is split (seg_end in columns,
+  // multiples of 128), columns of segment s read B = seg_b[s] from its own column 0: C = A . [B_0 | B_1 | ...] (one
+  // GEMM for the q / k / v or gate / up projections of one input).
+  int nseg, seg_k;
+  int seg_end[4];
+  const uint16_t* seg_a[4];
+  const uint16_t* seg_b[4];
+  int64_t seg_lda[4], seg_ldb[4];
   // kEpiStats: stats[2][chunks][N] fp32, chunk = m-tile * (waves along M) + wave row; each (chunk, column) is
   // written by exactly one lane (no atomics, deterministic), folded by bn.hip (pa_bn_fwd_nhwc_pre)
   float* stats;
@@ -293,6 +304,18 @@ __device__ __forceinline__ bf16x8_t frag(const char* img, int rbase, int s, int 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// segment of a K-tile / column index v (wave-uniform: constant-index selects, no dynamic kernel-argument indexing)
+__device__ __forceinline__ int seg_of(const GemmArgs& p, int v) {
+  int s = 0;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) s += (i + 1 < p.nseg && v >= p.seg_end[i]) ? 1 : 0;
+  return s;
+}
+template <class T>
+__device__ __forceinline__ T pick4(int s, T v0, T v1, T v2, T v3) {
+  return s == 0 ? v0 : (s == 1 ? v1 : (s == 2 ? v2 : v3));
 }
 
 // NW = 8: waves 2 (M) x 4 (N), wave tile 128 x BN/4, 2 waves per SIMD.
@@ -508,13 +531,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p0) {
   const int bid = (int)blockIdx.x;
   int pid;
   float* tail_out = nullptr;
+  int kt0 = 0;  // first global K-tile of this workgroup (tail slices start inside K)
   if (p.tail_split > 0 && bid >= p.full_tiles) {
     const int u = bid - p.full_tiles;
     const int ks = u % p.tail_split;
     pid = p.full_tiles + u / p.tail_split;
     p.K /= p.tail_split;
-    p.a += (int64_t)ks * p.K * (AK ? 1 : p.lda);
-    p.b += (int64_t)ks * p.K * (BKM ? 1 : p.ldb);
+    kt0 = ks * (p.K / kBK);
     tail_out = p.tail_ws + (int64_t)u * 65536;
   } else {
     pid = xcd_remap(bid, p.tail_split > 0 ? p.full_tiles : p.tiles_m * p.tiles_n);
@@ -524,23 +547,47 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p0) {
   const int m0 = tm * 256, n0 = tn * 256;
   const int nk = p.K / kBK;
 
+  // Staging of the A (h = 0, 2: rows m0, m0 + 128) or B (h = 1, 3: columns n0, n0 + 128) half of local K-tile t,
+  // through the operand segments when there are any (wave-uniform selects).
+  const bool kseg = p.nseg > 1 && p.seg_k, nseg = p.nseg > 1 && !p.seg_k;
+  auto stage_half = [&](int t, int h, char* dst) {
+    const int tg = kt0 + t;
+    int k0 = tg * kBK;
+    const uint16_t* a = p.a;
+    const uint16_t* b = p.b;
+    int64_t lda = p.lda, ldb = p.ldb;
+    if (kseg) {
+      const int s = seg_of(p, tg);
+      k0 = (tg - pick4(s, 0, p.seg_end[0], p.seg_end[1], p.seg_end[2])) * kBK;
+      a = pick4(s, p.seg_a[0], p.seg_a[1], p.seg_a[2], p.seg_a[3]);
+      b = pick4(s, p.seg_b[0], p.seg_b[1], p.seg_b[2], p.seg_b[3]);
+      lda = pick4(s, p.seg_lda[0], p.seg_lda[1], p.seg_lda[2], p.seg_lda[3]);
+      ldb = pick4(s, p.seg_ldb[0], p.seg_ldb[1], p.seg_ldb[2], p.seg_ldb[3]);
+    }
+    if (h == 0 || h == 2) {
+      stage<128, AK>(a, lda, m0 + (h == 2 ? 128 : 0), p.M, k0, dst, wave, lane);
+    } else {
+      int c0 = n0 + (h == 3 ? 128 : 0), cmax = p.N;
+      if (nseg) {  // column segments: segment s owns columns [seg_end[s-1], seg_end[s]) of C
+        const int s = seg_of(p, c0);
+        const int start = pick4(s, 0, p.seg_end[0], p.seg_end[1], p.seg_end[2]);
+        b = pick4(s, p.seg_b[0], p.seg_b[1], p.seg_b[2], p.seg_b[3]);
+        ldb = pick4(s, p.seg_ldb[0], p.seg_ldb[1], p.seg_ldb[2], p.seg_ldb[3]);
+        cmax = pick4(s, p.seg_end[0], p.seg_end[1], p.seg_end[2], p.seg_end[3]) - start;
+        c0 -= start;
+      }
+      stage<128, BKM>(b, ldb, c0, cmax, k0, dst, wave, lane);
+    }
+  };
   // issue half-tile j (tile j>>2, half j&3) into buffer (j>>2)&1
   auto issue = [&](int j) {
     const int t = j >> 2, h = j & 3;
-    char* dst = smem + (t & 1) * STAGE + h * HALF;
-    if (h == 0) stage<128, AK>(p.a, p.lda, m0, p.M, t * kBK, dst, wave, lane);
-    else if (h == 2) stage<128, AK>(p.a, p.lda, m0 + 128, p.M, t * kBK, dst, wave, lane);
-    else if (h == 1) stage<128, BKM>(p.b, p.ldb, n0, p.N, t * kBK, dst, wave, lane);
-    else stage<128, BKM>(p.b, p.ldb, n0 + 128, p.N, t * kBK, dst, wave, lane);
+    stage_half(t, h, smem + (t & 1) * STAGE + h * HALF);
   };
   // the same with the half known at compile time (steady-state body: no branch on h)
   auto issue_h = [&](int t, auto hc) {
     constexpr int h = decltype(hc)::value;
-    char* dst = smem + (t & 1) * STAGE + h * HALF;
-    if constexpr (h == 0) stage<128, AK>(p.a, p.lda, m0, p.M, t * kBK, dst, wave, lane);
-    else if constexpr (h == 2) stage<128, AK>(p.a, p.lda, m0 + 128, p.M, t * kBK, dst, wave, lane);
-    else if constexpr (h == 1) stage<128, BKM>(p.b, p.ldb, n0, p.N, t * kBK, dst, wave, lane);
-    else stage<128, BKM>(p.b, p.ldb, n0 + 128, p.N, t * kBK, dst, wave, lane);
+    stage_half(t, h, smem + (t & 1) * STAGE + h * HALF);
   };
 
   f32x4 acc[2][4][2][2];
@@ -1108,6 +1155,266 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// 256x256x64 tiles, 4 waves (one per SIMD, 128 x 128 outputs each, 256 fp32 accumulators pinned to AGPRs), two
+// LDS stages of one K64 tile (2 x 64 KiB), every fragment of a K-tile held in registers:
+//   iteration t, phase A: 64 MFMAs on k-substep 0 of tile t while the 16 fragments of substep 1 are read out of
+//                         stage t % 2; lgkmcnt(0); barrier -> stage t % 2 is free on every wave
+//   phase B:              64 MFMAs on substep 1; the 16 LDS-DMA pieces (1 KiB each) of tile t + 2 are issued into
+//                         stage t % 2 between the first 32; vmcnt(16) (tile t + 1 landed: only tile t + 2's pieces
+//                         stay in flight) + barrier; the substep-0 fragments of tile t + 1 are read between the
+//                         last MFMAs.
+// Two barriers per K64 tile, a tile's loads in flight for a whole iteration, and a third less LDS read traffic per
+// MFMA than the 8-wave ping-pong kernel (128 x 128 wave tiles). The structure of the fastest vendor TN kernel on
+// gfx950 (hipBLASLt MT256x256x64 4-wave stream-K, measured in profiles/gemm_step_shapes_r5.md), written here for
+// every operand layout: K-major images [256][64] (128-B rows, chunk XOR (row >> 1) & 7, conflict-free
+// ds_read_b128), MN-major images [64][256] (512-B rows, mn_swz, ds_read_b64_tr_b16).
+template <bool KMAJ>
+struct Loader64 {
+  uint64_t base;    // wave-uniform address of (first row / column of the tile, k = 0)
+  uint64_t kstep;   // bytes per K64 tile
+  int voff[8];      // per-lane byte offsets of this wave's 8 pieces of the 32-KiB operand image
+
+  __device__ __forceinline__ void init(const uint16_t* g, int64_t ld, int r0, int rmax, int wave, int lane) {
+    base = reinterpret_cast<uint64_t>(g) + (KMAJ ? (uint64_t)r0 * ld * 2 : (uint64_t)r0 * 2);
+    kstep = KMAJ ? 128 : (uint64_t)ld * 128;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int q = i * 4 + wave;  // 1-KiB piece of the operand image
+      if constexpr (KMAJ) {
+        const int row = q * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((row >> 1) & 7);
+        const int gr = min(r0 + row, rmax - 1) - r0;
+        voff[i] = gr * (int)ld * 2 + c * 16;
+      } else {
+        const int lin = q * 64 + lane;
+        const int row = lin >> 5;  // k
+        const int lc = (lin & 31) ^ mn_swz(row);
+        const int gc = min(r0 + lc * 8, rmax - 8) - r0;
+        voff[i] = row * (int)ld * 2 + gc * 2;
+      }
+    }
+  }
+  __device__ __forceinline__ void load(int t, int i, uint32_t img, int wave) const {
+    const uint64_t b = base + (uint64_t)t * kstep;
+    i32x4 srd;
+    srd[0] = (int)(uint32_t)b;
+    srd[1] = (int)((uint32_t)(b >> 32) & 0xffff);
+    srd[2] = -1;
+    srd[3] = 0x00020000;
+    const uint32_t m0 = img + (uint32_t)(i * 4 + wave) * 1024u;
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff[i]), "s"(srd),
+                 "s"(m0)
+                 : "memory");
+  }
+};
+
+template <bool AK, bool BKM>
+__global__ __launch_bounds__(256, 1) void gemm4k_kernel(GemmArgs p) {
+  constexpr int OPB = 256 * 64 * 2;  // 32 KiB per operand image
+  constexpr int STAGE = 2 * OPB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // balanced tail as in gemm256_kernel
+  const int bid = (int)blockIdx.x;
+  int pid;
+  float* tail_out = nullptr;
+  if (p.tail_split > 0 && bid >= p.full_tiles) {
+    const int u = bid - p.full_tiles;
+    const int ks = u % p.tail_split;
+    pid = p.full_tiles + u / p.tail_split;
+    p.K /= p.tail_split;
+    p.a += (int64_t)ks * p.K * (AK ? 1 : p.lda);
+    p.b += (int64_t)ks * p.K * (BKM ? 1 : p.ldb);
+    tail_out = p.tail_ws + (int64_t)u * 65536;
+  } else {
+    pid = xcd_remap(bid, p.tail_split > 0 ? p.full_tiles : p.tiles_m * p.tiles_n);
+  }
+  int tm, tn;
+  tile_coords(pid, p.tiles_m, p.tiles_n, &tm, &tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int nk = p.K / 64;
+
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  Loader64<AK> la;
+  Loader64<BKM> lb;
+  la.init(p.a, p.lda, m0, p.M, wv, lane);
+  lb.init(p.b, p.ldb, n0, p.N, wv, lane);
+  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>(smem);
+  // piece i (0..7: A, 8..15: B) of this wave's share of K-tile t into stage t % 2
+  auto piece = [&](int t, int i) {
+    const uint32_t st = lds0 + (uint32_t)(t & 1) * STAGE;
+    if (i < 8) la.load(t, i, st, wv);
+    else lb.load(t, i - 8, st + OPB, wv);
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  asm volatile("s_nop 4" ::: "memory");  // v_accvgpr_write of the zeros -> first MFMA reading them as C
+
+  bf16x8_t a0[8], b0[8], a1[8], b1[8];
+  const int ar = wm * 128, bc = wn * 128;
+  // fragment r (0..7: A row group r, 8..15: B column group r - 8) of k-substep s of the tile in `stage`; the
+  // MFMA loops run B-group-major (the first MFMA operand, B, stays the same for 8 consecutive MFMAs), so the first
+  // 8 MFMAs of a substep need all A fragments and B fragment 0: read in this order
+  auto rdfrag = [&](const char* stage, int s, int r, bf16x8_t(&a)[8], bf16x8_t(&b)[8]) {
+    if (r < 8) a[r] = frag<256, AK>(stage, ar + r * 16, s, lane);
+    else b[r - 8] = frag<256, BKM>(stage + OPB, bc + (r - 8) * 16, s, lane);
+  };
+
+  // Event placement (MFMA index m = 8 * g + k within a phase, mirroring the vendor schedule): phase A reads the A
+  // fragments of substep 1 in m 1..15, B1 at m 23, A(t + 2) pieces in m 24..39, B fragments of substep 1 in
+  // m 25..40, B2 at m 55, B(t + 2) pieces from m 56 of phase A to m 7 of phase B; B3 (tile t + 1 landed) at phase-B
+  // m 27; the substep-0 fragments of tile t + 1 over phase-B m 28..59.
+  auto iter = [&](int t, auto steady) {
+    constexpr bool S = decltype(steady)::value;
+    const char* cur = smem + (t & 1) * STAGE;
+    const char* nxt = smem + ((t + 1) & 1) * STAGE;
+    const bool iss = S || t + 2 < nk;
+    const bool more = S || t + 1 < nk;
+#pragma unroll
+    for (int g = 0; g < 8; ++g)  // g: B column group (MFMA operand A, the output columns)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {  // k: A row group
+        const int m = 8 * g + k;
+        mfma_acc(acc[k][g], b0[g], a0[k]);
+        if (m >= 1 && m <= 15 && (m & 1)) rdfrag(cur, 1, m >> 1, a1, b1);            // A substep 1: r 0..7
+        if (m == 23) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          bar();  // B1: every wave holds A(t)
+        }
+        if (m >= 24 && m <= 39 && !(m & 1) && iss) piece(t + 2, (m - 24) >> 1);     // A(t + 2): pieces 0..7
+        if (m >= 25 && m <= 40 && (m & 1)) rdfrag(cur, 1, 8 + ((m - 25) >> 1), a1, b1);  // B substep 1: r 8..15
+        if (m == 55) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          bar();  // B2: every wave holds B(t)
+        }
+        if (m >= 56 && !(m & 1) && iss) piece(t + 2, 8 + ((m - 56) >> 1));          // B(t + 2): pieces 8..11
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+    for (int g = 0; g < 8; ++g)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int m = 8 * g + k;
+        mfma_acc(acc[k][g], b1[g], a1[k]);
+        if (m <= 7 && !(m & 1) && iss) piece(t + 2, 12 + (m >> 1));                 // B(t + 2): pieces 12..15
+        if (m == 27) {
+          if (iss) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile t + 1 landed, t + 2 in flight
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          bar();  // B3: tile t + 1 visible to every wave
+        }
+        if (m >= 28 && m <= 59 && !(m & 1) && more) rdfrag(nxt, 0, (m - 28) >> 1, a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+  };
+
+  // prologue: tiles 0 and 1 in flight, substep 0 of tile 0 in registers
+#pragma unroll
+  for (int i = 0; i < 16; ++i) piece(0, i);
+  if (nk > 1) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) piece(1, i);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  bar();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) rdfrag(smem, 0, r, a0, b0);
+  int t = 0;
+#pragma unroll 1
+  for (; t + 2 < nk; ++t) iter(t, True_{});
+#pragma unroll 1
+  for (; t < nk; ++t) iter(t, False_{});
+  // the last MFMAs' results -> v_accvgpr_read by compiler code (hipcc pads nothing after an asm MFMA)
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 7" ::: "memory");
+
+  if (tail_out) {  // K-slice of a tail tile: raw fp32 partial, row-major 256 x 256
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = ar + i * 16 + (lane & 15);
+        const int c = bc + j * 16 + 4 * (lane >> 4);
+        const f32x4 v = acc[i][j];
+        *reinterpret_cast<float4*>(tail_out + r * 256 + c) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    return;
+  }
+
+  const int flags = p.flags;
+  if (!(flags & (kEpiAux | kEpiAccum | kEpiOutF32))) {
+    // one-pass bf16 epilogue (as gemm256_kernel): alpha / bias / GELU in registers, [256][264] bf16 image,
+    // row-coalesced 16-byte stores
+    uint16_t* im = reinterpret_cast<uint16_t*>(smem);
+    constexpr int RSB = kEpiRowStrideBf16;
+    bar();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = bc + j * 16 + 4 * (lane >> 4);
+      float bq[4] = {0.f, 0.f, 0.f, 0.f};
+      if ((flags & kEpiBias) && n0 + c < p.N) {
+        const uint2 braw = *reinterpret_cast<const uint2*>(p.bias + n0 + c);
+        bq[0] = lo_bf16(braw.x); bq[1] = hi_bf16(braw.x); bq[2] = lo_bf16(braw.y); bq[3] = hi_bf16(braw.y);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = ar + i * 16 + (lane & 15);
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = acc[i][j][e] * p.alpha + bq[e];
+          if (flags & kEpiGelu) v[e] = gelu_tanh(v[e]);
+        }
+        *reinterpret_cast<uint2*>(im + r * RSB + c) = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
+      }
+    }
+    bar();
+    const int ecb = (tid & 31) * 8, erb = tid >> 5;  // 8 rows per step
+    const int nb_ = n0 + ecb;
+    if (nb_ < p.N) {
+#pragma unroll 4
+      for (int step = 0; step < 32; ++step) {
+        const int r = step * 8 + erb;
+        const int m = m0 + r;
+        if (m >= p.M) break;
+        *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(p.c) + (int64_t)m * p.ldc + nb_) =
+            *reinterpret_cast<const uint4*>(im + r * RSB + ecb);
+      }
+    }
+    return;
+  }
+  // general epilogue through the fp32 LDS image, one 128-row half at a time
+  float* img = reinterpret_cast<float*>(smem);
+  float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  {
+    const int n = n0 + (tid & 31) * 8;
+    if ((flags & kEpiBias) && n < p.N) load8<bf16>(reinterpret_cast<const bf16*>(p.bias + n), bv);
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    bar();
+    if (wm == h) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int r = i * 16 + (lane & 15);
+          const int c = bc + j * 16 + 4 * (lane >> 4);
+          *reinterpret_cast<f32x4*>(img + r * kEpiRowStride + c) = acc[i][j];
+        }
+    }
+    bar();
+    epi_rows<256>(p, img, m0 + h * 128, n0, tid, bv);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // 256 x 160 x 64 tiles in a 3-stage LDS ring (3 x 52 KiB = 156 KiB of the 160 KiB LDS): two K-tiles
 // of glds stay in flight while one is consumed, so the global->LDS latency is hidden by two K-tiles of
 // MFMA work instead of one (PMC on the 256x256 two-stage kernel: 36 % of wave cycles waiting on
@@ -1650,6 +1957,65 @@ PA_EXPORT int pa_gemm_bf16_pp(const void* a, const void* b, void* c, const void*
   return (int)hipGetLastError();
 }
 
+// Segmented operands on the ping-pong kernel (GemmArgs::nseg): seg = [nseg][5] int64 host array of
+// {a_ptr, b_ptr, lda, ldb, end} per segment (end: K-tiles x 64 = K elements for seg_k = 1, columns for seg_k = 0),
+// same operand layouts in every segment. K = total K (seg_k) or the A operand's K; N = total columns. a / b in
+// the call are unused for the segmented operand. Workspace as pa_gemm_bf16_pp(M, N, K).
+PA_EXPORT int pa_gemm_bf16_pp_segs(const int64_t* seg, int nseg, int seg_k, const void* a, const void* b, void* c,
+                                   const void* bias, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
+                                   int64_t ldc, int a_kmajor, int b_kmajor, int flags, float alpha, void* ws,
+                                   hipStream_t st) {
+  if (nseg < 1 || nseg > 4 || K % kBK != 0 || N % 8 != 0 || ldc % 4 != 0) return 1;
+  if (!a_kmajor && M % 8 != 0) return 1;
+  if (flags & (kEpiAux | kEpiStats)) return 1;
+  if (M <= 0 || N <= 0) return 0;
+  GemmArgs g{};
+  g.a = (const uint16_t*)a; g.b = (const uint16_t*)b; g.c = c; g.bias = (const uint16_t*)bias;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.nseg = nseg; g.seg_k = seg_k;
+  int64_t prev = 0;
+  for (int s = 0; s < 4; ++s) {
+    const int64_t* e = seg + 5 * (s < nseg ? s : nseg - 1);
+    g.seg_a[s] = (const uint16_t*)e[0];
+    g.seg_b[s] = (const uint16_t*)e[1];
+    g.seg_lda[s] = e[2];
+    g.seg_ldb[s] = e[3];
+    if (s < nseg) {
+      const int64_t end = e[4];
+      if (end <= prev || e[2] % 8 != 0 || e[3] % 8 != 0) return 1;
+      if (seg_k ? (end % kBK != 0) : (end % 128 != 0 && s + 1 < nseg)) return 1;
+      g.seg_end[s] = (int)(seg_k ? end / kBK : end);
+      prev = end;
+    } else {
+      g.seg_end[s] = g.seg_end[nseg - 1];
+    }
+  }
+  if (seg_k ? prev != K : prev != N) return 1;
+  if (!seg_k && (lda % 8 != 0)) return 1;
+  if (seg_k && (flags & kEpiBias)) return 1;
+  g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.flags = flags; g.alpha = alpha;
+  g.c_split = M * ldc;
+  int full, split;
+  pp_plan(M, N, K, device_cus(), &full, &split);
+  if (split && !ws) split = 0;
+  g.tiles_m = (int)((M + 255) / 256);
+  g.tiles_n = (int)((N + 255) / 256);
+  const int T = g.tiles_m * g.tiles_n;
+  g.full_tiles = split ? full : T;
+  g.tail_split = split;
+  g.tail_ws = (float*)ws;
+  const int grid = split ? full + (T - full) * split : T;
+  int rc;
+  if (a_kmajor && !b_kmajor) rc = launch256<true, false>(g, 1, st, grid);
+  else if (a_kmajor && b_kmajor) rc = launch256<true, true>(g, 1, st, grid);
+  else if (!a_kmajor && !b_kmajor) rc = launch256<false, false>(g, 1, st, grid);
+  else rc = launch256<false, true>(g, 1, st, grid);
+  if (rc || !split) return rc;
+  hipLaunchKernelGGL(gemm_tail_reduce_k, dim3(T - full, 64), dim3(256), 0, st, g);
+  return (int)hipGetLastError();
+}
+
 // 4-wave 256x256 GEMM (gemm4w_kernel; same operands / flags / workspace as pa_gemm_bf16_pp).
 PA_EXPORT int pa_gemm_bf16_4w(const void* a, const void* b, void* c, const void* bias, void* aux, int64_t M, int64_t N,
                               int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor, int b_kmajor, int flags,
@@ -1690,6 +2056,52 @@ PA_EXPORT int pa_gemm_bf16_4w(const void* a, const void* b, void* c, const void*
   else if (!a_kmajor && !b_kmajor) PA_G4(false, false, 2);
   else PA_G4(false, true, 3);
 #undef PA_G4
+  int rc = (int)hipGetLastError();
+  if (rc || !split) return rc;
+  hipLaunchKernelGGL(gemm_tail_reduce_k, dim3(T - full, 64), dim3(256), 0, st, g);
+  return (int)hipGetLastError();
+}
+
+// 4-wave K64 GEMM (gemm4k_kernel; same operands / flags / workspace as pa_gemm_bf16_pp).
+PA_EXPORT int pa_gemm_bf16_4k(const void* a, const void* b, void* c, const void* bias, void* aux, int64_t M, int64_t N,
+                              int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor, int b_kmajor, int flags,
+                              float alpha, void* ws, hipStream_t st) {
+  if (K % kBK != 0 || N % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || ldc % 4 != 0) return 1;
+  if (!a_kmajor && M % 8 != 0) return 1;
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  GemmArgs g{};
+  g.a = (const uint16_t*)a; g.b = (const uint16_t*)b; g.c = c;
+  g.bias = (const uint16_t*)bias; g.aux = (uint16_t*)aux;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.flags = flags; g.alpha = alpha;
+  int full, split;
+  pp_plan(M, N, K, device_cus(), &full, &split);
+  if (split && !ws) split = 0;
+  g.tiles_m = (int)((M + 255) / 256);
+  g.tiles_n = (int)((N + 255) / 256);
+  const int T = g.tiles_m * g.tiles_n;
+  g.full_tiles = split ? full : T;
+  g.tail_split = split;
+  g.tail_ws = (float*)ws;
+  const int grid = split ? full + (T - full) * split : T;
+  constexpr int kLoop = 2 * 2 * 256 * 64 * 2, kEpiB = 256 * kEpiRowStrideBf16 * 2, kEpiF = 128 * kEpiRowStride * 4;
+  constexpr int smem = kLoop > kEpiB ? (kLoop > kEpiF ? kLoop : kEpiF) : (kEpiB > kEpiF ? kEpiB : kEpiF);
+  static bool attr_set[4] = {false, false, false, false};
+#define PA_G4K(AKV, BKV, I)                                                                                     \
+  do {                                                                                                          \
+    if (!attr_set[I]) {                                                                                         \
+      (void)hipFuncSetAttribute((const void*)gemm4k_kernel<AKV, BKV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                smem);                                                                          \
+      attr_set[I] = true;                                                                                       \
+    }                                                                                                           \
+    hipLaunchKernelGGL((gemm4k_kernel<AKV, BKV>), dim3(grid), dim3(256), smem, st, g);                          \
+  } while (0)
+  if (a_kmajor && !b_kmajor) PA_G4K(true, false, 0);
+  else if (a_kmajor && b_kmajor) PA_G4K(true, true, 1);
+  else if (!a_kmajor && !b_kmajor) PA_G4K(false, false, 2);
+  else PA_G4K(false, true, 3);
+#undef PA_G4K
   int rc = (int)hipGetLastError();
   if (rc || !split) return rc;
   hipLaunchKernelGGL(gemm_tail_reduce_k, dim3(T - full, 64), dim3(256), 0, st, g);

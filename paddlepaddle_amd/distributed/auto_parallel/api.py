@@ -423,7 +423,7 @@ class DistModel:
         if loss is not None and optimizer is not None and getattr(strategy, "full_graph", True) and any(
                 _is_dist(p._t) for p in layer.parameters()):
             from .static_engine import StaticEngine
-            self._engine = StaticEngine(layer, loss, getattr(optimizer, "_inner_opt", optimizer), strategy)
+            self._engine = StaticEngine(layer, loss, optimizer, strategy)
         self._loader = loader
         self._loss = loss
         self._opt = optimizer

@@ -185,7 +185,8 @@ _ELEMENTWISE = {
     "masked_fill", "erf", "sin", "cos", "reciprocal", "sign", "__eq__", "__ne__", "__lt__", "__gt__", "__le__",
     "__ge__", "logical_not", "cast", "astype", "bias_gelu", "gelu_tanh", "requires_grad_",
 }
-_ROWWISE = {"rms_norm", "layer_norm", "softmax", "log_softmax", "softmax_cross_entropy", "fused_softmax"}
+_ROWWISE = {"rms_norm", "layer_norm", "softmax", "log_softmax", "softmax_cross_entropy", "fused_softmax",
+            "rms_norm_residual", "layer_norm_residual"}
 _RESHAPE = {"view", "reshape", "flatten", "unflatten"}
 _TRANSPOSE = {"transpose", "permute", "t"}
 _REDUCE = {"sum", "mean"}
@@ -254,6 +255,22 @@ class _LNode:
 
 class StaticEngine:
     def __init__(self, layer, loss_fn, optimizer, strategy):
+        # a dist.shard_optimizer wrapper: the engine updates its local parameter shards with the inner optimizer;
+        # ZeRO partitioning of that state over a data-parallel mesh dim is not implemented here, so it must not be
+        # requested silently (degree 1 is the plain update)
+        shard_fn = getattr(optimizer, "_shard_fn", None)
+        inner = getattr(optimizer, "_inner_opt", optimizer)
+        if shard_fn is not None and getattr(shard_fn, "_mesh", None) is not None:
+            m, d = shard_fn._mesh, shard_fn._dim
+            size = m.get_dim_size(m.dim_names[d]) if isinstance(d, int) else m.get_dim_size(d)
+            if size > 1 or strategy.sharding.get("enable", False) and int(strategy.sharding.get("degree", 1)) > 1:
+                raise NotImplementedError(
+                    f"static auto-parallel engine: {type(shard_fn).__name__} over a mesh dim of size {size} "
+                    "(optimizer-state sharding) is not implemented; use the dygraph DistModel path or dp_config "
+                    "sharding_level 0")
+        elif strategy.sharding.get("enable", False) and int(strategy.sharding.get("degree", 1)) > 1:
+            raise NotImplementedError("static auto-parallel engine: strategy.sharding with degree > 1")
+        optimizer = inner
         self.layer, self.loss_fn, self.opt, self.strategy = layer, loss_fn, optimizer, strategy
         pp = strategy.pipeline
         self.acc = max(1, int(pp.accumulate_steps)) if pp.enable else 1
@@ -261,6 +278,19 @@ class StaticEngine:
         self.built = False
         self.rank = C.get_rank()
         self._consts = {}
+        # strategy fields this engine does not implement fail loudly instead of being ignored
+        unsupported = []
+        if strategy.recompute.get("enable", False):
+            unsupported.append("recompute (use models' use_recompute / fleet recompute on the dygraph path)")
+        if strategy.sp_optimization.get("enable", False):
+            unsupported.append("sp_optimization")
+        if strategy.mp_optimization.get("allreduce_matmul_grad_overlapping", False):
+            unsupported.append("mp_optimization.allreduce_matmul_grad_overlapping")
+        if strategy.gradient_merge.get("enable", False):
+            unsupported.append("gradient_merge (use strategy.pipeline.accumulate_steps)")
+        if unsupported:
+            raise NotImplementedError("static auto-parallel engine: unsupported strategy settings: " +
+                                      ", ".join(unsupported))
 
     # ---------------------------------------------------------------- build
     def _stage_meshes(self, params):
@@ -328,9 +358,43 @@ class StaticEngine:
                 if id(p) in saved:
                     p._t = saved[id(p)]
         self.loss_slot = prog._slot_of[id(loss._t)]
+        self._apply_passes()
         self._propagate_and_partition()
         self._localize_params()
         self.built = True
+
+    def _apply_passes(self):
+        """Program passes on the traced global program before placement propagation (reference: the engine's
+        fused passes, auto_parallel/static/engine.py:675 and static/pir_pass.py). ``strategy.fused_passes``:
+        ``sibling_linears`` (default on: q / k / v and gate / up linears of one input -> one multi_linear node, whose
+        weights keep their own placements and must agree to fuse), ``rms_norm_residual`` (default on: the residual
+        gradient of a pre-norm block summed inside the RMSNorm backward). ``strategy.amp`` runs auto_parallel_amp
+        on the program."""
+        from ..passes import new_pass
+        fp = self.strategy.fused_passes
+        self.pass_stats = {}
+        if fp.get("rms_norm_residual", True):
+            ctx = new_pass("fuse_rms_norm_residual").apply(self.prog, None)
+            self.pass_stats["rms_norm_residual"] = ctx.get_attr("fuse_rms_norm_residual.fused", 0)
+        if fp.get("sibling_linears", True):
+            info = self.info
+            p = new_pass("fuse_sibling_linears", {
+                "weights": set(self.param_slots.values()),
+                "group_key": lambda s: (self._mesh_key(info[s].mesh), tuple(map(str, info[s].pl)))
+                if s in info else None})
+            ctx = p.apply(self.prog, None)
+            self.pass_stats["sibling_linears"] = ctx.get_attr("fuse_sibling_linears.fused", 0)
+        amp = self.strategy.amp
+        if amp.get("enable", False):
+            ctx = new_pass("auto_parallel_amp", {"dtype": amp.get("dtype", "bfloat16")}).apply(self.prog, None)
+            self.pass_stats["amp"] = True
+
+    @staticmethod
+    def _mesh_key(m):
+        """Value identity of a ProcessMesh (parameters of one stage may carry distinct but equal mesh objects)."""
+        if m is None:
+            return None
+        return (tuple(int(i) for i in m.process_ids), tuple(int(d) for d in m.shape), tuple(m.dim_names or ()))
 
     def _batch_pl(self):
         m = self.meshes[0]
@@ -519,6 +583,15 @@ class StaticEngine:
             return [], rep, {}
         if name == "fused_linear" and len(refs) >= 2:
             return self._rule_linear(refs, ins, nd)
+        if name == "multi_linear" and len(refs) >= 2:
+            # sibling linears of one input (fuse_sibling_linears): the weights share their placements, so the
+            # single-linear rule of (x, W_0) holds for every W_i
+            want, out, ctp = self._rule_linear(refs[:2], ins[:2], nd)
+            want = list(want) + [want[1]] * (len(refs) - 2)
+            for r in refs[2:]:
+                if refs[1].i in ctp:
+                    ctp[r.i] = set(ctp[refs[1].i])
+            return want, out, ctp
         if name == "embedding" and len(refs) >= 2:
             return self._rule_embedding(refs, ins, nd)
         want = [list(i.pl) for i in ins]

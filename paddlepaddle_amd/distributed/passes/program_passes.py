@@ -21,7 +21,8 @@ import torch
 from .pass_base import PassBase, PassType, register_pass
 from ...static import program as P
 
-__all__ = ["FuseGemmEpiloguePass", "DeadCodeEliminationPass", "AMPPass", "FP16Pass", "GradientMergePass"]
+__all__ = ["FuseGemmEpiloguePass", "DeadCodeEliminationPass", "AMPPass", "FP16Pass", "GradientMergePass",
+           "FuseSiblingLinearsPass", "FuseRMSNormResidualPass"]
 
 _RELU = {"f:torch.nn.functional:relu", "f:torch:relu", "m:relu"}
 _GELU = {"o:paddlepaddle_amd.ops.activation:gelu", "f:torch.nn.functional:gelu"}
@@ -278,3 +279,129 @@ class GradientMergePass(PassBase):
             raise ValueError("auto_parallel_gradient_merge needs a program with optimizer.minimize(loss)")
         prog._grad_merge = (int(self.get_attr("k_steps", 1)), bool(self.get_attr("avg", True)))
         prog._gm_count = 0
+
+
+# ------------------------------------------------------------------------------------------------------------------
+_MULTI = "o:paddlepaddle_amd.ops.linear:multi_linear"
+
+
+@register_pass("fuse_sibling_linears")
+class FuseSiblingLinearsPass(PassBase):
+    """Sibling linears -> one ``ops.linear.multi_linear`` node (reference: fuse_attention_ffn_qkv_pass,
+    auto_parallel/static/engine.py:675, which concatenates the q / k / v and gate / up weights into new fused
+    parameters). Here every ``fused_linear(x, W_i)`` (no bias, no activation) that reads the same input x becomes
+    ONE node computing all outputs with an N-segmented GEMM and, in backward, the input gradient with one
+    K-segmented GEMM — the parameters stay separate, so sharding, checkpoints and optimizer state are untouched.
+
+    Attributes: ``weights`` (optional set of slots the W_i must belong to: the parameters), ``group_key`` (optional
+    callable slot -> key; only weights with equal keys fuse, e.g. their distributed placements), ``max_group``
+    (default 4: the segment limit of the GEMM)."""
+
+    def _type(self):
+        return PassType.FUSION_OPT
+
+    def _apply_single_impl(self, prog, startup, context):
+        ml = P._resolve(_MULTI)
+        weights = self.get_attr("weights")
+        key_of = self.get_attr("group_key") or (lambda s: None)
+        max_group = int(self.get_attr("max_group", 4))
+        nodes = prog.nodes
+        producer = {}
+        for i, n in enumerate(nodes):
+            if not isinstance(n, P.CFNode):
+                for s in P._node_writes(n):
+                    producer.setdefault(s, i)
+        groups = {}
+        for i, n in enumerate(nodes):
+            if isinstance(n, P.CFNode) or n.kind == "guard" or n.name != _LINEAR or n.kwargs:
+                continue
+            args = tuple(n.args)
+            if len(args) > 2 and any(a is not None for a in args[2:]):
+                continue  # bias / activation / hooks: keep the plain fused_linear
+            x = _slot(args[0]) if args else None
+            warg = args[1] if len(args) > 1 else None
+            if x is None or not isinstance(n.outs, P._Ref):
+                continue
+            if isinstance(warg, P._Ref):  # a traced weight (the auto-parallel engine's parameter slots)
+                w, wm = warg.i, prog._metas[warg.i]
+                if weights is not None and w not in weights:
+                    continue
+                key = key_of(w)
+            elif isinstance(warg, P._Const):  # a static-graph parameter captured as a program constant
+                w, wm, key = None, warg.t, None
+            else:
+                continue
+            if wm.dim() != 2:
+                continue
+            groups.setdefault((x, wm.shape[0], wm.dtype, key), []).append(i)
+        fused = 0
+        dead = set()
+        for (x, _, _, _), idxs in groups.items():
+            for c in range(0, len(idxs), max_group):
+                chunk = idxs[c:c + max_group]
+                if len(chunk) < 2:
+                    continue
+                first = chunk[0]
+                ws = [nodes[i].args[1] for i in chunk]
+                # every weight must exist where the first linear runs (parameters do; a derived weight must be
+                # produced before it)
+                if any(_slot(w) is not None and producer.get(_slot(w), -1) > first for w in ws):
+                    continue
+                outs = [nodes[i].outs for i in chunk]
+                nodes[first] = P.OpNode(ml, (nodes[first].args[0], list(ws)), {}, outs, "op", _MULTI)
+                dead.update(chunk[1:])
+                fused += len(chunk)
+        if dead:
+            prog.nodes[:] = [n for k, n in enumerate(nodes) if k not in dead]
+        context.set_attr("fuse_sibling_linears.fused", context.get_attr("fuse_sibling_linears.fused", 0) + fused)
+
+
+# the reference's name for the same rewrite
+PassBase._REGISTERED_PASSES["fuse_attention_ffn_qkv"] = FuseSiblingLinearsPass
+
+_RMS = "o:paddlepaddle_amd.ops.norm:rms_norm"
+_RMS_RES = "o:paddlepaddle_amd.ops.norm:rms_norm_residual"
+
+
+@register_pass("fuse_rms_norm_residual")
+class FuseRMSNormResidualPass(PassBase):
+    """Pre-norm residual blocks: ``h = rms_norm(x, w)`` where x also feeds a residual ``add`` becomes
+    ``(r, h) = rms_norm_residual(x, w)`` with the add reading r: on the HIP path the residual branch's gradient
+    is summed into dx inside the RMSNorm backward kernel (pa_rms_norm_bwd_res) instead of autograd's separate
+    bf16 accumulation add — the op-level form of the fusion models/llama.py applies in its norm layers."""
+
+    def _type(self):
+        return PassType.FUSION_OPT
+
+    def _apply_single_impl(self, prog, startup, context):
+        rr = P._resolve(_RMS_RES)
+        nodes = prog.nodes
+        readers = {}
+        for i, n in enumerate(nodes):
+            if isinstance(n, P.CFNode):
+                continue
+            for s in P._node_reads(n):
+                readers.setdefault(s, []).append(i)
+        fused = 0
+        for i, n in enumerate(list(nodes)):
+            if isinstance(n, P.CFNode) or n.name != _RMS or n.kwargs or not isinstance(n.outs, P._Ref):
+                continue
+            x = _slot(n.args[0]) if n.args else None
+            if x is None:
+                continue
+            others = [j for j in readers.get(x, []) if j != i]
+            adds = [j for j in others if nodes[j].name in _ADD and not nodes[j].kwargs and j > i
+                    and any(_slot(a) == x for a in nodes[j].args)]
+            if len(others) != 1 or len(adds) != 1:
+                continue  # x must feed exactly this norm and one residual add
+            j = adds[0]
+            m = prog._metas[x]
+            with torch._C.DisableTorchFunction():
+                r = prog._new_slot(torch.empty(tuple(m.shape), dtype=m.dtype, device="meta")
+                                   .requires_grad_(m.requires_grad))
+            nodes[i] = P.OpNode(rr, tuple(n.args), {}, (P._Ref(r), n.outs), "op", _RMS_RES)
+            a = nodes[j]
+            nodes[j] = P.OpNode(a.func, tuple(P._Ref(r) if _slot(v) == x else v for v in a.args), {}, a.outs, a.kind,
+                                a.name)
+            fused += 1
+        context.set_attr("fuse_rms_norm_residual.fused", context.get_attr("fuse_rms_norm_residual.fused", 0) + fused)

@@ -46,6 +46,9 @@ class LlamaConfig:
     pad_token_id: int = 0
     bos_token_id: int = 1
     eos_token_id: int = 2
+    # attention head width when it is not hidden_size / num_attention_heads (e.g. the tensor-parallel-local shape
+    # of one rank: LLaMA-2 70B at TP 2 keeps hidden 8192 but 32 query heads of 128)
+    attention_head_dim: int = 0
 
     @staticmethod
     def llama2_7b(**kw):
@@ -82,16 +85,18 @@ class LlamaConfig:
 
     @property
     def head_dim(self):
-        return self.hidden_size // self.num_attention_heads
+        return self.attention_head_dim or self.hidden_size // self.num_attention_heads
 
     def num_params(self):
         h, f, L, V = self.hidden_size, self.intermediate_size, self.num_hidden_layers, self.vocab_size
+        q = self.num_attention_heads * self.head_dim
         kv = self.num_key_value_heads * self.head_dim
-        per = h * (h + 2 * kv) + h * h + 3 * h * f + 2 * h
+        per = h * (q + 2 * kv) + q * h + 3 * h * f + 2 * h
         return L * per + V * h * (1 if self.tie_word_embeddings else 2) + h
 
     def flops_per_token(self, seq_len):
-        return 6 * self.num_params() + 12 * self.num_hidden_layers * self.hidden_size * seq_len
+        q = self.num_attention_heads * self.head_dim
+        return 6 * self.num_params() + 12 * self.num_hidden_layers * q * seq_len
 
 
 def _tp():
@@ -146,13 +151,14 @@ class LlamaAttention(nn.Layer):
         h = cfg.hidden_size
         out = (cfg.num_attention_heads + 2 * cfg.num_key_value_heads) * self.D
         init = nn.ParamAttr(initializer=I.Normal(0.0, cfg.initializer_range))
+        qw = cfg.num_attention_heads * self.D  # attention width (= h unless attention_head_dim is set)
         if self.tp > 1:
             tp = _tp()
             self.qkv_proj = tp.ColumnParallelLinear(h, out, weight_attr=init, has_bias=False, gather_output=False)
-            self.o_proj = tp.RowParallelLinear(h, h, weight_attr=init, has_bias=False, input_is_parallel=True)
+            self.o_proj = tp.RowParallelLinear(qw, h, weight_attr=init, has_bias=False, input_is_parallel=True)
         else:
             self.qkv_proj = nn.Linear(h, out, weight_attr=init, bias_attr=False)
-            self.o_proj = nn.Linear(h, h, weight_attr=init, bias_attr=False)
+            self.o_proj = nn.Linear(qw, h, weight_attr=init, bias_attr=False)
         self.rope = _Rope(self.D, cfg.rope_theta)
 
     def _qkv(self, x):

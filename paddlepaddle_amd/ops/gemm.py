@@ -76,16 +76,121 @@ def gemm(a, b, bias=None, gelu=False, aux=None, out=None, accumulate=False, alph
         flags |= EPI_OUT_F32
     if bn is None:
         bn = _pick_bn(M, N, bk)
-    if bn in (1, 2) and L.has("pa_gemm_bf16_pp"):  # 256x256 (1: 8-wave ping-pong, 2: 4-wave) + balanced tail
+    if bn in (1, 2, 3) and L.has("pa_gemm_bf16_pp"):
+        # 256x256 + balanced tail: 1 8-wave ping-pong, 2 4-wave K32 ring, 3 4-wave K64 two-stage (gemm4k_kernel)
         nb = int(L.lib().pa_gemm_pp_ws_bytes(M, N, K))
         ws = torch.empty(nb // 4, dtype=torch.float32, device=a.device) if nb else None
-        L.call("pa_gemm_bf16_pp" if bn == 1 else "pa_gemm_bf16_4w", L.ptr(a), L.ptr(b), L.ptr(out), L.ptr(bias),
+        fn = {1: "pa_gemm_bf16_pp", 2: "pa_gemm_bf16_4w", 3: "pa_gemm_bf16_4k"}[bn]
+        L.call(fn, L.ptr(a), L.ptr(b), L.ptr(out), L.ptr(bias),
                L.ptr(aux), M, N, K, lda, ldb, out.stride(0), int(ak), int(bk), flags, float(alpha), L.ptr(ws),
                L.stream_ptr())
         return out
     L.call("pa_gemm_bf16", L.ptr(a), L.ptr(b), L.ptr(out), L.ptr(bias), L.ptr(aux), M, N, K, lda, ldb, out.stride(0),
            int(ak), int(bk), flags, float(alpha), int(bn), 1, L.stream_ptr())
     return out
+
+
+def _seg_table(rows):
+    return torch.tensor(rows, dtype=torch.int64)  # host [nseg][5]: a_ptr, b_ptr, lda, ldb, end
+
+
+def gemm_kseg_supported(As, Bs):
+    """C = sum_i As[i] @ Bs[i] as one K-segmented launch: 1-4 segments, every pair passes ``supported``, the same
+    operand layouts in every segment, each K_i % 64 == 0, equal M / N."""
+    if not (L.has("pa_gemm_bf16_pp_segs") and 1 <= len(As) <= 4 and len(As) == len(Bs)):
+        return False
+    M, N = As[0].shape[0], Bs[0].shape[1]
+    la, lb = None, None
+    for a, b in zip(As, Bs):
+        if a.shape[0] != M or b.shape[1] != N or a.shape[1] != b.shape[0] or a.shape[1] % 64 or not supported(a, b):
+            return False
+        ka, kb = _layout(a, 0)[1], _layout(b, 1)[1]
+        if la is None:
+            la, lb = ka, kb
+        elif (ka, kb) != (la, lb):
+            return False
+    return True
+
+
+def gemm_kseg(As, Bs, out=None, accumulate=False, alpha=1.0):
+    """C = alpha * sum_i As[i] @ Bs[i] (``accumulate``: C +=) as ONE GEMM over K = sum K_i whose K-tiles read the
+    operand pair of their segment (csrc/kernels/gemm.hip pa_gemm_bf16_pp_segs, seg_k = 1): the data gradient of
+    sibling linears that share an input (dx = sum dy_i W_i^T), the weight gradients of two accumulation micro-batches
+    (ops/linear.py pair_weight_grads) — one launch, one output pass, no concatenated copies."""
+    M, N = As[0].shape[0], Bs[0].shape[1]
+    K = sum(a.shape[1] for a in As)
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=As[0].device)
+    assert out.stride(1) == 1 and out.stride(0) % 4 == 0
+    rows, end = [], 0
+    for a, b in zip(As, Bs):
+        end += a.shape[1]
+        rows.append([a.data_ptr(), b.data_ptr(), _layout(a, 0)[0], _layout(b, 1)[0], end])
+    ak, bk = _layout(As[0], 0)[1], _layout(Bs[0], 1)[1]
+    flags = (EPI_ACCUM if accumulate else 0) | (EPI_OUT_F32 if out.dtype == torch.float32 else 0)
+    nb = int(L.lib().pa_gemm_pp_ws_bytes(M, N, K))
+    ws = torch.empty(nb // 4, dtype=torch.float32, device=out.device) if nb else None
+    tab = _seg_table(rows)
+    rc = L.call("pa_gemm_bf16_pp_segs", tab.data_ptr(), len(rows), 1, L.ptr(As[0]), L.ptr(Bs[0]), L.ptr(out),
+                L.ptr(None), M, N, K, rows[0][2], rows[0][3], out.stride(0), int(ak), int(bk), flags, float(alpha),
+                L.ptr(ws), L.stream_ptr())
+    if rc:
+        raise RuntimeError(f"pa_gemm_bf16_pp_segs (K) failed ({rc}) for M={M} N={N} K={K}")
+    return out
+
+
+def gemm_nseg_supported(a, Bs):
+    """C = a @ [Bs[0] | Bs[1] | ...] as one N-segmented launch: 1-4 segments of the same layout and K, every
+    segment but the last 128-column aligned."""
+    if not (L.has("pa_gemm_bf16_pp_segs") and 1 <= len(Bs) <= 4):
+        return False
+    K = a.shape[1]
+    lay = None
+    for i, b in enumerate(Bs):
+        if b.shape[0] != K or not supported(a, b) or (i + 1 < len(Bs) and b.shape[1] % 128):
+            return False
+        kb = _layout(b, 1)[1]
+        if lay is None:
+            lay = kb
+        elif kb != lay:
+            return False
+    return True
+
+
+def gemm_nseg(a, Bs, out=None, alpha=1.0):
+    """C [M, sum N_i] = alpha * a @ [Bs[0] | Bs[1] | ...] as ONE GEMM whose column tiles read the weight of their
+    segment (pa_gemm_bf16_pp_segs, seg_k = 0): the q / k / v or gate / up projections of one input with separate
+    weight tensors, no concatenated weight copy; the per-projection outputs are column views of C."""
+    M, K = a.shape
+    N = sum(b.shape[1] for b in Bs)
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    assert out.stride(1) == 1 and out.stride(0) % 4 == 0
+    rows, end = [], 0
+    for b in Bs:
+        end += b.shape[1]
+        rows.append([a.data_ptr(), b.data_ptr(), _layout(a, 0)[0], _layout(b, 1)[0], end])
+    lda, ak = _layout(a, 0)
+    bk = _layout(Bs[0], 1)[1]
+    flags = EPI_OUT_F32 if out.dtype == torch.float32 else 0
+    nb = int(L.lib().pa_gemm_pp_ws_bytes(M, N, K))
+    ws = torch.empty(nb // 4, dtype=torch.float32, device=a.device) if nb else None
+    tab = _seg_table(rows)
+    rc = L.call("pa_gemm_bf16_pp_segs", tab.data_ptr(), len(rows), 0, L.ptr(a), L.ptr(Bs[0]), L.ptr(out),
+                L.ptr(None), M, N, K, lda, rows[0][3], out.stride(0), int(ak), int(bk), flags, float(alpha),
+                L.ptr(ws), L.stream_ptr())
+    if rc:
+        raise RuntimeError(f"pa_gemm_bf16_pp_segs (N) failed ({rc}) for M={M} N={N} K={K}")
+    return out
+
+
+def gemm_seg_supported(a1, a2, b1, b2):
+    return gemm_kseg_supported([a1, a2], [b1, b2])
+
+
+def gemm_seg(a1, a2, b1, b2, out=None, accumulate=False, alpha=1.0):
+    """C = alpha * (a1 @ b1 + a2 @ b2): the two-segment case of ``gemm_kseg``."""
+    return gemm_kseg([a1, a2], [b1, b2], out=out, accumulate=accumulate, alpha=alpha)
 
 
 def gemm_bn_stats(a, b, bias=None, bn=None):

@@ -269,6 +269,84 @@ def apply_weight_grads(queue):
     queue.clear()
 
 
+# ---------------------------------------------------------------------------------------------
+# Weight-gradient pairing across gradient-accumulation micro-batches. Every micro-batch of an accumulation window
+# accumulates dW = x^T dY into the same main-grad buffer (K = the micro-batch's tokens); each such GEMM re-reads
+# and re-writes the whole buffer and pays a round of tile prologues / epilogues. On MI355X the 288 GB of HBM hold
+# one micro-batch's weight-gradient operands (x, dY of every linear: ~26 GB for GPT-3 13B at 4096 tokens), so
+# inside ``pair_weight_grads("defer")`` a linear's main-grad dW GEMM is queued instead of run (its grad-ready
+# hook waits too), and inside ``pair_weight_grads("merge")`` the next micro-batch's dW GEMM of the same weight
+# runs as ONE two-segment product over K = 2T ([x_a | x_b]^T [dY_a ; dY_b], ops.gemm.gemm_seg: no concatenated
+# copy), accumulated once. Leaving a "merge" region runs every job still queued on its own; a weight met twice in
+# one "defer" region (tied weights) is paired right away. Reference: none (gradient accumulation in the
+# reference accumulates per micro-batch, fleet/meta_parallel/sharding); an MI355X-memory-specific fusion.
+_PAIR = types.SimpleNamespace(mode=None, jobs={})
+
+
+@contextlib.contextmanager
+def pair_weight_grads(mode):
+    """``mode``: "defer" (queue main-grad dW GEMMs), "merge" (pair with the queued ones; flush the rest on
+    exit) or None (plain)."""
+    if mode not in ("defer", "merge", None):
+        raise ValueError(f"pair_weight_grads: unknown mode {mode!r}")
+    prev = _PAIR.mode
+    _PAIR.mode = mode
+    try:
+        yield
+    finally:
+        _PAIR.mode = prev
+        if mode == "merge":
+            flush_paired_weight_grads()
+
+
+def flush_paired_weight_grads():
+    """Run every queued dW job on its own (then its grad-ready hook)."""
+    jobs = list(_PAIR.jobs.values())
+    _PAIR.jobs.clear()
+    for w, x2, dy2, buf, on_ready in jobs:
+        _wgrad(x2, dy2, acc=buf)
+        on_ready(w)
+
+
+def pending_weight_grads():
+    return len(_PAIR.jobs)
+
+
+def _wgrad_pair(xa, dya, xb, dyb, acc):
+    """acc += xa^T dya + xb^T dyb: one two-segment GEMM when the hand-written kernel takes it and wins."""
+    xta, xtb = xa.t(), xb.t()
+    if G.gemm_seg_supported(xta, xtb, dya, dyb):
+        key = ("wgrad2", xta.shape[0], dya.shape[1], xta.shape[1] + xtb.shape[1], acc.dtype)
+        scratch = []
+
+        def _s():
+            if not scratch:
+                scratch.append(torch.zeros_like(acc))
+            return scratch[0]
+        cands = {"hip": lambda: G.gemm_seg(xta, xtb, dya, dyb, out=_s(), accumulate=True),
+                 "blas": lambda: (_s().addmm_(xta, dya), _s().addmm_(xtb, dyb))}
+        if G.choose(key, cands) == "hip":
+            G.gemm_seg(xta, xtb, dya, dyb, out=acc, accumulate=True)
+            return
+    _wgrad(xa, dya, acc=acc)
+    _wgrad(xb, dyb, acc=acc)
+
+
+def _main_grad_wgrad(w, x2, dy2, buf, on_ready):
+    mode = _PAIR.mode
+    if mode is not None:
+        job = _PAIR.jobs.pop(id(w), None)
+        if job is not None:  # the queued half of this weight's pair (or a tied weight met twice)
+            _wgrad_pair(job[1], job[2], x2, dy2, buf)
+            on_ready(w)
+            return
+        if mode == "defer":
+            _PAIR.jobs[id(w)] = (w, x2, dy2, buf, on_ready)
+            return
+    _wgrad(x2, dy2, acc=buf)
+    on_ready(w)
+
+
 def _mm_grads(x2, w, dy2, need_x, need_w, dx_hook=None):
     """dX first, then dW. ``dx_hook(dx)`` (tensor parallelism: the column-parallel layer's dX all-reduce)
     starts an asynchronous collective on dX right after its GEMM and returns a finisher, called once the
@@ -284,8 +362,7 @@ def _mm_grads(x2, w, dy2, need_x, need_w, dx_hook=None):
         ent = _main_grad_of(w)
         if ent is not None and ent[1].dtype == dy2.dtype:
             _, buf, on_ready = ent
-            _wgrad(x2, dy2, acc=buf)
-            on_ready(w)
+            _main_grad_wgrad(w, x2, dy2, buf, on_ready)
         else:
             dw = _wgrad(x2, dy2)
     if fin is not None:
@@ -425,6 +502,73 @@ def fused_linear(x, w, b=None, act=None, dx_hook=None):
         h = fused_linear(x, w, b)
         return F.relu(h)
     raise ValueError(f"unsupported activation {act}")
+
+
+# ---------------------------------------------------------------------------------------------
+# Sibling linears: y_i = x @ W_i for several weights that read the same input (q / k / v, gate / up). One
+# N-segmented GEMM computes every y_i (the outputs are column views of one [.., sum N_i] tensor), the data
+# gradient dx = sum_i dy_i W_i^T is ONE K-segmented GEMM over the separate dy_i (no concatenated gradient and no
+# accumulation adds of partial dx), and each W_i gets its own weight gradient (main-grad / pairing aware).
+# Reference: the auto-parallel fuse_attention_ffn_qkv pass (auto_parallel/static/engine.py:675) fuses the
+# weights into one parameter; here the parameters stay separate and only the launches are fused, so sharding /
+# checkpoints / optimizer state see the original weights. The static auto-parallel engine's fuse_sibling_linears
+# pass rewrites traced programs onto this op (distributed/passes/fuse_sibling_linears.py).
+class _MultiLinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, *ws):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        out = G.gemm_nseg(x2, list(ws))
+        ctx.save_for_backward(x2, *ws)
+        ctx.shape = shape
+        ctx.widths = [w.shape[1] for w in ws]
+        outs = out.split(ctx.widths, dim=1)
+        return tuple(o.view(*shape[:-1], o.shape[1]) for o in outs)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        x2, *ws = ctx.saved_tensors
+        dy2s = []
+        for dy in dys:
+            if dy is None:
+                dy2s.append(None)
+                continue
+            dy2 = dy.reshape(-1, dy.shape[-1])
+            if dy2.dtype != x2.dtype:
+                dy2 = dy2.to(x2.dtype)
+            dy2s.append(dy2 if dy2.is_contiguous() else dy2.contiguous())
+        live = [i for i, d in enumerate(dy2s) if d is not None]
+        dx = None
+        if ctx.needs_input_grad[0] and live:
+            As, Bs = [dy2s[i] for i in live], [ws[i].t() for i in live]
+            if G.gemm_kseg_supported(As, Bs):
+                dx = G.gemm_kseg(As, Bs)
+            else:
+                dx = _dgrad(As[0], ws[live[0]])
+                for i in live[1:]:
+                    dx = dx + _dgrad(dy2s[i], ws[i])
+            dx = dx.view(ctx.shape)
+        grads = []
+        for i, w in enumerate(ws):
+            if dy2s[i] is None or not ctx.needs_input_grad[1 + i]:
+                grads.append(None)
+                continue
+            _, dw = _mm_grads(x2, w, dy2s[i], False, True)
+            grads.append(dw)
+        return (dx, *grads)
+
+
+@static_op
+def multi_linear(x, ws):
+    """[x @ W for W in ws] (no bias): one N-segmented GEMM forward, one K-segmented data-gradient GEMM backward on
+    the HIP path; separate matmuls elsewhere."""
+    ws = list(ws)
+    if len(ws) > 1 and len(ws) <= 4 and all(_hip_linear_ok(x, w, None) for w in ws) and \
+            G.gemm_nseg_supported(x.reshape(-1, x.shape[-1]), ws):
+        return list(_MultiLinearFn.apply(x, *ws))
+    return [fused_linear(x, w) for w in ws]
 
 
 # ---------------------------------------------------------------------------------------------

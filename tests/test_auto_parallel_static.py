@@ -90,6 +90,12 @@ def _worker_parallelize(rank, world, port, shape, acc, q):
     eng = dm._engine
     kinds = sorted({n.name for nodes in eng.stage_nodes for n in nodes if n.name in (
         "allreduce", "allgather", "slice", "copy_to_parallel")})
+    # program passes on the traced model (static_engine._apply_passes): q / k / v and gate / up of every layer are
+    # one multi_linear node, both RMSNorms of every layer carry the residual gradient
+    L = cfg.num_hidden_layers
+    assert eng.pass_stats == {"rms_norm_residual": 2 * L, "sibling_linears": 5 * L}, eng.pass_stats
+    names = [n.name.split(":")[-1] for nodes in eng.stage_nodes for n in nodes]
+    assert names.count("multi_linear") == 2 * L and names.count("rms_norm_residual") == 2 * L, names
     q.put((rank, losses, kinds, eng.my_stage))
     paddle.distributed.barrier()
 
@@ -145,3 +151,23 @@ def test_parallelize_plan_llama_matches_single_process(shape, acc):
         assert "allreduce" in kinds and "copy_to_parallel" in kinds
         stages.add(stage)
     assert stages == set(range(shape[0]))
+
+
+def test_static_engine_rejects_unimplemented_strategy_fields():
+    """Strategy fields the engine does not implement raise instead of being silently ignored."""
+    sys.path.insert(0, ROOT)
+    os.environ["PADDLE_AMD_FORCE_CPU"] = "1"
+    import paddlepaddle_amd as paddle
+    import paddlepaddle_amd.distributed as dist
+    from paddlepaddle_amd.distributed.auto_parallel.static_engine import StaticEngine
+    from paddlepaddle_amd.models.llama_auto import LlamaForCausalLMAuto, LlamaPretrainingCriterionAuto
+    dist.auto_parallel.set_mesh(None)
+    cfg = _cfg()
+    model = LlamaForCausalLMAuto(cfg)
+    opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters())
+    for field, key in (("recompute", "enable"), ("sp_optimization", "enable"), ("gradient_merge", "enable"),
+                       ("mp_optimization", "allreduce_matmul_grad_overlapping")):
+        st = dist.Strategy()
+        getattr(st, field)[key] = True
+        with pytest.raises(NotImplementedError, match=field):
+            StaticEngine(model, LlamaPretrainingCriterionAuto(cfg), opt, st)

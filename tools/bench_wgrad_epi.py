@@ -39,5 +39,26 @@ def main():
         print(f"wgrad [{I},{O}] K={T}: " + " | ".join(line), flush=True)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and len(sys.argv) == 1:
     main()
+
+
+def pair_main():
+    """Weight-gradient pairing: two K = 4096 accumulating products vs one two-segment K = 8192 product."""
+    from paddlepaddle_amd.ops import gemm as G2
+    dev, bf = "cuda", torch.bfloat16
+    T = 4096
+    for (I, O) in ((5120, 15360), (5120, 5120), (5120, 20480), (20480, 5120)):
+        xa, xb = (torch.randn(T, I, device=dev, dtype=bf) for _ in range(2))
+        da, db = (torch.randn(T, O, device=dev, dtype=bf) for _ in range(2))
+        g = torch.zeros(I, O, device=dev, dtype=bf)
+        fl = 4 * T * I * O
+        t2 = min(timed(lambda: (G2.gemm(xa.t(), da, out=g, accumulate=True),
+                                G2.gemm(xb.t(), db, out=g, accumulate=True)), 10) for _ in range(3))
+        t1 = min(timed(lambda: G2.gemm_seg(xa.t(), xb.t(), da, db, out=g, accumulate=True), 10) for _ in range(3))
+        print(f"wgrad pair [{I},{O}]: 2 x K=4096 {t2:7.1f}us {fl / t2 / 1e6:5.0f}TF | one K=4096+4096 "
+              f"{t1:7.1f}us {fl / t1 / 1e6:5.0f}TF | x{t2 / t1:.3f}", flush=True)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "pair":
+    pair_main()
