@@ -116,3 +116,40 @@ def test_gradient_merge_equals_big_batch_step(static_mode):
     np.testing.assert_array_equal(lin2.weight.numpy(), w0)  # no update inside the merge window
     exe.run(m2, feed={"x": xv[4:]}, fetch_list=[l2])
     np.testing.assert_allclose(lin2.weight.numpy(), lin1.weight.numpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_fuse_sibling_linears_and_rms_norm_residual_passes():
+    """fuse_sibling_linears (alias fuse_attention_ffn_qkv): linears sharing an input -> one multi_linear node;
+    fuse_rms_norm_residual: rms_norm whose input also feeds a residual add -> rms_norm_residual. Same outputs and
+    gradients as the unfused program (CPU replay)."""
+    import numpy as np
+    import paddlepaddle_amd as paddle
+    from paddlepaddle_amd import ops
+    from paddlepaddle_amd.distributed.passes import new_pass
+    from paddlepaddle_amd.framework.tensor import _wrap
+    paddle.set_device("cpu")
+    paddle.enable_static()
+    try:
+        main, start = paddle.static.Program(), paddle.static.Program()
+        with paddle.static.program_guard(main, start):
+            paddle.seed(2)
+            x = paddle.static.data("x", [4, 16], "float32")
+            w = paddle.create_parameter([16], "float32", default_initializer=paddle.nn.initializer.Constant(1.0))
+            h = _wrap(ops.rms_norm(x._t, w._t, 1e-6))
+            q, k, v = (paddle.nn.Linear(16, n, bias_attr=False)(h) for n in (16, 8, 8))
+            out = x + (q * q).sum(-1, keepdim=True) + k.sum(-1, keepdim=True) * v.sum(-1, keepdim=True)
+            loss = out.mean()
+        exe = paddle.static.Executor(paddle.CPUPlace())
+        xs = np.random.RandomState(0).rand(4, 16).astype("float32")
+        ref = exe.run(main, feed={"x": xs}, fetch_list=[out])[0]
+        names0 = [n.name.split(":")[-1] for n in main.nodes]
+        c1 = new_pass("fuse_rms_norm_residual").apply(main, start)
+        c2 = new_pass("fuse_attention_ffn_qkv").apply(main, start)
+        names = [n.name.split(":")[-1] for n in main.nodes]
+        got = exe.run(main, feed={"x": xs}, fetch_list=[out])[0]
+    finally:
+        paddle.disable_static()
+    assert c1.get_attr("fuse_rms_norm_residual.fused") == 1 and c2.get_attr("fuse_sibling_linears.fused") == 3
+    assert names0.count("fused_linear") == 3 and names.count("fused_linear") == 0
+    assert names.count("multi_linear") == 1 and "rms_norm_residual" in names and "rms_norm" not in names
+    np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-6)
