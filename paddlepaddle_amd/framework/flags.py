@@ -20,6 +20,8 @@ _FLAGS = {
     "FLAGS_sharding_bucket_mb": 256,
     "FLAGS_pir_native_interpreter": True,  # PIR programs run on the C++ interpreter (_C_interp) when every op maps
     "FLAGS_eager_backward_engine": "native",  # native (csrc/autograd/autograd_exec.cpp RunBackward) | torch
+    "FLAGS_weight_only_dequant_cache_mb": 4096,  # weight-only / LLM.int8: bf16 images of quantized weights kept
+                                                 # for the bf16 GEMM path (0 = dequantise per call)
     "FLAGS_gemm_backend": "auto",         # per-shape GEMM / conv backend: auto (timed) | hip | blas
     "FLAGS_sharding_stage3_keep_params": "auto",  # stage 3: keep gathered params until the optimizer step
     "FLAGS_conv_per_direction": True,     # NHWC conv: forward / dgrad / wgrad each on the faster of ours and MIOpen

@@ -131,7 +131,9 @@ def llm_int8_linear(x, weight, bias=None, weight_scale=None, threshold=6.0):
     K = xt.shape[-1]
     x2 = xt.reshape(-1, K)
     xq, xo, sx, _ = _llm_split(x2, float(threshold))
-    if xt.dtype == torch.bfloat16 and _ops.quant.available(xt) and x2.shape[0] <= _ops.quant.DECODE_MAX_M:
+    if xt.dtype == torch.bfloat16 and _ops.quant.available(xt):
+        # device kernels at every row count: the decode kernel / cached-image GEMM up to 64 rows, the MFMA GEMM
+        # form of the decomposition above (ops/quant.py llm_int8_gemm)
         y = _ops.quant.wo_linear(xt, w.contiguous(), s, b, 8, -1,
                                  llm=(xq.to(torch.bfloat16).contiguous(), xo.to(torch.bfloat16).contiguous(),
                                       sx.float().contiguous()))

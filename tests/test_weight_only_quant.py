@@ -169,7 +169,11 @@ def test_wo_gemm_kernel_matches_fp32_dequantized_reference(M, algo, group):
     x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
     bias = (torch.randn(N, device="cuda", generator=g) * 0.1).bfloat16()
     L.reset_calls()
-    y = Q.weight_only_linear(paddle.Tensor(x), q, paddle.Tensor(bias), s, algo.split("_")[-1], group_size=group)
+    paddle.set_flags({"FLAGS_weight_only_dequant_cache_mb": 0})  # the decode kernel itself / per-call dequant
+    try:
+        y = Q.weight_only_linear(paddle.Tensor(x), q, paddle.Tensor(bias), s, algo.split("_")[-1], group_size=group)
+    finally:
+        paddle.set_flags({"FLAGS_weight_only_dequant_cache_mb": 4096})
     torch.cuda.synchronize()
     assert L.calls("pa_wo_gemm" if M <= 64 else "pa_wo_dequant") == 1
     ref = _ref_gpu(x, q, s, algo, group, bias)
@@ -191,7 +195,11 @@ def test_llm_int8_kernel_matches_decomposition(M):
     x[:, 900] *= 25
     xb = x.bfloat16()
     L.reset_calls()
-    y = Q.llm_int8_linear(paddle.Tensor(xb), q, None, s, threshold=6.0)
+    paddle.set_flags({"FLAGS_weight_only_dequant_cache_mb": 0})  # the LLM.int8 decode kernel itself
+    try:
+        y = Q.llm_int8_linear(paddle.Tensor(xb), q, None, s, threshold=6.0)
+    finally:
+        paddle.set_flags({"FLAGS_weight_only_dequant_cache_mb": 4096})
     torch.cuda.synchronize()
     assert L.calls("pa_wo_gemm") == 1
     xq, xo, sx, outl = Q._llm_split(xb, 6.0)
@@ -199,3 +207,50 @@ def test_llm_int8_kernel_matches_decomposition(M):
     exact = (sx[:, None] * (xq @ q._t.float().t()) + xo @ q._t.float().t()) * s._t.float()
     err = (y._t.float() - exact).abs().max().item() / exact.abs().max().item()
     assert err < 1e-2, err
+
+
+@pytest.mark.gpu
+def test_llm_int8_long_inputs_run_the_mfma_gemm():
+    """LLM.int8 above 64 rows runs on device kernels (the MFMA GEMM on the exact int8 values, outlier
+    columns as x / sx), matching the exact decomposition."""
+    from paddlepaddle_amd.ops import _loader as L
+    paddle.set_device("gpu:0")
+    K, N, M = 2048, 1024, 512
+    q, s = Q.weight_quantize(_w(K, N, 4), "llm.int8")
+    q, s = paddle.Tensor(q._t.cuda()), paddle.Tensor(s._t.cuda())
+    g = torch.Generator(device="cuda").manual_seed(9)
+    x = torch.randn(M, K, device="cuda", generator=g)
+    x[:, 33] *= 30
+    xb = x.bfloat16()
+    L.reset_calls()
+    y = Q.llm_int8_linear(paddle.Tensor(xb), q, None, s, threshold=6.0)
+    torch.cuda.synchronize()
+    assert sum(L.calls(n) for n in ("pa_gemm_bf16", "pa_gemm_bf16_pp")) >= 1
+    xq, xo, sx, outl = Q._llm_split(xb, 6.0)
+    exact = (sx[:, None] * (xq @ q._t.float().t()) + xo @ q._t.float().t()) * s._t.float()
+    err = (y._t.float() - exact).abs().max().item() / exact.abs().max().item()
+    assert err < 1e-2, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [8, 48, 256])
+def test_weight_only_dispatch_uses_cached_image_and_stays_exact(M):
+    """Per-shape choice between the decode kernel and the bf16 GEMM on the cached dequantised image: every choice
+    matches the fp32 reference, and a long input dequantises the weight once, not per call."""
+    from paddlepaddle_amd.ops import _loader as L
+    from paddlepaddle_amd.ops import quant as OQ
+    paddle.set_device("gpu:0")
+    K, N = 4096, 4096
+    q, s = Q.weight_quantize(_w(K, N, 5), "weight_only_int8")
+    q, s = paddle.Tensor(q._t.cuda()), paddle.Tensor(s._t.cuda())
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    OQ._DQ_CACHE.clear()
+    ys = [Q.weight_only_linear(paddle.Tensor(x), q, None, s, "int8") for _ in range(3)]
+    L.reset_calls()
+    y = Q.weight_only_linear(paddle.Tensor(x), q, None, s, "int8")
+    torch.cuda.synchronize()
+    assert L.calls("pa_wo_dequant") == 0  # the image is cached
+    ref = _ref_gpu(x, q, s, "weight_only_int8", -1, None)
+    for out in ys + [y]:
+        err = (out._t.float() - ref).abs().max().item() / ref.abs().max().item()
+        assert err < 1e-2, err
