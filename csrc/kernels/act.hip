@@ -161,6 +161,52 @@ __global__ __launch_bounds__(256) void rope_k(const T* __restrict__ x, const flo
   }
 }
 
+// RoPE over the first NH heads of token rows with their own leading dims: the fused QKV projection layout
+// [B*S, ld] = [q heads | k heads | v heads]. Forward rotates q|k out of the projection into a packed buffer;
+// backward rotates dq|dk in place inside the one qkv-gradient buffer (each thread reads its elements before
+// writing them, so x == out is allowed: no __restrict__ on x / out).
+template <typename T, bool NEOX>
+__global__ __launch_bounds__(256) void rope_rows_k(const T* x, int64_t ldx, const float* __restrict__ cs,
+                                                   const float* __restrict__ sn, T* out, int64_t ldo, int64_t rows,
+                                                   int64_t S, int64_t NH, int64_t D, float sgn) {
+  const int64_t per_head = NEOX ? D / 16 : D / 8;
+  const int64_t per_row = NH * per_head;
+  const int64_t n = rows * per_row;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t tok = i / per_row;
+    const int64_t rem = i - tok * per_row;
+    const int64_t h = rem / per_head, k = rem - h * per_head;
+    const int64_t s = tok % S;
+    const T* xr = x + tok * ldx + h * D;
+    T* orow = out + tok * ldo + h * D;
+    const float* cr = cs + s * D;
+    const float* sr = sn + s * D;
+    if (NEOX) {
+      const int64_t d0 = k * 8, d1 = d0 + D / 2;
+      float a[8], b[8], oa[8], ob[8];
+      load8<T>(xr + d0, a);
+      load8<T>(xr + d1, b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        oa[j] = a[j] * cr[d0 + j] - b[j] * sr[d0 + j] * sgn;
+        ob[j] = b[j] * cr[d1 + j] + a[j] * sr[d1 + j] * sgn;
+      }
+      store8<T>(orow + d0, oa);
+      store8<T>(orow + d1, ob);
+    } else {
+      const int64_t d0 = k * 8;
+      float a[8], o[8];
+      load8<T>(xr + d0, a);
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        o[j] = a[j] * cr[d0 + j] - a[j + 1] * sr[d0 + j] * sgn;
+        o[j + 1] = a[j + 1] * cr[d0 + j + 1] + a[j] * sr[d0 + j + 1] * sgn;
+      }
+      store8<T>(orow + d0, o);
+    }
+  }
+}
+
 }  // namespace
 
 PA_EXPORT int pa_gelu_fwd(const void* x, void* y, int64_t n, int approx, int dtype, hipStream_t st) {
@@ -220,6 +266,22 @@ PA_EXPORT int pa_rope_fwd(const void* x, const float* cs, const float* sn, void*
   } else {
     PA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((rope_k<T, false>), dim3(grid_for(n)), dim3(256), 0, st,
                                                    (const T*)x, cs, sn, (T*)out, B, S, H, D, sgn));
+  }
+  PA_CHECK_LAUNCH();
+  return 0;
+}
+
+PA_EXPORT int pa_rope_rows(const void* x, int64_t ldx, const float* cs, const float* sn, void* out, int64_t ldo,
+                           int64_t rows, int64_t S, int64_t NH, int64_t D, int flags, int dtype, hipStream_t st) {
+  const bool neox = flags & 1;
+  const float sgn = (flags & 2) ? -1.f : 1.f;
+  const int64_t n = rows * NH * (neox ? D / 16 : D / 8);
+  if (neox) {
+    PA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((rope_rows_k<T, true>), dim3(grid_for(n)), dim3(256), 0, st,
+                                                   (const T*)x, ldx, cs, sn, (T*)out, ldo, rows, S, NH, D, sgn));
+  } else {
+    PA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((rope_rows_k<T, false>), dim3(grid_for(n)), dim3(256), 0, st,
+                                                   (const T*)x, ldx, cs, sn, (T*)out, ldo, rows, S, NH, D, sgn));
   }
   PA_CHECK_LAUNCH();
   return 0;

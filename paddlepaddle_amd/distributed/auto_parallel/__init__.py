@@ -8,3 +8,4 @@ from .api import (shard_tensor, dtensor_from_local, dtensor_to_local, dtensor_fr
 from .intermediate import (parallelize, parallelize_model, parallelize_optimizer, ColWiseParallel,  # noqa: F401,E402
                            RowWiseParallel, PrepareLayerInput, PrepareLayerOutput, SequenceParallelBegin,
                            SequenceParallelEnd, SequenceParallelEnable, SequenceParallelDisable, SplitPoint)
+from .interface import recompute, exclude_ops_in_recompute  # noqa: F401,E402

@@ -32,6 +32,7 @@ One process per GPU; collectives are RCCL over xGMI groups, one group per mesh d
 """
 from __future__ import annotations
 
+import contextlib
 import math
 
 import numpy as np
@@ -247,10 +248,20 @@ def _map_shard_through_reshape(in_shape, out_shape, d):
 # ------------------------------------------------------------------------------------ engine
 class _LNode:
     """A local op: ``fn(*materialized args, **kw)`` with outputs assigned to ``outs`` template."""
-    __slots__ = ("fn", "args", "kwargs", "outs", "name")
+    __slots__ = ("fn", "args", "kwargs", "outs", "name", "rc")
 
-    def __init__(self, fn, args, kwargs, outs, name):
-        self.fn, self.args, self.kwargs, self.outs, self.name = fn, args, kwargs, outs, name
+    def __init__(self, fn, args, kwargs, outs, name, rc=None):
+        self.fn, self.args, self.kwargs, self.outs, self.name, self.rc = fn, args, kwargs, outs, name, rc
+
+
+class _Seg:
+    """A recompute segment of a stage's local program: its nodes run under a non-reentrant checkpoint, so only
+    ``inputs`` are kept for backward and the segment is re-run (collectives included, in the same order on every
+    rank of the group) when its gradient is needed."""
+    __slots__ = ("nodes", "inputs", "outputs")
+
+    def __init__(self, nodes, inputs, outputs):
+        self.nodes, self.inputs, self.outputs = nodes, inputs, outputs
 
 
 class StaticEngine:
@@ -280,8 +291,9 @@ class StaticEngine:
         self._consts = {}
         # strategy fields this engine does not implement fail loudly instead of being ignored
         unsupported = []
-        if strategy.recompute.get("enable", False):
-            unsupported.append("recompute (use models' use_recompute / fleet recompute on the dygraph path)")
+        self.recompute = bool(strategy.recompute.get("enable", False))
+        if self.recompute and strategy.recompute.get("refined_ops_patterns"):
+            unsupported.append("recompute.refined_ops_patterns (selective recompute)")
         if strategy.sp_optimization.get("enable", False):
             unsupported.append("sp_optimization")
         if strategy.mp_optimization.get("allreduce_matmul_grad_overlapping", False):
@@ -348,20 +360,116 @@ class StaticEngine:
             p._t = meta
         self.reshard_ann = {}
         prog._pa_reshard = self.reshard_ann
+        hooks = self._recompute_hooks(prog) if self.recompute else []
         try:
             with P.trace_into(prog):
                 xs = [_wrap(prog._metas[s]) for s in self.feed_slots[:-1]]
                 out = self.layer(*xs)
                 loss = self.loss_fn(out, _wrap(prog._metas[self.feed_slots[-1]]))
         finally:
+            for h in hooks:
+                h.remove()
+            prog._rc = None
             for p in params:
                 if id(p) in saved:
                     p._t = saved[id(p)]
         self.loss_slot = prog._slot_of[id(loss._t)]
         self._apply_passes()
         self._propagate_and_partition()
+        self._build_segments()
         self._localize_params()
         self.built = True
+
+    def _recompute_hooks(self, prog):
+        """strategy.recompute: every block of the model's LayerLists (the repeated decoder layers) becomes a
+        recompute segment while tracing (full-block granularity, as the reference's recompute pass applies to the
+        blocks PaddleNLP wraps with ``recompute``); segments the model marks itself (auto_parallel.recompute /
+        fleet recompute) are kept as they are."""
+        from ...nn import LayerList
+        stack, hooks = [], []
+
+        def pre(layer, inputs):
+            cm = prog.recompute_scope()
+            cm.__enter__()
+            stack.append(cm)
+
+        def post(layer, inputs, out):
+            stack.pop().__exit__(None, None, None)
+
+        for sub in self.layer.sublayers(include_self=True):
+            if isinstance(sub, LayerList):
+                for blk in sub:
+                    hooks.append(blk.register_forward_pre_hook(pre))
+                    hooks.append(blk.register_forward_post_hook(post))
+        return hooks
+
+    def _build_segments(self):
+        """Group each stage's local nodes into recompute segments (contiguous runs of one recompute id), minus
+        ``strategy.recompute.no_recompute_segments`` (indices in program order). Segment inputs: slots read before
+        being produced inside; outputs: slots produced inside and read later, sent to another stage or the loss."""
+        skip = set(int(i) for i in (self.strategy.recompute.get("no_recompute_segments") or []))
+        self.stage_items = []
+        self.n_segments = 0
+        seg_index = {}
+        for s, nodes in enumerate(self.stage_nodes):
+            runs, cur, cur_rc = [], [], None
+            for nd in nodes:
+                rc = nd.rc if (self.recompute and nd.outs is not None) else None  # in-place ops stay outside
+                if rc is not None and rc == cur_rc:
+                    cur.append(nd)
+                    continue
+                if cur:
+                    runs.append((cur_rc, cur))
+                cur, cur_rc = [nd], rc
+            if cur:
+                runs.append((cur_rc, cur))
+            later_use = [set() for _ in runs]
+            acc = set(self.sends[s]) | {self.loss_slot}
+            for i in range(len(runs) - 1, -1, -1):
+                later_use[i] = set(acc)
+                for nd in runs[i][1]:
+                    acc.update(r.i for r in _flat_tensor_refs((nd.args, nd.kwargs), []))
+            items = []
+            for i, (rc, run) in enumerate(runs):
+                if rc is not None:
+                    idx = seg_index.setdefault(rc, len(seg_index))
+                    if idx in skip or len(run) < 2:
+                        rc = None
+                if rc is None:
+                    items.extend(run)
+                    continue
+                produced, inputs = set(), []
+                for nd in run:
+                    for r in _flat_tensor_refs((nd.args, nd.kwargs), []):
+                        if r.i not in produced and r.i not in inputs:
+                            inputs.append(r.i)
+                    produced.update(r.i for r in _flat_tensor_refs(nd.outs, []))
+                outputs = sorted(produced & later_use[i])
+                items.append(_Seg(run, inputs, outputs))
+                self.n_segments += 1
+            self.stage_items.append(items)
+
+    def _run_nodes(self, nodes, env):
+        for nd in nodes:
+            args = self._materialize(nd.args, env)
+            kw = self._materialize(nd.kwargs, env)
+            out = nd.fn(*args, **kw)
+            if nd.outs is not None:
+                P._assign(nd.outs, out, env)
+
+    def _run_segment(self, seg, env):
+        import torch.utils.checkpoint as ckpt
+
+        def fn(*vals):
+            sub = dict(zip(seg.inputs, vals))
+            self._run_nodes(seg.nodes, sub)
+            return tuple(sub[o] for o in seg.outputs)
+        from ...ops import linear as LIN
+        mode = LIN.capture_forward_mode()
+        outs = ckpt.checkpoint(fn, *[env[i] for i in seg.inputs], use_reentrant=False, preserve_rng_state=True,
+                               context_fn=lambda: (contextlib.nullcontext(), LIN.forward_mode(mode)))
+        for o, v in zip(seg.outputs, outs):
+            env[o] = v
 
     def _apply_passes(self):
         """Program passes on the traced global program before placement propagation (reference: the engine's
@@ -418,6 +526,7 @@ class StaticEngine:
         self.slot_stage = {}                                   # slot -> producing stage
         self.local_alias = [dict() for _ in range(nstage)]     # (slot, pl) -> converted local slot
         self._next = len(prog._metas) + 1
+        self._cur_rc = None
         for s in self.feed_slots:
             self.slot_stage[s] = None  # available everywhere
         for s in self.param_slots.values():
@@ -507,11 +616,12 @@ class StaticEngine:
         return cur
 
     def _emit(self, stage, name, fn, args, out_slot):
-        self.stage_nodes[stage].append(_LNode(fn, args, {}, P._Ref(out_slot), name))
+        self.stage_nodes[stage].append(_LNode(fn, args, {}, P._Ref(out_slot), name, self._cur_rc))
         self.slot_stage[out_slot] = stage
 
     def _partition_node(self, n):
         prog = self.prog
+        self._cur_rc = getattr(n, "rc", None)  # conversions emitted for this node belong to its segment
         refs = _flat_tensor_refs((n.args, n.kwargs), [])
         stage = self._stage_for(n, refs)
         for r in refs:
@@ -550,7 +660,7 @@ class StaticEngine:
             m = prog._metas[o.i]
             self.info[o.i] = _Info(mesh, out_pl, tuple(m.shape))
             self.slot_stage[o.i] = stage
-        self.stage_nodes[stage].append(_LNode(n.func, args, kwargs, n.outs, n.name))
+        self.stage_nodes[stage].append(_LNode(n.func, args, kwargs, n.outs, n.name, self._cur_rc))
         if n.outs is None:  # in-place op on its first argument
             for r in refs[:1]:
                 self.slot_stage[r.i] = stage
@@ -914,12 +1024,11 @@ class StaticEngine:
                 t.requires_grad_(True)
             env[slot] = t
             received.append((slot, t))
-        for nd in self.stage_nodes[s]:
-            args = self._materialize(nd.args, env)
-            kw = self._materialize(nd.kwargs, env)
-            out = nd.fn(*args, **kw)
-            if nd.outs is not None:
-                P._assign(nd.outs, out, env)
+        for it in self.stage_items[s]:
+            if isinstance(it, _Seg):
+                self._run_segment(it, env)
+            else:
+                self._run_nodes((it,), env)
         sent = []
         for slot, dsts in sorted(self.sends[s].items()):
             t = env[slot]

@@ -5,6 +5,8 @@ Uses the native non-reentrant checkpoint machinery: only the block input is kept
 re-run in backward under the saved RNG state (dropout masks identical)."""
 from __future__ import annotations
 
+import contextlib
+
 import torch
 import torch.utils.checkpoint as _ckpt
 
@@ -31,11 +33,19 @@ def recompute(function, *args, **kwargs):
     preserve = kwargs.pop("preserve_rng_state", True)
     kwargs.pop("use_reentrant", None)
     kwargs.pop("offload_indices", None)
+    from ...framework.trace_hook import _active_program
+    prog = _active_program()
+    if prog is not None:  # traced into a static program: the block becomes a recompute segment of the program
+        with prog.recompute_scope():
+            return function(*args, **kwargs)
 
     def f(*targs):
         return _u(function(*[_w(a) for a in targs], **kwargs))
 
-    out = _ckpt.checkpoint(f, *[_u(a) for a in args], use_reentrant=False, preserve_rng_state=preserve)
+    from ...ops import linear as LIN
+    mode = LIN.capture_forward_mode()  # the recompute inside backward takes the forward's op routing
+    out = _ckpt.checkpoint(f, *[_u(a) for a in args], use_reentrant=False, preserve_rng_state=preserve,
+                           context_fn=lambda: (contextlib.nullcontext(), LIN.forward_mode(mode)))
     return _w(out)
 
 

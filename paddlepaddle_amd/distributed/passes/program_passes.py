@@ -31,6 +31,12 @@ _MATMUL = {"f:torch:matmul", "m:matmul", "f:torch:mm", "m:mm", "m:__matmul__"}
 _LINEAR = "o:paddlepaddle_amd.ops.linear:fused_linear"
 
 
+
+def _keep_rc(node, src):
+    """A rewritten node stays in the recompute segment of the node it replaces."""
+    node.rc = getattr(src, "rc", None)
+    return node
+
 def _slot(t):
     return t.i if isinstance(t, P._Ref) else None
 
@@ -127,7 +133,7 @@ class FuseGemmEpiloguePass(PassBase):
                     ws, bs = _shape_of(prog, m.args[1]), _shape_of(prog, b)
                     if ws is None or bs is None or len(ws) != 2 or bs != (ws[1],):
                         continue
-                    nodes[j] = P.OpNode(lin, (m.args[0], m.args[1], b), {}, n.outs, "op", _LINEAR)
+                    nodes[j] = _keep_rc(P.OpNode(lin, (m.args[0], m.args[1], b), {}, n.outs, "op", _LINEAR), m)
                     del nodes[i]
                     fused += 1
                     changed = True
@@ -142,7 +148,7 @@ class FuseGemmEpiloguePass(PassBase):
                     m = nodes[i]
                     if m.name != _LINEAR or m.kwargs or len(m.args) != 3 or not isinstance(m.outs, P._Ref):
                         continue
-                    nodes[j] = P.OpNode(lin, tuple(m.args) + (act,), {}, n.outs, "op", _LINEAR)
+                    nodes[j] = _keep_rc(P.OpNode(lin, tuple(m.args) + (act,), {}, n.outs, "op", _LINEAR), m)
                     del nodes[i]
                     fused += 1
                     changed = True
@@ -236,11 +242,13 @@ class AMPPass(PassBase):
                 cm = torch.empty(m.shape, dtype=dt, device=meta_dev)
             s = prog._new_slot(cm)
             env[s] = cm
-            new_nodes.append(P.OpNode(to, (a, dt), {}, P._Ref(s), "torch", "m:to"))
+            new_nodes.append(_keep_rc(P.OpNode(to, (a, dt), {}, P._Ref(s), "torch", "m:to"), cur[0]))
             casts += 1
             return P._Ref(s)
 
+        cur = [None]
         for n in prog.nodes:
+            cur[0] = n
             if n.kind in ("op", "torch") and n.outs is not None:
                 if self._listed(n.name, black):
                     n.args = cast_arg(n.args, torch.float32)
@@ -348,7 +356,7 @@ class FuseSiblingLinearsPass(PassBase):
                 if any(_slot(w) is not None and producer.get(_slot(w), -1) > first for w in ws):
                     continue
                 outs = [nodes[i].outs for i in chunk]
-                nodes[first] = P.OpNode(ml, (nodes[first].args[0], list(ws)), {}, outs, "op", _MULTI)
+                nodes[first] = _keep_rc(P.OpNode(ml, (nodes[first].args[0], list(ws)), {}, outs, "op", _MULTI), nodes[first])
                 dead.update(chunk[1:])
                 fused += len(chunk)
         if dead:
@@ -399,9 +407,9 @@ class FuseRMSNormResidualPass(PassBase):
             with torch._C.DisableTorchFunction():
                 r = prog._new_slot(torch.empty(tuple(m.shape), dtype=m.dtype, device="meta")
                                    .requires_grad_(m.requires_grad))
-            nodes[i] = P.OpNode(rr, tuple(n.args), {}, (P._Ref(r), n.outs), "op", _RMS_RES)
+            nodes[i] = _keep_rc(P.OpNode(rr, tuple(n.args), {}, (P._Ref(r), n.outs), "op", _RMS_RES), n)
             a = nodes[j]
-            nodes[j] = P.OpNode(a.func, tuple(P._Ref(r) if _slot(v) == x else v for v in a.args), {}, a.outs, a.kind,
-                                a.name)
+            nodes[j] = _keep_rc(P.OpNode(a.func, tuple(P._Ref(r) if _slot(v) == x else v for v in a.args), {},
+                                         a.outs, a.kind, a.name), a)
             fused += 1
         context.set_attr("fuse_rms_norm_residual.fused", context.get_attr("fuse_rms_norm_residual.fused", 0) + fused)

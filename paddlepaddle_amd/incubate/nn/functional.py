@@ -156,12 +156,7 @@ def fused_rotary_position_embedding(q, k=None, v=None, sin=None, cos=None, posit
 
 # --------------------------------------------------------------------------------------- activations
 def swiglu(x, y=None, name=None):
-    xt = _t(x)
-    if y is None:
-        a, b = xt.chunk(2, -1)
-    else:
-        a, b = xt, _t(y)
-    return _wrap(_ops.swiglu(a, b))
+    return _wrap(_ops.swiglu(_t(x), None if y is None else _t(y)))
 
 
 def fused_bias_act(x, bias=None, dequant_scales=None, shift=None, smooth=None, act_method="gelu",

@@ -171,6 +171,14 @@ class LlamaAttention(nn.Layer):
     def forward(self, x, cache=None, pos=0):
         if cache is not None and isinstance(pos, torch.Tensor):
             return self._decode_step(x, cache, pos)
+        if cache is None and self.cfg.sep_parallel_degree <= 1:
+            # training / full-sequence path: projection -> RoPE -> attention as one op whose backward returns the
+            # whole qkv-projection gradient as one buffer (ops/attention.py qkv_rope_attention)
+            t = self.qkv_proj(x)._t
+            B, S = t.shape[0], t.shape[1]
+            cos, sin = self.rope.tables(pos + S, t.device)
+            o = _ops.qkv_rope_attention(t, cos[pos:pos + S], sin[pos:pos + S], self.H, self.Hkv, self.D)
+            return self.o_proj(_wrap(o.reshape(B, S, self.H * self.D)))
         q, k, v = self._qkv(x)
         B, S = q.shape[0], q.shape[1]
         if cache is None and self.cfg.sep_parallel_degree > 1:
@@ -249,9 +257,8 @@ class LlamaMLP(nn.Layer):
             self.down_proj = nn.Linear(f, h, weight_attr=init, bias_attr=False)
 
     def forward(self, x):
-        gu = self.gate_up_proj(x)._t
-        g, u = gu.chunk(2, -1)
-        return self.down_proj(_wrap(_ops.swiglu(g, u)))
+        # one-input swiglu: its backward writes d[gate | up] as one buffer (no chunk / cat in autograd)
+        return self.down_proj(_wrap(_ops.swiglu(self.gate_up_proj(x)._t)))
 
 
 class LlamaDecoderLayer(nn.Layer):

@@ -4,7 +4,8 @@ from .common import *  # noqa: F401,F403
 from .conv import *  # noqa: F401,F403
 from .distance import *  # noqa: F401,F403
 from .flash_attention import (flash_attention, scaled_dot_product_attention, flash_attn_unpadded,  # noqa: F401
-                              flash_attn_qkvpacked, flash_attention_with_sparse_mask)
+                              flash_attn_qkvpacked, flash_attention_with_sparse_mask,
+                              calc_reduced_attention_scores)
 from .loss import *  # noqa: F401,F403
 from .norm import *  # noqa: F401,F403
 from .pooling import *  # noqa: F401,F403

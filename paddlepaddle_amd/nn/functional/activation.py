@@ -186,8 +186,4 @@ def gumbel_softmax(x, temperature=1.0, hard=False, axis=-1, name=None):
 
 def swiglu(x, y=None, name=None):
     """Reference: python/paddle/incubate/nn/functional/swiglu.py. HIP kernel on MI355X."""
-    if y is None:
-        t = T(x)
-        a, b = t.chunk(2, dim=-1)
-        return _wrap(_ops.swiglu(a, b))
-    return _wrap(_ops.swiglu(T(x), T(y)))
+    return _wrap(_ops.swiglu(T(x), None if y is None else T(y)))

@@ -142,3 +142,30 @@ def flash_attention_with_sparse_mask(query, key, value, attn_mask_start_row_indi
     se = idx.unsqueeze(-1)
     o = _A.attention(q, k, v, causal=is_causal, startend_row_indices=se, dropout=dropout_p, training=training)
     return _wrap(o)
+
+
+def calc_reduced_attention_scores(query, key, softmax_lse, name=None):
+    """sum over the query rows of softmax(Q K^T / sqrt(d)) -> [B, H, 1, Sk] fp32 (inference: no gradient), with the
+    softmax normaliser taken from the forward's ``softmax_lse`` [B, H, >= Sq] (Reference:
+    python/paddle/nn/functional/flash_attention.py:2040). The probabilities are rebuilt block by block — 512 query
+    rows at a time through one batched bf16 GEMM with fp32 output — and summed in place, so no [Sq, Sk] matrix is
+    ever resident."""
+    q, k, lse = T(query), T(key), T(softmax_lse)
+    if getattr(query, "stop_gradient", True) is False or getattr(key, "stop_gradient", True) is False:
+        raise ValueError("calc_reduced_attention_scores() is for inference only (stop_gradient inputs)")
+    B, Sq, H, D = q.shape
+    Sk, Hk = k.shape[1], k.shape[2]
+    scale = 1.0 / math.sqrt(D)
+    kt = k.transpose(1, 2)                                   # [B, Hk, Sk, D]
+    if Hk != H:
+        kt = kt.repeat_interleave(H // Hk, 1)
+    out = torch.zeros(B, H, 1, Sk, dtype=torch.float32, device=q.device)
+    lse = lse.float()
+    with torch.no_grad():
+        for r0 in range(0, Sq, 512):
+            r1 = min(Sq, r0 + 512)
+            qb = q[:, r0:r1].transpose(1, 2)                 # [B, H, rb, D]
+            s = torch.matmul(qb, kt.transpose(-1, -2)).float() * scale
+            s.sub_(lse[:, :, r0:r1].unsqueeze(-1)).exp_()
+            out.add_(s.sum(2, keepdim=True))
+    return _wrap(out)

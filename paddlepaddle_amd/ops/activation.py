@@ -108,8 +108,44 @@ class _SwigluHIP(torch.autograd.Function):
         return da.reshape(ctx.shape), db.reshape(ctx.shape)
 
 
+class _SwigluPackedHIP(torch.autograd.Function):
+    """x [.., 2f] = [gate | up] (one projection's output) -> silu(gate) * up [.., f]. The gradient is one [.., 2f]
+    buffer written by the backward kernel: the gate/up halves never go through a chunk + cat in autograd."""
+
+    @staticmethod
+    def forward(ctx, x):
+        f = x.shape[-1] // 2
+        x2 = x.reshape(-1, 2 * f)
+        if x2.stride(1) != 1 or x2.stride(0) % 8 or x2.data_ptr() % 16:
+            x2 = x2.contiguous()
+        rows = x2.shape[0]
+        y = torch.empty(rows, f, dtype=x.dtype, device=x.device)
+        a2, b2 = x2[:, :f], x2[:, f:]
+        L.call("pa_swiglu_fwd", L.ptr(a2), L.ptr(b2), L.ptr(y), rows, f, x2.stride(0), L.dcode(x2), L.stream_ptr())
+        ctx.save_for_backward(x2)
+        ctx.shape = x.shape
+        return y.view(*x.shape[:-1], f)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x2,) = ctx.saved_tensors
+        rows, f = x2.shape[0], x2.shape[1] // 2
+        dyc = dy.contiguous().view(rows, f).to(x2.dtype)
+        dx = torch.empty(rows, 2 * f, dtype=x2.dtype, device=x2.device)
+        L.call("pa_swiglu_bwd", L.ptr(x2[:, :f]), L.ptr(x2[:, f:]), L.ptr(dyc), L.ptr(dx[:, :f]), L.ptr(dx[:, f:]),
+               rows, f, x2.stride(0) | (dx.stride(0) << 32), L.dcode(x2), L.stream_ptr())
+        return dx.view(ctx.shape)
+
+
 @static_op
-def swiglu(a, b):
+def swiglu(a, b=None):
+    """silu(a) * b; with ``b`` None, ``a`` is [.., 2f] = [gate | up] (Reference:
+    python/paddle/incubate/nn/functional/swiglu.py:22 — one-input form splits the last dim)."""
+    if b is None:
+        if L.hip_enabled_for(a) and a.dtype in L._DT and a.shape[-1] % 16 == 0:
+            return _SwigluPackedHIP.apply(a)
+        g, u = a.chunk(2, -1)
+        return F.silu(g) * u
     if L.hip_enabled_for(a) and a.dtype in L._DT and a.shape[-1] % 8 == 0 and a.shape == b.shape:
         return _SwigluHIP.apply(a, b)
     return F.silu(a) * b

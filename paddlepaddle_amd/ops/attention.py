@@ -269,6 +269,74 @@ class _FlashAttnQKVPackedHIP(torch.autograd.Function):
         return dqkv, None, None
 
 
+class _QKVRopeAttnHIP(torch.autograd.Function):
+    """Fused QKV projection output t [B, S, (H + 2*Hkv) * D] (per-token layout [q heads | k heads | v heads]) ->
+    RoPE(q), RoPE(k) -> causal flash attention -> o [B, S, H, D].
+
+    Forward: one row-strided RoPE launch rotates q|k out of t into a packed [B, S, H + Hkv, D] buffer; v is read
+    in place from t. Backward: the attention kernel writes dq, dk and dv straight into their column ranges of ONE
+    [B, S, W] gradient buffer and one in-place inverse rotation finishes dq|dk — the unfused path's per-tensor
+    rope launches, split-backward concatenation (CatArrayBatchedCopy) and its extra [B, S, W] round trip are gone.
+    Reference behaviour: the q/k/v split + fused_rotary_position_embedding + flash_attention sequence of
+    PaddleNLP's LlamaAttention (python/paddle/incubate/nn/functional/fused_rotary_position_embedding.py:22)."""
+
+    @staticmethod
+    def forward(ctx, t, cos, sin, H, Hkv, D, causal, scale, neox):
+        B, S, W = t.shape
+        if not t.is_contiguous():
+            t = t.contiguous()
+        qk = torch.empty(B, S, H + Hkv, D, dtype=t.dtype, device=t.device)
+        L.call("pa_rope_rows", L.ptr(t), W, L.ptr(cos), L.ptr(sin), L.ptr(qk), (H + Hkv) * D, B * S, S, H + Hkv, D,
+               int(neox), L.dcode(t), L.stream_ptr())
+        q, k = qk[:, :, :H], qk[:, :, H:]
+        v = t.view(B, S, H + 2 * Hkv, D)[:, :, H + Hkv:]
+        job = _Job(q, k, False, causal, scale, None, None, 0.0, 0, None, None, None, None)
+        o, lse = _fa_fwd(q, k, v, job)
+        ctx.save_for_backward(t, qk, cos, sin, o, lse)
+        ctx.job, ctx.dims, ctx.neox = job, (H, Hkv, D), neox
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        t, qk, cos, sin, o, lse = ctx.saved_tensors
+        H, Hkv, D = ctx.dims
+        B, S, W = t.shape
+        do = do.to(t.dtype)
+        if not _lastdim_contig(do):
+            do = do.contiguous()
+        g = torch.empty_like(t)
+        g4 = g.view(B, S, H + 2 * Hkv, D)
+        v = t.view(B, S, H + 2 * Hkv, D)[:, :, H + Hkv:]
+        _fa_bwd(qk[:, :, :H], qk[:, :, H:], v, o, lse, do, g4[:, :, :H], g4[:, :, H:H + Hkv], g4[:, :, H + Hkv:],
+                ctx.job)
+        L.call("pa_rope_rows", L.ptr(g), W, L.ptr(cos), L.ptr(sin), L.ptr(g), W, B * S, S, H + Hkv, D,
+               int(ctx.neox) | 2, L.dcode(g), L.stream_ptr())
+        return g, None, None, None, None, None, None, None, None
+
+
+@static_op
+def qkv_rope_attention(t, cos, sin, num_heads, num_kv_heads, head_dim, causal=True, scale=None, neox=True):
+    """Fused projection output t [B, S, (H + 2*Hkv) * D] -> attention(RoPE(q), RoPE(k), v) [B, S, H, D] with cos /
+    sin the fp32 [S, D] tables of these positions. The HIP path (bf16/fp16, D in {64, 128, 256}) hands the whole
+    qkv gradient back as one buffer; elsewhere it is the split + apply_rotary + flash_attention composition."""
+    H, Hkv, D = int(num_heads), int(num_kv_heads), int(head_dim)
+    B, S, W = t.shape
+    if W != (H + 2 * Hkv) * D or H % Hkv:
+        raise ValueError(f"qkv_rope_attention: width {W} != (H + 2*Hkv) * D = {(H + 2 * Hkv) * D}")
+    scale = 1.0 / math.sqrt(D) if scale is None else float(scale)
+    cos = cos.float().contiguous()
+    sin = sin.float().contiguous()
+    if (L.hip_enabled_for(t) and L.has("pa_rope_rows") and L.has("pa_flash_attn_fwd_ex")
+            and t.dtype in (torch.bfloat16, torch.float16) and D in (64, 128, 256) and cos.shape[0] >= S
+            and cos.shape[-1] == D):
+        return _QKVRopeAttnHIP.apply(t, cos, sin, H, Hkv, D, bool(causal), scale, bool(neox))
+    from .rope import apply_rotary
+    q, k, v = t.split([H * D, Hkv * D, Hkv * D], -1)
+    q = apply_rotary(q.reshape(B, S, H, D), cos, sin, neox)
+    k = apply_rotary(k.reshape(B, S, Hkv, D), cos, sin, neox)
+    return attention(q, k, v.reshape(B, S, Hkv, D), causal=causal, scale=scale)
+
+
 def _padded_dim(D):
     """Head dims the kernel instantiates: 64, 128, 256; others (multiples of 8) are zero-padded up to one."""
     if D % 8 != 0 or D > 256:

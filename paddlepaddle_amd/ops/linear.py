@@ -166,6 +166,9 @@ def unregister_main_grad(weight):
     _MAIN_GRAD.pop(id(weight), None)
 
 
+_SAME = object()
+
+
 def _main_grad_of(w):
     ent = _MAIN_GRAD.get(id(w))
     if ent is None or ent[0]() is not w:  # identity check: ids of dead tensors can be reused
@@ -243,6 +246,30 @@ def zero_bubble_forward(enable=True):
         yield
     finally:
         _ZB.route = prev
+
+
+def capture_forward_mode():
+    """The op-routing state of the running forward (zero-bubble weight-gradient routing), for a recompute that
+    re-runs this forward later inside backward: the recomputed ops must take the same path (same saved tensors)."""
+    return {"zb": getattr(_ZB, "route", False)}
+
+
+class forward_mode:
+    """Re-enterable context applying a captured forward mode (a checkpoint may recompute a segment more than
+    once, entering its recompute context each time)."""
+
+    def __init__(self, mode):
+        self.mode = mode
+        self.prev = []
+
+    def __enter__(self):
+        self.prev.append(getattr(_ZB, "route", False))
+        _ZB.route = self.mode["zb"]
+        return self
+
+    def __exit__(self, *exc):
+        _ZB.route = self.prev.pop()
+        return False
 
 
 def apply_weight_grads(queue):
@@ -347,18 +374,42 @@ def _main_grad_wgrad(w, x2, dy2, buf, on_ready):
     on_ready(w)
 
 
-def _mm_grads(x2, w, dy2, need_x, need_w, dx_hook=None):
+def _leaf_weights(*ws):
+    """Saved at forward: the parameters themselves (activation recompute hands saved tensors back detached, and
+    the zero-bubble queue / main-grad buffers are keyed by the parameter object)."""
+    return tuple(w if (isinstance(w, torch.Tensor) and w.requires_grad and w.is_leaf) else None for w in ws)
+
+
+def _w_ident(w, leaf, needed):
+    """The object gradient routing is keyed by: the parameter saved at forward (a checkpoint recompute hands the
+    saved weight back as a different tensor object), else ``w`` when it is a derived weight still attached to its
+    autograd chain (a cast / slice); None when it is neither — its gradient then flows back through autograd."""
+    if not needed:
+        return w
+    if leaf is not None:
+        return leaf
+    return w if w.grad_fn is not None else None
+
+
+def _mm_grads(x2, w, dy2, need_x, need_w, dx_hook=None, wid=_SAME):
     """dX first, then dW. ``dx_hook(dx)`` (tensor parallelism: the column-parallel layer's dX all-reduce)
     starts an asynchronous collective on dX right after its GEMM and returns a finisher, called once the
-    weight-gradient GEMM has been issued — the collective runs beside the dW GEMM instead of after it."""
+    weight-gradient GEMM has been issued — the collective runs beside the dW GEMM instead of after it.
+    ``wid``: the weight's identity for deferral / main-grad routing (see _w_ident); None = return dW."""
     dx = _dgrad(dy2, w) if need_x else None
     fin = dx_hook(dx) if (dx_hook is not None and dx is not None) else None
     dw = None
+    if wid is _SAME:
+        wid = w
     q = getattr(_ZB, "queue", None)
-    if need_w and q is not None:  # zero-bubble B step: the dW GEMM runs later, in a W step
-        q.append((w, x2, dy2))
+    if need_w and q is not None and wid is not None:  # zero-bubble B step: the dW GEMM runs later, in a W step
+        q.append((wid, x2, dy2))
+        need_w = False
+    if need_w and wid is None:
+        dw = _wgrad(x2, dy2)
         need_w = False
     if need_w:
+        w = wid
         ent = _main_grad_of(w)
         if ent is not None and ent[1].dtype == dy2.dtype:
             _, buf, on_ready = ent
@@ -395,6 +446,7 @@ class _LinearFn(torch.autograd.Function):
         x2 = x.reshape(-1, shape[-1])
         y = _fwd_mm(x2, w, b)
         ctx.save_for_backward(x2, w)
+        ctx.w_leaf = _leaf_weights(w)[0]
         ctx.has_b = b is not None
         ctx.bias = b
         ctx.shape = shape
@@ -409,7 +461,8 @@ class _LinearFn(torch.autograd.Function):
             dy2 = dy2.to(x2.dtype)
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
-        dx, dw = _mm_grads(x2, w, dy2, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.dx_hook)
+        dx, dw = _mm_grads(x2, w, dy2, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.dx_hook,
+                           wid=_w_ident(w, ctx.w_leaf, ctx.needs_input_grad[1]))
         db = None
         if ctx.has_b and ctx.needs_input_grad[2]:
             mg = _vector_main_grad(ctx.bias, dy2.dtype)
@@ -430,6 +483,7 @@ class _LinearBiasGeluFn(torch.autograd.Function):
         x2 = x.reshape(-1, shape[-1])
         y, h, bb = _fwd_bias_gelu(x2, w, b)
         ctx.save_for_backward(x2, w, bb, h)
+        ctx.w_leaf = _leaf_weights(w)[0]
         ctx.bias = b
         ctx.shape = shape
         ctx.dx_hook = dx_hook
@@ -449,7 +503,8 @@ class _LinearBiasGeluFn(torch.autograd.Function):
         if mg is not None:  # bias gradient added straight into its .grad buffer
             mg[1](ctx.bias)
             db = None
-        dx, dw = _mm_grads(x2, w, dh, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.dx_hook)
+        dx, dw = _mm_grads(x2, w, dh, ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.dx_hook,
+                           wid=_w_ident(w, ctx.w_leaf, ctx.needs_input_grad[1]))
         if dx is not None:
             dx = dx.view(ctx.shape)
         return dx, dw, db, None
@@ -522,6 +577,7 @@ class _MultiLinearFn(torch.autograd.Function):
             x2 = x2.contiguous()
         out = G.gemm_nseg(x2, list(ws))
         ctx.save_for_backward(x2, *ws)
+        ctx.w_leaves = _leaf_weights(*ws)
         ctx.shape = shape
         ctx.widths = [w.shape[1] for w in ws]
         outs = out.split(ctx.widths, dim=1)
@@ -555,7 +611,7 @@ class _MultiLinearFn(torch.autograd.Function):
             if dy2s[i] is None or not ctx.needs_input_grad[1 + i]:
                 grads.append(None)
                 continue
-            _, dw = _mm_grads(x2, w, dy2s[i], False, True)
+            _, dw = _mm_grads(x2, w, dy2s[i], False, True, wid=_w_ident(w, ctx.w_leaves[i], True))
             grads.append(dw)
         return (dx, *grads)
 

@@ -181,8 +181,7 @@ class GroupedExperts(nn.Layer):
         h = M.grouped_linear(xs, self.w1._t, offs, t(self.b1))
         if self.activation == "swiglu":
             from .. import ops as _ops
-            a, g = h.chunk(2, -1)
-            h = _ops.swiglu(a.contiguous(), g.contiguous())
+            h = _ops.swiglu(h)
         elif self.activation == "gelu":
             h = TF.gelu(h)
         elif self.activation == "relu":
@@ -356,8 +355,7 @@ def fused_moe(x, gate_weight, ffn1_weight, ffn2_weight, ffn1_bias=None, ffn1_sca
     b1 = ffn1_bias._t.reshape(E, -1) if ffn1_bias is not None else None
     b2 = ffn2_bias._t.reshape(E, -1) if ffn2_bias is not None else None
     h = M.grouped_linear(xf[tok], ffn1_weight._t, offs, b1)
-    a, bgate = h.chunk(2, -1)
-    h = _ops.swiglu(a.contiguous(), bgate.contiguous())
+    h = _ops.swiglu(h)
     y = M.grouped_linear(h, ffn2_weight._t, offs, b2)
     out = torch.zeros_like(xf).index_add(0, tok, (y * wts[:, None].to(y.dtype)).to(xf.dtype))
     return _wrap(out.reshape(xt.shape))

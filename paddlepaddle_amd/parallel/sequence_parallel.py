@@ -114,6 +114,7 @@ class _ColumnSPLinear(torch.autograd.Function):
             ctx.save_for_backward(full, w, bb, torch.cat(pres, 0))
         else:
             ctx.save_for_backward(full, w)
+        ctx.w_leaf = _lin._leaf_weights(w)[0]
         return y
 
     @staticmethod
@@ -140,7 +141,7 @@ class _ColumnSPLinear(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             _log("gemm", "wgrad")
-            dw = _wgrad_into(full, dh, w)
+            dw = _wgrad_into(full, dh, w, wid=_lin._w_ident(w, ctx.w_leaf, True))
         _wait(work, "reduce_scatter")
         return dx, dw, db, None, None
 
@@ -211,6 +212,7 @@ class _RowSPLinear(torch.autograd.Function):
             _wait(wk, "reduce")
         ctx.group = group
         ctx.save_for_backward(x, w)
+        ctx.w_leaf = _lin._leaf_weights(w)[0]
         return parts[r]
 
     @staticmethod
@@ -235,7 +237,8 @@ class _RowSPLinear(torch.autograd.Function):
                 dxs[j] = _lin._dgrad(dyj, w)
             if ctx.needs_input_grad[1]:
                 _log("gemm", "wgrad")
-                dw = _wgrad_into(xb[j], dyj, w, dw, last=(i == n - 1))
+                dw = _wgrad_into(xb[j], dyj, w, dw, last=(i == n - 1),
+                                 wid=_lin._w_ident(w, ctx.w_leaf, True))
         if n == 1:
             _wait(work, "all_gather")
         dx = torch.cat(dxs, 0) if ctx.needs_input_grad[0] else None
@@ -274,9 +277,11 @@ def _bias_gelu_grad(h, b, dy, bias, need_db):
     return dh, (dh.float().sum(0).to(b.dtype) if need_db else None)
 
 
-def _wgrad_into(x2, dy2, w, acc=None, last=True):
+def _wgrad_into(x2, dy2, w, acc=None, last=True, wid=None):
     """x2^T dy2 for weight ``w``: into its main-grad buffer when registered (the engine's grad-ready handler runs
-    after the last block), else a fresh dW / accumulated into ``acc``."""
+    after the last block), else a fresh dW / accumulated into ``acc``. ``wid``: the parameter ``w`` stands for
+    (ops/linear.py _w_ident: a recompute hands saved weights back detached)."""
+    w = w if wid is None else wid
     ent = _lin._main_grad_of(w)
     if ent is not None and ent[1].dtype == dy2.dtype:
         _, buf, on_ready = ent

@@ -82,11 +82,12 @@ class _Sym:
 
 
 class OpNode:
-    __slots__ = ("func", "args", "kwargs", "outs", "kind", "name")
+    __slots__ = ("func", "args", "kwargs", "outs", "kind", "name", "rc")
 
     def __init__(self, func, args, kwargs, outs, kind="torch", name=None):
         self.func, self.args, self.kwargs, self.outs, self.kind = func, args, kwargs, outs, kind
         self.name = name or _func_name(func)
+        self.rc = None  # recompute segment id (ops traced inside a recompute scope), None outside
 
     @property
     def type(self):
@@ -193,6 +194,8 @@ class Program:
         # a GuardNode instead of ending the trace (jit.to_static's graph-break path)
         self._shadow = None
         self._shadow_dev = None
+        self._rc = None          # recompute segment id stamped on the nodes being recorded
+        self._rc_ids = itertools.count(1)
 
     # ------------------------------------------------------------ slots / values
     def _new_slot(self, meta):
@@ -302,7 +305,21 @@ class Program:
         self._append(node)
         return out
 
+    @contextlib.contextmanager
+    def recompute_scope(self, enabled=True):
+        """Nodes recorded inside form one recompute segment (reference: auto_parallel/interface.py:210 recompute,
+        whose ops carry a recompute id the recompute pass groups by); ``enabled=False`` excludes them from any
+        enclosing segment (exclude_ops_in_recompute)."""
+        prev = self._rc
+        self._rc = next(self._rc_ids) if enabled else None
+        try:
+            yield self._rc
+        finally:
+            self._rc = prev
+
     def _append(self, node):
+        if self._rc is not None and hasattr(node, "rc"):
+            node.rc = self._rc
         self._cur.append(node)
         self._version += 1
         self._plans.clear()

@@ -24,7 +24,7 @@ def _cfg():
     return LlamaConfig.tiny(num_hidden_layers=4, num_attention_heads=4, num_key_value_heads=2)
 
 
-def _worker(rank, world, port, shape, acc, schedule, q):
+def _worker(rank, world, port, shape, acc, schedule, q, recompute=False):
     paddle = _setup(rank, world, port)
     import paddlepaddle_amd.distributed as dist
     from paddlepaddle_amd.models.llama_auto import LlamaForCausalLMAuto, LlamaPretrainingCriterionAuto
@@ -39,6 +39,7 @@ def _worker(rank, world, port, shape, acc, schedule, q):
     strategy.pipeline.enable = pp > 1 or acc > 1
     strategy.pipeline.accumulate_steps = acc
     strategy.pipeline.schedule_mode = schedule
+    strategy.recompute.enable = recompute
     dm = dist.to_static(model, None, crit, opt, strategy)
     assert dm._engine is not None
     ids = _data()
@@ -55,8 +56,17 @@ def _worker(rank, world, port, shape, acc, schedule, q):
         assert ep.meta_exchanges == len(ep.sent_meta) and ep.messages == STEPS * acc * len(ep.sent_meta), (
             ep.meta_exchanges, len(ep.sent_meta), ep.messages)
         assert ep.ordered and ep.headers == STEPS * len(ep.sent_meta), ep.headers  # one header per class per run
+    if recompute:  # every decoder layer of this stage runs as one checkpointed segment
+        from paddlepaddle_amd.distributed.auto_parallel.static_engine import _Seg
+        segs = [it for it in eng.stage_items[eng.my_stage] if isinstance(it, _Seg)]
+        assert len(segs) == cfg.num_hidden_layers // pp, len(segs)
+        assert all(len(sg.outputs) == 1 for sg in segs), [sg.outputs for sg in segs]
     q.put((rank, losses, kinds, eng.my_stage))
     paddle.distributed.barrier()
+
+
+def _worker_rc(rank, world, port, shape, acc, schedule, q):
+    _worker(rank, world, port, shape, acc, schedule, q, recompute=True)
 
 
 LLAMA_PLAN = {
@@ -139,6 +149,17 @@ def test_static_auto_parallel_llama_matches_single_process(shape, acc, schedule)
             assert "allreduce" in kinds and "copy_to_parallel" in kinds
 
 
+@pytest.mark.parametrize("shape,acc,schedule", [((1, 1, 2), 1, "1F1B"), ((2, 1, 2), 2, "1F1B"),
+                                                ((2, 1, 2), 4, "ZBH1")])
+def test_static_engine_recompute_matches_single_process(shape, acc, schedule):
+    """strategy.recompute: each decoder layer is a checkpointed segment of the stage program (its activations,
+    TP collectives included, rebuilt in backward); losses equal single-process training."""
+    ref = _reference()
+    res = _spawn(_worker_rc, shape, acc, schedule, world=int(np.prod(shape)))
+    for rank, losses, kinds, stage in res:
+        np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-5, err_msg=f"rank {rank} stage {stage}")
+
+
 @pytest.mark.parametrize("shape,acc", [((1, 1, 2), 1), ((4, 1, 2), 4)])
 def test_parallelize_plan_llama_matches_single_process(shape, acc):
     """dist.parallelize (pipeline split_spec + ColWise / RowWise plan) then dist.to_static: same losses as
@@ -165,9 +186,14 @@ def test_static_engine_rejects_unimplemented_strategy_fields():
     cfg = _cfg()
     model = LlamaForCausalLMAuto(cfg)
     opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters())
-    for field, key in (("recompute", "enable"), ("sp_optimization", "enable"), ("gradient_merge", "enable"),
+    for field, key in (("sp_optimization", "enable"), ("gradient_merge", "enable"),
                        ("mp_optimization", "allreduce_matmul_grad_overlapping")):
         st = dist.Strategy()
         getattr(st, field)[key] = True
         with pytest.raises(NotImplementedError, match=field):
             StaticEngine(model, LlamaPretrainingCriterionAuto(cfg), opt, st)
+    st = dist.Strategy()
+    st.recompute["enable"] = True
+    st.recompute["refined_ops_patterns"] = [{"main_ops": ["matmul"], "num": 1}]
+    with pytest.raises(NotImplementedError, match="refined_ops_patterns"):
+        StaticEngine(model, LlamaPretrainingCriterionAuto(cfg), opt, st)

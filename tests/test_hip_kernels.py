@@ -173,6 +173,23 @@ def test_swiglu_packed(dt):
     torch.testing.assert_close(xy.grad.float(), xr.grad, atol=_tol(dt) * 4, rtol=_tol(dt) * 2)
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_swiglu_one_input(dt):
+    """swiglu(x) with x = [gate | up]: one-buffer gradient straight from the kernel (no autograd cat)."""
+    xy = torch.randn(3, 40, 2 * 512, device=DEV).to(dt).requires_grad_(True)
+    y = ops.swiglu(xy)
+    _lib_loaded("pa_swiglu_fwd")
+    assert type(y.grad_fn).__name__ == "_SwigluPackedHIPBackward"
+    xr = xy.detach().float().requires_grad_(True)
+    ar, br = xr.chunk(2, -1)
+    yr = F.silu(ar) * br
+    torch.testing.assert_close(y.float(), yr, atol=_tol(dt) * 4, rtol=_tol(dt))
+    g = torch.randn_like(yr)
+    y.backward(g.to(dt))
+    yr.backward(g)
+    torch.testing.assert_close(xy.grad.float(), xr.grad, atol=_tol(dt) * 4, rtol=_tol(dt) * 2)
+
+
 @pytest.mark.parametrize("neox", [True, False])
 def test_rope(neox):
     from paddlepaddle_amd.ops.rope import rope_tables, _rotate_ref
