@@ -258,6 +258,7 @@ def llama_static_bench(args, paddle, world, dist_on):
     strategy.pipeline.schedule_mode = "1F1B"
     strategy.pipeline.accumulate_steps = args.accum
     strategy.pipeline.micro_batch_size = args.micro_batch
+    strategy.recompute.enable = bool(args.recompute)  # each decoder layer a checkpointed segment of the program
     dm = dist.to_static(model, None, crit, opt, strategy)
     dev = _dev()
     gb = args.micro_batch * args.accum * dp
@@ -277,7 +278,8 @@ def llama_static_bench(args, paddle, world, dist_on):
     eng = dm._engine
     log(f"[llama-static] {args.model} pp{pp} tp{tp} dp{dp}: loss={float(state['loss']):.4f} "
         f"step={dt / args.steps * 1000:.1f}ms tokens/s={tps:.0f} MFU={mfu * 100:.1f}% peak_mem={mem:.1f}GiB "
-        f"params={cfg.num_params() / 1e9:.2f}B passes={getattr(eng, 'pass_stats', {})}")
+        f"params={cfg.num_params() / 1e9:.2f}B passes={getattr(eng, 'pass_stats', {})} "
+        f"recompute_segments={getattr(eng, 'n_segments', 0)}")
     return tps, dt / args.steps * 1000, gb, mfu
 
 

@@ -22,6 +22,8 @@ _FLAGS = {
     "FLAGS_eager_backward_engine": "native",  # native (csrc/autograd/autograd_exec.cpp RunBackward) | torch
     "FLAGS_weight_only_dequant_cache_mb": 4096,  # weight-only / LLM.int8: bf16 images of quantized weights kept
                                                  # for the bf16 GEMM path (0 = dequantise per call)
+    "FLAGS_static_native_executor": "auto",  # static training programs on the native executor (_C_train):
+                                             # auto (GPU) | force (also CPU, ATen instructions only) | off
     "FLAGS_gemm_backend": "auto",         # per-shape GEMM / conv backend: auto (timed) | hip | blas
     "FLAGS_sharding_stage3_keep_params": "auto",  # stage 3: keep gathered params until the optimizer step
     "FLAGS_conv_per_direction": True,     # NHWC conv: forward / dgrad / wgrad each on the faster of ours and MIOpen

@@ -323,6 +323,19 @@ class Executor:
             plan = P.build_plan(prog, fetch, keep)
             prog._plans[key] = plan
         dev = self._device(prog)
+        nat = self._native_runner(prog, plan, fetch, dev, key) if not use_graph else None
+        if nat is not None:
+            try:
+                outs = nat.run(self._feed(prog, feed or {}, dev))
+            except RuntimeError as e:
+                if nat.runs:  # it ran before: a real failure of this step
+                    raise
+                # an operand the native kernels reject at run time: this program keeps the Python replay
+                prog._native_runners[(key, str(dev))] = None
+                prog._native_reason = f"first native run failed: {e}"
+            else:
+                nat.runs += 1
+                return [(_wrap(t).numpy() if return_numpy else _wrap(t)) for t in outs]
         if use_graph and dev.type == "cuda" and self._graph_ok(prog):
             outs = self._run_graph(prog, plan, fetch, feed or {}, dev, key)
             if outs is not None:
@@ -354,6 +367,23 @@ class Executor:
             t = t.detach() if isinstance(t, torch.Tensor) else t
             outs.append(_wrap(t).numpy() if return_numpy else _wrap(t))
         return outs
+
+    # ------------------------------------------------------------------ native training executor
+    def _native_runner(self, prog, plan, fetch, dev, key):
+        """The lowered program on the native executor (static/native_train.py) when FLAGS_static_native_executor
+        allows it and the program lowers; the reason it did not is kept on the program (``_native_reason``)."""
+        from ..framework.flags import flag
+        mode = str(flag("FLAGS_static_native_executor", "auto")).lower()
+        if mode in ("0", "off", "false") or (mode == "auto" and dev.type != "cuda"):
+            return None
+        cache = prog.__dict__.setdefault("_native_runners", {})
+        k = (key, str(dev))
+        if k not in cache:
+            from . import native_train
+            runner, reason = native_train.compile_training(prog, plan, fetch, dev, native_kernels=dev.type == "cuda")
+            cache[k] = runner
+            prog._native_reason = reason
+        return cache[k]
 
     # ------------------------------------------------------------------ hipGraph execution
     @staticmethod
