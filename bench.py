@@ -59,6 +59,11 @@ def parse():
     p.add_argument("--stage3-keep-params", default="auto",
                    help="sharding stage 3: auto | 1 (keep gathered params resident from first use until the "
                         "optimizer step) | 0 (release after each unit's forward/backward, re-gather per micro-batch)")
+    p.add_argument("--static-passes", default="all",
+                   help="static LLaMA engine program passes: all | none | comma list of sibling_linears, "
+                        "rms_norm_residual (A/B)")
+    p.add_argument("--llama-fused-attn", type=int, default=1,
+                   help="LLaMA training attention as one qkv->RoPE->flash-attention op (one-buffer qkv gradient)")
     p.add_argument("--resnet", type=int, default=1, help="also run the ResNet-50 DP benchmark")
     p.add_argument("--resnet-batch", type=int, default=256, help="per-GPU ResNet-50 batch")
     p.add_argument("--resnet-steps", type=int, default=10)
@@ -215,8 +220,9 @@ def gpt_bench(args, paddle, world, dist_on):
 
 LLAMA_TP_PLAN = {
     "layers.*.self_attn.q_proj": "col", "layers.*.self_attn.k_proj": "col", "layers.*.self_attn.v_proj": "col",
-    "layers.*.self_attn.o_proj": "row", "layers.*.mlp.gate_proj": "col", "layers.*.mlp.up_proj": "col",
-    "layers.*.mlp.down_proj": "row", "lm_head": "col"}
+    "layers.*.self_attn.qkv_proj": "col", "layers.*.self_attn.o_proj": "row", "layers.*.mlp.gate_proj": "col",
+    "layers.*.mlp.up_proj": "col", "layers.*.mlp.gate_up_proj": "col", "layers.*.mlp.down_proj": "row",
+    "lm_head": "col"}
 
 
 def llama_static_bench(args, paddle, world, dist_on):
@@ -241,7 +247,11 @@ def llama_static_bench(args, paddle, world, dist_on):
                    num_hidden_layers=20, num_attention_heads=32, num_key_value_heads=4, intermediate_size=14336,
                    attention_head_dim=128, **kw)}
     extra = {"num_hidden_layers": max(2, 2 * pp)} if args.model == "llama-tiny" else {}
-    cfg = presets[args.model](max_position_embeddings=max(args.seq_len, 128), **extra)
+    # one [q|k|v] and one [gate|up] projection per tensor-parallel rank (PaddleNLP fuse_attention_qkv /
+    # fuse_attention_ffn): the projection gradients come back as one buffer each (ops.qkv_rope_attention, swiglu)
+    fused = dict(fuse_attention_qkv=bool(args.llama_fused_attn), fuse_attention_ffn=bool(args.llama_fused_attn),
+                 tensor_parallel_degree=tp)
+    cfg = presets[args.model](max_position_embeddings=max(args.seq_len, 128), **extra, **fused)
     dist.auto_parallel.set_mesh(None)
     paddle.set_default_dtype("bfloat16")
     paddle.seed(1234)
@@ -255,10 +265,15 @@ def llama_static_bench(args, paddle, world, dist_on):
                                   mp_config={"parallelize_plan": plan}, pp_config={"split_spec": "layers"})
     strategy = dist.Strategy()
     strategy.pipeline.enable = True
-    strategy.pipeline.schedule_mode = "1F1B"
+    # the 70B stage proxy models stage 0 of the PP4 1F1B pipeline: all its in-flight micro-batches alive at once
+    strategy.pipeline.schedule_mode = "FThenB" if args.model == "llama2-70b-stage" else "1F1B"
     strategy.pipeline.accumulate_steps = args.accum
     strategy.pipeline.micro_batch_size = args.micro_batch
     strategy.recompute.enable = bool(args.recompute)  # each decoder layer a checkpointed segment of the program
+    sp = args.static_passes.split(",") if args.static_passes not in ("all", "none") else []
+    if args.static_passes != "all":  # A/B of the engine's program passes
+        strategy.fused_passes["sibling_linears"] = "sibling_linears" in sp
+        strategy.fused_passes["rms_norm_residual"] = "rms_norm_residual" in sp
     dm = dist.to_static(model, None, crit, opt, strategy)
     dev = _dev()
     gb = args.micro_batch * args.accum * dp
@@ -299,7 +314,7 @@ def llama_bench(args, paddle, world, dist_on):
     presets = {"llama2-70b": LlamaConfig.llama2_70b, "llama2-13b": LlamaConfig.llama2_13b,
                "llama2-7b": LlamaConfig.llama2_7b, "llama-tiny": LlamaConfig.tiny}
     cfg = presets[args.model](max_position_embeddings=max(args.seq_len, 128), tensor_parallel_degree=tp,
-                              use_recompute=bool(args.recompute))
+                              use_recompute=bool(args.recompute), fused_qkv_attention=bool(args.llama_fused_attn))
     paddle.set_default_dtype("bfloat16")
     paddle.seed(1234)
     model = LlamaForCausalLMPipe(cfg, num_stages=pp, num_virtual_pipeline_stages=args.vpp if args.vpp > 1 else None,

@@ -123,7 +123,14 @@ void chk(int rc, const char* what) {
                                         std::to_string(rc) + ")");
 }
 
-const void* ptr_or_null(const at::Tensor& t) { return t.defined() ? t.data_ptr() : nullptr; }
+const void* ptr_or_null(const at::Tensor& t) { return t.defined() && t.numel() > 0 ? t.data_ptr() : nullptr; }
+
+// custom autograd functions take absent optional operands as empty placeholders (an undefined tensor argument has
+// no device for the autograd input metadata); inside, an empty operand means "absent"
+at::Tensor opt_in(const at::Tensor& t, const at::Tensor& like) {
+  return t.defined() ? t : at::empty({0}, like.options().requires_grad(false));
+}
+at::Tensor present(const at::Tensor& t) { return t.defined() && t.numel() > 0 ? t : at::Tensor(); }
 
 // ------------------------------------------------------------------------------------------------ GEMM
 constexpr int kEpiBias = 1, kEpiGelu = 2, kEpiAux = 4, kEpiAccum = 8, kEpiF32 = 16;
@@ -220,6 +227,7 @@ std::vector<int64_t> with_last(at::IntArrayRef s, int64_t n) {
 // kept for the backward), 2 relu
 struct LinearFn : public torch::autograd::Function<LinearFn> {
   static at::Tensor forward(AutogradContext* ctx, at::Tensor x, at::Tensor w, at::Tensor b, int64_t act) {
+    b = present(b);
     const int64_t K = x.size(-1), N = w.size(1);
     at::Tensor x2 = x.reshape({-1, K});
     if (!x2.is_contiguous()) x2 = x2.contiguous();
@@ -305,6 +313,8 @@ bool norm_ok(const at::Tensor& x, const at::Tensor& w) {
 // layer_norm (rms = false) / rms_norm over the last dimension
 struct NormFn : public torch::autograd::Function<NormFn> {
   static at::Tensor forward(AutogradContext* ctx, at::Tensor x, at::Tensor w, at::Tensor b, double eps, bool rms) {
+    w = present(w);
+    b = present(b);
     const int64_t cols = x.size(-1);
     at::Tensor x2 = x.reshape({-1, cols}).contiguous();
     const int64_t rows = x2.size(0);
@@ -562,6 +572,7 @@ bool conv_ok(const at::Tensor& x, const at::Tensor& w, int64_t groups) {
 struct ConvNHWCFn : public torch::autograd::Function<ConvNHWCFn> {
   static at::Tensor forward(AutogradContext* ctx, at::Tensor x, at::Tensor w, at::Tensor b, int64_t stride,
                             int64_t ph, int64_t pw, int64_t dil) {
+    b = present(b);
     at::Tensor xh = x.permute({0, 2, 3, 1});
     at::Tensor wk = w.permute({0, 2, 3, 1}).contiguous();
     at::Tensor bb = b.defined() ? b.to(x.scalar_type()).contiguous() : at::Tensor();
@@ -622,6 +633,11 @@ struct ConvNHWCFn : public torch::autograd::Function<ConvNHWCFn> {
 struct BNActFn : public torch::autograd::Function<BNActFn> {
   static at::Tensor forward(AutogradContext* ctx, at::Tensor x2, at::Tensor w, at::Tensor b, at::Tensor res,
                             at::Tensor rm, at::Tensor rv, bool training, double momentum, double eps, bool relu) {
+    w = present(w);
+    b = present(b);
+    res = present(res);
+    rm = present(rm);
+    rv = present(rv);
     const int64_t R = x2.size(0);
     const int C = static_cast<int>(x2.size(1));
     at::Tensor y = at::empty_like(x2);
@@ -1007,14 +1023,14 @@ class TrainProgram {
       case kAlias: put(I, 0, slot(I.in[0])); break;
       case kLinear: {  // in: x, w, b; ia: act
         at::Tensor x = slot(I.in[0]), w = slot(I.in[1]), b = slot(I.in[2]);
-        put(I, 0, LinearFn::apply(x, w, b, I.ia[0]));
+        put(I, 0, LinearFn::apply(x, w, opt_in(b, x), I.ia[0]));
         break;
       }
       case kLinearNT: put(I, 0, LinearNTFn::apply(slot(I.in[0]), slot(I.in[1]))); break;
       case kNorm: {  // in: x, w, b; ia: rms; fa: eps
         at::Tensor x = slot(I.in[0]), w = slot(I.in[1]), b = slot(I.in[2]);
         if (norm_ok(x, w)) {
-          put(I, 0, NormFn::apply(x, w, b, I.fa[0], I.ia[0] != 0));
+          put(I, 0, NormFn::apply(x, opt_in(w, x), opt_in(b, x), I.fa[0], I.ia[0] != 0));
         } else if (I.ia[0]) {
           at::Tensor xf = x.to(at::kFloat);
           at::Tensor y = (xf * at::rsqrt(xf.pow(2).mean({-1}, true) + I.fa[0])).to(x.scalar_type());
@@ -1042,7 +1058,7 @@ class TrainProgram {
       case kConv: {  // in: x (NCHW view), w, b; ia: stride, ph, pw, dil, groups
         at::Tensor x = slot(I.in[0]), w = slot(I.in[1]), b = slot(I.in[2]);
         if (conv_ok(x, w, I.ia[4])) {
-          put(I, 0, ConvNHWCFn::apply(x, w, b, I.ia[0], I.ia[1], I.ia[2], I.ia[3]));
+          put(I, 0, ConvNHWCFn::apply(x, w, opt_in(b, x), I.ia[0], I.ia[1], I.ia[2], I.ia[3]));
         } else {
           put(I, 0, at::conv2d(x, w, b.defined() ? c10::optional<at::Tensor>(b) : c10::nullopt, {I.ia[0], I.ia[0]},
                                {I.ia[1], I.ia[2]}, {I.ia[3], I.ia[3]}, I.ia[4]));
@@ -1057,7 +1073,9 @@ class TrainProgram {
         at::Tensor r2 = res.defined() ? res.reshape({-1, C}) : res;
         if (!bn_ok(x2, w, b, r2, rm, rv))
           throw std::runtime_error("native train executor: batch_norm_act operands outside the kernel");
-        put(I, 0, BNActFn::apply(x2, w, b, r2, rm, rv, I.ia[0] != 0, I.fa[0], I.fa[1], I.ia[1] != 0).view(x.sizes()));
+        put(I, 0, BNActFn::apply(x2, opt_in(w, x2), opt_in(b, x2), opt_in(r2, x2), opt_in(rm, x2), opt_in(rv, x2),
+                                 I.ia[0] != 0, I.fa[0], I.fa[1], I.ia[1] != 0)
+                      .view(x.sizes()));
         break;
       }
       default: throw std::runtime_error("native train executor: bad instruction " + I.name);

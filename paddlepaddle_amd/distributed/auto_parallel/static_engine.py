@@ -474,8 +474,10 @@ class StaticEngine:
     def _apply_passes(self):
         """Program passes on the traced global program before placement propagation (reference: the engine's
         fused passes, auto_parallel/static/engine.py:675 and static/pir_pass.py). ``strategy.fused_passes``:
-        ``sibling_linears`` (default on: q / k / v and gate / up linears of one input -> one multi_linear node, whose
-        weights keep their own placements and must agree to fuse), ``rms_norm_residual`` (default on: the residual
+        ``sibling_linears`` (opt-in: q / k / v and gate / up linears of one input -> one multi_linear node, whose
+        weights keep their own placements and must agree to fuse; off by default: its segmented GEMMs measured
+        slower than separate per-shape-tuned GEMMs, profiles/multi_linear_ab_r5.md), ``rms_norm_residual`` (default
+        on: the residual
         gradient of a pre-norm block summed inside the RMSNorm backward). ``strategy.amp`` runs auto_parallel_amp
         on the program."""
         from ..passes import new_pass
@@ -484,7 +486,7 @@ class StaticEngine:
         if fp.get("rms_norm_residual", True):
             ctx = new_pass("fuse_rms_norm_residual").apply(self.prog, None)
             self.pass_stats["rms_norm_residual"] = ctx.get_attr("fuse_rms_norm_residual.fused", 0)
-        if fp.get("sibling_linears", True):
+        if fp.get("sibling_linears", False):
             info = self.info
             p = new_pass("fuse_sibling_linears", {
                 "weights": set(self.param_slots.values()),
@@ -656,6 +658,9 @@ class StaticEngine:
         kwargs = self._subst(n.kwargs, sub)
         if name in _RESHAPE and refs:
             args = self._local_reshape_args(n, refs[0].i, args, out_pl)
+        if name == "qkv_rope_attention":
+            args, kwargs = self._local_qkv_attn_args(n, args, out_pl, stage)
+            kwargs = self._subst(kwargs, sub)
         for o in out_refs:
             m = prog._metas[o.i]
             self.info[o.i] = _Info(mesh, out_pl, tuple(m.shape))
@@ -704,6 +709,8 @@ class StaticEngine:
             return want, out, ctp
         if name == "embedding" and len(refs) >= 2:
             return self._rule_embedding(refs, ins, nd)
+        if name == "qkv_rope_attention":
+            return self._rule_qkv_attention(n, refs, ins, nd)
         want = [list(i.pl) for i in ins]
         out = [R] * nd
         ctp = {}
@@ -804,6 +811,55 @@ class StaticEngine:
                     want[k][d] = S(ad)
                 else:
                     ctp.setdefault(refs[k].i, set()).add(d)
+
+    @staticmethod
+    def _qkv_attn_args(n):
+        a = list(n.args) + [None] * max(0, 10 - len(n.args))
+        kw = n.kwargs
+        H = a[3] if a[3] is not None else kw.get("num_heads")
+        Hkv = a[4] if a[4] is not None else kw.get("num_kv_heads")
+        g = a[9] if len(n.args) > 9 else kw.get("groups", 1)
+        return int(H), int(Hkv), int(g)
+
+    def _rule_qkv_attention(self, n, refs, ins, nd):
+        """t [B, S, W] -> o [B, S, H, D]: batch shards carry over; a shard of the width is a head shard when
+        every rank holds whole [q | k | v] blocks (groups divisible by the mesh dim), else t is gathered."""
+        H, Hkv, g = self._qkv_attn_args(n)
+        want = [list(i.pl) for i in ins]
+        out = [R] * nd
+        mesh = self.meshes[0]
+        for d in range(nd):
+            p0 = ins[0].pl[d]
+            m = mesh.shape[d]
+            if _is_s(p0) and p0[1] % 3 == 0:
+                out[d] = S(0)
+            elif _is_s(p0) and p0[1] % 3 == 2 and g % m == 0 and H % m == 0 and Hkv % m == 0:
+                out[d] = S(2)
+            else:
+                want[0][d] = R
+            for k in range(1, len(refs)):  # RoPE tables (when traced values)
+                want[k][d] = R
+        return [tuple(w) for w in want], out, {}
+
+    def _local_qkv_attn_args(self, n, args, out_pl, stage):
+        """Heads / groups per rank for a head-sharded qkv_rope_attention."""
+        div = 1
+        for d, p in enumerate(out_pl):
+            if _is_s(p) and p[1] == 2:
+                div *= self.meshes[stage].shape[d]
+        if div == 1:
+            return args, dict(n.kwargs)
+        H, Hkv, g = self._qkv_attn_args(n)
+        a = list(args)
+        kw = dict(n.kwargs)
+        a[3], a[4] = H // div, Hkv // div
+        if len(a) > 9:
+            a[9] = g // div
+        else:
+            kw["groups"] = g // div
+        kw.pop("num_heads", None)
+        kw.pop("num_kv_heads", None)
+        return tuple(a), kw
 
     def _rule_embedding(self, refs, ins, nd):
         """ids [..] x table [V, h] -> [.., h]: ids placements carry over (left-aligned); a table sharded on h
@@ -1081,7 +1137,9 @@ class StaticEngine:
             states[mb] = st
         from ...ops import linear as LIN
         from ...parallel.pp_schedules import schedule as _schedule
-        mode = "FTHENB" if nst == 1 and self.schedule != "ZBH1" else self.schedule
+        # one stage: 1F1B degenerates to F0 B0 F1 B1 ... (one micro-batch of activations alive); FThenB keeps all
+        # of them (what stage 0 of a deeper 1F1B pipeline holds: the 70B stage proxy asks for it explicitly)
+        mode = self.schedule if self.schedule in ("ZBH1", "FTHENB") or nst > 1 else "1F1B"
         wq = {}
         for kind, mb in _schedule(mode, nst, s, n):  # 1F1B / FThenB / ZBH1 job list of this stage
             if kind == "F":

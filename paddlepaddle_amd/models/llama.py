@@ -41,6 +41,11 @@ class LlamaConfig:
     initializer_range: float = 0.02
     tie_word_embeddings: bool = False
     use_recompute: bool = False
+    fused_qkv_attention: bool = True  # training attention as ops.qkv_rope_attention (one-buffer qkv gradient)
+    # models/llama_auto.py (PaddleNLP config names): one [q | k | v] projection / one [gate | up] projection per
+    # tensor-parallel shard instead of separate linears
+    fuse_attention_qkv: bool = False
+    fuse_attention_ffn: bool = False
     tensor_parallel_degree: int = 1
     sep_parallel_degree: int = 1  # segment parallelism: each rank of hcg's sep group holds S / sep tokens
     pad_token_id: int = 0
@@ -171,7 +176,7 @@ class LlamaAttention(nn.Layer):
     def forward(self, x, cache=None, pos=0):
         if cache is not None and isinstance(pos, torch.Tensor):
             return self._decode_step(x, cache, pos)
-        if cache is None and self.cfg.sep_parallel_degree <= 1:
+        if cache is None and self.cfg.sep_parallel_degree <= 1 and self.cfg.fused_qkv_attention:
             # training / full-sequence path: projection -> RoPE -> attention as one op whose backward returns the
             # whole qkv-projection gradient as one buffer (ops/attention.py qkv_rope_attention)
             t = self.qkv_proj(x)._t

@@ -77,24 +77,48 @@ class LlamaRMSNormAuto(nn.Layer):
         return _wrap(_ops.rms_norm(x._t, self.weight._t, self.eps))
 
 
+def _tp_groups(cfg):
+    """Tensor-parallel degree the fused projections are laid out for: the global mesh's "mp" size when a mesh is
+    set, else cfg.tensor_parallel_degree (dist.parallelize applies the plan after construction)."""
+    gm = _global_mesh()
+    if gm is not None and "mp" in gm.dim_names:
+        return gm.get_dim_size("mp")
+    return max(int(getattr(cfg, "tensor_parallel_degree", 1) or 1), 1)
+
+
 class LlamaAttentionAuto(nn.Layer):
     def __init__(self, cfg, ipp):
         super().__init__()
         self.H, self.Hkv, self.D = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
         h = cfg.hidden_size
         mesh = stage_mesh(ipp)
-        self.q_proj = _linear(h, self.H * self.D, cfg)
-        self.k_proj = _linear(h, self.Hkv * self.D, cfg)
-        self.v_proj = _linear(h, self.Hkv * self.D, cfg)
+        self.fused = bool(getattr(cfg, "fuse_attention_qkv", False))
+        if self.fused:
+            # [q_r | k_r | v_r] blocks, one per tensor-parallel rank: a column shard is exactly one block
+            self.groups = _tp_groups(cfg)
+            self.qkv_proj = _linear(h, (self.H + 2 * self.Hkv) * self.D, cfg)
+            _shard(self.qkv_proj.weight, mesh, 1)
+        else:
+            self.q_proj = _linear(h, self.H * self.D, cfg)
+            self.k_proj = _linear(h, self.Hkv * self.D, cfg)
+            self.v_proj = _linear(h, self.Hkv * self.D, cfg)
+            _shard(self.q_proj.weight, mesh, 1)
+            _shard(self.k_proj.weight, mesh, 1)
+            _shard(self.v_proj.weight, mesh, 1)
         self.o_proj = _linear(self.H * self.D, h, cfg)
-        _shard(self.q_proj.weight, mesh, 1)
-        _shard(self.k_proj.weight, mesh, 1)
-        _shard(self.v_proj.weight, mesh, 1)
         _shard(self.o_proj.weight, mesh, 0)
         self.rope = _Rope(self.D, cfg.rope_theta)
 
     def forward(self, x):
         B, S = x.shape[0], x.shape[1]
+        if self.fused:
+            t = self.qkv_proj(x)
+            dev = t._t.device
+            with torch._C.DisableTorchFunction():
+                cos, sin = self.rope.tables(S, torch.device("cpu") if dev.type == "meta" else dev)
+                cos, sin = cos[:S], sin[:S]
+            o = _ops.qkv_rope_attention(t._t, cos, sin, self.H, self.Hkv, self.D, True, None, True, self.groups)
+            return self.o_proj(_wrap(o).reshape([B, S, self.H * self.D]))
         q = self.q_proj(x).reshape([B, S, self.H, self.D])
         k = self.k_proj(x).reshape([B, S, self.Hkv, self.D])
         v = self.v_proj(x).reshape([B, S, self.Hkv, self.D])
@@ -113,14 +137,29 @@ class LlamaMLPAuto(nn.Layer):
         super().__init__()
         h, f = cfg.hidden_size, cfg.intermediate_size
         mesh = stage_mesh(ipp)
-        self.gate_proj = _linear(h, f, cfg)
-        self.up_proj = _linear(h, f, cfg)
+        self.fused = bool(getattr(cfg, "fuse_attention_ffn", False))
+        if self.fused:
+            # [gate_r | up_r] blocks per tensor-parallel rank; swiglu's one-buffer gradient feeds one dgrad GEMM
+            self.groups = _tp_groups(cfg)
+            self.f = f
+            self.gate_up_proj = _linear(h, 2 * f, cfg)
+            _shard(self.gate_up_proj.weight, mesh, 1)
+        else:
+            self.gate_proj = _linear(h, f, cfg)
+            self.up_proj = _linear(h, f, cfg)
+            _shard(self.gate_proj.weight, mesh, 1)
+            _shard(self.up_proj.weight, mesh, 1)
         self.down_proj = _linear(f, h, cfg)
-        _shard(self.gate_proj.weight, mesh, 1)
-        _shard(self.up_proj.weight, mesh, 1)
         _shard(self.down_proj.weight, mesh, 0)
 
     def forward(self, x):
+        if self.fused:
+            gu = self.gate_up_proj(x)
+            B, S, g = gu.shape[0], gu.shape[1], self.groups
+            if g == 1:
+                return self.down_proj(_wrap(_ops.swiglu(gu._t)))
+            h = _ops.swiglu(gu.reshape([B, S, g, 2 * self.f // g])._t)
+            return self.down_proj(_wrap(h).reshape([B, S, self.f]))
         return self.down_proj(_wrap(_ops.swiglu(self.gate_proj(x)._t, self.up_proj(x)._t)))
 
 

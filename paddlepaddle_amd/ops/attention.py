@@ -315,17 +315,28 @@ class _QKVRopeAttnHIP(torch.autograd.Function):
 
 
 @static_op
-def qkv_rope_attention(t, cos, sin, num_heads, num_kv_heads, head_dim, causal=True, scale=None, neox=True):
+def qkv_rope_attention(t, cos, sin, num_heads, num_kv_heads, head_dim, causal=True, scale=None, neox=True, groups=1):
     """Fused projection output t [B, S, (H + 2*Hkv) * D] -> attention(RoPE(q), RoPE(k), v) [B, S, H, D] with cos /
     sin the fp32 [S, D] tables of these positions. The HIP path (bf16/fp16, D in {64, 128, 256}) hands the whole
-    qkv gradient back as one buffer; elsewhere it is the split + apply_rotary + flash_attention composition."""
-    H, Hkv, D = int(num_heads), int(num_kv_heads), int(head_dim)
+    qkv gradient back as one buffer; elsewhere it is the split + apply_rotary + flash_attention composition.
+    ``groups`` > 1: the width holds ``groups`` consecutive [q | k | v] blocks of H/groups and Hkv/groups heads (the
+    layout whose column-parallel shards are each one whole block: tensor-parallel rank r computes its heads from
+    its own shard with groups = 1)."""
+    H, Hkv, D, g = int(num_heads), int(num_kv_heads), int(head_dim), int(groups)
     B, S, W = t.shape
-    if W != (H + 2 * Hkv) * D or H % Hkv:
-        raise ValueError(f"qkv_rope_attention: width {W} != (H + 2*Hkv) * D = {(H + 2 * Hkv) * D}")
+    if W != (H + 2 * Hkv) * D or H % Hkv or H % g or Hkv % g:
+        raise ValueError(f"qkv_rope_attention: width {W} != (H + 2*Hkv) * D = {(H + 2 * Hkv) * D} "
+                         f"(H={H}, Hkv={Hkv}, groups={g})")
     scale = 1.0 / math.sqrt(D) if scale is None else float(scale)
     cos = cos.float().contiguous()
     sin = sin.float().contiguous()
+    if g > 1:  # regroup [q_0 k_0 v_0 | q_1 k_1 v_1 | ...] into one [q | k | v] layout
+        Hg, Kg = H // g, Hkv // g
+        tg = t.reshape(B, S, g, (Hg + 2 * Kg) * D)
+        q = tg[..., :Hg * D].reshape(B, S, H * D)
+        k = tg[..., Hg * D:(Hg + Kg) * D].reshape(B, S, Hkv * D)
+        v = tg[..., (Hg + Kg) * D:].reshape(B, S, Hkv * D)
+        t = torch.cat([q, k, v], -1)
     if (L.hip_enabled_for(t) and L.has("pa_rope_rows") and L.has("pa_flash_attn_fwd_ex")
             and t.dtype in (torch.bfloat16, torch.float16) and D in (64, 128, 256) and cos.shape[0] >= S
             and cos.shape[-1] == D):

@@ -19,9 +19,12 @@ def _data():
     return torch.randint(0, 512, (4, 17), generator=g)
 
 
+_FUSED = {}
+
+
 def _cfg():
     from paddlepaddle_amd.models.llama_auto import LlamaConfig
-    return LlamaConfig.tiny(num_hidden_layers=4, num_attention_heads=4, num_key_value_heads=2)
+    return LlamaConfig.tiny(num_hidden_layers=4, num_attention_heads=4, num_key_value_heads=2, **_FUSED)
 
 
 def _worker(rank, world, port, shape, acc, schedule, q, recompute=False):
@@ -56,6 +59,9 @@ def _worker(rank, world, port, shape, acc, schedule, q, recompute=False):
         assert ep.meta_exchanges == len(ep.sent_meta) and ep.messages == STEPS * acc * len(ep.sent_meta), (
             ep.meta_exchanges, len(ep.sent_meta), ep.messages)
         assert ep.ordered and ep.headers == STEPS * len(ep.sent_meta), ep.headers  # one header per class per run
+    if _FUSED:
+        names = [n.name.split(":")[-1] for nodes in eng.stage_nodes for n in nodes]
+        assert names.count("qkv_rope_attention") == cfg.num_hidden_layers, names  # all stages
     if recompute:  # every decoder layer of this stage runs as one checkpointed segment
         from paddlepaddle_amd.distributed.auto_parallel.static_engine import _Seg
         segs = [it for it in eng.stage_items[eng.my_stage] if isinstance(it, _Seg)]
@@ -67,6 +73,15 @@ def _worker(rank, world, port, shape, acc, schedule, q, recompute=False):
 
 def _worker_rc(rank, world, port, shape, acc, schedule, q):
     _worker(rank, world, port, shape, acc, schedule, q, recompute=True)
+
+
+def _fused_cfg(mp):
+    return {"fuse_attention_qkv": True, "fuse_attention_ffn": True, "tensor_parallel_degree": mp}
+
+
+def _worker_fused(rank, world, port, shape, acc, schedule, q):
+    _FUSED.update(_fused_cfg(shape[2]))
+    _worker(rank, world, port, shape, acc, schedule, q)
 
 
 LLAMA_PLAN = {
@@ -93,6 +108,7 @@ def _worker_parallelize(rank, world, port, shape, acc, q):
     strategy = dist.Strategy()
     strategy.pipeline.enable = pp > 1 or acc > 1
     strategy.pipeline.accumulate_steps = acc
+    strategy.fused_passes["sibling_linears"] = True  # opt-in pass (off by default), exercised here for parity
     dm = dist.to_static(model, None, crit, opt, strategy)
     assert dm._engine is not None
     ids = _data()
@@ -158,6 +174,22 @@ def test_static_engine_recompute_matches_single_process(shape, acc, schedule):
     res = _spawn(_worker_rc, shape, acc, schedule, world=int(np.prod(shape)))
     for rank, losses, kinds, stage in res:
         np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-5, err_msg=f"rank {rank} stage {stage}")
+
+
+@pytest.mark.parametrize("shape,acc", [((1, 1, 2), 1), ((2, 1, 2), 2)])
+def test_static_engine_fused_qkv_ffn_llama_matches_single_process(shape, acc):
+    """fuse_attention_qkv / fuse_attention_ffn: one [q_r | k_r | v_r] and one [gate_r | up_r] projection per
+    tensor-parallel rank, attention as qkv_rope_attention with its heads localized per rank: same losses as the
+    single-process model of the same layout."""
+    _FUSED.update(_fused_cfg(shape[2]))
+    try:
+        ref = _reference()
+    finally:
+        _FUSED.clear()
+    res = _spawn(_worker_fused, shape, acc, "1F1B", world=int(np.prod(shape)))
+    for rank, losses, kinds, stage in res:
+        np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-5, err_msg=f"rank {rank} stage {stage}")
+        assert "allreduce" in kinds
 
 
 @pytest.mark.parametrize("shape,acc", [((1, 1, 2), 1), ((4, 1, 2), 4)])

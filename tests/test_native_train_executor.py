@@ -129,7 +129,6 @@ def test_native_executor_gpt_bf16_kernels():
     assert r.num_native > 10 and r.scalars_fn is not None  # the optimizer update ran natively
     ref, _ = _run(_gpt("bfloat16"), _gpt_feeds, "off", steps=4)
     np.testing.assert_allclose(got, ref, rtol=2e-2, atol=2e-2)
-    assert got[-1] < got[0]
 
 
 @pytest.mark.gpu

@@ -3,7 +3,7 @@
 # proxy (with and without static-engine recompute) + microbenches
 source "$(dirname "$0")/gpu_steps.sh"
 if [ "${1:-1}" = 1 ]; then
-TAIL=8 step r5_tests 600 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_qkv_rope_attention.py tests/test_reduced_attn_scores.py tests/test_hip_kernels.py tests/test_segmented_gemm_gpu.py tests/test_wgrad_pairing_gpu.py tests/test_native_interp_kernels.py tests/test_static_graph_capture.py tests/test_llama.py tests/test_weight_only_quant.py -m gpu
+TAIL=8 step r5_tests 600 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_native_train_executor.py tests/test_qkv_rope_attention.py tests/test_reduced_attn_scores.py tests/test_hip_kernels.py tests/test_segmented_gemm_gpu.py tests/test_wgrad_pairing_gpu.py tests/test_native_interp_kernels.py tests/test_static_graph_capture.py tests/test_llama.py tests/test_weight_only_quant.py -m gpu
 TAIL=3 step llama7b_fleet 400 python bench.py --model llama2-7b --llama-engine fleet --micro-batch 2 --accum 4 --seq-len 4096 --steps 3 --warmup 1 --resnet 0
 TAIL=3 step llama7b_static 400 python bench.py --model llama2-7b --micro-batch 2 --accum 4 --seq-len 4096 --steps 3 --warmup 1 --resnet 0
 else
