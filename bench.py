@@ -42,7 +42,7 @@ def parse():
     p.add_argument("--seq-len", type=int, default=2048)
     p.add_argument("--recompute", type=int, default=0)
     p.add_argument("--sharding-stage", type=int, default=3)
-    p.add_argument("--pair-wgrad", type=int, default=1,
+    p.add_argument("--pair-wgrad", type=int, default=0,
                    help="GPT: pair the weight-gradient GEMMs of consecutive accumulation micro-batches into one "
                         "K = 2T product (ops/linear.py pair_weight_grads)")
     p.add_argument("--tp", type=int, default=None,

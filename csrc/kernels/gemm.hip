@@ -515,7 +515,10 @@ using H3_ = IntC<3>;
 using True_ = IntC<1>;
 using False_ = IntC<0>;
 
-template <bool AK, bool BKM>
+// SEG: 0 plain operands; 1 K-segmented, 2 N-segmented operands (GemmArgs::nseg, pa_gemm_bf16_pp_segs). The
+// segment selection is compiled only into the segmented instantiations: the plain kernel's staging code (and its
+// register allocation) is the unsegmented ping-pong loop.
+template <bool AK, bool BKM, int SEG = 0>
 __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p0) {
   GemmArgs p = split_view<AK, BKM>(p0);
   constexpr int HALF = 128 * kBK * 2;  // 16 KiB
@@ -537,7 +540,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p0) {
     const int ks = u % p.tail_split;
     pid = p.full_tiles + u / p.tail_split;
     p.K /= p.tail_split;
-    kt0 = ks * (p.K / kBK);
+    if constexpr (SEG == 0) {  // plain operands: the slice's operand bases move (the round-4 kernel)
+      p.a += (int64_t)ks * p.K * (AK ? 1 : p.lda);
+      p.b += (int64_t)ks * p.K * (BKM ? 1 : p.ldb);
+    } else {  // segmented operands: the slice's first global K-tile selects the segment
+      kt0 = ks * (p.K / kBK);
+    }
     tail_out = p.tail_ws + (int64_t)u * 65536;
   } else {
     pid = xcd_remap(bid, p.tail_split > 0 ? p.full_tiles : p.tiles_m * p.tiles_n);
@@ -549,14 +557,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p0) {
 
   // Staging of the A (h = 0, 2: rows m0, m0 + 128) or B (h = 1, 3: columns n0, n0 + 128) half of local K-tile t,
   // through the operand segments when there are any (wave-uniform selects).
-  const bool kseg = p.nseg > 1 && p.seg_k, nseg = p.nseg > 1 && !p.seg_k;
   auto stage_half = [&](int t, int h, char* dst) {
-    const int tg = kt0 + t;
+    const int tg = SEG == 0 ? t : kt0 + t;
     int k0 = tg * kBK;
     const uint16_t* a = p.a;
     const uint16_t* b = p.b;
     int64_t lda = p.lda, ldb = p.ldb;
-    if (kseg) {
+    if constexpr (SEG == 1) {
       const int s = seg_of(p, tg);
       k0 = (tg - pick4(s, 0, p.seg_end[0], p.seg_end[1], p.seg_end[2])) * kBK;
       a = pick4(s, p.seg_a[0], p.seg_a[1], p.seg_a[2], p.seg_a[3]);
@@ -568,7 +575,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p0) {
       stage<128, AK>(a, lda, m0 + (h == 2 ? 128 : 0), p.M, k0, dst, wave, lane);
     } else {
       int c0 = n0 + (h == 3 ? 128 : 0), cmax = p.N;
-      if (nseg) {  // column segments: segment s owns columns [seg_end[s-1], seg_end[s]) of C
+      if constexpr (SEG == 2) {  // column segments: segment s owns columns [seg_end[s-1], seg_end[s]) of C
         const int s = seg_of(p, c0);
         const int start = pick4(s, 0, p.seg_end[0], p.seg_end[1], p.seg_end[2]);
         b = pick4(s, p.seg_b[0], p.seg_b[1], p.seg_b[2], p.seg_b[3]);
@@ -1664,8 +1671,8 @@ int launch3s(const GemmArgs& a0, int splits, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-template <bool AK, bool BKM>
-int launch256(const GemmArgs& a0, int splits, hipStream_t st, int grid = 0) {
+template <bool AK, bool BKM, int SEG>
+int launch256_seg(const GemmArgs& a0, int splits, hipStream_t st, int grid) {
   GemmArgs a = a0;
   a.tiles_m = (a.M + 255) / 256;
   a.tiles_n = (a.N + 255) / 256;
@@ -1678,12 +1685,19 @@ int launch256(const GemmArgs& a0, int splits, hipStream_t st, int grid = 0) {
   const int smem = kLoop > kEpi ? kLoop : kEpi;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKM>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)gemm256_kernel<AK, BKM, SEG>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               smem);
     attr_set = true;
   }
-  hipLaunchKernelGGL((gemm256_kernel<AK, BKM>), dim3(grid, splits), dim3(kThreads), smem, st, a);
+  hipLaunchKernelGGL((gemm256_kernel<AK, BKM, SEG>), dim3(grid, splits), dim3(kThreads), smem, st, a);
   return (int)hipGetLastError();
+}
+
+template <bool AK, bool BKM>
+int launch256(const GemmArgs& a0, int splits, hipStream_t st, int grid = 0, int seg = 0) {
+  if (seg == 1) return launch256_seg<AK, BKM, 1>(a0, splits, st, grid);
+  if (seg == 2) return launch256_seg<AK, BKM, 2>(a0, splits, st, grid);
+  return launch256_seg<AK, BKM, 0>(a0, splits, st, grid);
 }
 
 template <int BN, bool AK, bool BKM>
@@ -2007,10 +2021,11 @@ PA_EXPORT int pa_gemm_bf16_pp_segs(const int64_t* seg, int nseg, int seg_k, cons
   g.tail_ws = (float*)ws;
   const int grid = split ? full + (T - full) * split : T;
   int rc;
-  if (a_kmajor && !b_kmajor) rc = launch256<true, false>(g, 1, st, grid);
-  else if (a_kmajor && b_kmajor) rc = launch256<true, true>(g, 1, st, grid);
-  else if (!a_kmajor && !b_kmajor) rc = launch256<false, false>(g, 1, st, grid);
-  else rc = launch256<false, true>(g, 1, st, grid);
+  const int sg = nseg > 1 ? (seg_k ? 1 : 2) : 0;
+  if (a_kmajor && !b_kmajor) rc = launch256<true, false>(g, 1, st, grid, sg);
+  else if (a_kmajor && b_kmajor) rc = launch256<true, true>(g, 1, st, grid, sg);
+  else if (!a_kmajor && !b_kmajor) rc = launch256<false, false>(g, 1, st, grid, sg);
+  else rc = launch256<false, true>(g, 1, st, grid, sg);
   if (rc || !split) return rc;
   hipLaunchKernelGGL(gemm_tail_reduce_k, dim3(T - full, 64), dim3(256), 0, st, g);
   return (int)hipGetLastError();

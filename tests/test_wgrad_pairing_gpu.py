@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
                                             (768, 1280, 256, 448, torch.float32),
                                             (5120, 5120, 4096, 4096, torch.bfloat16)])
 def test_gemm_seg_matches_fp32(M, N, K1, K2, out_dt):
-    assert L.has("pa_gemm_bf16_pp_seg")
+    assert L.has("pa_gemm_bf16_pp_segs")
     torch.manual_seed(0)
     xa = torch.randn(K1, M, device="cuda", dtype=torch.bfloat16)
     xb = torch.randn(K2, M, device="cuda", dtype=torch.bfloat16)
