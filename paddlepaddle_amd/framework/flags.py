@@ -22,6 +22,7 @@ _FLAGS = {
     "FLAGS_eager_backward_engine": "native",  # native (csrc/autograd/autograd_exec.cpp RunBackward) | torch
     "FLAGS_weight_only_dequant_cache_mb": 4096,  # weight-only / LLM.int8: bf16 images of quantized weights kept
                                                  # for the bf16 GEMM path (0 = dequantise per call)
+    "FLAGS_fused_grad_accumulation": True,  # fleet pipeline engine: dW GEMMs / norm kernels add into .grad
     "FLAGS_static_native_executor": "auto",  # static training programs on the native executor (_C_train):
                                              # auto (GPU) | force (also CPU, ATen instructions only) | off
     "FLAGS_gemm_backend": "auto",         # per-shape GEMM / conv backend: auto (timed) | hip | blas

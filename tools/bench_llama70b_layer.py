@@ -32,7 +32,13 @@ def main():
     x.stop_gradient = False
     gy = paddle.Tensor(torch.randn(B, S, h, device="cuda", dtype=torch.bfloat16))
 
+    params = [p._t for p in layer.parameters()]
+
     def step():
+        # fresh gradients each step (a training step's optimizer consumes them): autograd hands the new gradient
+        # over instead of accumulating into the previous step's (no bf16 grad += kernels in the profile)
+        for t in params + [x._t]:
+            t.grad = None
         y = layer(x)
         y.backward(gy)
 
