@@ -338,7 +338,12 @@ def llama_bench(args, paddle, world, dist_on):
         mbs = [(paddle.Tensor(c), paddle.Tensor(d)) for c, d in zip(x._t.chunk(args.accum), y._t.chunk(args.accum))]
         crit = model._layers._loss_fn if hasattr(model, "_layers") else model._loss_fn
 
+        from paddlepaddle_amd.ops.linear import fuse_grad_accumulation
+        fused = {"params": None}
+
         def step():
+            # wgrad GEMMs / norm kernels accumulate the micro-batches' weight gradients into .grad in place
+            fused["params"] = fuse_grad_accumulation(model, fused["params"])
             for xi, yi in mbs:
                 loss = crit(model(xi), yi) * (1.0 / args.accum)
                 loss.backward()

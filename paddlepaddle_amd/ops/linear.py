@@ -162,6 +162,47 @@ def register_main_grad(weight, buffer, on_ready):
     _MAIN_GRAD[id(weight)] = (weakref.ref(weight), buffer, on_ready)
 
 
+_FUSE_TYPES = ("Linear", "ColumnParallelLinear", "RowParallelLinear", "LlamaRMSNorm", "RMSNorm", "LayerNorm",
+               "FusedLinear")
+
+
+def fuse_grad_accumulation(layer, params=None):
+    """Fused gradient accumulation (reference: fused_linear_param_grad_add_kernel.cu:146 / PaddleNLP main_grad):
+    the .grad buffer of every linear / norm parameter of ``layer`` is registered as its main-grad, so each
+    backward's weight-gradient GEMM adds into it in its epilogue (and the norm backward kernels add their column
+    sums) instead of autograd allocating a fresh dW and adding it into .grad with a separate pass. Parameters used
+    by more than one layer (tied weights) or owned by other layer types keep autograd accumulation. Call once per
+    step before the backwards (cheap: re-registers only buffers an optimizer replaced); pass the returned list back
+    as ``params``. The optimizer must clear gradients with set_to_zero=True (the default). Disabled by
+    FLAGS_fused_grad_accumulation=0."""
+    from ..framework.flags import flag
+    if not flag("FLAGS_fused_grad_accumulation", True):
+        return params or []
+    if params is None:
+        owners = {}
+        for sub in layer.sublayers(include_self=True):
+            for name, p in sub.named_parameters(include_sublayers=False):
+                owners.setdefault(id(p), []).append((type(sub).__name__, name, p))
+        params = []
+        for lst in owners.values():
+            tname, name, p = lst[0]
+            if (len(lst) == 1 and tname in _FUSE_TYPES and name in ("weight", "bias") and not p.stop_gradient
+                    and p._t.is_cuda and p._t.dim() in (1, 2) and p._t.dtype in (torch.bfloat16, torch.float16)):
+                params.append(p)
+
+    def ready(w):
+        for h in (getattr(w, "_post_accumulate_grad_hooks", None) or {}).values():
+            h(w)
+    for p in params:
+        t = p._t
+        if t.grad is None:
+            t.grad = torch.zeros_like(t)
+        ent = _main_grad_of(t)
+        if ent is None or ent[1].data_ptr() != t.grad.data_ptr():
+            register_main_grad(t, t.grad, ready)
+    return params
+
+
 def unregister_main_grad(weight):
     _MAIN_GRAD.pop(id(weight), None)
 

@@ -273,43 +273,9 @@ class PipelineParallel(nn.Layer):
             dist.broadcast(loss, self.group.ranks[-1], group=self.group.process_group)
         return _wrap(loss)
 
-    # Fused gradient accumulation (reference: fused_linear_param_grad_add_kernel.cu:146 / PaddleNLP main_grad): the
-    # gradient buffer of every linear / norm parameter is registered with ops.linear, so each micro-batch's weight
-    # gradient GEMM adds into it in its epilogue (and the norm backward kernels add their column sums) instead of
-    # autograd allocating a fresh dW and adding it into .grad with a separate bf16 pass. Parameters used by more
-    # than one layer (tied weights) or owned by other layer types keep autograd accumulation.
-    _FUSE_TYPES = ("Linear", "ColumnParallelLinear", "RowParallelLinear", "LlamaRMSNorm", "RMSNorm", "LayerNorm",
-                   "FusedLinear")
-
     def _fuse_grad_accumulation(self):
-        from ..framework.flags import flag
-        if not flag("FLAGS_fused_grad_accumulation", True):
-            return
-        from ..ops.linear import register_main_grad, _main_grad_of
-        regs = getattr(self, "_mg_params", None)
-        if regs is None:
-            owners = {}
-            for layer in self._layers.sublayers(include_self=True):
-                for name, p in layer.named_parameters(include_sublayers=False):
-                    owners.setdefault(id(p), []).append((type(layer).__name__, name, p))
-            regs = []
-            for lst in owners.values():
-                tname, name, p = lst[0]
-                if (len(lst) == 1 and tname in self._FUSE_TYPES and name in ("weight", "bias") and not p.stop_gradient
-                        and p._t.is_cuda and p._t.dim() in (1, 2) and p._t.dtype in (torch.bfloat16, torch.float16)):
-                    regs.append(p)
-            self._mg_params = regs
-
-        def ready(w):
-            for h in (getattr(w, "_post_accumulate_grad_hooks", None) or {}).values():
-                h(w)
-        for p in regs:
-            t = p._t
-            if t.grad is None:
-                t.grad = torch.zeros_like(t)
-            ent = _main_grad_of(t)
-            if ent is None or ent[1].data_ptr() != t.grad.data_ptr():
-                register_main_grad(t, t.grad, ready)
+        from ..ops.linear import fuse_grad_accumulation
+        self._mg_params = fuse_grad_accumulation(self._layers, getattr(self, "_mg_params", None))
 
     def train_batch(self, data, optimizer, lr_scheduler=None, scaler=None):
         self._layers.train()
