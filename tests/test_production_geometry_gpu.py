@@ -229,7 +229,7 @@ def test_llama2_decoder_layer_bf16_hip_vs_fp32(size):
     L.reset_calls()
     y, dx, gh = _gpt_layer_run(layer, x, gy, torch.bfloat16)
     torch.cuda.synchronize()
-    for k in ("pa_rms_norm_fwd", "pa_rms_norm_bwd", "pa_rope_fwd", "pa_swiglu_fwd", "pa_swiglu_bwd",
+    for k in ("pa_rms_norm_fwd", "pa_rms_norm_bwd", "pa_rope", "pa_swiglu_fwd", "pa_swiglu_bwd",
               "pa_flash_attn_fwd", "pa_flash_attn_bwd"):
         assert any(n.startswith(k) for n, v in L.CALLS.items() if v), (k, dict(L.CALLS))
     # the per-shape GEMM chooser may hand some shapes to hipBLASLt once earlier tests have timed them
