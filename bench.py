@@ -270,6 +270,7 @@ def llama_static_bench(args, paddle, world, dist_on):
     strategy.pipeline.accumulate_steps = args.accum
     strategy.pipeline.micro_batch_size = args.micro_batch
     strategy.recompute.enable = bool(args.recompute)  # each decoder layer a checkpointed segment of the program
+    strategy.mp_optimization["allreduce_matmul_grad_overlapping"] = True  # TP dX all-reduce beside the dW GEMM
     sp = args.static_passes.split(",") if args.static_passes not in ("all", "none") else []
     if args.static_passes != "all":  # A/B of the engine's program passes
         strategy.fused_passes["sibling_linears"] = "sibling_linears" in sp

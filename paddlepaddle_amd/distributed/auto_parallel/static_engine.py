@@ -254,6 +254,21 @@ class _LNode:
         self.fn, self.args, self.kwargs, self.outs, self.name, self.rc = fn, args, kwargs, outs, name, rc
 
 
+class _HookT:
+    """Template of a column-parallel linear's dX hook: the all-reduce over mesh dim ``d`` of the stage, issued
+    asynchronously after the dX GEMM so it overlaps the weight-gradient GEMM (ops/linear.py _mm_grads)."""
+    __slots__ = ("d",)
+
+    def __init__(self, d):
+        self.d = d
+
+
+def _dx_allreduce_hook(pg):
+    def hook(dx):
+        return dist.all_reduce(dx, group=pg, async_op=True).wait
+    return hook
+
+
 class _Seg:
     """A recompute segment of a stage's local program: its nodes run under a non-reentrant checkpoint, so only
     ``inputs`` are kept for backward and the segment is re-run (collectives included, in the same order on every
@@ -296,8 +311,6 @@ class StaticEngine:
             unsupported.append("recompute.refined_ops_patterns (selective recompute)")
         if strategy.sp_optimization.get("enable", False):
             unsupported.append("sp_optimization")
-        if strategy.mp_optimization.get("allreduce_matmul_grad_overlapping", False):
-            unsupported.append("mp_optimization.allreduce_matmul_grad_overlapping")
         if strategy.gradient_merge.get("enable", False):
             unsupported.append("gradient_merge (use strategy.pipeline.accumulate_steps)")
         if unsupported:
@@ -376,9 +389,46 @@ class StaticEngine:
         self.loss_slot = prog._slot_of[id(loss._t)]
         self._apply_passes()
         self._propagate_and_partition()
+        if self.strategy.mp_optimization.get("allreduce_matmul_grad_overlapping", False):
+            self._overlap_tp_dx_allreduce()
         self._build_segments()
         self._localize_params()
         self.built = True
+
+    def _overlap_tp_dx_allreduce(self):
+        """strategy.mp_optimization.allreduce_matmul_grad_overlapping (reference:
+        distributed/passes/allreduce_matmul_grad_overlapping.py): a copy_to_parallel whose only reader is a
+        fused_linear's input is folded into that linear as its dX hook — the tensor-parallel all-reduce of dX starts
+        right after the dX GEMM, on RCCL, while the dW GEMM runs, instead of after the whole linear backward."""
+        self.tp_overlapped = 0
+        for s, nodes in enumerate(self.stage_nodes):
+            readers = {}
+            for k, nd in enumerate(nodes):
+                for r in _flat_tensor_refs((nd.args, nd.kwargs), []):
+                    readers.setdefault(r.i, []).append(k)
+            sent = set(self.sends[s]) | {self.loss_slot}
+            drop = set()
+            for k, nd in enumerate(nodes):
+                if nd.name != "copy_to_parallel" or not isinstance(nd.outs, P._Ref):
+                    continue
+                out = nd.outs.i
+                rd = readers.get(out, [])
+                if out in sent or len(rd) != 1:
+                    continue
+                c = nodes[rd[0]]
+                if _short(c.name) != "fused_linear" or not c.args or not isinstance(c.args[0], P._Ref) or \
+                        c.args[0].i != out or len(c.args) > 4 or "dx_hook" in c.kwargs:
+                    continue
+                if any(r.i == out for r in _flat_tensor_refs((c.args[1:], c.kwargs), [])):
+                    continue
+                c.args = (nd.args[0],) + tuple(c.args[1:])
+                kw = dict(c.kwargs)
+                kw["dx_hook"] = _HookT(nd.args[1][2])
+                c.kwargs = kw
+                drop.add(k)
+                self.tp_overlapped += 1
+            if drop:
+                self.stage_nodes[s] = [nd for k, nd in enumerate(nodes) if k not in drop]
 
     def _recompute_hooks(self, prog):
         """strategy.recompute: every block of the model's LayerLists (the repeated decoder layers) becomes a
@@ -1055,6 +1105,9 @@ class StaticEngine:
             return t
         if tmpl is P._RUN_DEV:
             return self.dev
+        if isinstance(tmpl, _HookT):
+            pg = self.groups.get(self.my_stage, tmpl.d)[0]
+            return _dx_allreduce_hook(pg) if pg is not None else None
         if isinstance(tmpl, list):
             return [self._materialize(v, env) for v in tmpl]
         if isinstance(tmpl, tuple):

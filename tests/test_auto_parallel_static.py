@@ -27,7 +27,7 @@ def _cfg():
     return LlamaConfig.tiny(num_hidden_layers=4, num_attention_heads=4, num_key_value_heads=2, **_FUSED)
 
 
-def _worker(rank, world, port, shape, acc, schedule, q, recompute=False):
+def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap=False):
     paddle = _setup(rank, world, port)
     import paddlepaddle_amd.distributed as dist
     from paddlepaddle_amd.models.llama_auto import LlamaForCausalLMAuto, LlamaPretrainingCriterionAuto
@@ -43,6 +43,7 @@ def _worker(rank, world, port, shape, acc, schedule, q, recompute=False):
     strategy.pipeline.accumulate_steps = acc
     strategy.pipeline.schedule_mode = schedule
     strategy.recompute.enable = recompute
+    strategy.mp_optimization["allreduce_matmul_grad_overlapping"] = overlap
     dm = dist.to_static(model, None, crit, opt, strategy)
     assert dm._engine is not None
     ids = _data()
@@ -59,6 +60,8 @@ def _worker(rank, world, port, shape, acc, schedule, q, recompute=False):
         assert ep.meta_exchanges == len(ep.sent_meta) and ep.messages == STEPS * acc * len(ep.sent_meta), (
             ep.meta_exchanges, len(ep.sent_meta), ep.messages)
         assert ep.ordered and ep.headers == STEPS * len(ep.sent_meta), ep.headers  # one header per class per run
+    if overlap:  # the column-parallel linears' dX all-reduces became overlapped hooks (2 per layer)
+        assert eng.tp_overlapped >= 2 * cfg.num_hidden_layers // pp, eng.tp_overlapped  # + the LM head
     if _FUSED:
         names = [n.name.split(":")[-1] for nodes in eng.stage_nodes for n in nodes]
         assert names.count("qkv_rope_attention") == cfg.num_hidden_layers, names  # all stages
@@ -81,7 +84,7 @@ def _fused_cfg(mp):
 
 def _worker_fused(rank, world, port, shape, acc, schedule, q):
     _FUSED.update(_fused_cfg(shape[2]))
-    _worker(rank, world, port, shape, acc, schedule, q)
+    _worker(rank, world, port, shape, acc, schedule, q, overlap=shape[0] == 1)
 
 
 LLAMA_PLAN = {
@@ -218,8 +221,7 @@ def test_static_engine_rejects_unimplemented_strategy_fields():
     cfg = _cfg()
     model = LlamaForCausalLMAuto(cfg)
     opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters())
-    for field, key in (("sp_optimization", "enable"), ("gradient_merge", "enable"),
-                       ("mp_optimization", "allreduce_matmul_grad_overlapping")):
+    for field, key in (("sp_optimization", "enable"), ("gradient_merge", "enable")):
         st = dist.Strategy()
         getattr(st, field)[key] = True
         with pytest.raises(NotImplementedError, match=field):
