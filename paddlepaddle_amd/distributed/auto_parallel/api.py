@@ -194,9 +194,18 @@ def shard_layer(layer, process_mesh, shard_fn=None, input_fn=None, output_fn=Non
 
 
 class _ShardingStageBase:
-    def __init__(self, mesh=None, sharding_mesh_dim=0):
+    """Reference signature: ShardingStageN(sharding_mesh_dim, mesh=None) (auto_parallel/api.py:1382); the mesh dim may
+    be a name ("dp") or an index. A ProcessMesh given first (the earlier form of this API) is still accepted."""
+
+    def __init__(self, sharding_mesh_dim=None, mesh=None):
+        from .process_mesh import ProcessMesh
+        if isinstance(sharding_mesh_dim, ProcessMesh):
+            sharding_mesh_dim, mesh = (mesh if isinstance(mesh, (int, str)) else 0), sharding_mesh_dim
         self._mesh = mesh or get_mesh()
-        self._dim = sharding_mesh_dim
+        d = 0 if sharding_mesh_dim is None else sharding_mesh_dim
+        if isinstance(d, str) and self._mesh is not None:
+            d = list(self._mesh.dim_names or []).index(d)
+        self._dim = d
 
 
 class ShardingStage1(_ShardingStageBase):

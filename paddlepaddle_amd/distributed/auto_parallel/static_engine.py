@@ -284,18 +284,24 @@ class StaticEngine:
         # a dist.shard_optimizer wrapper: the engine updates its local parameter shards with the inner optimizer;
         # ZeRO partitioning of that state over a data-parallel mesh dim is not implemented here, so it must not be
         # requested silently (degree 1 is the plain update)
+        # ZeRO over a data-parallel mesh dim (dist.shard_optimizer ShardingStage1/2, or strategy.sharding):
+        # gradients reduce-scattered, the optimizer updating only this rank's shard, parameters all-gathered
+        # (_zero_setup / _zero_step). Stage 3 (parameters sharded between steps) is not implemented here.
         shard_fn = getattr(optimizer, "_shard_fn", None)
         inner = getattr(optimizer, "_inner_opt", optimizer)
+        self.zero_dim = None
         if shard_fn is not None and getattr(shard_fn, "_mesh", None) is not None:
             m, d = shard_fn._mesh, shard_fn._dim
             size = m.get_dim_size(m.dim_names[d]) if isinstance(d, int) else m.get_dim_size(d)
-            if size > 1 or strategy.sharding.get("enable", False) and int(strategy.sharding.get("degree", 1)) > 1:
-                raise NotImplementedError(
-                    f"static auto-parallel engine: {type(shard_fn).__name__} over a mesh dim of size {size} "
-                    "(optimizer-state sharding) is not implemented; use the dygraph DistModel path or dp_config "
-                    "sharding_level 0")
+            if size > 1:
+                if type(shard_fn).__name__ == "ShardingStage3":
+                    raise NotImplementedError("static auto-parallel engine: ShardingStage3 (parameter sharding); "
+                                              "use ShardingStage1 / ShardingStage2 or the dygraph DistModel path")
+                self.zero_dim = m.dim_names[d] if isinstance(d, int) else d
         elif strategy.sharding.get("enable", False) and int(strategy.sharding.get("degree", 1)) > 1:
-            raise NotImplementedError("static auto-parallel engine: strategy.sharding with degree > 1")
+            if int(strategy.sharding.get("stage", 1)) >= 3:
+                raise NotImplementedError("static auto-parallel engine: strategy.sharding stage 3")
+            self.zero_dim = "dp"
         optimizer = inner
         self.layer, self.loss_fn, self.opt, self.strategy = layer, loss_fn, optimizer, strategy
         pp = strategy.pipeline
@@ -393,6 +399,9 @@ class StaticEngine:
             self._overlap_tp_dx_allreduce()
         self._build_segments()
         self._localize_params()
+        if self._zero_d is not None:
+            self._zero_check_partition()
+            self._zero_setup()
         self.built = True
 
     def _overlap_tp_dx_allreduce(self):
@@ -579,6 +588,15 @@ class StaticEngine:
         self.local_alias = [dict() for _ in range(nstage)]     # (slot, pl) -> converted local slot
         self._next = len(prog._metas) + 1
         self._cur_rc = None
+        self._param_slot_set = set(self.param_slots.values())
+        names = list(self.meshes[0].dim_names or [])
+        self._zero_d = None
+        if self.zero_dim is not None:
+            if self.zero_dim not in names:
+                raise ValueError(f"static auto-parallel engine: sharding mesh dim {self.zero_dim!r} not in {names}")
+            self._zero_d = names.index(self.zero_dim)
+            if self.meshes[0].shape[self._zero_d] == 1:
+                self._zero_d = None
         for s in self.feed_slots:
             self.slot_stage[s] = None  # available everywhere
         for s in self.param_slots.values():
@@ -654,6 +672,12 @@ class StaticEngine:
         return cur
 
     def _copy_to_parallel(self, stage, slot, dims):
+        if self._zero_d is not None and slot in self._param_slot_set:
+            # ZeRO: a parameter's data-parallel gradient is not all-reduced per micro-batch; the local gradients
+            # accumulate and are reduce-scattered once per step (_zero_step)
+            dims = [d for d in dims if d != self._zero_d]
+            if not dims:
+                return slot
         key = (slot, ("ctp",) + tuple(dims))
         al = self.local_alias[stage]
         if key in al:
@@ -1034,6 +1058,123 @@ class StaticEngine:
         if clip is not None and hasattr(clip, "_extra_sq_norm_fn"):
             clip._param_sq_fn = self._param_sq
 
+    # ------------------------------------------------------------------ ZeRO (stage 1 / 2) over the dp mesh dim
+    def _zero_setup(self):
+        """Flat parameter / gradient buffers per (dtype, tensor-parallel placement) group; every local parameter
+        becomes a view of its group's flat buffer and its .grad a view of the flat gradient (autograd accumulates
+        into it in place). The optimizer is rebound to one shard Parameter per group: this rank's 1/D of the flat
+        buffer, so its moments / master weights exist for the shard only."""
+        from ...framework.tensor import Parameter
+        opt = self.opt
+        if getattr(opt, "_apply_decay_param_fun", None) is not None:
+            raise NotImplementedError("static engine ZeRO: apply_decay_param_fun (per-parameter decay)")
+        gr = self.groups.get(self.my_stage, self._zero_d)
+        self._zero_pg = gr[0]
+        D = _nranks(gr)
+        r = gr[1].index(self.rank) if gr[1] else 0
+        groups = {}
+        for slot, p in self.local_params.items():
+            t = p._t
+            if not t.requires_grad or t.numel() == 0:
+                continue
+            if p.optimize_attr.get("learning_rate", 1.0) != 1.0 or p.regularizer is not None or not p.need_clip:
+                raise NotImplementedError("static engine ZeRO: per-parameter lr / regularizer / need_clip")
+            pl = tuple(self.info[slot].pl)
+            groups.setdefault((t.dtype, pl), []).append((slot, p))
+        self._zero = []
+        shard_params = []
+        for (dt, pl), items in groups.items():
+            dev = items[0][1]._t.device
+            n = sum(p._t.numel() for _, p in items)
+            C = -(-n // D)
+            flat = torch.zeros(C * D, dtype=dt, device=dev)
+            gflat = torch.zeros(C * D, dtype=dt, device=dev)
+            o = 0
+            for slot, p in items:
+                t = p._t
+                k = t.numel()
+                flat[o:o + k].copy_(t.detach().reshape(-1))
+                v = flat[o:o + k].view(t.shape).requires_grad_(True)
+                from ...framework.tensor import _PARAM_OF
+                _PARAM_OF.pop(id(t), None)
+                _PARAM_OF[id(v)] = p
+                p._t = v
+                v.grad = gflat[o:o + k].view(t.shape)
+                o += k
+            sp = Parameter(flat[r * C:(r + 1) * C], name=f"zero_shard_{len(self._zero)}")
+            sp._t = flat[r * C:(r + 1) * C]  # a view into the flat buffer: the update lands in the parameters
+            sp._t.requires_grad_(True)
+            self._zero.append({"flat": flat, "gflat": gflat, "C": C, "shard": sp, "pl": pl,
+                               "sgrad": torch.empty(C, dtype=dt, device=dev)})
+            shard_params.append(sp)
+        opt._param_groups = [{"params": shard_params}]
+        opt._parameter_list = shard_params
+        clip = getattr(opt, "_grad_clip", None)
+        if clip is not None and hasattr(clip, "_extra_sq_norm_fn"):
+            clip._param_sq_fn = self._zero_param_sq
+
+    def _zero_check_partition(self):
+        """ZeRO reduce-scatters the parameters' local dp gradients itself: no data-parallel all-reduce of a
+        parameter (or of a conversion of one) may remain in a stage program, or it would be reduced twice."""
+        for nodes in self.stage_nodes:
+            producer = {}
+            for nd in nodes:
+                if isinstance(nd.outs, P._Ref):
+                    producer[nd.outs.i] = nd
+            for nd in nodes:
+                if nd.name != "copy_to_parallel" or nd.args[1][2] != self._zero_d:
+                    continue
+                src = nd.args[0].i
+                seen = 0
+                while src not in self._param_slot_set and src in producer and seen < 16:
+                    q = producer[src]
+                    if q.name not in ("allgather", "slice", "alias", "to_partial", "allreduce", "copy_to_parallel"):
+                        break
+                    src = q.args[0].i
+                    seen += 1
+                if src in self._param_slot_set:
+                    raise NotImplementedError("static engine ZeRO: a parameter reaches a data-parallel computation "
+                                              "through a placement conversion; use strategy.sharding off here")
+
+    def _zero_param_sq(self, params):
+        """Grad-norm^2 of the shards: each group's shard sum of squares, summed over the dp ranks (the shards
+        partition the flat gradient), over the tensor-parallel dims the group is sharded on, and over stages."""
+        tot = None
+        for z in self._zero:
+            g = z["shard"]._t.grad
+            if g is None:
+                continue
+            sq = g.float().pow(2).sum().reshape(1)
+            if self._zero_pg is not None:
+                dist.all_reduce(sq, group=self._zero_pg)
+            for d, pls in enumerate(z["pl"]):
+                if _is_s(pls) and d != self._zero_d:
+                    g2 = self.groups.get(self.my_stage, d)
+                    if g2[0] is not None:
+                        dist.all_reduce(sq, group=g2[0])
+            tot = sq if tot is None else tot + sq
+        if tot is None:
+            tot = torch.zeros(1, dtype=torch.float32, device=self.dev)
+        if len(self.meshes) > 1 and dist.is_initialized():
+            dist.all_reduce(tot, group=self._pp_group())
+        return tot[0]
+
+    def _zero_step(self):
+        """Reduce-scatter the accumulated flat gradients over dp, update the shards, all-gather the parameters."""
+        for z in self._zero:
+            if self._zero_pg is not None:
+                dist.reduce_scatter_tensor(z["sgrad"], z["gflat"], group=self._zero_pg)
+            else:
+                z["sgrad"].copy_(z["gflat"])
+            z["shard"]._t.grad = z["sgrad"]
+        self.opt.step()
+        with torch.no_grad():
+            for z in self._zero:
+                if self._zero_pg is not None:
+                    dist.all_gather_into_tensor(z["flat"], z["shard"]._t.detach(), group=self._zero_pg)
+                z["gflat"].zero_()
+                z["shard"]._t.grad = None
+
     def _param_sq(self, params):
         """Global grad-norm^2: sharded params summed over their mesh dims, replicated ones counted once,
         stages summed over the pipeline."""
@@ -1214,8 +1355,11 @@ class StaticEngine:
         if nst > 1:  # every rank reports the loss of the last stage
             loss = loss.clone()
             dist.all_reduce(loss, group=self._pp_group())
-        self.opt.step()
-        self.opt.clear_grad()
+        if getattr(self, "_zero", None):
+            self._zero_step()
+        else:
+            self.opt.step()
+            self.opt.clear_grad()
         from .. import collective_check as _cc
         if _cc.enabled():
             _cc.check_collectives("static engine step")

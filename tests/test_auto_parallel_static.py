@@ -27,7 +27,7 @@ def _cfg():
     return LlamaConfig.tiny(num_hidden_layers=4, num_attention_heads=4, num_key_value_heads=2, **_FUSED)
 
 
-def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap=False):
+def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap=False, zero=False):
     paddle = _setup(rank, world, port)
     import paddlepaddle_amd.distributed as dist
     from paddlepaddle_amd.models.llama_auto import LlamaForCausalLMAuto, LlamaPretrainingCriterionAuto
@@ -44,6 +44,10 @@ def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap
     strategy.pipeline.schedule_mode = schedule
     strategy.recompute.enable = recompute
     strategy.mp_optimization["allreduce_matmul_grad_overlapping"] = overlap
+    if zero:
+        strategy.sharding["enable"] = True
+        strategy.sharding["degree"] = dp
+        strategy.sharding["stage"] = 1
     dm = dist.to_static(model, None, crit, opt, strategy)
     assert dm._engine is not None
     ids = _data()
@@ -60,6 +64,11 @@ def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap
         assert ep.meta_exchanges == len(ep.sent_meta) and ep.messages == STEPS * acc * len(ep.sent_meta), (
             ep.meta_exchanges, len(ep.sent_meta), ep.messages)
         assert ep.ordered and ep.headers == STEPS * len(ep.sent_meta), ep.headers  # one header per class per run
+    if zero:  # optimizer state exists for this rank's shards only
+        shards = eng.opt._parameter_list
+        assert shards and all(sp.name.startswith("zero_shard") for sp in shards)
+        assert sum(sp._t.numel() for sp in shards) * dp >= sum(p._t.numel() for p in eng.local_params.values()
+                                                                 if p._t.requires_grad)
     if overlap:  # the column-parallel linears' dX all-reduces became overlapped hooks (2 per layer)
         assert eng.tp_overlapped >= 2 * cfg.num_hidden_layers // pp, eng.tp_overlapped  # + the LM head
     if _FUSED:
@@ -78,6 +87,20 @@ def _worker_rc(rank, world, port, shape, acc, schedule, q):
     _worker(rank, world, port, shape, acc, schedule, q, recompute=True)
 
 
+def _worker_zero(rank, world, port, shape, acc, schedule, q):
+    _worker(rank, world, port, shape, acc, schedule, q, zero=True)
+
+
+@pytest.mark.parametrize("shape,acc", [((1, 2, 1), 2), ((1, 2, 2), 1), ((2, 2, 1), 2)])
+def test_static_engine_zero_sharding_matches_single_process(shape, acc):
+    """strategy.sharding (ZeRO-1 over "dp"): local gradients reduce-scattered once per step, the optimizer on this
+    rank's shard of the flat parameters, parameters all-gathered: same losses as single-process training."""
+    ref = _reference()
+    res = _spawn(_worker_zero, shape, acc, "1F1B", world=int(np.prod(shape)))
+    for rank, losses, kinds, stage in res:
+        np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-5, err_msg=f"rank {rank} stage {stage}")
+
+
 def _fused_cfg(mp):
     return {"fuse_attention_qkv": True, "fuse_attention_ffn": True, "tensor_parallel_degree": mp}
 
@@ -93,7 +116,7 @@ LLAMA_PLAN = {
     "layers.*.mlp.down_proj": "row", "lm_head": "col"}
 
 
-def _worker_parallelize(rank, world, port, shape, acc, q):
+def _worker_parallelize(rank, world, port, shape, acc, q, level=0):
     """Plain single-card LLaMA built without a mesh, then distributed by dist.parallelize plans."""
     paddle = _setup(rank, world, port)
     import paddlepaddle_amd.distributed as dist
@@ -106,12 +129,12 @@ def _worker_parallelize(rank, world, port, shape, acc, q):
     opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
     mesh = dist.ProcessMesh(np.arange(pp * dp * mp).reshape(pp, dp, mp), dim_names=["pp", "dp", "mp"])
     plan = {k: (dist.ColWiseParallel() if v == "col" else dist.RowWiseParallel()) for k, v in LLAMA_PLAN.items()}
-    model, opt = dist.parallelize(model, opt, mesh, dp_config={"sharding_level": 0},
+    model, opt = dist.parallelize(model, opt, mesh, dp_config={"sharding_level": level},
                                   mp_config={"parallelize_plan": plan}, pp_config={"split_spec": "layers"})
     strategy = dist.Strategy()
     strategy.pipeline.enable = pp > 1 or acc > 1
     strategy.pipeline.accumulate_steps = acc
-    strategy.fused_passes["sibling_linears"] = True  # opt-in pass (off by default), exercised here for parity
+    strategy.fused_passes["sibling_linears"] = level == 0  # opt-in pass (off by default), exercised here for parity
     dm = dist.to_static(model, None, crit, opt, strategy)
     assert dm._engine is not None
     ids = _data()
@@ -122,9 +145,12 @@ def _worker_parallelize(rank, world, port, shape, acc, q):
     # program passes on the traced model (static_engine._apply_passes): q / k / v and gate / up of every layer are
     # one multi_linear node, both RMSNorms of every layer carry the residual gradient
     L = cfg.num_hidden_layers
-    assert eng.pass_stats == {"rms_norm_residual": 2 * L, "sibling_linears": 5 * L}, eng.pass_stats
-    names = [n.name.split(":")[-1] for nodes in eng.stage_nodes for n in nodes]
-    assert names.count("multi_linear") == 2 * L and names.count("rms_norm_residual") == 2 * L, names
+    if level == 0:
+        assert eng.pass_stats == {"rms_norm_residual": 2 * L, "sibling_linears": 5 * L}, eng.pass_stats
+        names = [n.name.split(":")[-1] for nodes in eng.stage_nodes for n in nodes]
+        assert names.count("multi_linear") == 2 * L and names.count("rms_norm_residual") == 2 * L, names
+    else:  # dist.shard_optimizer(ShardingStage1) from dp_config: ZeRO on the engine
+        assert eng._zero and all(sp.name.startswith("zero_shard") for sp in eng.opt._parameter_list)
     q.put((rank, losses, kinds, eng.my_stage))
     paddle.distributed.barrier()
 
@@ -193,6 +219,18 @@ def test_static_engine_fused_qkv_ffn_llama_matches_single_process(shape, acc):
     for rank, losses, kinds, stage in res:
         np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-5, err_msg=f"rank {rank} stage {stage}")
         assert "allreduce" in kinds
+
+
+def _worker_parallelize_zero(rank, world, port, shape, acc, q):
+    _worker_parallelize(rank, world, port, shape, acc, q, level=1)
+
+
+def test_parallelize_sharding_level1_zero_matches_single_process():
+    """dp_config sharding_level 1 -> dist.shard_optimizer(ShardingStage1) -> ZeRO on the static engine."""
+    ref = _reference()
+    res = _spawn(_worker_parallelize_zero, (1, 2, 2), 2, world=4)
+    for rank, losses, kinds, stage in res:
+        np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-5, err_msg=f"rank {rank} stage {stage}")
 
 
 @pytest.mark.parametrize("shape,acc", [((1, 1, 2), 1), ((4, 1, 2), 4)])
