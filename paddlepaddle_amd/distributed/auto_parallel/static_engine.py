@@ -591,12 +591,15 @@ class StaticEngine:
         self._param_slot_set = set(self.param_slots.values())
         names = list(self.meshes[0].dim_names or [])
         self._zero_d = None
-        if self.zero_dim is not None:
-            if self.zero_dim not in names:
-                raise ValueError(f"static auto-parallel engine: sharding mesh dim {self.zero_dim!r} not in {names}")
-            self._zero_d = names.index(self.zero_dim)
-            if self.meshes[0].shape[self._zero_d] == 1:
-                self._zero_d = None
+        sync_dim = self.zero_dim if self.zero_dim is not None else ("dp" if "dp" in names else None)
+        if self.zero_dim is not None and self.zero_dim not in names:
+            raise ValueError(f"static auto-parallel engine: sharding mesh dim {self.zero_dim!r} not in {names}")
+        if sync_dim is not None and self.meshes[0].shape[names.index(sync_dim)] > 1:
+            # data-parallel gradients of parameters are synchronised once per step on flat buffers (ZeRO:
+            # reduce-scatter; otherwise one all-reduce per buffer) instead of one all-reduce per parameter per
+            # micro-batch inside autograd
+            self._zero_d = names.index(sync_dim)
+        self._zero_shard = self.zero_dim is not None
         for s in self.feed_slots:
             self.slot_stage[s] = None  # available everywhere
         for s in self.param_slots.values():
@@ -1066,7 +1069,8 @@ class StaticEngine:
         buffer, so its moments / master weights exist for the shard only."""
         from ...framework.tensor import Parameter
         opt = self.opt
-        if getattr(opt, "_apply_decay_param_fun", None) is not None:
+        shard = self._zero_shard
+        if shard and getattr(opt, "_apply_decay_param_fun", None) is not None:
             raise NotImplementedError("static engine ZeRO: apply_decay_param_fun (per-parameter decay)")
         gr = self.groups.get(self.my_stage, self._zero_d)
         self._zero_pg = gr[0]
@@ -1077,7 +1081,8 @@ class StaticEngine:
             t = p._t
             if not t.requires_grad or t.numel() == 0:
                 continue
-            if p.optimize_attr.get("learning_rate", 1.0) != 1.0 or p.regularizer is not None or not p.need_clip:
+            if shard and (p.optimize_attr.get("learning_rate", 1.0) != 1.0 or p.regularizer is not None
+                          or not p.need_clip):
                 raise NotImplementedError("static engine ZeRO: per-parameter lr / regularizer / need_clip")
             pl = tuple(self.info[slot].pl)
             groups.setdefault((t.dtype, pl), []).append((slot, p))
@@ -1101,12 +1106,17 @@ class StaticEngine:
                 p._t = v
                 v.grad = gflat[o:o + k].view(t.shape)
                 o += k
-            sp = Parameter(flat[r * C:(r + 1) * C], name=f"zero_shard_{len(self._zero)}")
-            sp._t = flat[r * C:(r + 1) * C]  # a view into the flat buffer: the update lands in the parameters
-            sp._t.requires_grad_(True)
-            self._zero.append({"flat": flat, "gflat": gflat, "C": C, "shard": sp, "pl": pl,
-                               "sgrad": torch.empty(C, dtype=dt, device=dev)})
-            shard_params.append(sp)
+            z = {"flat": flat, "gflat": gflat, "C": C, "pl": pl, "shard": None}
+            if shard:
+                sp = Parameter(flat[r * C:(r + 1) * C], name=f"zero_shard_{len(self._zero)}")
+                sp._t = flat[r * C:(r + 1) * C]  # a view into the flat buffer: the update lands in the parameters
+                sp._t.requires_grad_(True)
+                z["shard"] = sp
+                z["sgrad"] = torch.empty(C, dtype=dt, device=dev)
+                shard_params.append(sp)
+            self._zero.append(z)
+        if not shard:
+            return
         opt._param_groups = [{"params": shard_params}]
         opt._parameter_list = shard_params
         clip = getattr(opt, "_grad_clip", None)
@@ -1160,7 +1170,16 @@ class StaticEngine:
         return tot[0]
 
     def _zero_step(self):
-        """Reduce-scatter the accumulated flat gradients over dp, update the shards, all-gather the parameters."""
+        """Reduce-scatter the accumulated flat gradients over dp, update the shards, all-gather the parameters
+        (without ZeRO: all-reduce each flat gradient once and update the parameters as usual)."""
+        if not self._zero_shard:
+            for z in self._zero:
+                if self._zero_pg is not None:
+                    dist.all_reduce(z["gflat"], group=self._zero_pg)
+            self.opt.step()
+            for z in self._zero:
+                z["gflat"].zero_()
+            return
         for z in self._zero:
             if self._zero_pg is not None:
                 dist.reduce_scatter_tensor(z["sgrad"], z["gflat"], group=self._zero_pg)
