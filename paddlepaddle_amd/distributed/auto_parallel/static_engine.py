@@ -289,7 +289,7 @@ class StaticEngine:
         # (_zero_setup / _zero_step). Stage 3 (parameters sharded between steps) is not implemented here.
         shard_fn = getattr(optimizer, "_shard_fn", None)
         inner = getattr(optimizer, "_inner_opt", optimizer)
-        self.zero_dim = None
+        self.zero_dim, self.zero_stage = None, 1
         if shard_fn is not None and getattr(shard_fn, "_mesh", None) is not None:
             m, d = shard_fn._mesh, shard_fn._dim
             size = m.get_dim_size(m.dim_names[d]) if isinstance(d, int) else m.get_dim_size(d)
@@ -298,10 +298,11 @@ class StaticEngine:
                     raise NotImplementedError("static auto-parallel engine: ShardingStage3 (parameter sharding); "
                                               "use ShardingStage1 / ShardingStage2 or the dygraph DistModel path")
                 self.zero_dim = m.dim_names[d] if isinstance(d, int) else d
+                self.zero_stage = 2 if type(shard_fn).__name__ == "ShardingStage2" else 1
         elif strategy.sharding.get("enable", False) and int(strategy.sharding.get("degree", 1)) > 1:
             if int(strategy.sharding.get("stage", 1)) >= 3:
                 raise NotImplementedError("static auto-parallel engine: strategy.sharding stage 3")
-            self.zero_dim = "dp"
+            self.zero_dim, self.zero_stage = "dp", int(strategy.sharding.get("stage", 1))
         optimizer = inner
         self.layer, self.loss_fn, self.opt, self.strategy = layer, loss_fn, optimizer, strategy
         pp = strategy.pipeline
@@ -379,7 +380,10 @@ class StaticEngine:
             p._t = meta
         self.reshard_ann = {}
         prog._pa_reshard = self.reshard_ann
-        hooks = self._recompute_hooks(prog) if self.recompute else []
+        cps = list(self.strategy.recompute.get("checkpoints") or []) if self.recompute else []
+        cp_slots = []
+        hooks = (self._checkpoint_hooks(prog, cps, cp_slots) if cps else self._recompute_hooks(prog)) \
+            if self.recompute else []
         try:
             with P.trace_into(prog):
                 xs = [_wrap(prog._metas[s]) for s in self.feed_slots[:-1]]
@@ -393,9 +397,13 @@ class StaticEngine:
                 if id(p) in saved:
                     p._t = saved[id(p)]
         self.loss_slot = prog._slot_of[id(loss._t)]
+        if cps:
+            from ..passes import new_pass
+            ctx = new_pass("auto_parallel_recompute", {"checkpoints": cp_slots}).apply(prog, None)
+            self.pass_stats_rc = ctx.get_attr("auto_parallel_recompute.segments", 0)
         self._apply_passes()
         self._propagate_and_partition()
-        if self.strategy.mp_optimization.get("allreduce_matmul_grad_overlapping", False):
+        if getattr(self.prog, "_pa_tp_overlap", False):
             self._overlap_tp_dx_allreduce()
         self._build_segments()
         self._localize_params()
@@ -438,6 +446,23 @@ class StaticEngine:
                 self.tp_overlapped += 1
             if drop:
                 self.stage_nodes[s] = [nd for k, nd in enumerate(nodes) if k not in drop]
+
+    def _checkpoint_hooks(self, prog, names, slots):
+        """strategy.recompute.checkpoints: names of sublayers (``layer.named_sublayers``) whose outputs are the
+        checkpoints; the auto_parallel_recompute pass turns the ops between consecutive checkpoints into recompute
+        segments after tracing."""
+        subs = dict(self.layer.named_sublayers())
+        missing = [n for n in names if n not in subs]
+        if missing:
+            raise ValueError(f"strategy.recompute.checkpoints: no sublayer named {missing}")
+
+        def post(layer, inputs, out):
+            o = out[0] if isinstance(out, (tuple, list)) else out
+            t = getattr(o, "_t", o)
+            if prog._is_traced(t):
+                slots.append(prog._slot_of[id(t)])
+
+        return [subs[n].register_forward_post_hook(post) for n in names]
 
     def _recompute_hooks(self, prog):
         """strategy.recompute: every block of the model's LayerLists (the repeated decoder layers) becomes a
@@ -553,6 +578,11 @@ class StaticEngine:
                 if s in info else None})
             ctx = p.apply(self.prog, None)
             self.pass_stats["sibling_linears"] = ctx.get_attr("fuse_sibling_linears.fused", 0)
+        if self.strategy.mp_optimization.get("allreduce_matmul_grad_overlapping", False):
+            new_pass("allreduce_matmul_grad_overlapping").apply(self.prog, None)
+        if self.zero_dim is not None:
+            new_pass("auto_parallel_sharding", {"stage": self.zero_stage, "sharding_mesh_dim": self.zero_dim}).apply(
+                self.prog, None)
         amp = self.strategy.amp
         if amp.get("enable", False):
             ctx = new_pass("auto_parallel_amp", {"dtype": amp.get("dtype", "bfloat16")}).apply(self.prog, None)

@@ -13,6 +13,9 @@
   by re-running each op on meta tensors, the same way the program was traced.
 * ``auto_parallel_gradient_merge`` (reference auto_parallel_gradient_merge.py): the Executor accumulates
   gradients over ``k_steps`` runs and applies the optimizer on the last one (``avg`` scales by 1/k).
+* ``auto_parallel_recompute``: ops between consecutive checkpoints become recompute segments (node.rc), run
+  checkpointed by the static auto-parallel engine; ``allreduce_matmul_grad_overlapping`` /
+  ``auto_parallel_sharding`` mark the program for the engine's partition-time TP dX overlap and ZeRO-1/2.
 """
 from __future__ import annotations
 
@@ -22,7 +25,8 @@ from .pass_base import PassBase, PassType, register_pass
 from ...static import program as P
 
 __all__ = ["FuseGemmEpiloguePass", "DeadCodeEliminationPass", "AMPPass", "FP16Pass", "GradientMergePass",
-           "FuseSiblingLinearsPass", "FuseRMSNormResidualPass"]
+           "FuseSiblingLinearsPass", "FuseRMSNormResidualPass",
+           "RecomputePass", "AllreduceMatmulGradOverlappingPass", "ShardingPass"]
 
 _RELU = {"f:torch.nn.functional:relu", "f:torch:relu", "m:relu"}
 _GELU = {"o:paddlepaddle_amd.ops.activation:gelu", "f:torch.nn.functional:gelu"}
@@ -413,3 +417,74 @@ class FuseRMSNormResidualPass(PassBase):
                                          a.outs, a.kind, a.name), a)
             fused += 1
         context.set_attr("fuse_rms_norm_residual.fused", context.get_attr("fuse_rms_norm_residual.fused", 0) + fused)
+
+
+# ------------------------------------------------------------------------------------------------------------------
+@register_pass("auto_parallel_recompute")
+class RecomputePass(PassBase):
+    """Activation recompute by checkpoints (reference: distributed/passes/auto_parallel_recompute.py): the ops
+    between consecutive ``checkpoints`` (value slots, or names the program knows) become recompute segments — the
+    static auto-parallel engine runs each as a checkpointed region whose activations are rebuilt in backward
+    (``strategy.recompute``). Without checkpoints the segments traced from ``recompute`` scopes are kept.
+    ``no_recompute_segments``: segment indices to leave alone. Ops that already carry a segment keep it."""
+
+    def _type(self):
+        return PassType.CALC_OPT
+
+    def _apply_single_impl(self, prog, startup, context):
+        cps = self.get_attr("checkpoints") or []
+        skip = set(int(i) for i in (self.get_attr("no_recompute_segments") or []))
+        marks = set(c for c in cps if isinstance(c, int)) | _vars_to_slots(
+            prog, [c for c in cps if not isinstance(c, int)])
+        segs = 0
+        if marks:
+            base = next(prog._rc_ids) * 100000
+            seg, cur = 0, []
+            for n in prog.nodes:
+                if isinstance(n, (P.CFNode, P.GuardNode)):
+                    continue
+                if n.rc is None and seg not in skip:
+                    n.rc = base + seg
+                    cur.append(n)
+                if P._node_writes(n) & marks:
+                    segs += bool(cur)
+                    seg, cur = seg + 1, []
+            for n in cur:  # the ops after the last checkpoint (the loss) are not recomputed
+                n.rc = None
+        else:
+            segs = len(set(n.rc for n in prog.nodes if getattr(n, "rc", None) is not None))
+        prog._pa_recompute = True
+        context.set_attr("auto_parallel_recompute.segments", segs)
+
+
+@register_pass("allreduce_matmul_grad_overlapping")
+class AllreduceMatmulGradOverlappingPass(PassBase):
+    """Reference: distributed/passes/allreduce_matmul_grad_overlapping.py — the tensor-parallel all-reduce of a
+    column-parallel linear's input gradient overlaps its weight-gradient GEMM. The partitioned per-rank program
+    only exists inside the static engine, so the pass marks the program and the engine folds each
+    ``copy_to_parallel -> fused_linear`` pair into the linear's asynchronous dX hook at partition time
+    (static_engine._overlap_tp_dx_allreduce; also selected by strategy.mp_optimization)."""
+
+    def _type(self):
+        return PassType.COMM_OPT
+
+    def _apply_single_impl(self, prog, startup, context):
+        prog._pa_tp_overlap = True
+
+
+@register_pass("auto_parallel_sharding")
+class ShardingPass(PassBase):
+    """Reference: distributed/passes/auto_parallel_sharding.py — optimizer-state sharding over a data-parallel
+    mesh dim. ``stage`` 1 / 2 (3 is not implemented on the static engine) and ``sharding_mesh_dim`` (default "dp")
+    are recorded on the program; the engine flattens the parameters per placement group, reduce-scatters the
+    accumulated gradients once per step, updates this rank's shards and all-gathers (static_engine._zero_*)."""
+
+    def _type(self):
+        return PassType.PARALLEL_OPT
+
+    def _check_self(self):
+        return int(self.get_attr("stage", 1)) in (1, 2)
+
+    def _apply_single_impl(self, prog, startup, context):
+        prog._pa_sharding = {"stage": int(self.get_attr("stage", 1)),
+                             "dim": self.get_attr("sharding_mesh_dim", "dp")}

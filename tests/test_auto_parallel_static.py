@@ -27,7 +27,7 @@ def _cfg():
     return LlamaConfig.tiny(num_hidden_layers=4, num_attention_heads=4, num_key_value_heads=2, **_FUSED)
 
 
-def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap=False, zero=False):
+def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap=False, zero=False, checkpoints=None):
     paddle = _setup(rank, world, port)
     import paddlepaddle_amd.distributed as dist
     from paddlepaddle_amd.models.llama_auto import LlamaForCausalLMAuto, LlamaPretrainingCriterionAuto
@@ -43,6 +43,8 @@ def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap
     strategy.pipeline.accumulate_steps = acc
     strategy.pipeline.schedule_mode = schedule
     strategy.recompute.enable = recompute
+    if checkpoints:
+        strategy.recompute["checkpoints"] = checkpoints
     strategy.mp_optimization["allreduce_matmul_grad_overlapping"] = overlap
     if zero:
         strategy.sharding["enable"] = True
@@ -74,7 +76,12 @@ def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap
     if _FUSED:
         names = [n.name.split(":")[-1] for nodes in eng.stage_nodes for n in nodes]
         assert names.count("qkv_rope_attention") == cfg.num_hidden_layers, names  # all stages
-    if recompute:  # every decoder layer of this stage runs as one checkpointed segment
+    if checkpoints:  # ops between consecutive checkpoints (auto_parallel_recompute pass) are segments
+        from paddlepaddle_amd.distributed.auto_parallel.static_engine import _Seg
+        assert eng.pass_stats_rc == len(checkpoints), eng.pass_stats_rc
+        segs = [it for it in eng.stage_items[eng.my_stage] if isinstance(it, _Seg)]
+        assert segs, eng.stage_items[eng.my_stage]
+    elif recompute:  # every decoder layer of this stage runs as one checkpointed segment
         from paddlepaddle_amd.distributed.auto_parallel.static_engine import _Seg
         segs = [it for it in eng.stage_items[eng.my_stage] if isinstance(it, _Seg)]
         assert len(segs) == cfg.num_hidden_layers // pp, len(segs)
@@ -85,6 +92,10 @@ def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap
 
 def _worker_rc(rank, world, port, shape, acc, schedule, q):
     _worker(rank, world, port, shape, acc, schedule, q, recompute=True)
+
+
+def _worker_cp(rank, world, port, shape, acc, schedule, q):
+    _worker(rank, world, port, shape, acc, schedule, q, recompute=True, checkpoints=["layers.0", "layers.2"])
 
 
 def _worker_zero(rank, world, port, shape, acc, schedule, q):
@@ -201,6 +212,16 @@ def test_static_engine_recompute_matches_single_process(shape, acc, schedule):
     TP collectives included, rebuilt in backward); losses equal single-process training."""
     ref = _reference()
     res = _spawn(_worker_rc, shape, acc, schedule, world=int(np.prod(shape)))
+    for rank, losses, kinds, stage in res:
+        np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-5, err_msg=f"rank {rank} stage {stage}")
+
+
+@pytest.mark.parametrize("shape,acc", [((1, 1, 2), 1), ((2, 1, 2), 2)])
+def test_static_engine_recompute_checkpoints_pass(shape, acc):
+    """strategy.recompute.checkpoints (sublayer outputs) -> the registered auto_parallel_recompute pass marks the
+    ops between consecutive checkpoints as recompute segments; losses equal single-process training."""
+    ref = _reference()
+    res = _spawn(_worker_cp, shape, acc, "1F1B", world=int(np.prod(shape)))
     for rank, losses, kinds, stage in res:
         np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-5, err_msg=f"rank {rank} stage {stage}")
 

@@ -153,3 +153,30 @@ def test_fuse_sibling_linears_and_rms_norm_residual_passes():
     assert names0.count("fused_linear") == 3 and names.count("fused_linear") == 0
     assert names.count("multi_linear") == 1 and "rms_norm_residual" in names and "rms_norm" not in names
     np.testing.assert_allclose(got, ref, rtol=1e-6, atol=1e-6)
+
+
+def test_recompute_overlap_sharding_passes_mark_program(static_mode):
+    """auto_parallel_recompute: the ops up to each checkpoint form one recompute segment, the ops after the last
+    checkpoint none; no_recompute_segments leaves a segment out. allreduce_matmul_grad_overlapping /
+    auto_parallel_sharding mark the program for the static engine (which applies them at partition time)."""
+    main, st, x, y, z = _mlp()
+    h_slot = next(P._refs(n.outs, [])[0] for n in main.nodes if n.name.split(":")[-1] == "relu")
+    y_slot = main._slot_of[id(y._t)]
+    ctx = dp.new_pass("auto_parallel_recompute", {"checkpoints": [h_slot, y]}).apply([main], [st])
+    assert ctx.get_attr("auto_parallel_recompute.segments") == 2
+    order = [n for n in main.nodes if not isinstance(n, P.GuardNode)]
+    ends = [i for i, n in enumerate(order) if P._node_writes(n) & {h_slot, y_slot}]
+    rc = [n.rc for n in order]
+    assert len(set(rc[:ends[0] + 1])) == 1 and rc[0] is not None
+    assert len(set(rc[ends[0] + 1:ends[1] + 1])) == 1 and rc[ends[1]] not in (None, rc[0])
+    assert all(r is None for r in rc[ends[1] + 1:])  # mean(y) is not recomputed
+    m2, s2, x2, y2, _ = _mlp()
+    h2 = next(P._refs(n.outs, [])[0] for n in m2.nodes if n.name.split(":")[-1] == "relu")
+    dp.new_pass("auto_parallel_recompute", {"checkpoints": [h2, y2], "no_recompute_segments": [0]}).apply([m2], [s2])
+    o2 = [n for n in m2.nodes if not isinstance(n, P.GuardNode)]
+    assert o2[0].rc is None and any(n.rc is not None for n in o2)
+    dp.new_pass("allreduce_matmul_grad_overlapping").apply([main], [st])
+    assert dp.new_pass("auto_parallel_sharding", {"stage": 3}).apply([main], [st]) is not None
+    assert not hasattr(main, "_pa_sharding")  # stage 3 fails _check_self: not applied
+    dp.new_pass("auto_parallel_sharding", {"stage": 2, "sharding_mesh_dim": "dp"}).apply([main], [st])
+    assert main._pa_tp_overlap and main._pa_sharding == {"stage": 2, "dim": "dp"}
