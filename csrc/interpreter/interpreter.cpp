@@ -198,7 +198,12 @@ enum Op : int {
   kLayerNorm, kBatchNorm, kScale, kReshape, kTranspose, kUnsqueeze, kSqueeze, kFlatten, kConcat, kStack, kSplit,
   kSplitNum, kSlice, kCast, kConv2d, kPool2d, kMean, kSum, kMax, kMin, kArgmax, kEmbedding, kGather, kExpand, kTile,
   kWhere, kClip, kIdentity, kFull, kFullLike, kShape, kFullIntArray, kRmsNorm, kLinear, kFlashAttn, kFlashAttnQKV,
-  kArange
+  kArange, kLess, kLessEq, kGreater, kGreaterEq, kEqual, kNotEqual, kLogicalAnd, kLogicalOr, kLogicalNot,
+  kIncrement,
+  // control flow (structured pd_op.if / pd_op.while lowered to branches by framework/native_interp.py):
+  kJump,         // pc = target
+  kJumpIfFalse,  // pc = target unless in[0] (a scalar bool tensor) is true
+  kMove          // out[k] = in[k] for every k, all inputs read before any output is written (yield / block args)
 };
 
 const std::unordered_map<std::string, int>& op_table() {
@@ -217,7 +222,11 @@ const std::unordered_map<std::string, int>& op_table() {
       {"gather", kGather}, {"expand", kExpand}, {"tile", kTile}, {"where", kWhere}, {"clip", kClip},
       {"assign", kIdentity}, {"dropout", kIdentity}, {"full", kFull}, {"full_like", kFullLike}, {"shape", kShape},
       {"full_int_array", kFullIntArray}, {"rms_norm", kRmsNorm}, {"fused_linear", kLinear},
-      {"flash_attn", kFlashAttn}, {"flash_attn_qkvpacked", kFlashAttnQKV}, {"arange", kArange}};
+      {"flash_attn", kFlashAttn}, {"flash_attn_qkvpacked", kFlashAttnQKV}, {"arange", kArange},
+      {"less_than", kLess}, {"less_equal", kLessEq}, {"greater_than", kGreater}, {"greater_equal", kGreaterEq},
+      {"equal", kEqual}, {"not_equal", kNotEqual}, {"logical_and", kLogicalAnd}, {"logical_or", kLogicalOr},
+      {"logical_not", kLogicalNot}, {"increment", kIncrement}, {"increment_", kIncrement},
+      {"__jump", kJump}, {"__jump_if_false", kJumpIfFalse}, {"__move", kMove}};
   return t;
 }
 
@@ -339,9 +348,25 @@ class Interpreter {
     for (size_t n = 0; n < code_.size(); ++n)
       for (int s : code_[n].in)
         if (s >= 0) last[s] = static_cast<int>(n);
+    // loops (a backward jump at b to t <= b, the loop exit at b + 1): a slot read inside [t, b] but written outside
+    // it (defined before the loop, a feed or a parameter) is read again by the next iteration, so it is released
+    // only once the loop has exited
+    for (size_t b = 0; b < code_.size(); ++b) {
+      if (code_[b].op != kJump) continue;
+      const int t = static_cast<int>(code_[b].i("target", 0));
+      if (t > static_cast<int>(b)) continue;
+      std::vector<char> inside_w(slots_.size(), 0);
+      for (size_t n = t; n <= b; ++n)
+        for (int s : code_[n].out)
+          if (s >= 0) inside_w[s] = 1;
+      for (size_t n = t; n <= b; ++n)
+        for (int s : code_[n].in)
+          if (s >= 0 && !inside_w[s]) last[s] = std::max(last[s], static_cast<int>(b) + 1);
+    }
     release_.assign(code_.size(), {});
     for (size_t s = 0; s < last.size(); ++s)
-      if (last[s] >= 0 && !keep_[s]) release_[last[s]].push_back(static_cast<int>(s));
+      if (last[s] >= 0 && last[s] < static_cast<int>(code_.size()) && !keep_[s])
+        release_[last[s]].push_back(static_cast<int>(s));
     // outputs never read (e.g. a dropout mask) are dropped right after their producer
     for (size_t n = 0; n < code_.size(); ++n)
       for (int s : code_[n].out)
@@ -359,20 +384,36 @@ class Interpreter {
     peak_live_ = 0;
     int64_t live = 0;
     for (const auto& s : slots_) live += s.defined() ? 1 : 0;
-    for (size_t n = 0; n < code_.size(); ++n) {
-      exec(code_[n]);
-      for (int s : code_[n].out) live += (s >= 0 && slots_[s].defined()) ? 1 : 0;
+    const size_t ncode = code_.size();
+    int64_t steps = 0;
+    for (size_t n = 0; n < ncode;) {
+      const Instr& I = code_[n];
+      size_t next = n + 1;
+      if (I.op == kJump) {
+        next = static_cast<size_t>(I.i("target", 0));
+      } else if (I.op == kJumpIfFalse) {
+        const at::Tensor& c = in(I, 0);
+        if (!c.defined() || c.numel() != 1)
+          throw std::runtime_error("interpreter: control-flow condition is not a one-element tensor");
+        if (!c.item().toBool()) next = static_cast<size_t>(I.i("target", 0));
+      } else {
+        exec(I);
+      }
+      for (int s : I.out) live += (s >= 0 && slots_[s].defined()) ? 1 : 0;
       peak_live_ = std::max(peak_live_, live);
       for (int s : release_[n]) {
         if (slots_[s].defined()) --live;
         slots_[s] = at::Tensor();
       }
+      if (++steps > max_steps_) throw std::runtime_error("interpreter: instruction budget exceeded (endless loop?)");
+      n = next;
     }
     std::vector<at::Tensor> out;
     out.reserve(fetch_.size());
     for (int s : fetch_) out.push_back(slots_[s]);
-    for (const auto& f : feeds)
-      if (!keep_[f.first]) slots_[f.first] = at::Tensor();
+    // branches not taken / loops leave slots whose last reader did not run: drop every non-persistent slot
+    for (size_t s = 0; s < slots_.size(); ++s)
+      if (!keep_[s]) slots_[s] = at::Tensor();
     return out;
   }
 
@@ -668,6 +709,23 @@ class Interpreter {
       case kWhere: put(I, 0, at::where(in(I, 0), in(I, 1), in(I, 2))); break;
       case kClip: put(I, 0, at::clamp(in(I, 0), I.f("min", -3.4e38), I.f("max", 3.4e38))); break;
       case kIdentity: put(I, 0, in(I, 0)); break;
+      case kLess: put(I, 0, at::lt(in(I, 0), in(I, 1))); break;
+      case kLessEq: put(I, 0, at::le(in(I, 0), in(I, 1))); break;
+      case kGreater: put(I, 0, at::gt(in(I, 0), in(I, 1))); break;
+      case kGreaterEq: put(I, 0, at::ge(in(I, 0), in(I, 1))); break;
+      case kEqual: put(I, 0, at::eq(in(I, 0), in(I, 1))); break;
+      case kNotEqual: put(I, 0, at::ne(in(I, 0), in(I, 1))); break;
+      case kLogicalAnd: put(I, 0, at::logical_and(in(I, 0), in(I, 1))); break;
+      case kLogicalOr: put(I, 0, at::logical_or(in(I, 0), in(I, 1))); break;
+      case kLogicalNot: put(I, 0, at::logical_not(in(I, 0))); break;
+      case kIncrement: put(I, 0, at::add(in(I, 0), I.f("value", 1.0))); break;  // out of place (no aliasing)
+      case kMove: {
+        std::vector<at::Tensor> vals;
+        vals.reserve(I.in.size());
+        for (size_t k = 0; k < I.in.size(); ++k) vals.push_back(in(I, k));
+        for (size_t k = 0; k < vals.size(); ++k) put(I, k, std::move(vals[k]));
+        break;
+      }
       case kFull: {
         auto opts = at::TensorOptions().dtype(dtype_of(I.s("dtype", "float32"))).device(device_);
         put(I, 0, at::full(I.v("shape"), I.f("value", 0.0), opts));
@@ -702,6 +760,7 @@ class Interpreter {
   std::vector<Instr> code_;
   std::vector<int> keep_, fetch_, persistent_;
   std::vector<std::vector<int>> release_;
+  int64_t max_steps_ = int64_t(1) << 40;
   int64_t peak_live_ = 0;
 };
 

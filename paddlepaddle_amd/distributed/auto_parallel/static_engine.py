@@ -316,6 +316,9 @@ class StaticEngine:
         self.recompute = bool(strategy.recompute.get("enable", False))
         if self.recompute and strategy.recompute.get("refined_ops_patterns"):
             unsupported.append("recompute.refined_ops_patterns (selective recompute)")
+        if self.schedule not in self._PASS_OF:
+            unsupported.append(f"pipeline.schedule_mode {pp.schedule_mode!r} (one of FThenB / 1F1B / Eager1F1B / "
+                               f"ZBH1; virtual pipelines run on fleet PipelineParallelWithInterleave)")
         if strategy.sp_optimization.get("enable", False):
             unsupported.append("sp_optimization")
         if strategy.gradient_merge.get("enable", False):
@@ -1359,6 +1362,22 @@ class StaticEngine:
                 g = t.grad if t.grad is not None else torch.zeros_like(t)
                 p2p.send(g, self._peer(self.slot_stage[slot]), ("B", slot, mb))
 
+    _PASS_OF = {"FTHENB": "FThenB", "1F1B": "1F1B", "EAGER1F1B": "Eager1F1B", "ZBH1": "ZBH1"}
+
+    def _job_list(self, mode, nst, s, n):
+        """The stage's job list from the registered pipeline_scheduler_<mode> pass (cached per configuration)."""
+        key = (mode, nst, s, n)
+        if getattr(self, "_jobs_key", None) != key:
+            from ..passes import new_pass
+            from ..passes.pipeline_scheduler import job_pairs
+            name = self._PASS_OF.get(mode)
+            if name is None:
+                raise ValueError(f"static auto-parallel engine: unsupported pipeline schedule_mode {mode!r}")
+            ctx = new_pass(f"pipeline_scheduler_{name}", {"num_micro_batches": n, "pp_stage": s,
+                                                          "pp_degree": nst}).apply(self.prog, None)
+            self._jobs, self._jobs_key = job_pairs(ctx.get_attr("pipeline_scheduler.job_list")), key
+        return self._jobs
+
     def step(self, inputs, labels):
         if not self.built:
             self.build(inputs, labels)
@@ -1379,12 +1398,11 @@ class StaticEngine:
                 losses.append(st[2].detach().float().reshape(()))
             states[mb] = st
         from ...ops import linear as LIN
-        from ...parallel.pp_schedules import schedule as _schedule
         # one stage: 1F1B degenerates to F0 B0 F1 B1 ... (one micro-batch of activations alive); FThenB keeps all
         # of them (what stage 0 of a deeper 1F1B pipeline holds: the 70B stage proxy asks for it explicitly)
-        mode = self.schedule if self.schedule in ("ZBH1", "FTHENB") or nst > 1 else "1F1B"
+        mode = self.schedule if self.schedule in ("ZBH1", "FTHENB", "EAGER1F1B") or nst > 1 else "1F1B"
         wq = {}
-        for kind, mb in _schedule(mode, nst, s, n):  # 1F1B / FThenB / ZBH1 job list of this stage
+        for kind, mb in self._job_list(mode, nst, s, n):  # this stage's jobs from the pipeline_scheduler pass
             if kind == "F":
                 if mode == "ZBH1":
                     with LIN.zero_bubble_forward():

@@ -253,7 +253,7 @@ def _all_reduce_raw(t, op=ReduceOp.SUM, group=None, async_op=False):
     return dist.all_reduce(t, op=_TORCH_OP[op], group=_pg(group), async_op=async_op)
 
 
-def _static_comm(tensor, name, fn):
+def _static_comm(tensor, name, fn, meta=None):
     """Inside a static program being built: record the collective as one in-place "comm" node (replayed on
     the executor's communication stream, static/program.py _Streams). Returns True when recorded."""
     from ..framework.trace_hook import _active_program
@@ -266,13 +266,15 @@ def _static_comm(tensor, name, fn):
     def run(x):
         fn(x)
         return None
+    run._pa_comm = meta  # (kind, op, group) for the fuse_all_reduce pass
     prog._append(OpNode(run, (prog._template(t),), {}, None, kind="comm", name="c:" + name))
     return True
 
 
 def all_reduce(tensor, op=ReduceOp.SUM, group=None, sync_op=True, use_calc_stream=False):
     if is_initialized() and get_world_size(group) > 1 and _static_comm(
-            tensor, "all_reduce", lambda x: dist.all_reduce(x, op=_TORCH_OP[op], group=_pg(group))):
+            tensor, "all_reduce", lambda x: dist.all_reduce(x, op=_TORCH_OP[op], group=_pg(group)),
+            ("all_reduce", op, group)):
         return _ret(None, sync_op)
     if not is_initialized() or get_world_size(group) == 1:
         return _ret(None, sync_op)

@@ -4,5 +4,6 @@ from .pass_base import PassBase, PassContext, PassManager, PassType, new_pass, r
 from .program_passes import (  # noqa: F401
     AMPPass, DeadCodeEliminationPass, FP16Pass, FuseGemmEpiloguePass, GradientMergePass,
 )
+from . import pipeline_scheduler  # noqa: F401  (pipeline_scheduler_* passes)
 
 __all__ = ["new_pass", "PassManager", "PassContext"]

@@ -16,6 +16,8 @@
 * ``auto_parallel_recompute``: ops between consecutive checkpoints become recompute segments (node.rc), run
   checkpointed by the static auto-parallel engine; ``allreduce_matmul_grad_overlapping`` /
   ``auto_parallel_sharding`` mark the program for the engine's partition-time TP dX overlap and ZeRO-1/2.
+* ``fuse_bn_act`` / ``fuse_bn_add_act`` / ``fuse_elewise_add_act``: batch_norm (+ residual) + relu -> one
+  batch_norm_act_nhwc node; bias add + tanh GELU -> one bias_gelu node.
 """
 from __future__ import annotations
 
@@ -26,7 +28,8 @@ from ...static import program as P
 
 __all__ = ["FuseGemmEpiloguePass", "DeadCodeEliminationPass", "AMPPass", "FP16Pass", "GradientMergePass",
            "FuseSiblingLinearsPass", "FuseRMSNormResidualPass",
-           "RecomputePass", "AllreduceMatmulGradOverlappingPass", "ShardingPass"]
+           "RecomputePass", "AllreduceMatmulGradOverlappingPass", "ShardingPass", "FuseBNActPass",
+           "FuseBNAddActPass", "FuseElewiseAddActPass"]
 
 _RELU = {"f:torch.nn.functional:relu", "f:torch:relu", "m:relu"}
 _GELU = {"o:paddlepaddle_amd.ops.activation:gelu", "f:torch.nn.functional:gelu"}
@@ -488,3 +491,221 @@ class ShardingPass(PassBase):
     def _apply_single_impl(self, prog, startup, context):
         prog._pa_sharding = {"stage": int(self.get_attr("stage", 1)),
                              "dim": self.get_attr("sharding_mesh_dim", "dp")}
+
+
+# ------------------------------------------------------------------------------------------------------------------
+_BN = "o:paddlepaddle_amd.ops.bn:batch_norm_act_nhwc"
+_BIAS_GELU = "o:paddlepaddle_amd.ops.activation:bias_gelu"
+
+
+def _bn_args(n):
+    """Positional (x, w, b, rm, rv, training, momentum, eps, act, residual, grad_sink) of a BN node, or None."""
+    if n.name != _BN or n.kwargs or len(n.args) != 11 or not isinstance(n.outs, P._Ref):
+        return None
+    return list(n.args)
+
+
+class _Producers:
+    def __init__(self, prog, keep):
+        self.nodes = prog.nodes
+        self.uses = _use_counts(self.nodes)
+        self.producer = {}
+        for i, n in enumerate(self.nodes):
+            if not isinstance(n, P.CFNode):
+                for s in P._node_writes(n):
+                    self.producer.setdefault(s, i)
+        self.keep = keep
+
+    def single(self, ref):
+        s = _slot(ref)
+        return s is not None and self.uses.get(s, 0) == 1 and s not in self.keep
+
+    def of(self, ref):
+        i = self.producer.get(_slot(ref))
+        return (i, self.nodes[i]) if i is not None else (None, None)
+
+
+def _rewrite_until_fixed(prog, keep, step):
+    fused = 0
+    while True:
+        pr = _Producers(prog, keep)
+        done = False
+        for j, n in enumerate(pr.nodes):
+            if isinstance(n, P.CFNode) or n.kind == "guard":
+                continue
+            if step(pr, j, n):
+                fused += 1
+                done = True
+                break
+        if not done:
+            return fused
+
+
+@register_pass("fuse_bn_act")
+class FuseBNActPass(PassBase):
+    """Reference passes/cpp_pass.py FuseBatchNormActPass (fuse_bn_act_pass.cc): batch_norm followed by relu
+    becomes ONE batch_norm_act_nhwc node with the ReLU in the kernel's epilogue (ops/bn.py, csrc/kernels/bn.hip),
+    so the normalised activation is not written and re-read by a separate ReLU."""
+    _after = ("auto_parallel_amp", "auto_parallel_fp16")
+
+    def _type(self):
+        return PassType.FUSION_OPT
+
+    def _apply_single_impl(self, prog, startup, context):
+        bn = P._resolve(_BN)
+
+        def step(pr, j, n):
+            if _act_of(n) != "relu":
+                return False
+            i, m = pr.of(n.args[0])
+            a = _bn_args(m) if m is not None else None
+            if a is None or a[8] is not None or not pr.single(n.args[0]):
+                return False
+            a[8] = "relu"
+            pr.nodes[j] = _keep_rc(P.OpNode(bn, tuple(a), {}, n.outs, m.kind, _BN), m)
+            del pr.nodes[i]
+            return True
+
+        n = _rewrite_until_fixed(prog, _protected(prog, self.get_attr("fetch_vars")), step)
+        context.set_attr("fuse_bn_act.fused", context.get_attr("fuse_bn_act.fused", 0) + n)
+
+
+@register_pass("fuse_bn_add_act")
+class FuseBNAddActPass(PassBase):
+    """Reference cpp_pass.py FuseBatchNormAddActPass: batch_norm -> + residual -> relu becomes ONE
+    batch_norm_act_nhwc(residual=..., act="relu") node (the residual add and ReLU in the BN apply kernel; the
+    backward emits the residual's gradient from the same kernel)."""
+    _after = ("auto_parallel_amp", "auto_parallel_fp16")
+
+    def _type(self):
+        return PassType.FUSION_OPT
+
+    def _apply_single_impl(self, prog, startup, context):
+        bn = P._resolve(_BN)
+
+        def step(pr, k, n):
+            if _act_of(n) != "relu" or not pr.single(n.args[0]):
+                return False
+            j, add = pr.of(n.args[0])
+            if add is None or add.name not in _ADD or len(add.args) != 2 or add.kwargs:
+                return False
+            for x, r in (add.args, add.args[::-1]):
+                i, m = pr.of(x)
+                a = _bn_args(m) if m is not None else None
+                if a is None or a[8] is not None or a[9] is not None or not pr.single(x) or _slot(r) is None:
+                    continue
+                if _shape_of(prog, r) != _shape_of(prog, x) or prog._metas[_slot(r)].dtype != \
+                        prog._metas[_slot(x)].dtype:
+                    continue
+                a[8], a[9] = "relu", r
+                pr.nodes[k] = _keep_rc(P.OpNode(bn, tuple(a), {}, n.outs, m.kind, _BN), m)
+                for d in sorted((i, j), reverse=True):
+                    del pr.nodes[d]
+                return True
+            return False
+
+        n = _rewrite_until_fixed(prog, _protected(prog, self.get_attr("fetch_vars")), step)
+        context.set_attr("fuse_bn_add_act.fused", context.get_attr("fuse_bn_add_act.fused", 0) + n)
+
+
+@register_pass("fuse_elewise_add_act")
+class FuseElewiseAddActPass(PassBase):
+    """Reference cpp_pass.py FuseElementwiseAddActPass: ``x + b`` (b a vector over the last dim) followed by the
+    tanh GELU becomes ONE bias_gelu node (ops/activation.py, one HIP kernel forward and backward). A matmul
+    producer is left to fuse_gemm_epilogue, which folds bias and GELU into the GEMM itself."""
+    _after = ("auto_parallel_amp", "auto_parallel_fp16", "fuse_gemm_epilogue")
+
+    def _type(self):
+        return PassType.FUSION_OPT
+
+    def _apply_single_impl(self, prog, startup, context):
+        bg = P._resolve(_BIAS_GELU)
+
+        def step(pr, k, n):
+            if _act_of(n) != "gelu" or not pr.single(n.args[0]):
+                return False
+            j, add = pr.of(n.args[0])
+            if add is None or add.name not in _ADD or len(add.args) != 2 or add.kwargs:
+                return False
+            for x, b in (add.args, add.args[::-1]):
+                xs, bs = _shape_of(prog, x), _shape_of(prog, b)
+                if _slot(x) is None or xs is None or bs is None or len(xs) < 1 or bs != (xs[-1],):
+                    continue
+                pi, pm = pr.of(x)
+                if pm is not None and pm.name in _MATMUL:
+                    continue  # the GEMM epilogue pass owns this pattern
+                pr.nodes[k] = _keep_rc(P.OpNode(bg, (x, b), {}, n.outs, "op", _BIAS_GELU), add)
+                del pr.nodes[j]
+                return True
+            return False
+
+        n = _rewrite_until_fixed(prog, _protected(prog, self.get_attr("fetch_vars")), step)
+        context.set_attr("fuse_elewise_add_act.fused", context.get_attr("fuse_elewise_add_act.fused", 0) + n)
+
+
+@register_pass("fuse_all_reduce")
+class FuseAllReducePass(PassBase):
+    """Reference passes/fuse_all_reduce.py: consecutive all-reduces of one group / reduce op / dtype become ONE
+    coalesced all-reduce over a flat buffer (the tensors are packed, reduced once and unpacked), up to
+    ``max_memory_size`` bytes per bucket (default 256 MiB: few, large messages suit the per-link xGMI rings)."""
+
+    def _type(self):
+        return PassType.COMM_OPT
+
+    def _apply_single_impl(self, prog, startup, context):
+        cap = int(self.get_attr("max_memory_size", 256 << 20))
+        nodes, out, fused, run = prog.nodes, [], 0, []
+
+        def meta(n):
+            m = getattr(n.func, "_pa_comm", None) if n.kind == "comm" else None
+            if m is None or m[0] != "all_reduce" or len(n.args) != 1 or _slot(n.args[0]) is None:
+                return None
+            t = prog._metas[_slot(n.args[0])]
+            return (m[1], id(m[2]) if m[2] is not None else None, t.dtype), m, t.numel() * t.element_size()
+
+        def flush():
+            nonlocal fused
+            if len(run) > 1:
+                out.append(_keep_rc(_coalesced([n for n, _ in run]), run[0][0]))
+                fused += len(run) - 1
+            else:
+                out.extend(n for n, _ in run)
+            run.clear()
+
+        size = 0
+        for n in nodes:
+            mk = meta(n) if not isinstance(n, P.CFNode) else None
+            if mk is None:
+                flush()
+                size = 0
+                out.append(n)
+                continue
+            key, m, nbytes = mk
+            if run and (run[0][1][0] != key or size + nbytes > cap or
+                        any(_slot(r.args[0]) == _slot(n.args[0]) for r, _ in run)):
+                flush()
+                size = 0
+            run.append((n, (key, m)))
+            size += nbytes
+        flush()
+        prog.nodes[:] = out
+        context.set_attr("fuse_all_reduce.fused", context.get_attr("fuse_all_reduce.fused", 0) + fused)
+
+
+def _coalesced(nodes):
+    import torch.distributed as tdist
+    from ..collective import _TORCH_OP, _pg
+    _, op, group = nodes[0].func._pa_comm
+    refs = tuple(n.args[0] for n in nodes)
+
+    def run(*xs):
+        flat = torch.cat([x.reshape(-1) for x in xs])
+        tdist.all_reduce(flat, op=_TORCH_OP[op], group=_pg(group))
+        off = 0
+        for x in xs:
+            k = x.numel()
+            x.copy_(flat[off:off + k].view_as(x))
+            off += k
+        return None
+    run._pa_comm = ("all_reduce_coalesced", op, group)
+    return P.OpNode(run, refs, {}, None, kind="comm", name="c:all_reduce_coalesced")

@@ -133,58 +133,100 @@ def compile_program(program, params, device):
 
     plan = []        # (op, in_slots, out_slots, attrs)
     feed_slots, fetch_slots, bound = [], [], []
-    for name, operands, results, attrs, _types in _fuse_linear(program.ops):
-        dialect, _, short = name.partition(".")
-        if name == "builtin.parameter":
-            bound.append((slot(results[0]), params[attrs["parameter_name"]]._t))
-            continue
-        if name in ("pd_op.data", "pd_op.feed"):
-            feed_slots.append((attrs["name"], slot(results[0])))
-            continue
-        if name in ("pd_op.fetch", "builtin.shadow_output"):
-            continue
-        if name == "builtin.combine":
-            lists[results[0]] = list(operands)
-            continue
-        if name == "builtin.split":
-            lists.setdefault(("split", operands[0]), results)
-            continue
-        if dialect != "pd_op" or short not in supported:
-            return None
-        a = {k: _attr_value(v) for k, v in attrs.items()}
-        a = {k: v for k, v in a.items() if v is not None}
-        if short == "full":
-            consts[results[0]] = a.get("value", 0.0)
-        elif short == "full_int_array":
-            consts[results[0]] = [int(x) for x in (a.get("value") or [])]
-        mut = _MUTABLE.get(short, {})
-        ins = []
-        for i, v in enumerate(operands):
-            if i in mut:
-                if v not in consts:
-                    return None  # a data-dependent shape / axis: keep the Python replay
-                c = consts[v]
-                a[mut[i]] = c
+
+    def emit(op, ins, outs, a):
+        plan.append((op, ins, outs, a))
+        return a
+
+    def lower(ops):
+        """Appends the instructions of one block; False when an op has no native mapping."""
+        for op in _fuse_linear([o for o in ops if o[0] != "cf.yield"]):
+            name, operands, results, attrs, _types = op
+            dialect, _, short = name.partition(".")
+            if name == "builtin.parameter":
+                bound.append((slot(results[0]), params[attrs["parameter_name"]]._t))
                 continue
-            if v == 0:
-                ins.append(-1)
-            elif v in lists:  # a combined operand list (concat / stack inputs)
-                ins.extend(slot(x) for x in lists[v])
-            else:
-                ins.append(slot(v))
-        outs = []
-        for r in results:
-            split = lists.get(("split", r))
-            if split is not None:
-                outs.extend(slot(x) for x in split)
-            else:
-                outs.append(slot(r))
-        if short in ("pool2d",) and "kernel_size" in a and not isinstance(a["kernel_size"], list):
-            a["kernel_size"] = [int(a["kernel_size"])] * 2
-        for key in ("axis",):
-            if short in ("concat", "split", "split_with_num", "gather", "argmax") and isinstance(a.get(key), list):
-                a[key] = a[key][0] if a[key] else 0
-        plan.append((short, ins, outs, a))
+            if name in ("pd_op.data", "pd_op.feed"):
+                feed_slots.append((attrs["name"], slot(results[0])))
+                continue
+            if name in ("pd_op.fetch", "builtin.shadow_output"):
+                continue
+            if name == "builtin.combine":
+                lists[results[0]] = list(operands)
+                continue
+            if name == "builtin.split":
+                lists.setdefault(("split", operands[0]), results)
+                continue
+            if name == "pd_op.if":
+                # jump_if_false -> else; true block; move yields -> results; jump -> end; else: false block; move
+                t_blk, f_blk = op.regions
+                jf = emit("__jump_if_false", [slot(operands[0])], [], {"target": -1})
+                if not lower(t_blk.ops):
+                    return False
+                emit("__move", [slot(v) for v in t_blk.yields()], [slot(r) for r in results], {})
+                je = emit("__jump", [], [], {"target": -1})
+                jf["target"] = len(plan)
+                if not lower(f_blk.ops):
+                    return False
+                emit("__move", [slot(v) for v in f_blk.yields()], [slot(r) for r in results], {})
+                je["target"] = len(plan)
+                continue
+            if name == "pd_op.while":
+                # args <- loop values, c <- cond; top: jump_if_false c -> exit; body; (c, args) <- yields;
+                # jump -> top; exit: results <- args
+                body = op.regions[0]
+                c = slot(("while_cond", id(op)))
+                emit("__move", [slot(v) for v in operands[1:]] + [slot(operands[0])],
+                     [slot(a) for a in body.args] + [c], {})
+                top = len(plan)
+                jf = emit("__jump_if_false", [c], [], {"target": -1})
+                if not lower(body.ops):
+                    return False
+                y = body.yields()
+                emit("__move", [slot(v) for v in y], [c] + [slot(a) for a in body.args], {})
+                emit("__jump", [], [], {"target": top})
+                jf["target"] = len(plan)
+                emit("__move", [slot(a) for a in body.args], [slot(r) for r in results], {})
+                continue
+            if dialect != "pd_op" or short not in supported:
+                return False
+            a = {k: _attr_value(v) for k, v in attrs.items()}
+            a = {k: v for k, v in a.items() if v is not None}
+            if short == "full":
+                consts[results[0]] = a.get("value", 0.0)
+            elif short == "full_int_array":
+                consts[results[0]] = [int(x) for x in (a.get("value") or [])]
+            mut = _MUTABLE.get(short, {})
+            ins = []
+            for i, v in enumerate(operands):
+                if i in mut:
+                    if v not in consts:
+                        return False  # a data-dependent shape / axis: keep the Python replay
+                    a[mut[i]] = consts[v]
+                    continue
+                if v == 0:
+                    ins.append(-1)
+                elif v in lists:  # a combined operand list (concat / stack inputs)
+                    ins.extend(slot(x) for x in lists[v])
+                else:
+                    ins.append(slot(v))
+            outs = []
+            for r in results:
+                split = lists.get(("split", r))
+                if split is not None:
+                    outs.extend(slot(x) for x in split)
+                else:
+                    outs.append(slot(r))
+            if short in ("pool2d",) and "kernel_size" in a and not isinstance(a["kernel_size"], list):
+                a["kernel_size"] = [int(a["kernel_size"])] * 2
+            for key in ("axis",):
+                if short in ("concat", "split", "split_with_num", "gather", "argmax") and isinstance(a.get(key), list):
+                    a[key] = a[key][0] if a[key] else 0
+            emit(short, ins, outs, a)
+        return True
+
+    if not lower(program.ops):
+        return None
     # builtin.split results whose producer was not a multi-output op stay unresolved
     fetch_slots = [slot(v) for _, v in program.fetch]
     dev = str(device)

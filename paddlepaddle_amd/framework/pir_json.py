@@ -204,6 +204,39 @@ class PirWriter:
         return self.op("full", [], {"shape": a_intarray(shape), "value": a_f64(value), "dtype": a_dtype(dtype),
                                     "place": a_place(1)}, [dtensor(dtype, shape)])[0]
 
+    def block(self, args_types=()):
+        """Open a sub-block (for if_ / while_): ops appended until the matching end_block() go into it; its
+        arguments (block-argument ids count down from -1) are returned."""
+        if not hasattr(self, "_stack"):
+            self._stack, self._next_arg = [], -1
+        args = []
+        for ty in args_types:
+            args.append(self._next_arg)
+            self.types[self._next_arg] = ty
+            self._next_arg -= 1
+        self._stack.append((self.ops, args))
+        self.ops = []
+        return args
+
+    def end_block(self, yields):
+        self.op("2.yield", list(yields), {}, [])
+        ops, (outer, args) = self.ops, self._stack.pop()
+        self.ops = outer
+        return {"#": f"block_{len(self._stack)}", "args": [{"#": a, "TT": self.types[a]} for a in args], "ops": ops}
+
+    def if_(self, cond, true_block, false_block, out_types):
+        """pd_op.if with two closed blocks (from end_block); returns the result ids."""
+        outs = self.op("if", [cond], {}, out_types)
+        self.ops[-1]["regions"] = [{"#": "region_t", "blocks": [true_block]}, {"#": "region_f", "blocks": [false_block]}]
+        return outs
+
+    def while_(self, cond, vids, body_block):
+        """pd_op.while over loop values ``vids`` (body args = their values per iteration, body yields the next
+        condition then the next values); returns the result ids."""
+        outs = self.op("while", [cond] + list(vids), {}, [self.types[v] for v in vids])
+        self.ops[-1]["regions"] = [{"#": "region_w", "blocks": [body_block]}]
+        return outs
+
     def combine(self, vids):
         return self.op("0.combine", list(vids), {}, [vec_type([self.types[v] for v in vids])])[0]
 
@@ -369,37 +402,76 @@ def from_builder(b, trainable=False):
 
 
 # ------------------------------------------------------------------------------------------- reader / runner
+class PirOp(tuple):
+    """(name, operand ids, result ids, attrs, result types) — plus ``regions``: the op's sub-blocks (pd_op.if:
+    true / false block; pd_op.while: body block), each a PirBlock."""
+
+    def __new__(cls, name, operands, results, attrs, types, regions=()):
+        o = super().__new__(cls, (name, operands, results, attrs, types))
+        o.regions = list(regions)
+        return o
+
+
+class PirBlock:
+    """One block: argument value ids (block arguments count down from -1) and its ops."""
+
+    def __init__(self, args, ops):
+        self.args, self.ops = args, ops
+
+    def yields(self):
+        """Operand ids of the block's terminating cf.yield ([] when it has none)."""
+        return list(self.ops[-1][1]) if self.ops and self.ops[-1][0] == "cf.yield" else []
+
+
+_DIALECTS = {"0": "builtin", "1": "pd_op", "2": "cf", "3": "custom_op", "4": "pd_dist"}
+
+
 class PirProgram:
-    """Block 0 of a PIR JSON program: ops as (name, operand ids, result ids, attrs, result types)."""
+    """Block 0 of a PIR JSON program: ops as (name, operand ids, result ids, attrs, result types); control-flow ops
+    (pd_op.if / pd_op.while) carry their sub-blocks (reference ir_serialize.cc WriteOp: an op's "regions")."""
 
     def __init__(self, data):
         if not (isinstance(data, dict) and data.get("base_code", {}).get("magic") == MAGIC):
             raise ValueError("not a PIR program (base_code.magic != 'pir')")
         self.version = data["base_code"].get("version")
         self.trainable = bool(data["base_code"].get("trainable", False))
-        block = data["program"]["regions"][0]["blocks"][0]
-        self.ops = []
         self.params = []  # (name, value id, (dtype, shape)) in program order
         self.feed_names, self.fetch = [], []
-        for op in block["ops"]:
+        self.ops = self._block(data["program"]["regions"][0]["blocks"][0], top=True).ops
+
+    def _block(self, bj, top=False):
+        ops = []
+        for op in bj["ops"]:
             name = op["#"]
             if name == "p":
                 res = op["O"]
                 pname = op["A"][3]
                 self.params.append((pname, res["%"], decode_type(res.get("TT"))))
-                self.ops.append(("builtin.parameter", [], [res["%"]], {"parameter_name": pname}, [res.get("TT")]))
+                ops.append(PirOp("builtin.parameter", [], [res["%"]], {"parameter_name": pname}, [res.get("TT")]))
                 continue
             dialect, _, short = name.partition(".")
-            full = {"0": "builtin", "1": "pd_op", "2": "cf", "3": "custom_op", "4": "pd_dist"}.get(dialect, dialect)
-            full = full + "." + short
+            full = _DIALECTS.get(dialect, dialect) + "." + short
             operands = [x["%"] for x in op.get("I", [])]
             results = [x["%"] for x in op.get("O", [])]
             attrs = {a["N"]: decode_attr(a["AT"]) for a in op.get("A", [])}
-            self.ops.append((full, operands, results, attrs, [x.get("TT") for x in op.get("O", [])]))
+            regions = [self._block(r["blocks"][0]) for r in op.get("regions", []) if r.get("blocks")]
+            ops.append(PirOp(full, operands, results, attrs, [x.get("TT") for x in op.get("O", [])], regions))
+            if not top:
+                continue
             if full in ("pd_op.data", "pd_op.feed"):
                 self.feed_names.append(attrs["name"])
             elif full == "pd_op.fetch":
                 self.fetch.append((attrs.get("name", f"fetch{len(self.fetch)}"), operands[0]))
+        return PirBlock([a["#"] for a in bj.get("args", [])], ops)
+
+    def all_ops(self):
+        """Every op of the program, sub-blocks included (depth first)."""
+        def walk(ops):
+            for o in ops:
+                yield o
+                for b in getattr(o, "regions", ()):
+                    yield from walk(b.ops)
+        return list(walk(self.ops))
 
     @property
     def fetch_names(self):
@@ -532,6 +604,18 @@ _RUN = {
     "pd_op.full": _full, "pd_op.full_int_array": _full_int_array,
     "pd_op.full_like": lambda ins, a: [_P().full_like(ins[0], _scalar(ins[1]), dtype=a.get("dtype") or None)],
     "pd_op.assign": lambda ins, a: [ins[0]],
+    "pd_op.less_than": lambda ins, a: [_P().less_than(ins[0], ins[1])],
+    "pd_op.less_equal": lambda ins, a: [_P().less_equal(ins[0], ins[1])],
+    "pd_op.greater_than": lambda ins, a: [_P().greater_than(ins[0], ins[1])],
+    "pd_op.greater_equal": lambda ins, a: [_P().greater_equal(ins[0], ins[1])],
+    "pd_op.equal": lambda ins, a: [_P().equal(ins[0], ins[1])],
+    "pd_op.not_equal": lambda ins, a: [_P().not_equal(ins[0], ins[1])],
+    "pd_op.logical_and": lambda ins, a: [_P().logical_and(ins[0], ins[1])],
+    "pd_op.logical_or": lambda ins, a: [_P().logical_or(ins[0], ins[1])],
+    "pd_op.logical_not": lambda ins, a: [_P().logical_not(ins[0])],
+    # increment_ runs out of place: the result is a new value (no aliasing of the loop's input)
+    "pd_op.increment": lambda ins, a: [ins[0] + a.get("value", 1.0)],
+    "pd_op.increment_": lambda ins, a: [ins[0] + a.get("value", 1.0)],
     "pd_op.matmul": lambda ins, a: [_P().matmul(ins[0], ins[1], transpose_x=a.get("transpose_x", False),
                                                 transpose_y=a.get("transpose_y", False))],
     "pd_op.add": lambda ins, a: [ins[0] + ins[1]], "pd_op.subtract": lambda ins, a: [ins[0] - ins[1]],
@@ -604,8 +688,9 @@ class PirRunner:
         self.program = program
         self.params = params  # name -> Tensor
         known = set(_RUN) | {"pd_op.data", "pd_op.feed", "pd_op.fetch", "builtin.parameter", "builtin.combine",
-                             "builtin.split", "builtin.shadow_output", "builtin.constant"}
-        missing = sorted({o[0] for o in program.ops} - known)
+                             "builtin.split", "builtin.shadow_output", "builtin.constant", "pd_op.if",
+                             "pd_op.while", "cf.yield"}
+        missing = sorted({o[0] for o in program.all_ops()} - known)
         if missing:
             raise NotImplementedError(f"PIR program uses operations without a mapping: {missing}")
 
@@ -619,34 +704,55 @@ class PirRunner:
 
     def run(self, feeds):
         from . import grad_mode
-        P = _P()
         env = {}
+        self._fi = 0
         with grad_mode.no_grad():
-            fi = 0
-            for name, operands, results, attrs, types in self.program.ops:
-                ins = [env.get(v) if v != 0 else None for v in operands]
-                if name == "builtin.parameter":
-                    env[results[0]] = self.params[attrs["parameter_name"]]
-                    continue
-                if name in ("pd_op.data", "pd_op.feed"):
-                    key = attrs.get("name")
-                    v = feeds[key] if isinstance(feeds, dict) else feeds[fi]
-                    fi += 1
-                    env[results[0]] = v if isinstance(v, P.Tensor) else P.to_tensor(np.asarray(v))
-                    continue
-                if name in ("pd_op.fetch", "builtin.shadow_output"):
-                    continue
-                if name == "builtin.combine":
-                    env[results[0]] = list(ins)
-                    continue
-                if name == "builtin.split":
-                    for r, v in zip(results, ins[0]):
-                        env[r] = v
-                    continue
-                outs = _RUN[name](ins, attrs)
-                for r, v in zip(results, outs):
-                    env[r] = v
+            self._block(self.program.ops, env, feeds)
         return [env[v] for _, v in self.program.fetch]
+
+    def _block(self, ops, env, feeds):
+        """Runs ``ops`` in ``env``; returns the operands of a terminating cf.yield (sub-blocks)."""
+        P = _P()
+        for op in ops:
+            name, operands, results, attrs, types = op
+            ins = [env.get(v) if v != 0 else None for v in operands]
+            if name == "cf.yield":
+                return ins
+            if name == "builtin.parameter":
+                env[results[0]] = self.params[attrs["parameter_name"]]
+                continue
+            if name in ("pd_op.data", "pd_op.feed"):
+                key = attrs.get("name")
+                v = feeds[key] if isinstance(feeds, dict) else feeds[self._fi]
+                self._fi += 1
+                env[results[0]] = v if isinstance(v, P.Tensor) else P.to_tensor(np.asarray(v))
+                continue
+            if name in ("pd_op.fetch", "builtin.shadow_output"):
+                continue
+            if name == "builtin.combine":
+                env[results[0]] = list(ins)
+                continue
+            if name == "builtin.split":
+                for r, v in zip(results, ins[0]):
+                    env[r] = v
+                continue
+            if name == "pd_op.if":  # reference IfOp: true / false block, each ending in cf.yield
+                blk = op.regions[0] if bool(_scalar(ins[0])) else op.regions[1]
+                outs = self._block(blk.ops, env, feeds) or []
+            elif name == "pd_op.while":  # reference WhileOp: operands (cond, vars), body yields (cond, vars)
+                body = op.regions[0]
+                cond, vals = ins[0], list(ins[1:])
+                while bool(_scalar(cond)):
+                    for a, v in zip(body.args, vals):
+                        env[a] = v
+                    y = self._block(body.ops, env, feeds)
+                    cond, vals = y[0], list(y[1:])
+                outs = vals
+            else:
+                outs = _RUN[name](ins, attrs)
+            for r, v in zip(results, outs):
+                env[r] = v
+        return None
 
 
 def load(path_prefix, device=None):

@@ -370,12 +370,12 @@ class PipelineParallelWithInterleave(PipelineParallel):
                              f"pipeline degree ({S}) for the interleaved schedule")
 
     def _chunk_of(self, k, forward):
-        v = (k // self.num_stages) % self.V
-        return v if forward else self.V - 1 - v
+        from .pp_schedules import vpp_chunk
+        return vpp_chunk(k, self.num_stages, self.V, forward)
 
     def _mb_of(self, k):
-        S = self.num_stages
-        return (k // (S * self.V)) * S + k % S
+        from .pp_schedules import vpp_mb
+        return vpp_mb(k, self.num_stages, self.V)
 
     def _vforward(self, k, mb_in, mb_lb, store, losses):
         v, mb = self._chunk_of(k, True), self._mb_of(k)
@@ -413,21 +413,14 @@ class PipelineParallelWithInterleave(PipelineParallel):
         n = self.accumulate_steps
         mb_in = self._split(inputs) if self.stage_id == 0 else [None] * n
         mb_lb = self._split(labels) if (self.stage_id == self.num_stages - 1 and labels is not None) else [None] * n
-        total = n * self.V
-        warm = min((self.num_stages - self.stage_id - 1) * 2 + (self.V - 1) * self.num_stages, total)
+        from .pp_schedules import vpp
         store, losses = {}, []
-        fk = bk = 0
-        for _ in range(warm):
-            self._vforward(fk, mb_in, mb_lb, store, losses)
-            fk += 1
-        for _ in range(total - warm):
-            self._vforward(fk, mb_in, mb_lb, store, losses)
-            fk += 1
-            self._vbackward(bk, store)
-            bk += 1
-        while bk < total:
-            self._vbackward(bk, store)
-            bk += 1
+        self.jobs = vpp(self.num_stages, self.stage_id, n, self.V)  # interleaved 1F1B job list of this stage
+        for kind, k in self.jobs:
+            if kind == "F":
+                self._vforward(k, mb_in, mb_lb, store, losses)
+            else:
+                self._vbackward(k, store)
         self.is_last = self.stage_id == self.num_stages - 1  # loss lives on the last stage's last chunk
         return self._finish(losses)
 

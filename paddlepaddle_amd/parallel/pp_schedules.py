@@ -16,7 +16,7 @@ reaches the previous stage one W earlier per hop than with a fused backward.
 """
 from __future__ import annotations
 
-__all__ = ["schedule", "fthenb", "one_f_one_b", "zbh1", "SCHEDULES"]
+__all__ = ["schedule", "fthenb", "one_f_one_b", "eager_1f1b", "zbh1", "vpp", "vpp_chunk", "vpp_mb", "SCHEDULES"]
 
 
 def fthenb(n_stages, stage, n_mb):
@@ -29,6 +29,21 @@ def one_f_one_b(n_stages, stage, n_mb):
     fi, bi = warm, 0
     while fi < n_mb:
         out += [("F", fi), ("B", bi)]
+        fi += 1
+        bi += 1
+    out += [("B", i) for i in range(bi, n_mb)]
+    return out
+
+
+def eager_1f1b(n_stages, stage, n_mb):
+    """1F1B with 2 * (stages - stage) - 1 warm-up forwards (reference pipeline_eager_1f1b.py): one more
+    activation in flight per hop than 1F1B, so a stage's next forward input is already on its way while it runs
+    a backward (send / receive overlap); steady phase B then F."""
+    warm = min(2 * (n_stages - stage) - 1, n_mb)
+    out = [("F", i) for i in range(warm)]
+    fi, bi = warm, 0
+    while fi < n_mb:
+        out += [("B", bi), ("F", fi)]
         fi += 1
         bi += 1
     out += [("B", i) for i in range(bi, n_mb)]
@@ -56,7 +71,31 @@ def zbh1(n_stages, stage, n_mb):
     return out
 
 
-SCHEDULES = {"FTHENB": fthenb, "1F1B": one_f_one_b, "ZBH1": zbh1}
+def vpp(n_stages, stage, n_mb, n_chunks):
+    """Interleaved 1F1B over ``n_chunks`` model chunks per stage (reference pipeline_vpp.py): jobs ("F", k) /
+    ("B", k) over virtual micro-steps k in [0, n_mb * n_chunks); vpp_chunk / vpp_mb map k to (chunk, micro-batch):
+    groups of ``n_stages`` micro-batches walk the chunks in order (forward) or reverse order (backward)."""
+    if n_mb % n_stages:
+        raise ValueError(f"accumulate_steps ({n_mb}) must be a multiple of the pipeline degree ({n_stages})")
+    total = n_mb * n_chunks
+    warm = min((n_stages - stage - 1) * 2 + (n_chunks - 1) * n_stages, total)
+    out = [("F", k) for k in range(warm)]
+    for i in range(total - warm):
+        out += [("F", warm + i), ("B", i)]
+    out += [("B", k) for k in range(total - warm, total)]
+    return out
+
+
+def vpp_chunk(k, n_stages, n_chunks, forward=True):
+    v = (k // n_stages) % n_chunks
+    return v if forward else n_chunks - 1 - v
+
+
+def vpp_mb(k, n_stages, n_chunks):
+    return (k // (n_stages * n_chunks)) * n_stages + k % n_stages
+
+
+SCHEDULES = {"FTHENB": fthenb, "1F1B": one_f_one_b, "EAGER1F1B": eager_1f1b, "ZBH1": zbh1}
 
 
 def schedule(mode, n_stages, stage, n_mb):

@@ -642,7 +642,9 @@ def _node_reads(n):
 
 def _node_writes(n):
     w = set(_refs(n.outs, []))
-    if _is_inplace(n):
+    if n.kind == "comm":
+        w |= set(_refs(n.args, []))  # a collective writes every tensor it is given (coalesced: all of them)
+    elif _is_inplace(n):
         w |= set(_refs(n.args[:1], []))  # in-place: the receiver is written
     return w
 

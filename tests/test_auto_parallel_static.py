@@ -194,6 +194,7 @@ def _reference():
     ((4, 1, 2), 4, "1F1B"),     # the reference's PP4 x TP2 configuration, 8 ranks
     ((2, 2, 2), 2, "FThenB"),   # pipeline x data x tensor parallel, 8 ranks
     ((2, 1, 2), 4, "ZBH1"),     # zero-bubble: weight gradients deferred into the cool-down
+    ((2, 1, 2), 4, "Eager1F1B"),  # 2 (pp - stage) - 1 warm-up forwards
 ])
 def test_static_auto_parallel_llama_matches_single_process(shape, acc, schedule):
     ref = _reference()

@@ -1,6 +1,8 @@
 """paddle.distributed.passes (reference python/paddle/distributed/passes/): pass registry / manager ordering,
 and each registered pass against the un-rewritten program: same fetched values (fusion, DCE), bf16 GEMMs
 with fp32 reductions (AMP), and k-step gradient merge == one step on the concatenated batch."""
+import os
+
 import numpy as np
 import pytest
 
@@ -180,3 +182,77 @@ def test_recompute_overlap_sharding_passes_mark_program(static_mode):
     assert not hasattr(main, "_pa_sharding")  # stage 3 fails _check_self: not applied
     dp.new_pass("auto_parallel_sharding", {"stage": 2, "sharding_mesh_dim": "dp"}).apply([main], [st])
     assert main._pa_tp_overlap and main._pa_sharding == {"stage": 2, "dim": "dp"}
+
+
+def test_bn_act_and_add_act_fusion_passes_keep_results(static_mode):
+    """fuse_bn_act / fuse_bn_add_act: batch_norm (+ residual) -> relu becomes one batch_norm_act_nhwc node;
+    fuse_elewise_add_act: x + b -> tanh GELU becomes one bias_gelu node. Same outputs and input gradients."""
+    paddle.set_device("cpu")
+    paddle.seed(3)
+    main, st = paddle.static.Program(), paddle.static.Program()
+    with paddle.static.program_guard(main, st):
+        x = paddle.static.data("x", [2, 4, 4, 8], "float32")
+        r = paddle.static.data("r", [2, 4, 4, 8], "float32")
+        x.stop_gradient = r.stop_gradient = False
+        bn1 = paddle.nn.BatchNorm2D(8, data_format="NHWC")
+        bn2 = paddle.nn.BatchNorm2D(8, data_format="NHWC")
+        y = paddle.nn.functional.relu(bn1(x) + r)
+        z = paddle.nn.functional.relu(bn2(x))
+        b = paddle.create_parameter([8], "float32")
+        g = paddle.nn.functional.gelu(x + b, approximate=True)
+        loss = (y * y).mean() + z.mean() + (g * g).mean()
+        gx, gr = paddle.static.gradients([loss], [x, r])
+    exe = paddle.static.Executor(paddle.CPUPlace())
+    rs = np.random.RandomState(0)
+    feed = {"x": rs.randn(2, 4, 4, 8).astype("float32"), "r": rs.randn(2, 4, 4, 8).astype("float32")}
+    ref = exe.run(main, feed=feed, fetch_list=[y, z, g, gx, gr])
+    names0 = [n.name.split(":")[-1] for n in main.nodes]
+    ctx = dp.PassManager([dp.new_pass("fuse_bn_add_act"), dp.new_pass("fuse_bn_act"),
+                          dp.new_pass("fuse_elewise_add_act")]).apply([main], [st])
+    names = [n.name.split(":")[-1] for n in main.nodes]
+    got = exe.run(main, feed=feed, fetch_list=[y, z, g, gx, gr])
+    assert ctx.get_attr("fuse_bn_add_act.fused") == 1 and ctx.get_attr("fuse_bn_act.fused") == 1
+    assert ctx.get_attr("fuse_elewise_add_act.fused") == 1
+    assert names0.count("relu") == 2 and names.count("relu") == 0 and "bias_gelu" in names
+    assert names.count("batch_norm_act_nhwc") == 2
+    for a, e in zip(got, ref):
+        np.testing.assert_allclose(a, e, rtol=1e-5, atol=1e-5)
+
+
+def _fuse_ar_worker(rank, world, port, q):
+    import sys as _s
+    _s.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_distributed_cpu import _setup
+    paddle = _setup(rank, world, port)
+    from paddlepaddle_amd.distributed import passes as dps
+    paddle.enable_static()
+    main, st = paddle.static.Program(), paddle.static.Program()
+    with paddle.static.program_guard(main, st):
+        a = paddle.static.data("a", [3, 4], "float32")
+        b = paddle.static.data("b", [5], "float32")
+        c = paddle.static.data("c", [2], "float32")
+        ha, hb, hc = a * 2.0, b + 1.0, c * 1.0
+        for t in (ha, hb, hc):
+            paddle.distributed.all_reduce(t)
+        out = ha.sum() + hb.sum() + hc.sum()
+    exe = paddle.static.Executor(paddle.CPUPlace())
+    feed = {"a": np.full((3, 4), rank + 1, "float32"), "b": np.full((5,), rank, "float32"),
+            "c": np.full((2,), 3 * rank, "float32")}
+    ref = exe.run(main, feed=feed, fetch_list=[ha, hb, hc, out])
+    ctx = dps.new_pass("fuse_all_reduce").apply([main], [st])
+    got = exe.run(main, feed=feed, fetch_list=[ha, hb, hc, out])
+    names = [n.name for n in main.nodes if n.kind == "comm"]
+    paddle.disable_static()
+    q.put((rank, ctx.get_attr("fuse_all_reduce.fused"), names, [g.tolist() for g in got],
+           [r.tolist() for r in ref]))
+
+
+def test_fuse_all_reduce_pass_coalesces_collectives():
+    """fuse_all_reduce: three consecutive static all-reduces become one coalesced all-reduce (gloo, 2 ranks)
+    with the same results."""
+    from test_distributed_cpu import _spawn
+    res = _spawn(_fuse_ar_worker, world=2)
+    for rank, fused, names, got, ref in res:
+        assert fused == 2 and names == ["c:all_reduce_coalesced"], (fused, names)
+        assert got == ref
+        assert ref[0][0][0] == 6.0 and ref[1][0] == 1 + 2 and ref[2][0] == 3.0

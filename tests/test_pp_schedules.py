@@ -24,8 +24,50 @@ def test_job_lists_are_valid(p, n):
                 pend.discard(mb)
             peak = max(peak, len(pend))
         assert peak <= warm + 1
+        eager = S.eager_1f1b(p, s, n)
+        S.check(eager, n, False)
+        # 2 (p - s) - 1 forwards before the first backward (capped by the micro-batch count)
+        assert [k for k, _ in eager[:min(2 * (p - s) - 1, n)]] == ["F"] * min(2 * (p - s) - 1, n)
     with pytest.raises(ValueError):
         S.schedule("nope", 2, 0, 2)
+
+
+@pytest.mark.parametrize("p,n,v", [(2, 2, 2), (2, 4, 2), (4, 8, 2), (4, 4, 3)])
+def test_vpp_job_lists_cover_every_chunk(p, n, v):
+    for s in range(p):
+        jobs = S.vpp(p, s, n, v)
+        fw = [(S.vpp_mb(k, p, v), S.vpp_chunk(k, p, v, True)) for kind, k in jobs if kind == "F"]
+        bw = [(S.vpp_mb(k, p, v), S.vpp_chunk(k, p, v, False)) for kind, k in jobs if kind == "B"]
+        assert sorted(fw) == sorted(bw) == sorted((m, c) for m in range(n) for c in range(v))
+        for m in range(n):  # chunks of a micro-batch run forward in order and backward in reverse order
+            assert [c for mb, c in fw if mb == m] == list(range(v))
+            assert [c for mb, c in bw if mb == m] == list(range(v))[::-1]
+    with pytest.raises(ValueError):
+        S.vpp(4, 0, 6, 2)
+
+
+def test_pipeline_scheduler_passes_build_job_lists():
+    """pipeline_scheduler_<mode> passes (reference pipeline_scheduler_pass/): the stage's job list, optimizer job
+    last, on the program and in the pass context."""
+    from paddlepaddle_amd.distributed.passes import new_pass
+    from paddlepaddle_amd.distributed.passes.pipeline_scheduler import OPT, job_pairs
+    from paddlepaddle_amd.static import program as P
+    fns = {"FThenB": S.fthenb, "1F1B": S.one_f_one_b, "Eager1F1B": S.eager_1f1b, "ZBH1": S.zbh1}
+    for name, fn in fns.items():
+        prog = P.Program()
+        ctx = new_pass(f"pipeline_scheduler_{name}", {"num_micro_batches": 8, "pp_stage": 1,
+                                                      "pp_degree": 4}).apply(prog, None)
+        jobs = ctx.get_attr("pipeline_scheduler.job_list")
+        assert jobs is prog._pa_jobs and jobs[-1].type() == OPT
+        assert job_pairs(jobs) == fn(4, 1, 8)
+    prog = P.Program()
+    ctx = new_pass("pipeline_scheduler_VPP", {"num_micro_batches": 4, "pp_stage": 0, "pp_degree": 2,
+                                              "vpp_degree": 2}).apply(prog, None)
+    jobs = ctx.get_attr("pipeline_scheduler.job_list")
+    assert len(jobs) == 2 * 4 * 2 + 1 and {j.chunk_id() for j in jobs[:-1]} == {0, 1}
+    # missing attributes: the pass does not apply
+    assert new_pass("pipeline_scheduler_1F1B").apply(P.Program(), None).get_attr(
+        "pipeline_scheduler.job_list") is None
 
 
 def test_deferred_weight_grads_equal_fused_backward():
