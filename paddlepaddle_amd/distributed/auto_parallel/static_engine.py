@@ -321,8 +321,12 @@ class StaticEngine:
                                f"ZBH1; virtual pipelines run on fleet PipelineParallelWithInterleave)")
         if strategy.sp_optimization.get("enable", False):
             unsupported.append("sp_optimization")
-        if strategy.gradient_merge.get("enable", False):
-            unsupported.append("gradient_merge (use strategy.pipeline.accumulate_steps)")
+        # strategy.gradient_merge (reference passes/auto_parallel_gradient_merge.py): gradients of k_steps calls
+        # accumulate; the k-th call (scaled by 1/k when avg) synchronises them and runs the optimizer
+        gm = strategy.gradient_merge
+        self.gm_k = max(1, int(gm.get("k_steps", 1))) if gm.get("enable", False) else 1
+        self.gm_avg = bool(gm.get("avg", True))
+        self._gm_count = 0
         if unsupported:
             raise NotImplementedError("static auto-parallel engine: unsupported strategy settings: " +
                                       ", ".join(unsupported))
@@ -1202,6 +1206,27 @@ class StaticEngine:
             dist.all_reduce(tot, group=self._pp_group())
         return tot[0]
 
+    def _scale_grads(self, f):
+        """Gradient merge with avg: the accumulated gradients (flat buffers when they exist) times ``f``."""
+        with torch.no_grad():
+            if getattr(self, "_zero", None):
+                for z in self._zero:
+                    z["gflat"].mul_(f)
+                # parameters outside the flat buffers (if any) keep autograd gradients
+            seen = {id(z["gflat"]) for z in (getattr(self, "_zero", None) or [])}
+            for p in self.opt._parameter_list:
+                g = p._t.grad
+                if g is None or id(g) in seen or self._in_flat(g):
+                    continue
+                g.mul_(f)
+
+    def _in_flat(self, g):
+        for z in getattr(self, "_zero", None) or []:
+            base = z["gflat"]
+            if g.untyped_storage().data_ptr() == base.untyped_storage().data_ptr():
+                return True
+        return False
+
     def _zero_step(self):
         """Reduce-scatter the accumulated flat gradients over dp, update the shards, all-gather the parameters
         (without ZeRO: all-reduce each flat gradient once and update the parameters as usual)."""
@@ -1422,11 +1447,15 @@ class StaticEngine:
         if nst > 1:  # every rank reports the loss of the last stage
             loss = loss.clone()
             dist.all_reduce(loss, group=self._pp_group())
-        if getattr(self, "_zero", None):
-            self._zero_step()
-        else:
-            self.opt.step()
-            self.opt.clear_grad()
+        self._gm_count += 1
+        if self._gm_count % self.gm_k == 0:
+            if self.gm_k > 1 and self.gm_avg:
+                self._scale_grads(1.0 / self.gm_k)
+            if getattr(self, "_zero", None):
+                self._zero_step()
+            else:
+                self.opt.step()
+                self.opt.clear_grad()
         from .. import collective_check as _cc
         if _cc.enabled():
             _cc.check_collectives("static engine step")

@@ -27,7 +27,8 @@ def _cfg():
     return LlamaConfig.tiny(num_hidden_layers=4, num_attention_heads=4, num_key_value_heads=2, **_FUSED)
 
 
-def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap=False, zero=False, checkpoints=None):
+def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap=False, zero=False, checkpoints=None,
+            gm=1):
     paddle = _setup(rank, world, port)
     import paddlepaddle_amd.distributed as dist
     from paddlepaddle_amd.models.llama_auto import LlamaForCausalLMAuto, LlamaPretrainingCriterionAuto
@@ -45,6 +46,9 @@ def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap
     strategy.recompute.enable = recompute
     if checkpoints:
         strategy.recompute["checkpoints"] = checkpoints
+    if gm > 1:
+        strategy.gradient_merge["enable"] = True
+        strategy.gradient_merge["k_steps"] = gm
     strategy.mp_optimization["allreduce_matmul_grad_overlapping"] = overlap
     if zero:
         strategy.sharding["enable"] = True
@@ -54,9 +58,12 @@ def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap
     assert dm._engine is not None
     ids = _data()
     losses = []
-    for _ in range(STEPS):
+    for _ in range(STEPS * gm):
         loss = dm(paddle.Tensor(ids[:, :-1]), paddle.Tensor(ids[:, 1:]))
         losses.append(float(loss))
+    if gm > 1:  # no update inside a merge window; k identical batches averaged == one step on that batch
+        np.testing.assert_allclose(losses[1::gm], losses[::gm], rtol=1e-6)
+        losses = losses[::gm]
     eng = dm._engine
     kinds = sorted({n.name for nodes in eng.stage_nodes for n in nodes if n.name in (
         "allreduce", "allgather", "slice", "copy_to_parallel")})
@@ -98,6 +105,10 @@ def _worker_cp(rank, world, port, shape, acc, schedule, q):
     _worker(rank, world, port, shape, acc, schedule, q, recompute=True, checkpoints=["layers.0", "layers.2"])
 
 
+def _worker_gm(rank, world, port, shape, acc, schedule, q):
+    _worker(rank, world, port, shape, acc, schedule, q, gm=2, zero=shape[1] > 1)
+
+
 def _worker_zero(rank, world, port, shape, acc, schedule, q):
     _worker(rank, world, port, shape, acc, schedule, q, zero=True)
 
@@ -108,6 +119,16 @@ def test_static_engine_zero_sharding_matches_single_process(shape, acc):
     rank's shard of the flat parameters, parameters all-gathered: same losses as single-process training."""
     ref = _reference()
     res = _spawn(_worker_zero, shape, acc, "1F1B", world=int(np.prod(shape)))
+    for rank, losses, kinds, stage in res:
+        np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-5, err_msg=f"rank {rank} stage {stage}")
+
+
+@pytest.mark.parametrize("shape,acc", [((1, 1, 2), 1), ((1, 2, 2), 2)])
+def test_static_engine_gradient_merge_matches_single_process(shape, acc):
+    """strategy.gradient_merge (k_steps 2, avg): the optimizer runs every second call on the averaged gradients
+    (also with ZeRO over dp); with the same batch each call this equals single-process training."""
+    ref = _reference()
+    res = _spawn(_worker_gm, shape, acc, "1F1B", world=int(np.prod(shape)))
     for rank, losses, kinds, stage in res:
         np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-5, err_msg=f"rank {rank} stage {stage}")
 
@@ -281,11 +302,16 @@ def test_static_engine_rejects_unimplemented_strategy_fields():
     cfg = _cfg()
     model = LlamaForCausalLMAuto(cfg)
     opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters())
-    for field, key in (("sp_optimization", "enable"), ("gradient_merge", "enable")):
+    for field, key in (("sp_optimization", "enable"),):
         st = dist.Strategy()
         getattr(st, field)[key] = True
         with pytest.raises(NotImplementedError, match=field):
             StaticEngine(model, LlamaPretrainingCriterionAuto(cfg), opt, st)
+    st = dist.Strategy()
+    st.pipeline.enable = True
+    st.pipeline.schedule_mode = "VPP"
+    with pytest.raises(NotImplementedError, match="schedule_mode"):
+        StaticEngine(model, LlamaPretrainingCriterionAuto(cfg), opt, st)
     st = dist.Strategy()
     st.recompute["enable"] = True
     st.recompute["refined_ops_patterns"] = [{"main_ops": ["matmul"], "num": 1}]

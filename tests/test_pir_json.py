@@ -217,3 +217,21 @@ def test_pir_control_flow_if_while(tmp_path, native):
         ey, en = _cf_expect(x, n)
         np.testing.assert_allclose(np.asarray(out.numpy()), ey, rtol=1e-6)
         assert int(np.asarray(steps.numpy()).reshape(-1)[0]) == en
+
+
+@pytest.mark.gpu
+def test_pir_control_flow_native_interpreter_gpu(tmp_path):
+    """The same while / if program on the GPU through the native interpreter (device-resident loop state; the
+    branch conditions are read back per iteration, as the reference's WhileInstruction does)."""
+    from paddlepaddle_amd.framework import native_interp
+    import torch
+    prefix = _cf_program(tmp_path)
+    runner = pir.load(prefix, device=torch.device("cuda:0"))
+    assert isinstance(runner, native_interp.NativeRunner)
+    for xs, n in (([1.0, -2.0, 3.0, 0.5], 3), ([-5.0, -1.0, 0.0, 1.0], 1)):
+        x = np.array(xs, "float32")
+        out, steps = runner.run({"x": x, "n": np.array([n], "int64")})
+        assert out._t.is_cuda
+        ey, en = _cf_expect(x, n)
+        np.testing.assert_allclose(out._t.cpu().numpy(), ey, rtol=1e-6)
+        assert int(steps._t.cpu().reshape(-1)[0]) == en
