@@ -34,6 +34,7 @@ from __future__ import annotations
 
 import contextlib
 import math
+import operator
 
 import numpy as np
 import torch
@@ -309,6 +310,7 @@ class StaticEngine:
         self.acc = max(1, int(pp.accumulate_steps)) if pp.enable else 1
         self.schedule = str(pp.schedule_mode).upper() if pp.enable else "1F1B"
         self.built = False
+        self._cnodes = {}  # id(local node) -> compiled argument builders (_compile_node)
         self.rank = C.get_rank()
         self._consts = {}
         # strategy fields this engine does not implement fail loudly instead of being ignored
@@ -541,12 +543,51 @@ class StaticEngine:
             self.stage_items.append(items)
 
     def _run_nodes(self, nodes, env):
+        cn = self._cnodes
         for nd in nodes:
-            args = self._materialize(nd.args, env)
-            kw = self._materialize(nd.kwargs, env)
-            out = nd.fn(*args, **kw)
-            if nd.outs is not None:
-                P._assign(nd.outs, out, env)
+            c = cn.get(id(nd))
+            if c is None:
+                c = cn[id(nd)] = self._compile_node(nd)
+            fn, sa, a, sk, k, oi, outs = c
+            out = fn(*(a if sa else a(env)), **(k if sk else k(env)))
+            if oi is not None:
+                env[oi] = out
+            elif outs is not None:
+                P._assign(outs, out, env)
+
+    def _compile_node(self, nd):
+        """Per-node argument builders, made once: what _materialize resolves on every call (process groups,
+        constants on the device, dX hooks, literals) is fixed up front, leaving only the slot lookups per run."""
+        sa, a = self._compile_tmpl(tuple(nd.args))
+        sk, k = self._compile_tmpl(dict(nd.kwargs))
+        oi = nd.outs.i if isinstance(nd.outs, P._Ref) else None
+        return nd.fn, sa, a, sk, k, oi, nd.outs
+
+    def _compile_tmpl(self, tmpl):
+        """(True, value) for a template without slot references, else (False, env -> value)."""
+        if isinstance(tmpl, P._Ref):
+            return False, operator.itemgetter(tmpl.i)
+        if isinstance(tmpl, tuple) and len(tmpl) == 3 and tmpl[0] == "G":
+            return True, self.groups.get(self.my_stage, tmpl[2])
+        if isinstance(tmpl, (P._Const, _HookT)) or tmpl is P._RUN_DEV:
+            return True, self._materialize(tmpl, None)
+        if isinstance(tmpl, (list, tuple)):
+            parts = [self._compile_tmpl(v) for v in tmpl]
+            mk = list if isinstance(tmpl, list) else tuple
+            if mk is tuple and all(st for st, _ in parts):
+                return True, tuple(v for _, v in parts)
+            return False, lambda env: mk([v if st else v(env) for st, v in parts])
+        if isinstance(tmpl, dict):
+            parts = {key: self._compile_tmpl(v) for key, v in tmpl.items()}
+            if all(st for st, _ in parts.values()):
+                return True, {key: v for key, (_, v) in parts.items()}
+            return False, lambda env: {key: (v if st else v(env)) for key, (st, v) in parts.items()}
+        if isinstance(tmpl, slice):
+            parts = [self._compile_tmpl(v) for v in (tmpl.start, tmpl.stop, tmpl.step)]
+            if all(st for st, _ in parts):
+                return True, slice(*(v for _, v in parts))
+            return False, lambda env: slice(*(v if st else v(env) for st, v in parts))
+        return True, tmpl
 
     def _run_segment(self, seg, env):
         import torch.utils.checkpoint as ckpt
