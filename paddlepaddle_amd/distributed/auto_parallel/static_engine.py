@@ -103,6 +103,12 @@ def _my(gr):
     return 0 if gr[1] is None else gr[1].index(C.get_rank())
 
 
+def gr_n(eng, stage, d):
+    """Size of mesh dim ``d`` of ``stage``'s mesh."""
+    m = eng.meshes[stage]
+    return int(m.shape[d])
+
+
 class _AllReduce(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gr, avg):
@@ -148,6 +154,28 @@ class _Slice(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         return _gather(g, ctx.gr, ctx.dim), None, None
+
+
+class _ReduceScatter(torch.autograd.Function):
+    """Partial -> Shard(dim) in one collective (strategy.sp_optimization; reference
+    passes/auto_parallel_sequence_parallel_optimization.py fuses the allreduce + split pair the same way): the
+    reduce-scatter moves 1/n of the all-reduce's bytes out of each rank. Backward: all-gather along ``dim``."""
+
+    @staticmethod
+    def forward(ctx, x, gr, dim, avg):
+        n = _nranks(gr)
+        ctx.gr, ctx.dim, ctx.scale = gr, dim, (1.0 / n if avg else 1.0)
+        xm = x.movedim(dim, 0).contiguous()
+        out = torch.empty((xm.shape[0] // n,) + tuple(xm.shape[1:]), dtype=x.dtype, device=x.device)
+        dist.reduce_scatter_tensor(out, xm, group=gr[0])
+        if avg:
+            out.mul_(ctx.scale)
+        return out.movedim(0, dim).contiguous()
+
+    @staticmethod
+    def backward(ctx, g):
+        g = _gather(g, ctx.gr, ctx.dim)
+        return (g * ctx.scale if ctx.scale != 1.0 else g), None, None, None
 
 
 class _ToPartial(torch.autograd.Function):
@@ -321,8 +349,9 @@ class StaticEngine:
         if self.schedule not in self._PASS_OF:
             unsupported.append(f"pipeline.schedule_mode {pp.schedule_mode!r} (one of FThenB / 1F1B / Eager1F1B / "
                                f"ZBH1; virtual pipelines run on fleet PipelineParallelWithInterleave)")
-        if strategy.sp_optimization.get("enable", False):
-            unsupported.append("sp_optimization")
+        # strategy.sp_optimization: Partial -> Shard reshards (a row-parallel output entering a sequence-parallel
+        # region) as one reduce-scatter (_ReduceScatter) instead of all-reduce + slice
+        self.sp_opt = bool(strategy.sp_optimization.get("enable", False))
         # strategy.gradient_merge (reference passes/auto_parallel_gradient_merge.py): gradients of k_steps calls
         # accumulate; the k-th call (scaled by 1/k when avg) synchronises them and runs the optimizer
         gm = strategy.gradient_merge
@@ -723,6 +752,14 @@ class StaticEngine:
             if h == w:
                 continue
             gr = ("G", stage, d)
+            if _is_p(h) and _is_s(w) and self.sp_opt and gr_n(self, stage, d) > 1 and \
+                    shape[w[1]] % gr_n(self, stage, d) == 0 and all(
+                        not _is_s(pl[e]) or pl[e][1] != w[1] for e in range(len(pl)) if e != d):
+                out = self._new()  # Partial -> Shard: one reduce-scatter instead of all-reduce + slice
+                self._emit(stage, "reduce_scatter", _ReduceScatter.apply, (P._Ref(cur), gr, w[1], h[1] == "avg"),
+                           out)
+                cur, pl[d] = out, w
+                continue
             if _is_p(h):
                 out = self._new()
                 self._emit(stage, "allreduce", _AllReduce.apply, (P._Ref(cur), gr, h[1] == "avg"), out)

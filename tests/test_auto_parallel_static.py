@@ -302,11 +302,6 @@ def test_static_engine_rejects_unimplemented_strategy_fields():
     cfg = _cfg()
     model = LlamaForCausalLMAuto(cfg)
     opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters())
-    for field, key in (("sp_optimization", "enable"),):
-        st = dist.Strategy()
-        getattr(st, field)[key] = True
-        with pytest.raises(NotImplementedError, match=field):
-            StaticEngine(model, LlamaPretrainingCriterionAuto(cfg), opt, st)
     st = dist.Strategy()
     st.pipeline.enable = True
     st.pipeline.schedule_mode = "VPP"
