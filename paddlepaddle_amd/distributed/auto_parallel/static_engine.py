@@ -344,8 +344,7 @@ class StaticEngine:
         # strategy fields this engine does not implement fail loudly instead of being ignored
         unsupported = []
         self.recompute = bool(strategy.recompute.get("enable", False))
-        if self.recompute and strategy.recompute.get("refined_ops_patterns"):
-            unsupported.append("recompute.refined_ops_patterns (selective recompute)")
+        self.refined = list(strategy.recompute.get("refined_ops_patterns") or []) if self.recompute else []
         if self.schedule not in self._PASS_OF:
             unsupported.append(f"pipeline.schedule_mode {pp.schedule_mode!r} (one of FThenB / 1F1B / Eager1F1B / "
                                f"ZBH1; virtual pipelines run on fleet PipelineParallelWithInterleave)")
@@ -532,11 +531,16 @@ class StaticEngine:
         skip = set(int(i) for i in (self.strategy.recompute.get("no_recompute_segments") or []))
         self.stage_items = []
         self.n_segments = 0
+        self.refined_kept = 0
         seg_index = {}
         for s, nodes in enumerate(self.stage_nodes):
+            kept = self._refined_excluded(nodes)
+            self.refined_kept += len(kept)
             runs, cur, cur_rc = [], [], None
             for nd in nodes:
                 rc = nd.rc if (self.recompute and nd.outs is not None) else None  # in-place ops stay outside
+                if id(nd) in kept:
+                    rc = None  # selective recompute: this op's output is kept, the segment splits around it
                 if rc is not None and rc == cur_rc:
                     cur.append(nd)
                     continue
@@ -570,6 +574,44 @@ class StaticEngine:
                 items.append(_Seg(run, inputs, outputs))
                 self.n_segments += 1
             self.stage_items.append(items)
+
+    # reference op names of refined_ops_patterns -> the node names they cover here
+    _REFINED_ALIASES = {
+        "matmul": {"fused_linear", "matmul", "mm", "linear", "multi_linear"},
+        "matmul_v2": {"fused_linear", "matmul", "mm", "linear", "multi_linear"},
+        "flash_attn": {"flash_attention", "qkv_rope_attention", "scaled_dot_product_attention", "flash_attn"},
+        "fused_rope": {"fused_rotary_position_embedding", "apply_rotary_pos_emb", "rope"},
+        "softmax": {"softmax"}, "swiglu": {"swiglu"}, "rms_norm": {"rms_norm", "rms_norm_residual"},
+    }
+
+    def _refined_excluded(self, nodes):
+        """strategy.recompute.refined_ops_patterns (reference auto_parallel_recompute.py selective recompute): per
+        recompute segment, the first ``num`` ops (-1: all) matching ``main_ops`` — with ``pre_ops`` / ``suf_ops``
+        as the ops right before / after, when given — are left out of the recompute; their outputs are kept."""
+        if not self.refined:
+            return set()
+        names = [_short(nd.name) for nd in nodes]
+
+        def hit(pat_ops, name):
+            return any(name == o or name in self._REFINED_ALIASES.get(o, ()) for o in pat_ops)
+        out, count = set(), {}
+        for pi, pat in enumerate(self.refined):
+            main = list(pat.get("main_ops") or [])
+            pre, suf = list(pat.get("pre_ops") or []), list(pat.get("suf_ops") or [])
+            num = int(pat.get("num", -1))
+            for k, nd in enumerate(nodes):
+                if nd.rc is None or not hit(main, names[k]):
+                    continue
+                if pre and not (k > 0 and nodes[k - 1].rc == nd.rc and hit(pre, names[k - 1])):
+                    continue
+                if suf and not (k + 1 < len(nodes) and nodes[k + 1].rc == nd.rc and hit(suf, names[k + 1])):
+                    continue
+                c = count.get((pi, nd.rc), 0)
+                if num >= 0 and c >= num:
+                    continue
+                count[(pi, nd.rc)] = c + 1
+                out.add(id(nd))
+        return out
 
     def _run_nodes(self, nodes, env):
         cn = self._cnodes

@@ -28,7 +28,7 @@ def _cfg():
 
 
 def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap=False, zero=False, checkpoints=None,
-            gm=1):
+            gm=1, refined=None):
     paddle = _setup(rank, world, port)
     import paddlepaddle_amd.distributed as dist
     from paddlepaddle_amd.models.llama_auto import LlamaForCausalLMAuto, LlamaPretrainingCriterionAuto
@@ -46,6 +46,8 @@ def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap
     strategy.recompute.enable = recompute
     if checkpoints:
         strategy.recompute["checkpoints"] = checkpoints
+    if refined:
+        strategy.recompute["refined_ops_patterns"] = refined
     if gm > 1:
         strategy.gradient_merge["enable"] = True
         strategy.gradient_merge["k_steps"] = gm
@@ -88,6 +90,8 @@ def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap
         assert eng.pass_stats_rc == len(checkpoints), eng.pass_stats_rc
         segs = [it for it in eng.stage_items[eng.my_stage] if isinstance(it, _Seg)]
         assert segs, eng.stage_items[eng.my_stage]
+    elif refined:  # the first matmul of every layer segment is kept: each layer splits into two segments
+        assert eng.refined_kept == cfg.num_hidden_layers, eng.refined_kept  # counted over all stages
     elif recompute:  # every decoder layer of this stage runs as one checkpointed segment
         from paddlepaddle_amd.distributed.auto_parallel.static_engine import _Seg
         segs = [it for it in eng.stage_items[eng.my_stage] if isinstance(it, _Seg)]
@@ -109,6 +113,10 @@ def _worker_gm(rank, world, port, shape, acc, schedule, q):
     _worker(rank, world, port, shape, acc, schedule, q, gm=2, zero=shape[1] > 1)
 
 
+def _worker_refined(rank, world, port, shape, acc, schedule, q):
+    _worker(rank, world, port, shape, acc, schedule, q, recompute=True, refined=[{"main_ops": ["matmul"], "num": 1}])
+
+
 def _worker_zero(rank, world, port, shape, acc, schedule, q):
     _worker(rank, world, port, shape, acc, schedule, q, zero=True)
 
@@ -119,6 +127,16 @@ def test_static_engine_zero_sharding_matches_single_process(shape, acc):
     rank's shard of the flat parameters, parameters all-gathered: same losses as single-process training."""
     ref = _reference()
     res = _spawn(_worker_zero, shape, acc, "1F1B", world=int(np.prod(shape)))
+    for rank, losses, kinds, stage in res:
+        np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-5, err_msg=f"rank {rank} stage {stage}")
+
+
+@pytest.mark.parametrize("shape,acc", [((1, 1, 2), 1), ((2, 1, 2), 2)])
+def test_static_engine_selective_recompute_matches_single_process(shape, acc):
+    """strategy.recompute.refined_ops_patterns: the first matmul of every recompute segment is kept (not
+    recomputed); the segment splits around it and training matches the single process."""
+    ref = _reference()
+    res = _spawn(_worker_refined, shape, acc, "1F1B", world=int(np.prod(shape)))
     for rank, losses, kinds, stage in res:
         np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-5, err_msg=f"rank {rank} stage {stage}")
 
@@ -307,8 +325,4 @@ def test_static_engine_rejects_unimplemented_strategy_fields():
     st.pipeline.schedule_mode = "VPP"
     with pytest.raises(NotImplementedError, match="schedule_mode"):
         StaticEngine(model, LlamaPretrainingCriterionAuto(cfg), opt, st)
-    st = dist.Strategy()
-    st.recompute["enable"] = True
-    st.recompute["refined_ops_patterns"] = [{"main_ops": ["matmul"], "num": 1}]
-    with pytest.raises(NotImplementedError, match="refined_ops_patterns"):
-        StaticEngine(model, LlamaPretrainingCriterionAuto(cfg), opt, st)
+
