@@ -295,7 +295,7 @@ def llama_static_bench(args, paddle, world, dist_on):
     log(f"[llama-static] {args.model} pp{pp} tp{tp} dp{dp}: loss={float(state['loss']):.4f} "
         f"step={dt / args.steps * 1000:.1f}ms tokens/s={tps:.0f} MFU={mfu * 100:.1f}% peak_mem={mem:.1f}GiB "
         f"params={cfg.num_params() / 1e9:.2f}B passes={getattr(eng, 'pass_stats', {})} "
-        f"recompute_segments={getattr(eng, 'n_segments', 0)}")
+        f"recompute_segments={getattr(eng, 'n_segments', 0)} fused_grad_params={getattr(eng, 'fused_grads', 0)}")
     return tps, dt / args.steps * 1000, gb, mfu
 
 

@@ -292,6 +292,10 @@ class _HookT:
         self.d = d
 
 
+def _grad_ready_noop(w):
+    """Main-grad ready callback of the engine's parameters: gradients are consumed at the end of the step."""
+
+
 def _dx_allreduce_hook(pg):
     def hook(dx):
         return dist.all_reduce(dx, group=pg, async_op=True).wait
@@ -1306,12 +1310,13 @@ class StaticEngine:
     def _zero_param_sq(self, params):
         """Grad-norm^2 of the shards: each group's shard sum of squares, summed over the dp ranks (the shards
         partition the flat gradient), over the tensor-parallel dims the group is sharded on, and over stages."""
+        from ...ops.optim import global_sq_norm
         tot = None
         for z in self._zero:
             g = z["shard"]._t.grad
             if g is None:
                 continue
-            sq = g.float().pow(2).sum().reshape(1)
+            sq = global_sq_norm([g]).reshape(1).float()
             if self._zero_pg is not None:
                 dist.all_reduce(sq, group=self._zero_pg)
             for d, pls in enumerate(z["pl"]):
@@ -1325,6 +1330,29 @@ class StaticEngine:
         if len(self.meshes) > 1 and dist.is_initialized():
             dist.all_reduce(tot, group=self._pp_group())
         return tot[0]
+
+    def _fuse_grads(self):
+        """Fused gradient accumulation (as fleet's ops.linear.fuse_grad_accumulation): every local linear / norm
+        weight's .grad (a view of the flat gradient buffer when there is one) is registered as its main grad, so
+        the weight-gradient GEMMs of the accumulation micro-batches add into it in their epilogue (norms: their
+        backward kernels add the column sums) instead of autograd allocating a fresh dW per micro-batch and adding
+        it into .grad. Re-registers only buffers an optimizer replaced. FLAGS_fused_grad_accumulation=0: off."""
+        from ...framework.flags import flag
+        if not flag("FLAGS_fused_grad_accumulation", True):
+            return
+        from ...ops.linear import _main_grad_of, register_main_grad
+        self.fused_grads = 0
+        for p in self.local_params.values():
+            t = p._t
+            if not (t.requires_grad and t.is_leaf and t.is_cuda and t.dim() in (1, 2)
+                    and t.dtype in (torch.bfloat16, torch.float16)):
+                continue
+            if t.grad is None:
+                t.grad = torch.zeros_like(t)
+            ent = _main_grad_of(t)
+            if ent is None or ent[1].data_ptr() != t.grad.data_ptr():
+                register_main_grad(t, t.grad, _grad_ready_noop)
+            self.fused_grads += 1
 
     def _scale_grads(self, f):
         """Gradient merge with avg: the accumulated gradients (flat buffers when they exist) times ``f``."""
@@ -1374,23 +1402,27 @@ class StaticEngine:
 
     def _param_sq(self, params):
         """Global grad-norm^2: sharded params summed over their mesh dims, replicated ones counted once,
-        stages summed over the pipeline."""
+        stages summed over the pipeline. Parameters sharded over the same mesh dims form one group: one
+        multi-tensor sum-of-squares launch (ops.optim.global_sq_norm) and one all-reduce per sharded dim."""
+        from ...ops.optim import global_sq_norm
         dev = params[0]._t.device if params else torch.device("cpu")
-        tot = torch.zeros(1, dtype=torch.float32, device=dev)
         by_id = {id(p): s for s, p in self.local_params.items()}
+        groups = {}
         for p in params:
             g = p._t.grad
             if g is None:
                 continue
+            dims = ()
             slot = by_id.get(id(p))
-            sq = g.float().pow(2).sum().reshape(1)
             if slot is not None:
-                inf = self.info[slot]
-                for d, pl in enumerate(inf.pl):
-                    if _is_s(pl):
-                        gr = self.groups.get(self.my_stage, d)
-                        if gr[0] is not None:
-                            dist.all_reduce(sq, group=gr[0])
+                dims = tuple(d for d, pl in enumerate(self.info[slot].pl)
+                             if _is_s(pl) and self.groups.get(self.my_stage, d)[0] is not None)
+            groups.setdefault(dims, []).append(g)
+        tot = torch.zeros(1, dtype=torch.float32, device=dev)
+        for dims, gs in groups.items():
+            sq = global_sq_norm(gs).reshape(1).float()
+            for d in dims:
+                dist.all_reduce(sq, group=self.groups.get(self.my_stage, d)[0])
             tot += sq
         if len(self.meshes) > 1 and dist.is_initialized():
             # sum over the stages: ranks with the same coordinate in every stage mesh
@@ -1532,6 +1564,7 @@ class StaticEngine:
             self._p2p = _P2P(self.dev)  # built once on every rank (its host twin is a collective group creation)
         p2p = self._p2p
         p2p.begin_run()
+        self._fuse_grads()
         nst = len(self.meshes)
         s = self.my_stage
         n = self.acc
