@@ -64,8 +64,10 @@ __device__ __forceinline__ void stage_op(const uint8_t* __restrict__ g, int64_t 
 __device__ __forceinline__ i32x8 frag(const char* img, int rbase, int lane) {
   const int row = rbase + (lane & 15);
   const int c0 = 2 * (lane >> 4), sw = (row >> 1) & 7;
-  const uint4 lo = *reinterpret_cast<const uint4*>(img + row * 128 + ((c0 ^ sw) << 4));
-  const uint4 hi = *reinterpret_cast<const uint4*>(img + row * 128 + (((c0 + 1) ^ sw) << 4));
+  // chunks c0, c0 + 1 (c0 even) sit at (c0 ^ sw) and (c0 ^ sw) ^ 1: the second address is the first XOR 16
+  const int off = row * 128 + ((c0 ^ sw) << 4);
+  const uint4 lo = *reinterpret_cast<const uint4*>(img + off);
+  const uint4 hi = *reinterpret_cast<const uint4*>(img + (off ^ 16));
   i32x8 f;
   f[0] = (int)lo.x; f[1] = (int)lo.y; f[2] = (int)lo.z; f[3] = (int)lo.w;
   f[4] = (int)hi.x; f[5] = (int)hi.y; f[6] = (int)hi.z; f[7] = (int)hi.w;
@@ -165,6 +167,287 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_kernel(Fp8Args p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Ping-pong fp8 kernel: gemm.hip's 256x256 8-phase schedule (gemm256_kernel) at the fp8 byte geometry. A K-tile
+// of 128 fp8 is 128 bytes per row — the bf16 kernel's 64-element tile byte for byte — so the staging (four 16-KiB
+// half-tiles per K-tile, each issued six phases ahead by global_load_lds), the counted vmcnt waits, the barrier
+// stagger of the wm == 1 waves (one wave per SIMD in its MFMA cluster while the other reads LDS) and the LDS
+// swizzle are unchanged; per phase a wave runs 8 v_mfma_scale_f32_16x16x128_f8f6f4 (= the 16 bf16 16x16x32
+// MFMAs' cycles at twice the FLOPs). Fragments: lane l holds row (l & 15) and k-bytes [32 (l >> 4), +32) of the
+// 128-byte row (chunks 2g, 2g + 1). Wave (wm, wn) owns rows {wm*64.., 128+wm*64..} x cols {wn*32.., 128+wn*32..}.
+// Epilogue: alpha, bias, activation in registers, the 16-bit tile staged through LDS, 16-byte row stores
+// (N % 8 == 0).
+__device__ __forceinline__ void bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __forceinline__ void vm_wait(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// one half-tile: 128 rows x 128 k-bytes -> LDS [128][128 B], chunk c of row r at c ^ ((r >> 1) & 7); 2 glds / lane
+__device__ __forceinline__ void stage_half8(const uint8_t* __restrict__ g, int64_t ld, int r0, int rmax, int k0,
+                                            char* img, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = i * 8 + wave;
+    const int row = q * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ ((row >> 1) & 7);
+    int gr = r0 + row;
+    gr = gr < rmax ? gr : rmax - 1;
+    glds16(g + (int64_t)gr * ld + k0 + lc * 16, img + q * 1024);
+  }
+}
+
+// C += B-frag x A-frag on the unscaled v_mfma_f32_16x16x128_f8f6f4 (formats in cbsz / blgp); PA_FP8_SCALED_MFMA
+// selects the block-scaled form with unit E8M0 scales instead (the builtin: an extra scale operand pair).
+template <int FA, int FB>
+__device__ __forceinline__ f32x4 mfma8(const i32x8& b, const i32x8& a, f32x4 c) {
+#ifdef PA_FP8_SCALED_MFMA
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(b, a, c, FB, FA, 0, 127, 0, 127);
+#else
+  if constexpr (FB == 0 && FA == 0) {
+    asm("v_mfma_f32_16x16x128_f8f6f4 %0, %1, %2, %0" : "+v"(c) : "v"(b), "v"(a));
+  } else if constexpr (FB == 1 && FA == 0) {
+    asm("v_mfma_f32_16x16x128_f8f6f4 %0, %1, %2, %0 cbsz:1" : "+v"(c) : "v"(b), "v"(a));
+  } else if constexpr (FB == 0 && FA == 1) {
+    asm("v_mfma_f32_16x16x128_f8f6f4 %0, %1, %2, %0 blgp:1" : "+v"(c) : "v"(b), "v"(a));
+  } else {
+    asm("v_mfma_f32_16x16x128_f8f6f4 %0, %1, %2, %0 cbsz:1 blgp:1" : "+v"(c) : "v"(b), "v"(a));
+  }
+  return c;
+#endif
+}
+
+template <int V>
+struct IntC {
+  static constexpr int value = V;
+};
+
+constexpr int kPPThreads = 512;
+constexpr int kEpiRS = 264;  // 16-bit values per row of the epilogue image (528-byte rows)
+
+template <int FA, int FB, bool OUT_F16>
+__global__ __launch_bounds__(kPPThreads, 1) void gemm_fp8_pp_kernel(Fp8Args p) {
+  constexpr int HALF = 128 * kKB;  // 16 KiB
+  constexpr int STAGE = 4 * HALF;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int pid = xcd_remap((int)blockIdx.x, nwg);
+  constexpr int GM = 8;
+  const int per_group = GM * p.tiles_n;
+  const int first_m = (pid / per_group) * GM;
+  const int gsz = min(p.tiles_m - first_m, GM);
+  const int tm = first_m + (pid % per_group) % gsz;
+  const int tn = (pid % per_group) / gsz;
+  const int m0 = tm * kTile, n0 = tn * kTile;
+  const int nk = p.K / kKB;
+
+  auto stage_h = [&](int t, int h, char* dst) {
+    const int k0 = t * kKB;
+    if (h == 0 || h == 2) stage_half8(p.a, p.lda, m0 + (h == 2 ? 128 : 0), p.M, k0, dst, wave, lane);
+    else stage_half8(p.b, p.ldb, n0 + (h == 3 ? 128 : 0), p.N, k0, dst, wave, lane);
+  };
+  auto issue = [&](int j) {
+    const int t = j >> 2, h = j & 3;
+    stage_h(t, h, smem + (t & 1) * STAGE + h * HALF);
+  };
+  auto issue_h = [&](int t, auto hc) {
+    constexpr int h = decltype(hc)::value;
+    stage_h(t, h, smem + (t & 1) * STAGE + h * HALF);
+  };
+
+  f32x4 acc[2][4][2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][i][b][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int last_j = 4 * nk - 1;
+  auto wait_for = [&](int phase, int jstar) {
+    const int issued = min(phase + 6, last_j);
+    vm_wait(2 * max(issued - jstar, 0));
+  };
+  const int npro = min(6, 4 * nk);
+#pragma unroll 1
+  for (int j = 0; j < npro; ++j) issue(j);
+  vm_wait(2 * max(min(5, last_j) - 1, 0));
+  bar();
+  const bool lag = __builtin_amdgcn_readfirstlane(wm) == 1;
+  if (lag) bar();
+
+  i32x8 af[4], bl[2], br[2];
+  const int ar = wm * 64, bc = wn * 32;
+
+  auto ktile = [&](int t, auto steady) {
+    constexpr bool S = decltype(steady)::value;
+    const char* buf = smem + (t & 1) * STAGE;
+    const int ph = 4 * t;
+    // phase 0: read A-top + B-left; MFMA (top, L)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bl[j] = frag(buf + HALF, bc + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = frag(buf, ar + i * 16, lane);
+    if (S) {
+      issue_h(t + 1, IntC<2>{});
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      if (ph + 6 <= last_j) issue(ph + 6);
+      wait_for(ph, ph + 3);
+    }
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[0][i][0][j] =
+            mfma8<FA, FB>(bl[j], af[i], acc[0][i][0][j]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // phase 1: read B-right; MFMA (top, R)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) br[j] = frag(buf + 3 * HALF, bc + j * 16, lane);
+    if (S) {
+      issue_h(t + 1, IntC<3>{});
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    } else {
+      if (ph + 7 <= last_j) issue(ph + 7);
+      wait_for(ph + 1, ph + 2);
+    }
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[0][i][1][j] =
+            mfma8<FA, FB>(br[j], af[i], acc[0][i][1][j]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // phase 2: read A-bottom; MFMA (bottom, L)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = frag(buf + 2 * HALF, ar + i * 16, lane);
+    if (S) issue_h(t + 2, IntC<0>{});
+    else if (ph + 8 <= last_j) issue(ph + 8);
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[1][i][0][j] =
+            mfma8<FA, FB>(bl[j], af[i], acc[1][i][0][j]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // phase 3: wait for H0 / H1 of tile t + 1; MFMA (bottom, R)
+    if (S) {
+      issue_h(t + 2, IntC<1>{});
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      if (ph + 9 <= last_j) issue(ph + 9);
+      if (t + 1 < nk) wait_for(ph + 3, ph + 5);
+    }
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[1][i][1][j] =
+            mfma8<FA, FB>(br[j], af[i], acc[1][i][1][j]);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+  };
+  const int nsteady = max(nk - 2, 0);
+  int t = 0;
+#pragma unroll 1
+  for (; t < nsteady; ++t) ktile(t, IntC<1>{});
+#pragma unroll 1
+  for (; t < nk; ++t) ktile(t, IntC<0>{});
+  if (!lag) bar();
+
+  // epilogue: alpha, bias, activation in registers; the 16-bit tile through LDS ([256][264]); row stores.
+  // The MFMAs are inline asm, so the compiler's hazard tracking does not see their results: wait out the
+  // MFMA -> VALU read latency of the last accumulators explicitly.
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  uint16_t* im = reinterpret_cast<uint16_t*>(smem);
+  bar();
+#pragma unroll
+  for (int bh = 0; bh < 2; ++bh)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = bh * 128 + bc + j * 16 + 4 * (lane >> 4);
+      float bq[4] = {0.f, 0.f, 0.f, 0.f};
+      if (p.bias && n0 + c < p.N) {
+        const uint2 braw = *reinterpret_cast<const uint2*>(p.bias + n0 + c);
+        if (OUT_F16) {
+          bq[0] = lo_f16(braw.x); bq[1] = hi_f16(braw.x); bq[2] = lo_f16(braw.y); bq[3] = hi_f16(braw.y);
+        } else {
+          bq[0] = lo_bf16(braw.x); bq[1] = hi_bf16(braw.x); bq[2] = lo_bf16(braw.y); bq[3] = hi_bf16(braw.y);
+        }
+      }
+#pragma unroll
+      for (int ah = 0; ah < 2; ++ah)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = ah * 128 + ar + i * 16 + (lane & 15);
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = act_f(acc[ah][i][bh][j][e] * p.alpha + bq[e], p.act);
+          *reinterpret_cast<uint2*>(im + r * kEpiRS + c) =
+              OUT_F16 ? make_uint2(pack_f16(v[0], v[1]), pack_f16(v[2], v[3]))
+                      : make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
+        }
+    }
+  bar();
+  const int ecb = (tid & 31) * 8, erb = tid >> 5;
+  const int nb_ = n0 + ecb;
+  if (nb_ < p.N) {
+#pragma unroll 4
+    for (int step = 0; step < 16; ++step) {
+      const int r = step * 16 + erb;
+      const int m = m0 + r;
+      if (m >= p.M) break;
+      *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(p.c) + (int64_t)m * p.ldc + nb_) =
+          *reinterpret_cast<const uint4*>(im + r * kEpiRS + ecb);
+    }
+  }
+}
+
+template <int FA, int FB, bool F16>
+int launch_pp(const Fp8Args& g, hipStream_t st) {
+  static bool attr = false;
+  // two 64-KiB stages; the epilogue image [256][264] x 2 B (132 KiB) reuses them and is the larger
+  constexpr int smem = (2 * 4 * 128 * kKB) > (kTile * kEpiRS * 2) ? (2 * 4 * 128 * kKB) : (kTile * kEpiRS * 2);
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_fp8_pp_kernel<FA, FB, F16>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm_fp8_pp_kernel<FA, FB, F16>), dim3(g.tiles_m * g.tiles_n), dim3(kPPThreads), smem, st, g);
+  return (int)hipGetLastError();
+}
+
 template <int FA, int FB, bool F16>
 int launch(const Fp8Args& g, hipStream_t st) {
   static bool attr = false;
@@ -179,9 +462,13 @@ int launch(const Fp8Args& g, hipStream_t st) {
 }
 
 template <int FA, int FB>
-int launch_out(const Fp8Args& g, int out_f16, hipStream_t st) {
+int launch_out(const Fp8Args& g, int out_f16, bool pp, hipStream_t st) {
+  if (pp) return out_f16 ? launch_pp<FA, FB, true>(g, st) : launch_pp<FA, FB, false>(g, st);
   return out_f16 ? launch<FA, FB, true>(g, st) : launch<FA, FB, false>(g, st);
 }
+
+// kernel choice: 0 auto (ping-pong when N % 8 == 0 and ldc % 8 == 0), 1 generic, 2 ping-pong (as auto)
+int g_fp8_kernel = 0;
 
 }  // namespace
 
@@ -200,8 +487,15 @@ PA_EXPORT int pa_gemm_fp8(const void* a, const void* b, void* c, const void* bia
   g.tiles_m = (int)((M + kTile - 1) / kTile);
   g.tiles_n = (int)((N + kTile - 1) / kTile);
   g.alpha = alpha; g.act = act;
-  if (fmt_a == 0 && fmt_b == 0) return launch_out<0, 0>(g, out_f16, st);
-  if (fmt_a == 0 && fmt_b == 1) return launch_out<0, 1>(g, out_f16, st);
-  if (fmt_a == 1 && fmt_b == 0) return launch_out<1, 0>(g, out_f16, st);
-  return launch_out<1, 1>(g, out_f16, st);
+  const bool pp = g_fp8_kernel != 1 && N % 8 == 0 && ldc % 8 == 0;
+  if (fmt_a == 0 && fmt_b == 0) return launch_out<0, 0>(g, out_f16, pp, st);
+  if (fmt_a == 0 && fmt_b == 1) return launch_out<0, 1>(g, out_f16, pp, st);
+  if (fmt_a == 1 && fmt_b == 0) return launch_out<1, 0>(g, out_f16, pp, st);
+  return launch_out<1, 1>(g, out_f16, pp, st);
+}
+
+// 0 auto, 1 generic kernel only (A/B and tests)
+PA_EXPORT int pa_gemm_fp8_set_kernel(int k) {
+  g_fp8_kernel = k;
+  return 0;
 }

@@ -32,6 +32,18 @@ def hip_ok(a, b_nk, bias, out_dtype):
             and b_nk.data_ptr() % 16 == 0 and (bias is None or bias.is_contiguous()))
 
 
+def set_kernel(kind):
+    """fp8 GEMM kernel choice: "auto" (the ping-pong 256x256 schedule when N % 8 == 0, else the generic kernel) or
+    "generic"; returns the previous choice (A/B measurements and tests)."""
+    global _KERNEL
+    old, _KERNEL = _KERNEL, kind
+    L.call("pa_gemm_fp8_set_kernel", {"auto": 0, "generic": 1}[kind])
+    return old
+
+
+_KERNEL = "auto"
+
+
 def gemm_fp8(a, b_nk, bias=None, alpha=1.0, act="identity", out_dtype=torch.float16):
     """a [M, K] and b_nk [N, K] fp8 (both K-major) -> [M, N] in out_dtype."""
     if act not in _ACT:

@@ -66,6 +66,29 @@ def test_fp8_gemm_matches_dequantised_reference_gpu(fa, fb, odt, act, bias, shap
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(300, 264, 384), (1000, 2048, 1280), (256, 256, 128), (77, 520, 256),
+                                   (513, 776, 896)])
+@pytest.mark.parametrize("kernel", ["auto", "generic"])
+def test_fp8_gemm_kernels_exact_on_small_integers_gpu(shape, kernel):
+    """Both fp8 kernels — the ping-pong 256x256 schedule (auto, N % 8 == 0) and the generic one — exact on
+    small-integer data: ragged M / N tiles, a single K-tile (K = 128) and two (K = 256)."""
+    from paddlepaddle_amd.ops import fp8 as F8
+    M, N, K = shape
+    g = torch.Generator().manual_seed(5)
+    a = torch.randint(-3, 4, (M, K), generator=g).float()
+    b = torch.randint(-2, 3, (N, K), generator=g).float()
+    bias = torch.randint(-4, 5, (N,), generator=g).float()
+    a8, b8 = a.to(torch.float8_e4m3fn).cuda(), b.to(torch.float8_e4m3fn).cuda()
+    old = F8.set_kernel(kernel)
+    try:
+        out = gemm_fp8(a8, b8, bias.to(torch.bfloat16).cuda(), 0.5, "relu", torch.bfloat16)
+    finally:
+        F8.set_kernel(old)
+    ref = torch.relu(0.5 * (a @ b.t()) + bias)
+    torch.testing.assert_close(out.float().cpu(), ref.to(torch.bfloat16).float(), rtol=0, atol=0)
+
+
+@pytest.mark.gpu
 def test_fp8_fused_api_weight_layouts_gpu():
     g = torch.Generator().manual_seed(3)
     x = torch.randn(2, 96, 512, generator=g).to(torch.float8_e4m3fn).cuda()

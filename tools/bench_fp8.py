@@ -5,6 +5,7 @@ import sys
 import torch
 
 sys.path.insert(0, ".")
+from paddlepaddle_amd.ops import fp8 as F8  # noqa: E402
 from paddlepaddle_amd.ops.fp8 import gemm_fp8  # noqa: E402
 
 
@@ -34,9 +35,13 @@ def main():
         bf16 = lambda: torch.mm(a16, b16.t())  # noqa: E731
         ref = (a.float() @ b.float().t())
         err = ((mine().float() - ref).abs().max() / ref.abs().max()).item()
-        res = {"mine": [], "hipblaslt_fp8": [], "hipblaslt_bf16": []}
+        del ref
+        res = {"mine": [], "mine_generic": [], "hipblaslt_fp8": [], "hipblaslt_bf16": []}
         for _ in range(3):
             res["mine"].append(timeit(mine))
+            F8.set_kernel("generic")
+            res["mine_generic"].append(timeit(mine))
+            F8.set_kernel("auto")
             try:
                 res["hipblaslt_fp8"].append(timeit(blas8))
             except RuntimeError as ex:
@@ -48,7 +53,7 @@ def main():
             t = min(v)
             line += f" {k} {fl / t / 1e9:6.0f} TF ({t:.3f} ms)"
         print(line + f" | err {err:.1e}", flush=True)
-        del a, b, a16, b16, ref
+        del a, b, a16, b16
 
 
 if __name__ == "__main__":
