@@ -40,6 +40,10 @@ struct Fp8Args {
   int tiles_m, tiles_n;
   float alpha;
   int act;  // 0 identity, 1 gelu (erf), 2 relu
+  // balanced tail (ping-pong kernel, as gemm.hip's): tiles [full_tiles, tiles) are cut along K into tail_split
+  // slices that write fp32 256 x 256 partials to tail_ws; gemm_fp8_tail_reduce_k sums them and applies the epilogue
+  int full_tiles, tail_split;
+  float* tail_ws;
 };
 
 __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
@@ -235,6 +239,78 @@ struct IntC {
   static constexpr int value = V;
 };
 
+// grouped tile order (8 m-tiles per group), as gemm.hip tile_coords
+__device__ __forceinline__ void tile_coords8(int pid, int tiles_m, int tiles_n, int* tm, int* tn) {
+  constexpr int GM = 8;
+  const int per_group = GM * tiles_n;
+  const int first_m = (pid / per_group) * GM;
+  const int gsz = min(tiles_m - first_m, GM);
+  *tm = first_m + (pid % per_group) % gsz;
+  *tn = (pid % per_group) / gsz;
+}
+
+// balanced-tail reduction: tail tile b = tile full_tiles + b; a thread sums the slices' partials of 4 columns and
+// applies the epilogue
+template <bool OUT_F16>
+__global__ __launch_bounds__(256) void gemm_fp8_tail_reduce_k(Fp8Args p) {
+  const int b = blockIdx.x;
+  int tm, tn;
+  tile_coords8(p.full_tiles + b, p.tiles_m, p.tiles_n, &tm, &tn);
+  const int e = (blockIdx.y * 256 + threadIdx.x) * 4;
+  const int r = e >> 8, c = e & 255;
+  const int m = tm * 256 + r, n = tn * 256 + c;
+  if (m >= p.M || n >= p.N) return;
+  const float* src = p.tail_ws + (int64_t)b * p.tail_split * 65536 + e;
+  float4 a = *reinterpret_cast<const float4*>(src);
+  for (int k = 1; k < p.tail_split; ++k) {
+    const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)k * 65536);
+    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+  }
+  float bq[4] = {0.f, 0.f, 0.f, 0.f};
+  if (p.bias) {
+    const uint2 braw = *reinterpret_cast<const uint2*>(p.bias + n);
+    if (OUT_F16) {
+      bq[0] = lo_f16(braw.x); bq[1] = hi_f16(braw.x); bq[2] = lo_f16(braw.y); bq[3] = hi_f16(braw.y);
+    } else {
+      bq[0] = lo_bf16(braw.x); bq[1] = hi_bf16(braw.x); bq[2] = lo_bf16(braw.y); bq[3] = hi_bf16(braw.y);
+    }
+  }
+  const float av[4] = {a.x, a.y, a.z, a.w};
+  float v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = act_f(av[q] * p.alpha + bq[q], p.act);
+  *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.c) + (int64_t)m * p.ldc + n) =
+      OUT_F16 ? make_uint2(pack_f16(v[0], v[1]), pack_f16(v[2], v[3]))
+              : make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
+}
+
+int device_cus8() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  return cus;
+}
+
+// tail plan: the remainder of the last whole wave of tiles is cut along K so the last wave fills the chip (only
+// when it covers at most half of it and every slice keeps at least 4 K-tiles of 128)
+void pp_plan8(int64_t M, int64_t N, int64_t K, int cus, int* full, int* split) {
+  const int64_t T = ((M + 255) / 256) * ((N + 255) / 256);
+  const int64_t nk = K / kKB;
+  *full = (int)T;
+  *split = 0;
+  if (T <= cus) return;
+  const int64_t r = T % cus;
+  if (r == 0 || 2 * r > cus) return;
+  int sp = 1;
+  while (r * sp * 2 <= cus && nk % (sp * 2) == 0 && nk / (sp * 2) >= 4) sp *= 2;
+  if (sp == 1) return;
+  *full = (int)(T - r);
+  *split = sp;
+}
+
 constexpr int kPPThreads = 512;
 constexpr int kEpiRS = 264;  // 16-bit values per row of the epilogue image (528-byte rows)
 
@@ -246,14 +322,22 @@ __global__ __launch_bounds__(kPPThreads, 1) void gemm_fp8_pp_kernel(Fp8Args p) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 2, wn = wave & 3;
 
-  const int nwg = p.tiles_m * p.tiles_n;
-  const int pid = xcd_remap((int)blockIdx.x, nwg);
-  constexpr int GM = 8;
-  const int per_group = GM * p.tiles_n;
-  const int first_m = (pid / per_group) * GM;
-  const int gsz = min(p.tiles_m - first_m, GM);
-  const int tm = first_m + (pid % per_group) % gsz;
-  const int tn = (pid % per_group) / gsz;
+  const int bid = (int)blockIdx.x;
+  int pid;
+  float* tail_out = nullptr;
+  if (p.tail_split > 0 && bid >= p.full_tiles) {  // K slice of a tail tile
+    const int u = bid - p.full_tiles;
+    const int ks = u % p.tail_split;
+    pid = p.full_tiles + u / p.tail_split;
+    p.K /= p.tail_split;
+    p.a += (int64_t)ks * p.K;
+    p.b += (int64_t)ks * p.K;
+    tail_out = p.tail_ws + (int64_t)u * 65536;
+  } else {
+    pid = xcd_remap(bid, p.tail_split > 0 ? p.full_tiles : p.tiles_m * p.tiles_n);
+  }
+  int tm, tn;
+  tile_coords8(pid, p.tiles_m, p.tiles_n, &tm, &tn);
   const int m0 = tm * kTile, n0 = tn * kTile;
   const int nk = p.K / kKB;
 
@@ -385,6 +469,24 @@ __global__ __launch_bounds__(kPPThreads, 1) void gemm_fp8_pp_kernel(Fp8Args p) {
   for (; t < nk; ++t) ktile(t, IntC<0>{});
   if (!lag) bar();
 
+  if (tail_out) {  // raw fp32 partial of this K slice, row-major 256 x 256
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#pragma unroll
+    for (int bh = 0; bh < 2; ++bh)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ah = 0; ah < 2; ++ah)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = ah * 128 + ar + i * 16 + (lane & 15);
+            const int c = bh * 128 + bc + j * 16 + 4 * (lane >> 4);
+            const f32x4 v = acc[ah][i][bh][j];
+            *reinterpret_cast<float4*>(tail_out + r * 256 + c) = make_float4(v[0], v[1], v[2], v[3]);
+          }
+    return;
+  }
+
   // epilogue: alpha, bias, activation in registers; the 16-bit tile through LDS ([256][264]); row stores.
   // The MFMAs are inline asm, so the compiler's hazard tracking does not see their results: wait out the
   // MFMA -> VALU read latency of the last accumulators explicitly.
@@ -444,7 +546,12 @@ int launch_pp(const Fp8Args& g, hipStream_t st) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_fp8_pp_kernel<FA, FB, F16>), dim3(g.tiles_m * g.tiles_n), dim3(kPPThreads), smem, st, g);
+  const int T = g.tiles_m * g.tiles_n;
+  const int grid = g.tail_split ? g.full_tiles + (T - g.full_tiles) * g.tail_split : T;
+  hipLaunchKernelGGL((gemm_fp8_pp_kernel<FA, FB, F16>), dim3(grid), dim3(kPPThreads), smem, st, g);
+  int rc = (int)hipGetLastError();
+  if (rc || !g.tail_split) return rc;
+  hipLaunchKernelGGL((gemm_fp8_tail_reduce_k<F16>), dim3(T - g.full_tiles, 64), dim3(256), 0, st, g);
   return (int)hipGetLastError();
 }
 
@@ -474,9 +581,35 @@ int g_fp8_kernel = 0;
 
 // fmt_a / fmt_b: 0 = e4m3fn, 1 = e5m2. act: 0 identity, 1 gelu, 2 relu. bias: [N] in the output dtype or null.
 // Returns 1 for an unsupported shape / stride (K % 128, N % 4, leading dims % 16 bytes).
+// Workspace (bytes) the ping-pong fp8 GEMM's balanced tail needs (0: none).
+PA_EXPORT int64_t pa_gemm_fp8_ws_bytes(int64_t M, int64_t N, int64_t K) {
+  int full, split;
+  pp_plan8(M, N, K, device_cus8(), &full, &split);
+  if (!split) return 0;
+  const int64_t T = ((M + 255) / 256) * ((N + 255) / 256);
+  return (T - full) * split * 65536 * 4;
+}
+
+static int fp8_impl(const void* a, const void* b, void* c, const void* bias, int64_t M, int64_t N, int64_t K,
+                    int64_t lda, int64_t ldb, int64_t ldc, int fmt_a, int fmt_b, float alpha, int act, int out_f16,
+                    void* ws, hipStream_t st);
+
 PA_EXPORT int pa_gemm_fp8(const void* a, const void* b, void* c, const void* bias, int64_t M, int64_t N, int64_t K,
                           int64_t lda, int64_t ldb, int64_t ldc, int fmt_a, int fmt_b, float alpha, int act,
                           int out_f16, hipStream_t st) {
+  return fp8_impl(a, b, c, bias, M, N, K, lda, ldb, ldc, fmt_a, fmt_b, alpha, act, out_f16, nullptr, st);
+}
+
+// the same with the balanced-tail workspace (pa_gemm_fp8_ws_bytes(M, N, K) bytes; may be null when that is 0)
+PA_EXPORT int pa_gemm_fp8_ws(const void* a, const void* b, void* c, const void* bias, int64_t M, int64_t N, int64_t K,
+                             int64_t lda, int64_t ldb, int64_t ldc, int fmt_a, int fmt_b, float alpha, int act,
+                             int out_f16, void* ws, hipStream_t st) {
+  return fp8_impl(a, b, c, bias, M, N, K, lda, ldb, ldc, fmt_a, fmt_b, alpha, act, out_f16, ws, st);
+}
+
+static int fp8_impl(const void* a, const void* b, void* c, const void* bias, int64_t M, int64_t N, int64_t K,
+                    int64_t lda, int64_t ldb, int64_t ldc, int fmt_a, int fmt_b, float alpha, int act, int out_f16,
+                    void* ws, hipStream_t st) {
   if (K % kKB != 0 || N % 4 != 0 || lda % 16 != 0 || ldb % 16 != 0 || ldc % 4 != 0) return 1;
   if (fmt_a < 0 || fmt_a > 1 || fmt_b < 0 || fmt_b > 1 || act < 0 || act > 2) return 1;
   if (M <= 0 || N <= 0) return 0;
@@ -488,6 +621,17 @@ PA_EXPORT int pa_gemm_fp8(const void* a, const void* b, void* c, const void* bia
   g.tiles_n = (int)((N + kTile - 1) / kTile);
   g.alpha = alpha; g.act = act;
   const bool pp = g_fp8_kernel != 1 && N % 8 == 0 && ldc % 8 == 0;
+  g.full_tiles = g.tiles_m * g.tiles_n;
+  g.tail_split = 0;
+  if (pp && ws) {
+    int full, split;
+    pp_plan8(M, N, K, device_cus8(), &full, &split);
+    if (split) {
+      g.full_tiles = full;
+      g.tail_split = split;
+      g.tail_ws = (float*)ws;
+    }
+  }
   if (fmt_a == 0 && fmt_b == 0) return launch_out<0, 0>(g, out_f16, pp, st);
   if (fmt_a == 0 && fmt_b == 1) return launch_out<0, 1>(g, out_f16, pp, st);
   if (fmt_a == 1 && fmt_b == 0) return launch_out<1, 0>(g, out_f16, pp, st);

@@ -61,6 +61,13 @@ def gemm_fp8(a, b_nk, bias=None, alpha=1.0, act="identity", out_dtype=torch.floa
         return _ref(a, b_nk, bias, alpha, act, out_dtype)
     out = torch.empty(M, N, dtype=out_dtype, device=a.device)
     bias_c = None if bias is None else bias.to(out_dtype).contiguous()
+    if L.has("pa_gemm_fp8_ws"):  # the ping-pong kernel's balanced tail: K-sliced last wave of tiles
+        nb = int(L.lib().pa_gemm_fp8_ws_bytes(M, N, K))
+        ws = torch.empty(nb // 4, dtype=torch.float32, device=a.device) if nb else None
+        L.call("pa_gemm_fp8_ws", L.ptr(a), L.ptr(b_nk), L.ptr(out), L.ptr(bias_c), M, N, K, a.stride(0),
+               b_nk.stride(0), out.stride(0), _FMT[a.dtype], _FMT[b_nk.dtype], float(alpha), _ACT[act],
+               1 if out_dtype == torch.float16 else 0, L.ptr(ws), L.stream_ptr())
+        return out
     L.call("pa_gemm_fp8", L.ptr(a), L.ptr(b_nk), L.ptr(out), L.ptr(bias_c), M, N, K, a.stride(0), b_nk.stride(0),
            out.stride(0), _FMT[a.dtype], _FMT[b_nk.dtype], float(alpha), _ACT[act],
            1 if out_dtype == torch.float16 else 0, L.stream_ptr())
