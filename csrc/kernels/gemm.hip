@@ -1971,6 +1971,43 @@ PA_EXPORT int pa_gemm_bf16_pp(const void* a, const void* b, void* c, const void*
   return (int)hipGetLastError();
 }
 
+// Split-K on the ping-pong kernel: every tile cut into `splits` K slices (the balanced-tail machinery with no
+// whole tiles), fp32 256 x 256 partials in ws (tiles x splits x 256 KiB), summed with the epilogue by
+// gemm_tail_reduce_k — for products with few output tiles and a long K (the weight gradients of convolutions over
+// all pixels of a batch). Requires (K / 64) % splits == 0.
+PA_EXPORT int64_t pa_gemm_pp_splitk_ws_bytes(int64_t M, int64_t N, int splits) {
+  return ((M + 255) / 256) * ((N + 255) / 256) * (int64_t)splits * 65536 * 4;
+}
+
+PA_EXPORT int pa_gemm_bf16_pp_splitk(const void* a, const void* b, void* c, int64_t M, int64_t N, int64_t K,
+                                     int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor, int b_kmajor, int flags,
+                                     float alpha, int splits, void* ws, hipStream_t st) {
+  if (K % kBK != 0 || N % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || ldc % 4 != 0 || splits < 1) return 1;
+  if ((K / kBK) % splits != 0 || !ws || (flags & ~(kEpiOutF32 | kEpiAccum))) return 1;
+  if (!a_kmajor && M % 8 != 0) return 1;
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  GemmArgs g{};
+  g.a = (const uint16_t*)a; g.b = (const uint16_t*)b; g.c = c;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.flags = flags; g.alpha = alpha;
+  g.tiles_m = (int)((M + 255) / 256);
+  g.tiles_n = (int)((N + 255) / 256);
+  const int T = g.tiles_m * g.tiles_n;
+  g.full_tiles = 0;
+  g.tail_split = splits;
+  g.tail_ws = (float*)ws;
+  const int grid = T * splits;
+  int rc;
+  if (a_kmajor && !b_kmajor) rc = launch256<true, false>(g, 1, st, grid);
+  else if (a_kmajor && b_kmajor) rc = launch256<true, true>(g, 1, st, grid);
+  else if (!a_kmajor && !b_kmajor) rc = launch256<false, false>(g, 1, st, grid);
+  else rc = launch256<false, true>(g, 1, st, grid);
+  if (rc) return rc;
+  hipLaunchKernelGGL(gemm_tail_reduce_k, dim3(T, 64), dim3(256), 0, st, g);
+  return (int)hipGetLastError();
+}
+
 // Segmented operands on the ping-pong kernel (GemmArgs::nseg): seg = [nseg][5] int64 host array of
 // {a_ptr, b_ptr, lda, ldb, end} per segment (end: K-tiles x 64 = K elements for seg_k = 1, columns for seg_k = 0),
 // same operand layouts in every segment. K = total K (seg_k) or the A operand's K; N = total columns. a / b in

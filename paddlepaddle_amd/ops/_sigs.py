@@ -72,6 +72,9 @@ SIGS = {
     "pa_gemm_bf16_pp_segs": [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32,
                              _i32, _f32, _vp, _vp],
     "pa_gemm_pp_ws_bytes": [_i64, _i64, _i64],
+    "pa_gemm_pp_splitk_ws_bytes": [_i64, _i64, _i32],
+    "pa_gemm_bf16_pp_splitk": [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _f32, _i32, _vp,
+                               _vp],
     "pa_gemm_fp8": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _f32, _i32, _i32, _vp],
     "pa_gemm_fp8_set_kernel": [_i32],
     "pa_gemm_fp8_ws": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _f32, _i32, _i32, _vp, _vp],
@@ -132,5 +135,5 @@ SIGS = {
     "pa_version": [],
 }
 
-RET_I64 = {"pa_gemm_pp_ws_bytes", "pa_gemm_fp8_ws_bytes", "pa_bn_pre_ws", "pa_gemm_skinny_stats_chunks", "pa_conv_skinny_stats_chunks",
+RET_I64 = {"pa_gemm_pp_ws_bytes", "pa_gemm_fp8_ws_bytes", "pa_gemm_pp_splitk_ws_bytes", "pa_bn_pre_ws", "pa_gemm_skinny_stats_chunks", "pa_conv_skinny_stats_chunks",
            "pa_colsum_nparts"}

@@ -77,6 +77,20 @@ def _splits(M, N, K):
     return G.pick_splits(M, N, K, bn=G._pick_bn(M, N, False))
 
 
+def _wgrad_1x1(a, b, splits, dtype):
+    """dW = dY^T . X of a 1x1 convolution (K = every pixel of the batch): split-K on the generic kernel or on the
+    ping-pong 256x256 kernel, whichever the per-shape timing picks (the ping-pong form needs >= 256-wide outputs to
+    pay off)."""
+    M, N, K = a.shape[0], b.shape[1], a.shape[1]
+    sp = G.pp_splits(M, N, K)
+    if M >= 256 and N >= 256 and G.gemm_pp_splitk_ok(a, b, sp):
+        ch = G.choose(("wgrad1x1", M, N, K), {"hip": lambda: G.gemm_splitk(a, b, splits, out_dtype=dtype),
+                                              "hip_pp": lambda: G.gemm_pp_splitk(a, b, sp, dtype)})
+        if ch == "hip_pp":
+            return G.gemm_pp_splitk(a, b, sp, dtype)
+    return G.gemm_splitk(a, b, splits, out_dtype=dtype)
+
+
 class _Conv1x1(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, stride, sink=None):
@@ -117,7 +131,7 @@ class _Conv1x1(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             P = dy2.shape[0]
             if P % 64 == 0:
-                dw = G.gemm_splitk(dy2.t(), x2, _splits(Cout, Cin, P), out_dtype=w2.dtype)
+                dw = _wgrad_1x1(dy2.t(), x2, _splits(Cout, Cin, P), w2.dtype)
             else:  # pixel count not a multiple of the 64-deep K tile
                 dw = torch.mm(dy2.t(), x2)
             dw = dw.view(Cout, Cin, 1, 1)

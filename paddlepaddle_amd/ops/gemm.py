@@ -226,6 +226,43 @@ def gemm_splitk(a, b, splits, out_dtype=torch.bfloat16, bn=None):
     return reduce_slabs(ws, out_dtype)
 
 
+def pp_splits(M, N, K, cus=256, max_ws_bytes=256 << 20):
+    """K-split factor of the ping-pong split-K GEMM: 1-2 workgroups per CU, slices of >= 4 K-tiles (64), fp32
+    partial tiles within the workspace budget; 0 when no split fits."""
+    T = -(-M // 256) * -(-N // 256)
+    nk = K // 64
+    s = 1
+    while T * s * 2 <= 2 * cus and nk % (s * 2) == 0 and nk // (s * 2) >= 4 and T * s * 2 * 262144 <= max_ws_bytes:
+        s *= 2
+    return s if s > 1 else 0
+
+
+def gemm_pp_splitk_ok(a, b, splits):
+    if not (splits and L.has("pa_gemm_bf16_pp_splitk") and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
+            and a.is_cuda and L.hip_enabled_for(a)):
+        return False
+    M, K = a.shape
+    N = b.shape[1]
+    la, lb = _layout(a, 0), _layout(b, 1)
+    return (la is not None and lb is not None and K % 64 == 0 and (K // 64) % splits == 0 and N % 8 == 0
+            and la[0] % 8 == 0 and lb[0] % 8 == 0 and (la[1] or M % 8 == 0))
+
+
+def gemm_pp_splitk(a, b, splits, out_dtype=torch.bfloat16):
+    """C = a @ b on the ping-pong 256x256 kernel with every tile cut into ``splits`` K slices (fp32 partial tiles
+    summed, with the cast, by the tail-reduction kernel): the split-K form for few output tiles and a long K."""
+    M, K = a.shape
+    N = b.shape[1]
+    lda, ak = _layout(a, 0)
+    ldb, bk = _layout(b, 1)
+    out = torch.empty(M, N, dtype=out_dtype, device=a.device)
+    ws = torch.empty(int(L.lib().pa_gemm_pp_splitk_ws_bytes(M, N, splits)) // 4, dtype=torch.float32,
+                     device=a.device)
+    L.call("pa_gemm_bf16_pp_splitk", L.ptr(a), L.ptr(b), L.ptr(out), M, N, K, lda, ldb, out.stride(0), int(ak),
+           int(bk), EPI_OUT_F32 if out_dtype == torch.float32 else 0, 1.0, int(splits), L.ptr(ws), L.stream_ptr())
+    return out
+
+
 def reduce_slabs(ws, out_dtype):
     """[splits, M, N] fp32 split-K partials -> [M, N] out_dtype; bf16 in one HIP pass (sum + cast)."""
     splits, M, N = ws.shape
