@@ -353,6 +353,11 @@ class ShardingHybridModel(_Layer):
         return self._layers.named_parameters(prefix, include_sublayers, remove_duplicate)
 
 
+def _world_pg():
+    """The default process group when more than one rank trains (static data parallelism without a topology)."""
+    return dist.group.WORLD if dist.is_initialized() and dist.get_world_size() > 1 else None
+
+
 class HybridParallelOptimizer:
     """Reference: dygraph_optimizer/hybrid_parallel_optimizer.py — global-norm clip across mp/pp/sharding,
     sharding stage-1 optimizer-state partition when sharding_degree > 1."""
@@ -405,6 +410,18 @@ class HybridParallelOptimizer:
     clear_gradients = clear_grad
 
     def minimize(self, loss, startup_program=None, parameters=None, no_grad_set=None):
+        from ...static import _static_mode
+        if _static_mode.enabled:
+            # static collective training (reference fleet/meta_optimizers/raw_program_optimizer.py: c_allreduce_sum
+            # + 1/nranks scale after the backward): the program records the optimizer and the data-parallel group;
+            # the Executor averages the gradients over it (one coalesced all-reduce per dtype) before the update
+            from ...static import default_main_program
+            prog = default_main_program()
+            prog._set_optimizer(self._inner_opt, loss)
+            g = self._hcg.get_data_parallel_group() if self._hcg is not None else None
+            prog._dp_sync = g.process_group if g is not None and g.nranks > 1 else (
+                None if g is not None else _world_pg())
+            return [], []
         loss.backward()
         self.step()
 

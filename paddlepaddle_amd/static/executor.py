@@ -352,6 +352,7 @@ class Executor:
             if gm is None:
                 optimizer.clear_grad(set_to_zero=False)
                 env[ls].backward()
+                _dp_sync(prog, optimizer)
                 optimizer.step()
             else:
                 k, avg = gm
@@ -360,6 +361,7 @@ class Executor:
                 (env[ls] / k if avg else env[ls]).backward()
                 prog._gm_count += 1
                 if prog._gm_count % k == 0:
+                    _dp_sync(prog, optimizer)
                     optimizer.step()
         outs = []
         for s in fetch:
@@ -390,7 +392,7 @@ class Executor:
     def _graph_ok(prog):
         """Programs whose run is one fixed launch sequence: no guard nodes (data-dependent Python decisions),
         no dynamic dims, no gradient merge (host-side step counting)."""
-        if prog._dyn or getattr(prog, "_grad_merge", None) is not None:
+        if prog._dyn or getattr(prog, "_grad_merge", None) is not None or getattr(prog, "_dp_sync", None) is not None:
             return False
         return not any(isinstance(n, P.GuardNode) for n in prog.nodes)
 
@@ -569,3 +571,29 @@ def create_global_var(shape, value, dtype, persistable=False, force_cpu=False, n
 def create_parameter(shape, dtype, name=None, attr=None, is_bias=False, default_initializer=None):
     from .. import create_parameter as _cp
     return _cp(shape, dtype, name, attr, is_bias, default_initializer)
+
+
+def _dp_sync(prog, optimizer):
+    """Static collective data parallelism (fleet.distributed_optimizer(...).minimize in static mode): average the
+    gradients over the program's data-parallel group — one coalesced all-reduce per dtype (reference
+    raw_program_optimizer: c_allreduce_sum + scale 1 / nranks, fused by fuse_all_reduce)."""
+    pg = getattr(prog, "_dp_sync", None)
+    if pg is None:
+        return
+    import torch.distributed as tdist
+    n = tdist.get_world_size(pg)
+    by_dtype = {}
+    for p in optimizer._parameter_list:
+        g = p._t.grad
+        if g is not None:
+            by_dtype.setdefault(g.dtype, []).append(g)
+    with torch.no_grad():
+        for gs in by_dtype.values():
+            flat = torch.cat([g.reshape(-1) for g in gs])
+            tdist.all_reduce(flat, group=pg)
+            flat.mul_(1.0 / n)
+            off = 0
+            for g in gs:
+                k = g.numel()
+                g.copy_(flat[off:off + k].view_as(g))
+                off += k

@@ -471,6 +471,8 @@ def compile_training(prog, plan, fetch, dev, native_kernels=True):
         return None, "_C_train not built"
     if prog._dyn or getattr(prog, "_grad_merge", None) is not None:
         return None, "dynamic dims / gradient merge"
+    if getattr(prog, "_dp_sync", None) is not None:
+        return None, "data-parallel gradient synchronisation (static collective training)"
     opt_entry = prog._optimize
     low = _Lowering(prog, dev, native_kernels)
     try:
