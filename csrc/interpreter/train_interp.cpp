@@ -812,6 +812,10 @@ class TrainProgram {
 
   void set_loss(int slot) { loss_ = slot; }
 
+  // called with the optimizer parameters' gradients after the backward, before clipping / the update (static
+  // collective data parallelism: the gradient all-reduce over the data-parallel group)
+  void set_grad_hook(py::object fn) { grad_hook_ = std::move(fn); }
+
   // one optimizer group: masters[i] is read only where has_master[i] (fp32 master weights of low-precision params)
   void add_optimizer(const std::string& kind, std::vector<at::Tensor> params, std::vector<at::Tensor> masters,
                      std::vector<int64_t> has_master, std::vector<at::Tensor> m1, std::vector<at::Tensor> m2,
@@ -876,6 +880,14 @@ class TrainProgram {
         zero_grads();
         torch::autograd::backward({loss});
       }
+    }
+    if (backward && !opt_.empty() && grad_hook_ && !grad_hook_.is_none()) {
+      std::vector<at::Tensor> gs;
+      for (auto& g : opt_)
+        for (auto& p : g.params)
+          if (p.grad().defined()) gs.push_back(p.grad());
+      py::gil_scoped_acquire gil;  // run() is bound with the GIL released
+      grad_hook_(gs);
     }
     if (backward && !opt_.empty()) {
       at::NoGradGuard ng;
@@ -1088,6 +1100,7 @@ class TrainProgram {
   std::vector<int> persistent_, fetch_;
   std::vector<std::vector<int>> release_;
   std::vector<OptGroup> opt_;
+  py::object grad_hook_;
   int loss_ = -1;
 };
 
@@ -1104,6 +1117,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("add_native", &TrainProgram::add_native)
       .def("bind", &TrainProgram::bind)
       .def("set_loss", &TrainProgram::set_loss)
+      .def("set_grad_hook", &TrainProgram::set_grad_hook)
       .def("add_optimizer", &TrainProgram::add_optimizer)
       .def("finalize", &TrainProgram::finalize)
       .def("run", &TrainProgram::run, py::arg("feeds"), py::arg("backward"), py::arg("scalars"), py::arg("clip_norm"),

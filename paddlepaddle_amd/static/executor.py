@@ -580,13 +580,16 @@ def _dp_sync(prog, optimizer):
     pg = getattr(prog, "_dp_sync", None)
     if pg is None:
         return
+    _allreduce_mean([p._t.grad for p in optimizer._parameter_list if p._t.grad is not None], pg)
+
+
+def _allreduce_mean(grads, pg):
+    """grads <- mean over ``pg``: one flat all-reduce per dtype (also the native executor's gradient hook)."""
     import torch.distributed as tdist
     n = tdist.get_world_size(pg)
     by_dtype = {}
-    for p in optimizer._parameter_list:
-        g = p._t.grad
-        if g is not None:
-            by_dtype.setdefault(g.dtype, []).append(g)
+    for g in grads:
+        by_dtype.setdefault(g.dtype, []).append(g)
     with torch.no_grad():
         for gs in by_dtype.values():
             flat = torch.cat([g.reshape(-1) for g in gs])

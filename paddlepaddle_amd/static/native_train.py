@@ -460,6 +460,10 @@ class NativeTrainRunner:
             self.opt.clear_grad(set_to_zero=False)
         outs = self.tp.run(feeds, train, scalars, self.clip_norm)
         if train and self.scalars_fn is None:  # forward + backward native, update by the Python optimizer
+            pg = getattr(self, "dp_pg", None)
+            if pg is not None:  # static collective DP (the native update runs it as the executor's gradient hook)
+                from .executor import _allreduce_mean
+                _allreduce_mean([p._t.grad for p in self.opt._parameter_list if p._t.grad is not None], pg)
             self.opt.step()
         return outs
 
@@ -471,8 +475,6 @@ def compile_training(prog, plan, fetch, dev, native_kernels=True):
         return None, "_C_train not built"
     if prog._dyn or getattr(prog, "_grad_merge", None) is not None:
         return None, "dynamic dims / gradient merge"
-    if getattr(prog, "_dp_sync", None) is not None:
-        return None, "data-parallel gradient synchronisation (static collective training)"
     opt_entry = prog._optimize
     low = _Lowering(prog, dev, native_kernels)
     try:
@@ -523,6 +525,12 @@ def _build(m, low, prog, fetch, dev, native_kernels, opt_entry):
                 tp.add_optimizer(kind, [p._t for p in params], [mm if mm is not None else p._t
                                                                  for p, mm in zip(params, masters)],
                                  [int(mm is not None) for mm in masters], m1, m2, coeff, lr_mult)
+    pg = getattr(prog, "_dp_sync", None)
+    if pg is not None:  # static collective DP: average the gradients before the update
+        from . import executor as _ex
+        tp.set_grad_hook(lambda grads: _ex._allreduce_mean(grads, pg))
     tp.finalize(list(fetch))
     feed_slots = {name: v[0] for name, v in prog.feeds.items()}
-    return NativeTrainRunner(tp, feed_slots, fetch, opt, scalars_fn, clip_norm, set(prog._need_grad_slots), low), None
+    runner = NativeTrainRunner(tp, feed_slots, fetch, opt, scalars_fn, clip_norm, set(prog._need_grad_slots), low)
+    runner.dp_pg = pg
+    return runner, None

@@ -164,3 +164,33 @@ def test_native_executor_conv_bn_block_bf16():
         assert calls.get(k, 0) > 0, (k, calls)
     ref, _ = _run(build, feeds, "off", steps=3)
     np.testing.assert_allclose(got, ref, rtol=3e-2, atol=3e-2)
+
+
+@pytest.mark.gpu
+def test_native_executor_dp_gradient_hook_gpu(monkeypatch):
+    """Static collective DP on the native update: the executor's gradient hook (the data-parallel all-reduce) runs
+    once per step between the C++ backward and the fused AdamW kernel, on the gradients of every parameter."""
+    from paddlepaddle_amd.static import executor as EX
+    seen = []
+
+    def fake(grads, pg):
+        seen.append((len(grads), pg))
+    monkeypatch.setattr(EX, "_allreduce_mean", fake)
+    paddle.set_device("gpu:0")
+    paddle.set_flags({"FLAGS_static_native_executor": "auto"})
+    paddle.enable_static()
+    try:
+        main, start = paddle.static.Program(), paddle.static.Program()
+        with paddle.static.program_guard(main, start):
+            paddle.seed(3)
+            loss = _mlp()
+        main._dp_sync = "dp-group"
+        exe = paddle.static.Executor()
+        rng = np.random.RandomState(0)
+        for _ in range(3):
+            exe.run(main, feed=_mlp_feeds(rng), fetch_list=[loss])
+        r = _runners(main)
+        assert r and r[0].scalars_fn is not None, main._native_reason  # the update ran natively
+        assert seen == [(4, "dp-group")] * 3, seen
+    finally:
+        paddle.disable_static()

@@ -2,6 +2,7 @@
 mode, meta_optimizers/raw_program_optimizer.py — c_allreduce_sum + 1/nranks scale of every gradient after the
 backward): 2 gloo ranks on half batches train like one process on the whole batch."""
 import numpy as np
+import pytest
 
 from test_distributed_cpu import _setup, _spawn
 
@@ -30,8 +31,9 @@ def _build(paddle, fleet=None):
     return main, loss
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, native, q):
     paddle = _setup(rank, world, port)
+    paddle.set_flags({"FLAGS_static_native_executor": "force" if native else "off"})
     from paddlepaddle_amd.distributed import fleet
     fleet.init(is_collective=True)
     main, loss = _build(paddle, fleet)
@@ -44,12 +46,17 @@ def _worker(rank, world, port, q):
         lv, = exe.run(main, feed={"x": xs[half], "y": ys[half]}, fetch_list=[loss])
         losses.append(float(lv))
     params = [p.numpy().copy() for p in main.all_parameters()]
+    runners = [r for r in main.__dict__.get("_native_runners", {}).values() if r is not None]
+    assert bool(runners) == native, (native, main.__dict__.get("_native_reason"))
     paddle.disable_static()
     q.put((rank, losses, params))
     paddle.distributed.barrier()
 
 
-def test_static_collective_dp_matches_whole_batch():
+@pytest.mark.parametrize("native", [False, True])
+def test_static_collective_dp_matches_whole_batch(native):
+    """Python replay and the native training executor (_C_train: the all-reduce as its gradient hook between the
+    backward and the fused update)."""
     import os
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -61,7 +68,7 @@ def test_static_collective_dp_matches_whole_batch():
     ref = [float(exe.run(main, feed={"x": xs, "y": ys}, fetch_list=[loss])[0]) for _ in range(STEPS)]
     ref_params = [p.numpy().copy() for p in main.all_parameters()]
     paddle.disable_static()
-    res = sorted(_spawn(_worker, world=2))
+    res = sorted(_spawn(_worker, native, world=2))
     (_, l0, p0), (_, l1, p1) = res
     # the mean of the ranks' half-batch losses is the whole-batch loss; parameters stay identical on both ranks
     np.testing.assert_allclose((np.array(l0) + np.array(l1)) / 2, ref, rtol=1e-5, atol=1e-6)
