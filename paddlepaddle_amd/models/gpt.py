@@ -41,7 +41,8 @@ class GPTConfig:
     layer_norm_eps: float = 1e-5
     tie_word_embeddings: bool = True
     use_recompute: bool = False
-    recompute_granularity: str = "full"
+    recompute_granularity: str = "full"  # full (decoder layer) | full_attn (attention block) | core_attn
+    no_recompute_layers: tuple = ()       # layer indices kept out of recompute
     tensor_parallel_degree: int = 1
     sequence_parallel: bool = False
     fuse_attention_qkv: bool = True
@@ -187,9 +188,18 @@ class GPTAttention(nn.Layer):
         qkv = self.qkv_proj(x)._t  # [B, S, 3*h_local]
         B, S = qkv.shape[0], qkv.shape[1]
         qkv = qkv.view(B, S, self.local_heads, 3, self.head_dim)
-        o = _ops.flash_attention_qkvpacked(qkv, causal=True, dropout=self.attn_dropout, training=self.training)
+        o = self._core(qkv)
         o = o.reshape(B, S, self.local_heads * self.head_dim)
         return self.out_proj(_wrap(o))
+
+    def _core(self, qkv):
+        """The attention core, checkpointed under recompute_granularity core_attn (``_rc_core``)."""
+        def fn(t):
+            return _ops.flash_attention_qkvpacked(t, causal=True, dropout=self.attn_dropout, training=self.training)
+        if getattr(self, "_rc_core", False):
+            from ..distributed.fleet.recompute import recompute
+            return recompute(lambda a: _wrap(fn(a._t)), _wrap(qkv))._t
+        return fn(qkv)
 
     def _forward_sp(self, x):
         sp = _sp()
@@ -261,14 +271,27 @@ class GPTDecoderLayer(nn.Layer):
         r, h = _ops.layer_norm_residual(x._t, norm.weight._t, norm.bias._t, norm._epsilon)
         return r, _wrap(h)
 
+    def _attn(self, h):
+        """Self-attention under the layer's recompute granularity (GPTModel sets ``_rc``)."""
+        return _gpt_attn(self, h)
+
     def forward(self, x):
         # residual + dropout fused in one HIP pass (mask regenerated from a seed in backward)
         p = self.dropout1.p if self.training else 0.0
         r, h = self._ln(self.norm1, x)
-        x = _wrap(_ops.dropout_add(self.self_attn(h)._t, r, p, self.training))
+        x = _wrap(_ops.dropout_add(self._attn(h)._t, r, p, self.training))
         r, h = self._ln(self.norm2, x)
         x = _wrap(_ops.dropout_add(self.mlp(h)._t, r, p, self.training))
         return x
+
+
+def _gpt_attn(layer, h):
+    g = getattr(layer, "_rc", None)
+    if g == "full_attn":
+        from ..distributed.fleet.recompute import recompute
+        return recompute(layer.self_attn, h)
+    layer.self_attn._rc_core = g == "core_attn"
+    return layer.self_attn(h)
 
 
 class GPTModel(nn.Layer):
@@ -288,10 +311,17 @@ class GPTModel(nn.Layer):
                 layer.self_attn.bs = bs
         x = self.embeddings(input_ids, position_ids)
         rc = self.config.use_recompute and self.training
+        gran = self.config.recompute_granularity
+        skip = set(self.config.no_recompute_layers or ())
         if rc:
             from ..distributed.fleet.recompute import recompute
-        for layer in self.layers:
-            x = recompute(layer, x) if rc else layer(x)
+        for i, layer in enumerate(self.layers):
+            on = rc and i not in skip
+            if on and gran == "full":
+                x = recompute(layer, x)
+            else:
+                layer._rc = gran if on else None  # full_attn / core_attn: the layer checkpoints part of itself
+                x = layer(x)
         return self.norm(x)
 
 

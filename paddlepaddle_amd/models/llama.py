@@ -41,6 +41,8 @@ class LlamaConfig:
     initializer_range: float = 0.02
     tie_word_embeddings: bool = False
     use_recompute: bool = False
+    recompute_granularity: str = "full"  # full (decoder layer) | full_attn (attention block) | core_attn (attention core)
+    no_recompute_layers: tuple = ()      # layer indices kept out of recompute (PaddleNLP no_recompute_layers)
     fused_qkv_attention: bool = True  # training attention as ops.qkv_rope_attention (one-buffer qkv gradient)
     # models/llama_auto.py (PaddleNLP config names): one [q | k | v] projection / one [gate | up] projection per
     # tensor-parallel shard instead of separate linears
@@ -145,6 +147,15 @@ class _Rope:
         return self.cos, self.sin
 
 
+def _core(attn, fn, *ts):
+    """The attention core ``fn(*ts)`` (torch tensors), checkpointed when the layer's recompute granularity is
+    core_attn (``attn._rc_core``): only its inputs are kept, the core is re-run in backward."""
+    if getattr(attn, "_rc_core", False):
+        from ..distributed.fleet.recompute import recompute
+        return recompute(lambda *a: _wrap(fn(*[x._t for x in a])), *[_wrap(x) for x in ts])._t
+    return fn(*ts)
+
+
 class LlamaAttention(nn.Layer):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
@@ -182,7 +193,8 @@ class LlamaAttention(nn.Layer):
             t = self.qkv_proj(x)._t
             B, S = t.shape[0], t.shape[1]
             cos, sin = self.rope.tables(pos + S, t.device)
-            o = _ops.qkv_rope_attention(t, cos[pos:pos + S], sin[pos:pos + S], self.H, self.Hkv, self.D)
+            c, sn = cos[pos:pos + S], sin[pos:pos + S]
+            o = _core(self, lambda tt: _ops.qkv_rope_attention(tt, c, sn, self.H, self.Hkv, self.D), t)
             return self.o_proj(_wrap(o.reshape(B, S, self.H * self.D)))
         q, k, v = self._qkv(x)
         B, S = q.shape[0], q.shape[1]
@@ -201,7 +213,7 @@ class LlamaAttention(nn.Layer):
             causal = S > 1
         else:
             causal = True
-        o = _ops.flash_attention(q, k, v, causal=causal)
+        o = _core(self, lambda qq, kk, vv: _ops.flash_attention(qq, kk, vv, causal=causal), q, k, v)
         return self.o_proj(_wrap(o.reshape(B, S, self.H * self.D)))
 
     def _forward_sep(self, q, k, v, B, S):
@@ -282,13 +294,23 @@ class LlamaDecoderLayer(nn.Layer):
             # backward kernel (LlamaRMSNorm(residual=True) -> ops.rms_norm_residual, a recorded static op, so a
             # captured program keeps it) instead of autograd's separate accumulation add
             r, h = n1(x, residual=True)
-            t = r._t + self.self_attn(h, cache, pos)._t
+            t = r._t + self._attn(h, cache, pos)._t
             r, h = n2(_wrap(t), residual=True)
             return _wrap(r._t + self.mlp(h)._t)
-        h = self.self_attn(self.input_layernorm(x), cache, pos)
+        h = self._attn(self.input_layernorm(x), cache, pos)
         x = _wrap(x._t + h._t)
         h = self.mlp(self.post_attention_layernorm(x))
         return _wrap(x._t + h._t)
+
+    def _attn(self, h, cache, pos):
+        """Self-attention under the layer's recompute granularity (LlamaModel sets ``_rc``): full_attn checkpoints
+        the attention block (projections included), core_attn only the attention core."""
+        g = getattr(self, "_rc", None) if cache is None else None
+        if g == "full_attn":
+            from ..distributed.fleet.recompute import recompute
+            return recompute(self.self_attn, h)
+        self.self_attn._rc_core = g == "core_attn"
+        return self.self_attn(h, cache, pos)
 
 
 class LlamaModel(nn.Layer):
@@ -325,12 +347,16 @@ class LlamaModel(nn.Layer):
         if not torch.is_grad_enabled() and len(self.layers) > 0 and x._t.is_cuda:
             return self._forward_infer(x, caches, pos)
         rc = self.config.use_recompute and self.training and caches is None
+        gran = self.config.recompute_granularity
+        skip = set(self.config.no_recompute_layers or ())
         if rc:
             from ..distributed.fleet.recompute import recompute
         for i, layer in enumerate(self.layers):
-            if rc:
+            on = rc and i not in skip
+            if on and gran == "full":
                 x = recompute(layer, x)
             else:
+                layer._rc = gran if on else None  # full_attn / core_attn: the layer checkpoints part of itself
                 x = layer(x, None if caches is None else caches[i], pos)
         return self.norm(x)
 
