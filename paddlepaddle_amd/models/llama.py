@@ -49,6 +49,7 @@ class LlamaConfig:
     fuse_attention_qkv: bool = False
     fuse_attention_ffn: bool = False
     tensor_parallel_degree: int = 1
+    sequence_parallel: bool = False  # with TP: activations between the TP regions split over tokens (Megatron SP)
     sep_parallel_degree: int = 1  # segment parallelism: each rank of hcg's sep group holds S / sep tokens
     pad_token_id: int = 0
     bos_token_id: int = 1
@@ -111,11 +112,25 @@ def _tp():
     return tp
 
 
+def _sp():
+    from ..parallel import sequence_parallel as sp
+    return sp
+
+
+def _use_sp(cfg):
+    """Sequence parallelism (training, TP > 1): norms / residual adds on this rank's token block; the column
+    linears all-gather the tokens overlapped with their GEMM, the row linears reduce-scatter them."""
+    return bool(getattr(cfg, "sequence_parallel", False)) and cfg.tensor_parallel_degree > 1 \
+        and cfg.sep_parallel_degree <= 1
+
+
 class LlamaRMSNorm(nn.Layer):
     def __init__(self, cfg):
         super().__init__()
         self.weight = self.create_parameter([cfg.hidden_size], default_initializer=I.Constant(1.0))
         self.eps = cfg.rms_norm_eps
+        if _use_sp(cfg):  # sees only this rank's tokens: its gradient is summed over the mp group per step
+            _sp().mark_sequence_parallel(self.weight)
 
     def forward(self, x, residual=False):
         """``residual=True`` (pre-norm training blocks): returns (x_residual, rms_norm(x)) — use x_residual for the
@@ -184,7 +199,20 @@ class LlamaAttention(nn.Layer):
         q, k, v = t.split([self.H * self.D, self.Hkv * self.D, self.Hkv * self.D], -1)
         return q.view(B, S, self.H, self.D), k.view(B, S, self.Hkv, self.D), v.view(B, S, self.Hkv, self.D)
 
+    def _forward_sp(self, x):
+        """Sequence-parallel training: x is this rank's token block [B*S/mp, h]; the qkv projection all-gathers the
+        tokens under its GEMM, the o projection reduce-scatters them back (parallel/sequence_parallel.py)."""
+        sp = _sp()
+        B, S = self.bs
+        t = sp.column_sp_linear(x._t, self.qkv_proj.weight._t, None).view(B, S, -1)
+        cos, sin = self.rope.tables(S, t.device)
+        c, sn = cos[:S], sin[:S]
+        o = _core(self, lambda tt: _ops.qkv_rope_attention(tt, c, sn, self.H, self.Hkv, self.D), t)
+        return _wrap(sp.row_sp_linear(o.reshape(B * S, self.H * self.D), self.o_proj.weight._t))
+
     def forward(self, x, cache=None, pos=0):
+        if cache is None and getattr(self, "bs", None) is not None and x._t.dim() == 2:
+            return self._forward_sp(x)
         if cache is not None and isinstance(pos, torch.Tensor):
             return self._decode_step(x, cache, pos)
         if cache is None and self.cfg.sep_parallel_degree <= 1 and self.cfg.fused_qkv_attention:
@@ -272,8 +300,13 @@ class LlamaMLP(nn.Layer):
         else:
             self.gate_up_proj = nn.Linear(h, 2 * f, weight_attr=init, bias_attr=False)
             self.down_proj = nn.Linear(f, h, weight_attr=init, bias_attr=False)
+        self.sp = _use_sp(cfg)
 
     def forward(self, x):
+        if self.tp > 1 and x._t.dim() == 2 and getattr(self, "sp", False):  # sequence parallel: token block in / out
+            sp = _sp()
+            h = _ops.swiglu(sp.column_sp_linear(x._t, self.gate_up_proj.weight._t, None))
+            return _wrap(sp.row_sp_linear(h, self.down_proj.weight._t))
         # one-input swiglu: its backward writes d[gate | up] as one buffer (no chunk / cat in autograd)
         return self.down_proj(_wrap(_ops.swiglu(self.gate_up_proj(x)._t)))
 
@@ -343,9 +376,18 @@ class LlamaModel(nn.Layer):
         return _wrap(out)
 
     def forward(self, input_ids, caches=None, pos=0):
-        x = self.embed_tokens(input_ids)
-        if not torch.is_grad_enabled() and len(self.layers) > 0 and x._t.is_cuda:
-            return self._forward_infer(x, caches, pos)
+        sp_on = _use_sp(self.config) and caches is None and self.training and torch.is_grad_enabled()
+        B, S = input_ids.shape[0], input_ids.shape[-1]
+        for layer in self.layers:
+            layer.self_attn.bs = (B, S) if sp_on else None
+        self.sp_bs = (B, S) if sp_on else None
+        if sp_on:  # this rank's token block: the vocab-parallel partial embeddings reduce-scattered over tokens
+            emb = self.embed_tokens.local_lookup(input_ids._t).reshape(B * S, -1)
+            x = _wrap(_sp().reduce_scatter_tokens(emb))
+        else:
+            x = self.embed_tokens(input_ids)
+            if not torch.is_grad_enabled() and len(self.layers) > 0 and x._t.is_cuda:
+                return self._forward_infer(x, caches, pos)
         rc = self.config.use_recompute and self.training and caches is None
         gran = self.config.recompute_granularity
         skip = set(self.config.no_recompute_layers or ())
@@ -376,6 +418,10 @@ class LlamaForCausalLM(nn.Layer):
     def _logits(self, h):
         w = self.llama.embed_tokens.weight if self.config.tie_word_embeddings else self.lm_head_weight
         ht = h._t if h._t.dtype == w._t.dtype else h._t.to(w._t.dtype)
+        bs = getattr(getattr(self, "llama", None), "sp_bs", None)  # (the pipeline head shares this method)
+        if bs is not None and ht.dim() == 2:
+            # token blocks -> vocab-parallel logits of all tokens (the token all-gather overlaps the GEMM)
+            return _wrap(_sp().column_sp_linear_nt(ht, w._t).view(bs[0], bs[1], -1))
         if self.config.tensor_parallel_degree > 1:
             ht = _tp().c_identity(ht)
         return _wrap(torch.matmul(ht, w._t.t()))
@@ -537,6 +583,10 @@ class LlamaHeadPipe(nn.Layer):
         h = self.norm(x)
         w = self.lm_head_weight
         ht = h._t if h._t.dtype == w._t.dtype else h._t.to(w._t.dtype)
+        bs = getattr(getattr(self, "llama", None), "sp_bs", None)  # (the pipeline head shares this method)
+        if bs is not None and ht.dim() == 2:
+            # token blocks -> vocab-parallel logits of all tokens (the token all-gather overlaps the GEMM)
+            return _wrap(_sp().column_sp_linear_nt(ht, w._t).view(bs[0], bs[1], -1))
         if self.config.tensor_parallel_degree > 1:
             ht = _tp().c_identity(ht)
         return _wrap(torch.matmul(ht, w._t.t()))
@@ -549,6 +599,9 @@ def LlamaForCausalLMPipe(cfg: LlamaConfig, num_stages=None, num_virtual_pipeline
     tensor parallelism (cfg.tensor_parallel_degree) and interleaved virtual stages: the PP4 x TP2 layout of
     the 70B config puts 20 decoder layers and 8.75B parameters on each MI355X."""
     from ..parallel.pipeline import LayerDesc, PipelineLayer
+    if _use_sp(cfg):
+        raise NotImplementedError("LlamaForCausalLMPipe: sequence_parallel is implemented on LlamaForCausalLM "
+                                  "(fleet tensor parallelism without the pipeline layer)")
     descs = [LayerDesc(LlamaEmbeddingPipe, cfg)]
     descs += [LayerDesc(LlamaDecoderLayerPipe, cfg) for _ in range(cfg.num_hidden_layers)]
     descs.append(LayerDesc(LlamaHeadPipe, cfg))

@@ -244,7 +244,7 @@ def _llama_tp_shard(name, full, rank, world, cfg):
     return full
 
 
-def _llama_tp_worker(rank, world, port, q):
+def _llama_tp_worker(rank, world, port, q, sp=False):
     paddle = _setup(rank, world, port)
     from paddlepaddle_amd.models.llama import LlamaConfig, LlamaForCausalLM, LlamaPretrainingCriterion
     paddle.seed(4)
@@ -252,15 +252,17 @@ def _llama_tp_worker(rank, world, port, q):
     full = LlamaForCausalLM(cfg1)
     full_sd = {k: v._t.detach().clone() for k, v in full.state_dict().items()}
     fleet = _fleet_init(paddle, mp_degree=2)
-    cfg = LlamaConfig.tiny(tensor_parallel_degree=2)
+    cfg = LlamaConfig.tiny(tensor_parallel_degree=2, sequence_parallel=sp)
     model, crit = LlamaForCausalLM(cfg), LlamaPretrainingCriterion(cfg)
     with torch.no_grad():
         for k, v in model.state_dict().items():
             v._t.copy_(_llama_tp_shard(k, full_sd[k], rank, world, cfg))
     opt = paddle.optimizer.AdamW(1e-2, parameters=model.parameters(), grad_clip=paddle.nn.ClipGradByGlobalNorm(0.5))
+    inner = model
     model = fleet.distributed_model(model)
     opt = fleet.distributed_optimizer(opt)
     losses = _train(paddle, model, crit, opt, _data(cfg))
+    assert (inner.llama.sp_bs is not None) == sp  # the sequence-parallel path ran
     q.put((rank, losses))
     paddle.distributed.barrier()
 
@@ -278,6 +280,14 @@ def test_llama_tensor_parallel_matches_single_process():
     res = _spawn(_llama_tp_worker)
     for _, l in res:
         np.testing.assert_allclose(l, ref, rtol=1e-4, atol=1e-5)
+    # sequence parallelism: norms / residuals on token blocks, all-gather / reduce-scatter around the TP linears
+    res = _spawn(_llama_tp_sp_worker)
+    for _, l in res:
+        np.testing.assert_allclose(l, ref, rtol=1e-4, atol=1e-5)
+
+
+def _llama_tp_sp_worker(rank, world, port, q):
+    _llama_tp_worker(rank, world, port, q, sp=True)
 
 
 # ----------------------------------------------------------------------------- interleaved pipeline (VPP)
