@@ -67,9 +67,10 @@ def parse():
     p.add_argument("--resnet", type=int, default=1, help="also run the ResNet-50 DP benchmark")
     p.add_argument("--resnet-batch", type=int, default=256, help="per-GPU ResNet-50 batch")
     p.add_argument("--resnet-steps", type=int, default=10)
-    p.add_argument("--resnet-graph", type=int, default=0,
-                   help="capture the ResNet-50 training step into a hipGraph and replay it (1 GPU; measured "
-                        "+0.8%%: the eager step already keeps the GPU ~97%% busy)")
+    p.add_argument("--resnet-graph", type=int, default=1,
+                   help="capture the ResNet-50 training step into a hipGraph and replay it (1 GPU only; "
+                        "round 5 same-box A/B: 9,456 / 9,475 vs 9,245 / 9,308 img/s eager, "
+                        "profiles/resnet50_graph_ab_r5.log); multi-rank runs keep eager steps")
     p.add_argument("--resnet-layout", default="nhwc", choices=["nhwc", "nchw-autotune"],
                    help="nhwc: channels-last model; nchw-autotune: Paddle's default NCHW model with "
                         "FLAGS_layout_autotune (NHWC kernels on channels-last views)")
@@ -399,12 +400,18 @@ def resnet_bench(args, paddle, world, dist_on):
             step()
         torch.cuda.synchronize()
         from paddlepaddle_amd.device.cuda.graphs import CUDAGraph
-        g = CUDAGraph()
-        g.capture_begin()
-        step()
-        g.capture_end()
-        run = g.replay
-        resnet_bench.graph = True
+        try:
+            g = CUDAGraph()
+            g.capture_begin()
+            try:
+                step()
+            finally:
+                g.capture_end()
+            run = g.replay
+            resnet_bench.graph = True
+        except Exception as e:  # pragma: no cover - capture unsupported here: keep eager steps
+            log(f"[resnet50] hipGraph capture failed ({type(e).__name__}: {e}); timing eager steps")
+            torch.cuda.synchronize()
     dt = timed(run, args.resnet_steps, max(args.warmup, 3), dist_on)
     ips = args.resnet_steps * B * world / dt
     log(f"[resnet50] step={dt / args.resnet_steps * 1000:.1f}ms img/s={ips:.0f}" +
