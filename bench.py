@@ -223,7 +223,7 @@ LLAMA_TP_PLAN = {
     "layers.*.self_attn.q_proj": "col", "layers.*.self_attn.k_proj": "col", "layers.*.self_attn.v_proj": "col",
     "layers.*.self_attn.qkv_proj": "col", "layers.*.self_attn.o_proj": "row", "layers.*.mlp.gate_proj": "col",
     "layers.*.mlp.up_proj": "col", "layers.*.mlp.gate_up_proj": "col", "layers.*.mlp.down_proj": "row",
-    "lm_head": "col"}
+    "lm_head": "col", "embed_tokens": "row"}  # vocab-parallel embedding and (engine) vocab-parallel cross entropy
 
 
 def llama_static_bench(args, paddle, world, dist_on):

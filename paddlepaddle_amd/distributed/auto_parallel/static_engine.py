@@ -103,6 +103,32 @@ def _my(gr):
     return 0 if gr[1] is None else gr[1].index(C.get_rank())
 
 
+def _vp_cross_entropy(logits, labels, ignore_index, gr):
+    """Vocab-parallel softmax cross entropy on this rank's vocabulary slice (reference passes
+    auto_parallel_replace_with_parallel_cross_entropy.py -> c_softmax_with_cross_entropy): one all-gather of the
+    per-token (logsumexp, label logit) pairs over the group instead of gathering the logits."""
+    import types
+    from ...ops.loss import softmax_cross_entropy
+    from ...parallel.tensor_parallel import _ParallelCE
+    if gr[0] is None:
+        return softmax_cross_entropy(logits, labels, ignore_index)
+    g = types.SimpleNamespace(nranks=_nranks(gr), rank=_my(gr), process_group=gr[0])
+    V = logits.shape[-1]
+    return _ParallelCE.apply(logits.reshape(-1, V), labels.reshape(-1).long(), g, ignore_index).view(labels.shape)
+
+
+def _vp_embedding(ids, weight, gr):
+    """Vocab-parallel embedding lookup (reference passes auto_parallel_c_embedding_pass.py -> c_embedding): rows of
+    this rank's vocabulary slice, zero for ids owned by other ranks — a Partial(sum) output the engine all-reduces
+    where a replicated value is needed, instead of gathering the table."""
+    per = weight.shape[0]
+    start = _my(gr) * per
+    local = ids - start
+    mask = (local < 0) | (local >= per)
+    emb = torch.nn.functional.embedding(local.masked_fill(mask, 0), weight)
+    return emb.masked_fill(mask.unsqueeze(-1), 0.0)
+
+
 def gr_n(eng, stage, d):
     """Size of mesh dim ``d`` of ``stage``'s mesh."""
     m = eng.meshes[stage]
@@ -355,6 +381,10 @@ class StaticEngine:
         # strategy.sp_optimization: Partial -> Shard reshards (a row-parallel output entering a sequence-parallel
         # region) as one reduce-scatter (_ReduceScatter) instead of all-reduce + slice
         self.sp_opt = bool(strategy.sp_optimization.get("enable", False))
+        # vocabulary-sharded cross entropy / embedding on the local slice (reference passes
+        # replace_with_parallel_cross_entropy / auto_parallel_c_embedding_pass); FLAGS-free switch for A/B
+        self.vocab_parallel = bool(strategy.fused_passes.get("vocab_parallel", True))
+        self.vocab_parallel_ops = 0
         # strategy.gradient_merge (reference passes/auto_parallel_gradient_merge.py): gradients of k_steps calls
         # accumulate; the k-th call (scaled by 1/k when avg) synchronises them and runs the optimizer
         gm = strategy.gradient_merge
@@ -884,6 +914,11 @@ class StaticEngine:
                 self._alias(stage, o.i, loc, want)
             return
         want, out_pl, ctp = self._rule(n, name, refs, nd)
+        fn = n.func
+        vp = None
+        if self.vocab_parallel and name in ("softmax_cross_entropy", "embedding"):
+            want, out_pl = [list(w) for w in want], list(out_pl)
+            vp = self._vocab_parallel(name, refs, nd, want, out_pl, stage)
         # inputs: convert to the wanted placements, wrap replicated inputs of split computations
         sub = {}
         for r, w in zip(refs, want):
@@ -899,14 +934,45 @@ class StaticEngine:
         if name == "qkv_rope_attention":
             args, kwargs = self._local_qkv_attn_args(n, args, out_pl, stage)
             kwargs = self._subst(kwargs, sub)
+        if vp is not None:  # vocabulary-sharded CE / embedding on the local slice (+ the group's collective)
+            fn, d = vp
+            if name == "embedding":
+                args, kwargs = (args[0], args[1], ("G", stage, d)), {}
+            else:
+                ign = args[2] if len(args) > 2 else kwargs.get("ignore_index", -100)
+                args, kwargs = (args[0], args[1], ign, ("G", stage, d)), {}
+            self.vocab_parallel_ops += 1
         for o in out_refs:
             m = prog._metas[o.i]
             self.info[o.i] = _Info(mesh, out_pl, tuple(m.shape))
             self.slot_stage[o.i] = stage
-        self.stage_nodes[stage].append(_LNode(n.func, args, kwargs, n.outs, n.name, self._cur_rc))
+        self.stage_nodes[stage].append(_LNode(fn, args, kwargs, n.outs, n.name, self._cur_rc))
         if n.outs is None:  # in-place op on its first argument
             for r in refs[:1]:
                 self.slot_stage[r.i] = stage
+
+    def _vocab_parallel(self, name, refs, nd, want, out_pl, stage):
+        """(local function, mesh dim) when ``n`` is a softmax cross entropy whose logits are sharded on the vocabulary
+        (last) dim, or an embedding lookup whose table is sharded on the vocabulary (first) dim, over exactly one mesh
+        dim; the wanted / output placements are rewritten for the local computation (labels / ids replicated on that
+        dim; CE output replicated, embedding output Partial(sum))."""
+        if name not in ("softmax_cross_entropy", "embedding") or len(refs) < 2:
+            return None
+        a, b = self.info[refs[0].i], self.info[refs[1].i]
+        if name == "softmax_cross_entropy":
+            rank = len(a.shape)
+            dims = [d for d in range(nd) if _is_s(a.pl[d]) and a.pl[d][1] % rank == rank - 1]
+            if len(dims) != 1 or a.shape[-1] % max(gr_n(self, stage, dims[0]), 1):
+                return None
+            d = dims[0]
+            want[0][d], want[1][d], out_pl[d] = a.pl[d], R, R
+            return _vp_cross_entropy, d
+        dims = [d for d in range(nd) if _is_s(b.pl[d]) and b.pl[d][1] % 2 == 0]
+        if len(dims) != 1 or _is_s(a.pl[dims[0]]):
+            return None
+        d = dims[0]
+        want[0][d], want[1][d], out_pl[d] = R, b.pl[d], PSUM()
+        return _vp_embedding, d
 
     def _alias(self, stage, out_slot, src_slot, pl):
         self._emit(stage, "alias", lambda x: x, (P._Ref(src_slot),), out_slot)

@@ -69,6 +69,9 @@ def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap
     eng = dm._engine
     kinds = sorted({n.name for nodes in eng.stage_nodes for n in nodes if n.name in (
         "allreduce", "allgather", "slice", "copy_to_parallel")})
+    if mp > 1 and eng.my_stage == len(eng.meshes) - 1:
+        # the vocab-sharded LM head feeds the vocab-parallel cross entropy (no logits gather)
+        assert eng.vocab_parallel_ops >= 1, eng.vocab_parallel_ops
     if pp > 1:
         # pipeline p2p (parallel/p2p.py): the meta of each (peer, direction, slot) crossed once in the whole run
         ep = eng._p2p.ep
@@ -163,7 +166,7 @@ def _worker_fused(rank, world, port, shape, acc, schedule, q):
 LLAMA_PLAN = {
     "layers.*.self_attn.q_proj": "col", "layers.*.self_attn.k_proj": "col", "layers.*.self_attn.v_proj": "col",
     "layers.*.self_attn.o_proj": "row", "layers.*.mlp.gate_proj": "col", "layers.*.mlp.up_proj": "col",
-    "layers.*.mlp.down_proj": "row", "lm_head": "col"}
+    "layers.*.mlp.down_proj": "row", "lm_head": "col", "embed_tokens": "row"}  # vocab-parallel embedding
 
 
 def _worker_parallelize(rank, world, port, shape, acc, q, level=0):
@@ -192,6 +195,8 @@ def _worker_parallelize(rank, world, port, shape, acc, q, level=0):
     eng = dm._engine
     kinds = sorted({n.name for nodes in eng.stage_nodes for n in nodes if n.name in (
         "allreduce", "allgather", "slice", "copy_to_parallel")})
+    if mp > 1:  # vocab-parallel embedding (Partial output) and cross entropy on the local vocabulary slices
+        assert eng.vocab_parallel_ops >= 2, eng.vocab_parallel_ops
     # program passes on the traced model (static_engine._apply_passes): q / k / v and gate / up of every layer are
     # one multi_linear node, both RMSNorms of every layer carry the residual gradient
     L = cfg.num_hidden_layers
