@@ -733,6 +733,9 @@ class StaticEngine:
             self.pass_stats["sibling_linears"] = ctx.get_attr("fuse_sibling_linears.fused", 0)
         if self.strategy.mp_optimization.get("allreduce_matmul_grad_overlapping", False):
             new_pass("allreduce_matmul_grad_overlapping").apply(self.prog, None)
+        if self.vocab_parallel:  # vocabulary-sharded CE / embedding on the local slices
+            new_pass("replace_with_parallel_cross_entropy").apply(self.prog, None)
+            new_pass("auto_parallel_c_embedding_pass").apply(self.prog, None)
         if self.zero_dim is not None:
             new_pass("auto_parallel_sharding", {"stage": self.zero_stage, "sharding_mesh_dim": self.zero_dim}).apply(
                 self.prog, None)
@@ -916,7 +919,8 @@ class StaticEngine:
         want, out_pl, ctp = self._rule(n, name, refs, nd)
         fn = n.func
         vp = None
-        if self.vocab_parallel and name in ("softmax_cross_entropy", "embedding"):
+        if (name == "softmax_cross_entropy" and getattr(prog, "_pa_vocab_ce", False)) or (
+                name == "embedding" and getattr(prog, "_pa_vocab_emb", False)):
             want, out_pl = [list(w) for w in want], list(out_pl)
             vp = self._vocab_parallel(name, refs, nd, want, out_pl, stage)
         # inputs: convert to the wanted placements, wrap replicated inputs of split computations

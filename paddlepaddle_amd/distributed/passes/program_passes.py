@@ -29,7 +29,8 @@ from ...static import program as P
 __all__ = ["FuseGemmEpiloguePass", "DeadCodeEliminationPass", "AMPPass", "FP16Pass", "GradientMergePass",
            "FuseSiblingLinearsPass", "FuseRMSNormResidualPass",
            "RecomputePass", "AllreduceMatmulGradOverlappingPass", "ShardingPass", "FuseBNActPass",
-           "FuseBNAddActPass", "FuseElewiseAddActPass"]
+           "FuseBNAddActPass", "FuseElewiseAddActPass", "FuseAllReducePass", "ReplaceWithParallelCrossEntropyPass",
+           "CEmbeddingPass"]
 
 _RELU = {"f:torch.nn.functional:relu", "f:torch:relu", "m:relu"}
 _GELU = {"o:paddlepaddle_amd.ops.activation:gelu", "f:torch.nn.functional:gelu"}
@@ -709,3 +710,31 @@ def _coalesced(nodes):
         return None
     run._pa_comm = ("all_reduce_coalesced", op, group)
     return P.OpNode(run, refs, {}, None, kind="comm", name="c:all_reduce_coalesced")
+
+
+@register_pass("replace_with_parallel_cross_entropy")
+class ReplaceWithParallelCrossEntropyPass(PassBase):
+    """Reference passes/auto_parallel_replace_with_parallel_cross_entropy.py: a softmax cross entropy whose logits
+    are sharded on the vocabulary runs on the local slice (c_softmax_with_cross_entropy) instead of gathering the
+    logits. The per-rank program exists only inside the static engine, so the pass marks the program and the
+    engine rewrites the op at partition time (static_engine._vocab_parallel: one all-gather of per-token
+    (logsumexp, label logit) pairs)."""
+
+    def _type(self):
+        return PassType.PARALLEL_OPT
+
+    def _apply_single_impl(self, prog, startup, context):
+        prog._pa_vocab_ce = True
+
+
+@register_pass("auto_parallel_c_embedding_pass")
+class CEmbeddingPass(PassBase):
+    """Reference passes/auto_parallel_c_embedding.py: an embedding lookup into a vocabulary-sharded table becomes
+    c_embedding (masked local lookup, Partial(sum) output) instead of gathering the table; marks the program for
+    the static engine's partition-time rewrite (static_engine._vocab_parallel)."""
+
+    def _type(self):
+        return PassType.PARALLEL_OPT
+
+    def _apply_single_impl(self, prog, startup, context):
+        prog._pa_vocab_emb = True

@@ -256,3 +256,14 @@ def test_fuse_all_reduce_pass_coalesces_collectives():
         assert fused == 2 and names == ["c:all_reduce_coalesced"], (fused, names)
         assert got == ref
         assert ref[0][0][0] == 6.0 and ref[1][0] == 1 + 2 and ref[2][0] == 3.0
+
+
+def test_vocab_parallel_passes_mark_program(static_mode):
+    """replace_with_parallel_cross_entropy / auto_parallel_c_embedding_pass mark the program for the static engine
+    (which rewrites the ops at partition time; parity in tests/test_auto_parallel_static.py)."""
+    main, st, *_ = _mlp()
+    ctx = dp.PassManager([dp.new_pass("replace_with_parallel_cross_entropy"),
+                          dp.new_pass("auto_parallel_c_embedding_pass")]).apply([main], [st])
+    assert main._pa_vocab_ce and main._pa_vocab_emb
+    assert len(dp.PassBase._REGISTERED_PASSES) >= 22
+    assert ctx is not None
