@@ -584,19 +584,28 @@ def _dp_sync(prog, optimizer):
 
 
 def _allreduce_mean(grads, pg):
-    """grads <- mean over ``pg``: one flat all-reduce per dtype (also the native executor's gradient hook)."""
+    """grads <- mean over ``pg``: flat all-reduces per dtype in buckets of FLAGS_dp_bucket_mb (few, large messages
+    for the xGMI rings without a second copy of every gradient); also the native executor's gradient hook."""
     import torch.distributed as tdist
+    from ..framework.flags import flag
     n = tdist.get_world_size(pg)
+    cap = max(1, int(flag("FLAGS_dp_bucket_mb", 128))) << 20
     by_dtype = {}
     for g in grads:
         by_dtype.setdefault(g.dtype, []).append(g)
     with torch.no_grad():
         for gs in by_dtype.values():
-            flat = torch.cat([g.reshape(-1) for g in gs])
-            tdist.all_reduce(flat, group=pg)
-            flat.mul_(1.0 / n)
-            off = 0
-            for g in gs:
-                k = g.numel()
-                g.copy_(flat[off:off + k].view_as(g))
-                off += k
+            bucket, size = [], 0
+            for i, g in enumerate(gs):
+                bucket.append(g)
+                size += g.numel() * g.element_size()
+                if size >= cap or i == len(gs) - 1:
+                    flat = torch.cat([x.reshape(-1) for x in bucket])
+                    tdist.all_reduce(flat, group=pg)
+                    flat.mul_(1.0 / n)
+                    off = 0
+                    for x in bucket:
+                        k = x.numel()
+                        x.copy_(flat[off:off + k].view_as(x))
+                        off += k
+                    bucket, size = [], 0
