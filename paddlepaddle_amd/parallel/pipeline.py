@@ -165,6 +165,9 @@ class PipelineParallel(nn.Layer):
         self._dp_sync = hcg.get_data_parallel_world_size() > 1
         self._p2p = None
         self._p2p_ordered = True  # 1F1B / FThenB / ZBH1 consume each directed channel in production order
+        # job order of the non-interleaved schedule (parallel/pp_schedules.py; ZBH1 is its own class)
+        mode = str(cfg.get("schedule_mode", "1F1B")).upper()
+        self.schedule_mode = mode if mode in ("1F1B", "FTHENB", "EAGER1F1B") else "1F1B"
 
     # --------------------------------------------------------------- p2p
     def _dev(self):
@@ -230,31 +233,20 @@ class PipelineParallel(nn.Layer):
         inputs, labels = (data if isinstance(data, (list, tuple)) and len(data) == 2 else (data, None))
         mb_in = self._split(inputs) if self.is_first else [None] * self.accumulate_steps
         mb_lb = self._split(labels) if (self.is_last and labels is not None) else [None] * self.accumulate_steps
-        n = self.accumulate_steps
-        warm = min(self.num_stages - self.stage_id - 1, n)
-        steady = n - warm
-        queue = []
-        losses = []
-        fi = bi = 0
-        for _ in range(warm):
-            x, y = self._forward_step(mb_in[fi], mb_lb[fi], fi)
-            queue.append((x, y))
-            if self.is_last:
-                losses.append(y)
-            fi += 1
-        for i in range(steady):
-            x, y = self._forward_step(mb_in[fi], mb_lb[fi], fi)
-            queue.append((x, y))
-            if self.is_last:
-                losses.append(y)
-            fi += 1
-            inp, out = queue.pop(0)
-            self._backward_step(inp, out, bi)
-            bi += 1
-        for _ in range(warm):
-            inp, out = queue.pop(0)
-            self._backward_step(inp, out, bi)
-            bi += 1
+        from .pp_schedules import schedule
+        queue, losses = {}, []
+        # 1F1B (default), FThenB or Eager1F1B job list of this stage: F = forward of micro-batch mb (its input
+        # received from the previous stage), B = its backward (the output gradient received from the next stage)
+        self.jobs = schedule(self.schedule_mode, self.num_stages, self.stage_id, self.accumulate_steps)
+        for kind, mb in self.jobs:
+            if kind == "F":
+                x, y = self._forward_step(mb_in[mb], mb_lb[mb], mb)
+                queue[mb] = (x, y)
+                if self.is_last:
+                    losses.append(y)
+            else:
+                inp, out = queue.pop(mb)
+                self._backward_step(inp, out, mb)
         return self._finish(losses)
 
     def _finish(self, losses):

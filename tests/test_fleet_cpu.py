@@ -141,6 +141,10 @@ def _pp_worker(rank, world, port, q, schedule="1F1B"):
         from paddlepaddle_amd.parallel.pipeline import PipelineParallelZeroBubble
         assert type(model) is PipelineParallelZeroBubble and model.deferred_wgrads > 0
         assert any(k == "W" for k, _ in model.jobs)
+    elif schedule in ("FThenB", "Eager1F1B"):  # the stage walked that schedule's job list
+        from paddlepaddle_amd.parallel import pp_schedules as PS
+        assert model.schedule_mode == schedule.upper()
+        assert model.jobs == PS.schedule(schedule.upper(), model.num_stages, model.stage_id, model.accumulate_steps)
     # p2p meta (shape / dtype) crossed each directed channel once; every later message carried only its tag
     ep = model._p2p
     assert ep.meta_exchanges == 1 and ep.messages == 3 * 2 + (2 if rank == 0 else 0), (ep.meta_exchanges,
@@ -152,7 +156,7 @@ def _pp_worker(rank, world, port, q, schedule="1F1B"):
     paddle.distributed.barrier()
 
 
-@pytest.mark.parametrize("schedule", ["1F1B", "ZBH1"])
+@pytest.mark.parametrize("schedule", ["1F1B", "ZBH1", "FThenB", "Eager1F1B"])
 def test_pipeline_1f1b_matches_single_process(schedule):
     sys.path.insert(0, ROOT)
     os.environ["PADDLE_AMD_FORCE_CPU"] = "1"
