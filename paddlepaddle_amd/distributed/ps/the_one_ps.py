@@ -514,6 +514,20 @@ class PsRuntime:
                 p._t.copy_(w.view_as(p._t).to(p._t.dtype))
             ent[1] = ver
 
+    def pull_dense(self, names=None):
+        """Overwrite the registered dense parameters (all, or ``names``) with the servers' current values; returns
+        how many were pulled (reference communicator.cc PullDense / RecvNoBarrier)."""
+        n = 0
+        for name, ent in self._dense.items():
+            if names is not None and name not in names:
+                continue
+            w, ver = self.client.pull_dense(name, 0)
+            with torch.no_grad():
+                ent[0]._t.copy_(w.view_as(ent[0]._t).to(ent[0]._t.dtype))
+            ent[1] = max(ent[1], ver)
+            n += 1
+        return n
+
     def save(self, dirname, mode=0):
         if self.comm is not None:
             self.comm.flush()

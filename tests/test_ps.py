@@ -176,9 +176,16 @@ def _ps_proc(role, index, n_servers, n_trainers, port, a_sync, outdir, q):
         fleet.barrier_worker()
         n_saved = fleet.save_persistables(None, outdir) if index == 0 else None
         fleet.barrier_worker()
+        from paddlepaddle_amd.distributed.communicator import Communicator
+        comm = Communicator(mode="ASYNC" if a_sync else "SYNC")
+        comm.start()
+        assert comm.create_client_to_client_connection() and comm.is_running()
+        # the servers' dense tables back into the parameters: after the barrier both trainers read one value
+        n_pulled = comm.pull_dense([fc.weight]) + comm.recv()
+        comm.stop()
         w = fc.weight.numpy().copy()
         fleet.stop_worker()
-        q.put(("trainer", index, (losses, w, n_saved)))
+        q.put(("trainer", index, (losses, w, n_saved, n_pulled)))
     except Exception as e:  # pragma: no cover - surfaced by the parent
         import traceback
         q.put(("error", index, traceback.format_exc() + repr(e)))
@@ -212,7 +219,7 @@ def _run_ps(a_sync, tmp_path, n_servers=2, n_trainers=2):
 @pytest.mark.timeout(300)
 def test_ps_sync_training_two_servers_two_trainers(tmp_path):
     res = _run_ps(False, tmp_path)
-    (l0, w0, n_saved), (l1, w1, _) = res[("trainer", 0)], res[("trainer", 1)]
+    (l0, w0, n_saved, _), (l1, w1, _, _) = res[("trainer", 0)], res[("trainer", 1)]
     # sync mode: one averaged dense update per step, so both trainers hold identical dense weights
     np.testing.assert_allclose(w0, w1, rtol=0, atol=0)
     for losses in (l0, l1):
@@ -232,6 +239,10 @@ def test_ps_async_training(tmp_path):
     for i in range(2):
         losses = res[("trainer", i)][0]
         assert np.mean(losses[-8:]) < np.mean(losses[:8]), losses
+    # Communicator.pull_dense / recv: one weight, then both dense tables (weight, bias); after the final barrier
+    # the pulled values are the servers' and agree between the trainers although their async steps did not
+    assert res[("trainer", 0)][3] == 1 + 2
+    np.testing.assert_allclose(res[("trainer", 0)][1], res[("trainer", 1)][1], rtol=0, atol=0)
 
 
 def test_rpc_api_single_worker():
