@@ -258,3 +258,19 @@ def test_rpc_api_single_worker():
         assert rpc.get_worker_info("solo").rank == 0
     finally:
         rpc.shutdown()
+
+
+def test_communicator_handle_without_ps_worker():
+    """No parameter-server worker: the handle tracks its run state and the table calls raise instead of
+    silently doing nothing (reference communicator.py:129-201)."""
+    from paddlepaddle_amd.distributed.communicator import Communicator
+    c = Communicator(mode="SYNC")
+    assert c.mode == "sync" and not c.is_running()
+    c.start()
+    assert c.is_running()
+    with pytest.raises(RuntimeError, match="init_worker"):
+        c.pull_dense(None)
+    with pytest.raises(RuntimeError, match="init_worker"):
+        c.create_client_to_client_connection()
+    c.stop()
+    assert not c.is_running()
