@@ -106,10 +106,22 @@ PA_EXPORT int pa_flash_attn_fwd(const void* q, const void* k, const void* v, voi
 // strides: host array of 24 int64 = q, k, v, o, do, dq, dk, dv  (each b,s,h). dk / dv are [.., Hk, D] (summed
 // over the query heads of each KV head in-kernel). dq_acc: fp32 [rows, H, D] contiguous, rows = B*Sq
 // (dense) or total_q (varlen, `q_rows`); delta: same layout as lse.
-PA_EXPORT int pa_flash_attn_bwd_ex(const void* q, const void* k, const void* v, const void* o, const void* dout,
-                                   const float* lse, void* dq, void* dk, void* dv, float* dq_acc, float* delta,
-                                   const int64_t* strides, int B, int Sq, int Sk, int H, int Hk, int D, float scale,
-                                   int causal, int64_t q_rows, const PaAttnExtra* ex, hipStream_t st) {
+// dS route eligibility (fa_bwd16_kernel<.., true> + fa_bwd_dq_kernel): D = 128, no mask / flashmask / dropout,
+// dense batches. The caller allocates the dS^T scratch [B*H][ceil128(Sk)][ceil128(Sq)] 16-bit elements.
+PA_EXPORT int pa_flash_attn_bwd_ds_ok(int D, int has_mask, int has_fm, int dropout, int varlen) {
+  const char* env = getenv("PA_FA_BWD_DS");
+  if (env != nullptr && atoi(env) == 0) return 0;
+  const char* k16_env = getenv("PA_FA_BWD16");
+  if (k16_env != nullptr && atoi(k16_env) != 1) return 0;
+  const char* abl_env = getenv("PA_FA_BWD_ABL");
+  if (abl_env != nullptr && atoi(abl_env) != 0) return 0;
+  return D == 128 && !has_mask && !has_fm && !dropout && !varlen;
+}
+
+static int flash_attn_bwd_impl(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                               const float* lse, void* dq, void* dk, void* dv, float* dq_acc, float* delta,
+                               const int64_t* strides, int B, int Sq, int Sk, int H, int Hk, int D, float scale,
+                               int causal, int64_t q_rows, const PaAttnExtra* ex, void* ds, hipStream_t st) {
   if (H % Hk != 0) return 3;
   if (D != 128 && D != 64 && D != 256) return 4;
   const int64_t* qs = strides; const int64_t* ks = strides + 3; const int64_t* vs = strides + 6;
@@ -129,7 +141,21 @@ PA_EXPORT int pa_flash_attn_bwd_ex(const void* q, const void* k, const void* v, 
                          DS, H, D, st);
   PA_CHECK_LAUNCH();
   const int64_t rows = varlen ? q_rows : (int64_t)B * Sq;
-  hipMemsetAsync(dq_acc, 0, (size_t)rows * H * D * sizeof(float), st);
+  a.ds = nullptr;
+  a.ds_ld = 0;
+  a.ds_rows = 0;
+  a.dq = (uint16_t*)dq;
+  for (int i = 0; i < 3; ++i) a.dqs[i] = dqs[i];
+  a.dq_grp = 0;
+  if (ds != nullptr) {
+    if (varlen || D != 128) return 7;
+    a.ds = (uint16_t*)ds;
+    a.ds_ld = (Sq + 127) / 128 * 128;
+    a.ds_rows = (Sk + 127) / 128 * 128;
+    a.dq_grp = fa_group(B * H, (Sq + 127) / 128, 64);
+  } else {
+    hipMemsetAsync(dq_acc, 0, (size_t)rows * H * D * sizeof(float), st);
+  }
   a.q = (const uint16_t*)q; a.k = (const uint16_t*)k; a.v = (const uint16_t*)v; a.o = (const uint16_t*)o;
   a.dout = (const uint16_t*)dout; a.lse = lse; a.dq_acc = dq_acc; a.delta = delta;
   a.dk = (uint16_t*)dk; a.dv = (uint16_t*)dv;
@@ -149,14 +175,37 @@ PA_EXPORT int pa_flash_attn_bwd_ex(const void* q, const void* k, const void* v, 
   dim3 grid((unsigned)(B * Hk * nkb));
   const int feat = fa_features(a.mask_kind, a.fm, a.dropout);
   if (feat < 0) return 6;
+  if (ds != nullptr && feat != 0) return 7;
   if (f16) pa_fa_bwd_f16(a, D, feat, grid, st);
   else fa_bwd_dispatch<false>(a, D, feat, grid, st);
   PA_CHECK_LAUNCH();
+  if (ds != nullptr) return 0;  // dQ written by fa_bwd_dq_kernel
   if (f16) pa_fa_bwd_aux_f16(1, a, nullptr, nullptr, nullptr, nullptr, nullptr, dq_acc, (uint16_t*)dq, dqs, DB, DS, H, D,
                              st);
   else fa_bwd_aux<false>(1, a, nullptr, nullptr, nullptr, nullptr, nullptr, dq_acc, (uint16_t*)dq, dqs, DB, DS, H, D, st);
   PA_CHECK_LAUNCH();
   return 0;
+}
+
+PA_EXPORT int pa_flash_attn_bwd_ex(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                                   const float* lse, void* dq, void* dk, void* dv, float* dq_acc, float* delta,
+                                   const int64_t* strides, int B, int Sq, int Sk, int H, int Hk, int D, float scale,
+                                   int causal, int64_t q_rows, const PaAttnExtra* ex, hipStream_t st) {
+  return flash_attn_bwd_impl(q, k, v, o, dout, lse, dq, dk, dv, dq_acc, delta, strides, B, Sq, Sk, H, Hk, D, scale,
+                             causal, q_rows, ex, nullptr, st);
+}
+
+// the dS route: ds = scratch of pa_flash_attn_bwd_ds_bytes bytes; dq_acc unused (may be null)
+PA_EXPORT int64_t pa_flash_attn_bwd_ds_bytes(int B, int Sq, int Sk, int H) {
+  return (int64_t)B * H * ((Sk + 127) / 128 * 128) * ((Sq + 127) / 128 * 128) * 2;
+}
+
+PA_EXPORT int pa_flash_attn_bwd_ds(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                                   const float* lse, void* dq, void* dk, void* dv, void* ds, float* delta,
+                                   const int64_t* strides, int B, int Sq, int Sk, int H, int Hk, int D, float scale,
+                                   int causal, const PaAttnExtra* ex, hipStream_t st) {
+  return flash_attn_bwd_impl(q, k, v, o, dout, lse, dq, dk, dv, nullptr, delta, strides, B, Sq, Sk, H, Hk, D, scale,
+                             causal, (int64_t)B * Sq, ex, ds, st);
 }
 
 PA_EXPORT int pa_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,

@@ -596,6 +596,11 @@ struct BwdArgs {
   int64_t lse_s[2];
   int abl;  // measurement ablations (0 in normal runs): 1 dQ atomics dropped, 2 dQ step skipped, 4 dK/dV GEMMs skipped
   int k16;  // 1: the 8-wave 16-keys-per-wave kernel (fa_bwd16_kernel) for D = 128 without mask / dropout
+  // dS route (fa_bwd16_kernel<.., true> + fa_bwd_dq_kernel): unscaled dS^T tiles [B*H][ds_rows keys][ds_ld queries]
+  // (16-bit) instead of fp32 dQ atomics; ds == nullptr: the atomics kernels
+  uint16_t* ds; int64_t ds_ld; int ds_rows;
+  uint16_t* dq; int64_t dqs[3];
+  int dq_grp;  // block_map group of the dQ kernel's grid
 };
 
 // delta[b,h,q] = sum_d dO * O   (delta / lse index = b * lse_s0 + h * lse_s1 + q)
@@ -1076,7 +1081,12 @@ __device__ __forceinline__ int dst_off(int row, int col4) {
   return row * 64 + ((col4 ^ ((row >> 1) & 7)) << 3);
 }
 
-template <bool F16>
+// DSQ (the dS route): the pipelined dQ step is replaced by a coalesced copy of the block's dS^T image
+// [128 keys][32 queries] to p.ds (one 16-byte store per thread); fa_bwd_dq_kernel computes dQ = scale * dS K from
+// it. No fp32 dQ buffer, no atomics (they held the kernel at the chip's atomic rate: 4096 fp32 adds per block
+// per workgroup), no convert pass. Query blocks start at a 128-aligned row so every dS^T tile the dQ kernel
+// reads below the causal diagonal has been written (zeros where masked).
+template <bool F16, bool DSQ>
 __global__ __launch_bounds__(512, 1) void fa_bwd16_kernel(BwdArgs p) {
   constexpr int D = 128, NCH = 16, NW = 8, NT = NW * 64, BK = 128, BM = 32;
   constexpr int KT_BYTES = BK * D * 2;
@@ -1142,7 +1152,7 @@ __global__ __launch_bounds__(512, 1) void fa_bwd16_kernel(BwdArgs p) {
 
   int q_begin0 = 0;
   if (p.causal) q_begin0 = max(0, kb * BK - shift);
-  q_begin0 = (q_begin0 / BM) * BM;
+  q_begin0 = DSQ ? (q_begin0 / 128) * 128 : (q_begin0 / BM) * BM;
   const int h0 = hk * G;
   const int64_t dq_row0 = varlen ? (int64_t)q_start : (int64_t)b * p.Sq;
 
@@ -1207,6 +1217,17 @@ __global__ __launch_bounds__(512, 1) void fa_bwd16_kernel(BwdArgs p) {
         __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(qacc[qt][i] * p.scale, dq_rsrc, off, 0, 0);
       }
   };
+  // DSQ: thread -> (key row tid / 4, 8-query chunk tid % 4) of the [128][32] dS^T image; one global_store_dwordx4
+  // (inline asm: exactly one vector-memory op per lane, which the counted vmcnt at the loop top relies on)
+  const int st_row = tid >> 2, st_c = tid & 3;
+  const int st_o0 = dst_off(st_row, 2 * st_c), st_o1 = dst_off(st_row, 2 * st_c + 1);
+  auto ds_store = [&](const char* dsb, int h, int qb0) {
+    const uint2 lo = *reinterpret_cast<const uint2*>(dsb + st_o0);
+    const uint2 hi2 = *reinterpret_cast<const uint2*>(dsb + st_o1);
+    const u32x4 v = {lo.x, lo.y, hi2.x, hi2.y};
+    uint16_t* dst = p.ds + ((int64_t)(b * p.H + h) * p.ds_rows + kb * BK + st_row) * p.ds_ld + qb0 + 8 * st_c;
+    asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(dst), "v"(v) : "memory");
+  };
 
   for (int hi = 0; hi < G; ++hi) {
     const int h = h0 + hi;
@@ -1222,12 +1243,20 @@ __global__ __launch_bounds__(512, 1) void fa_bwd16_kernel(BwdArgs p) {
       const int sl = it & 1;
       // this block's stage has landed: the loads were issued in the previous pass, before its 8 dQ atomics
       if (!last) {
-        if (it >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (it >= 2) {
+          if constexpr (DSQ) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
       }
       lds_barrier();  // every wave's stage data visible; the previous pass's reads of the other stage done
       if (!last && it + 1 < n_qb) prefetch(h, q0 + BM, sl ^ 1);
-      if (it > 0 && p.k16 == 1) dq_step(ds_lds + (((it - 1) & 1) * DST_BYTES), h, q0 - BM);
+      if constexpr (DSQ) {
+        if (it > 0) ds_store(ds_lds + (((it - 1) & 1) * DST_BYTES), h, q0 - BM);
+      } else {
+        if (it > 0 && p.k16 == 1) dq_step(ds_lds + (((it - 1) & 1) * DST_BYTES), h, q0 - BM);
+      }
       if (last) break;
 
       const char* q_lds = q_st + sl * QT_BYTES;
@@ -1325,6 +1354,108 @@ __global__ __launch_bounds__(512, 1) void fa_bwd16_kernel(BwdArgs p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// dQ of the dS route: dQ[b, q, h, :] = scale * sum_key dS[q][key] K[b, key, hk, :] from the dS^T tiles written by
+// fa_bwd16_kernel<.., true>. One workgroup = 4 waves = 128 queries x 128 d of one (batch, head); key steps of 64.
+// Both operands are MN-major 64-row images ([64 keys][128 queries] of dS^T, [64 keys][128 d] of K, 256-byte rows)
+// filled by LDS-DMA with the chunk swizzle on the source address, read with ds_read_b64_tr_b16 (the MN-major
+// fragment read of gemm.hip). Waves 2 x 2, 64 x 64 outputs each (4 x 4 MFMA 16x16x32 tiles). Two LDS stages
+// (64 KiB): two workgroups per CU. Causal: key steps up to the block's last visible key; heaviest blocks first.
+__device__ __forceinline__ int dq_swz(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
+
+__device__ __forceinline__ Frag dq_frag(const char* img, int rbase, int s, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+  const int col = rbase + pp * 4;
+  const int lc = col >> 3, sub = (col & 7) * 2;
+  const int k1 = s * 32 + g * 8 + q, k2 = k1 + 4;
+  Frag f;
+  f.h[0] = lds_tr(img, k1 * 256 + ((lc ^ dq_swz(k1)) << 4) + sub);
+  f.h[1] = lds_tr(img, k2 * 256 + ((lc ^ dq_swz(k2)) << 4) + sub);
+  return f;
+}
+
+template <bool F16>
+__global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs p) {
+  constexpr int TB = 64 * 128 * 2;  // one operand image: 16 KiB
+  __shared__ __attribute__((aligned(1024))) char smem[4 * TB];
+  const int nqb = (p.Sq + 127) / 128;
+  int bh, rank;
+  block_map((int)blockIdx.x, p.B * p.H, nqb, p.dq_grp, bh, rank);
+  const int qb = p.causal ? (nqb - 1 - rank) : rank;
+  const int b = bh / p.H, h = bh % p.H, hk = h / (p.H / p.Hk);
+  const int q0 = qb * 128;
+  const int shift = p.Sk - p.Sq;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int wm = w >> 1, wn = w & 1;
+  int kend = p.Sk;
+  if (p.causal) kend = min(p.Sk, min(q0 + 127, p.Sq - 1) + shift + 1);
+  const int nkt = kend > 0 ? (kend + 63) / 64 : 0;
+
+  const uint16_t* ds = p.ds + (int64_t)bh * p.ds_rows * p.ds_ld + q0;
+  const uint16_t* kb = p.k + (int64_t)b * p.ks[0] + (int64_t)hk * p.ks[2];
+  // per-lane staging geometry: 4 pieces of 1 KiB per operand per wave (piece = 4 k-rows of 256 B)
+  int srow[4], scol[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int lin = (i * 4 + w) * 64 + lane;
+    srow[i] = lin >> 4;
+    scol[i] = ((lin & 15) ^ dq_swz(srow[i])) * 8;
+  }
+  auto issue = [&](int t, int st) {
+    char* a_img = smem + st * 2 * TB;
+    char* b_img = a_img + TB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int key = t * 64 + srow[i];
+      glds16_fa(ds + (int64_t)key * p.ds_ld + scol[i], a_img + (i * 4 + w) * 1024);
+      const int kc = key < p.Sk ? key : p.Sk - 1;
+      glds16_fa(kb + (int64_t)kc * p.ks[1] + scol[i], b_img + (i * 4 + w) * 1024);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nkt > 0) issue(0, 0);
+  for (int t = 0; t < nkt; ++t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t (the only loads in flight) has landed
+    lds_barrier();                                      // ... for every wave; stage (t+1)&1 no longer read
+    if (t + 1 < nkt) issue(t + 1, (t + 1) & 1);
+    const char* a_img = smem + (t & 1) * 2 * TB;
+    const char* b_img = a_img + TB;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      Frag af[4], bf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = dq_frag(a_img, wm * 64 + i * 16, s, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = dq_frag(b_img, wn * 64 + j * 16, s, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16<F16>(bf[j], af[i], acc[i][j]);
+    }
+  }
+  // lane: query q0 + 64wm + 16i + (lane & 15), d = 64wn + 16j + 4(lane >> 4) .. +3
+  uint16_t* dqb = p.dq + (int64_t)b * p.dqs[0] + (int64_t)h * p.dqs[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = q0 + wm * 64 + i * 16 + (lane & 15);
+    if (q >= p.Sq) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int d = wn * 64 + j * 16 + 4 * (lane >> 4);
+      uint2 o;
+      o.x = pack2<F16>(acc[i][j][0] * p.scale, acc[i][j][1] * p.scale);
+      o.y = pack2<F16>(acc[i][j][2] * p.scale, acc[i][j][3] * p.scale);
+      *reinterpret_cast<uint2*>(dqb + (int64_t)q * p.dqs[1] + d) = o;
+    }
+  }
+}
+
 // ---- launch helpers (one instantiation set per 16-bit type: flash_attn.hip = bf16, flash_attn_f16.hip = fp16)
 template <int D, bool F16, int MW>
 void fa_fwd_feat(const FwdArgs& a, int feat, dim3 grid, hipStream_t st) {
@@ -1369,8 +1500,14 @@ void fa_bwd_feat(const BwdArgs& a, int feat, dim3 grid, hipStream_t st) {
 
 template <bool F16>
 void fa_bwd_dispatch(const BwdArgs& a, int D, int feat, dim3 grid, hipStream_t st) {
+  if (D == 128 && feat == 0 && a.ds != nullptr) {  // dS route (the caller checked eligibility)
+    hipLaunchKernelGGL((fa_bwd16_kernel<F16, true>), grid, dim3(512), 0, st, a);
+    const int nqb = (a.Sq + 127) / 128;
+    hipLaunchKernelGGL((fa_bwd_dq_kernel<F16>), dim3((unsigned)(a.B * a.H * nqb)), dim3(256), 0, st, a);
+    return;
+  }
   if (D == 128 && feat == 0 && a.k16 && a.abl == 0) {
-    hipLaunchKernelGGL((fa_bwd16_kernel<F16>), grid, dim3(512), 0, st, a);
+    hipLaunchKernelGGL((fa_bwd16_kernel<F16, false>), grid, dim3(512), 0, st, a);
     return;
   }
   if (D == 128) fa_bwd_feat<128, F16, 4, true>(a, feat, grid, st);

@@ -52,6 +52,10 @@ SIGS = {
                              _vp],
     "pa_flash_attn_bwd_ex": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                              _i32, _i32, _i32, _i32, _i32, _i32, _f32, _i32, _i64, _vp, _vp],
+    "pa_flash_attn_bwd_ds": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                             _i32, _i32, _i32, _i32, _i32, _i32, _f32, _i32, _vp, _vp],
+    "pa_flash_attn_bwd_ds_ok": [_i32, _i32, _i32, _i32, _i32],
+    "pa_flash_attn_bwd_ds_bytes": [_i32, _i32, _i32, _i32],
     "pa_fa_fm_stats": [_vp, _i32, _i32, _i32, _i32, _i32, _i64, _i64, _i32, _vp, _vp],
     "pa_paged_decode_attn": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
                              _i64, _i64, _f32, _vp],
@@ -135,5 +139,5 @@ SIGS = {
     "pa_version": [],
 }
 
-RET_I64 = {"pa_gemm_pp_ws_bytes", "pa_gemm_fp8_ws_bytes", "pa_gemm_pp_splitk_ws_bytes", "pa_bn_pre_ws", "pa_gemm_skinny_stats_chunks", "pa_conv_skinny_stats_chunks",
+RET_I64 = {"pa_flash_attn_bwd_ds_bytes", "pa_gemm_pp_ws_bytes", "pa_gemm_fp8_ws_bytes", "pa_gemm_pp_splitk_ws_bytes", "pa_bn_pre_ws", "pa_gemm_skinny_stats_chunks", "pa_conv_skinny_stats_chunks",
            "pa_colsum_nparts"}

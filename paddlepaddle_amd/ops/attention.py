@@ -207,11 +207,30 @@ def _fa_fwd(q, k, v, job):
     return o, lse
 
 
+def _ds_budget_bytes():
+    import os
+    return int(float(os.environ.get("PA_FA_BWD_DS_MAX_GB", "16")) * (1 << 30))
+
+
 def _fa_bwd(q, k, v, o, lse, do, dq, dk, dv, job):
-    dq_acc = torch.empty(job.q_rows, job.H, job.D, dtype=torch.float32, device=q.device)
     delta = torch.empty(job.lse_shape(), dtype=torch.float32, device=q.device)
     st = _i64arr(_strides(q) + _strides(k) + _strides(v) + _strides(o) + _strides(do) + _strides(dq)
                  + _strides(dk) + _strides(dv))
+    ex = job.ex
+    lib = L.lib()
+    if lib.pa_flash_attn_bwd_ds_ok(int(job.D), int(bool(ex.mask)), int(bool(ex.fm)), int(ex.drop_p > 0),
+                                   int(job.varlen)):
+        nbytes = int(lib.pa_flash_attn_bwd_ds_bytes(job.B, job.Sq, job.Sk, job.H))
+        if nbytes <= _ds_budget_bytes():
+            # dS route: unscaled dS^T tiles (16-bit) in a transient scratch, dQ = scale * dS K by its own kernel;
+            # no fp32 dQ buffer / atomics / convert pass (csrc/kernels/flash_attn_kernels.h fa_bwd_dq_kernel)
+            ds = torch.empty(nbytes // 2, dtype=q.dtype, device=q.device)
+            L.CALLS["flash_attn_bwd_ds"] = L.CALLS.get("flash_attn_bwd_ds", 0) + 1
+            L.call("pa_flash_attn_bwd_ds", L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(o), L.ptr(do), L.ptr(lse), L.ptr(dq),
+                   L.ptr(dk), L.ptr(dv), L.ptr(ds), L.ptr(delta), st, job.B, job.Sq, job.Sk, job.H, job.Hk, job.D,
+                   job.scale, int(job.causal), ctypes.addressof(job.ex), L.stream_ptr())
+            return
+    dq_acc = torch.empty(job.q_rows, job.H, job.D, dtype=torch.float32, device=q.device)
     L.call("pa_flash_attn_bwd_ex", L.ptr(q), L.ptr(k), L.ptr(v), L.ptr(o), L.ptr(do), L.ptr(lse), L.ptr(dq),
            L.ptr(dk), L.ptr(dv), L.ptr(dq_acc), L.ptr(delta), st, job.B, job.Sq, job.Sk, job.H, job.Hk, job.D,
            job.scale, int(job.causal), int(job.q_rows), ctypes.addressof(job.ex), L.stream_ptr())

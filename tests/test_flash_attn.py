@@ -33,7 +33,8 @@ def _run(B, Sq, Sk, H, Hk, D, causal, dt=torch.bfloat16, spike=False, seed=0):
         scale = b.abs().max().item() + 1e-6
         e = (a.float() - b).abs().max().item() / scale
         assert e < 2.5e-2, f"{name} rel err {e}"
-    assert L.calls("pa_flash_attn_fwd_ex") > 0 and L.calls("pa_flash_attn_bwd_ex") > 0
+    assert L.calls("pa_flash_attn_fwd_ex") > 0
+    assert L.calls("pa_flash_attn_bwd_ex") + L.calls("pa_flash_attn_bwd_ds") > 0
     assert L.calls("attn_aten_fallback") == 0
 
 
@@ -98,3 +99,20 @@ def test_fa_bwd16_kernel(monkeypatch, causal, shape, k16):
     monkeypatch.setenv("PA_FA_BWD16", k16)
     B, Sq, Sk, H, Hk = shape
     _run(B, Sq, Sk, H, Hk, 128, causal)
+
+
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("shape", [(2, 256, 256, 4, 4), (1, 300, 300, 2, 2), (2, 192, 192, 8, 2), (1, 128, 320, 2, 2),
+                                   (1, 320, 128, 2, 1), (1, 200, 456, 4, 2), (1, 1024, 1024, 2, 2)])
+@pytest.mark.parametrize("ds", ["1", "0"])
+def test_fa_bwd_ds_route(monkeypatch, causal, shape, ds):
+    """D = 128 backward through the dS route (dS^T tiles + the dQ kernel, no fp32 atomics; the default) and the
+    atomics kernel (PA_FA_BWD_DS=0), against the fp32 reference: ragged lengths, GQA, Sq < Sk and Sq > Sk causal."""
+    monkeypatch.setenv("PA_FA_BWD_DS", ds)
+    B, Sq, Sk, H, Hk = shape
+    L.reset_calls()
+    _run(B, Sq, Sk, H, Hk, 128, causal)
+    if ds == "1":
+        assert L.calls("flash_attn_bwd_ds") > 0 and L.calls("pa_flash_attn_bwd_ex") == 0
+    else:
+        assert L.calls("flash_attn_bwd_ds") == 0 and L.calls("pa_flash_attn_bwd_ex") > 0
