@@ -114,7 +114,8 @@ def _vp_cross_entropy(logits, labels, ignore_index, gr):
         return softmax_cross_entropy(logits, labels, ignore_index)
     g = types.SimpleNamespace(nranks=_nranks(gr), rank=_my(gr), process_group=gr[0])
     V = logits.shape[-1]
-    return _ParallelCE.apply(logits.reshape(-1, V), labels.reshape(-1).long(), g, ignore_index).view(labels.shape)
+    # shaped like the traced op's output (logits.shape[:-1]), also for Paddle-style [B, S, 1] labels
+    return _ParallelCE.apply(logits.reshape(-1, V), labels.reshape(-1).long(), g, ignore_index).view(logits.shape[:-1])
 
 
 def _vp_embedding(ids, weight, gr):
@@ -473,15 +474,87 @@ class StaticEngine:
             ctx = new_pass("auto_parallel_recompute", {"checkpoints": cp_slots}).apply(prog, None)
             self.pass_stats_rc = ctx.get_attr("auto_parallel_recompute.segments", 0)
         self._apply_passes()
+        info0 = {k: _Info(v.mesh, v.pl, v.shape) for k, v in self.info.items()}
+        self._keep_ctp = set()
         self._propagate_and_partition()
+        red = self._dp_reduced_params() if self._zero_d is not None else set()
+        if red:
+            if self._zero_shard:
+                raise NotImplementedError("static engine ZeRO: a parameter reaches a data-parallel computation through "
+                                          "another op (e.g. a transposed / tied weight); use strategy.sharding off here")
+            # plain data parallelism: such parameters keep their per-micro-batch all-reduce inside autograd (for
+            # every use, also the direct ones) and stay out of the once-per-step flat-buffer synchronisation
+            self._keep_ctp = red
+            self.info = info0
+            self.vocab_parallel_ops = 0
+            self._propagate_and_partition()
         if getattr(self.prog, "_pa_tp_overlap", False):
             self._overlap_tp_dx_allreduce()
         self._build_segments()
         self._localize_params()
         if self._zero_d is not None:
-            self._zero_check_partition()
+            if self._zero_shard:
+                self._zero_check_partition()
             self._zero_setup()
         self.built = True
+
+    _CONVERSIONS = ("allgather", "slice", "alias", "to_partial", "allreduce", "reduce_scatter", "copy_to_parallel")
+
+    def _dp_reduced_params(self):
+        """Parameter slots whose gradient must not be synchronised once per step on the flat buffers, because it is
+        not the sum of per-rank local-batch contributions:
+        (a) ancestors of a non-parameter slot that enters a dp-split computation through copy_to_parallel (a
+            placement conversion of a parameter): that gradient is all-reduced inside autograd already;
+        (b) parameters read (directly or through conversions) by a computation whose output is replicated over the
+            dp dim (e.g. a weight used after its dp-sharded input was gathered, or a transposed / tied weight): every
+            rank holds that whole contribution, summing would scale it by the dp degree.
+        Those keep the per-micro-batch all-reduce of every dp-split use (the pre-ZeRO semantics)."""
+        out = set()
+        zd = self._zero_d
+        for nodes in self.stage_nodes:
+            producer, readers = {}, {}
+            for nd in nodes:
+                for o in _flat_tensor_refs(nd.outs, []) if nd.outs is not None else []:
+                    producer[o.i] = nd
+                for r in _flat_tensor_refs((nd.args, nd.kwargs), []):
+                    readers.setdefault(r.i, []).append(nd)
+            for nd in nodes:  # (a)
+                if nd.name != "copy_to_parallel" or nd.args[1][2] != zd:
+                    continue
+                src = nd.args[0].i
+                if src in self._param_slot_set:
+                    continue
+                stack, seen = [src], set()
+                while stack:
+                    sl = stack.pop()
+                    if sl in seen:
+                        continue
+                    seen.add(sl)
+                    if sl in self._param_slot_set:
+                        out.add(sl)
+                        continue
+                    q = producer.get(sl)
+                    if q is not None:
+                        stack.extend(r.i for r in _flat_tensor_refs((q.args, q.kwargs), []))
+            for ps in self._param_slot_set:  # (b)
+                if ps in out:
+                    continue
+                stack, seen = [ps], set()
+                while stack and ps not in out:
+                    sl = stack.pop()
+                    if sl in seen:
+                        continue
+                    seen.add(sl)
+                    for nd in readers.get(sl, ()):
+                        outs = _flat_tensor_refs(nd.outs, []) if nd.outs is not None else []
+                        if nd.name in self._CONVERSIONS:
+                            stack.extend(o.i for o in outs)
+                            continue
+                        inf = self.info.get(outs[0].i) if outs else None
+                        if inf is not None and len(inf.pl) > zd and not (_is_s(inf.pl[zd]) or _is_p(inf.pl[zd])):
+                            out.add(ps)
+                            break
+        return out
 
     def _overlap_tp_dx_allreduce(self):
         """strategy.mp_optimization.allreduce_matmul_grad_overlapping (reference:
@@ -869,7 +942,7 @@ class StaticEngine:
         return cur
 
     def _copy_to_parallel(self, stage, slot, dims):
-        if self._zero_d is not None and slot in self._param_slot_set:
+        if self._zero_d is not None and slot in self._param_slot_set and slot not in self._keep_ctp:
             # ZeRO: a parameter's data-parallel gradient is not all-reduced per micro-batch; the local gradients
             # accumulate and are reduce-scattered once per step (_zero_step)
             dims = [d for d in dims if d != self._zero_d]
@@ -922,7 +995,7 @@ class StaticEngine:
         if (name == "softmax_cross_entropy" and getattr(prog, "_pa_vocab_ce", False)) or (
                 name == "embedding" and getattr(prog, "_pa_vocab_emb", False)):
             want, out_pl = [list(w) for w in want], list(out_pl)
-            vp = self._vocab_parallel(name, refs, nd, want, out_pl, stage)
+            vp = self._vocab_parallel(n, name, refs, nd, want, out_pl, stage)
         # inputs: convert to the wanted placements, wrap replicated inputs of split computations
         sub = {}
         for r, w in zip(refs, want):
@@ -955,7 +1028,7 @@ class StaticEngine:
             for r in refs[:1]:
                 self.slot_stage[r.i] = stage
 
-    def _vocab_parallel(self, name, refs, nd, want, out_pl, stage):
+    def _vocab_parallel(self, n, name, refs, nd, want, out_pl, stage):
         """(local function, mesh dim) when ``n`` is a softmax cross entropy whose logits are sharded on the vocabulary
         (last) dim, or an embedding lookup whose table is sharded on the vocabulary (first) dim, over exactly one mesh
         dim; the wanted / output placements are rewritten for the local computation (labels / ids replicated on that
@@ -975,6 +1048,16 @@ class StaticEngine:
         if len(dims) != 1 or _is_s(a.pl[dims[0]]):
             return None
         d = dims[0]
+        # equal row shards only (start = rank * rows), and no padding_idx / max_norm / sparse arguments: those keep
+        # the table-gather path, whose lookup is the traced op itself
+        if b.shape[0] % max(gr_n(self, stage, d), 1):
+            return None
+        names = ("padding_idx", "max_norm", "norm_type", "scale_grad_by_freq", "sparse")
+        ex = dict(zip(names, n.args[2:]))
+        ex.update({k: v for k, v in (n.kwargs or {}).items() if k in names})
+        if ex.get("padding_idx") is not None or ex.get("max_norm") is not None or ex.get("scale_grad_by_freq") \
+                or ex.get("sparse"):
+            return None
         want[0][d], want[1][d], out_pl[d] = R, b.pl[d], PSUM()
         return _vp_embedding, d
 
@@ -1310,7 +1393,7 @@ class StaticEngine:
         groups = {}
         for slot, p in self.local_params.items():
             t = p._t
-            if not t.requires_grad or t.numel() == 0:
+            if not t.requires_grad or t.numel() == 0 or slot in self._keep_ctp:
                 continue
             if shard and (p.optimize_attr.get("learning_rate", 1.0) != 1.0 or p.regularizer is not None
                           or not p.need_clip):
@@ -1455,6 +1538,10 @@ class StaticEngine:
             self.opt.step()
             for z in self._zero:
                 z["gflat"].zero_()
+            for slot in self._keep_ctp:  # outside the flat buffers (in-autograd dp all-reduce): cleared as usual
+                p = self.local_params.get(slot)
+                if p is not None and p._t.grad is not None:
+                    p._t.grad = None
             return
         for z in self._zero:
             if self._zero_pg is not None:
