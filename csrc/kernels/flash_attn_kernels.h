@@ -1217,15 +1217,23 @@ __global__ __launch_bounds__(512, 1) void fa_bwd16_kernel(BwdArgs p) {
         __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(qacc[qt][i] * p.scale, dq_rsrc, off, 0, 0);
       }
   };
-  // DSQ: thread -> (key row tid / 4, 8-query chunk tid % 4) of the [128][32] dS^T image; one global_store_dwordx4
-  // (inline asm: exactly one vector-memory op per lane, which the counted vmcnt at the loop top relies on)
-  const int st_row = tid >> 2, st_c = tid & 3;
-  const int st_o0 = dst_off(st_row, 2 * st_c), st_o1 = dst_off(st_row, 2 * st_c + 1);
+  // DSQ: the block's dS [32 q][128 keys] goes to the scratch in key groups of 32: group g (keys 32g..32g+31) is a
+  // row-major [ds_ld queries][32 keys] matrix, so a dQ key step reads 128 contiguous 64-byte rows (one 8 KiB run)
+  // and this store writes 4 runs of 2 KiB. Wave w reads the fragment (keys 32ks.., queries 16qt..) of the dS^T image
+  // transposed (the dQ operand read of the atomics kernel): lane (r16, kg) holds keys 8kg..8kg+7 of query 16qt + r16
+  // = 16 contiguous bytes; one global_store_dwordx4 per lane (inline asm: exactly one vector-memory op, which the
+  // counted vmcnt at the loop top relies on), 1 KiB contiguous per wave instruction.
+  const int st_ks = w >> 1, st_qt = w & 1;
+  const int st_o0 = (dst_off(8 * kg + tq, tp) ^ (32 * st_qt)) + 2048 * st_ks;
+  const int st_o1 = (dst_off(8 * kg + 4 + tq, tp) ^ (32 * st_qt)) + 2048 * st_ks;
+  const int64_t nkg = p.ds_rows / 32;
   auto ds_store = [&](const char* dsb, int h, int qb0) {
-    const uint2 lo = *reinterpret_cast<const uint2*>(dsb + st_o0);
-    const uint2 hi2 = *reinterpret_cast<const uint2*>(dsb + st_o1);
-    const u32x4 v = {lo.x, lo.y, hi2.x, hi2.y};
-    uint16_t* dst = p.ds + ((int64_t)(b * p.H + h) * p.ds_rows + kb * BK + st_row) * p.ds_ld + qb0 + 8 * st_c;
+    Frag a;
+    a.h[0] = lds_tr(dsb, st_o0);
+    a.h[1] = lds_tr(dsb, st_o1);
+    const u32x4 v = {a.u.x, a.u.y, a.u.z, a.u.w};
+    uint16_t* dst = p.ds + (((int64_t)(b * p.H + h) * nkg + kb * 4 + st_ks) * p.ds_ld + qb0 + 16 * st_qt + r16) * 32 +
+                    8 * kg;
     asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(dst), "v"(v) : "memory");
   };
 
@@ -1355,29 +1363,39 @@ __global__ __launch_bounds__(512, 1) void fa_bwd16_kernel(BwdArgs p) {
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// dQ of the dS route: dQ[b, q, h, :] = scale * sum_key dS[q][key] K[b, key, hk, :] from the dS^T tiles written by
-// fa_bwd16_kernel<.., true>. One workgroup = 4 waves = 128 queries x 128 d of one (batch, head); key steps of 64.
-// Both operands are MN-major 64-row images ([64 keys][128 queries] of dS^T, [64 keys][128 d] of K, 256-byte rows)
-// filled by LDS-DMA with the chunk swizzle on the source address, read with ds_read_b64_tr_b16 (the MN-major
-// fragment read of gemm.hip). Waves 2 x 2, 64 x 64 outputs each (4 x 4 MFMA 16x16x32 tiles). Two LDS stages
-// (64 KiB): two workgroups per CU. Causal: key steps up to the block's last visible key; heaviest blocks first.
+// dQ of the dS route: dQ[b, q, h, :] = scale * sum_key dS[q][key] K[b, key, hk, :] from the dS tiles written by
+// fa_bwd16_kernel<.., true> (key groups of 32: [ds_ld queries][32 keys] row-major each). One workgroup = 4 waves =
+// 128 queries x 128 d of one (batch, head); key steps of 32 = one key group: the A operand is one contiguous 8 KiB
+// run ([128 q][32 keys], K-major: ds_read_b128 fragments, 16-byte chunks swizzled by ((row >> 3) & 1) << 1), the B
+// operand K [32 keys][128 d] an MN-major image read with ds_read_b64_tr_b16 (the MN-major fragment read of
+// gemm.hip). Both filled by LDS-DMA with the swizzle on the source address. Waves 2 x 2, 64 x 64 outputs each
+// (4 x 4 MFMA 16x16x32 tiles). The dS stream is read once from HBM, so the loop is load-latency bound: a 4-slot LDS
+// ring (64 KiB) keeps three key steps in flight per workgroup and two workgroups share a CU. Causal: key steps up to
+// the block's last visible key; heaviest blocks first.
 __device__ __forceinline__ int dq_swz(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
 
-__device__ __forceinline__ Frag dq_frag(const char* img, int rbase, int s, int lane) {
+__device__ __forceinline__ Frag dq_frag(const char* img, int rbase, int lane) {
   const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
   const int col = rbase + pp * 4;
   const int lc = col >> 3, sub = (col & 7) * 2;
-  const int k1 = s * 32 + g * 8 + q, k2 = k1 + 4;
+  const int k1 = g * 8 + q, k2 = k1 + 4;
   Frag f;
   f.h[0] = lds_tr(img, k1 * 256 + ((lc ^ dq_swz(k1)) << 4) + sub);
   f.h[1] = lds_tr(img, k2 * 256 + ((lc ^ dq_swz(k2)) << 4) + sub);
   return f;
 }
 
+__device__ __forceinline__ void dq_wait_after(int n) {  // "all but the 4 n youngest loads" (4 glds per lane per step)
+  if (n >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 template <bool F16>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs p) {
-  constexpr int TB = 64 * 128 * 2;  // one operand image: 16 KiB
-  __shared__ __attribute__((aligned(1024))) char smem[4 * TB];
+  constexpr int TB = 32 * 128 * 2;  // one operand image: 8 KiB
+  constexpr int NS = 4;             // ring slots
+  __shared__ __attribute__((aligned(1024))) char smem[NS * 2 * TB];
   const int nqb = (p.Sq + 127) / 128;
   int bh, rank;
   block_map((int)blockIdx.x, p.B * p.H, nqb, p.dq_grp, bh, rank);
@@ -1389,25 +1407,29 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs p) {
   const int wm = w >> 1, wn = w & 1;
   int kend = p.Sk;
   if (p.causal) kend = min(p.Sk, min(q0 + 127, p.Sq - 1) + shift + 1);
-  const int nkt = kend > 0 ? (kend + 63) / 64 : 0;
+  const int nkt = kend > 0 ? (kend + 31) / 32 : 0;
 
-  const uint16_t* ds = p.ds + (int64_t)bh * p.ds_rows * p.ds_ld + q0;
+  const uint16_t* ds = p.ds + ((int64_t)bh * (p.ds_rows / 32) * p.ds_ld + q0) * 32;  // key group 0, query q0
+  const int64_t ds_grp = p.ds_ld * 32;                                               // elements per key group
   const uint16_t* kb = p.k + (int64_t)b * p.ks[0] + (int64_t)hk * p.ks[2];
-  // per-lane staging geometry: 4 pieces of 1 KiB per operand per wave (piece = 4 k-rows of 256 B)
-  int srow[4], scol[4];
+  // per-lane staging geometry: 2 pieces of 1 KiB per operand per wave. A (K-major): piece = 16 query rows of 64 B;
+  // B (MN-major): piece = 4 key rows of 256 B
+  int aoff[2], srow[2], scol[2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 2; ++i) {
     const int lin = (i * 4 + w) * 64 + lane;
+    const int arow = lin >> 2;
+    aoff[i] = arow * 32 + (((lin & 3) ^ (((arow >> 3) & 1) << 1)) * 8);
     srow[i] = lin >> 4;
     scol[i] = ((lin & 15) ^ dq_swz(srow[i])) * 8;
   }
-  auto issue = [&](int t, int st) {
-    char* a_img = smem + st * 2 * TB;
+  auto issue = [&](int t) {
+    char* a_img = smem + (t % NS) * 2 * TB;
     char* b_img = a_img + TB;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int key = t * 64 + srow[i];
-      glds16_fa(ds + (int64_t)key * p.ds_ld + scol[i], a_img + (i * 4 + w) * 1024);
+    for (int i = 0; i < 2; ++i) {
+      glds16_fa(ds + t * ds_grp + aoff[i], a_img + (i * 4 + w) * 1024);
+      const int key = t * 32 + srow[i];
       const int kc = key < p.Sk ? key : p.Sk - 1;
       glds16_fa(kb + (int64_t)kc * p.ks[1] + scol[i], b_img + (i * 4 + w) * 1024);
     }
@@ -1419,25 +1441,25 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(BwdArgs p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nkt > 0) issue(0, 0);
+  for (int t = 0; t < min(nkt, NS - 1); ++t) issue(t);
   for (int t = 0; t < nkt; ++t) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t (the only loads in flight) has landed
-    lds_barrier();                                      // ... for every wave; stage (t+1)&1 no longer read
-    if (t + 1 < nkt) issue(t + 1, (t + 1) & 1);
-    const char* a_img = smem + (t & 1) * 2 * TB;
+    dq_wait_after(min(nkt - 1 - t, NS - 2));  // step t landed (this wave's part); later steps stay in flight
+    lds_barrier();                            // ... for every wave; slot (t - 1) % NS no longer read
+    if (t + NS - 1 < nkt) issue(t + NS - 1);
+    const char* a_img = smem + (t % NS) * 2 * TB;
     const char* b_img = a_img + TB;
+    Frag af[4], bf[4];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      Frag af[4], bf[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = dq_frag(a_img, wm * 64 + i * 16, s, lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bf[j] = dq_frag(b_img, wn * 64 + j * 16, s, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16<F16>(bf[j], af[i], acc[i][j]);
+    for (int i = 0; i < 4; ++i) {  // A[q = row][keys 8c..8c+7], c = lane >> 4
+      const int row = wm * 64 + i * 16 + (lane & 15);
+      af[i].u = lds_b128(a_img, row * 64 + (((lane >> 4) ^ (((row >> 3) & 1) << 1)) << 4));
     }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[j] = dq_frag(b_img, wn * 64 + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16<F16>(bf[j], af[i], acc[i][j]);
   }
   // lane: query q0 + 64wm + 16i + (lane & 15), d = 64wn + 16j + 4(lane >> 4) .. +3
   uint16_t* dqb = p.dq + (int64_t)b * p.dqs[0] + (int64_t)h * p.dqs[2];
