@@ -1654,6 +1654,8 @@ class StaticEngine:
         for slot, v in zip(self.feed_slots, self._feeds_local(inputs, labels, mb)):
             env[slot] = v.to(self.dev)
         received = []
+        if not self.stage_inputs[s]:
+            p2p.flush()  # nothing to receive: the sends queued by the previous job go out now
         for slot in sorted(self.stage_inputs[s]):
             t = p2p.recv(self._peer(self.slot_stage[slot]), ("F", slot, mb))
             if t.is_floating_point():
@@ -1677,6 +1679,8 @@ class StaticEngine:
     def _backward_mb(self, mb, state, p2p):
         received, sent, loss = state
         outs, grads = [], []
+        if not any(t.requires_grad for _slot, t, _d in sent):
+            p2p.flush()  # no output gradient to receive (last stage)
         for slot, t, dsts in sent:
             if not t.requires_grad:
                 continue
@@ -1751,6 +1755,7 @@ class StaticEngine:
             elif kind == "B":
                 self._backward_mb(mb, states.pop(mb), p2p)
             else:
+                p2p.flush()
                 LIN.apply_weight_grads(wq.pop(mb))
         p2p.join()
         loss = torch.stack(losses).mean() if losses else torch.zeros((), device=self.dev)
@@ -1778,12 +1783,14 @@ class _P2P:
     the meta cache persists. Keys are ("F" | "B", slot, micro-batch)."""
 
     def __init__(self, dev):
-        from ...parallel.p2p import P2P, host_twin
+        from ...parallel.p2p import P2P, host_twin, payload_twin
         ws = dist.get_world_size() if dist.is_initialized() else 1
         host = host_twin([list(range(ws))], dist.get_rank()) if ws > 1 else None
+        down = payload_twin([list(range(ws))], dist.get_rank()) if ws > 1 else None
         # ordered: every stage walks its 1F1B / FThenB / ZBH1 job list and its slots in sorted order, so each
-        # directed channel is consumed in production order (no per-message header, parallel/p2p.py)
-        self.ep = P2P(dev, None, host, ordered=True)
+        # directed channel is consumed in production order (no per-message header, parallel/p2p.py); payloads to a
+        # lower rank on the world's twin group, batched per job with the queued sends (pp_comm.py)
+        self.ep = P2P(dev, None, host, ordered=True, down_group=down)
 
     @staticmethod
     def _tag(key):
@@ -1798,6 +1805,9 @@ class _P2P:
 
     def join(self):
         self.ep.join()
+
+    def flush(self):
+        self.ep.flush()
 
     def begin_run(self):
         self.ep.begin_run()

@@ -107,6 +107,11 @@ class HybridCommunicateGroup:
         if self._pp_degree > 1 and C.is_initialized():
             from ...parallel.p2p import host_twin
             self._pipe_host = host_twin(self._topo.get_comm_list("pipe"), self.global_rank)
+        # payload twin of the pipe groups: p2p messages to a lower rank travel there (parallel/p2p.py)
+        self._pipe_down = None
+        if self._pp_degree > 1 and C.is_initialized():
+            from ...parallel.p2p import payload_twin
+            self._pipe_down = payload_twin(self._topo.get_comm_list("pipe"), self.global_rank)
         # check group for global grad-norm (all ranks that hold distinct param shards)
         self._check_group = None
 
@@ -185,8 +190,12 @@ class HybridCommunicateGroup:
         return self._groups["pipe"]
 
     def get_pipe_parallel_host_group(self):
-        """gloo twin of this rank's pipe group (None on gloo worlds, where the group itself carries host tensors)."""
+        """gloo twin of this rank's pipe group (headers and tags of pipeline p2p travel there)."""
         return self._pipe_host
+
+    def get_pipe_parallel_down_group(self):
+        """Second payload group of this rank's pipe group (messages to a lower rank; parallel/p2p.py)."""
+        return self._pipe_down
 
     def is_first_stage(self):
         return self.stage_id == 0

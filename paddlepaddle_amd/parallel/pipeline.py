@@ -180,8 +180,11 @@ class PipelineParallel(nn.Layer):
         if self._p2p is None:
             host = self._hcg.get_pipe_parallel_host_group() if hasattr(self._hcg, "get_pipe_parallel_host_group") \
                 else None
+            down = self._hcg.get_pipe_parallel_down_group() if hasattr(self._hcg, "get_pipe_parallel_down_group") \
+                else None
             # ordered (no per-message header) unless the schedule consumes a channel out of production order
-            self._p2p = P2P(self._dev(), self.group.process_group, host, ordered=self._p2p_ordered)
+            self._p2p = P2P(self._dev(), self.group.process_group, host, ordered=self._p2p_ordered,
+                            record=getattr(self, "_p2p_record", False), down_group=down)
         return self._p2p
 
     def _send(self, t, dst, kind=_FWD, key=(0, 0)):
@@ -206,8 +209,14 @@ class PipelineParallel(nn.Layer):
         n = self.accumulate_steps
         return [_wrap(c) for c in t.chunk(n, 0)]
 
+    def _flush(self):
+        """A job that receives nothing issues the sends the previous job queued before its compute (p2p.py)."""
+        if self._p2p is not None:
+            self._p2p.flush()
+
     def _forward_step(self, mb_input, mb_label, mb=0):
         if self.is_first:
+            self._flush()
             x = mb_input
         else:
             xt = self._recv(self.prev_rank, _FWD, (0, mb)).requires_grad_(True)
@@ -221,6 +230,7 @@ class PipelineParallel(nn.Layer):
 
     def _backward_step(self, inp, out, mb=0):
         if self.is_last:
+            self._flush()
             (out._t / self.accumulate_steps).backward()
         else:
             g = self._recv(self.next_rank, _BWD, (0, mb))
@@ -252,11 +262,10 @@ class PipelineParallel(nn.Layer):
     def _finish(self, losses):
         self._join_sends()
         if self._dp_sync:
-            g = self._hcg.get_data_parallel_group()
-            for p in self._layers.parameters():
-                if p._t.grad is not None:
-                    dist.all_reduce(p._t.grad, op=dist.ReduceOp.SUM, group=g.process_group)
-                    p._t.grad.mul_(1.0 / g.nranks)
+            # PP x DP: the stage's gradients averaged over its data-parallel group in flat per-dtype buckets (reference
+            # hybrid_parallel_util.fused_allreduce_gradients), not one all-reduce + scale per parameter
+            from ..distributed.fleet.utils.hybrid_parallel_util import fused_allreduce_gradients
+            fused_allreduce_gradients(list(self._layers.parameters()), self._hcg)
         # broadcast the mean loss from the last stage
         loss = torch.zeros((), device=self._dev())
         if self.is_last and losses:
@@ -337,6 +346,7 @@ class PipelineParallelZeroBubble(PipelineParallel):
                 wq[mb] = q
                 self.deferred_wgrads += len(q)
             else:
+                self._flush()
                 LIN.apply_weight_grads(wq.pop(mb))
         return self._finish(losses)
 
@@ -374,6 +384,7 @@ class PipelineParallelWithInterleave(PipelineParallel):
         first = self.stage_id == 0 and v == 0
         last = self.stage_id == self.num_stages - 1 and v == self.V - 1
         if first:
+            self._flush()
             x = mb_in[mb]
         else:
             # chunk v of stage 0 consumes chunk v-1 of the last stage (ring wrap)
@@ -392,6 +403,7 @@ class PipelineParallelWithInterleave(PipelineParallel):
         last = self.stage_id == self.num_stages - 1 and v == self.V - 1
         x, out = store.pop((v, mb))
         if last:
+            self._flush()
             (out._t / self.accumulate_steps).backward()
         else:
             # the gradient of chunk v's output comes from chunk v (or v+1 across the wrap) downstream
