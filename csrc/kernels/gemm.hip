@@ -59,7 +59,11 @@ enum EpiFlags : int {
   kEpiStats = 32,     // per-column batch-norm partials of the stored C (sum, sum of squares) to stats
   kEpiStatsBwd = 64,  // with kEpiStats: BN-backward partials instead (C is the BN's output gradient):
                       // sum dyp, sum dyp * (x - mean), dyp = relu mask (x * scale + shift > 0) of the stored C
+  kEpiGeluBwd = 128,  // C = result * gelu'(aux): aux holds the GELU's pre-activation (the data gradient of the
+                      // linear after a GELU, fused with the GELU backward; 256x256 kernels, staged epilogue)
+  kEpiColSum = 256,   // column sums of the result per 256-row tile to stats[tiles_m][N] (fp32; bias gradient)
 };
+constexpr int kEpiStaged = kEpiAux | kEpiAccum | kEpiOutF32 | kEpiGeluBwd | kEpiColSum;
 
 struct GemmArgs {
   const uint16_t* a;
@@ -515,6 +519,112 @@ using H3_ = IntC<3>;
 using True_ = IntC<1>;
 using False_ = IntC<0>;
 
+// Coalesced epilogue pass over 128 rows of a 256-column tile from the fp32 LDS image (kEpiRowStride floats per
+// row): each thread owns 8 consecutive columns and walks the rows NT / 32 at a time. Epilogues that read global
+// memory (accumulate into C, the GELU backward's pre-activation) issue the reads of 8 row steps before the first
+// is used: one memory latency per 8 steps instead of one per step (the loop-carried form left each step waiting
+// on its own read). kEpiGeluBwd excludes kEpiAccum.
+template <int NT>
+__device__ __forceinline__ void epi_rows(const GemmArgs& p, const float* img, int m_base, int n0, int tid,
+                                         const float* bv, float* cs) {
+  constexpr int RS = kEpiRowStride;
+  constexpr int RSTEP = NT / 32;
+  constexpr int NSTEP = 128 / RSTEP;
+  constexpr int G = 4;  // reads in flight per thread: register room next to the live accumulators
+  const int ec = (tid & 31) * 8, er = tid / 32;
+  const int n = n0 + ec;
+  if (n >= p.N) return;
+  const int flags = p.flags;
+  const bool f32 = flags & kEpiOutF32;
+  const bool rd_pre = flags & kEpiGeluBwd, rd_c = (flags & kEpiAccum) && !rd_pre;
+#pragma unroll 1
+  for (int g0 = 0; g0 < NSTEP; g0 += G) {
+    uint4 rd[G][2];
+    if (rd_pre || rd_c) {
+#pragma unroll
+      for (int s = 0; s < G; ++s) {
+        const int m = m_base + (g0 + s) * RSTEP + er;
+        rd[s][0] = rd[s][1] = make_uint4(0u, 0u, 0u, 0u);
+        if (m < p.M) {
+          const int64_t off = (int64_t)m * p.ldc + n;
+          if (rd_pre) {
+            rd[s][0] = *reinterpret_cast<const uint4*>(p.aux + off);
+          } else if (f32) {
+            rd[s][0] = *reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(p.c) + off);
+            rd[s][1] = *reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(p.c) + off + 4);
+          } else {
+            rd[s][0] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(p.c) + off);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < G; ++s) {
+      const int r = (g0 + s) * RSTEP + er;
+      const int m = m_base + r;
+      if (m >= p.M) break;
+      float v[8];
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(img + r * RS + ec);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(img + r * RS + ec + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = lo[e] * p.alpha + bv[e];
+        v[4 + e] = hi[e] * p.alpha + bv[4 + e];
+      }
+      const int64_t off = (int64_t)m * p.ldc + n;
+      if (flags & kEpiAux) store8<bf16>(reinterpret_cast<bf16*>(p.aux + off), v);
+      if (flags & kEpiGelu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
+      }
+      // the 8 bf16 (or fp32) values this step read ahead
+      float o[8];
+      if (rd_pre || (rd_c && !f32)) {
+        const uint4 u = rd[s][0];
+        o[0] = lo_bf16(u.x); o[1] = hi_bf16(u.x); o[2] = lo_bf16(u.y); o[3] = hi_bf16(u.y);
+        o[4] = lo_bf16(u.z); o[5] = hi_bf16(u.z); o[6] = lo_bf16(u.w); o[7] = hi_bf16(u.w);
+      } else if (rd_c) {
+        const uint4 u0 = rd[s][0], u1 = rd[s][1];
+        o[0] = __uint_as_float(u0.x); o[1] = __uint_as_float(u0.y); o[2] = __uint_as_float(u0.z);
+        o[3] = __uint_as_float(u0.w); o[4] = __uint_as_float(u1.x); o[5] = __uint_as_float(u1.y);
+        o[6] = __uint_as_float(u1.z); o[7] = __uint_as_float(u1.w);
+      }
+      if (rd_pre) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= gelu_tanh_grad_fast(o[e]);
+      } else if (rd_c) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += o[e];
+      }
+      if (flags & kEpiColSum) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) cs[e] += v[e];
+      }
+      if (f32) store8<float>(reinterpret_cast<float*>(p.c) + off, v);
+      else store8<bf16>(reinterpret_cast<bf16*>(reinterpret_cast<uint16_t*>(p.c) + off), v);
+    }
+  }
+}
+
+// kEpiColSum: the per-thread column sums of epi_rows (8 columns, its rows of the tile) folded over the NT / 32
+// threads that share those columns through LDS; one fp32 store per column of the tile (no atomics, deterministic).
+template <int NT>
+__device__ __forceinline__ void colsum_finish(const GemmArgs& p, float* red, const float* cs, int tid, int m0,
+                                              int n0) {
+  constexpr int R = NT / 32;
+  const int ec = (tid & 31) * 8, er = tid / 32;
+  __syncthreads();  // every thread is done reading the epilogue image
+  *reinterpret_cast<float4*>(red + er * 256 + ec) = make_float4(cs[0], cs[1], cs[2], cs[3]);
+  *reinterpret_cast<float4*>(red + er * 256 + ec + 4) = make_float4(cs[4], cs[5], cs[6], cs[7]);
+  __syncthreads();
+  for (int c = tid; c < 256; c += NT) {
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < R; ++r) s += red[r * 256 + c];
+    if (n0 + c < p.N) p.stats[(int64_t)(m0 >> 8) * p.N + n0 + c] = s;
+  }
+}
+
 // SEG: 0 plain operands; 1 K-segmented, 2 N-segmented operands (GemmArgs::nseg, pa_gemm_bf16_pp_segs). The
 // segment selection is compiled only into the segmented instantiations: the plain kernel's staging code (and its
 // register allocation) is the unsegmented ping-pong loop.
@@ -756,7 +866,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p0) {
   // (aux / accumulate read-modify-write) far below the HBM rate.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int flags = p.flags;
-  if (!(flags & (kEpiAux | kEpiAccum | kEpiOutF32))) {
+  if (!(flags & kEpiStaged)) {
     // bf16 output without aux / accumulate: alpha, bias and GELU applied in registers, the finished bf16 tile
     // staged through LDS in one pass ([256][264] bf16, 528-byte rows) instead of two fp32 halves
     uint16_t* im = reinterpret_cast<uint16_t*>(smem);
@@ -803,12 +913,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p0) {
   }
   float* img = reinterpret_cast<float*>(smem);
   constexpr int RS = kEpiRowStride;  // floats per image row
-  const int ec = (tid & 31) * 8;     // this thread's 8 columns of the tile
-  const int er = tid >> 5;           // first row (of 16 per step)
-  const int n = n0 + ec;
-  const bool n_ok = n < p.N;
   float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if ((flags & kEpiBias) && n_ok) load8<bf16>(reinterpret_cast<const bf16*>(p.bias + n), bv);
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  {
+    const int n = n0 + (tid & 31) * 8;
+    if ((flags & kEpiBias) && n < p.N) load8<bf16>(reinterpret_cast<const bf16*>(p.bias + n), bv);
+  }
 #pragma unroll
   for (int ah = 0; ah < 2; ++ah) {
     bar();
@@ -823,47 +933,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm256_kernel(GemmArgs p0) {
           *reinterpret_cast<f32x4*>(img + r * RS + c) = acc[ah][i][bh][j];
         }
     bar();
-    if (!n_ok) continue;
-#pragma unroll 2
-    for (int step = 0; step < 8; ++step) {
-      const int r = step * 16 + er;
-      const int m = m0 + ah * 128 + r;
-      if (m >= p.M) break;
-      float v[8];
-      const f32x4 lo = *reinterpret_cast<const f32x4*>(img + r * RS + ec);
-      const f32x4 hi = *reinterpret_cast<const f32x4*>(img + r * RS + ec + 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = lo[e] * p.alpha + bv[e];
-        v[4 + e] = hi[e] * p.alpha + bv[4 + e];
-      }
-      const int64_t off = (int64_t)m * p.ldc + n;
-      if (flags & kEpiAux) store8<bf16>(reinterpret_cast<bf16*>(p.aux + off), v);
-      if (flags & kEpiGelu) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
-      }
-      if (flags & kEpiOutF32) {
-        float* cp = reinterpret_cast<float*>(p.c) + off;
-        if (flags & kEpiAccum) {
-          float o[8];
-          load8<float>(cp, o);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += o[e];
-        }
-        store8<float>(cp, v);
-      } else {
-        bf16* cp = reinterpret_cast<bf16*>(reinterpret_cast<uint16_t*>(p.c) + off);
-        if (flags & kEpiAccum) {
-          float o[8];
-          load8<bf16>(cp, o);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += o[e];
-        }
-        store8<bf16>(cp, v);
-      }
-    }
+    epi_rows<kThreads>(p, img, m0 + ah * 128, n0, tid, bv, cs);
   }
+  if (flags & kEpiColSum) colsum_finish<kThreads>(p, img, cs, tid, m0, n0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -954,58 +1026,6 @@ __device__ __forceinline__ void wait_tiles_after(int n_after) {
   else if (n_after == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   else if (n_after == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// Coalesced epilogue pass over 128 rows of a 256-column tile from the fp32 LDS image (kEpiRowStride floats per
-// row): each thread owns 8 consecutive columns and walks the rows NT / 32 at a time.
-template <int NT>
-__device__ __forceinline__ void epi_rows(const GemmArgs& p, const float* img, int m_base, int n0, int tid,
-                                         const float* bv) {
-  constexpr int RS = kEpiRowStride;
-  constexpr int RSTEP = NT / 32;
-  const int ec = (tid & 31) * 8, er = tid / 32;
-  const int n = n0 + ec;
-  if (n >= p.N) return;
-  const int flags = p.flags;
-#pragma unroll 2
-  for (int step = 0; step < 128 / RSTEP; ++step) {
-    const int r = step * RSTEP + er;
-    const int m = m_base + r;
-    if (m >= p.M) break;
-    float v[8];
-    const f32x4 lo = *reinterpret_cast<const f32x4*>(img + r * RS + ec);
-    const f32x4 hi = *reinterpret_cast<const f32x4*>(img + r * RS + ec + 4);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      v[e] = lo[e] * p.alpha + bv[e];
-      v[4 + e] = hi[e] * p.alpha + bv[4 + e];
-    }
-    const int64_t off = (int64_t)m * p.ldc + n;
-    if (flags & kEpiAux) store8<bf16>(reinterpret_cast<bf16*>(p.aux + off), v);
-    if (flags & kEpiGelu) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
-    }
-    if (flags & kEpiOutF32) {
-      float* cp = reinterpret_cast<float*>(p.c) + off;
-      if (flags & kEpiAccum) {
-        float o[8];
-        load8<float>(cp, o);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += o[e];
-      }
-      store8<float>(cp, v);
-    } else {
-      bf16* cp = reinterpret_cast<bf16*>(reinterpret_cast<uint16_t*>(p.c) + off);
-      if (flags & kEpiAccum) {
-        float o[8];
-        load8<bf16>(cp, o);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += o[e];
-      }
-      store8<bf16>(cp, v);
-    }
-  }
 }
 
 // ABL (diagnostic ablations, timing only, wrong results): 1 = no global loads in the K-loop, 2 = no global
@@ -1138,6 +1158,7 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
 
   // epilogue through LDS, one 128-row half at a time (the two waves with wm == half write their accumulators)
   float* img = reinterpret_cast<float*>(smem);
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   {
     const int n = n0 + (tid & 31) * 8;
@@ -1157,268 +1178,9 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(GemmArgs p) {
         }
     }
     bar();
-    epi_rows<256>(p, img, m0 + h * 128, n0, tid, bv);
+    epi_rows<256>(p, img, m0 + h * 128, n0, tid, bv, cs);
   }
-}
-
-// ---------------------------------------------------------------------------------------------
-// 256x256x64 tiles, 4 waves (one per SIMD, 128 x 128 outputs each, 256 fp32 accumulators pinned to AGPRs), two
-// LDS stages of one K64 tile (2 x 64 KiB), every fragment of a K-tile held in registers:
-//   iteration t, phase A: 64 MFMAs on k-substep 0 of tile t while the 16 fragments of substep 1 are read out of
-//                         stage t % 2; lgkmcnt(0); barrier -> stage t % 2 is free on every wave
-//   phase B:              64 MFMAs on substep 1; the 16 LDS-DMA pieces (1 KiB each) of tile t + 2 are issued into
-//                         stage t % 2 between the first 32; vmcnt(16) (tile t + 1 landed: only tile t + 2's pieces
-//                         stay in flight) + barrier; the substep-0 fragments of tile t + 1 are read between the
-//                         last MFMAs.
-// Two barriers per K64 tile, a tile's loads in flight for a whole iteration, and a third less LDS read traffic per
-// MFMA than the 8-wave ping-pong kernel (128 x 128 wave tiles). The structure of the fastest vendor TN kernel on
-// gfx950 (hipBLASLt MT256x256x64 4-wave stream-K, measured in profiles/gemm_step_shapes_r5.md), written here for
-// every operand layout: K-major images [256][64] (128-B rows, chunk XOR (row >> 1) & 7, conflict-free
-// ds_read_b128), MN-major images [64][256] (512-B rows, mn_swz, ds_read_b64_tr_b16).
-template <bool KMAJ>
-struct Loader64 {
-  uint64_t base;    // wave-uniform address of (first row / column of the tile, k = 0)
-  uint64_t kstep;   // bytes per K64 tile
-  int voff[8];      // per-lane byte offsets of this wave's 8 pieces of the 32-KiB operand image
-
-  __device__ __forceinline__ void init(const uint16_t* g, int64_t ld, int r0, int rmax, int wave, int lane) {
-    base = reinterpret_cast<uint64_t>(g) + (KMAJ ? (uint64_t)r0 * ld * 2 : (uint64_t)r0 * 2);
-    kstep = KMAJ ? 128 : (uint64_t)ld * 128;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int q = i * 4 + wave;  // 1-KiB piece of the operand image
-      if constexpr (KMAJ) {
-        const int row = q * 8 + (lane >> 3);
-        const int c = (lane & 7) ^ ((row >> 1) & 7);
-        const int gr = min(r0 + row, rmax - 1) - r0;
-        voff[i] = gr * (int)ld * 2 + c * 16;
-      } else {
-        const int lin = q * 64 + lane;
-        const int row = lin >> 5;  // k
-        const int lc = (lin & 31) ^ mn_swz(row);
-        const int gc = min(r0 + lc * 8, rmax - 8) - r0;
-        voff[i] = row * (int)ld * 2 + gc * 2;
-      }
-    }
-  }
-  __device__ __forceinline__ void load(int t, int i, uint32_t img, int wave) const {
-    const uint64_t b = base + (uint64_t)t * kstep;
-    i32x4 srd;
-    srd[0] = (int)(uint32_t)b;
-    srd[1] = (int)((uint32_t)(b >> 32) & 0xffff);
-    srd[2] = -1;
-    srd[3] = 0x00020000;
-    const uint32_t m0 = img + (uint32_t)(i * 4 + wave) * 1024u;
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff[i]), "s"(srd),
-                 "s"(m0)
-                 : "memory");
-  }
-};
-
-template <bool AK, bool BKM>
-__global__ __launch_bounds__(256, 1) void gemm4k_kernel(GemmArgs p) {
-  constexpr int OPB = 256 * 64 * 2;  // 32 KiB per operand image
-  constexpr int STAGE = 2 * OPB;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int wm = wave >> 1, wn = wave & 1;
-
-  // balanced tail as in gemm256_kernel
-  const int bid = (int)blockIdx.x;
-  int pid;
-  float* tail_out = nullptr;
-  if (p.tail_split > 0 && bid >= p.full_tiles) {
-    const int u = bid - p.full_tiles;
-    const int ks = u % p.tail_split;
-    pid = p.full_tiles + u / p.tail_split;
-    p.K /= p.tail_split;
-    p.a += (int64_t)ks * p.K * (AK ? 1 : p.lda);
-    p.b += (int64_t)ks * p.K * (BKM ? 1 : p.ldb);
-    tail_out = p.tail_ws + (int64_t)u * 65536;
-  } else {
-    pid = xcd_remap(bid, p.tail_split > 0 ? p.full_tiles : p.tiles_m * p.tiles_n);
-  }
-  int tm, tn;
-  tile_coords(pid, p.tiles_m, p.tiles_n, &tm, &tn);
-  const int m0 = tm * 256, n0 = tn * 256;
-  const int nk = p.K / 64;
-
-  const int wv = __builtin_amdgcn_readfirstlane(wave);
-  Loader64<AK> la;
-  Loader64<BKM> lb;
-  la.init(p.a, p.lda, m0, p.M, wv, lane);
-  lb.init(p.b, p.ldb, n0, p.N, wv, lane);
-  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>(smem);
-  // piece i (0..7: A, 8..15: B) of this wave's share of K-tile t into stage t % 2
-  auto piece = [&](int t, int i) {
-    const uint32_t st = lds0 + (uint32_t)(t & 1) * STAGE;
-    if (i < 8) la.load(t, i, st, wv);
-    else lb.load(t, i - 8, st + OPB, wv);
-  };
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  asm volatile("s_nop 4" ::: "memory");  // v_accvgpr_write of the zeros -> first MFMA reading them as C
-
-  bf16x8_t a0[8], b0[8], a1[8], b1[8];
-  const int ar = wm * 128, bc = wn * 128;
-  // fragment r (0..7: A row group r, 8..15: B column group r - 8) of k-substep s of the tile in `stage`; the
-  // MFMA loops run B-group-major (the first MFMA operand, B, stays the same for 8 consecutive MFMAs), so the first
-  // 8 MFMAs of a substep need all A fragments and B fragment 0: read in this order
-  auto rdfrag = [&](const char* stage, int s, int r, bf16x8_t(&a)[8], bf16x8_t(&b)[8]) {
-    if (r < 8) a[r] = frag<256, AK>(stage, ar + r * 16, s, lane);
-    else b[r - 8] = frag<256, BKM>(stage + OPB, bc + (r - 8) * 16, s, lane);
-  };
-
-  // Event placement (MFMA index m = 8 * g + k within a phase, mirroring the vendor schedule): phase A reads the A
-  // fragments of substep 1 in m 1..15, B1 at m 23, A(t + 2) pieces in m 24..39, B fragments of substep 1 in
-  // m 25..40, B2 at m 55, B(t + 2) pieces from m 56 of phase A to m 7 of phase B; B3 (tile t + 1 landed) at phase-B
-  // m 27; the substep-0 fragments of tile t + 1 over phase-B m 28..59.
-  auto iter = [&](int t, auto steady) {
-    constexpr bool S = decltype(steady)::value;
-    const char* cur = smem + (t & 1) * STAGE;
-    const char* nxt = smem + ((t + 1) & 1) * STAGE;
-    const bool iss = S || t + 2 < nk;
-    const bool more = S || t + 1 < nk;
-#pragma unroll
-    for (int g = 0; g < 8; ++g)  // g: B column group (MFMA operand A, the output columns)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {  // k: A row group
-        const int m = 8 * g + k;
-        mfma_acc(acc[k][g], b0[g], a0[k]);
-        if (m >= 1 && m <= 15 && (m & 1)) rdfrag(cur, 1, m >> 1, a1, b1);            // A substep 1: r 0..7
-        if (m == 23) {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          bar();  // B1: every wave holds A(t)
-        }
-        if (m >= 24 && m <= 39 && !(m & 1) && iss) piece(t + 2, (m - 24) >> 1);     // A(t + 2): pieces 0..7
-        if (m >= 25 && m <= 40 && (m & 1)) rdfrag(cur, 1, 8 + ((m - 25) >> 1), a1, b1);  // B substep 1: r 8..15
-        if (m == 55) {
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          bar();  // B2: every wave holds B(t)
-        }
-        if (m >= 56 && !(m & 1) && iss) piece(t + 2, 8 + ((m - 56) >> 1));          // B(t + 2): pieces 8..11
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#pragma unroll
-    for (int g = 0; g < 8; ++g)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int m = 8 * g + k;
-        mfma_acc(acc[k][g], b1[g], a1[k]);
-        if (m <= 7 && !(m & 1) && iss) piece(t + 2, 12 + (m >> 1));                 // B(t + 2): pieces 12..15
-        if (m == 27) {
-          if (iss) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile t + 1 landed, t + 2 in flight
-          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          bar();  // B3: tile t + 1 visible to every wave
-        }
-        if (m >= 28 && m <= 59 && !(m & 1) && more) rdfrag(nxt, 0, (m - 28) >> 1, a0, b0);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-  };
-
-  // prologue: tiles 0 and 1 in flight, substep 0 of tile 0 in registers
-#pragma unroll
-  for (int i = 0; i < 16; ++i) piece(0, i);
-  if (nk > 1) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) piece(1, i);
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  bar();
-#pragma unroll
-  for (int r = 0; r < 16; ++r) rdfrag(smem, 0, r, a0, b0);
-  int t = 0;
-#pragma unroll 1
-  for (; t + 2 < nk; ++t) iter(t, True_{});
-#pragma unroll 1
-  for (; t < nk; ++t) iter(t, False_{});
-  // the last MFMAs' results -> v_accvgpr_read by compiler code (hipcc pads nothing after an asm MFMA)
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 15\n\ts_nop 7" ::: "memory");
-
-  if (tail_out) {  // K-slice of a tail tile: raw fp32 partial, row-major 256 x 256
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int r = ar + i * 16 + (lane & 15);
-        const int c = bc + j * 16 + 4 * (lane >> 4);
-        const f32x4 v = acc[i][j];
-        *reinterpret_cast<float4*>(tail_out + r * 256 + c) = make_float4(v[0], v[1], v[2], v[3]);
-      }
-    return;
-  }
-
-  const int flags = p.flags;
-  if (!(flags & (kEpiAux | kEpiAccum | kEpiOutF32))) {
-    // one-pass bf16 epilogue (as gemm256_kernel): alpha / bias / GELU in registers, [256][264] bf16 image,
-    // row-coalesced 16-byte stores
-    uint16_t* im = reinterpret_cast<uint16_t*>(smem);
-    constexpr int RSB = kEpiRowStrideBf16;
-    bar();
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = bc + j * 16 + 4 * (lane >> 4);
-      float bq[4] = {0.f, 0.f, 0.f, 0.f};
-      if ((flags & kEpiBias) && n0 + c < p.N) {
-        const uint2 braw = *reinterpret_cast<const uint2*>(p.bias + n0 + c);
-        bq[0] = lo_bf16(braw.x); bq[1] = hi_bf16(braw.x); bq[2] = lo_bf16(braw.y); bq[3] = hi_bf16(braw.y);
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int r = ar + i * 16 + (lane & 15);
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[e] = acc[i][j][e] * p.alpha + bq[e];
-          if (flags & kEpiGelu) v[e] = gelu_tanh(v[e]);
-        }
-        *reinterpret_cast<uint2*>(im + r * RSB + c) = make_uint2(pack_bf16(v[0], v[1]), pack_bf16(v[2], v[3]));
-      }
-    }
-    bar();
-    const int ecb = (tid & 31) * 8, erb = tid >> 5;  // 8 rows per step
-    const int nb_ = n0 + ecb;
-    if (nb_ < p.N) {
-#pragma unroll 4
-      for (int step = 0; step < 32; ++step) {
-        const int r = step * 8 + erb;
-        const int m = m0 + r;
-        if (m >= p.M) break;
-        *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(p.c) + (int64_t)m * p.ldc + nb_) =
-            *reinterpret_cast<const uint4*>(im + r * RSB + ecb);
-      }
-    }
-    return;
-  }
-  // general epilogue through the fp32 LDS image, one 128-row half at a time
-  float* img = reinterpret_cast<float*>(smem);
-  float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  {
-    const int n = n0 + (tid & 31) * 8;
-    if ((flags & kEpiBias) && n < p.N) load8<bf16>(reinterpret_cast<const bf16*>(p.bias + n), bv);
-  }
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    bar();
-    if (wm == h) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int r = i * 16 + (lane & 15);
-          const int c = bc + j * 16 + 4 * (lane >> 4);
-          *reinterpret_cast<f32x4*>(img + r * kEpiRowStride + c) = acc[i][j];
-        }
-    }
-    bar();
-    epi_rows<256>(p, img, m0 + h * 128, n0, tid, bv);
-  }
+  if (p.flags & kEpiColSum) colsum_finish<256>(p, img, cs, tid, m0, n0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1936,21 +1698,27 @@ PA_EXPORT int64_t pa_gemm_pp_ws_bytes(int64_t M, int64_t N, int64_t K) {
   return (T - full) * split * 65536 * 4;
 }
 
-// Ping-pong 256x256 GEMM (same operands / flags as pa_gemm_bf16, no split-K) with the balanced tail;
-// ws: pa_gemm_pp_ws_bytes(M, N, K) bytes (may be null when that is 0).
-PA_EXPORT int pa_gemm_bf16_pp(const void* a, const void* b, void* c, const void* bias, void* aux, int64_t M, int64_t N,
-                              int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor, int b_kmajor, int flags,
-                              float alpha, void* ws, hipStream_t st) {
-  if (K % kBK != 0 || N % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || ldc % 4 != 0) return 1;
+namespace {
+template <bool AK, bool BKM>
+int launch4w(const GemmArgs& g, int grid, hipStream_t st) {
+  constexpr int kLoop = 4 * 2 * 256 * 32 * 2, kEpi = 128 * kEpiRowStride * 4;
+  constexpr int smem = kLoop > kEpi ? kLoop : kEpi;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)gemm4w_kernel<AK, BKM>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((gemm4w_kernel<AK, BKM>), dim3(grid), dim3(256), smem, st, g);
+  return (int)hipGetLastError();
+}
+
+// One 256x256-tile GEMM on kernel `kern` (1 8-wave ping-pong, 2 4-wave K32 ring) with the balanced tail when ws is given (pp_plan); g holds operands, sizes and epilogue fields.
+int run_tile256(int kern, GemmArgs g, int a_kmajor, int b_kmajor, void* ws, hipStream_t st) {
+  const int64_t M = g.M, N = g.N, K = g.K;
+  if (K % kBK != 0 || N % 8 != 0 || g.lda % 8 != 0 || g.ldb % 8 != 0 || g.ldc % 4 != 0) return 1;
   if (!a_kmajor && M % 8 != 0) return 1;
   if (M <= 0 || N <= 0 || K <= 0) return 0;
-  GemmArgs g{};
-  g.a = (const uint16_t*)a; g.b = (const uint16_t*)b; g.c = c;
-  g.bias = (const uint16_t*)bias; g.aux = (uint16_t*)aux;
-  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
-  g.M = (int)M; g.N = (int)N; g.K = (int)K;
-  g.flags = flags; g.alpha = alpha;
-  g.c_split = M * ldc;
+  g.c_split = M * g.ldc;
   int full, split;
   pp_plan(M, N, K, device_cus(), &full, &split);
   if (split && !ws) split = 0;
@@ -1961,14 +1729,39 @@ PA_EXPORT int pa_gemm_bf16_pp(const void* a, const void* b, void* c, const void*
   g.tail_split = split;
   g.tail_ws = (float*)ws;
   const int grid = split ? full + (T - full) * split : T;
+  const int lay = (a_kmajor ? 0 : 2) + (b_kmajor ? 1 : 0);
   int rc;
-  if (a_kmajor && !b_kmajor) rc = launch256<true, false>(g, 1, st, grid);
-  else if (a_kmajor && b_kmajor) rc = launch256<true, true>(g, 1, st, grid);
-  else if (!a_kmajor && !b_kmajor) rc = launch256<false, false>(g, 1, st, grid);
-  else rc = launch256<false, true>(g, 1, st, grid);
+  if (kern == 1) {
+    rc = lay == 0 ? launch256<true, false>(g, 1, st, grid) : lay == 1 ? launch256<true, true>(g, 1, st, grid)
+       : lay == 2 ? launch256<false, false>(g, 1, st, grid) : launch256<false, true>(g, 1, st, grid);
+  } else {
+    rc = lay == 0 ? launch4w<true, false>(g, grid, st) : lay == 1 ? launch4w<true, true>(g, grid, st)
+       : lay == 2 ? launch4w<false, false>(g, grid, st) : launch4w<false, true>(g, grid, st);
+  }
   if (rc || !split) return rc;
   hipLaunchKernelGGL(gemm_tail_reduce_k, dim3(T - full, 64), dim3(256), 0, st, g);
   return (int)hipGetLastError();
+}
+
+GemmArgs tile256_args(const void* a, const void* b, void* c, const void* bias, void* aux, int64_t M, int64_t N,
+                      int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int flags, float alpha) {
+  GemmArgs g{};
+  g.a = (const uint16_t*)a; g.b = (const uint16_t*)b; g.c = c;
+  g.bias = (const uint16_t*)bias; g.aux = (uint16_t*)aux;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.flags = flags; g.alpha = alpha;
+  return g;
+}
+}  // namespace
+
+// Ping-pong 256x256 GEMM (same operands / flags as pa_gemm_bf16, no split-K) with the balanced tail;
+// ws: pa_gemm_pp_ws_bytes(M, N, K) bytes (may be null when that is 0).
+PA_EXPORT int pa_gemm_bf16_pp(const void* a, const void* b, void* c, const void* bias, void* aux, int64_t M, int64_t N,
+                              int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor, int b_kmajor, int flags,
+                              float alpha, void* ws, hipStream_t st) {
+  return run_tile256(1, tile256_args(a, b, c, bias, aux, M, N, K, lda, ldb, ldc, flags, alpha), a_kmajor, b_kmajor,
+                     ws, st);
 }
 
 // Split-K on the ping-pong kernel: every tile cut into `splits` K slices (the balanced-tail machinery with no
@@ -2072,92 +1865,23 @@ PA_EXPORT int pa_gemm_bf16_pp_segs(const int64_t* seg, int nseg, int seg_k, cons
 PA_EXPORT int pa_gemm_bf16_4w(const void* a, const void* b, void* c, const void* bias, void* aux, int64_t M, int64_t N,
                               int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor, int b_kmajor, int flags,
                               float alpha, void* ws, hipStream_t st) {
-  if (K % kBK != 0 || N % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || ldc % 4 != 0) return 1;
-  if (!a_kmajor && M % 8 != 0) return 1;
-  if (M <= 0 || N <= 0 || K <= 0) return 0;
-  GemmArgs g{};
-  g.a = (const uint16_t*)a; g.b = (const uint16_t*)b; g.c = c;
-  g.bias = (const uint16_t*)bias; g.aux = (uint16_t*)aux;
-  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
-  g.M = (int)M; g.N = (int)N; g.K = (int)K;
-  g.flags = flags; g.alpha = alpha;
-  int full, split;
-  pp_plan(M, N, K, device_cus(), &full, &split);
-  if (split && !ws) split = 0;
-  g.tiles_m = (int)((M + 255) / 256);
-  g.tiles_n = (int)((N + 255) / 256);
-  const int T = g.tiles_m * g.tiles_n;
-  g.full_tiles = split ? full : T;
-  g.tail_split = split;
-  g.tail_ws = (float*)ws;
-  const int grid = split ? full + (T - full) * split : T;
-  constexpr int kLoop = 4 * 2 * 256 * 32 * 2, kEpi = 128 * kEpiRowStride * 4;
-  constexpr int smem = kLoop > kEpi ? kLoop : kEpi;
-  static bool attr_set[4] = {false, false, false, false};
-#define PA_G4(AKV, BKV, I)                                                                                      \
-  do {                                                                                                          \
-    if (!attr_set[I]) {                                                                                         \
-      (void)hipFuncSetAttribute((const void*)gemm4w_kernel<AKV, BKV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                smem);                                                                          \
-      attr_set[I] = true;                                                                                       \
-    }                                                                                                           \
-    hipLaunchKernelGGL((gemm4w_kernel<AKV, BKV>), dim3(grid), dim3(256), smem, st, g);                          \
-  } while (0)
-  if (a_kmajor && !b_kmajor) PA_G4(true, false, 0);
-  else if (a_kmajor && b_kmajor) PA_G4(true, true, 1);
-  else if (!a_kmajor && !b_kmajor) PA_G4(false, false, 2);
-  else PA_G4(false, true, 3);
-#undef PA_G4
-  int rc = (int)hipGetLastError();
-  if (rc || !split) return rc;
-  hipLaunchKernelGGL(gemm_tail_reduce_k, dim3(T - full, 64), dim3(256), 0, st, g);
-  return (int)hipGetLastError();
+  return run_tile256(2, tile256_args(a, b, c, bias, aux, M, N, K, lda, ldb, ldc, flags, alpha), a_kmajor, b_kmajor,
+                     ws, st);
 }
 
-// 4-wave K64 GEMM (gemm4k_kernel; same operands / flags / workspace as pa_gemm_bf16_pp).
-PA_EXPORT int pa_gemm_bf16_4k(const void* a, const void* b, void* c, const void* bias, void* aux, int64_t M, int64_t N,
-                              int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor, int b_kmajor, int flags,
-                              float alpha, void* ws, hipStream_t st) {
-  if (K % kBK != 0 || N % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || ldc % 4 != 0) return 1;
-  if (!a_kmajor && M % 8 != 0) return 1;
-  if (M <= 0 || N <= 0 || K <= 0) return 0;
-  GemmArgs g{};
-  g.a = (const uint16_t*)a; g.b = (const uint16_t*)b; g.c = c;
-  g.bias = (const uint16_t*)bias; g.aux = (uint16_t*)aux;
-  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
-  g.M = (int)M; g.N = (int)N; g.K = (int)K;
-  g.flags = flags; g.alpha = alpha;
-  int full, split;
-  pp_plan(M, N, K, device_cus(), &full, &split);
-  if (split && !ws) split = 0;
-  g.tiles_m = (int)((M + 255) / 256);
-  g.tiles_n = (int)((N + 255) / 256);
-  const int T = g.tiles_m * g.tiles_n;
-  g.full_tiles = split ? full : T;
-  g.tail_split = split;
-  g.tail_ws = (float*)ws;
-  const int grid = split ? full + (T - full) * split : T;
-  constexpr int kLoop = 2 * 2 * 256 * 64 * 2, kEpiB = 256 * kEpiRowStrideBf16 * 2, kEpiF = 128 * kEpiRowStride * 4;
-  constexpr int smem = kLoop > kEpiB ? (kLoop > kEpiF ? kLoop : kEpiF) : (kEpiB > kEpiF ? kEpiB : kEpiF);
-  static bool attr_set[4] = {false, false, false, false};
-#define PA_G4K(AKV, BKV, I)                                                                                     \
-  do {                                                                                                          \
-    if (!attr_set[I]) {                                                                                         \
-      (void)hipFuncSetAttribute((const void*)gemm4k_kernel<AKV, BKV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                smem);                                                                          \
-      attr_set[I] = true;                                                                                       \
-    }                                                                                                           \
-    hipLaunchKernelGGL((gemm4k_kernel<AKV, BKV>), dim3(grid), dim3(256), smem, st, g);                          \
-  } while (0)
-  if (a_kmajor && !b_kmajor) PA_G4K(true, false, 0);
-  else if (a_kmajor && b_kmajor) PA_G4K(true, true, 1);
-  else if (!a_kmajor && !b_kmajor) PA_G4K(false, false, 2);
-  else PA_G4K(false, true, 3);
-#undef PA_G4K
-  int rc = (int)hipGetLastError();
-  if (rc || !split) return rc;
-  hipLaunchKernelGGL(gemm_tail_reduce_k, dim3(T - full, 64), dim3(256), 0, st, g);
-  return (int)hipGetLastError();
+// Data gradient of the linear after a tanh-GELU, fused with the GELU backward and the first linear's bias gradient
+// (reference fusion/gpu/fused_feedforward_grad: the dropout/activation backward runs as its own pass there):
+// dh = (a . b) * gelu'(pre) (bf16, [M][ldc]) and colsum[tiles_m][N] = per-256-row-tile column sums of dh (fp32,
+// folded into the bias gradient by pa_fold_partials with nparts = tiles_m). kern: as run_tile256; no balanced tail
+// (the column sums are per whole tile). pre: the forward's stored pre-activation (x . W1 + b1), same layout as dh.
+PA_EXPORT int pa_gemm_bf16_dgelu(const void* a, const void* b, void* dh, const void* pre, float* colsum, int64_t M,
+                                 int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor,
+                                 int b_kmajor, int kern, hipStream_t st) {
+  if (!pre || !colsum || kern < 1 || kern > 2) return 1;
+  GemmArgs g = tile256_args(a, b, dh, nullptr, const_cast<void*>(pre), M, N, K, lda, ldb, ldc,
+                            kEpiGeluBwd | kEpiColSum, 1.f);
+  g.stats = colsum;
+  return run_tile256(kern, g, a_kmajor, b_kmajor, nullptr, st);
 }
 
 // Diagnostic ablations of gemm4w_kernel (A K-major, B MN-major, no tail): timing only.

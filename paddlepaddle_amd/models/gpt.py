@@ -214,6 +214,12 @@ class GPTAttention(nn.Layer):
         return _wrap(y + self.out_proj.bias._t)
 
 
+def _tracing():
+    """A static program is being traced (its passes / SPMD rules see the two linears, not the fused op)."""
+    from ..framework.trace_hook import _active_program
+    return _active_program() is not None
+
+
 class GPTMLP(nn.Layer):
     def __init__(self, cfg: GPTConfig):
         super().__init__()
@@ -249,6 +255,13 @@ class GPTMLP(nn.Layer):
             xt = x._t
             if xt.dtype != w.dtype:
                 xt = xt.to(w.dtype)
+            l2 = self.linear2
+            w2, b2 = l2.weight._t, l2.bias._t
+            if (w.dtype in (torch.bfloat16, torch.float16) and w2.dtype == w.dtype and b2.dtype == w.dtype
+                    and not (l2._forward_pre_hooks or l2._forward_post_hooks or _tracing())):
+                # fc1 -> GELU -> fc2 as one op: its backward runs the GELU backward (and fc1's bias gradient) in
+                # fc2's data-gradient GEMM epilogue (ops/linear.py _FFNGeluFn)
+                return _wrap(_ops.ffn_gelu(xt, w, b, w2, b2))
             h = _wrap(_ops.fused_linear(xt, w, b, act="gelu"))
         return self.linear2(h)
 

@@ -11,7 +11,7 @@ from .norm import rms_norm, rms_norm_residual, layer_norm, layer_norm_residual, 
 from .loss import softmax_cross_entropy  # noqa: F401
 from .attention import flash_attention, flash_attention_qkvpacked, qkv_rope_attention, attention_reference, paged_decode_attention, dense_decode_attention  # noqa: F401,E501
 from .rope import apply_rotary, decode_rope_cache  # noqa: F401
-from .linear import fused_linear, colsum, linear_nt  # noqa: F401
+from .linear import fused_linear, colsum, linear_nt, ffn_gelu  # noqa: F401
 from .lm_head import lm_head_cross_entropy  # noqa: F401
 from .dropout import dropout_add  # noqa: F401
 from . import optim  # noqa: F401

@@ -76,11 +76,11 @@ def gemm(a, b, bias=None, gelu=False, aux=None, out=None, accumulate=False, alph
         flags |= EPI_OUT_F32
     if bn is None:
         bn = _pick_bn(M, N, bk)
-    if bn in (1, 2, 3) and L.has("pa_gemm_bf16_pp"):
-        # 256x256 + balanced tail: 1 8-wave ping-pong, 2 4-wave K32 ring, 3 4-wave K64 two-stage (gemm4k_kernel)
+    if bn in (1, 2) and L.has("pa_gemm_bf16_pp"):
+        # 256x256 + balanced tail: 1 8-wave ping-pong, 2 4-wave K32 ring
         nb = int(L.lib().pa_gemm_pp_ws_bytes(M, N, K))
         ws = torch.empty(nb // 4, dtype=torch.float32, device=a.device) if nb else None
-        fn = {1: "pa_gemm_bf16_pp", 2: "pa_gemm_bf16_4w", 3: "pa_gemm_bf16_4k"}[bn]
+        fn = {1: "pa_gemm_bf16_pp", 2: "pa_gemm_bf16_4w"}[bn]
         L.call(fn, L.ptr(a), L.ptr(b), L.ptr(out), L.ptr(bias),
                L.ptr(aux), M, N, K, lda, ldb, out.stride(0), int(ak), int(bk), flags, float(alpha), L.ptr(ws),
                L.stream_ptr())
@@ -88,6 +88,28 @@ def gemm(a, b, bias=None, gelu=False, aux=None, out=None, accumulate=False, alph
     L.call("pa_gemm_bf16", L.ptr(a), L.ptr(b), L.ptr(out), L.ptr(bias), L.ptr(aux), M, N, K, lda, ldb, out.stride(0),
            int(ak), int(bk), flags, float(alpha), int(bn), 1, L.stream_ptr())
     return out
+
+
+def gemm_dgelu_supported(a, b, pre):
+    """pa_gemm_bf16_dgelu conditions: a bf16 GEMM the 256x256 kernels take, pre-activation [M, N] bf16 rows."""
+    return (supported(a, b) and L.has("pa_gemm_bf16_dgelu") and pre.dtype == torch.bfloat16 and pre.dim() == 2
+            and tuple(pre.shape) == (a.shape[0], b.shape[1]) and pre.stride(1) == 1 and pre.stride(0) == b.shape[1]
+            and pre.data_ptr() % 16 == 0 and b.shape[1] % 8 == 0)
+
+
+def gemm_dgelu(a, b, pre, kern=1):
+    """(dh, parts): dh = (a @ b) * gelu_tanh'(pre) (bf16) and the per-256-row-tile column sums of dh
+    (fp32 [ceil(M / 256), N]; fold with pa_fold_partials for the bias gradient). kern: 1 ping-pong, 2 4-wave K32
+    (csrc/kernels/gemm.hip pa_gemm_bf16_dgelu)."""
+    M, K = a.shape
+    N = b.shape[1]
+    lda, ak = _layout(a, 0)
+    ldb, bk = _layout(b, 1)
+    dh = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    parts = torch.empty(-(-M // 256), N, dtype=torch.float32, device=a.device)
+    L.call("pa_gemm_bf16_dgelu", L.ptr(a), L.ptr(b), L.ptr(dh), L.ptr(pre), L.ptr(parts), M, N, K, lda, ldb, N,
+           int(ak), int(bk), int(kern), L.stream_ptr())
+    return dh, parts
 
 
 def _seg_table(rows):

@@ -551,6 +551,104 @@ class _LinearBiasGeluFn(torch.autograd.Function):
         return dx, dw, db, None
 
 
+def _bias_gelu_bwd(h, b, dg, db_acc=None):
+    """(dh, db) of y = gelu(h + b) given dg = dL/dy (one pass, pa_bias_gelu_bwd); db added into ``db_acc``."""
+    rows, cols = h.shape
+    dh = torch.empty_like(h)
+    db = db_acc if db_acc is not None else torch.empty(cols, dtype=b.dtype, device=b.device)
+    ws = torch.empty(256 * cols, dtype=torch.float32, device=h.device)
+    L.call("pa_bias_gelu_bwd", L.ptr(h), L.ptr(b), L.ptr(dg), L.ptr(dh), L.ptr(db), L.ptr(ws), rows, cols,
+           L.dcode(h) | ((db_acc is not None) << 8), L.stream_ptr())
+    return dh, db
+
+
+def _dgrad_gelu(dy2, w2, h, b1, pre_biased, db_acc=None):
+    """(dh, db1) of the FFN's hidden layer: dh = (dy2 . w2^T) * gelu'(h + b1), db1 = column sums of dh (added into
+    ``db_acc`` when given). When the forward stored the biased pre-activation (hand-written GEMM, ``pre_biased``)
+    the GELU backward and the bias-gradient column sums can run in the data-gradient GEMM's epilogue
+    (pa_gemm_bf16_dgelu: no dY.W^T round trip through HBM); timed per shape against the separate dgrad GEMM +
+    pa_bias_gelu_bwd pass (ops/gemm.py choose())."""
+    w2t = w2.t()
+    rows, cols = h.shape
+
+    def split(acc=None):
+        return _bias_gelu_bwd(h, b1, _dgrad(dy2, w2), acc)
+
+    if pre_biased and G.gemm_dgelu_supported(dy2, w2t, h):
+        def fused(kern, acc=None):
+            dh, parts = G.gemm_dgelu(dy2, w2t, h, kern)
+            db = acc if acc is not None else torch.empty(cols, dtype=h.dtype, device=h.device)
+            L.call("pa_fold_partials", L.ptr(parts), L.ptr(db), cols, parts.shape[0],
+                   L.dcode(h) | ((acc is not None) << 8), L.stream_ptr())
+            return dh, db
+        key = ("dgrad_gelu", dy2.shape[0], cols, dy2.shape[1])
+        cands = {"blas": split, "hip": lambda: fused(1), "hip_4w": lambda: fused(2)}
+        ch = G.choose(key, cands)
+        if ch != "blas":
+            CALLS["dgrad_gelu_fused"] += 1
+            return fused({"hip": 1, "hip_4w": 2}[ch], db_acc)
+    return split(db_acc)
+
+
+CALLS = {"dgrad_gelu_fused": 0}
+
+
+class _FFNGeluFn(torch.autograd.Function):
+    """y = gelu(x W1 + b1) W2 + b2 as one autograd node (the GELU'd hidden activation has exactly one consumer
+    here, so its gradient can be produced already multiplied by gelu' — see _dgrad_gelu). Reference:
+    incubate/nn/functional/fused_transformer.py fused_feedforward (fused_feedforward_grad kernel); saved
+    tensors are the same as two separate linears (x, pre-activation, hidden activation)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, dx_hook=None):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        a, h, bb = _fwd_bias_gelu(x2, w1, b1)
+        y = _fwd_mm(a, w2, b2)
+        ctx.save_for_backward(x2, w1, bb, h, a, w2)
+        ctx.pre_biased = bb is not b1  # hand-written forward: h holds x W1 + b1, bb is zeros
+        ctx.w_leaf = _leaf_weights(w1, w2)
+        ctx.b1, ctx.b2 = b1, b2
+        ctx.shape = shape
+        ctx.dx_hook = dx_hook
+        return y.view(*shape[:-1], w2.shape[1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w1, bb, h, a, w2 = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        dy2 = dy.reshape(-1, dy.shape[-1]).to(h.dtype).contiguous()
+        db2 = None
+        if ctx.b2 is not None and need[4]:
+            mg = _vector_main_grad(ctx.b2, dy2.dtype)
+            if mg is not None:
+                colsum(dy2, acc=mg[0])
+                mg[1](ctx.b2)
+            else:
+                db2 = colsum(dy2)
+        mg1 = _vector_main_grad(ctx.b1, h.dtype) if need[2] else None
+        dh, db1 = _dgrad_gelu(dy2, w2, h, bb, ctx.pre_biased, mg1[0] if mg1 is not None else None)
+        if mg1 is not None:
+            mg1[1](ctx.b1)
+            db1 = None
+        elif not need[2]:
+            db1 = None
+        _, dw2 = _mm_grads(a, w2, dy2, False, need[3], wid=_w_ident(w2, ctx.w_leaf[1], need[3]))
+        dx, dw1 = _mm_grads(x2, w1, dh, need[0], need[1], ctx.dx_hook, wid=_w_ident(w1, ctx.w_leaf[0], need[1]))
+        if dx is not None:
+            dx = dx.view(ctx.shape)
+        return dx, dw1, db1, dw2, db2, None
+
+
+@static_op
+def ffn_gelu(x, w1, b1, w2, b2=None, dx_hook=None):
+    """gelu_tanh(x @ w1 + b1) @ w2 + b2 — the GPT MLP (fc1 -> GELU -> fc2) as one fused-backward op on the HIP
+    path; two fused_linear calls otherwise."""
+    if _hip_linear_ok(x, w1, b1) and b1 is not None and _hip_linear_ok(x, w2, b2) and w1.shape[1] == w2.shape[0]:
+        return _FFNGeluFn.apply(x, w1, b1, w2, b2, dx_hook)
+    return fused_linear(fused_linear(x, w1, b1, act="gelu", dx_hook=dx_hook), w2, b2)
+
+
 def _hip_linear_ok(x, w, b):
     return (L.hip_enabled_for(x) and x.dtype in (torch.bfloat16, torch.float16) and w.dtype == x.dtype
             and (b is None or b.dtype == x.dtype) and w.shape[1] % 8 == 0 and w.dim() == 2)

@@ -1,8 +1,8 @@
 """The 13B layer's GEMMs (tools/bench_step_gemms.py shapes and epilogues) on each hand-written 256x256 variant:
-bn=1 8-wave ping-pong, bn=3 4-wave K64 two-stage, plus hipBLASLt; checks each variant against the ping-pong output
+bn=1 8-wave ping-pong, bn=2 4-wave K32 ring, plus hipBLASLt; checks each variant against the ping-pong output
 first (same operands), then times them back to back.
 
-    python tools/bench_gemm_variants.py [iters] [variants, e.g. 1,3]
+    python tools/bench_gemm_variants.py [iters] [variants, e.g. 1,2]
 """
 import sys
 import time
@@ -17,7 +17,7 @@ from bench_step_gemms import timed  # noqa: E402
 
 def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-    variants = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 3]
+    variants = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 2]
     dev, bf = "cuda", torch.bfloat16
     torch.manual_seed(0)
     w8 = torch.randn(8192, 8192, device=dev, dtype=bf)
