@@ -62,8 +62,9 @@ enum EpiFlags : int {
   kEpiGeluBwd = 128,  // C = result * gelu'(aux): aux holds the GELU's pre-activation (the data gradient of the
                       // linear after a GELU, fused with the GELU backward; 256x256 kernels, staged epilogue)
   kEpiColSum = 256,   // column sums of the result per 256-row tile to stats[tiles_m][N] (fp32; bias gradient)
+  kEpiResid = 512,    // C = result + res (bf16 [M][ldc]): the residual add after an output projection
 };
-constexpr int kEpiStaged = kEpiAux | kEpiAccum | kEpiOutF32 | kEpiGeluBwd | kEpiColSum;
+constexpr int kEpiStaged = kEpiAux | kEpiAccum | kEpiOutF32 | kEpiGeluBwd | kEpiColSum | kEpiResid;
 
 struct GemmArgs {
   const uint16_t* a;
@@ -106,6 +107,8 @@ struct GemmArgs {
   const uint16_t* bn_x;
   const float* bn_ss;
   const float* bn_mean;
+  // kEpiResid: the residual read by the epilogue (bf16, leading dimension ldc)
+  const uint16_t* res;
 };
 
 // split-K view: slice blockIdx.y of K (p.K elements each) and its own fp32 output slab
@@ -523,7 +526,7 @@ using False_ = IntC<0>;
 // row): each thread owns 8 consecutive columns and walks the rows NT / 32 at a time. Epilogues that read global
 // memory (accumulate into C, the GELU backward's pre-activation) issue the reads of 8 row steps before the first
 // is used: one memory latency per 8 steps instead of one per step (the loop-carried form left each step waiting
-// on its own read). kEpiGeluBwd excludes kEpiAccum.
+// on its own read). kEpiGeluBwd excludes kEpiAccum and kEpiResid; kEpiResid excludes kEpiAccum.
 template <int NT>
 __device__ __forceinline__ void epi_rows(const GemmArgs& p, const float* img, int m_base, int n0, int tid,
                                          const float* bv, float* cs) {
@@ -536,11 +539,12 @@ __device__ __forceinline__ void epi_rows(const GemmArgs& p, const float* img, in
   if (n >= p.N) return;
   const int flags = p.flags;
   const bool f32 = flags & kEpiOutF32;
-  const bool rd_pre = flags & kEpiGeluBwd, rd_c = (flags & kEpiAccum) && !rd_pre;
+  const bool rd_pre = flags & kEpiGeluBwd, rd_res = (flags & kEpiResid) && !rd_pre;
+  const bool rd_c = (flags & kEpiAccum) && !rd_pre && !rd_res;
 #pragma unroll 1
   for (int g0 = 0; g0 < NSTEP; g0 += G) {
     uint4 rd[G][2];
-    if (rd_pre || rd_c) {
+    if (rd_pre || rd_res || rd_c) {
 #pragma unroll
       for (int s = 0; s < G; ++s) {
         const int m = m_base + (g0 + s) * RSTEP + er;
@@ -549,6 +553,8 @@ __device__ __forceinline__ void epi_rows(const GemmArgs& p, const float* img, in
           const int64_t off = (int64_t)m * p.ldc + n;
           if (rd_pre) {
             rd[s][0] = *reinterpret_cast<const uint4*>(p.aux + off);
+          } else if (rd_res) {
+            rd[s][0] = *reinterpret_cast<const uint4*>(p.res + off);
           } else if (f32) {
             rd[s][0] = *reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(p.c) + off);
             rd[s][1] = *reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(p.c) + off + 4);
@@ -579,7 +585,7 @@ __device__ __forceinline__ void epi_rows(const GemmArgs& p, const float* img, in
       }
       // the 8 bf16 (or fp32) values this step read ahead
       float o[8];
-      if (rd_pre || (rd_c && !f32)) {
+      if (rd_pre || rd_res || (rd_c && !f32)) {
         const uint4 u = rd[s][0];
         o[0] = lo_bf16(u.x); o[1] = hi_bf16(u.x); o[2] = lo_bf16(u.y); o[3] = hi_bf16(u.y);
         o[4] = lo_bf16(u.z); o[5] = hi_bf16(u.z); o[6] = lo_bf16(u.w); o[7] = hi_bf16(u.w);
@@ -592,7 +598,7 @@ __device__ __forceinline__ void epi_rows(const GemmArgs& p, const float* img, in
       if (rd_pre) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] *= gelu_tanh_grad_fast(o[e]);
-      } else if (rd_c) {
+      } else if (rd_c || rd_res) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += o[e];
       }
@@ -1642,6 +1648,10 @@ __global__ __launch_bounds__(256) void gemm_tail_reduce_k(GemmArgs p) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) v[q] = gelu_tanh(v[q]);
   }
+  if (flags & kEpiResid) {
+    const uint2 rr = *reinterpret_cast<const uint2*>(p.res + off);
+    v[0] += lo_bf16(rr.x); v[1] += hi_bf16(rr.x); v[2] += lo_bf16(rr.y); v[3] += hi_bf16(rr.y);
+  }
   if (flags & kEpiOutF32) {
     float4* cp = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.c) + off);
     if (flags & kEpiAccum) {
@@ -1867,6 +1877,19 @@ PA_EXPORT int pa_gemm_bf16_4w(const void* a, const void* b, void* c, const void*
                               float alpha, void* ws, hipStream_t st) {
   return run_tile256(2, tile256_args(a, b, c, bias, aux, M, N, K, lda, ldb, ldc, flags, alpha), a_kmajor, b_kmajor,
                      ws, st);
+}
+
+// Output projection with the residual add in its epilogue: C = a . b (+ bias) + res (bf16, [M][ldc]; may not alias
+// C). Ping-pong kernel with the balanced tail (ws as pa_gemm_bf16_pp). Replaces the separate elementwise add after
+// the attention / MLP output projections of a pre-norm decoder layer (one read of the residual instead of a
+// read of both summands and a write).
+PA_EXPORT int pa_gemm_bf16_res(const void* a, const void* b, void* c, const void* bias, const void* res, int64_t M,
+                               int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int a_kmajor, int b_kmajor,
+                               void* ws, hipStream_t st) {
+  if (!res || res == c) return 1;
+  GemmArgs g = tile256_args(a, b, c, bias, nullptr, M, N, K, lda, ldb, ldc, (bias ? kEpiBias : 0) | kEpiResid, 1.f);
+  g.res = (const uint16_t*)res;
+  return run_tile256(1, g, a_kmajor, b_kmajor, ws, st);
 }
 
 // Data gradient of the linear after a tanh-GELU, fused with the GELU backward and the first linear's bias gradient

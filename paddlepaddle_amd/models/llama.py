@@ -171,6 +171,29 @@ def _core(attn, fn, *ts):
     return fn(*ts)
 
 
+def _add_res(y, residual):
+    return y if residual is None else _wrap(y._t + residual._t)
+
+
+def _proj_res(layer, h, residual):
+    """``layer(h) + residual``. For a plain hook-free linear (tp = 1) outside static tracing the add runs in the
+    GEMM (ops.fused_linear residual=: the epilogue reads the residual, or hipBLASLt's C input) — no separate
+    elementwise pass over the hidden states; its gradient is the output gradient itself."""
+    if residual is None:
+        return layer(h)
+    w = layer.weight._t
+    b = layer.bias._t if getattr(layer, "bias", None) is not None else None
+    if (type(layer) is nn.Linear and not (layer._forward_pre_hooks or layer._forward_post_hooks)
+            and h._t.dtype == w.dtype and residual._t.dtype == w.dtype and not _tracing()):
+        return _wrap(_ops.fused_linear(h._t, w, b, residual=residual._t))
+    return _wrap(layer(h)._t + residual._t)
+
+
+def _tracing():
+    from ..framework.trace_hook import _active_program
+    return _active_program() is not None
+
+
 class LlamaAttention(nn.Layer):
     def __init__(self, cfg: LlamaConfig):
         super().__init__()
@@ -210,11 +233,13 @@ class LlamaAttention(nn.Layer):
         o = _core(self, lambda tt: _ops.qkv_rope_attention(tt, c, sn, self.H, self.Hkv, self.D), t)
         return _wrap(sp.row_sp_linear(o.reshape(B * S, self.H * self.D), self.o_proj.weight._t))
 
-    def forward(self, x, cache=None, pos=0):
+    def forward(self, x, cache=None, pos=0, residual=None):
+        """``residual``: return ``residual + attention output`` (the decoder's residual add, done by the
+        o-projection GEMM on the plain training path — _proj_res)."""
         if cache is None and getattr(self, "bs", None) is not None and x._t.dim() == 2:
-            return self._forward_sp(x)
+            return _add_res(self._forward_sp(x), residual)
         if cache is not None and isinstance(pos, torch.Tensor):
-            return self._decode_step(x, cache, pos)
+            return _add_res(self._decode_step(x, cache, pos), residual)
         if cache is None and self.cfg.sep_parallel_degree <= 1 and self.cfg.fused_qkv_attention:
             # training / full-sequence path: projection -> RoPE -> attention as one op whose backward returns the
             # whole qkv-projection gradient as one buffer (ops/attention.py qkv_rope_attention)
@@ -223,11 +248,11 @@ class LlamaAttention(nn.Layer):
             cos, sin = self.rope.tables(pos + S, t.device)
             c, sn = cos[pos:pos + S], sin[pos:pos + S]
             o = _core(self, lambda tt: _ops.qkv_rope_attention(tt, c, sn, self.H, self.Hkv, self.D), t)
-            return self.o_proj(_wrap(o.reshape(B, S, self.H * self.D)))
+            return _proj_res(self.o_proj, _wrap(o.reshape(B, S, self.H * self.D)), residual)
         q, k, v = self._qkv(x)
         B, S = q.shape[0], q.shape[1]
         if cache is None and self.cfg.sep_parallel_degree > 1:
-            return self._forward_sep(q, k, v, B, S)
+            return _add_res(self._forward_sep(q, k, v, B, S), residual)
         cos, sin = self.rope.tables(pos + S, q.device)
         q = _ops.apply_rotary(q, cos[pos:pos + S], sin[pos:pos + S])
         k = _ops.apply_rotary(k, cos[pos:pos + S], sin[pos:pos + S])
@@ -242,7 +267,7 @@ class LlamaAttention(nn.Layer):
         else:
             causal = True
         o = _core(self, lambda qq, kk, vv: _ops.flash_attention(qq, kk, vv, causal=causal), q, k, v)
-        return self.o_proj(_wrap(o.reshape(B, S, self.H * self.D)))
+        return _proj_res(self.o_proj, _wrap(o.reshape(B, S, self.H * self.D)), residual)
 
     def _forward_sep(self, q, k, v, B, S):
         """Segment-parallel training step: this rank holds tokens [r * S, (r + 1) * S) of every sequence;
@@ -302,13 +327,14 @@ class LlamaMLP(nn.Layer):
             self.down_proj = nn.Linear(f, h, weight_attr=init, bias_attr=False)
         self.sp = _use_sp(cfg)
 
-    def forward(self, x):
+    def forward(self, x, residual=None):
+        """``residual``: return ``residual + MLP output`` (added by the down-projection GEMM when it can be)."""
         if self.tp > 1 and x._t.dim() == 2 and getattr(self, "sp", False):  # sequence parallel: token block in / out
             sp = _sp()
             h = _ops.swiglu(sp.column_sp_linear(x._t, self.gate_up_proj.weight._t, None))
-            return _wrap(sp.row_sp_linear(h, self.down_proj.weight._t))
+            return _add_res(_wrap(sp.row_sp_linear(h, self.down_proj.weight._t)), residual)
         # one-input swiglu: its backward writes d[gate | up] as one buffer (no chunk / cat in autograd)
-        return self.down_proj(_wrap(_ops.swiglu(self.gate_up_proj(x)._t)))
+        return _proj_res(self.down_proj, _wrap(_ops.swiglu(self.gate_up_proj(x)._t)), residual)
 
 
 class LlamaDecoderLayer(nn.Layer):
@@ -326,24 +352,28 @@ class LlamaDecoderLayer(nn.Layer):
             # training: each residual branch's gradient is summed into the RMSNorm input gradient by the norm's
             # backward kernel (LlamaRMSNorm(residual=True) -> ops.rms_norm_residual, a recorded static op, so a
             # captured program keeps it) instead of autograd's separate accumulation add
+            # the residual adds themselves run in the o / down projection GEMMs' epilogues (_proj_res)
             r, h = n1(x, residual=True)
-            t = r._t + self._attn(h, cache, pos)._t
-            r, h = n2(_wrap(t), residual=True)
-            return _wrap(r._t + self.mlp(h)._t)
+            t = self._attn(h, cache, pos, residual=r)
+            r, h = n2(t, residual=True)
+            return self.mlp(h, residual=r)
         h = self._attn(self.input_layernorm(x), cache, pos)
         x = _wrap(x._t + h._t)
         h = self.mlp(self.post_attention_layernorm(x))
         return _wrap(x._t + h._t)
 
-    def _attn(self, h, cache, pos):
+    def _attn(self, h, cache, pos, residual=None):
         """Self-attention under the layer's recompute granularity (LlamaModel sets ``_rc``): full_attn checkpoints
-        the attention block (projections included), core_attn only the attention core."""
+        the attention block (projections included), core_attn only the attention core. ``residual``: added to the
+        output (by the o-projection GEMM outside full_attn recompute)."""
         g = getattr(self, "_rc", None) if cache is None else None
         if g == "full_attn":
             from ..distributed.fleet.recompute import recompute
-            return recompute(self.self_attn, h)
+            return _add_res(recompute(self.self_attn, h), residual)
         self.self_attn._rc_core = g == "core_attn"
-        return self.self_attn(h, cache, pos)
+        if residual is None:
+            return self.self_attn(h, cache, pos)
+        return self.self_attn(h, cache, pos, residual=residual)
 
 
 class LlamaModel(nn.Layer):

@@ -71,6 +71,7 @@ SIGS = {
                         _vp, _vp],
     "pa_gemm_bf16_4w": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _f32,
                         _vp, _vp],
+    "pa_gemm_bf16_res": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _vp, _vp],
     "pa_gemm_bf16_dgelu": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _vp],
     "pa_gemm_bf16_pp_segs": [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32,
                              _i32, _f32, _vp, _vp],

@@ -90,6 +90,28 @@ def gemm(a, b, bias=None, gelu=False, aux=None, out=None, accumulate=False, alph
     return out
 
 
+def res_supported(a, b, res):
+    """pa_gemm_bf16_res conditions: the ping-pong kernel takes a @ b, residual [M, N] bf16 contiguous rows."""
+    return (supported(a, b) and L.has("pa_gemm_bf16_res") and res.dtype == torch.bfloat16 and res.dim() == 2
+            and tuple(res.shape) == (a.shape[0], b.shape[1]) and res.stride(1) == 1
+            and res.stride(0) == b.shape[1] and res.data_ptr() % 16 == 0 and b.shape[1] % 8 == 0)
+
+
+def gemm_res(a, b, res, bias=None):
+    """a @ b (+ bias) + res in one launch (csrc/kernels/gemm.hip pa_gemm_bf16_res: the residual is read by the
+    epilogue), ping-pong kernel with its balanced tail."""
+    M, K = a.shape
+    N = b.shape[1]
+    lda, ak = _layout(a, 0)
+    ldb, bk = _layout(b, 1)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    nb = int(L.lib().pa_gemm_pp_ws_bytes(M, N, K))
+    ws = torch.empty(nb // 4, dtype=torch.float32, device=a.device) if nb else None
+    L.call("pa_gemm_bf16_res", L.ptr(a), L.ptr(b), L.ptr(out), L.ptr(bias), L.ptr(res), M, N, K, lda, ldb, N,
+           int(ak), int(bk), L.ptr(ws), L.stream_ptr())
+    return out
+
+
 def gemm_dgelu_supported(a, b, pre):
     """pa_gemm_bf16_dgelu conditions: a bf16 GEMM the 256x256 kernels take, pre-activation [M, N] bf16 rows."""
     return (supported(a, b) and L.has("pa_gemm_bf16_dgelu") and pre.dtype == torch.bfloat16 and pre.dim() == 2

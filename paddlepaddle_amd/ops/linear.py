@@ -100,6 +100,21 @@ def _blas_fwd(x2, w, b=None):
     return torch.addmm(b, x2, wv) if b is not None else torch.mm(x2, wv)
 
 
+def _fwd_mm_res(x2, w, b, r2):
+    """x2 @ w (+ b) + r2: the residual add in the GEMM (hand-written epilogue, or hipBLASLt's beta = 1 C input),
+    timed per shape like every other forward GEMM."""
+    if G.res_supported(x2, w, r2):
+        key = ("fwd_res", x2.shape[0], w.shape[1], x2.shape[1], b is not None)
+
+        def blas():
+            y = torch.addmm(r2, x2, w)
+            return y.add_(b) if b is not None else y
+        if G.choose(key, {"blas": blas, "hip": lambda: G.gemm_res(x2, w, r2, bias=b)}) == "hip":
+            return G.gemm_res(x2, w, r2, bias=b)
+        return blas()
+    return _fwd_mm(x2, w, b).add_(r2)
+
+
 def _fwd_mm(x2, w, b=None):
     if x2.shape[0] <= 64 and G.small_m_supported(x2, w):
         M, K, N = x2.shape[0], x2.shape[1], w.shape[1]
@@ -481,11 +496,17 @@ class _GradHook(torch.autograd.Function):
 
 
 class _LinearFn(torch.autograd.Function):
+    """y = x W (+ b) (+ residual): one node; the residual's gradient is dY itself."""
+
     @staticmethod
-    def forward(ctx, x, w, b, dx_hook=None):
+    def forward(ctx, x, w, b, dx_hook=None, residual=None):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
-        y = _fwd_mm(x2, w, b)
+        if residual is not None:
+            y = _fwd_mm_res(x2, w, b, residual.reshape(-1, w.shape[1]).contiguous())
+        else:
+            y = _fwd_mm(x2, w, b)
+        ctx.res_shape = None if residual is None else residual.shape
         ctx.save_for_backward(x2, w)
         ctx.w_leaf = _leaf_weights(w)[0]
         ctx.has_b = b is not None
@@ -514,7 +535,8 @@ class _LinearFn(torch.autograd.Function):
                 db = colsum(dy2)
         if dx is not None:
             dx = dx.view(ctx.shape)
-        return dx, dw, db, None
+        dres = dy.reshape(ctx.res_shape) if (ctx.res_shape is not None and ctx.needs_input_grad[4]) else None
+        return dx, dw, db, None, dres
 
 
 class _LinearBiasGeluFn(torch.autograd.Function):
@@ -590,7 +612,7 @@ def _dgrad_gelu(dy2, w2, h, b1, pre_biased, db_acc=None):
     return split(db_acc)
 
 
-CALLS = {"dgrad_gelu_fused": 0}
+CALLS = {"dgrad_gelu_fused": 0, "linear_residual": 0}
 
 
 class _FFNGeluFn(torch.autograd.Function):
@@ -655,9 +677,18 @@ def _hip_linear_ok(x, w, b):
 
 
 @static_op
-def fused_linear(x, w, b=None, act=None, dx_hook=None):
-    """y = act(x @ w + b). ``dx_hook``: see _mm_grads (runs on the input gradient in backward)."""
+def fused_linear(x, w, b=None, act=None, dx_hook=None, residual=None):
+    """y = act(x @ w + b) (+ residual). ``dx_hook``: see _mm_grads (runs on the input gradient in backward).
+    ``residual`` (no activation): the pre-norm decoder's residual add done by the GEMM (reference
+    incubate/nn/functional/fused_rms_norm.py residual=, fused_linear_param_grad_add)."""
     hip = _hip_linear_ok(x, w, b)
+    if residual is not None:
+        if act is not None:
+            raise ValueError("fused_linear: residual= takes no activation")
+        if hip and residual.dtype == x.dtype and residual.numel() == x.numel() // x.shape[-1] * w.shape[1]:
+            CALLS["linear_residual"] += 1
+            return _LinearFn.apply(x, w, b, dx_hook, residual)
+        return fused_linear(x, w, b, dx_hook=dx_hook) + residual
     if not hip and getattr(_ZB, "route", False) and w.dim() == 2 and torch.is_grad_enabled():
         # zero-bubble forward off the HIP path: the deferrable autograd function, activation applied after
         y = _LinearFn.apply(x, w, b, dx_hook)
