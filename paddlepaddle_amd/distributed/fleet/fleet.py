@@ -193,12 +193,18 @@ class _Fleet:
             return self._sharded_model
         if mode == ParallelMode.PIPELINE_PARALLEL:
             from ...parallel.pipeline import (PipelineParallel, PipelineParallelWithInterleave,
-                                              PipelineParallelWithInterleaveFthenB, PipelineParallelZeroBubble)
+                                              PipelineParallelWithInterleaveFthenB, PipelineParallelZeroBubble,
+                                              PipelineParallelZeroBubbleVPP)
+            mode_ = str((self._strategy.pipeline_configs or {}).get("schedule_mode", "1F1B")).upper()
             if getattr(model, "get_num_virtual_stages", lambda: 1)() > 1:
                 # reference fleet/model.py:160-178: interleaved 1F1B when accumulate_steps >= 2 * pp,
                 # all-forward-then-all-backward when pp <= accumulate_steps < 2 * pp
                 acc = int((self._strategy.pipeline_configs or {}).get("accumulate_steps", 1))
                 pp = hcg.get_pipe_parallel_world_size()
+                if mode_ == "ZBVPP":
+                    if acc % pp:
+                        raise ValueError(f"ZBVPP: accumulate_steps({acc}) must be a multiple of pp_degree({pp})")
+                    return PipelineParallelZeroBubbleVPP(model, hcg, self._strategy)
                 if acc >= 2 * pp:
                     return PipelineParallelWithInterleave(model, hcg, self._strategy)
                 if pp <= acc:

@@ -15,7 +15,7 @@ from .pass_base import PassBase, PassType, register_pass
 from ...parallel import pp_schedules as PS
 
 __all__ = ["Job", "PipelineFThenBPass", "Pipeline1F1BPass", "PipelineEager1F1BPass", "PipelineZBH1Pass",
-           "PipelineVPPPass"]
+           "PipelineVPPPass", "PipelineZBVPPPass"]
 
 FORWARD, BACKWARD, BACKWARD_W, OPT = "forward", "backward", "backward_w", "optimizer"
 _KIND = {"F": FORWARD, "B": BACKWARD, "W": BACKWARD_W}
@@ -112,6 +112,21 @@ class PipelineVPPPass(_PipelinePassBase):
         n, s, d = (int(self.get_attr(k)) for k in ("num_micro_batches", "pp_stage", "pp_degree"))
         v = int(self.get_attr("vpp_degree", 1))
         jobs = [Job(_KIND[k], PS.vpp_mb(i, d, v), PS.vpp_chunk(i, d, v, k == "F")) for k, i in PS.vpp(d, s, n, v)]
+        jobs.append(Job(OPT))
+        return jobs
+
+
+@register_pass("pipeline_scheduler_ZBVPP")
+class PipelineZBVPPPass(PipelineVPPPass):
+    """Zero-bubble interleaved schedule (reference pipeline_zero_bubble.py ZBVPP): the VPP job order with each
+    virtual step's weight gradients as a separate backward_w job (parallel/pp_schedules.py zbvpp; executed by
+    parallel/pipeline.py PipelineParallelZeroBubbleVPP)."""
+    _mode = "ZBVPP"
+
+    def _create_job_list(self):
+        n, s, d = (int(self.get_attr(k)) for k in ("num_micro_batches", "pp_stage", "pp_degree"))
+        v = int(self.get_attr("vpp_degree", 1))
+        jobs = [Job(_KIND[k], PS.vpp_mb(i, d, v), PS.vpp_chunk(i, d, v, k == "F")) for k, i in PS.zbvpp(d, s, n, v)]
         jobs.append(Job(OPT))
         return jobs
 

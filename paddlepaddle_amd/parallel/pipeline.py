@@ -444,6 +444,40 @@ class PipelineParallelWithInterleave(PipelineParallel):
         return [l._t for l in losses]
 
 
+class PipelineParallelZeroBubbleVPP(PipelineParallelWithInterleave):
+    """Interleaved pipeline with the weight gradients split off (reference ZBVPP,
+    distributed/passes/pipeline_scheduler_pass/pipeline_zero_bubble.py; fleet picks it for
+    ``schedule_mode = "ZBVPP"`` with virtual stages): job order parallel/pp_schedules.py zbvpp; a B job runs the
+    chunk's input gradient with the linears' dW GEMMs recorded (ops/linear.py defer_weight_grads), its W job runs
+    them later — in the cool-down, while the stage would otherwise wait for the next gradient from downstream."""
+
+    def forward_backward_pipeline(self, data, scaler=None):
+        from ..ops import linear as LIN
+        from .pp_schedules import zbvpp
+        inputs, labels = (data if isinstance(data, (list, tuple)) and len(data) == 2 else (data, None))
+        n = self.accumulate_steps
+        mb_in = self._split(inputs) if self.stage_id == 0 else [None] * n
+        mb_lb = self._split(labels) if (self.stage_id == self.num_stages - 1 and labels is not None) else [None] * n
+        store, wq, losses = {}, {}, []
+        self.jobs = zbvpp(self.num_stages, self.stage_id, n, self.V)
+        self.deferred_wgrads = 0
+        for kind, k in self.jobs:
+            if kind == "F":
+                with LIN.zero_bubble_forward():
+                    self._vforward(k, mb_in, mb_lb, store, losses)
+            elif kind == "B":
+                q = []
+                with LIN.defer_weight_grads(q):
+                    self._vbackward(k, store)
+                wq[k] = q
+                self.deferred_wgrads += len(q)
+            else:
+                self._flush()
+                LIN.apply_weight_grads(wq.pop(k))
+        self.is_last = self.stage_id == self.num_stages - 1
+        return self._finish(losses)
+
+
 class PipelineParallelWithInterleaveFthenB(PipelineParallelWithInterleave):
     """Virtual pipeline that runs every forward micro-step first, then every backward (reference
     pipeline_parallel.py:2261 PipelineParallelWithInterleaveFthenB, chosen by fleet when

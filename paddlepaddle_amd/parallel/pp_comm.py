@@ -30,7 +30,7 @@ from __future__ import annotations
 
 import collections
 
-from .pp_schedules import schedule, vpp, vpp_chunk, vpp_mb
+from .pp_schedules import schedule, vpp, vpp_chunk, vpp_mb, zbvpp
 
 __all__ = ["programs", "simulate", "Deadlock"]
 
@@ -59,12 +59,16 @@ def _chain_msgs(mode, S, M):
     return comm
 
 
-def _vpp_msgs(S, M, V):
-    """Interleaved 1F1B over V chunks per stage (ring), in the message keys of parallel/pipeline.py."""
+def _vpp_msgs(S, M, V, zb=False):
+    """Interleaved 1F1B over V chunks per stage (ring), in the message keys of parallel/pipeline.py; zb: the ZBVPP
+    order (W jobs communicate nothing)."""
     comm = []
     for s in range(S):
         cs = []
-        for kind, k in vpp(S, s, M, V):
+        for kind, k in (zbvpp if zb else vpp)(S, s, M, V):
+            if kind == "W":
+                cs.append(([], []))
+                continue
             if kind == "F":
                 v, mb = vpp_chunk(k, S, V, True), vpp_mb(k, S, V)
                 first, last = s == 0 and v == 0, s == S - 1 and v == V - 1
@@ -86,8 +90,8 @@ def programs(mode, S, M, V=1, batched=True, ordered=None, split_directions=True)
     batched group is issued as one batch per direction (to a higher / lower rank: two communicators), sends'
     directions first — what parallel/p2p.py does."""
     mode = str(mode).upper()
-    comm = _vpp_msgs(S, M, V) if mode == "VPP" else _chain_msgs(mode, S, M)
-    ordered = (mode != "VPP") if ordered is None else ordered
+    comm = _vpp_msgs(S, M, V, mode == "ZBVPP") if mode in ("VPP", "ZBVPP") else _chain_msgs(mode, S, M)
+    ordered = (mode not in ("VPP", "ZBVPP")) if ordered is None else ordered
     # production order of every directed channel (the order the sender queues its messages)
     prod = collections.defaultdict(list)
     for s in range(S):

@@ -16,7 +16,8 @@ reaches the previous stage one W earlier per hop than with a fused backward.
 """
 from __future__ import annotations
 
-__all__ = ["schedule", "fthenb", "one_f_one_b", "eager_1f1b", "zbh1", "vpp", "vpp_chunk", "vpp_mb", "SCHEDULES"]
+__all__ = ["schedule", "fthenb", "one_f_one_b", "eager_1f1b", "zbh1", "vpp", "zbvpp", "vpp_chunk", "vpp_mb",
+           "SCHEDULES"]
 
 
 def fthenb(n_stages, stage, n_mb):
@@ -83,6 +84,28 @@ def vpp(n_stages, stage, n_mb, n_chunks):
     for i in range(total - warm):
         out += [("F", warm + i), ("B", i)]
     out += [("B", k) for k in range(total - warm, total)]
+    return out
+
+
+def zbvpp(n_stages, stage, n_mb, n_chunks):
+    """Zero-bubble interleaved schedule (reference pipeline_scheduler_pass/pipeline_zero_bubble.py ZBVPP): the VPP
+    order of forward / input-gradient jobs over virtual micro-steps, with each step's weight gradients split off
+    as ("W", k) jobs the way zbh1 places them — during the steady phase at most ``stages - stage - 1`` W jobs stay
+    pending (the 1F1B activation bound), each cool-down backward is followed by one W (the W GEMMs fill the
+    bubbles while the stage waits for the next gradient from downstream), the rest run after the last backward."""
+    base = vpp(n_stages, stage, n_mb, n_chunks)
+    total = n_mb * n_chunks
+    warm = min((n_stages - stage - 1) * 2 + (n_chunks - 1) * n_stages, total)
+    bound = n_stages - stage - 1
+    out, pending = [], []
+    for kind, k in base:
+        out.append((kind, k))
+        if kind != "B":
+            continue
+        pending.append(k)
+        if k >= total - warm or len(pending) > bound:  # cool-down backward, or over the steady-phase bound
+            out.append(("W", pending.pop(0)))
+    out += [("W", k) for k in pending]
     return out
 
 

@@ -302,13 +302,13 @@ def _vpp_descs(paddle):
             LayerDesc(nn.Linear, 32, 32), LayerDesc(nn.Tanh), LayerDesc(nn.Linear, 32, 8), LayerDesc(nn.Tanh)]
 
 
-def _vpp_worker(rank, world, port, acc, q):
+def _vpp_worker(rank, world, port, acc, schedule, q):
     paddle = _setup(rank, world, port)
     from paddlepaddle_amd.parallel.pipeline import (PipelineLayer, PipelineParallelWithInterleave,
-                                                    PipelineParallelWithInterleaveFthenB)
+                                                    PipelineParallelWithInterleaveFthenB, PipelineParallelZeroBubbleVPP)
     paddle.seed(11)
     full = [d.build_layer() for d in _vpp_descs(paddle)]
-    fleet = _fleet_init(paddle, acc=acc, pp_degree=2)
+    fleet = _fleet_init(paddle, acc=acc, schedule=schedule, pp_degree=2)
     pl = PipelineLayer(_vpp_descs(paddle), num_stages=2, loss_fn=_mse, num_virtual_pipeline_stages=2)
     # chunks: segments of 2 layers; stage s holds segments s and 2 + s
     idx = {}
@@ -323,16 +323,21 @@ def _vpp_worker(rank, world, port, acc, q):
     opt = paddle.optimizer.SGD(0.1, parameters=pl.parameters())
     model = fleet.distributed_model(pl)
     # fleet picks the schedule like the reference: interleaved 1F1B for acc >= 2 pp, FThenB for pp <= acc < 2 pp
-    assert type(model) is (PipelineParallelWithInterleave if acc >= 4 else PipelineParallelWithInterleaveFthenB)
+    if schedule == "ZBVPP":
+        assert type(model) is PipelineParallelZeroBubbleVPP
+    else:
+        assert type(model) is (PipelineParallelWithInterleave if acc >= 4 else PipelineParallelWithInterleaveFthenB)
     x, y = _pp_data()
     losses = [float(model.train_batch([paddle.Tensor(x), paddle.Tensor(y)], opt)) for _ in range(2)]
+    if schedule == "ZBVPP":  # weight gradients really were deferred into W jobs
+        assert model.deferred_wgrads > 0 and any(k == "W" for k, _ in model.jobs)
     params = {f"{i}.{k}": v.numpy() for i, f in idx.items() for k, v in f.state_dict().items()}
     q.put((rank, losses, params, None))
     paddle.distributed.barrier()
 
 
-@pytest.mark.parametrize("acc", [4, 2])
-def test_pipeline_interleaved_matches_single_process(acc):
+@pytest.mark.parametrize("acc,schedule", [(4, "1F1B"), (2, "1F1B"), (4, "ZBVPP")])
+def test_pipeline_interleaved_matches_single_process(acc, schedule):
     sys.path.insert(0, ROOT)
     os.environ["PADDLE_AMD_FORCE_CPU"] = "1"
     import paddlepaddle_amd as paddle
@@ -354,7 +359,7 @@ def test_pipeline_interleaved_matches_single_process(acc):
         opt.clear_grad()
         ref.append(float(loss))
     ref_params = {f"{i}.{k}": v.numpy() for i, l in enumerate(layers) for k, v in l.state_dict().items()}
-    res = _spawn(_vpp_worker, acc)
+    res = _spawn(_vpp_worker, acc, schedule)
     (_, l0, p0, _), (_, l1, p1, _) = res
     np.testing.assert_allclose(l0, ref, rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(l1, ref, rtol=1e-5, atol=1e-6)

@@ -27,12 +27,25 @@ def test_schedules_cannot_deadlock(mode, host_waits):
     assert n > 0
 
 
+@pytest.mark.parametrize("mode", ["VPP", "ZBVPP"])
 @pytest.mark.parametrize("host_waits", [False, True])
-def test_interleaved_schedule_cannot_deadlock(host_waits):
+def test_interleaved_schedule_cannot_deadlock(host_waits, mode):
     for S in range(2, 9):
         for V in (2, 3, 4):
             for M in range(S, 17, S):
-                C.simulate(C.programs("VPP", S, M, V), host_waits=host_waits)
+                C.simulate(C.programs(mode, S, M, V), host_waits=host_waits)
+
+
+def test_zbvpp_jobs_valid():
+    from paddlepaddle_amd.parallel import pp_schedules as PS
+    for S in range(2, 6):
+        for V in (2, 3):
+            for M in range(S, 13, S):
+                for s in range(S):
+                    jobs = PS.zbvpp(S, s, M, V)
+                    base = PS.vpp(S, s, M, V)
+                    assert [j for j in jobs if j[0] != "W"] == base  # the VPP order with W jobs inserted
+                    PS.check(jobs, M * V, split_w=True)
 
 
 @pytest.mark.parametrize("mode", ["1F1B", "Eager1F1B", "ZBH1"])
@@ -75,7 +88,7 @@ def _rec_worker(rank, world, port, schedule, acc, q):
     paddle = _setup(rank, world, port)
     from paddlepaddle_amd.parallel.pipeline import PipelineLayer
     fleet = _fleet_init(paddle, acc=acc, pp_degree=2, schedule=schedule)
-    vpp = schedule == "VPP"
+    vpp = schedule in ("VPP", "ZBVPP")
     pl = PipelineLayer(_mlp_descs(paddle), num_stages=2, loss_fn=_mse,
                        num_virtual_pipeline_stages=2 if vpp else None)
     opt = paddle.optimizer.SGD(1e-2, parameters=pl.parameters())
@@ -95,11 +108,12 @@ def _key(k):
     return (kind, int(k[1]), int(k[2]))
 
 
-@pytest.mark.parametrize("schedule,acc", [("1F1B", 4), ("ZBH1", 4), ("Eager1F1B", 4), ("FThenB", 2), ("VPP", 4)])
+@pytest.mark.parametrize("schedule,acc", [("1F1B", 4), ("ZBH1", 4), ("Eager1F1B", 4), ("FThenB", 2), ("VPP", 4),
+                                          ("ZBVPP", 4)])
 def test_engine_issues_modelled_program(schedule, acc):
     from test_distributed_cpu import _spawn
     res = dict(_spawn(_rec_worker, schedule, acc, world=2))
-    progs = C.programs(schedule, 2, acc, V=2 if schedule == "VPP" else 1)
+    progs = C.programs(schedule, 2, acc, V=2 if schedule in ("VPP", "ZBVPP") else 1)
     for rank in (0, 1):
         want = [tuple((op[0], op[2] if op[0] == "s" else op[1], _key(op[3][2])) for op in g) for g in progs[rank]]
         assert res[rank] == want, (rank, res[rank], want)

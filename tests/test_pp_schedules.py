@@ -65,6 +65,10 @@ def test_pipeline_scheduler_passes_build_job_lists():
                                               "vpp_degree": 2}).apply(prog, None)
     jobs = ctx.get_attr("pipeline_scheduler.job_list")
     assert len(jobs) == 2 * 4 * 2 + 1 and {j.chunk_id() for j in jobs[:-1]} == {0, 1}
+    ctx = new_pass("pipeline_scheduler_ZBVPP", {"num_micro_batches": 4, "pp_stage": 0, "pp_degree": 2,
+                                                "vpp_degree": 2}).apply(P.Program(), None)
+    jobs = ctx.get_attr("pipeline_scheduler.job_list")
+    assert len(jobs) == 3 * 4 * 2 + 1 and sum(j.type() == "backward_w" for j in jobs) == 8
     # missing attributes: the pass does not apply
     assert new_pass("pipeline_scheduler_1F1B").apply(P.Program(), None).get_attr(
         "pipeline_scheduler.job_list") is None
