@@ -1371,9 +1371,10 @@ class StaticEngine:
             from ...framework.tensor import _PARAM_OF
             _PARAM_OF[id(loc)] = p
             self.local_params[slot] = p
-        clip = getattr(self.opt, "_grad_clip", None)
-        if clip is not None and hasattr(clip, "_extra_sq_norm_fn"):
-            clip._param_sq_fn = self._param_sq
+        # the global-norm clip over the partitioned program (reference passes/auto_parallel_grad_clip.py)
+        from ..passes import new_pass
+        new_pass("auto_parallel_grad_clip", {"optimizer": self.opt, "sq_norm_fn": self._param_sq}).apply(
+            self.prog, None)
 
     # ------------------------------------------------------------------ ZeRO (stage 1 / 2) over the dp mesh dim
     def _zero_setup(self):
@@ -1433,9 +1434,9 @@ class StaticEngine:
             return
         opt._param_groups = [{"params": shard_params}]
         opt._parameter_list = shard_params
-        clip = getattr(opt, "_grad_clip", None)
-        if clip is not None and hasattr(clip, "_extra_sq_norm_fn"):
-            clip._param_sq_fn = self._zero_param_sq
+        from ..passes import new_pass
+        new_pass("auto_parallel_grad_clip", {"optimizer": opt, "sq_norm_fn": self._zero_param_sq}).apply(
+            self.prog, None)
 
     def _zero_check_partition(self):
         """ZeRO reduce-scatters the parameters' local dp gradients itself: no data-parallel all-reduce of a

@@ -5,5 +5,6 @@ from .program_passes import (  # noqa: F401
     AMPPass, DeadCodeEliminationPass, FP16Pass, FuseGemmEpiloguePass, GradientMergePass,
 )
 from . import pipeline_scheduler  # noqa: F401  (pipeline_scheduler_* passes)
+from . import fusion_passes  # noqa: F401  (fused_feedforward / fused_attention / ... and auto-parallel passes)
 
 __all__ = ["new_pass", "PassManager", "PassContext"]

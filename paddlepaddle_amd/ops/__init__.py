@@ -9,7 +9,7 @@ from __future__ import annotations
 from .activation import gelu, silu, swiglu, softmax, bias_gelu  # noqa: F401
 from .norm import rms_norm, rms_norm_residual, layer_norm, layer_norm_residual, add_rms_norm  # noqa: F401
 from .loss import softmax_cross_entropy  # noqa: F401
-from .attention import flash_attention, flash_attention_qkvpacked, qkv_rope_attention, attention_reference, paged_decode_attention, dense_decode_attention  # noqa: F401,E501
+from .attention import flash_attention, attention_bhsd, flash_attention_qkvpacked, qkv_rope_attention, attention_reference, paged_decode_attention, dense_decode_attention  # noqa: F401,E501
 from .rope import apply_rotary, decode_rope_cache  # noqa: F401
 from .linear import fused_linear, colsum, linear_nt, ffn_gelu  # noqa: F401
 from .lm_head import lm_head_cross_entropy  # noqa: F401

@@ -537,6 +537,14 @@ def _decode_launch(q, kc, vc, tables, lens, Hkv, bs, blk_stride, head_stride, sc
 
 
 @static_op
+def attention_bhsd(q, k, v, scale=None, mask=None, causal=False):
+    """softmax(q k^T * scale (+ mask)) v over [B, H, S, D] tensors (the math-attention layout of traced programs),
+    on the flash-attention kernel: the target of the fuse_dot_product_attention program pass. Returns [B, H, Sq, D]."""
+    o = attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), causal=causal, scale=scale, mask=mask)
+    return o.transpose(1, 2)
+
+
+@static_op
 def paged_decode_attention(q, key_cache, value_cache, block_tables, lens, scale=None, max_len=None):
     """One-token-per-sequence attention over a paged KV cache (block_multihead_attention decode).
     q [N,H,D]; caches [num_blocks,Hkv,block_size,D]; block_tables [N,max_blocks]; lens [N] cached

@@ -228,9 +228,19 @@ def scope_guard(scope):
 
 
 class BuildStrategy:
+    """Graph-build options; the fusion switches select registered program passes (distributed/passes), applied
+    once to a CompiledProgram's program on its first run (reference framework/ir.py:56 apply_build_strategy)."""
+
     def __init__(self):
         self.fuse_elewise_add_act_ops = False
         self.fuse_bn_act_ops = False
+        self.fuse_bn_add_act_ops = False
+        self.fuse_gemm_epilogue = False
+        self.fused_attention = False
+        self.fused_feedforward = False
+        self.fuse_dot_product_attention = False
+        self.fuse_adamw = False
+        self.fuse_all_optimizer_ops = False
         self.enable_inplace = True
         self.memory_optimize = True
         self.fuse_all_reduce_ops = True
@@ -247,10 +257,30 @@ class ExecutionStrategy:
         self.num_iteration_per_drop_scope = 100
 
 
+# BuildStrategy switch -> pass, in application order (AMP-independent fusions first, GEMM epilogue before the
+# passes that consume fused_linear nodes)
+_BUILD_PASSES = (("fuse_bn_act_ops", "fuse_bn_act"), ("fuse_bn_add_act_ops", "fuse_bn_add_act"),
+                 ("fuse_dot_product_attention", "fuse_dot_product_attention"),
+                 ("fuse_gemm_epilogue", "fuse_gemm_epilogue"), ("fused_feedforward", "fused_feedforward"),
+                 ("fused_attention", "fused_attention"), ("fuse_elewise_add_act_ops", "fuse_elewise_add_act"),
+                 ("fuse_adamw", "fuse_adamw"), ("fuse_all_optimizer_ops", "fuse_optimizer"))
+
+
+def apply_build_strategy(program, build_strategy):
+    """Apply the passes ``build_strategy`` enables to ``program`` (in place); returns {pass: context}."""
+    from ..distributed.passes import new_pass
+    done = {}
+    for attr, name in _BUILD_PASSES:
+        if getattr(build_strategy, attr, False):
+            done[name] = new_pass(name).apply(program, None)
+    return done
+
+
 class CompiledProgram:
     def __init__(self, program_or_graph, build_strategy=None):
         self._program = program_or_graph
         self._build_strategy = build_strategy or BuildStrategy()
+        self._applied = None  # {pass name: context} once the build strategy's passes ran
 
     def with_data_parallel(self, loss_name=None, build_strategy=None, exec_strategy=None, places=None):
         return self
@@ -303,6 +333,8 @@ class Executor:
         if isinstance(prog, CompiledProgram):
             bs = prog._build_strategy
             use_graph = bool(getattr(bs, "allow_cuda_graph_capture", False) or getattr(bs, "build_cuda_graph", False))
+            if prog._applied is None and isinstance(prog._program, P.Program):
+                prog._applied = apply_build_strategy(prog._program, bs)
             prog = prog._program
         from ..framework.program_desc import ProgramDescRunner
         from ..framework.pir_json import PirRunner
@@ -349,19 +381,28 @@ class Executor:
         if opt is not None:
             optimizer, ls = opt
             gm = getattr(prog, "_grad_merge", None)  # (k_steps, avg) from auto_parallel_gradient_merge
-            if gm is None:
+            k, avg = gm if gm is not None else (1, False)
+            count = getattr(prog, "_gm_count", 0)
+            if count % k == 0:
                 optimizer.clear_grad(set_to_zero=False)
-                env[ls].backward()
-                _dp_sync(prog, optimizer)
-                optimizer.step()
-            else:
-                k, avg = gm
-                if prog._gm_count % k == 0:
-                    optimizer.clear_grad(set_to_zero=False)
-                (env[ls] / k if avg else env[ls]).backward()
-                prog._gm_count += 1
-                if prog._gm_count % k == 0:
+                _master_grads_clear(prog, optimizer)
+            last = (count + 1) % k == 0
+            # auto_parallel_data_parallel_optimization: bucket all-reduces launched from backward hooks
+            red = _OverlapReducer(prog, optimizer) if last and _dp_overlap(prog) else None
+            (env[ls] / k if avg else env[ls]).backward()
+            _master_grads_accumulate(prog, optimizer)
+            if gm is not None:
+                prog._gm_count = count + 1
+            if last:
+                if red is not None:
+                    red.finish()
+                elif _master_on(prog):
+                    pg = getattr(prog, "_dp_sync", None)
+                    if pg is not None:  # the fp32 sums are what data parallelism averages
+                        _allreduce_mean(list(getattr(prog, "_pa_main_grads", {}).values()), pg)
+                else:
                     _dp_sync(prog, optimizer)
+                with _master_grads_as_grads(prog, optimizer):
                     optimizer.step()
         outs = []
         for s in fetch:
@@ -571,6 +612,134 @@ def create_global_var(shape, value, dtype, persistable=False, force_cpu=False, n
 def create_parameter(shape, dtype, name=None, attr=None, is_bias=False, default_initializer=None):
     from .. import create_parameter as _cp
     return _cp(shape, dtype, name, attr, is_bias, default_initializer)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# auto_parallel_master_grad_pass: fp32 gradient accumulation for 16-bit parameters
+def _master_on(prog):
+    return bool(getattr(prog, "_pa_master_grad", False))
+
+
+def _master_grads_clear(prog, optimizer):
+    if _master_on(prog):
+        prog._pa_main_grads = {}
+
+
+@torch.no_grad()
+def _master_grads_accumulate(prog, optimizer):
+    """Each backward's 16-bit gradient is added into the parameter's fp32 main gradient and released."""
+    if not _master_on(prog):
+        return
+    mg = prog.__dict__.setdefault("_pa_main_grads", {})
+    for p in optimizer._parameter_list:
+        g = p._t.grad
+        if g is None or g.dtype not in (torch.bfloat16, torch.float16):
+            continue
+        acc = mg.get(id(p))
+        if acc is None:
+            mg[id(p)] = g.float()
+        else:
+            acc.add_(g.float())
+        p._t.grad = None
+
+
+@contextlib.contextmanager
+def _master_grads_as_grads(prog, optimizer):
+    """The optimizer step (and the data-parallel reduction before it) reads the fp32 sums, rounded once."""
+    if not _master_on(prog):
+        yield
+        return
+    mg = getattr(prog, "_pa_main_grads", {})
+    with torch.no_grad():
+        for p in optimizer._parameter_list:
+            acc = mg.get(id(p))
+            if acc is not None:
+                p._t.grad = acc.to(p._t.dtype)
+    try:
+        yield
+    finally:
+        prog._pa_main_grads = {}
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# auto_parallel_data_parallel_optimization: gradient buckets all-reduced from backward hooks
+def _dp_overlap(prog):
+    cfg = getattr(prog, "_pa_dp_opt", None)
+    return (cfg is not None and cfg.get("overlap", True) and getattr(prog, "_dp_sync", None) is not None
+            and not _master_on(prog))
+
+
+DP_OVERLAP_STATS = {"launched_in_backward": 0}
+
+
+class _OverlapReducer:
+    """Buckets (one dtype each, ``bucket_mb``) over the parameters in reverse registration order — the order
+    backward produces their gradients; a bucket's flat all-reduce starts (async, on the communicator's stream)
+    from the post-accumulate hook of its last parameter, overlapping the rest of backward. finish() waits,
+    averages and scatters back; buckets whose hooks never fired (unused parameters) reduce there."""
+
+    def __init__(self, prog, optimizer):
+        import torch.distributed as tdist
+        self.pg = prog._dp_sync
+        self.n = tdist.get_world_size(self.pg)
+        cap = int(prog._pa_dp_opt["bucket_bytes"])
+        params = [p for p in optimizer._parameter_list if p._t.requires_grad]
+        self.buckets, self.of = [], {}
+        cur, size, dt = [], 0, None
+        for p in reversed(params):
+            nb = p._t.numel() * p._t.element_size()
+            if cur and (p._t.dtype != dt or size + nb > cap):
+                self.buckets.append(cur)
+                cur, size = [], 0
+            cur.append(p)
+            size += nb
+            dt = p._t.dtype
+        if cur:
+            self.buckets.append(cur)
+        self.pending = [len(b) for b in self.buckets]
+        self.work = [None] * len(self.buckets)
+        self.flat = [None] * len(self.buckets)
+        self.handles = []
+        for bi, b in enumerate(self.buckets):
+            for p in b:
+                self.handles.append(p._t.register_post_accumulate_grad_hook(self._hook(bi)))
+
+    def _hook(self, bi):
+        def h(_t):
+            self.pending[bi] -= 1
+            if self.pending[bi] == 0:
+                self._launch(bi)
+        return h
+
+    @torch.no_grad()
+    def _launch(self, bi):
+        import torch.distributed as tdist
+        b = self.buckets[bi]
+        if any(p._t.grad is None for p in b):
+            return
+        flat = torch.cat([p._t.grad.reshape(-1) for p in b])
+        self.flat[bi] = flat
+        self.work[bi] = tdist.all_reduce(flat, group=self.pg, async_op=True)
+        DP_OVERLAP_STATS["launched_in_backward"] += 1
+
+    @torch.no_grad()
+    def finish(self):
+        for h in self.handles:
+            h.remove()
+        rest = []
+        for bi, b in enumerate(self.buckets):
+            if self.work[bi] is None:
+                rest.extend(p._t.grad for p in b if p._t.grad is not None)
+                continue
+            self.work[bi].wait()
+            flat = self.flat[bi].mul_(1.0 / self.n)
+            off = 0
+            for p in b:
+                k = p._t.numel()
+                p._t.grad.copy_(flat[off:off + k].view_as(p._t.grad))
+                off += k
+        if rest:
+            _allreduce_mean(rest, self.pg)
 
 
 def _dp_sync(prog, optimizer):

@@ -1,0 +1,172 @@
+"""Fusion / auto-parallel program passes of distributed/passes/fusion_passes.py on traced static programs:
+each rewrite is checked for the node it produces and for unchanged results (forward outputs, trained parameters)
+against the unrewritten program. Reference: distributed/passes/cpp_pass.py:76-141,
+auto_parallel_master_grad.py:84, auto_parallel_quantization.py:48, framework/ir.py:56 (build strategy)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+os.environ["PADDLE_AMD_FORCE_CPU"] = "1"
+import paddlepaddle_amd as paddle  # noqa: E402
+from paddlepaddle_amd.distributed.passes import new_pass  # noqa: E402
+
+
+@pytest.fixture(autouse=True)
+def _static():
+    paddle.enable_static()
+    yield
+    paddle.disable_static()
+
+
+def _names(prog):
+    return [n.name.rsplit(":", 1)[-1] for n in prog.nodes]
+
+
+def _run(prog, feed, fetch):
+    exe = paddle.static.Executor(paddle.CPUPlace())
+    return [np.array(v) for v in exe.run(prog, feed=feed, fetch_list=fetch)]
+
+
+def _ffn_program(fold_first):
+    main, start = paddle.static.Program(), paddle.static.Program()
+    with paddle.static.program_guard(main, start):
+        paddle.seed(3)
+        x = paddle.static.data("x", [4, 8, 16], "float32")
+        l1, l2 = paddle.nn.Linear(16, 64), paddle.nn.Linear(64, 16)
+        y = l2(paddle.nn.functional.gelu(l1(x), approximate=True))
+        out = y + x
+    if fold_first:
+        new_pass("fuse_gemm_epilogue").apply(main, None)
+    return main, out
+
+
+@pytest.mark.parametrize("fold_first", [True, False])
+def test_fused_feedforward_rewrites_fc_gelu_fc(fold_first):
+    main, out = _ffn_program(fold_first)
+    feed = {"x": np.random.RandomState(0).randn(4, 8, 16).astype("float32")}
+    ref, = _run(main, feed, [out])
+    ctx = new_pass("fused_feedforward").apply(main, None)
+    assert ctx.get_attr("fused_feedforward.fused") == 1
+    assert "ffn_gelu" in _names(main) and "gelu" not in _names(main)
+    got, = _run(main, feed, [out])
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5)
+
+
+def test_fused_attention_folds_residual_into_out_projection():
+    main, out = _ffn_program(True)
+    feed = {"x": np.random.RandomState(1).randn(4, 8, 16).astype("float32")}
+    ref, = _run(main, feed, [out])
+    ctx = new_pass("fused_attention").apply(main, None)
+    assert ctx.get_attr("fused_attention.fused") == 1 and "add" not in _names(main)
+    lin = [n for n in main.nodes if n.name.endswith("fused_linear")][-1]
+    assert len(lin.args) == 6 and lin.args[5] is not None  # residual= operand
+    got, = _run(main, feed, [out])
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("with_mask", [False, True])
+def test_fuse_dot_product_attention(with_mask):
+    main, start = paddle.static.Program(), paddle.static.Program()
+    B, H, S, D = 2, 4, 16, 8
+    with paddle.static.program_guard(main, start):
+        q = paddle.static.data("q", [B, H, S, D], "float32")
+        k = paddle.static.data("k", [B, H, S, D], "float32")
+        v = paddle.static.data("v", [B, H, S, D], "float32")
+        s = paddle.matmul(q, k, transpose_y=True) * (D ** -0.5)
+        if with_mask:
+            m = paddle.static.data("m", [B, 1, S, S], "float32")
+            s = s + m
+        o = paddle.matmul(paddle.nn.functional.softmax(s, axis=-1), v)
+    rs = np.random.RandomState(2)
+    feed = {n: rs.randn(B, H, S, D).astype("float32") for n in "qkv"}
+    if with_mask:
+        feed["m"] = np.where(rs.rand(B, 1, S, S) > 0.2, 0.0, -1e4).astype("float32")
+    ref, = _run(main, feed, [o])
+    ctx = new_pass("fuse_dot_product_attention").apply(main, None)
+    assert ctx.get_attr("fuse_dot_product_attention.fused") == 1
+    assert _names(main) == ["attention_bhsd"]
+    got, = _run(main, feed, [o])
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-5)
+
+
+def _train_program(opt_fn, dtype="float32", groups=False):
+    main, start = paddle.static.Program(), paddle.static.Program()
+    with paddle.static.program_guard(main, start):
+        paddle.seed(5)
+        x = paddle.static.data("x", [8, 16], dtype)
+        y = paddle.static.data("y", [8, 4], dtype)
+        l1, l2 = paddle.nn.Linear(16, 32), paddle.nn.Linear(32, 4)
+        if dtype != "float32":
+            for p in list(l1.parameters()) + list(l2.parameters()):
+                p._t.data = p._t.data.to(torch.bfloat16)
+        loss = paddle.mean((l2(paddle.nn.functional.relu(l1(x))) - y) ** 2)
+        params = [{"params": l1.parameters()}, {"params": l2.parameters()}] if groups else None
+        opt = opt_fn(params)
+        opt.minimize(loss)
+    return main, loss
+
+
+def _data(dtype="float32"):
+    rs = np.random.RandomState(7)
+    x, y = rs.randn(8, 16), rs.randn(8, 4)
+    if dtype == "float32":
+        return {"x": x.astype("float32"), "y": y.astype("float32")}
+    return {"x": torch.tensor(x).bfloat16(), "y": torch.tensor(y).bfloat16()}
+
+
+@pytest.mark.parametrize("name", ["fuse_adamw", "fuse_optimizer"])
+def test_fuse_optimizer_merges_equal_groups(name):
+    res = []
+    for apply in (False, True):
+        main, loss = _train_program(lambda ps: paddle.optimizer.AdamW(0.01, parameters=ps), groups=True)
+        if apply:
+            ctx = new_pass(name).apply(main, None)
+            assert ctx.get_attr(f"{name}.merged_groups") == 1
+            assert len(main._optimize[0]._param_groups) == 1
+        res.append([float(_run(main, _data(), [loss])[0]) for _ in range(3)])
+    np.testing.assert_allclose(res[1], res[0], rtol=1e-6)
+
+
+def test_master_grad_accumulates_fp32_across_gradient_merge():
+    main, loss = _train_program(lambda ps: paddle.optimizer.SGD(0.5), dtype="bfloat16")
+    new_pass("auto_parallel_gradient_merge", {"k_steps": 2, "avg": False}).apply(main, None)
+    new_pass("auto_parallel_master_grad_pass").apply(main, None)
+    params = main.all_parameters()
+    w0 = [p._t.detach().float().clone() for p in params]
+    _run(main, _data("bf16"), [loss])
+    assert all(p._t.grad is None for p in params)  # released into the fp32 main gradients
+    assert all(g.dtype == torch.float32 for g in main._pa_main_grads.values()) and main._pa_main_grads
+    mg = {k: v.clone() for k, v in main._pa_main_grads.items()}
+    _run(main, _data("bf16"), [loss])
+    # the update used 2 x the fp32 per-micro-step gradient, rounded once to bf16
+    for p, w in zip(params, w0):
+        g = (2 * mg[id(p)]).to(torch.bfloat16).float()
+        np.testing.assert_allclose(p._t.detach().float().numpy(), (w - 0.5 * g).to(torch.bfloat16).float().numpy(),
+                                   rtol=1e-2, atol=1e-2)
+
+
+def test_quantization_pass_inserts_fake_quant():
+    main, loss = _train_program(lambda ps: paddle.optimizer.SGD(0.1))
+    ctx = new_pass("auto_parallel_quantization", {"weight_bits": 8, "activation_bits": 8}).apply(main, None)
+    assert ctx.get_attr("auto_parallel_quantization.quantized") == 2
+    names = _names(main)
+    assert names.count("qat_fake_quant_act") == 2 and names.count("qat_fake_quant_weight") == 2
+    losses = [float(_run(main, _data(), [loss])[0]) for _ in range(4)]
+    assert losses[-1] < losses[0]
+
+
+def test_build_strategy_applies_fusion_passes_on_first_run():
+    main, out = _ffn_program(False)
+    feed = {"x": np.random.RandomState(4).randn(4, 8, 16).astype("float32")}
+    ref, = _run(main, feed, [out])
+    bs = paddle.static.BuildStrategy()
+    bs.fuse_gemm_epilogue = True
+    bs.fused_feedforward = True
+    bs.fused_attention = True
+    cp = paddle.static.CompiledProgram(main, build_strategy=bs)
+    got, = _run(cp, feed, [out])
+    assert set(cp._applied) == {"fuse_gemm_epilogue", "fused_feedforward", "fused_attention"}
+    assert "ffn_gelu" in _names(main)
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5)

@@ -33,11 +33,16 @@ def _build(paddle, fleet=None):
 
 def _worker(rank, world, port, native, q):
     paddle = _setup(rank, world, port)
+    overlap = native == "overlap"
+    native = native is True
     paddle.set_flags({"FLAGS_static_native_executor": "force" if native else "off"})
     from paddlepaddle_amd.distributed import fleet
     fleet.init(is_collective=True)
     main, loss = _build(paddle, fleet)
     assert main._dp_sync is not None
+    if overlap:  # auto_parallel_data_parallel_optimization: 2 KiB buckets -> several all-reduces from backward
+        from paddlepaddle_amd.distributed.passes import new_pass
+        new_pass("auto_parallel_data_parallel_optimization", {"bucket_size_mb": 2.0 / 1024}).apply(main, None)
     exe = paddle.static.Executor(paddle.CPUPlace())
     xs, ys = _data()
     half = slice(rank * 4, rank * 4 + 4)
@@ -48,12 +53,15 @@ def _worker(rank, world, port, native, q):
     params = [p.numpy().copy() for p in main.all_parameters()]
     runners = [r for r in main.__dict__.get("_native_runners", {}).values() if r is not None]
     assert bool(runners) == native, (native, main.__dict__.get("_native_reason"))
+    if overlap:
+        from paddlepaddle_amd.static.executor import DP_OVERLAP_STATS
+        assert DP_OVERLAP_STATS["launched_in_backward"] >= 2 * STEPS
     paddle.disable_static()
     q.put((rank, losses, params))
     paddle.distributed.barrier()
 
 
-@pytest.mark.parametrize("native", [False, True])
+@pytest.mark.parametrize("native", [False, True, "overlap"])
 def test_static_collective_dp_matches_whole_batch(native):
     """Python replay and the native training executor (_C_train: the all-reduce as its gradient hook between the
     backward and the fused update)."""
