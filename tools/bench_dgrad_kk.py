@@ -44,3 +44,23 @@ for name, (M, N, K) in SHAPES.items():
           + f"  hip/blas {min(r['bn1'], r['bn2']) / r['blas']:.3f}", flush=True)
     del dys, ws
 print("sum: " + "  ".join(f"{k} {v:.0f}us" for k, v in tot.items()))
+
+# the other two layouts of a training step: forward x @ W (A K-major, B MN-major) and weight gradient x^T dY (both
+# MN-major), GPT-3 13B / LLaMA-2 70B shapes
+OTHER = {"13b fwd fc1": ("fwd", 4096, 20480, 5120), "13b fwd fc2": ("fwd", 4096, 5120, 20480),
+         "70b fwd o": ("fwd", 4096, 8192, 8192), "13b wgrad fc1": ("wgrad", 5120, 20480, 4096),
+         "13b wgrad qkv": ("wgrad", 5120, 15360, 4096), "70b wgrad o": ("wgrad", 8192, 8192, 4096)}
+for name, (kind, M, N, K) in OTHER.items():
+    if kind == "fwd":
+        As = [torch.randn(M, K, device="cuda", dtype=torch.bfloat16) for _ in range(3)]
+        Bs = [(torch.randn(K, N, device="cuda") * 0.02).to(torch.bfloat16) for _ in range(3)]
+    else:  # dW [M = in, N = out] = x^T dY, x [K tokens, in], dY [K, out]
+        As = [torch.randn(K, M, device="cuda", dtype=torch.bfloat16).t() for _ in range(3)]
+        Bs = [torch.randn(K, N, device="cuda", dtype=torch.bfloat16) for _ in range(3)]
+    r = {"blas": t_us(lambda i: torch.mm(As[i % 3], Bs[i % 3]))}
+    for bn in (1, 2):
+        r[f"bn{bn}"] = t_us(lambda i, bn=bn: G.gemm(As[i % 3], Bs[i % 3], bn=bn))
+    fl = 2 * M * N * K
+    print(f"{name:14s} M{M} N{N} K{K}: " + "  ".join(f"{k} {v:7.0f}us {fl / v / 1e6:5.0f}TF" for k, v in r.items()),
+          flush=True)
+    del As, Bs
