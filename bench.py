@@ -200,10 +200,13 @@ def gpt_bench(args, paddle, world, dist_on):
     tokens = args.steps * args.accum * B * S * n_shard
     tps = tokens / dt
     fpt = cfg.flops_per_token(S, recompute=False)
-    mfu = tps * fpt / (PEAK_BF16 * world)
+    mfu = tps * fpt / (PEAK_BF16 * world)  # 6N + causal attention FLOPs
+    # strict 6N: parameter GEMM FLOPs only (non-embedding parameters), the attention score / value products left out
+    gpt_bench.mfu_strict = tps * 6 * (cfg.num_params() - cfg.max_position_embeddings * cfg.hidden_size) / (
+        PEAK_BF16 * world)
     mem = paddle.device.cuda.max_memory_allocated() / 2**30 if dev.type == "cuda" else 0.0
     log(f"[gpt] loss={float(state['loss']):.4f} step={dt / args.steps * 1000:.1f}ms tokens/s={tps:.0f} "
-        f"MFU(6N model flops)={mfu * 100:.1f}% mem={mem:.1f}GiB")
+        f"MFU(6N + attention)={mfu * 100:.1f}% MFU(strict 6N)={gpt_bench.mfu_strict * 100:.1f}% mem={mem:.1f}GiB")
     try:
         from paddlepaddle_amd.ops import gemm as _G
         ch = _G.choices()
@@ -515,7 +518,11 @@ def main():
                                              if getattr(gpt_bench, "keep_params", None) else
                                              "released after each block, re-gathered per micro-batch")}
                           if (args.sharding_stage == 3 and not is_llama and world // max(args.tp, 1) > 1) else {})},
-            "mfu_6N": round(mfu, 4) if mfu is not None else None,
+            # model-FLOPs utilisation at the 2.5 PF dense bf16 peak: 6N plus the causal attention products, and the
+            # strict 6N form (parameter GEMMs only)
+            "mfu_6N_plus_attn": round(mfu, 4) if mfu is not None else None,
+            "mfu_6N_strict": (round(gpt_bench.mfu_strict, 4) if (mfu is not None and not is_llama
+                                                                  and hasattr(gpt_bench, "mfu_strict")) else None),
             "secondary": {"metric": "ResNet50 img/s (bf16 NHWC, DP)", "value": round(ips, 1) if ips else None,
                           "per_gpu_batch": args.resnet_batch,
                           "step": "hipGraph replay" if getattr(resnet_bench, "graph", False) else "eager"},
