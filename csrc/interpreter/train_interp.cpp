@@ -869,19 +869,26 @@ class TrainProgram {
                               std::vector<std::vector<double>> scalars, double clip_norm) {
     for (const auto& f : feeds) slots_.at(f.first) = f.second;
     at::Tensor loss;
+    // progress of this run, read by the executor when it raised: a failed step may be replayed elsewhere only if
+    // it failed in the forward before any instruction with device side effects completed
+    phase_ = 0;
+    done_ = 0;
     {
       at::AutoGradMode grad_mode(backward);
       for (size_t n = 0; n < code_.size(); ++n) {
         exec(code_[n]);
+        done_ = static_cast<int64_t>(n) + 1;
         for (int s : release_[n]) slots_[s] = at::Tensor();
       }
       if (backward) {
+        phase_ = 1;
         loss = slots_.at(loss_);
         zero_grads();
         torch::autograd::backward({loss});
       }
     }
     if (backward && !opt_.empty() && grad_hook_ && !grad_hook_.is_none()) {
+      phase_ = 2;
       std::vector<at::Tensor> gs;
       for (auto& g : opt_)
         for (auto& p : g.params)
@@ -890,6 +897,7 @@ class TrainProgram {
       grad_hook_(gs);
     }
     if (backward && !opt_.empty()) {
+      phase_ = 3;
       at::NoGradGuard ng;
       at::Tensor inv_scale = clip_norm > 0 ? clip_coef(clip_norm) : at::Tensor();
       for (size_t g = 0; g < opt_.size(); ++g) step(opt_[g], g < scalars.size() ? scalars[g] : std::vector<double>{},
@@ -908,6 +916,10 @@ class TrainProgram {
   }
 
   int64_t num_instructions() const { return static_cast<int64_t>(code_.size()); }
+  // phase of the last run when it stopped (0 forward, 1 backward, 2 gradient hook, 3 update) and the number of
+  // forward instructions it completed
+  int64_t phase() const { return phase_; }
+  int64_t done() const { return done_; }
   int64_t num_native() const {
     int64_t n = 0;
     for (const auto& I : code_) n += I.kind != kAten && I.kind != kAlias;
@@ -1101,6 +1113,7 @@ class TrainProgram {
   std::vector<std::vector<int>> release_;
   std::vector<OptGroup> opt_;
   py::object grad_hook_;
+  int64_t phase_ = 0, done_ = 0;
   int loss_ = -1;
 };
 
@@ -1123,5 +1136,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("run", &TrainProgram::run, py::arg("feeds"), py::arg("backward"), py::arg("scalars"), py::arg("clip_norm"),
            py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("num_instructions", &TrainProgram::num_instructions)
-      .def_property_readonly("num_native", &TrainProgram::num_native);
+      .def_property_readonly("num_native", &TrainProgram::num_native)
+      .def_property_readonly("phase", &TrainProgram::phase)
+      .def_property_readonly("done", &TrainProgram::done);
 }

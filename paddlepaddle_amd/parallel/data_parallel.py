@@ -67,7 +67,8 @@ class DataParallel(Layer):
         self._buckets = []
         self._param_loc = {}
         self._queued = False
-        self._next_launch = 0  # index of the next bucket to all-reduce (launch order = bucket order)
+        self._next_launch = 0  # position in _order of the next bucket to all-reduce
+        self._order = []
         if self._world > 1:
             self._broadcast_params()
             self._build_buckets(comm_buffer_size, last_comm_buffer_size)
@@ -111,6 +112,13 @@ class DataParallel(Layer):
                     p._t.grad = b.view(j)
                     p._dp_bucket = (b, j)  # Optimizer.clear_grad keeps the bucket views (one memset per bucket)
                     p._t.register_post_accumulate_grad_hook(self._make_hook(p))
+        # launch order across dtype groups by expected readiness: a bucket is complete when its earliest-registered
+        # parameter gets its gradient, and backward reaches parameters in reverse registration order. Sorting by
+        # that (stable, the same on every rank) interleaves the groups' buckets instead of holding every bucket of
+        # the second group behind the first group's last one
+        reg = {id(p): i for i, p in enumerate(params)}
+        self._order = sorted(range(len(self._buckets)),
+                             key=lambda bi: -min(reg[id(p)] for p in self._buckets[bi].params))
 
     def _make_hook(self, p):
         def hook(t):
@@ -140,9 +148,9 @@ class DataParallel(Layer):
             self._launch_ready()
 
     def _launch_ready(self):
-        """Launch every full bucket at the head of the launch order (bucket-index order)."""
+        """Launch every full bucket at the head of the launch order (``_order``, by expected readiness)."""
         while self._next_launch < len(self._buckets):
-            b = self._buckets[self._next_launch]
+            b = self._buckets[self._order[self._next_launch]]
             if b.work is not None or len(b.ready) < len(b.params):
                 break
             self._launch(b)
@@ -162,7 +170,7 @@ class DataParallel(Layer):
         # the rest in bucket order; buckets with unused params keep those slices as they are (zero after
         # clear_grad) and are reduced like the others
         while self._next_launch < len(self._buckets):
-            self._launch(self._buckets[self._next_launch])
+            self._launch(self._buckets[self._order[self._next_launch]])
             self._next_launch += 1
         for b in self._buckets:
             b.work.wait()

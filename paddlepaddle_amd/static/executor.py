@@ -360,7 +360,9 @@ class Executor:
             try:
                 outs = nat.run(self._feed(prog, feed or {}, dev))
             except RuntimeError as e:
-                if nat.runs:  # it ran before: a real failure of this step
+                # it ran before (a real failure of this step), or it got far enough to change device state (BN
+                # statistics, gradients, the dp all-reduce, the update): replaying it would apply that twice
+                if nat.runs or not nat.replayable():
                     raise
                 # an operand the native kernels reject at run time: this program keeps the Python replay
                 prog._native_runners[(key, str(dev))] = None

@@ -431,6 +431,16 @@ class NativeTrainRunner:
         self._lowering = lowering  # keeps bound tensors alive
         self.runs = 0
 
+    def replayable(self):
+        """After run() raised: True when the step may be replayed by another executor without applying device
+        state twice — it stopped in the forward (no backward, gradient all-reduce or update ran) and neither a
+        completed instruction nor the failing one writes an input in place (BN running statistics, in-place ATen
+        ops)."""
+        if self.tp.phase != 0:
+            return False
+        upto = min(self.tp.done + 1, len(self._lowering.instrs))
+        return not any(_mutates(ins) for ins in self._lowering.instrs[:upto])
+
     def run(self, env):
         feeds = []
         for s, t in env.items():
@@ -466,6 +476,18 @@ class NativeTrainRunner:
                 _allreduce_mean([p._t.grad for p in self.opt._parameter_list if p._t.grad is not None], pg)
             self.opt.step()
         return outs
+
+
+def _mutates(ins):
+    """Whether a lowered instruction writes device state that outlives the step."""
+    if ins[0] == "native":
+        return ins[1] == "batch_norm_act"
+    name, overload = ins[1], ins[2]
+    try:
+        op = getattr(getattr(torch.ops.aten, name.split("::")[-1]), overload or "default")
+    except AttributeError:
+        return True  # unknown: assume it does
+    return any(a.alias_info is not None and a.alias_info.is_write for a in op._schema.arguments)
 
 
 def compile_training(prog, plan, fetch, dev, native_kernels=True):

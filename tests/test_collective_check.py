@@ -50,7 +50,7 @@ def _diverge_worker(rank, world, port, how, q):
         model = paddle.DataParallel(paddle.nn.Sequential(*lin), comm_buffer_size=1e-6, last_comm_buffer_size=1e-6)
         assert len(model._buckets) == 2
         if rank == 1:
-            model._buckets.reverse()
+            model._order.reverse()
         try:
             model(paddle.ones([2, 8])).sum().backward()
         except cc.CollectiveMismatchError as e:

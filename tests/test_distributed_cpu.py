@@ -449,3 +449,25 @@ def _moe_exchange_worker(rank, world, port, q):
 
 def test_moe_global_scatter_gather_two_ranks():
     _spawn(_moe_exchange_worker)
+
+
+def test_data_parallel_launch_order_interleaves_dtype_groups():
+    """Bucket launch order follows expected gradient readiness (reverse registration of each bucket's earliest
+    parameter) across dtype groups, so an fp32 group's buckets are not held behind the bf16 group's last one."""
+    import paddlepaddle_amd as paddle
+    from paddlepaddle_amd.parallel.data_parallel import DataParallel
+    layers = []
+    for i in range(4):
+        lin = paddle.nn.Linear(8, 8)
+        lin.weight._t.data = lin.weight._t.data.bfloat16()  # bf16 weights, fp32 biases: two dtype groups
+        layers.append(lin)
+    model = paddle.nn.Sequential(*layers)
+    dp = DataParallel(model)  # world 1: no buckets yet
+    dp._world = 2
+    dp._build_buckets(1e-6, 1e-6)  # one parameter per bucket
+    params = [p for p in model.parameters() if not p.stop_gradient]
+    reg = {id(p): i for i, p in enumerate(params)}
+    first = [min(reg[id(p)] for p in dp._buckets[bi].params) for bi in dp._order]
+    assert first == sorted(first, reverse=True)
+    dts = [dp._buckets[bi].params[0]._t.dtype for bi in dp._order]
+    assert dts[:2] == [torch.float32, torch.bfloat16]  # the last layer's bias, then its weight: groups interleave

@@ -194,3 +194,26 @@ def test_native_executor_dp_gradient_hook_gpu(monkeypatch):
         assert seen == [(4, "dp-group")] * 3, seen
     finally:
         paddle.disable_static()
+
+
+def test_native_executor_replay_only_before_side_effects():
+    """A failed native step may be replayed by the Python executor only when it stopped in the forward before any
+    instruction writing persistent state (BN statistics, in-place ops) had run."""
+    assert NT._mutates(("native", "batch_norm_act", [], [], [], []))
+    assert not NT._mutates(("native", "linear", [], [], [], []))
+    assert NT._mutates(("aten", "add_", "Tensor", [], [0]))
+    assert not NT._mutates(("aten", "add", "Tensor", [], [0]))
+
+    class TP:
+        def __init__(self, phase, done):
+            self.phase, self.done = phase, done
+
+    class Low:
+        instrs = [("aten", "mm", "default", [], [0]), ("native", "batch_norm_act", [], [], [], []),
+                  ("aten", "relu", "default", [], [0])]
+
+    r = NT.NativeTrainRunner.__new__(NT.NativeTrainRunner)
+    r._lowering = Low()
+    for phase, done, ok in [(0, 0, True), (0, 1, False), (0, 2, False), (1, 3, False), (3, 3, False)]:
+        r.tp = TP(phase, done)
+        assert r.replayable() is ok, (phase, done)
