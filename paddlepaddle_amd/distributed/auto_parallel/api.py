@@ -407,8 +407,10 @@ class Strategy:
         self.sharding = _Cfg(enable=False, stage=1, degree=8, **c.get("sharding", {}))
         self.fused_passes = _Cfg(enable=False, gemm_epilogue=False, dropout_add=False, **c.get("fused_passes", {}))
         self.gradient_merge = _Cfg(enable=False, k_steps=1, avg=True, **c.get("gradient_merge", {}))
+        # vpp_degree / vpp_seg_method: model chunks per stage and the layer class that segments them (reference
+        # auto_parallel/constants.py:203-204)
         self.pipeline = _Cfg(enable=False, schedule_mode="1F1B", micro_batch_size=1, accumulate_steps=1,
-                             **c.get("pipeline", {}))
+                             vpp_degree=1, vpp_seg_method="", **c.get("pipeline", {}))
         self.amp = _Cfg(enable=False, dtype="float16", level="O1", init_loss_scaling=32768.0, **c.get("amp", {}))
         self.recompute = _Cfg(enable=False, **c.get("recompute", {}))
         self.mp_optimization = _Cfg(allreduce_matmul_grad_overlapping=False)

@@ -132,7 +132,7 @@ def _vp_embedding(ids, weight, gr):
 
 def gr_n(eng, stage, d):
     """Size of mesh dim ``d`` of ``stage``'s mesh."""
-    m = eng.meshes[stage]
+    m = eng._smesh(stage)
     return int(m.shape[d])
 
 
@@ -368,6 +368,10 @@ class StaticEngine:
         pp = strategy.pipeline
         self.acc = max(1, int(pp.accumulate_steps)) if pp.enable else 1
         self.schedule = str(pp.schedule_mode).upper() if pp.enable else "1F1B"
+        # virtual pipeline (reference pir_pass.py:1004 complete_chunk_id + pipeline_vpp.py): the layers of class
+        # ``vpp_seg_method`` split into pp * vpp_degree chunks, chunk i on stage mesh i % pp as model chunk i // pp
+        self.vpp = max(1, int(pp.get("vpp_degree", 1) or 1)) if pp.enable else 1
+        self.vpp_seg = str(pp.get("vpp_seg_method", "") or "") if pp.enable else ""
         self.built = False
         self._cnodes = {}  # id(local node) -> compiled argument builders (_compile_node)
         self.rank = C.get_rank()
@@ -378,7 +382,12 @@ class StaticEngine:
         self.refined = list(strategy.recompute.get("refined_ops_patterns") or []) if self.recompute else []
         if self.schedule not in self._PASS_OF:
             unsupported.append(f"pipeline.schedule_mode {pp.schedule_mode!r} (one of FThenB / 1F1B / Eager1F1B / "
-                               f"ZBH1; virtual pipelines run on fleet PipelineParallelWithInterleave)")
+                               f"ZBH1 / VPP / ZBVPP)")
+        elif self.schedule in ("VPP", "ZBVPP") and (self.vpp < 2 or not self.vpp_seg):
+            unsupported.append(f"pipeline.schedule_mode {self.schedule} without pipeline.vpp_degree >= 2 and "
+                               f"pipeline.vpp_seg_method (the class name of the layers that form the chunks)")
+        elif self.vpp > 1 and self.schedule not in ("VPP", "ZBVPP"):
+            unsupported.append(f"pipeline.vpp_degree {self.vpp} with schedule_mode {self.schedule} (VPP / ZBVPP)")
         # strategy.sp_optimization: Partial -> Shard reshards (a row-parallel output entering a sequence-parallel
         # region) as one reduce-scatter (_ReduceScatter) instead of all-reduce + slice
         self.sp_opt = bool(strategy.sp_optimization.get("enable", False))
@@ -456,6 +465,8 @@ class StaticEngine:
         cp_slots = []
         hooks = (self._checkpoint_hooks(prog, cps, cp_slots) if cps else self._recompute_hooks(prog)) \
             if self.recompute else []
+        if self.vpp > 1:
+            hooks += self._vpp_hooks(prog)
         try:
             with P.trace_into(prog):
                 xs = [_wrap(prog._metas[s]) for s in self.feed_slots[:-1]]
@@ -469,6 +480,8 @@ class StaticEngine:
                 if id(p) in saved:
                     p._t = saved[id(p)]
         self.loss_slot = prog._slot_of[id(loss._t)]
+        if self.vpp > 1:
+            self._vpp_chunks(prog)
         if cps:
             from ..passes import new_pass
             ctx = new_pass("auto_parallel_recompute", {"checkpoints": cp_slots}).apply(prog, None)
@@ -497,6 +510,38 @@ class StaticEngine:
                 self._zero_check_partition()
             self._zero_setup()
         self.built = True
+
+    # ---------------------------------------------------------------- virtual pipeline chunks
+    def _vpp_hooks(self, prog):
+        """Program position of every ``vpp_seg_method`` layer's first op, recorded while tracing."""
+        self._seg_starts = []
+        subs = [l for l in self.layer.sublayers(include_self=True) if type(l).__name__ == self.vpp_seg]
+        if not subs:
+            raise ValueError(f"pipeline.vpp_seg_method {self.vpp_seg!r}: no sublayer of that class")
+
+        def pre(layer, inputs):
+            self._seg_starts.append(len(prog.nodes))
+        return [l.register_forward_pre_hook(pre) for l in subs]
+
+    def _vpp_chunks(self, prog):
+        """Virtual stage of every traced node (``_vs_of``, by node identity: nodes the fusion passes create later
+        inherit it from their predecessor): the seg layers split into pp * vpp equal chunks; ops before the
+        first layer belong to chunk 0, ops after the last to the last chunk."""
+        import bisect
+        npp, starts = len(self.meshes), self._seg_starts
+        nch = npp * self.vpp
+        if len(starts) % nch:
+            raise ValueError(f"VPP: {len(starts)} {self.vpp_seg} layers do not split into pp ({npp}) x vpp_degree "
+                             f"({self.vpp}) chunks")
+        per = len(starts) // nch
+        self._vs_of = {}
+        for j, n in enumerate(prog.nodes):
+            li = min(max(bisect.bisect_right(starts, j) - 1, 0), len(starts) - 1)
+            self._vs_of[id(n)] = li // per
+
+    def _smesh(self, stage):
+        """Mesh of a (virtual) stage."""
+        return self.meshes[stage % len(self.meshes)]
 
     _CONVERSIONS = ("allgather", "slice", "alias", "to_partial", "allreduce", "reduce_scatter", "copy_to_parallel")
 
@@ -839,7 +884,7 @@ class StaticEngine:
     # ---------------------------------------------------------------- propagation + partition
     def _propagate_and_partition(self):
         prog = self.prog
-        nstage = len(self.meshes)
+        nstage = len(self.meshes) * self.vpp  # virtual stages: chunk c of mesh m is stage c * pp + m
         self.stage_nodes = [[] for _ in range(nstage)]
         self.stage_inputs = [set() for _ in range(nstage)]     # slots received from earlier stages
         self.sends = [dict() for _ in range(nstage)]           # slot -> set(dst stages)
@@ -863,6 +908,8 @@ class StaticEngine:
             self.slot_stage[s] = None  # available everywhere
         for s in self.param_slots.values():
             self.slot_stage[s] = self.stage_of_mesh.get(self.info[s].mesh, 0)
+        if self.vpp > 1:
+            self._vpp_param_stages(prog)
         for n in prog.nodes:
             if isinstance(n, P.CFNode):
                 raise NotImplementedError("control flow inside an auto-parallel program")
@@ -872,7 +919,31 @@ class StaticEngine:
         self._next += 1
         return self._next
 
+    def _vpp_param_stages(self, prog):
+        """VPP: a parameter lives in the chunk of its first reader; its annotated mesh must be that chunk's."""
+        vs = None
+        pslots = set(self.param_slots.values())
+        for n in prog.nodes:
+            vs = self._vs_of.get(id(n), vs)
+            if vs is None:
+                vs = 0
+            self._vs_of[id(n)] = vs
+            for r in _flat_tensor_refs((n.args, n.kwargs), []):
+                if r.i in pslots:
+                    pslots.discard(r.i)
+                    if self.info[r.i].mesh != self._smesh(vs):
+                        raise NotImplementedError(
+                            f"VPP: a parameter of chunk {vs // len(self.meshes)} on stage {vs % len(self.meshes)} is "
+                            f"annotated on another mesh; place layer chunk i on pp mesh i % pp")
+                    self.slot_stage[r.i] = vs
+
     def _stage_for(self, node, in_refs):
+        if self.vpp > 1:
+            vs = self._vs_of[id(node)]
+            if node.kind == "reshard" and self.reshard_ann[id(node)][0] != self._smesh(vs):
+                raise NotImplementedError(f"VPP: a reshard inside chunk {vs // len(self.meshes)} targets another "
+                                          f"stage mesh; place layer chunk i on pp mesh i % pp")
+            return vs
         if node.kind == "reshard":
             mesh, _ = self.reshard_ann[id(node)]
             return self.stage_of_mesh.get(mesh, 0)
@@ -937,7 +1008,7 @@ class StaticEngine:
                 cur, pl[d] = out, w
             elif _is_p(w):
                 raise NotImplementedError(f"conversion to a Partial placement ({h} -> {w})")
-        self.info[cur] = _Info(self.meshes[stage], pl, shape)
+        self.info[cur] = _Info(self._smesh(stage), pl, shape)
         al[key] = cur
         return cur
 
@@ -972,7 +1043,7 @@ class StaticEngine:
         stage = self._stage_for(n, refs)
         for r in refs:
             self._avail(r.i, stage)
-        mesh = self.meshes[stage]
+        mesh = self._smesh(stage)
         nd = mesh.ndim
         for r in refs:
             inf = self.info.get(r.i)
@@ -1063,7 +1134,7 @@ class StaticEngine:
 
     def _alias(self, stage, out_slot, src_slot, pl):
         self._emit(stage, "alias", lambda x: x, (P._Ref(src_slot),), out_slot)
-        self.info[out_slot] = _Info(self.meshes[stage], pl, self.info[src_slot].shape)
+        self.info[out_slot] = _Info(self._smesh(stage), pl, self.info[src_slot].shape)
 
     @staticmethod
     def _subst(tmpl, sub):
@@ -1237,7 +1308,7 @@ class StaticEngine:
         div = 1
         for d, p in enumerate(out_pl):
             if _is_s(p) and p[1] == 2:
-                div *= self.meshes[stage].shape[d]
+                div *= self._smesh(stage).shape[d]
         if div == 1:
             return args, dict(n.kwargs)
         H, Hkv, g = self._qkv_attn_args(n)
@@ -1366,7 +1437,8 @@ class StaticEngine:
                 loc = t.to_local() if self.rank in self.info[slot].mesh else torch.empty(0, dtype=t.dtype)
             else:
                 loc = t
-            loc = loc.detach().clone().requires_grad_(not p.stop_gradient and st == self.my_stage)
+            mine = st is not None and st % len(self.meshes) == self.my_stage
+            loc = loc.detach().clone().requires_grad_(not p.stop_gradient and mine)
             p._t = loc
             from ...framework.tensor import _PARAM_OF
             _PARAM_OF[id(loc)] = p
@@ -1603,7 +1675,7 @@ class StaticEngine:
     def _peer(self, dst_stage):
         src_mesh = self.meshes[self.my_stage].mesh
         idx = np.argwhere(src_mesh == self.rank)[0]
-        return int(self.meshes[dst_stage].mesh[tuple(idx)])
+        return int(self._smesh(dst_stage).mesh[tuple(idx)])
 
     def _feeds_local(self, inputs, labels, mb):
         vals = []
@@ -1647,8 +1719,8 @@ class StaticEngine:
                          self._materialize(tmpl.step, env))
         return tmpl
 
-    def _forward_mb(self, mb, inputs, labels, p2p):
-        s = self.my_stage
+    def _forward_mb(self, mb, inputs, labels, p2p, s=None):
+        s = self.my_stage if s is None else s
         env = {}
         for slot, p in self.local_params.items():
             env[slot] = p._t
@@ -1701,7 +1773,8 @@ class StaticEngine:
                 g = t.grad if t.grad is not None else torch.zeros_like(t)
                 p2p.send(g, self._peer(self.slot_stage[slot]), ("B", slot, mb))
 
-    _PASS_OF = {"FTHENB": "FThenB", "1F1B": "1F1B", "EAGER1F1B": "Eager1F1B", "ZBH1": "ZBH1"}
+    _PASS_OF = {"FTHENB": "FThenB", "1F1B": "1F1B", "EAGER1F1B": "Eager1F1B", "ZBH1": "ZBH1", "VPP": "VPP",
+                "ZBVPP": "ZBVPP"}
 
     def _job_list(self, mode, nst, s, n):
         """The stage's job list from the registered pipeline_scheduler_<mode> pass (cached per configuration)."""
@@ -1712,10 +1785,46 @@ class StaticEngine:
             name = self._PASS_OF.get(mode)
             if name is None:
                 raise ValueError(f"static auto-parallel engine: unsupported pipeline schedule_mode {mode!r}")
-            ctx = new_pass(f"pipeline_scheduler_{name}", {"num_micro_batches": n, "pp_stage": s,
-                                                          "pp_degree": nst}).apply(self.prog, None)
-            self._jobs, self._jobs_key = job_pairs(ctx.get_attr("pipeline_scheduler.job_list")), key
+            ctx = new_pass(f"pipeline_scheduler_{name}", {"num_micro_batches": n, "pp_stage": s, "pp_degree": nst,
+                                                          "vpp_degree": self.vpp}).apply(self.prog, None)
+            jobs = ctx.get_attr("pipeline_scheduler.job_list")
+            # (kind, micro-batch) — plus the model chunk for the virtual schedules
+            self._jobs = [(k, mb, j.chunk_id()) for (k, mb), j in zip(job_pairs(jobs), jobs)] if self.vpp > 1 \
+                else job_pairs(jobs)
+            self._jobs_key = key
         return self._jobs
+
+    def _vpp_forward(self, inputs, labels, p2p, states, losses):
+        def fwd(mb, vs):
+            st = self._forward_mb(mb, inputs, labels, p2p, vs)
+            if st[2] is not None:
+                losses.append(st[2].detach().float().reshape(()))
+            states[(vs, mb)] = st
+        return fwd
+
+    def _vpp_run(self, nst, s, n, fwd, states, p2p):
+        """The interleaved (VPP) or zero-bubble interleaved (ZBVPP) job list of this stage: job (kind, mb, chunk)
+        runs virtual stage chunk * pp + stage; ZBVPP's W jobs apply the dW GEMMs its B job recorded."""
+        from ...ops import linear as LIN
+        zb = self.schedule == "ZBVPP"
+        wq = {}
+        for kind, mb, c in self._job_list(self.schedule, nst, s, n):
+            vs = c * nst + s
+            if kind == "F":
+                if zb:
+                    with LIN.zero_bubble_forward():
+                        fwd(mb, vs)
+                else:
+                    fwd(mb, vs)
+            elif kind == "B" and zb:
+                q = wq[(c, mb)] = []
+                with LIN.defer_weight_grads(q):
+                    self._backward_mb(mb, states.pop((vs, mb)), p2p)
+            elif kind == "B":
+                self._backward_mb(mb, states.pop((vs, mb)), p2p)
+            else:
+                p2p.flush()
+                LIN.apply_weight_grads(wq.pop((c, mb)))
 
     def step(self, inputs, labels):
         if not self.built:
@@ -1723,7 +1832,9 @@ class StaticEngine:
         from ...framework.place import _get_torch_device
         self.dev = _get_torch_device()
         if getattr(self, "_p2p", None) is None:
-            self._p2p = _P2P(self.dev)  # built once on every rank (its host twin is a collective group creation)
+            # built once on every rank (its host twin is a collective group creation); the interleaved schedules
+            # consume a ring channel's chunks out of production order: tagged messages + stash
+            self._p2p = _P2P(self.dev, ordered=self.vpp == 1)
         p2p = self._p2p
         p2p.begin_run()
         self._fuse_grads()
@@ -1742,7 +1853,9 @@ class StaticEngine:
         # of them (what stage 0 of a deeper 1F1B pipeline holds: the 70B stage proxy asks for it explicitly)
         mode = self.schedule if self.schedule in ("ZBH1", "FTHENB", "EAGER1F1B") or nst > 1 else "1F1B"
         wq = {}
-        for kind, mb in self._job_list(mode, nst, s, n):  # this stage's jobs from the pipeline_scheduler pass
+        if self.vpp > 1:
+            self._vpp_run(nst, s, n, self._vpp_forward(inputs, labels, p2p, states, losses), states, p2p)
+        for kind, mb in (self._job_list(mode, nst, s, n) if self.vpp == 1 else ()):  # this stage's jobs from the pipeline_scheduler pass
             if kind == "F":
                 if mode == "ZBH1":
                     with LIN.zero_bubble_forward():
@@ -1783,7 +1896,7 @@ class _P2P:
     meta on a gloo twin of the world, meta once per (channel, shape), payloads on RCCL), kept across steps so
     the meta cache persists. Keys are ("F" | "B", slot, micro-batch)."""
 
-    def __init__(self, dev):
+    def __init__(self, dev, ordered=True):
         from ...parallel.p2p import P2P, host_twin, payload_twin
         ws = dist.get_world_size() if dist.is_initialized() else 1
         host = host_twin([list(range(ws))], dist.get_rank()) if ws > 1 else None
@@ -1791,7 +1904,7 @@ class _P2P:
         # ordered: every stage walks its 1F1B / FThenB / ZBH1 job list and its slots in sorted order, so each
         # directed channel is consumed in production order (no per-message header, parallel/p2p.py); payloads to a
         # lower rank on the world's twin group, batched per job with the queued sends (pp_comm.py)
-        self.ep = P2P(dev, None, host, ordered=True, down_group=down)
+        self.ep = P2P(dev, None, host, ordered=ordered, down_group=down)
 
     @staticmethod
     def _tag(key):

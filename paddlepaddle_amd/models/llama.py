@@ -51,6 +51,7 @@ class LlamaConfig:
     tensor_parallel_degree: int = 1
     sequence_parallel: bool = False  # with TP: activations between the TP regions split over tokens (Megatron SP)
     sep_parallel_degree: int = 1  # segment parallelism: each rank of hcg's sep group holds S / sep tokens
+    virtual_pp_degree: int = 1  # auto-parallel VPP: layer chunk c of pp * vpp goes to pp mesh c % pp (llama_auto)
     pad_token_id: int = 0
     bos_token_id: int = 1
     eos_token_id: int = 2

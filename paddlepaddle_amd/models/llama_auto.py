@@ -188,12 +188,16 @@ class LlamaForCausalLMAuto(nn.Layer):
         self.config = cfg
         pp = num_stages()
         L = cfg.num_hidden_layers
-        per = max(L // pp, 1)
+        # with virtual_pp_degree v the layers form pp * v chunks, chunk c on pp mesh c % pp (the interleaved layout
+        # the static engine's VPP schedule runs: strategy.pipeline.vpp_degree = v, vpp_seg_method =
+        # "LlamaDecoderLayerAuto"); v = 1 is the contiguous layout
+        nch = pp * max(1, int(getattr(cfg, "virtual_pp_degree", 1) or 1))
+        per = max(L // nch, 1)
         first, last = stage_mesh(0), stage_mesh(pp - 1)
         self.embed_tokens = nn.Embedding(cfg.vocab_size, cfg.hidden_size,
                                          weight_attr=nn.ParamAttr(initializer=I.Normal(0.0, cfg.initializer_range)))
         _shard(self.embed_tokens.weight, first)
-        self.layers = nn.LayerList([LlamaDecoderLayerAuto(cfg, min(i // per, pp - 1), i % per == 0 and i > 0)
+        self.layers = nn.LayerList([LlamaDecoderLayerAuto(cfg, min(i // per, nch - 1) % pp, i % per == 0 and i > 0)
                                     for i in range(L)])
         self.norm = LlamaRMSNormAuto(cfg, last)
         self.lm_head = _linear(cfg.hidden_size, cfg.vocab_size, cfg)

@@ -20,15 +20,16 @@ def _data():
 
 
 _FUSED = {}
+_EXTRA = {}  # other LlamaConfig overrides (virtual_pp_degree)
 
 
 def _cfg():
     from paddlepaddle_amd.models.llama_auto import LlamaConfig
-    return LlamaConfig.tiny(num_hidden_layers=4, num_attention_heads=4, num_key_value_heads=2, **_FUSED)
+    return LlamaConfig.tiny(num_hidden_layers=4, num_attention_heads=4, num_key_value_heads=2, **_FUSED, **_EXTRA)
 
 
 def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap=False, zero=False, checkpoints=None,
-            gm=1, refined=None):
+            gm=1, refined=None, vpp=1):
     paddle = _setup(rank, world, port)
     import paddlepaddle_amd.distributed as dist
     from paddlepaddle_amd.models.llama_auto import LlamaForCausalLMAuto, LlamaPretrainingCriterionAuto
@@ -43,6 +44,9 @@ def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap
     strategy.pipeline.enable = pp > 1 or acc > 1
     strategy.pipeline.accumulate_steps = acc
     strategy.pipeline.schedule_mode = schedule
+    if vpp > 1:
+        strategy.pipeline.vpp_degree = vpp
+        strategy.pipeline.vpp_seg_method = "LlamaDecoderLayerAuto"
     strategy.recompute.enable = recompute
     if checkpoints:
         strategy.recompute["checkpoints"] = checkpoints
@@ -77,7 +81,13 @@ def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap
         ep = eng._p2p.ep
         assert ep.meta_exchanges == len(ep.sent_meta) and ep.messages == STEPS * acc * len(ep.sent_meta), (
             ep.meta_exchanges, len(ep.sent_meta), ep.messages)
-        assert ep.ordered and ep.headers == STEPS * len(ep.sent_meta), ep.headers  # one header per class per run
+        if vpp == 1:
+            assert ep.ordered and ep.headers == STEPS * len(ep.sent_meta), ep.headers  # one header per class per run
+        else:  # chunks of a ring channel interleave: tagged messages
+            assert not ep.ordered
+            # every virtual stage holds one layer chunk; this rank runs vpp of them
+            mine = [vs for vs in range(len(eng.stage_nodes)) if vs % pp == eng.my_stage]
+            assert len(mine) == vpp and all(eng.stage_nodes[vs] for vs in mine)
     if zero:  # optimizer state exists for this rank's shards only
         shards = eng.opt._parameter_list
         assert shards and all(sp.name.startswith("zero_shard") for sp in shards)
@@ -102,6 +112,11 @@ def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap
         assert all(len(sg.outputs) == 1 for sg in segs), [sg.outputs for sg in segs]
     q.put((rank, losses, kinds, eng.my_stage))
     paddle.distributed.barrier()
+
+
+def _worker_vpp(rank, world, port, shape, acc, schedule, q):
+    _EXTRA["virtual_pp_degree"] = 2
+    _worker(rank, world, port, shape, acc, schedule, q, vpp=2)
 
 
 def _worker_rc(rank, world, port, shape, acc, schedule, q):
@@ -311,6 +326,22 @@ def test_parallelize_plan_llama_matches_single_process(shape, acc):
         assert "allreduce" in kinds and "copy_to_parallel" in kinds
         stages.add(stage)
     assert stages == set(range(shape[0]))
+
+
+@pytest.mark.parametrize("shape,acc,schedule", [((2, 1, 1), 4, "VPP"), ((2, 1, 2), 4, "VPP"), ((2, 1, 1), 2, "ZBVPP")])
+def test_static_engine_vpp_matches_single_process(shape, acc, schedule):
+    """strategy.pipeline vpp_degree 2 + vpp_seg_method: the decoder layers form pp x 2 chunks (chunk c on pp mesh
+    c % pp, LlamaConfig.virtual_pp_degree), each rank runs two model chunks through the interleaved (VPP) or
+    zero-bubble interleaved (ZBVPP) job list of the pipeline_scheduler pass; losses equal single-process
+    training (reference passes/pipeline_scheduler_pass/pipeline_vpp.py, pipeline_zero_bubble.py ZBVPP)."""
+    _EXTRA["virtual_pp_degree"] = 2
+    try:
+        ref = _reference()
+    finally:
+        _EXTRA.clear()
+    res = _spawn(_worker_vpp, shape, acc, schedule, world=int(np.prod(shape)))
+    for rank, losses, kinds, stage in res:
+        np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-5, err_msg=f"rank {rank} stage {stage}")
 
 
 def test_static_engine_rejects_unimplemented_strategy_fields():

@@ -36,7 +36,8 @@ def _check(B, Sq, Sk, H, Hk, D, causal=False, mask=None, startend=None, dt=torch
     for name, a, b in (("dq", q.grad, qr.grad), ("dk", k.grad, kr.grad), ("dv", v.grad, vr.grad)):
         e = (a.float() - b).abs().max().item() / (b.abs().max().item() + 1e-6)
         assert e < 3e-2, f"{name} rel err {e}"
-    assert L.calls("pa_flash_attn_fwd_ex") > 0 and L.calls("pa_flash_attn_bwd_ex") > 0
+    assert L.calls("pa_flash_attn_fwd_ex") > 0
+    assert L.calls("pa_flash_attn_bwd_ex") + L.calls("pa_flash_attn_bwd_ds") > 0  # the dS route takes the plain cases
     assert L.calls("attn_aten_fallback") == 0
 
 

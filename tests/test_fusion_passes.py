@@ -8,13 +8,14 @@ import numpy as np
 import pytest
 import torch
 
-os.environ["PADDLE_AMD_FORCE_CPU"] = "1"
 import paddlepaddle_amd as paddle  # noqa: E402
 from paddlepaddle_amd.distributed.passes import new_pass  # noqa: E402
 
 
 @pytest.fixture(autouse=True)
-def _static():
+def _static(monkeypatch):
+    # set per test, not at import: a module-level setting leaks into every process a later GPU test starts
+    monkeypatch.setenv("PADDLE_AMD_FORCE_CPU", "1")
     paddle.enable_static()
     yield
     paddle.disable_static()

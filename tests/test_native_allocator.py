@@ -108,6 +108,7 @@ print("JSON" + json.dumps(s))
 @pytest.mark.gpu
 def test_native_allocator_drives_training_gpu():
     env = dict(os.environ, PADDLE_AMD_ALLOCATOR="auto_growth", REPO=ROOT)
+    env.pop("PADDLE_AMD_FORCE_CPU", None)  # a CPU-parity test earlier in the same process may have set it
     r = subprocess.run([sys.executable, "-c", _CHILD], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     s = json.loads(r.stdout.split("JSON", 1)[1])
