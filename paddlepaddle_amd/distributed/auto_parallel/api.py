@@ -457,6 +457,8 @@ class DistModel:
         self.network.eval()
 
     def __call__(self, *args):
+        if self._engine is not None and self._mode != "train":
+            self._engine.gather_params()  # ZeRO-3 keeps only shards between steps
         if self._mode == "predict":
             from ...framework.grad_mode import no_grad
             with no_grad():
@@ -483,12 +485,16 @@ class DistModel:
         return loss
 
     def state_dict(self, mode="all"):
+        if self._engine is not None:
+            self._engine.gather_params()
         sd = dict(self.network.state_dict())
         if mode in ("all", "opt") and self._opt is not None:
             sd.update({f"opt.{k}": v for k, v in self._opt.state_dict().items()})
         return sd
 
     def set_state_dict(self, sd):
+        if self._engine is not None:
+            self._engine.gather_params()  # written into the gathered buffers; the next step re-shards them
         self.network.set_state_dict({k: v for k, v in sd.items() if not k.startswith("opt.")})
 
     def parameters(self):

@@ -344,9 +344,11 @@ class StaticEngine:
         # a dist.shard_optimizer wrapper: the engine updates its local parameter shards with the inner optimizer;
         # ZeRO partitioning of that state over a data-parallel mesh dim is not implemented here, so it must not be
         # requested silently (degree 1 is the plain update)
-        # ZeRO over a data-parallel mesh dim (dist.shard_optimizer ShardingStage1/2, or strategy.sharding):
+        # ZeRO over a data-parallel mesh dim (dist.shard_optimizer ShardingStage1/2/3, or strategy.sharding):
         # gradients reduce-scattered, the optimizer updating only this rank's shard, parameters all-gathered
-        # (_zero_setup / _zero_step). Stage 3 (parameters sharded between steps) is not implemented here.
+        # (_zero_setup / _zero_step). Stage 3 keeps only the shard between steps: the parameters are all-gathered
+        # when a step starts and released after its update (_zero3_gather / _zero3_release; reference
+        # passes/auto_parallel_sharding.py:741 stage 3).
         shard_fn = getattr(optimizer, "_shard_fn", None)
         inner = getattr(optimizer, "_inner_opt", optimizer)
         self.zero_dim, self.zero_stage = None, 1
@@ -354,15 +356,10 @@ class StaticEngine:
             m, d = shard_fn._mesh, shard_fn._dim
             size = m.get_dim_size(m.dim_names[d]) if isinstance(d, int) else m.get_dim_size(d)
             if size > 1:
-                if type(shard_fn).__name__ == "ShardingStage3":
-                    raise NotImplementedError("static auto-parallel engine: ShardingStage3 (parameter sharding); "
-                                              "use ShardingStage1 / ShardingStage2 or the dygraph DistModel path")
                 self.zero_dim = m.dim_names[d] if isinstance(d, int) else d
-                self.zero_stage = 2 if type(shard_fn).__name__ == "ShardingStage2" else 1
+                self.zero_stage = {"ShardingStage2": 2, "ShardingStage3": 3}.get(type(shard_fn).__name__, 1)
         elif strategy.sharding.get("enable", False) and int(strategy.sharding.get("degree", 1)) > 1:
-            if int(strategy.sharding.get("stage", 1)) >= 3:
-                raise NotImplementedError("static auto-parallel engine: strategy.sharding stage 3")
-            self.zero_dim, self.zero_stage = "dp", int(strategy.sharding.get("stage", 1))
+            self.zero_dim, self.zero_stage = "dp", min(3, int(strategy.sharding.get("stage", 1)))
         optimizer = inner
         self.layer, self.loss_fn, self.opt, self.strategy = layer, loss_fn, optimizer, strategy
         pp = strategy.pipeline
@@ -1493,10 +1490,14 @@ class StaticEngine:
                 p._t = v
                 v.grad = gflat[o:o + k].view(t.shape)
                 o += k
-            z = {"flat": flat, "gflat": gflat, "C": C, "pl": pl, "shard": None}
+            z = {"flat": flat, "gflat": gflat, "C": C, "pl": pl, "shard": None, "D": D, "r": r, "dt": dt, "dev": dev,
+                 "items": [(p, tuple(p._t.shape)) for _, p in items]}
             if shard:
-                sp = Parameter(flat[r * C:(r + 1) * C], name=f"zero_shard_{len(self._zero)}")
-                sp._t = flat[r * C:(r + 1) * C]  # a view into the flat buffer: the update lands in the parameters
+                # stages 1/2: a view into the flat buffer (the update lands in the parameters); stage 3: the shard is
+                # its own storage, the only copy of the parameters kept between steps
+                sb = flat[r * C:(r + 1) * C] if self.zero_stage < 3 else flat[r * C:(r + 1) * C].clone()
+                sp = Parameter(sb, name=f"zero_shard_{len(self._zero)}")
+                sp._t = sb
                 sp._t.requires_grad_(True)
                 z["shard"] = sp
                 z["sgrad"] = torch.empty(C, dtype=dt, device=dev)
@@ -1509,6 +1510,60 @@ class StaticEngine:
         from ..passes import new_pass
         new_pass("auto_parallel_grad_clip", {"optimizer": opt, "sq_norm_fn": self._zero_param_sq}).apply(
             self.prog, None)
+        if self.zero_stage == 3:
+            self._zero3_release()
+
+    # ------------------------------------------------------------------ ZeRO stage 3: parameters sharded between steps
+    def _zero3_views(self, z, grads):
+        """Every local parameter of group ``z`` as a leaf view of the gathered flat buffer (and its .grad a view of
+        the flat gradient when ``grads``)."""
+        from ...framework.tensor import _PARAM_OF
+        o = 0
+        for p, shape in z["items"]:
+            k = int(np.prod(shape)) if shape else 1
+            v = z["flat"][o:o + k].view(shape).requires_grad_(True)
+            _PARAM_OF.pop(id(p._t), None)
+            _PARAM_OF[id(v)] = p
+            p._t = v
+            if grads:
+                v.grad = z["gflat"][o:o + k].view(shape)
+            o += k
+
+    def _zero3_gather(self, grads=True):
+        """All-gather the parameter shards into full flat buffers (one all-gather per group). A buffer that is
+        already gathered (gather_params for eval / state_dict) holds the current values — its own slice goes back
+        into the shard first, so writes through the full parameters (set_state_dict) are kept."""
+        with torch.no_grad():
+            for z in self._zero:
+                sh = z["shard"]._t
+                if z["flat"] is not None:
+                    sh.copy_(z["flat"][z["r"] * z["C"]:(z["r"] + 1) * z["C"]])
+                else:
+                    z["flat"] = torch.empty(z["C"] * z["D"], dtype=z["dt"], device=z["dev"])
+                    if self._zero_pg is not None:
+                        dist.all_gather_into_tensor(z["flat"], sh.detach(), group=self._zero_pg)
+                    else:
+                        z["flat"].copy_(sh)
+                if grads and z["gflat"] is None:
+                    z["gflat"] = torch.zeros(z["C"] * z["D"], dtype=z["dt"], device=z["dev"])
+                self._zero3_views(z, grads)
+        self.zero3_gathers = getattr(self, "zero3_gathers", 0) + 1
+
+    def _zero3_release(self):
+        """Drop the full parameter and gradient buffers: only the shards (and the optimizer state of the shards)
+        stay resident until the next step gathers again."""
+        from ...framework.tensor import _PARAM_OF
+        for z in self._zero:
+            z["flat"] = z["gflat"] = None
+            for p, _shape in z["items"]:
+                _PARAM_OF.pop(id(p._t), None)
+                p._t = torch.empty(0, dtype=z["dt"], device=z["dev"])
+
+    def gather_params(self):
+        """Full local parameters outside a training step (eval / predict / state_dict under ZeRO stage 3)."""
+        if self.built and self.zero_stage == 3 and getattr(self, "_zero", None) and self._zero_shard and \
+                any(z["flat"] is None for z in self._zero):
+            self._zero3_gather(grads=False)
 
     def _zero_check_partition(self):
         """ZeRO reduce-scatters the parameters' local dp gradients itself: no data-parallel all-reduce of a
@@ -1623,6 +1678,11 @@ class StaticEngine:
                 z["sgrad"].copy_(z["gflat"])
             z["shard"]._t.grad = z["sgrad"]
         self.opt.step()
+        if self.zero_stage == 3:
+            for z in self._zero:
+                z["shard"]._t.grad = None
+            self._zero3_release()
+            return
         with torch.no_grad():
             for z in self._zero:
                 if self._zero_pg is not None:
@@ -1837,6 +1897,9 @@ class StaticEngine:
             self._p2p = _P2P(self.dev, ordered=self.vpp == 1)
         p2p = self._p2p
         p2p.begin_run()
+        if self.zero_stage == 3 and self._zero_shard and getattr(self, "_zero", None) and \
+                any(z["gflat"] is None for z in self._zero):
+            self._zero3_gather()  # ZeRO-3: full parameters for this step (released again after the update)
         self._fuse_grads()
         nst = len(self.meshes)
         s = self.my_stage

@@ -479,15 +479,16 @@ class AllreduceMatmulGradOverlappingPass(PassBase):
 @register_pass("auto_parallel_sharding")
 class ShardingPass(PassBase):
     """Reference: distributed/passes/auto_parallel_sharding.py — optimizer-state sharding over a data-parallel
-    mesh dim. ``stage`` 1 / 2 (3 is not implemented on the static engine) and ``sharding_mesh_dim`` (default "dp")
-    are recorded on the program; the engine flattens the parameters per placement group, reduce-scatters the
-    accumulated gradients once per step, updates this rank's shards and all-gathers (static_engine._zero_*)."""
+    mesh dim. ``stage`` 1 / 2 / 3 and ``sharding_mesh_dim`` (default "dp") are recorded on the program; the engine
+    flattens the parameters per placement group, reduce-scatters the accumulated gradients once per step, updates
+    this rank's shards and all-gathers them (static_engine._zero_*); at stage 3 only the shards stay resident
+    between steps (gathered when a step starts, released after its update)."""
 
     def _type(self):
         return PassType.PARALLEL_OPT
 
     def _check_self(self):
-        return int(self.get_attr("stage", 1)) in (1, 2)
+        return int(self.get_attr("stage", 1)) in (1, 2, 3)
 
     def _apply_single_impl(self, prog, startup, context):
         prog._pa_sharding = {"stage": int(self.get_attr("stage", 1)),

@@ -59,7 +59,7 @@ def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap
     if zero:
         strategy.sharding["enable"] = True
         strategy.sharding["degree"] = dp
-        strategy.sharding["stage"] = 1
+        strategy.sharding["stage"] = int(zero)
     dm = dist.to_static(model, None, crit, opt, strategy)
     assert dm._engine is not None
     ids = _data()
@@ -91,6 +91,12 @@ def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap
     if zero:  # optimizer state exists for this rank's shards only
         shards = eng.opt._parameter_list
         assert shards and all(sp.name.startswith("zero_shard") for sp in shards)
+        if int(zero) == 3:
+            # between steps only the shards are resident; state_dict gathers the full local parameters
+            held = [p for z in eng._zero for p, _ in z["items"]]
+            assert held and all(p._t.numel() == 0 for p in held) and eng.zero3_gathers == STEPS
+            dm.state_dict(mode="param")
+            assert all(p._t.numel() > 0 for p in held)
         assert sum(sp._t.numel() for sp in shards) * dp >= sum(p._t.numel() for p in eng.local_params.values()
                                                                  if p._t.requires_grad)
     if overlap:  # the column-parallel linears' dX all-reduces became overlapped hooks (2 per layer)
@@ -137,6 +143,21 @@ def _worker_refined(rank, world, port, shape, acc, schedule, q):
 
 def _worker_zero(rank, world, port, shape, acc, schedule, q):
     _worker(rank, world, port, shape, acc, schedule, q, zero=True)
+
+
+def _worker_zero3(rank, world, port, shape, acc, schedule, q):
+    _worker(rank, world, port, shape, acc, schedule, q, zero=3)
+
+
+@pytest.mark.parametrize("shape,acc", [((1, 2, 1), 2), ((2, 2, 1), 2), ((1, 2, 2), 1)])
+def test_static_engine_zero3_matches_single_process(shape, acc):
+    """strategy.sharding stage 3 (reference passes/auto_parallel_sharding.py:741): parameters sharded between
+    steps — all-gathered when a step starts, gradients reduce-scattered, the shard updated, the full buffers
+    released — same losses as single-process training."""
+    ref = _reference()
+    res = _spawn(_worker_zero3, shape, acc, "1F1B", world=int(np.prod(shape)))
+    for rank, losses, kinds, stage in res:
+        np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-5, err_msg=f"rank {rank} stage {stage}")
 
 
 @pytest.mark.parametrize("shape,acc", [((1, 2, 1), 2), ((1, 2, 2), 1), ((2, 2, 1), 2)])
