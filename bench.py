@@ -37,8 +37,11 @@ def parse():
                    help="gpt3-13b | gpt3-6.7b | gpt3-1.3b | tiny | llama2-70b | llama2-13b | llama2-7b | llama-tiny")
     p.add_argument("--pp", type=int, default=1, help="pipeline degree (LLaMA pipeline path)")
     p.add_argument("--vpp", type=int, default=1, help="virtual pipeline stages per rank (interleaved 1F1B)")
-    p.add_argument("--micro-batch", type=int, default=2)
-    p.add_argument("--accum", type=int, default=8, help="gradient accumulation steps per optimizer step")
+    # global batch 16 sequences per GPU either way; GPT-3 13B defaults to 4 x 4 (M = 8192 tokens per GEMM: 2.5
+    # rounds of 256x256 tiles on the N = 5120 shapes instead of 1.25, half the gradient-accumulation epilogues;
+    # 243 GiB of the 288: 2.3-2.5 % over 2 x 8 on one box, profiles/gpt13b_microbatch_ab_r6.md); the other models 2 x 8
+    p.add_argument("--micro-batch", type=int, default=None)
+    p.add_argument("--accum", type=int, default=None, help="gradient accumulation steps per optimizer step")
     p.add_argument("--seq-len", type=int, default=2048)
     p.add_argument("--recompute", type=int, default=0)
     p.add_argument("--sharding-stage", type=int, default=3)
@@ -77,7 +80,11 @@ def parse():
     p.add_argument("--skip-gpt", type=int, default=0)
     p.add_argument("--allocator", default="native", choices=["native", "torch"],
                    help="device allocator: the framework's auto-growth best-fit allocator or PyTorch's")
-    return p.parse_args()
+    a = p.parse_args()
+    mb, acc = (4, 4) if a.model == "gpt3-13b" else (2, 8)
+    a.micro_batch = mb if a.micro_batch is None else a.micro_batch
+    a.accum = acc if a.accum is None else a.accum
+    return a
 
 
 def log(*a):
