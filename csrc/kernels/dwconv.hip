@@ -10,6 +10,9 @@
 //   wgrad    dw[kh,kw,c]   = sum_{n,oh,ow} dy[n,oh,ow,c] * x[n, oh*s-p+kh*d, ow*s-p+kw*d, c]
 //            -> per-lane fp32 partials [nparts, KT, C] over pixel stripes (up to 9 taps per pass), folded by
 //               pa_reduce_parts (norm.hip) on the host side.
+// Pre-activation ReLU (reference fuse_relu_depthwise_conv_pass / depthwise_conv2d fuse_relu_before_depthwise_conv,
+// shape[14] = 1): the convolution reads relu(x) — forward and weight gradient clamp x on load, the data gradient
+// is masked by x > 0 — so the ReLU output is never written or re-read.
 #include "common.h"
 
 using namespace pa;
@@ -17,7 +20,7 @@ using namespace pa;
 namespace {
 
 struct DwArgs {
-  int N, H, W, C, Ho, Wo, KH, KW, sh, sw, ph, pw, dh, dw;
+  int N, H, W, C, Ho, Wo, KH, KW, sh, sw, ph, pw, dh, dw, relu;
 };
 
 template <typename T>
@@ -47,6 +50,9 @@ __global__ __launch_bounds__(256) void dw_fwd_k(const T* __restrict__ x, const T
         float xv[8], wv[8];
         load8<T>(xrow + (int64_t)iw * a.C, xv);
         load8<T>(wt + (int64_t)(kh * a.KW + kw) * a.C + c0, wv);
+        if (a.relu)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) xv[j] = fmaxf(xv[j], 0.f);
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] = fmaf(xv[j], wv[j], acc[j]);
       }
@@ -57,7 +63,7 @@ __global__ __launch_bounds__(256) void dw_fwd_k(const T* __restrict__ x, const T
 
 template <typename T>
 __global__ __launch_bounds__(256) void dw_dgrad_k(const T* __restrict__ dy, const T* __restrict__ wt,
-                                                  T* __restrict__ dx, DwArgs a) {
+                                                  const T* __restrict__ x, T* __restrict__ dx, DwArgs a) {
   const int cg = a.C / 8;
   const int64_t total = (int64_t)a.N * a.H * a.W * cg;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
@@ -88,7 +94,14 @@ __global__ __launch_bounds__(256) void dw_dgrad_k(const T* __restrict__ dy, cons
         for (int j = 0; j < 8; ++j) acc[j] = fmaf(gv[j], wv[j], acc[j]);
       }
     }
-    store8<T>(dx + (((int64_t)n * a.H + ih) * a.W + iw) * a.C + c0, acc);
+    const int64_t o = (((int64_t)n * a.H + ih) * a.W + iw) * a.C + c0;
+    if (a.relu) {  // d relu(x) / dx: the gradient passes where x > 0
+      float xv[8];
+      load8<T>(x + o, xv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = xv[j] > 0.f ? acc[j] : 0.f;
+    }
+    store8<T>(dx + o, acc);
   }
 }
 
@@ -132,6 +145,9 @@ __global__ __launch_bounds__(256) void dw_wgrad_k(const T* __restrict__ x, const
       if (t < KT && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) {
         float xv[8];
         load8<T>(x + (((int64_t)n * a.H + ih) * a.W + iw) * a.C + c0, xv);
+        if (a.relu)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) xv[j] = fmaxf(xv[j], 0.f);
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[t][j] = fmaf(gv[j], xv[j], acc[t][j]);
       }
@@ -159,12 +175,13 @@ DwArgs make_args(const int* s) {
   DwArgs a;
   a.N = s[0]; a.H = s[1]; a.W = s[2]; a.C = s[3]; a.Ho = s[4]; a.Wo = s[5]; a.KH = s[6]; a.KW = s[7];
   a.sh = s[8]; a.sw = s[9]; a.ph = s[10]; a.pw = s[11]; a.dh = s[12]; a.dw = s[13];
+  a.relu = s[14];
   return a;
 }
 
 }  // namespace
 
-// shape: int32[14] = N, H, W, C, Ho, Wo, KH, KW, sh, sw, ph, pw, dh, dw; wt: filter as [KH*KW, C]
+// shape: int32[15] = N, H, W, C, Ho, Wo, KH, KW, sh, sw, ph, pw, dh, dw, pre-ReLU; wt: filter as [KH*KW, C]
 PA_EXPORT int pa_dwconv_fwd(const void* x, const void* wt, const void* bias, void* y, const int* shape, int dtype,
                             hipStream_t st) {
   const DwArgs a = make_args(shape);
@@ -176,12 +193,15 @@ PA_EXPORT int pa_dwconv_fwd(const void* x, const void* wt, const void* bias, voi
   return 0;
 }
 
-PA_EXPORT int pa_dwconv_dgrad(const void* dy, const void* wt, void* dx, const int* shape, int dtype, hipStream_t st) {
+// x: the forward input (read only with the pre-ReLU flag, for the mask; may be null otherwise)
+PA_EXPORT int pa_dwconv_dgrad(const void* dy, const void* wt, const void* x, void* dx, const int* shape, int dtype,
+                              hipStream_t st) {
   const DwArgs a = make_args(shape);
   if (a.C % 8) return 3;
+  if (a.relu && x == nullptr) return 4;
   const unsigned g = grid_for((int64_t)a.N * a.H * a.W * (a.C / 8));
   PA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL((dw_dgrad_k<T>), dim3(g), dim3(256), 0, st, (const T*)dy,
-                                                 (const T*)wt, (T*)dx, a));
+                                                 (const T*)wt, (const T*)x, (T*)dx, a));
   PA_CHECK_LAUNCH();
   return 0;
 }

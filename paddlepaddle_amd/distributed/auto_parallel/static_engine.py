@@ -854,6 +854,9 @@ class StaticEngine:
         if self.zero_dim is not None:
             new_pass("auto_parallel_sharding", {"stage": self.zero_stage, "sharding_mesh_dim": self.zero_dim}).apply(
                 self.prog, None)
+        if self.sp_opt:  # strategy.sp_optimization: Partial -> Shard conversions as one reduce-scatter
+            new_pass("auto_parallel_sequence_parallel_optimization").apply(self.prog, None)
+        self.sp_opt = bool(getattr(self.prog, "_pa_sp_opt", False))
         amp = self.strategy.amp
         if amp.get("enable", False):
             ctx = new_pass("auto_parallel_amp", {"dtype": amp.get("dtype", "bfloat16")}).apply(self.prog, None)

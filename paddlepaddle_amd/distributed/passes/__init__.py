@@ -6,5 +6,6 @@ from .program_passes import (  # noqa: F401
 )
 from . import pipeline_scheduler  # noqa: F401  (pipeline_scheduler_* passes)
 from . import fusion_passes  # noqa: F401  (fused_feedforward / fused_attention / ... and auto-parallel passes)
+from . import conv_passes  # noqa: F401  (fuse_relu_depthwise_conv / fuse_resunit)
 
 __all__ = ["new_pass", "PassManager", "PassContext"]

@@ -323,3 +323,54 @@ class QuantizationPass(PassBase):
         cfg = {k: self.get_attr(k) for k in keys if self.get_attr(k) is not None}
         quant_aware(prog, config=cfg)
         context.set_attr("auto_parallel_quantization.quantized", len(getattr(prog, "_quant_nodes", [])))
+
+
+# ------------------------------------------------------------------------------------------------------------------
+from .program_passes import GradientMergePass  # noqa: E402
+
+
+@register_pass("auto_parallel_gradient_merge_pass")
+class GradientMergeAliasPass(GradientMergePass):
+    """The reference's registered name for gradient merge (auto_parallel_gradient_merge.py:808); the same pass as
+    ``auto_parallel_gradient_merge``: the Executor / engine accumulate ``k_steps`` runs and update on the last."""
+
+
+@register_pass("auto_parallel_sequence_parallel_optimization")
+class SequenceParallelOptimizationPass(PassBase):
+    """Reference auto_parallel_sequence_parallel_optimization.py:32 (strategy.sp_optimization): a row-parallel
+    output that enters a sequence-parallel region is reduced with ONE reduce-scatter instead of an all-reduce
+    followed by a slice (``_fuse_allreduce_split`` there). The pass marks the program; the static engine's
+    partitioner emits the reduce-scatter for every Partial -> Shard conversion of a marked program
+    (static_engine._convert)."""
+
+    def _type(self):
+        return PassType.COMM_OPT
+
+    def _apply_single_impl(self, prog, startup, context):
+        prog._pa_sp_opt = True
+        context.set_attr("auto_parallel_sequence_parallel_optimization.enabled", True)
+
+
+@register_pass("auto_parallel_pipeline")
+class AutoParallelPipelinePass(PassBase):
+    """Reference auto_parallel_pipeline.py:48 (the static pipeline pass of the auto-parallel engine): builds the
+    stage's job list for ``schedule_mode`` (FThenB / 1F1B / Eager1F1B / ZBH1 / VPP / ZBVPP) through the registered
+    ``pipeline_scheduler_<mode>`` pass and returns it as ``auto_parallel_pipeline.job_list``."""
+
+    _MODES = {"FTHENB": "FThenB", "1F1B": "1F1B", "EAGER1F1B": "Eager1F1B", "ZBH1": "ZBH1", "VPP": "VPP",
+              "ZBVPP": "ZBVPP"}
+
+    def _type(self):
+        return PassType.PARALLEL_OPT
+
+    def _check_self(self):
+        return str(self.get_attr("schedule_mode", "1F1B")).upper() in self._MODES
+
+    def _apply_single_impl(self, prog, startup, context):
+        from .pass_base import new_pass
+        mode = self._MODES[str(self.get_attr("schedule_mode", "1F1B")).upper()]
+        attrs = {k: self.get_attr(k) for k in ("num_micro_batches", "pp_stage", "pp_degree", "vpp_degree")
+                 if self.get_attr(k) is not None}
+        ctx = new_pass(f"pipeline_scheduler_{mode}", attrs).apply(prog, startup)
+        context.set_attr("auto_parallel_pipeline.job_list", ctx.get_attr("pipeline_scheduler.job_list"))
+        context.set_attr("auto_parallel_pipeline.mode", mode)

@@ -62,7 +62,7 @@ SIGS = {
     # gemm epilogue companions
     "pa_colsum": [_vp, _vp, _vp, _i64, _i64, _i32, _vp],
     "pa_dwconv_fwd": [_vp, _vp, _vp, _vp, _vp, _i32, _vp],
-    "pa_dwconv_dgrad": [_vp, _vp, _vp, _vp, _i32, _vp],
+    "pa_dwconv_dgrad": [_vp, _vp, _vp, _vp, _vp, _i32, _vp],
     "pa_dwconv_wgrad_parts": [_vp, _vp],
     "pa_dwconv_wgrad": [_vp, _vp, _vp, _vp, _i32, _vp],
     "pa_gemm_bf16": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _f32,

@@ -22,20 +22,20 @@ def eligible(x, w, groups):
     return groups == C and w.shape[0] == C and w.shape[1] == 1 and C % 8 == 0 and x.numel() > 0
 
 
-def _shape(x, w, stride, pad, dil):
+def _shape(x, w, stride, pad, dil, relu=False):
     N, H, W, C = x.shape
     KH, KW = int(w.shape[2]), int(w.shape[3])
     Ho = (H + 2 * pad[0] - dil[0] * (KH - 1) - 1) // stride[0] + 1
     Wo = (W + 2 * pad[1] - dil[1] * (KW - 1) - 1) // stride[1] + 1
-    return torch.tensor([N, H, W, C, Ho, Wo, KH, KW, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1]],
-                        dtype=torch.int32), Ho, Wo
+    return torch.tensor([N, H, W, C, Ho, Wo, KH, KW, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1],
+                         int(bool(relu))], dtype=torch.int32), Ho, Wo
 
 
 class _DWConv(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, stride, pad, dil):
+    def forward(ctx, x, w, b, stride, pad, dil, relu=False):
         N, H, W, C = x.shape
-        shp, Ho, Wo = _shape(x, w, stride, pad, dil)
+        shp, Ho, Wo = _shape(x, w, stride, pad, dil, relu)
         wt = w.reshape(C, -1).t().contiguous()  # [KH*KW, C]: one tap's 8 channel weights per vector load
         y = torch.empty(N, Ho, Wo, C, dtype=x.dtype, device=x.device)
         L.call("pa_dwconv_fwd", L.ptr(x), L.ptr(wt), L.ptr(None if b is None else b.contiguous()), L.ptr(y),
@@ -53,7 +53,8 @@ class _DWConv(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            L.call("pa_dwconv_dgrad", L.ptr(dy), L.ptr(wt), L.ptr(dx), L.ptr(shp), L.dcode(x), L.stream_ptr())
+            L.call("pa_dwconv_dgrad", L.ptr(dy), L.ptr(wt), L.ptr(x), L.ptr(dx), L.ptr(shp), L.dcode(x),
+                   L.stream_ptr())
         if ctx.needs_input_grad[1]:
             pp = torch.zeros(4, dtype=torch.int32)
             L.call("pa_dwconv_wgrad_parts", L.ptr(shp), L.ptr(pp))
@@ -67,17 +68,21 @@ class _DWConv(torch.autograd.Function):
             dw = out.view(taps, C).t().reshape(ctx.wshape)
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = colsum(dy.view(-1, C))
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, None
 
 
-def depthwise_conv2d_nhwc(x, w, b, stride, pad, dil, fallback):
+def depthwise_conv2d_nhwc(x, w, b, stride, pad, dil, fallback, pre_relu=False):
     """NHWC depthwise convolution on the HIP kernels when they measured faster than MIOpen for this shape
-    (``fallback(x, w)`` is the MIOpen path); None means: use the fallback."""
+    (``fallback(x, w)`` is the MIOpen path); None means: use the fallback. ``pre_relu``: convolve relu(x) (the
+    ReLU applied on the kernels' loads and its mask in the data gradient; the fallback gets relu(x))."""
     key = ("dwconv", tuple(x.shape), tuple(w.shape), tuple(stride), tuple(pad), tuple(dil), b is not None,
-           x.requires_grad or w.requires_grad)
+           x.requires_grad or w.requires_grad, bool(pre_relu))
+    if pre_relu:
+        plain = fallback
+        fallback = lambda xx, ww: plain(torch.relu(xx), ww)  # noqa: E731
 
     def run(xx, ww):
-        return _DWConv.apply(xx, ww, b, tuple(stride), tuple(pad), tuple(dil))
+        return _DWConv.apply(xx, ww, b, tuple(stride), tuple(pad), tuple(dil), bool(pre_relu))
 
     def bench(fn):
         def go():

@@ -241,6 +241,8 @@ class BuildStrategy:
         self.fuse_dot_product_attention = False
         self.fuse_adamw = False
         self.fuse_all_optimizer_ops = False
+        self.fuse_relu_depthwise_conv = False
+        self.fuse_resunit = False
         self.enable_inplace = True
         self.memory_optimize = True
         self.fuse_all_reduce_ops = True
@@ -259,7 +261,9 @@ class ExecutionStrategy:
 
 # BuildStrategy switch -> pass, in application order (AMP-independent fusions first, GEMM epilogue before the
 # passes that consume fused_linear nodes)
-_BUILD_PASSES = (("fuse_bn_act_ops", "fuse_bn_act"), ("fuse_bn_add_act_ops", "fuse_bn_add_act"),
+_BUILD_PASSES = (("fuse_relu_depthwise_conv", "fuse_relu_depthwise_conv"),
+                 ("fuse_bn_act_ops", "fuse_bn_act"), ("fuse_bn_add_act_ops", "fuse_bn_add_act"),
+                 ("fuse_resunit", "fuse_resunit"),
                  ("fuse_dot_product_attention", "fuse_dot_product_attention"),
                  ("fuse_gemm_epilogue", "fuse_gemm_epilogue"), ("fused_feedforward", "fused_feedforward"),
                  ("fused_attention", "fused_attention"), ("fuse_elewise_add_act_ops", "fuse_elewise_add_act"),

@@ -84,3 +84,38 @@ def test_conv2d_transpose_stride1_nhwc_on_conv_kernels(K, pad):
             assert err <= 3e-2 * max(1.0, ref.abs().max().item()), err
     finally:
         paddle.set_flags({"FLAGS_gemm_backend": "auto"})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("case", [CASES[0], CASES[1], CASES[4]])
+def test_relu_depthwise_fused_hip_kernels(case, dt):
+    """ops.fused_conv.relu_depthwise_conv2d (the fuse_relu_depthwise_conv node): the ReLU on the kernels' loads and
+    as the data-gradient mask, against relu + conv2d in fp32 — values and x / w / b gradients."""
+    from paddlepaddle_amd.ops.fused_conv import relu_depthwise_conv2d
+    N, H, W, C, K, s, p, d, bias = case
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(N, H, W, C, generator=g)
+    w = torch.randn(C, 1, K, K, generator=g) * 0.3
+    b = torch.randn(C, generator=g) if bias else None
+    xr, wr = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True) if bias else None
+    yr = F.conv2d(torch.relu(xr.permute(0, 3, 1, 2)), wr, br, s, p, d, C)
+    gy = torch.cos(yr.detach())
+    yr.backward(gy)
+    paddle.set_flags({"FLAGS_gemm_backend": "hip"})
+    try:
+        L.CALLS.clear()
+        xc, wc = x.cuda().to(dt).requires_grad_(True), w.cuda().to(dt).requires_grad_(True)
+        bc = b.cuda().to(dt).requires_grad_(True) if bias else None
+        y = relu_depthwise_conv2d(xc, wc, bc, s, p, d, C, True)
+        y.backward(gy.cuda().to(dt))
+        for n in ("pa_dwconv_fwd", "pa_dwconv_dgrad", "pa_dwconv_wgrad"):
+            assert L.calls(n) > 0, (n, dict(L.CALLS))
+    finally:
+        paddle.set_flags({"FLAGS_gemm_backend": "auto"})
+    tol = 2e-2 if dt == torch.bfloat16 else 1e-4
+    for got, ref in ((y, yr), (xc.grad.permute(0, 3, 1, 2), xr.grad.permute(0, 3, 1, 2)), (wc.grad, wr.grad)) + \
+            (((bc.grad, br.grad),) if bias else ()):
+        err = (got.float().cpu() - ref).abs().max().item()
+        assert err <= tol * max(1.0, ref.abs().max().item()), (case, err)

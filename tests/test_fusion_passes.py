@@ -171,3 +171,51 @@ def test_build_strategy_applies_fusion_passes_on_first_run():
     assert set(cp._applied) == {"fuse_gemm_epilogue", "fused_feedforward", "fused_attention"}
     assert "ffn_gelu" in _names(main)
     np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5)
+
+
+def _conv_program(kind):
+    main, start = paddle.static.Program(), paddle.static.Program()
+    with paddle.static.program_guard(main, start):
+        paddle.seed(7)
+        x = paddle.static.data("x", [2, 6, 6, 8], "float32")
+        if kind == "dw":  # relu -> depthwise conv on a channels-last layer, and on an NCHW one
+            y = paddle.nn.Conv2D(8, 8, 3, padding=1, groups=8, data_format="NHWC")(paddle.nn.functional.relu(x))
+            z = paddle.transpose(y, [0, 3, 1, 2])
+            out = paddle.nn.Conv2D(8, 8, 3, padding=1, groups=8, bias_attr=False)(paddle.nn.functional.relu(z))
+        else:  # conv -> BN -> + x -> relu, then conv -> BN -> relu (the two ResNet unit forms)
+            c1 = paddle.nn.Conv2D(8, 8, 3, padding=1, data_format="NHWC", bias_attr=False)
+            b1 = paddle.nn.BatchNorm2D(8, data_format="NHWC")
+            h = paddle.nn.functional.relu(b1(c1(x)) + x)
+            c2 = paddle.nn.Conv2D(8, 8, 1, data_format="NHWC", bias_attr=False)
+            b2 = paddle.nn.BatchNorm2D(8, data_format="NHWC")
+            out = paddle.nn.functional.relu(b2(c2(h)))
+        loss = (out * out).mean()
+        opt = paddle.optimizer.SGD(0.1)
+        opt.minimize(loss)
+    return main, loss
+
+
+@pytest.mark.parametrize("kind", ["dw", "resunit"])
+def test_conv_fusion_passes_match_unfused(kind):
+    """fuse_relu_depthwise_conv (relu folded into the depthwise conv) and fuse_resunit (conv -> BN (+ add) (+ relu)
+    as one conv_bn_unit node, after fuse_bn_act / fuse_bn_add_act): same losses over training steps as the
+    unrewritten program (reference cpp_pass.py:63 / :171)."""
+    feed = {"x": np.random.RandomState(3).randn(2, 6, 6, 8).astype("float32")}
+    losses = []
+    for fuse in (False, True):
+        main, loss = _conv_program(kind)
+        if fuse:
+            if kind == "dw":
+                ctx = new_pass("fuse_relu_depthwise_conv").apply(main, None)
+                assert ctx.get_attr("fuse_relu_depthwise_conv.fused") == 2
+                assert _names(main).count("relu_depthwise_conv2d") == 2 and "relu" not in _names(main)
+            else:
+                new_pass("fuse_bn_add_act").apply(main, None)
+                new_pass("fuse_bn_act").apply(main, None)
+                ctx = new_pass("fuse_resunit").apply(main, None)
+                assert ctx.get_attr("fuse_resunit.fused") == 2
+                assert _names(main).count("conv_bn_unit") == 2
+                assert "conv2d" not in _names(main) and "batch_norm_act_nhwc" not in _names(main)
+        losses.append([float(_run(main, feed, [loss])[0]) for _ in range(3)])
+    np.testing.assert_allclose(losses[1], losses[0], rtol=1e-5, atol=1e-6)
+    assert losses[0][-1] < losses[0][0]
