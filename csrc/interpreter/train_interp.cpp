@@ -23,6 +23,7 @@
 #include <torch/csrc/jit/python/pybind_utils.h>
 #include <ATen/core/dispatch/Dispatcher.h>
 #include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
 #include <hip/hip_runtime_api.h>
 
 #include <cmath>
@@ -701,7 +702,7 @@ bool bn_ok(const at::Tensor& x2, const at::Tensor& w, const at::Tensor& b, const
 }
 
 // ------------------------------------------------------------------------------------------------ program
-enum Kind : int { kAten = 0, kLinear, kLinearNT, kNorm, kFlash, kFlashQKV, kSoftmaxCE, kConv, kBN, kAlias };
+enum Kind : int { kAten = 0, kLinear, kLinearNT, kNorm, kFlash, kFlashQKV, kSoftmaxCE, kConv, kBN, kAlias, kComm };
 
 enum ArgKind : int { kSlot = 0, kSlotList = 1, kConst = 2, kRunDevice = 3, kOptSlotList = 4 };
 
@@ -803,6 +804,20 @@ class TrainProgram {
     code_.push_back(std::move(I));
   }
 
+  // a collective of the program (in place on its operand slots): run on the program's communication stream, after
+  // the compute stream's work so far (its inputs exist); a later instruction reading a slot it wrote waits for it
+  // with an event (reference new_executor/interpreter/stream_analyzer.cc: communication ops on their own stream,
+  // cross-stream dependencies as events; dependency_builder.cc: read-after-write edges on the written vars)
+  void add_comm(py::object fn, std::vector<int> slots, const std::string& name) {
+    Instr I;
+    I.kind = kComm;
+    I.name = name;
+    I.in = std::move(slots);
+    I.ia = {static_cast<int64_t>(comm_fns_.size())};
+    comm_fns_.push_back(std::move(fn));
+    code_.push_back(std::move(I));
+  }
+
   // parameters (leaf tensors requiring grad), buffers and constants: persistent slots
   void bind(int slot, at::Tensor t) {
     grow(slot + 1);
@@ -854,6 +869,8 @@ class TrainProgram {
         if (s >= 0) fn(s);
     };
     for (size_t n = 0; n < code_.size(); ++n) reads(code_[n], [&](int s) { last.at(s) = static_cast<int>(n); });
+    reads_.assign(code_.size(), {});
+    for (size_t n = 0; n < code_.size(); ++n) reads(code_[n], [&](int s) { reads_[n].push_back(s); });
     release_.assign(code_.size(), {});
     for (size_t s = 0; s < last.size(); ++s)
       if (last[s] >= 0 && !keep[s]) release_[last[s]].push_back(static_cast<int>(s));
@@ -876,10 +893,16 @@ class TrainProgram {
     {
       at::AutoGradMode grad_mode(backward);
       for (size_t n = 0; n < code_.size(); ++n) {
-        exec(code_[n]);
+        if (code_[n].kind == kComm) {
+          exec_comm(code_[n]);
+        } else {
+          wait_pending(n);
+          exec(code_[n]);
+        }
         done_ = static_cast<int64_t>(n) + 1;
         for (int s : release_[n]) slots_[s] = at::Tensor();
       }
+      join_comm();
       if (backward) {
         phase_ = 1;
         loss = slots_.at(loss_);
@@ -916,13 +939,24 @@ class TrainProgram {
   }
 
   int64_t num_instructions() const { return static_cast<int64_t>(code_.size()); }
+  int64_t num_comm() const {
+    int64_t n = 0;
+    for (const auto& I : code_) n += I.kind == kComm;
+    return n;
+  }
+
+  ~TrainProgram() {
+    for (hipEvent_t e : events_) (void)hipEventDestroy(e);
+    py::gil_scoped_acquire gil;
+    comm_fns_.clear();
+  }
   // phase of the last run when it stopped (0 forward, 1 backward, 2 gradient hook, 3 update) and the number of
   // forward instructions it completed
   int64_t phase() const { return phase_; }
   int64_t done() const { return done_; }
   int64_t num_native() const {
     int64_t n = 0;
-    for (const auto& I : code_) n += I.kind != kAten && I.kind != kAlias;
+    for (const auto& I : code_) n += I.kind != kAten && I.kind != kAlias && I.kind != kComm;
     return n;
   }
 
@@ -1003,6 +1037,76 @@ class TrainProgram {
   }
 
   at::Tensor slot(int s) const { return s >= 0 ? slots_.at(s) : at::Tensor(); }
+
+  // ---- communication stream
+  hipEvent_t next_event() {
+    if (ev_next_ == events_.size()) {
+      hipEvent_t e;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+        throw std::runtime_error("native train executor: hipEventCreate failed");
+      events_.push_back(e);
+    }
+    return events_[ev_next_++];
+  }
+
+  void exec_comm(const Instr& I) {
+    std::vector<at::Tensor> ts;
+    for (int s : I.in) ts.push_back(slots_.at(s));
+    const bool gpu = !ts.empty() && ts[0].is_cuda();
+    if (!gpu) {  // host collectives (gloo on CPU tensors): in program order on the caller's thread
+      py::gil_scoped_acquire gil;
+      py::tuple args(ts.size());
+      for (size_t i = 0; i < ts.size(); ++i) args[i] = py::cast(ts[i]);
+      comm_fns_.at(I.ia[0])(*args);
+      count("comm");
+      return;
+    }
+    const c10::DeviceIndex dev = ts[0].device().index();
+    if (!comm_stream_) comm_stream_ = c10::hip::getStreamFromPool(false, dev);
+    hipStream_t comp = c10::hip::getCurrentHIPStream(dev).stream();
+    hipEvent_t ready = next_event();  // the collective's inputs: everything issued on the compute stream so far
+    if (hipEventRecord(ready, comp) != hipSuccess || hipStreamWaitEvent(comm_stream_->stream(), ready, 0) != hipSuccess)
+      throw std::runtime_error("native train executor: stream dependency failed");
+    {
+      c10::hip::HIPStreamGuard guard(*comm_stream_);
+      py::gil_scoped_acquire gil;
+      py::tuple args(ts.size());
+      for (size_t i = 0; i < ts.size(); ++i) args[i] = py::cast(ts[i]);
+      comm_fns_.at(I.ia[0])(*args);
+    }
+    hipEvent_t done = next_event();
+    if (hipEventRecord(done, comm_stream_->stream()) != hipSuccess)
+      throw std::runtime_error("native train executor: hipEventRecord failed");
+    for (int s : I.in) pending_[s] = done;
+    for (auto& t : ts) comm_keep_.push_back(t);  // alive (not reused by the compute stream) until join_comm
+    count("comm");
+  }
+
+  // a compute instruction reading a slot a collective wrote: the compute stream waits for that collective
+  void wait_pending(size_t n) {
+    if (pending_.empty()) return;
+    for (int s : reads_[n]) {
+      auto it = pending_.find(s);
+      if (it == pending_.end()) continue;
+      hipStream_t comp = c10::hip::getCurrentHIPStream().stream();
+      if (hipStreamWaitEvent(comp, it->second, 0) != hipSuccess)
+        throw std::runtime_error("native train executor: hipStreamWaitEvent failed");
+      pending_.erase(it);
+    }
+  }
+
+  // end of the forward: the compute stream waits for every outstanding collective; their operands may be freed
+  void join_comm() {
+    if (comm_stream_ && ev_next_ > 0) {
+      hipEvent_t all = next_event();
+      hipStream_t comp = c10::hip::getCurrentHIPStream().stream();
+      if (hipEventRecord(all, comm_stream_->stream()) != hipSuccess || hipStreamWaitEvent(comp, all, 0) != hipSuccess)
+        throw std::runtime_error("native train executor: stream join failed");
+    }
+    pending_.clear();
+    comm_keep_.clear();
+    ev_next_ = 0;
+  }
   void put(const Instr& I, size_t k, const at::Tensor& t) {
     if (k < I.outs.size() && !I.outs[k].empty() && I.outs[k][0] >= 0) slots_[I.outs[k][0]] = t;
   }
@@ -1114,6 +1218,13 @@ class TrainProgram {
   std::vector<OptGroup> opt_;
   py::object grad_hook_;
   int64_t phase_ = 0, done_ = 0;
+  std::vector<std::vector<int>> reads_;  // per instruction: slots it reads (event waits)
+  std::vector<py::object> comm_fns_;
+  c10::optional<c10::hip::HIPStream> comm_stream_;
+  std::unordered_map<int, hipEvent_t> pending_;  // slot -> event of the collective that wrote it
+  std::vector<hipEvent_t> events_;
+  size_t ev_next_ = 0;
+  std::vector<at::Tensor> comm_keep_;
   int loss_ = -1;
 };
 
@@ -1128,6 +1239,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("grow", &TrainProgram::grow)
       .def("add_aten", &TrainProgram::add_aten)
       .def("add_native", &TrainProgram::add_native)
+      .def("add_comm", &TrainProgram::add_comm)
       .def("bind", &TrainProgram::bind)
       .def("set_loss", &TrainProgram::set_loss)
       .def("set_grad_hook", &TrainProgram::set_grad_hook)
@@ -1137,6 +1249,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("num_instructions", &TrainProgram::num_instructions)
       .def_property_readonly("num_native", &TrainProgram::num_native)
+      .def_property_readonly("num_comm", &TrainProgram::num_comm)
       .def_property_readonly("phase", &TrainProgram::phase)
       .def_property_readonly("done", &TrainProgram::done);
 }

@@ -16,8 +16,14 @@ backward is the C++ autograd engine over what the instructions recorded:
     multi-tensor kernel launch over a pointer table built in C++; its state tensors are the Python optimizer's own
     accumulators, so state_dict / checkpoints see every native step.
 
+  * collectives of the program (``c:`` comm nodes: all_reduce / broadcast / the fuse_all_reduce coalesced
+    buckets) become communication instructions: issued on the executor's own HIP stream after the compute issued
+    before them, with an event that the first later instruction reading what they wrote waits on, so compute that
+    does not depend on a collective overlaps it (reference new_executor/interpreter/stream_analyzer.cc:44,
+    dependency_builder.cc:87).
+
 ``compile_training`` returns None (with ``reason``) for programs it cannot lower — control flow, guards, gradient
-merge, comm ops, optimizers or clips outside the list above — and the Executor keeps the Python replay.
+merge, optimizers or clips outside the list above — and the Executor keeps the Python replay.
 """
 from __future__ import annotations
 
@@ -428,6 +434,7 @@ class NativeTrainRunner:
         self.need_grad = need_grad_slots
         self.num_instructions = tp.num_instructions
         self.num_native = tp.num_native
+        self.num_comm = tp.num_comm
         self._lowering = lowering  # keeps bound tensors alive
         self.runs = 0
 
@@ -480,6 +487,8 @@ class NativeTrainRunner:
 
 def _mutates(ins):
     """Whether a lowered instruction writes device state that outlives the step."""
+    if ins[0] == "comm":
+        return True  # a collective: other ranks took part, it cannot be issued again alone
     if ins[0] == "native":
         return ins[1] == "batch_norm_act"
     name, overload = ins[1], ins[2]
@@ -513,8 +522,13 @@ def _lower_all(low, plan, native_kernels):
     if True:
         for i in plan.order:
             n = plan.nodes[i]
-            if isinstance(n, (P.CFNode, P.GuardNode)) or n.kind in ("comm", "grad", "guard"):
+            if isinstance(n, (P.CFNode, P.GuardNode)) or n.kind in ("grad", "guard"):
                 raise Unsupported(f"{type(n).__name__} {n.name}")
+            if n.kind == "comm":  # a collective: an instruction on the executor's communication stream
+                if not n.args or not all(isinstance(a, P._Ref) for a in n.args) or n.kwargs:
+                    raise Unsupported(f"collective {n.name} with non-tensor operands")
+                low.instrs.append(("comm", n.func, [a.i for a in n.args], n.name))
+                continue
             if native_kernels and low.lower_native(n):
                 continue
             low.lower_generic(n)
@@ -526,6 +540,8 @@ def _build(m, low, prog, fetch, dev, native_kernels, opt_entry):
         for ins in low.instrs:
             if ins[0] == "aten":
                 tp.add_aten(f"{ins[1]}", ins[2], [tuple(a) for a in ins[3]], ins[4])
+            elif ins[0] == "comm":
+                tp.add_comm(ins[1], ins[2], ins[3])
             else:
                 tp.add_native(ins[1], ins[2], ins[3], ins[4], ins[5])
     except Exception as e:  # noqa: BLE001 - an operator argument the schema conversion rejects

@@ -217,3 +217,65 @@ def test_native_executor_replay_only_before_side_effects():
     for phase, done, ok in [(0, 0, True), (0, 1, False), (0, 2, False), (1, 3, False), (3, 3, False)]:
         r.tp = TP(phase, done)
         assert r.replayable() is ok, (phase, done)
+
+
+def _comm_build(fn=None):
+    def build():
+        from paddlepaddle_amd.distributed.collective import _static_comm
+        x = paddle.static.data("x", [32, 16], "float32")
+        t = paddle.static.data("t", [32, 1], "float32")
+        h = paddle.nn.Linear(16, 64)(x)
+        if fn is None:
+            paddle.distributed.all_reduce(h)  # a c:all_reduce node of the program
+        else:
+            assert _static_comm(h, "scale", fn)
+        side = paddle.nn.Linear(16, 64)(x)  # independent of the collective: overlaps it on the compute stream
+        loss = ((paddle.nn.Linear(64, 1)(paddle.nn.functional.relu(h) + side) - t) ** 2).mean()
+        paddle.optimizer.AdamW(learning_rate=0.01).minimize(loss)
+        return loss
+    return build
+
+
+def _comm_worker(rank, world, port, q):
+    from test_distributed_cpu import _setup
+    _setup(rank, world, port)
+    out = {}
+    for mode in ("off", "force"):
+        losses, main = _run(_comm_build(), _mlp_feeds, mode)
+        rs = _runners(main)
+        out[mode] = (losses, [r.num_comm for r in rs])
+    q.put((rank, out))
+
+
+def test_native_executor_collective_instructions_gloo():
+    """A program with an all_reduce node lowers onto the native executor as a communication instruction (2 gloo
+    ranks): same losses as the Python replay on both ranks."""
+    from test_distributed_cpu import _spawn
+    for rank, out in _spawn(_comm_worker, world=2):
+        ref, _ = out["off"]
+        got, ncomm = out["force"]
+        assert ncomm == [1], ncomm
+        np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_native_executor_comm_stream_gpu():
+    """GPU: the communication instruction runs on the executor's own stream (not the compute stream), and the
+    instruction reading what it wrote waits for it through an event: same losses as the Python replay (which
+    runs collectives on its own comm stream too)."""
+    import torch
+    seen = []
+
+    def scale(x):  # an in-place "collective" on the current (communication) stream
+        seen.append(torch.cuda.current_stream().cuda_stream)
+        x.mul_(0.5)
+
+    NT.reset_kernel_calls()
+    ref, _ = _run(_comm_build(scale), _mlp_feeds, "off")
+    seen.clear()
+    got, main = _run(_comm_build(scale), _mlp_feeds, "on")
+    rs = _runners(main)
+    assert len(rs) == 1 and rs[0].num_comm == 1, main.__dict__.get("_native_reason")
+    assert NT.kernel_calls().get("comm", 0) == 3
+    assert seen and all(s != torch.cuda.default_stream().cuda_stream for s in seen), seen
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-5)
