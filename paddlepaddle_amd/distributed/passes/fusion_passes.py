@@ -374,3 +374,83 @@ class AutoParallelPipelinePass(PassBase):
         ctx = new_pass(f"pipeline_scheduler_{mode}", attrs).apply(prog, startup)
         context.set_attr("auto_parallel_pipeline.job_list", ctx.get_attr("pipeline_scheduler.job_list"))
         context.set_attr("auto_parallel_pipeline.mode", mode)
+
+
+_SUM = 0  # distributed.collective.ReduceOp.SUM
+
+
+def _first_rank_of(comm_node):
+    """Whether this process is rank 0 of the group of a recorded collective (meta = (kind, op, group))."""
+    meta = getattr(comm_node.func, "_pa_comm", None)
+    group = meta[2] if isinstance(meta, tuple) and len(meta) > 2 else None
+    from .. import collective as C
+    return C.get_rank(group) == 0 if group is not None else C.get_rank() == 0
+
+
+@register_pass("auto_parallel_fused_linear_promotion")
+class FusedLinearPromotionPass(PassBase):
+    """Reference auto_parallel_fused_linear_promotion.py:130: in tensor parallelism a row-parallel linear is
+    ``matmul -> all_reduce(sum) -> + bias``, which keeps the bias add out of the GEMM. The bias is promoted in front
+    of the reduction on the group's first rank only — ``fused_linear(x, W, b)`` there (the bias in the hand-written
+    GEMM's epilogue), the plain matmul on the other ranks — and the add disappears (its output aliases the reduced
+    tensor). The reduction then sums exactly one copy of the bias. Only the first rank's bias gets a gradient (and
+    an update), as in the reference."""
+    _after = ("auto_parallel_amp", "auto_parallel_fp16")
+
+    def _type(self):
+        return PassType.FUSION_OPT
+
+    def _apply_single_impl(self, prog, startup, context):
+        lin = P._resolve(_LINEAR)
+        keep = _protected(prog, self.get_attr("fetch_vars"))
+
+        def step(pr, k, n):
+            if n.name not in _ADD or len(n.args) != 2 or n.kwargs or not isinstance(n.outs, P._Ref):
+                return False
+            for h, b in (n.args, n.args[::-1]):
+                s = _slot(h)
+                hs, bs = _shape_of(prog, h), _shape_of(prog, b)
+                if s is None or hs is None or bs is None or bs != (hs[-1],) or s in keep:
+                    continue
+                writers = [i for i in range(k) if s in P._node_writes(pr.nodes[i])]
+                if len(writers) != 2 or pr.uses.get(s, 0) != 2:  # created by the matmul, reduced in place, read here
+                    continue
+                i_m, i_c = writers
+                m, c = pr.nodes[i_m], pr.nodes[i_c]
+                meta = getattr(c.func, "_pa_comm", None)
+                if c.kind != "comm" or not isinstance(meta, tuple) or meta[0] != "all_reduce" or \
+                        meta[1] != _SUM or len(c.args) != 1:
+                    continue
+                if m.name not in _MATMUL or len(m.args) != 2 or m.kwargs:
+                    continue
+                ws = _shape_of(prog, m.args[1])
+                if ws is None or len(ws) != 2 or ws[1] != bs[0]:
+                    continue
+                if _first_rank_of(c):
+                    pr.nodes[i_m] = _keep_rc(P.OpNode(lin, (m.args[0], m.args[1], b), {}, m.outs, "op", _LINEAR), m)
+                pr.nodes[k] = _keep_rc(P.OpNode(torch.Tensor.view_as, (h, h), {}, n.outs, "op", "m:view_as"), n)
+                return True
+            return False
+
+        n = _rewrite_until_fixed(prog, keep, step)
+        context.set_attr("auto_parallel_fused_linear_promotion.promoted",
+                         context.get_attr("auto_parallel_fused_linear_promotion.promoted", 0) + n)
+
+
+@register_pass("auto_parallel_supplement_explicit_dependencies")
+class SupplementExplicitDependenciesPass(PassBase):
+    """Reference auto_parallel_supplement_explicit_dependencies.py:41: a graph executor that may reorder ops must
+    not let the ranks issue their collectives in different orders (a hang). The executors here replay an ordered
+    instruction list, and the native scheduler (static/program.py build_plan) issues collectives as early as their
+    inputs allow — the pass pins program order instead: it adds an explicit ordering edge from every collective to
+    the next one (``prog._pa_comm_chain``, honoured by build_plan), so the scheduled order of the collectives is
+    the traced order on every rank whatever the priorities of the ops between them. Returns the chain length as
+    ``auto_parallel_supplement_explicit_dependencies.chained``."""
+
+    def _type(self):
+        return PassType.COMM_OPT
+
+    def _apply_single_impl(self, prog, startup, context):
+        comm = [i for i, n in enumerate(prog.nodes) if not isinstance(n, P.CFNode) and n.kind == "comm"]
+        prog._pa_comm_chain = [id(prog.nodes[i]) for i in comm]
+        context.set_attr("auto_parallel_supplement_explicit_dependencies.chained", max(0, len(comm) - 1))

@@ -580,6 +580,12 @@ def build_plan(program, fetch_slots, keep_slots=()):
                 edges.add((pos_of[last_writer[s]], k))
             creator.setdefault(s, i)
             last_writer[s] = i
+    # auto_parallel_supplement_explicit_dependencies: consecutive collectives keep their traced order
+    chain = getattr(program, "_pa_comm_chain", None)
+    if chain:
+        at = {id(nodes[i]): k for k, i in enumerate(idx)}
+        ks = [at[c] for c in chain if c in at]
+        edges.update(zip(ks, ks[1:]))
     keep_nodes = {pos_of[creator[s]] for s in set(fetch_slots) | set(keep_slots) if s in creator}
     keep_nodes |= {k for k, i in enumerate(idx) if nodes[i].kind == "guard"}
     # collectives are issued as soon as their inputs exist (they run on the comm stream and overlap the

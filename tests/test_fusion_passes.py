@@ -219,3 +219,69 @@ def test_conv_fusion_passes_match_unfused(kind):
         losses.append([float(_run(main, feed, [loss])[0]) for _ in range(3)])
     np.testing.assert_allclose(losses[1], losses[0], rtol=1e-5, atol=1e-6)
     assert losses[0][-1] < losses[0][0]
+
+
+def _promo_worker(rank, world, port, q):
+    import sys
+    from test_distributed_cpu import _setup
+    pd = _setup(rank, world, port)
+    from paddlepaddle_amd.distributed.passes import new_pass as np_
+    out = []
+    for promote in (False, True):
+        pd.enable_static()
+        main, start = pd.static.Program(), pd.static.Program()
+        with pd.static.program_guard(main, start):
+            pd.seed(11 + rank)  # row-parallel: each rank its own slice of W
+            x = pd.static.data("x", [8, 16], "float32")
+            w = pd.create_parameter([16, 8], "float32")
+            pd.seed(5)  # the bias is replicated
+            b = pd.create_parameter([8], "float32", is_bias=True,
+                                    default_initializer=pd.nn.initializer.Normal(0.0, 1.0))
+            h = pd.matmul(x, w)
+            pd.distributed.all_reduce(h)
+            y = h + b
+            loss = (y * y).mean()
+            pd.optimizer.SGD(0.05).minimize(loss)
+        if promote:
+            ctx = np_("auto_parallel_fused_linear_promotion").apply(main, None)
+            names = [n.name.rsplit(":", 1)[-1] for n in main.nodes]
+            assert ctx.get_attr("auto_parallel_fused_linear_promotion.promoted") == 1
+            assert ("fused_linear" in names) == (rank == 0) and "add" not in names, names
+        exe = pd.static.Executor(pd.CPUPlace())
+        xs = np.random.RandomState(rank).randn(8, 16).astype("float32")
+        out.append([float(exe.run(main, feed={"x": xs}, fetch_list=[loss])[0]) for _ in range(3)])
+        pd.disable_static()
+    q.put((rank, out))
+
+
+def test_fused_linear_promotion_row_parallel_gloo(monkeypatch):
+    """auto_parallel_fused_linear_promotion (reference auto_parallel_fused_linear_promotion.py:130): matmul ->
+    all_reduce -> + bias becomes fused_linear(x, W, b) on the group's first rank (the plain matmul elsewhere) with
+    the add removed; 2 gloo ranks train with the same losses as the unpromoted program."""
+    from test_distributed_cpu import _spawn
+    for rank, (ref, got) in _spawn(_promo_worker, world=2):
+        np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)
+        assert ref[-1] < ref[0]
+
+
+def test_supplement_explicit_dependencies_orders_collectives():
+    """auto_parallel_supplement_explicit_dependencies: the collectives are chained in program order for the
+    scheduler (static/program.py build_plan honours the chain; a reversed chain reverses their issue order)."""
+    from paddlepaddle_amd.distributed.collective import _static_comm
+    from paddlepaddle_amd.static import program as P
+    main, start = paddle.static.Program(), paddle.static.Program()
+    with paddle.static.program_guard(main, start):
+        x = paddle.static.data("x", [4, 4], "float32")
+        ts = [x * float(i + 2) for i in range(3)]
+        for t in ts:
+            assert _static_comm(t, "all_reduce", lambda v: None)
+        out = ts[0] + ts[1] + ts[2]
+    ctx = new_pass("auto_parallel_supplement_explicit_dependencies").apply(main, None)
+    assert ctx.get_attr("auto_parallel_supplement_explicit_dependencies.chained") == 2
+    comm = [n for n in main.nodes if n.kind == "comm"]
+    slot = main._slot_of[id(out._t)]
+    order = [main.nodes[i] for i in P.build_plan(main, [slot]).order if main.nodes[i].kind == "comm"]
+    assert order == comm
+    main._pa_comm_chain = main._pa_comm_chain[::-1]
+    order = [main.nodes[i] for i in P.build_plan(main, [slot]).order if main.nodes[i].kind == "comm"]
+    assert order == comm[::-1]
