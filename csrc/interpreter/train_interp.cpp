@@ -226,6 +226,16 @@ std::vector<int64_t> with_last(at::IntArrayRef s, int64_t n) {
 // ------------------------------------------------------------------------------------------------ linear
 // y = act(x @ W + b), W [in, out] (paddle layout); act 0 none, 1 tanh-GELU (epilogue of the GEMM, pre-activation
 // kept for the backward), 2 relu
+// The function's output reshaped to ``sizes`` over the same storage, WITHOUT autograd view tracking: a view returned
+// from a custom Function may not be modified in place (the program's in-place collectives write these outputs); used
+// only where the function saves nothing that aliases the output.
+inline at::Tensor out_alias(const at::Tensor& y, at::IntArrayRef sizes) {
+  at::Tensor v = y.view(sizes);
+  at::Tensor t = at::empty({0}, y.options());
+  t.set_(v.storage(), v.storage_offset(), v.sizes(), v.strides());
+  return t;
+}
+
 struct LinearFn : public torch::autograd::Function<LinearFn> {
   static at::Tensor forward(AutogradContext* ctx, at::Tensor x, at::Tensor w, at::Tensor b, int64_t act) {
     b = present(b);
@@ -259,7 +269,8 @@ struct LinearFn : public torch::autograd::Function<LinearFn> {
     ctx->saved_data["act"] = act;
     ctx->saved_data["has_b"] = b.defined();
     ctx->saved_data["shape"] = x.sizes().vec();
-    return y.view(with_last(x.sizes(), N));
+    if (act == 2) return y.view(with_last(x.sizes(), N));  // y is the saved relu mask: keep autograd's view checks
+    return out_alias(y, with_last(x.sizes(), N));
   }
 
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
@@ -289,7 +300,7 @@ struct LinearNTFn : public torch::autograd::Function<LinearNTFn> {
     at::Tensor y = matmul2d(x2, w.t());
     ctx->save_for_backward({x2, w});
     ctx->saved_data["shape"] = x.sizes().vec();
-    return y.view(with_last(x.sizes(), N));
+    return out_alias(y, with_last(x.sizes(), N));
   }
 
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
@@ -342,7 +353,7 @@ struct NormFn : public torch::autograd::Function<NormFn> {
     ctx->saved_data["has_b"] = b.defined();
     ctx->saved_data["wdt"] = static_cast<int64_t>(w.defined() ? w.scalar_type() : x2.scalar_type());
     ctx->saved_data["bdt"] = static_cast<int64_t>(b.defined() ? b.scalar_type() : x2.scalar_type());
-    return y.view(x.sizes());
+    return out_alias(y, x.sizes());
   }
 
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
@@ -513,7 +524,7 @@ struct SoftmaxCEFn : public torch::autograd::Function<SoftmaxCEFn> {
     ctx->saved_data["ignore"] = ignore;
     ctx->saved_data["shape"] = logits.sizes().vec();
     std::vector<int64_t> out(logits.sizes().begin(), logits.sizes().end() - 1);
-    return loss.view(out);
+    return out_alias(loss, out);
   }
 
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
