@@ -178,8 +178,10 @@ def test_recompute_overlap_sharding_passes_mark_program(static_mode):
     o2 = [n for n in m2.nodes if not isinstance(n, P.GuardNode)]
     assert o2[0].rc is None and any(n.rc is not None for n in o2)
     dp.new_pass("allreduce_matmul_grad_overlapping").apply([main], [st])
-    assert dp.new_pass("auto_parallel_sharding", {"stage": 3}).apply([main], [st]) is not None
-    assert not hasattr(main, "_pa_sharding")  # stage 3 fails _check_self: not applied
+    assert dp.new_pass("auto_parallel_sharding", {"stage": 4}).apply([main], [st]) is not None
+    assert not hasattr(main, "_pa_sharding")  # no stage 4: fails _check_self, not applied
+    dp.new_pass("auto_parallel_sharding", {"stage": 3}).apply([main], [st])
+    assert main._pa_sharding == {"stage": 3, "dim": "dp"}  # stage 3 on the static engine since round 6
     dp.new_pass("auto_parallel_sharding", {"stage": 2, "sharding_mesh_dim": "dp"}).apply([main], [st])
     assert main._pa_tp_overlap and main._pa_sharding == {"stage": 2, "dim": "dp"}
 
