@@ -217,7 +217,7 @@ def gpt_bench(args, paddle, world, dist_on):
     try:
         from paddlepaddle_amd.ops import gemm as _G
         ch = _G.choices()
-        log(f"[gpt] GEMM backend per shape: {sum(v == 'hip' for v in ch.values())} hand-written / "
+        log(f"[gpt] GEMM backend per shape: {sum(v.startswith('hip') for v in ch.values())} hand-written / "
             f"{sum(v == 'blas' for v in ch.values())} hipBLASLt: " +
             "; ".join(f"{k[0]}{list(k[1:4])}={v}" for k, v in sorted(ch.items(), key=str)))
     except Exception:  # pragma: no cover

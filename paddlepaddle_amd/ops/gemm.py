@@ -292,18 +292,24 @@ def gemm_pp_splitk_ok(a, b, splits):
             and la[0] % 8 == 0 and lb[0] % 8 == 0 and (la[1] or M % 8 == 0))
 
 
-def gemm_pp_splitk(a, b, splits, out_dtype=torch.bfloat16):
+def gemm_pp_splitk(a, b, splits, out_dtype=torch.bfloat16, out=None, accumulate=False):
     """C = a @ b on the ping-pong 256x256 kernel with every tile cut into ``splits`` K slices (fp32 partial tiles
-    summed, with the cast, by the tail-reduction kernel): the split-K form for few output tiles and a long K."""
+    summed, with the cast, by the tail-reduction kernel): the split-K form for few output tiles and a long K.
+    ``out`` + ``accumulate``: C += a @ b in place (the reduction reads C; gradient-accumulation fusion)."""
     M, K = a.shape
     N = b.shape[1]
     lda, ak = _layout(a, 0)
     ldb, bk = _layout(b, 1)
-    out = torch.empty(M, N, dtype=out_dtype, device=a.device)
+    if out is None:
+        out = torch.empty(M, N, dtype=out_dtype, device=a.device)
+    elif out.shape != (M, N) or out.stride(1) != 1 or out.stride(0) % 4 or out.dtype not in (torch.bfloat16,
+                                                                                           torch.float32):
+        raise ValueError("gemm_pp_splitk: out must be a row-major [M, N] bf16 / fp32 tensor")
     ws = torch.empty(int(L.lib().pa_gemm_pp_splitk_ws_bytes(M, N, splits)) // 4, dtype=torch.float32,
                      device=a.device)
+    flags = (EPI_OUT_F32 if out.dtype == torch.float32 else 0) | (EPI_ACCUM if accumulate else 0)
     L.call("pa_gemm_bf16_pp_splitk", L.ptr(a), L.ptr(b), L.ptr(out), M, N, K, lda, ldb, out.stride(0), int(ak),
-           int(bk), EPI_OUT_F32 if out_dtype == torch.float32 else 0, 1.0, int(splits), L.ptr(ws), L.stream_ptr())
+           int(bk), flags, 1.0, int(splits), L.ptr(ws), L.stream_ptr())
     return out
 
 

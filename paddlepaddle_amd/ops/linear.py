@@ -246,8 +246,13 @@ def _wgrad(x2, dy2, acc=None):
     xt = x2.t()
     if G.supported(xt, dy2):
         key = ("wgrad", xt.shape[0], dy2.shape[1], xt.shape[1], None if acc is None else acc.dtype)
+        # few output tiles over a long K (weights of small layers, many tokens): the split-K ping-pong kernel
+        sk = G.pp_splits(*key[1:4]) if -(-key[1] // 256) * -(-key[2] // 256) < 256 else 0
+        sk = sk if G.gemm_pp_splitk_ok(xt, dy2, sk) and (acc is None or acc.is_contiguous()) else 0
         if acc is None:
             cands = {"blas": lambda: torch.mm(xt, dy2), "hip": lambda: G.gemm(xt, dy2)}
+            if sk:
+                cands["hip_sk"] = lambda: G.gemm_pp_splitk(xt, dy2, sk, dy2.dtype)
         else:
             scratch = []
 
@@ -257,11 +262,18 @@ def _wgrad(x2, dy2, acc=None):
                 return scratch[0]
             cands = {"blas": lambda: _s().addmm_(xt, dy2),
                      "hip": lambda: G.gemm(xt, dy2, out=_s(), accumulate=True)}
+            if sk:
+                cands["hip_sk"] = lambda: G.gemm_pp_splitk(xt, dy2, sk, out=_s(), accumulate=True)
         ch = G.choose(key, cands)
         if ch == "hip":
             if acc is None:
                 return G.gemm(xt, dy2)
             G.gemm(xt, dy2, out=acc, accumulate=True)
+            return acc
+        if ch == "hip_sk":
+            if acc is None:
+                return G.gemm_pp_splitk(xt, dy2, sk, dy2.dtype)
+            G.gemm_pp_splitk(xt, dy2, sk, out=acc, accumulate=True)
             return acc
     if acc is None:
         return torch.mm(xt, dy2)

@@ -27,3 +27,24 @@ def test_pp_splitk_matches_fp32(M, N, K, a_t):
     ref = a.float() @ b.float()
     err = (out.float() - ref).abs().max() / ref.abs().max()
     assert err < 1e-2, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_pp_splitk_accumulate_wgrad(dt):
+    """C += x^T dY on the split-K ping-pong kernel (the linear weight-gradient candidate for few output tiles over
+    many tokens, e.g. GPT-3 1.3B's 2048 x 2048 weights at 32k tokens): accumulated into an existing bf16 / fp32
+    gradient, against the fp32 reference; the linear backward picks it by measured time (ops/linear.py)."""
+    g = torch.Generator(device="cuda").manual_seed(1)
+    M, N, K = 512, 768, 8192
+    x = torch.randn(K, M, device="cuda", dtype=torch.bfloat16, generator=g)
+    dy = torch.randn(K, N, device="cuda", dtype=torch.bfloat16, generator=g)
+    acc = torch.randn(M, N, device="cuda", dtype=dt, generator=g)
+    ref = acc.float() + x.t().float() @ dy.float()
+    sp = G.pp_splits(M, N, K)
+    assert sp > 1 and G.gemm_pp_splitk_ok(x.t(), dy, sp)
+    n0 = L.calls("pa_gemm_bf16_pp_splitk")
+    out = G.gemm_pp_splitk(x.t(), dy, sp, out=acc, accumulate=True)
+    assert out is acc and L.calls("pa_gemm_bf16_pp_splitk") == n0 + 1
+    err = (acc.float() - ref).abs().max() / ref.abs().max()
+    assert err < 1e-2, err
