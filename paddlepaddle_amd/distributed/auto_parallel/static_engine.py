@@ -1556,9 +1556,11 @@ class StaticEngine:
         """Drop the full parameter and gradient buffers: only the shards (and the optimizer state of the shards)
         stay resident until the next step gathers again."""
         from ...framework.tensor import _PARAM_OF
+        from ...ops.linear import unregister_main_grad
         for z in self._zero:
             z["flat"] = z["gflat"] = None
             for p, _shape in z["items"]:
+                unregister_main_grad(p._t)  # the main-grad registration holds a view of the released gradient
                 _PARAM_OF.pop(id(p._t), None)
                 p._t = torch.empty(0, dtype=z["dt"], device=z["dev"])
 

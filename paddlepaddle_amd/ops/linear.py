@@ -174,7 +174,13 @@ def register_main_grad(weight, buffer, on_ready):
     ``on_ready(weight)`` afterwards. Used by GroupShardedEngine for the flat grad buffers."""
     if buffer.shape != weight.shape or buffer.dtype != weight.dtype:
         raise ValueError("main-grad buffer must match the weight's shape and dtype")
-    _MAIN_GRAD[id(weight)] = (weakref.ref(weight), buffer, on_ready)
+    key = id(weight)
+
+    def _drop(ref):  # the weight died: release its buffer view (engines re-create weights, e.g. ZeRO-3 gathers)
+        ent = _MAIN_GRAD.get(key)
+        if ent is not None and ent[0] is ref:
+            del _MAIN_GRAD[key]
+    _MAIN_GRAD[key] = (weakref.ref(weight, _drop), buffer, on_ready)
 
 
 _FUSE_TYPES = ("Linear", "ColumnParallelLinear", "RowParallelLinear", "LlamaRMSNorm", "RMSNorm", "LayerNorm",
