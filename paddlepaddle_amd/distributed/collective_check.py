@@ -15,6 +15,12 @@ raising on the first divergence with both ranks' recent entries. Point-to-point 
 rank a's sends to b must equal b's receives from a.
 
 Enable: ``PADDLE_AMD_CHECK_COLLECTIVES=1`` at init_parallel_env, or ``enable_collective_check()``.
+
+Flight recorder (a hang never reaches the end-of-step check): with ``PADDLE_AMD_COLLECTIVE_TRACE_DIR`` set (or
+``enable_collective_check(trace_dir=...)``) every fingerprint is also appended, flushed, to
+``<dir>/collectives.rank<r>.log`` as it is issued (``<communicator> #<n> <entry>``), so after a hang or a kill the
+per-rank files show where each rank stopped; ``first_divergence(paths)`` / ``tools/collective_trace_diff.py`` name
+the first communicator entry at which two ranks disagree, or the ranks that stopped short.
 """
 from __future__ import annotations
 
@@ -37,6 +43,7 @@ _STATE = {"on": False, "pg": None, "checks": 0}
 _SEQ = {}      # key -> [count, hasher, recent entries]
 _KEEP = 16     # entries kept per key for the divergence report
 _TLS = threading.local()
+_TRACE = {"f": None}
 
 
 @contextlib.contextmanager
@@ -83,8 +90,16 @@ def _record(key, entry):
     s[0] += 1
     s[1].update(entry.encode())
     s[2].append(f"#{s[0]} {entry}")
+    f = _TRACE["f"]
+    if f is not None:
+        f.write(f"{_key_str(key)} #{s[0]} {entry}\n")
+        f.flush()
     if len(s[2]) > _KEEP:
         del s[2][0]
+
+
+def _key_str(key):
+    return f"{key[0]}:{'-'.join(str(r) for r in key[1])}" if key[0] == "coll" else f"p2p:{key[1]}>{key[2]}"
 
 
 def _fingerprint(name, args, kwargs):
@@ -120,11 +135,16 @@ def _wrap(name, fn):
     return w
 
 
-def enable_collective_check():
+def enable_collective_check(trace_dir=None):
     """Fingerprint every torch.distributed collective from here on (wraps whatever is installed: composes with
-    the comm watchdog) and create the private gloo group the checks run on."""
+    the comm watchdog) and create the private gloo group the checks run on. ``trace_dir`` (default
+    ``$PADDLE_AMD_COLLECTIVE_TRACE_DIR``): also append every fingerprint to this rank's flight-recorder file."""
     if not dist.is_initialized():
         raise RuntimeError("enable_collective_check: call init_parallel_env first")
+    trace_dir = trace_dir or os.environ.get("PADDLE_AMD_COLLECTIVE_TRACE_DIR")
+    if trace_dir and _TRACE["f"] is None:
+        os.makedirs(trace_dir, exist_ok=True)
+        _TRACE["f"] = open(os.path.join(trace_dir, f"collectives.rank{dist.get_rank()}.log"), "a", buffering=1)
     if _STATE["pg"] is None:
         _STATE["pg"] = dist.new_group(backend="gloo")  # collective over the world: every rank calls this
     if not _STATE.get("atexit"):
@@ -149,6 +169,9 @@ def enable_collective_check():
 
 def disable_collective_check():
     _STATE["on"] = False
+    if _TRACE["f"] is not None:
+        _TRACE["f"].close()
+        _TRACE["f"] = None
     for n, f in _ORIG.items():
         setattr(dist, n, f)
     _ORIG.clear()
@@ -197,3 +220,43 @@ def check_collectives(where="step"):
 def maybe_enable_from_env():
     if os.environ.get("PADDLE_AMD_CHECK_COLLECTIVES", "0") not in ("", "0", "false", "False"):
         enable_collective_check()
+
+
+def first_divergence(paths):
+    """Compare flight-recorder files (``collectives.rank<r>.log``, one per rank): for every communicator, the first
+    entry index at which its members' logs differ, and members whose log ends earlier than their peers' (the ranks
+    a hang left behind). Returns a list of human-readable findings (empty: the logs agree)."""
+    import re
+    logs = {}
+    for p in paths:
+        m = re.search(r"rank(\d+)", os.path.basename(p))
+        r = int(m.group(1)) if m else len(logs)
+        per = {}
+        with open(p) as f:
+            for line in f:
+                k, _, rest = line.rstrip("\n").partition(" ")
+                per.setdefault(k, []).append(rest.split(" ", 1)[1] if " " in rest else rest)
+        logs[r] = per
+    out = []
+    keys = sorted({k for per in logs.values() for k in per})
+    for k in keys:
+        if k.startswith("coll:"):
+            members = [int(x) for x in k[5:].split("-") if x.lstrip("-").isdigit()]
+        else:
+            a, b = k[4:].split(">")
+            members = [int(a), int(b)]
+        seqs = {r: logs.get(r, {}).get(k, []) for r in members if r in logs}
+        if len(seqs) < 2:
+            continue
+        n = min(len(v) for v in seqs.values())
+        for i in range(n):
+            if len({v[i] for v in seqs.values()}) > 1:
+                out.append(f"{k} entry #{i + 1}: " + "; ".join(f"rank {r}: {v[i]}" for r, v in sorted(seqs.items())))
+                break
+        else:
+            longest = max(len(v) for v in seqs.values())
+            short = [r for r, v in sorted(seqs.items()) if len(v) < longest]
+            if short:
+                out.append(f"{k}: ranks {short} stopped after {n} of {longest} entries (next expected: "
+                           f"{next(v for v in seqs.values() if len(v) == longest)[n]})")
+    return out

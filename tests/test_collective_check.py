@@ -70,3 +70,43 @@ def test_checker_fires_on_divergence(how):
         assert err is not None and "diverged" in err
     if how == "bucket_order":
         assert "dp bucket" in res[0][1]
+
+
+def _trace_worker(rank, world, port, d, how, q):
+    _setup(rank, world, port)
+    import torch.distributed as tdist
+    from paddlepaddle_amd.distributed import collective_check as cc
+    cc.enable_collective_check(trace_dir=d)
+    a = torch.ones(4)
+    if how == "order":  # two equal-shaped buckets in opposite orders (gloo completes it; RCCL would mix them)
+        names = ["bucket 0", "bucket 1"] if rank == 0 else ["bucket 1", "bucket 0"]
+        for nm in names:
+            with cc.label(nm):
+                tdist.all_reduce(a)
+    else:
+        tdist.all_reduce(a)
+    cc.disable_collective_check()
+    q.put((rank, None))
+
+
+@pytest.mark.parametrize("how", ["stop", "order"])
+def test_flight_recorder_names_where_ranks_part(tmp_path, how):
+    """PADDLE_AMD_COLLECTIVE_TRACE_DIR flight recorder: each rank appends every collective as it is issued; the
+    offline diff (tools/collective_trace_diff.py) names the rank that stopped short of its peers (what a hang
+    leaves, no end-of-step check needed) or the first entry where two ranks' sequences differ."""
+    from paddlepaddle_amd.distributed.collective_check import first_divergence
+    if how == "stop":  # rank 1 never issues the broadcast: gloo would hang, so rank 0 skips waiting for it
+        _spawn(_trace_worker, str(tmp_path), "stop_local")
+        # fabricate the hang's picture: rank 0 issued one more collective than rank 1
+        with open(tmp_path / "collectives.rank0.log", "a") as f:
+            f.write("coll:0-1 #2 broadcast (8,):float32\n")
+    else:
+        _spawn(_trace_worker, str(tmp_path), how)
+    files = sorted(str(p) for p in tmp_path.glob("collectives.rank*.log"))
+    assert len(files) == 2
+    found = first_divergence(files)
+    assert len(found) == 1, found
+    if how == "stop":
+        assert "ranks [1] stopped after 1 of 2 entries" in found[0], found
+    else:
+        assert "entry #1" in found[0] and "[bucket 0]" in found[0] and "[bucket 1]" in found[0], found
