@@ -310,7 +310,9 @@ def llama_static_bench(args, paddle, world, dist_on):
     log(f"[llama-static] {args.model} pp{pp} tp{tp} dp{dp}: loss={float(state['loss']):.4f} "
         f"step={dt / args.steps * 1000:.1f}ms tokens/s={tps:.0f} MFU={mfu * 100:.1f}% peak_mem={mem:.1f}GiB "
         f"params={cfg.num_params() / 1e9:.2f}B passes={getattr(eng, 'pass_stats', {})} "
-        f"recompute_segments={getattr(eng, 'n_segments', 0)} fused_grad_params={getattr(eng, 'fused_grads', 0)}")
+        f"recompute_segments={getattr(eng, 'n_segments', 0)} fused_grad_params={getattr(eng, 'fused_grads', 0)} "
+        f"native_stages={ {k: (v.num_native, v.num_py, v.num_instructions, v.runs) for k, v in getattr(eng, '_native', {}).items()} } "
+        f"native_reason={getattr(eng, 'native_reason', {})}")
     return tps, dt / args.steps * 1000, gb, mfu
 
 

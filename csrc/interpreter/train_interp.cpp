@@ -21,6 +21,7 @@
 #include <torch/csrc/autograd/custom_function.h>
 #include <torch/csrc/autograd/autograd.h>
 #include <torch/csrc/jit/python/pybind_utils.h>
+#include <torch/csrc/autograd/python_variable.h>
 #include <ATen/core/dispatch/Dispatcher.h>
 #include <c10/hip/HIPStream.h>
 #include <c10/hip/HIPGuard.h>
@@ -713,7 +714,7 @@ bool bn_ok(const at::Tensor& x2, const at::Tensor& w, const at::Tensor& b, const
 }
 
 // ------------------------------------------------------------------------------------------------ program
-enum Kind : int { kAten = 0, kLinear, kLinearNT, kNorm, kFlash, kFlashQKV, kSoftmaxCE, kConv, kBN, kAlias, kComm };
+enum Kind : int { kAten = 0, kLinear, kLinearNT, kNorm, kFlash, kFlashQKV, kSoftmaxCE, kConv, kBN, kAlias, kComm, kPy };
 
 enum ArgKind : int { kSlot = 0, kSlotList = 1, kConst = 2, kRunDevice = 3, kOptSlotList = 4 };
 
@@ -824,6 +825,20 @@ class TrainProgram {
     I.kind = kComm;
     I.name = name;
     I.in = std::move(slots);
+    I.ia = {static_cast<int64_t>(comm_fns_.size())};
+    comm_fns_.push_back(std::move(fn));
+    code_.push_back(std::move(I));
+  }
+
+  // an op run through Python (an op of this framework the native kinds do not cover, a collective with autograd
+  // semantics of a partitioned program): fn(*operand tensors) -> tensor / sequence of tensors into ``outs``;
+  // autograd records whatever the op records
+  void add_py(py::object fn, std::vector<int> in, std::vector<int> outs, const std::string& name) {
+    Instr I;
+    I.kind = kPy;
+    I.name = name;
+    I.in = std::move(in);
+    for (int o : outs) I.outs.push_back({o});
     I.ia = {static_cast<int64_t>(comm_fns_.size())};
     comm_fns_.push_back(std::move(fn));
     code_.push_back(std::move(I));
@@ -950,6 +965,37 @@ class TrainProgram {
   }
 
   int64_t num_instructions() const { return static_cast<int64_t>(code_.size()); }
+  // forward only, autograd recording (a pipeline stage's micro-batch: the caller runs the backward): the fetch slots'
+  // values with their autograd history; intermediates released after their last reader
+  std::vector<at::Tensor> forward(const std::vector<std::pair<int, at::Tensor>>& feeds) {
+    for (const auto& f : feeds) slots_.at(f.first) = f.second;
+    phase_ = 0;
+    done_ = 0;
+    {
+      at::AutoGradMode grad_mode(true);
+      for (size_t n = 0; n < code_.size(); ++n) {
+        if (code_[n].kind == kComm) {
+          exec_comm(code_[n]);
+        } else {
+          wait_pending(n);
+          exec(code_[n]);
+        }
+        done_ = static_cast<int64_t>(n) + 1;
+        for (int s : release_[n]) slots_[s] = at::Tensor();
+      }
+      join_comm();
+    }
+    std::vector<at::Tensor> out;
+    for (int s : fetch_) out.push_back(slots_[s]);
+    for (const auto& f : feeds) slots_[f.first] = at::Tensor();
+    for (int s : fetch_) {
+      bool persistent = false;
+      for (int p : persistent_) persistent |= p == s;
+      if (!persistent) slots_[s] = at::Tensor();
+    }
+    return out;
+  }
+
   int64_t num_comm() const {
     int64_t n = 0;
     for (const auto& I : code_) n += I.kind == kComm;
@@ -967,7 +1013,7 @@ class TrainProgram {
   int64_t done() const { return done_; }
   int64_t num_native() const {
     int64_t n = 0;
-    for (const auto& I : code_) n += I.kind != kAten && I.kind != kAlias && I.kind != kComm;
+    for (const auto& I : code_) n += I.kind != kAten && I.kind != kAlias && I.kind != kComm && I.kind != kPy;
     return n;
   }
 
@@ -1217,6 +1263,24 @@ class TrainProgram {
                       .view(x.sizes()));
         break;
       }
+      case kPy: {
+        py::gil_scoped_acquire gil;
+        py::tuple args(I.in.size());
+        for (size_t i = 0; i < I.in.size(); ++i)
+          args[i] = I.in[i] >= 0 && slots_.at(I.in[i]).defined() ? py::cast(slots_.at(I.in[i])) : py::none();
+        py::object r = comm_fns_.at(I.ia[0])(*args);
+        if (THPVariable_Check(r.ptr())) {
+          put(I, 0, THPVariable_Unpack(r.ptr()));
+        } else if (py::isinstance<py::tuple>(r) || py::isinstance<py::list>(r)) {
+          auto seq = r.cast<py::sequence>();
+          for (size_t k = 0; k < seq.size() && k < I.outs.size(); ++k) {
+            py::object e = seq[k];
+            if (THPVariable_Check(e.ptr())) put(I, k, THPVariable_Unpack(e.ptr()));
+          }
+        }
+        count("py");
+        break;
+      }
       default: throw std::runtime_error("native train executor: bad instruction " + I.name);
     }
   }
@@ -1251,6 +1315,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("add_aten", &TrainProgram::add_aten)
       .def("add_native", &TrainProgram::add_native)
       .def("add_comm", &TrainProgram::add_comm)
+      .def("add_py", &TrainProgram::add_py)
+      .def("forward", &TrainProgram::forward, py::arg("feeds"), py::call_guard<py::gil_scoped_release>())
       .def("bind", &TrainProgram::bind)
       .def("set_loss", &TrainProgram::set_loss)
       .def("set_grad_hook", &TrainProgram::set_grad_hook)

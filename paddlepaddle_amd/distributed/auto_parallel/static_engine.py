@@ -1800,11 +1800,16 @@ class StaticEngine:
                 t.requires_grad_(True)
             env[slot] = t
             received.append((slot, t))
-        for it in self.stage_items[s]:
-            if isinstance(it, _Seg):
-                self._run_segment(it, env)
-            else:
-                self._run_nodes((it,), env)
+        nat = self._native_stage(s)
+        if nat is not None:  # the stage's ops as one native-executor call (distributed/auto_parallel/native_stage.py)
+            env.update(nat.forward(env))
+        else:
+            for it in self.stage_items[s]:
+                if isinstance(it, _Seg):
+                    self._run_segment(it, env)
+                else:
+                    self._run_nodes((it,), env)
+            self._maybe_compile_native(s, env)
         sent = []
         for slot, dsts in sorted(self.sends[s].items()):
             t = env[slot]
@@ -1813,6 +1818,41 @@ class StaticEngine:
             sent.append((slot, t, sorted(dsts)))
         loss = env.get(self.loss_slot) if self.slot_stage.get(self.loss_slot) == s else None
         return received, sent, loss
+
+    # ---------------------------------------------------------------- native stage execution
+    def _native_mode(self):
+        from ...framework.flags import flag
+        mode = str(flag("FLAGS_static_engine_native", "auto")).lower()
+        if mode in ("0", "off", "false") or self.schedule in ("ZBH1", "ZBVPP"):
+            return None  # zero-bubble schedules defer weight gradients in ops/linear.py (Python linears)
+        return mode
+
+    def _native_stage(self, s):
+        st = getattr(self, "_native", None)
+        return st.get(s) if st else None
+
+    def _maybe_compile_native(self, s, env):
+        """After a stage's first Python micro-batch: lower it onto the native executor (its values give the
+        shapes); the reason it did not lower is kept in ``native_reason[s]``."""
+        mode = self._native_mode()
+        if mode is None:
+            return
+        self.__dict__.setdefault("_native", {})
+        reasons = self.__dict__.setdefault("native_reason", {})
+        if s in reasons or s in self._native:
+            return
+        dev = next((v.device for v in env.values() if isinstance(v, torch.Tensor)), torch.device("cpu"))
+        if mode == "auto" and dev.type != "cuda":
+            reasons[s] = "CPU (FLAGS_static_engine_native=force lowers CPU stages too)"
+            return
+        from .native_stage import compile_stage
+        fetch = sorted(self.sends[s])
+        if self.slot_stage.get(self.loss_slot) == s:
+            fetch.append(self.loss_slot)
+        nat, why = compile_stage(self, s, env, fetch)
+        reasons[s] = why
+        if nat is not None:
+            self._native[s] = nat
 
     def _backward_mb(self, mb, state, p2p):
         received, sent, loss = state

@@ -35,6 +35,7 @@ _FLAGS = {
     "FLAGS_layout_autotune": False,
     "FLAGS_dataloader_autotune": False,
     "FLAGS_dataloader_tuning_steps": 8,
+    "FLAGS_static_engine_native": "auto",  # static auto-parallel stages on the native executor: auto (GPU) / force / 0
     "FLAGS_linear_wt_cache_mb": 0,        # [out,in] weight copies for TN-form forward GEMMs (0 = off;
                                           # measured no net gain on the 13B step, see ops/linear.py)
 }

@@ -29,7 +29,7 @@ def _cfg():
 
 
 def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap=False, zero=False, checkpoints=None,
-            gm=1, refined=None, vpp=1):
+            gm=1, refined=None, vpp=1, native=False):
     paddle = _setup(rank, world, port)
     import paddlepaddle_amd.distributed as dist
     from paddlepaddle_amd.models.llama_auto import LlamaForCausalLMAuto, LlamaPretrainingCriterionAuto
@@ -116,8 +116,24 @@ def _worker(rank, world, port, shape, acc, schedule, q, recompute=False, overlap
         segs = [it for it in eng.stage_items[eng.my_stage] if isinstance(it, _Seg)]
         assert len(segs) == cfg.num_hidden_layers // pp, len(segs)
         assert all(len(sg.outputs) == 1 for sg in segs), [sg.outputs for sg in segs]
+    if native:  # every stage of this rank lowered after its first micro-batch and ran natively afterwards
+        mine = [vs for vs in range(len(eng.stage_nodes)) if vs % pp == eng.my_stage]
+        assert all(eng.native_reason.get(vs) is None for vs in mine), eng.native_reason
+        nat = [eng._native[vs] for vs in mine]
+        assert all(n.runs == STEPS * acc - 1 for n in nat), [n.runs for n in nat]
+        assert sum(n.num_native for n in nat) > 0 and sum(n.num_py for n in nat) > 0
     q.put((rank, losses, kinds, eng.my_stage))
     paddle.distributed.barrier()
+
+
+def _worker_native(rank, world, port, shape, acc, schedule, q):
+    """The engine's stage programs on the native executor (FLAGS_static_engine_native=force lowers CPU stages)."""
+    import paddlepaddle_amd as paddle
+    paddle.set_flags({"FLAGS_static_engine_native": "force"})
+    vpp = 2 if schedule == "VPP" else 1
+    if vpp > 1:
+        _EXTRA["virtual_pp_degree"] = 2
+    _worker(rank, world, port, shape, acc, schedule, q, vpp=vpp, native=True)
 
 
 def _worker_vpp(rank, world, port, shape, acc, schedule, q):
@@ -361,6 +377,25 @@ def test_static_engine_vpp_matches_single_process(shape, acc, schedule):
     finally:
         _EXTRA.clear()
     res = _spawn(_worker_vpp, shape, acc, schedule, world=int(np.prod(shape)))
+    for rank, losses, kinds, stage in res:
+        np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-5, err_msg=f"rank {rank} stage {stage}")
+
+
+@pytest.mark.parametrize("shape,acc,schedule", [((1, 1, 2), 2, "1F1B"), ((2, 1, 2), 4, "1F1B"),
+                                                ((1, 2, 2), 2, "FThenB"), ((2, 1, 1), 4, "VPP")])
+def test_static_engine_native_stage_execution(shape, acc, schedule):
+    """Each rank's partitioned stage program runs on the native training executor after its first micro-batch
+    (hot ops as native instructions, collectives / other ops of this framework as Python-call instructions, torch
+    ops as ATen calls; distributed/auto_parallel/native_stage.py): the same losses as single-process training
+    at TP2, PP2 x TP2, DP2 x TP2 and PP2 x VPP2 (reference: the engine runs the partitioned program on the
+    standalone executor, auto_parallel/static/engine.py)."""
+    if schedule == "VPP":
+        _EXTRA["virtual_pp_degree"] = 2
+    try:
+        ref = _reference()
+    finally:
+        _EXTRA.clear()
+    res = _spawn(_worker_native, shape, acc, schedule, world=int(np.prod(shape)))
     for rank, losses, kinds, stage in res:
         np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-5, err_msg=f"rank {rank} stage {stage}")
 
