@@ -22,7 +22,6 @@ from __future__ import annotations
 
 import torch
 
-from ...static import program as P
 from ...static import native_train as NT
 
 __all__ = ["compile_stage", "NativeStage"]
@@ -91,7 +90,9 @@ def compile_stage(eng, s, env, fetch):
         for k, v in env.items():
             if isinstance(v, torch.Tensor):
                 metas[k] = torch.empty_like(v, device="meta").requires_grad_(v.requires_grad)
-    low = NT._Lowering(_StageProg(metas), env[next(iter(env))].device if env else torch.device("cpu"), True)
+    dev = next((v.device for v in env.values() if isinstance(v, torch.Tensor)), torch.device("cpu"))
+    gpu = dev.type == "cuda"  # the native kinds launch HIP kernels: on CPU every op of ours is a Python call
+    low = NT._Lowering(_StageProg(metas), dev, gpu)
     produced = set()
     n_native = n_py = 0
     try:
@@ -102,7 +103,7 @@ def compile_stage(eng, s, env, fetch):
                 if nd.outs is None:
                     return None, f"in-place op {nd.name}"
                 ours = nd.name.startswith("o:")
-                if not _has_engine_tmpl((nd.args, nd.kwargs)) and ours and low.lower_native(node):
+                if gpu and not _has_engine_tmpl((nd.args, nd.kwargs)) and ours and low.lower_native(node):
                     n_native += 1
                 elif ours or _has_engine_tmpl((nd.args, nd.kwargs)) or not nd.name.startswith(("f:", "m:", "p:")):
                     fn, sa, a, sk, k, _oi, _o = eng._compile_node(nd)
