@@ -89,7 +89,10 @@ def compile_stage(eng, s, env, fetch):
         metas = [None] * top
         for k, v in env.items():
             if isinstance(v, torch.Tensor):
-                metas[k] = torch.empty_like(v, device="meta").requires_grad_(v.requires_grad)
+                # the exact strides (views such as the q / k / v slices of a fused projection are not dense): an op
+                # replayed on the meta decides view vs copy the way it will at run time
+                metas[k] = torch.empty_strided(v.size(), v.stride(), dtype=v.dtype,
+                                               device="meta").requires_grad_(v.requires_grad)
     dev = next((v.device for v in env.values() if isinstance(v, torch.Tensor)), torch.device("cpu"))
     gpu = dev.type == "cuda"  # the native kinds launch HIP kernels: on CPU every op of ours is a Python call
     low = NT._Lowering(_StageProg(metas), dev, gpu)
