@@ -803,13 +803,42 @@ class _Conv3dNDHWC(torch.autograd.Function):
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         stride, pads, dil, has_b = ctx.cfg
+        dy = dy.contiguous()
         mask = [ctx.needs_input_grad[0], ctx.needs_input_grad[1], has_b and ctx.needs_input_grad[2]]
-        gi, gw, gb = torch.ops.aten.convolution_backward(
+        gi = None
+        if mask[0] and _dgrad3d_own_ok(x, w, stride, pads, dil):
+            key = ("conv3d", tuple(x.shape), tuple(w.shape), stride, pads, dil)
+            ch = _pick(key, lambda: _dgrad3d_own(dy, w, pads, dil), lambda: _dgrad3d_mi(dy, x, w, stride, pads, dil))
+            gi = _dgrad3d_own(dy, w, pads, dil) if ch == "hip" else _dgrad3d_mi(dy, x, w, stride, pads, dil)
+            mask[0] = False
+        gi2, gw, gb = torch.ops.aten.convolution_backward(
             dy.permute(0, 4, 1, 2, 3), x.permute(0, 4, 1, 2, 3), w, [w.shape[0]] if has_b else None, [stride] * 3,
-            list(pads), [dil] * 3, False, [0, 0, 0], 1, mask)
-        if gi is not None:
-            gi = gi.permute(0, 2, 3, 4, 1).contiguous()
+            list(pads), [dil] * 3, False, [0, 0, 0], 1, mask) if any(mask) else (None, None, None)
+        if gi2 is not None:
+            gi = gi2.permute(0, 2, 3, 4, 1).contiguous()
         return gi, gw, gb, None, None, None
+
+
+def _dgrad3d_own_ok(x, w, stride, pads, dil):
+    """Stride-1 data gradient as a forward convolution of dY (Cout channels in) on the implicit GEMM: the kernel's
+    input-channel tile needs Cout % 64, its output C % 8, and the mirrored padding dil (K - 1) - p >= 0."""
+    if stride != 1 or not L.has("pa_conv3d_ndhwc_fwd") or w.shape[0] % 64 or x.shape[4] % 8:
+        return False
+    return all(dil * (k - 1) - p >= 0 for k, p in zip(w.shape[2:], pads))
+
+
+def _dgrad3d_own(dy, w, pads, dil):
+    """dX = conv3d(dY, W flipped in every tap dim with in / out channels swapped, padding dil (K - 1) - p), NDHWC."""
+    wf = w.flip(2, 3, 4).transpose(0, 1)  # [C, Cout, KD, KH, KW]
+    pd = tuple(dil * (k - 1) - p for k, p in zip(w.shape[2:], pads))
+    return _conv3d_own(dy, wf, None, 1, pd, dil)
+
+
+def _dgrad3d_mi(dy, x, w, stride, pads, dil):
+    gi = torch.ops.aten.convolution_backward(
+        dy.permute(0, 4, 1, 2, 3), x.permute(0, 4, 1, 2, 3), w, None, [stride] * 3, list(pads), [dil] * 3, False,
+        [0, 0, 0], 1, [True, False, False])[0]
+    return gi.permute(0, 2, 3, 4, 1).contiguous()
 
 
 def conv3d_ndhwc_ok(x, w, groups, stride, pads, dil):
@@ -822,6 +851,7 @@ def conv3d_ndhwc_ok(x, w, groups, stride, pads, dil):
 
 
 def conv3d_ndhwc(x, w, b, stride, pads, dil):
-    """NDHWC 3-D convolution: forward on the faster of the hand-written implicit GEMM and MIOpen (timed per shape),
-    both gradients on MIOpen."""
+    """NDHWC 3-D convolution: forward, and the stride-1 data gradient (a forward convolution of dY with the flipped,
+    in/out-swapped filter), each on the faster of the hand-written implicit GEMM and MIOpen (timed per shape); the
+    weight gradient on MIOpen."""
     return _Conv3dNDHWC.apply(x, w, b, int(stride), tuple(int(p) for p in pads), int(dil))

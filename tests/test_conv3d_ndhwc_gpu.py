@@ -51,3 +51,24 @@ def test_conv3d_functional_ndhwc_forward_and_backward():
     assert _rel(y._t, yr.permute(0, 2, 3, 4, 1).detach()) < 2e-2
     assert _rel(xt.grad._t, xr.grad.permute(0, 2, 3, 4, 1)) < 3e-2
     assert _rel(wt.grad._t, wr.grad) < 3e-2
+
+
+@pytest.mark.parametrize("cin,cout,k,pad", [(64, 64, 3, 1), (96, 128, 3, 1), (64, 64, 1, 0), (32, 64, 3, 0)])
+def test_conv3d_data_gradient_on_implicit_gemm(cin, cout, k, pad):
+    """Stride-1 data gradient on the hand-written kernel: dY convolved with the flipped, in/out-swapped filter
+    (padding K - 1 - p) against PyTorch fp32 conv3d's input gradient."""
+    g = torch.Generator(device="cuda").manual_seed(cin + cout + k)
+    x = torch.randn(2, 6, 10, 10, cin, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(cout, cin, k, k, k, device="cuda", generator=g) / (cin * k ** 3) ** 0.5).bfloat16()
+    Do = 6 + 2 * pad - (k - 1)
+    Ho = 10 + 2 * pad - (k - 1)
+    dy = torch.randn(2, Do, Ho, Ho, cout, device="cuda", generator=g).bfloat16()
+    assert C._dgrad3d_own_ok(x, w, 1, (pad,) * 3, 1)
+    L.reset_calls()
+    gi = C._dgrad3d_own(dy, w, (pad,) * 3, 1)
+    assert L.calls("pa_conv3d_ndhwc_fwd") == 1
+    xr = x.float().permute(0, 4, 1, 2, 3).requires_grad_(True)
+    torch.nn.functional.conv3d(xr, w.float(), None, 1, pad).backward(dy.float().permute(0, 4, 1, 2, 3))
+    ref = xr.grad.permute(0, 2, 3, 4, 1)
+    assert tuple(gi.shape) == tuple(ref.shape)
+    assert _rel(gi, ref) < 2e-2
