@@ -14,9 +14,10 @@ micro-batch ran in Python, into one TrainProgram whose ``forward`` runs the micr
   * torch-level ops become boxed ATen dispatcher calls captured on meta tensors of the shapes the first
     micro-batch produced.
 
-The backward stays the caller's (torch autograd over what the instructions recorded); p2p sends / receives and the
-schedule stay in the engine. Stages with recompute segments and the zero-bubble schedules (whose deferred
-weight gradients live in ops/linear.py) keep the Python replay.
+Recompute segments are one Python-call instruction each (the engine's checkpointed run of the segment). The
+backward stays the caller's (torch autograd over what the instructions recorded); p2p sends / receives and the
+schedule stay in the engine. The zero-bubble schedules (whose deferred weight gradients live in ops/linear.py) keep
+the Python replay.
 """
 from __future__ import annotations
 
@@ -82,8 +83,6 @@ def compile_stage(eng, s, env, fetch):
         return None, "_C_train not built"
     from .static_engine import _Seg, _flat_tensor_refs
     items = eng.stage_items[s]
-    if any(isinstance(it, _Seg) for it in items):
-        return None, "recompute segments"
     with torch._C.DisableTorchFunction():
         top = max([k for k in env] + [0]) + 1
         metas = [None] * top
@@ -101,6 +100,15 @@ def compile_stage(eng, s, env, fetch):
     try:
         with NT._NoTrace():
             for nd in items:
+                if isinstance(nd, _Seg):  # a recompute segment: one Python call of the engine's checkpointed run
+                    def seg_call(*ts, seg=nd):
+                        e = dict(zip(seg.inputs, ts))
+                        eng._run_segment(seg, e)
+                        return tuple(e[o] for o in seg.outputs)
+                    low.instrs.append(("py", seg_call, list(nd.inputs), list(nd.outputs), "recompute_segment"))
+                    produced.update(nd.outputs)
+                    n_py += 1
+                    continue
                 node = _Node(nd)
                 outs = [r.i for r in _flat_tensor_refs(nd.outs, [])] if nd.outs is not None else []
                 if nd.outs is None:

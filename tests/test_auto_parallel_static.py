@@ -133,7 +133,7 @@ def _worker_native(rank, world, port, shape, acc, schedule, q):
     vpp = 2 if schedule == "VPP" else 1
     if vpp > 1:
         _EXTRA["virtual_pp_degree"] = 2
-    _worker(rank, world, port, shape, acc, schedule, q, vpp=vpp, native=True)
+    _worker(rank, world, port, shape, acc, schedule, q, vpp=vpp, native=True, recompute=schedule == "FThenB")
 
 
 def _worker_vpp(rank, world, port, shape, acc, schedule, q):
@@ -387,8 +387,9 @@ def test_static_engine_native_stage_execution(shape, acc, schedule):
     """Each rank's partitioned stage program runs on the native training executor after its first micro-batch
     (hot ops as native instructions, collectives / other ops of this framework as Python-call instructions, torch
     ops as ATen calls; distributed/auto_parallel/native_stage.py): the same losses as single-process training
-    at TP2, PP2 x TP2, DP2 x TP2 and PP2 x VPP2 (reference: the engine runs the partitioned program on the
-    standalone executor, auto_parallel/static/engine.py)."""
+    at TP2, PP2 x TP2, DP2 x TP2 (with recompute: each checkpointed decoder layer one Python-call instruction) and
+    PP2 x VPP2 (reference: the engine runs the partitioned program on the standalone executor,
+    auto_parallel/static/engine.py)."""
     if schedule == "VPP":
         _EXTRA["virtual_pp_degree"] = 2
     try:
