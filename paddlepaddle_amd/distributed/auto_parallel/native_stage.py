@@ -16,8 +16,8 @@ micro-batch ran in Python, into one TrainProgram whose ``forward`` runs the micr
 
 Recompute segments are one Python-call instruction each (the engine's checkpointed run of the segment). The
 backward stays the caller's (torch autograd over what the instructions recorded); p2p sends / receives and the
-schedule stay in the engine. The zero-bubble schedules (whose deferred weight gradients live in ops/linear.py) keep
-the Python replay.
+schedule stay in the engine. Under the zero-bubble schedules the linears stay Python calls (their deferred
+weight-gradient GEMMs live in ops/linear.py).
 """
 from __future__ import annotations
 
@@ -74,10 +74,11 @@ class NativeStage:
         return dict(zip(self.fetch, outs))
 
 
-def compile_stage(eng, s, env, fetch):
+def compile_stage(eng, s, env, fetch, python_linears=False):
     """Lower virtual stage ``s`` of engine ``eng`` using the values its first micro-batch left in ``env`` (their
-    shapes / dtypes); ``fetch``: the slots the engine reads after the stage (sends, loss). Returns
-    (NativeStage, None) or (None, reason)."""
+    shapes / dtypes); ``fetch``: the slots the engine reads after the stage (sends, loss); ``python_linears``: the
+    linears stay Python-call instructions (the zero-bubble schedules defer their weight-gradient GEMMs through
+    ops/linear.py). Returns (NativeStage, None) or (None, reason)."""
     m = NT._module()
     if m is None:
         return None, "_C_train not built"
@@ -114,7 +115,8 @@ def compile_stage(eng, s, env, fetch):
                 if nd.outs is None:
                     return None, f"in-place op {nd.name}"
                 ours = nd.name.startswith("o:")
-                if gpu and not _has_engine_tmpl((nd.args, nd.kwargs)) and ours and low.lower_native(node):
+                lin = python_linears and nd.name.rsplit(":", 1)[-1] in ("fused_linear", "linear_nt")
+                if gpu and not lin and not _has_engine_tmpl((nd.args, nd.kwargs)) and ours and low.lower_native(node):
                     n_native += 1
                 elif ours or _has_engine_tmpl((nd.args, nd.kwargs)) or not nd.name.startswith(("f:", "m:", "p:")):
                     fn, sa, a, sk, k, _oi, _o = eng._compile_node(nd)

@@ -1823,9 +1823,7 @@ class StaticEngine:
     def _native_mode(self):
         from ...framework.flags import flag
         mode = str(flag("FLAGS_static_engine_native", "auto")).lower()
-        if mode in ("0", "off", "false") or self.schedule in ("ZBH1", "ZBVPP"):
-            return None  # zero-bubble schedules defer weight gradients in ops/linear.py (Python linears)
-        return mode
+        return None if mode in ("0", "off", "false") else mode
 
     def _native_stage(self, s):
         st = getattr(self, "_native", None)
@@ -1849,7 +1847,8 @@ class StaticEngine:
         fetch = sorted(self.sends[s])
         if self.slot_stage.get(self.loss_slot) == s:
             fetch.append(self.loss_slot)
-        nat, why = compile_stage(self, s, env, fetch)
+        # zero-bubble schedules defer the linears' weight gradients in ops/linear.py: those stay Python calls
+        nat, why = compile_stage(self, s, env, fetch, python_linears=self.schedule in ("ZBH1", "ZBVPP"))
         reasons[s] = why
         if nat is not None:
             self._native[s] = nat
