@@ -285,3 +285,26 @@ def test_supplement_explicit_dependencies_orders_collectives():
     main._pa_comm_chain = main._pa_comm_chain[::-1]
     order = [main.nodes[i] for i in P.build_plan(main, [slot]).order if main.nodes[i].kind == "comm"]
     assert order == comm[::-1]
+
+
+def test_auto_parallel_registry_passes():
+    """auto_parallel_gradient_merge_pass (the reference's name), auto_parallel_sequence_parallel_optimization (marks
+    the program for the engine's reduce-scatter reshards) and auto_parallel_pipeline (the job list of the
+    configured schedule, VPP chunks included)."""
+    from paddlepaddle_amd.distributed.passes.pipeline_scheduler import job_pairs
+    main, out = _ffn_program(False)
+    with paddle.static.program_guard(main):
+        paddle.optimizer.SGD(0.1).minimize(out.mean())
+    new_pass("auto_parallel_gradient_merge_pass", {"k_steps": 4, "avg": True}).apply(main, None)
+    assert main._grad_merge == (4, True)
+    ctx = new_pass("auto_parallel_sequence_parallel_optimization").apply(main, None)
+    assert main._pa_sp_opt and ctx.get_attr("auto_parallel_sequence_parallel_optimization.enabled")
+    ctx = new_pass("auto_parallel_pipeline", {"schedule_mode": "1F1B", "num_micro_batches": 4, "pp_stage": 0,
+                                              "pp_degree": 2}).apply(main, None)
+    assert ctx.get_attr("auto_parallel_pipeline.mode") == "1F1B"
+    assert job_pairs(ctx.get_attr("auto_parallel_pipeline.job_list")) == [
+        ("F", 0), ("F", 1), ("B", 0), ("F", 2), ("B", 1), ("F", 3), ("B", 2), ("B", 3)]
+    ctx = new_pass("auto_parallel_pipeline", {"schedule_mode": "VPP", "num_micro_batches": 4, "pp_stage": 1,
+                                              "pp_degree": 2, "vpp_degree": 2}).apply(main, None)
+    jobs = ctx.get_attr("auto_parallel_pipeline.job_list")
+    assert {j.chunk_id() for j in jobs if j.type() == "forward"} == {0, 1}
