@@ -208,3 +208,7 @@ def _maybe_native_allocator():
 from os import environ as _os_env  # noqa: E402
 
 _maybe_native_allocator()
+
+# reference module paths (paddle.x.y.z files) that this framework implements in an enclosing package
+from ._compat_import import install as _install_compat_paths  # noqa: E402
+_install_compat_paths()
