@@ -28,6 +28,34 @@ USER_FACING = {"amp.auto_cast", "distributed.fleet.recompute.recompute", "distri
                "distributed.fleet.meta_parallel.parallel_layers.random", "nn.functional.flash_attention"}
 
 
+# names found in ANOTHER module of this package are bound only where checked by hand to be the same API (a bare
+# name match is not enough: shufflenetv2.InvertedResidual is not mobilenet's, utils.flops.flops is not hapi's)
+SAME_API = {
+    "distributed.fleet.meta_parallel.parallel_layers": {"RNGStatesTracker"},
+    "distributed.fleet.meta_parallel.parallel_layers.random": {"RNGStatesTracker"},
+    "distributed.io": {"is_persistable", "load_persistables", "save_persistables"},
+    "framework.framework": {"get_default_dtype", "set_default_dtype"},
+    "hapi.hub": {"help", "list"},
+    "incubate.autograd.primitives": None,  # every name: the paddle tensor op of that name
+    "incubate.nn.loss": {"identity_loss"},
+    "incubate.nn.memory_efficient_attention": {"memory_efficient_attention"},
+    "jit.api": {"HookRemoveHelper"},
+    "nn.initializer.lazy_init": {"LazyGuard"},
+    "nn.quant.qat": {"QuantedConv2D", "QuantedLinear"},
+    "nn.quant.qat.conv": {"QuantedConv2D"},
+    "nn.quant.qat.linear": {"QuantedLinear"},
+    "optimizer.lbfgs": {"dot"},
+    "quantization.observers.abs_max": {"AbsmaxObserverLayer"},
+    "quantization.observers.groupwise": {"GroupWiseWeightObserverLayer"},
+    "quantization.quanters.abs_max": {"FakeQuanterWithAbsMaxObserverLayer"},
+    "static.amp.debugging": {"collect_operator_stats"},
+    "static.nn.common": {"ExponentialMovingAverage"},
+    "static.nn.metric": {"auc", "ctr_metric_bundle"},
+    "static.nn.sequence_lod": {"sequence_mask"},
+    "tensor.attribute": None,
+}
+
+
 def public_names(path):
     tree = ast.parse(open(path).read())
     alln, defs, reexp = None, [], []
@@ -56,7 +84,21 @@ def main():
     ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference/python/paddle"
     os.environ["PADDLE_AMD_NO_COMPAT_PATHS"] = "1"  # real modules only
     import paddlepaddle_amd  # noqa: F401
-    table = {}
+    table, extra = {}, {}
+    index = {}  # public name -> {module defining the object}
+    for mname, m in list(sys.modules.items()):
+        if not mname.startswith("paddlepaddle_amd") or m is None:
+            continue
+        for n, o in list(vars(m).items()):
+            if n.startswith("_") or isinstance(o, type(sys)):
+                continue
+            om = getattr(o, "__module__", None)
+            if isinstance(om, str) and om.startswith("paddlepaddle_amd") and om == mname:
+                index.setdefault(n, set()).add(mname)
+
+    def elsewhere(n):
+        c = index.get(n, set())
+        return next(iter(c))[len("paddlepaddle_amd."):] if len(c) == 1 else None
     for root, _dirs, files in sorted(os.walk(ref)):
         rel = os.path.relpath(root, ref)
         if any(rel == s or rel.startswith(s + "/") for s in SKIP):
@@ -84,6 +126,12 @@ def main():
             else:
                 continue
             have = sorted({n for n in names if hasattr(anc, n)})
+            for n in sorted(set(names) - set(have)):  # implemented in another module of this package
+                o = elsewhere(n)
+                ok = mod in SAME_API and (SAME_API[mod] is None or n in SAME_API[mod])
+                if o is not None and ok:
+                    extra.setdefault(mod, {})[n] = o
+            have = sorted(set(have) | set(extra.get(mod, {})))
             # every public name implemented, or (partial) at least half of them: the alias exposes what exists and
             # the table lists the rest
             if len(have) == len(set(names)) or (have and (2 * len(have) >= len(set(names)) or mod in USER_FACING)):
@@ -97,6 +145,10 @@ def main():
         for k in sorted(table):
             src, names, _miss = table[k]
             fh.write(f"    {k!r}: ({src!r}, {names!r}),\n")
+        fh.write("}\n\n# names of an alias path implemented in another module of this framework\nEXTRA = {\n")
+        for k in sorted(extra):
+            if k in table:
+                fh.write(f"    {k!r}: {extra[k]!r},\n")
         fh.write("}\n\nMISSING = {\n")
         for k in sorted(table):
             if table[k][2]:
