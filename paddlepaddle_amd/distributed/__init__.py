@@ -15,6 +15,7 @@ from .auto_parallel.intermediate import (parallelize, ColWiseParallel, RowWisePa
                                          SequenceParallelEnd, SequenceParallelEnable, SequenceParallelDisable,
                                          SplitPoint)
 from ..parallel.data_parallel import DataParallel  # noqa: F401,E402
+from .fleet.utils.hybrid_parallel_util import sync_params_buffers  # noqa: F401,E402
 from .extras import *  # noqa: F401,F403,E402
 from . import communicator  # noqa: F401,E402
 from .watchdog import enable_comm_watchdog, disable_comm_watchdog  # noqa: F401,E402

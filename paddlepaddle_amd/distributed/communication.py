@@ -5,6 +5,11 @@ from .collective import (all_reduce, all_gather, broadcast, reduce, reduce_scatt
                          alltoall, alltoall_single, send, recv, isend, irecv, ReduceOp)
 
 
+def is_avg_reduce_op_supported():
+    """ReduceOp.AVG runs natively on RCCL (the DP / sharding paths use it; gloo gets SUM + scale)."""
+    return True
+
+
 from . import comm_stream as stream  # noqa: E402  (explicit sync_op / use_calc_stream semantics)
 
 import sys as _sys  # noqa: E402

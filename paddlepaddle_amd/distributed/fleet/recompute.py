@@ -29,6 +29,51 @@ def _w(x):
     return x
 
 
+def detach_variable(inputs):
+    """Detached copies of the tensors in ``inputs`` (tensors or tuples of tensors; anything else passes through),
+    each keeping its ``stop_gradient`` flag (reference recompute.py:62 — the helper PaddleNLP's own recompute
+    wrappers import)."""
+    def one(t):
+        if not isinstance(t, Tensor):
+            return t
+        d = t.detach()
+        d.stop_gradient = t.stop_gradient
+        return d
+
+    return tuple(tuple(one(i) for i in v) if type(v) is tuple else one(v) for v in inputs)
+
+
+def check_recompute_necessary(inputs):
+    """Warn when no tensor input of a recompute block needs a gradient (recompute.py:98): its backward never
+    runs, so checkpointing it only costs a forward."""
+    flags = []
+    for v in inputs:
+        for t in (v if type(v) is tuple else (v,)):
+            if isinstance(t, Tensor):
+                flags.append(t.stop_gradient)
+    if flags and all(flags):
+        import logging
+        logging.getLogger(__name__).warning(
+            "[Recompute]: none of the inputs of this recompute block needs a gradient; recomputing it in backward "
+            "is unnecessary")
+
+
+@contextlib.contextmanager
+def switch_rng_state_tracker(rng_state, tracker):
+    """Run a block under the given global RNG state and tensor-parallel RNG tracker states, restoring both after
+    (recompute.py:116: a recomputed block redraws the forward's dropout masks)."""
+    from ... import get_rng_state, set_rng_state
+    from ...parallel.tensor_parallel import get_rng_state_tracker
+    orig, orig_tracker = get_rng_state(), get_rng_state_tracker().get_states_tracker()
+    set_rng_state(rng_state)
+    get_rng_state_tracker().set_states_tracker(tracker)
+    try:
+        yield
+    finally:
+        set_rng_state(orig)
+        get_rng_state_tracker().set_states_tracker(orig_tracker)
+
+
 def recompute(function, *args, **kwargs):
     preserve = kwargs.pop("preserve_rng_state", True)
     kwargs.pop("use_reentrant", None)

@@ -132,6 +132,18 @@ def _broadcast_params(model, group, src_rank, skip_distributed, fuse_params=True
                 o += k
 
 
+def sync_params_buffers(model, comm_group=None, src_rank=0, is_model_parallel=False, fuse_params=True):
+    """Broadcast ``model``'s parameters and buffers from ``src_rank`` over ``comm_group`` (world when None), one
+    flat broadcast per dtype when ``fuse_params``; with ``is_model_parallel`` the tensor-parallel shards
+    (``is_distributed``) stay as they are (reference python/paddle/distributed/parallel.py sync_params_buffers)."""
+    if comm_group is None:
+        if not dist.is_initialized() or dist.get_world_size() <= 1:
+            return
+        from ...collective import _get_global_group
+        comm_group = _get_global_group()
+    _broadcast_params(model, comm_group, src_rank, is_model_parallel, fuse_params)
+
+
 def broadcast_mp_parameters(model, hcg, fuse_params=True):
     g = hcg.get_model_parallel_group()
     _broadcast_params(model, g, hcg.get_model_parallel_group_src_rank(), True, fuse_params)
