@@ -46,21 +46,90 @@ def auto_cast(enable=True, custom_white_list=None, custom_black_list=None, level
 amp_guard = auto_cast
 
 
+class AMPGlobalState:
+    """What decorate() recorded for the rest of the run (reference auto_cast.py AMPGlobalState): the decorated
+    models' parameters, whether gradients of low-precision parameters are kept in fp32 (master_grad) and the
+    low-precision dtype."""
+
+    def __init__(self):
+        self.model_parameters = []
+        self.use_master_grad = False
+        self.already_register_final_backward_hook = False
+        self.already_classify_params_meets_need = False
+        self.amp_dtype = "float32"
+
+    def __setattr__(self, name, value):
+        self.__dict__[name] = value
+
+
+_AMP_GLOBAL = AMPGlobalState()
+
+
+def amp_global_state():
+    return _AMP_GLOBAL
+
+
+def amp_state():
+    """The auto_cast state in force (enabled, level, dtype, op lists)."""
+    return STATE
+
+
+def _norm_types():
+    from ..nn.layer.norm import _BatchNormBase, LayerNorm, GroupNorm, _InstanceNormBase
+    return (_BatchNormBase, LayerNorm, GroupNorm, _InstanceNormBase)
+
+
+def need_keep_fp32(layer, dtype):
+    """O2 keeps normalization layers (and layers marked by set_excluded_layers) in fp32."""
+    return isinstance(layer, _norm_types()) or getattr(layer, "_cast_to_low_precision", True) is False
+
+
+def set_excluded_layers(models, excluded_layers):
+    """Mark layers (instances, or every sublayer of the given types) to stay fp32 under O2 decorate."""
+    ms = models if isinstance(models, (list, tuple)) else [models]
+    ex = excluded_layers if isinstance(excluded_layers, (list, tuple)) else [excluded_layers]
+    types_ = tuple(e for e in ex if isinstance(e, type))
+    insts = [e for e in ex if not isinstance(e, type)]
+    for m in ms:
+        for l in m.sublayers(include_self=True):
+            if (types_ and isinstance(l, types_)) or any(l is i for i in insts):
+                for sub in l.sublayers(include_self=True):
+                    object.__setattr__(sub, "_cast_to_low_precision", False)
+
+
+def check_models(models):
+    from ..nn.layer.layers import Layer
+    for m in models:
+        if not isinstance(m, Layer):
+            raise RuntimeError(f"Current train mode is pure fp16, models should be paddle.nn.Layer, but receive "
+                               f"{type(m)}.")
+
+
+def check_optimizers(optimizers):
+    from ..optimizer.optimizer import Optimizer
+    for o in optimizers:
+        if not isinstance(o, Optimizer):
+            raise RuntimeError(f"Current train mode is pure fp16, optimizers should be paddle.optimizer.Optimizer,"
+                               f" but receive {type(o)}.")
+
+
 def decorate(models, optimizers=None, level="O1", dtype="float16", master_weight=None, save_dtype=None,
              master_grad=False, excluded_layers=None):
     """O2: cast model parameters to dtype (norm layers stay fp32) and turn on optimizer master weights."""
-    from ..nn.layer.norm import _BatchNormBase, LayerNorm, GroupNorm, _InstanceNormBase
     single_model = not isinstance(models, (list, tuple))
     ms = [models] if single_model else list(models)
     if level == "O2":
+        check_models(ms)
         td = _dt.to_torch_dtype(dtype)
-        keep = (_BatchNormBase, LayerNorm, GroupNorm, _InstanceNormBase)
         if excluded_layers is not None:
-            ex = excluded_layers if isinstance(excluded_layers, (list, tuple)) else [excluded_layers]
-            keep = keep + tuple(e for e in ex if isinstance(e, type))
+            set_excluded_layers(ms, excluded_layers)
+        g = amp_global_state()
+        g.use_master_grad = bool(master_grad)
+        g.amp_dtype = dtype
         for m in ms:
+            g.model_parameters.extend(m.parameters())
             for l in m.sublayers(include_self=True):
-                if isinstance(l, keep):
+                if need_keep_fp32(l, dtype):
                     continue
                 for p in l._parameters.values():
                     if p is not None and p._t.is_floating_point() and p._t.dtype != td:
@@ -74,6 +143,9 @@ def decorate(models, optimizers=None, level="O1", dtype="float16", master_weight
     if optimizers is None:
         return models
     return models, optimizers
+
+
+amp_decorate = decorate
 
 
 def is_auto_cast_enabled():
