@@ -1,5 +1,5 @@
 """fleet.meta_parallel. Reference: python/paddle/distributed/fleet/meta_parallel/__init__.py."""
-from ....parallel.pipeline import (LayerDesc, SharedLayerDesc, PipelineLayer, PipelineParallel,  # noqa: F401
+from ....parallel.pipeline import (LayerDesc, SharedLayerDesc, PipelineLayer, PipelineParallel, SegmentLayers,  # noqa: F401
                                    PipelineParallelWithInterleave, PipelineParallelWithInterleaveFthenB,
                                    PipelineParallelZeroBubble, PipelineParallelZeroBubbleVPP)
 from ....parallel.segment_parallel import SegmentParallel  # noqa: F401

@@ -19,6 +19,8 @@ ring's wrap edge) can never be mismatched, on gloo or RCCL alike.
 """
 from __future__ import annotations
 
+import re
+
 import math
 
 import torch
@@ -66,6 +68,71 @@ class _SharedCall(nn.Layer):
         return self.fn(self.layer, x)
 
 
+class SegmentLayers:
+    """Stage boundaries of a PipelineLayer's descriptor list (reference pp_layers.py:93 SegmentLayers):
+
+    * ``"uniform"``: equal counts, the remainder going to the LAST parts;
+    * ``"layer:<regex>"``: equal numbers of the descriptors whose class / function name matches the regex
+      (case-insensitive) per part — each boundary right after a part's last matching layer, so leading layers
+      (embedding) join the first part and trailing ones (norm, head) the last; the count must divide evenly;
+    * a list of boundaries (``[0, b1, ..]``; the final ``len(layers)`` may be left out).
+
+    With ``num_virtual_pipeline_stage`` the list is cut into num_parts x that many chunks."""
+
+    def __init__(self, layers_desc, num_parts, method="uniform", num_virtual_pipeline_stage=None):
+        self._layers_desc = list(layers_desc)
+        self.method = method
+        self.num_parts = num_parts
+        self.num_items = len(self._layers_desc)
+        self.num_virtual_pipeline_stage = num_virtual_pipeline_stage
+        self.total_parts = num_parts * (num_virtual_pipeline_stage or 1)
+        if self.num_items < self.num_parts:
+            raise ValueError(f"{self.num_items} layers cannot be split into {self.num_parts} pipeline stages")
+
+    def do_segment(self):
+        m = self.method
+        if isinstance(m, (list, tuple)):
+            b = [int(x) for x in m]
+            if not b or b[0] != 0 or any(x < 0 or x > self.num_items for x in b) or b != sorted(b):
+                raise ValueError(f"seg_method {list(m)}: boundaries must start at 0, ascend and stay <= "
+                                 f"{self.num_items}")
+            if len(b) == self.total_parts:  # last boundary left out
+                b.append(self.num_items)
+            if len(b) != self.total_parts + 1:
+                raise ValueError(f"seg_method {list(m)} has {len(b) - 1} parts, {self.total_parts} needed")
+            return b
+        if m == "uniform":
+            return self.uniform(self.num_items, self.total_parts)
+        if isinstance(m, str) and m.startswith("layer:"):
+            rx = re.compile(m.split(":", 1)[1], re.IGNORECASE)
+            hits = [i for i, d in enumerate(self._layers_desc) if (nm := self._name(d)) is not None and rx.search(nm)]
+            if not hits:
+                raise ValueError(f"seg_method {m!r}: no layer matches")
+            if len(hits) % self.total_parts:
+                raise ValueError(f"seg_method {m!r}: {len(hits)} matching layers do not divide into "
+                                 f"{self.total_parts} parts")
+            per = len(hits) // self.total_parts
+            return [0] + [hits[k * per - 1] + 1 for k in range(1, self.total_parts)] + [self.num_items]
+        raise ValueError(f"seg_method {m!r} is not supported (uniform, layer:<regex> or a boundary list)")
+
+    @staticmethod
+    def _name(d):
+        if isinstance(d, LayerDesc):
+            f = d.layer_func
+            return getattr(f, "__name__", type(f).__name__)
+        if isinstance(d, nn.Layer):
+            return type(d).__name__
+        return getattr(d, "__name__", None)
+
+    @staticmethod
+    def uniform(num_items, num_parts):
+        base, extra = divmod(num_items, num_parts)
+        out = [0]
+        for i in range(1, num_parts + 1):
+            out.append(out[-1] + base + (1 if i > num_parts - extra else 0))
+        return out
+
+
 class PipelineLayer(nn.Layer):
     def __init__(self, layers, num_stages=None, topology=None, loss_fn=None, seg_method="uniform",
                  recompute_interval=0, recompute_ctx=None, num_virtual_pipeline_stages=None):
@@ -83,6 +150,7 @@ class PipelineLayer(nn.Layer):
         V = int(num_virtual_pipeline_stages or 1)
         self._num_virtual_stages = V
         self.segment_parts = self._segment(n, num_stages * V, seg_method)
+        assert len(self.segment_parts) == num_stages * V + 1, self.segment_parts
         self.run_function = []
         self.shared_layers = nn.LayerDict()
         self._built = nn.LayerList()
@@ -118,16 +186,9 @@ class PipelineLayer(nn.Layer):
     def get_model_chunks(self):
         return self._model_chunks
 
-    @staticmethod
-    def _segment(n, stages, method):
-        if isinstance(method, (list, tuple)):
-            return list(method)
-        base = n // stages
-        extra = n % stages
-        parts = [0]
-        for s in range(stages):
-            parts.append(parts[-1] + base + (1 if s < extra else 0))
-        return parts
+    def _segment(self, n, stages, method):
+        return SegmentLayers(self._layers_desc, self._num_stages, method,
+                             self._num_virtual_stages if self._num_virtual_stages > 1 else None).do_segment()
 
     def get_stage_from_index(self, idx):
         for c in range(len(self.segment_parts) - 1):

@@ -1,0 +1,57 @@
+"""PipelineLayer stage boundaries (reference pp_layers.py:93 SegmentLayers): uniform with the remainder on the last
+stages, ``layer:<regex>`` balancing the matching layers, explicit boundary lists, virtual stages."""
+import pytest
+
+import paddlepaddle_amd.nn as nn
+from paddlepaddle_amd.distributed.fleet.meta_parallel import LayerDesc, SegmentLayers
+
+
+class Embed(nn.Layer):
+    pass
+
+
+class DecoderLayer(nn.Layer):
+    pass
+
+
+class Head(nn.Layer):
+    pass
+
+
+def _descs(n_dec):
+    return [LayerDesc(Embed)] + [LayerDesc(DecoderLayer) for _ in range(n_dec)] + [LayerDesc(Head)]
+
+
+def test_uniform_puts_the_remainder_on_the_last_stages():
+    assert SegmentLayers(_descs(8), 4).do_segment() == [0, 2, 4, 7, 10]
+    assert SegmentLayers(list(range(35)), 4).do_segment() == [0, 8, 17, 26, 35]
+    assert SegmentLayers(list(range(8)), 4).do_segment() == [0, 2, 4, 6, 8]
+
+
+def test_layer_regex_balances_matching_layers():
+    d = _descs(8)
+    # embedding joins the first stage, head the last; 2 decoders per stage
+    assert SegmentLayers(d, 4, "layer:DecoderLayer").do_segment() == [0, 3, 5, 7, 10]
+    assert SegmentLayers(d, 4, "layer:decoderlayer").do_segment() == [0, 3, 5, 7, 10]  # case-insensitive
+    assert SegmentLayers(d, 2, "layer:Decoder", num_virtual_pipeline_stage=2).do_segment() == [0, 3, 5, 7, 10]
+    with pytest.raises(ValueError):
+        SegmentLayers(_descs(6), 4, "layer:DecoderLayer").do_segment()  # 6 does not divide into 4
+    with pytest.raises(ValueError):
+        SegmentLayers(d, 2, "layer:NoSuchLayer").do_segment()
+
+
+def test_boundary_lists():
+    d = _descs(8)
+    assert SegmentLayers(d, 2, [0, 4]).do_segment() == [0, 4, 10]
+    assert SegmentLayers(d, 2, [0, 4, 10]).do_segment() == [0, 4, 10]
+    with pytest.raises(ValueError):
+        SegmentLayers(d, 3, [0, 4]).do_segment()
+    with pytest.raises(ValueError):
+        SegmentLayers(d, 2, [1, 4, 10]).do_segment()
+
+
+def test_pipeline_layer_uses_it(monkeypatch):
+    from paddlepaddle_amd.distributed.fleet.meta_parallel import PipelineLayer
+    pl = PipelineLayer(_descs(8), num_stages=4, seg_method="layer:DecoderLayer")
+    assert pl.segment_parts == [0, 3, 5, 7, 10]
+    assert [type(l).__name__ for l in pl.run_function] == ["Embed", "DecoderLayer", "DecoderLayer"]
