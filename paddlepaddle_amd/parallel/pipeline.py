@@ -196,15 +196,34 @@ class PipelineLayer(nn.Layer):
                 return c % self._num_stages
         return self._num_stages - 1
 
+    @staticmethod
+    def _run(fns):
+        def run(*x):
+            x = x[0] if len(x) == 1 else x
+            for f in fns:
+                x = f(x)
+            return x
+        return run
+
+    @staticmethod
+    def _need_recompute(fns, inputs):
+        """A segment is recomputed only if some input needs a gradient and it holds parameters."""
+        if not any(isinstance(t, Tensor) and not t.stop_gradient for t in inputs):
+            return False
+        return any(isinstance(f, nn.Layer) and len(list(f.parameters())) > 0 for f in fns)
+
     def forward(self, x, chunk_id=None):
+        """Run this stage's (or model chunk's) layers; with ``recompute_interval`` = k the layers go in
+        consecutive segments of k, each recomputed in backward as one checkpoint (reference pp_layers.py:793)."""
         from ..distributed.fleet.recompute import recompute
         fns = self.run_function if chunk_id is None else self._model_chunks[chunk_id]
-        for i, f in enumerate(fns):
-            if self._recompute_interval and self.training and i % self._recompute_interval == 0 and \
-                    isinstance(f, nn.Layer):
-                x = recompute(f, x)
-            else:
-                x = f(x)
+        k = self._recompute_interval
+        if not k or not self.training:
+            return self._run(fns)(x)
+        for lo in range(0, len(fns), k):
+            seg = fns[lo:lo + k]
+            args = x if isinstance(x, tuple) else (x,)
+            x = recompute(self._run(seg), *args) if self._need_recompute(seg, args) else self._run(seg)(*args)
         return x
 
 

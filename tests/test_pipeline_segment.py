@@ -55,3 +55,32 @@ def test_pipeline_layer_uses_it(monkeypatch):
     pl = PipelineLayer(_descs(8), num_stages=4, seg_method="layer:DecoderLayer")
     assert pl.segment_parts == [0, 3, 5, 7, 10]
     assert [type(l).__name__ for l in pl.run_function] == ["Embed", "DecoderLayer", "DecoderLayer"]
+
+
+def test_recompute_interval_checkpoints_segments_of_k_layers(monkeypatch):
+    import numpy as np
+    import paddlepaddle_amd as paddle
+    import importlib
+    R = importlib.import_module("paddlepaddle_amd.distributed.fleet.recompute")
+    from paddlepaddle_amd.distributed.fleet.meta_parallel import PipelineLayer
+
+    def build(k):
+        paddle.seed(3)
+        return PipelineLayer([LayerDesc(nn.Linear, 6, 6) for _ in range(5)], num_stages=1, recompute_interval=k)
+
+    x = paddle.randn([4, 6])
+    x.stop_gradient = False
+    ref = build(0)
+    ref(x).sum().backward()
+    calls = []
+    orig = R.recompute
+    monkeypatch.setattr(R, "recompute", lambda fn, *a, **kw: (calls.append(len(a)), orig(fn, *a, **kw))[1])
+    pl = build(2)
+    pl(x).sum().backward()
+    assert len(calls) == 3  # segments [0, 2), [2, 4), [4, 5)
+    for p, q in zip(ref.parameters(), pl.parameters()):
+        np.testing.assert_allclose(p.grad.numpy(), q.grad.numpy(), rtol=1e-5, atol=1e-6)
+    calls.clear()
+    x2 = paddle.randn([4, 6])  # stop_gradient input: the first segment's output still needs grad (parameters)
+    pl(x2).sum().backward()
+    assert len(calls) == 2
