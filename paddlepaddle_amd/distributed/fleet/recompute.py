@@ -95,21 +95,30 @@ def recompute(function, *args, **kwargs):
 
 
 def recompute_sequential(ctx, functions, *args, **kwargs):
-    segments = ctx.get("segments", 1) if isinstance(ctx, dict) else 1
+    """Split ``functions`` (a Sequential or a list of layers) into ``ctx["segments"]`` parts of len // segments
+    layers; the first segments - 1 parts are checkpointed, the rest runs plainly (the reference's split,
+    recompute.py:659 — with one segment nothing is recomputed). ``ctx["preserve_rng_state"]`` goes to each
+    checkpoint."""
+    ctx = ctx if isinstance(ctx, dict) else {}
+    segments = int(ctx.get("segments", 1))
+    kwargs.setdefault("preserve_rng_state", ctx.get("preserve_rng_state", True))
     layers = list(functions.children()) if hasattr(functions, "children") else list(functions)
-    n = len(layers)
-    seg = max(n // segments, 1)
-    x = args[0] if len(args) == 1 else args
+    size = len(layers) // segments if segments > 0 else len(layers)
 
     def run(lo, hi):
-        def f(inp):
+        def f(*inp):
+            x = inp[0] if len(inp) == 1 else inp
             for l in layers[lo:hi]:
-                inp = l(inp)
-            return inp
+                x = l(x)
+            return x
         return f
-    for lo in range(0, n, seg):
-        x = recompute(run(lo, min(lo + seg, n)), x, **kwargs)
-    return x
+
+    x = args[0] if len(args) == 1 else args
+    end = 0
+    for lo in range(0, size * (segments - 1), size):
+        end = lo + size
+        x = recompute(run(lo, end), *(x if isinstance(x, tuple) else (x,)), **kwargs)
+    return run(end, len(layers))(*(x if isinstance(x, tuple) else (x,)))
 
 
 def recompute_hybrid(ctx, function, *args, **kwargs):

@@ -84,3 +84,28 @@ def test_recompute_interval_checkpoints_segments_of_k_layers(monkeypatch):
     x2 = paddle.randn([4, 6])  # stop_gradient input: the first segment's output still needs grad (parameters)
     pl(x2).sum().backward()
     assert len(calls) == 2
+
+
+def test_recompute_sequential_checkpoints_all_but_the_last_segment(monkeypatch):
+    import importlib
+    import numpy as np
+    import paddlepaddle_amd as paddle
+    R = importlib.import_module("paddlepaddle_amd.distributed.fleet.recompute")
+    paddle.seed(4)
+    seq = paddle.nn.Sequential(*[paddle.nn.Linear(5, 5) for _ in range(6)])
+    x = paddle.randn([3, 5])
+    x.stop_gradient = False
+    seq(x).sum().backward()
+    ref = [p.grad.numpy().copy() for p in seq.parameters()]
+    seq.clear_gradients()
+    calls = []
+    orig = R.recompute
+    monkeypatch.setattr(R, "recompute", lambda fn, *a, **kw: (calls.append(kw.get("preserve_rng_state")),
+                                                              orig(fn, *a, **kw))[1])
+    R.recompute_sequential({"segments": 3, "preserve_rng_state": False}, seq, x).sum().backward()
+    assert calls == [False, False]  # segments [0, 2) and [2, 4) checkpointed, [4, 6) plain
+    for r, p in zip(ref, seq.parameters()):
+        np.testing.assert_allclose(r, p.grad.numpy(), rtol=1e-5, atol=1e-6)
+    calls.clear()
+    R.recompute_sequential({"segments": 1}, seq, x)
+    assert calls == []
