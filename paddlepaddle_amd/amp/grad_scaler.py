@@ -19,7 +19,7 @@ class OptimizerState(Enum):
 
 class AmpScaler:
     def __init__(self, enable=True, init_loss_scaling=2.0 ** 15, incr_ratio=2.0, decr_ratio=0.5,
-                 incr_every_n_steps=1000, decr_every_n_nan_or_inf=2, use_dynamic_loss_scaling=True):
+                 incr_every_n_steps=1000, decr_every_n_nan_or_inf=1, use_dynamic_loss_scaling=True):
         self._enable = enable
         self._scale = float(init_loss_scaling) if enable else 1.0
         self._incr_ratio, self._decr_ratio = incr_ratio, decr_ratio

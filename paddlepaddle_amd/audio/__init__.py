@@ -220,8 +220,8 @@ _WINDOWS = {
 
 
 class Spectrogram(nn.Layer):
-    def __init__(self, n_fft=512, hop_length=None, win_length=None, window="hann", power=2.0, center=True,
-                 pad_mode="reflect", dtype="float32"):
+    def __init__(self, n_fft=512, hop_length=512, win_length=None, window="hann", power=1.0, center=True,
+                 pad_mode="reflect", dtype="float32"):  # reference audio/features/layers.py defaults
         super().__init__()
         self.n_fft, self.hop = n_fft, hop_length or (win_length or n_fft) // 4
         self.win_length = win_length or n_fft
@@ -249,7 +249,7 @@ class MelSpectrogram(nn.Layer):
 
 
 class LogMelSpectrogram(nn.Layer):
-    def __init__(self, sr=22050, n_fft=2048, hop_length=512, win_length=None, window="hann", power=2.0, center=True,
+    def __init__(self, sr=22050, n_fft=512, hop_length=None, win_length=None, window="hann", power=2.0, center=True,
                  pad_mode="reflect", n_mels=64, f_min=50.0, f_max=None, htk=False, norm="slaney", ref_value=1.0,
                  amin=1e-10, top_db=None, dtype="float32"):
         super().__init__()
@@ -262,7 +262,7 @@ class LogMelSpectrogram(nn.Layer):
 
 
 class MFCC(nn.Layer):
-    def __init__(self, sr=22050, n_mfcc=40, n_fft=2048, hop_length=512, win_length=None, window="hann", power=2.0,
+    def __init__(self, sr=22050, n_mfcc=40, n_fft=512, hop_length=None, win_length=None, window="hann", power=2.0,
                  center=True, pad_mode="reflect", n_mels=64, f_min=50.0, f_max=None, htk=False, norm="slaney",
                  ref_value=1.0, amin=1e-10, top_db=None, dtype="float32"):
         super().__init__()

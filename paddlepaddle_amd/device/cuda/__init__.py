@@ -31,8 +31,15 @@ def _dev(device):
 
 
 class Stream:
-    def __init__(self, device=None, priority=2, blocking=False):
+    def __init__(self, device=None, priority=2, stream_base=None, blocking=False):
+        if stream_base is not None:  # wrap an existing stream (ours or a torch one)
+            self._s = stream_base._s if isinstance(stream_base, Stream) else stream_base
+            return
         self._s = torch.cuda.Stream(device=_dev(device), priority=-1 if priority == 1 else 0)
+
+    @property
+    def stream_base(self):
+        return self._s
 
     @property
     def cuda_stream(self):

@@ -35,9 +35,9 @@ _TORCH_OP = {ReduceOp.SUM: dist.ReduceOp.SUM, ReduceOp.MAX: dist.ReduceOp.MAX, R
 class Group:
     """A communication group (paddle.distributed.collective.Group)."""
 
-    def __init__(self, rank_in_group, gid, ranks, pg=None, name=None):
+    def __init__(self, rank_in_group, id, ranks, pg=None, name=None):  # noqa: A002 - reference keyword
         self.rank = rank_in_group
-        self.id = gid
+        self.id = id
         self.ranks = list(ranks)
         self.nranks = len(ranks)
         self.process_group = pg

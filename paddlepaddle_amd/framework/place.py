@@ -84,11 +84,24 @@ class CUDAPinnedPlace(Place):
 
 
 class XPUPlace(CPUPlace):  # not supported on this hardware, kept for import compatibility
-    pass
+    def __init__(self, dev_id=0):
+        super().__init__()
+        self._dev_id = int(dev_id)
+
+    def get_device_id(self):
+        return self._dev_id
 
 
 class CustomPlace(CPUPlace):
-    pass
+    def __init__(self, dev_type="custom", dev_id=0):
+        super().__init__()
+        self._dev_type, self._dev_id = dev_type, int(dev_id)
+
+    def get_device_id(self):
+        return self._dev_id
+
+    def get_device_type(self):
+        return self._dev_type
 
 
 IPUPlace = CPUPlace
@@ -119,7 +132,7 @@ def is_compiled_with_distribute():
     return True
 
 
-def is_compiled_with_custom_device(name=None):
+def is_compiled_with_custom_device(device_type=None):
     return False
 
 

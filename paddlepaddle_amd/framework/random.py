@@ -10,9 +10,9 @@ import torch
 _seed = None
 
 
-def seed(s):
+def seed(seed):
     global _seed
-    _seed = int(s)
+    _seed = int(seed)
     torch.manual_seed(_seed)
     np.random.seed(_seed % (2**32))
     _pyrandom.seed(_seed)

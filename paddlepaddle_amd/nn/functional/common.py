@@ -98,7 +98,7 @@ def zeropad2d(x, padding, data_format="NCHW", name=None):
 
 
 def interpolate(x, size=None, scale_factor=None, mode="nearest", align_corners=False, align_mode=0,
-                data_format=None, recompute_scale_factor=None, name=None):
+                data_format=None, name=None, recompute_scale_factor=None):
     t = T(x)
     nd = t.dim()
     if data_format is None:

@@ -57,7 +57,11 @@ class Normal(Initializer):
             t.normal_(self.mean, self.std)
 
 
-NormalInitializer = Normal
+class NormalInitializer(Normal):
+    """Legacy name (reference nn/initializer/normal.py NormalInitializer): (loc, scale, seed)."""
+
+    def __init__(self, loc=0.0, scale=1.0, seed=0):
+        super().__init__(loc, scale)
 
 
 class TruncatedNormal(Initializer):
@@ -71,7 +75,11 @@ class TruncatedNormal(Initializer):
         t.copy_(tmp)
 
 
-TruncatedNormalInitializer = TruncatedNormal
+class TruncatedNormalInitializer(TruncatedNormal):
+    """Legacy name: (loc, scale, seed, a, b) — truncation at a / b standard deviations."""
+
+    def __init__(self, loc=0.0, scale=1.0, seed=0, a=-2.0, b=2.0):
+        super().__init__(loc, scale, a, b)
 
 
 class Uniform(Initializer):
@@ -83,7 +91,19 @@ class Uniform(Initializer):
         t.copy_(tmp)
 
 
-UniformInitializer = Uniform
+class UniformInitializer(Uniform):
+    """Legacy name (reference uniform.py UniformInitializer): (low, high, seed, diag_num, diag_step, diag_val);
+    with diag_num > 0 the flat elements i * diag_step + i (i < diag_num) are set to diag_val afterwards."""
+
+    def __init__(self, low=-1.0, high=1.0, seed=0, diag_num=0, diag_step=0, diag_val=1.0):
+        super().__init__(low, high)
+        self.diag_num, self.diag_step, self.diag_val = int(diag_num), int(diag_step), float(diag_val)
+
+    def _init(self, t):
+        super()._init(t)
+        if self.diag_num > 0:
+            idx = torch.arange(self.diag_num, device=t.device) * (self.diag_step + 1)
+            t.view(-1).index_fill_(0, idx, self.diag_val)
 
 
 class XavierNormal(Initializer):
@@ -110,7 +130,14 @@ class XavierUniform(Initializer):
         Uniform(-lim, lim)._init(t)
 
 
-XavierInitializer = XavierUniform
+class XavierInitializer(Initializer):
+    """Legacy name (reference xavier.py XavierInitializer): (uniform, fan_in, fan_out, seed)."""
+
+    def __init__(self, uniform=True, fan_in=None, fan_out=None, seed=0):
+        self._impl = (XavierUniform if uniform else XavierNormal)(fan_in, fan_out)
+
+    def _init(self, t):
+        self._impl._init(t)
 
 
 def calculate_gain(nonlinearity, param=None):
@@ -151,7 +178,15 @@ class KaimingUniform(Initializer):
         Uniform(-lim, lim)._init(t)
 
 
-MSRAInitializer = KaimingNormal
+class MSRAInitializer(Initializer):
+    """Legacy name (reference kaiming.py MSRAInitializer): (uniform, fan_in, seed, negative_slope,
+    nonlinearity); uniform by default like the reference."""
+
+    def __init__(self, uniform=True, fan_in=None, seed=0, negative_slope=0, nonlinearity="relu"):
+        self._impl = (KaimingUniform if uniform else KaimingNormal)(fan_in, negative_slope, nonlinearity)
+
+    def _init(self, t):
+        self._impl._init(t)
 
 
 class Assign(Initializer):

@@ -56,6 +56,9 @@ RReLU = _simple("RReLU", F.rrelu, (("lower", 1.0 / 8.0), ("upper", 1.0 / 3.0)))
 
 
 class Softmax2D(Layer):
+    def __init__(self, name=None):
+        super().__init__()
+
     def forward(self, x):
         return F.softmax(x, axis=-3)
 

@@ -69,7 +69,8 @@ class AdaptiveLogSoftmaxWithLoss(Layer):
     """Efficient softmax approximation (Grave et al.): a head over the shortlist + one logit per tail cluster,
     each cluster a low-rank (in -> in / div_value^(i+1)) projection."""
 
-    def __init__(self, in_features, n_classes, cutoffs, div_value=4.0, head_bias=False, name=None):
+    def __init__(self, in_features, n_classes, cutoffs, weight_attr=None, bias_attr=None, div_value=4.0,
+                 head_bias=False, name=None):
         super().__init__()
         cutoffs = list(cutoffs)
         if sorted(cutoffs) != cutoffs or min(cutoffs) <= 0 or max(cutoffs) >= n_classes or \
@@ -80,14 +81,14 @@ class AdaptiveLogSoftmaxWithLoss(Layer):
         self.shortlist_size = self.cutoffs[0]
         self.n_clusters = len(self.cutoffs) - 1
         self.head_size = self.shortlist_size + self.n_clusters
-        self.head_weight = self.create_parameter([in_features, self.head_size])
-        self.head_bias = self.create_parameter([self.head_size], is_bias=True) if head_bias else None
+        self.head_weight = self.create_parameter([in_features, self.head_size], attr=weight_attr)
+        self.head_bias = self.create_parameter([self.head_size], attr=bias_attr, is_bias=True) if head_bias else None
         self.tail_weights = []
         for i in range(self.n_clusters):
             hsz = int(in_features // (div_value ** (i + 1)))
             osz = self.cutoffs[i + 1] - self.cutoffs[i]
-            proj = self.create_parameter([in_features, hsz])
-            out = self.create_parameter([hsz, osz])
+            proj = self.create_parameter([in_features, hsz], attr=weight_attr)
+            out = self.create_parameter([hsz, osz], attr=weight_attr)
             self.add_parameter(f"tail_{i}_proj", proj)
             self.add_parameter(f"tail_{i}_out", out)
             self.tail_weights.append([proj, out])

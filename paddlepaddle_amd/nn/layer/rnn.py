@@ -187,10 +187,27 @@ class _RNNBase(Layer):
 class LSTM(_RNNBase):
     _mode, _gates = "LSTM", 4
 
+    def __init__(self, input_size, hidden_size, num_layers=1, direction="forward", time_major=False, dropout=0.0,
+                 weight_ih_attr=None, weight_hh_attr=None, bias_ih_attr=None, bias_hh_attr=None, proj_size=0,
+                 name=None):  # reference positional order (rnn.py LSTM)
+        super().__init__(input_size, hidden_size, num_layers, direction, time_major, dropout, weight_ih_attr,
+                         weight_hh_attr, bias_ih_attr, bias_hh_attr, name, proj_size=proj_size)
+
 
 class GRU(_RNNBase):
     _mode, _gates = "GRU", 3
 
+    def __init__(self, input_size, hidden_size, num_layers=1, direction="forward", time_major=False, dropout=0.0,
+                 weight_ih_attr=None, weight_hh_attr=None, bias_ih_attr=None, bias_hh_attr=None, name=None):
+        super().__init__(input_size, hidden_size, num_layers, direction, time_major, dropout, weight_ih_attr,
+                         weight_hh_attr, bias_ih_attr, bias_hh_attr, name)
+
 
 class SimpleRNN(_RNNBase):
     _mode, _gates = "RNN", 1
+
+    def __init__(self, input_size, hidden_size, num_layers=1, direction="forward", time_major=False, dropout=0.0,
+                 activation="tanh", weight_ih_attr=None, weight_hh_attr=None, bias_ih_attr=None, bias_hh_attr=None,
+                 name=None):  # reference positional order: activation after dropout
+        super().__init__(input_size, hidden_size, num_layers, direction, time_major, dropout, weight_ih_attr,
+                         weight_hh_attr, bias_ih_attr, bias_hh_attr, name, activation=activation)

@@ -242,7 +242,7 @@ class Lamb(_PerParam):
 class NAdam(_PerParam):
     _acc_names = ("moment1", "moment2", "mu_product")
 
-    def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1.0e-8, momentum_decay=0.004,
+    def __init__(self, learning_rate=0.002, beta1=0.9, beta2=0.999, epsilon=1.0e-8, momentum_decay=0.004,
                  parameters=None, weight_decay=None, grad_clip=None, name=None):
         super().__init__(learning_rate, parameters, weight_decay, grad_clip, name)
         self._b1, self._b2, self._eps, self._md = beta1, beta2, epsilon, momentum_decay

@@ -88,7 +88,11 @@ class _Factory:
 
     def __init__(self, cls, display, args=(), kwargs=None):
         self.cls, self._display = cls, display
-        sig = [p for p in inspect.signature(cls.__init__).parameters.values() if p.name != "self"]
+        # the layer being quantized is the instance's first argument (reference observer / quanter layers), not a
+        # factory argument
+        params = inspect.signature(cls.__init__).parameters
+        self._takes_layer = "layer" in params
+        sig = [p for p in params.values() if p.name not in ("self", "layer")]
         bound = {p.name: p.default for p in sig if p.default is not inspect.Parameter.empty}
         for p, v in zip(sig, args):
             bound[p.name] = v
@@ -97,7 +101,7 @@ class _Factory:
         self.kwargs = {k: bound[k] for k in order if k in bound}
 
     def _instance(self, layer=None):
-        return self.cls(**self.kwargs)
+        return self.cls(layer, **self.kwargs) if self._takes_layer else self.cls(**self.kwargs)
 
     def __str__(self):
         return f"{self._display}(" + ",".join(f"{k}={v}" for k, v in self.kwargs.items()) + ")"
@@ -118,8 +122,9 @@ def quanter(class_name):
 
 # ------------------------------------------------------------------------------ observers / quanters
 class AbsmaxObserverLayer(BaseObserver):
-    def __init__(self, quant_bits=8):
+    def __init__(self, layer=None, quant_bits=8):
         super().__init__()
+        self._layer = layer
         self._bits = quant_bits
         self.register_buffer("_absmax", _wrap(torch.zeros(())))
 
@@ -132,8 +137,9 @@ class AbsmaxObserverLayer(BaseObserver):
 
 
 class GroupWiseWeightObserverLayer(BaseObserver):
-    def __init__(self, quant_bits=4, group_size=128):
+    def __init__(self, layer=None, quant_bits=8, group_size=128):
         super().__init__()
+        self._layer = layer
         self._bits, self.group_size = quant_bits, group_size
         self._scales = None
 
@@ -146,8 +152,9 @@ class GroupWiseWeightObserverLayer(BaseObserver):
 
 
 class FakeQuanterWithAbsMaxObserverLayer(BaseQuanter):
-    def __init__(self, name=None, moving_rate=0.9, bit_length=8, dtype="float32"):
+    def __init__(self, layer=None, name=None, moving_rate=0.9, bit_length=8, dtype="float32"):
         super().__init__()
+        self._layer = layer
         self._bits = bit_length
         self.moving_rate = moving_rate
         self.register_buffer("_scale", _wrap(torch.zeros(())))

@@ -331,8 +331,8 @@ def put_along_axis(arr, indices, values, axis, reduce="assign", include_self=Tru
     return _wrap(t.scatter_reduce(axis, i, v, red, include_self=include_self))
 
 
-def put_along_axis_(arr, indices, values, axis, reduce="assign", include_self=True):
-    arr._t.copy_(put_along_axis(arr, indices, values, axis, reduce, include_self)._t)
+def put_along_axis_(arr, indices, values, axis, reduce="assign", include_self=True, broadcast=True):
+    arr._t.copy_(put_along_axis(arr, indices, values, axis, reduce, include_self, broadcast)._t)
     return arr
 
 

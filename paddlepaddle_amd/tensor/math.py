@@ -214,6 +214,40 @@ mod = _g["remainder"]
 mod_ = _g["remainder_"]
 
 
+def _with_out(base, arity):
+    """Reference signature of the logic / bitwise ops (tensor/logic.py): an optional ``out`` tensor that receives
+    the result (and is returned)."""
+    def put(r, out):
+        if out is None:
+            return r
+        out._t.resize_(r._t.shape).copy_(r._t)
+        return out
+    if arity == 2:
+        def op(x, y, out=None, name=None):
+            return put(base(x, y), out)
+    else:
+        def op(x, out=None, name=None):
+            return put(base(x), out)
+    op.__name__, op.__qualname__, op.__doc__ = base.__name__, base.__name__, base.__doc__
+    return op
+
+
+for _n in ("bitwise_and", "bitwise_or", "bitwise_xor", "logical_and", "logical_or", "logical_xor"):
+    _g[_n] = _with_out(_g[_n], 2)
+for _n in ("bitwise_not", "logical_not"):
+    _g[_n] = _with_out(_g[_n], 1)
+bitwise_invert = _g["bitwise_not"]
+
+
+def trunc(input, name=None):
+    return _wrap(torch.trunc(T(input)))
+
+
+def trunc_(input, name=None):
+    input._t.trunc_()
+    return input
+
+
 def _unsigned_of(dt):
     return {torch.int8: torch.uint8, torch.int16: torch.int16, torch.int32: torch.int32,
             torch.int64: torch.int64, torch.uint8: torch.uint8}[dt]

@@ -62,8 +62,8 @@ def map_structure(func, *structure):
     return func(*structure)
 
 
-def pack_sequence_as(structure, flat):
-    it = iter(flat)
+def pack_sequence_as(structure, flat_sequence):
+    it = iter(flat_sequence)
 
     def _p(s):
         if isinstance(s, (list, tuple)):
