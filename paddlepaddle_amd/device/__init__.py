@@ -8,7 +8,17 @@ from ..framework.place import (set_device, get_device, is_compiled_with_cuda, is
                                is_compiled_with_custom_device, CPUPlace, CUDAPlace)
 from . import cuda  # noqa: F401
 from . import pinned  # noqa: F401
-from .cuda import Stream, Event, current_stream, stream_guard, synchronize  # noqa: F401
+from .cuda import Stream, current_stream, stream_guard, synchronize  # noqa: F401
+from .cuda import Event as _CudaEvent
+
+
+class Event(_CudaEvent):
+    """paddle.device.Event: the device comes first (reference device/__init__.py Event(device, enable_timing,
+    blocking, interprocess)); paddle.device.cuda.Event keeps (enable_timing, blocking, interprocess)."""
+
+    def __init__(self, device=None, enable_timing=False, blocking=False, interprocess=False):
+        super().__init__(enable_timing, blocking, interprocess)
+        self.device = device
 
 
 def get_all_device_type():

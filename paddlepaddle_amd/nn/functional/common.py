@@ -64,7 +64,7 @@ def feature_alpha_dropout(x, p=0.5, training=True, name=None):
     return _wrap(F.feature_alpha_dropout(T(x), p, training))
 
 
-def pad(x, pad, mode="constant", value=0.0, data_format="NCHW", pad_from_left_axis=True, name=None):
+def pad(x, pad, mode="constant", value=0.0, data_format=None, pad_from_left_axis=True, name=None):
     """paddle.nn.functional.pad. Reference: python/paddle/nn/functional/common.py pad (Note 1-3):
     constant mode with a list whose length is not 2*(N-2) pads whole axes — a 2N list from the first axis
     forward (``pad_from_left_axis``) or from the last axis backward, a shorter list from the last axis;

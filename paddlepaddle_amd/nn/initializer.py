@@ -133,8 +133,8 @@ class XavierUniform(Initializer):
 class XavierInitializer(Initializer):
     """Legacy name (reference xavier.py XavierInitializer): (uniform, fan_in, fan_out, seed)."""
 
-    def __init__(self, uniform=True, fan_in=None, fan_out=None, seed=0):
-        self._impl = (XavierUniform if uniform else XavierNormal)(fan_in, fan_out)
+    def __init__(self, uniform=True, fan_in=None, fan_out=None, seed=0, gain=1.0):
+        self._impl = (XavierUniform if uniform else XavierNormal)(fan_in, fan_out, gain)
 
     def _init(self, t):
         self._impl._init(t)

@@ -210,9 +210,9 @@ class LocalResponseNorm(Layer):
 
 
 class SpectralNorm(Layer):
-    def __init__(self, weight_shape, dim=0, power_iters=1, epsilon=1e-12, dtype="float32"):
+    def __init__(self, weight_shape, dim=0, power_iters=1, eps=1e-12, dtype="float32"):
         super().__init__()
-        self._dim, self._power_iters, self._eps = dim, power_iters, epsilon
+        self._dim, self._power_iters, self._eps = dim, power_iters, eps
         h = weight_shape[dim]
         w = int(np.prod(weight_shape)) // h
         self.weight_u = self.create_parameter([h], default_initializer=I.Normal(0.0, 1.0))

@@ -48,7 +48,7 @@ def test_defaults_match_reference():
 
 
 def test_legacy_initializers():
-    assert _params(I.XavierInitializer.__init__)[1:] == ["uniform", "fan_in", "fan_out", "seed"]
+    assert _params(I.XavierInitializer.__init__)[1:] == ["uniform", "fan_in", "fan_out", "seed", "gain"]
     assert _params(I.MSRAInitializer.__init__)[1:] == ["uniform", "fan_in", "seed", "negative_slope", "nonlinearity"]
     assert _params(I.NormalInitializer.__init__)[1:] == ["loc", "scale", "seed"]
     w = paddle.zeros([3, 3])
