@@ -124,7 +124,7 @@ def quanter(class_name):
 class AbsmaxObserverLayer(BaseObserver):
     def __init__(self, layer=None, quant_bits=8):
         super().__init__()
-        self._layer = layer
+        object.__setattr__(self, "_layer", layer)  # a reference, not a sublayer (no parameter re-registration)
         self._bits = quant_bits
         self.register_buffer("_absmax", _wrap(torch.zeros(())))
 
@@ -139,7 +139,7 @@ class AbsmaxObserverLayer(BaseObserver):
 class GroupWiseWeightObserverLayer(BaseObserver):
     def __init__(self, layer=None, quant_bits=8, group_size=128):
         super().__init__()
-        self._layer = layer
+        object.__setattr__(self, "_layer", layer)  # a reference, not a sublayer (no parameter re-registration)
         self._bits, self.group_size = quant_bits, group_size
         self._scales = None
 
@@ -154,7 +154,7 @@ class GroupWiseWeightObserverLayer(BaseObserver):
 class FakeQuanterWithAbsMaxObserverLayer(BaseQuanter):
     def __init__(self, layer=None, name=None, moving_rate=0.9, bit_length=8, dtype="float32"):
         super().__init__()
-        self._layer = layer
+        object.__setattr__(self, "_layer", layer)  # a reference, not a sublayer (no parameter re-registration)
         self._bits = bit_length
         self.moving_rate = moving_rate
         self.register_buffer("_scale", _wrap(torch.zeros(())))
